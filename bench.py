@@ -1,0 +1,214 @@
+"""Benchmark: DiLoCo outer step (fused delta + population mean + Nesterov SGD) on MI355X.
+
+Metric (BASELINE.json): "GB/s of param bytes reduced per outer step (device-resident)".
+  value = (total workers K) x P x (bytes per worker element) / (wall time of one step),
+  aggregated over all ranks.
+
+Default workload (N=1): the 1.3B-parameter GPT layout (P = 1,315,723,264, 292 tensors), a
+population of 8 bf16 workers resident on the GPU, fp32 global weights and fp32 momentum,
+diloco.py's outer optimiser (lr 0.7, momentum 0.9, Nesterov) in steady state (carried buffer).
+N>1: weak scaling, 8 workers resident per GPU (population 8N), RCCL reduce-scatter / all-gather.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0. Also reports the fused kernel's own duration (HIP events on the
+stream it is launched on), the HBM roofline fraction, and the CPU oracle timed on this host.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0        # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+DT = {"f32": torch.float32, "bf16": torch.bfloat16}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--layout", default="gpt_1p3b")
+    p.add_argument("--workers-per-gpu", type=int, default=8)
+    p.add_argument("--theta-dtype", default="f32", choices=DT)
+    p.add_argument("--worker-dtype", default="bf16", choices=DT)
+    p.add_argument("--lr", type=float, default=0.7)
+    p.add_argument("--momentum", type=float, default=0.9)
+    p.add_argument("--nesterov", type=int, default=1)
+    p.add_argument("--mode", default="reduce", choices=["reduce", "exact"])
+    p.add_argument("--bucket-elems", type=int, default=1 << 26)
+    p.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
+    p.add_argument("--cpu-sample-elems", type=int, default=1 << 24)
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return p.parse_args()
+
+
+def synth_population(theta: torch.Tensor, workers: list[torch.Tensor], seed: int) -> None:
+    """theta ~ N(0, 0.02^2); worker k = theta + N(0, 1e-3^2), on the device."""
+    g = torch.Generator(device=theta.device).manual_seed(seed)
+    chunk = 1 << 26
+    n = theta.numel()
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        t = torch.randn(b - a, generator=g, device=theta.device) * 0.02
+        theta[a:b].copy_(t)
+        for w in workers:
+            w[a:b].copy_(t + torch.randn(b - a, generator=g, device=theta.device) * 1e-3)
+
+
+def cpu_baseline(args, theta_dtype, worker_dtype, k):
+    """The CPU oracle (the reference's op sequence restated in C, OpenMP) on a bounded sample."""
+    from oracle import oracle
+    n = args.cpu_sample_elems
+    g = torch.Generator().manual_seed(1)
+    theta = (torch.randn(n, generator=g) * 0.02).to(theta_dtype)
+    workers = [(theta.float() + torch.randn(n, generator=g) * 1e-3).to(worker_dtype) for _ in range(k)]
+    mom = torch.zeros(n, dtype=theta_dtype)
+    oracle.outer_step(theta, workers, mom, False, args.lr, args.momentum, bool(args.nesterov))
+    times = []
+    t_end = time.perf_counter() + args.cpu_baseline_seconds
+    while time.perf_counter() < t_end or len(times) < 2:
+        t0 = time.perf_counter()
+        oracle.outer_step(theta, workers, mom, True, args.lr, args.momentum, bool(args.nesterov))
+        times.append(time.perf_counter() - t0)
+    times.sort()
+    t = times[len(times) // 2]
+    gbps = k * n * torch.finfo(worker_dtype).bits / 8 / t / 1e9
+    return {"value": round(gbps, 3), "unit": "GB/s", "cores": oracle.max_threads(), "kind": "port",
+            "sample": f"{n} elements x {k} workers (fused delta+mean+SGD, oracle/edt_oracle.c, "
+                      f"median of {len(times)} reps over {args.cpu_baseline_seconds:.0f}s)"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if not (world == 1 and args.gpus == 1):
+            raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch with torchrun")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from evolutionarydistributedtraining_amd import ops
+    from evolutionarydistributedtraining_amd.layouts import LAYOUTS
+    from evolutionarydistributedtraining_amd.diloco import OuterSync
+    from evolutionarydistributedtraining_amd.params import ParamArena
+
+    layout = LAYOUTS[args.layout]()
+    tdt, wdt = DT[args.theta_dtype], DT[args.worker_dtype]
+    k_local = args.workers_per_gpu
+    k_total = k_local * world
+    P = layout.total
+    if world == 1:
+        theta = ParamArena(layout, tdt, dev)
+        workers = [ParamArena(layout, wdt, dev) for _ in range(k_local)]
+        synth_population(theta.flat, [w.flat for w in workers], seed=1234)
+        sync = OuterSync(theta, workers, args.lr, args.momentum, bool(args.nesterov))
+        step = sync.step
+        kernel_name = "outer_kernel"
+    else:
+        from evolutionarydistributedtraining_amd.distributed import ShardedOuterSync
+        sync = ShardedOuterSync(layout, tdt, wdt, k_local, dev, args.lr, args.momentum, bool(args.nesterov),
+                                mode=args.mode, bucket_elems=args.bucket_elems)
+        synth_population(sync.theta.flat, [w.flat for w in sync.workers], seed=1234 + 0)
+        # replicas of theta must agree: rank 0's values everywhere
+        dist.broadcast(sync.theta_buf, 0)
+        step = sync.step
+        kernel_name = "outer_kernel" if args.mode == "exact" else "outer_kernel(partial)"
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # fused-kernel duration, measured with HIP events on the launch stream (torch's current)
+    kern_ms = None
+    if world == 1:
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        if world == 1:
+            ev[i][0].record()
+        step()
+        if world == 1:
+            ev[i][1].record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    ms_per_step = elapsed / args.steps * 1e3
+    if world == 1:
+        ks = sorted(a.elapsed_time(b) for a, b in ev)
+        kern_ms = sum(ks) / len(ks)
+
+    bytes_reduced = k_total * P * torch.finfo(wdt).bits // 8
+    value = bytes_reduced / (ms_per_step / 1e3) / 1e9
+
+    if rank == 0:
+        bg = torch.finfo(tdt).bits // 8
+        bw = torch.finfo(wdt).bits // 8
+        per_elem = k_local * bw + 2 * bg + (2 * bg if args.momentum else 0)
+        algo_bytes = per_elem * P                       # one launch, steady state (carried buffer)
+        roofline = None
+        if world == 1:
+            achieved = algo_bytes / (kern_ms / 1e3) / 1e9
+            traffic = None
+            if os.path.exists(args.traffic_json):
+                try:
+                    with open(args.traffic_json) as f:
+                        tj = json.load(f)
+                    key = f"{args.layout}/K{k_local}/{args.theta_dtype}-{args.worker_dtype}"
+                    traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
+                except (OSError, ValueError):
+                    traffic = None
+            roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                        "kernel": kernel_name, "kernel_ms": round(kern_ms, 4),
+                        "bytes_per_elem": per_elem, "algo_bytes_per_launch": algo_bytes}
+        out = {
+            "metric": "GB/s of param bytes reduced per outer step (device-resident), 1/2/4/8 GPUs",
+            "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32" if tdt == torch.float32 else "bf16",
+            "data": "synthetic (theta ~ N(0,.02^2), worker = theta + N(0,1e-3^2), seeded on device)",
+            "config": {"workload": f"DiLoCo outer step, {args.layout} P={P} T={len(layout)}, "
+                                   f"{k_local} {args.worker_dtype} workers resident per GPU, "
+                                   f"{args.theta_dtype} theta+momentum, lr {args.lr} mu {args.momentum} "
+                                   f"nesterov {bool(args.nesterov)}",
+                       "params": P, "tensors": len(layout), "workers_per_gpu": k_local,
+                       "population": k_total, "worker_dtype": args.worker_dtype,
+                       "theta_dtype": args.theta_dtype,
+                       "parallelism": "single GPU" if world == 1 else f"dp{world} {args.mode} (RCCL)"},
+        }
+        if roofline:
+            out["roofline"] = roofline
+        if world == 1 and args.cpu_baseline_seconds > 0:
+            out["cpu_baseline"] = cpu_baseline(args, tdt, wdt, k_local)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

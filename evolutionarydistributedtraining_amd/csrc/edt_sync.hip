@@ -1,0 +1,816 @@
+// edt_sync.hip — CDNA4 (gfx950) kernels for the outer-loop sync hot path and their C ABI
+// (declared in include/edt_sync.h).
+//
+// Everything here is element-wise and HBM-bound: no MFMA. Each thread moves 8 elements per
+// iteration with 16-byte loads (one bf16 x8 or two fp32 x4 per operand), a grid-stride loop
+// keeps ~2k workgroups resident, and every operand is read once and written once.
+//
+// Numerics mirror the reference's PyTorch-CPU / numpy kernels bit for bit:
+//  * fp32 regime: each torch op is one IEEE fp32 op; `add(x, y, alpha=a)` is fmaf(a, y, x)
+//    (torch's vectorised CPU add is an FMA, tails included); true division by K.
+//  * bf16 regime: each torch op is computed in fp32 and rounded to bf16 (RNE); `mul_(s)` uses
+//    the fp32 scalar, `add(..., alpha=a)` first rounds alpha to bf16.
+// The file must be compiled with -ffp-contract=off so that no unintended FMA is formed.
+
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <type_traits>
+
+#include "edt_sync.h"
+
+namespace {
+
+constexpr int kBlock = 256;        // 4 waves
+constexpr int kVec = 8;            // elements per thread per iteration
+constexpr int kMaxBlocks = 2048;   // 256 CUs x 8 resident workgroups
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+thread_local char g_err[512];
+
+int fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+int check_launch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(EDT_ERR_LAUNCH, "%s: launch failed: %s", what, hipGetErrorString(e));
+    return EDT_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// bf16 helpers: a bf16 is the top half of an fp32; conversion f32->bf16 is v_cvt_pk_bf16_f32
+// (round-to-nearest-even, as c10::BFloat16).
+
+__device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+__device__ __forceinline__ uint32_t pack_bf(float lo, float hi) {
+    bf16x2 r = __builtin_convertvector((f32x2){lo, hi}, bf16x2);
+    return __builtin_bit_cast(uint32_t, r);
+}
+__host__ __device__ inline float host_round_bf16(float x) {   // used for scalars on the host
+    uint32_t u;
+    memcpy(&u, &x, 4);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return x;
+    u = (u + 0x7fffu + ((u >> 16) & 1u)) & 0xffff0000u;
+    float r;
+    memcpy(&r, &u, 4);
+    return r;
+}
+
+// Round each of the N values to the precision of dtype DT (no-op for fp32).
+template <int DT, int N>
+__device__ __forceinline__ void rnd(float (&x)[N]) {
+    if constexpr (DT == EDT_BF16) {
+        if constexpr (N % 2 == 0) {
+#pragma unroll
+            for (int j = 0; j < N; j += 2) {
+                uint32_t p = pack_bf(x[j], x[j + 1]);
+                x[j] = bf_lo(p);
+                x[j + 1] = bf_hi(p);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < N; ++j) x[j] = bf_lo(pack_bf(x[j], 0.f));
+        }
+    }
+}
+
+// Load / store N (= 8 or 1) consecutive elements of a buffer of dtype DT as fp32.
+// Index `i` is the element index of the first element (a multiple of 8 when N == 8).
+template <int DT, int N>
+__device__ __forceinline__ void ld(const void* __restrict__ p, uint64_t i, float (&x)[N]) {
+    if constexpr (DT == EDT_F32) {
+        const float* q = static_cast<const float*>(p) + i;
+        if constexpr (N == 8) {
+            f32x4 a = *reinterpret_cast<const f32x4*>(q);
+            f32x4 b = *reinterpret_cast<const f32x4*>(q + 4);
+            x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
+            x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < N; ++j) x[j] = q[j];
+        }
+    } else {
+        const uint16_t* q = static_cast<const uint16_t*>(p) + i;
+        if constexpr (N == 8) {
+            u32x4 w = *reinterpret_cast<const u32x4*>(q);
+            x[0] = bf_lo(w.x); x[1] = bf_hi(w.x); x[2] = bf_lo(w.y); x[3] = bf_hi(w.y);
+            x[4] = bf_lo(w.z); x[5] = bf_hi(w.z); x[6] = bf_lo(w.w); x[7] = bf_hi(w.w);
+        } else {
+#pragma unroll
+            for (int j = 0; j < N; ++j) x[j] = __uint_as_float(uint32_t(q[j]) << 16);
+        }
+    }
+}
+
+// Stores round-to-nearest-even into DT (values are already DT-exact in the bf16 regime).
+template <int DT, int N>
+__device__ __forceinline__ void st(void* __restrict__ p, uint64_t i, const float (&x)[N]) {
+    if constexpr (DT == EDT_F32) {
+        float* q = static_cast<float*>(p) + i;
+        if constexpr (N == 8) {
+            *reinterpret_cast<f32x4*>(q) = (f32x4){x[0], x[1], x[2], x[3]};
+            *reinterpret_cast<f32x4*>(q + 4) = (f32x4){x[4], x[5], x[6], x[7]};
+        } else {
+#pragma unroll
+            for (int j = 0; j < N; ++j) q[j] = x[j];
+        }
+    } else {
+        uint16_t* q = static_cast<uint16_t*>(p) + i;
+        if constexpr (N == 8) {
+            u32x4 w;
+            w.x = pack_bf(x[0], x[1]); w.y = pack_bf(x[2], x[3]);
+            w.z = pack_bf(x[4], x[5]); w.w = pack_bf(x[6], x[7]);
+            *reinterpret_cast<u32x4*>(q) = w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < N; ++j) q[j] = uint16_t(pack_bf(x[j], 0.f) & 0xffffu);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// SGD scalars, rounded on the host exactly as torch rounds them.
+
+struct SgdScalars {
+    float mul_mu;      // buf.mul_(momentum): fp32 scalar
+    float alpha_mu;    // grad.add(buf, alpha=momentum): alpha in the tensor dtype
+    float alpha_nlr;   // param.add_(grad, alpha=-lr): alpha in the tensor dtype
+    int use_momentum;  // momentum != 0
+    int has_buf;       // momentum buffer carried from a previous step
+    int nesterov;
+};
+
+SgdScalars make_sgd(int gdt, double lr, double mu, int has_buf, int nesterov) {
+    SgdScalars s;
+    s.mul_mu = (float)mu;
+    s.alpha_mu = gdt == EDT_BF16 ? host_round_bf16((float)mu) : (float)mu;
+    s.alpha_nlr = gdt == EDT_BF16 ? host_round_bf16((float)(-lr)) : (float)(-lr);
+    s.use_momentum = mu != 0.0;
+    s.has_buf = has_buf;
+    s.nesterov = nesterov;
+    return s;
+}
+
+// torch.optim.sgd._single_tensor_sgd for one group of N elements, in regime GDT.
+// grad is the pseudo-gradient (already in GDT precision); theta is updated in registers,
+// the momentum buffer is read from / written to `mom` at element i.
+template <int GDT, int N>
+__device__ __forceinline__ void sgd_update(float (&theta)[N], const float (&grad)[N], void* mom,
+                                           uint64_t i, const SgdScalars& s) {
+    float u[N];
+    if (s.use_momentum) {
+        float b[N];
+        if (s.has_buf) {
+            ld<GDT, N>(mom, i, b);
+#pragma unroll
+            for (int j = 0; j < N; ++j) b[j] = b[j] * s.mul_mu;      // buf.mul_(momentum)
+            rnd<GDT>(b);
+#pragma unroll
+            for (int j = 0; j < N; ++j) b[j] = b[j] + grad[j];       // .add_(grad, alpha=1)
+            rnd<GDT>(b);
+        } else {
+#pragma unroll
+            for (int j = 0; j < N; ++j) b[j] = grad[j];              // buf = grad.clone()
+        }
+        st<GDT, N>(mom, i, b);
+        if (s.nesterov) {
+#pragma unroll
+            for (int j = 0; j < N; ++j) u[j] = __builtin_fmaf(s.alpha_mu, b[j], grad[j]);
+            rnd<GDT>(u);
+        } else {
+#pragma unroll
+            for (int j = 0; j < N; ++j) u[j] = b[j];
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < N; ++j) u[j] = grad[j];
+    }
+#pragma unroll
+    for (int j = 0; j < N; ++j) theta[j] = __builtin_fmaf(s.alpha_nlr, u[j], theta[j]);
+    rnd<GDT>(theta);
+}
+
+// ---------------------------------------------------------------------------------------
+// DiLoCo outer step
+
+struct Workers {
+    const void* p[EDT_MAX_WORKERS];
+};
+
+struct OuterArgs {
+    void* theta;
+    void* mom;
+    float* acc_out;      // partial mode
+    uint64_t n;
+    int K;               // workers in this launch
+    float kdiv;          // divisor (K_total)
+    float kinv;          // 1/K_total when K_total is a power of two
+    int div_exact;       // 1: true division, 0: multiply by kinv (identical for powers of two)
+    int accumulate;      // partial mode: add into acc_out
+    SgdScalars sgd;
+    Workers w;
+};
+
+enum { MODE_FUSED = 0, MODE_PARTIAL = 1 };
+
+// Per-element accumulation acc = sum_k round(round(w_k - g) / K) in the precision of GDT
+// (worker-major order, EDT_LM/diloco.py:243-246). MODE_PARTIAL sums the rounded quotients
+// in fp32 instead (the cross-rank sum is then an fp32 RCCL reduction).
+template <int GDT, int WDT, int KC, int DIV, int MODE, int N>
+__device__ __forceinline__ void outer_elems(const OuterArgs& a, uint64_t i) {
+    float g[N], acc[N];
+    ld<GDT, N>(a.theta, i, g);
+    if (MODE == MODE_PARTIAL && a.accumulate) {
+        ld<EDT_F32, N>(a.acc_out, i, acc);      // continue the running sum in worker order
+    } else {
+#pragma unroll
+        for (int j = 0; j < N; ++j) acc[j] = 0.f;
+    }
+    const int K = KC > 0 ? KC : a.K;
+    auto body = [&](int k) {
+        float w[N];
+        ld<WDT, N>(a.w.p[k], i, w);
+#pragma unroll
+        for (int j = 0; j < N; ++j) w[j] = w[j] - g[j];              // trained - base
+        rnd<GDT>(w);
+        if constexpr (DIV) {
+#pragma unroll
+            for (int j = 0; j < N; ++j) w[j] = w[j] / a.kdiv;        // delta / num_models
+        } else {
+#pragma unroll
+            for (int j = 0; j < N; ++j) w[j] = w[j] * a.kinv;
+        }
+        rnd<GDT>(w);
+#pragma unroll
+        for (int j = 0; j < N; ++j) acc[j] = acc[j] + w[j];          // acc += delta / K
+        if constexpr (MODE == MODE_FUSED) rnd<GDT>(acc);
+    };
+    if constexpr (KC > 0) {
+#pragma unroll
+        for (int k = 0; k < KC; ++k) body(k);
+    } else {
+#pragma unroll 4
+        for (int k = 0; k < K; ++k) body(k);
+    }
+    if constexpr (MODE == MODE_PARTIAL) {
+        st<EDT_F32, N>(a.acc_out, i, acc);
+    } else {
+        float grad[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) grad[j] = -acc[j];               // p.grad = -avg_delta
+        sgd_update<GDT, N>(g, grad, a.mom, i, a.sgd);
+        st<GDT, N>(a.theta, i, g);
+    }
+}
+
+// DIV = 1: true division by K (torch CPU `delta / num_models`); DIV = 0: multiply by 1/K,
+// bit-identical when K is a power of two.
+template <int GDT, int WDT, int KC, int DIV, int MODE, int N>
+__global__ __launch_bounds__(kBlock) void outer_kernel(OuterArgs a) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if constexpr (N == kVec) {
+        const uint64_t nv = a.n / kVec;
+        for (uint64_t v = tid; v < nv; v += stride) outer_elems<GDT, WDT, KC, DIV, MODE, kVec>(a, v * kVec);
+        const uint64_t t = nv * kVec + tid;      // scalar tail (< 8 elements)
+        if (t < a.n) outer_elems<GDT, WDT, KC, DIV, MODE, 1>(a, t);
+    } else {
+        for (uint64_t e = tid; e < a.n; e += stride) outer_elems<GDT, WDT, KC, DIV, MODE, 1>(a, e);
+    }
+}
+
+// SGD from a reduced fp32 sum (sharded multi-GPU step).
+template <int GDT, int N>
+__global__ __launch_bounds__(kBlock) void sgd_apply_kernel(void* theta, const float* acc, void* mom,
+                                                           uint64_t n, SgdScalars s) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    auto elems = [&](auto tagN, uint64_t i) {
+        constexpr int M = decltype(tagN)::value;
+        float g[M], a[M], grad[M];
+        ld<GDT, M>(theta, i, g);
+        ld<EDT_F32, M>(acc, i, a);
+        rnd<GDT>(a);
+#pragma unroll
+        for (int j = 0; j < M; ++j) grad[j] = -a[j];
+        sgd_update<GDT, M>(g, grad, mom, i, s);
+        st<GDT, M>(theta, i, g);
+    };
+    using V8 = std::integral_constant<int, kVec>;
+    using V1 = std::integral_constant<int, 1>;
+    if constexpr (N == kVec) {
+        const uint64_t nv = n / kVec;
+        for (uint64_t v = tid; v < nv; v += stride) elems(V8{}, v * kVec);
+        const uint64_t t = nv * kVec + tid;
+        if (t < n) elems(V1{}, t);
+    } else {
+        for (uint64_t e = tid; e < n; e += stride) elems(V1{}, e);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// EDT pair merge: child = SGD step of lerp(0.5, b1, b2) towards the parents' trained weights.
+
+struct PairArgs {
+    const void* b1;
+    const void* b2;
+    const void* m1;
+    const void* m2;
+    void* out;
+    void* mom;
+    uint64_t n;
+    SgdScalars sgd;
+};
+
+template <int GDT, int WDT, int N>
+__device__ __forceinline__ void pair_elems(const PairArgs& a, uint64_t i) {
+    float base[N];
+    if (a.b2) {                        // run_linear_merge_5050: lerp(0.5, b1, b2) in the model dtype
+        float x[N], y[N];
+        ld<WDT, N>(a.b1, i, x);
+        ld<WDT, N>(a.b2, i, y);
+#pragma unroll
+        for (int j = 0; j < N; ++j) { x[j] = x[j] * 0.5f; y[j] = y[j] * 0.5f; }   // (1-.5)*v0, .5*v1
+        rnd<WDT>(x);
+        rnd<WDT>(y);
+#pragma unroll
+        for (int j = 0; j < N; ++j) base[j] = x[j] + y[j];
+        rnd<WDT>(base);
+    } else {                           // run_sgd on an already merged base model (dtype GDT)
+        ld<GDT, N>(a.b1, i, base);
+    }
+    rnd<GDT>(base);                    // load_state_dict into the base model's dtype
+    float d1[N], d2[N];
+    ld<WDT, N>(a.m1, i, d1);
+    ld<WDT, N>(a.m2, i, d2);
+#pragma unroll
+    for (int j = 0; j < N; ++j) { d1[j] = d1[j] - base[j]; d2[j] = d2[j] - base[j]; }
+    rnd<GDT>(d1);
+    rnd<GDT>(d2);
+#pragma unroll
+    for (int j = 0; j < N; ++j) d1[j] = d1[j] + d2[j];
+    rnd<GDT>(d1);
+#pragma unroll
+    for (int j = 0; j < N; ++j) d1[j] = d1[j] * 0.5f;              // / num_models (= 2)
+    rnd<GDT>(d1);
+    float grad[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) grad[j] = -(0.f + d1[j]);           // acc = zeros + delta
+    sgd_update<GDT, N>(base, grad, a.mom, i, a.sgd);
+    st<GDT, N>(a.out, i, base);
+}
+
+template <int GDT, int WDT, int N>
+__global__ __launch_bounds__(kBlock) void pair_kernel(PairArgs a) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if constexpr (N == kVec) {
+        const uint64_t nv = a.n / kVec;
+        for (uint64_t v = tid; v < nv; v += stride) pair_elems<GDT, WDT, kVec>(a, v * kVec);
+        const uint64_t t = nv * kVec + tid;
+        if (t < a.n) pair_elems<GDT, WDT, 1>(a, t);
+    } else {
+        for (uint64_t e = tid; e < a.n; e += stride) pair_elems<GDT, WDT, 1>(a, e);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// lerp with a scalar t: out = round(round(c0*v0) + round(c1*v1)) in compute dtype CDT.
+
+template <int IDT, int ODT, int CDT, int N>
+__device__ __forceinline__ void lerp_elems(const void* v0, const void* v1, void* out, uint64_t i,
+                                           float c0, float c1) {
+    float x[N], y[N];
+    ld<IDT, N>(v0, i, x);
+    ld<IDT, N>(v1, i, y);
+#pragma unroll
+    for (int j = 0; j < N; ++j) { x[j] = c0 * x[j]; y[j] = c1 * y[j]; }
+    rnd<CDT>(x);
+    rnd<CDT>(y);
+#pragma unroll
+    for (int j = 0; j < N; ++j) x[j] = x[j] + y[j];
+    rnd<CDT>(x);
+    st<ODT, N>(out, i, x);
+}
+
+template <int IDT, int ODT, int CDT, int N>
+__global__ __launch_bounds__(kBlock) void lerp_kernel(const void* v0, const void* v1, void* out,
+                                                      uint64_t n, float c0, float c1) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if constexpr (N == kVec) {
+        const uint64_t nv = n / kVec;
+        for (uint64_t v = tid; v < nv; v += stride) lerp_elems<IDT, ODT, CDT, kVec>(v0, v1, out, v * kVec, c0, c1);
+        const uint64_t t = nv * kVec + tid;
+        if (t < n) lerp_elems<IDT, ODT, CDT, 1>(v0, v1, out, t, c0, c1);
+    } else {
+        for (uint64_t e = tid; e < n; e += stride) lerp_elems<IDT, ODT, CDT, 1>(v0, v1, out, e, c0, c1);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// SLERP. chunk_desc[3c .. 3c+2] = {start, length, segment}; chunks never cross a segment.
+
+__device__ __forceinline__ double wave_sum(double x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    return x;
+}
+
+template <int IDT>
+__global__ __launch_bounds__(kBlock) void slerp_stats_kernel(const void* v0, const void* v1,
+                                                             const uint64_t* chunks, int64_t nchunks,
+                                                             double* partial) {
+    __shared__ double red[3][kBlock / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+        const uint64_t start = chunks[3 * c], len = chunks[3 * c + 1];
+        const uint64_t end = start + len;
+        double s00 = 0.0, s11 = 0.0, s01 = 0.0;
+        const uint64_t a = (start + kVec - 1) / kVec * kVec;      // aligned body [a, b)
+        const uint64_t b = end / kVec * kVec;
+        if (a < b) {
+            for (uint64_t i = a + (uint64_t)threadIdx.x * kVec; i < b; i += (uint64_t)kBlock * kVec) {
+                float x[kVec], y[kVec];
+                ld<IDT, kVec>(v0, i, x);
+                ld<IDT, kVec>(v1, i, y);
+#pragma unroll
+                for (int j = 0; j < kVec; ++j) {
+                    const double dx = x[j], dy = y[j];
+                    s00 = __builtin_fma(dx, dx, s00);
+                    s11 = __builtin_fma(dy, dy, s11);
+                    s01 = __builtin_fma(dx, dy, s01);
+                }
+            }
+        }
+        // head [start, min(a, end)) and tail [max(b, a), end): fewer than 16 elements
+        const uint64_t h_end = a < end ? a : end;
+        const uint64_t t_beg = b > a ? b : h_end;
+        const uint64_t nh = h_end - start, nt = end - t_beg;
+        if ((uint64_t)threadIdx.x < nh + nt) {
+            const uint64_t i = threadIdx.x < nh ? start + threadIdx.x : t_beg + (threadIdx.x - nh);
+            float x[1], y[1];
+            ld<IDT, 1>(v0, i, x);
+            ld<IDT, 1>(v1, i, y);
+            const double dx = x[0], dy = y[0];
+            s00 = __builtin_fma(dx, dx, s00);
+            s11 = __builtin_fma(dy, dy, s11);
+            s01 = __builtin_fma(dx, dy, s01);
+        }
+        s00 = wave_sum(s00);
+        s11 = wave_sum(s11);
+        s01 = wave_sum(s01);
+        if (lane == 0) { red[0][wave] = s00; red[1][wave] = s11; red[2][wave] = s01; }
+        __syncthreads();
+        if (threadIdx.x < 3) {
+            double s = 0.0;
+#pragma unroll
+            for (int w = 0; w < kBlock / 64; ++w) s += red[threadIdx.x][w];
+            partial[3 * c + threadIdx.x] = s;
+        }
+        __syncthreads();
+    }
+}
+
+// One wave per segment: fixed-order reduction of the chunk sums, then the reference's scalar
+// math in fp32 (numpy float32 scalars, NEP 50: python floats enter as fp32).
+__global__ __launch_bounds__(kBlock) void slerp_coef_kernel(const double* partial, const int32_t* first,
+                                                            int nseg, const double* tvals,
+                                                            float thr, float eps, float* coef,
+                                                            float* dot_out) {
+    const int lane = threadIdx.x & 63;
+    const int seg = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    if (seg >= nseg) return;
+    double s00 = 0.0, s11 = 0.0, s01 = 0.0;
+    for (int c = first[seg] + lane; c < first[seg + 1]; c += 64) {
+        s00 += partial[3 * c];
+        s11 += partial[3 * c + 1];
+        s01 += partial[3 * c + 2];
+    }
+    s00 = wave_sum(s00);
+    s11 = wave_sum(s11);
+    s01 = wave_sum(s01);
+    if (lane != 0) return;
+    const float n0 = (float)sqrt(s00), n1 = (float)sqrt(s11);      // np.linalg.norm (fp32)
+    const double d0 = n0 > eps ? (double)n0 : 1.0;                  // normalize() divides only if > eps
+    const double d1 = n1 > eps ? (double)n1 : 1.0;
+    const float dot = (float)(s01 / (d0 * d1));
+    const double t = tvals[seg];
+    float c0, c1;
+    if (fabsf(dot) > thr) {                                         // lerp on the originals
+        c0 = (float)(1.0 - t);
+        c1 = (float)t;
+    } else {
+        const float th0 = acosf(dot);
+        const float s0 = sinf(th0);
+        const float tht = th0 * (float)t;
+        const float st_ = sinf(tht);
+        c0 = sinf(th0 - tht) / s0;
+        c1 = st_ / s0;
+    }
+    coef[2 * seg] = c0;
+    coef[2 * seg + 1] = c1;
+    if (dot_out) dot_out[seg] = dot;
+}
+
+template <int IDT, int ODT>
+__global__ __launch_bounds__(kBlock) void slerp_blend_kernel(const void* v0, const void* v1, void* out,
+                                                             const uint64_t* chunks, int64_t nchunks,
+                                                             const float* coef) {
+    for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+        const uint64_t start = chunks[3 * c], len = chunks[3 * c + 1], seg = chunks[3 * c + 2];
+        const uint64_t end = start + len;
+        const float c0 = coef[2 * seg], c1 = coef[2 * seg + 1];
+        const uint64_t a = (start + kVec - 1) / kVec * kVec;
+        const uint64_t b = end / kVec * kVec;
+        if (a < b) {
+            for (uint64_t i = a + (uint64_t)threadIdx.x * kVec; i < b; i += (uint64_t)kBlock * kVec)
+                lerp_elems<IDT, ODT, EDT_F32, kVec>(v0, v1, out, i, c0, c1);
+        }
+        const uint64_t h_end = a < end ? a : end;
+        const uint64_t t_beg = b > a ? b : h_end;
+        const uint64_t nh = h_end - start, nt = end - t_beg;
+        if ((uint64_t)threadIdx.x < nh + nt) {
+            const uint64_t i = threadIdx.x < nh ? start + threadIdx.x : t_beg + (threadIdx.x - nh);
+            lerp_elems<IDT, ODT, EDT_F32, 1>(v0, v1, out, i, c0, c1);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// host-side dispatch helpers
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+unsigned grid_for(uint64_t n, bool vec) {
+    const uint64_t per = vec ? (uint64_t)kBlock * kVec : (uint64_t)kBlock;
+    uint64_t g = (n + per - 1) / per;
+    if (g < 1) g = 1;
+    if (g > kMaxBlocks) g = kMaxBlocks;
+    return (unsigned)g;
+}
+
+bool valid_pair(int gdt, int wdt) {
+    return (gdt == EDT_F32 && (wdt == EDT_F32 || wdt == EDT_BF16)) || (gdt == EDT_BF16 && wdt == EDT_BF16);
+}
+
+template <int GDT, int WDT, int MODE>
+int launch_outer_k(const OuterArgs& a, bool vec, hipStream_t s) {
+    const unsigned g = grid_for(a.n, vec);
+#define EDT_LAUNCH_K(KC, DIV)                                                                    \
+    do {                                                                                         \
+        if (vec) outer_kernel<GDT, WDT, KC, DIV, MODE, kVec><<<g, kBlock, 0, s>>>(a);            \
+        else outer_kernel<GDT, WDT, KC, DIV, MODE, 1><<<g, kBlock, 0, s>>>(a);                   \
+    } while (0)
+    // compile-time worker counts for the common populations; the divisor is K_total
+    if (a.K == 1 && !a.div_exact) EDT_LAUNCH_K(1, 0);
+    else if (a.K == 2 && !a.div_exact) EDT_LAUNCH_K(2, 0);
+    else if (a.K == 3 && a.div_exact) EDT_LAUNCH_K(3, 1);
+    else if (a.K == 4 && !a.div_exact) EDT_LAUNCH_K(4, 0);
+    else if (a.K == 8 && !a.div_exact) EDT_LAUNCH_K(8, 0);
+    else if (a.div_exact) EDT_LAUNCH_K(0, 1);
+    else EDT_LAUNCH_K(0, 0);
+#undef EDT_LAUNCH_K
+    return check_launch("outer_kernel");
+}
+
+template <int MODE>
+int launch_outer(int gdt, int wdt, const OuterArgs& a, bool vec, hipStream_t s) {
+    if (gdt == EDT_F32 && wdt == EDT_F32) return launch_outer_k<EDT_F32, EDT_F32, MODE>(a, vec, s);
+    if (gdt == EDT_F32 && wdt == EDT_BF16) return launch_outer_k<EDT_F32, EDT_BF16, MODE>(a, vec, s);
+    return launch_outer_k<EDT_BF16, EDT_BF16, MODE>(a, vec, s);
+}
+
+bool is_pow2(int k) { return k > 0 && (k & (k - 1)) == 0; }
+
+int fill_outer(OuterArgs& a, const void* theta, const void* const* theta_k, int K, int K_total, uint64_t n) {
+    memset(&a, 0, sizeof(a));
+    if (!theta && n) return fail(EDT_ERR_ARG, "theta_g is null");
+    if (K < 1 || K > EDT_MAX_WORKERS)
+        return fail(EDT_ERR_ARG, "worker count %d out of range [1, %d]", K, EDT_MAX_WORKERS);
+    if (K_total < 1) return fail(EDT_ERR_ARG, "total worker count %d < 1", K_total);
+    if (!theta_k) return fail(EDT_ERR_ARG, "theta_k is null");
+    for (int k = 0; k < K; ++k) {
+        if (!theta_k[k] && n) return fail(EDT_ERR_ARG, "theta_k[%d] is null", k);
+        a.w.p[k] = theta_k[k];
+    }
+    a.theta = const_cast<void*>(theta);
+    a.n = n;
+    a.K = K;
+    a.kdiv = (float)K_total;
+    a.kinv = 1.0f / (float)K_total;
+    a.div_exact = is_pow2(K_total) ? 0 : 1;
+    return EDT_OK;
+}
+
+}  // namespace
+
+// =========================================================================================
+// C ABI
+
+extern "C" {
+
+const char* edt_last_error(void) { return g_err; }
+const char* edt_version(void) { return "edt_sync 0.1.0 gfx950"; }
+
+int edt_outer_step_bytes_per_elem(int gdt, int wdt, int K, int with_momentum) {
+    const int bg = gdt == EDT_BF16 ? 2 : 4, bw = wdt == EDT_BF16 ? 2 : 4;
+    return K * bw + 2 * bg + (with_momentum ? 2 * bg : 0);
+}
+
+int edt_outer_step(void* theta_g, int gdt, const void* const* theta_k, int wdt, int K,
+                   void* momentum, int has_momentum, uint64_t n, double lr, double momentum_coef,
+                   int nesterov, void* stream) {
+    g_err[0] = 0;
+    if (!valid_pair(gdt, wdt)) return fail(EDT_ERR_ARG, "unsupported dtype pair (gdt/wdt)");
+    OuterArgs a;
+    int rc = fill_outer(a, theta_g, theta_k, K, K, n);
+    if (rc) return rc;
+    a.sgd = make_sgd(gdt, lr, momentum_coef, has_momentum, nesterov);
+    if (a.sgd.use_momentum && !momentum && n) return fail(EDT_ERR_ARG, "momentum buffer is null");
+    a.mom = momentum;
+    if (n == 0) return EDT_OK;
+    bool vec = aligned16(theta_g) && (!a.sgd.use_momentum || aligned16(momentum));
+    for (int k = 0; k < K; ++k) vec = vec && aligned16(theta_k[k]);
+    return launch_outer<MODE_FUSED>(gdt, wdt, a, vec, (hipStream_t)stream);
+}
+
+int edt_delta_partial(const void* theta_g, int gdt, const void* const* theta_k, int wdt, int K_local,
+                      int K_total, uint64_t n, float* acc_f32, int accumulate, void* stream) {
+    g_err[0] = 0;
+    if (!valid_pair(gdt, wdt)) return fail(EDT_ERR_ARG, "unsupported dtype pair (gdt/wdt)");
+    OuterArgs a;
+    int rc = fill_outer(a, theta_g, theta_k, K_local, K_total, n);
+    if (rc) return rc;
+    if (!acc_f32 && n) return fail(EDT_ERR_ARG, "acc_f32 is null");
+    a.acc_out = acc_f32;
+    a.accumulate = accumulate;
+    if (n == 0) return EDT_OK;
+    bool vec = aligned16(theta_g) && aligned16(acc_f32);
+    for (int k = 0; k < K_local; ++k) vec = vec && aligned16(theta_k[k]);
+    return launch_outer<MODE_PARTIAL>(gdt, wdt, a, vec, (hipStream_t)stream);
+}
+
+int edt_sgd_apply(void* theta_g, int gdt, const float* acc_f32, void* momentum, int has_momentum,
+                  uint64_t n, double lr, double momentum_coef, int nesterov, void* stream) {
+    g_err[0] = 0;
+    if (gdt != EDT_F32 && gdt != EDT_BF16) return fail(EDT_ERR_ARG, "unsupported dtype");
+    if (n == 0) return EDT_OK;
+    if (!theta_g || !acc_f32) return fail(EDT_ERR_ARG, "null buffer");
+    SgdScalars s = make_sgd(gdt, lr, momentum_coef, has_momentum, nesterov);
+    if (s.use_momentum && !momentum) return fail(EDT_ERR_ARG, "momentum buffer is null");
+    const bool vec = aligned16(theta_g) && aligned16(acc_f32) && (!s.use_momentum || aligned16(momentum));
+    const unsigned g = grid_for(n, vec);
+    hipStream_t st = (hipStream_t)stream;
+    if (gdt == EDT_F32) {
+        if (vec) sgd_apply_kernel<EDT_F32, kVec><<<g, kBlock, 0, st>>>(theta_g, acc_f32, momentum, n, s);
+        else sgd_apply_kernel<EDT_F32, 1><<<g, kBlock, 0, st>>>(theta_g, acc_f32, momentum, n, s);
+    } else {
+        if (vec) sgd_apply_kernel<EDT_BF16, kVec><<<g, kBlock, 0, st>>>(theta_g, acc_f32, momentum, n, s);
+        else sgd_apply_kernel<EDT_BF16, 1><<<g, kBlock, 0, st>>>(theta_g, acc_f32, momentum, n, s);
+    }
+    return check_launch("sgd_apply_kernel");
+}
+
+int edt_pair_merge(const void* b1, const void* b2, const void* m1, const void* m2, int wdt,
+                   void* theta_out, int gdt, void* momentum, int has_momentum, uint64_t n, double lr,
+                   double momentum_coef, int nesterov, void* stream) {
+    g_err[0] = 0;
+    if (!valid_pair(gdt, wdt)) return fail(EDT_ERR_ARG, "unsupported dtype pair (gdt/wdt)");
+    if (n == 0) return EDT_OK;
+    if (!b1 || !m1 || !m2 || !theta_out) return fail(EDT_ERR_ARG, "null buffer");
+    PairArgs a;
+    a.b1 = b1; a.b2 = b2; a.m1 = m1; a.m2 = m2; a.out = theta_out; a.mom = momentum; a.n = n;
+    a.sgd = make_sgd(gdt, lr, momentum_coef, has_momentum, nesterov);
+    if (a.sgd.use_momentum && !momentum) return fail(EDT_ERR_ARG, "momentum buffer is null");
+    const bool vec = aligned16(b1) && (!b2 || aligned16(b2)) && aligned16(m1) && aligned16(m2) &&
+                     aligned16(theta_out) && (!a.sgd.use_momentum || aligned16(momentum));
+    const unsigned g = grid_for(n, vec);
+    hipStream_t s = (hipStream_t)stream;
+    if (gdt == EDT_F32 && wdt == EDT_F32) {
+        if (vec) pair_kernel<EDT_F32, EDT_F32, kVec><<<g, kBlock, 0, s>>>(a);
+        else pair_kernel<EDT_F32, EDT_F32, 1><<<g, kBlock, 0, s>>>(a);
+    } else if (gdt == EDT_F32) {
+        if (vec) pair_kernel<EDT_F32, EDT_BF16, kVec><<<g, kBlock, 0, s>>>(a);
+        else pair_kernel<EDT_F32, EDT_BF16, 1><<<g, kBlock, 0, s>>>(a);
+    } else {
+        if (vec) pair_kernel<EDT_BF16, EDT_BF16, kVec><<<g, kBlock, 0, s>>>(a);
+        else pair_kernel<EDT_BF16, EDT_BF16, 1><<<g, kBlock, 0, s>>>(a);
+    }
+    return check_launch("pair_kernel");
+}
+
+int edt_lerp(const void* v0, const void* v1, int in_dt, void* out, int out_dt, int cdt, uint64_t n,
+             double t, void* stream) {
+    g_err[0] = 0;
+    if ((in_dt | out_dt | cdt) & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
+    if (in_dt == EDT_F32 && cdt == EDT_BF16) return fail(EDT_ERR_ARG, "bf16 compute of fp32 inputs unsupported");
+    if (n == 0) return EDT_OK;
+    if (!v0 || !v1 || !out) return fail(EDT_ERR_ARG, "null buffer");
+    const float c0 = (float)(1.0 - t), c1 = (float)t;
+    const bool vec = aligned16(v0) && aligned16(v1) && aligned16(out);
+    const unsigned g = grid_for(n, vec);
+    hipStream_t s = (hipStream_t)stream;
+#define EDT_LERP(I, O, C)                                                                  \
+    do {                                                                                   \
+        if (vec) lerp_kernel<I, O, C, kVec><<<g, kBlock, 0, s>>>(v0, v1, out, n, c0, c1);   \
+        else lerp_kernel<I, O, C, 1><<<g, kBlock, 0, s>>>(v0, v1, out, n, c0, c1);          \
+    } while (0)
+    if (in_dt == EDT_F32) {
+        if (out_dt == EDT_F32) EDT_LERP(EDT_F32, EDT_F32, EDT_F32);
+        else EDT_LERP(EDT_F32, EDT_BF16, EDT_F32);
+    } else if (cdt == EDT_F32) {
+        if (out_dt == EDT_F32) EDT_LERP(EDT_BF16, EDT_F32, EDT_F32);
+        else EDT_LERP(EDT_BF16, EDT_BF16, EDT_F32);
+    } else {
+        if (out_dt == EDT_F32) EDT_LERP(EDT_BF16, EDT_F32, EDT_BF16);
+        else EDT_LERP(EDT_BF16, EDT_BF16, EDT_BF16);
+    }
+#undef EDT_LERP
+    return check_launch("lerp_kernel");
+}
+
+int64_t edt_slerp_make_chunks(const uint64_t* seg_offsets, int nseg, uint32_t chunk_elems,
+                              uint64_t* chunk_desc, int64_t max_chunks, int32_t* seg_first_chunk) {
+    g_err[0] = 0;
+    if (nseg < 0 || !seg_offsets || chunk_elems == 0) return fail(EDT_ERR_ARG, "bad segment table");
+    int64_t c = 0;
+    for (int s = 0; s < nseg; ++s) {
+        if (seg_first_chunk) seg_first_chunk[s] = (int32_t)c;
+        const uint64_t a = seg_offsets[s], b = seg_offsets[s + 1];
+        if (b < a) return fail(EDT_ERR_ARG, "segment offsets decrease at segment %d", s);
+        for (uint64_t x = a; x < b; x += chunk_elems) {
+            if (c < max_chunks && chunk_desc) {
+                chunk_desc[3 * c] = x;
+                chunk_desc[3 * c + 1] = (b - x) < chunk_elems ? (b - x) : chunk_elems;
+                chunk_desc[3 * c + 2] = (uint64_t)s;
+            }
+            ++c;
+        }
+    }
+    if (seg_first_chunk) seg_first_chunk[nseg] = (int32_t)c;
+    if (c > max_chunks) return -c - 1;
+    return c;
+}
+
+int edt_slerp_stats(const void* v0, const void* v1, int in_dt, const uint64_t* chunk_desc, int64_t nchunks,
+                    double* partial, void* stream) {
+    g_err[0] = 0;
+    if (in_dt & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
+    if (nchunks == 0) return EDT_OK;
+    if (!v0 || !v1 || !chunk_desc || !partial) return fail(EDT_ERR_ARG, "null buffer");
+    if (!aligned16(v0) || !aligned16(v1)) return fail(EDT_ERR_ARG, "slerp inputs must be 16-byte aligned");
+    const unsigned g = (unsigned)(nchunks < kMaxBlocks ? nchunks : kMaxBlocks);
+    hipStream_t s = (hipStream_t)stream;
+    if (in_dt == EDT_F32) slerp_stats_kernel<EDT_F32><<<g, kBlock, 0, s>>>(v0, v1, chunk_desc, nchunks, partial);
+    else slerp_stats_kernel<EDT_BF16><<<g, kBlock, 0, s>>>(v0, v1, chunk_desc, nchunks, partial);
+    return check_launch("slerp_stats_kernel");
+}
+
+int edt_slerp_coef(const double* partial, const int32_t* seg_first_chunk, int nseg, const double* t,
+                   double dot_threshold, double eps, float* coef, float* dot_out, void* stream) {
+    g_err[0] = 0;
+    if (nseg == 0) return EDT_OK;
+    if (!partial || !seg_first_chunk || !t || !coef) return fail(EDT_ERR_ARG, "null buffer");
+    const int per = kBlock / 64;
+    const unsigned g = (unsigned)((nseg + per - 1) / per);
+    slerp_coef_kernel<<<g, kBlock, 0, (hipStream_t)stream>>>(partial, seg_first_chunk, nseg, t,
+                                                            (float)dot_threshold, (float)eps, coef, dot_out);
+    return check_launch("slerp_coef_kernel");
+}
+
+int edt_slerp_blend(const void* v0, const void* v1, int in_dt, void* out, int out_dt, const uint64_t* chunk_desc,
+                    int64_t nchunks, const float* coef, void* stream) {
+    g_err[0] = 0;
+    if ((in_dt | out_dt) & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
+    if (nchunks == 0) return EDT_OK;
+    if (!v0 || !v1 || !out || !chunk_desc || !coef) return fail(EDT_ERR_ARG, "null buffer");
+    if (!aligned16(v0) || !aligned16(v1) || !aligned16(out))
+        return fail(EDT_ERR_ARG, "slerp buffers must be 16-byte aligned");
+    const unsigned g = (unsigned)(nchunks < kMaxBlocks ? nchunks : kMaxBlocks);
+    hipStream_t s = (hipStream_t)stream;
+    if (in_dt == EDT_F32 && out_dt == EDT_F32)
+        slerp_blend_kernel<EDT_F32, EDT_F32><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef);
+    else if (in_dt == EDT_F32)
+        slerp_blend_kernel<EDT_F32, EDT_BF16><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef);
+    else if (out_dt == EDT_F32)
+        slerp_blend_kernel<EDT_BF16, EDT_F32><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef);
+    else
+        slerp_blend_kernel<EDT_BF16, EDT_BF16><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef);
+    return check_launch("slerp_blend_kernel");
+}
+
+}  // extern "C"

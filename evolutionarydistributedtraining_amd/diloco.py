@@ -1,0 +1,172 @@
+"""DiLoCo outer step on MI355X — the drop-in for EDT_LM/diloco.py:238-289 (== diloco_sim.py:233-299).
+
+Reference behaviour (per parameter tensor i, worker-major, torch CPU ops):
+    acc_i = 0;  for k in trained_models: acc_i += (theta_k,i - theta_g,i) / K
+    p.grad = -acc_i
+    torch.optim.SGD(lr, momentum, nesterov).step()          # single-tensor path
+with the SGD object carried across generations by `load_state_dict` (diloco.py:258-286), so the
+momentum buffer survives the base model being reloaded. Defaults: diloco.py lr 0.7, momentum 0.9,
+nesterov True (:253-255); diloco_sim.py lr 1.0, momentum 0.0, nesterov False (:248-250).
+
+Here the whole step is ONE fused HIP launch over flat parameter arenas (see `ops.outer_step`).
+`outer_step()` keeps the reference's tensor-list surface; `OuterSync` is the arena-native form
+the benchmark and the multi-GPU path use.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import ops
+from ._lib import EDT_MAX_WORKERS, EdtError
+from .params import ParamArena, ParamLayout, flat_view, pack, unpack_
+
+DILOCO_DEFAULTS = dict(lr=0.7, momentum=0.9, nesterov=True)        # EDT_LM/diloco.py:253-255
+DILOCO_SIM_DEFAULTS = dict(lr=1.0, momentum=0.0, nesterov=False)   # EDT_LM/diloco_sim.py:248-250
+
+
+class OuterState:
+    """The outer optimiser's state across generations: one flat momentum buffer in
+    `parameters()` order — what the reference keeps in the master's `outer_optimizer`
+    (EDT_LM/diloco.py:100,258-289). Also serialises to the torch `SGD.state_dict()` format
+    (`outer_optim.pt`, as EDT_LM/train/crossover.py:231-232 writes per individual)."""
+
+    def __init__(self):
+        self.momentum: torch.Tensor | None = None   # flat, dtype of theta_g
+        self.has_momentum = False                   # False until the first momentum step
+        self.hparams = dict(DILOCO_DEFAULTS)
+        self.steps = 0
+
+    def buffer_for(self, theta: torch.Tensor) -> torch.Tensor:
+        if self.momentum is None:
+            self.momentum = torch.zeros_like(theta)
+            self.has_momentum = False
+        elif self.momentum.numel() != theta.numel():
+            raise EdtError("outer-optimizer state does not match the parameter count "
+                           f"({self.momentum.numel()} vs {theta.numel()})")
+        elif self.momentum.dtype != theta.dtype or self.momentum.device != theta.device:
+            # torch's load_state_dict casts state to the param's dtype/device
+            self.momentum = self.momentum.to(dtype=theta.dtype, device=theta.device)
+        return self.momentum
+
+    # --- torch.optim.SGD state_dict interop (index-keyed, as load_state_dict carries it) ---
+    def state_dict(self, layout: ParamLayout) -> dict:
+        state = {}
+        if self.momentum is not None and self.has_momentum:
+            for i, v in enumerate(layout.views(self.momentum)):
+                state[i] = {"momentum_buffer": v.detach().to("cpu", copy=True)}
+        group = dict(lr=self.hparams["lr"], momentum=self.hparams["momentum"], dampening=0,
+                     weight_decay=0, nesterov=self.hparams["nesterov"], maximize=False,
+                     foreach=None, differentiable=False, fused=None,
+                     params=list(range(len(layout))))
+        return {"state": state, "param_groups": [group]}
+
+    def load_state_dict(self, sd: dict, layout: ParamLayout, dtype: torch.dtype, device) -> None:
+        group = sd["param_groups"][0]
+        self.hparams = dict(lr=group["lr"], momentum=group["momentum"], nesterov=group["nesterov"])
+        bufs = [sd["state"].get(i, {}).get("momentum_buffer") for i in range(len(layout))]
+        if all(b is None for b in bufs):
+            self.momentum, self.has_momentum = None, False
+            return
+        if any(b is None for b in bufs):
+            raise EdtError("partial momentum state is not supported (every parameter needs a buffer)")
+        flat = torch.empty(layout.total, dtype=dtype, device=device)
+        for v, b in zip(layout.views(flat), bufs):
+            v.copy_(b)
+        self.momentum, self.has_momentum = flat, True
+
+    def save(self, path: str, layout: ParamLayout) -> None:
+        torch.save(self.state_dict(layout), path)
+
+    @classmethod
+    def load(cls, path: str, layout: ParamLayout, dtype, device) -> "OuterState":
+        st = cls()
+        st.load_state_dict(torch.load(path, map_location="cpu", weights_only=True), layout, dtype, device)
+        return st
+
+
+def _step_flat(theta: torch.Tensor, workers: list[torch.Tensor], state: OuterState, lr: float,
+               momentum: float, nesterov: bool) -> None:
+    state.hparams = dict(lr=lr, momentum=momentum, nesterov=nesterov)
+    mom = state.buffer_for(theta) if momentum != 0 else None
+    has = state.has_momentum if momentum != 0 else False
+    ops.outer_step(theta, workers, mom, has, lr, momentum, nesterov)
+    if momentum != 0:
+        state.has_momentum = True
+    state.steps += 1
+
+
+def outer_step(base_params, worker_params, state: OuterState | None = None, lr: float = 0.7,
+               momentum: float = 0.9, nesterov: bool = True) -> OuterState:
+    """Drop-in for EDT_LM/diloco.py:238-289 on device-resident parameters.
+
+    base_params:   list of the global model's parameters (`list(base_model.parameters())`),
+                   updated in place.
+    worker_params: K lists of the trained replicas' parameters, same order.
+    state:         the carried outer-optimiser state (None on the first generation).
+    Zero-copy when each list is a run of views of one arena (`params.arena_of_module`);
+    otherwise the tensors are packed into flat scratch buffers on the device first.
+    """
+    state = state or OuterState()
+    base_params = list(base_params)
+    worker_params = [list(w) for w in worker_params]
+    if not worker_params:
+        raise EdtError("no trained models")
+    if len(worker_params) > EDT_MAX_WORKERS:
+        raise EdtError(f"{len(worker_params)} workers; one fused launch takes at most {EDT_MAX_WORKERS}")
+    for w in worker_params:
+        if len(w) != len(base_params) or any(a.shape != b.shape for a, b in zip(w, base_params)):
+            raise EdtError("trained model parameters do not match the base model")
+    with torch.no_grad():
+        theta = flat_view(base_params)
+        copied = theta is None
+        if copied:
+            theta = pack(base_params)
+        flats = []
+        for w in worker_params:
+            f = flat_view(w)
+            flats.append(f if f is not None else pack(w))
+        wdt = {f.dtype for f in flats}
+        if len(wdt) != 1:
+            raise EdtError("all trained models must share one dtype")
+        _step_flat(theta, flats, state, lr, momentum, nesterov)
+        if copied:
+            unpack_(theta, base_params)
+    return state
+
+
+class OuterSync:
+    """Arena-native DiLoCo outer step for a population resident in HBM.
+
+    theta:   global parameters (master) — float32 or bfloat16 arena
+    workers: K replica arenas (bfloat16 or float32) the inner loops trained
+    """
+
+    def __init__(self, theta: ParamArena, workers: list[ParamArena], lr: float = 0.7,
+                 momentum: float = 0.9, nesterov: bool = True, state: OuterState | None = None):
+        self.theta = theta
+        self.workers = workers
+        self.lr, self.momentum, self.nesterov = lr, momentum, nesterov
+        self.state = state or OuterState()
+
+    def step(self) -> None:
+        _step_flat(self.theta.flat, [w.flat for w in self.workers], self.state, self.lr,
+                   self.momentum, self.nesterov)
+
+    def broadcast_(self) -> None:
+        """Start every worker from the new global weights (what saving base_model to every
+        worker dir does, EDT_LM/diloco.py:302-308)."""
+        for w in self.workers:
+            w.flat.copy_(self.theta.flat)
+
+    @property
+    def bytes_reduced(self) -> int:
+        """Metric bytes of one step: K x P x bytes per worker element."""
+        return sum(w.flat.numel() * w.flat.element_size() for w in self.workers)
+
+    def traffic_bytes(self) -> int:
+        """Algorithmic HBM bytes of one fused step: every operand read once / written once."""
+        n = self.theta.flat.numel()
+        b = self.bytes_reduced + 2 * n * self.theta.flat.element_size()
+        if self.momentum != 0:
+            b += (2 if self.state.has_momentum else 1) * n * self.theta.flat.element_size()
+        return b

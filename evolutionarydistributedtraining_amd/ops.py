@@ -1,0 +1,155 @@
+"""Flat-buffer operators: one call = one fused HIP launch over a whole parameter arena.
+
+Every function takes device-resident, contiguous tensors (flat views of the population's
+parameter arenas, see `params.ParamArena`) and launches on the current HIP stream. Nothing here
+synchronises, allocates persistent memory or falls back to the CPU: a missing library or device
+raises `EdtError`.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib as L
+
+
+def outer_step(theta: torch.Tensor, workers: list[torch.Tensor], momentum: torch.Tensor | None,
+               has_momentum: bool, lr: float, momentum_coef: float, nesterov: bool) -> None:
+    """Fused DiLoCo outer step (EDT_LM/diloco.py:238-289): theta and momentum updated in place.
+
+    theta: flat float32/bfloat16; workers: K (<= 32) flat tensors of one dtype; momentum: flat,
+    theta's dtype (required when momentum_coef != 0)."""
+    lib = L.lib()
+    if not 1 <= len(workers) <= L.EDT_MAX_WORKERS:
+        raise L.EdtError(f"{len(workers)} workers: one launch takes 1..{L.EDT_MAX_WORKERS}")
+    L.require_device(theta, momentum, *workers)
+    n = theta.numel()
+    for w in workers:
+        if w.numel() != n or w.dtype != workers[0].dtype:
+            raise L.EdtError("every worker buffer must match theta's size and share one dtype")
+    if momentum is not None and (momentum.numel() != n or momentum.dtype != theta.dtype):
+        raise L.EdtError("momentum must have theta's size and dtype")
+    L.check(lib.edt_outer_step(L.ptr(theta), L.dtype_code(theta), L.ptr_array(workers),
+                               L.dtype_code(workers[0]), len(workers), L.ptr(momentum),
+                               int(has_momentum), n, float(lr), float(momentum_coef),
+                               int(nesterov), L.stream_ptr(theta.device)), "edt_outer_step")
+
+
+def delta_partial(theta: torch.Tensor, workers: list[torch.Tensor], k_total: int,
+                  acc: torch.Tensor, accumulate: bool = False) -> None:
+    """acc (fp32) (+)= sum over the local workers of round((theta_k - theta) / k_total)."""
+    lib = L.lib()
+    L.require_device(theta, acc, *workers)
+    if acc.dtype != torch.float32 or acc.numel() != theta.numel():
+        raise L.EdtError("acc must be a float32 buffer of theta's size")
+    L.check(lib.edt_delta_partial(L.ptr(theta), L.dtype_code(theta), L.ptr_array(workers),
+                                  L.dtype_code(workers[0]), len(workers), int(k_total),
+                                  theta.numel(), L.ptr(acc), int(accumulate),
+                                  L.stream_ptr(theta.device)), "edt_delta_partial")
+
+
+def sgd_apply(theta: torch.Tensor, acc: torch.Tensor, momentum: torch.Tensor | None,
+              has_momentum: bool, lr: float, momentum_coef: float, nesterov: bool) -> None:
+    """grad = -round(acc); torch.optim.SGD step on theta (shard) in place."""
+    lib = L.lib()
+    L.require_device(theta, acc, momentum)
+    if acc.dtype != torch.float32 or acc.numel() != theta.numel():
+        raise L.EdtError("acc must be a float32 buffer of theta's size")
+    L.check(lib.edt_sgd_apply(L.ptr(theta), L.dtype_code(theta), L.ptr(acc), L.ptr(momentum),
+                              int(has_momentum), theta.numel(), float(lr), float(momentum_coef),
+                              int(nesterov), L.stream_ptr(theta.device)), "edt_sgd_apply")
+
+
+def pair_merge(b1: torch.Tensor, b2: torch.Tensor | None, m1: torch.Tensor, m2: torch.Tensor,
+               out: torch.Tensor, momentum: torch.Tensor | None, has_momentum: bool, lr: float,
+               momentum_coef: float, nesterov: bool) -> None:
+    """EDT child = SGD step of lerp(.5, b1, b2) towards m1, m2 (EDT_LM/train/crossover.py:150-230).
+    b2 None: b1 is the already merged base (dtype of `out`)."""
+    lib = L.lib()
+    L.require_device(b1, b2, m1, m2, out, momentum)
+    n = out.numel()
+    if any(t is not None and t.numel() != n for t in (b1, b2, m1, m2, momentum)):
+        raise L.EdtError("pair-merge buffers must all have the same size")
+    L.check(lib.edt_pair_merge(L.ptr(b1), L.ptr(b2), L.ptr(m1), L.ptr(m2), L.dtype_code(m1),
+                               L.ptr(out), L.dtype_code(out), L.ptr(momentum), int(has_momentum), n,
+                               float(lr), float(momentum_coef), int(nesterov),
+                               L.stream_ptr(out.device)), "edt_pair_merge")
+
+
+def lerp(t: float, v0: torch.Tensor, v1: torch.Tensor, out: torch.Tensor | None = None,
+         compute_dtype: torch.dtype | None = None) -> torch.Tensor:
+    """(1-t)*v0 + t*v1 with the rounding of three torch ops in compute_dtype (default: v0's)."""
+    lib = L.lib()
+    cdt = compute_dtype or v0.dtype
+    if out is None:
+        out = torch.empty_like(v0, dtype=cdt)
+    L.require_device(v0, v1, out)
+    if v1.dtype != v0.dtype or v1.numel() != v0.numel() or out.numel() != v0.numel():
+        raise L.EdtError("lerp operands must match")
+    L.check(lib.edt_lerp(L.ptr(v0), L.ptr(v1), L.dtype_code(v0), L.ptr(out), L.dtype_code(out),
+                         L.dtype_code(cdt), v0.numel(), float(t), L.stream_ptr(v0.device)), "edt_lerp")
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+# SLERP over a multi-tensor arena
+
+@dataclass
+class SlerpPlan:
+    """Chunk table for a segment layout, resident on the device (built once per layout)."""
+    seg_offsets: list[int]
+    chunks: torch.Tensor          # int64 [nchunks, 3] = start, length, segment
+    seg_first: torch.Tensor       # int32 [nseg + 1]
+    partial: torch.Tensor         # float64 [nchunks, 3] workspace
+    coef: torch.Tensor            # float32 [nseg, 2]
+    dots: torch.Tensor            # float32 [nseg]
+    nchunks: int
+
+    @property
+    def nseg(self) -> int:
+        return len(self.seg_offsets) - 1
+
+
+def make_slerp_plan(seg_offsets: list[int], device: torch.device,
+                    chunk_elems: int = 1 << 16) -> SlerpPlan:
+    lib = L.load_library()
+    nseg = len(seg_offsets) - 1
+    offs = (ctypes.c_uint64 * max(1, nseg + 1))(*seg_offsets)
+    first = (ctypes.c_int32 * (nseg + 1))()
+    need = lib.edt_slerp_make_chunks(offs, nseg, chunk_elems, None, 0, first)
+    nchunks = -need - 1 if need < 0 else need
+    desc = (ctypes.c_uint64 * max(1, 3 * nchunks))()
+    got = lib.edt_slerp_make_chunks(offs, nseg, chunk_elems, desc, nchunks, first)
+    if got != nchunks:
+        L.check(-1, "edt_slerp_make_chunks")
+    chunks = torch.tensor(list(desc)[:3 * nchunks], dtype=torch.int64).view(-1, 3).to(device)
+    seg_first = torch.tensor(list(first), dtype=torch.int32).to(device)
+    return SlerpPlan(list(seg_offsets), chunks, seg_first,
+                     torch.empty((max(1, nchunks), 3), dtype=torch.float64, device=device),
+                     torch.empty((max(1, nseg), 2), dtype=torch.float32, device=device),
+                     torch.empty(max(1, nseg), dtype=torch.float32, device=device), nchunks)
+
+
+def slerp_arena(plan: SlerpPlan, v0: torch.Tensor, v1: torch.Tensor, out: torch.Tensor,
+                t: torch.Tensor, dot_threshold: float = 0.9995, eps: float = 1e-8) -> None:
+    """SLERP every segment of v0/v1 with its own t (float64 device tensor [nseg]) into out.
+    Three launches: chunk sums, per-segment coefficients, blend (EDT_RL/crossover.py:11-43)."""
+    lib = L.lib()
+    L.require_device(v0, v1, out, t)
+    if v1.dtype != v0.dtype or v0.numel() != plan.seg_offsets[-1] or v1.numel() != v0.numel() \
+            or out.numel() != v0.numel():
+        raise L.EdtError("slerp arenas must match the plan's layout")
+    if t.dtype != torch.float64 or t.numel() < plan.nseg:
+        raise L.EdtError("t must be a float64 device tensor with one value per segment")
+    s = L.stream_ptr(v0.device)
+    idt = L.dtype_code(v0)
+    L.check(lib.edt_slerp_stats(L.ptr(v0), L.ptr(v1), idt, L.ptr(plan.chunks), plan.nchunks,
+                                L.ptr(plan.partial), s), "edt_slerp_stats")
+    L.check(lib.edt_slerp_coef(L.ptr(plan.partial), L.ptr(plan.seg_first), plan.nseg, L.ptr(t),
+                               float(dot_threshold), float(eps), L.ptr(plan.coef), L.ptr(plan.dots),
+                               s), "edt_slerp_coef")
+    L.check(lib.edt_slerp_blend(L.ptr(v0), L.ptr(v1), idt, L.ptr(out), L.dtype_code(out),
+                                L.ptr(plan.chunks), plan.nchunks, L.ptr(plan.coef), s),
+            "edt_slerp_blend")

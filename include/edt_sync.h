@@ -1,0 +1,125 @@
+/*
+ * edt_sync.h — C ABI of the MI355X (gfx950) outer-loop sync library `libedt_sync.so`.
+ *
+ * The reference (BarryFutureman/EvolutionaryDistributedTraining) has no FFI: its hot path is
+ * Python/PyTorch-CPU code. Each entry point below replaces one piece of that code; the
+ * reference location it replaces is cited on the declaration (paths relative to the reference
+ * root). The Python shim `evolutionarydistributedtraining_amd` binds these with ctypes and keeps
+ * the reference's call surfaces.
+ *
+ * Conventions
+ *  - Every pointer argument named *device* is HBM memory owned by the caller (PyTorch tensors,
+ *    `data_ptr()`); the library never allocates device memory and never synchronises.
+ *  - `stream` is a hipStream_t (NULL = the legacy default stream). All work is stream-ordered
+ *    and asynchronous; every call is hipGraph-capturable.
+ *  - Element counts are uint64_t; buffers are flat, parameters laid out back to back in
+ *    `model.parameters()` order (the index order the reference's optimizer state uses).
+ *  - Scalars arrive as doubles and are rounded exactly as the reference's torch/numpy code
+ *    rounds them (fp32 scalar for `mul_`, tensor-dtype `alpha` for `add(..., alpha=)`).
+ *  - Return 0 on success or a negative EDT_ERR_* code; edt_last_error() then holds a
+ *    thread-local message.
+ */
+#ifndef EDT_SYNC_H
+#define EDT_SYNC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum { EDT_F32 = 0, EDT_BF16 = 1 } edt_dtype_t;
+
+enum {
+    EDT_OK = 0,
+    EDT_ERR_ARG = -1,      /* bad argument (null pointer, unsupported dtype pair, K out of range) */
+    EDT_ERR_LAUNCH = -2,   /* kernel launch failed (hipGetLastError) */
+};
+
+#define EDT_MAX_WORKERS 32   /* workers consumed by one fused launch */
+
+/* ---- DiLoCo outer step ------------------------------------------------------------------
+ * Replaces EDT_LM/diloco.py:238-289 (== EDT_LM/diloco_sim.py:233-299):
+ *   acc = 0; for k: acc += (theta_k - theta_g) / K      (worker-major, true division by K)
+ *   grad = -acc; torch.optim.SGD(lr, momentum, nesterov).step()  (single-tensor CPU path)
+ * fused in one pass over HBM. theta_g and momentum are updated in place.
+ * dtype pairs (gdt, wdt): (F32,F32), (F32,BF16) [torch promotion: math in fp32], (BF16,BF16)
+ * [every op rounded to bf16 as torch's CPU kernels do]. momentum has dtype gdt and is only
+ * touched when momentum_coef != 0; has_momentum = 0 reproduces the first step
+ * (`buf = grad.clone()`), 1 the carried buffer (`load_state_dict` carry, diloco.py:258-286).
+ * theta_k: host array of K device pointers, 1 <= K <= EDT_MAX_WORKERS. */
+int edt_outer_step(void* theta_g, int gdt, const void* const* theta_k, int wdt, int K,
+                   void* momentum, int has_momentum, uint64_t n,
+                   double lr, double momentum_coef, int nesterov, void* stream);
+
+/* Partial delta sum for the sharded multi-GPU step (EDT_LM/diloco.py:243-246 restricted to the
+ * workers resident on this rank): acc_f32[i] (+)= sum_{k<K_local} round_g((theta_k - theta_g)/K_total).
+ * accumulate = 0 starts from zero, 1 continues the running fp32 sum already in acc_f32 (so two
+ * launches over workers [0,a) and [a,K) add in the same order as one launch over [0,K)).
+ * The cross-rank sum then goes over RCCL. */
+int edt_delta_partial(const void* theta_g, int gdt, const void* const* theta_k, int wdt,
+                      int K_local, int K_total, uint64_t n, float* acc_f32, int accumulate,
+                      void* stream);
+
+/* SGD on a shard from a reduced fp32 pseudo-gradient sum: grad = -round_g(acc_f32), then the
+ * torch.optim.SGD single-tensor update of EDT_LM/diloco.py:252-289. */
+int edt_sgd_apply(void* theta_g, int gdt, const float* acc_f32, void* momentum, int has_momentum,
+                  uint64_t n, double lr, double momentum_coef, int nesterov, void* stream);
+
+/* ---- EDT pairwise merge -------------------------------------------------------------------
+ * Replaces EDT_LM/train/crossover.py:150-163 + 166-230 for one child:
+ *   B = lerp(0.5, b1, b2)                         (run_linear_merge_5050, in the model dtype wdt)
+ *   d = ((m1 - B) + (m2 - B)) / 2 ; grad = -d      (run_sgd, in the base dtype gdt)
+ *   SGD(lr, momentum, nesterov).step() with the parent's momentum when has_momentum = 1.
+ * Writes the child parameters to theta_out (gdt) and the new momentum buffer in place.
+ * The parents' bases b1/b2 and trained weights m1/m2 have dtype wdt. b2 may be NULL: b1 is
+ * then the already merged base of dtype gdt (run_sgd called on a given base_model). */
+int edt_pair_merge(const void* b1, const void* b2, const void* m1, const void* m2, int wdt,
+                   void* theta_out, int gdt, void* momentum, int has_momentum, uint64_t n,
+                   double lr, double momentum_coef, int nesterov, void* stream);
+
+/* lerp(t, v0, v1) = (1-t)*v0 + t*v1 as three rounded ops in compute dtype cdt (= the tensors'
+ * dtype for torch, F32 for numpy), stored as out_dt.
+ * Replaces EDT_LM/train/crossover.py:50-51 / EDT_RL/crossover.py:46-47 when applied per tensor. */
+int edt_lerp(const void* v0, const void* v1, int in_dt, void* out, int out_dt, int cdt,
+             uint64_t n, double t, void* stream);
+
+/* ---- SLERP crossover (EDT_RL/crossover.py:11-43, EDT_EVOMERGE/train/crossover.py:14-46) ------
+ * Multi-tensor: the parents v0, v1 are flat buffers holding `nseg` tensors; segment s spans
+ * [seg_offsets[s], seg_offsets[s+1]). Work is cut into chunks that never cross a segment.
+ *
+ * edt_slerp_make_chunks (HOST function): fills chunk_desc (3 uint64 per chunk:
+ *   start, length, segment) and seg_first_chunk (nseg+1) for chunk length `chunk_elems`;
+ *   returns the chunk count, or the required count (negated - 1) if max_chunks is too small. */
+int64_t edt_slerp_make_chunks(const uint64_t* seg_offsets_host, int nseg, uint32_t chunk_elems,
+                              uint64_t* chunk_desc_host, int64_t max_chunks,
+                              int32_t* seg_first_chunk_host);
+
+/* Pass 1: per-chunk sums  partial[c] = { sum v0^2, sum v1^2, sum v0*v1 }  (fp64). */
+int edt_slerp_stats(const void* v0, const void* v1, int in_dt, const uint64_t* chunk_desc,
+                    int64_t nchunks, double* partial, void* stream);
+
+/* Per segment: reduce the chunk sums in a fixed order, form the norms, the normalised dot and
+ * the blend coefficients coef[2s], coef[2s+1] exactly as the reference's branch does:
+ *   |dot| > dot_threshold -> (1-t, t) (lerp);  else (sin((1-t)th)/sin th, sin(t th)/sin th).
+ * t: device array of nseg doubles (interpolate_t / global t per key). dot_out (nullable): the
+ * fp32 dot per segment. */
+int edt_slerp_coef(const double* partial, const int32_t* seg_first_chunk, int nseg,
+                   const double* t, double dot_threshold, double eps, float* coef,
+                   float* dot_out, void* stream);
+
+/* Pass 2: out = coef0*v0 + coef1*v1 in fp32 (numpy: two rounded products, one rounded sum),
+ * stored as out_dt (RN to bf16 when the merged model is bf16, EDT_EVOMERGE/train/crossover.py:142). */
+int edt_slerp_blend(const void* v0, const void* v1, int in_dt, void* out, int out_dt,
+                    const uint64_t* chunk_desc, int64_t nchunks, const float* coef, void* stream);
+
+/* ---- misc ---- */
+const char* edt_last_error(void);
+const char* edt_version(void);
+/* bytes of device memory the kernels above may touch per element, for roofline accounting */
+int edt_outer_step_bytes_per_elem(int gdt, int wdt, int K, int with_momentum);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EDT_SYNC_H */

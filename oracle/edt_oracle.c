@@ -1,0 +1,208 @@
+/*
+ * edt_oracle.c — CPU restatement of the reference's outer-loop sync arithmetic.
+ *
+ * TEST INFRASTRUCTURE ONLY. This is the checker the parity tests, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg compare the HIP kernels against; the product library never links
+ * or calls it. It is pinned against golden vectors produced by the reference's own code
+ * (tests/golden/gen_golden.py -> tests/test_oracle_golden.py).
+ *
+ * Each function restates, element by element and in the same op order, what the reference's
+ * PyTorch CPU ops compute:
+ *   oracle_outer_step   EDT_LM/diloco.py:238-289 (== EDT_LM/diloco_sim.py:233-299)
+ *                       + torch/optim/sgd.py _single_tensor_sgd (momentum, nesterov)
+ *   oracle_pair_merge   EDT_LM/train/crossover.py:150-163 (lerp .5) + 166-230 (run_sgd)
+ *   oracle_lerp         EDT_LM/train/crossover.py:50-51 on torch tensors / EDT_RL/crossover.py:46-47
+ * Rounding model (verified against the goldens):
+ *   fp32  : one IEEE op per torch op; add(x, y, alpha=a) == fmaf(a, y, x); x / K true division.
+ *   bf16  : every op computed in fp32, then rounded to bf16 RNE (c10::BFloat16); the alpha of
+ *           add(..., alpha=a) is first rounded to bf16; mul_(s) uses the fp32 scalar.
+ *           torch's CPU add(x, y, alpha) is vectorised: x + alpha*y is ONE fp32 fma rounded to
+ *           bf16 -- except on the scalar tail of each contiguous run its vectorised loop handles
+ *           (the last numel % 32 elements of a tensor, per parallel chunk, on an AVX-512 host),
+ *           where it is BFloat16 arithmetic: round(x + round(alpha*y)). `tail` (nullable, one
+ *           byte per element, 1 = scalar-tail element) selects that form, so the oracle can
+ *           reproduce the reference bit for bit; tail = NULL is the vectorised semantics the HIP
+ *           kernels implement on every element.
+ * Build: see oracle/Makefile (gcc -O2 -ffp-contract=off: no FMA except the explicit fmaf()).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+enum { OR_F32 = 0, OR_BF16 = 1 };
+
+static inline float bf2f(uint16_t h) {
+    uint32_t u = (uint32_t)h << 16;
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+}
+
+static inline uint16_t f2bf(float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0;        /* NaN, as c10 */
+    return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+/* value of x rounded to dtype dt, as fp32 */
+static inline float rnd(int dt, float x) { return dt == OR_BF16 ? bf2f(f2bf(x)) : x; }
+
+static inline float load(const void* p, int dt, uint64_t i) {
+    return dt == OR_BF16 ? bf2f(((const uint16_t*)p)[i]) : ((const float*)p)[i];
+}
+
+static inline void store(void* p, int dt, uint64_t i, float x) {
+    if (dt == OR_BF16) ((uint16_t*)p)[i] = f2bf(x);
+    else ((float*)p)[i] = x;
+}
+
+typedef struct {
+    float mul_mu, alpha_mu, alpha_nlr;
+    int use_mom, has_buf, nesterov;
+} sgd_t;
+
+static sgd_t make_sgd(int gdt, double lr, double mu, int has_buf, int nesterov) {
+    sgd_t s;
+    s.mul_mu = (float)mu;                         /* buf.mul_(momentum): fp32 opmath scalar */
+    s.alpha_mu = rnd(gdt, (float)mu);             /* alpha cast to the tensor dtype */
+    s.alpha_nlr = rnd(gdt, (float)(-lr));
+    s.use_mom = mu != 0.0;
+    s.has_buf = has_buf;
+    s.nesterov = nesterov;
+    return s;
+}
+
+/* add(x, y, alpha=a) in dtype dt: vectorised form, or BFloat16 scalar-tail form */
+static inline float add_alpha(int dt, float x, float a, float y, int scalar_tail) {
+    if (dt == OR_BF16 && scalar_tail) return rnd(dt, x + rnd(dt, a * y));
+    return rnd(dt, fmaf(a, y, x));
+}
+
+/* torch.optim.SGD single-tensor step on one element; returns the new parameter. */
+static inline float sgd_elem(int gdt, const sgd_t* s, float theta, float grad, void* mom, uint64_t i,
+                             int tail) {
+    float u = grad;
+    if (s->use_mom) {
+        float b;
+        if (s->has_buf) {
+            b = rnd(gdt, load(mom, gdt, i) * s->mul_mu);  /* buf.mul_(momentum) */
+            b = rnd(gdt, b + grad);                       /* .add_(grad, alpha=1 - dampening) */
+        } else {
+            b = grad;                                     /* buf = grad.clone() */
+        }
+        store(mom, gdt, i, b);
+        u = s->nesterov ? add_alpha(gdt, grad, s->alpha_mu, b, tail) : b;   /* grad.add(buf, alpha=mu) */
+    }
+    return add_alpha(gdt, theta, s->alpha_nlr, u, tail);                   /* param.add_(grad, alpha=-lr) */
+}
+
+/* DiLoCo outer step, in place on theta (gdt) and mom (gdt). */
+int oracle_outer_step(void* theta, int gdt, const void* const* workers, int wdt, int K, void* mom,
+                      int has_buf, uint64_t n, double lr, double mu, int nesterov,
+                      const uint8_t* tail) {
+    if (K < 1) return -1;
+    if (gdt == OR_BF16 && wdt != OR_BF16) return -1;
+    const sgd_t s = make_sgd(gdt, lr, mu, has_buf, nesterov);
+    const float kf = (float)K;
+#pragma omp parallel for schedule(static)
+    for (int64_t ii = 0; ii < (int64_t)n; ++ii) {
+        const uint64_t i = (uint64_t)ii;
+        const float g = load(theta, gdt, i);
+        float acc = 0.0f;                                           /* zeros_like(base) */
+        for (int k = 0; k < K; ++k) {
+            float d = rnd(gdt, load(workers[k], wdt, i) - g);       /* trained - base */
+            d = rnd(gdt, d / kf);                                   /* delta / num_models */
+            acc = rnd(gdt, acc + d);                                /* acc += ... */
+        }
+        store(theta, gdt, i, sgd_elem(gdt, &s, g, -acc, mom, i, tail ? tail[i] : 0));   /* grad = -acc */
+    }
+    return 0;
+}
+
+/* Sharded form, part 1: acc (+)= sum_k round_g(round_g(w_k - g) / K_total), fp32 running sum
+ * (accumulate = 1 continues from acc). Restates EDT_LM/diloco.py:243-246 over a worker subset. */
+int oracle_delta_partial(const void* theta, int gdt, const void* const* workers, int wdt, int K,
+                         int K_total, uint64_t n, float* acc, int accumulate) {
+    if (gdt == OR_BF16 && wdt != OR_BF16) return -1;
+    const float kf = (float)K_total;
+#pragma omp parallel for schedule(static)
+    for (int64_t ii = 0; ii < (int64_t)n; ++ii) {
+        const uint64_t i = (uint64_t)ii;
+        const float g = load(theta, gdt, i);
+        float a = accumulate ? acc[i] : 0.0f;
+        for (int k = 0; k < K; ++k) {
+            float d = rnd(gdt, load(workers[k], wdt, i) - g);
+            d = rnd(gdt, d / kf);
+            a = a + d;
+        }
+        acc[i] = a;
+    }
+    return 0;
+}
+
+/* Sharded form, part 2: grad = -round_g(acc); SGD step (diloco.py:248-289). */
+int oracle_sgd_apply(void* theta, int gdt, const float* acc, void* mom, int has_buf, uint64_t n,
+                     double lr, double mu, int nesterov) {
+    const sgd_t s = make_sgd(gdt, lr, mu, has_buf, nesterov);
+#pragma omp parallel for schedule(static)
+    for (int64_t ii = 0; ii < (int64_t)n; ++ii) {
+        const uint64_t i = (uint64_t)ii;
+        const float g = load(theta, gdt, i);
+        store(theta, gdt, i, sgd_elem(gdt, &s, g, -rnd(gdt, acc[i]), mom, i, 0));
+    }
+    return 0;
+}
+
+/* EDT pair merge for one child: base = lerp(.5, b1, b2) in wdt (b2 == NULL: b1 is the base, gdt),
+ * d = ((m1-B)+(m2-B))/2 in gdt, SGD; writes theta_out (gdt) and mom (gdt). */
+int oracle_pair_merge(const void* b1, const void* b2, const void* m1, const void* m2, int wdt,
+                      void* theta_out, int gdt, void* mom, int has_buf, uint64_t n, double lr,
+                      double mu, int nesterov, const uint8_t* tail) {
+    if (gdt == OR_BF16 && wdt != OR_BF16) return -1;
+    const sgd_t s = make_sgd(gdt, lr, mu, has_buf, nesterov);
+#pragma omp parallel for schedule(static)
+    for (int64_t ii = 0; ii < (int64_t)n; ++ii) {
+        const uint64_t i = (uint64_t)ii;
+        float base;
+        if (b2) {
+            const float x = rnd(wdt, 0.5f * load(b1, wdt, i));     /* (1 - 0.5) * v0 */
+            const float y = rnd(wdt, 0.5f * load(b2, wdt, i));     /* 0.5 * v1 */
+            base = rnd(wdt, x + y);
+        } else {
+            base = load(b1, gdt, i);                                /* merged base, dtype gdt */
+        }
+        base = rnd(gdt, base);                                      /* load_state_dict copy */
+        const float d1 = rnd(gdt, load(m1, wdt, i) - base);
+        const float d2 = rnd(gdt, load(m2, wdt, i) - base);
+        float d = rnd(gdt, d1 + d2);
+        d = rnd(gdt, d / 2.0f);                                     /* / num_models */
+        const float acc = rnd(gdt, 0.0f + d);                       /* zeros + delta */
+        store(theta_out, gdt, i, sgd_elem(gdt, &s, base, -acc, mom, i, tail ? tail[i] : 0));
+    }
+    return 0;
+}
+
+/* (1-t)*v0 + t*v1 with three rounded ops in compute dtype cdt, stored as out_dt. */
+int oracle_lerp(const void* v0, const void* v1, int in_dt, void* out, int out_dt, int cdt,
+                uint64_t n, double t) {
+    const float c0 = (float)(1.0 - t), c1 = (float)t;
+#pragma omp parallel for schedule(static)
+    for (int64_t ii = 0; ii < (int64_t)n; ++ii) {
+        const uint64_t i = (uint64_t)ii;
+        const float x = rnd(cdt, c0 * load(v0, in_dt, i));
+        const float y = rnd(cdt, c1 * load(v1, in_dt, i));
+        store(out, out_dt, i, rnd(cdt, x + y));
+    }
+    return 0;
+}
+
+/* Threads the OpenMP loops above may use (for the bench's cpu_baseline report). */
+int oracle_max_threads(void) {
+#ifdef _OPENMP
+    extern int omp_get_max_threads(void);
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}

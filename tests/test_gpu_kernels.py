@@ -1,0 +1,287 @@
+"""HIP kernels vs the CPU oracle and the reference's golden vectors (needs an MI355X).
+
+Bars (stated per test):
+  * vs the oracle in its vectorised-torch semantics (tail=None): bit-exact, every element.
+  * vs the reference goldens: fp32 regimes bit-exact; bf16 regime bit-exact except on the
+    elements torch's CPU kernels send down their scalar tail (oracle.torch_cpu_tail_mask), where
+    the reference itself rounds add(..., alpha) twice: there |diff| <= 1 bf16 ulp.
+  * SLERP: the reference's dot is an fp32 BLAS/pairwise sum; ours is an fp64 sum. Coefficients
+    agree to ~1e-6 relative, so |out - ref| <= 2e-6 * (|c0 v0| + |c1 v1|) + 1e-30.
+"""
+import json
+import os
+
+import pytest
+import torch
+
+from tests.golden_data import GOLDEN_DIR, bits, flat
+
+pytestmark = pytest.mark.gpu
+
+with open(os.path.join(GOLDEN_DIR, "manifest.json")) as _f:
+    _M = json.load(_f)
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from evolutionarydistributedtraining_amd import ops as o
+    return o
+
+
+def ulp_bf16(x: torch.Tensor) -> torch.Tensor:
+    """Size of one bf16 ulp at |x| (as float32)."""
+    a = x.float().abs().clamp_min(torch.finfo(torch.bfloat16).tiny)
+    e = torch.floor(torch.log2(a))
+    return torch.exp2(e - 7)
+
+
+def assert_matches_reference(got, want, tail, what):
+    if got.dtype == torch.float32:
+        assert torch.equal(bits(got), bits(want)), f"{what}: fp32 not bit-exact"
+        return
+    diff = bits(got) != bits(want)
+    outside = diff & (tail == 0)
+    assert not outside.any(), f"{what}: {int(outside.sum())} mismatches outside torch's scalar tails"
+    if diff.any():
+        d = (got.float() - want.float()).abs()[diff]
+        assert (d <= ulp_bf16(want[diff]) * 1.0001).all(), f"{what}: tail diff > 1 ulp"
+
+
+@pytest.mark.parametrize("idx", range(len(_M["diloco"])))
+def test_diloco_golden(golden, oracle, dev, ops, idx):
+    c = golden.diloco_cases()[idx]
+    T = len(c["shapes"])
+    numels = [int(torch.Size(s).numel()) for s in c["shapes"]]
+    tail = oracle.torch_cpu_tail_mask(numels)
+    prev_buf = None
+    for step in c["steps"]:
+        pre = step["prefix"]
+        theta = flat(golden.tlist("diloco", f"{pre}/base", T)).contiguous()
+        workers = [flat(golden.tlist("diloco", f"{pre}/worker{k}", T)).contiguous() for k in range(c["K"])]
+        mu = c["momentum"]
+        if mu == 0:
+            mom, has = None, False
+        elif prev_buf is None:
+            mom, has = torch.zeros_like(theta), False
+        else:
+            mom, has = prev_buf.clone(), True
+        th_d = theta.to(dev)
+        mom_d = None if mom is None else mom.to(dev)
+        ops.outer_step(th_d, [w.to(dev) for w in workers], mom_d, has, c["lr"], mu, c["nesterov"])
+        # oracle, vectorised semantics: bit-exact on every element
+        oracle.outer_step(theta, workers, mom, has, c["lr"], mu, c["nesterov"])
+        got = th_d.cpu()
+        assert torch.equal(bits(got), bits(theta)), f"{pre}: kernel != oracle"
+        want = flat(golden.tlist("diloco", f"{pre}/out_theta", T))
+        assert_matches_reference(got, want, tail, pre)
+        if step["has_out_buf"]:
+            gb = mom_d.cpu()
+            assert torch.equal(bits(gb), bits(mom)), f"{pre}: momentum kernel != oracle"
+            assert torch.equal(bits(gb), bits(flat(golden.tlist("diloco", f"{pre}/out_buf", T))))
+            prev_buf = gb
+
+
+def _rand_case(n, K, gdt, wdt, seed):
+    g = torch.Generator().manual_seed(seed)
+    theta = (torch.randn(n, generator=g) * 0.02).to(gdt)
+    workers = [(theta.float() + torch.randn(n, generator=g) * 1e-3).to(wdt) for _ in range(K)]
+    mom = (torch.randn(n, generator=g) * 1e-3).to(gdt)
+    return theta, workers, mom
+
+
+REGIMES = [(torch.float32, torch.float32), (torch.float32, torch.bfloat16), (torch.bfloat16, torch.bfloat16)]
+
+
+@pytest.mark.parametrize("gdt,wdt", REGIMES)
+@pytest.mark.parametrize("K", [1, 2, 3, 4, 5, 8, 16, 32])
+@pytest.mark.parametrize("n", [1, 7, 8, 9, 4097, 1_000_003])
+def test_outer_step_vs_oracle(oracle, dev, ops, gdt, wdt, K, n):
+    if n == 1_000_003 and K not in (3, 8, 32):
+        pytest.skip("large size: representative K only")
+    theta, workers, mom = _rand_case(n, K, gdt, wdt, seed=K * 1000 + n)
+    for has, (lr, mu, nest) in [(False, (0.7, 0.9, True)), (True, (0.7, 0.9, True)),
+                                (True, (0.5, 0.8, False)), (False, (1.0, 0.0, False))]:
+        th, m = theta.clone(), mom.clone()
+        th_d, m_d = th.to(dev), m.to(dev)
+        ops.outer_step(th_d, [w.to(dev) for w in workers], m_d if mu else None, has, lr, mu, nest)
+        oracle.outer_step(th, workers, m if mu else None, has, lr, mu, nest)
+        assert torch.equal(bits(th_d.cpu()), bits(th)), (has, lr, mu, nest)
+        if mu:
+            assert torch.equal(bits(m_d.cpu()), bits(m))
+
+
+@pytest.mark.parametrize("gdt,wdt", REGIMES)
+def test_outer_step_misaligned_views(oracle, dev, ops, gdt, wdt):
+    """Views starting off a 16-byte boundary take the scalar path; results are unchanged."""
+    n, K = 3001, 3
+    theta, workers, mom = _rand_case(n + 1, K, gdt, wdt, seed=7)
+    th_d = theta.to(dev)[1:]
+    ws_d = [w.to(dev)[1:] for w in workers]
+    m_d = mom.to(dev)[1:]
+    ops.outer_step(th_d, ws_d, m_d, True, 0.7, 0.9, True)
+    th, m = theta[1:].clone(), mom[1:].clone()
+    oracle.outer_step(th, [w[1:].clone() for w in workers], m, True, 0.7, 0.9, True)
+    assert torch.equal(bits(th_d.cpu()), bits(th))
+    assert torch.equal(bits(m_d.cpu()), bits(m))
+
+
+def test_outer_step_edge_values(oracle, dev, ops):
+    """Signed zeros, identical replicas, subnormals, large values and deltas."""
+    vals = torch.tensor([0.0, -0.0, 1e-40, -1e-40, 3.0, -2.5, 1e30, -3e38, 1.0, 0.02])
+    theta = vals.clone()
+    workers = [vals.clone(), vals + torch.tensor([1e-3, -0.0, 1e-40, 0, 0.25, 0, 1e29, 0, -1e-7, 5e-4])]
+    for gdt in (torch.float32, torch.bfloat16):
+        th, ws = theta.to(gdt), [w.to(gdt) for w in workers]
+        m = torch.zeros_like(th)
+        th_d, m_d = th.to(dev), m.to(dev)
+        ops.outer_step(th_d, [w.to(dev) for w in ws], m_d, False, 0.7, 0.9, True)
+        oracle.outer_step(th, ws, m, False, 0.7, 0.9, True)
+        assert torch.equal(bits(th_d.cpu()), bits(th))
+
+
+@pytest.mark.parametrize("gdt,wdt", REGIMES)
+def test_partial_then_sgd(oracle, dev, ops, gdt, wdt):
+    """Sharded form: fp32 partial sums + sgd_apply == fused step (fp32 regimes: bit-exact,
+    the fp32 partial accumulates in the same order; bf16: <= 1 bf16 ulp, the fused form
+    rounds the running sum to bf16 after every worker, as the reference does)."""
+    n, K = 100_003, 4
+    theta, workers, mom = _rand_case(n, K, gdt, wdt, seed=11)
+    th_d, m_d = theta.to(dev), mom.to(dev)
+    ws_d = [w.to(dev) for w in workers]
+    acc = torch.empty(n, dtype=torch.float32, device=dev)
+    ops.delta_partial(th_d, ws_d[:2], K, acc, accumulate=False)
+    ops.delta_partial(th_d, ws_d[2:], K, acc, accumulate=True)
+    ops.sgd_apply(th_d, acc, m_d, True, 0.7, 0.9, True)
+    th, m = theta.clone(), mom.clone()
+    oracle.outer_step(th, workers, m, True, 0.7, 0.9, True)
+    got = th_d.cpu()
+    if gdt == torch.float32:
+        assert torch.equal(bits(got), bits(th))
+    else:
+        d = (got.float() - th.float()).abs()
+        assert (d <= ulp_bf16(th) * 1.0001).all()
+
+
+@pytest.mark.parametrize("idx", range(len(_M["pair_merge"])))
+def test_pair_merge_golden(golden, oracle, dev, ops, idx):
+    from tests.test_oracle_golden import pair_inputs
+    c = golden.pair_cases()[idx]
+    p = pair_inputs(golden, c)
+    tail = oracle.torch_cpu_tail_mask([int(torch.Size(s).numel()) for s in c["shapes"]])
+    n = p["b1"].numel()
+    out_d = torch.empty(n, dtype=p["bdt"], device=dev)
+    mom_d = None if p["mom"] is None else p["mom"].to(dev)
+    ops.pair_merge(p["b1"].to(dev), p["b2"].to(dev), p["m1"].to(dev), p["m2"].to(dev), out_d, mom_d,
+                   p["has"], p["lr"], p["mu"], p["nesterov"])
+    out = torch.empty(n, dtype=p["bdt"])
+    mom = None if p["mom"] is None else p["mom"].clone()
+    oracle.pair_merge(p["b1"], p["b2"], p["m1"], p["m2"], out, mom, p["has"], p["lr"], p["mu"], p["nesterov"])
+    assert torch.equal(bits(out_d.cpu()), bits(out)), "kernel != oracle"
+    assert_matches_reference(out_d.cpu(), p["want_theta"], tail, c["name"])
+    if p["want_buf"] is not None:
+        assert torch.equal(bits(mom_d.cpu()), bits(p["want_buf"].to(p["bdt"])))
+    # merged base alone (run_linear_merge_5050)
+    base_d = ops.lerp(0.5, p["b1"].to(dev), p["b2"].to(dev)).to(p["bdt"])
+    assert torch.equal(bits(base_d.cpu()), bits(p["want_base"]))
+    # base-given form (run_sgd on a merged base model)
+    out2 = torch.empty_like(out_d)
+    mom2 = None if p["mom"] is None else pair_inputs(golden, c)["mom"].to(dev)
+    ops.pair_merge(base_d, None, p["m1"].to(dev), p["m2"].to(dev), out2, mom2, p["has"], p["lr"], p["mu"],
+                   p["nesterov"])
+    assert torch.equal(bits(out2.cpu()), bits(out))
+
+
+@pytest.mark.parametrize("in_dt,cdt,out_dt", [(torch.float32, torch.float32, torch.float32),
+                                              (torch.bfloat16, torch.bfloat16, torch.bfloat16),
+                                              (torch.bfloat16, torch.float32, torch.float32),
+                                              (torch.bfloat16, torch.float32, torch.bfloat16)])
+@pytest.mark.parametrize("t", [0.0, 0.5, 0.43333333333333335, 1.0])
+def test_lerp_vs_oracle(oracle, dev, ops, in_dt, cdt, out_dt, t):
+    g = torch.Generator().manual_seed(3)
+    n = 70_001
+    v0 = (torch.randn(n, generator=g) * 0.02).to(in_dt)
+    v1 = (torch.randn(n, generator=g) * 0.02).to(in_dt)
+    out_d = torch.empty(n, dtype=out_dt, device=dev)
+    ops.lerp(t, v0.to(dev), v1.to(dev), out=out_d, compute_dtype=cdt)
+    want = oracle.lerp(t, v0, v1, compute_dtype=cdt, out_dtype=out_dt)
+    assert torch.equal(bits(out_d.cpu()), bits(want))
+
+
+def _slerp_tol(c0, c1, v0, v1):
+    return 2e-6 * (abs(float(c0)) * v0.float().abs() + abs(float(c1)) * v1.float().abs()) + 1e-30
+
+
+def test_slerp_golden(golden, oracle, dev, ops):
+    """Each golden SLERP case as a one-segment arena: branch, dot and output vs the reference."""
+    t = golden.tensors("slerp")
+    for c in golden.slerp_cases():
+        v0, v1 = t[f"{c['inputs']}/v0"].reshape(-1), t[f"{c['inputs']}/v1"].reshape(-1)
+        want = t[f"{c['name']}/out"].reshape(-1)
+        n = v0.numel()
+        plan = ops.make_slerp_plan([0, n], dev, chunk_elems=1024)
+        out_d = torch.empty(n, dtype=torch.float32, device=dev)
+        ops.slerp_arena(plan, v0.to(dev), v1.to(dev), out_d,
+                        torch.tensor([c["t"]], dtype=torch.float64, device=dev))
+        dot = plan.dots[0].item()
+        assert abs(dot - c["ref_dot"]) <= 2e-6, (c["name"], dot, c["ref_dot"])
+        assert (abs(dot) > 0.9995) == c["lerp_branch"], c["name"]
+        c0, c1, _ = oracle.slerp_coefficients(c["t"], v0, v1)
+        got = out_d.cpu()
+        err = (got - want).abs()
+        assert (err <= _slerp_tol(c0, c1, v0, v1)).all(), (c["name"], err.max().item())
+        if c["lerp_branch"]:
+            assert torch.equal(bits(got), bits(want)), c["name"]   # same coefficients -> exact
+
+
+@pytest.mark.parametrize("in_dt,out_dt", [(torch.float32, torch.float32), (torch.bfloat16, torch.float32),
+                                          (torch.bfloat16, torch.bfloat16)])
+def test_slerp_multi_segment(oracle, dev, ops, in_dt, out_dt):
+    """Ragged multi-tensor arena (empty, 1-element, odd, chunk-crossing segments), per-segment t."""
+    g = torch.Generator().manual_seed(5)
+    sizes = [0, 1, 7, 33, 4096, 70_001, 0, 129, 200_000]
+    offs = [0]
+    for s in sizes:
+        offs.append(offs[-1] + s)
+    v0 = torch.randn(offs[-1], generator=g) * 0.02
+    v1 = v0 + torch.randn(offs[-1], generator=g) * 0.02 * 0.05
+    v1[offs[4]:offs[5]] = 2 * v0[offs[4]:offs[5]]               # parallel -> lerp branch
+    v0[offs[7]:offs[8]] = 0                                      # zero tensor
+    v0, v1 = v0.to(in_dt), v1.to(in_dt)
+    ts = torch.tensor([0.5, 0.0, 1.0, 0.43333333333333335, 0.5, 0.7, 0.5, 0.2, 0.9], dtype=torch.float64)
+    plan = ops.make_slerp_plan(offs, dev, chunk_elems=4096)
+    out_d = torch.empty(offs[-1], dtype=out_dt, device=dev)
+    ops.slerp_arena(plan, v0.to(dev), v1.to(dev), out_d, ts.to(dev))
+    got = out_d.cpu().float()
+    for s in range(len(sizes)):
+        a, b = offs[s], offs[s + 1]
+        if a == b:
+            continue
+        want = oracle.slerp(float(ts[s]), v0[a:b], v1[a:b])
+        c0, c1, _ = oracle.slerp_coefficients(float(ts[s]), v0[a:b], v1[a:b])
+        tol = _slerp_tol(c0, c1, v0[a:b], v1[a:b])
+        if out_dt == torch.bfloat16:
+            want = want.bfloat16().float()
+            tol = tol + ulp_bf16(want)
+        assert ((got[a:b] - want).abs() <= tol).all(), s
+
+
+def test_errors_are_raised(dev, ops):
+    from evolutionarydistributedtraining_amd import EdtError
+    th = torch.zeros(16, device=dev)
+    with pytest.raises(EdtError):
+        ops.outer_step(th, [], None, False, 0.7, 0.0, False)
+    with pytest.raises(EdtError):
+        ops.outer_step(th, [torch.zeros(15, device=dev)], None, False, 0.7, 0.0, False)
+    with pytest.raises(EdtError):
+        ops.outer_step(th, [torch.zeros(16, device=dev)] * 33, None, False, 0.7, 0.0, False)
+    with pytest.raises(EdtError):   # bf16 master with fp32 workers is not a torch-promotable pair
+        ops.outer_step(th.bfloat16(), [torch.zeros(16, device=dev)], None, False, 0.7, 0.0, False)
+    with pytest.raises(EdtError):   # host tensors are refused: no CPU path
+        ops.outer_step(torch.zeros(16), [torch.zeros(16)], None, False, 0.7, 0.0, False)
