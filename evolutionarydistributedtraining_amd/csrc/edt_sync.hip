@@ -24,9 +24,28 @@
 
 namespace {
 
-constexpr int kBlock = 256;        // 4 waves
-constexpr int kVec = 8;            // elements per thread per iteration
-constexpr int kMaxBlocks = 2048;   // 256 CUs x 8 resident workgroups
+// Tunables (overridable at build time for the variant sweep in scripts/kernel_variants.py).
+// Measured on MI355X, 1.3B params x 8 bf16 workers (profiles/r01_variants.txt): 256 blocks per
+// CU (short grid-stride runs, no tail of late blocks) + non-temporal worker loads is fastest,
+// 6.78 ms = 6.21 TB/s vs 7.36 ms for 8 blocks per CU with default-policy loads.
+#ifndef EDT_BLOCKS_PER_CU
+#define EDT_BLOCKS_PER_CU 256
+#endif
+#ifndef EDT_NT_LOADS          // non-temporal loads for the once-read worker streams
+#define EDT_NT_LOADS 1
+#endif
+#ifndef EDT_NT_STORES         // non-temporal stores for theta / momentum
+#define EDT_NT_STORES 0
+#endif
+
+#ifndef EDT_MIN_WAVES           // __launch_bounds__ minimum waves per SIMD for the stream kernels
+#define EDT_MIN_WAVES 1
+#endif
+
+constexpr int kBlock = 256;                         // 4 waves
+constexpr int kVec = 8;                             // elements per thread per iteration
+// grid cap for the grid-stride loops: 256 CUs x workgroups per CU (0 = one pass, no cap)
+constexpr uint64_t kMaxBlocks = EDT_BLOCKS_PER_CU > 0 ? 256ull * EDT_BLOCKS_PER_CU : (1ull << 31) - 1;
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -89,13 +108,24 @@ __device__ __forceinline__ void rnd(float (&x)[N]) {
 
 // Load / store N (= 8 or 1) consecutive elements of a buffer of dtype DT as fp32.
 // Index `i` is the element index of the first element (a multiple of 8 when N == 8).
-template <int DT, int N>
+template <typename V, bool NT>
+__device__ __forceinline__ V vload(const V* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <typename V, bool NT>
+__device__ __forceinline__ void vstore(V* p, V v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+template <int DT, int N, bool NT = false>
 __device__ __forceinline__ void ld(const void* __restrict__ p, uint64_t i, float (&x)[N]) {
     if constexpr (DT == EDT_F32) {
         const float* q = static_cast<const float*>(p) + i;
         if constexpr (N == 8) {
-            f32x4 a = *reinterpret_cast<const f32x4*>(q);
-            f32x4 b = *reinterpret_cast<const f32x4*>(q + 4);
+            f32x4 a = vload<f32x4, NT>(reinterpret_cast<const f32x4*>(q));
+            f32x4 b = vload<f32x4, NT>(reinterpret_cast<const f32x4*>(q + 4));
             x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
             x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
         } else {
@@ -105,7 +135,7 @@ __device__ __forceinline__ void ld(const void* __restrict__ p, uint64_t i, float
     } else {
         const uint16_t* q = static_cast<const uint16_t*>(p) + i;
         if constexpr (N == 8) {
-            u32x4 w = *reinterpret_cast<const u32x4*>(q);
+            u32x4 w = vload<u32x4, NT>(reinterpret_cast<const u32x4*>(q));
             x[0] = bf_lo(w.x); x[1] = bf_hi(w.x); x[2] = bf_lo(w.y); x[3] = bf_hi(w.y);
             x[4] = bf_lo(w.z); x[5] = bf_hi(w.z); x[6] = bf_lo(w.w); x[7] = bf_hi(w.w);
         } else {
@@ -116,13 +146,13 @@ __device__ __forceinline__ void ld(const void* __restrict__ p, uint64_t i, float
 }
 
 // Stores round-to-nearest-even into DT (values are already DT-exact in the bf16 regime).
-template <int DT, int N>
+template <int DT, int N, bool NT = (EDT_NT_STORES != 0)>
 __device__ __forceinline__ void st(void* __restrict__ p, uint64_t i, const float (&x)[N]) {
     if constexpr (DT == EDT_F32) {
         float* q = static_cast<float*>(p) + i;
         if constexpr (N == 8) {
-            *reinterpret_cast<f32x4*>(q) = (f32x4){x[0], x[1], x[2], x[3]};
-            *reinterpret_cast<f32x4*>(q + 4) = (f32x4){x[4], x[5], x[6], x[7]};
+            vstore<f32x4, NT>(reinterpret_cast<f32x4*>(q), (f32x4){x[0], x[1], x[2], x[3]});
+            vstore<f32x4, NT>(reinterpret_cast<f32x4*>(q + 4), (f32x4){x[4], x[5], x[6], x[7]});
         } else {
 #pragma unroll
             for (int j = 0; j < N; ++j) q[j] = x[j];
@@ -133,7 +163,7 @@ __device__ __forceinline__ void st(void* __restrict__ p, uint64_t i, const float
             u32x4 w;
             w.x = pack_bf(x[0], x[1]); w.y = pack_bf(x[2], x[3]);
             w.z = pack_bf(x[4], x[5]); w.w = pack_bf(x[6], x[7]);
-            *reinterpret_cast<u32x4*>(q) = w;
+            vstore<u32x4, NT>(reinterpret_cast<u32x4*>(q), w);
         } else {
 #pragma unroll
             for (int j = 0; j < N; ++j) q[j] = uint16_t(pack_bf(x[j], 0.f) & 0xffffu);
@@ -167,16 +197,21 @@ SgdScalars make_sgd(int gdt, double lr, double mu, int has_buf, int nesterov) {
 // torch.optim.sgd._single_tensor_sgd for one group of N elements, in regime GDT.
 // grad is the pseudo-gradient (already in GDT precision); theta is updated in registers,
 // the momentum buffer is read from / written to `mom` at element i.
+// Loads the carried momentum buffer (issued together with the other operand loads).
+template <int GDT, int N>
+__device__ __forceinline__ void ld_momentum(const void* mom, uint64_t i, const SgdScalars& s, float (&b)[N]) {
+    if (s.use_momentum && s.has_buf) ld<GDT, N>(mom, i, b);
+}
+
 template <int GDT, int N>
 __device__ __forceinline__ void sgd_update(float (&theta)[N], const float (&grad)[N], void* mom,
-                                           uint64_t i, const SgdScalars& s) {
+                                           uint64_t i, const SgdScalars& s, const float (&b_in)[N]) {
     float u[N];
     if (s.use_momentum) {
         float b[N];
         if (s.has_buf) {
-            ld<GDT, N>(mom, i, b);
 #pragma unroll
-            for (int j = 0; j < N; ++j) b[j] = b[j] * s.mul_mu;      // buf.mul_(momentum)
+            for (int j = 0; j < N; ++j) b[j] = b_in[j] * s.mul_mu;   // buf.mul_(momentum)
             rnd<GDT>(b);
 #pragma unroll
             for (int j = 0; j < N; ++j) b[j] = b[j] + grad[j];       // .add_(grad, alpha=1)
@@ -231,8 +266,9 @@ enum { MODE_FUSED = 0, MODE_PARTIAL = 1 };
 // in fp32 instead (the cross-rank sum is then an fp32 RCCL reduction).
 template <int GDT, int WDT, int KC, int DIV, int MODE, int N>
 __device__ __forceinline__ void outer_elems(const OuterArgs& a, uint64_t i) {
-    float g[N], acc[N];
+    float g[N], acc[N], b_in[N];
     ld<GDT, N>(a.theta, i, g);
+    if constexpr (MODE == MODE_FUSED) ld_momentum<GDT, N>(a.mom, i, a.sgd, b_in);
     if (MODE == MODE_PARTIAL && a.accumulate) {
         ld<EDT_F32, N>(a.acc_out, i, acc);      // continue the running sum in worker order
     } else {
@@ -242,7 +278,7 @@ __device__ __forceinline__ void outer_elems(const OuterArgs& a, uint64_t i) {
     const int K = KC > 0 ? KC : a.K;
     auto body = [&](int k) {
         float w[N];
-        ld<WDT, N>(a.w.p[k], i, w);
+        ld<WDT, N, EDT_NT_LOADS != 0>(a.w.p[k], i, w);
 #pragma unroll
         for (int j = 0; j < N; ++j) w[j] = w[j] - g[j];              // trained - base
         rnd<GDT>(w);
@@ -271,7 +307,7 @@ __device__ __forceinline__ void outer_elems(const OuterArgs& a, uint64_t i) {
         float grad[N];
 #pragma unroll
         for (int j = 0; j < N; ++j) grad[j] = -acc[j];               // p.grad = -avg_delta
-        sgd_update<GDT, N>(g, grad, a.mom, i, a.sgd);
+        sgd_update<GDT, N>(g, grad, a.mom, i, a.sgd, b_in);
         st<GDT, N>(a.theta, i, g);
     }
 }
@@ -279,7 +315,7 @@ __device__ __forceinline__ void outer_elems(const OuterArgs& a, uint64_t i) {
 // DIV = 1: true division by K (torch CPU `delta / num_models`); DIV = 0: multiply by 1/K,
 // bit-identical when K is a power of two.
 template <int GDT, int WDT, int KC, int DIV, int MODE, int N>
-__global__ __launch_bounds__(kBlock) void outer_kernel(OuterArgs a) {
+__global__ __launch_bounds__(kBlock, EDT_MIN_WAVES) void outer_kernel(OuterArgs a) {
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
     const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if constexpr (N == kVec) {
@@ -300,13 +336,14 @@ __global__ __launch_bounds__(kBlock) void sgd_apply_kernel(void* theta, const fl
     const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     auto elems = [&](auto tagN, uint64_t i) {
         constexpr int M = decltype(tagN)::value;
-        float g[M], a[M], grad[M];
+        float g[M], a[M], grad[M], b_in[M];
         ld<GDT, M>(theta, i, g);
         ld<EDT_F32, M>(acc, i, a);
+        ld_momentum<GDT, M>(mom, i, s, b_in);
         rnd<GDT>(a);
 #pragma unroll
         for (int j = 0; j < M; ++j) grad[j] = -a[j];
-        sgd_update<GDT, M>(g, grad, mom, i, s);
+        sgd_update<GDT, M>(g, grad, mom, i, s, b_in);
         st<GDT, M>(theta, i, g);
     };
     using V8 = std::integral_constant<int, kVec>;
@@ -337,11 +374,12 @@ struct PairArgs {
 
 template <int GDT, int WDT, int N>
 __device__ __forceinline__ void pair_elems(const PairArgs& a, uint64_t i) {
-    float base[N];
+    float base[N], b_in[N];
+    ld_momentum<GDT, N>(a.mom, i, a.sgd, b_in);
     if (a.b2) {                        // run_linear_merge_5050: lerp(0.5, b1, b2) in the model dtype
         float x[N], y[N];
-        ld<WDT, N>(a.b1, i, x);
-        ld<WDT, N>(a.b2, i, y);
+        ld<WDT, N, EDT_NT_LOADS != 0>(a.b1, i, x);
+        ld<WDT, N, EDT_NT_LOADS != 0>(a.b2, i, y);
 #pragma unroll
         for (int j = 0; j < N; ++j) { x[j] = x[j] * 0.5f; y[j] = y[j] * 0.5f; }   // (1-.5)*v0, .5*v1
         rnd<WDT>(x);
@@ -354,8 +392,8 @@ __device__ __forceinline__ void pair_elems(const PairArgs& a, uint64_t i) {
     }
     rnd<GDT>(base);                    // load_state_dict into the base model's dtype
     float d1[N], d2[N];
-    ld<WDT, N>(a.m1, i, d1);
-    ld<WDT, N>(a.m2, i, d2);
+    ld<WDT, N, EDT_NT_LOADS != 0>(a.m1, i, d1);
+    ld<WDT, N, EDT_NT_LOADS != 0>(a.m2, i, d2);
 #pragma unroll
     for (int j = 0; j < N; ++j) { d1[j] = d1[j] - base[j]; d2[j] = d2[j] - base[j]; }
     rnd<GDT>(d1);
@@ -369,7 +407,7 @@ __device__ __forceinline__ void pair_elems(const PairArgs& a, uint64_t i) {
     float grad[N];
 #pragma unroll
     for (int j = 0; j < N; ++j) grad[j] = -(0.f + d1[j]);           // acc = zeros + delta
-    sgd_update<GDT, N>(base, grad, a.mom, i, a.sgd);
+    sgd_update<GDT, N>(base, grad, a.mom, i, a.sgd, b_in);
     st<GDT, N>(a.out, i, base);
 }
 
@@ -773,7 +811,7 @@ int edt_slerp_stats(const void* v0, const void* v1, int in_dt, const uint64_t* c
     if (nchunks == 0) return EDT_OK;
     if (!v0 || !v1 || !chunk_desc || !partial) return fail(EDT_ERR_ARG, "null buffer");
     if (!aligned16(v0) || !aligned16(v1)) return fail(EDT_ERR_ARG, "slerp inputs must be 16-byte aligned");
-    const unsigned g = (unsigned)(nchunks < kMaxBlocks ? nchunks : kMaxBlocks);
+    const unsigned g = (unsigned)((uint64_t)nchunks < kMaxBlocks ? (uint64_t)nchunks : kMaxBlocks);
     hipStream_t s = (hipStream_t)stream;
     if (in_dt == EDT_F32) slerp_stats_kernel<EDT_F32><<<g, kBlock, 0, s>>>(v0, v1, chunk_desc, nchunks, partial);
     else slerp_stats_kernel<EDT_BF16><<<g, kBlock, 0, s>>>(v0, v1, chunk_desc, nchunks, partial);
@@ -800,7 +838,7 @@ int edt_slerp_blend(const void* v0, const void* v1, int in_dt, void* out, int ou
     if (!v0 || !v1 || !out || !chunk_desc || !coef) return fail(EDT_ERR_ARG, "null buffer");
     if (!aligned16(v0) || !aligned16(v1) || !aligned16(out))
         return fail(EDT_ERR_ARG, "slerp buffers must be 16-byte aligned");
-    const unsigned g = (unsigned)(nchunks < kMaxBlocks ? nchunks : kMaxBlocks);
+    const unsigned g = (unsigned)((uint64_t)nchunks < kMaxBlocks ? (uint64_t)nchunks : kMaxBlocks);
     hipStream_t s = (hipStream_t)stream;
     if (in_dt == EDT_F32 && out_dt == EDT_F32)
         slerp_blend_kernel<EDT_F32, EDT_F32><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef);

@@ -1,0 +1,110 @@
+"""A/B sweep of build-time variants of the fused outer-step kernel, interleaved in one process.
+
+    python scripts/kernel_variants.py --build            # here: hipcc the variants into build/variants/
+    python scripts/kernel_variants.py --rounds 5         # on the GPU box: time them
+
+Each variant is the same source (evolutionarydistributedtraining_amd/csrc/edt_sync.hip) built with
+different -D tunables; each is loaded as its own ctypes library and timed with HIP events on the
+1.3B-parameter, K=8 bf16-worker, fp32-master configuration of bench.py.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+VDIR = os.path.join(ROOT, "build", "variants")
+
+NT = ["-DEDT_NT_LOADS=1"]
+VARIANTS = {
+    "default": [],                                             # the shipped tunables
+    "base": ["-DEDT_BLOCKS_PER_CU=8", "-DEDT_NT_LOADS=0"],     # round-1 first build
+    "bpc64": ["-DEDT_BLOCKS_PER_CU=64", "-DEDT_NT_LOADS=0"],
+    "bpc6_nt": ["-DEDT_BLOCKS_PER_CU=6"] + NT,
+    "bpc12_nt": ["-DEDT_BLOCKS_PER_CU=12"] + NT,
+    "bpc24_nt": ["-DEDT_BLOCKS_PER_CU=24"] + NT,
+    "bpc64_nt": ["-DEDT_BLOCKS_PER_CU=64"] + NT,
+    "bpc256_nt": ["-DEDT_BLOCKS_PER_CU=256"] + NT,
+    "oneshot_nt": ["-DEDT_BLOCKS_PER_CU=0"] + NT,
+    "oneshot": ["-DEDT_BLOCKS_PER_CU=0", "-DEDT_NT_LOADS=0"],
+    "w8_bpc64_nt": ["-DEDT_BLOCKS_PER_CU=64", "-DEDT_MIN_WAVES=8"] + NT,
+    "w8_oneshot_nt": ["-DEDT_BLOCKS_PER_CU=0", "-DEDT_MIN_WAVES=8"] + NT,
+}
+
+
+def build(names):
+    from evolutionarydistributedtraining_amd.build import build_library
+    os.makedirs(VDIR, exist_ok=True)
+    for n in names:
+        out = os.path.join(VDIR, f"{n}.so")
+        build_library(force=True, extra_flags=VARIANTS[n], out=out)
+        print("built", out)
+
+
+def run(names, rounds, iters, layout_name, k):
+    import torch
+    from evolutionarydistributedtraining_amd import _lib as L
+    from evolutionarydistributedtraining_amd.layouts import LAYOUTS
+    dev = torch.device("cuda:0")
+    P = LAYOUTS[layout_name]().total
+    theta = torch.randn(P, device=dev) * 0.02
+    workers = [(theta + torch.randn(P, device=dev) * 1e-3).bfloat16() for _ in range(k)]
+    mom = torch.zeros(P, device=dev)
+    libs = {}
+    for n in names:
+        lib = ctypes.CDLL(os.path.join(VDIR, f"{n}.so"))
+        f = lib.edt_outer_step
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,
+                      ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_double,
+                      ctypes.c_double, ctypes.c_int, ctypes.c_void_p]
+        libs[n] = f
+    arr = L.ptr_array(workers)
+    stream = L.stream_ptr(dev)
+    bytes_per = k * 2 + 8 + 8
+    times = {n: [] for n in names}
+
+    def launch(f):
+        rc = f(ctypes.c_void_p(theta.data_ptr()), 0, arr, 1, k, ctypes.c_void_p(mom.data_ptr()), 1, P,
+               0.7, 0.9, 1, stream)
+        assert rc == 0
+    for n in names:                       # warm-up, first-step buffer init
+        launch(libs[n])
+    torch.cuda.synchronize()
+    for r in range(rounds):
+        for n in names:
+            evs = [torch.cuda.Event(enable_timing=True) for _ in range(2 * iters)]
+            for i in range(iters):
+                evs[2 * i].record()
+                launch(libs[n])
+                evs[2 * i + 1].record()
+            torch.cuda.synchronize()
+            times[n] += [evs[2 * i].elapsed_time(evs[2 * i + 1]) for i in range(iters)]
+    res = {}
+    for n in names:
+        med = statistics.median(times[n])
+        res[n] = {"median_ms": round(med, 4), "min_ms": round(min(times[n]), 4),
+                  "TBps": round(bytes_per * P / med / 1e9, 3)}
+    print(json.dumps({"layout": layout_name, "K": k, "variants": res}, indent=1))
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build", action="store_true")
+    ap.add_argument("--variants", default=",".join(VARIANTS))
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--layout", default="gpt_1p3b")
+    ap.add_argument("--k", type=int, default=8)
+    a = ap.parse_args()
+    names = a.variants.split(",")
+    if a.build:
+        build(names)
+    else:
+        run(names, a.rounds, a.iters, a.layout, a.k)

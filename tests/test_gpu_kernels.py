@@ -4,7 +4,9 @@ Bars (stated per test):
   * vs the oracle in its vectorised-torch semantics (tail=None): bit-exact, every element.
   * vs the reference goldens: fp32 regimes bit-exact; bf16 regime bit-exact except on the
     elements torch's CPU kernels send down their scalar tail (oracle.torch_cpu_tail_mask), where
-    the reference itself rounds add(..., alpha) twice: there |diff| <= 1 bf16 ulp.
+    the reference itself rounds add(..., alpha) twice (the oracle reproduces both forms bit for
+    bit, tests/test_oracle_golden.py). There the SGD direction u differs by <= 1 bf16 ulp, so
+    |diff| <= 2 ulp(theta_out) + 2 ulp(|theta_out - theta_in|).
   * SLERP: the reference's dot is an fp32 BLAS/pairwise sum; ours is an fp64 sum. Coefficients
     agree to ~1e-6 relative, so |out - ref| <= 2e-6 * (|c0 v0| + |c1 v1|) + 1e-30.
 """
@@ -42,7 +44,13 @@ def ulp_bf16(x: torch.Tensor) -> torch.Tensor:
     return torch.exp2(e - 7)
 
 
-def assert_matches_reference(got, want, tail, what):
+def update_tol(want, theta_in):
+    """Bound for a result whose SGD direction differs by one bf16 rounding."""
+    step = (want.float() - theta_in.float()).abs()
+    return 2 * ulp_bf16(want) + 2 * ulp_bf16(step)
+
+
+def assert_matches_reference(got, want, tail, what, theta_in):
     if got.dtype == torch.float32:
         assert torch.equal(bits(got), bits(want)), f"{what}: fp32 not bit-exact"
         return
@@ -51,7 +59,7 @@ def assert_matches_reference(got, want, tail, what):
     assert not outside.any(), f"{what}: {int(outside.sum())} mismatches outside torch's scalar tails"
     if diff.any():
         d = (got.float() - want.float()).abs()[diff]
-        assert (d <= ulp_bf16(want[diff]) * 1.0001).all(), f"{what}: tail diff > 1 ulp"
+        assert (d <= update_tol(want, theta_in)[diff] * 1.0001).all(), f"{what}: tail diff too large"
 
 
 @pytest.mark.parametrize("idx", range(len(_M["diloco"])))
@@ -73,6 +81,7 @@ def test_diloco_golden(golden, oracle, dev, ops, idx):
         else:
             mom, has = prev_buf.clone(), True
         th_d = theta.to(dev)
+        theta_in = theta.clone()
         mom_d = None if mom is None else mom.to(dev)
         ops.outer_step(th_d, [w.to(dev) for w in workers], mom_d, has, c["lr"], mu, c["nesterov"])
         # oracle, vectorised semantics: bit-exact on every element
@@ -80,7 +89,7 @@ def test_diloco_golden(golden, oracle, dev, ops, idx):
         got = th_d.cpu()
         assert torch.equal(bits(got), bits(theta)), f"{pre}: kernel != oracle"
         want = flat(golden.tlist("diloco", f"{pre}/out_theta", T))
-        assert_matches_reference(got, want, tail, pre)
+        assert_matches_reference(got, want, tail, pre, theta_in)
         if step["has_out_buf"]:
             gb = mom_d.cpu()
             assert torch.equal(bits(gb), bits(mom)), f"{pre}: momentum kernel != oracle"
@@ -149,8 +158,9 @@ def test_outer_step_edge_values(oracle, dev, ops):
 @pytest.mark.parametrize("gdt,wdt", REGIMES)
 def test_partial_then_sgd(oracle, dev, ops, gdt, wdt):
     """Sharded form: fp32 partial sums + sgd_apply == fused step (fp32 regimes: bit-exact,
-    the fp32 partial accumulates in the same order; bf16: <= 1 bf16 ulp, the fused form
-    rounds the running sum to bf16 after every worker, as the reference does)."""
+    the fp32 partial accumulates in the same order; bf16: the fused form rounds the running sum
+    to bf16 after every worker, as the reference does, so the SGD direction differs by a few
+    bf16 ulps of its terms: |diff| <= 2 ulp(theta_out) + 4 ulp(|update| + lr (|buf'| + mu |buf|)))."""
     n, K = 100_003, 4
     theta, workers, mom = _rand_case(n, K, gdt, wdt, seed=11)
     th_d, m_d = theta.to(dev), mom.to(dev)
@@ -164,9 +174,10 @@ def test_partial_then_sgd(oracle, dev, ops, gdt, wdt):
     got = th_d.cpu()
     if gdt == torch.float32:
         assert torch.equal(bits(got), bits(th))
-    else:
+    else:   # fp32 running sum vs the reference's bf16-rounded one: the direction differs slightly
         d = (got.float() - th.float()).abs()
-        assert (d <= ulp_bf16(th) * 1.0001).all()
+        scale = (th.float() - theta.float()).abs() + 0.7 * (m.float().abs() + 0.9 * mom.float().abs())
+        assert (d <= (2 * ulp_bf16(th) + 4 * ulp_bf16(scale)) * 1.0001).all()
 
 
 @pytest.mark.parametrize("idx", range(len(_M["pair_merge"])))
@@ -184,7 +195,7 @@ def test_pair_merge_golden(golden, oracle, dev, ops, idx):
     mom = None if p["mom"] is None else p["mom"].clone()
     oracle.pair_merge(p["b1"], p["b2"], p["m1"], p["m2"], out, mom, p["has"], p["lr"], p["mu"], p["nesterov"])
     assert torch.equal(bits(out_d.cpu()), bits(out)), "kernel != oracle"
-    assert_matches_reference(out_d.cpu(), p["want_theta"], tail, c["name"])
+    assert_matches_reference(out_d.cpu(), p["want_theta"], tail, c["name"], p["want_base"])
     if p["want_buf"] is not None:
         assert torch.equal(bits(mom_d.cpu()), bits(p["want_buf"].to(p["bdt"])))
     # merged base alone (run_linear_merge_5050)
