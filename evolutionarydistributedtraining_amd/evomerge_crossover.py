@@ -1,0 +1,119 @@
+"""Drop-in for EDT_EVOMERGE/train/crossover.py: SLERP crossover of two 7B-class causal LMs (bf16)
+on a worker, driven by EDT_EVOMERGE/edt.py:262-280 through the CLI
+
+    python -m evolutionarydistributedtraining_amd.evomerge_crossover --model1_path A --model2_path B --output_path O
+
+The reference moves each tensor to the GPU and back and SLERPs it in numpy (its LazyTensorLoader,
+EDT_EVOMERGE/train/crossover.py:86-146); here both bodies are merged in HBM in one multi-tensor
+pass and the bf16 result is written straight into model_1's body (the reference's
+`model_merged.model.load_state_dict`, :142, rounds the fp32 SLERP to bf16 the same way).
+"""
+from __future__ import annotations
+
+import json
+import os
+
+import torch
+
+from .merge import interpolate_t, lerp, merge_plan, slerp, slerp_state_dicts, uniform_dna_crossover
+
+__all__ = ["slerp", "lerp", "interpolate_t", "load_model_from_path", "run_slerp_merge_from_config",
+           "run_linear_merge_5050", "crossover_main", "uniform_dna_crossover", "SELF_ATTN_T_CURVE",
+           "MLP_T_CURVE"]
+
+SELF_ATTN_T_CURVE = [0, 0.5, 0.3, 0.7, 1]      # EDT_EVOMERGE/train/crossover.py:174-175
+MLP_T_CURVE = [1, 0.5, 0.7, 0.3, 0]
+
+
+def _device():
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def load_model_from_path(folder_path: str):
+    """bf16 AutoModelForCausalLM on the GPU (EDT_EVOMERGE/train/crossover.py:66-69)."""
+    from transformers import AutoConfig, AutoModelForCausalLM
+    config = AutoConfig.from_pretrained(folder_path, trust_remote_code=True, cache_dir="cache")
+    model = AutoModelForCausalLM.from_pretrained(folder_path, config=config, torch_dtype=torch.bfloat16,
+                                                 trust_remote_code=True, cache_dir="cache")
+    return model.to(_device())
+
+
+def run_slerp_merge_from_config(merge_config_dict: dict, model_1, model_2, config_1, config_2,
+                                merge_output_path: str, base_model, device=None) -> str:
+    """SLERP model_1 / model_2 (bodies, `.model`) into base_model.model and save base_model
+    (EDT_EVOMERGE/train/crossover.py:104-146). `device` picks the GPU (None: current)."""
+    num_layers = min(config_1.num_hidden_layers, config_2.num_hidden_layers)
+    sd1, sd2 = model_1.state_dict(), model_2.state_dict()
+    plan = merge_plan(list(sd1.keys()), num_layers, merge_config_dict)
+    target = base_model.model
+    out_dtype = next(target.parameters()).dtype
+    dev = torch.device(device) if device not in (None, "cpu") else None
+    merged = slerp_state_dicts(sd1, sd2, plan, out_dtype=out_dtype, device=dev)
+    target.load_state_dict(merged)
+    base_model.save_pretrained(merge_output_path)
+    print("SLERP merging complete! Model saved at:", merge_output_path)
+    return merge_output_path
+
+
+def run_linear_merge_5050(model_1, model_2, config_1, config_2, merge_output_path: str) -> str:
+    """t = 0.5 lerp of every state-dict tensor into AutoModel.from_config, saved
+    (EDT_EVOMERGE/train/crossover.py:149-163)."""
+    from transformers import AutoModel
+    merged_model = AutoModel.from_config(model_1.config, trust_remote_code=True)
+    sd1, sd2 = model_1.state_dict(), model_2.state_dict()
+    merged = {k: lerp(0.5, sd1[k], sd2[k]) for k in sd1.keys()}
+    merged_model.load_state_dict(merged)
+    merged_model.save_pretrained(merge_output_path)
+    print("Linear 50-50 merging complete! Model saved at:", merge_output_path)
+    return merge_output_path
+
+
+def slerp_config(model1_path: str, model2_path: str, num_layers: int) -> dict:
+    return {
+        "slices": [{"sources": [{"model": model1_path, "layer_range": [0, num_layers]},
+                                {"model": model2_path, "layer_range": [0, num_layers]}]}],
+        "merge_method": "slerp", "base_model": model1_path,
+        "parameters": {"t": [{"filter": "self_attn", "value": SELF_ATTN_T_CURVE},
+                             {"filter": "mlp", "value": MLP_T_CURVE}, {"value": 0.5}]},
+        "dtype": "float32", "tokenizer_source": None,
+    }
+
+
+def crossover_main(model1_path: str, model2_path: str, output_path: str) -> None:
+    """Child of two parents: SLERP into parent 1, tokenizer, genome.json
+    (EDT_EVOMERGE/train/crossover.py:166-229)."""
+    from transformers import AutoTokenizer
+    model_1 = load_model_from_path(model1_path)
+    model_2 = load_model_from_path(model2_path)
+    num_layers = min(model_1.config.num_hidden_layers, model_2.config.num_hidden_layers)
+    cfg = slerp_config(model1_path, model2_path, num_layers)
+    tokenizer = AutoTokenizer.from_pretrained(model1_path, trust_remote_code=True, cache_dir="cache")
+    tokenizer.save_pretrained(output_path)
+    run_slerp_merge_from_config(cfg, model_1.model, model_2.model, model_1.config, model_2.config,
+                                output_path, base_model=model_1)
+    with open(os.path.join(model1_path, "genome.json")) as f:
+        p1 = json.load(f)
+    with open(os.path.join(model2_path, "genome.json")) as f:
+        p2 = json.load(f)
+    for g in (p1, p2):
+        g.pop("p1", None)
+        g.pop("p2", None)
+    genome = {"fitness": 0.0, "model_path": output_path,
+              "dna": uniform_dna_crossover(p1["dna"], p2["dna"]), "p1": p1, "p2": p2}
+    with open(os.path.join(output_path, "genome.json"), "w") as f:
+        json.dump(genome, f, indent=4)
+    print("Done!")
+
+
+def main(argv=None):
+    import argparse
+    ap = argparse.ArgumentParser(description="SLERP merge two Hugging Face models (MI355X).")
+    ap.add_argument("--model1_path", type=str, required=True)
+    ap.add_argument("--model2_path", type=str, required=True)
+    ap.add_argument("--output_path", type=str, default="crossover_result")
+    a = ap.parse_args(argv)
+    crossover_main(a.model1_path, a.model2_path, a.output_path)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,172 @@
+"""Model-level crossover math shared by the RL / EVOMERGE / LM surfaces.
+
+The reference merges two state dicts key by key in Python, each key a numpy SLERP on the CPU
+(EDT_RL/crossover.py:84-135, EDT_EVOMERGE/train/crossover.py:104-146). Here both parents are
+packed into two flat HBM arenas (one segment per key), the per-key t values are computed on the
+host exactly as the reference does, and the whole merge is three launches (chunk sums,
+per-segment coefficients, blend) — see ops.slerp_arena.
+"""
+from __future__ import annotations
+
+import numbers
+
+import numpy as np
+import torch
+
+from . import ops
+from ._lib import EdtError
+
+
+# ------------------------------------------------------------------------------------------
+# host-side scalar logic (bit-identical python-float arithmetic to the reference)
+
+def lerp(t, v0, v1):
+    """(1 - t) * v0 + t * v1 (EDT_RL/crossover.py:46-47, EDT_LM/train/crossover.py:50-51).
+
+    Python numbers: plain float arithmetic (as interpolate_t uses it). torch tensors: one fused
+    launch with torch's rounding in the tensors' dtype (output on the inputs' device). numpy
+    arrays: float32 math as numpy does it, computed on the GPU, returned as numpy."""
+    if isinstance(v0, numbers.Number) and isinstance(v1, numbers.Number):
+        return (1 - t) * v0 + t * v1
+    if isinstance(v0, np.ndarray) or isinstance(v1, np.ndarray):
+        a = torch.from_numpy(np.ascontiguousarray(v0, dtype=np.float32))
+        b = torch.from_numpy(np.ascontiguousarray(v1, dtype=np.float32))
+        return lerp(t, a, b).numpy()
+    dev = _compute_device(v0)
+    a = v0.detach().to(dev).contiguous()
+    b = v1.detach().to(device=dev, dtype=a.dtype).contiguous()
+    out = ops.lerp(float(t), a.reshape(-1), b.reshape(-1)).view(a.shape)
+    return out if v0.is_cuda else out.cpu()
+
+
+def interpolate_t(layer_idx, num_layers, t_curve):
+    """Piecewise-linear t over the layer index (EDT_RL/crossover.py:70-81)."""
+    if layer_idx < 0:
+        return t_curve[0]
+    if layer_idx >= num_layers - 1:
+        return t_curve[-1]
+    position = layer_idx / (num_layers - 1) * (len(t_curve) - 1)
+    lo = int(position)
+    hi = min(lo + 1, len(t_curve) - 1)
+    return lerp(position - lo, t_curve[lo], t_curve[hi])
+
+
+def parse_t_parameters(merge_config_dict: dict):
+    """{filter: curve} and the global t of a MergeKit-style config (EDT_RL/crossover.py:99-100)."""
+    ts = merge_config_dict["parameters"]["t"]
+    param_t = {p["filter"]: p["value"] for p in ts if "filter" in p}
+    global_t = next((p["value"] for p in ts if "filter" not in p), 0.5)
+    return param_t, global_t
+
+
+def t_for_key(key: str, num_layers: int, param_t: dict, global_t):
+    """The reference's key routing (EDT_RL/crossover.py:108-122): the t for `key`, or None when
+    the key is skipped (a layer index beyond num_layers)."""
+    if "layer" in key:
+        layer_idx = int(key.split(".")[1])
+        if layer_idx >= num_layers:
+            return None
+        if "self_attn" in key and "self_attn" in param_t:
+            return interpolate_t(layer_idx, num_layers, param_t["self_attn"])
+        if "mlp" in key and "mlp" in param_t:
+            return interpolate_t(layer_idx, num_layers, param_t["mlp"])
+        return global_t
+    return global_t
+
+
+def merge_plan(keys, num_layers: int, merge_config_dict: dict):
+    """[(key, t)] in state-dict order, skipped keys removed."""
+    param_t, global_t = parse_t_parameters(merge_config_dict)
+    out = []
+    for k in keys:
+        t = t_for_key(k, num_layers, param_t, global_t)
+        if t is not None:
+            out.append((k, float(t)))
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+# device-side merges
+
+def _compute_device(*tensors) -> torch.device:
+    for t in tensors:
+        if isinstance(t, torch.Tensor) and t.is_cuda:
+            return t.device
+    if not torch.cuda.is_available():
+        raise EdtError("no HIP device visible: the crossover kernels run on MI355X only")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+_plans: dict = {}
+
+
+def _plan_for(offsets, device):
+    key = (tuple(offsets), str(device))
+    plan = _plans.get(key)
+    if plan is None:
+        if len(_plans) > 8:
+            _plans.clear()
+        plan = _plans[key] = ops.make_slerp_plan(list(offsets), device)
+    return plan
+
+
+def slerp_tensors(pairs, ts, out_dtype=torch.float32, device=None, dot_threshold=0.9995,
+                  eps=1e-8) -> list[torch.Tensor]:
+    """SLERP of each (v0, v1) pair with its own t, all in ONE multi-tensor pass.
+
+    Inputs are upcast to float32 exactly like the reference's `.float().numpy()` when the two
+    parents' dtypes differ; results are float32 (the reference returns float32) or `out_dtype`
+    (rounded to nearest even, as load_state_dict into a bf16 model does)."""
+    pairs = list(pairs)
+    if not pairs:
+        return []
+    dev = device or _compute_device(*[t for p in pairs for t in p])
+    in_dt = pairs[0][0].dtype
+    if any(a.dtype != in_dt or b.dtype != in_dt for a, b in pairs) or in_dt not in (torch.float32, torch.bfloat16):
+        in_dt = torch.float32
+    offsets = [0]
+    for a, b in pairs:
+        if a.shape != b.shape:
+            raise EdtError(f"parents disagree on a tensor shape: {tuple(a.shape)} vs {tuple(b.shape)}")
+        offsets.append(offsets[-1] + a.numel())
+    total = offsets[-1]
+    v0 = torch.empty(total, dtype=in_dt, device=dev)
+    v1 = torch.empty(total, dtype=in_dt, device=dev)
+    for (a, b), s, e in zip(pairs, offsets[:-1], offsets[1:]):
+        v0[s:e].copy_(a.detach().reshape(-1))
+        v1[s:e].copy_(b.detach().reshape(-1))
+    out = torch.empty(total, dtype=out_dtype, device=dev)
+    plan = _plan_for(offsets, dev)
+    tt = torch.tensor([float(t) for t in ts], dtype=torch.float64).to(dev)
+    ops.slerp_arena(plan, v0, v1, out, tt, dot_threshold, eps)
+    return [out[s:e].view(a.shape) for (a, _), s, e in zip(pairs, offsets[:-1], offsets[1:])]
+
+
+def slerp(t, v0, v1, DOT_THRESHOLD=0.9995, eps=1e-8):
+    """SLERP of one tensor pair (EDT_RL/crossover.py:11-43): float32 result, on the inputs'
+    device (CPU in, CPU out; numpy in, numpy out)."""
+    as_numpy = isinstance(v0, np.ndarray) and isinstance(v1, np.ndarray)
+    a = torch.from_numpy(np.ascontiguousarray(v0)) if isinstance(v0, np.ndarray) else v0
+    b = torch.from_numpy(np.ascontiguousarray(v1)) if isinstance(v1, np.ndarray) else v1
+    res = slerp_tensors([(a, b)], [t], dot_threshold=DOT_THRESHOLD, eps=eps)[0]
+    if as_numpy:
+        return res.cpu().numpy()
+    on_device = (isinstance(v0, torch.Tensor) and v0.is_cuda) or (isinstance(v1, torch.Tensor) and v1.is_cuda)
+    return res if on_device else res.cpu()
+
+
+def slerp_state_dicts(sd1: dict, sd2: dict, plan, out_dtype=torch.float32, device=None,
+                      dot_threshold=0.9995, eps=1e-8) -> dict:
+    """Merged state dict {key: tensor} for plan = [(key, t)] (see merge_plan)."""
+    keys = [k for k, _ in plan]
+    res = slerp_tensors([(sd1[k], sd2[k]) for k in keys], [t for _, t in plan], out_dtype, device,
+                        dot_threshold, eps)
+    return dict(zip(keys, res))
+
+
+def uniform_dna_crossover(dna1, dna2):
+    """Per gene, parent 1's value if np.random.rand() > 0.5 else parent 2's, with numpy's global
+    RNG (EDT_LM/train/crossover.py:318-321, EDT_RL/crossover.py:167-170)."""
+    assert len(dna1) == len(dna2), "DNA lengths must be the same for uniform crossover."
+    from_first = [np.random.rand() > 0.5 for _ in dna1]     # one draw per gene, in gene order
+    return [a if f else b for a, b, f in zip(dna1, dna2, from_first)]

@@ -1,0 +1,272 @@
+"""The reference's call surfaces, end to end on the GPU, against the golden vectors the reference
+produced: DiLoCo `outer_step` on model parameter lists, the EDT-LM `run_sgd` / `crossover_main`
+worker flow (HF folders, genome.json, outer_optim.pt), the RL `crossover(g1, g2, out)` over
+Policy/Value folders and the EVOMERGE `run_slerp_merge_from_config` on bf16 Qwen2 bodies.
+Tolerances as in test_gpu_kernels.py (SLERP: fp64 vs fp32 dot; bf16: scalar-tail rounding)."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+from safetensors.torch import load_file
+
+from tests.golden_data import bits, flat
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda:0")
+
+
+def _ulp_bf16(x):
+    a = x.float().abs().clamp_min(torch.finfo(torch.bfloat16).tiny)
+    return torch.exp2(torch.floor(torch.log2(a)) - 7)
+
+
+def _tiny_llama_cfg(dtype="bfloat16"):
+    from transformers import LlamaConfig
+    return LlamaConfig(vocab_size=24, hidden_size=8, intermediate_size=16, num_hidden_layers=4,
+                       num_attention_heads=2, num_key_value_heads=1, tie_word_embeddings=False, dtype=dtype)
+
+
+def _llama(tensors, dtype=torch.bfloat16, cfg_dtype="bfloat16"):
+    from transformers import LlamaForCausalLM
+    m = LlamaForCausalLM(_tiny_llama_cfg(cfg_dtype)).to(dtype)
+    with torch.no_grad():
+        for p, t in zip(m.parameters(), tensors):
+            p.copy_(t)
+    return m
+
+
+def _save_tokenizer(path):
+    from tokenizers import Tokenizer, models, pre_tokenizers
+    from transformers import PreTrainedTokenizerFast
+    vocab = {"[UNK]": 0, **{f"w{i}": i + 1 for i in range(23)}}
+    tok = Tokenizer(models.WordLevel(vocab, unk_token="[UNK]"))
+    tok.pre_tokenizer = pre_tokenizers.Whitespace()
+    PreTrainedTokenizerFast(tokenizer_object=tok, unk_token="[UNK]").save_pretrained(path)
+
+
+# ------------------------------------------------------------------------------------------
+def test_diloco_outer_step_surface(golden, oracle, dev):
+    """outer_step(list(base.parameters()), [list(m.parameters())...], state) over two generations,
+    arena (zero-copy) and packed paths, vs the oracle and the reference goldens."""
+    from evolutionarydistributedtraining_amd import OuterState, arena_of_module, outer_step
+    c = [c for c in golden.diloco_cases() if c["K"] == 3 and c["global_dtype"] == "f32"
+         and c["worker_dtype"] == "f32" and c["nesterov"] and c["momentum"] == 0.9][0]
+    T = len(c["shapes"])
+    for zero_copy in (True, False):
+        state = None
+        for step in c["steps"]:
+            pre = step["prefix"]
+            base = torch.nn.ParameterList([torch.nn.Parameter(t.clone()) for t in golden.tlist("diloco", f"{pre}/base", T)]).to(dev)
+            trained = [torch.nn.ParameterList([torch.nn.Parameter(t.clone()) for t in
+                                               golden.tlist("diloco", f"{pre}/worker{k}", T)]).to(dev)
+                       for k in range(c["K"])]
+            if zero_copy:
+                arena_of_module(base)
+                for m in trained:
+                    arena_of_module(m)
+            state = outer_step(list(base.parameters()), [list(m.parameters()) for m in trained], state,
+                               lr=c["lr"], momentum=c["momentum"], nesterov=c["nesterov"])
+            got = flat([p.detach().cpu() for p in base.parameters()])
+            want = flat(golden.tlist("diloco", f"{pre}/out_theta", T))
+            assert torch.equal(bits(got), bits(want)), (pre, zero_copy)
+            assert torch.equal(bits(state.momentum.cpu()), bits(flat(golden.tlist("diloco", f"{pre}/out_buf", T))))
+        assert isinstance(state, OuterState) and state.steps == 2
+
+
+def _pair_case(golden, name):
+    c = [c for c in golden.pair_cases() if c["name"].endswith(name)][0]
+    T = c["n_tensors"]
+    g = lambda tag: golden.tlist("pair_merge", f"{c['name']}/{tag}", T)
+    return c, g
+
+
+@pytest.mark.parametrize("name", ["both_parent1_rule", "p2_only", "gen0_fresh", "gen0_sig_defaults"])
+def test_lm_run_sgd_surface(golden, oracle, dev, tmp_path, name):
+    from evolutionarydistributedtraining_amd import lm_crossover
+    from tests.test_oracle_golden import pair_inputs
+    c, g = _pair_case(golden, name)
+    p1 = tmp_path / "m1" / c["generation"]
+    p2 = tmp_path / "m2" / c["generation"]
+    out = tmp_path / "child"
+    for d in (p1, p2):
+        d.mkdir(parents=True)
+
+    def write_optim(path, bufs):
+        ps = [torch.nn.Parameter(b.clone()) for b in bufs]
+        o = torch.optim.SGD(ps, lr=0.7, momentum=0.9, nesterov=True)
+        for p, b in zip(ps, bufs):
+            o.state[p]["momentum_buffer"] = b.clone()
+        torch.save(o.state_dict(), path)
+    if c["parent1_optim"]:
+        write_optim(p1 / "outer_optim.pt", g("buf1"))
+    if c["parent2_optim"]:
+        write_optim(p2 / "outer_optim.pt", g("buf2"))
+    m1, m2 = _llama(g("m1")).to(dev), _llama(g("m2")).to(dev)
+    base = _llama(g("merged_base")).to(dev)
+    lm_crossover.run_sgd(m1, m2, base, str(out), str(p1), str(p2), lr=c["call_lr"],
+                         momentum=c["call_momentum"], nesterov=c["call_nesterov"])
+    got = flat([p.detach().cpu() for p in base.parameters()])
+    p = pair_inputs(golden, c)
+    ref = torch.empty_like(got)
+    mom = None if p["mom"] is None else p["mom"].clone()
+    oracle.pair_merge(p["b1"], p["b2"], p["m1"], p["m2"], ref, mom, p["has"], p["lr"], p["mu"], p["nesterov"])
+    assert torch.equal(bits(got), bits(ref))                        # == vectorised reference semantics
+    want = flat(g("out_theta"))
+    tail = oracle.torch_cpu_tail_mask([int(torch.Size(s).numel()) for s in c["shapes"]])
+    diff = bits(got) != bits(want)
+    assert not (diff & (tail == 0)).any()
+    sd = torch.load(out / "outer_optim.pt", weights_only=True)
+    assert sd["param_groups"][0]["momentum"] == p["mu"]
+    if c["has_out_buf"]:
+        got_buf = flat([sd["state"][i]["momentum_buffer"] for i in range(c["n_tensors"])])
+        assert torch.equal(bits(got_buf), bits(flat(g("out_buf"))))
+    else:
+        assert sd["state"] == {}
+    assert (out / "model.safetensors").exists()
+
+
+def test_lm_run_sgd_requires_parent_state(dev, tmp_path, golden):
+    from evolutionarydistributedtraining_amd import lm_crossover
+    c, g = _pair_case(golden, "p1_only")
+    m = _llama(g("m1")).to(dev)
+    with pytest.raises(NotImplementedError):
+        lm_crossover.run_sgd(m, m, _llama(g("b1")).to(dev), str(tmp_path / "o"), str(tmp_path / "a" / "Gen0003"),
+                             str(tmp_path / "b" / "Gen0003"), 0.7, 0.9, True)
+
+
+def test_lm_crossover_main_cli_flow(golden, oracle, dev, tmp_path):
+    """Parent dirs with genome.json -> child dir: model, tokenizer, genome, outer_optim.pt,
+    optimizer.pt carried from parent 1's trained dir (EDT_LM/train/crossover.py:240-315)."""
+    from evolutionarydistributedtraining_amd import lm_crossover
+    from tests.test_oracle_golden import pair_inputs
+    c, g = _pair_case(golden, "both_parent1_rule")
+    dirs = {}
+    for tag in ("1", "2"):
+        base_dir = tmp_path / f"m{tag}" / "Gen0003"
+        mut_dir = tmp_path / f"m{tag}" / "Gen0003_mutation"
+        _llama(g(f"b{tag}")).save_pretrained(base_dir)
+        _llama(g(f"m{tag}")).save_pretrained(mut_dir)
+        _save_tokenizer(mut_dir)
+        (mut_dir / "optimizer.pt").write_bytes(f"inner-optimizer-{tag}".encode())
+        ps = [torch.nn.Parameter(b.clone()) for b in g(f"buf{tag}")]
+        o = torch.optim.SGD(ps, lr=0.7, momentum=0.9, nesterov=True)
+        for p_, b in zip(ps, g(f"buf{tag}")):
+            o.state[p_]["momentum_buffer"] = b.clone()
+        torch.save(o.state_dict(), base_dir / "outer_optim.pt")
+        with open(base_dir / "genome.json", "w") as f:
+            json.dump({"fitness": 1.0, "model_path": str(base_dir), "mutation_path": str(mut_dir),
+                       "dna": [0, 1, 2] if tag == "1" else [3, 2, 1], "p1": {"x": 1}}, f)
+        dirs[tag] = base_dir
+    out = tmp_path / "child" / "Gen0004"
+    np.random.seed(123)
+    lm_crossover.crossover_main(str(dirs["1"]), str(dirs["2"]), str(out))
+    sd = load_file(str(out / "model.safetensors"))
+    from transformers import LlamaForCausalLM
+    names = [n for n, _ in LlamaForCausalLM(_tiny_llama_cfg()).named_parameters()]
+    got = flat([sd[n] for n in names])
+    p = pair_inputs(golden, c)
+    ref = torch.empty_like(got)
+    oracle.pair_merge(p["b1"], p["b2"], p["m1"], p["m2"], ref, p["mom"].clone(), True, 0.7, 0.9, True)
+    assert torch.equal(bits(got), bits(ref))
+    genome = json.load(open(out / "genome.json"))
+    np.random.seed(123)
+    from evolutionarydistributedtraining_amd.merge import uniform_dna_crossover
+    assert genome["dna"] == uniform_dna_crossover([0, 1, 2], [3, 2, 1])
+    assert "p1" not in genome["p1"] and genome["fitness"] == 0.0 and genome["model_path"] == str(out)
+    assert (out / "optimizer.pt").read_bytes() == b"inner-optimizer-1"
+    assert (out / "tokenizer.json").exists() or (out / "tokenizer_config.json").exists()
+    osd = torch.load(out / "outer_optim.pt", weights_only=True)
+    got_buf = flat([osd["state"][i]["momentum_buffer"] for i in range(c["n_tensors"])])
+    assert torch.equal(bits(got_buf), bits(flat(g("out_buf"))))
+
+
+def _slerp_tol(want_out, p1, p2, rel=3e-6):
+    return rel * (p1.float().abs() + p2.float().abs()) + 1e-30
+
+
+def test_rl_crossover_surface(golden, dev, tmp_path):
+    """crossover(g1, g2, out) over Policy/Value folders (fp32), vs the reference's saved output."""
+    from transformers import LlamaForCausalLM
+    from evolutionarydistributedtraining_amd import rl_crossover
+    t = golden.tensors("merge_models")
+    rec = [r for r in golden.manifest["merge_models"] if r["name"] == "rl_crossover"][0]
+    gs = {}
+    for tag in ("p1", "p2"):
+        root = tmp_path / tag
+        for part in ("Policy", "Value"):
+            m = LlamaForCausalLM(_tiny_llama_cfg("float32"))
+            keys = rec["parts"][part]["keys"]
+            sd = {"model." + k: t[f"merge_models/rl/{part}/{tag}/{k}"] for k in keys}
+            sd["lm_head.weight"] = torch.zeros_like(m.lm_head.weight)
+            m.load_state_dict(sd)
+            m.save_pretrained(root / part)
+        gs[tag] = {"model_path": str(root), "env": {"env_name": "wb",
+                   "reward_dna": [1, 2, 3, 4, 5, 6] if tag == "p1" else [6, 5, 4, 3, 2, 1], "agents": []}}
+    np.random.seed(rec["np_seed"])
+    child = rl_crossover.crossover(gs["p1"], gs["p2"], str(tmp_path / "child"))
+    assert child["env"]["reward_dna"] == rec["reward_dna"]
+    assert child["p1"] is gs["p1"] and child["model_path"] == str(tmp_path / "child")
+    for part in ("Policy", "Value"):
+        out = load_file(str(tmp_path / "child" / part / "model.safetensors"))
+        for k in rec["parts"][part]["keys"]:
+            want = t[f"merge_models/rl/{part}/out/{k}"]
+            a, b = t[f"merge_models/rl/{part}/p1/{k}"], t[f"merge_models/rl/{part}/p2/{k}"]
+            assert out[k].dtype == torch.float32
+            assert ((out[k] - want).abs() <= _slerp_tol(want, a, b)).all(), (part, k)
+
+
+def test_evomerge_surface(golden, dev, tmp_path):
+    """run_slerp_merge_from_config on bf16 Qwen2 bodies, result written into model_1 (bf16)."""
+    from transformers import Qwen2Config, Qwen2ForCausalLM
+    from evolutionarydistributedtraining_amd import evomerge_crossover as ev
+    t = golden.tensors("merge_models")
+    rec = [r for r in golden.manifest["merge_models"] if r["name"] == "evomerge"][0]
+    cfg = Qwen2Config(vocab_size=24, hidden_size=8, intermediate_size=16, num_hidden_layers=5,
+                      num_attention_heads=2, num_key_value_heads=1, tie_word_embeddings=False)
+    models = []
+    for tag in ("p1", "p2"):
+        m = Qwen2ForCausalLM(cfg).to(torch.bfloat16)
+        m.model.load_state_dict({k: t[f"merge_models/evomerge/{tag}/{k}"] for k in rec["keys"]})
+        with torch.no_grad():
+            m.lm_head.weight.copy_(t["merge_models/evomerge/out_lm_head"])
+        models.append(m.to(dev))
+    merge_cfg = ev.slerp_config("a", "b", 5)
+    ev.run_slerp_merge_from_config(merge_cfg, models[0].model, models[1].model, cfg, cfg, str(tmp_path / "o"),
+                                   base_model=models[0])
+    sd = models[0].model.state_dict()
+    n_exact = n = 0
+    for k in rec["keys"]:
+        want = t[f"merge_models/evomerge/out/{k}"]
+        got = sd[k].cpu()
+        assert got.dtype == torch.bfloat16
+        d = (got.float() - want.float()).abs()
+        assert (d <= _ulp_bf16(want) * 1.0001).all(), k          # fp32 result within tol -> <= 1 bf16 ulp
+        n_exact += int((d == 0).sum())
+        n += d.numel()
+    assert n_exact / n > 0.98
+    assert torch.equal(models[0].lm_head.weight.cpu(), t["merge_models/evomerge/out_lm_head"])
+    assert (tmp_path / "o" / "model.safetensors").exists()
+
+
+def test_single_tensor_slerp_api(golden, dev):
+    """slerp(t, v0, v1) on CPU tensors / numpy arrays / device tensors returns like the reference."""
+    from evolutionarydistributedtraining_amd.merge import slerp
+    ts = golden.tensors("slerp")
+    c = [c for c in golden.slerp_cases() if c["name"] == "slerp/generic_f32_t2"][0]
+    v0, v1 = ts[f"{c['inputs']}/v0"], ts[f"{c['inputs']}/v1"]
+    want = ts[f"{c['name']}/out"]
+    r_cpu = slerp(c["t"], v0, v1)
+    assert r_cpu.device.type == "cpu" and r_cpu.shape == want.shape
+    assert ((r_cpu - want).abs() <= _slerp_tol(want, v0, v1)).all()
+    r_np = slerp(c["t"], v0.numpy(), v1.numpy())
+    assert isinstance(r_np, np.ndarray)
+    r_dev = slerp(c["t"], v0.to(dev), v1.to(dev))
+    assert r_dev.is_cuda and torch.equal(r_dev.cpu(), r_cpu)

@@ -1,0 +1,168 @@
+"""Host-side logic of the shim (no GPU): key routing, t curves, DNA crossover, outer-state I/O,
+parameter arenas, layouts, and the C ABI library surface."""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from evolutionarydistributedtraining_amd import merge
+from evolutionarydistributedtraining_amd.diloco import OuterState
+from evolutionarydistributedtraining_amd.layouts import LAYOUTS
+from evolutionarydistributedtraining_amd.params import (ParamArena, ParamLayout, arena_of_module, flat_view,
+                                                        pack, unpack_)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_interpolate_t_matches_reference_tables(golden):
+    for tab in golden.manifest["interpolate_t"]:
+        got = [merge.interpolate_t(i, tab["num_layers"], tab["t_curve"]) for i in tab["layer_idx"]]
+        assert got == tab["t"], tab          # python floats, bit-identical
+
+
+def test_known_t_values():
+    attn, mlp = [0, 0.5, 0.3, 0.7, 1], [1, 0.5, 0.7, 0.3, 0]
+    assert [merge.interpolate_t(i, 4, attn) for i in range(4)] == pytest.approx([0, 0.43333, 0.56667, 1], abs=1e-5)
+    assert [merge.interpolate_t(i, 4, mlp) for i in range(4)] == pytest.approx([1, 0.56667, 0.43333, 0], abs=1e-5)
+
+
+def test_key_routing():
+    cfg = {"parameters": {"t": [{"filter": "self_attn", "value": [0, 0.5, 0.3, 0.7, 1]},
+                                {"filter": "mlp", "value": [1, 0.5, 0.7, 0.3, 0]}, {"value": 0.5}]}}
+    param_t, global_t = merge.parse_t_parameters(cfg)
+    assert global_t == 0.5 and set(param_t) == {"self_attn", "mlp"}
+    assert merge.t_for_key("embed_tokens.weight", 4, param_t, global_t) == 0.5
+    assert merge.t_for_key("norm.weight", 4, param_t, global_t) == 0.5
+    assert merge.t_for_key("layers.0.self_attn.q_proj.weight", 4, param_t, global_t) == 0
+    assert merge.t_for_key("layers.3.mlp.down_proj.weight", 4, param_t, global_t) == 0
+    assert merge.t_for_key("layers.1.input_layernorm.weight", 4, param_t, global_t) == 0.5
+    assert merge.t_for_key("layers.4.mlp.up_proj.weight", 4, param_t, global_t) is None      # skipped
+    with pytest.raises(ValueError):                 # same failure as the reference's int() parse
+        merge.t_for_key("model.layers.0.mlp.up_proj.weight", 4, param_t, global_t)
+    # no global entry -> 0.5 default
+    assert merge.parse_t_parameters({"parameters": {"t": [{"filter": "mlp", "value": [0, 1]}]}})[1] == 0.5
+
+
+def test_merge_plan_on_golden_model_keys(golden):
+    for case in golden.manifest["merge_models"]:
+        if case["name"] != "evomerge":
+            continue
+        cfg = {"parameters": {"t": [{"filter": "self_attn", "value": [0, 0.5, 0.3, 0.7, 1]},
+                                    {"filter": "mlp", "value": [1, 0.5, 0.7, 0.3, 0]}, {"value": 0.5}]}}
+        plan = merge.merge_plan(case["keys"], case["num_hidden_layers"], cfg)
+        assert [k for k, _ in plan] == case["keys"]
+
+
+def test_uniform_dna_crossover_matches_reference_draws(golden):
+    for rec in golden.manifest["dna_crossover"]:
+        np.random.seed(rec["seed"])
+        got = [merge.uniform_dna_crossover(rec["dna1"], rec["dna2"]) for _ in rec["draws"]]
+        assert got == rec["draws"]
+    with pytest.raises(AssertionError):
+        merge.uniform_dna_crossover([1, 2], [1])
+
+
+def test_python_number_lerp():
+    assert merge.lerp(0.25, 1.0, 3.0) == (1 - 0.25) * 1.0 + 0.25 * 3.0
+
+
+def test_outer_state_round_trip(tmp_path):
+    layout = ParamLayout([(3, 2), (5,), (1,)])
+    st = OuterState()
+    st.momentum = torch.arange(layout.total, dtype=torch.float32)
+    st.has_momentum = True
+    st.hparams = dict(lr=0.7, momentum=0.9, nesterov=True)
+    path = str(tmp_path / "outer_optim.pt")
+    st.save(path, layout)
+    sd = torch.load(path, weights_only=True)
+    ref = torch.optim.SGD([torch.nn.Parameter(torch.zeros(1))], lr=0.7, momentum=0.9, nesterov=True).state_dict()
+    assert set(sd["param_groups"][0]) == set(ref["param_groups"][0])
+    assert sd["param_groups"][0]["params"] == [0, 1, 2]
+    assert sd["state"][1]["momentum_buffer"].shape == (5,)
+    st2 = OuterState.load(path, layout, torch.bfloat16, "cpu")
+    assert st2.has_momentum and st2.momentum.dtype == torch.bfloat16
+    assert torch.equal(st2.momentum.float(), st.momentum.bfloat16().float())
+    # no buffers (momentum 0) -> fresh state
+    st3 = OuterState()
+    st3.hparams = dict(lr=1.0, momentum=0.0, nesterov=False)
+    st3.save(path, layout)
+    assert OuterState.load(path, layout, torch.float32, "cpu").momentum is None
+
+
+def test_param_layout_and_views():
+    ts = [torch.randn(3, 4), torch.randn(7), torch.randn(2, 2, 2)]
+    flat = pack(ts)
+    layout = ParamLayout.of(ts)
+    assert layout.total == 12 + 7 + 8 and layout.offsets == [0, 12, 19, 27]
+    views = layout.views(flat)
+    assert all(torch.equal(a, b) for a, b in zip(views, ts))
+    fv = flat_view(views)
+    assert fv is not None and fv.data_ptr() == flat.data_ptr() and fv.numel() == flat.numel()
+    assert flat_view(ts) is None                       # separate allocations
+    assert flat_view([views[0], views[2]]) is None     # not consecutive
+    for t in ts:
+        t.zero_()
+    unpack_(flat, ts)
+    assert torch.equal(pack(ts), flat)
+
+
+def test_bind_module_into_arena():
+    m = torch.nn.Sequential(torch.nn.Linear(4, 3), torch.nn.Linear(3, 2))
+    before = [p.detach().clone() for p in m.parameters()]
+    arena = arena_of_module(m)
+    assert all(torch.equal(a, b) for a, b in zip(m.parameters(), before))
+    fv = flat_view(list(m.parameters()))
+    assert fv is not None and fv.data_ptr() == arena.flat.data_ptr()
+    arena.flat.add_(1.0)                                # an arena update is a module update
+    assert all(torch.equal(a, b + 1) for a, b in zip(m.parameters(), before))
+    assert isinstance(ParamArena.from_tensors(before), ParamArena)
+
+
+@pytest.mark.parametrize("name,P,T", [("tiny_llama", 6_570_560, 39), ("gpt2_small", 124_439_808, 148),
+                                      ("gpt_1p3b", 1_315_723_264, 292), ("qwen2p5_7b_body", 7_070_619_136, 338)])
+def test_layouts_match_survey_counts(name, P, T):
+    lay = LAYOUTS[name]()
+    assert lay.total == P and len(lay) == T
+
+
+def test_library_exports_every_header_symbol():
+    from evolutionarydistributedtraining_amd import _lib
+    lib = _lib.load_library()
+    with open(os.path.join(ROOT, "include", "edt_sync.h")) as f:
+        header = f.read()
+    names = set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(edt_\w+)\s*\(", header, re.M))
+    assert len(names) >= 12
+    for n in names:
+        assert hasattr(lib, n), n
+    bound = {n for n, _, _ in _lib.SIGNATURES}
+    assert names == bound, names ^ bound
+    assert lib.edt_version().startswith(b"edt_sync")
+    assert lib.edt_outer_step_bytes_per_elem(0, 1, 8, 1) == 32
+
+
+def test_chunk_table_host_function():
+    import ctypes
+    from evolutionarydistributedtraining_amd import _lib
+    lib = _lib.load_library()
+    offs = (ctypes.c_uint64 * 5)(0, 0, 5, 70000, 70001)
+    first = (ctypes.c_int32 * 5)()
+    need = lib.edt_slerp_make_chunks(offs, 4, 32768, None, 0, first)
+    assert need < 0
+    n = -need - 1
+    desc = (ctypes.c_uint64 * (3 * n))()
+    assert lib.edt_slerp_make_chunks(offs, 4, 32768, desc, n, first) == n
+    chunks = [tuple(desc[3 * i:3 * i + 3]) for i in range(n)]
+    assert chunks == [(0, 5, 1), (5, 32768, 2), (32773, 32768, 2), (65541, 4459, 2), (70000, 1, 3)]
+    assert list(first) == [0, 0, 1, 4, 5]
+
+
+def test_product_path_refuses_without_device():
+    from evolutionarydistributedtraining_amd import EdtError, ops
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    with pytest.raises(EdtError):
+        ops.outer_step(torch.zeros(8), [torch.zeros(8)], None, False, 0.7, 0.0, False)
+    with pytest.raises(EdtError):
+        merge.slerp(0.5, torch.zeros(4), torch.ones(4))
