@@ -202,6 +202,21 @@ def main():
         }
         if roofline:
             out["roofline"] = roofline
+        if world == 1:   # what a plain device-to-device copy reaches on this device, same process
+            src = torch.empty(1 << 29, dtype=torch.float32, device=dev)
+            dst = torch.empty_like(src)
+            dst.copy_(src)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(5):
+                dst.copy_(src)
+            b.record()
+            torch.cuda.synchronize()
+            roofline["device_copy_GBps"] = round(5 * 2 * src.numel() * 4 / (a.elapsed_time(b) / 1e3) / 1e9, 1)
+            del src, dst
+        prop = torch.cuda.get_device_properties(dev)
+        out["device"] = {"name": prop.name, "arch": getattr(prop, "gcnArchName", ""),
+                         "cus": prop.multi_processor_count, "hbm_gib": round(prop.total_memory / 2**30, 1)}
         if world == 1 and args.cpu_baseline_seconds > 0:
             out["cpu_baseline"] = cpu_baseline(args, tdt, wdt, k_local)
         print(json.dumps(out), flush=True)

@@ -1,0 +1,95 @@
+"""Device-resident throughput of the other hot-path kernels (HIP events, one process):
+
+  pair_merge  EDT child (lerp .5 + 2-parent delta + Nesterov SGD), gpt_1p3b, bf16 model + bf16 base
+              algorithmic bytes/elem: 4 parents x 2 + child 2 + momentum r/w 4 = 14
+  slerp       SLERP crossover of two qwen2p5_7b_body parents (bf16 in, bf16 out), 338 segments
+              algorithmic bytes/elem: 2 x 2 in + 2 out = 6 (the 2-pass form reads the parents twice: 10)
+  lerp        run_linear_merge_5050 on gpt_1p3b bf16: 2 x 2 in + 2 out = 6
+
+    python scripts/bench_ops.py [--ops pair,slerp,lerp] [--iters 5]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+PEAK = 8000.0
+
+
+def timed(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    out = []
+    for _ in range(iters):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        torch.cuda.synchronize()
+        out.append(a.elapsed_time(b))
+    out.sort()
+    return out[len(out) // 2]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ops", default="pair,slerp,lerp")
+    ap.add_argument("--iters", type=int, default=5)
+    a = ap.parse_args()
+    from evolutionarydistributedtraining_amd import ops
+    from evolutionarydistributedtraining_amd.layouts import gpt_1p3b, qwen2p5_7b_body
+    dev = torch.device("cuda:0")
+    res = {}
+    bf = torch.bfloat16
+    if "pair" in a.ops or "lerp" in a.ops:
+        P = gpt_1p3b().total
+        b1 = (torch.randn(P, device=dev) * 0.02).to(bf)
+        b2 = (torch.randn(P, device=dev) * 0.02).to(bf)
+        if "pair" in a.ops:
+            m1 = (b1.float() + torch.randn(P, device=dev) * 1e-3).to(bf)
+            m2 = (b2.float() + torch.randn(P, device=dev) * 1e-3).to(bf)
+            out = torch.empty(P, dtype=bf, device=dev)
+            mom = (torch.randn(P, device=dev) * 1e-3).to(bf)
+            ms = timed(lambda: ops.pair_merge(b1, b2, m1, m2, out, mom, True, 0.7, 0.9, True), a.iters)
+            gbs = 14 * P / ms / 1e6
+            res["pair_merge"] = {"P": P, "ms": round(ms, 3), "GBps": round(gbs, 1), "frac": round(gbs / PEAK, 4),
+                                 "bytes_per_elem": 14}
+            del m1, m2, out, mom
+        if "lerp" in a.ops:
+            out = torch.empty(P, dtype=bf, device=dev)
+            ms = timed(lambda: ops.lerp(0.5, b1, b2, out=out), a.iters)
+            gbs = 6 * P / ms / 1e6
+            res["lerp"] = {"P": P, "ms": round(ms, 3), "GBps": round(gbs, 1), "frac": round(gbs / PEAK, 4),
+                           "bytes_per_elem": 6}
+        del b1, b2
+        torch.cuda.empty_cache()
+    if "slerp" in a.ops:
+        lay = qwen2p5_7b_body()
+        P = lay.total
+        v0 = torch.empty(P, dtype=bf, device=dev)
+        v1 = torch.empty(P, dtype=bf, device=dev)
+        step = 1 << 28
+        for s in range(0, P, step):
+            e = min(P, s + step)
+            x = torch.randn(e - s, device=dev) * 0.02
+            v0[s:e] = x.to(bf)
+            v1[s:e] = (x + torch.randn(e - s, device=dev) * 1e-3).to(bf)
+            del x
+        out = torch.empty(P, dtype=bf, device=dev)
+        plan = ops.make_slerp_plan(lay.offsets, dev)
+        t = torch.full((len(lay),), 0.5, dtype=torch.float64, device=dev)
+        ms = timed(lambda: ops.slerp_arena(plan, v0, v1, out, t), a.iters)
+        gbs = 6 * P / ms / 1e6
+        res["slerp"] = {"P": P, "segments": len(lay), "chunks": plan.nchunks, "ms": round(ms, 3),
+                        "GBps_algorithmic": round(gbs, 1), "frac": round(gbs / PEAK, 4), "bytes_per_elem": 6,
+                        "GBps_moved_2pass": round(10 * P / ms / 1e6, 1)}
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

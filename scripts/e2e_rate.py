@@ -1,0 +1,98 @@
+"""End-to-end DiLoCo outer-step rate when the population arrives from the host (PCIe-inclusive).
+
+In the reference the replicas come from other hosts through checkpoints on a shared disk
+(EDT_LM/diloco.py:231-235) and the new global weights go back the same way (:302-308). This
+measures the device side of that edge: K worker arenas in pinned host memory -> H2D -> fused
+outer step -> D2H of the new theta, (a) serial and (b) bucketed, H2D of bucket b+1 on a copy
+stream overlapping the kernel on bucket b. Reported as the metric (K x P x bytes / time) and as
+PCIe GB/s moved. Not the bench `value` (that one is device-resident).
+
+    python scripts/e2e_rate.py [--layout gpt2_small --k 8 --bucket-elems 16777216]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--layout", default="gpt2_small")
+    ap.add_argument("--k", type=int, default=8)
+    ap.add_argument("--bucket-elems", type=int, default=1 << 24)
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    from evolutionarydistributedtraining_amd import ops
+    from evolutionarydistributedtraining_amd.layouts import LAYOUTS
+    dev = torch.device("cuda:0")
+    P = LAYOUTS[a.layout]().total
+    g = torch.Generator().manual_seed(0)
+    theta_h = (torch.randn(P, generator=g) * 0.02).pin_memory()
+    workers_h = [(theta_h + torch.randn(P, generator=g) * 1e-3).bfloat16().pin_memory() for _ in range(a.k)]
+    theta_out_h = torch.empty(P, dtype=torch.float32).pin_memory()
+    theta_d = torch.empty(P, device=dev)
+    mom_d = torch.zeros(P, device=dev)
+    workers_d = [torch.empty(P, dtype=torch.bfloat16, device=dev) for _ in range(a.k)]
+    metric_bytes = a.k * P * 2
+    pcie_bytes = metric_bytes + 4 * P + 4 * P     # workers + theta in, theta out
+
+    def serial():
+        theta_d.copy_(theta_h, non_blocking=True)
+        for wd, wh in zip(workers_d, workers_h):
+            wd.copy_(wh, non_blocking=True)
+        ops.outer_step(theta_d, workers_d, mom_d, True, 0.7, 0.9, True)
+        theta_out_h.copy_(theta_d, non_blocking=True)
+
+    copy = torch.cuda.Stream(dev)
+    comp = torch.cuda.current_stream(dev)
+
+    def pipelined():
+        evs = []
+        B = a.bucket_elems
+        for s in range(0, P, B):
+            e = min(P, s + B)
+            with torch.cuda.stream(copy):
+                theta_d[s:e].copy_(theta_h[s:e], non_blocking=True)
+                for wd, wh in zip(workers_d, workers_h):
+                    wd[s:e].copy_(wh[s:e], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(copy)
+            evs.append((s, e, ev))
+        for s, e, ev in evs:
+            comp.wait_event(ev)
+            ops.outer_step(theta_d[s:e], [w[s:e] for w in workers_d], mom_d[s:e], True, 0.7, 0.9, True)
+            theta_out_h[s:e].copy_(theta_d[s:e], non_blocking=True)
+
+    res = {}
+    for name, fn in (("serial", serial), ("pipelined", pipelined)):
+        fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(a.reps):
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        t = min(ts)
+        res[name] = {"ms": round(t * 1e3, 2), "metric_GBps": round(metric_bytes / t / 1e9, 2),
+                     "pcie_GBps": round(pcie_bytes / t / 1e9, 2)}
+    # kernel alone, device-resident, for reference
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.reps):
+        ops.outer_step(theta_d, workers_d, mom_d, True, 0.7, 0.9, True)
+    torch.cuda.synchronize()
+    tk = (time.perf_counter() - t0) / a.reps
+    res["device_resident"] = {"ms": round(tk * 1e3, 3), "metric_GBps": round(metric_bytes / tk / 1e9, 1)}
+    print(json.dumps({"layout": a.layout, "P": P, "K": a.k, "bucket_elems": a.bucket_elems, **res}))
+
+
+if __name__ == "__main__":
+    main()
