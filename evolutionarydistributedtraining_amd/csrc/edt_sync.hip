@@ -428,12 +428,12 @@ __global__ __launch_bounds__(kBlock) void pair_kernel(PairArgs a) {
 // ---------------------------------------------------------------------------------------
 // lerp with a scalar t: out = round(round(c0*v0) + round(c1*v1)) in compute dtype CDT.
 
-template <int IDT, int ODT, int CDT, int N>
+template <int IDT, int ODT, int CDT, int N, bool NTL = false, bool NTS = (EDT_NT_STORES != 0)>
 __device__ __forceinline__ void lerp_elems(const void* v0, const void* v1, void* out, uint64_t i,
                                            float c0, float c1) {
     float x[N], y[N];
-    ld<IDT, N>(v0, i, x);
-    ld<IDT, N>(v1, i, y);
+    ld<IDT, N, NTL>(v0, i, x);
+    ld<IDT, N, NTL>(v1, i, y);
 #pragma unroll
     for (int j = 0; j < N; ++j) { x[j] = c0 * x[j]; y[j] = c1 * y[j]; }
     rnd<CDT>(x);
@@ -441,7 +441,7 @@ __device__ __forceinline__ void lerp_elems(const void* v0, const void* v1, void*
 #pragma unroll
     for (int j = 0; j < N; ++j) x[j] = x[j] + y[j];
     rnd<CDT>(x);
-    st<ODT, N>(out, i, x);
+    st<ODT, N, NTS>(out, i, x);
 }
 
 template <int IDT, int ODT, int CDT, int N>
@@ -468,63 +468,98 @@ __device__ __forceinline__ double wave_sum(double x) {
     return x;
 }
 
+// Block-wide sums {v0.v0, v1.v1, v0.v1} over one chunk [start, start+len), fp64 per thread,
+// fixed reduction order (wave shuffles, then waves in order). Valid in thread 0.
+template <int IDT>
+__device__ __forceinline__ void chunk_sums(const void* v0, const void* v1, uint64_t start, uint64_t len,
+                                           double (*red)[kBlock / 64], double (&out)[3]) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t end = start + len;
+    double s00 = 0.0, s11 = 0.0, s01 = 0.0;
+    const uint64_t a = (start + kVec - 1) / kVec * kVec;      // aligned body [a, b)
+    const uint64_t b = end / kVec * kVec;
+    if (a < b) {
+        for (uint64_t i = a + (uint64_t)threadIdx.x * kVec; i < b; i += (uint64_t)kBlock * kVec) {
+            float x[kVec], y[kVec];
+            ld<IDT, kVec>(v0, i, x);
+            ld<IDT, kVec>(v1, i, y);
+#pragma unroll
+            for (int j = 0; j < kVec; ++j) {
+                const double dx = x[j], dy = y[j];
+                s00 = __builtin_fma(dx, dx, s00);
+                s11 = __builtin_fma(dy, dy, s11);
+                s01 = __builtin_fma(dx, dy, s01);
+            }
+        }
+    }
+    // head [start, min(a, end)) and tail [max(b, a), end): fewer than 16 elements
+    const uint64_t h_end = a < end ? a : end;
+    const uint64_t t_beg = b > a ? b : h_end;
+    const uint64_t nh = h_end - start, nt = end - t_beg;
+    if ((uint64_t)threadIdx.x < nh + nt) {
+        const uint64_t i = threadIdx.x < nh ? start + threadIdx.x : t_beg + (threadIdx.x - nh);
+        float x[1], y[1];
+        ld<IDT, 1>(v0, i, x);
+        ld<IDT, 1>(v1, i, y);
+        const double dx = x[0], dy = y[0];
+        s00 = __builtin_fma(dx, dx, s00);
+        s11 = __builtin_fma(dy, dy, s11);
+        s01 = __builtin_fma(dx, dy, s01);
+    }
+    s00 = wave_sum(s00);
+    s11 = wave_sum(s11);
+    s01 = wave_sum(s01);
+    if (lane == 0) { red[0][wave] = s00; red[1][wave] = s11; red[2][wave] = s01; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            double acc = 0.0;
+#pragma unroll
+            for (int w = 0; w < kBlock / 64; ++w) acc += red[q][w];
+            out[q] = acc;
+        }
+    }
+    __syncthreads();
+}
+
+// The reference's scalar SLERP math (EDT_RL/crossover.py:24-45) from the three sums, in fp32 as
+// numpy does it for float32 scalars (NEP 50: python floats enter as fp32).
+__device__ __forceinline__ void slerp_coefficients(double s00, double s11, double s01, double t, float thr,
+                                                   float eps, float& c0, float& c1, float& dot) {
+    const float n0 = (float)sqrt(s00), n1 = (float)sqrt(s11);      // np.linalg.norm (fp32)
+    const double d0 = n0 > eps ? (double)n0 : 1.0;                  // normalize() divides only if > eps
+    const double d1 = n1 > eps ? (double)n1 : 1.0;
+    dot = (float)(s01 / (d0 * d1));
+    if (fabsf(dot) > thr) {                                         // lerp on the originals
+        c0 = (float)(1.0 - t);
+        c1 = (float)t;
+    } else {
+        const float th0 = acosf(dot);
+        const float s0 = sinf(th0);
+        const float tht = th0 * (float)t;
+        c0 = sinf(th0 - tht) / s0;
+        c1 = sinf(tht) / s0;
+    }
+}
+
 template <int IDT>
 __global__ __launch_bounds__(kBlock) void slerp_stats_kernel(const void* v0, const void* v1,
                                                              const uint64_t* chunks, int64_t nchunks,
                                                              double* partial) {
     __shared__ double red[3][kBlock / 64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
-        const uint64_t start = chunks[3 * c], len = chunks[3 * c + 1];
-        const uint64_t end = start + len;
-        double s00 = 0.0, s11 = 0.0, s01 = 0.0;
-        const uint64_t a = (start + kVec - 1) / kVec * kVec;      // aligned body [a, b)
-        const uint64_t b = end / kVec * kVec;
-        if (a < b) {
-            for (uint64_t i = a + (uint64_t)threadIdx.x * kVec; i < b; i += (uint64_t)kBlock * kVec) {
-                float x[kVec], y[kVec];
-                ld<IDT, kVec>(v0, i, x);
-                ld<IDT, kVec>(v1, i, y);
-#pragma unroll
-                for (int j = 0; j < kVec; ++j) {
-                    const double dx = x[j], dy = y[j];
-                    s00 = __builtin_fma(dx, dx, s00);
-                    s11 = __builtin_fma(dy, dy, s11);
-                    s01 = __builtin_fma(dx, dy, s01);
-                }
-            }
+        double sums[3];
+        chunk_sums<IDT>(v0, v1, chunks[3 * c], chunks[3 * c + 1], red, sums);
+        if (threadIdx.x == 0) {
+            partial[3 * c] = sums[0];
+            partial[3 * c + 1] = sums[1];
+            partial[3 * c + 2] = sums[2];
         }
-        // head [start, min(a, end)) and tail [max(b, a), end): fewer than 16 elements
-        const uint64_t h_end = a < end ? a : end;
-        const uint64_t t_beg = b > a ? b : h_end;
-        const uint64_t nh = h_end - start, nt = end - t_beg;
-        if ((uint64_t)threadIdx.x < nh + nt) {
-            const uint64_t i = threadIdx.x < nh ? start + threadIdx.x : t_beg + (threadIdx.x - nh);
-            float x[1], y[1];
-            ld<IDT, 1>(v0, i, x);
-            ld<IDT, 1>(v1, i, y);
-            const double dx = x[0], dy = y[0];
-            s00 = __builtin_fma(dx, dx, s00);
-            s11 = __builtin_fma(dy, dy, s11);
-            s01 = __builtin_fma(dx, dy, s01);
-        }
-        s00 = wave_sum(s00);
-        s11 = wave_sum(s11);
-        s01 = wave_sum(s01);
-        if (lane == 0) { red[0][wave] = s00; red[1][wave] = s11; red[2][wave] = s01; }
-        __syncthreads();
-        if (threadIdx.x < 3) {
-            double s = 0.0;
-#pragma unroll
-            for (int w = 0; w < kBlock / 64; ++w) s += red[threadIdx.x][w];
-            partial[3 * c + threadIdx.x] = s;
-        }
-        __syncthreads();
     }
 }
 
-// One wave per segment: fixed-order reduction of the chunk sums, then the reference's scalar
-// math in fp32 (numpy float32 scalars, NEP 50: python floats enter as fp32).
+// One wave per segment: fixed-order reduction of the chunk sums, then the coefficients.
 __global__ __launch_bounds__(kBlock) void slerp_coef_kernel(const double* partial, const int32_t* first,
                                                             int nseg, const double* tvals,
                                                             float thr, float eps, float* coef,
@@ -542,23 +577,8 @@ __global__ __launch_bounds__(kBlock) void slerp_coef_kernel(const double* partia
     s11 = wave_sum(s11);
     s01 = wave_sum(s01);
     if (lane != 0) return;
-    const float n0 = (float)sqrt(s00), n1 = (float)sqrt(s11);      // np.linalg.norm (fp32)
-    const double d0 = n0 > eps ? (double)n0 : 1.0;                  // normalize() divides only if > eps
-    const double d1 = n1 > eps ? (double)n1 : 1.0;
-    const float dot = (float)(s01 / (d0 * d1));
-    const double t = tvals[seg];
-    float c0, c1;
-    if (fabsf(dot) > thr) {                                         // lerp on the originals
-        c0 = (float)(1.0 - t);
-        c1 = (float)t;
-    } else {
-        const float th0 = acosf(dot);
-        const float s0 = sinf(th0);
-        const float tht = th0 * (float)t;
-        const float st_ = sinf(tht);
-        c0 = sinf(th0 - tht) / s0;
-        c1 = st_ / s0;
-    }
+    float c0, c1, dot;
+    slerp_coefficients(s00, s11, s01, tvals[seg], thr, eps, c0, c1, dot);
     coef[2 * seg] = c0;
     coef[2 * seg + 1] = c1;
     if (dot_out) dot_out[seg] = dot;
@@ -849,6 +869,16 @@ int edt_slerp_blend(const void* v0, const void* v1, int in_dt, void* out, int ou
     else
         slerp_blend_kernel<EDT_BF16, EDT_BF16><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef);
     return check_launch("slerp_blend_kernel");
+}
+
+int edt_slerp_merge(const void* v0, const void* v1, int in_dt, void* out, int out_dt, const uint64_t* chunk_desc,
+                    int64_t nchunks, const int32_t* seg_first_chunk, int nseg, const double* t, double dot_threshold,
+                    double eps, double* partial, float* coef, float* dot_out, void* stream) {
+    int rc = edt_slerp_stats(v0, v1, in_dt, chunk_desc, nchunks, partial, stream);
+    if (rc) return rc;
+    rc = edt_slerp_coef(partial, seg_first_chunk, nseg, t, dot_threshold, eps, coef, dot_out, stream);
+    if (rc) return rc;
+    return edt_slerp_blend(v0, v1, in_dt, out, out_dt, chunk_desc, nchunks, coef, stream);
 }
 
 }  // extern "C"

@@ -113,7 +113,7 @@ class SlerpPlan:
 
 
 def make_slerp_plan(seg_offsets: list[int], device: torch.device,
-                    chunk_elems: int = 1 << 16) -> SlerpPlan:
+                    chunk_elems: int = 1 << 14) -> SlerpPlan:
     lib = L.load_library()
     nseg = len(seg_offsets) - 1
     offs = (ctypes.c_uint64 * max(1, nseg + 1))(*seg_offsets)
@@ -124,7 +124,8 @@ def make_slerp_plan(seg_offsets: list[int], device: torch.device,
     got = lib.edt_slerp_make_chunks(offs, nseg, chunk_elems, desc, nchunks, first)
     if got != nchunks:
         L.check(-1, "edt_slerp_make_chunks")
-    chunks = torch.tensor(list(desc)[:3 * nchunks], dtype=torch.int64).view(-1, 3).to(device)
+    import numpy as np
+    chunks = torch.from_numpy(np.ctypeslib.as_array(desc).astype(np.int64)[:3 * nchunks].copy()).view(-1, 3).to(device)
     seg_first = torch.tensor(list(first), dtype=torch.int32).to(device)
     return SlerpPlan(list(seg_offsets), chunks, seg_first,
                      torch.empty((max(1, nchunks), 3), dtype=torch.float64, device=device),
@@ -134,8 +135,8 @@ def make_slerp_plan(seg_offsets: list[int], device: torch.device,
 
 def slerp_arena(plan: SlerpPlan, v0: torch.Tensor, v1: torch.Tensor, out: torch.Tensor,
                 t: torch.Tensor, dot_threshold: float = 0.9995, eps: float = 1e-8) -> None:
-    """SLERP every segment of v0/v1 with its own t (float64 device tensor [nseg]) into out.
-    Three launches: chunk sums, per-segment coefficients, blend (EDT_RL/crossover.py:11-43)."""
+    """SLERP every segment of v0/v1 with its own t (float64 device tensor [nseg]) into out
+    (EDT_RL/crossover.py:11-43): chunk sums, per-segment coefficients, blend (edt_slerp_merge)."""
     lib = L.lib()
     L.require_device(v0, v1, out, t)
     if v1.dtype != v0.dtype or v0.numel() != plan.seg_offsets[-1] or v1.numel() != v0.numel() \
@@ -143,13 +144,7 @@ def slerp_arena(plan: SlerpPlan, v0: torch.Tensor, v1: torch.Tensor, out: torch.
         raise L.EdtError("slerp arenas must match the plan's layout")
     if t.dtype != torch.float64 or t.numel() < plan.nseg:
         raise L.EdtError("t must be a float64 device tensor with one value per segment")
-    s = L.stream_ptr(v0.device)
-    idt = L.dtype_code(v0)
-    L.check(lib.edt_slerp_stats(L.ptr(v0), L.ptr(v1), idt, L.ptr(plan.chunks), plan.nchunks,
-                                L.ptr(plan.partial), s), "edt_slerp_stats")
-    L.check(lib.edt_slerp_coef(L.ptr(plan.partial), L.ptr(plan.seg_first), plan.nseg, L.ptr(t),
-                               float(dot_threshold), float(eps), L.ptr(plan.coef), L.ptr(plan.dots),
-                               s), "edt_slerp_coef")
-    L.check(lib.edt_slerp_blend(L.ptr(v0), L.ptr(v1), idt, L.ptr(out), L.dtype_code(out),
-                                L.ptr(plan.chunks), plan.nchunks, L.ptr(plan.coef), s),
-            "edt_slerp_blend")
+    L.check(lib.edt_slerp_merge(L.ptr(v0), L.ptr(v1), L.dtype_code(v0), L.ptr(out), L.dtype_code(out),
+                                L.ptr(plan.chunks), plan.nchunks, L.ptr(plan.seg_first), plan.nseg, L.ptr(t),
+                                float(dot_threshold), float(eps), L.ptr(plan.partial), L.ptr(plan.coef),
+                                L.ptr(plan.dots), L.stream_ptr(v0.device)), "edt_slerp_merge")

@@ -113,6 +113,15 @@ int edt_slerp_coef(const double* partial, const int32_t* seg_first_chunk, int ns
 int edt_slerp_blend(const void* v0, const void* v1, int in_dt, void* out, int out_dt,
                     const uint64_t* chunk_desc, int64_t nchunks, const float* coef, void* stream);
 
+/* The three passes above in one call (stats -> coef -> blend), stream-ordered. A
+ * segment-grouped variant that re-reads each group from the Infinity Cache measured slower on
+ * MI355X (launch count; 87 % of a 7B body's bytes sit in tensors larger than the cache), so the
+ * whole-arena form is the one shipped. */
+int edt_slerp_merge(const void* v0, const void* v1, int in_dt, void* out, int out_dt,
+                    const uint64_t* chunk_desc, int64_t nchunks, const int32_t* seg_first_chunk, int nseg,
+                    const double* t, double dot_threshold, double eps, double* partial, float* coef,
+                    float* dot_out, void* stream);
+
 /* ---- misc ---- */
 const char* edt_last_error(void);
 const char* edt_version(void);

@@ -38,6 +38,68 @@ VARIANTS = {
 }
 
 
+SLERP_VARIANTS = {"s_default": []}
+VARIANTS.update(SLERP_VARIANTS)
+
+
+def run_slerp(names, rounds, layout_name):
+    """Qwen2.5-7B-body-sized SLERP (bf16 in/out) per variant library: the grouped merge at
+    several group sizes, and the whole-arena three-pass form."""
+    import torch
+    from evolutionarydistributedtraining_amd import _lib as L
+    from evolutionarydistributedtraining_amd import ops
+    from evolutionarydistributedtraining_amd.layouts import LAYOUTS
+    dev = torch.device("cuda:0")
+    lay = LAYOUTS[layout_name]()
+    P = lay.total
+    bf = torch.bfloat16
+    v0 = torch.empty(P, dtype=bf, device=dev)
+    v1 = torch.empty(P, dtype=bf, device=dev)
+    for s0 in range(0, P, 1 << 28):
+        e = min(P, s0 + (1 << 28))
+        x = torch.randn(e - s0, device=dev) * 0.02
+        v0[s0:e] = x.to(bf)
+        v1[s0:e] = (x + torch.randn(e - s0, device=dev) * 1e-3).to(bf)
+        del x
+    out = torch.empty(P, dtype=bf, device=dev)
+    plan = ops.make_slerp_plan(lay.offsets, dev)
+    t = torch.full((len(lay),), 0.5, dtype=torch.float64, device=dev)
+    stream = L.stream_ptr(dev)
+    libs = {}
+    for n in names:
+        lib = ctypes.CDLL(os.path.join(VDIR, f"{n}.so"))
+        for name, res, args in L.SIGNATURES:
+            f = getattr(lib, name)
+            f.restype, f.argtypes = res, args
+        libs[n] = lib
+    P_ = L.ptr
+    cases = {}
+    for n in names:
+        lib = libs[n]
+
+        def three(lib=lib):
+            assert lib.edt_slerp_stats(P_(v0), P_(v1), 1, P_(plan.chunks), plan.nchunks, P_(plan.partial), stream) == 0
+            assert lib.edt_slerp_coef(P_(plan.partial), P_(plan.seg_first), plan.nseg, P_(t), 0.9995, 1e-8,
+                                      P_(plan.coef), P_(plan.dots), stream) == 0
+            return lib.edt_slerp_blend(P_(v0), P_(v1), 1, P_(out), 1, P_(plan.chunks), plan.nchunks, P_(plan.coef), stream)
+        cases[f"{n}/threepass"] = three
+    times = {k: [] for k in cases}
+    for k, f in cases.items():
+        assert f() == 0
+    torch.cuda.synchronize()
+    for _ in range(rounds):
+        for k, f in cases.items():
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            f()
+            b.record()
+            torch.cuda.synchronize()
+            times[k].append(a.elapsed_time(b))
+    res = {k: {"median_ms": round(statistics.median(v), 3), "algo_TBps": round(6 * P / statistics.median(v) / 1e9, 3)}
+           for k, v in times.items()}
+    print(json.dumps({"layout": layout_name, "P": P, "op": "slerp", "variants": res}, indent=1))
+
+
 def build(names):
     from evolutionarydistributedtraining_amd.build import build_library
     os.makedirs(VDIR, exist_ok=True)
@@ -102,9 +164,12 @@ if __name__ == "__main__":
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--layout", default="gpt_1p3b")
     ap.add_argument("--k", type=int, default=8)
+    ap.add_argument("--op", default="outer", choices=["outer", "slerp"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:
         build(names)
+    elif a.op == "slerp":
+        run_slerp(names, a.rounds, a.layout if a.layout != "gpt_1p3b" else "qwen2p5_7b_body")
     else:
         run(names, a.rounds, a.iters, a.layout, a.k)
