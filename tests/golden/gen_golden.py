@@ -156,6 +156,32 @@ def gen_diloco(manifest, tensors):
                     "nesterov": nest, "shapes": [list(s) for s in SHAPES], "steps": steps,
                 })
     manifest["diloco"] = cases
+    # one large bf16 case: tensors above torch's 32768-element grain are split over threads, and
+    # every parallel chunk has its own scalar tail (pins the oracle's tail model at scale)
+    rel, first, last, (lr, mu, nest) = DILOCO_BLOCKS["diloco"]
+    code = _block(rel, first, last)
+    gen = torch.Generator().manual_seed(4321)
+    shapes = [(70_001,), (257, 160)]
+    base = [(torch.randn(sh, generator=gen) * 0.02).bfloat16() for sh in shapes]
+    workers = [[(b.float() + torch.randn(b.shape, generator=gen) * 1e-3).bfloat16() for b in base] for _ in range(3)]
+    opt = None
+    theta0, _, opt = _exec_diloco(code, base, workers, {}, opt)
+    workers2 = [[(b.float() + torch.randn(b.shape, generator=gen) * 1e-3).bfloat16() for b in theta0] for _ in range(3)]
+    theta1, bufs1, _ = _exec_diloco(code, theta0, workers2, {}, opt)
+    pre = "diloco_large"
+    for i, t in enumerate(base):
+        tensors[f"{pre}/s0/base/{i}"] = t
+    for k in range(3):
+        for i in range(len(shapes)):
+            tensors[f"{pre}/s0/worker{k}/{i}"] = workers[k][i]
+            tensors[f"{pre}/s1/worker{k}/{i}"] = workers2[k][i]
+    for i in range(len(shapes)):
+        tensors[f"{pre}/s0/out_theta/{i}"] = theta0[i]
+        tensors[f"{pre}/s1/out_theta/{i}"] = theta1[i]
+        tensors[f"{pre}/s1/out_buf/{i}"] = bufs1[i]
+    manifest["diloco_large"] = {"name": pre, "source": f"{rel}:{first}-{last}", "K": 3, "dtype": "bf16",
+                                "lr": lr, "momentum": mu, "nesterov": nest, "shapes": [list(x) for x in shapes],
+                                "torch_num_threads": torch.get_num_threads()}
 
 
 # ----------------------------------------------------------------------------------------

@@ -1,0 +1,168 @@
+"""Full BASELINE sizes on the GPU, checked through size-independent properties:
+
+* element locality: the outer step / pair merge / lerp are element-wise, so any window of the
+  1.3B-parameter arena (beyond 2^31 elements' worth of bytes: 64-bit indexing) can be checked
+  against the oracle on its own — random windows plus the arena's ragged end;
+* SLERP on the Qwen2.5-7B body layout (7.07B elements, 338 segments): small segments checked
+  whole against the oracle; every segment's dot against an independent fp64 torch reduction;
+* hipGraph capture/replay and cross-stream ordering give the same bits as eager launches.
+"""
+import pytest
+import torch
+
+from tests.golden_data import bits
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda:0")
+
+
+def _windows(n, count, width, seed):
+    g = torch.Generator().manual_seed(seed)
+    starts = torch.randint(0, n - width, (count,), generator=g).tolist()
+    return sorted(starts) + [n - 777]          # ... and the ragged end (tail < 8 elements)
+
+
+def test_outer_step_1p3b_windows(oracle, dev):
+    from evolutionarydistributedtraining_amd import ops
+    from evolutionarydistributedtraining_amd.layouts import gpt_1p3b
+    P = gpt_1p3b().total
+    K, W = 8, 4096
+    gen = torch.Generator(device=dev).manual_seed(3)
+    theta = torch.randn(P, device=dev, generator=gen) * 0.02
+    workers = [(theta + torch.randn(P, device=dev, generator=gen) * 1e-3).bfloat16() for _ in range(K)]
+    mom = torch.randn(P, device=dev, generator=gen) * 1e-3
+    wins = _windows(P, 48, W, 11)
+    widths = [W] * 48 + [777]
+    before = [(theta[s:s + w].cpu(), [x[s:s + w].cpu() for x in workers], mom[s:s + w].cpu())
+              for s, w in zip(wins, widths)]
+    ops.outer_step(theta, workers, mom, True, 0.7, 0.9, True)
+    torch.cuda.synchronize()
+    for (s, w), (th, ws, m) in zip(zip(wins, widths), before):
+        oracle.outer_step(th, ws, m, True, 0.7, 0.9, True)
+        assert torch.equal(bits(theta[s:s + w].cpu()), bits(th)), s
+        assert torch.equal(bits(mom[s:s + w].cpu()), bits(m)), s
+    assert wins[-1] * 4 > 2 ** 32          # the checked end lies beyond 4 GiB of fp32
+
+
+def test_pair_merge_1p3b_windows(oracle, dev):
+    from evolutionarydistributedtraining_amd import ops
+    from evolutionarydistributedtraining_amd.layouts import gpt_1p3b
+    P = gpt_1p3b().total
+    gen = torch.Generator(device=dev).manual_seed(4)
+    bf = torch.bfloat16
+    b1, b2 = [(torch.randn(P, device=dev, generator=gen) * 0.02).to(bf) for _ in range(2)]
+    m1 = (b1.float() + torch.randn(P, device=dev, generator=gen) * 1e-3).to(bf)
+    m2 = (b2.float() + torch.randn(P, device=dev, generator=gen) * 1e-3).to(bf)
+    mom = (torch.randn(P, device=dev, generator=gen) * 1e-3).to(bf)
+    out = torch.empty(P, dtype=bf, device=dev)
+    wins = _windows(P, 32, 4096, 12)
+    widths = [4096] * 32 + [777]
+    mom_before = [mom[s:s + w].cpu() for s, w in zip(wins, widths)]
+    ops.pair_merge(b1, b2, m1, m2, out, mom, True, 0.7, 0.9, True)
+    torch.cuda.synchronize()
+    for (s, w), m in zip(zip(wins, widths), mom_before):
+        o = torch.empty(w, dtype=bf)
+        oracle.pair_merge(b1[s:s + w].cpu(), b2[s:s + w].cpu(), m1[s:s + w].cpu(), m2[s:s + w].cpu(), o, m, True,
+                          0.7, 0.9, True)
+        assert torch.equal(bits(out[s:s + w].cpu()), bits(o)), s
+        assert torch.equal(bits(mom[s:s + w].cpu()), bits(m)), s
+
+
+def test_slerp_qwen7b_body(oracle, dev):
+    from evolutionarydistributedtraining_amd import ops
+    from evolutionarydistributedtraining_amd.layouts import qwen2p5_7b_body
+    lay = qwen2p5_7b_body()
+    P = lay.total
+    bf = torch.bfloat16
+    gen = torch.Generator(device=dev).manual_seed(5)
+    v0 = torch.empty(P, dtype=bf, device=dev)
+    v1 = torch.empty(P, dtype=bf, device=dev)
+    step = 1 << 28
+    for s in range(0, P, step):
+        e = min(P, s + step)
+        x = torch.randn(e - s, device=dev, generator=gen) * 0.02
+        v0[s:e] = x.to(bf)
+        v1[s:e] = (x + torch.randn(e - s, device=dev, generator=gen) * 0.02 * 0.05).to(bf)
+    from evolutionarydistributedtraining_amd.merge import merge_plan
+    from evolutionarydistributedtraining_amd.evomerge_crossover import slerp_config
+    tplan = merge_plan(lay.names, 28, slerp_config("a", "b", 28))
+    assert len(tplan) == len(lay)
+    t = torch.tensor([tv for _, tv in tplan], dtype=torch.float64, device=dev)
+    plan = ops.make_slerp_plan(lay.offsets, dev)
+    out = torch.empty(P, dtype=bf, device=dev)
+    ops.slerp_arena(plan, v0, v1, out, t)
+    torch.cuda.synchronize()
+    dots = plan.dots[:len(lay)].cpu()
+    for s in range(len(lay)):                # independent fp64 reduction of every segment
+        a, b = lay.offsets[s], lay.offsets[s + 1]
+        x, y = v0[a:b].double(), v1[a:b].double()
+        ref = (x * y).sum() / (x.norm() * y.norm())
+        assert abs(dots[s].item() - ref.item()) < 2e-6, (s, lay.names[s])
+    small = [s for s in range(len(lay)) if lay.numels[s] <= 4_000_000][:40]
+    for s in small:                          # whole small segments vs the oracle
+        a, b = lay.offsets[s], lay.offsets[s + 1]
+        x, y = v0[a:b].cpu(), v1[a:b].cpu()
+        want = oracle.slerp(float(t[s]), x, y).bfloat16().float()
+        c0, c1, _ = oracle.slerp_coefficients(float(t[s]), x, y)
+        tol = 2e-6 * (abs(float(c0)) * x.float().abs() + abs(float(c1)) * y.float().abs())
+        tol = tol + torch.exp2(torch.floor(torch.log2(want.abs().clamp_min(1e-38))) - 7)
+        assert ((out[a:b].cpu().float() - want).abs() <= tol).all(), lay.names[s]
+
+
+def test_graph_capture_replay_bit_identical(dev):
+    """The C ABI launches are stream-ordered and allocation-free: capture into a hipGraph."""
+    from evolutionarydistributedtraining_amd import ops
+    n, K = 1_000_003, 4
+    gen = torch.Generator(device=dev).manual_seed(6)
+    theta0 = torch.randn(n, device=dev, generator=gen) * 0.02
+    workers = [(theta0 + torch.randn(n, device=dev, generator=gen) * 1e-3).bfloat16() for _ in range(K)]
+    mom0 = torch.randn(n, device=dev, generator=gen) * 1e-3
+    th_e, m_e = theta0.clone(), mom0.clone()
+    for _ in range(3):
+        ops.outer_step(th_e, workers, m_e, True, 0.7, 0.9, True)
+    th_g, m_g = theta0.clone(), mom0.clone()
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(graph, stream=s):
+            ops.outer_step(th_g, workers, m_g, True, 0.7, 0.9, True)
+    torch.cuda.current_stream(dev).wait_stream(s)
+    th_g.copy_(theta0)
+    m_g.copy_(mom0)
+    for _ in range(3):
+        graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(bits(th_g.cpu()), bits(th_e.cpu()))
+    assert torch.equal(bits(m_g.cpu()), bits(m_e.cpu()))
+
+
+def test_cross_stream_ordering(dev):
+    """Producer on one stream, the outer step on another, ordered by an event only."""
+    from evolutionarydistributedtraining_amd import ops
+    n, K = 4_000_037, 3
+    gen = torch.Generator(device=dev).manual_seed(7)
+    theta = torch.randn(n, device=dev, generator=gen) * 0.02
+    src = [(theta + torch.randn(n, device=dev, generator=gen) * 1e-3).bfloat16() for _ in range(K)]
+    ref_t = theta.clone()
+    ops.outer_step(ref_t, src, None, False, 1.0, 0.0, False)
+    producer, consumer = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    dst = [torch.zeros_like(x) for x in src]
+    th = theta.clone()
+    torch.cuda.synchronize()
+    with torch.cuda.stream(producer):
+        for d, x in zip(dst, src):
+            d.copy_(x)
+        ev = torch.cuda.Event()
+        ev.record(producer)
+    with torch.cuda.stream(consumer):
+        consumer.wait_event(ev)
+        ops.outer_step(th, dst, None, False, 1.0, 0.0, False)
+    torch.cuda.synchronize()
+    assert torch.equal(bits(th.cpu()), bits(ref_t.cpu()))

@@ -112,3 +112,23 @@ def test_slerp_oracle_bit_exact(golden, oracle):
         assert torch.equal(bits(got), bits(want)), c["name"]
         n_lerp += lerp_branch
     assert 0 < n_lerp < len(golden.slerp_cases())
+
+
+def test_diloco_large_bf16_parallel_tails(golden, oracle):
+    """A bf16 case with tensors above torch's parallel grain: the reference's scalar tails fall at
+    the end of every parallel chunk; the oracle's tail model reproduces it bit for bit."""
+    c = golden.manifest["diloco_large"]
+    T = len(c["shapes"])
+    numels = [int(torch.Size(s).numel()) for s in c["shapes"]]
+    tail = oracle.torch_cpu_tail_mask(numels, num_threads=c["torch_num_threads"])
+    pre = c["name"]
+    theta = flat(golden.tlist("diloco", f"{pre}/s0/base", T)).contiguous()
+    mom = torch.zeros_like(theta)
+    for step in (0, 1):
+        ws = [flat(golden.tlist("diloco", f"{pre}/s{step}/worker{k}", T)).contiguous() for k in range(c["K"])]
+        oracle.outer_step(theta, ws, mom, step == 1, c["lr"], c["momentum"], c["nesterov"], tail)
+        want = flat(golden.tlist("diloco", f"{pre}/s{step}/out_theta", T))
+        assert torch.equal(bits(theta), bits(want)), step
+    assert torch.equal(bits(mom), bits(flat(golden.tlist("diloco", f"{pre}/s1/out_buf", T))))
+    # and without the tail model the differences are confined to those tail elements
+    assert int(tail.sum()) < 0.01 * tail.numel()
