@@ -148,3 +148,84 @@ class ShardedOuterSync:
         if self.mode == "reduce":
             return int(f * self.n_pad * (4 + bg))
         return int(f * self.n_pad * (self.k_local * self.worker_bufs[0].element_size() + bg))
+
+
+class PopulationCrossover:
+    """EDT / SLERP children across GPUs: one population member per rank (member r on rank r,
+    child c built on rank c). The only exchange is point-to-point: a grouped batch of RCCL
+    send/recv delivers each child's parents to its rank (schedule.exchange_plan: one transfer per
+    (member, destination), each over the direct xGMI link between the two GPUs); the merge itself
+    is the single-GPU kernel, with no collective.
+
+    The reference does this through the shared disk: every worker loads both parents' checkpoint
+    directories (EDT_LM/train/crossover.py:255-258, EDT_EVOMERGE/train/crossover.py:167-168), and
+    the RL master merges pairs one after another in one process (EDT_RL/edt.py:286-299)."""
+
+    def __init__(self, layout: ParamLayout, dtype: torch.dtype, device, group=None, kernels=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.kernels = kernels or _ops
+        self.layout = layout
+        self.device = device
+        self.dtype = dtype
+        self._bufs = {}
+        self._plan = None
+
+    def _buf(self, key, dtype=None):
+        if key not in self._bufs:
+            self._bufs[key] = torch.empty(self.layout.total, dtype=dtype or self.dtype, device=self.device)
+        return self._bufs[key]
+
+    def _exchange(self, pairs, payload):
+        """payload(member_is_first_parent) -> tensors this rank ships for its member; returns the
+        parents' tensor lists for this rank's child: ([...] of parent 1, [...] of parent 2)."""
+        from .schedule import exchange_plan
+        n = self.world
+        if len(pairs) != n:
+            raise ValueError(f"{len(pairs)} children for {n} ranks: one child per rank")
+        plan = exchange_plan(pairs, list(range(n)), list(range(n)))
+        mine = plan[self.rank]
+        ops_ = []
+        for m, dst in mine["send"]:
+            i, j = pairs[dst]
+            for t in payload(m == i):
+                ops_.append(dist.P2POp(dist.isend, t, dst, self.group))
+        i, j = pairs[self.rank]
+        got = {}
+        for m, src in mine["recv"]:
+            first = m == i                       # parent 1 also ships its momentum
+            like = payload(first)
+            bufs = [self._buf(("recv", first, k), t.dtype) for k, t in enumerate(like)]
+            for b in bufs:
+                ops_.append(dist.P2POp(dist.irecv, b, src, self.group))
+            got[m] = bufs
+        if ops_:
+            for w in dist.batch_isend_irecv(ops_):
+                w.wait()
+        par1 = payload(True) if i == self.rank else got[i]
+        par2 = payload(False) if j == self.rank else got[j]
+        return par1, par2
+
+    def slerp_step(self, member: torch.Tensor, pairs, t: torch.Tensor, out: torch.Tensor,
+                   dot_threshold: float = 0.9995, eps: float = 1e-8) -> None:
+        """SLERP child of pairs[rank] into `out` (EDT_RL/crossover.py:84-135 per Policy/Value;
+        EDT_EVOMERGE/train/crossover.py:104-146). member: this rank's flat parameters."""
+        (p1,), (p2,) = self._exchange(pairs, lambda first: [member])
+        if self._plan is None:
+            self._plan = self.kernels.make_slerp_plan(self.layout.offsets, self.device)
+        self.kernels.slerp_arena(self._plan, p1, p2, out, t, dot_threshold, eps)
+
+    def pair_merge_step(self, base: torch.Tensor, trained: torch.Tensor, momentum: torch.Tensor | None,
+                        pairs, out: torch.Tensor, out_momentum: torch.Tensor | None, lr: float = 0.7,
+                        mu: float = 0.9, nesterov: bool = True, has_momentum: bool = True) -> None:
+        """EDT-LM child of pairs[rank] (EDT_LM/train/crossover.py:150-237): parent 1 ships
+        (base, trained, outer momentum) — its momentum is the one the child inherits — parent 2
+        ships (base, trained)."""
+        def payload(first):
+            return [base, trained] + ([momentum] if first and momentum is not None else [])
+        par1, par2 = self._exchange(pairs, payload)
+        if out_momentum is not None and len(par1) > 2:
+            out_momentum.copy_(par1[2])
+        self.kernels.pair_merge(par1[0], par2[0], par1[1], par2[1], out, out_momentum,
+                                has_momentum and len(par1) > 2, lr, mu, nesterov)

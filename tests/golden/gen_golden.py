@@ -446,15 +446,58 @@ def gen_merge_models(manifest, tensors):
     manifest["merge_models"] = out_cases
 
 
+# ----------------------------------------------------------------------------------------
+# selection (module-level nested defs in the masters: compiled from the source text)
+
+SELECTION_DEFS = {
+    "rank_based_lm_sim": ("EDT_LM/edt_sim.py", 177, 214, "rank_based_selection"),
+    "rank_based_lm": ("EDT_LM/edt.py", 185, 211, "rank_based_selection"),
+    "tournament_lm": ("EDT_LM/edt.py", 213, 224, "tournament_selection"),
+    "rank_based_evomerge": ("EDT_EVOMERGE/edt.py", 193, 230, "rank_based_selection"),
+    "roulette_rl": ("EDT_RL/edt.py", 221, 240, "roulette_wheel_selection"),
+    "rank_based_rl": ("EDT_RL/edt.py", 243, 261, "rank_based_selection"),
+}
+
+
+def gen_selection(manifest, tensors):
+    import random
+    recs = []
+    genomes = [{"model_path": f"m{i}/Gen0003", "fitness": f, "dna": [i % 4, 1, 2]}
+               for i, f in enumerate([0.31, 0.52, 0.18, 0.52, 0.77, 0.05, 0.44, 0.29])]
+    for name, (rel, first, last, fn) in SELECTION_DEFS.items():
+        ns = {"random": random, "YELLOW": "", "RESET": "", "print": lambda *a, **k: None}
+        exec(_block(rel, first, last), ns)
+        f = ns[fn]
+        for seed in (0, 3, 11):
+            for num_pairs in (1, 4, 7):
+                args = (genomes, num_pairs)
+                extra = []
+                if name == "roulette_rl":
+                    for scale in (0.1, 1.3, 2.5):
+                        random.seed(seed)
+                        pairs = f(genomes, num_pairs, scale)
+                        recs.append({"fn": name, "source": f"{rel}:{first}-{last}", "seed": seed,
+                                     "num_pairs": num_pairs, "scale": scale,
+                                     "pairs": [[genomes.index(a), genomes.index(b)] for a, b in pairs]})
+                    continue
+                random.seed(seed)
+                pairs = f(*args, *extra)
+                recs.append({"fn": name, "source": f"{rel}:{first}-{last}", "seed": seed, "num_pairs": num_pairs,
+                             "pairs": [[genomes.index(a), genomes.index(b)] for a, b in pairs]})
+    manifest["selection"] = {"genomes": genomes, "cases": recs}
+
+
 def main():
     torch.manual_seed(0)
     manifest = {"generated_with": {"torch": torch.__version__, "numpy": np.__version__}}
     import transformers
     manifest["generated_with"]["transformers"] = transformers.__version__
     for fn, fname in ((gen_diloco, "diloco"), (gen_pair_merge, "pair_merge"),
-                      (gen_slerp, "slerp"), (gen_merge_models, "merge_models")):
+                      (gen_slerp, "slerp"), (gen_merge_models, "merge_models"), (gen_selection, None)):
         tensors = {}
         fn(manifest, tensors)
+        if fname is None:
+            continue
         tensors = {k: v.detach().contiguous().clone() for k, v in tensors.items()}
         save_file(tensors, os.path.join(HERE, f"{fname}.safetensors"))
         print(f"{fname}: {len(tensors)} tensors")

@@ -104,3 +104,82 @@ def test_sharded_outer_step_world2(tmp_path, oracle, mode, tdt, wdt):
         scale = 0.7 * (mom_ref.float().abs() * 1.9)
         tol = 2 * _ulp(th_ref, tdt) + 4 * _ulp(scale, tdt)
         assert ((got.float() - th_ref.float()).abs() <= tol).all()
+
+
+# ------------------------------------------------------------------------------------------
+# population crossover across ranks (one member per rank), CPU oracle as the kernels
+
+class _OracleKernels:
+    """Test-only stand-in for the HIP kernels (the product default is ops)."""
+
+    def __init__(self, oracle):
+        self.o = oracle
+
+    def make_slerp_plan(self, offsets, device):
+        return list(offsets)
+
+    def slerp_arena(self, plan, v0, v1, out, t, thr, eps):
+        for s in range(len(plan) - 1):
+            a, b = plan[s], plan[s + 1]
+            out[a:b] = self.o.slerp(float(t[s]), v0[a:b], v1[a:b], thr, eps).to(out.dtype)
+
+    def pair_merge(self, b1, b2, m1, m2, out, mom, has, lr, mu, nesterov):
+        self.o.pair_merge(b1, b2, m1, m2, out, mom, has, lr, mu, nesterov)
+
+
+POP_SHAPES = [(33, 7), (5,), (300,)]
+
+
+def _member(r, kind):
+    g = torch.Generator().manual_seed(1000 + r)
+    from evolutionarydistributedtraining_amd.params import ParamLayout
+    n = ParamLayout(POP_SHAPES).total
+    base = (torch.randn(n, generator=g) * 0.02).to(torch.bfloat16)
+    trained = (base.float() + torch.randn(n, generator=g) * 1e-3).to(torch.bfloat16)
+    mom = (torch.randn(n, generator=g) * 1e-3).to(torch.bfloat16)
+    return base, trained, mom
+
+
+def _pop_worker(rank, world, port, pairs, outdir):
+    import torch.distributed as dist
+
+    from evolutionarydistributedtraining_amd.distributed import PopulationCrossover
+    from evolutionarydistributedtraining_amd.params import ParamLayout
+    from oracle import oracle
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    layout = ParamLayout(POP_SHAPES)
+    pc = PopulationCrossover(layout, torch.bfloat16, "cpu", kernels=_OracleKernels(oracle))
+    base, trained, mom = _member(rank, "lm")
+    t = torch.tensor([0.3, 0.5, 0.9], dtype=torch.float64)
+    child_slerp = torch.empty(layout.total, dtype=torch.float32)
+    pc.slerp_step(trained, pairs, t, child_slerp)
+    child = torch.empty(layout.total, dtype=torch.bfloat16)
+    child_mom = torch.empty_like(mom)
+    pc.pair_merge_step(base, trained, mom, pairs, child, child_mom)
+    torch.save({"slerp": child_slerp, "child": child, "mom": child_mom}, os.path.join(outdir, f"pop{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.slow
+def test_population_crossover_world3(tmp_path, oracle):
+    world = 3
+    pairs = [(1, 2), (0, 0), (2, 0)]          # child 1 is a self-pair; member 0 goes to two ranks
+    port = _free_port()
+    mp.start_processes(_pop_worker, args=(world, port, pairs, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    from evolutionarydistributedtraining_amd.params import ParamLayout
+    offs = ParamLayout(POP_SHAPES).offsets
+    t = [0.3, 0.5, 0.9]
+    members = [_member(r, "lm") for r in range(world)]
+    for c, (i, j) in enumerate(pairs):
+        got = torch.load(tmp_path / f"pop{c}.pt", weights_only=True)
+        want = torch.cat([oracle.slerp(t[s], members[i][1][offs[s]:offs[s + 1]], members[j][1][offs[s]:offs[s + 1]])
+                          for s in range(3)])
+        assert torch.equal(got["slerp"], want), c
+        out = torch.empty(offs[-1], dtype=torch.bfloat16)
+        mom = members[i][2].clone()
+        oracle.pair_merge(members[i][0], members[j][0], members[i][1], members[j][1], out, mom, True, 0.7, 0.9, True)
+        assert torch.equal(got["child"].view(torch.int16), out.view(torch.int16)), c
+        assert torch.equal(got["mom"].view(torch.int16), mom.view(torch.int16)), c
