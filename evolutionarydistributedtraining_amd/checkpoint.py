@@ -1,0 +1,182 @@
+"""Checkpoint edge of the outer step.
+
+The reference gathers the population with K x `from_pretrained` and broadcasts the new global
+model with K x `save_pretrained` (EDT_LM/diloco.py:231-235, 302-308): per tensor Python objects,
+a CPU model per replica. Here a HF checkpoint directory (`model.safetensors`, or sharded with
+`model.safetensors.index.json`) is read straight into a flat parameter arena: the safetensors
+header gives every tensor's byte range, runs of consecutive tensors are read with `readinto`
+into pinned host staging buffers and copied host->device asynchronously on a copy stream, two
+staging buffers in flight, so disk/page-cache reads overlap the PCIe transfers. Writing is the
+reverse (device->pinned->file) and produces a file `safetensors`/`transformers` load unchanged.
+"""
+from __future__ import annotations
+
+import json
+import os
+import struct
+
+import torch
+
+from .params import ParamLayout
+
+_ST_DTYPES = {"F32": torch.float32, "BF16": torch.bfloat16, "F16": torch.float16, "F64": torch.float64,
+              "I64": torch.int64, "I32": torch.int32, "I16": torch.int16, "I8": torch.int8, "U8": torch.uint8,
+              "BOOL": torch.bool}
+_ST_NAMES = {v: k for k, v in _ST_DTYPES.items()}
+
+
+def read_header(path: str):
+    """(header dict, byte offset of the data section) of a .safetensors file."""
+    with open(path, "rb") as f:
+        (n,) = struct.unpack("<Q", f.read(8))
+        header = json.loads(f.read(n))
+    return header, 8 + n
+
+
+def checkpoint_files(model_dir: str) -> dict[str, str]:
+    """tensor name -> file for a HF save_pretrained directory (single or sharded)."""
+    idx = os.path.join(model_dir, "model.safetensors.index.json")
+    if os.path.exists(idx):
+        with open(idx) as f:
+            wm = json.load(f)["weight_map"]
+        return {k: os.path.join(model_dir, v) for k, v in wm.items()}
+    path = os.path.join(model_dir, "model.safetensors")
+    header, _ = read_header(path)
+    return {k: path for k in header if k != "__metadata__"}
+
+
+class _Staging:
+    """Two pinned host buffers used round-robin, each guarded by the event of its last copy."""
+
+    def __init__(self, nbytes: int, device):
+        pin = device.type == "cuda"
+        self.bufs = [torch.empty(nbytes, dtype=torch.uint8, pin_memory=pin) for _ in range(2)]
+        self.events = [None, None]
+        self.i = 0
+        self.stream = torch.cuda.Stream(device) if device.type == "cuda" else None
+
+    def next(self):
+        i = self.i
+        self.i ^= 1
+        if self.events[i] is not None:
+            self.events[i].synchronize()
+        return i, self.bufs[i]
+
+    def record(self, i):
+        if self.stream is not None:
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+            self.events[i] = ev
+
+
+def read_into_arena(model_dir: str, layout: ParamLayout, flat: torch.Tensor,
+                    names: list[str] | None = None, staging_bytes: int = 64 << 20) -> torch.Tensor:
+    """Fill `flat` (layout order) from a HF checkpoint directory. A checkpoint tensor whose dtype
+    differs from the arena's is converted on the device after the copy (torch copy_ rounding,
+    as load_state_dict does)."""
+    names = names or layout.names
+    if len(names) != len(layout):
+        raise ValueError("layout needs a name per tensor")
+    files = checkpoint_files(model_dir)
+    headers = {p: read_header(p) for p in set(files.values())}
+    dev = flat.device
+    es = flat.element_size()
+    stage = _Staging(staging_bytes, dev)
+    copy_stream = stage.stream
+    if copy_stream is not None:        # earlier kernels on the compute stream may still read `flat`
+        copy_stream.wait_stream(torch.cuda.current_stream(dev))
+    # group consecutive arena tensors that are also consecutive, same-dtype byte ranges in one file
+    runs = []
+    for k, name in enumerate(names):
+        if name not in files:
+            raise KeyError(f"{name} not in checkpoint {model_dir}")
+        path = files[name]
+        h, base = headers[path]
+        meta = h[name]
+        dt = _ST_DTYPES[meta["dtype"]]
+        if list(meta["shape"]) != list(layout.shapes[k]):
+            raise ValueError(f"{name}: checkpoint shape {meta['shape']} != {list(layout.shapes[k])}")
+        b0, b1 = meta["data_offsets"]
+        r = runs[-1] if runs else None
+        if r and r["path"] == path and r["dtype"] == dt and r["fend"] == base + b0 and dt == flat.dtype:
+            r["fend"] = base + b1
+            r["n"] += layout.numels[k]
+        else:
+            runs.append({"path": path, "dtype": dt, "fbeg": base + b0, "fend": base + b1,
+                         "arena": layout.offsets[k], "n": layout.numels[k]})
+    handles = {}
+    try:
+        for r in runs:
+            f = handles.setdefault(r["path"], open(r["path"], "rb", buffering=0))
+            res = torch.empty(0, dtype=r["dtype"]).element_size()
+            done = 0
+            total = r["fend"] - r["fbeg"]
+            while done < total:
+                i, buf = stage.next()
+                nb = min(total - done, buf.numel() // res * res)
+                f.seek(r["fbeg"] + done)
+                mv = memoryview(buf.numpy())[:nb]
+                got = f.readinto(mv)
+                if got != nb:
+                    raise IOError(f"short read from {r['path']}")
+                src = buf[:nb].view(r["dtype"])
+                a = r["arena"] + done // res
+                dst = flat[a:a + nb // res]
+                if copy_stream is not None:
+                    with torch.cuda.stream(copy_stream):
+                        dst.copy_(src, non_blocking=True) if r["dtype"] == flat.dtype else \
+                            dst.copy_(src.to(dev, non_blocking=True))
+                    stage.record(i)
+                else:
+                    dst.copy_(src)
+                done += nb
+    finally:
+        for f in handles.values():
+            f.close()
+    if copy_stream is not None:
+        torch.cuda.current_stream(dev).wait_stream(copy_stream)
+    return flat
+
+
+def write_from_arena(path: str, layout: ParamLayout, flat: torch.Tensor, names: list[str] | None = None,
+                     metadata: dict | None = None, staging_bytes: int = 64 << 20) -> None:
+    """Write `flat` as a .safetensors file (tensors in layout order, one contiguous data section)."""
+    names = names or layout.names
+    dt = flat.dtype
+    es = flat.element_size()
+    header = {"__metadata__": metadata or {"format": "pt"}}
+    off = 0
+    for name, shape, n in zip(names, layout.shapes, layout.numels):
+        header[name] = {"dtype": _ST_NAMES[dt], "shape": list(shape), "data_offsets": [off, off + n * es]}
+        off += n * es
+    hb = json.dumps(header, separators=(",", ":")).encode()
+    hb += b" " * ((8 - len(hb) % 8) % 8)
+    dev = flat.device
+    host = torch.empty(min(staging_bytes // es, max(1, flat.numel())), dtype=dt,
+                       pin_memory=dev.type == "cuda")
+    tmp = path + ".tmp"
+    with open(tmp, "wb") as f:
+        f.write(struct.pack("<Q", len(hb)))
+        f.write(hb)
+        for a in range(0, flat.numel(), host.numel()):
+            b = min(flat.numel(), a + host.numel())
+            h = host[:b - a]
+            h.copy_(flat[a:b])
+            if dev.type == "cuda":
+                torch.cuda.current_stream(dev).synchronize()
+            f.write(memoryview(h.view(torch.uint8).numpy()))
+    os.replace(tmp, path)
+
+
+def save_to_dirs(dirs: list[str], layout: ParamLayout, flat: torch.Tensor, names=None) -> None:
+    """The broadcast edge (EDT_LM/diloco.py:302-308): the new global model to every worker dir.
+    Written once, then copied file-to-file (no repeated device->host traffic)."""
+    import shutil
+    if not dirs:
+        return
+    os.makedirs(dirs[0], exist_ok=True)
+    first = os.path.join(dirs[0], "model.safetensors")
+    write_from_arena(first, layout, flat, names)
+    for d in dirs[1:]:
+        os.makedirs(d, exist_ok=True)
+        shutil.copyfile(first, os.path.join(d, "model.safetensors"))

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--k", type=int, default=8)
     ap.add_argument("--bucket-elems", type=int, default=1 << 24)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--disk-dir", default=None, help="also time the checkpoint edge through files here")
     a = ap.parse_args()
     from evolutionarydistributedtraining_amd import ops
     from evolutionarydistributedtraining_amd.layouts import LAYOUTS
@@ -91,7 +92,63 @@ def main():
     torch.cuda.synchronize()
     tk = (time.perf_counter() - t0) / a.reps
     res["device_resident"] = {"ms": round(tk * 1e3, 3), "metric_GBps": round(metric_bytes / tk / 1e9, 1)}
+    if a.disk_dir:
+        res["checkpoint_edge"] = disk_edge(a, P, workers_h, theta_d, mom_d, workers_d, metric_bytes)
     print(json.dumps({"layout": a.layout, "P": P, "K": a.k, "bucket_elems": a.bucket_elems, **res}))
+
+
+def disk_edge(a, P, workers_h, theta_d, mom_d, workers_d, metric_bytes):
+    """The gather/broadcast edge through checkpoint files (EDT_LM/diloco.py:231-235, 302-308):
+    K worker dirs -> arenas (checkpoint.read_into_arena) -> outer step -> new theta to K dirs
+    (checkpoint.save_to_dirs), against safetensors.load_file/save_file per worker (the loader
+    HF from_pretrained/save_pretrained use), page cache warm for both."""
+    import shutil
+    import tempfile
+    from safetensors.torch import load_file, save_file
+    from evolutionarydistributedtraining_amd import checkpoint, ops
+    from evolutionarydistributedtraining_amd.layouts import LAYOUTS
+    lay = LAYOUTS[a.layout]()
+    root = tempfile.mkdtemp(dir=a.disk_dir)
+    try:
+        dirs = [os.path.join(root, f"w{k}") for k in range(a.k)]
+        for d, wh in zip(dirs, workers_h):
+            os.makedirs(d)
+            checkpoint.write_from_arena(os.path.join(d, "model.safetensors"), lay, wh)
+        out_dirs = [os.path.join(root, f"o{k}") for k in range(a.k)]
+        out = {}
+        for rep in range(2):                      # second pass: warm page cache
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for d, wd in zip(dirs, workers_d):
+                checkpoint.read_into_arena(d, lay, wd)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            ops.outer_step(theta_d, workers_d, mom_d, True, 0.7, 0.9, True)
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            checkpoint.save_to_dirs(out_dirs, lay, theta_d)
+            t3 = time.perf_counter()
+            out = {"read_ms": round((t1 - t0) * 1e3, 1), "step_ms": round((t2 - t1) * 1e3, 2),
+                   "write_ms": round((t3 - t2) * 1e3, 1),
+                   "read_GBps": round(metric_bytes / (t1 - t0) / 1e9, 2),
+                   "total_metric_GBps": round(metric_bytes / (t3 - t0) / 1e9, 2)}
+        # per-worker safetensors load/save, as from_pretrained / save_pretrained do it
+        t0 = time.perf_counter()
+        for d, wd in zip(dirs, workers_d):
+            sd = load_file(os.path.join(d, "model.safetensors"))
+            for v, (k, x) in zip(lay.views(wd), sd.items()):
+                v.copy_(x)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        cpu_theta = {n: v.detach().cpu().contiguous() for n, v in zip(lay.names, lay.views(theta_d))}
+        for d in out_dirs:
+            save_file(cpu_theta, os.path.join(d, "ref.safetensors"))
+        t2 = time.perf_counter()
+        out["safetensors_load_ms"] = round((t1 - t0) * 1e3, 1)
+        out["safetensors_save_ms"] = round((t2 - t1) * 1e3, 1)
+        return out
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,63 @@
+"""Checkpoint edge: HF save_pretrained directories (single file and sharded) read straight into a
+flat parameter arena, and arenas written back as safetensors that HF loads unchanged. I/O only,
+so the arena may live on the CPU here; the GPU form is exercised in scripts/e2e_rate.py."""
+import os
+import shutil
+
+import pytest
+import torch
+from safetensors.torch import load_file
+
+from evolutionarydistributedtraining_amd import checkpoint
+from evolutionarydistributedtraining_amd.params import ParamArena, ParamLayout, pack
+
+
+def _tiny(dtype):
+    from transformers import LlamaConfig, LlamaForCausalLM
+    cfg = LlamaConfig(vocab_size=40, hidden_size=16, intermediate_size=24, num_hidden_layers=3,
+                      num_attention_heads=2, num_key_value_heads=1, tie_word_embeddings=False)
+    torch.manual_seed(0)
+    return LlamaForCausalLM(cfg).to(dtype)
+
+
+@pytest.mark.parametrize("shard", [None, "8KB"])
+@pytest.mark.parametrize("ckpt_dtype,arena_dtype", [(torch.bfloat16, torch.bfloat16), (torch.float32, torch.float32),
+                                                    (torch.bfloat16, torch.float32)])
+def test_read_hf_checkpoint_into_arena(tmp_path, shard, ckpt_dtype, arena_dtype):
+    m = _tiny(ckpt_dtype)
+    kw = {"max_shard_size": shard} if shard else {}
+    m.save_pretrained(tmp_path, **kw)
+    if shard:
+        assert os.path.exists(tmp_path / "model.safetensors.index.json")
+    layout = ParamLayout.of_module(m)
+    arena = ParamArena(layout, arena_dtype, "cpu")
+    checkpoint.read_into_arena(str(tmp_path), layout, arena.flat, staging_bytes=4096)
+    want = pack(list(m.parameters()), dtype=arena_dtype)
+    assert torch.equal(arena.flat, want)
+
+
+def test_write_arena_is_loadable_by_safetensors_and_hf(tmp_path):
+    from transformers import LlamaForCausalLM
+    m = _tiny(torch.bfloat16)
+    m.save_pretrained(tmp_path / "src")
+    layout = ParamLayout.of_module(m)
+    flat = pack(list(m.parameters())) * 2
+    out = tmp_path / "dst"
+    checkpoint.save_to_dirs([str(out), str(tmp_path / "dst2")], layout, flat)
+    sd = load_file(str(out / "model.safetensors"))
+    for (name, p), v in zip(m.named_parameters(), layout.views(flat)):
+        assert torch.equal(sd[name], v)
+    shutil.copy(tmp_path / "src" / "config.json", out / "config.json")
+    m2 = LlamaForCausalLM.from_pretrained(out, dtype=torch.bfloat16)
+    for a, b in zip(m2.parameters(), layout.views(flat)):
+        assert torch.equal(a, b)
+    assert (tmp_path / "dst2" / "model.safetensors").read_bytes() == (out / "model.safetensors").read_bytes()
+
+
+def test_shape_mismatch_is_an_error(tmp_path):
+    m = _tiny(torch.float32)
+    m.save_pretrained(tmp_path)
+    layout = ParamLayout.of_module(m)
+    bad = ParamLayout([(1,)] + layout.shapes[1:], layout.names)
+    with pytest.raises(ValueError):
+        checkpoint.read_into_arena(str(tmp_path), bad, torch.empty(bad.total))
