@@ -138,45 +138,57 @@ def read_into_arena(model_dir: str, layout: ParamLayout, flat: torch.Tensor,
     return flat
 
 
-def write_from_arena(path: str, layout: ParamLayout, flat: torch.Tensor, names: list[str] | None = None,
-                     metadata: dict | None = None, staging_bytes: int = 64 << 20) -> None:
-    """Write `flat` as a .safetensors file (tensors in layout order, one contiguous data section)."""
-    names = names or layout.names
-    dt = flat.dtype
-    es = flat.element_size()
+def _header_bytes(layout: ParamLayout, names, dtype, metadata) -> bytes:
+    es = torch.empty(0, dtype=dtype).element_size()
     header = {"__metadata__": metadata or {"format": "pt"}}
     off = 0
     for name, shape, n in zip(names, layout.shapes, layout.numels):
-        header[name] = {"dtype": _ST_NAMES[dt], "shape": list(shape), "data_offsets": [off, off + n * es]}
+        header[name] = {"dtype": _ST_NAMES[dtype], "shape": list(shape), "data_offsets": [off, off + n * es]}
         off += n * es
     hb = json.dumps(header, separators=(",", ":")).encode()
-    hb += b" " * ((8 - len(hb) % 8) % 8)
-    dev = flat.device
-    host = torch.empty(min(staging_bytes // es, max(1, flat.numel())), dtype=dt,
-                       pin_memory=dev.type == "cuda")
+    hb += b" " * ((8 - len(hb) % 8) % 8)          # data section 8-byte aligned
+    return struct.pack("<Q", len(hb)) + hb
+
+
+_pinned: dict = {}
+
+
+def _host_copy(flat: torch.Tensor) -> torch.Tensor:
+    if flat.device.type != "cuda":
+        return flat.contiguous()
+    key = (flat.numel(), flat.dtype)
+    host = _pinned.get(key)
+    if host is None:                              # pinning is slow: keep the last buffer
+        _pinned.clear()
+        host = _pinned[key] = torch.empty(flat.numel(), dtype=flat.dtype, pin_memory=True)
+    host.copy_(flat)                              # one device->host transfer, synchronous
+    return host
+
+
+def _write_file(path: str, header: bytes, host: torch.Tensor) -> None:
     tmp = path + ".tmp"
     with open(tmp, "wb") as f:
-        f.write(struct.pack("<Q", len(hb)))
-        f.write(hb)
-        for a in range(0, flat.numel(), host.numel()):
-            b = min(flat.numel(), a + host.numel())
-            h = host[:b - a]
-            h.copy_(flat[a:b])
-            if dev.type == "cuda":
-                torch.cuda.current_stream(dev).synchronize()
-            f.write(memoryview(h.view(torch.uint8).numpy()))
+        f.write(header)
+        f.write(memoryview(host.view(torch.uint8).numpy()))
     os.replace(tmp, path)
 
 
+def write_from_arena(path: str, layout: ParamLayout, flat: torch.Tensor, names: list[str] | None = None,
+                     metadata: dict | None = None) -> None:
+    """Write `flat` as a .safetensors file (tensors in layout order, one contiguous data section)."""
+    _write_file(path, _header_bytes(layout, names or layout.names, flat.dtype, metadata), _host_copy(flat))
+
+
 def save_to_dirs(dirs: list[str], layout: ParamLayout, flat: torch.Tensor, names=None) -> None:
-    """The broadcast edge (EDT_LM/diloco.py:302-308): the new global model to every worker dir.
-    Written once, then copied file-to-file (no repeated device->host traffic)."""
-    import shutil
+    """The broadcast edge (EDT_LM/diloco.py:302-308): the new global model to every worker dir —
+    one device->host copy, then the K files written by a thread pool (as the reference's
+    ThreadPoolExecutor save does)."""
+    from concurrent.futures import ThreadPoolExecutor
     if not dirs:
         return
-    os.makedirs(dirs[0], exist_ok=True)
-    first = os.path.join(dirs[0], "model.safetensors")
-    write_from_arena(first, layout, flat, names)
-    for d in dirs[1:]:
+    header = _header_bytes(layout, names or layout.names, flat.dtype, None)
+    host = _host_copy(flat)
+    for d in dirs:
         os.makedirs(d, exist_ok=True)
-        shutil.copyfile(first, os.path.join(d, "model.safetensors"))
+    with ThreadPoolExecutor(max_workers=min(len(dirs), 16)) as ex:
+        list(ex.map(lambda d: _write_file(os.path.join(d, "model.safetensors"), header, host), dirs))

@@ -136,8 +136,8 @@ def disk_edge(a, P, workers_h, theta_d, mom_d, workers_d, metric_bytes):
         t0 = time.perf_counter()
         for d, wd in zip(dirs, workers_d):
             sd = load_file(os.path.join(d, "model.safetensors"))
-            for v, (k, x) in zip(lay.views(wd), sd.items()):
-                v.copy_(x)
+            for v, n in zip(lay.views(wd), lay.names):
+                v.copy_(sd[n])
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         cpu_theta = {n: v.detach().cpu().contiguous() for n, v in zip(lay.names, lay.views(theta_d))}
