@@ -14,6 +14,8 @@ the benchmark and the multi-GPU path use.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import ops
@@ -170,3 +172,67 @@ class OuterSync:
         if self.momentum != 0:
             b += (2 if self.state.has_momentum else 1) * n * self.theta.flat.element_size()
         return b
+
+
+class DirOuterSync:
+    """The whole outer step of EDT_LM/diloco.py:224-308 on checkpoint directories, with no HF
+    model objects: the base (GenN of worker 0) and the K trained replicas (GenN+1) are read
+    straight into HBM arenas (checkpoint.read_into_arena), the fused kernel runs, and the new
+    global weights are written to every worker's GenN+1 dir (checkpoint.save_to_dirs) together
+    with the base dir's config/tokenizer files. Arenas and the outer state persist across
+    generations, so the momentum carry of diloco.py:258-286 needs no state_dict round trip.
+
+    names: parameter names in `model.parameters()` order (e.g. `ParamLayout.of_module(model).names`)
+    — the index order of the momentum; default: the checkpoint's own tensor order."""
+
+    def __init__(self, device=None, theta_dtype=None, worker_dtype=None, names=None,
+                 lr=0.7, momentum=0.9, nesterov=True, state: OuterState | None = None):
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.theta_dtype, self.worker_dtype, self.names = theta_dtype, worker_dtype, names
+        self.lr, self.momentum, self.nesterov = lr, momentum, nesterov
+        self.state = state or OuterState()
+        self.layout = None
+        self.theta = None
+        self.workers: list[ParamArena] = []
+        self._written: set[str] = set()     # dirs holding the resident theta (last step's output)
+
+    def _layout_from(self, model_dir):
+        from .checkpoint import checkpoint_files, read_header, _ST_DTYPES
+        files = checkpoint_files(model_dir)
+        metas = {}
+        for path in set(files.values()):
+            h, base = read_header(path)
+            for k, v in h.items():
+                if k != "__metadata__":
+                    metas[k] = (path, v)
+        names = self.names or sorted(metas, key=lambda k: (metas[k][0], metas[k][1]["data_offsets"][0]))
+        dt = _ST_DTYPES[metas[names[0]][1]["dtype"]]
+        return ParamLayout([tuple(metas[n][1]["shape"]) for n in names], names), dt
+
+    def step(self, base_dir: str, worker_dirs: list[str], out_dirs: list[str] | None = None) -> OuterState:
+        import shutil
+        from .checkpoint import read_into_arena, save_to_dirs
+        if self.layout is None:
+            self.layout, ckpt_dt = self._layout_from(base_dir)
+            self.theta_dtype = self.theta_dtype or ckpt_dt
+            self.worker_dtype = self.worker_dtype or ckpt_dt
+            self.theta = ParamArena(self.layout, self.theta_dtype, self.device)
+        while len(self.workers) < len(worker_dirs):
+            self.workers.append(ParamArena(self.layout, self.worker_dtype, self.device))
+        if os.path.abspath(base_dir) not in self._written:   # else theta is already resident
+            read_into_arena(base_dir, self.layout, self.theta.flat)
+        for d, arena in zip(worker_dirs, self.workers):
+            read_into_arena(d, self.layout, arena.flat)
+        _step_flat(self.theta.flat, [w.flat for w in self.workers[:len(worker_dirs)]], self.state,
+                   self.lr, self.momentum, self.nesterov)
+        out_dirs = worker_dirs if out_dirs is None else out_dirs
+        save_to_dirs(out_dirs, self.layout, self.theta.flat)
+        self._written = {os.path.abspath(d) for d in out_dirs}
+        for d in out_dirs:                  # config / generation config / tokenizer of the base
+            for f in os.listdir(base_dir):
+                src = os.path.join(base_dir, f)
+                if os.path.isfile(src) and not f.startswith("model.safetensors") and f not in (
+                        "genome.json", "optimizer.pt", "scheduler.pt", "outer_optim.pt"):
+                    if os.path.abspath(src) != os.path.abspath(os.path.join(d, f)):
+                        shutil.copyfile(src, os.path.join(d, f))
+        return self.state

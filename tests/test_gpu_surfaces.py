@@ -270,3 +270,40 @@ def test_single_tensor_slerp_api(golden, dev):
     assert isinstance(r_np, np.ndarray)
     r_dev = slerp(c["t"], v0.to(dev), v1.to(dev))
     assert r_dev.is_cuda and torch.equal(r_dev.cpu(), r_cpu)
+
+
+def test_dir_outer_sync_two_generations(oracle, dev, tmp_path):
+    """DirOuterSync: checkpoint dirs in, fused step, checkpoint dirs out (EDT_LM/diloco.py:224-308),
+    two generations with the momentum carried, vs the oracle; outputs load with HF."""
+    from transformers import LlamaForCausalLM
+    from evolutionarydistributedtraining_amd.diloco import DirOuterSync
+    from evolutionarydistributedtraining_amd.params import ParamLayout, pack
+    K = 3
+    base = _llama([p.detach() for p in _llama([]).parameters()], torch.bfloat16)
+    g = torch.Generator().manual_seed(21)
+    with torch.no_grad():
+        for p in base.parameters():
+            p.copy_(torch.randn(p.shape, generator=g) * 0.02)
+    layout = ParamLayout.of_module(base)
+    base.save_pretrained(tmp_path / "w0" / "Gen0000")
+    sync = DirOuterSync(device=dev, names=layout.names, lr=0.7, momentum=0.9, nesterov=True)
+    theta = pack(list(base.parameters()))
+    mom = torch.zeros_like(theta)
+    prev = str(tmp_path / "w0" / "Gen0000")
+    for gen in range(2):
+        dirs = []
+        workers = []
+        for k in range(K):
+            d = tmp_path / f"w{k}" / f"Gen{gen + 1:04d}"
+            m = _llama([(t.float() + torch.randn(t.shape, generator=g) * 1e-3).bfloat16()
+                        for t in layout.views(theta)])
+            m.save_pretrained(d)
+            dirs.append(str(d))
+            workers.append(pack(list(m.parameters())))
+        sync.step(prev, dirs)
+        oracle.outer_step(theta, workers, mom, gen > 0, 0.7, 0.9, True)
+        for d in dirs:
+            got = LlamaForCausalLM.from_pretrained(d, dtype=torch.bfloat16)
+            assert torch.equal(bits(pack(list(got.parameters()))), bits(theta)), (gen, d)
+        prev = dirs[0]
+    assert torch.equal(bits(sync.state.momentum.cpu()), bits(mom))
