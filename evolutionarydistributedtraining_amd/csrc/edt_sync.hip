@@ -31,13 +31,16 @@ namespace {
 #ifndef EDT_BLOCKS_PER_CU
 #define EDT_BLOCKS_PER_CU 256
 #endif
-#ifndef EDT_NT_LOADS          // non-temporal loads for the once-read worker streams
-#define EDT_NT_LOADS 1
+#ifndef EDT_NT_LOADS          // non-temporal loads for the once-read bf16 worker streams
+#define EDT_NT_LOADS 1        // (fp32 streams: measured 1.6x SLOWER with nt, 17.5 vs 11.2 ms)
 #endif
 #ifndef EDT_NT_STORES         // non-temporal stores for theta / momentum
 #define EDT_NT_STORES 0
 #endif
 
+#ifndef EDT_NT_LERP             // non-temporal loads of lerp's two (read-once) inputs
+#define EDT_NT_LERP 0
+#endif
 #ifndef EDT_MIN_WAVES           // __launch_bounds__ minimum waves per SIMD for the stream kernels
 #define EDT_MIN_WAVES 1
 #endif
@@ -278,7 +281,7 @@ __device__ __forceinline__ void outer_elems(const OuterArgs& a, uint64_t i) {
     const int K = KC > 0 ? KC : a.K;
     auto body = [&](int k) {
         float w[N];
-        ld<WDT, N, EDT_NT_LOADS != 0>(a.w.p[k], i, w);
+        ld<WDT, N, EDT_NT_LOADS != 0 && WDT == EDT_BF16>(a.w.p[k], i, w);
 #pragma unroll
         for (int j = 0; j < N; ++j) w[j] = w[j] - g[j];              // trained - base
         rnd<GDT>(w);
@@ -378,8 +381,8 @@ __device__ __forceinline__ void pair_elems(const PairArgs& a, uint64_t i) {
     ld_momentum<GDT, N>(a.mom, i, a.sgd, b_in);
     if (a.b2) {                        // run_linear_merge_5050: lerp(0.5, b1, b2) in the model dtype
         float x[N], y[N];
-        ld<WDT, N, EDT_NT_LOADS != 0>(a.b1, i, x);
-        ld<WDT, N, EDT_NT_LOADS != 0>(a.b2, i, y);
+        ld<WDT, N, EDT_NT_LOADS != 0 && WDT == EDT_BF16>(a.b1, i, x);
+        ld<WDT, N, EDT_NT_LOADS != 0 && WDT == EDT_BF16>(a.b2, i, y);
 #pragma unroll
         for (int j = 0; j < N; ++j) { x[j] = x[j] * 0.5f; y[j] = y[j] * 0.5f; }   // (1-.5)*v0, .5*v1
         rnd<WDT>(x);
@@ -392,8 +395,8 @@ __device__ __forceinline__ void pair_elems(const PairArgs& a, uint64_t i) {
     }
     rnd<GDT>(base);                    // load_state_dict into the base model's dtype
     float d1[N], d2[N];
-    ld<WDT, N, EDT_NT_LOADS != 0>(a.m1, i, d1);
-    ld<WDT, N, EDT_NT_LOADS != 0>(a.m2, i, d2);
+    ld<WDT, N, EDT_NT_LOADS != 0 && WDT == EDT_BF16>(a.m1, i, d1);
+    ld<WDT, N, EDT_NT_LOADS != 0 && WDT == EDT_BF16>(a.m2, i, d2);
 #pragma unroll
     for (int j = 0; j < N; ++j) { d1[j] = d1[j] - base[j]; d2[j] = d2[j] - base[j]; }
     rnd<GDT>(d1);
@@ -451,7 +454,8 @@ __global__ __launch_bounds__(kBlock) void lerp_kernel(const void* v0, const void
     const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if constexpr (N == kVec) {
         const uint64_t nv = n / kVec;
-        for (uint64_t v = tid; v < nv; v += stride) lerp_elems<IDT, ODT, CDT, kVec>(v0, v1, out, v * kVec, c0, c1);
+        for (uint64_t v = tid; v < nv; v += stride)
+            lerp_elems<IDT, ODT, CDT, kVec, EDT_NT_LERP != 0>(v0, v1, out, v * kVec, c0, c1);
         const uint64_t t = nv * kVec + tid;
         if (t < n) lerp_elems<IDT, ODT, CDT, 1>(v0, v1, out, t, c0, c1);
     } else {

@@ -39,6 +39,51 @@ VARIANTS = {
 
 
 SLERP_VARIANTS = {"s_default": []}
+VARIANTS.update({"lerp_nt": ["-DEDT_NT_LERP=1"], "nt0": ["-DEDT_NT_LOADS=0"],
+                 "bpc32_nt0": ["-DEDT_BLOCKS_PER_CU=32", "-DEDT_NT_LOADS=0"]})
+
+
+def run_stream_ops(names, rounds, iters):
+    """lerp (1.3B bf16, 6 B/elem) and pair merge (1.3B bf16, 14 B/elem) per variant library."""
+    import torch
+    from evolutionarydistributedtraining_amd import _lib as L
+    from evolutionarydistributedtraining_amd.layouts import gpt_1p3b
+    dev = torch.device("cuda:0")
+    P = gpt_1p3b().total
+    bf = torch.bfloat16
+    a = (torch.randn(P, device=dev) * 0.02).to(bf)
+    b = (torch.randn(P, device=dev) * 0.02).to(bf)
+    m1 = (a.float() + 1e-3).to(bf)
+    m2 = (b.float() + 1e-3).to(bf)
+    out = torch.empty(P, dtype=bf, device=dev)
+    mom = torch.zeros(P, dtype=bf, device=dev)
+    st = L.stream_ptr(dev)
+    Pp = L.ptr
+    cases = {}
+    for n in names:
+        lib = ctypes.CDLL(os.path.join(VDIR, f"{n}.so"))
+        for name, res, args in L.SIGNATURES:
+            f = getattr(lib, name)
+            f.restype, f.argtypes = res, args
+        cases[f"{n}/lerp"] = (6, lambda lib=lib: lib.edt_lerp(Pp(a), Pp(b), 1, Pp(out), 1, 1, P, 0.5, st))
+        cases[f"{n}/pair"] = (14, lambda lib=lib: lib.edt_pair_merge(Pp(a), Pp(b), Pp(m1), Pp(m2), 1, Pp(out), 1,
+                                                                     Pp(mom), 1, P, 0.7, 0.9, 1, st))
+    times = {k: [] for k in cases}
+    for k, (_, f) in cases.items():
+        assert f() == 0
+    torch.cuda.synchronize()
+    for _ in range(rounds):
+        for k, (_, f) in cases.items():
+            evs = [torch.cuda.Event(enable_timing=True) for _ in range(2 * iters)]
+            for i in range(iters):
+                evs[2 * i].record()
+                f()
+                evs[2 * i + 1].record()
+            torch.cuda.synchronize()
+            times[k] += [evs[2 * i].elapsed_time(evs[2 * i + 1]) for i in range(iters)]
+    res = {k: {"median_ms": round(statistics.median(v), 4),
+               "TBps": round(cases[k][0] * P / statistics.median(v) / 1e9, 3)} for k, v in times.items()}
+    print(json.dumps({"op": "stream", "P": P, "variants": res}, indent=1))
 VARIANTS.update(SLERP_VARIANTS)
 
 
@@ -164,11 +209,13 @@ if __name__ == "__main__":
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--layout", default="gpt_1p3b")
     ap.add_argument("--k", type=int, default=8)
-    ap.add_argument("--op", default="outer", choices=["outer", "slerp"])
+    ap.add_argument("--op", default="outer", choices=["outer", "slerp", "stream"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:
         build(names)
+    elif a.op == "stream":
+        run_stream_ops(names, a.rounds, a.iters)
     elif a.op == "slerp":
         run_slerp(names, a.rounds, a.layout if a.layout != "gpt_1p3b" else "qwen2p5_7b_body")
     else:
