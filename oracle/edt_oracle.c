@@ -23,7 +23,8 @@
  *           byte per element, 1 = scalar-tail element) selects that form, so the oracle can
  *           reproduce the reference bit for bit; tail = NULL is the vectorised semantics the HIP
  *           kernels implement on every element.
- * Build: see oracle/Makefile (gcc -O2 -ffp-contract=off: no FMA except the explicit fmaf()).
+ * Build: see oracle/Makefile (gcc -O3 -march=x86-64-v3 -ffp-contract=off: the only FMAs are the
+ * explicit fmaf() calls, which x86-64-v3 executes as one vfmadd instead of a libm call).
  */
 #include <math.h>
 #include <stdint.h>
@@ -97,7 +98,33 @@ static inline float sgd_elem(int gdt, const sgd_t* s, float theta, float grad, v
     return add_alpha(gdt, theta, s->alpha_nlr, u, tail);                   /* param.add_(grad, alpha=-lr) */
 }
 
-/* DiLoCo outer step, in place on theta (gdt) and mom (gdt). */
+/* DiLoCo outer step, in place on theta (gdt) and mom (gdt). One loop body per dtype regime
+ * (GDT/WDT compile-time constants) so gcc vectorises the per-element chain. */
+#define OB 512   /* elements per block: the worker loop runs inside, vectorised over the block */
+#define OUTER_LOOP(GDT, WDT)                                                                      \
+    _Pragma("omp parallel for schedule(static)")                                                  \
+    for (int64_t bb = 0; bb < ((int64_t)n + OB - 1) / OB; ++bb) {                                 \
+        const uint64_t i0 = (uint64_t)bb * OB;                                                    \
+        const int m = (int)((n - i0) < OB ? (n - i0) : OB);                                       \
+        float g[OB], acc[OB];                                                                     \
+        for (int e = 0; e < m; ++e) {                                                             \
+            g[e] = load(theta, GDT, i0 + e);                                                      \
+            acc[e] = 0.0f;                                         /* zeros_like(base) */         \
+        }                                                                                         \
+        for (int k = 0; k < K; ++k) {                              /* worker-major, as :243 */    \
+            const void* w = workers[k];                                                           \
+            for (int e = 0; e < m; ++e) {                                                         \
+                float d = rnd(GDT, load(w, WDT, i0 + e) - g[e]);   /* trained - base */           \
+                d = rnd(GDT, pow2 ? d * kinv : d / kf);            /* delta / num_models */       \
+                acc[e] = rnd(GDT, acc[e] + d);                     /* acc += ... */               \
+            }                                                                                     \
+        }                                                                                         \
+        for (int e = 0; e < m; ++e) {                                                             \
+            const uint64_t i = i0 + e;                                                            \
+            store(theta, GDT, i, sgd_elem(GDT, &s, g[e], -acc[e], mom, i, tail ? tail[i] : 0));   \
+        }                                                                                         \
+    }
+
 int oracle_outer_step(void* theta, int gdt, const void* const* workers, int wdt, int K, void* mom,
                       int has_buf, uint64_t n, double lr, double mu, int nesterov,
                       const uint8_t* tail) {
@@ -105,17 +132,14 @@ int oracle_outer_step(void* theta, int gdt, const void* const* workers, int wdt,
     if (gdt == OR_BF16 && wdt != OR_BF16) return -1;
     const sgd_t s = make_sgd(gdt, lr, mu, has_buf, nesterov);
     const float kf = (float)K;
-#pragma omp parallel for schedule(static)
-    for (int64_t ii = 0; ii < (int64_t)n; ++ii) {
-        const uint64_t i = (uint64_t)ii;
-        const float g = load(theta, gdt, i);
-        float acc = 0.0f;                                           /* zeros_like(base) */
-        for (int k = 0; k < K; ++k) {
-            float d = rnd(gdt, load(workers[k], wdt, i) - g);       /* trained - base */
-            d = rnd(gdt, d / kf);                                   /* delta / num_models */
-            acc = rnd(gdt, acc + d);                                /* acc += ... */
-        }
-        store(theta, gdt, i, sgd_elem(gdt, &s, g, -acc, mom, i, tail ? tail[i] : 0));   /* grad = -acc */
+    const int pow2 = (K & (K - 1)) == 0;          /* x * (1/K) == x / K exactly for K = 2^j */
+    const float kinv = 1.0f / kf;
+    if (gdt == OR_BF16) {
+        OUTER_LOOP(OR_BF16, OR_BF16)
+    } else if (wdt == OR_BF16) {
+        OUTER_LOOP(OR_F32, OR_BF16)
+    } else {
+        OUTER_LOOP(OR_F32, OR_F32)
     }
     return 0;
 }
