@@ -28,6 +28,7 @@ _I = ctypes.c_int
 _D = ctypes.c_double
 SIGNATURES = [
     ("edt_outer_step", _I, [_P, _I, ctypes.POINTER(_P), _I, _I, _P, _I, _U64, _D, _D, _I, _P]),
+    ("edt_outer_step_ws", _I, [_P, _I, ctypes.POINTER(_P), _I, _I, _P, _I, _U64, _D, _D, _I, _P, _P]),
     ("edt_delta_partial", _I, [_P, _I, ctypes.POINTER(_P), _I, _I, _I, _U64, _P, _I, _P]),
     ("edt_sgd_apply", _I, [_P, _I, _P, _P, _I, _U64, _D, _D, _I, _P]),
     ("edt_pair_merge", _I, [_P, _P, _P, _P, _I, _P, _I, _P, _I, _U64, _D, _D, _I, _P]),

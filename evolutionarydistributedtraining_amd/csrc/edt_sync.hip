@@ -258,11 +258,16 @@ struct OuterArgs {
     float kinv;          // 1/K_total when K_total is a power of two
     int div_exact;       // 1: true division, 0: multiply by kinv (identical for powers of two)
     int accumulate;      // partial mode: add into acc_out
+    void* acc_ws;        // chain mode: running sum in theta's dtype between launches
+    int acc_in;          // chain mode: start from acc_ws
+    int acc_store;       // chain mode: store the running sum to acc_ws (no SGD)
     SgdScalars sgd;
     Workers w;
 };
 
-enum { MODE_FUSED = 0, MODE_PARTIAL = 1 };
+// MODE_CHAIN = MODE_FUSED for populations above EDT_MAX_WORKERS: launches of <= 32 workers
+// carry the running sum in theta's dtype (lossless: it is rounded to that dtype after every add).
+enum { MODE_FUSED = 0, MODE_PARTIAL = 1, MODE_CHAIN = 2 };
 
 // Per-element accumulation acc = sum_k round(round(w_k - g) / K) in the precision of GDT
 // (worker-major order, EDT_LM/diloco.py:243-246). MODE_PARTIAL sums the rounded quotients
@@ -271,9 +276,11 @@ template <int GDT, int WDT, int KC, int DIV, int MODE, int N>
 __device__ __forceinline__ void outer_elems(const OuterArgs& a, uint64_t i) {
     float g[N], acc[N], b_in[N];
     ld<GDT, N>(a.theta, i, g);
-    if constexpr (MODE == MODE_FUSED) ld_momentum<GDT, N>(a.mom, i, a.sgd, b_in);
+    if constexpr (MODE != MODE_PARTIAL) ld_momentum<GDT, N>(a.mom, i, a.sgd, b_in);
     if (MODE == MODE_PARTIAL && a.accumulate) {
         ld<EDT_F32, N>(a.acc_out, i, acc);      // continue the running sum in worker order
+    } else if (MODE == MODE_CHAIN && a.acc_in) {
+        ld<GDT, N>(a.acc_ws, i, acc);
     } else {
 #pragma unroll
         for (int j = 0; j < N; ++j) acc[j] = 0.f;
@@ -295,7 +302,7 @@ __device__ __forceinline__ void outer_elems(const OuterArgs& a, uint64_t i) {
         rnd<GDT>(w);
 #pragma unroll
         for (int j = 0; j < N; ++j) acc[j] = acc[j] + w[j];          // acc += delta / K
-        if constexpr (MODE == MODE_FUSED) rnd<GDT>(acc);
+        if constexpr (MODE != MODE_PARTIAL) rnd<GDT>(acc);
     };
     if constexpr (KC > 0) {
 #pragma unroll
@@ -306,6 +313,8 @@ __device__ __forceinline__ void outer_elems(const OuterArgs& a, uint64_t i) {
     }
     if constexpr (MODE == MODE_PARTIAL) {
         st<EDT_F32, N>(a.acc_out, i, acc);
+    } else if (MODE == MODE_CHAIN && a.acc_store) {
+        st<GDT, N>(a.acc_ws, i, acc);
     } else {
         float grad[N];
 #pragma unroll
@@ -638,6 +647,11 @@ int launch_outer_k(const OuterArgs& a, bool vec, hipStream_t s) {
         else outer_kernel<GDT, WDT, KC, DIV, MODE, 1><<<g, kBlock, 0, s>>>(a);                   \
     } while (0)
     // compile-time worker counts for the common populations; the divisor is K_total
+    if constexpr (MODE == MODE_CHAIN) {
+        if (a.div_exact) EDT_LAUNCH_K(0, 1);
+        else EDT_LAUNCH_K(0, 0);
+        return check_launch("outer_kernel");
+    }
     if (a.K == 1 && !a.div_exact) EDT_LAUNCH_K(1, 0);
     else if (a.K == 2 && !a.div_exact) EDT_LAUNCH_K(2, 0);
     else if (a.K == 3 && a.div_exact) EDT_LAUNCH_K(3, 1);
@@ -708,6 +722,38 @@ int edt_outer_step(void* theta_g, int gdt, const void* const* theta_k, int wdt, 
     bool vec = aligned16(theta_g) && (!a.sgd.use_momentum || aligned16(momentum));
     for (int k = 0; k < K; ++k) vec = vec && aligned16(theta_k[k]);
     return launch_outer<MODE_FUSED>(gdt, wdt, a, vec, (hipStream_t)stream);
+}
+
+int edt_outer_step_ws(void* theta_g, int gdt, const void* const* theta_k, int wdt, int K, void* momentum,
+                      int has_momentum, uint64_t n, double lr, double momentum_coef, int nesterov, void* workspace,
+                      void* stream) {
+    if (K <= EDT_MAX_WORKERS)
+        return edt_outer_step(theta_g, gdt, theta_k, wdt, K, momentum, has_momentum, n, lr, momentum_coef, nesterov,
+                              stream);
+    g_err[0] = 0;
+    if (!valid_pair(gdt, wdt)) return fail(EDT_ERR_ARG, "unsupported dtype pair (gdt/wdt)");
+    if (!workspace && n) return fail(EDT_ERR_ARG, "K = %d > %d needs a workspace of n elements of theta's dtype",
+                                     K, EDT_MAX_WORKERS);
+    if (!theta_k) return fail(EDT_ERR_ARG, "theta_k is null");
+    const SgdScalars sg = make_sgd(gdt, lr, momentum_coef, has_momentum, nesterov);
+    if (sg.use_momentum && !momentum && n) return fail(EDT_ERR_ARG, "momentum buffer is null");
+    if (n == 0) return EDT_OK;
+    bool vec = aligned16(theta_g) && aligned16(workspace) && (!sg.use_momentum || aligned16(momentum));
+    for (int k = 0; k < K; ++k) vec = vec && theta_k[k] && aligned16(theta_k[k]);
+    for (int k0 = 0; k0 < K; k0 += EDT_MAX_WORKERS) {       // worker order preserved across launches
+        const int kc = K - k0 < EDT_MAX_WORKERS ? K - k0 : EDT_MAX_WORKERS;
+        OuterArgs a;
+        int rc = fill_outer(a, theta_g, theta_k + k0, kc, K, n);
+        if (rc) return rc;
+        a.sgd = sg;
+        a.mom = momentum;
+        a.acc_ws = workspace;
+        a.acc_in = k0 > 0;
+        a.acc_store = k0 + kc < K;
+        rc = launch_outer<MODE_CHAIN>(gdt, wdt, a, vec, (hipStream_t)stream);
+        if (rc) return rc;
+    }
+    return EDT_OK;
 }
 
 int edt_delta_partial(const void* theta_g, int gdt, const void* const* theta_k, int wdt, int K_local,

@@ -19,7 +19,7 @@ import os
 import torch
 
 from . import ops
-from ._lib import EDT_MAX_WORKERS, EdtError
+from ._lib import EdtError
 from .params import ParamArena, ParamLayout, flat_view, pack, unpack_
 
 DILOCO_DEFAULTS = dict(lr=0.7, momentum=0.9, nesterov=True)        # EDT_LM/diloco.py:253-255
@@ -113,8 +113,6 @@ def outer_step(base_params, worker_params, state: OuterState | None = None, lr: 
     worker_params = [list(w) for w in worker_params]
     if not worker_params:
         raise EdtError("no trained models")
-    if len(worker_params) > EDT_MAX_WORKERS:
-        raise EdtError(f"{len(worker_params)} workers; one fused launch takes at most {EDT_MAX_WORKERS}")
     for w in worker_params:
         if len(w) != len(base_params) or any(a.shape != b.shape for a, b in zip(w, base_params)):
             raise EdtError("trained model parameters do not match the base model")

@@ -19,11 +19,11 @@ def outer_step(theta: torch.Tensor, workers: list[torch.Tensor], momentum: torch
                has_momentum: bool, lr: float, momentum_coef: float, nesterov: bool) -> None:
     """Fused DiLoCo outer step (EDT_LM/diloco.py:238-289): theta and momentum updated in place.
 
-    theta: flat float32/bfloat16; workers: K (<= 32) flat tensors of one dtype; momentum: flat,
-    theta's dtype (required when momentum_coef != 0)."""
+    theta: flat float32/bfloat16; workers: K flat tensors of one dtype (K > 32: chained launches
+    through a scratch running sum); momentum: flat, theta's dtype (required when momentum_coef != 0)."""
     lib = L.lib()
-    if not 1 <= len(workers) <= L.EDT_MAX_WORKERS:
-        raise L.EdtError(f"{len(workers)} workers: one launch takes 1..{L.EDT_MAX_WORKERS}")
+    if not workers:
+        raise L.EdtError("no workers")
     L.require_device(theta, momentum, *workers)
     n = theta.numel()
     for w in workers:
@@ -31,10 +31,17 @@ def outer_step(theta: torch.Tensor, workers: list[torch.Tensor], momentum: torch
             raise L.EdtError("every worker buffer must match theta's size and share one dtype")
     if momentum is not None and (momentum.numel() != n or momentum.dtype != theta.dtype):
         raise L.EdtError("momentum must have theta's size and dtype")
-    L.check(lib.edt_outer_step(L.ptr(theta), L.dtype_code(theta), L.ptr_array(workers),
-                               L.dtype_code(workers[0]), len(workers), L.ptr(momentum),
-                               int(has_momentum), n, float(lr), float(momentum_coef),
-                               int(nesterov), L.stream_ptr(theta.device)), "edt_outer_step")
+    if len(workers) <= L.EDT_MAX_WORKERS:
+        L.check(lib.edt_outer_step(L.ptr(theta), L.dtype_code(theta), L.ptr_array(workers),
+                                   L.dtype_code(workers[0]), len(workers), L.ptr(momentum),
+                                   int(has_momentum), n, float(lr), float(momentum_coef),
+                                   int(nesterov), L.stream_ptr(theta.device)), "edt_outer_step")
+        return
+    ws = torch.empty_like(theta)
+    L.check(lib.edt_outer_step_ws(L.ptr(theta), L.dtype_code(theta), L.ptr_array(workers),
+                                  L.dtype_code(workers[0]), len(workers), L.ptr(momentum),
+                                  int(has_momentum), n, float(lr), float(momentum_coef), int(nesterov),
+                                  L.ptr(ws), L.stream_ptr(theta.device)), "edt_outer_step_ws")
 
 
 def delta_partial(theta: torch.Tensor, workers: list[torch.Tensor], k_total: int,

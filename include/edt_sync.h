@@ -52,6 +52,14 @@ int edt_outer_step(void* theta_g, int gdt, const void* const* theta_k, int wdt, 
                    void* momentum, int has_momentum, uint64_t n,
                    double lr, double momentum_coef, int nesterov, void* stream);
 
+/* The same step for any population size: K > EDT_MAX_WORKERS runs as consecutive launches of
+ * <= 32 workers (the reference's worker order), the running sum carried in `workspace` (n
+ * elements of theta's dtype: lossless, the sum is rounded to that dtype after every add).
+ * K <= 32: identical to edt_outer_step (workspace unused, may be NULL). */
+int edt_outer_step_ws(void* theta_g, int gdt, const void* const* theta_k, int wdt, int K,
+                      void* momentum, int has_momentum, uint64_t n, double lr, double momentum_coef,
+                      int nesterov, void* workspace, void* stream);
+
 /* Partial delta sum for the sharded multi-GPU step (EDT_LM/diloco.py:243-246 restricted to the
  * workers resident on this rank): acc_f32[i] (+)= sum_{k<K_local} round_g((theta_k - theta_g)/K_total).
  * accumulate = 0 starts from zero, 1 continues the running fp32 sum already in acc_f32 (so two

@@ -109,10 +109,11 @@ REGIMES = [(torch.float32, torch.float32), (torch.float32, torch.bfloat16), (tor
 
 
 @pytest.mark.parametrize("gdt,wdt", REGIMES)
-@pytest.mark.parametrize("K", [1, 2, 3, 4, 5, 8, 16, 32])
+@pytest.mark.parametrize("K", [1, 2, 3, 4, 5, 8, 16, 32, 33, 48, 64])
 @pytest.mark.parametrize("n", [1, 7, 8, 9, 4097, 1_000_003])
 def test_outer_step_vs_oracle(oracle, dev, ops, gdt, wdt, K, n):
-    if n == 1_000_003 and K not in (3, 8, 32):
+    """K > 32 runs as chained launches carrying the running sum (edt_outer_step_ws)."""
+    if n == 1_000_003 and K not in (3, 8, 32, 48):
         pytest.skip("large size: representative K only")
     theta, workers, mom = _rand_case(n, K, gdt, wdt, seed=K * 1000 + n)
     for has, (lr, mu, nest) in [(False, (0.7, 0.9, True)), (True, (0.7, 0.9, True)),
@@ -295,8 +296,9 @@ def test_errors_are_raised(dev, ops):
         ops.outer_step(th, [], None, False, 0.7, 0.0, False)
     with pytest.raises(EdtError):
         ops.outer_step(th, [torch.zeros(15, device=dev)], None, False, 0.7, 0.0, False)
-    with pytest.raises(EdtError):
-        ops.outer_step(th, [torch.zeros(16, device=dev)] * 33, None, False, 0.7, 0.0, False)
+    with pytest.raises(EdtError):   # a worker of the wrong size anywhere in a chained population
+        ops.outer_step(th, [torch.zeros(16, device=dev)] * 40 + [torch.zeros(15, device=dev)], None, False,
+                       0.7, 0.0, False)
     with pytest.raises(EdtError):   # bf16 master with fp32 workers is not a torch-promotable pair
         ops.outer_step(th.bfloat16(), [torch.zeros(16, device=dev)], None, False, 0.7, 0.0, False)
     with pytest.raises(EdtError):   # host tensors are refused: no CPU path
