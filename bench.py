@@ -29,6 +29,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0        # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+XGMI_LINK_GBPS = 153.0        # per xGMI link; 7 links per GPU, one to each peer
 DT = {"f32": torch.float32, "bf16": torch.bfloat16}
 
 
@@ -44,7 +45,7 @@ def parse():
     p.add_argument("--lr", type=float, default=0.7)
     p.add_argument("--momentum", type=float, default=0.9)
     p.add_argument("--nesterov", type=int, default=1)
-    p.add_argument("--mode", default="reduce", choices=["reduce", "exact"])
+    p.add_argument("--mode", default="auto", choices=["reduce", "exact", "auto"])
     p.add_argument("--bucket-elems", type=int, default=1 << 26)
     p.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     p.add_argument("--cpu-sample-elems", type=int, default=1 << 24)
@@ -127,7 +128,7 @@ def main():
         # replicas of theta must agree: rank 0's values everywhere
         dist.broadcast(sync.theta_buf, 0)
         step = sync.step
-        kernel_name = "outer_kernel" if args.mode == "exact" else "outer_kernel(partial)"
+        kernel_name = "outer_kernel" if sync.mode == "exact" else "outer_kernel(partial)"
 
     for _ in range(args.warmup):
         step()
@@ -198,8 +199,17 @@ def main():
                        "params": P, "tensors": len(layout), "workers_per_gpu": k_local,
                        "population": k_total, "worker_dtype": args.worker_dtype,
                        "theta_dtype": args.theta_dtype,
-                       "parallelism": "single GPU" if world == 1 else f"dp{world} {args.mode} (RCCL)"},
+                       "parallelism": "single GPU" if world == 1 else f"dp{world} {sync.mode} (RCCL)"},
         }
+        if world > 1:
+            # the exchange dominates: bytes this rank puts on xGMI per step over the whole step time
+            # (the local HBM pass is inside that time), against the rank's links to its N-1 peers
+            wire = sync.wire_bytes()
+            achieved = wire / (ms_per_step / 1e3) / 1e9
+            peak = XGMI_LINK_GBPS * (world - 1)
+            roofline = {"bound": "xgmi", "achieved": round(achieved, 1), "peak": peak, "unit": "GB/s",
+                        "frac": round(achieved / peak, 4), "traffic": None, "wire_bytes_per_rank": wire,
+                        "schedule": sync.mode}
         if roofline:
             out["roofline"] = roofline
         if world == 1:   # what a plain device-to-device copy reaches on this device, same process

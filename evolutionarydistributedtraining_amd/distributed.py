@@ -14,7 +14,8 @@ overlaps the HBM-bound kernels on the compute stream:
   mode="exact"   all-to-all of the raw worker shards to their owners, then the single-GPU fused
                  kernel on each shard (the reference's worker order, bit-exact), all-gather of
                  theta. Wire bytes: (N-1)/N * P * (K_local * b_w + b_g) — the cheaper schedule
-                 when K_local * b_w <= 4 (one bf16 population member per GPU).
+                 when K_local * b_w <= 4 (one bf16 population member per GPU). mode="auto"
+                 (default) picks the schedule with fewer wire bytes.
 
 Every rank holds a full replica of theta (what the next inner loop starts from) and 1/N of the
 momentum. Ranks own contiguous shards of every bucket.
@@ -34,12 +35,15 @@ from .params import ParamArena, ParamLayout
 class ShardedOuterSync:
     def __init__(self, layout: ParamLayout, theta_dtype: torch.dtype, worker_dtype: torch.dtype,
                  k_local: int, device, lr: float = 0.7, momentum: float = 0.9, nesterov: bool = True,
-                 mode: str = "reduce", bucket_elems: int = 1 << 26, group=None, kernels=None):
-        if mode not in ("reduce", "exact"):
+                 mode: str = "auto", bucket_elems: int = 1 << 26, group=None, kernels=None):
+        if mode not in ("reduce", "exact", "auto"):
             raise ValueError(mode)
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
+        if mode == "auto":   # fewer bytes on the wire: fp32 partial sums vs the raw worker shards
+            wb = torch.empty(0, dtype=worker_dtype).element_size()
+            mode = "exact" if k_local * wb <= 4 else "reduce"
         self.kernels = kernels or _ops
         self.mode = mode
         self.layout = layout
