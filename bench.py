@@ -124,7 +124,7 @@ def main():
         from evolutionarydistributedtraining_amd.distributed import ShardedOuterSync
         sync = ShardedOuterSync(layout, tdt, wdt, k_local, dev, args.lr, args.momentum, bool(args.nesterov),
                                 mode=args.mode, bucket_elems=args.bucket_elems)
-        synth_population(sync.theta.flat, [w.flat for w in sync.workers], seed=1234 + 0)
+        synth_population(sync.theta.flat, [w.flat for w in sync.workers], seed=1234 + 7919 * rank)
         # replicas of theta must agree: rank 0's values everywhere
         dist.broadcast(sync.theta_buf, 0)
         step = sync.step
