@@ -307,3 +307,34 @@ def test_dir_outer_sync_two_generations(oracle, dev, tmp_path):
             assert torch.equal(bits(pack(list(got.parameters()))), bits(theta)), (gen, d)
         prev = dirs[0]
     assert torch.equal(bits(sync.state.momentum.cpu()), bits(mom))
+
+
+@pytest.mark.parametrize("mode", ["reduce", "exact"])
+def test_sharded_outer_step_rccl_world1(oracle, dev, tmp_path, mode):
+    """The multi-GPU schedule on the real RCCL backend (one rank: the collectives degenerate, but
+    the in-place reduce-scatter / all-gather, async waits and stream ordering are RCCL's)."""
+    import torch.distributed as dist
+    from evolutionarydistributedtraining_amd.distributed import ShardedOuterSync
+    from evolutionarydistributedtraining_amd.params import ParamLayout
+    store = dist.FileStore(str(tmp_path / "store"), 1)
+    dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=dev)
+    try:
+        layout = ParamLayout([(1000, 37), (4097,), (3,)])
+        sync = ShardedOuterSync(layout, torch.float32, torch.bfloat16, 3, dev, 0.7, 0.9, True, mode=mode,
+                                bucket_elems=8192)
+        assert sync.mode == mode and len(sync.buckets) > 3
+        g = torch.Generator().manual_seed(8)
+        theta = torch.randn(layout.total, generator=g) * 0.02
+        mom = torch.zeros(layout.total)
+        sync.theta.flat.copy_(theta)
+        for step in range(2):
+            ws = [(theta + torch.randn(layout.total, generator=g) * 1e-3).bfloat16() for _ in range(3)]
+            for a, w in zip(sync.workers, ws):
+                a.flat.copy_(w)
+            sync.step()
+            oracle.outer_step(theta, ws, mom, step > 0, 0.7, 0.9, True)
+        torch.cuda.synchronize()
+        assert torch.equal(bits(sync.theta.flat.cpu()), bits(theta))      # fp32: same order, bit-exact
+        assert torch.equal(bits(sync.mom_shard[:layout.total].cpu()), bits(mom))
+    finally:
+        dist.destroy_process_group()
