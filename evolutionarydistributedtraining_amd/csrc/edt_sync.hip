@@ -19,6 +19,7 @@
 #include <string.h>
 
 #include <type_traits>
+#include <vector>
 
 #include "edt_sync.h"
 
@@ -263,6 +264,27 @@ struct OuterArgs {
     int acc_store;       // chain mode: store the running sum to acc_ws (no SGD)
     SgdScalars sgd;
     Workers w;
+    __device__ __forceinline__ const void* wp(int k) const { return w.p[k]; }
+};
+
+// One tensor of a tensor-list launch (outer_list_kernel), seen through outer_elems: the same
+// fields, worker pointers read from the device-resident table (theta_k[k * T + t]).
+struct TensorArgs {
+    void* theta;
+    void* mom;
+    float* acc_out;
+    int K;
+    float kdiv;
+    float kinv;
+    int accumulate;
+    void* acc_ws;
+    int acc_in;
+    int acc_store;
+    SgdScalars sgd;
+    const void* const* w;
+    uint64_t T;
+    uint64_t t;
+    __device__ __forceinline__ const void* wp(int k) const { return w[(uint64_t)k * T + t]; }
 };
 
 // MODE_CHAIN = MODE_FUSED for populations above EDT_MAX_WORKERS: launches of <= 32 workers
@@ -272,8 +294,8 @@ enum { MODE_FUSED = 0, MODE_PARTIAL = 1, MODE_CHAIN = 2 };
 // Per-element accumulation acc = sum_k round(round(w_k - g) / K) in the precision of GDT
 // (worker-major order, EDT_LM/diloco.py:243-246). MODE_PARTIAL sums the rounded quotients
 // in fp32 instead (the cross-rank sum is then an fp32 RCCL reduction).
-template <int GDT, int WDT, int KC, int DIV, int MODE, int N>
-__device__ __forceinline__ void outer_elems(const OuterArgs& a, uint64_t i) {
+template <int GDT, int WDT, int KC, int DIV, int MODE, int N, class A>
+__device__ __forceinline__ void outer_elems(const A& a, uint64_t i) {
     float g[N], acc[N], b_in[N];
     ld<GDT, N>(a.theta, i, g);
     if constexpr (MODE != MODE_PARTIAL) ld_momentum<GDT, N>(a.mom, i, a.sgd, b_in);
@@ -288,7 +310,7 @@ __device__ __forceinline__ void outer_elems(const OuterArgs& a, uint64_t i) {
     const int K = KC > 0 ? KC : a.K;
     auto body = [&](int k) {
         float w[N];
-        ld<WDT, N, EDT_NT_LOADS != 0 && WDT == EDT_BF16>(a.w.p[k], i, w);
+        ld<WDT, N, EDT_NT_LOADS != 0 && WDT == EDT_BF16>(a.wp(k), i, w);
 #pragma unroll
         for (int j = 0; j < N; ++j) w[j] = w[j] - g[j];              // trained - base
         rnd<GDT>(w);
@@ -337,6 +359,68 @@ __global__ __launch_bounds__(kBlock, EDT_MIN_WAVES) void outer_kernel(OuterArgs 
         if (t < a.n) outer_elems<GDT, WDT, KC, DIV, MODE, 1>(a, t);
     } else {
         for (uint64_t e = tid; e < a.n; e += stride) outer_elems<GDT, WDT, KC, DIV, MODE, 1>(a, e);
+    }
+}
+
+// Tensor-list form: the parameters are T separate allocations (HF models loaded straight to
+// the GPU), described by a table in device memory. Workgroup b handles chunk b - prefix[t] of
+// tensor t (binary search over the chunk prefix sums; uniform, so scalar loads), kListChunk
+// elements with the same per-thread 8-element body as outer_kernel. Tensors whose operands are
+// not all 16-byte aligned take the scalar body.
+constexpr uint64_t kListChunk = (uint64_t)kBlock * kVec * 16;      // 32768 elements per workgroup
+constexpr uint64_t kVecFlag = 1ull << 63;                          // numel[t] bit: vector body ok
+
+struct ListArgs {
+    const uint64_t* prefix;     // T + 1 chunk prefix sums
+    const uint64_t* numel;      // T, kVecFlag | numel
+    void* const* theta;         // T
+    void* const* mom;           // T (unused without momentum)
+    const void* const* w;       // K * T, worker-major
+    uint64_t T;
+    int K;
+    float kdiv;
+    float kinv;
+    SgdScalars sgd;
+};
+
+template <int GDT, int WDT, int KC, int DIV>
+__global__ __launch_bounds__(kBlock, EDT_MIN_WAVES) void outer_list_kernel(ListArgs L) {
+    const uint64_t b = blockIdx.x;
+    uint64_t lo = 0, hi = L.T;                       // last t with prefix[t] <= b
+    while (hi - lo > 1) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (L.prefix[mid] <= b) lo = mid;
+        else hi = mid;
+    }
+    const uint64_t t = lo;
+    const uint64_t nf = L.numel[t];
+    const uint64_t n = nf & ~kVecFlag;
+    const uint64_t c0 = (b - L.prefix[t]) * kListChunk;
+    const uint64_t c1 = c0 + kListChunk < n ? c0 + kListChunk : n;
+    TensorArgs a;
+    a.theta = L.theta[t];
+    a.mom = L.sgd.use_momentum ? L.mom[t] : nullptr;
+    a.acc_out = nullptr;
+    a.K = L.K;
+    a.kdiv = L.kdiv;
+    a.kinv = L.kinv;
+    a.accumulate = 0;
+    a.acc_ws = nullptr;
+    a.acc_in = 0;
+    a.acc_store = 0;
+    a.sgd = L.sgd;
+    a.w = L.w;
+    a.T = L.T;
+    a.t = t;
+    if (nf & kVecFlag) {
+        const uint64_t vend = c0 + (c1 - c0) / kVec * kVec;
+        for (uint64_t i = c0 + (uint64_t)threadIdx.x * kVec; i < vend; i += (uint64_t)kBlock * kVec)
+            outer_elems<GDT, WDT, KC, DIV, MODE_FUSED, kVec>(a, i);
+        const uint64_t i = vend + threadIdx.x;
+        if (i < c1) outer_elems<GDT, WDT, KC, DIV, MODE_FUSED, 1>(a, i);
+    } else {
+        for (uint64_t i = c0 + threadIdx.x; i < c1; i += kBlock)
+            outer_elems<GDT, WDT, KC, DIV, MODE_FUSED, 1>(a, i);
     }
 }
 
@@ -670,6 +754,20 @@ int launch_outer(int gdt, int wdt, const OuterArgs& a, bool vec, hipStream_t s) 
     return launch_outer_k<EDT_BF16, EDT_BF16, MODE>(a, vec, s);
 }
 
+template <int GDT, int WDT>
+int launch_list_k(const ListArgs& L, int div_exact, unsigned grid, hipStream_t s) {
+#define EDT_LAUNCH_L(KC, DIV) outer_list_kernel<GDT, WDT, KC, DIV><<<grid, kBlock, 0, s>>>(L)
+    if (L.K == 1 && !div_exact) EDT_LAUNCH_L(1, 0);
+    else if (L.K == 2 && !div_exact) EDT_LAUNCH_L(2, 0);
+    else if (L.K == 3 && div_exact) EDT_LAUNCH_L(3, 1);
+    else if (L.K == 4 && !div_exact) EDT_LAUNCH_L(4, 0);
+    else if (L.K == 8 && !div_exact) EDT_LAUNCH_L(8, 0);
+    else if (div_exact) EDT_LAUNCH_L(0, 1);
+    else EDT_LAUNCH_L(0, 0);
+#undef EDT_LAUNCH_L
+    return check_launch("outer_list_kernel");
+}
+
 bool is_pow2(int k) { return k > 0 && (k & (k - 1)) == 0; }
 
 int fill_outer(OuterArgs& a, const void* theta, const void* const* theta_k, int K, int K_total, uint64_t n) {
@@ -754,6 +852,85 @@ int edt_outer_step_ws(void* theta_g, int gdt, const void* const* theta_k, int wd
         if (rc) return rc;
     }
     return EDT_OK;
+}
+
+uint64_t edt_outer_list_workspace_bytes(int T, int K) {
+    if (T < 0 || K < 1) return 0;
+    return (uint64_t)(4 * (uint64_t)T + 1 + (uint64_t)K * T) * sizeof(uint64_t);
+}
+
+int edt_outer_step_list(void* const* theta_t, int gdt, const void* const* theta_k, int wdt, int K,
+                        void* const* momentum_t, int has_momentum, const uint64_t* numel, int T,
+                        double lr, double momentum_coef, int nesterov, void* workspace,
+                        uint64_t workspace_bytes, void* stream) {
+    g_err[0] = 0;
+    if (!valid_pair(gdt, wdt)) return fail(EDT_ERR_ARG, "unsupported dtype pair (gdt/wdt)");
+    if (K < 1 || K > EDT_MAX_WORKERS)
+        return fail(EDT_ERR_ARG, "worker count %d out of range [1, %d]", K, EDT_MAX_WORKERS);
+    if (T < 0) return fail(EDT_ERR_ARG, "tensor count %d < 0", T);
+    if (T == 0) return EDT_OK;
+    if (!theta_t || !theta_k || !numel) return fail(EDT_ERR_ARG, "null tensor table");
+    const SgdScalars sg = make_sgd(gdt, lr, momentum_coef, has_momentum, nesterov);
+    if (sg.use_momentum && !momentum_t) return fail(EDT_ERR_ARG, "momentum table is null");
+    const uint64_t need = edt_outer_list_workspace_bytes(T, K);
+    if (!workspace || workspace_bytes < need)
+        return fail(EDT_ERR_ARG, "workspace of %llu bytes needed", (unsigned long long)need);
+    if (reinterpret_cast<uintptr_t>(workspace) & 7u) return fail(EDT_ERR_ARG, "workspace must be 8-byte aligned");
+    // table: prefix[T+1] | numel[T] | theta[T] | mom[T] | w[K*T]   (all 8-byte words)
+    thread_local std::vector<uint64_t> h;
+    h.assign(need / sizeof(uint64_t), 0);
+    uint64_t* prefix = h.data();
+    uint64_t* nflag = prefix + T + 1;
+    uint64_t* pth = nflag + T;
+    uint64_t* pmo = pth + T;
+    uint64_t* pw = pmo + T;
+    for (int t = 0; t < T; ++t) {
+        const uint64_t n = numel[t];
+        if (n >= kVecFlag) return fail(EDT_ERR_ARG, "tensor %d too large", t);
+        bool vec = true;
+        if (n) {
+            if (!theta_t[t]) return fail(EDT_ERR_ARG, "theta_t[%d] is null", t);
+            vec = aligned16(theta_t[t]);
+            if (sg.use_momentum) {
+                if (!momentum_t[t]) return fail(EDT_ERR_ARG, "momentum_t[%d] is null", t);
+                vec = vec && aligned16(momentum_t[t]);
+            }
+            for (int k = 0; k < K; ++k) {
+                const void* p = theta_k[(uint64_t)k * T + t];
+                if (!p) return fail(EDT_ERR_ARG, "theta_k[%d][%d] is null", k, t);
+                vec = vec && aligned16(p);
+            }
+        }
+        prefix[t + 1] = prefix[t] + (n + kListChunk - 1) / kListChunk;
+        nflag[t] = n | (vec ? kVecFlag : 0);
+        pth[t] = reinterpret_cast<uintptr_t>(theta_t[t]);
+        pmo[t] = sg.use_momentum ? reinterpret_cast<uintptr_t>(momentum_t[t]) : 0;
+        for (int k = 0; k < K; ++k) pw[(uint64_t)k * T + t] = reinterpret_cast<uintptr_t>(theta_k[(uint64_t)k * T + t]);
+    }
+    const uint64_t chunks = prefix[T];
+    if (chunks == 0) return EDT_OK;
+    if (chunks > 0x7fffffffull) return fail(EDT_ERR_ARG, "too many elements for one launch");
+    hipStream_t st = (hipStream_t)stream;
+    // pageable source: the copy is staged before hipMemcpyAsync returns, stream-ordered on the device
+    hipError_t e = hipMemcpyAsync(workspace, h.data(), need, hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return fail(EDT_ERR_LAUNCH, "tensor table upload failed: %s", hipGetErrorString(e));
+    const uint64_t* d = static_cast<const uint64_t*>(workspace);
+    ListArgs L;
+    L.prefix = d;
+    L.numel = d + T + 1;
+    L.theta = reinterpret_cast<void* const*>(d + 2 * (uint64_t)T + 1);
+    L.mom = reinterpret_cast<void* const*>(d + 3 * (uint64_t)T + 1);
+    L.w = reinterpret_cast<const void* const*>(d + 4 * (uint64_t)T + 1);
+    L.T = (uint64_t)T;
+    L.K = K;
+    L.kdiv = (float)K;
+    L.kinv = 1.0f / (float)K;
+    L.sgd = sg;
+    const int div_exact = is_pow2(K) ? 0 : 1;
+    const unsigned grid = (unsigned)chunks;
+    if (gdt == EDT_F32 && wdt == EDT_F32) return launch_list_k<EDT_F32, EDT_F32>(L, div_exact, grid, st);
+    if (gdt == EDT_F32) return launch_list_k<EDT_F32, EDT_BF16>(L, div_exact, grid, st);
+    return launch_list_k<EDT_BF16, EDT_BF16>(L, div_exact, grid, st);
 }
 
 int edt_delta_partial(const void* theta_g, int gdt, const void* const* theta_k, int wdt, int K_local,

@@ -38,13 +38,16 @@ class OuterState:
         self.hparams = dict(DILOCO_DEFAULTS)
         self.steps = 0
 
-    def buffer_for(self, theta: torch.Tensor) -> torch.Tensor:
+    def buffer_for(self, theta: torch.Tensor, numel: int | None = None) -> torch.Tensor:
+        """The flat momentum for parameters like `theta` (numel: total count when theta is
+        only the first of a tensor list)."""
+        numel = theta.numel() if numel is None else numel
         if self.momentum is None:
-            self.momentum = torch.zeros_like(theta)
+            self.momentum = torch.zeros(numel, dtype=theta.dtype, device=theta.device)
             self.has_momentum = False
-        elif self.momentum.numel() != theta.numel():
+        elif self.momentum.numel() != numel:
             raise EdtError("outer-optimizer state does not match the parameter count "
-                           f"({self.momentum.numel()} vs {theta.numel()})")
+                           f"({self.momentum.numel()} vs {numel})")
         elif self.momentum.dtype != theta.dtype or self.momentum.device != theta.device:
             # torch's load_state_dict casts state to the param's dtype/device
             self.momentum = self.momentum.to(dtype=theta.dtype, device=theta.device)
@@ -97,6 +100,20 @@ def _step_flat(theta: torch.Tensor, workers: list[torch.Tensor], state: OuterSta
     state.steps += 1
 
 
+def _step_list(thetas: list[torch.Tensor], workers: list[list[torch.Tensor]], state: OuterState,
+               lr: float, momentum: float, nesterov: bool) -> None:
+    state.hparams = dict(lr=lr, momentum=momentum, nesterov=nesterov)
+    moms = None
+    if momentum != 0:
+        flat = state.buffer_for(thetas[0], sum(t.numel() for t in thetas))
+        moms = ParamLayout.of(thetas).views(flat)
+    ops.outer_step_list(thetas, workers, moms, state.has_momentum if momentum != 0 else False,
+                        lr, momentum, nesterov)
+    if momentum != 0:
+        state.has_momentum = True
+    state.steps += 1
+
+
 def outer_step(base_params, worker_params, state: OuterState | None = None, lr: float = 0.7,
                momentum: float = 0.9, nesterov: bool = True) -> OuterState:
     """Drop-in for EDT_LM/diloco.py:238-289 on device-resident parameters.
@@ -105,8 +122,9 @@ def outer_step(base_params, worker_params, state: OuterState | None = None, lr: 
                    updated in place.
     worker_params: K lists of the trained replicas' parameters, same order.
     state:         the carried outer-optimiser state (None on the first generation).
-    Zero-copy when each list is a run of views of one arena (`params.arena_of_module`);
-    otherwise the tensors are packed into flat scratch buffers on the device first.
+    One launch either way: over the flat arenas when each list is a run of views of one arena
+    (`params.arena_of_module`), else over the tensor lists themselves (`ops.outer_step_list`,
+    no packing). Only populations above 32 workers with separate tensors are packed first.
     """
     state = state or OuterState()
     base_params = list(base_params)
@@ -118,13 +136,17 @@ def outer_step(base_params, worker_params, state: OuterState | None = None, lr: 
             raise EdtError("trained model parameters do not match the base model")
     with torch.no_grad():
         theta = flat_view(base_params)
+        flats = [flat_view(w) for w in worker_params]
+        if theta is None or any(f is None for f in flats):
+            if len(worker_params) <= 32 and base_params and all(p.is_cuda for p in base_params):
+                if len({w[0].dtype for w in worker_params}) != 1:
+                    raise EdtError("all trained models must share one dtype")
+                _step_list(base_params, worker_params, state, lr, momentum, nesterov)
+                return state
         copied = theta is None
         if copied:
             theta = pack(base_params)
-        flats = []
-        for w in worker_params:
-            f = flat_view(w)
-            flats.append(f if f is not None else pack(w))
+        flats = [f if f is not None else pack(w) for f, w in zip(flats, worker_params)]
         wdt = {f.dtype for f in flats}
         if len(wdt) != 1:
             raise EdtError("all trained models must share one dtype")

@@ -44,6 +44,45 @@ def outer_step(theta: torch.Tensor, workers: list[torch.Tensor], momentum: torch
                                   L.ptr(ws), L.stream_ptr(theta.device)), "edt_outer_step_ws")
 
 
+def outer_step_list(thetas: list[torch.Tensor], workers: list[list[torch.Tensor]],
+                    momenta: list[torch.Tensor] | None, has_momentum: bool, lr: float,
+                    momentum_coef: float, nesterov: bool) -> None:
+    """`outer_step` over T separate tensors per model (e.g. `list(model.parameters())` of
+    models loaded on the GPU) in ONE launch, without packing: thetas[t], workers[k][t],
+    momenta[t] (theta's dtype, required when momentum_coef != 0), all updated in place."""
+    lib = L.lib()
+    T, K = len(thetas), len(workers)
+    if K == 0:
+        raise L.EdtError("no workers")
+    if K > L.EDT_MAX_WORKERS:
+        raise L.EdtError(f"tensor-list step takes at most {L.EDT_MAX_WORKERS} workers")
+    flat_w = [t for w in workers for t in w]
+    L.require_device(*thetas, *flat_w, *(momenta or []))
+    if any(len(w) != T for w in workers):
+        raise L.EdtError("every worker needs one tensor per parameter")
+    gdt, wdt = thetas[0].dtype, workers[0][0].dtype if T else thetas[0].dtype
+    for t in range(T):
+        n = thetas[t].numel()
+        if thetas[t].dtype != gdt:
+            raise L.EdtError("all parameters of the base model must share one dtype")
+        for w in workers:
+            if w[t].numel() != n or w[t].dtype != wdt:
+                raise L.EdtError(f"worker tensor {t} does not match the base parameter")
+        if momenta is not None and (momenta[t].numel() != n or momenta[t].dtype != gdt):
+            raise L.EdtError(f"momentum tensor {t} must match the parameter's size and dtype")
+    if momentum_coef != 0 and momenta is None:
+        raise L.EdtError("momentum tensors are required when momentum != 0")
+    if T == 0:
+        return
+    numel = (ctypes.c_uint64 * T)(*[t.numel() for t in thetas])
+    nbytes = lib.edt_outer_list_workspace_bytes(T, K)
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=thetas[0].device)
+    L.check(lib.edt_outer_step_list(L.ptr_array(thetas), L.dtype_code(gdt), L.ptr_array(flat_w),
+                                    L.dtype_code(wdt), K, L.ptr_array(momenta) if momenta is not None else None,
+                                    int(has_momentum), numel, T, float(lr), float(momentum_coef), int(nesterov),
+                                    L.ptr(ws), nbytes, L.stream_ptr(thetas[0].device)), "edt_outer_step_list")
+
+
 def delta_partial(theta: torch.Tensor, workers: list[torch.Tensor], k_total: int,
                   acc: torch.Tensor, accumulate: bool = False) -> None:
     """acc (fp32) (+)= sum over the local workers of round((theta_k - theta) / k_total)."""

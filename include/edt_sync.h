@@ -60,6 +60,23 @@ int edt_outer_step_ws(void* theta_g, int gdt, const void* const* theta_k, int wd
                       void* momentum, int has_momentum, uint64_t n, double lr, double momentum_coef,
                       int nesterov, void* workspace, void* stream);
 
+/* Tensor-list form of edt_outer_step, for parameters that are T separate device allocations
+ * (`list(model.parameters())` of models loaded straight to the GPU, the reference's own objects at
+ * EDT_LM/diloco.py:231-246): one launch over all tensors, no packing into a flat buffer.
+ *   theta_t[T], momentum_t[T]   host arrays of device pointers (momentum_t unused, may be NULL,
+ *                               when momentum == 0)
+ *   theta_k[K * T]              worker-major: theta_k[k * T + t] is tensor t of worker k
+ *   numel[T]                    element count of each tensor (0 allowed)
+ * The per-tensor math is exactly edt_outer_step's. The tensor table (pointers, sizes, chunk
+ * offsets) is copied into `workspace` (device memory, 8-byte aligned, at least
+ * edt_outer_list_workspace_bytes(T, K)) by a stream-ordered copy, so the workspace must not be
+ * reused before the launch has run. 1 <= K <= EDT_MAX_WORKERS. */
+uint64_t edt_outer_list_workspace_bytes(int T, int K);
+int edt_outer_step_list(void* const* theta_t, int gdt, const void* const* theta_k, int wdt, int K,
+                        void* const* momentum_t, int has_momentum, const uint64_t* numel, int T,
+                        double lr, double momentum, int nesterov, void* workspace,
+                        uint64_t workspace_bytes, void* stream);
+
 /* Partial delta sum for the sharded multi-GPU step (EDT_LM/diloco.py:243-246 restricted to the
  * workers resident on this rank): acc_f32[i] (+)= sum_{k<K_local} round_g((theta_k - theta_g)/K_total).
  * accumulate = 0 starts from zero, 1 continues the running fp32 sum already in acc_f32 (so two

@@ -5,6 +5,9 @@
   slerp       SLERP crossover of two qwen2p5_7b_body parents (bf16 in, bf16 out), 338 segments
               algorithmic bytes/elem: 2 x 2 in + 2 out = 6 (the 2-pass form reads the parents twice: 10)
   lerp        run_linear_merge_5050 on gpt_1p3b bf16: 2 x 2 in + 2 out = 6
+  outer_list  DiLoCo step over SEPARATE tensors (gpt_1p3b: 292 per model, K = 8 bf16 workers, fp32
+              theta + momentum; edt_outer_step_list) beside the flat-arena launch on the same data:
+              8 x 2 + 4 x 4 = 32 bytes/elem
 
     python scripts/bench_ops.py [--ops pair,slerp,lerp] [--iters 5]
 """
@@ -38,7 +41,7 @@ def timed(fn, iters):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--ops", default="pair,slerp,lerp")
+    ap.add_argument("--ops", default="pair,slerp,lerp,outer_list")
     ap.add_argument("--iters", type=int, default=5)
     a = ap.parse_args()
     from evolutionarydistributedtraining_amd import ops
@@ -67,6 +70,27 @@ def main():
             res["lerp"] = {"P": P, "ms": round(ms, 3), "GBps": round(gbs, 1), "frac": round(gbs / PEAK, 4),
                            "bytes_per_elem": 6}
         del b1, b2
+        torch.cuda.empty_cache()
+    if "outer_list" in a.ops:
+        lay = gpt_1p3b()
+        P, K = lay.total, 8
+        theta = torch.randn(P, device=dev) * 0.02
+        mom = torch.randn(P, device=dev) * 1e-3
+        workers = [(theta + torch.randn(P, device=dev) * 1e-3).to(bf) for _ in range(K)]
+        ms_flat = timed(lambda: ops.outer_step(theta, workers, mom, True, 0.7, 0.9, True), a.iters)
+        th_t = [v.clone() for v in lay.views(theta)]
+        mo_t = [v.clone() for v in lay.views(mom)]
+        del theta, mom
+        w_t = []
+        for w in workers:
+            w_t.append([v.clone() for v in lay.views(w)])
+        del workers, w
+        torch.cuda.empty_cache()
+        ms = timed(lambda: ops.outer_step_list(th_t, w_t, mo_t, True, 0.7, 0.9, True), a.iters)
+        res["outer_list"] = {"P": P, "tensors": len(lay), "K": K, "ms": round(ms, 3),
+                             "GBps": round(32 * P / ms / 1e6, 1), "frac": round(32 * P / ms / 1e6 / PEAK, 4),
+                             "flat_ms": round(ms_flat, 3), "bytes_per_elem": 32}
+        del th_t, mo_t, w_t
         torch.cuda.empty_cache()
     if "slerp" in a.ops:
         lay = qwen2p5_7b_body()

@@ -97,6 +97,78 @@ def test_diloco_golden(golden, oracle, dev, ops, idx):
             prev_buf = gb
 
 
+@pytest.mark.parametrize("idx", range(len(_M["diloco"])))
+def test_diloco_golden_tensor_list(golden, oracle, dev, ops, idx):
+    """The tensor-list launch (edt_outer_step_list) on the golden cases: one device tensor per
+    parameter, as `list(model.parameters())` hands them over; same bars as the flat launch."""
+    c = golden.diloco_cases()[idx]
+    T = len(c["shapes"])
+    numels = [int(torch.Size(s).numel()) for s in c["shapes"]]
+    tail = oracle.torch_cpu_tail_mask(numels)
+    prev_buf = None
+    for step in c["steps"]:
+        pre = step["prefix"]
+        base = golden.tlist("diloco", f"{pre}/base", T)
+        workers = [golden.tlist("diloco", f"{pre}/worker{k}", T) for k in range(c["K"])]
+        mu = c["momentum"]
+        theta = flat(base).contiguous()
+        theta_in = theta.clone()
+        if mu == 0:
+            mom, has = None, False
+        elif prev_buf is None:
+            mom, has = torch.zeros_like(theta), False
+        else:
+            mom, has = prev_buf.clone(), True
+        th_d = [t.contiguous().to(dev) for t in base]
+        ws_d = [[t.contiguous().to(dev) for t in w] for w in workers]
+        mom_d = None if mom is None else [m.contiguous().to(dev) for m in
+                                          torch.split(mom, numels)]
+        ops.outer_step_list(th_d, ws_d, mom_d, has, c["lr"], mu, c["nesterov"])
+        oracle.outer_step(theta, [flat(w).contiguous() for w in workers], mom, has, c["lr"], mu, c["nesterov"])
+        got = flat([t.cpu() for t in th_d])
+        assert torch.equal(bits(got), bits(theta)), f"{pre}: list kernel != oracle"
+        assert_matches_reference(got, flat(golden.tlist("diloco", f"{pre}/out_theta", T)), tail, pre, theta_in)
+        if step["has_out_buf"]:
+            gb = flat([m.cpu() for m in mom_d])
+            assert torch.equal(bits(gb), bits(mom))
+            prev_buf = gb
+
+
+@pytest.mark.parametrize("gdt,wdt", [(torch.float32, torch.float32), (torch.float32, torch.bfloat16),
+                                     (torch.bfloat16, torch.bfloat16)])
+@pytest.mark.parametrize("K", [1, 3, 5, 8, 32])
+def test_outer_step_list_vs_oracle(oracle, dev, ops, gdt, wdt, K):
+    """Ragged tensor lists: empty tensors, sizes around the 32768-element chunk and the 8-element
+    vector, a tensor off a 16-byte boundary (scalar body), separate allocations per worker."""
+    numels = [0, 1, 7, 8, 9, 32767, 32768, 32769, 100_003, 0, 65536 * 3 + 5, 13]
+    n = sum(numels)
+    theta, workers, mom = _rand_case(n, K, gdt, wdt, seed=K + 17)
+    offs = [0]
+    for x in numels:
+        offs.append(offs[-1] + x)
+
+    def split(v):   # separate allocations; tensor 4 starts 2 elements into its buffer
+        out = []
+        for t, (a, b) in enumerate(zip(offs, offs[1:])):
+            if t == 4:
+                buf = torch.empty(b - a + 2, dtype=v.dtype, device=dev)
+                buf[2:].copy_(v[a:b])
+                out.append(buf[2:])
+            else:
+                out.append(v[a:b].to(dev).clone())
+        return out
+
+    for has, (lr, mu, nest) in [(False, (0.7, 0.9, True)), (True, (0.7, 0.9, True)),
+                                (True, (0.5, 0.8, False)), (False, (1.0, 0.0, False))]:
+        th, m = theta.clone(), mom.clone()
+        th_d, m_d, ws_d = split(th), split(m), [split(w) for w in workers]
+        ops.outer_step_list(th_d, ws_d, m_d if mu else None, has, lr, mu, nest)
+        oracle.outer_step(th, workers, m if mu else None, has, lr, mu, nest)
+        assert torch.equal(bits(torch.cat([t.cpu() for t in th_d])), bits(th)), (has, lr, mu, nest)
+        if mu:
+            assert torch.equal(bits(torch.cat([t.cpu() for t in m_d])), bits(m))
+
+
 def _rand_case(n, K, gdt, wdt, seed):
     g = torch.Generator().manual_seed(seed)
     theta = (torch.randn(n, generator=g) * 0.02).to(gdt)

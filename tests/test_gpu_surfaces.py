@@ -55,7 +55,7 @@ def _save_tokenizer(path):
 # ------------------------------------------------------------------------------------------
 def test_diloco_outer_step_surface(golden, oracle, dev):
     """outer_step(list(base.parameters()), [list(m.parameters())...], state) over two generations,
-    arena (zero-copy) and packed paths, vs the oracle and the reference goldens."""
+    arena (flat launch) and separate-tensor (tensor-list launch) paths, vs the reference goldens."""
     from evolutionarydistributedtraining_amd import OuterState, arena_of_module, outer_step
     c = [c for c in golden.diloco_cases() if c["K"] == 3 and c["global_dtype"] == "f32"
          and c["worker_dtype"] == "f32" and c["nesterov"] and c["momentum"] == 0.9][0]

@@ -132,7 +132,7 @@ def test_library_exports_every_header_symbol():
     lib = _lib.load_library()
     with open(os.path.join(ROOT, "include", "edt_sync.h")) as f:
         header = f.read()
-    names = set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(edt_\w+)\s*\(", header, re.M))
+    names = set(re.findall(r"^\s*(?:int|int64_t|uint64_t|const char\*)\s+(edt_\w+)\s*\(", header, re.M))
     assert len(names) >= 12
     for n in names:
         assert hasattr(lib, n), n
