@@ -640,14 +640,23 @@ __device__ __forceinline__ void slerp_coefficients(double s00, double s11, doubl
     }
 }
 
+// seg_ptrs (tensor-list form, may be null): per segment {v0, v1, out} device pointers; chunk
+// starts are then relative to their segment. Null: v0 / v1 / out are flat arenas.
 template <int IDT>
 __global__ __launch_bounds__(kBlock) void slerp_stats_kernel(const void* v0, const void* v1,
                                                              const uint64_t* chunks, int64_t nchunks,
-                                                             double* partial) {
+                                                             double* partial, const uint64_t* seg_ptrs) {
     __shared__ double red[3][kBlock / 64];
     for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
         double sums[3];
-        chunk_sums<IDT>(v0, v1, chunks[3 * c], chunks[3 * c + 1], red, sums);
+        const void* a = v0;
+        const void* b = v1;
+        if (seg_ptrs) {
+            const uint64_t seg = chunks[3 * c + 2];
+            a = reinterpret_cast<const void*>(seg_ptrs[3 * seg]);
+            b = reinterpret_cast<const void*>(seg_ptrs[3 * seg + 1]);
+        }
+        chunk_sums<IDT>(a, b, chunks[3 * c], chunks[3 * c + 1], red, sums);
         if (threadIdx.x == 0) {
             partial[3 * c] = sums[0];
             partial[3 * c + 1] = sums[1];
@@ -684,9 +693,14 @@ __global__ __launch_bounds__(kBlock) void slerp_coef_kernel(const double* partia
 template <int IDT, int ODT>
 __global__ __launch_bounds__(kBlock) void slerp_blend_kernel(const void* v0, const void* v1, void* out,
                                                              const uint64_t* chunks, int64_t nchunks,
-                                                             const float* coef) {
+                                                             const float* coef, const uint64_t* seg_ptrs) {
     for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
         const uint64_t start = chunks[3 * c], len = chunks[3 * c + 1], seg = chunks[3 * c + 2];
+        if (seg_ptrs) {
+            v0 = reinterpret_cast<const void*>(seg_ptrs[3 * seg]);
+            v1 = reinterpret_cast<const void*>(seg_ptrs[3 * seg + 1]);
+            out = reinterpret_cast<void*>(seg_ptrs[3 * seg + 2]);
+        }
         const uint64_t end = start + len;
         const float c0 = coef[2 * seg], c1 = coef[2 * seg + 1];
         const uint64_t a = (start + kVec - 1) / kVec * kVec;
@@ -1051,18 +1065,51 @@ int64_t edt_slerp_make_chunks(const uint64_t* seg_offsets, int nseg, uint32_t ch
     return c;
 }
 
+}  // extern "C"
+
+namespace {
+
+int slerp_stats_impl(const void* v0, const void* v1, int in_dt, const uint64_t* chunk_desc, int64_t nchunks,
+                     double* partial, const uint64_t* seg_ptrs, void* stream) {
+    if (in_dt & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
+    if (nchunks == 0) return EDT_OK;
+    if (!chunk_desc || !partial) return fail(EDT_ERR_ARG, "null buffer");
+    const unsigned g = (unsigned)((uint64_t)nchunks < kMaxBlocks ? (uint64_t)nchunks : kMaxBlocks);
+    hipStream_t s = (hipStream_t)stream;
+    if (in_dt == EDT_F32) slerp_stats_kernel<EDT_F32><<<g, kBlock, 0, s>>>(v0, v1, chunk_desc, nchunks, partial, seg_ptrs);
+    else slerp_stats_kernel<EDT_BF16><<<g, kBlock, 0, s>>>(v0, v1, chunk_desc, nchunks, partial, seg_ptrs);
+    return check_launch("slerp_stats_kernel");
+}
+
+int slerp_blend_impl(const void* v0, const void* v1, int in_dt, void* out, int out_dt, const uint64_t* chunk_desc,
+                     int64_t nchunks, const float* coef, const uint64_t* seg_ptrs, void* stream) {
+    if ((in_dt | out_dt) & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
+    if (nchunks == 0) return EDT_OK;
+    if (!chunk_desc || !coef) return fail(EDT_ERR_ARG, "null buffer");
+    const unsigned g = (unsigned)((uint64_t)nchunks < kMaxBlocks ? (uint64_t)nchunks : kMaxBlocks);
+    hipStream_t s = (hipStream_t)stream;
+    if (in_dt == EDT_F32 && out_dt == EDT_F32)
+        slerp_blend_kernel<EDT_F32, EDT_F32><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, seg_ptrs);
+    else if (in_dt == EDT_F32)
+        slerp_blend_kernel<EDT_F32, EDT_BF16><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, seg_ptrs);
+    else if (out_dt == EDT_F32)
+        slerp_blend_kernel<EDT_BF16, EDT_F32><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, seg_ptrs);
+    else
+        slerp_blend_kernel<EDT_BF16, EDT_BF16><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, seg_ptrs);
+    return check_launch("slerp_blend_kernel");
+}
+
+}  // namespace
+
+extern "C" {
+
 int edt_slerp_stats(const void* v0, const void* v1, int in_dt, const uint64_t* chunk_desc, int64_t nchunks,
                     double* partial, void* stream) {
     g_err[0] = 0;
-    if (in_dt & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
     if (nchunks == 0) return EDT_OK;
-    if (!v0 || !v1 || !chunk_desc || !partial) return fail(EDT_ERR_ARG, "null buffer");
+    if (!v0 || !v1) return fail(EDT_ERR_ARG, "null buffer");
     if (!aligned16(v0) || !aligned16(v1)) return fail(EDT_ERR_ARG, "slerp inputs must be 16-byte aligned");
-    const unsigned g = (unsigned)((uint64_t)nchunks < kMaxBlocks ? (uint64_t)nchunks : kMaxBlocks);
-    hipStream_t s = (hipStream_t)stream;
-    if (in_dt == EDT_F32) slerp_stats_kernel<EDT_F32><<<g, kBlock, 0, s>>>(v0, v1, chunk_desc, nchunks, partial);
-    else slerp_stats_kernel<EDT_BF16><<<g, kBlock, 0, s>>>(v0, v1, chunk_desc, nchunks, partial);
-    return check_launch("slerp_stats_kernel");
+    return slerp_stats_impl(v0, v1, in_dt, chunk_desc, nchunks, partial, nullptr, stream);
 }
 
 int edt_slerp_coef(const double* partial, const int32_t* seg_first_chunk, int nseg, const double* t,
@@ -1080,22 +1127,11 @@ int edt_slerp_coef(const double* partial, const int32_t* seg_first_chunk, int ns
 int edt_slerp_blend(const void* v0, const void* v1, int in_dt, void* out, int out_dt, const uint64_t* chunk_desc,
                     int64_t nchunks, const float* coef, void* stream) {
     g_err[0] = 0;
-    if ((in_dt | out_dt) & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
     if (nchunks == 0) return EDT_OK;
-    if (!v0 || !v1 || !out || !chunk_desc || !coef) return fail(EDT_ERR_ARG, "null buffer");
+    if (!v0 || !v1 || !out) return fail(EDT_ERR_ARG, "null buffer");
     if (!aligned16(v0) || !aligned16(v1) || !aligned16(out))
         return fail(EDT_ERR_ARG, "slerp buffers must be 16-byte aligned");
-    const unsigned g = (unsigned)((uint64_t)nchunks < kMaxBlocks ? (uint64_t)nchunks : kMaxBlocks);
-    hipStream_t s = (hipStream_t)stream;
-    if (in_dt == EDT_F32 && out_dt == EDT_F32)
-        slerp_blend_kernel<EDT_F32, EDT_F32><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef);
-    else if (in_dt == EDT_F32)
-        slerp_blend_kernel<EDT_F32, EDT_BF16><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef);
-    else if (out_dt == EDT_F32)
-        slerp_blend_kernel<EDT_BF16, EDT_F32><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef);
-    else
-        slerp_blend_kernel<EDT_BF16, EDT_BF16><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef);
-    return check_launch("slerp_blend_kernel");
+    return slerp_blend_impl(v0, v1, in_dt, out, out_dt, chunk_desc, nchunks, coef, nullptr, stream);
 }
 
 int edt_slerp_merge(const void* v0, const void* v1, int in_dt, void* out, int out_dt, const uint64_t* chunk_desc,
@@ -1106,6 +1142,39 @@ int edt_slerp_merge(const void* v0, const void* v1, int in_dt, void* out, int ou
     rc = edt_slerp_coef(partial, seg_first_chunk, nseg, t, dot_threshold, eps, coef, dot_out, stream);
     if (rc) return rc;
     return edt_slerp_blend(v0, v1, in_dt, out, out_dt, chunk_desc, nchunks, coef, stream);
+}
+
+int edt_slerp_merge_list(const void* const* v0_t, const void* const* v1_t, int in_dt, void* const* out_t,
+                         int out_dt, const uint64_t* chunk_desc, int64_t nchunks, const int32_t* seg_first_chunk,
+                         int nseg, const double* t, double dot_threshold, double eps, double* partial, float* coef,
+                         float* dot_out, void* workspace, uint64_t workspace_bytes, void* stream) {
+    g_err[0] = 0;
+    if (nseg < 0) return fail(EDT_ERR_ARG, "segment count %d < 0", nseg);
+    if (nseg == 0 || nchunks == 0) return EDT_OK;
+    if (!v0_t || !v1_t || !out_t) return fail(EDT_ERR_ARG, "null tensor table");
+    const uint64_t need = 3ull * sizeof(uint64_t) * (uint64_t)nseg;
+    if (!workspace || workspace_bytes < need)
+        return fail(EDT_ERR_ARG, "workspace of %llu bytes needed", (unsigned long long)need);
+    if (reinterpret_cast<uintptr_t>(workspace) & 7u) return fail(EDT_ERR_ARG, "workspace must be 8-byte aligned");
+    thread_local std::vector<uint64_t> h;
+    h.assign(3 * (size_t)nseg, 0);
+    for (int i = 0; i < nseg; ++i) {
+        // a null pointer is only valid for an empty segment (it has no chunks, so it is never read)
+        if (!aligned16(v0_t[i]) || !aligned16(v1_t[i]) || !aligned16(out_t[i]))
+            return fail(EDT_ERR_ARG, "tensor %d is not 16-byte aligned", i);
+        h[3 * i] = reinterpret_cast<uintptr_t>(v0_t[i]);
+        h[3 * i + 1] = reinterpret_cast<uintptr_t>(v1_t[i]);
+        h[3 * i + 2] = reinterpret_cast<uintptr_t>(out_t[i]);
+    }
+    // pageable source: staged before hipMemcpyAsync returns, stream-ordered on the device
+    hipError_t e = hipMemcpyAsync(workspace, h.data(), need, hipMemcpyHostToDevice, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(EDT_ERR_LAUNCH, "tensor table upload failed: %s", hipGetErrorString(e));
+    const uint64_t* seg_ptrs = static_cast<const uint64_t*>(workspace);
+    int rc = slerp_stats_impl(nullptr, nullptr, in_dt, chunk_desc, nchunks, partial, seg_ptrs, stream);
+    if (rc) return rc;
+    rc = edt_slerp_coef(partial, seg_first_chunk, nseg, t, dot_threshold, eps, coef, dot_out, stream);
+    if (rc) return rc;
+    return slerp_blend_impl(nullptr, nullptr, in_dt, nullptr, out_dt, chunk_desc, nchunks, coef, seg_ptrs, stream);
 }
 
 }  // extern "C"

@@ -48,8 +48,13 @@ def run_slerp_merge_from_config(merge_config_dict: dict, model_1, model_2, confi
     target = base_model.model
     out_dtype = next(target.parameters()).dtype
     dev = torch.device(device) if device not in (None, "cpu") else None
-    merged = slerp_state_dicts(sd1, sd2, plan, out_dtype=out_dtype, device=dev)
-    target.load_state_dict(merged)
+    tsd = target.state_dict()
+    if set(tsd) == {k for k, _ in plan}:
+        # the merge lands in the target's own tensors (== load_state_dict of the merged dict);
+        # the target may be model_1 itself (the reference passes base_model=model_1)
+        slerp_state_dicts(sd1, sd2, plan, out_dtype=out_dtype, device=dev, out=tsd)
+    else:                                   # load_state_dict reports the key mismatch
+        target.load_state_dict(slerp_state_dicts(sd1, sd2, plan, out_dtype=out_dtype, device=dev))
     base_model.save_pretrained(merge_output_path)
     print("SLERP merging complete! Model saved at:", merge_output_path)
     return merge_output_path

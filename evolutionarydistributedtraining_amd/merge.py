@@ -1,10 +1,12 @@
 """Model-level crossover math shared by the RL / EVOMERGE / LM surfaces.
 
 The reference merges two state dicts key by key in Python, each key a numpy SLERP on the CPU
-(EDT_RL/crossover.py:84-135, EDT_EVOMERGE/train/crossover.py:104-146). Here both parents are
-packed into two flat HBM arenas (one segment per key), the per-key t values are computed on the
-host exactly as the reference does, and the whole merge is three launches (chunk sums,
-per-segment coefficients, blend) — see ops.slerp_arena.
+(EDT_RL/crossover.py:84-135, EDT_EVOMERGE/train/crossover.py:104-146). Here the per-key t values
+are computed on the host exactly as the reference does, and the whole merge is three launches
+(chunk sums, per-segment coefficients, blend) with one segment per key: over the parents' own
+device tensors (ops.slerp_list, results optionally written straight into the target model), or
+over two flat HBM arenas the parents are packed into when they are not on the device
+(ops.slerp_arena).
 """
 from __future__ import annotations
 
@@ -100,23 +102,62 @@ def _compute_device(*tensors) -> torch.device:
 _plans: dict = {}
 
 
-def _plan_for(offsets, device):
-    key = (tuple(offsets), str(device))
+def _plan_for(offsets, device, relative=False):
+    key = (tuple(offsets), str(device), relative)
     plan = _plans.get(key)
     if plan is None:
         if len(_plans) > 8:
             _plans.clear()
-        plan = _plans[key] = ops.make_slerp_plan(list(offsets), device)
+        plan = _plans[key] = ops.make_slerp_plan(list(offsets), device, relative=relative)
     return plan
 
 
+def _listable(tensors, dev) -> bool:
+    """Device tensors the tensor-list kernels can address directly."""
+    return all(isinstance(t, torch.Tensor) and t.device == dev and t.is_contiguous()
+               and t.data_ptr() % 16 == 0 for t in tensors)
+
+
+def _writes_are_safe(pairs, outs) -> bool:
+    """out[i] may alias its own inputs exactly (the blend is element-wise, after every sum);
+    any other overlap of an output with an input or another output is unsafe in one pass."""
+    spans = []
+    for i, ((a, b), o) in enumerate(zip(pairs, outs)):
+        for tag, t in (("in", a), ("in", b), ("out", o)):
+            n = t.numel() * t.element_size()
+            if n:
+                spans.append((t.data_ptr(), t.data_ptr() + n, tag, i))
+    groups = {}
+    for a, e, tag, i in spans:
+        groups.setdefault((a, e), []).append((tag, i))
+    for members in groups.values():
+        out_idx = {i for tag, i in members if tag == "out"}
+        if len(out_idx) > 1 or (out_idx and any(i not in out_idx for _, i in members)):
+            return False
+    end, open_out = -1, False
+    for (a, e) in sorted(groups):
+        has_out = any(tag == "out" for tag, _ in groups[(a, e)])
+        if a < end and (has_out or open_out):
+            return False
+        if e > end:
+            end, open_out = e, has_out
+        else:
+            open_out = open_out or has_out
+    return True
+
+
 def slerp_tensors(pairs, ts, out_dtype=torch.float32, device=None, dot_threshold=0.9995,
-                  eps=1e-8) -> list[torch.Tensor]:
+                  eps=1e-8, out=None) -> list[torch.Tensor]:
     """SLERP of each (v0, v1) pair with its own t, all in ONE multi-tensor pass.
 
     Inputs are upcast to float32 exactly like the reference's `.float().numpy()` when the two
     parents' dtypes differ; results are float32 (the reference returns float32) or `out_dtype`
-    (rounded to nearest even, as load_state_dict into a bf16 model does)."""
+    (rounded to nearest even, as load_state_dict into a bf16 model does). `out`: optional list of
+    destination tensors (e.g. the target model's parameters, which may be the first parent's
+    own tensors), written in place.
+
+    Parents already on the device are read where they lie (edt_slerp_merge_list); anything
+    else is first packed into two flat arenas (edt_slerp_merge)."""
     pairs = list(pairs)
     if not pairs:
         return []
@@ -129,17 +170,38 @@ def slerp_tensors(pairs, ts, out_dtype=torch.float32, device=None, dot_threshold
         if a.shape != b.shape:
             raise EdtError(f"parents disagree on a tensor shape: {tuple(a.shape)} vs {tuple(b.shape)}")
         offsets.append(offsets[-1] + a.numel())
+    if out is not None:
+        out = list(out)
+        if len(out) != len(pairs) or any(o.shape != a.shape for o, (a, _) in zip(out, pairs)):
+            raise EdtError("out must hold one tensor per pair, shaped like the parents")
+        dts = {o.dtype for o in out}
+        out_dtype = out[0].dtype if len(dts) == 1 else torch.float32   # mixed: round once, in copy_
+    tt = torch.tensor([float(t) for t in ts], dtype=torch.float64).to(dev)
+    if all(a.dtype == in_dt and b.dtype == in_dt for a, b in pairs) and _listable([t for p in pairs for t in p], dev):
+        outs = out
+        if outs is None:
+            outs = [torch.empty(a.shape, dtype=out_dtype, device=dev) for a, _ in pairs]
+        if _listable(outs, dev) and all(o.dtype == out_dtype for o in outs) and _writes_are_safe(pairs, outs):
+            plan = _plan_for(offsets, dev, relative=True)
+            ops.slerp_list(plan, [a.detach() for a, _ in pairs], [b.detach() for _, b in pairs],
+                           [o.detach() for o in outs], tt, dot_threshold, eps)
+            return outs
     total = offsets[-1]
     v0 = torch.empty(total, dtype=in_dt, device=dev)
     v1 = torch.empty(total, dtype=in_dt, device=dev)
     for (a, b), s, e in zip(pairs, offsets[:-1], offsets[1:]):
         v0[s:e].copy_(a.detach().reshape(-1))
         v1[s:e].copy_(b.detach().reshape(-1))
-    out = torch.empty(total, dtype=out_dtype, device=dev)
+    res = torch.empty(total, dtype=out_dtype, device=dev)
     plan = _plan_for(offsets, dev)
-    tt = torch.tensor([float(t) for t in ts], dtype=torch.float64).to(dev)
-    ops.slerp_arena(plan, v0, v1, out, tt, dot_threshold, eps)
-    return [out[s:e].view(a.shape) for (a, _), s, e in zip(pairs, offsets[:-1], offsets[1:])]
+    ops.slerp_arena(plan, v0, v1, res, tt, dot_threshold, eps)
+    views = [res[s:e].view(a.shape) for (a, _), s, e in zip(pairs, offsets[:-1], offsets[1:])]
+    if out is None:
+        return views
+    with torch.no_grad():
+        for o, v in zip(out, views):
+            o.copy_(v)
+    return out
 
 
 def slerp(t, v0, v1, DOT_THRESHOLD=0.9995, eps=1e-8):
@@ -156,11 +218,12 @@ def slerp(t, v0, v1, DOT_THRESHOLD=0.9995, eps=1e-8):
 
 
 def slerp_state_dicts(sd1: dict, sd2: dict, plan, out_dtype=torch.float32, device=None,
-                      dot_threshold=0.9995, eps=1e-8) -> dict:
-    """Merged state dict {key: tensor} for plan = [(key, t)] (see merge_plan)."""
+                      dot_threshold=0.9995, eps=1e-8, out: dict | None = None) -> dict:
+    """Merged state dict {key: tensor} for plan = [(key, t)] (see merge_plan). `out`: a state
+    dict to write the results into (e.g. the target model's, == load_state_dict of the merge)."""
     keys = [k for k, _ in plan]
     res = slerp_tensors([(sd1[k], sd2[k]) for k in keys], [t for _, t in plan], out_dtype, device,
-                        dot_threshold, eps)
+                        dot_threshold, eps, out=None if out is None else [out[k] for k in keys])
     return dict(zip(keys, res))
 
 

@@ -152,6 +152,7 @@ class SlerpPlan:
     coef: torch.Tensor            # float32 [nseg, 2]
     dots: torch.Tensor            # float32 [nseg]
     nchunks: int
+    relative: bool = False        # chunk starts relative to their segment (tensor-list form)
 
     @property
     def nseg(self) -> int:
@@ -159,7 +160,9 @@ class SlerpPlan:
 
 
 def make_slerp_plan(seg_offsets: list[int], device: torch.device,
-                    chunk_elems: int = 1 << 14) -> SlerpPlan:
+                    chunk_elems: int = 1 << 14, relative: bool = False) -> SlerpPlan:
+    """relative=True: chunk starts are offsets inside their segment, for `slerp_list` over
+    separate tensors (one segment per tensor)."""
     lib = L.load_library()
     nseg = len(seg_offsets) - 1
     offs = (ctypes.c_uint64 * max(1, nseg + 1))(*seg_offsets)
@@ -171,12 +174,15 @@ def make_slerp_plan(seg_offsets: list[int], device: torch.device,
     if got != nchunks:
         L.check(-1, "edt_slerp_make_chunks")
     import numpy as np
-    chunks = torch.from_numpy(np.ctypeslib.as_array(desc).astype(np.int64)[:3 * nchunks].copy()).view(-1, 3).to(device)
+    host = np.ctypeslib.as_array(desc).astype(np.int64)[:3 * nchunks].copy().reshape(-1, 3)
+    if relative and nchunks:
+        host[:, 0] -= np.asarray(seg_offsets, dtype=np.int64)[host[:, 2]]
+    chunks = torch.from_numpy(host).to(device)
     seg_first = torch.tensor(list(first), dtype=torch.int32).to(device)
     return SlerpPlan(list(seg_offsets), chunks, seg_first,
                      torch.empty((max(1, nchunks), 3), dtype=torch.float64, device=device),
                      torch.empty((max(1, nseg), 2), dtype=torch.float32, device=device),
-                     torch.empty(max(1, nseg), dtype=torch.float32, device=device), nchunks)
+                     torch.empty(max(1, nseg), dtype=torch.float32, device=device), nchunks, relative)
 
 
 def slerp_arena(plan: SlerpPlan, v0: torch.Tensor, v1: torch.Tensor, out: torch.Tensor,
@@ -190,7 +196,37 @@ def slerp_arena(plan: SlerpPlan, v0: torch.Tensor, v1: torch.Tensor, out: torch.
         raise L.EdtError("slerp arenas must match the plan's layout")
     if t.dtype != torch.float64 or t.numel() < plan.nseg:
         raise L.EdtError("t must be a float64 device tensor with one value per segment")
+    if plan.relative:
+        raise L.EdtError("a relative (tensor-list) plan drives slerp_list, not slerp_arena")
     L.check(lib.edt_slerp_merge(L.ptr(v0), L.ptr(v1), L.dtype_code(v0), L.ptr(out), L.dtype_code(out),
                                 L.ptr(plan.chunks), plan.nchunks, L.ptr(plan.seg_first), plan.nseg, L.ptr(t),
                                 float(dot_threshold), float(eps), L.ptr(plan.partial), L.ptr(plan.coef),
                                 L.ptr(plan.dots), L.stream_ptr(v0.device)), "edt_slerp_merge")
+
+
+def slerp_list(plan: SlerpPlan, v0s: list[torch.Tensor], v1s: list[torch.Tensor], outs: list[torch.Tensor],
+               t: torch.Tensor, dot_threshold: float = 0.9995, eps: float = 1e-8) -> None:
+    """`slerp_arena` over separate tensors (one segment each, e.g. two models' state-dict
+    tensors), writing straight into `outs` (e.g. the target model's parameters): no packing.
+    Every tensor must be contiguous and 16-byte aligned; plan = make_slerp_plan(...,
+    relative=True) over the tensors' sizes."""
+    lib = L.lib()
+    T = len(v0s)
+    if not plan.relative or T != plan.nseg or len(v1s) != T or len(outs) != T:
+        raise L.EdtError("slerp_list needs a relative plan with one segment per tensor")
+    L.require_device(*v0s, *v1s, *outs, t)
+    in_dt, out_dt = v0s[0].dtype, outs[0].dtype
+    for i in range(T):
+        n = plan.seg_offsets[i + 1] - plan.seg_offsets[i]
+        if v0s[i].numel() != n or v1s[i].numel() != n or outs[i].numel() != n:
+            raise L.EdtError(f"tensor {i} does not match the plan's layout")
+        if v0s[i].dtype != in_dt or v1s[i].dtype != in_dt or outs[i].dtype != out_dt:
+            raise L.EdtError("slerp_list: one input dtype and one output dtype")
+    if t.dtype != torch.float64 or t.numel() < T:
+        raise L.EdtError("t must be a float64 device tensor with one value per segment")
+    ws = torch.empty(max(1, 3 * T), dtype=torch.int64, device=t.device)
+    L.check(lib.edt_slerp_merge_list(L.ptr_array(v0s), L.ptr_array(v1s), L.dtype_code(in_dt),
+                                     L.ptr_array(outs), L.dtype_code(out_dt), L.ptr(plan.chunks), plan.nchunks,
+                                     L.ptr(plan.seg_first), T, L.ptr(t), float(dot_threshold), float(eps),
+                                     L.ptr(plan.partial), L.ptr(plan.coef), L.ptr(plan.dots), L.ptr(ws),
+                                     ws.numel() * 8, L.stream_ptr(t.device)), "edt_slerp_merge_list")

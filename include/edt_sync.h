@@ -147,6 +147,20 @@ int edt_slerp_merge(const void* v0, const void* v1, int in_dt, void* out, int ou
                     const double* t, double dot_threshold, double eps, double* partial, float* coef,
                     float* dot_out, void* stream);
 
+/* Tensor-list form of edt_slerp_merge: segment i is its own tensor pair v0_t[i], v1_t[i] and is
+ * written to out_t[i] (host arrays of nseg device pointers, each 16-byte aligned; NULL only for
+ * empty segments), e.g. two
+ * models' state-dict tensors merged straight into a third model's parameters
+ * (EDT_EVOMERGE/train/crossover.py:104-146 without the state-dict copies). chunk_desc holds
+ * starts RELATIVE to their segment (edt_slerp_make_chunks output minus seg_offsets[segment]).
+ * The pointer table (24 bytes per segment) is copied into `workspace` (device, 8-byte aligned)
+ * by a stream-ordered copy. */
+int edt_slerp_merge_list(const void* const* v0_t, const void* const* v1_t, int in_dt,
+                         void* const* out_t, int out_dt, const uint64_t* chunk_desc, int64_t nchunks,
+                         const int32_t* seg_first_chunk, int nseg, const double* t,
+                         double dot_threshold, double eps, double* partial, float* coef,
+                         float* dot_out, void* workspace, uint64_t workspace_bytes, void* stream);
+
 /* ---- misc ---- */
 const char* edt_last_error(void);
 const char* edt_version(void);

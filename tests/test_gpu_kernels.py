@@ -361,6 +361,37 @@ def test_slerp_multi_segment(oracle, dev, ops, in_dt, out_dt):
         assert ((got[a:b] - want).abs() <= tol).all(), s
 
 
+@pytest.mark.parametrize("in_dt,out_dt", [(torch.float32, torch.float32), (torch.bfloat16, torch.float32),
+                                          (torch.bfloat16, torch.bfloat16)])
+def test_slerp_list_matches_arena(dev, ops, in_dt, out_dt):
+    """The tensor-list SLERP (separate tensors, relative chunk starts) is bit-identical to the
+    arena SLERP on the same data: same chunking, same fixed-order sums. Also in place into v0."""
+    from evolutionarydistributedtraining_amd.merge import slerp_tensors
+    g = torch.Generator().manual_seed(11)
+    sizes = [0, 1, 7, 33, 4096, 70_001, 0, 129, 200_000]
+    offs = [0]
+    for x in sizes:
+        offs.append(offs[-1] + x)
+    v0 = (torch.randn(offs[-1], generator=g) * 0.02).to(in_dt)
+    v1 = (v0.float() + torch.randn(offs[-1], generator=g) * 1e-3).to(in_dt)
+    ts = torch.tensor([0.5, 0.0, 1.0, 0.3, 0.5, 0.7, 0.5, 0.2, 0.9], dtype=torch.float64)
+    plan = ops.make_slerp_plan(offs, dev)              # default chunking, as slerp_tensors uses
+    ref = torch.empty(offs[-1], dtype=out_dt, device=dev)
+    ops.slerp_arena(plan, v0.to(dev), v1.to(dev), ref, ts.to(dev))
+    ref_dots = plan.dots.cpu().clone()
+    a0 = [v0[a:b].to(dev).clone() for a, b in zip(offs, offs[1:])]
+    a1 = [v1[a:b].to(dev).clone() for a, b in zip(offs, offs[1:])]
+    outs = [torch.empty(x, dtype=out_dt, device=dev) for x in sizes]
+    lplan = ops.make_slerp_plan(offs, dev, relative=True)
+    ops.slerp_list(lplan, a0, a1, outs, ts.to(dev))
+    assert torch.equal(bits(torch.cat([o.cpu() for o in outs])), bits(ref.cpu()))
+    assert torch.equal(lplan.dots.cpu(), ref_dots)
+    if in_dt == out_dt:                     # merged into the first parent's own tensors
+        res = slerp_tensors(list(zip(a0, a1)), ts.tolist(), out=a0)
+        assert res is a0 or all(r.data_ptr() == x.data_ptr() for r, x in zip(res, a0))
+        assert torch.equal(bits(torch.cat([x.cpu() for x in a0])), bits(ref.cpu()))
+
+
 def test_errors_are_raised(dev, ops):
     from evolutionarydistributedtraining_amd import EdtError
     th = torch.zeros(16, device=dev)
