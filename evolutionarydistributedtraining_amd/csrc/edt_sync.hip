@@ -348,11 +348,26 @@ __device__ __forceinline__ void outer_elems(const A& a, uint64_t i) {
 
 // DIV = 1: true division by K (torch CPU `delta / num_models`); DIV = 0: multiply by 1/K,
 // bit-identical when K is a power of two.
+#ifndef EDT_FLAT_ITERS          // 8-element vectors per thread per grid-stride step (chunked loop)
+#define EDT_FLAT_ITERS 1
+#endif
+
 template <int GDT, int WDT, int KC, int DIV, int MODE, int N>
 __global__ __launch_bounds__(kBlock, EDT_MIN_WAVES) void outer_kernel(OuterArgs a) {
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
     const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if constexpr (N == kVec) {
+    if constexpr (N == kVec && EDT_FLAT_ITERS > 1) {
+        // workgroup-contiguous chunks of kBlock * kVec * EDT_FLAT_ITERS elements, grid-stride
+        constexpr uint64_t chunk = (uint64_t)kBlock * kVec * EDT_FLAT_ITERS;
+        const uint64_t nvec = a.n / kVec * kVec;
+        for (uint64_t c0 = (uint64_t)blockIdx.x * chunk; c0 < nvec; c0 += (uint64_t)gridDim.x * chunk) {
+            const uint64_t c1 = c0 + chunk < nvec ? c0 + chunk : nvec;
+            for (uint64_t i = c0 + (uint64_t)threadIdx.x * kVec; i < c1; i += (uint64_t)kBlock * kVec)
+                outer_elems<GDT, WDT, KC, DIV, MODE, kVec>(a, i);
+        }
+        const uint64_t t = nvec + tid;
+        if (t < a.n) outer_elems<GDT, WDT, KC, DIV, MODE, 1>(a, t);
+    } else if constexpr (N == kVec) {
         const uint64_t nv = a.n / kVec;
         for (uint64_t v = tid; v < nv; v += stride) outer_elems<GDT, WDT, KC, DIV, MODE, kVec>(a, v * kVec);
         const uint64_t t = nv * kVec + tid;      // scalar tail (< 8 elements)
@@ -363,11 +378,15 @@ __global__ __launch_bounds__(kBlock, EDT_MIN_WAVES) void outer_kernel(OuterArgs 
 }
 
 // Tensor-list form: the parameters are T separate allocations (HF models loaded straight to
-// the GPU), described by a table in device memory. Workgroup b handles chunk b - prefix[t] of
-// tensor t (binary search over the chunk prefix sums; uniform, so scalar loads), kListChunk
-// elements with the same per-thread 8-element body as outer_kernel. Tensors whose operands are
-// not all 16-byte aligned take the scalar body.
-constexpr uint64_t kListChunk = (uint64_t)kBlock * kVec * 16;      // 32768 elements per workgroup
+// the GPU), described by a table in device memory. The flat index space is cut into chunks of
+// kListChunk elements that never cross a tensor; a grid-stride loop (as outer_kernel's) hands
+// chunk b to a workgroup, which finds its tensor t by a binary search over the chunk prefix
+// sums (uniform across the workgroup) and runs the same per-thread 8-element body as
+// outer_kernel on it. Tensors whose operands are not all 16-byte aligned take the scalar body.
+#ifndef EDT_LIST_ITERS          // 8-element iterations per thread per chunk
+#define EDT_LIST_ITERS 2        // measured: 2-4 with the grid-stride loop beat 1 and 8-64
+#endif
+constexpr uint64_t kListChunk = (uint64_t)kBlock * kVec * EDT_LIST_ITERS;   // 4096 elements
 constexpr uint64_t kVecFlag = 1ull << 63;                          // numel[t] bit: vector body ok
 
 struct ListArgs {
@@ -377,6 +396,7 @@ struct ListArgs {
     void* const* mom;           // T (unused without momentum)
     const void* const* w;       // K * T, worker-major
     uint64_t T;
+    uint64_t chunks;            // prefix[T]
     int K;
     float kdiv;
     float kinv;
@@ -384,18 +404,17 @@ struct ListArgs {
 };
 
 template <int GDT, int WDT, int KC, int DIV>
-__global__ __launch_bounds__(kBlock, EDT_MIN_WAVES) void outer_list_kernel(ListArgs L) {
-    const uint64_t b = blockIdx.x;
+__device__ __forceinline__ void outer_list_chunk(const ListArgs& L, const uint64_t* prefix, uint64_t b) {
     uint64_t lo = 0, hi = L.T;                       // last t with prefix[t] <= b
     while (hi - lo > 1) {
         const uint64_t mid = (lo + hi) >> 1;
-        if (L.prefix[mid] <= b) lo = mid;
+        if (prefix[mid] <= b) lo = mid;
         else hi = mid;
     }
     const uint64_t t = lo;
     const uint64_t nf = L.numel[t];
     const uint64_t n = nf & ~kVecFlag;
-    const uint64_t c0 = (b - L.prefix[t]) * kListChunk;
+    const uint64_t c0 = (b - prefix[t]) * kListChunk;
     const uint64_t c1 = c0 + kListChunk < n ? c0 + kListChunk : n;
     TensorArgs a;
     a.theta = L.theta[t];
@@ -422,6 +441,21 @@ __global__ __launch_bounds__(kBlock, EDT_MIN_WAVES) void outer_list_kernel(ListA
         for (uint64_t i = c0 + threadIdx.x; i < c1; i += kBlock)
             outer_elems<GDT, WDT, KC, DIV, MODE_FUSED, 1>(a, i);
     }
+}
+
+// LDS = true: the chunk prefix sums are staged in LDS once per workgroup (dynamic shared
+// memory, (T + 1) x 8 bytes), so the per-chunk tensor search costs LDS reads, not a chain of
+// dependent global loads; LDS = false (very long tensor lists) searches the global table.
+template <int GDT, int WDT, int KC, int DIV, bool LDS>
+__global__ __launch_bounds__(kBlock, EDT_MIN_WAVES) void outer_list_kernel(ListArgs L) {
+    extern __shared__ uint64_t s_prefix[];
+    const uint64_t* prefix = L.prefix;
+    if constexpr (LDS) {
+        for (uint64_t i = threadIdx.x; i <= L.T; i += kBlock) s_prefix[i] = L.prefix[i];
+        __syncthreads();
+        prefix = s_prefix;
+    }
+    for (uint64_t b = blockIdx.x; b < L.chunks; b += gridDim.x) outer_list_chunk<GDT, WDT, KC, DIV>(L, prefix, b);
 }
 
 // SGD from a reduced fp32 sum (sharded multi-GPU step).
@@ -768,9 +802,17 @@ int launch_outer(int gdt, int wdt, const OuterArgs& a, bool vec, hipStream_t s) 
     return launch_outer_k<EDT_BF16, EDT_BF16, MODE>(a, vec, s);
 }
 
+constexpr uint64_t kListLdsMaxTensors = 8191;          // (T + 1) x 8 B <= 64 KiB of LDS
+
 template <int GDT, int WDT>
 int launch_list_k(const ListArgs& L, int div_exact, unsigned grid, hipStream_t s) {
-#define EDT_LAUNCH_L(KC, DIV) outer_list_kernel<GDT, WDT, KC, DIV><<<grid, kBlock, 0, s>>>(L)
+    const bool lds = L.T <= kListLdsMaxTensors;
+    const size_t shm = lds ? (size_t)(L.T + 1) * sizeof(uint64_t) : 0;
+#define EDT_LAUNCH_L(KC, DIV)                                                                    \
+    do {                                                                                         \
+        if (lds) outer_list_kernel<GDT, WDT, KC, DIV, true><<<grid, kBlock, shm, s>>>(L);        \
+        else outer_list_kernel<GDT, WDT, KC, DIV, false><<<grid, kBlock, 0, s>>>(L);             \
+    } while (0)
     if (L.K == 1 && !div_exact) EDT_LAUNCH_L(1, 0);
     else if (L.K == 2 && !div_exact) EDT_LAUNCH_L(2, 0);
     else if (L.K == 3 && div_exact) EDT_LAUNCH_L(3, 1);
@@ -936,12 +978,13 @@ int edt_outer_step_list(void* const* theta_t, int gdt, const void* const* theta_
     L.mom = reinterpret_cast<void* const*>(d + 3 * (uint64_t)T + 1);
     L.w = reinterpret_cast<const void* const*>(d + 4 * (uint64_t)T + 1);
     L.T = (uint64_t)T;
+    L.chunks = chunks;
     L.K = K;
     L.kdiv = (float)K;
     L.kinv = 1.0f / (float)K;
     L.sgd = sg;
     const int div_exact = is_pow2(K) ? 0 : 1;
-    const unsigned grid = (unsigned)chunks;
+    const unsigned grid = chunks > kMaxBlocks ? (unsigned)kMaxBlocks : (unsigned)chunks;   // grid-stride
     if (gdt == EDT_F32 && wdt == EDT_F32) return launch_list_k<EDT_F32, EDT_F32>(L, div_exact, grid, st);
     if (gdt == EDT_F32) return launch_list_k<EDT_F32, EDT_BF16>(L, div_exact, grid, st);
     return launch_list_k<EDT_BF16, EDT_BF16>(L, div_exact, grid, st);

@@ -85,6 +85,63 @@ def run_stream_ops(names, rounds, iters):
                "TBps": round(cases[k][0] * P / statistics.median(v) / 1e9, 3)} for k, v in times.items()}
     print(json.dumps({"op": "stream", "P": P, "variants": res}, indent=1))
 VARIANTS.update(SLERP_VARIANTS)
+VARIANTS.update({f"li{i}": [f"-DEDT_LIST_ITERS={i}"] for i in (1, 2, 4, 8, 16)})
+VARIANTS.update({f"fi{i}": [f"-DEDT_FLAT_ITERS={i}"] for i in (2, 4)})
+
+
+def run_list(names, rounds, iters):
+    """Flat-arena vs tensor-list outer step (gpt_1p3b as 292 separate tensors per model, K = 8
+    bf16 workers, fp32 theta + momentum) per variant library."""
+    import torch
+    from evolutionarydistributedtraining_amd import _lib as L
+    from evolutionarydistributedtraining_amd.layouts import gpt_1p3b
+    dev = torch.device("cuda:0")
+    lay = gpt_1p3b()
+    P, K, T = lay.total, 8, len(lay)
+    theta = torch.randn(P, device=dev) * 0.02
+    mom = torch.zeros(P, device=dev)
+    workers = [(theta + torch.randn(P, device=dev) * 1e-3).bfloat16() for _ in range(K)]
+    th_t = [v.clone() for v in lay.views(theta)]
+    mo_t = [v.clone() for v in lay.views(mom)]
+    w_t = [[v.clone() for v in lay.views(w)] for w in workers]
+    st = L.stream_ptr(dev)
+    Pp = L.ptr
+    numel = (ctypes.c_uint64 * T)(*lay.numels)
+    a_th, a_mo = L.ptr_array(th_t), L.ptr_array(mo_t)
+    a_w = L.ptr_array([t for w in w_t for t in w])
+    a_flat = L.ptr_array(workers)
+    ws = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
+    one_th, one_mo = L.ptr_array([theta]), L.ptr_array([mom])     # the flat arenas as a 1-tensor list
+    one_n = (ctypes.c_uint64 * 1)(P)
+    cases = {}
+    for n in names:
+        lib = ctypes.CDLL(os.path.join(VDIR, f"{n}.so"))
+        for name, res, args in L.SIGNATURES:
+            f = getattr(lib, name)
+            f.restype, f.argtypes = res, args
+        cases[f"{n}/flat"] = lambda lib=lib: lib.edt_outer_step(Pp(theta), 0, a_flat, 1, K, Pp(mom), 1, P, 0.7, 0.9,
+                                                                1, st)
+        cases[f"{n}/list"] = lambda lib=lib: lib.edt_outer_step_list(a_th, 0, a_w, 1, K, a_mo, 1, numel, T, 0.7, 0.9,
+                                                                     1, Pp(ws), ws.numel(), st)
+        cases[f"{n}/flat_as_list1"] = lambda lib=lib: lib.edt_outer_step_list(one_th, 0, a_flat, 1, K, one_mo, 1,
+                                                                              one_n, 1, 0.7, 0.9, 1, Pp(ws),
+                                                                              ws.numel(), st)
+    times = {k: [] for k in cases}
+    for f in cases.values():
+        assert f() == 0
+    torch.cuda.synchronize()
+    for _ in range(rounds):
+        for k, f in cases.items():
+            evs = [torch.cuda.Event(enable_timing=True) for _ in range(2 * iters)]
+            for i in range(iters):
+                evs[2 * i].record()
+                f()
+                evs[2 * i + 1].record()
+            torch.cuda.synchronize()
+            times[k] += [evs[2 * i].elapsed_time(evs[2 * i + 1]) for i in range(iters)]
+    res = {k: {"median_ms": round(statistics.median(v), 4), "TBps": round(32 * P / statistics.median(v) / 1e9, 3)}
+           for k, v in times.items()}
+    print(json.dumps({"op": "list", "P": P, "tensors": T, "variants": res}, indent=1))
 
 
 def run_slerp(names, rounds, layout_name):
@@ -209,13 +266,15 @@ if __name__ == "__main__":
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--layout", default="gpt_1p3b")
     ap.add_argument("--k", type=int, default=8)
-    ap.add_argument("--op", default="outer", choices=["outer", "slerp", "stream"])
+    ap.add_argument("--op", default="outer", choices=["outer", "slerp", "stream", "list"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:
         build(names)
     elif a.op == "stream":
         run_stream_ops(names, a.rounds, a.iters)
+    elif a.op == "list":
+        run_list(names, a.rounds, a.iters)
     elif a.op == "slerp":
         run_slerp(names, a.rounds, a.layout if a.layout != "gpt_1p3b" else "qwen2p5_7b_body")
     else:
