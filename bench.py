@@ -7,7 +7,11 @@ Metric (BASELINE.json): "GB/s of param bytes reduced per outer step (device-resi
 Default workload (N=1): the 1.3B-parameter GPT layout (P = 1,315,723,264, 292 tensors), a
 population of 8 bf16 workers resident on the GPU, fp32 global weights and fp32 momentum,
 diloco.py's outer optimiser (lr 0.7, momentum 0.9, Nesterov) in steady state (carried buffer).
-N>1: weak scaling, 8 workers resident per GPU (population 8N), RCCL reduce-scatter / all-gather.
+N>1 (BASELINE configs "8 workers over 8 GPUs"): the population stays K = 8 and
+is spread 8/N workers per GPU (strong scaling); the cross-replica step runs over RCCL (xGMI):
+reduce-scatter of fp32 partial sums + sharded SGD + all-gather of theta, or all-to-all of the raw
+worker shards + the fused kernel per shard (bit-exact), whichever puts fewer bytes on the wire.
+`--workers-per-gpu W` instead fixes W workers per GPU (weak scaling, population W*N).
 
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
@@ -39,7 +43,8 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--layout", default="gpt_1p3b")
-    p.add_argument("--workers-per-gpu", type=int, default=8)
+    p.add_argument("--population", type=int, default=8, help="total workers K (strong scaling)")
+    p.add_argument("--workers-per-gpu", type=int, default=None, help="fixed per GPU (weak scaling)")
     p.add_argument("--theta-dtype", default="f32", choices=DT)
     p.add_argument("--worker-dtype", default="bf16", choices=DT)
     p.add_argument("--lr", type=float, default=0.7)
@@ -49,6 +54,8 @@ def parse():
     p.add_argument("--bucket-elems", type=int, default=1 << 26)
     p.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     p.add_argument("--cpu-sample-elems", type=int, default=1 << 24)
+    p.add_argument("--sharded", action="store_true",
+                   help="run the multi-GPU (RCCL) schedule even at world size 1 (launch with torchrun)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return p.parse_args()
 
@@ -98,9 +105,10 @@ def main():
         if not (world == 1 and args.gpus == 1):
             raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch with torchrun")
     torch.cuda.set_device(local)
+    sharded = world > 1 or args.sharded    # --sharded: the multi-GPU code path on one rank
     dev = torch.device("cuda", local)
     import torch.distributed as dist
-    if world > 1:
+    if sharded:
         dist.init_process_group("nccl", device_id=dev)
 
     from evolutionarydistributedtraining_amd import ops
@@ -110,10 +118,15 @@ def main():
 
     layout = LAYOUTS[args.layout]()
     tdt, wdt = DT[args.theta_dtype], DT[args.worker_dtype]
-    k_local = args.workers_per_gpu
+    if args.workers_per_gpu:
+        k_local, scaling = args.workers_per_gpu, "weak"
+    else:
+        if args.population % world:
+            raise SystemExit(f"population {args.population} does not split over {world} GPUs")
+        k_local, scaling = args.population // world, "strong"
     k_total = k_local * world
     P = layout.total
-    if world == 1:
+    if not sharded:
         theta = ParamArena(layout, tdt, dev)
         workers = [ParamArena(layout, wdt, dev) for _ in range(k_local)]
         synth_population(theta.flat, [w.flat for w in workers], seed=1234)
@@ -136,29 +149,29 @@ def main():
 
     # fused-kernel duration, measured with HIP events on the launch stream (torch's current)
     kern_ms = None
-    if world == 1:
+    if not sharded:
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 
-    if world > 1:
+    if sharded:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        if world == 1:
+        if not sharded:
             ev[i][0].record()
         step()
-        if world == 1:
+        if not sharded:
             ev[i][1].record()
     torch.cuda.synchronize()
-    if world > 1:
+    if sharded:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if sharded:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     ms_per_step = elapsed / args.steps * 1e3
-    if world == 1:
+    if not sharded:
         ks = sorted(a.elapsed_time(b) for a, b in ev)
         kern_ms = sum(ks) / len(ks)
 
@@ -171,7 +184,7 @@ def main():
         per_elem = k_local * bw + 2 * bg + (2 * bg if args.momentum else 0)
         algo_bytes = per_elem * P                       # one launch, steady state (carried buffer)
         roofline = None
-        if world == 1:
+        if not sharded:
             achieved = algo_bytes / (kern_ms / 1e3) / 1e9
             traffic = None
             if os.path.exists(args.traffic_json):
@@ -190,29 +203,30 @@ def main():
             "metric": "GB/s of param bytes reduced per outer step (device-resident), 1/2/4/8 GPUs",
             "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32" if tdt == torch.float32 else "bf16",
+            "scaling": scaling, "vs_baseline": None, "dtype": "f32" if tdt == torch.float32 else "bf16",
             "data": "synthetic (theta ~ N(0,.02^2), worker = theta + N(0,1e-3^2), seeded on device)",
             "config": {"workload": f"DiLoCo outer step, {args.layout} P={P} T={len(layout)}, "
-                                   f"{k_local} {args.worker_dtype} workers resident per GPU, "
+                                   f"population {k_total} ({k_local} {args.worker_dtype} workers resident per GPU), "
                                    f"{args.theta_dtype} theta+momentum, lr {args.lr} mu {args.momentum} "
                                    f"nesterov {bool(args.nesterov)}",
                        "params": P, "tensors": len(layout), "workers_per_gpu": k_local,
                        "population": k_total, "worker_dtype": args.worker_dtype,
                        "theta_dtype": args.theta_dtype,
-                       "parallelism": "single GPU" if world == 1 else f"dp{world} {sync.mode} (RCCL)"},
+                       "parallelism": "single GPU" if not sharded else f"dp{world} {sync.mode} (RCCL)"},
         }
-        if world > 1:
+        if sharded:
             # the exchange dominates: bytes this rank puts on xGMI per step over the whole step time
             # (the local HBM pass is inside that time), against the rank's links to its N-1 peers
             wire = sync.wire_bytes()
             achieved = wire / (ms_per_step / 1e3) / 1e9
             peak = XGMI_LINK_GBPS * (world - 1)
             roofline = {"bound": "xgmi", "achieved": round(achieved, 1), "peak": peak, "unit": "GB/s",
-                        "frac": round(achieved / peak, 4), "traffic": None, "wire_bytes_per_rank": wire,
+                        "frac": round(achieved / peak, 4) if peak else None, "traffic": None,
+                        "wire_bytes_per_rank": wire,
                         "schedule": sync.mode}
         if roofline:
             out["roofline"] = roofline
-        if world == 1:   # what a plain device-to-device copy reaches on this device, same process
+        if not sharded:   # what a plain device-to-device copy reaches on this device, same process
             src = torch.empty(1 << 29, dtype=torch.float32, device=dev)
             dst = torch.empty_like(src)
             dst.copy_(src)
@@ -227,10 +241,10 @@ def main():
         prop = torch.cuda.get_device_properties(dev)
         out["device"] = {"name": prop.name, "arch": getattr(prop, "gcnArchName", ""),
                          "cus": prop.multi_processor_count, "hbm_gib": round(prop.total_memory / 2**30, 1)}
-        if world == 1 and args.cpu_baseline_seconds > 0:
+        if not sharded and args.cpu_baseline_seconds > 0:
             out["cpu_baseline"] = cpu_baseline(args, tdt, wdt, k_local)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if sharded:
         dist.barrier()
         dist.destroy_process_group()
 

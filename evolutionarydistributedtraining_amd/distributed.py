@@ -72,9 +72,8 @@ class ShardedOuterSync:
             self.acc = torch.zeros(self.n_pad, dtype=torch.float32, device=device)
             self.acc_shard = None if self.inplace else torch.empty(shard_total, dtype=torch.float32, device=device)
         else:
-            per = self.bucket // self.world
-            self.send = torch.empty(self.world * k_local * per, dtype=worker_dtype, device=device)
-            self.recv = torch.empty(self.world * k_local * per, dtype=worker_dtype, device=device)
+            # recv[j][b:e] viewed [src rank][per]: local worker j of every rank, this rank's shard
+            self.recv = [torch.empty(self.n_pad, dtype=worker_dtype, device=device) for _ in range(k_local)]
 
     # ---------------------------------------------------------------------------------------
     def _shard(self, b, e):
@@ -106,19 +105,25 @@ class ShardedOuterSync:
                 mom_off += per
                 gathers.append(self._gather(b, e, s0, s1))
         else:
+            # phase 1: every bucket's all-to-all, straight from the worker arenas (a worker's
+            # bucket [b, e) is already laid out [dest rank][per]); one collective per local worker
+            works = []
             for b, e in self.buckets:
+                works.append([dist.all_to_all_single(self.recv[j][b:e], wb[b:e], group=self.group,
+                                                     async_op=True)
+                              for j, wb in enumerate(self.worker_bufs)])
+            # phase 2: as each bucket lands, the single-GPU fused step on the owned shard
+            for (b, e), ws in zip(self.buckets, works):
+                for w in ws:
+                    w.wait()
                 per = (e - b) // self.world
-                # pack: [dest rank][local worker][per]
-                sv = self.send[:self.world * self.k_local * per].view(self.world, self.k_local, per)
-                for j, wb in enumerate(self.worker_bufs):
-                    sv[:, j, :].copy_(wb[b:e].view(self.world, per))
-                rv = self.recv[:self.world * self.k_local * per]
-                dist.all_to_all_single(rv, sv.reshape(-1), group=self.group)
-                rv = rv.view(self.world * self.k_local, per)     # [src rank][local worker] = global k
+                rv = [r[b:e].view(self.world, per) for r in self.recv]
+                # global worker k = src * K_local + j: the reference's worker order
+                shards = [rv[j][src] for src in range(self.world) for j in range(self.k_local)]
                 s0, s1 = self._shard(b, e)
                 mom = None if self.mom_shard is None else self.mom_shard[mom_off:mom_off + per]
-                k.outer_step(self.theta_buf[s0:s1], [rv[i] for i in range(self.k_total)], mom,
-                             self.has_momentum, self.lr, self.momentum, self.nesterov)
+                k.outer_step(self.theta_buf[s0:s1], shards, mom, self.has_momentum, self.lr,
+                             self.momentum, self.nesterov)
                 mom_off += per
                 gathers.append(self._gather(b, e, s0, s1))
         for g in gathers:
