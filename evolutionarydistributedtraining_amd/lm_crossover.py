@@ -155,8 +155,38 @@ def run_sgd(model_1, model_2, base_model, output_path, model1_path, model2_path,
     return output_path
 
 
-def crossover_main(model1_path, model2_path, output_path):
-    """EDT_LM/train/crossover.py:240-315 with run_linear_merge_5050 + run_sgd fused."""
+def _read_parents_direct(paths, dev):
+    """The child model (`from_config` of the first trained model's config, bf16, built on the
+    GPU) bound to a flat arena, and the four parents' checkpoints read straight into bf16 arenas
+    in the child's `parameters()` order (checkpoint.read_into_arena: safetensors -> pinned host
+    -> HBM, no model objects). None when a checkpoint lacks one of the child's parameter names
+    (the caller then loads the parents with from_pretrained)."""
+    from transformers import AutoConfig, AutoModelForCausalLM
+    from .checkpoint import checkpoint_files, read_into_arena
+    from .params import ParamArena, bind_module_
+    config = AutoConfig.from_pretrained(paths[0], trust_remote_code=True, cache_dir="cache")
+    config.dtype = torch.bfloat16            # what from_pretrained(torch_dtype=bf16) leaves in model_1.config
+    with torch.device(dev):
+        child = AutoModelForCausalLM.from_config(config)
+    layout = ParamLayout.of_module(child)
+    for p in paths:
+        try:
+            have = checkpoint_files(p)
+        except (OSError, ValueError):
+            return None
+        if any(n not in have for n in layout.names):
+            return None
+    dtype = next(child.parameters()).dtype
+    arena = bind_module_(child, ParamArena(layout, dtype, dev), copy=False)
+    parents = [read_into_arena(p, layout, torch.empty(layout.total, dtype=dtype, device=dev)) for p in paths]
+    return child, arena, parents
+
+
+def crossover_main(model1_path, model2_path, output_path, direct: bool = True):
+    """EDT_LM/train/crossover.py:240-315 with run_linear_merge_5050 + run_sgd fused.
+
+    direct=True reads the four parent checkpoints straight into HBM arenas (SURVEY 8(f)1's I/O
+    edge); the results are the same as through from_pretrained (same bf16 conversion)."""
     from transformers import AutoModelForCausalLM, AutoTokenizer
     with open(os.path.join(model1_path, "genome.json")) as f:
         p1_genome = json.load(f)
@@ -165,11 +195,24 @@ def crossover_main(model1_path, model2_path, output_path):
     base1_path, base2_path = model1_path, model2_path
     trained1_path, trained2_path = p1_genome.get("mutation_path"), p2_genome.get("mutation_path")
 
-    model_1 = load_model_from_path(trained1_path)
-    model_2 = load_model_from_path(trained2_path)
-    base_1 = load_model_from_path(base1_path)
-    base_2 = load_model_from_path(base2_path)
-    child = AutoModelForCausalLM.from_config(model_1.config).to(_device())
+    dev = _device()
+    got = _read_parents_direct([trained1_path, trained2_path, base1_path, base2_path], dev) if direct else None
+    if got is not None:
+        child, _, (m1, m2, b1, b2) = got
+    else:
+        model_1 = load_model_from_path(trained1_path)
+        model_2 = load_model_from_path(trained2_path)
+        base_1 = load_model_from_path(base1_path)
+        base_2 = load_model_from_path(base2_path)
+        child = AutoModelForCausalLM.from_config(model_1.config).to(dev)
+        # the state dicts of the bases and parameters() of the trained models share one order
+        # for untied HF causal LMs; both sides are packed into flat arenas in parameters() order
+        with torch.no_grad():
+            b1 = pack(list(base_1.parameters()), device=dev)
+            b2 = pack(list(base_2.parameters()), dtype=b1.dtype, device=dev)
+            m1 = pack(list(model_1.parameters()), dtype=b1.dtype, device=dev)
+            m2 = pack(list(model_2.parameters()), dtype=b1.dtype, device=dev)
+        del model_1, model_2, base_1, base_2
     child_params = list(child.parameters())
 
     tokenizer = AutoTokenizer.from_pretrained(trained1_path, trust_remote_code=True, cache_dir="cache")
@@ -189,14 +232,7 @@ def crossover_main(model1_path, model2_path, output_path):
         json.dump({"fitness": 0.0, "model_path": output_path, "dna": dna, "p1": p1_genome,
                    "p2": p2_genome}, f, indent=4)
 
-    # the state dicts of the bases and parameters() of the trained models share one order for
-    # untied HF causal LMs; both sides are packed into flat arenas in parameters() order
-    dev = _device()
     with torch.no_grad():
-        b1 = pack(list(base_1.parameters()), device=dev)
-        b2 = pack(list(base_2.parameters()), dtype=b1.dtype, device=dev)
-        m1 = pack(list(model_1.parameters()), dtype=b1.dtype, device=dev)
-        m2 = pack(list(model_2.parameters()), dtype=b1.dtype, device=dev)
         state_sd = load_parent_outer_state(base1_path, base2_path)
         _child_step(b1, b2, m1, m2, child_params, ParamLayout.of(child_params), state_sd, lr, momentum,
                     nesterov, output_path)

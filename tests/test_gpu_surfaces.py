@@ -142,9 +142,11 @@ def test_lm_run_sgd_requires_parent_state(dev, tmp_path, golden):
                              str(tmp_path / "b" / "Gen0003"), 0.7, 0.9, True)
 
 
-def test_lm_crossover_main_cli_flow(golden, oracle, dev, tmp_path):
+@pytest.mark.parametrize("direct", [True, False])
+def test_lm_crossover_main_cli_flow(golden, oracle, dev, tmp_path, direct):
     """Parent dirs with genome.json -> child dir: model, tokenizer, genome, outer_optim.pt,
-    optimizer.pt carried from parent 1's trained dir (EDT_LM/train/crossover.py:240-315)."""
+    optimizer.pt carried from parent 1's trained dir (EDT_LM/train/crossover.py:240-315).
+    direct: parents read straight into HBM arenas; else through from_pretrained."""
     from evolutionarydistributedtraining_amd import lm_crossover
     from tests.test_oracle_golden import pair_inputs
     c, g = _pair_case(golden, "both_parent1_rule")
@@ -167,7 +169,7 @@ def test_lm_crossover_main_cli_flow(golden, oracle, dev, tmp_path):
         dirs[tag] = base_dir
     out = tmp_path / "child" / "Gen0004"
     np.random.seed(123)
-    lm_crossover.crossover_main(str(dirs["1"]), str(dirs["2"]), str(out))
+    lm_crossover.crossover_main(str(dirs["1"]), str(dirs["2"]), str(out), direct=direct)
     sd = load_file(str(out / "model.safetensors"))
     from transformers import LlamaForCausalLM
     names = [n for n, _ in LlamaForCausalLM(_tiny_llama_cfg()).named_parameters()]
