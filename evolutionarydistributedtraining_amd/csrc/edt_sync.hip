@@ -348,26 +348,11 @@ __device__ __forceinline__ void outer_elems(const A& a, uint64_t i) {
 
 // DIV = 1: true division by K (torch CPU `delta / num_models`); DIV = 0: multiply by 1/K,
 // bit-identical when K is a power of two.
-#ifndef EDT_FLAT_ITERS          // 8-element vectors per thread per grid-stride step (chunked loop)
-#define EDT_FLAT_ITERS 1
-#endif
-
 template <int GDT, int WDT, int KC, int DIV, int MODE, int N>
 __global__ __launch_bounds__(kBlock, EDT_MIN_WAVES) void outer_kernel(OuterArgs a) {
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
     const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if constexpr (N == kVec && EDT_FLAT_ITERS > 1) {
-        // workgroup-contiguous chunks of kBlock * kVec * EDT_FLAT_ITERS elements, grid-stride
-        constexpr uint64_t chunk = (uint64_t)kBlock * kVec * EDT_FLAT_ITERS;
-        const uint64_t nvec = a.n / kVec * kVec;
-        for (uint64_t c0 = (uint64_t)blockIdx.x * chunk; c0 < nvec; c0 += (uint64_t)gridDim.x * chunk) {
-            const uint64_t c1 = c0 + chunk < nvec ? c0 + chunk : nvec;
-            for (uint64_t i = c0 + (uint64_t)threadIdx.x * kVec; i < c1; i += (uint64_t)kBlock * kVec)
-                outer_elems<GDT, WDT, KC, DIV, MODE, kVec>(a, i);
-        }
-        const uint64_t t = nvec + tid;
-        if (t < a.n) outer_elems<GDT, WDT, KC, DIV, MODE, 1>(a, t);
-    } else if constexpr (N == kVec) {
+    if constexpr (N == kVec) {
         const uint64_t nv = a.n / kVec;
         for (uint64_t v = tid; v < nv; v += stride) outer_elems<GDT, WDT, KC, DIV, MODE, kVec>(a, v * kVec);
         const uint64_t t = nv * kVec + tid;      // scalar tail (< 8 elements)

@@ -86,7 +86,6 @@ def run_stream_ops(names, rounds, iters):
     print(json.dumps({"op": "stream", "P": P, "variants": res}, indent=1))
 VARIANTS.update(SLERP_VARIANTS)
 VARIANTS.update({f"li{i}": [f"-DEDT_LIST_ITERS={i}"] for i in (1, 2, 4, 8, 16)})
-VARIANTS.update({f"fi{i}": [f"-DEDT_FLAT_ITERS={i}"] for i in (2, 4)})
 
 
 def run_list(names, rounds, iters):

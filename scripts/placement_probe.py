@@ -1,12 +1,12 @@
 """Probe: does WHERE the operands live change the fused step's speed on a given box?
 
 One process, interleaved timing (HIP events) of the DiLoCo step on the 1.3B layout, K = 8 bf16
-workers, fp32 theta + momentum, with the same values placed as
-  arena      one allocation per operand (what bench.py does)
-  stagger    the ten operands carved from one buffer, operand j shifted by j x (4 KiB + 256 B)
-  list       292 separate allocations per operand, tensor-list launch (edt_outer_step_list)
-  arena_l1   the arenas again, through the tensor-list launch as a one-tensor list
-plus a plain device copy as the box's speed reference.
+workers, fp32 theta + momentum. Every case runs the tensor-list launch (edt_outer_step_list,
+292 tensors; on par with the flat launch) over the same values, each operand placed as
+  A   views of one arena per operand (what bench.py allocates)
+  S   separate allocations, one per tensor
+  Gx  views of one arena per operand, operand j's arena shifted by j * x bytes
+and the flat launch over the arenas as the reference point, plus a plain device copy.
 
     python scripts/placement_probe.py [--rounds 3 --iters 5]
 """
@@ -42,38 +42,46 @@ def main():
     theta = torch.randn(P, device=dev, generator=g) * 0.02
     mom = torch.zeros(P, device=dev)
     workers = [(theta + torch.randn(P, device=dev, generator=g) * 1e-3).bfloat16() for _ in range(K)]
-    cases = {}
-    a_w = L.ptr_array(workers)
-    cases["arena"] = lambda: lib.edt_outer_step(Pp(theta), 0, a_w, 1, K, Pp(mom), 1, P, 0.7, 0.9, 1, st)
-    ws = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
-    one_th, one_mo, one_n = L.ptr_array([theta]), L.ptr_array([mom]), (ctypes.c_uint64 * 1)(P)
-    cases["arena_l1"] = lambda: lib.edt_outer_step_list(one_th, 0, a_w, 1, K, one_mo, 1, one_n, 1, 0.7, 0.9, 1,
-                                                        Pp(ws), ws.numel(), st)
-    # staggered: one byte buffer, operand j at offset sum of sizes + j * (4096 + 256)
-    sizes = [P * 4, P * 4] + [P * 2] * K
-    shift = 4096 + 256
-    big = torch.empty(sum(sizes) + len(sizes) * shift + 256, dtype=torch.uint8, device=dev)
-    views, off = [], 0
-    for j, nb in enumerate(sizes):
-        off += shift
-        views.append(big[off:off + nb])
-        off += nb
-    s_th = views[0].view(torch.float32)
-    s_mo = views[1].view(torch.float32)
-    s_w = [v.view(torch.bfloat16) for v in views[2:]]
-    s_th.copy_(theta)
-    s_mo.copy_(mom)
-    for d, w in zip(s_w, workers):
-        d.copy_(w)
-    a_sw = L.ptr_array(s_w)
-    cases["stagger"] = lambda: lib.edt_outer_step(Pp(s_th), 0, a_sw, 1, K, Pp(s_mo), 1, P, 0.7, 0.9, 1, st)
-    th_t = [v.clone() for v in lay.views(theta)]
-    mo_t = [v.clone() for v in lay.views(mom)]
-    w_t = [[v.clone() for v in lay.views(w)] for w in workers]
+    ops_ = [theta, mom] + workers                       # operand j
     numel = (ctypes.c_uint64 * T)(*lay.numels)
-    l_th, l_mo, l_w = L.ptr_array(th_t), L.ptr_array(mo_t), L.ptr_array([t for w in w_t for t in w])
-    cases["list"] = lambda: lib.edt_outer_step_list(l_th, 0, l_w, 1, K, l_mo, 1, numel, T, 0.7, 0.9, 1,
-                                                    Pp(ws), ws.numel(), st)
+    ws = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
+    keep = []
+
+    def place(j, how):
+        src = ops_[j]
+        if how == "A":
+            return lay.views(src)
+        if how == "S":
+            ts = [v.clone() for v in lay.views(src)]
+            keep.append(ts)
+            return ts
+        shift = int(how[1:]) * j                          # "G<bytes>"
+        nb = src.numel() * src.element_size()
+        buf = torch.empty(nb + shift + 256, dtype=torch.uint8, device=dev)
+        v = buf[shift:shift + nb].view(src.dtype)
+        v.copy_(src)
+        keep.append(buf)
+        return lay.views(v)
+
+    cases = {}
+
+    def add(name, hows):
+        tl = [place(j, h) for j, h in enumerate(hows)]
+        a_th, a_mo = L.ptr_array(tl[0]), L.ptr_array(tl[1])
+        a_w = L.ptr_array([t for w in tl[2:] for t in w])
+        cases[name] = lambda: lib.edt_outer_step_list(a_th, 0, a_w, 1, K, a_mo, 1, numel, T, 0.7, 0.9, 1,
+                                                      Pp(ws), ws.numel(), st)
+
+    a_w = L.ptr_array(workers)
+    cases["flat_arena"] = lambda: lib.edt_outer_step(Pp(theta), 0, a_w, 1, K, Pp(mom), 1, P, 0.7, 0.9, 1, st)
+    add("list_A", ["A"] * 10)
+    add("list_S", ["S"] * 10)
+    add("theta_mom_S", ["S", "S"] + ["A"] * K)
+    add("workers_S", ["A", "A"] + ["S"] * K)
+    add("G4352", ["G4352"] * 10)
+    add("G1052672", ["G1052672"] * 10)                   # 1 MiB + 4 KiB
+    add("G37748736", ["G37748736"] * 10)                 # 36 MiB
+    torch.cuda.empty_cache()
     src = torch.empty(1 << 29, dtype=torch.float32, device=dev)
     dst = torch.empty_like(src)
     cases["copy_4GiB"] = lambda: (dst.copy_(src), 0)[1]
