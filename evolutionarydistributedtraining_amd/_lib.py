@@ -35,6 +35,7 @@ SIGNATURES = [
     ("edt_delta_partial", _I, [_P, _I, ctypes.POINTER(_P), _I, _I, _I, _U64, _P, _I, _P]),
     ("edt_sgd_apply", _I, [_P, _I, _P, _P, _I, _U64, _D, _D, _I, _P]),
     ("edt_pair_merge", _I, [_P, _P, _P, _P, _I, _P, _I, _P, _I, _U64, _D, _D, _I, _P]),
+    ("edt_pair_merge_to", _I, [_P, _P, _P, _P, _I, _P, _I, _P, _P, _I, _U64, _D, _D, _I, _P]),
     ("edt_lerp", _I, [_P, _P, _I, _P, _I, _I, _U64, _D, _P]),
     ("edt_slerp_make_chunks", ctypes.c_int64,
      [ctypes.POINTER(_U64), _I, ctypes.c_uint32, ctypes.POINTER(_U64), ctypes.c_int64,

@@ -482,7 +482,8 @@ struct PairArgs {
     const void* m1;
     const void* m2;
     void* out;
-    void* mom;
+    const void* mom_in;   // carried buffer read (the donor parent's); may equal mom
+    void* mom;            // the child's buffer written
     uint64_t n;
     SgdScalars sgd;
 };
@@ -490,7 +491,7 @@ struct PairArgs {
 template <int GDT, int WDT, int N>
 __device__ __forceinline__ void pair_elems(const PairArgs& a, uint64_t i) {
     float base[N], b_in[N];
-    ld_momentum<GDT, N>(a.mom, i, a.sgd, b_in);
+    ld_momentum<GDT, N>(a.mom_in, i, a.sgd, b_in);
     if (a.b2) {                        // run_linear_merge_5050: lerp(0.5, b1, b2) in the model dtype
         float x[N], y[N];
         ld<WDT, N, EDT_NT_LOADS != 0 && WDT == EDT_BF16>(a.b1, i, x);
@@ -1015,16 +1016,26 @@ int edt_sgd_apply(void* theta_g, int gdt, const float* acc_f32, void* momentum, 
 int edt_pair_merge(const void* b1, const void* b2, const void* m1, const void* m2, int wdt,
                    void* theta_out, int gdt, void* momentum, int has_momentum, uint64_t n, double lr,
                    double momentum_coef, int nesterov, void* stream) {
+    return edt_pair_merge_to(b1, b2, m1, m2, wdt, theta_out, gdt, momentum, momentum, has_momentum, n, lr,
+                             momentum_coef, nesterov, stream);
+}
+
+int edt_pair_merge_to(const void* b1, const void* b2, const void* m1, const void* m2, int wdt,
+                      void* theta_out, int gdt, const void* momentum_in, void* momentum, int has_momentum,
+                      uint64_t n, double lr, double momentum_coef, int nesterov, void* stream) {
     g_err[0] = 0;
     if (!valid_pair(gdt, wdt)) return fail(EDT_ERR_ARG, "unsupported dtype pair (gdt/wdt)");
     if (n == 0) return EDT_OK;
     if (!b1 || !m1 || !m2 || !theta_out) return fail(EDT_ERR_ARG, "null buffer");
     PairArgs a;
     a.b1 = b1; a.b2 = b2; a.m1 = m1; a.m2 = m2; a.out = theta_out; a.mom = momentum; a.n = n;
+    a.mom_in = momentum_in;
     a.sgd = make_sgd(gdt, lr, momentum_coef, has_momentum, nesterov);
     if (a.sgd.use_momentum && !momentum) return fail(EDT_ERR_ARG, "momentum buffer is null");
+    if (a.sgd.use_momentum && has_momentum && !momentum_in) return fail(EDT_ERR_ARG, "carried momentum is null");
     const bool vec = aligned16(b1) && (!b2 || aligned16(b2)) && aligned16(m1) && aligned16(m2) &&
-                     aligned16(theta_out) && (!a.sgd.use_momentum || aligned16(momentum));
+                     aligned16(theta_out) && (!a.sgd.use_momentum || aligned16(momentum)) &&
+                     (!a.sgd.use_momentum || !has_momentum || aligned16(momentum_in));
     const unsigned g = grid_for(n, vec);
     hipStream_t s = (hipStream_t)stream;
     if (gdt == EDT_F32 && wdt == EDT_F32) {

@@ -110,18 +110,23 @@ def sgd_apply(theta: torch.Tensor, acc: torch.Tensor, momentum: torch.Tensor | N
 
 def pair_merge(b1: torch.Tensor, b2: torch.Tensor | None, m1: torch.Tensor, m2: torch.Tensor,
                out: torch.Tensor, momentum: torch.Tensor | None, has_momentum: bool, lr: float,
-               momentum_coef: float, nesterov: bool) -> None:
+               momentum_coef: float, nesterov: bool, momentum_in: torch.Tensor | None = None) -> None:
     """EDT child = SGD step of lerp(.5, b1, b2) towards m1, m2 (EDT_LM/train/crossover.py:150-230).
-    b2 None: b1 is the already merged base (dtype of `out`)."""
+    b2 None: b1 is the already merged base (dtype of `out`). momentum is updated in place, or,
+    with `momentum_in` (the donor parent's buffer, left intact), written fresh
+    (edt_pair_merge_to)."""
     lib = L.lib()
-    L.require_device(b1, b2, m1, m2, out, momentum)
+    L.require_device(b1, b2, m1, m2, out, momentum, momentum_in)
     n = out.numel()
-    if any(t is not None and t.numel() != n for t in (b1, b2, m1, m2, momentum)):
+    if any(t is not None and t.numel() != n for t in (b1, b2, m1, m2, momentum, momentum_in)):
         raise L.EdtError("pair-merge buffers must all have the same size")
-    L.check(lib.edt_pair_merge(L.ptr(b1), L.ptr(b2), L.ptr(m1), L.ptr(m2), L.dtype_code(m1),
-                               L.ptr(out), L.dtype_code(out), L.ptr(momentum), int(has_momentum), n,
-                               float(lr), float(momentum_coef), int(nesterov),
-                               L.stream_ptr(out.device)), "edt_pair_merge")
+    if momentum_in is not None and momentum is not None and momentum_in.dtype != momentum.dtype:
+        raise L.EdtError("momentum_in and momentum must share a dtype")
+    mom_in = momentum if momentum_in is None else momentum_in
+    L.check(lib.edt_pair_merge_to(L.ptr(b1), L.ptr(b2), L.ptr(m1), L.ptr(m2), L.dtype_code(m1),
+                                  L.ptr(out), L.dtype_code(out), L.ptr(mom_in), L.ptr(momentum),
+                                  int(has_momentum), n, float(lr), float(momentum_coef), int(nesterov),
+                                  L.stream_ptr(out.device)), "edt_pair_merge_to")
 
 
 def lerp(t: float, v0: torch.Tensor, v1: torch.Tensor, out: torch.Tensor | None = None,

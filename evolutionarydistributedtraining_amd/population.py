@@ -1,0 +1,328 @@
+"""Rank-resident EDT generations: the population stays in HBM across
+generations; selection, parent exchange and the merge never touch a disk.
+
+The reference moves every individual through the shared disk each generation: the master
+selects pairs from genome.json fitness values (EDT_LM/edt_sim.py:177-240, EDT_RL/edt.py:
+221-272), then each worker's crossover.py loads both parents' base and trained checkpoints,
+merges, and saves the child (EDT_LM/edt_sim.py:244-256 -> EDT_LM/train/crossover.py:240-315;
+EDT_RL/edt.py:286-299 -> EDT_RL/crossover.py:173-201). Here:
+
+  * members live in flat parameter arenas, `members_per_rank` of them on each rank (one process
+    per GPU; every member on one GPU when the world is 1);
+  * the selection runs on rank 0 with the reference's own selection functions (schedule.py,
+    draw for draw) and the replicated host state (genomes, momentum flags) is broadcast;
+  * child c replaces member c and is built on member c's rank; the parents it needs arrive by
+    grouped point-to-point transfers (schedule.exchange_plan, RCCL send/recv over xGMI: one
+    transfer per (member, destination rank));
+  * the merge is the single-GPU kernel: kind="sgd" is the EDT-LM child (edt_pair_merge:
+    lerp(0.5) of the bases + SGD step along the mean pseudo-gradient with the donor's outer
+    momentum, EDT_LM/train/crossover.py:150-232), kind="slerp" the EDT-RL / EVOMERGE child
+    (edt_slerp_merge with per-tensor t, EDT_RL/crossover.py:84-135);
+  * children are written into spare arenas and swapped in after every transfer of the
+    generation has completed (a parent may feed several children).
+
+The inner loop (SFT / PPO) and fitness evaluation are the caller's: `trained(m)` / `params(m)`
+are the arenas it updates (params.bind_module_ points a model's parameters into one).
+"""
+from __future__ import annotations
+
+import random
+
+import torch
+import torch.distributed as dist
+
+from . import ops as _ops
+from . import schedule
+from ._lib import EdtError
+from .merge import uniform_dna_crossover
+from .params import ParamLayout
+
+
+class ResidentPopulation:
+    """kind="sgd":   member m holds base (the generation's start weights, GenN), trained (after
+                     the inner loop, the genome's mutation_path) and its outer momentum.
+       kind="slerp": member m holds params (its Policy+Value keys, one segment per key) and the
+                     per-segment t of the merge (`seg_t`, e.g. merge.merge_plan's t values).
+
+    genomes: the initial genome dicts in member order (EDT-LM: {"dna": [...]};
+    EDT-RL: {"env": {"env_name", "reward_dna", "agents"}}); "fitness" and "model_path" are
+    filled in here ("model_path" = a per-member, per-generation id)."""
+
+    def __init__(self, layout: ParamLayout, dtype: torch.dtype, device, genomes: list[dict],
+                 kind: str = "sgd", momentum_dtype: torch.dtype | None = None, seg_t=None,
+                 lr: float = 0.7, momentum: float = 0.9, nesterov: bool = True,
+                 dot_threshold: float = 0.9995, eps: float = 1e-8, elitism: int = 0,
+                 group=None, kernels=None):
+        if kind not in ("sgd", "slerp"):
+            raise ValueError(kind)
+        self.kind = kind
+        self.layout = layout
+        self.dtype = dtype
+        self.device = torch.device(device)
+        self.kernels = kernels or _ops
+        self.group = group
+        self.distributed = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if self.distributed else 1
+        self.rank = dist.get_rank(group) if self.distributed else 0
+        self.P = len(genomes)
+        if self.P == 0 or self.P % self.world:
+            raise EdtError(f"population {self.P} does not split over {self.world} ranks")
+        self.M = self.P // self.world
+        self.lr, self.momentum, self.nesterov = lr, momentum, nesterov
+        self.dot_threshold, self.eps = dot_threshold, eps
+        self.elitism = elitism
+        self.generation = 0
+        self.genomes = [dict(g) for g in genomes]
+        self.has_momentum = [False] * self.P
+        self._fitness = None
+        n = layout.total
+        mdt = momentum_dtype or dtype
+
+        def arena(dt):
+            return torch.zeros(n, dtype=dt, device=self.device)
+
+        self._slot = {m: m - self.rank * self.M for m in self.local_members()}
+        if kind == "sgd":
+            self._base = [arena(dtype) for _ in range(self.M)]
+            self._trained = [arena(dtype) for _ in range(self.M)]
+            self._mom = [arena(mdt) if momentum else None for _ in range(self.M)]
+            self._child = [arena(dtype) for _ in range(self.M)]
+            self._child_mom = [arena(mdt) if momentum else None for _ in range(self.M)]
+        else:
+            if seg_t is None or len(seg_t) != len(layout):
+                raise EdtError("kind='slerp' needs one t per tensor of the layout (seg_t)")
+            self._params = [arena(dtype) for _ in range(self.M)]
+            self._child = [arena(dtype) for _ in range(self.M)]   # RN to the member dtype (bf16: :142)
+            self._t = torch.tensor([float(t) for t in seg_t], dtype=torch.float64).to(self.device)
+            self._plan = None
+        self._recv = {}
+
+    # ---- member access ---------------------------------------------------------------------
+    def local_members(self) -> list[int]:
+        return list(range(self.rank * self.M, (self.rank + 1) * self.M))
+
+    def owner(self, m: int) -> int:
+        return m // self.M
+
+    def _local(self, m):
+        if m not in self._slot:
+            raise EdtError(f"member {m} lives on rank {self.owner(m)}, not {self.rank}")
+        return self._slot[m]
+
+    def base(self, m: int) -> torch.Tensor:
+        return self._base[self._local(m)]
+
+    def trained(self, m: int) -> torch.Tensor:
+        return self._trained[self._local(m)]
+
+    def outer_momentum(self, m: int) -> torch.Tensor | None:
+        return self._mom[self._local(m)]
+
+    def params(self, m: int) -> torch.Tensor:
+        return self._params[self._local(m)]
+
+    def begin_inner(self) -> None:
+        """Start every local member's inner loop from its base (mutation.py trains a copy of
+        GenN; at generation 0 the reference copies Gen0000 to Gen0000_mutated)."""
+        if self.kind == "sgd":
+            for b, t in zip(self._base, self._trained):
+                t.copy_(b)
+
+    def model_path(self, m: int, generation: int | None = None) -> str:
+        g = self.generation if generation is None else generation
+        return f"member{m}/Gen{g:04d}"
+
+    # ---- selection (rank 0, broadcast) -----------------------------------------------------
+    def _sync_host(self, obj):
+        if self.world == 1:
+            return obj
+        box = [obj]
+        dist.broadcast_object_list(box, src=self.group_rank0(), group=self.group)
+        return box[0]
+
+    def group_rank0(self) -> int:
+        return dist.get_global_rank(self.group, 0) if self.group is not None else 0
+
+    def select(self, fitness: list[float], method: str | None = None, scale: float | None = None):
+        """Parent pairs (member indices) for the next generation, chosen on rank 0.
+
+        sgd:   edt_sim.py:233-240: rank_based_selection of P - elitism pairs, then (elite,
+               elite) pairs for the top `elitism` genomes; a population of one pairs with itself.
+        slerp: EDT_RL/edt.py:267-272: roulette_wheel_selection of P pairs with
+               scale = roulette_scale(generation, max_generations) (pass `scale`)."""
+        if len(fitness) != self.P:
+            raise EdtError(f"{len(fitness)} fitness values for {self.P} members")
+        pairs = None
+        if self.rank == 0:
+            genomes = []
+            for m, (g, f) in enumerate(zip(self.genomes, fitness)):
+                g = dict(g)
+                g["fitness"] = f
+                g["model_path"] = self.model_path(m)
+                genomes.append(g)
+            method = method or ("rank" if self.kind == "sgd" else "roulette")
+            if self.P == 1:
+                sel = [(genomes[0], genomes[0])]
+            elif method == "rank":
+                sel = schedule.rank_based_selection(genomes, self.P - self.elitism)
+                ranked = sorted(genomes, key=lambda g: g["fitness"], reverse=True)
+                sel += [(e, e) for e in ranked[:self.elitism]]
+            elif method == "roulette":
+                sel = schedule.roulette_wheel_selection(genomes, self.P, 1.0 if scale is None else scale)
+            elif method == "tournament":
+                sel = schedule.tournament_selection(genomes, self.P)
+            else:
+                raise ValueError(method)
+            pairs = schedule.pair_indices(sel, genomes)
+            self._fitness = list(fitness)
+        pairs = self._sync_host(pairs)
+        return [tuple(p) for p in pairs]
+
+    # ---- crossover -------------------------------------------------------------------------
+    def _donors(self, pairs):
+        """Whose outer momentum child c inherits (EDT_LM/train/crossover.py:183-227): parent 1's
+        when it has one, else parent 2's; none at generation 0; otherwise an error."""
+        out = []
+        for i, j in pairs:
+            if self.has_momentum[i]:
+                out.append(i)
+            elif self.has_momentum[j]:
+                out.append(j)
+            elif self.generation == 0 or self.momentum == 0:
+                out.append(None)
+            else:
+                raise NotImplementedError(f"What, no outer_optim.pt for {self.model_path(i)} or {self.model_path(j)}?")
+        return out
+
+    def _payload(self, m, with_state):
+        s = self._local(m)
+        if self.kind == "slerp":
+            return [self._params[s]]
+        out = [self._base[s], self._trained[s]]
+        if with_state:
+            out.append(self._mom[s])
+        return out
+
+    def _recv_like(self, key, like):
+        buf = self._recv.get(key)
+        if buf is None or buf.dtype != like.dtype or buf.numel() != like.numel():
+            buf = self._recv[key] = torch.empty_like(like)
+        return buf
+
+    def _exchange(self, pairs, donors):
+        """Grouped send/recv of every parent a local child needs; {member: [tensors]}."""
+        owner = [self.owner(m) for m in range(self.P)]
+        have = {m: None for m in self.local_members()}
+        if self.world == 1:
+            return {m: self._payload(m, True) for m in have}
+        plan = schedule.exchange_plan(pairs, owner, owner)
+        mine = plan.get(self.rank, {"send": [], "recv": []})
+
+        def with_state(m, dst):
+            return self.kind == "sgd" and any(donors[c] == m and owner[c] == dst for c in range(self.P))
+
+        p2p = []
+        for m, dst in mine["send"]:
+            for t in self._payload(m, with_state(m, dst)):
+                p2p.append(dist.P2POp(dist.isend, t, dst, self.group))
+        got = {m: self._payload(m, True) for m in have}
+        like = self._payload(self.local_members()[0], self.kind == "sgd")
+        for slot, (m, src) in enumerate(mine["recv"]):
+            n = len(like) if with_state(m, self.rank) else (1 if self.kind == "slerp" else 2)
+            bufs = [self._recv_like((slot, k), like[k]) for k in range(n)]
+            p2p.extend(dist.P2POp(dist.irecv, b, src, self.group) for b in bufs)
+            got[m] = bufs
+        if p2p:
+            for w in dist.batch_isend_irecv(p2p):
+                w.wait()
+        return got
+
+    def crossover(self, pairs) -> None:
+        """Build child c of pairs[c] = (i, j) on member c's rank, for every c, then make the
+        children the population (generation + 1)."""
+        pairs = [tuple(p) for p in pairs]
+        if len(pairs) != self.P:
+            raise EdtError(f"{len(pairs)} pairs for a population of {self.P}")
+        donors = self._donors(pairs) if self.kind == "sgd" else [None] * self.P
+        got = self._exchange(pairs, donors)
+        k = self.kernels
+        for c in self.local_members():
+            i, j = pairs[c]
+            s = self._local(c)
+            if self.kind == "sgd":
+                b1, m1 = got[i][0], got[i][1]
+                b2, m2 = got[j][0], got[j][1]
+                mom = self._child_mom[s]
+                has = donors[c] is not None and self.momentum != 0
+                # (has = False: the first step writes buf = grad.clone() without reading it)
+                # the donor's buffer is read in place (it may feed other children): no copy
+                k.pair_merge(b1, b2, m1, m2, self._child[s], mom, has, self.lr, self.momentum,
+                             self.nesterov, momentum_in=got[donors[c]][2] if has else None)
+            else:
+                if self._plan is None:
+                    self._plan = k.make_slerp_plan(self.layout.offsets, self.device)
+                k.slerp_arena(self._plan, got[i][0], got[j][0], self._child[s], self._t,
+                              self.dot_threshold, self.eps)
+        # every transfer and merge of this generation is enqueued/complete: swap the children in
+        if self.kind == "sgd":
+            self._base, self._child = self._child, self._base
+            if self.momentum:
+                self._mom, self._child_mom = self._child_mom, self._mom
+        else:
+            self._params, self._child = self._child, self._params
+        self._genomes_after(pairs)
+        if self.kind == "sgd" and self.momentum:
+            self.has_momentum = [True] * self.P
+        self.generation += 1
+
+    def _genomes_after(self, pairs):
+        """Child genomes (rank 0, numpy's global RNG, child order; broadcast): EDT-LM
+        {"fitness": 0, "dna", "p1", "p2"} with the parents' own p1/p2 dropped
+        (EDT_LM/train/crossover.py:296-309); EDT-RL {"env": {env_name, reward_dna, agents: []},
+        "p1", "p2"} (EDT_RL/crossover.py:186-201; parents' p1/p2 dropped here too, so the record
+        stays one level deep)."""
+        new = None
+        if self.rank == 0:
+            new = []
+            for c, (i, j) in enumerate(pairs):
+                g1, g2 = dict(self.genomes[i]), dict(self.genomes[j])
+                for g, m in ((g1, i), (g2, j)):
+                    g.pop("p1", None)
+                    g.pop("p2", None)
+                    g["model_path"] = self.model_path(m)
+                    if self._fitness is not None:
+                        g["fitness"] = self._fitness[m]
+                if self.kind == "sgd":
+                    child = {"fitness": 0.0, "model_path": self.model_path(c, self.generation + 1),
+                             "dna": uniform_dna_crossover(g1["dna"], g2["dna"]), "p1": g1, "p2": g2}
+                else:
+                    env = g1["env"]
+                    child = {"model_path": self.model_path(c, self.generation + 1),
+                             "env": {"env_name": env["env_name"],
+                                     "reward_dna": uniform_dna_crossover(env["reward_dna"], g2["env"]["reward_dna"]),
+                                     "agents": []},
+                             "p1": g1, "p2": g2}
+                new.append(child)
+        self.genomes = self._sync_host(new)
+
+    # ---- mutation schedule (host) ----------------------------------------------------------
+    def mutation_flags(self, probability: float = 0.5) -> list[bool]:
+        """Which children mutate their DNA this generation (EDT_LM/edt_sim.py:282-296: shuffle
+        the machines with `random.shuffle`, flag the first round(p * P)); chosen on rank 0."""
+        flags = None
+        if self.rank == 0:
+            order = list(range(self.P))
+            random.shuffle(order)
+            k = max(1, int(round(probability * self.P)))
+            chosen = set(order[:k])
+            flags = [m in chosen for m in range(self.P)]
+        flags = self._sync_host(flags)
+        for g, f in zip(self.genomes, flags):
+            g["dna_mutated"] = f
+        return flags
+
+    def step(self, fitness: list[float], **select_kw):
+        """One generation's data path: select -> exchange -> merge -> swap. Returns the pairs."""
+        pairs = self.select(fitness, **select_kw)
+        self.crossover(pairs)
+        return pairs

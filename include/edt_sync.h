@@ -103,6 +103,15 @@ int edt_pair_merge(const void* b1, const void* b2, const void* m1, const void* m
                    void* theta_out, int gdt, void* momentum, int has_momentum, uint64_t n,
                    double lr, double momentum_coef, int nesterov, void* stream);
 
+/* edt_pair_merge with the inherited momentum read from `momentum_in` (the donor parent's
+ * outer_optim.pt buffer, EDT_LM/train/crossover.py:183-219) and the child's written to
+ * `momentum_out`: the donor stays intact for the other children it feeds, and no copy of it is
+ * made first. momentum_in == momentum_out is edt_pair_merge. */
+int edt_pair_merge_to(const void* b1, const void* b2, const void* m1, const void* m2, int wdt,
+                      void* theta_out, int gdt, const void* momentum_in, void* momentum_out,
+                      int has_momentum, uint64_t n, double lr, double momentum_coef, int nesterov,
+                      void* stream);
+
 /* lerp(t, v0, v1) = (1-t)*v0 + t*v1 as three rounded ops in compute dtype cdt (= the tensors'
  * dtype for torch, F32 for numpy), stored as out_dt.
  * Replaces EDT_LM/train/crossover.py:50-51 / EDT_RL/crossover.py:46-47 when applied per tensor. */

@@ -1,0 +1,99 @@
+"""One EDT generation's data path with the population resident in HBM (population.py,
+SURVEY.md §8(f) row 4), on one GPU: selection -> (no exchange at world 1) -> P child merges ->
+swap. Compare: the reference moves each child through the shared disk (crossover.py loads four
+checkpoints and saves one; profiles/r01_crossover_e2e.json: 0.24 s per 162M child with the
+direct arena reader, 3.7 s through from_pretrained).
+
+  sgd    EDT-LM children (edt_pair_merge_to), bf16 members + bf16 outer momentum, steady state
+         (every member carries momentum). Algorithmic bytes per child and element:
+         4 parents x 2 + child 2 + donor momentum read 2 + child momentum write 2 = 14
+  slerp  EDT-RL / EVOMERGE children (edt_slerp_merge, per-tensor t), bf16 in / bf16 out:
+         2 x 2 in + 2 out = 6 algorithmic (the two-pass form reads the parents twice: 10)
+
+    python scripts/bench_generation.py [--layout gpt2_small] [--population 8] [--iters 5]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import random
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+PEAK_TBPS = 8.0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--layout", default="gpt2_small")
+    ap.add_argument("--population", type=int, default=8)
+    ap.add_argument("--kinds", default="sgd,slerp")
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    from evolutionarydistributedtraining_amd.layouts import LAYOUTS
+    from evolutionarydistributedtraining_amd.merge import merge_plan
+    from evolutionarydistributedtraining_amd.population import ResidentPopulation
+    dev = torch.device("cuda:0")
+    layout = LAYOUTS[a.layout]()
+    n, P = layout.total, a.population
+    out = {"layout": a.layout, "params": n, "population": P, "results": {}}
+    for kind in a.kinds.split(","):
+        random.seed(0)
+        if kind == "sgd":
+            genomes = [{"dna": [m % 4, (m + 1) % 4, (m + 2) % 4]} for m in range(P)]
+            pop = ResidentPopulation(layout, torch.bfloat16, dev, genomes, kind="sgd", elitism=1)
+            arenas = [pop.base(m) for m in range(P)] + [pop.trained(m) for m in range(P)]
+        else:
+            genomes = [{"env": {"env_name": "e", "reward_dna": [m] * 6, "agents": []}} for m in range(P)]
+            t = [t for _, t in merge_plan(layout.names, 24, {"parameters": {"t": [
+                {"filter": "self_attn", "value": [0, .5, .3, .7, 1]}, {"filter": "mlp", "value": [1, .5, .7, .3, 0]},
+                {"value": 0.5}]}})]
+            if len(t) != len(layout):
+                t = [0.5] * len(layout)
+            pop = ResidentPopulation(layout, torch.bfloat16, dev, genomes, kind="slerp", seg_t=t)
+            arenas = [pop.params(m) for m in range(P)]
+        g = torch.Generator(device=dev).manual_seed(1)
+        for x in arenas:
+            x.copy_(torch.randn(n, generator=g, device=dev) * 0.02)
+        fitness = [float(m) for m in range(P)]
+        pop.step(fitness)                      # generation 0 (first-step momentum), warm-up
+        torch.cuda.synchronize()
+        times, host = [], []
+        for _ in range(a.iters):
+            h0 = time.perf_counter()
+            pairs = pop.select(fitness)
+            host.append(time.perf_counter() - h0)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            pop.crossover(pairs)
+            e1.record()
+            torch.cuda.synchronize()
+            times.append(e0.elapsed_time(e1))
+        times.sort()
+        ms = times[len(times) // 2]
+        bpe = 14 if kind == "sgd" else 6
+        moved = 14 if kind == "sgd" else 10
+        algo = bpe * n * P
+        out["results"][kind] = {
+            "generation_ms": round(ms, 3), "per_child_ms": round(ms / P, 4),
+            "algo_bytes": algo, "algo_TBps": round(algo / ms / 1e9, 3),
+            "frac_of_8TBps": round(algo / ms / 1e9 / PEAK_TBPS, 4),
+            "moved_TBps": round(moved * n * P / ms / 1e9, 3),
+            "host_select_ms": round(1e3 * sorted(host)[len(host) // 2], 3),
+        }
+        print(kind, out["results"][kind], flush=True)
+        del pop, arenas
+        torch.cuda.empty_cache()
+    print(json.dumps(out))
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,30 @@
+"""Test-only stand-in for the HIP kernels: the CPU oracle behind the same call surface as
+`evolutionarydistributedtraining_amd.ops` (the product default). Used to exercise the
+multi-rank host logic (gloo, CPU) and as the checker of the GPU runs."""
+
+
+class OracleKernels:
+    def __init__(self, oracle):
+        self.o = oracle
+
+    def make_slerp_plan(self, offsets, device):
+        return list(offsets)
+
+    def slerp_arena(self, plan, v0, v1, out, t, thr, eps):
+        for s in range(len(plan) - 1):
+            a, b = plan[s], plan[s + 1]
+            out[a:b] = self.o.slerp(float(t[s]), v0[a:b], v1[a:b], thr, eps).to(out.dtype)
+
+    def pair_merge(self, b1, b2, m1, m2, out, mom, has, lr, mu, nesterov, momentum_in=None):
+        if momentum_in is not None and mom is not None:
+            mom.copy_(momentum_in)
+        self.o.pair_merge(b1, b2, m1, m2, out, mom, has, lr, mu, nesterov)
+
+    def outer_step(self, theta, workers, mom, has, lr, mu, nesterov):
+        self.o.outer_step(theta, workers, mom, has, lr, mu, nesterov)
+
+    def delta_partial(self, theta, workers, k_total, acc, accumulate=False):
+        self.o.delta_partial(theta, workers, k_total, acc, accumulate)
+
+    def sgd_apply(self, theta, acc, mom, has, lr, mu, nesterov):
+        self.o.sgd_apply(theta, acc, mom, has, lr, mu, nesterov)

@@ -109,22 +109,7 @@ def test_sharded_outer_step_world2(tmp_path, oracle, mode, tdt, wdt):
 # ------------------------------------------------------------------------------------------
 # population crossover across ranks (one member per rank), CPU oracle as the kernels
 
-class _OracleKernels:
-    """Test-only stand-in for the HIP kernels (the product default is ops)."""
-
-    def __init__(self, oracle):
-        self.o = oracle
-
-    def make_slerp_plan(self, offsets, device):
-        return list(offsets)
-
-    def slerp_arena(self, plan, v0, v1, out, t, thr, eps):
-        for s in range(len(plan) - 1):
-            a, b = plan[s], plan[s + 1]
-            out[a:b] = self.o.slerp(float(t[s]), v0[a:b], v1[a:b], thr, eps).to(out.dtype)
-
-    def pair_merge(self, b1, b2, m1, m2, out, mom, has, lr, mu, nesterov):
-        self.o.pair_merge(b1, b2, m1, m2, out, mom, has, lr, mu, nesterov)
+from tests.oracle_kernels import OracleKernels as _OracleKernels  # noqa: E402
 
 
 POP_SHAPES = [(33, 7), (5,), (300,)]

@@ -280,6 +280,17 @@ def test_pair_merge_golden(golden, oracle, dev, ops, idx):
     ops.pair_merge(base_d, None, p["m1"].to(dev), p["m2"].to(dev), out2, mom2, p["has"], p["lr"], p["mu"],
                    p["nesterov"])
     assert torch.equal(bits(out2.cpu()), bits(out))
+    # donor form (edt_pair_merge_to): carried momentum read from a separate buffer, left intact
+    if p["mom"] is not None:
+        donor = pair_inputs(golden, c)["mom"].to(dev)
+        keep = donor.clone()
+        out3 = torch.empty_like(out_d)
+        mom3 = torch.full_like(donor, float("nan"))
+        ops.pair_merge(p["b1"].to(dev), p["b2"].to(dev), p["m1"].to(dev), p["m2"].to(dev), out3, mom3,
+                       p["has"], p["lr"], p["mu"], p["nesterov"], momentum_in=donor)
+        assert torch.equal(bits(out3.cpu()), bits(out))
+        assert torch.equal(bits(mom3.cpu()), bits(mom_d.cpu()))
+        assert torch.equal(bits(donor.cpu()), bits(keep.cpu()))
 
 
 @pytest.mark.parametrize("in_dt,cdt,out_dt", [(torch.float32, torch.float32, torch.float32),

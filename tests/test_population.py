@@ -1,0 +1,236 @@
+"""Rank-resident EDT generations (population.ResidentPopulation).
+
+The check is a plain restatement of the reference's generation flow, driven by the same seeded
+host RNGs: EDT-LM (EDT_LM/edt_sim.py:175-256 -> EDT_LM/train/crossover.py:240-315: rank
+selection + elitism, per child lerp(0.5) of the bases, SGD merge with the first parent's outer
+momentum, uniform DNA crossover) and EDT-RL (EDT_RL/edt.py:264-299 -> EDT_RL/crossover.py:
+173-201: roulette selection, per-key SLERP, reward-DNA crossover), with the CPU oracle doing the
+arithmetic. The resident population must give the same members, momenta and genomes:
+  * CPU, world 1 and gloo world 2 (two members per rank), oracle kernels: bit-exact;
+  * MI355X, HIP kernels: EDT-LM bit-exact; SLERP within the SLERP parity bar.
+The inner loop is synthetic (trained = base + seeded noise) and fitness is seeded, so the
+selections do not depend on the arithmetic.
+"""
+import os
+import random
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+SHAPES = [(33, 7), (5,), (300,), (1,), (64, 9)]
+POP = 4
+GENS = 3
+SEG_T = [0.5, 0.43333, 0.56667, 0.5, 1.0]
+
+
+def _init(m, n, dtype):
+    g = torch.Generator().manual_seed(500 + m)
+    return (torch.randn(n, generator=g) * 0.02).to(dtype)
+
+
+def _noise(gen, m, n):
+    g = torch.Generator().manual_seed(10_000 * gen + m)
+    return torch.randn(n, generator=g) * 1e-3
+
+
+def _fitness(gen):
+    r = random.Random(77 + gen)
+    return [round(r.uniform(0, 10), 3) for _ in range(POP)]
+
+
+def _genomes(kind):
+    if kind == "sgd":
+        return [{"dna": [m, 10 + m, 20 + m]} for m in range(POP)]
+    return [{"env": {"env_name": "arena", "reward_dna": [m, m + 1, m + 2, m + 3, m + 4, m + 5], "agents": []}}
+            for m in range(POP)]
+
+
+def _dtype(kind):
+    return torch.bfloat16 if kind == "sgd" else torch.float32
+
+
+def _scale(gen):
+    from evolutionarydistributedtraining_amd.schedule import roulette_scale
+    return roulette_scale(gen + 1, 10)
+
+
+def run_resident(kind, device, kernels=None):
+    """The resident population over GENS generations; returns this rank's members."""
+    from evolutionarydistributedtraining_amd.params import ParamLayout
+    from evolutionarydistributedtraining_amd.population import ResidentPopulation
+    layout = ParamLayout(SHAPES)
+    n, dt = layout.total, _dtype(kind)
+    random.seed(7)
+    np.random.seed(7)
+    pop = ResidentPopulation(layout, dt, device, _genomes(kind), kind=kind, elitism=1 if kind == "sgd" else 0,
+                             seg_t=SEG_T if kind == "slerp" else None, kernels=kernels)
+    for m in pop.local_members():
+        (pop.base(m) if kind == "sgd" else pop.params(m)).copy_(_init(m, n, dt))
+    for gen in range(GENS):
+        pop.begin_inner()
+        for m in pop.local_members():
+            t = pop.trained(m) if kind == "sgd" else pop.params(m)
+            t.copy_((t.cpu().float() + _noise(gen, m, n)).to(dt))
+        if kind == "sgd":
+            pop.step(_fitness(gen))
+        else:
+            pop.step(_fitness(gen), scale=_scale(gen))
+    out = {}
+    for m in pop.local_members():
+        if kind == "sgd":
+            out[m] = {"base": pop.base(m).cpu(), "mom": pop.outer_momentum(m).cpu()}
+        else:
+            out[m] = {"params": pop.params(m).cpu()}
+    return out, pop.genomes
+
+
+def reference_flow(kind, oracle):
+    """The reference's generation loop restated with the oracle's arithmetic."""
+    from evolutionarydistributedtraining_amd import schedule
+    from evolutionarydistributedtraining_amd.merge import uniform_dna_crossover
+    from evolutionarydistributedtraining_amd.params import ParamLayout
+    layout = ParamLayout(SHAPES)
+    n, dt, offs = layout.total, _dtype(kind), layout.offsets
+    random.seed(7)
+    np.random.seed(7)
+    genomes = _genomes(kind)
+    base = [_init(m, n, dt) for m in range(POP)]
+    mom = [None] * POP                      # outer_optim.pt of each member's GenN dir
+    for gen in range(GENS):
+        if kind == "sgd":
+            trained = [(b.float() + _noise(gen, m, n)).to(dt) for m, b in enumerate(base)]
+        else:
+            base = [(b.float() + _noise(gen, m, n)).to(dt) for m, b in enumerate(base)]
+        fit = _fitness(gen)
+        all_g = []
+        for m, g in enumerate(genomes):
+            g = dict(g)
+            g.update(fitness=fit[m], model_path=f"member{m}/Gen{gen:04d}")
+            all_g.append(g)
+        if kind == "sgd":
+            sel = schedule.rank_based_selection(all_g, POP - 1)
+            sel += [(e, e) for e in sorted(all_g, key=lambda g: g["fitness"], reverse=True)[:1]]
+        else:
+            sel = schedule.roulette_wheel_selection(all_g, POP, _scale(gen))
+        idx = {g["model_path"]: m for m, g in enumerate(all_g)}
+        new_base, new_mom, new_genomes = [], [], []
+        for c, (g1, g2) in enumerate(sel):
+            i, j = idx[g1["model_path"]], idx[g2["model_path"]]
+            p1, p2 = dict(g1), dict(g2)
+            for p in (p1, p2):
+                p.pop("p1", None)
+                p.pop("p2", None)
+            if kind == "sgd":
+                donor = mom[i] if mom[i] is not None else mom[j]
+                if donor is None and gen > 0:
+                    raise NotImplementedError
+                m_out = donor.clone() if donor is not None else torch.zeros(n, dtype=dt)
+                out = torch.empty(n, dtype=dt)
+                oracle.pair_merge(base[i], base[j], trained[i], trained[j], out, m_out, donor is not None,
+                                  0.7, 0.9, True)
+                new_mom.append(m_out)
+                new_genomes.append({"fitness": 0.0, "model_path": f"member{c}/Gen{gen + 1:04d}",
+                                    "dna": uniform_dna_crossover(p1["dna"], p2["dna"]), "p1": p1, "p2": p2})
+            else:
+                out = torch.cat([oracle.slerp(SEG_T[s], base[i][offs[s]:offs[s + 1]], base[j][offs[s]:offs[s + 1]])
+                                 for s in range(len(SHAPES))]).to(dt)
+                env = p1["env"]
+                new_genomes.append({"model_path": f"member{c}/Gen{gen + 1:04d}",
+                                    "env": {"env_name": env["env_name"],
+                                            "reward_dna": uniform_dna_crossover(env["reward_dna"],
+                                                                                p2["env"]["reward_dna"]),
+                                            "agents": []},
+                                    "p1": p1, "p2": p2})
+            new_base.append(out)
+        base, genomes = new_base, new_genomes
+        if kind == "sgd":
+            mom = new_mom
+    return base, mom, genomes
+
+
+def _bits(t):
+    return t.view(torch.int16) if t.dtype == torch.bfloat16 else t.view(torch.int32)
+
+
+@pytest.mark.parametrize("kind", ["sgd", "slerp"])
+def test_resident_world1_matches_reference_flow(oracle, kind):
+    from tests.oracle_kernels import OracleKernels
+    got, genomes = run_resident(kind, "cpu", OracleKernels(oracle))
+    base, mom, want_genomes = reference_flow(kind, oracle)
+    assert genomes == want_genomes
+    for m in range(POP):
+        if kind == "sgd":
+            assert torch.equal(_bits(got[m]["base"]), _bits(base[m])), m
+            assert torch.equal(_bits(got[m]["mom"]), _bits(mom[m])), m
+        else:
+            assert torch.equal(_bits(got[m]["params"]), _bits(base[m])), m
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _world_worker(rank, world, port, kind, outdir):
+    import torch.distributed as dist
+
+    from oracle import oracle
+    from tests.oracle_kernels import OracleKernels
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    got, genomes = run_resident(kind, "cpu", OracleKernels(oracle))
+    torch.save({"members": got, "genomes": genomes}, os.path.join(outdir, f"r{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("kind", ["sgd", "slerp"])
+def test_resident_world2_matches_world1(tmp_path, oracle, kind):
+    world = 2
+    mp.start_processes(_world_worker, args=(world, _free_port(), kind, str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    res = [torch.load(tmp_path / f"r{r}.pt", weights_only=True) for r in range(world)]
+    base, mom, want_genomes = reference_flow(kind, oracle)
+    for r in range(world):
+        assert res[r]["genomes"] == want_genomes
+        assert sorted(res[r]["members"]) == [2 * r, 2 * r + 1]
+        for m, d in res[r]["members"].items():
+            if kind == "sgd":
+                assert torch.equal(_bits(d["base"]), _bits(base[m])), m
+                assert torch.equal(_bits(d["mom"]), _bits(mom[m])), m
+            else:
+                assert torch.equal(_bits(d["params"]), _bits(base[m])), m
+
+
+def test_resident_rejects_missing_momentum(oracle):
+    """Past generation 0 a child whose parents have no outer state is an error, as in
+    EDT_LM/train/crossover.py:226-227."""
+    from evolutionarydistributedtraining_amd.params import ParamLayout
+    from evolutionarydistributedtraining_amd.population import ResidentPopulation
+    from tests.oracle_kernels import OracleKernels
+    pop = ResidentPopulation(ParamLayout(SHAPES), torch.bfloat16, "cpu", _genomes("sgd"),
+                             kernels=OracleKernels(oracle))
+    pop.generation = 1
+    with pytest.raises(NotImplementedError):
+        pop.crossover([(0, 1), (1, 2), (2, 3), (3, 0)])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["sgd", "slerp"])
+def test_resident_gpu_matches_reference_flow(oracle, kind):
+    got, genomes = run_resident(kind, torch.device("cuda:0"))
+    base, mom, want_genomes = reference_flow(kind, oracle)
+    assert genomes == want_genomes
+    for m in range(POP):
+        if kind == "sgd":
+            assert torch.equal(_bits(got[m]["base"]), _bits(base[m])), m
+            assert torch.equal(_bits(got[m]["mom"]), _bits(mom[m])), m
+        else:
+            # SLERP parity bar: the fp64 dot vs the reference's fp32 one
+            diff = (got[m]["params"] - base[m]).abs()
+            assert (diff <= 1e-5 * base[m].abs() + 1e-8).all(), (m, diff.max().item())
