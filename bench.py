@@ -10,7 +10,9 @@ diloco.py's outer optimiser (lr 0.7, momentum 0.9, Nesterov) in steady state (ca
 N>1 (BASELINE configs "8 workers over 8 GPUs"): the population stays K = 8 and
 is spread 8/N workers per GPU (strong scaling); the cross-replica step runs over RCCL (xGMI):
 reduce-scatter of fp32 partial sums + sharded SGD + all-gather of theta, or all-to-all of the raw
-worker shards + the fused kernel per shard (bit-exact), whichever puts fewer bytes on the wire.
+worker shards + the fused kernel per shard (bit-exact) + all-gather of the new theta rounded to
+bf16 straight into the worker arenas (the fp32 master stays sharded), whichever puts fewer bytes
+on the wire (distributed.py).
 `--workers-per-gpu W` instead fixes W workers per GPU (weak scaling, population W*N).
 
     python bench.py [--gpus N --steps K --warmup W]
@@ -51,6 +53,9 @@ def parse():
     p.add_argument("--momentum", type=float, default=0.9)
     p.add_argument("--nesterov", type=int, default=1)
     p.add_argument("--mode", default="auto", choices=["reduce", "exact", "auto"])
+    p.add_argument("--broadcast", default="auto", choices=["theta", "workers", "auto"],
+                   help="N>1: all-gather the fp32 theta replica, or the new theta rounded into the "
+                        "worker arenas (fp32 master kept sharded)")
     p.add_argument("--bucket-elems", type=int, default=1 << 26)
     p.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     p.add_argument("--cpu-sample-elems", type=int, default=1 << 24)
@@ -136,7 +141,7 @@ def main():
     else:
         from evolutionarydistributedtraining_amd.distributed import ShardedOuterSync
         sync = ShardedOuterSync(layout, tdt, wdt, k_local, dev, args.lr, args.momentum, bool(args.nesterov),
-                                mode=args.mode, bucket_elems=args.bucket_elems)
+                                mode=args.mode, bucket_elems=args.bucket_elems, broadcast=args.broadcast)
         synth_population(sync.theta.flat, [w.flat for w in sync.workers], seed=1234 + 7919 * rank)
         # replicas of theta must agree: rank 0's values everywhere
         dist.broadcast(sync.theta_buf, 0)
@@ -212,7 +217,8 @@ def main():
                        "params": P, "tensors": len(layout), "workers_per_gpu": k_local,
                        "population": k_total, "worker_dtype": args.worker_dtype,
                        "theta_dtype": args.theta_dtype,
-                       "parallelism": "single GPU" if not sharded else f"dp{world} {sync.mode} (RCCL)"},
+                       "parallelism": "single GPU" if not sharded else
+                                       f"dp{world} {sync.mode}/{sync.broadcast} (RCCL)"},
         }
         if sharded:
             # the exchange dominates: bytes this rank puts on xGMI per step over the whole step time
@@ -223,7 +229,7 @@ def main():
             roofline = {"bound": "xgmi", "achieved": round(achieved, 1), "peak": peak, "unit": "GB/s",
                         "frac": round(achieved / peak, 4) if peak else None, "traffic": None,
                         "wire_bytes_per_rank": wire,
-                        "schedule": sync.mode}
+                        "schedule": f"{sync.mode}/{sync.broadcast}"}
         if roofline:
             out["roofline"] = roofline
         if not sharded:   # what a plain device-to-device copy reaches on this device, same process

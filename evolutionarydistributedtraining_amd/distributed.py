@@ -13,12 +13,20 @@ overlaps the HBM-bound kernels on the compute stream:
                  reference's sequential order: fp32 <= 2 ulp, bf16 <= 1 bf16 ulp.
   mode="exact"   all-to-all of the raw worker shards to their owners, then the single-GPU fused
                  kernel on each shard (the reference's worker order, bit-exact), all-gather of
-                 theta. Wire bytes: (N-1)/N * P * (K_local * b_w + b_g) — the cheaper schedule
-                 when K_local * b_w <= 4 (one bf16 population member per GPU). mode="auto"
-                 (default) picks the schedule with fewer wire bytes.
+                 theta. Wire bytes: (N-1)/N * P * (K_local * b_w + b_g).
+  broadcast      what the all-gather delivers to every rank. "theta": the full master replica
+                 (theta's dtype). "workers" (exact mode only): the new theta rounded to the worker
+                 dtype, straight into every local worker arena — the start of the next inner
+                 loop, which is all the reference ships to the workers (diloco.py:302-308 saves
+                 the base to every worker dir; the bf16 workers load it rounded). The fp32 master
+                 then stays sharded (each rank updates only the shard it owns; `gather_theta()`
+                 assembles it on demand, e.g. for a checkpoint). Wire bytes:
+                 (N-1)/N * P * (K_local + 1) * b_w.
+  mode="auto" / broadcast="auto" (defaults) pick the combination with the fewest wire bytes:
+  at K = 8 bf16 workers, fp32 theta: N = 2 reduce/theta (8 B/elem), N = 4 and 8 exact/workers
+  (6 and 4 B/elem).
 
-Every rank holds a full replica of theta (what the next inner loop starts from) and 1/N of the
-momentum. Ranks own contiguous shards of every bucket.
+Every rank holds 1/N of the momentum and owns contiguous shards of every bucket.
 """
 from __future__ import annotations
 
@@ -35,17 +43,26 @@ from .params import ParamArena, ParamLayout
 class ShardedOuterSync:
     def __init__(self, layout: ParamLayout, theta_dtype: torch.dtype, worker_dtype: torch.dtype,
                  k_local: int, device, lr: float = 0.7, momentum: float = 0.9, nesterov: bool = True,
-                 mode: str = "auto", bucket_elems: int = 1 << 26, group=None, kernels=None):
-        if mode not in ("reduce", "exact", "auto"):
-            raise ValueError(mode)
+                 mode: str = "auto", bucket_elems: int = 1 << 26, group=None, kernels=None,
+                 broadcast: str = "auto"):
+        if mode not in ("reduce", "exact", "auto") or broadcast not in ("theta", "workers", "auto"):
+            raise ValueError((mode, broadcast))
+        if mode == "reduce" and broadcast == "workers":
+            raise ValueError("the reduce schedule needs the full theta replica (broadcast='theta')")
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        if mode == "auto":   # fewer bytes on the wire: fp32 partial sums vs the raw worker shards
-            wb = torch.empty(0, dtype=worker_dtype).element_size()
-            mode = "exact" if k_local * wb <= 4 else "reduce"
+        wb = torch.empty(0, dtype=worker_dtype).element_size()
+        gb = torch.empty(0, dtype=theta_dtype).element_size()
+        cands = {("reduce", "theta"): 4 + gb, ("exact", "theta"): k_local * wb + gb,
+                 ("exact", "workers"): (k_local + 1) * wb}
+        cands = {key: v for key, v in cands.items()
+                 if mode in ("auto", key[0]) and broadcast in ("auto", key[1])}
+        # fewest wire bytes per element; ties go to the bit-exact schedule
+        mode, broadcast = min(cands, key=lambda key: (cands[key], key[0] != "exact", key[1] != "workers"))
         self.kernels = kernels or _ops
         self.mode = mode
+        self.broadcast = broadcast
         self.layout = layout
         self.lr, self.momentum, self.nesterov = lr, momentum, nesterov
         self.k_local = k_local
@@ -125,9 +142,15 @@ class ShardedOuterSync:
                 k.outer_step(self.theta_buf[s0:s1], shards, mom, self.has_momentum, self.lr,
                              self.momentum, self.nesterov)
                 mom_off += per
-                gathers.append(self._gather(b, e, s0, s1))
+                if self.broadcast == "workers":
+                    gathers.append(self._gather_to_workers(b, e, s0, s1))
+                else:
+                    gathers.append(self._gather(b, e, s0, s1))
         for g in gathers:
             g.wait()
+        if self.broadcast == "workers":
+            for w in self.worker_bufs[1:]:          # every local worker starts from the same theta
+                w.copy_(self.worker_bufs[0])
         if self.momentum:
             self.has_momentum = True
 
@@ -145,6 +168,24 @@ class ShardedOuterSync:
         src = self.theta_buf[s0:s1] if self.inplace else self.theta_buf[s0:s1].clone()
         return dist.all_gather_into_tensor(self.theta_buf[b:e], src, group=self.group, async_op=True)
 
+    def _gather_to_workers(self, b, e, s0, s1):
+        """The new theta shard of bucket [b, e), rounded to the worker dtype (torch copy_: RNE),
+        all-gathered into local worker 0's arena (its bucket was consumed by the all-to-all)."""
+        w0 = self.worker_bufs[0]
+        w0[s0:s1].copy_(self.theta_buf[s0:s1])
+        src = w0[s0:s1] if self.inplace else w0[s0:s1].clone()
+        return dist.all_gather_into_tensor(w0[b:e], src, group=self.group, async_op=True)
+
+    def gather_theta(self) -> torch.Tensor:
+        """The full master theta on every rank (with broadcast="workers" it is kept sharded;
+        this assembles it, e.g. for a checkpoint). Returns the flat theta (length P)."""
+        if self.broadcast == "workers":
+            for b, e in self.buckets:
+                s0, s1 = self._shard(b, e)
+                src = self.theta_buf[s0:s1] if self.inplace else self.theta_buf[s0:s1].clone()
+                dist.all_gather_into_tensor(self.theta_buf[b:e], src, group=self.group)
+        return self.theta.flat
+
     # ---------------------------------------------------------------------------------------
     def bytes_reduced(self) -> int:
         """Metric bytes of one step on this rank: K_local x P x bytes per worker element."""
@@ -154,9 +195,10 @@ class ShardedOuterSync:
         """Bytes this rank sends over xGMI per step (ring/all-to-all lower bound)."""
         f = (self.world - 1) / self.world
         bg = self.theta_buf.element_size()
+        wb = self.worker_bufs[0].element_size()
         if self.mode == "reduce":
             return int(f * self.n_pad * (4 + bg))
-        return int(f * self.n_pad * (self.k_local * self.worker_bufs[0].element_size() + bg))
+        return int(f * self.n_pad * (self.k_local * wb + (wb if self.broadcast == "workers" else bg)))
 
 
 class PopulationCrossover:

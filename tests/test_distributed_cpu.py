@@ -37,7 +37,7 @@ def _population(dtype_theta, dtype_w):
     return layout, theta, steps
 
 
-def _worker(rank, port, mode, tdt, wdt, outdir):
+def _worker(rank, port, mode, tdt, wdt, outdir, broadcast="theta"):
     import torch.distributed as dist
 
     from evolutionarydistributedtraining_amd.distributed import ShardedOuterSync
@@ -46,15 +46,16 @@ def _worker(rank, port, mode, tdt, wdt, outdir):
     dist.init_process_group("gloo", rank=rank, world_size=WORLD)
     layout, theta, steps = _population(tdt, wdt)
     sync = ShardedOuterSync(layout, tdt, wdt, K_LOCAL, "cpu", lr=0.7, momentum=0.9, nesterov=True,
-                            mode=mode, bucket_elems=1024, kernels=oracle)
-    assert len(sync.buckets) > 1
+                            mode=mode, bucket_elems=1024, kernels=oracle, broadcast=broadcast)
+    assert len(sync.buckets) > 1 and (sync.mode, sync.broadcast) == (mode, broadcast)
     sync.theta.flat.copy_(theta)
     for workers in steps:
         for j, arena in enumerate(sync.workers):
             arena.flat.copy_(workers[rank * K_LOCAL + j])
         sync.step()
-    torch.save({"theta": sync.theta.flat.clone(), "mom_shard": sync.mom_shard.clone(),
-                "buckets": sync.buckets}, os.path.join(outdir, f"rank{rank}.pt"))
+    workers = [w.flat.clone() for w in sync.workers]     # before gather_theta: what the step left
+    torch.save({"theta": sync.gather_theta().clone(), "mom_shard": sync.mom_shard.clone(),
+                "buckets": sync.buckets, "workers": workers}, os.path.join(outdir, f"rank{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -75,11 +76,11 @@ def _ulp(x, dt):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("mode", ["exact", "reduce"])
+@pytest.mark.parametrize("mode,broadcast", [("exact", "theta"), ("exact", "workers"), ("reduce", "theta")])
 @pytest.mark.parametrize("tdt,wdt", [(torch.float32, torch.bfloat16), (torch.bfloat16, torch.bfloat16)])
-def test_sharded_outer_step_world2(tmp_path, oracle, mode, tdt, wdt):
+def test_sharded_outer_step_world2(tmp_path, oracle, mode, broadcast, tdt, wdt):
     port = _free_port()
-    mp.start_processes(_worker, args=(port, mode, tdt, wdt, str(tmp_path)), nprocs=WORLD, join=True,
+    mp.start_processes(_worker, args=(port, mode, tdt, wdt, str(tmp_path), broadcast), nprocs=WORLD, join=True,
                        start_method="spawn")
     res = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(WORLD)]
     th_ref, mom_ref = _reference(tdt, wdt)
@@ -100,6 +101,11 @@ def test_sharded_outer_step_world2(tmp_path, oracle, mode, tdt, wdt):
     if mode == "exact":
         assert torch.equal(bits(got), bits(th_ref))
         assert torch.equal(bits(mom), bits(mom_ref))
+        if broadcast == "workers":       # every local worker now starts from round_w(theta)
+            want = th_ref.to(wdt).view(torch.int16)
+            for r in range(WORLD):
+                for w in res[r]["workers"]:
+                    assert torch.equal(w[:n].view(torch.int16), want)
     else:
         scale = 0.7 * (mom_ref.float().abs() * 1.9)
         tol = 2 * _ulp(th_ref, tdt) + 4 * _ulp(scale, tdt)

@@ -311,8 +311,8 @@ def test_dir_outer_sync_two_generations(oracle, dev, tmp_path):
     assert torch.equal(bits(sync.state.momentum.cpu()), bits(mom))
 
 
-@pytest.mark.parametrize("mode", ["reduce", "exact"])
-def test_sharded_outer_step_rccl_world1(oracle, dev, tmp_path, mode):
+@pytest.mark.parametrize("mode,broadcast", [("reduce", "theta"), ("exact", "theta"), ("exact", "workers")])
+def test_sharded_outer_step_rccl_world1(oracle, dev, tmp_path, mode, broadcast):
     """The multi-GPU schedule on the real RCCL backend (one rank: the collectives degenerate, but
     the in-place reduce-scatter / all-gather, async waits and stream ordering are RCCL's)."""
     import torch.distributed as dist
@@ -323,8 +323,8 @@ def test_sharded_outer_step_rccl_world1(oracle, dev, tmp_path, mode):
     try:
         layout = ParamLayout([(1000, 37), (4097,), (3,)])
         sync = ShardedOuterSync(layout, torch.float32, torch.bfloat16, 3, dev, 0.7, 0.9, True, mode=mode,
-                                bucket_elems=8192)
-        assert sync.mode == mode and len(sync.buckets) > 3
+                                bucket_elems=8192, broadcast=broadcast)
+        assert (sync.mode, sync.broadcast) == (mode, broadcast) and len(sync.buckets) > 3
         g = torch.Generator().manual_seed(8)
         theta = torch.randn(layout.total, generator=g) * 0.02
         mom = torch.zeros(layout.total)
@@ -336,7 +336,10 @@ def test_sharded_outer_step_rccl_world1(oracle, dev, tmp_path, mode):
             sync.step()
             oracle.outer_step(theta, ws, mom, step > 0, 0.7, 0.9, True)
         torch.cuda.synchronize()
-        assert torch.equal(bits(sync.theta.flat.cpu()), bits(theta))      # fp32: same order, bit-exact
+        if broadcast == "workers":
+            for a in sync.workers:
+                assert torch.equal(bits(a.flat.cpu()), bits(theta.bfloat16()))
+        assert torch.equal(bits(sync.gather_theta().cpu()), bits(theta))   # fp32: same order, bit-exact
         assert torch.equal(bits(sync.mom_shard[:layout.total].cpu()), bits(mom))
     finally:
         dist.destroy_process_group()
