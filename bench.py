@@ -101,6 +101,28 @@ def cpu_baseline(args, theta_dtype, worker_dtype, k):
                       f"median of {len(times)} reps over {args.cpu_baseline_seconds:.0f}s)"}
 
 
+def stream_ceiling_ms(theta, workers, momentum, iters=10):
+    """Median HIP-event time of edt_probe_stream over the step's own operands (None if the
+    step runs without momentum: the probe always reads and writes a momentum stream)."""
+    if momentum is None:
+        return None
+    from evolutionarydistributedtraining_amd import _lib as L
+    lib = L.lib()
+    arr = L.ptr_array(workers)
+    st = L.stream_ptr(theta.device)
+    call = lambda: L.check(lib.edt_probe_stream(L.ptr(theta), L.dtype_code(theta), arr, L.dtype_code(workers[0]),
+                                                len(workers), L.ptr(momentum), theta.numel(), st), "edt_probe_stream")
+    call()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
+    for a, b in ev:
+        a.record()
+        call()
+        b.record()
+    torch.cuda.synchronize()
+    ts = sorted(a.elapsed_time(b) for a, b in ev)
+    return ts[len(ts) // 2]
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -244,6 +266,13 @@ def main():
             torch.cuda.synchronize()
             roofline["device_copy_GBps"] = round(5 * 2 * src.numel() * 4 / (a.elapsed_time(b) / 1e3) / 1e9, 1)
             del src, dst
+            # the step's own access pattern with a trivial body (edt_probe_stream), same arenas:
+            # the memory-system ceiling of this step on this device, measured after the timed steps
+            probe_ms = stream_ceiling_ms(theta.flat, [w.flat for w in workers], sync.state.momentum)
+            if probe_ms:
+                ceil = algo_bytes / (probe_ms / 1e3) / 1e9
+                roofline["stream_ceiling_GBps"] = round(ceil, 1)
+                roofline["frac_of_stream_ceiling"] = round(roofline["achieved"] / ceil, 4)
         prop = torch.cuda.get_device_properties(dev)
         out["device"] = {"name": prop.name, "arch": getattr(prop, "gcnArchName", ""),
                          "cus": prop.multi_processor_count, "hbm_gib": round(prop.total_memory / 2**30, 1)}

@@ -46,6 +46,7 @@ SIGNATURES = [
     ("edt_slerp_merge", _I, [_P, _P, _I, _P, _I, _P, ctypes.c_int64, _P, _I, _P, _D, _D, _P, _P, _P, _P]),
     ("edt_slerp_merge_list", _I, [ctypes.POINTER(_P), ctypes.POINTER(_P), _I, ctypes.POINTER(_P), _I, _P,
                                   ctypes.c_int64, _P, _I, _P, _D, _D, _P, _P, _P, _P, _U64, _P]),
+    ("edt_probe_stream", _I, [_P, _I, ctypes.POINTER(_P), _I, _I, _P, _U64, _P]),
     ("edt_last_error", ctypes.c_char_p, []),
     ("edt_version", ctypes.c_char_p, []),
     ("edt_outer_step_bytes_per_elem", _I, [_I, _I, _I, _I]),

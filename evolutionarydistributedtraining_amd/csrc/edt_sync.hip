@@ -740,6 +740,42 @@ __global__ __launch_bounds__(kBlock) void slerp_blend_kernel(const void* v0, con
 }
 
 // ---------------------------------------------------------------------------------------
+// Diagnostic: the fused step's access pattern (same operands, loads, stores, cache policy, grid)
+// with a trivial body. Its time is the memory-system ceiling of the step on the device at hand:
+// the fused kernel's time over it says how much of the step is anything but HBM traffic.
+
+template <int GDT, int WDT, int KC, int N>
+__device__ __forceinline__ void probe_elems(const OuterArgs& a, uint64_t i) {
+    float g[N], b[N], acc[N];
+    ld<GDT, N>(a.theta, i, g);
+    ld<GDT, N>(a.mom, i, b);
+#pragma unroll
+    for (int j = 0; j < N; ++j) acc[j] = 0.f;
+    const int K = KC > 0 ? KC : a.K;
+#pragma unroll 8
+    for (int k = 0; k < K; ++k) {
+        float w[N];
+        ld<WDT, N, EDT_NT_LOADS != 0 && WDT == EDT_BF16>(a.wp(k), i, w);
+#pragma unroll
+        for (int j = 0; j < N; ++j) acc[j] += w[j];
+    }
+#pragma unroll
+    for (int j = 0; j < N; ++j) { g[j] += acc[j] * 1e-30f; b[j] += acc[j] * 1e-30f; }
+    st<GDT, N>(a.theta, i, g);
+    st<GDT, N>(a.mom, i, b);
+}
+
+template <int GDT, int WDT, int KC>
+__global__ __launch_bounds__(kBlock, EDT_MIN_WAVES) void probe_kernel(OuterArgs a) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t nv = a.n / kVec;
+    for (uint64_t v = tid; v < nv; v += stride) probe_elems<GDT, WDT, KC, kVec>(a, v * kVec);
+    const uint64_t t = nv * kVec + tid;
+    if (t < a.n) probe_elems<GDT, WDT, KC, 1>(a, t);
+}
+
+// ---------------------------------------------------------------------------------------
 // host-side dispatch helpers
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
@@ -841,6 +877,34 @@ extern "C" {
 
 const char* edt_last_error(void) { return g_err; }
 const char* edt_version(void) { return "edt_sync 0.1.0 gfx950"; }
+
+int edt_probe_stream(void* theta_g, int gdt, const void* const* theta_k, int wdt, int K, void* momentum,
+                     uint64_t n, void* stream) {
+    g_err[0] = 0;
+    if (!valid_pair(gdt, wdt)) return fail(EDT_ERR_ARG, "unsupported dtype pair (gdt/wdt)");
+    OuterArgs a;
+    int rc = fill_outer(a, theta_g, theta_k, K, K, n);
+    if (rc) return rc;
+    if (!momentum) return fail(EDT_ERR_ARG, "momentum is null");
+    a.mom = momentum;
+    bool vec = aligned16(theta_g) && aligned16(momentum);
+    for (int k = 0; k < K; ++k) vec = vec && aligned16(theta_k[k]);
+    if (!vec) return fail(EDT_ERR_ARG, "the probe needs 16-byte aligned operands");
+    if (n == 0) return EDT_OK;
+    const unsigned g = grid_for(n, true);
+    hipStream_t s = (hipStream_t)stream;
+    if (gdt == EDT_F32 && wdt == EDT_BF16) {
+        if (K == 8) probe_kernel<EDT_F32, EDT_BF16, 8><<<g, kBlock, 0, s>>>(a);
+        else probe_kernel<EDT_F32, EDT_BF16, 0><<<g, kBlock, 0, s>>>(a);
+    } else if (gdt == EDT_F32) {
+        if (K == 8) probe_kernel<EDT_F32, EDT_F32, 8><<<g, kBlock, 0, s>>>(a);
+        else probe_kernel<EDT_F32, EDT_F32, 0><<<g, kBlock, 0, s>>>(a);
+    } else {
+        if (K == 8) probe_kernel<EDT_BF16, EDT_BF16, 8><<<g, kBlock, 0, s>>>(a);
+        else probe_kernel<EDT_BF16, EDT_BF16, 0><<<g, kBlock, 0, s>>>(a);
+    }
+    return check_launch("probe_kernel");
+}
 
 int edt_outer_step_bytes_per_elem(int gdt, int wdt, int K, int with_momentum) {
     const int bg = gdt == EDT_BF16 ? 2 : 4, bw = wdt == EDT_BF16 ? 2 : 4;

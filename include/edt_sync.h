@@ -173,6 +173,14 @@ int edt_slerp_merge_list(const void* const* v0_t, const void* const* v1_t, int i
 /* ---- misc ---- */
 const char* edt_last_error(void);
 const char* edt_version(void);
+/* Diagnostic (not a reference surface): edt_outer_step's exact access pattern on the same
+ * operands (theta and momentum read and written, K workers read with the same loads, cache policy
+ * and grid) with a trivial body that perturbs theta and momentum by ~1e-30 relative. Its time is
+ * the memory-system ceiling of the fused step on the device at hand (bench.py reports both).
+ * Operands must be 16-byte aligned. */
+int edt_probe_stream(void* theta_g, int gdt, const void* const* theta_k, int wdt, int K, void* momentum,
+                     uint64_t n, void* stream);
+
 /* bytes of device memory the kernels above may touch per element, for roofline accounting */
 int edt_outer_step_bytes_per_elem(int gdt, int wdt, int K, int with_momentum);
 
