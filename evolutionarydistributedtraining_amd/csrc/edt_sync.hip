@@ -740,6 +740,109 @@ __global__ __launch_bounds__(kBlock) void slerp_blend_kernel(const void* v0, con
 }
 
 // ---------------------------------------------------------------------------------------
+// SLERP for a resident population (EDT_RL/edt.py:286-299 merges every selected pair of one
+// generation): ONE pass over the M <= 8 members per chunk forms every member's squared norm and
+// every pair's dot — the upper triangle of the Gram matrix, M(M+1)/2 fp64 sums per chunk — where
+// per-child stats passes would read each child's two parents. A child's (|vi|^2, |vj|^2, vi.vj)
+// are then read out of it. Every sum is bit-identical to chunk_sums() on (vi, vj): the same
+// per-thread FMA sequence in element order (an FMA's product is exact, so vi*vj == vj*vi), the
+// same wave and block reductions; the coefficients therefore equal edt_slerp_merge's.
+
+constexpr int kGramMaxMembers = 8;
+struct Members {
+    const void* p[kGramMaxMembers];
+};
+
+__host__ __device__ constexpr int tri_index(int a, int b, int M) {   // a <= b < M
+    return a * M - a * (a - 1) / 2 + (b - a);
+}
+
+template <int IDT, int M, int N>
+__device__ __forceinline__ void gram_accumulate(const Members& mem, uint64_t i, double (&g)[M * (M + 1) / 2]) {
+    float x[M][N];
+#pragma unroll
+    for (int m = 0; m < M; ++m) ld<IDT, N>(mem.p[m], i, x[m]);
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+#pragma unroll
+        for (int a = 0; a < M; ++a) {
+            const double da = x[a][j];
+#pragma unroll
+            for (int b = a; b < M; ++b) {
+                const double db = x[b][j];
+                g[tri_index(a, b, M)] = __builtin_fma(da, db, g[tri_index(a, b, M)]);
+            }
+        }
+    }
+}
+
+template <int IDT, int M>
+__global__ __launch_bounds__(kBlock) void slerp_gram_kernel(Members mem, const uint64_t* chunks, int64_t nchunks,
+                                                            double* gram) {
+    constexpr int NT = M * (M + 1) / 2;
+    __shared__ double red[NT][kBlock / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+        const uint64_t start = chunks[3 * c], end = start + chunks[3 * c + 1];
+        double g[NT];
+#pragma unroll
+        for (int q = 0; q < NT; ++q) g[q] = 0.0;
+        const uint64_t a = (start + kVec - 1) / kVec * kVec;
+        const uint64_t b = end / kVec * kVec;
+        if (a < b) {
+            for (uint64_t i = a + (uint64_t)threadIdx.x * kVec; i < b; i += (uint64_t)kBlock * kVec)
+                gram_accumulate<IDT, M, kVec>(mem, i, g);
+        }
+        const uint64_t h_end = a < end ? a : end;
+        const uint64_t t_beg = b > a ? b : h_end;
+        const uint64_t nh = h_end - start, nt = end - t_beg;
+        if ((uint64_t)threadIdx.x < nh + nt) {
+            const uint64_t i = threadIdx.x < nh ? start + threadIdx.x : t_beg + (threadIdx.x - nh);
+            gram_accumulate<IDT, M, 1>(mem, i, g);
+        }
+#pragma unroll
+        for (int q = 0; q < NT; ++q) {
+            const double v = wave_sum(g[q]);
+            if (lane == 0) red[q][wave] = v;
+        }
+        __syncthreads();
+        if (threadIdx.x < NT) {
+            double acc = 0.0;
+#pragma unroll
+            for (int w = 0; w < kBlock / 64; ++w) acc += red[threadIdx.x][w];
+            gram[(uint64_t)c * NT + threadIdx.x] = acc;
+        }
+        __syncthreads();
+    }
+}
+
+// One wave per segment for the pair (i, j): slerp_coef_kernel's fixed-order reduction over the
+// chunks, reading the three Gram columns of the pair.
+__global__ __launch_bounds__(kBlock) void slerp_gram_coef_kernel(const double* gram, int NT, int qi, int qj, int qd,
+                                                                 const int32_t* first, int nseg,
+                                                                 const double* tvals, float thr, float eps,
+                                                                 float* coef, float* dot_out) {
+    const int lane = threadIdx.x & 63;
+    const int seg = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    if (seg >= nseg) return;
+    double s00 = 0.0, s11 = 0.0, s01 = 0.0;
+    for (int c = first[seg] + lane; c < first[seg + 1]; c += 64) {
+        s00 += gram[(uint64_t)c * NT + qi];
+        s11 += gram[(uint64_t)c * NT + qj];
+        s01 += gram[(uint64_t)c * NT + qd];
+    }
+    s00 = wave_sum(s00);
+    s11 = wave_sum(s11);
+    s01 = wave_sum(s01);
+    if (lane != 0) return;
+    float c0, c1, dot;
+    slerp_coefficients(s00, s11, s01, tvals[seg], thr, eps, c0, c1, dot);
+    coef[2 * seg] = c0;
+    coef[2 * seg + 1] = c1;
+    if (dot_out) dot_out[seg] = dot;
+}
+
+// ---------------------------------------------------------------------------------------
 // Diagnostic: the fused step's access pattern (same operands, loads, stores, cache policy, grid)
 // with a trivial body. Its time is the memory-system ceiling of the step on the device at hand:
 // the fused kernel's time over it says how much of the step is anything but HBM traffic.
@@ -1245,6 +1348,69 @@ int edt_slerp_merge(const void* v0, const void* v1, int in_dt, void* out, int ou
     rc = edt_slerp_coef(partial, seg_first_chunk, nseg, t, dot_threshold, eps, coef, dot_out, stream);
     if (rc) return rc;
     return edt_slerp_blend(v0, v1, in_dt, out, out_dt, chunk_desc, nchunks, coef, stream);
+}
+
+uint64_t edt_slerp_population_gram_doubles(int nmembers, int64_t nchunks) {
+    if (nmembers < 1 || nmembers > kGramMaxMembers || nchunks < 0) return 0;
+    return (uint64_t)nchunks * (uint64_t)(nmembers * (nmembers + 1) / 2);
+}
+
+int edt_slerp_population(const void* const* members, int nmembers, int in_dt, const int32_t* pairs, int npairs,
+                         void* const* outs, int out_dt, const uint64_t* chunk_desc, int64_t nchunks,
+                         const int32_t* seg_first_chunk, int nseg, const double* t, double dot_threshold,
+                         double eps, double* gram, float* coef, float* dot_out, void* stream) {
+    g_err[0] = 0;
+    if ((in_dt | out_dt) & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
+    if (nmembers < 1 || nmembers > kGramMaxMembers)
+        return fail(EDT_ERR_ARG, "member count %d out of range [1, %d]", nmembers, kGramMaxMembers);
+    if (npairs < 0 || nseg < 0 || nchunks < 0) return fail(EDT_ERR_ARG, "negative count");
+    if (npairs == 0 || nseg == 0 || nchunks == 0) return EDT_OK;
+    if (!members || !pairs || !outs || !chunk_desc || !seg_first_chunk || !t || !gram || !coef)
+        return fail(EDT_ERR_ARG, "null buffer");
+    Members mem;
+    memset(&mem, 0, sizeof(mem));
+    for (int m = 0; m < nmembers; ++m) {
+        if (!aligned16(members[m]) || !members[m]) return fail(EDT_ERR_ARG, "member %d is null or not 16-byte aligned", m);
+        mem.p[m] = members[m];
+    }
+    for (int q = 0; q < npairs; ++q) {
+        const int i = pairs[2 * q], j = pairs[2 * q + 1];
+        if (i < 0 || j < 0 || i >= nmembers || j >= nmembers) return fail(EDT_ERR_ARG, "pair %d: member out of range", q);
+        if (!outs[q] || !aligned16(outs[q])) return fail(EDT_ERR_ARG, "output %d is null or not 16-byte aligned", q);
+        for (int m = 0; m < nmembers; ++m)
+            if (outs[q] == members[m]) return fail(EDT_ERR_ARG, "output %d aliases member %d", q, m);
+    }
+    hipStream_t s = (hipStream_t)stream;
+    const unsigned g = (unsigned)((uint64_t)nchunks < kMaxBlocks ? (uint64_t)nchunks : kMaxBlocks);
+#define EDT_GRAM(M)                                                                                  \
+    case M:                                                                                          \
+        if (in_dt == EDT_F32) slerp_gram_kernel<EDT_F32, M><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, gram); \
+        else slerp_gram_kernel<EDT_BF16, M><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, gram);              \
+        break;
+    switch (nmembers) {
+        EDT_GRAM(1) EDT_GRAM(2) EDT_GRAM(3) EDT_GRAM(4) EDT_GRAM(5) EDT_GRAM(6) EDT_GRAM(7) EDT_GRAM(8)
+    }
+#undef EDT_GRAM
+    int rc = check_launch("slerp_gram_kernel");
+    if (rc) return rc;
+    const int M = nmembers, NT = M * (M + 1) / 2;
+    const unsigned gc = (unsigned)((nseg + kBlock / 64 - 1) / (kBlock / 64));
+    for (int q = 0; q < npairs; ++q) {
+        const int i = pairs[2 * q], j = pairs[2 * q + 1];
+        const int lo = i < j ? i : j, hi = i < j ? j : i;
+        slerp_gram_coef_kernel<<<gc, kBlock, 0, s>>>(gram, NT, tri_index(i, i, M), tri_index(j, j, M),
+                                                     tri_index(lo, hi, M), seg_first_chunk, nseg, t,
+                                                     (float)dot_threshold, (float)eps, coef + 2 * (size_t)nseg * q,
+                                                     dot_out ? dot_out + (size_t)nseg * q : nullptr);
+        rc = check_launch("slerp_gram_coef_kernel");
+        if (rc) return rc;
+    }
+    for (int q = 0; q < npairs; ++q) {
+        rc = slerp_blend_impl(members[pairs[2 * q]], members[pairs[2 * q + 1]], in_dt, outs[q], out_dt, chunk_desc,
+                              nchunks, coef + 2 * (size_t)nseg * q, nullptr, stream);
+        if (rc) return rc;
+    }
+    return EDT_OK;
 }
 
 int edt_slerp_merge_list(const void* const* v0_t, const void* const* v1_t, int in_dt, void* const* out_t,

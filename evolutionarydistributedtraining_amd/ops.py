@@ -235,3 +235,41 @@ def slerp_list(plan: SlerpPlan, v0s: list[torch.Tensor], v1s: list[torch.Tensor]
                                      L.ptr(plan.seg_first), T, L.ptr(t), float(dot_threshold), float(eps),
                                      L.ptr(plan.partial), L.ptr(plan.coef), L.ptr(plan.dots), L.ptr(ws),
                                      ws.numel() * 8, L.stream_ptr(t.device)), "edt_slerp_merge_list")
+
+
+def slerp_population(plan: SlerpPlan, members: list[torch.Tensor], pairs, outs: list[torch.Tensor],
+                     t: torch.Tensor, dot_threshold: float = 0.9995, eps: float = 1e-8) -> torch.Tensor:
+    """SLERP child q of members[pairs[q][0]], members[pairs[q][1]] into outs[q], for every q
+    (EDT_RL/edt.py:286-299 -> EDT_RL/crossover.py:84-135 per child), with ONE stats pass over
+    the members (their Gram matrix per chunk) instead of a stats pass per child
+    (edt_slerp_population; at most 8 members). Results are bit-identical to slerp_arena per
+    child. Returns the per-child, per-segment fp32 dots ([npairs, nseg])."""
+    lib = L.lib()
+    M, Q = len(members), len(pairs)
+    if not 1 <= M <= 8:
+        raise L.EdtError(f"slerp_population takes 1..8 members, got {M} (use slerp_arena per child)")
+    if plan.relative:
+        raise L.EdtError("slerp_population runs over flat member arenas (a non-relative plan)")
+    if len(outs) != Q:
+        raise L.EdtError("one output per pair")
+    L.require_device(*members, *outs, t)
+    n = plan.seg_offsets[-1]
+    in_dt, out_dt = members[0].dtype, outs[0].dtype if outs else members[0].dtype
+    if any(m.dtype != in_dt or m.numel() != n for m in members) or any(o.dtype != out_dt or o.numel() != n for o in outs):
+        raise L.EdtError("members / outputs must match the plan's layout and share one dtype each")
+    if t.dtype != torch.float64 or t.numel() < plan.nseg:
+        raise L.EdtError("t must be a float64 device tensor with one value per segment")
+    dev = t.device
+    need = int(lib.edt_slerp_population_gram_doubles(M, plan.nchunks))
+    gram = getattr(plan, "_gram", None)
+    if gram is None or gram.numel() < max(1, need):
+        gram = plan._gram = torch.empty(max(1, need), dtype=torch.float64, device=dev)
+    coef = torch.empty((max(1, Q), max(1, plan.nseg), 2), dtype=torch.float32, device=dev)
+    dots = torch.empty((max(1, Q), max(1, plan.nseg)), dtype=torch.float32, device=dev)
+    flat_pairs = (ctypes.c_int32 * max(1, 2 * Q))(*[int(x) for p in pairs for x in p])
+    L.check(lib.edt_slerp_population(L.ptr_array(members), M, L.dtype_code(in_dt), flat_pairs, Q,
+                                     L.ptr_array(outs), L.dtype_code(out_dt), L.ptr(plan.chunks), plan.nchunks,
+                                     L.ptr(plan.seg_first), plan.nseg, L.ptr(t), float(dot_threshold), float(eps),
+                                     L.ptr(gram), L.ptr(coef), L.ptr(dots), L.stream_ptr(dev)),
+            "edt_slerp_population")
+    return dots[:Q, :plan.nseg]

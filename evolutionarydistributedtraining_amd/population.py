@@ -245,24 +245,18 @@ class ResidentPopulation:
             raise EdtError(f"{len(pairs)} pairs for a population of {self.P}")
         donors = self._donors(pairs) if self.kind == "sgd" else [None] * self.P
         got = self._exchange(pairs, donors)
-        k = self.kernels
-        for c in self.local_members():
-            i, j = pairs[c]
-            s = self._local(c)
-            if self.kind == "sgd":
-                b1, m1 = got[i][0], got[i][1]
-                b2, m2 = got[j][0], got[j][1]
-                mom = self._child_mom[s]
+        if self.kind == "slerp":
+            self._slerp_children(pairs, got)
+        else:
+            for c in self.local_members():
+                i, j = pairs[c]
+                s = self._local(c)
                 has = donors[c] is not None and self.momentum != 0
-                # (has = False: the first step writes buf = grad.clone() without reading it)
-                # the donor's buffer is read in place (it may feed other children): no copy
-                k.pair_merge(b1, b2, m1, m2, self._child[s], mom, has, self.lr, self.momentum,
-                             self.nesterov, momentum_in=got[donors[c]][2] if has else None)
-            else:
-                if self._plan is None:
-                    self._plan = k.make_slerp_plan(self.layout.offsets, self.device)
-                k.slerp_arena(self._plan, got[i][0], got[j][0], self._child[s], self._t,
-                              self.dot_threshold, self.eps)
+                # the donor's buffer is read in place (it may feed other children): no copy.
+                # has = False (generation 0): the first step writes buf = grad.clone() unread
+                self.kernels.pair_merge(got[i][0], got[j][0], got[i][1], got[j][1], self._child[s],
+                                        self._child_mom[s], has, self.lr, self.momentum, self.nesterov,
+                                        momentum_in=got[donors[c]][2] if has else None)
         # every transfer and merge of this generation is enqueued/complete: swap the children in
         if self.kind == "sgd":
             self._base, self._child = self._child, self._base
@@ -274,6 +268,27 @@ class ResidentPopulation:
         if self.kind == "sgd" and self.momentum:
             self.has_momentum = [True] * self.P
         self.generation += 1
+
+    def _slerp_children(self, pairs, got):
+        """SLERP every local child. With at most 8 distinct parent arenas on this rank (all the
+        members of a population of <= 8 on one GPU) one Gram pass over them serves every child
+        (ops.slerp_population: each member read once for the stats instead of twice per child);
+        otherwise one edt_slerp_merge per child. Bit-identical either way."""
+        k = self.kernels
+        if self._plan is None:
+            self._plan = k.make_slerp_plan(self.layout.offsets, self.device)
+        local = self.local_members()
+        srcs = sorted({m for c in local for m in pairs[c]})
+        if len(srcs) <= 8 and hasattr(k, "slerp_population"):
+            where = {m: q for q, m in enumerate(srcs)}
+            k.slerp_population(self._plan, [got[m][0] for m in srcs],
+                               [(where[pairs[c][0]], where[pairs[c][1]]) for c in local],
+                               [self._child[self._local(c)] for c in local], self._t, self.dot_threshold, self.eps)
+            return
+        for c in local:
+            i, j = pairs[c]
+            k.slerp_arena(self._plan, got[i][0], got[j][0], self._child[self._local(c)], self._t,
+                          self.dot_threshold, self.eps)
 
     def _genomes_after(self, pairs):
         """Child genomes (rank 0, numpy's global RNG, child order; broadcast): EDT-LM

@@ -170,6 +170,21 @@ int edt_slerp_merge_list(const void* const* v0_t, const void* const* v1_t, int i
                          double dot_threshold, double eps, double* partial, float* coef,
                          float* dot_out, void* workspace, uint64_t workspace_bytes, void* stream);
 
+/* SLERP children of a resident population (EDT_RL/edt.py:286-299: every selected pair of one
+ * generation, EDT_RL/crossover.py:84-135 per child) in 2 + 2*npairs launches: ONE pass over the
+ * nmembers (<= 8) flat member arenas forms every member's squared norm and every pair's dot per
+ * chunk (the Gram upper triangle, `gram`: edt_slerp_population_gram_doubles(nmembers, nchunks)
+ * doubles of device workspace), then per child the coefficients (from pairs[2q], pairs[2q+1] =
+ * member indices, host array) and the blend into outs[q] (host array of device pointers; no
+ * output may alias a member). Each child's sums, coefficients and output are bit-identical to
+ * edt_slerp_merge on (members[i], members[j]); the stats pass reads each member once instead of
+ * two parents per child. coef: [npairs][nseg][2] floats; dot_out (nullable): [npairs][nseg]. */
+uint64_t edt_slerp_population_gram_doubles(int nmembers, int64_t nchunks);
+int edt_slerp_population(const void* const* members, int nmembers, int in_dt, const int32_t* pairs, int npairs,
+                         void* const* outs, int out_dt, const uint64_t* chunk_desc, int64_t nchunks,
+                         const int32_t* seg_first_chunk, int nseg, const double* t, double dot_threshold,
+                         double eps, double* gram, float* coef, float* dot_out, void* stream);
+
 /* ---- misc ---- */
 const char* edt_last_error(void);
 const char* edt_version(void);

@@ -7,8 +7,10 @@ direct arena reader, 3.7 s through from_pretrained).
   sgd    EDT-LM children (edt_pair_merge_to), bf16 members + bf16 outer momentum, steady state
          (every member carries momentum). Algorithmic bytes per child and element:
          4 parents x 2 + child 2 + donor momentum read 2 + child momentum write 2 = 14
-  slerp  EDT-RL / EVOMERGE children (edt_slerp_merge, per-tensor t), bf16 in / bf16 out:
-         2 x 2 in + 2 out = 6 algorithmic (the two-pass form reads the parents twice: 10)
+  slerp  EDT-RL / EVOMERGE children, per-tensor t, bf16 in / bf16 out: 2 x 2 in + 2 out = 6
+         algorithmic per child; moved: one Gram stats pass over the P <= 8 members
+         (edt_slerp_population: 2 B per member) + per child a blend (2 x 2 in + 2 out) = 8 per
+         child (10 with a stats pass per child, edt_slerp_merge)
 
     python scripts/bench_generation.py [--layout gpt2_small] [--population 8] [--iters 5]
 """
@@ -77,7 +79,8 @@ def main():
         times.sort()
         ms = times[len(times) // 2]
         bpe = 14 if kind == "sgd" else 6
-        moved = 14 if kind == "sgd" else 10
+        # slerp: one Gram stats pass over the members (P <= 8: each read once) + per-child blends
+        moved = 14 if kind == "sgd" else (8 if P <= 8 else 10)
         algo = bpe * n * P
         out["results"][kind] = {
             "generation_ms": round(ms, 3), "per_child_ms": round(ms / P, 4),

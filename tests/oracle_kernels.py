@@ -15,6 +15,10 @@ class OracleKernels:
             a, b = plan[s], plan[s + 1]
             out[a:b] = self.o.slerp(float(t[s]), v0[a:b], v1[a:b], thr, eps).to(out.dtype)
 
+    def slerp_population(self, plan, members, pairs, outs, t, thr, eps):
+        for (i, j), out in zip(pairs, outs):
+            self.slerp_arena(plan, members[i], members[j], out, t, thr, eps)
+
     def pair_merge(self, b1, b2, m1, m2, out, mom, has, lr, mu, nesterov, momentum_in=None):
         if momentum_in is not None and mom is not None:
             mom.copy_(momentum_in)

@@ -403,6 +403,35 @@ def test_slerp_list_matches_arena(dev, ops, in_dt, out_dt):
         assert torch.equal(bits(torch.cat([x.cpu() for x in a0])), bits(ref.cpu()))
 
 
+@pytest.mark.parametrize("in_dt,out_dt", [(torch.float32, torch.float32), (torch.bfloat16, torch.bfloat16)])
+@pytest.mark.parametrize("nmem", [1, 2, 3, 5, 8])
+def test_slerp_population_matches_per_child(dev, ops, in_dt, out_dt, nmem):
+    """edt_slerp_population (one Gram pass over the members, then per-child coefficients and
+    blends) is bit-identical to edt_slerp_merge per child: same sums, coefficients and outputs.
+    Ragged segments, a zero segment, a parallel pair (lerp branch), self-pairs."""
+    g = torch.Generator().manual_seed(40 + nmem)
+    sizes = [0, 1, 7, 33, 4096, 70_001, 0, 129, 200_003]
+    offs = [0]
+    for x in sizes:
+        offs.append(offs[-1] + x)
+    base = torch.randn(offs[-1], generator=g) * 0.02
+    mem = [base + torch.randn(offs[-1], generator=g) * 1e-3 * (m + 1) for m in range(nmem)]
+    if nmem > 1:
+        mem[1][offs[4]:offs[5]] = 2 * mem[0][offs[4]:offs[5]]      # parallel -> lerp branch
+    mem[0][offs[7]:offs[8]] = 0                                      # zero tensor
+    mem = [m.to(in_dt).to(dev) for m in mem]
+    pairs = [(i % nmem, (3 * i + 1) % nmem) for i in range(max(nmem, 3))] + [(0, 0)]
+    ts = torch.tensor([0.5, 0.0, 1.0, 0.43333333333333335, 0.5, 0.7, 0.5, 0.2, 0.9], dtype=torch.float64).to(dev)
+    plan = ops.make_slerp_plan(offs, dev, chunk_elems=4096)
+    outs = [torch.full((offs[-1],), float("nan"), dtype=out_dt, device=dev) for _ in pairs]
+    dots = ops.slerp_population(plan, mem, pairs, outs, ts)
+    for q, (i, j) in enumerate(pairs):
+        want = torch.empty(offs[-1], dtype=out_dt, device=dev)
+        ops.slerp_arena(plan, mem[i], mem[j], want, ts)
+        assert torch.equal(bits(outs[q].cpu()), bits(want.cpu())), (q, i, j)
+        assert torch.equal(dots[q].cpu(), plan.dots.cpu()), (q, i, j)
+
+
 def test_errors_are_raised(dev, ops):
     from evolutionarydistributedtraining_amd import EdtError
     th = torch.zeros(16, device=dev)
