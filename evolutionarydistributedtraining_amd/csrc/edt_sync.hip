@@ -42,6 +42,19 @@ namespace {
 #ifndef EDT_NT_LERP             // non-temporal loads of lerp's two (read-once) inputs
 #define EDT_NT_LERP 0
 #endif
+// SLERP of two Qwen2.5-7B bodies (bf16, profiles/r01_slerp_variants.json, two boxes): non-temporal
+// parent loads + one workgroup per segment for the chunk-sum reduction + 64 Ki-element chunks
+// 11.23 / 11.41 ms, against 12.14 / 12.27 ms for default loads, one wave per segment and 16 Ki
+// chunks. The population form (edt_slerp_population) keeps default-policy loads (2 % faster).
+#ifndef EDT_NT_SLERP            // non-temporal loads of the SLERP parents (stats and blend passes)
+#define EDT_NT_SLERP 1
+#endif
+#ifndef EDT_SLERP_BPC           // workgroups per CU for the chunk-looping SLERP passes
+#define EDT_SLERP_BPC 256
+#endif
+#ifndef EDT_SLERP_COEF_BLOCK    // 1: one workgroup per segment for the chunk-sum reduction (else one wave)
+#define EDT_SLERP_COEF_BLOCK 1
+#endif
 #ifndef EDT_MIN_WAVES           // __launch_bounds__ minimum waves per SIMD for the stream kernels
 #define EDT_MIN_WAVES 1
 #endif
@@ -50,6 +63,11 @@ constexpr int kBlock = 256;                         // 4 waves
 constexpr int kVec = 8;                             // elements per thread per iteration
 // grid cap for the grid-stride loops: 256 CUs x workgroups per CU (0 = one pass, no cap)
 constexpr uint64_t kMaxBlocks = EDT_BLOCKS_PER_CU > 0 ? 256ull * EDT_BLOCKS_PER_CU : (1ull << 31) - 1;
+
+constexpr uint64_t kSlerpMaxBlocks = 256ull * EDT_SLERP_BPC;
+inline unsigned slerp_grid(int64_t nchunks) {
+    return (unsigned)((uint64_t)nchunks < kSlerpMaxBlocks ? (uint64_t)nchunks : kSlerpMaxBlocks);
+}
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -598,8 +616,8 @@ __device__ __forceinline__ void chunk_sums(const void* v0, const void* v1, uint6
     if (a < b) {
         for (uint64_t i = a + (uint64_t)threadIdx.x * kVec; i < b; i += (uint64_t)kBlock * kVec) {
             float x[kVec], y[kVec];
-            ld<IDT, kVec>(v0, i, x);
-            ld<IDT, kVec>(v1, i, y);
+            ld<IDT, kVec, EDT_NT_SLERP != 0 && IDT == EDT_BF16>(v0, i, x);
+            ld<IDT, kVec, EDT_NT_SLERP != 0 && IDT == EDT_BF16>(v1, i, y);
 #pragma unroll
             for (int j = 0; j < kVec; ++j) {
                 const double dx = x[j], dy = y[j];
@@ -685,32 +703,67 @@ __global__ __launch_bounds__(kBlock) void slerp_stats_kernel(const void* v0, con
     }
 }
 
-// One wave per segment: fixed-order reduction of the chunk sums, then the coefficients.
+// Fixed-order reduction of a segment's chunk sums: column q of rows [c0, c1) of a row-major table
+// with `stride` doubles per row, for the three columns (q0, q1, q2). EDT_SLERP_COEF_BLOCK = 0: one
+// wave per segment (lane-strided, then a wave sum); 1: one workgroup per segment (thread-strided,
+// wave sums, then the waves in order). Every coefficient kernel uses this one order.
+constexpr int kCoefThreads = EDT_SLERP_COEF_BLOCK ? kBlock : 64;
+
+__device__ __forceinline__ bool segment_sums(const double* tab, int stride, int q0, int q1, int q2, int c0,
+                                             int c1, double (&out)[3]) {
+    const int tid = EDT_SLERP_COEF_BLOCK ? (int)threadIdx.x : (int)(threadIdx.x & 63);
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+    for (int c = c0 + tid; c < c1; c += kCoefThreads) {
+        s0 += tab[(uint64_t)c * stride + q0];
+        s1 += tab[(uint64_t)c * stride + q1];
+        s2 += tab[(uint64_t)c * stride + q2];
+    }
+    s0 = wave_sum(s0);
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    if constexpr (EDT_SLERP_COEF_BLOCK) {
+        __shared__ double red[3][kBlock / 64];
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        if (lane == 0) { red[0][wave] = s0; red[1][wave] = s1; red[2][wave] = s2; }
+        __syncthreads();
+        if (threadIdx.x != 0) return false;
+        s0 = s1 = s2 = 0.0;
+#pragma unroll
+        for (int w = 0; w < kBlock / 64; ++w) { s0 += red[0][w]; s1 += red[1][w]; s2 += red[2][w]; }
+    } else {
+        if ((threadIdx.x & 63) != 0) return false;
+    }
+    out[0] = s0;
+    out[1] = s1;
+    out[2] = s2;
+    return true;
+}
+
+__device__ __forceinline__ int coef_segment() {
+    return EDT_SLERP_COEF_BLOCK ? (int)blockIdx.x : (int)(blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
+}
+
+inline unsigned coef_grid(int nseg) {
+    return EDT_SLERP_COEF_BLOCK ? (unsigned)nseg : (unsigned)((nseg + kBlock / 64 - 1) / (kBlock / 64));
+}
+
+// Per segment: the reduction above, then the coefficients.
 __global__ __launch_bounds__(kBlock) void slerp_coef_kernel(const double* partial, const int32_t* first,
                                                             int nseg, const double* tvals,
                                                             float thr, float eps, float* coef,
                                                             float* dot_out) {
-    const int lane = threadIdx.x & 63;
-    const int seg = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const int seg = coef_segment();
     if (seg >= nseg) return;
-    double s00 = 0.0, s11 = 0.0, s01 = 0.0;
-    for (int c = first[seg] + lane; c < first[seg + 1]; c += 64) {
-        s00 += partial[3 * c];
-        s11 += partial[3 * c + 1];
-        s01 += partial[3 * c + 2];
-    }
-    s00 = wave_sum(s00);
-    s11 = wave_sum(s11);
-    s01 = wave_sum(s01);
-    if (lane != 0) return;
+    double sums[3];
+    if (!segment_sums(partial, 3, 0, 1, 2, first[seg], first[seg + 1], sums)) return;
     float c0, c1, dot;
-    slerp_coefficients(s00, s11, s01, tvals[seg], thr, eps, c0, c1, dot);
+    slerp_coefficients(sums[0], sums[1], sums[2], tvals[seg], thr, eps, c0, c1, dot);
     coef[2 * seg] = c0;
     coef[2 * seg + 1] = c1;
     if (dot_out) dot_out[seg] = dot;
 }
 
-template <int IDT, int ODT>
+template <int IDT, int ODT, bool NT = (EDT_NT_SLERP != 0 && IDT == EDT_BF16)>
 __global__ __launch_bounds__(kBlock) void slerp_blend_kernel(const void* v0, const void* v1, void* out,
                                                              const uint64_t* chunks, int64_t nchunks,
                                                              const float* coef, const uint64_t* seg_ptrs) {
@@ -727,7 +780,7 @@ __global__ __launch_bounds__(kBlock) void slerp_blend_kernel(const void* v0, con
         const uint64_t b = end / kVec * kVec;
         if (a < b) {
             for (uint64_t i = a + (uint64_t)threadIdx.x * kVec; i < b; i += (uint64_t)kBlock * kVec)
-                lerp_elems<IDT, ODT, EDT_F32, kVec>(v0, v1, out, i, c0, c1);
+                lerp_elems<IDT, ODT, EDT_F32, kVec, NT>(v0, v1, out, i, c0, c1);
         }
         const uint64_t h_end = a < end ? a : end;
         const uint64_t t_beg = b > a ? b : h_end;
@@ -761,7 +814,7 @@ template <int IDT, int M, int N>
 __device__ __forceinline__ void gram_accumulate(const Members& mem, uint64_t i, double (&g)[M * (M + 1) / 2]) {
     float x[M][N];
 #pragma unroll
-    for (int m = 0; m < M; ++m) ld<IDT, N>(mem.p[m], i, x[m]);
+    for (int m = 0; m < M; ++m) ld<IDT, N>(mem.p[m], i, x[m]);   // default policy: measured faster here
 #pragma unroll
     for (int j = 0; j < N; ++j) {
 #pragma unroll
@@ -816,27 +869,18 @@ __global__ __launch_bounds__(kBlock) void slerp_gram_kernel(Members mem, const u
     }
 }
 
-// One wave per segment for the pair (i, j): slerp_coef_kernel's fixed-order reduction over the
-// chunks, reading the three Gram columns of the pair.
+// Per segment for the pair (i, j): slerp_coef_kernel's reduction over the chunks, reading the
+// three Gram columns of the pair.
 __global__ __launch_bounds__(kBlock) void slerp_gram_coef_kernel(const double* gram, int NT, int qi, int qj, int qd,
                                                                  const int32_t* first, int nseg,
                                                                  const double* tvals, float thr, float eps,
                                                                  float* coef, float* dot_out) {
-    const int lane = threadIdx.x & 63;
-    const int seg = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const int seg = coef_segment();
     if (seg >= nseg) return;
-    double s00 = 0.0, s11 = 0.0, s01 = 0.0;
-    for (int c = first[seg] + lane; c < first[seg + 1]; c += 64) {
-        s00 += gram[(uint64_t)c * NT + qi];
-        s11 += gram[(uint64_t)c * NT + qj];
-        s01 += gram[(uint64_t)c * NT + qd];
-    }
-    s00 = wave_sum(s00);
-    s11 = wave_sum(s11);
-    s01 = wave_sum(s01);
-    if (lane != 0) return;
+    double sums[3];
+    if (!segment_sums(gram, NT, qi, qj, qd, first[seg], first[seg + 1], sums)) return;
     float c0, c1, dot;
-    slerp_coefficients(s00, s11, s01, tvals[seg], thr, eps, c0, c1, dot);
+    slerp_coefficients(sums[0], sums[1], sums[2], tvals[seg], thr, eps, c0, c1, dot);
     coef[2 * seg] = c0;
     coef[2 * seg + 1] = c1;
     if (dot_out) dot_out[seg] = dot;
@@ -1280,7 +1324,7 @@ int slerp_stats_impl(const void* v0, const void* v1, int in_dt, const uint64_t* 
     if (in_dt & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
     if (nchunks == 0) return EDT_OK;
     if (!chunk_desc || !partial) return fail(EDT_ERR_ARG, "null buffer");
-    const unsigned g = (unsigned)((uint64_t)nchunks < kMaxBlocks ? (uint64_t)nchunks : kMaxBlocks);
+    const unsigned g = slerp_grid(nchunks);
     hipStream_t s = (hipStream_t)stream;
     if (in_dt == EDT_F32) slerp_stats_kernel<EDT_F32><<<g, kBlock, 0, s>>>(v0, v1, chunk_desc, nchunks, partial, seg_ptrs);
     else slerp_stats_kernel<EDT_BF16><<<g, kBlock, 0, s>>>(v0, v1, chunk_desc, nchunks, partial, seg_ptrs);
@@ -1288,20 +1332,24 @@ int slerp_stats_impl(const void* v0, const void* v1, int in_dt, const uint64_t* 
 }
 
 int slerp_blend_impl(const void* v0, const void* v1, int in_dt, void* out, int out_dt, const uint64_t* chunk_desc,
-                     int64_t nchunks, const float* coef, const uint64_t* seg_ptrs, void* stream) {
+                     int64_t nchunks, const float* coef, const uint64_t* seg_ptrs, void* stream, bool nt = true) {
     if ((in_dt | out_dt) & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
     if (nchunks == 0) return EDT_OK;
     if (!chunk_desc || !coef) return fail(EDT_ERR_ARG, "null buffer");
-    const unsigned g = (unsigned)((uint64_t)nchunks < kMaxBlocks ? (uint64_t)nchunks : kMaxBlocks);
+    const unsigned g = slerp_grid(nchunks);
     hipStream_t s = (hipStream_t)stream;
     if (in_dt == EDT_F32 && out_dt == EDT_F32)
         slerp_blend_kernel<EDT_F32, EDT_F32><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, seg_ptrs);
     else if (in_dt == EDT_F32)
         slerp_blend_kernel<EDT_F32, EDT_BF16><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, seg_ptrs);
-    else if (out_dt == EDT_F32)
+    else if (out_dt == EDT_F32 && nt)
         slerp_blend_kernel<EDT_BF16, EDT_F32><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, seg_ptrs);
-    else
+    else if (out_dt == EDT_F32)
+        slerp_blend_kernel<EDT_BF16, EDT_F32, false><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, seg_ptrs);
+    else if (nt)
         slerp_blend_kernel<EDT_BF16, EDT_BF16><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, seg_ptrs);
+    else
+        slerp_blend_kernel<EDT_BF16, EDT_BF16, false><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, seg_ptrs);
     return check_launch("slerp_blend_kernel");
 }
 
@@ -1323,8 +1371,7 @@ int edt_slerp_coef(const double* partial, const int32_t* seg_first_chunk, int ns
     g_err[0] = 0;
     if (nseg == 0) return EDT_OK;
     if (!partial || !seg_first_chunk || !t || !coef) return fail(EDT_ERR_ARG, "null buffer");
-    const int per = kBlock / 64;
-    const unsigned g = (unsigned)((nseg + per - 1) / per);
+    const unsigned g = coef_grid(nseg);
     slerp_coef_kernel<<<g, kBlock, 0, (hipStream_t)stream>>>(partial, seg_first_chunk, nseg, t,
                                                             (float)dot_threshold, (float)eps, coef, dot_out);
     return check_launch("slerp_coef_kernel");
@@ -1381,7 +1428,7 @@ int edt_slerp_population(const void* const* members, int nmembers, int in_dt, co
             if (outs[q] == members[m]) return fail(EDT_ERR_ARG, "output %d aliases member %d", q, m);
     }
     hipStream_t s = (hipStream_t)stream;
-    const unsigned g = (unsigned)((uint64_t)nchunks < kMaxBlocks ? (uint64_t)nchunks : kMaxBlocks);
+    const unsigned g = slerp_grid(nchunks);
 #define EDT_GRAM(M)                                                                                  \
     case M:                                                                                          \
         if (in_dt == EDT_F32) slerp_gram_kernel<EDT_F32, M><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, gram); \
@@ -1394,7 +1441,7 @@ int edt_slerp_population(const void* const* members, int nmembers, int in_dt, co
     int rc = check_launch("slerp_gram_kernel");
     if (rc) return rc;
     const int M = nmembers, NT = M * (M + 1) / 2;
-    const unsigned gc = (unsigned)((nseg + kBlock / 64 - 1) / (kBlock / 64));
+    const unsigned gc = coef_grid(nseg);
     for (int q = 0; q < npairs; ++q) {
         const int i = pairs[2 * q], j = pairs[2 * q + 1];
         const int lo = i < j ? i : j, hi = i < j ? j : i;
@@ -1406,8 +1453,9 @@ int edt_slerp_population(const void* const* members, int nmembers, int in_dt, co
         if (rc) return rc;
     }
     for (int q = 0; q < npairs; ++q) {
+        // default-policy loads: each member feeds ~2 children (measured: nt 2 % slower here)
         rc = slerp_blend_impl(members[pairs[2 * q]], members[pairs[2 * q + 1]], in_dt, outs[q], out_dt, chunk_desc,
-                              nchunks, coef + 2 * (size_t)nseg * q, nullptr, stream);
+                              nchunks, coef + 2 * (size_t)nseg * q, nullptr, stream, false);
         if (rc) return rc;
     }
     return EDT_OK;

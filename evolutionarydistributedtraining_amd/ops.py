@@ -165,7 +165,7 @@ class SlerpPlan:
 
 
 def make_slerp_plan(seg_offsets: list[int], device: torch.device,
-                    chunk_elems: int = 1 << 14, relative: bool = False) -> SlerpPlan:
+                    chunk_elems: int = 1 << 16, relative: bool = False) -> SlerpPlan:
     """relative=True: chunk starts are offsets inside their segment, for `slerp_list` over
     separate tensors (one segment per tensor)."""
     lib = L.load_library()

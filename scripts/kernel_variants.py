@@ -38,7 +38,14 @@ VARIANTS = {
 }
 
 
-SLERP_VARIANTS = {"s_default": []}
+SLERP_VARIANTS = {"s_default": [],
+                  # explicit flags, independent of the shipped defaults
+                  "s_plain": ["-DEDT_NT_SLERP=0", "-DEDT_SLERP_COEF_BLOCK=0"],
+                  "s_nt": ["-DEDT_NT_SLERP=1", "-DEDT_SLERP_COEF_BLOCK=0"],
+                  "s_coefblk": ["-DEDT_NT_SLERP=0", "-DEDT_SLERP_COEF_BLOCK=1"],
+                  "s_nt_coefblk": ["-DEDT_NT_SLERP=1", "-DEDT_SLERP_COEF_BLOCK=1"],
+                  "s_bpc32_nt": ["-DEDT_SLERP_BPC=32", "-DEDT_NT_SLERP=1"],
+                  "s_bpc8_nt": ["-DEDT_SLERP_BPC=8", "-DEDT_NT_SLERP=1"]}
 VARIANTS.update({"lerp_nt": ["-DEDT_NT_LERP=1"], "nt0": ["-DEDT_NT_LOADS=0"],
                  "bpc32_nt0": ["-DEDT_BLOCKS_PER_CU=32", "-DEDT_NT_LOADS=0"]})
 
@@ -163,7 +170,7 @@ def run_slerp(names, rounds, layout_name):
         v1[s0:e] = (x + torch.randn(e - s0, device=dev) * 1e-3).to(bf)
         del x
     out = torch.empty(P, dtype=bf, device=dev)
-    plan = ops.make_slerp_plan(lay.offsets, dev)
+    plans = {ce: ops.make_slerp_plan(lay.offsets, dev, chunk_elems=ce) for ce in (1 << 14, 1 << 16)}
     t = torch.full((len(lay),), 0.5, dtype=torch.float64, device=dev)
     stream = L.stream_ptr(dev)
     libs = {}
@@ -177,13 +184,15 @@ def run_slerp(names, rounds, layout_name):
     cases = {}
     for n in names:
         lib = libs[n]
-
-        def three(lib=lib):
-            assert lib.edt_slerp_stats(P_(v0), P_(v1), 1, P_(plan.chunks), plan.nchunks, P_(plan.partial), stream) == 0
-            assert lib.edt_slerp_coef(P_(plan.partial), P_(plan.seg_first), plan.nseg, P_(t), 0.9995, 1e-8,
-                                      P_(plan.coef), P_(plan.dots), stream) == 0
-            return lib.edt_slerp_blend(P_(v0), P_(v1), 1, P_(out), 1, P_(plan.chunks), plan.nchunks, P_(plan.coef), stream)
-        cases[f"{n}/threepass"] = three
+        for ce, plan in plans.items():
+            def three(lib=lib, plan=plan):
+                assert lib.edt_slerp_stats(P_(v0), P_(v1), 1, P_(plan.chunks), plan.nchunks, P_(plan.partial),
+                                           stream) == 0
+                assert lib.edt_slerp_coef(P_(plan.partial), P_(plan.seg_first), plan.nseg, P_(t), 0.9995, 1e-8,
+                                          P_(plan.coef), P_(plan.dots), stream) == 0
+                return lib.edt_slerp_blend(P_(v0), P_(v1), 1, P_(out), 1, P_(plan.chunks), plan.nchunks,
+                                           P_(plan.coef), stream)
+            cases[f"{n}/chunk{ce >> 10}k"] = three
     times = {k: [] for k in cases}
     for k, f in cases.items():
         assert f() == 0
@@ -199,6 +208,55 @@ def run_slerp(names, rounds, layout_name):
     res = {k: {"median_ms": round(statistics.median(v), 3), "algo_TBps": round(6 * P / statistics.median(v) / 1e9, 3)}
            for k, v in times.items()}
     print(json.dumps({"layout": layout_name, "P": P, "op": "slerp", "variants": res}, indent=1))
+
+
+def run_slerp_pop(names, rounds, layout_name="gpt_1p3b", P_members=8):
+    """One resident SLERP generation (edt_slerp_population: Gram pass + per-child blends) over
+    8 bf16 members of the layout, per variant library."""
+    import torch
+    from evolutionarydistributedtraining_amd import _lib as L
+    from evolutionarydistributedtraining_amd import ops
+    from evolutionarydistributedtraining_amd.layouts import LAYOUTS
+    dev = torch.device("cuda:0")
+    lay = LAYOUTS[layout_name]()
+    P = lay.total
+    g = torch.Generator(device=dev).manual_seed(2)
+    mem = [(torch.randn(P, device=dev, generator=g) * 0.02).bfloat16() for _ in range(P_members)]
+    outs = [torch.empty(P, dtype=torch.bfloat16, device=dev) for _ in range(P_members)]
+    pairs = [(i, (i + 3) % P_members) for i in range(P_members)]
+    t = torch.full((len(lay),), 0.5, dtype=torch.float64, device=dev)
+    stream = L.stream_ptr(dev)
+    plans = {ce: ops.make_slerp_plan(lay.offsets, dev, chunk_elems=ce) for ce in (1 << 14, 1 << 16)}
+    grams = {ce: torch.empty(pl.nchunks * 36, dtype=torch.float64, device=dev) for ce, pl in plans.items()}
+    coef = torch.empty(P_members * len(lay) * 2, dtype=torch.float32, device=dev)
+    flat = (ctypes.c_int32 * (2 * P_members))(*[x for p in pairs for x in p])
+    am, ao = L.ptr_array(mem), L.ptr_array(outs)
+    cases = {}
+    for n in names:
+        lib = ctypes.CDLL(os.path.join(VDIR, f"{n}.so"))
+        for name, res, args in L.SIGNATURES:
+            f = getattr(lib, name)
+            f.restype, f.argtypes = res, args
+        for ce, pl in plans.items():
+            cases[f"{n}/chunk{ce >> 10}k"] = (lambda lib=lib, pl=pl, gr=grams[ce]: lib.edt_slerp_population(
+                am, P_members, 1, flat, P_members, ao, 1, L.ptr(pl.chunks), pl.nchunks, L.ptr(pl.seg_first),
+                pl.nseg, L.ptr(t), 0.9995, 1e-8, L.ptr(gr), L.ptr(coef), None, stream))
+    times = {k: [] for k in cases}
+    for f in cases.values():
+        assert f() == 0
+    torch.cuda.synchronize()
+    for _ in range(rounds):
+        for k, f in cases.items():
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            f()
+            b.record()
+            torch.cuda.synchronize()
+            times[k].append(a.elapsed_time(b))
+    res = {k: {"median_ms": round(statistics.median(v), 3),
+               "moved_TBps": round(8 * P * P_members / statistics.median(v) / 1e9, 3)} for k, v in times.items()}
+    print(json.dumps({"layout": layout_name, "P": P, "members": P_members, "op": "slerp_pop", "variants": res},
+                     indent=1))
 
 
 def build(names):
@@ -265,7 +323,7 @@ if __name__ == "__main__":
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--layout", default="gpt_1p3b")
     ap.add_argument("--k", type=int, default=8)
-    ap.add_argument("--op", default="outer", choices=["outer", "slerp", "stream", "list"])
+    ap.add_argument("--op", default="outer", choices=["outer", "slerp", "slerp_pop", "stream", "list"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:
@@ -274,6 +332,8 @@ if __name__ == "__main__":
         run_stream_ops(names, a.rounds, a.iters)
     elif a.op == "list":
         run_list(names, a.rounds, a.iters)
+    elif a.op == "slerp_pop":
+        run_slerp_pop(names, a.rounds)
     elif a.op == "slerp":
         run_slerp(names, a.rounds, a.layout if a.layout != "gpt_1p3b" else "qwen2p5_7b_body")
     else:
