@@ -14,6 +14,7 @@ from __future__ import annotations
 import json
 import os
 import struct
+import threading
 
 import torch
 
@@ -46,10 +47,14 @@ def checkpoint_files(model_dir: str) -> dict[str, str]:
 
 
 class _Staging:
-    """Two pinned host buffers used round-robin, each guarded by the event of its last copy."""
+    """Two pinned host buffers used round-robin, each guarded by the event of its last copy,
+    and the copy stream their host->device copies run on. Pooled (pinning is slow): a reader
+    takes one from the pool and returns it; the events keep a reused buffer from being
+    overwritten before its last copy has drained."""
 
     def __init__(self, nbytes: int, device):
         pin = device.type == "cuda"
+        self.nbytes, self.device = nbytes, device
         self.bufs = [torch.empty(nbytes, dtype=torch.uint8, pin_memory=pin) for _ in range(2)]
         self.events = [None, None]
         self.i = 0
@@ -69,11 +74,31 @@ class _Staging:
             self.events[i] = ev
 
 
+_stage_pool: list[_Staging] = []
+_stage_lock = threading.Lock()
+
+
+def _acquire_stage(nbytes: int, device) -> _Staging:
+    with _stage_lock:
+        for k, st in enumerate(_stage_pool):
+            if st.nbytes == nbytes and st.device == device:
+                return _stage_pool.pop(k)
+    return _Staging(nbytes, device)
+
+
+def _release_stage(st: _Staging) -> None:
+    with _stage_lock:
+        if len(_stage_pool) < 32:
+            _stage_pool.append(st)
+
+
 def read_into_arena(model_dir: str, layout: ParamLayout, flat: torch.Tensor,
-                    names: list[str] | None = None, staging_bytes: int = 64 << 20) -> torch.Tensor:
+                    names: list[str] | None = None, staging_bytes: int = 64 << 20,
+                    caller_stream=None) -> torch.Tensor:
     """Fill `flat` (layout order) from a HF checkpoint directory. A checkpoint tensor whose dtype
     differs from the arena's is converted on the device after the copy (torch copy_ rounding,
-    as load_state_dict does)."""
+    as load_state_dict does). The copies are ordered after, and the arena is ready on, the
+    caller's current stream (or `caller_stream`)."""
     names = names or layout.names
     if len(names) != len(layout):
         raise ValueError("layout needs a name per tensor")
@@ -81,10 +106,12 @@ def read_into_arena(model_dir: str, layout: ParamLayout, flat: torch.Tensor,
     headers = {p: read_header(p) for p in set(files.values())}
     dev = flat.device
     es = flat.element_size()
-    stage = _Staging(staging_bytes, dev)
+    stage = _acquire_stage(staging_bytes, dev)
     copy_stream = stage.stream
+    caller = None
     if copy_stream is not None:        # earlier kernels on the compute stream may still read `flat`
-        copy_stream.wait_stream(torch.cuda.current_stream(dev))
+        caller = caller_stream or torch.cuda.current_stream(dev)
+        copy_stream.wait_stream(caller)
     # group consecutive arena tensors that are also consecutive, same-dtype byte ranges in one file
     runs = []
     for k, name in enumerate(names):
@@ -133,9 +160,38 @@ def read_into_arena(model_dir: str, layout: ParamLayout, flat: torch.Tensor,
     finally:
         for f in handles.values():
             f.close()
+        _release_stage(stage)
     if copy_stream is not None:
-        torch.cuda.current_stream(dev).wait_stream(copy_stream)
+        caller.wait_stream(copy_stream)
     return flat
+
+
+def read_many(items, layout: ParamLayout, names: list[str] | None = None, threads: int = 8,
+              staging_bytes: int = 64 << 20) -> None:
+    """read_into_arena for several (model_dir, flat) pairs at once — the K worker checkpoints of
+    a generation (EDT_LM/diloco.py:231-235 loads them one after another): one reader thread per
+    checkpoint (file reads release the GIL), each with its own pinned staging pair and copy
+    stream, so page-cache/disk reads of one worker overlap the PCIe copies of another. The arenas
+    are ready on the caller's current stream when this returns."""
+    from concurrent.futures import ThreadPoolExecutor
+    items = list(items)
+    if not items:
+        return
+    dev = items[0][1].device
+    caller = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
+    if threads <= 1 or len(items) == 1:
+        for d, flat in items:
+            read_into_arena(d, layout, flat, names, staging_bytes, caller)
+        return
+
+    def one(item):
+        d, flat = item
+        if dev.type == "cuda":
+            torch.cuda.set_device(dev)
+        read_into_arena(d, layout, flat, names, staging_bytes, caller)
+
+    with ThreadPoolExecutor(max_workers=min(threads, len(items))) as ex:
+        list(ex.map(one, items))
 
 
 def _header_bytes(layout: ParamLayout, names, dtype, metadata) -> bytes:

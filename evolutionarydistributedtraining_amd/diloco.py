@@ -231,7 +231,7 @@ class DirOuterSync:
 
     def step(self, base_dir: str, worker_dirs: list[str], out_dirs: list[str] | None = None) -> OuterState:
         import shutil
-        from .checkpoint import read_into_arena, save_to_dirs
+        from .checkpoint import read_many, save_to_dirs
         if self.layout is None:
             self.layout, ckpt_dt = self._layout_from(base_dir)
             self.theta_dtype = self.theta_dtype or ckpt_dt
@@ -239,10 +239,10 @@ class DirOuterSync:
             self.theta = ParamArena(self.layout, self.theta_dtype, self.device)
         while len(self.workers) < len(worker_dirs):
             self.workers.append(ParamArena(self.layout, self.worker_dtype, self.device))
+        items = [(d, arena.flat) for d, arena in zip(worker_dirs, self.workers)]
         if os.path.abspath(base_dir) not in self._written:   # else theta is already resident
-            read_into_arena(base_dir, self.layout, self.theta.flat)
-        for d, arena in zip(worker_dirs, self.workers):
-            read_into_arena(d, self.layout, arena.flat)
+            items.insert(0, (base_dir, self.theta.flat))
+        read_many(items, self.layout, self.names)        # the K + 1 checkpoints read in parallel
         _step_flat(self.theta.flat, [w.flat for w in self.workers[:len(worker_dirs)]], self.state,
                    self.lr, self.momentum, self.nesterov)
         out_dirs = worker_dirs if out_dirs is None else out_dirs

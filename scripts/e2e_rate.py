@@ -119,8 +119,13 @@ def disk_edge(a, P, workers_h, theta_d, mom_d, workers_d, metric_bytes):
         for rep in range(2):                      # second pass: warm page cache
             torch.cuda.synchronize()
             t0 = time.perf_counter()
+            tr = time.perf_counter()
             for d, wd in zip(dirs, workers_d):
                 checkpoint.read_into_arena(d, lay, wd)
+            torch.cuda.synchronize()
+            serial_read = time.perf_counter() - tr
+            t0 = time.perf_counter()
+            checkpoint.read_many(list(zip(dirs, workers_d)), lay, threads=a.k)
             torch.cuda.synchronize()
             t1 = time.perf_counter()
             ops.outer_step(theta_d, workers_d, mom_d, True, 0.7, 0.9, True)
@@ -128,7 +133,8 @@ def disk_edge(a, P, workers_h, theta_d, mom_d, workers_d, metric_bytes):
             t2 = time.perf_counter()
             checkpoint.save_to_dirs(out_dirs, lay, theta_d)
             t3 = time.perf_counter()
-            out = {"read_ms": round((t1 - t0) * 1e3, 1), "step_ms": round((t2 - t1) * 1e3, 2),
+            out = {"read_serial_ms": round(serial_read * 1e3, 1),
+                   "read_ms": round((t1 - t0) * 1e3, 1), "step_ms": round((t2 - t1) * 1e3, 2),
                    "write_ms": round((t3 - t2) * 1e3, 1),
                    "read_GBps": round(metric_bytes / (t1 - t0) / 1e9, 2),
                    "total_metric_GBps": round(metric_bytes / (t3 - t0) / 1e9, 2)}
