@@ -5,8 +5,11 @@ Metric (BASELINE.json): "GB/s of param bytes reduced per outer step (device-resi
   aggregated over all ranks.
 
 Default workload (N=1): the 1.3B-parameter GPT layout (P = 1,315,723,264, 292 tensors), a
-population of 8 bf16 workers resident on the GPU, fp32 global weights and fp32 momentum,
-diloco.py's outer optimiser (lr 0.7, momentum 0.9, Nesterov) in steady state (carried buffer).
+population of 8 workers resident on the GPU, everything fp32 — the dtype the reference computes
+the outer step in as written (transformers 4.x `from_pretrained` loads fp32) —
+and diloco.py's outer optimiser (lr 0.7, momentum 0.9, Nesterov) in steady state (carried
+buffer). `--theta-dtype bf16 --worker-dtype bf16` is the all-bf16 form (transformers 5.x, BASELINE
+cfg4's "bf16 params"); `--worker-dtype bf16` alone keeps an fp32 master with bf16 replicas.
 N>1 (BASELINE configs "8 workers over 8 GPUs"): the population stays K = 8 and
 is spread 8/N workers per GPU (strong scaling); the cross-replica step runs over RCCL (xGMI):
 reduce-scatter of fp32 partial sums + sharded SGD + all-gather of theta, or all-to-all of the raw
@@ -48,7 +51,7 @@ def parse():
     p.add_argument("--population", type=int, default=8, help="total workers K (strong scaling)")
     p.add_argument("--workers-per-gpu", type=int, default=None, help="fixed per GPU (weak scaling)")
     p.add_argument("--theta-dtype", default="f32", choices=DT)
-    p.add_argument("--worker-dtype", default="bf16", choices=DT)
+    p.add_argument("--worker-dtype", default="f32", choices=DT)
     p.add_argument("--lr", type=float, default=0.7)
     p.add_argument("--momentum", type=float, default=0.9)
     p.add_argument("--nesterov", type=int, default=1)

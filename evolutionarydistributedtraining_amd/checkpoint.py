@@ -105,7 +105,6 @@ def read_into_arena(model_dir: str, layout: ParamLayout, flat: torch.Tensor,
     files = checkpoint_files(model_dir)
     headers = {p: read_header(p) for p in set(files.values())}
     dev = flat.device
-    es = flat.element_size()
     stage = _acquire_stage(staging_bytes, dev)
     copy_stream = stage.stream
     caller = None

@@ -55,6 +55,18 @@ namespace {
 #ifndef EDT_SLERP_COEF_BLOCK    // 1: one workgroup per segment for the chunk-sum reduction (else one wave)
 #define EDT_SLERP_COEF_BLOCK 1
 #endif
+// outer_kernel / probe_kernel element mapping (see ld()): 0 = 8 consecutive elements per thread,
+// 1 = wave-contiguous "split halves", 2 = split halves when workers and theta are fp32. Same speed
+// in every regime (profiles/r01_split_halves.json), but with 8 fp32 worker streams the 32-B-strided
+// pairs of 16-B loads fetch ~20 % more than the algorithmic bytes (FETCH_SIZE; served mostly by
+// the Infinity Cache) while split halves fetch exactly them (profiles/pmc_traffic.json).
+#ifndef EDT_SPLIT_HALVES
+#define EDT_SPLIT_HALVES 2
+#endif
+template <int GDT, int WDT>
+constexpr bool split_halves() {
+    return EDT_SPLIT_HALVES == 1 || (EDT_SPLIT_HALVES == 2 && GDT == EDT_F32 && WDT == EDT_F32);
+}
 #ifndef EDT_MIN_WAVES           // __launch_bounds__ minimum waves per SIMD for the stream kernels
 #define EDT_MIN_WAVES 1
 #endif
@@ -72,6 +84,7 @@ inline unsigned slerp_grid(int64_t nchunks) {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
 thread_local char g_err[512];
@@ -141,13 +154,17 @@ __device__ __forceinline__ void vstore(V* p, V v) {
     else *p = v;
 }
 
-template <int DT, int N, bool NT = false>
+// An 8-element group is elements [i, i+4) and [i+H2, i+H2+4): H2 = 4 is 8 consecutive elements
+// (one 16-B access per bf16 operand, two per fp32 operand, 32 B apart across lanes); H2 = 4 x
+// workgroup size ("split halves") makes every access of a wave contiguous across its lanes (fp32:
+// 16 B per lane; bf16: 8 B per lane, twice).
+template <int DT, int N, bool NT = false, int H2 = 4>
 __device__ __forceinline__ void ld(const void* __restrict__ p, uint64_t i, float (&x)[N]) {
     if constexpr (DT == EDT_F32) {
         const float* q = static_cast<const float*>(p) + i;
         if constexpr (N == 8) {
             f32x4 a = vload<f32x4, NT>(reinterpret_cast<const f32x4*>(q));
-            f32x4 b = vload<f32x4, NT>(reinterpret_cast<const f32x4*>(q + 4));
+            f32x4 b = vload<f32x4, NT>(reinterpret_cast<const f32x4*>(q + H2));
             x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
             x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
         } else {
@@ -156,10 +173,15 @@ __device__ __forceinline__ void ld(const void* __restrict__ p, uint64_t i, float
         }
     } else {
         const uint16_t* q = static_cast<const uint16_t*>(p) + i;
-        if constexpr (N == 8) {
+        if constexpr (N == 8 && H2 == 4) {
             u32x4 w = vload<u32x4, NT>(reinterpret_cast<const u32x4*>(q));
             x[0] = bf_lo(w.x); x[1] = bf_hi(w.x); x[2] = bf_lo(w.y); x[3] = bf_hi(w.y);
             x[4] = bf_lo(w.z); x[5] = bf_hi(w.z); x[6] = bf_lo(w.w); x[7] = bf_hi(w.w);
+        } else if constexpr (N == 8) {
+            u32x2 w0 = vload<u32x2, NT>(reinterpret_cast<const u32x2*>(q));
+            u32x2 w1 = vload<u32x2, NT>(reinterpret_cast<const u32x2*>(q + H2));
+            x[0] = bf_lo(w0.x); x[1] = bf_hi(w0.x); x[2] = bf_lo(w0.y); x[3] = bf_hi(w0.y);
+            x[4] = bf_lo(w1.x); x[5] = bf_hi(w1.x); x[6] = bf_lo(w1.y); x[7] = bf_hi(w1.y);
         } else {
 #pragma unroll
             for (int j = 0; j < N; ++j) x[j] = __uint_as_float(uint32_t(q[j]) << 16);
@@ -168,24 +190,30 @@ __device__ __forceinline__ void ld(const void* __restrict__ p, uint64_t i, float
 }
 
 // Stores round-to-nearest-even into DT (values are already DT-exact in the bf16 regime).
-template <int DT, int N, bool NT = (EDT_NT_STORES != 0)>
+template <int DT, int N, bool NT = (EDT_NT_STORES != 0), int H2 = 4>
 __device__ __forceinline__ void st(void* __restrict__ p, uint64_t i, const float (&x)[N]) {
     if constexpr (DT == EDT_F32) {
         float* q = static_cast<float*>(p) + i;
         if constexpr (N == 8) {
             vstore<f32x4, NT>(reinterpret_cast<f32x4*>(q), (f32x4){x[0], x[1], x[2], x[3]});
-            vstore<f32x4, NT>(reinterpret_cast<f32x4*>(q + 4), (f32x4){x[4], x[5], x[6], x[7]});
+            vstore<f32x4, NT>(reinterpret_cast<f32x4*>(q + H2), (f32x4){x[4], x[5], x[6], x[7]});
         } else {
 #pragma unroll
             for (int j = 0; j < N; ++j) q[j] = x[j];
         }
     } else {
         uint16_t* q = static_cast<uint16_t*>(p) + i;
-        if constexpr (N == 8) {
+        if constexpr (N == 8 && H2 == 4) {
             u32x4 w;
             w.x = pack_bf(x[0], x[1]); w.y = pack_bf(x[2], x[3]);
             w.z = pack_bf(x[4], x[5]); w.w = pack_bf(x[6], x[7]);
             vstore<u32x4, NT>(reinterpret_cast<u32x4*>(q), w);
+        } else if constexpr (N == 8) {
+            u32x2 w0, w1;
+            w0.x = pack_bf(x[0], x[1]); w0.y = pack_bf(x[2], x[3]);
+            w1.x = pack_bf(x[4], x[5]); w1.y = pack_bf(x[6], x[7]);
+            vstore<u32x2, NT>(reinterpret_cast<u32x2*>(q), w0);
+            vstore<u32x2, NT>(reinterpret_cast<u32x2*>(q + H2), w1);
         } else {
 #pragma unroll
             for (int j = 0; j < N; ++j) q[j] = uint16_t(pack_bf(x[j], 0.f) & 0xffffu);
@@ -220,12 +248,12 @@ SgdScalars make_sgd(int gdt, double lr, double mu, int has_buf, int nesterov) {
 // grad is the pseudo-gradient (already in GDT precision); theta is updated in registers,
 // the momentum buffer is read from / written to `mom` at element i.
 // Loads the carried momentum buffer (issued together with the other operand loads).
-template <int GDT, int N>
+template <int GDT, int N, int H2 = 4>
 __device__ __forceinline__ void ld_momentum(const void* mom, uint64_t i, const SgdScalars& s, float (&b)[N]) {
-    if (s.use_momentum && s.has_buf) ld<GDT, N>(mom, i, b);
+    if (s.use_momentum && s.has_buf) ld<GDT, N, false, H2>(mom, i, b);
 }
 
-template <int GDT, int N>
+template <int GDT, int N, int H2 = 4>
 __device__ __forceinline__ void sgd_update(float (&theta)[N], const float (&grad)[N], void* mom,
                                            uint64_t i, const SgdScalars& s, const float (&b_in)[N]) {
     float u[N];
@@ -242,7 +270,7 @@ __device__ __forceinline__ void sgd_update(float (&theta)[N], const float (&grad
 #pragma unroll
             for (int j = 0; j < N; ++j) b[j] = grad[j];              // buf = grad.clone()
         }
-        st<GDT, N>(mom, i, b);
+        st<GDT, N, (EDT_NT_STORES != 0), H2>(mom, i, b);
         if (s.nesterov) {
 #pragma unroll
             for (int j = 0; j < N; ++j) u[j] = __builtin_fmaf(s.alpha_mu, b[j], grad[j]);
@@ -312,15 +340,15 @@ enum { MODE_FUSED = 0, MODE_PARTIAL = 1, MODE_CHAIN = 2 };
 // Per-element accumulation acc = sum_k round(round(w_k - g) / K) in the precision of GDT
 // (worker-major order, EDT_LM/diloco.py:243-246). MODE_PARTIAL sums the rounded quotients
 // in fp32 instead (the cross-rank sum is then an fp32 RCCL reduction).
-template <int GDT, int WDT, int KC, int DIV, int MODE, int N, class A>
+template <int GDT, int WDT, int KC, int DIV, int MODE, int N, class A, int H2 = 4>
 __device__ __forceinline__ void outer_elems(const A& a, uint64_t i) {
     float g[N], acc[N], b_in[N];
-    ld<GDT, N>(a.theta, i, g);
-    if constexpr (MODE != MODE_PARTIAL) ld_momentum<GDT, N>(a.mom, i, a.sgd, b_in);
+    ld<GDT, N, false, H2>(a.theta, i, g);
+    if constexpr (MODE != MODE_PARTIAL) ld_momentum<GDT, N, H2>(a.mom, i, a.sgd, b_in);
     if (MODE == MODE_PARTIAL && a.accumulate) {
-        ld<EDT_F32, N>(a.acc_out, i, acc);      // continue the running sum in worker order
+        ld<EDT_F32, N, false, H2>(a.acc_out, i, acc);      // continue the running sum in worker order
     } else if (MODE == MODE_CHAIN && a.acc_in) {
-        ld<GDT, N>(a.acc_ws, i, acc);
+        ld<GDT, N, false, H2>(a.acc_ws, i, acc);
     } else {
 #pragma unroll
         for (int j = 0; j < N; ++j) acc[j] = 0.f;
@@ -328,7 +356,7 @@ __device__ __forceinline__ void outer_elems(const A& a, uint64_t i) {
     const int K = KC > 0 ? KC : a.K;
     auto body = [&](int k) {
         float w[N];
-        ld<WDT, N, EDT_NT_LOADS != 0 && WDT == EDT_BF16>(a.wp(k), i, w);
+        ld<WDT, N, EDT_NT_LOADS != 0 && WDT == EDT_BF16, H2>(a.wp(k), i, w);
 #pragma unroll
         for (int j = 0; j < N; ++j) w[j] = w[j] - g[j];              // trained - base
         rnd<GDT>(w);
@@ -352,15 +380,15 @@ __device__ __forceinline__ void outer_elems(const A& a, uint64_t i) {
         for (int k = 0; k < K; ++k) body(k);
     }
     if constexpr (MODE == MODE_PARTIAL) {
-        st<EDT_F32, N>(a.acc_out, i, acc);
+        st<EDT_F32, N, (EDT_NT_STORES != 0), H2>(a.acc_out, i, acc);
     } else if (MODE == MODE_CHAIN && a.acc_store) {
-        st<GDT, N>(a.acc_ws, i, acc);
+        st<GDT, N, (EDT_NT_STORES != 0), H2>(a.acc_ws, i, acc);
     } else {
         float grad[N];
 #pragma unroll
         for (int j = 0; j < N; ++j) grad[j] = -acc[j];               // p.grad = -avg_delta
-        sgd_update<GDT, N>(g, grad, a.mom, i, a.sgd, b_in);
-        st<GDT, N>(a.theta, i, g);
+        sgd_update<GDT, N, H2>(g, grad, a.mom, i, a.sgd, b_in);
+        st<GDT, N, (EDT_NT_STORES != 0), H2>(a.theta, i, g);
     }
 }
 
@@ -370,7 +398,15 @@ template <int GDT, int WDT, int KC, int DIV, int MODE, int N>
 __global__ __launch_bounds__(kBlock, EDT_MIN_WAVES) void outer_kernel(OuterArgs a) {
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
     const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if constexpr (N == kVec) {
+    if constexpr (N == kVec && split_halves<GDT, WDT>()) {
+        // tiles of kBlock x 8 elements; thread t owns [4t, 4t+4) and [4(kBlock+t), +4) of a tile
+        constexpr int H2 = 4 * kBlock;
+        const uint64_t nv = a.n / (kVec * kBlock) * kBlock;
+        for (uint64_t v = tid; v < nv; v += stride)
+            outer_elems<GDT, WDT, KC, DIV, MODE, kVec, OuterArgs, H2>(a, v * kVec - 4 * threadIdx.x);
+        for (uint64_t e = nv * kVec + tid; e < a.n; e += stride)     // scalar tail (< 8 x kBlock)
+            outer_elems<GDT, WDT, KC, DIV, MODE, 1>(a, e);
+    } else if constexpr (N == kVec) {
         const uint64_t nv = a.n / kVec;
         for (uint64_t v = tid; v < nv; v += stride) outer_elems<GDT, WDT, KC, DIV, MODE, kVec>(a, v * kVec);
         const uint64_t t = nv * kVec + tid;      // scalar tail (< 8 elements)
@@ -891,35 +927,42 @@ __global__ __launch_bounds__(kBlock) void slerp_gram_coef_kernel(const double* g
 // with a trivial body. Its time is the memory-system ceiling of the step on the device at hand:
 // the fused kernel's time over it says how much of the step is anything but HBM traffic.
 
-template <int GDT, int WDT, int KC, int N>
+template <int GDT, int WDT, int KC, int N, int H2 = 4>
 __device__ __forceinline__ void probe_elems(const OuterArgs& a, uint64_t i) {
     float g[N], b[N], acc[N];
-    ld<GDT, N>(a.theta, i, g);
-    ld<GDT, N>(a.mom, i, b);
+    ld<GDT, N, false, H2>(a.theta, i, g);
+    ld<GDT, N, false, H2>(a.mom, i, b);
 #pragma unroll
     for (int j = 0; j < N; ++j) acc[j] = 0.f;
     const int K = KC > 0 ? KC : a.K;
 #pragma unroll 8
     for (int k = 0; k < K; ++k) {
         float w[N];
-        ld<WDT, N, EDT_NT_LOADS != 0 && WDT == EDT_BF16>(a.wp(k), i, w);
+        ld<WDT, N, EDT_NT_LOADS != 0 && WDT == EDT_BF16, H2>(a.wp(k), i, w);
 #pragma unroll
         for (int j = 0; j < N; ++j) acc[j] += w[j];
     }
 #pragma unroll
     for (int j = 0; j < N; ++j) { g[j] += acc[j] * 1e-30f; b[j] += acc[j] * 1e-30f; }
-    st<GDT, N>(a.theta, i, g);
-    st<GDT, N>(a.mom, i, b);
+    st<GDT, N, (EDT_NT_STORES != 0), H2>(a.theta, i, g);
+    st<GDT, N, (EDT_NT_STORES != 0), H2>(a.mom, i, b);
 }
 
 template <int GDT, int WDT, int KC>
 __global__ __launch_bounds__(kBlock, EDT_MIN_WAVES) void probe_kernel(OuterArgs a) {
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
     const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    const uint64_t nv = a.n / kVec;
-    for (uint64_t v = tid; v < nv; v += stride) probe_elems<GDT, WDT, KC, kVec>(a, v * kVec);
-    const uint64_t t = nv * kVec + tid;
-    if (t < a.n) probe_elems<GDT, WDT, KC, 1>(a, t);
+    if constexpr (split_halves<GDT, WDT>()) {
+        constexpr int H2 = 4 * kBlock;
+        const uint64_t nv = a.n / (kVec * kBlock) * kBlock;
+        for (uint64_t v = tid; v < nv; v += stride) probe_elems<GDT, WDT, KC, kVec, H2>(a, v * kVec - 4 * threadIdx.x);
+        for (uint64_t e = nv * kVec + tid; e < a.n; e += stride) probe_elems<GDT, WDT, KC, 1>(a, e);
+    } else {
+        const uint64_t nv = a.n / kVec;
+        for (uint64_t v = tid; v < nv; v += stride) probe_elems<GDT, WDT, KC, kVec>(a, v * kVec);
+        const uint64_t t = nv * kVec + tid;
+        if (t < a.n) probe_elems<GDT, WDT, KC, 1>(a, t);
+    }
 }
 
 // ---------------------------------------------------------------------------------------

@@ -92,6 +92,8 @@ def run_stream_ops(names, rounds, iters):
                "TBps": round(cases[k][0] * P / statistics.median(v) / 1e9, 3)} for k, v in times.items()}
     print(json.dumps({"op": "stream", "P": P, "variants": res}, indent=1))
 VARIANTS.update(SLERP_VARIANTS)
+VARIANTS.update({"split0": ["-DEDT_SPLIT_HALVES=0"], "split1": ["-DEDT_SPLIT_HALVES=1"],
+                 "split1_nt0": ["-DEDT_SPLIT_HALVES=1", "-DEDT_NT_LOADS=0"]})
 VARIANTS.update({f"li{i}": [f"-DEDT_LIST_ITERS={i}"] for i in (1, 2, 4, 8, 16)})
 
 
@@ -268,15 +270,16 @@ def build(names):
         print("built", out)
 
 
-def run(names, rounds, iters, layout_name, k):
+def run(names, rounds, iters, layout_name, k, tdt="f32", wdt="bf16"):
     import torch
     from evolutionarydistributedtraining_amd import _lib as L
     from evolutionarydistributedtraining_amd.layouts import LAYOUTS
     dev = torch.device("cuda:0")
     P = LAYOUTS[layout_name]().total
-    theta = torch.randn(P, device=dev) * 0.02
-    workers = [(theta + torch.randn(P, device=dev) * 1e-3).bfloat16() for _ in range(k)]
-    mom = torch.zeros(P, device=dev)
+    DT = {"f32": torch.float32, "bf16": torch.bfloat16}
+    theta = (torch.randn(P, device=dev) * 0.02).to(DT[tdt])
+    workers = [(theta.float() + torch.randn(P, device=dev) * 1e-3).to(DT[wdt]) for _ in range(k)]
+    mom = torch.zeros(P, device=dev, dtype=DT[tdt])
     libs = {}
     for n in names:
         lib = ctypes.CDLL(os.path.join(VDIR, f"{n}.so"))
@@ -288,12 +291,13 @@ def run(names, rounds, iters, layout_name, k):
         libs[n] = f
     arr = L.ptr_array(workers)
     stream = L.stream_ptr(dev)
-    bytes_per = k * 2 + 8 + 8
+    bw, bg = (2 if wdt == "bf16" else 4), (2 if tdt == "bf16" else 4)
+    bytes_per = k * bw + 4 * bg
     times = {n: [] for n in names}
 
     def launch(f):
-        rc = f(ctypes.c_void_p(theta.data_ptr()), 0, arr, 1, k, ctypes.c_void_p(mom.data_ptr()), 1, P,
-               0.7, 0.9, 1, stream)
+        rc = f(ctypes.c_void_p(theta.data_ptr()), L.dtype_code(theta), arr, L.dtype_code(workers[0]), k,
+               ctypes.c_void_p(mom.data_ptr()), 1, P, 0.7, 0.9, 1, stream)
         assert rc == 0
     for n in names:                       # warm-up, first-step buffer init
         launch(libs[n])
@@ -312,7 +316,7 @@ def run(names, rounds, iters, layout_name, k):
         med = statistics.median(times[n])
         res[n] = {"median_ms": round(med, 4), "min_ms": round(min(times[n]), 4),
                   "TBps": round(bytes_per * P / med / 1e9, 3)}
-    print(json.dumps({"layout": layout_name, "K": k, "variants": res}, indent=1))
+    print(json.dumps({"layout": layout_name, "K": k, "theta": tdt, "workers": wdt, "variants": res}, indent=1))
 
 
 if __name__ == "__main__":
@@ -323,6 +327,8 @@ if __name__ == "__main__":
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--layout", default="gpt_1p3b")
     ap.add_argument("--k", type=int, default=8)
+    ap.add_argument("--tdt", default="f32")
+    ap.add_argument("--wdt", default="bf16")
     ap.add_argument("--op", default="outer", choices=["outer", "slerp", "slerp_pop", "stream", "list"])
     a = ap.parse_args()
     names = a.variants.split(",")
@@ -337,4 +343,4 @@ if __name__ == "__main__":
     elif a.op == "slerp":
         run_slerp(names, a.rounds, a.layout if a.layout != "gpt_1p3b" else "qwen2p5_7b_body")
     else:
-        run(names, a.rounds, a.iters, a.layout, a.k)
+        run(names, a.rounds, a.iters, a.layout, a.k, a.tdt, a.wdt)

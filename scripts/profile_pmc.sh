@@ -3,7 +3,7 @@
 # (MI355X_MICROARCH.md: FETCH_SIZE and WRITE_SIZE cannot share a pass; never with trace domains).
 set -u
 cd "$(dirname "$0")/.."
-R=$(pwd); OUT=$R/gpurun_out/pmc
+R=$(pwd); OUT=$R/gpurun_out/pmc${PMC_TAG:-}
 mkdir -p $OUT
 ARGS="--steps 3 --warmup 1 --cpu-baseline-seconds 0 ${BENCH_ARGS:-}"
 for C in FETCH_SIZE WRITE_SIZE; do
