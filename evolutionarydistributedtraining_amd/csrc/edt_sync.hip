@@ -63,6 +63,17 @@ namespace {
 #ifndef EDT_SPLIT_HALVES
 #define EDT_SPLIT_HALVES 2
 #endif
+// Non-temporal loads for the once-read worker streams: bf16 always (EDT_NT_LOADS); fp32 with the
+// split-halves mapping (EDT_NT_F32: 10.61 vs 11.03 ms on 1.3B x 8 fp32, profiles/r01_f32_variants.json;
+// with the 8-consecutive mapping nt was 1.6x slower, so it never applies there).
+#ifndef EDT_NT_F32
+#define EDT_NT_F32 1
+#endif
+template <int WDT, int H2>
+constexpr bool nt_worker_loads() {
+    return EDT_NT_LOADS != 0 && (WDT == EDT_BF16 || (EDT_NT_F32 != 0 && H2 != 4));
+}
+
 template <int GDT, int WDT>
 constexpr bool split_halves() {
     return EDT_SPLIT_HALVES == 1 || (EDT_SPLIT_HALVES == 2 && GDT == EDT_F32 && WDT == EDT_F32);
@@ -356,7 +367,7 @@ __device__ __forceinline__ void outer_elems(const A& a, uint64_t i) {
     const int K = KC > 0 ? KC : a.K;
     auto body = [&](int k) {
         float w[N];
-        ld<WDT, N, EDT_NT_LOADS != 0 && WDT == EDT_BF16, H2>(a.wp(k), i, w);
+        ld<WDT, N, nt_worker_loads<WDT, H2>(), H2>(a.wp(k), i, w);
 #pragma unroll
         for (int j = 0; j < N; ++j) w[j] = w[j] - g[j];              // trained - base
         rnd<GDT>(w);
@@ -938,7 +949,7 @@ __device__ __forceinline__ void probe_elems(const OuterArgs& a, uint64_t i) {
 #pragma unroll 8
     for (int k = 0; k < K; ++k) {
         float w[N];
-        ld<WDT, N, EDT_NT_LOADS != 0 && WDT == EDT_BF16, H2>(a.wp(k), i, w);
+        ld<WDT, N, nt_worker_loads<WDT, H2>(), H2>(a.wp(k), i, w);
 #pragma unroll
         for (int j = 0; j < N; ++j) acc[j] += w[j];
     }

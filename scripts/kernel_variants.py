@@ -92,6 +92,13 @@ def run_stream_ops(names, rounds, iters):
                "TBps": round(cases[k][0] * P / statistics.median(v) / 1e9, 3)} for k, v in times.items()}
     print(json.dumps({"op": "stream", "P": P, "variants": res}, indent=1))
 VARIANTS.update(SLERP_VARIANTS)
+VARIANTS.update({"f32_nt": ["-DEDT_NT_F32=1"], "f32_bpc64": ["-DEDT_BLOCKS_PER_CU=64"],
+                 "f32_bpc32": ["-DEDT_BLOCKS_PER_CU=32"], "f32_oneshot": ["-DEDT_BLOCKS_PER_CU=0"],
+                 "f32_nt_bpc64": ["-DEDT_NT_F32=1", "-DEDT_BLOCKS_PER_CU=64"],
+                 "f32_w2": ["-DEDT_MIN_WAVES=2"],
+                 "f32_nt_oneshot": ["-DEDT_NT_F32=1", "-DEDT_BLOCKS_PER_CU=0"],
+                 "f32_nt_ntst": ["-DEDT_NT_F32=1", "-DEDT_NT_STORES=1"],
+                 "f32_nt_bpc128": ["-DEDT_NT_F32=1", "-DEDT_BLOCKS_PER_CU=128"]})
 VARIANTS.update({"split0": ["-DEDT_SPLIT_HALVES=0"], "split1": ["-DEDT_SPLIT_HALVES=1"],
                  "split1_nt0": ["-DEDT_SPLIT_HALVES=1", "-DEDT_NT_LOADS=0"]})
 VARIANTS.update({f"li{i}": [f"-DEDT_LIST_ITERS={i}"] for i in (1, 2, 4, 8, 16)})
