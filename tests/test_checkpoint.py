@@ -61,3 +61,24 @@ def test_shape_mismatch_is_an_error(tmp_path):
     bad = ParamLayout([(1,)] + layout.shapes[1:], layout.names)
     with pytest.raises(ValueError):
         checkpoint.read_into_arena(str(tmp_path), bad, torch.empty(bad.total))
+
+
+def test_read_many_parallel_matches_serial(tmp_path):
+    """checkpoint.read_many (one reader thread per checkpoint, pooled staging) fills every arena
+    exactly as read_into_arena does one after another."""
+    layout = None
+    dirs, want = [], []
+    for k in range(5):
+        m = _tiny(torch.bfloat16)
+        with torch.no_grad():
+            for p in m.parameters():
+                p.add_(k)                       # distinct checkpoints
+        d = tmp_path / f"w{k}"
+        m.save_pretrained(d, **({"max_shard_size": "8KB"} if k % 2 else {}))
+        layout = layout or ParamLayout.of_module(m)
+        dirs.append(str(d))
+        want.append(pack(list(m.parameters())))
+    arenas = [torch.full((layout.total,), float("nan"), dtype=torch.bfloat16) for _ in dirs]
+    checkpoint.read_many(list(zip(dirs, arenas)), layout, threads=4, staging_bytes=4096)
+    for a, w in zip(arenas, want):
+        assert torch.equal(a, w)
