@@ -64,6 +64,9 @@ def parse():
     p.add_argument("--cpu-sample-elems", type=int, default=1 << 24)
     p.add_argument("--sharded", action="store_true",
                    help="run the multi-GPU (RCCL) schedule even at world size 1 (launch with torchrun)")
+    p.add_argument("--weak-companion", type=int, default=1,
+                   help="N>1: after the timed strong-scaling steps, also time W = population workers per GPU "
+                        "(weak scaling) and report it beside the value as 'weak_scaling'")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return p.parse_args()
 
@@ -124,6 +127,34 @@ def stream_ceiling_ms(theta, workers, momentum, iters=10):
     torch.cuda.synchronize()
     ts = sorted(a.elapsed_time(b) for a, b in ev)
     return ts[len(ts) // 2]
+
+
+def time_sharded(args, layout, tdt, wdt, k_local, dev, rank, steps, warmup):
+    """Build a ShardedOuterSync with k_local workers per rank, warm it up and time `steps` steps
+    (barrier + synchronize on both sides, max over ranks). Returns (ms_per_step, mode/broadcast,
+    wire bytes per rank); frees the arenas."""
+    import torch.distributed as dist
+    from evolutionarydistributedtraining_amd.distributed import ShardedOuterSync
+    sync = ShardedOuterSync(layout, tdt, wdt, k_local, dev, args.lr, args.momentum, bool(args.nesterov),
+                            mode=args.mode, bucket_elems=args.bucket_elems, broadcast=args.broadcast)
+    synth_population(sync.theta.flat, [w.flat for w in sync.workers], seed=4321 + 7919 * rank)
+    dist.broadcast(sync.theta_buf, 0)
+    for _ in range(warmup):
+        sync.step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        sync.step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    res = (t.item() / steps * 1e3, f"{sync.mode}/{sync.broadcast}", sync.wire_bytes())
+    del sync
+    torch.cuda.empty_cache()
+    return res
 
 
 def main():
@@ -208,6 +239,23 @@ def main():
     bytes_reduced = k_total * P * torch.finfo(wdt).bits // 8
     value = bytes_reduced / (ms_per_step / 1e3) / 1e9
 
+    sched = f"{sync.mode}/{sync.broadcast}" if sharded else None
+    wire_main = sync.wire_bytes() if sharded else None
+    weak = None
+    if sharded and scaling == "strong" and args.weak_companion:     # (world 1: --sharded rehearsal)
+        # the same schedule with the N = 1 population on EVERY rank (population x N): per-GPU work
+        # fixed, so value_N / (N value_1) isolates the cost of the xGMI exchange
+        del sync, step
+        torch.cuda.empty_cache()
+        w_ms, w_sched, w_wire = time_sharded(args, layout, tdt, wdt, args.population, dev, rank,
+                                             args.steps, args.warmup)
+        w_bytes = args.population * world * P * torch.finfo(wdt).bits // 8
+        weak = {"workers_per_gpu": args.population, "population": args.population * world,
+                "ms_per_step": round(w_ms, 4), "value": round(w_bytes / (w_ms / 1e3) / 1e9, 2),
+                "unit": "GB/s", "schedule": w_sched, "wire_bytes_per_rank": w_wire,
+                "note": "companion measurement after the timed strong-scaling steps; not the value"}
+        sync = None
+
     if rank == 0:
         bg = torch.finfo(tdt).bits // 8
         bw = torch.finfo(wdt).bits // 8
@@ -243,20 +291,22 @@ def main():
                        "population": k_total, "worker_dtype": args.worker_dtype,
                        "theta_dtype": args.theta_dtype,
                        "parallelism": "single GPU" if not sharded else
-                                       f"dp{world} {sync.mode}/{sync.broadcast} (RCCL)"},
+                                       f"dp{world} {sched} (RCCL)"},
         }
         if sharded:
             # the exchange dominates: bytes this rank puts on xGMI per step over the whole step time
             # (the local HBM pass is inside that time), against the rank's links to its N-1 peers
-            wire = sync.wire_bytes()
+            wire = wire_main
             achieved = wire / (ms_per_step / 1e3) / 1e9
             peak = XGMI_LINK_GBPS * (world - 1)
             roofline = {"bound": "xgmi", "achieved": round(achieved, 1), "peak": peak, "unit": "GB/s",
                         "frac": round(achieved / peak, 4) if peak else None, "traffic": None,
                         "wire_bytes_per_rank": wire,
-                        "schedule": f"{sync.mode}/{sync.broadcast}"}
+                        "schedule": sched}
         if roofline:
             out["roofline"] = roofline
+        if weak:
+            out["weak_scaling"] = weak
         if not sharded:   # what a plain device-to-device copy reaches on this device, same process
             src = torch.empty(1 << 29, dtype=torch.float32, device=dev)
             dst = torch.empty_like(src)
