@@ -481,7 +481,15 @@ __device__ __forceinline__ void outer_list_chunk(const ListArgs& L, const uint64
     a.w = L.w;
     a.T = L.T;
     a.t = t;
-    if (nf & kVecFlag) {
+    if ((nf & kVecFlag) && split_halves<GDT, WDT>()) {
+        // tiles of kBlock x 8 elements in split-halves order (as outer_kernel), then a scalar tail
+        constexpr uint64_t tile = (uint64_t)kBlock * kVec;
+        const uint64_t vend = c0 + (c1 - c0) / tile * tile;
+        for (uint64_t i = c0 + 4ull * threadIdx.x; i < vend; i += tile)
+            outer_elems<GDT, WDT, KC, DIV, MODE_FUSED, kVec, TensorArgs, 4 * kBlock>(a, i);
+        for (uint64_t i = vend + threadIdx.x; i < c1; i += kBlock)
+            outer_elems<GDT, WDT, KC, DIV, MODE_FUSED, 1>(a, i);
+    } else if (nf & kVecFlag) {
         const uint64_t vend = c0 + (c1 - c0) / kVec * kVec;
         for (uint64_t i = c0 + (uint64_t)threadIdx.x * kVec; i < vend; i += (uint64_t)kBlock * kVec)
             outer_elems<GDT, WDT, KC, DIV, MODE_FUSED, kVec>(a, i);

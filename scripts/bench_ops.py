@@ -43,6 +43,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ops", default="pair,slerp,lerp,outer_list")
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--list-wdt", default="bf16", choices=["bf16", "f32"], help="outer_list worker dtype")
     a = ap.parse_args()
     from evolutionarydistributedtraining_amd import ops
     from evolutionarydistributedtraining_amd.layouts import gpt_1p3b, qwen2p5_7b_body
@@ -76,7 +77,9 @@ def main():
         P, K = lay.total, 8
         theta = torch.randn(P, device=dev) * 0.02
         mom = torch.randn(P, device=dev) * 1e-3
-        workers = [(theta + torch.randn(P, device=dev) * 1e-3).to(bf) for _ in range(K)]
+        lw = bf if a.list_wdt == "bf16" else torch.float32
+        workers = [(theta + torch.randn(P, device=dev) * 1e-3).to(lw) for _ in range(K)]
+        bpe = K * workers[0].element_size() + 16
         ms_flat = timed(lambda: ops.outer_step(theta, workers, mom, True, 0.7, 0.9, True), a.iters)
         th_t = [v.clone() for v in lay.views(theta)]
         mo_t = [v.clone() for v in lay.views(mom)]
@@ -87,9 +90,9 @@ def main():
         del workers, w
         torch.cuda.empty_cache()
         ms = timed(lambda: ops.outer_step_list(th_t, w_t, mo_t, True, 0.7, 0.9, True), a.iters)
-        res["outer_list"] = {"P": P, "tensors": len(lay), "K": K, "ms": round(ms, 3),
-                             "GBps": round(32 * P / ms / 1e6, 1), "frac": round(32 * P / ms / 1e6 / PEAK, 4),
-                             "flat_ms": round(ms_flat, 3), "bytes_per_elem": 32}
+        res["outer_list"] = {"P": P, "tensors": len(lay), "K": K, "worker_dtype": a.list_wdt, "ms": round(ms, 3),
+                             "GBps": round(bpe * P / ms / 1e6, 1), "frac": round(bpe * P / ms / 1e6 / PEAK, 4),
+                             "flat_ms": round(ms_flat, 3), "bytes_per_elem": bpe}
         del th_t, mo_t, w_t
         torch.cuda.empty_cache()
     if "slerp" in a.ops:

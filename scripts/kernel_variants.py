@@ -104,9 +104,9 @@ VARIANTS.update({"split0": ["-DEDT_SPLIT_HALVES=0"], "split1": ["-DEDT_SPLIT_HAL
 VARIANTS.update({f"li{i}": [f"-DEDT_LIST_ITERS={i}"] for i in (1, 2, 4, 8, 16)})
 
 
-def run_list(names, rounds, iters):
+def run_list(names, rounds, iters, wdt="bf16"):
     """Flat-arena vs tensor-list outer step (gpt_1p3b as 292 separate tensors per model, K = 8
-    bf16 workers, fp32 theta + momentum) per variant library."""
+    workers, fp32 theta + momentum) per variant library."""
     import torch
     from evolutionarydistributedtraining_amd import _lib as L
     from evolutionarydistributedtraining_amd.layouts import gpt_1p3b
@@ -115,7 +115,10 @@ def run_list(names, rounds, iters):
     P, K, T = lay.total, 8, len(lay)
     theta = torch.randn(P, device=dev) * 0.02
     mom = torch.zeros(P, device=dev)
-    workers = [(theta + torch.randn(P, device=dev) * 1e-3).bfloat16() for _ in range(K)]
+    workers = [(theta + torch.randn(P, device=dev) * 1e-3).to(torch.bfloat16 if wdt == "bf16" else torch.float32)
+               for _ in range(K)]
+    wc = L.dtype_code(workers[0])
+    bpe = K * workers[0].element_size() + 16
     th_t = [v.clone() for v in lay.views(theta)]
     mo_t = [v.clone() for v in lay.views(mom)]
     w_t = [[v.clone() for v in lay.views(w)] for w in workers]
@@ -128,19 +131,24 @@ def run_list(names, rounds, iters):
     ws = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
     one_th, one_mo = L.ptr_array([theta]), L.ptr_array([mom])     # the flat arenas as a 1-tensor list
     one_n = (ctypes.c_uint64 * 1)(P)
+    # the flat arenas as the 292-tensor list of their views (same memory as flat, per-tensor chunks)
+    v_th, v_mo = L.ptr_array(lay.views(theta)), L.ptr_array(lay.views(mom))
+    v_w = L.ptr_array([t for w in workers for t in lay.views(w)])
     cases = {}
     for n in names:
         lib = ctypes.CDLL(os.path.join(VDIR, f"{n}.so"))
         for name, res, args in L.SIGNATURES:
             f = getattr(lib, name)
             f.restype, f.argtypes = res, args
-        cases[f"{n}/flat"] = lambda lib=lib: lib.edt_outer_step(Pp(theta), 0, a_flat, 1, K, Pp(mom), 1, P, 0.7, 0.9,
+        cases[f"{n}/flat"] = lambda lib=lib: lib.edt_outer_step(Pp(theta), 0, a_flat, wc, K, Pp(mom), 1, P, 0.7, 0.9,
                                                                 1, st)
-        cases[f"{n}/list"] = lambda lib=lib: lib.edt_outer_step_list(a_th, 0, a_w, 1, K, a_mo, 1, numel, T, 0.7, 0.9,
+        cases[f"{n}/list"] = lambda lib=lib: lib.edt_outer_step_list(a_th, 0, a_w, wc, K, a_mo, 1, numel, T, 0.7, 0.9,
                                                                      1, Pp(ws), ws.numel(), st)
-        cases[f"{n}/flat_as_list1"] = lambda lib=lib: lib.edt_outer_step_list(one_th, 0, a_flat, 1, K, one_mo, 1,
+        cases[f"{n}/flat_as_list1"] = lambda lib=lib: lib.edt_outer_step_list(one_th, 0, a_flat, wc, K, one_mo, 1,
                                                                               one_n, 1, 0.7, 0.9, 1, Pp(ws),
                                                                               ws.numel(), st)
+        cases[f"{n}/flat_as_views"] = lambda lib=lib: lib.edt_outer_step_list(v_th, 0, v_w, wc, K, v_mo, 1, numel, T,
+                                                                              0.7, 0.9, 1, Pp(ws), ws.numel(), st)
     times = {k: [] for k in cases}
     for f in cases.values():
         assert f() == 0
@@ -154,9 +162,9 @@ def run_list(names, rounds, iters):
                 evs[2 * i + 1].record()
             torch.cuda.synchronize()
             times[k] += [evs[2 * i].elapsed_time(evs[2 * i + 1]) for i in range(iters)]
-    res = {k: {"median_ms": round(statistics.median(v), 4), "TBps": round(32 * P / statistics.median(v) / 1e9, 3)}
+    res = {k: {"median_ms": round(statistics.median(v), 4), "TBps": round(bpe * P / statistics.median(v) / 1e9, 3)}
            for k, v in times.items()}
-    print(json.dumps({"op": "list", "P": P, "tensors": T, "variants": res}, indent=1))
+    print(json.dumps({"op": "list", "P": P, "tensors": T, "workers": wdt, "variants": res}, indent=1))
 
 
 def run_slerp(names, rounds, layout_name):
@@ -344,7 +352,7 @@ if __name__ == "__main__":
     elif a.op == "stream":
         run_stream_ops(names, a.rounds, a.iters)
     elif a.op == "list":
-        run_list(names, a.rounds, a.iters)
+        run_list(names, a.rounds, a.iters, a.wdt)
     elif a.op == "slerp_pop":
         run_slerp_pop(names, a.rounds)
     elif a.op == "slerp":

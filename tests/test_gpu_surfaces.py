@@ -311,8 +311,9 @@ def test_dir_outer_sync_two_generations(oracle, dev, tmp_path):
     assert torch.equal(bits(sync.state.momentum.cpu()), bits(mom))
 
 
+@pytest.mark.parametrize("wdt", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("mode,broadcast", [("reduce", "theta"), ("exact", "theta"), ("exact", "workers")])
-def test_sharded_outer_step_rccl_world1(oracle, dev, tmp_path, mode, broadcast):
+def test_sharded_outer_step_rccl_world1(oracle, dev, tmp_path, mode, broadcast, wdt):
     """The multi-GPU schedule on the real RCCL backend (one rank: the collectives degenerate, but
     the in-place reduce-scatter / all-gather, async waits and stream ordering are RCCL's)."""
     import torch.distributed as dist
@@ -322,7 +323,7 @@ def test_sharded_outer_step_rccl_world1(oracle, dev, tmp_path, mode, broadcast):
     dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=dev)
     try:
         layout = ParamLayout([(1000, 37), (4097,), (3,)])
-        sync = ShardedOuterSync(layout, torch.float32, torch.bfloat16, 3, dev, 0.7, 0.9, True, mode=mode,
+        sync = ShardedOuterSync(layout, torch.float32, wdt, 3, dev, 0.7, 0.9, True, mode=mode,
                                 bucket_elems=8192, broadcast=broadcast)
         assert (sync.mode, sync.broadcast) == (mode, broadcast) and len(sync.buckets) > 3
         g = torch.Generator().manual_seed(8)
@@ -330,7 +331,7 @@ def test_sharded_outer_step_rccl_world1(oracle, dev, tmp_path, mode, broadcast):
         mom = torch.zeros(layout.total)
         sync.theta.flat.copy_(theta)
         for step in range(2):
-            ws = [(theta + torch.randn(layout.total, generator=g) * 1e-3).bfloat16() for _ in range(3)]
+            ws = [(theta + torch.randn(layout.total, generator=g) * 1e-3).to(wdt) for _ in range(3)]
             for a, w in zip(sync.workers, ws):
                 a.flat.copy_(w)
             sync.step()
@@ -338,7 +339,7 @@ def test_sharded_outer_step_rccl_world1(oracle, dev, tmp_path, mode, broadcast):
         torch.cuda.synchronize()
         if broadcast == "workers":
             for a in sync.workers:
-                assert torch.equal(bits(a.flat.cpu()), bits(theta.bfloat16()))
+                assert torch.equal(bits(a.flat.cpu()), bits(theta.to(wdt)))
         assert torch.equal(bits(sync.gather_theta().cpu()), bits(theta))   # fp32: same order, bit-exact
         assert torch.equal(bits(sync.mom_shard[:layout.total].cpu()), bits(mom))
     finally:
