@@ -18,8 +18,8 @@ if [ "${PROFILE:-1}" = "1" ]; then
   echo "== rocprofv3 kernel trace"
   R=$(pwd)
   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
-      -d $R/$OUT/prof -o bench -- python3 $R/bench.py --steps 10 --warmup 3 --cpu-baseline-seconds 0 ${BENCH_ARGS:-} \
-      > $R/$OUT/prof.log 2>&1); s=$?; tail -3 $OUT/prof.log; stop_if_fatal $s
+      -d $R/$OUT/prof -o bench -- python3 $R/bench.py ${BENCH_ARGS:-} \
+      > $R/$OUT/prof.log 2>&1); s=$?; tail -3 $OUT/prof.log; stop_if_fatal $s   # the bench command itself
   find $OUT/prof -name "*stats*" | head
 fi
 echo "== done"
