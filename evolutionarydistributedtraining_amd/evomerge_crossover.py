@@ -15,11 +15,12 @@ import os
 
 import torch
 
-from .merge import interpolate_t, lerp, merge_plan, slerp, slerp_state_dicts, uniform_dna_crossover
+from .merge import (LazyTensorLoader, interpolate_t, lerp, maybe_torch, merge_plan, normalize, slerp,  # noqa: F401
+                    slerp_state_dicts, uniform_dna_crossover)
 
 __all__ = ["slerp", "lerp", "interpolate_t", "load_model_from_path", "run_slerp_merge_from_config",
            "run_linear_merge_5050", "crossover_main", "uniform_dna_crossover", "SELF_ATTN_T_CURVE",
-           "MLP_T_CURVE"]
+           "MLP_T_CURVE", "LazyTensorLoader", "maybe_torch", "normalize"]
 
 SELF_ATTN_T_CURVE = [0, 0.5, 0.3, 0.7, 1]      # EDT_EVOMERGE/train/crossover.py:174-175
 MLP_T_CURVE = [1, 0.5, 0.7, 0.3, 0]

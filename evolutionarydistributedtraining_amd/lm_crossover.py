@@ -22,12 +22,12 @@ from . import ops
 from ._lib import EdtError
 from .diloco import OuterState
 from .evomerge_crossover import run_slerp_merge_from_config  # noqa: F401  (same surface as :105-147)
-from .merge import interpolate_t, lerp, slerp, uniform_dna_crossover  # noqa: F401
+from .merge import LazyTensorLoader, interpolate_t, lerp, maybe_torch, normalize, slerp, uniform_dna_crossover  # noqa: F401
 from .params import ParamLayout, flat_view, pack, unpack_
 
 __all__ = ["lerp", "slerp", "interpolate_t", "load_model_from_path", "run_slerp_merge_from_config",
            "run_linear_merge_5050", "run_sgd", "crossover_main", "uniform_dna_crossover",
-           "load_parent_outer_state"]
+           "load_parent_outer_state", "LazyTensorLoader", "maybe_torch", "normalize"]
 
 # hyper-parameter tables of the DNA (EDT_LM/train/crossover.py:286-294). The reference picks
 # entries 0 / 1 / -1 regardless of the DNA: lr 0.7, momentum 0.9, nesterov True.

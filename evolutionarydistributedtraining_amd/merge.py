@@ -11,6 +11,7 @@ over two flat HBM arenas the parents are packed into when they are not on the de
 from __future__ import annotations
 
 import numbers
+import threading
 
 import numpy as np
 import torch
@@ -39,6 +40,44 @@ def lerp(t, v0, v1):
     b = v1.detach().to(device=dev, dtype=a.dtype).contiguous()
     out = ops.lerp(float(t), a.reshape(-1), b.reshape(-1)).view(a.shape)
     return out if v0.is_cuda else out.cpu()
+
+
+def maybe_torch(v, is_torch):
+    """numpy -> torch when the caller passed torch (EDT_LM/train/crossover.py:54-57; host helper
+    of the reference's numpy SLERP, kept for callers that import it)."""
+    if is_torch:
+        return torch.from_numpy(v)
+    return v
+
+
+def normalize(v, eps):
+    """v / ||v|| when the norm exceeds eps (EDT_LM/train/crossover.py:60-64; host helper on numpy
+    arrays — the device SLERP forms the norms inside its stats pass)."""
+    norm_v = np.linalg.norm(v)
+    if norm_v > eps:
+        v = v / norm_v
+    return v
+
+
+class LazyTensorLoader:
+    """A model's state dict fetched once, on first use, then served per key on `device`
+    (EDT_LM/train/crossover.py:87-102, EDT_EVOMERGE/train/crossover.py:86-101)."""
+
+    def __init__(self, model, device="cpu"):
+        self.model = model
+        self.state_dict = None
+        self.lock = threading.Lock()
+        self.device = device
+
+    def get_tensor(self, key):
+        with self.lock:
+            if self.state_dict is None:
+                self.state_dict = self.model.state_dict()
+            return self.state_dict[key].to(self.device)
+
+    def flush(self):
+        with self.lock:
+            self.state_dict = None
 
 
 def interpolate_t(layer_idx, num_layers, t_curve):

@@ -8,10 +8,11 @@ from __future__ import annotations
 
 import os
 
-from .merge import interpolate_t, lerp, merge_plan, slerp, slerp_state_dicts, uniform_dna_crossover
+from .merge import (interpolate_t, lerp, maybe_torch, merge_plan, normalize, slerp,  # noqa: F401
+                    slerp_state_dicts, uniform_dna_crossover)
 
 __all__ = ["slerp", "lerp", "interpolate_t", "load_model_from_folder", "run_slerp_merge_from_config",
-           "run_slerp_merge", "uniform_crossover", "crossover", "SELF_ATTN_T_CURVE", "MLP_T_CURVE"]
+           "run_slerp_merge", "uniform_crossover", "crossover", "SELF_ATTN_T_CURVE", "MLP_T_CURVE", "maybe_torch", "normalize"]
 
 # hard-coded layer curves of run_slerp_merge (EDT_RL/crossover.py:146-147)
 SELF_ATTN_T_CURVE = [0, 0.5, 0.3, 0.7, 1]
