@@ -203,10 +203,15 @@ class DirOuterSync:
     generations, so the momentum carry of diloco.py:258-286 needs no state_dict round trip.
 
     names: parameter names in `model.parameters()` order (e.g. `ParamLayout.of_module(model).names`)
-    — the index order of the momentum; default: the checkpoint's own tensor order."""
+    — the index order of the momentum; default: the checkpoint's own tensor order.
+    state_path: the outer optimiser's state file (torch `SGD.state_dict()` format, as
+    `outer_optim.pt`): loaded before the first step when it exists and rewritten after every step,
+    so a restarted master resumes the momentum carry (the reference keeps it in RAM only,
+    EDT_LM/diloco.py:100)."""
 
     def __init__(self, device=None, theta_dtype=None, worker_dtype=None, names=None,
-                 lr=0.7, momentum=0.9, nesterov=True, state: OuterState | None = None):
+                 lr=0.7, momentum=0.9, nesterov=True, state: OuterState | None = None,
+                 state_path: str | None = None):
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.theta_dtype, self.worker_dtype, self.names = theta_dtype, worker_dtype, names
         self.lr, self.momentum, self.nesterov = lr, momentum, nesterov
@@ -215,6 +220,7 @@ class DirOuterSync:
         self.theta = None
         self.workers: list[ParamArena] = []
         self._written: set[str] = set()     # dirs holding the resident theta (last step's output)
+        self.state_path = state_path
 
     def _layout_from(self, model_dir):
         from .checkpoint import checkpoint_files, read_header, _ST_DTYPES
@@ -237,6 +243,8 @@ class DirOuterSync:
             self.theta_dtype = self.theta_dtype or ckpt_dt
             self.worker_dtype = self.worker_dtype or ckpt_dt
             self.theta = ParamArena(self.layout, self.theta_dtype, self.device)
+            if self.state_path and os.path.exists(self.state_path) and self.state.momentum is None:
+                self.state = OuterState.load(self.state_path, self.layout, self.theta_dtype, self.device)
         while len(self.workers) < len(worker_dirs):
             self.workers.append(ParamArena(self.layout, self.worker_dtype, self.device))
         items = [(d, arena.flat) for d, arena in zip(worker_dirs, self.workers)]
@@ -247,6 +255,9 @@ class DirOuterSync:
                    self.lr, self.momentum, self.nesterov)
         out_dirs = worker_dirs if out_dirs is None else out_dirs
         save_to_dirs(out_dirs, self.layout, self.theta.flat)
+        if self.state_path:                  # durable carry: write-then-rename
+            self.state.save(self.state_path + ".tmp", self.layout)
+            os.replace(self.state_path + ".tmp", self.state_path)
         self._written = {os.path.abspath(d) for d in out_dirs}
         for d in out_dirs:                  # config / generation config / tokenizer of the base
             for f in os.listdir(base_dir):

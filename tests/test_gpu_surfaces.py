@@ -276,7 +276,8 @@ def test_single_tensor_slerp_api(golden, dev):
 
 def test_dir_outer_sync_two_generations(oracle, dev, tmp_path):
     """DirOuterSync: checkpoint dirs in, fused step, checkpoint dirs out (EDT_LM/diloco.py:224-308),
-    two generations with the momentum carried, vs the oracle; outputs load with HF."""
+    two generations with the momentum carried across a master restart (state_path), vs the
+    oracle; outputs load with HF."""
     from transformers import LlamaForCausalLM
     from evolutionarydistributedtraining_amd.diloco import DirOuterSync
     from evolutionarydistributedtraining_amd.params import ParamLayout, pack
@@ -288,7 +289,8 @@ def test_dir_outer_sync_two_generations(oracle, dev, tmp_path):
             p.copy_(torch.randn(p.shape, generator=g) * 0.02)
     layout = ParamLayout.of_module(base)
     base.save_pretrained(tmp_path / "w0" / "Gen0000")
-    sync = DirOuterSync(device=dev, names=layout.names, lr=0.7, momentum=0.9, nesterov=True)
+    state_path = str(tmp_path / "outer_optim.pt")
+    sync = DirOuterSync(device=dev, names=layout.names, lr=0.7, momentum=0.9, nesterov=True, state_path=state_path)
     theta = pack(list(base.parameters()))
     mom = torch.zeros_like(theta)
     prev = str(tmp_path / "w0" / "Gen0000")
@@ -302,6 +304,9 @@ def test_dir_outer_sync_two_generations(oracle, dev, tmp_path):
             m.save_pretrained(d)
             dirs.append(str(d))
             workers.append(pack(list(m.parameters())))
+        if gen == 1:        # a restarted master: the momentum carry comes back from state_path
+            sync = DirOuterSync(device=dev, names=layout.names, lr=0.7, momentum=0.9, nesterov=True,
+                                state_path=state_path)
         sync.step(prev, dirs)
         oracle.outer_step(theta, workers, mom, gen > 0, 0.7, 0.9, True)
         for d in dirs:
