@@ -36,6 +36,10 @@ SIGNATURES = [
     ("edt_sgd_apply", _I, [_P, _I, _P, _P, _I, _U64, _D, _D, _I, _P]),
     ("edt_pair_merge", _I, [_P, _P, _P, _P, _I, _P, _I, _P, _I, _U64, _D, _D, _I, _P]),
     ("edt_pair_merge_to", _I, [_P, _P, _P, _P, _I, _P, _I, _P, _P, _I, _U64, _D, _D, _I, _P]),
+    ("edt_pair_merge_population", _I, [ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_P),
+                                       ctypes.POINTER(_P), _I, ctypes.POINTER(_P), _I, ctypes.POINTER(_P),
+                                       ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_int32), _I, _U64, _D, _D, _I,
+                                       _P]),
     ("edt_lerp", _I, [_P, _P, _I, _P, _I, _I, _U64, _D, _P]),
     ("edt_slerp_make_chunks", ctypes.c_int64,
      [ctypes.POINTER(_U64), _I, ctypes.c_uint32, ctypes.POINTER(_U64), ctypes.c_int64,

@@ -561,14 +561,14 @@ struct PairArgs {
     SgdScalars sgd;
 };
 
-template <int GDT, int WDT, int N>
+template <int GDT, int WDT, int N, bool NT = (EDT_NT_LOADS != 0 && WDT == EDT_BF16)>
 __device__ __forceinline__ void pair_elems(const PairArgs& a, uint64_t i) {
     float base[N], b_in[N];
     ld_momentum<GDT, N>(a.mom_in, i, a.sgd, b_in);
     if (a.b2) {                        // run_linear_merge_5050: lerp(0.5, b1, b2) in the model dtype
         float x[N], y[N];
-        ld<WDT, N, EDT_NT_LOADS != 0 && WDT == EDT_BF16>(a.b1, i, x);
-        ld<WDT, N, EDT_NT_LOADS != 0 && WDT == EDT_BF16>(a.b2, i, y);
+        ld<WDT, N, NT>(a.b1, i, x);
+        ld<WDT, N, NT>(a.b2, i, y);
 #pragma unroll
         for (int j = 0; j < N; ++j) { x[j] = x[j] * 0.5f; y[j] = y[j] * 0.5f; }   // (1-.5)*v0, .5*v1
         rnd<WDT>(x);
@@ -581,8 +581,8 @@ __device__ __forceinline__ void pair_elems(const PairArgs& a, uint64_t i) {
     }
     rnd<GDT>(base);                    // load_state_dict into the base model's dtype
     float d1[N], d2[N];
-    ld<WDT, N, EDT_NT_LOADS != 0 && WDT == EDT_BF16>(a.m1, i, d1);
-    ld<WDT, N, EDT_NT_LOADS != 0 && WDT == EDT_BF16>(a.m2, i, d2);
+    ld<WDT, N, NT>(a.m1, i, d1);
+    ld<WDT, N, NT>(a.m2, i, d2);
 #pragma unroll
     for (int j = 0; j < N; ++j) { d1[j] = d1[j] - base[j]; d2[j] = d2[j] - base[j]; }
     rnd<GDT>(d1);
@@ -611,6 +611,43 @@ __global__ __launch_bounds__(kBlock) void pair_kernel(PairArgs a) {
         if (t < a.n) pair_elems<GDT, WDT, 1>(a, t);
     } else {
         for (uint64_t e = tid; e < a.n; e += stride) pair_elems<GDT, WDT, 1>(a, e);
+    }
+}
+
+// EDT-LM children of a resident population in ONE launch (EDT_LM/edt_sim.py:244-256 builds one
+// child per machine from the selected pairs). A parent feeds ~2 children; the workgroups of every
+// child for the same chunk of elements carry the same blockIdx % 8 (they share an XCD, hence an
+// L2) and are dispatched together, and the parents are read with default-policy loads, so a
+// parent chunk crosses HBM once and its other readers hit the L2 / Infinity Cache. Per child the
+// element math is pair_elems' (bit-identical to edt_pair_merge_to).
+constexpr int kPopMaxChildren = 16;
+constexpr uint64_t kPopChunk = (uint64_t)kBlock * kVec * 4;     // 8192 elements per workgroup
+
+struct PopPairArgs {
+    PairArgs c[kPopMaxChildren];
+    int nchildren;
+    uint64_t nchunks;
+};
+
+template <int GDT, int WDT, bool VEC>
+__global__ __launch_bounds__(kBlock) void pair_population_kernel(PopPairArgs P) {
+    const uint64_t bid = blockIdx.x;
+    const uint64_t per_group = 8ull * (uint64_t)P.nchildren;
+    const uint64_t r = bid % per_group;
+    const int child = (int)(r / 8);
+    const uint64_t chunk = (bid / per_group) * 8 + (r % 8);
+    if (chunk >= P.nchunks) return;
+    const PairArgs& a = P.c[child];
+    const uint64_t c0 = chunk * kPopChunk;
+    const uint64_t c1 = c0 + kPopChunk < a.n ? c0 + kPopChunk : a.n;
+    if constexpr (VEC) {
+        const uint64_t vend = c0 + (c1 - c0) / kVec * kVec;
+        for (uint64_t i = c0 + (uint64_t)threadIdx.x * kVec; i < vend; i += (uint64_t)kBlock * kVec)
+            pair_elems<GDT, WDT, kVec, false>(a, i);
+        const uint64_t i = vend + threadIdx.x;
+        if (i < c1) pair_elems<GDT, WDT, 1, false>(a, i);
+    } else {
+        for (uint64_t i = c0 + threadIdx.x; i < c1; i += kBlock) pair_elems<GDT, WDT, 1, false>(a, i);
     }
 }
 
@@ -921,6 +958,48 @@ __global__ __launch_bounds__(kBlock) void slerp_gram_kernel(Members mem, const u
             gram[(uint64_t)c * NT + threadIdx.x] = acc;
         }
         __syncthreads();
+    }
+}
+
+// The blends of every child in one launch, with pair_population_kernel's placement: the
+// workgroups of all children for one chunk carry the same blockIdx % 8 (one XCD, one L2) and run
+// together, so a member that is a parent of several children is read from HBM once per chunk.
+// Same per-element math as slerp_blend_kernel (lerp_elems with the child's coefficients).
+constexpr int kBlendMaxChildren = 16;
+struct BlendChildren {
+    const void* v0[kBlendMaxChildren];
+    const void* v1[kBlendMaxChildren];
+    void* out[kBlendMaxChildren];
+    const float* coef[kBlendMaxChildren];     // [nseg][2] of the child
+    int nchildren;
+};
+
+template <int IDT, int ODT>
+__global__ __launch_bounds__(kBlock) void slerp_blend_population_kernel(BlendChildren B, const uint64_t* chunks,
+                                                                        int64_t nchunks) {
+    const uint64_t per_group = 8ull * (uint64_t)B.nchildren;
+    const uint64_t r = blockIdx.x % per_group;
+    const int child = (int)(r / 8);
+    const int64_t c = (int64_t)((blockIdx.x / per_group) * 8 + (r % 8));
+    if (c >= nchunks) return;
+    const uint64_t start = chunks[3 * c], len = chunks[3 * c + 1], seg = chunks[3 * c + 2];
+    const void* v0 = B.v0[child];
+    const void* v1 = B.v1[child];
+    void* out = B.out[child];
+    const float c0 = B.coef[child][2 * seg], c1 = B.coef[child][2 * seg + 1];
+    const uint64_t end = start + len;
+    const uint64_t a = (start + kVec - 1) / kVec * kVec;
+    const uint64_t b = end / kVec * kVec;
+    if (a < b) {
+        for (uint64_t i = a + (uint64_t)threadIdx.x * kVec; i < b; i += (uint64_t)kBlock * kVec)
+            lerp_elems<IDT, ODT, EDT_F32, kVec, false>(v0, v1, out, i, c0, c1);
+    }
+    const uint64_t h_end = a < end ? a : end;
+    const uint64_t t_beg = b > a ? b : h_end;
+    const uint64_t nh = h_end - start, nt = end - t_beg;
+    if ((uint64_t)threadIdx.x < nh + nt) {
+        const uint64_t i = threadIdx.x < nh ? start + threadIdx.x : t_beg + (threadIdx.x - nh);
+        lerp_elems<IDT, ODT, EDT_F32, 1>(v0, v1, out, i, c0, c1);
     }
 }
 
@@ -1324,6 +1403,62 @@ int edt_pair_merge_to(const void* b1, const void* b2, const void* m1, const void
     return check_launch("pair_kernel");
 }
 
+int edt_pair_merge_population(const void* const* b1, const void* const* b2, const void* const* m1,
+                              const void* const* m2, int wdt, void* const* out, int gdt,
+                              const void* const* momentum_in, void* const* momentum_out,
+                              const int32_t* has_momentum, int nchildren, uint64_t n, double lr,
+                              double momentum_coef, int nesterov, void* stream) {
+    g_err[0] = 0;
+    if (!valid_pair(gdt, wdt)) return fail(EDT_ERR_ARG, "unsupported dtype pair (gdt/wdt)");
+    if (nchildren < 1 || nchildren > kPopMaxChildren)
+        return fail(EDT_ERR_ARG, "child count %d out of range [1, %d]", nchildren, kPopMaxChildren);
+    if (!b1 || !b2 || !m1 || !m2 || !out) return fail(EDT_ERR_ARG, "null pointer table");
+    if (n == 0) return EDT_OK;
+    PopPairArgs P;
+    memset(&P, 0, sizeof(P));
+    P.nchildren = nchildren;
+    P.nchunks = (n + kPopChunk - 1) / kPopChunk;
+    bool vec = true;
+    for (int c = 0; c < nchildren; ++c) {
+        PairArgs& a = P.c[c];
+        const int has = has_momentum ? has_momentum[c] : 0;
+        a.b1 = b1[c]; a.b2 = b2[c]; a.m1 = m1[c]; a.m2 = m2[c]; a.out = out[c]; a.n = n;
+        a.mom = momentum_out ? momentum_out[c] : nullptr;
+        a.mom_in = momentum_in ? momentum_in[c] : nullptr;
+        a.sgd = make_sgd(gdt, lr, momentum_coef, has, nesterov);
+        if (!a.b1 || !a.b2 || !a.m1 || !a.m2 || !a.out) return fail(EDT_ERR_ARG, "child %d: null buffer", c);
+        if (a.sgd.use_momentum && !a.mom) return fail(EDT_ERR_ARG, "child %d: momentum buffer is null", c);
+        if (a.sgd.use_momentum && has && !a.mom_in) return fail(EDT_ERR_ARG, "child %d: carried momentum is null", c);
+        for (int d = 0; d < c; ++d)
+            if (P.c[d].out == a.out || (a.mom && P.c[d].mom == a.mom))
+                return fail(EDT_ERR_ARG, "children %d and %d write the same buffer", d, c);
+        for (int d = 0; d < nchildren; ++d) {           // outputs never alias an input of any child
+            const bool reads_mom = momentum_in && has_momentum && has_momentum[d];
+            const void* ins[5] = {b1[d], b2[d], m1[d], m2[d], reads_mom ? momentum_in[d] : nullptr};
+            for (const void* q : ins)
+                if (q && (q == a.out || q == a.mom))
+                    return fail(EDT_ERR_ARG, "child %d writes an input of child %d", c, d);
+        }
+        vec = vec && aligned16(a.b1) && aligned16(a.b2) && aligned16(a.m1) && aligned16(a.m2) && aligned16(a.out) &&
+              (!a.sgd.use_momentum || (aligned16(a.mom) && (!has || aligned16(a.mom_in))));
+    }
+    const uint64_t groups = (P.nchunks + 7) / 8;
+    const uint64_t blocks = groups * 8ull * (uint64_t)nchildren;
+    if (blocks > 0x7fffffffull) return fail(EDT_ERR_ARG, "too many elements for one launch");
+    const unsigned g = (unsigned)blocks;
+    hipStream_t s = (hipStream_t)stream;
+#define EDT_POP(G, W)                                                                   \
+    do {                                                                                \
+        if (vec) pair_population_kernel<G, W, true><<<g, kBlock, 0, s>>>(P);            \
+        else pair_population_kernel<G, W, false><<<g, kBlock, 0, s>>>(P);               \
+    } while (0)
+    if (gdt == EDT_F32 && wdt == EDT_F32) EDT_POP(EDT_F32, EDT_F32);
+    else if (gdt == EDT_F32) EDT_POP(EDT_F32, EDT_BF16);
+    else EDT_POP(EDT_BF16, EDT_BF16);
+#undef EDT_POP
+    return check_launch("pair_population_kernel");
+}
+
 int edt_lerp(const void* v0, const void* v1, int in_dt, void* out, int out_dt, int cdt, uint64_t n,
              double t, void* stream) {
     g_err[0] = 0;
@@ -1514,10 +1649,30 @@ int edt_slerp_population(const void* const* members, int nmembers, int in_dt, co
         rc = check_launch("slerp_gram_coef_kernel");
         if (rc) return rc;
     }
-    for (int q = 0; q < npairs; ++q) {
-        // default-policy loads: each member feeds ~2 children (measured: nt 2 % slower here)
-        rc = slerp_blend_impl(members[pairs[2 * q]], members[pairs[2 * q + 1]], in_dt, outs[q], out_dt, chunk_desc,
-                              nchunks, coef + 2 * (size_t)nseg * q, nullptr, stream, false);
+    // the blends: every child in one co-located launch (groups of <= 16 children)
+    for (int q0 = 0; q0 < npairs; q0 += kBlendMaxChildren) {
+        BlendChildren B;
+        memset(&B, 0, sizeof(B));
+        B.nchildren = npairs - q0 < kBlendMaxChildren ? npairs - q0 : kBlendMaxChildren;
+        for (int k = 0; k < B.nchildren; ++k) {
+            const int q = q0 + k;
+            B.v0[k] = members[pairs[2 * q]];
+            B.v1[k] = members[pairs[2 * q + 1]];
+            B.out[k] = outs[q];
+            B.coef[k] = coef + 2 * (size_t)nseg * q;
+        }
+        const uint64_t blocks = ((uint64_t)nchunks + 7) / 8 * 8ull * (uint64_t)B.nchildren;
+        if (blocks > 0x7fffffffull) return fail(EDT_ERR_ARG, "too many chunks for one launch");
+        const unsigned gb = (unsigned)blocks;
+        if (in_dt == EDT_F32 && out_dt == EDT_F32)
+            slerp_blend_population_kernel<EDT_F32, EDT_F32><<<gb, kBlock, 0, s>>>(B, chunk_desc, nchunks);
+        else if (in_dt == EDT_F32)
+            slerp_blend_population_kernel<EDT_F32, EDT_BF16><<<gb, kBlock, 0, s>>>(B, chunk_desc, nchunks);
+        else if (out_dt == EDT_F32)
+            slerp_blend_population_kernel<EDT_BF16, EDT_F32><<<gb, kBlock, 0, s>>>(B, chunk_desc, nchunks);
+        else
+            slerp_blend_population_kernel<EDT_BF16, EDT_BF16><<<gb, kBlock, 0, s>>>(B, chunk_desc, nchunks);
+        rc = check_launch("slerp_blend_population_kernel");
         if (rc) return rc;
     }
     return EDT_OK;

@@ -273,3 +273,35 @@ def slerp_population(plan: SlerpPlan, members: list[torch.Tensor], pairs, outs: 
                                      L.ptr(gram), L.ptr(coef), L.ptr(dots), L.stream_ptr(dev)),
             "edt_slerp_population")
     return dots[:Q, :plan.nseg]
+
+
+def pair_merge_population(children, lr: float, momentum_coef: float, nesterov: bool) -> None:
+    """Every EDT-LM child of a resident population in one launch (edt_pair_merge_population).
+    children: dicts with b1, b2, m1, m2 (parent arenas, repeated across children), out, and
+    momentum_in / momentum (the donor's buffer, read; the child's, written) / has_momentum.
+    Bit-identical to pair_merge(..., momentum_in=...) per child; parents shared by several
+    children cross HBM once (same-XCD workgroups, cache reuse)."""
+    lib = L.lib()
+    C = len(children)
+    if not 1 <= C <= 16:
+        raise L.EdtError(f"pair_merge_population takes 1..16 children, got {C} (use pair_merge per child)")
+    first = children[0]
+    n = first["out"].numel()
+    wdt, gdt = first["m1"].dtype, first["out"].dtype
+    for ch in children:
+        ts = [ch[k] for k in ("b1", "b2", "m1", "m2", "out")] + [ch.get("momentum"), ch.get("momentum_in")]
+        L.require_device(*ts)
+        if any(t is not None and t.numel() != n for t in ts):
+            raise L.EdtError("pair-merge buffers must all have the same size")
+        if any(ch[k].dtype != wdt for k in ("b1", "b2", "m1", "m2")) or ch["out"].dtype != gdt:
+            raise L.EdtError("one parent dtype and one child dtype for the whole population")
+    has = (ctypes.c_int32 * C)(*[int(bool(ch.get("has_momentum"))) for ch in children])
+    mom_out = [ch.get("momentum") for ch in children]
+    mom_in = [ch.get("momentum_in") if ch.get("has_momentum") else None for ch in children]
+    arr = lambda ts: (ctypes.c_void_p * C)(*[0 if t is None else t.data_ptr() for t in ts])
+    L.check(lib.edt_pair_merge_population(
+        L.ptr_array([ch["b1"] for ch in children]), L.ptr_array([ch["b2"] for ch in children]),
+        L.ptr_array([ch["m1"] for ch in children]), L.ptr_array([ch["m2"] for ch in children]),
+        L.dtype_code(wdt), L.ptr_array([ch["out"] for ch in children]), L.dtype_code(gdt),
+        arr(mom_in), arr(mom_out), has, C, n, float(lr), float(momentum_coef), int(nesterov),
+        L.stream_ptr(first["out"].device)), "edt_pair_merge_population")

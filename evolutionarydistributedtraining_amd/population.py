@@ -248,15 +248,7 @@ class ResidentPopulation:
         if self.kind == "slerp":
             self._slerp_children(pairs, got)
         else:
-            for c in self.local_members():
-                i, j = pairs[c]
-                s = self._local(c)
-                has = donors[c] is not None and self.momentum != 0
-                # the donor's buffer is read in place (it may feed other children): no copy.
-                # has = False (generation 0): the first step writes buf = grad.clone() unread
-                self.kernels.pair_merge(got[i][0], got[j][0], got[i][1], got[j][1], self._child[s],
-                                        self._child_mom[s], has, self.lr, self.momentum, self.nesterov,
-                                        momentum_in=got[donors[c]][2] if has else None)
+            self._sgd_children(pairs, got, donors)
         # every transfer and merge of this generation is enqueued/complete: swap the children in
         if self.kind == "sgd":
             self._base, self._child = self._child, self._base
@@ -268,6 +260,29 @@ class ResidentPopulation:
         if self.kind == "sgd" and self.momentum:
             self.has_momentum = [True] * self.P
         self.generation += 1
+
+    def _sgd_children(self, pairs, got, donors):
+        """EDT-LM merge of every local child: the donor's momentum buffer is read in place (it may
+        feed other children; has = False at generation 0: the first step writes buf =
+        grad.clone() without reading). Up to 16 local children go in ONE launch whose
+        workgroups share an XCD per chunk, so a parent that feeds several children crosses HBM
+        once (ops.pair_merge_population); bit-identical to one pair_merge per child."""
+        k = self.kernels
+        local = self.local_members()
+        children = []
+        for c in local:
+            i, j = pairs[c]
+            s = self._local(c)
+            has = donors[c] is not None and self.momentum != 0
+            children.append({"b1": got[i][0], "b2": got[j][0], "m1": got[i][1], "m2": got[j][1],
+                             "out": self._child[s], "momentum": self._child_mom[s],
+                             "momentum_in": got[donors[c]][2] if has else None, "has_momentum": has})
+        if hasattr(k, "pair_merge_population") and len(children) <= 16:
+            k.pair_merge_population(children, self.lr, self.momentum, self.nesterov)
+            return
+        for ch in children:
+            k.pair_merge(ch["b1"], ch["b2"], ch["m1"], ch["m2"], ch["out"], ch["momentum"], ch["has_momentum"],
+                         self.lr, self.momentum, self.nesterov, momentum_in=ch["momentum_in"])
 
     def _slerp_children(self, pairs, got):
         """SLERP every local child. With at most 8 distinct parent arenas on this rank (all the

@@ -112,6 +112,19 @@ int edt_pair_merge_to(const void* b1, const void* b2, const void* m1, const void
                       int has_momentum, uint64_t n, double lr, double momentum_coef, int nesterov,
                       void* stream);
 
+/* Every EDT-LM child of a resident population in ONE launch (EDT_LM/edt_sim.py:244-256: one child
+ * per machine from the selected pairs): child c is edt_pair_merge_to(b1[c], b2[c], m1[c], m2[c],
+ * out[c], momentum_in[c] -> momentum_out[c], has_momentum[c]) — host arrays of nchildren (<= 16)
+ * device pointers; parents repeat across children (a parent feeds ~2). The workgroups of all
+ * children for one chunk of elements share an XCD (blockIdx % 8) and run together, so each parent
+ * chunk is fetched from HBM once and served from L2 / the Infinity Cache to its other readers.
+ * Results are bit-identical to the per-child calls. Outputs must not alias any input. */
+int edt_pair_merge_population(const void* const* b1, const void* const* b2, const void* const* m1,
+                              const void* const* m2, int wdt, void* const* out, int gdt,
+                              const void* const* momentum_in, void* const* momentum_out,
+                              const int32_t* has_momentum, int nchildren, uint64_t n, double lr,
+                              double momentum_coef, int nesterov, void* stream);
+
 /* lerp(t, v0, v1) = (1-t)*v0 + t*v1 as three rounded ops in compute dtype cdt (= the tensors'
  * dtype for torch, F32 for numpy), stored as out_dt.
  * Replaces EDT_LM/train/crossover.py:50-51 / EDT_RL/crossover.py:46-47 when applied per tensor. */

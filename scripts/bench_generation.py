@@ -4,13 +4,16 @@ swap. Compare: the reference moves each child through the shared disk (crossover
 checkpoints and saves one; profiles/r01_crossover_e2e.json: 0.24 s per 162M child with the
 direct arena reader, 3.7 s through from_pretrained).
 
-  sgd    EDT-LM children (edt_pair_merge_to), bf16 members + bf16 outer momentum, steady state
-         (every member carries momentum). Algorithmic bytes per child and element:
-         4 parents x 2 + child 2 + donor momentum read 2 + child momentum write 2 = 14
-  slerp  EDT-RL / EVOMERGE children, per-tensor t, bf16 in / bf16 out: 2 x 2 in + 2 out = 6
-         algorithmic per child; moved: one Gram stats pass over the P <= 8 members
-         (edt_slerp_population: 2 B per member) + per child a blend (2 x 2 in + 2 out) = 8 per
-         child (10 with a stats pass per child, edt_slerp_merge)
+  sgd    EDT-LM children (edt_pair_merge_population: all children in one launch, a parent's
+         chunk read from HBM once for all its children), bf16 members + bf16 outer momentum, steady
+         state. Per child and element (children independent): 4 parents x 2 +
+         child 2 + donor momentum read 2 + child momentum write 2 = 14 B. The generation's floor:
+         every distinct parent's base and trained weights (+ momentum if a donor) once, every
+         child and its momentum once.
+  slerp  EDT-RL / EVOMERGE children, per-tensor t, bf16 in / bf16 out: 2 x 2 in + 2 out = 6 B per
+         child; edt_slerp_population runs one Gram stats pass over the members and one
+         co-located blend launch for all children, so its floor is two reads of every distinct
+         parent + one write per child.
 
     python scripts/bench_generation.py [--layout gpt2_small] [--population 8] [--iters 5]
 """
@@ -65,7 +68,7 @@ def main():
         fitness = [float(m) for m in range(P)]
         pop.step(fitness)                      # generation 0 (first-step momentum), warm-up
         torch.cuda.synchronize()
-        times, host = [], []
+        times, host, used = [], [], None
         for _ in range(a.iters):
             h0 = time.perf_counter()
             pairs = pop.select(fitness)
@@ -76,17 +79,25 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             times.append(e0.elapsed_time(e1))
+            used = pairs
         times.sort()
         ms = times[len(times) // 2]
-        bpe = 14 if kind == "sgd" else 6
-        # slerp: one Gram stats pass over the members (P <= 8: each read once) + per-child blends
-        moved = 14 if kind == "sgd" else (8 if P <= 8 else 10)
-        algo = bpe * n * P
+        # SURVEY 8(d) accounting, children independent: 14 B (sgd) / 6 B (slerp) per child and element
+        per_child = 14 if kind == "sgd" else 6
+        survey = per_child * n * P
+        # the generation's floor: every distinct parent array read once (per pass), every output once
+        parents = sorted({m for pr in used for m in pr})
+        donors = {i for i, _ in used}                     # steady state: parent 1 carries momentum
+        if kind == "sgd":
+            floor = n * (len(parents) * 2 * 2 + len(donors) * 2 + P * 2 * 2)
+        else:
+            floor = n * (2 * len(parents) * 2 + P * 2)    # Gram pass + blend pass, bf16 in / out
         out["results"][kind] = {
             "generation_ms": round(ms, 3), "per_child_ms": round(ms / P, 4),
-            "algo_bytes": algo, "algo_TBps": round(algo / ms / 1e9, 3),
-            "frac_of_8TBps": round(algo / ms / 1e9 / PEAK_TBPS, 4),
-            "moved_TBps": round(moved * n * P / ms / 1e9, 3),
+            "survey_bytes": survey, "survey_TBps": round(survey / ms / 1e9, 3),
+            "floor_bytes": floor, "floor_TBps": round(floor / ms / 1e9, 3),
+            "frac_of_8TBps_at_floor": round(floor / ms / 1e9 / PEAK_TBPS, 4),
+            "distinct_parents": len(parents),
             "host_select_ms": round(1e3 * sorted(host)[len(host) // 2], 3),
         }
         print(kind, out["results"][kind], flush=True)

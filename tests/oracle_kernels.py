@@ -24,6 +24,11 @@ class OracleKernels:
             mom.copy_(momentum_in)
         self.o.pair_merge(b1, b2, m1, m2, out, mom, has, lr, mu, nesterov)
 
+    def pair_merge_population(self, children, lr, mu, nesterov):
+        for ch in children:
+            self.pair_merge(ch["b1"], ch["b2"], ch["m1"], ch["m2"], ch["out"], ch["momentum"], ch["has_momentum"],
+                            lr, mu, nesterov, momentum_in=ch["momentum_in"])
+
     def outer_step(self, theta, workers, mom, has, lr, mu, nesterov):
         self.o.outer_step(theta, workers, mom, has, lr, mu, nesterov)
 

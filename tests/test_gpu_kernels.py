@@ -434,6 +434,41 @@ def test_slerp_population_matches_per_child(dev, ops, in_dt, out_dt, nmem):
         assert torch.equal(dots[q].cpu(), plan.dots.cpu()), (q, i, j)
 
 
+@pytest.mark.parametrize("gdt,wdt", REGIMES)
+@pytest.mark.parametrize("n", [1, 8191, 70_001, 1_000_003])
+def test_pair_merge_population_matches_per_child(dev, ops, gdt, wdt, n):
+    """edt_pair_merge_population (every child in one launch, same-XCD workgroups per chunk) is
+    bit-identical to edt_pair_merge_to per child: shared parents, self-pairs, children with and
+    without a carried momentum; also through the unaligned (scalar) body."""
+    g = torch.Generator().manual_seed(n % 997)
+    M = 5
+    base = [(torch.randn(n + 1, generator=g) * 0.02).to(wdt).to(dev) for _ in range(M)]
+    trained = [(b.float() + torch.randn(n + 1, generator=g).to(dev) * 1e-3).to(wdt) for b in base]
+    moms = [(torch.randn(n + 1, generator=g) * 1e-3).to(gdt).to(dev) for _ in range(M)]
+    pairs = [(0, 1), (1, 0), (2, 2), (3, 1), (4, 0), (0, 3), (2, 4), (1, 1)]
+    for off in (0, 1):                              # off = 1: 4-byte-shifted views -> scalar body
+        sl = lambda t: t[off:off + n]
+        children, want = [], []
+        for c, (i, j) in enumerate(pairs):
+            has = c % 3 != 0
+            ch = {"b1": sl(base[i]), "b2": sl(base[j]), "m1": sl(trained[i]), "m2": sl(trained[j]),
+                  "out": torch.full((n,), float("nan"), dtype=gdt, device=dev),
+                  "momentum": torch.full((n,), float("nan"), dtype=gdt, device=dev),
+                  "momentum_in": sl(moms[i]) if has else None, "has_momentum": has}
+            children.append(ch)
+            out = torch.empty(n, dtype=gdt, device=dev)
+            mom = torch.empty(n, dtype=gdt, device=dev)
+            ops.pair_merge(ch["b1"], ch["b2"], ch["m1"], ch["m2"], out, mom, has, 0.7, 0.9, True,
+                           momentum_in=ch["momentum_in"])
+            want.append((out, mom))
+        ops.pair_merge_population(children, 0.7, 0.9, True)
+        for c, (ch, (out, mom)) in enumerate(zip(children, want)):
+            assert torch.equal(bits(ch["out"].cpu()), bits(out.cpu())), (off, c)
+            assert torch.equal(bits(ch["momentum"].cpu()), bits(mom.cpu())), (off, c)
+    for m in moms:                                  # donors are read, never written
+        assert not torch.isnan(m.float()).any()
+
+
 def test_errors_are_raised(dev, ops):
     from evolutionarydistributedtraining_amd import EdtError
     th = torch.zeros(16, device=dev)
