@@ -23,6 +23,17 @@ from ._lib import EdtError
 from .params import ParamArena, ParamLayout, flat_view, pack, unpack_
 
 DILOCO_DEFAULTS = dict(lr=0.7, momentum=0.9, nesterov=True)        # EDT_LM/diloco.py:253-255
+
+
+def check_sgd_hparams(lr: float, momentum: float, nesterov: bool) -> None:
+    """The argument checks torch.optim.SGD's constructor makes (the reference builds one per outer
+    step, EDT_LM/diloco.py:253-257, EDT_LM/train/crossover.py:185-230), with its messages."""
+    if lr < 0.0:
+        raise ValueError(f"Invalid learning rate: {lr}")
+    if momentum < 0.0:
+        raise ValueError(f"Invalid momentum value: {momentum}")
+    if nesterov and momentum <= 0:
+        raise ValueError("Nesterov momentum requires a momentum and zero dampening")
 DILOCO_SIM_DEFAULTS = dict(lr=1.0, momentum=0.0, nesterov=False)   # EDT_LM/diloco_sim.py:248-250
 
 
@@ -91,6 +102,7 @@ class OuterState:
 
 def _step_flat(theta: torch.Tensor, workers: list[torch.Tensor], state: OuterState, lr: float,
                momentum: float, nesterov: bool) -> None:
+    check_sgd_hparams(lr, momentum, nesterov)
     state.hparams = dict(lr=lr, momentum=momentum, nesterov=nesterov)
     mom = state.buffer_for(theta) if momentum != 0 else None
     has = state.has_momentum if momentum != 0 else False
@@ -102,6 +114,7 @@ def _step_flat(theta: torch.Tensor, workers: list[torch.Tensor], state: OuterSta
 
 def _step_list(thetas: list[torch.Tensor], workers: list[list[torch.Tensor]], state: OuterState,
                lr: float, momentum: float, nesterov: bool) -> None:
+    check_sgd_hparams(lr, momentum, nesterov)
     state.hparams = dict(lr=lr, momentum=momentum, nesterov=nesterov)
     moms = None
     if momentum != 0:

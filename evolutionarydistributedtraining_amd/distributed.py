@@ -36,7 +36,7 @@ import torch
 import torch.distributed as dist
 
 from . import ops as _ops
-from .diloco import OuterState
+from .diloco import OuterState, check_sgd_hparams
 from .params import ParamArena, ParamLayout
 
 
@@ -49,6 +49,7 @@ class ShardedOuterSync:
             raise ValueError((mode, broadcast))
         if mode == "reduce" and broadcast == "workers":
             raise ValueError("the reduce schedule needs the full theta replica (broadcast='theta')")
+        check_sgd_hparams(lr, momentum, nesterov)
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)

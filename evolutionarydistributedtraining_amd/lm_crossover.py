@@ -20,7 +20,7 @@ import torch
 
 from . import ops
 from ._lib import EdtError
-from .diloco import OuterState
+from .diloco import OuterState, check_sgd_hparams
 from .evomerge_crossover import run_slerp_merge_from_config  # noqa: F401  (same surface as :105-147)
 from .merge import LazyTensorLoader, interpolate_t, lerp, maybe_torch, normalize, slerp, uniform_dna_crossover  # noqa: F401
 from .params import ParamLayout, flat_view, pack, unpack_
@@ -117,6 +117,7 @@ def _child_step(b1, b2, m1, m2, base_params, layout, state_sd, lr, momentum, nes
     if state_sd is not None:
         st.load_state_dict(state_sd, layout, theta.dtype, theta.device)
         lr, momentum, nesterov = st.hparams["lr"], st.hparams["momentum"], st.hparams["nesterov"]
+    check_sgd_hparams(lr, momentum, nesterov)          # optim.SGD(...) at :228-230
     mom = None
     if momentum != 0:
         mom = st.momentum if st.has_momentum else torch.zeros_like(theta)

@@ -55,6 +55,9 @@ class ResidentPopulation:
                  group=None, kernels=None):
         if kind not in ("sgd", "slerp"):
             raise ValueError(kind)
+        if kind == "sgd":
+            from .diloco import check_sgd_hparams
+            check_sgd_hparams(lr, momentum, nesterov)
         self.kind = kind
         self.layout = layout
         self.dtype = dtype
