@@ -26,8 +26,11 @@ are the arenas it updates (params.bind_module_ points a model's parameters into 
 """
 from __future__ import annotations
 
+import json
+import os
 import random
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -337,6 +340,70 @@ class ResidentPopulation:
                              "p1": g1, "p2": g2}
                 new.append(child)
         self.genomes = self._sync_host(new)
+
+    # ---- persistence (resume a resident run) ------------------------------------------------
+    def _member_tensors(self, m):
+        s = self._local(m)
+        if self.kind == "slerp":
+            return [("params", self._params[s])]
+        out = [("base", self._base[s]), ("trained", self._trained[s])]
+        if self._mom[s] is not None:
+            out.append(("outer_momentum", self._mom[s]))
+        return out
+
+    def _names(self):
+        return self.layout.names or [f"param.{i}" for i in range(len(self.layout))]
+
+    def save(self, path: str, rng: bool = True) -> None:
+        """Every local member's arenas as safetensors checkpoints under
+        path/member{m}/{base,trained,outer_momentum | params}/model.safetensors, and (rank 0)
+        path/population.json: generation, genomes, momentum flags and, with rng=True, the
+        states of the host RNGs the selection and DNA crossover draw from (python `random`,
+        numpy's global RNG), so a resumed run continues draw for draw. The reference keeps
+        this state in RAM and on the shared disk between its scripts (genome.json per dir,
+        outer_optim.pt per individual)."""
+        from .checkpoint import write_from_arena
+        names = self._names()
+        for m in self.local_members():
+            for tag, t in self._member_tensors(m):
+                d = os.path.join(path, f"member{m}", tag)
+                os.makedirs(d, exist_ok=True)
+                write_from_arena(os.path.join(d, "model.safetensors"), self.layout, t, names)
+        if self.rank == 0:
+            meta = {"kind": self.kind, "population": self.P, "generation": self.generation,
+                    "genomes": self.genomes, "has_momentum": self.has_momentum}
+            if rng:
+                st = random.getstate()
+                ns = np.random.get_state()
+                meta["rng"] = {"python": [st[0], list(st[1]), st[2]],
+                               "numpy": [ns[0], ns[1].tolist(), int(ns[2]), int(ns[3]), float(ns[4])]}
+            os.makedirs(path, exist_ok=True)
+            with open(os.path.join(path, "population.json.tmp"), "w") as f:
+                json.dump(meta, f)
+            os.replace(os.path.join(path, "population.json.tmp"), os.path.join(path, "population.json"))
+        if self.world > 1:
+            dist.barrier(group=self.group)
+
+    def load(self, path: str, rng: bool = True) -> None:
+        """Restore what save() wrote (same layout, kind and population; any world size that
+        divides the population: each rank reads its own members)."""
+        from .checkpoint import read_into_arena
+        with open(os.path.join(path, "population.json")) as f:
+            meta = json.load(f)
+        if meta["kind"] != self.kind or meta["population"] != self.P:
+            raise EdtError(f"{path} holds a {meta['kind']} population of {meta['population']}")
+        self.generation = meta["generation"]
+        self.genomes = meta["genomes"]
+        self.has_momentum = list(meta["has_momentum"])
+        names = self._names()
+        for m in self.local_members():
+            for tag, t in self._member_tensors(m):
+                read_into_arena(os.path.join(path, f"member{m}", tag), self.layout, t, names)
+        if rng and "rng" in meta and self.rank == 0:
+            py = meta["rng"]["python"]
+            random.setstate((py[0], tuple(py[1]), py[2]))
+            ns = meta["rng"]["numpy"]
+            np.random.set_state((ns[0], np.asarray(ns[1], dtype=np.uint32), ns[2], ns[3], ns[4]))
 
     # ---- mutation schedule (host) ----------------------------------------------------------
     def mutation_flags(self, probability: float = 0.5) -> list[bool]:

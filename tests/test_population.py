@@ -234,3 +234,48 @@ def test_resident_gpu_matches_reference_flow(oracle, kind):
             # SLERP parity bar: the fp64 dot vs the reference's fp32 one
             diff = (got[m]["params"] - base[m]).abs()
             assert (diff <= 1e-5 * base[m].abs() + 1e-8).all(), (m, diff.max().item())
+
+
+def test_resident_save_load_resumes_exactly(tmp_path, oracle):
+    """Three generations straight vs two, save(), a fresh population load()ed, one more: the
+    same members, momenta and genomes (host RNG states restored with them)."""
+    from evolutionarydistributedtraining_amd.params import ParamLayout
+    from evolutionarydistributedtraining_amd.population import ResidentPopulation
+    from tests.oracle_kernels import OracleKernels
+    layout = ParamLayout(SHAPES)
+    n, dt = layout.total, torch.bfloat16
+
+    def fresh():
+        return ResidentPopulation(layout, dt, "cpu", _genomes("sgd"), elitism=1, kernels=OracleKernels(oracle))
+
+    def gens(pop, lo, hi):
+        for gen in range(lo, hi):
+            pop.begin_inner()
+            for m in pop.local_members():
+                t = pop.trained(m)
+                t.copy_((t.float() + _noise(gen, m, n)).to(dt))
+            pop.step(_fitness(gen))
+
+    random.seed(7)
+    np.random.seed(7)
+    a = fresh()
+    for m in a.local_members():
+        a.base(m).copy_(_init(m, n, dt))
+    gens(a, 0, GENS)
+    random.seed(7)
+    np.random.seed(7)
+    b = fresh()
+    for m in b.local_members():
+        b.base(m).copy_(_init(m, n, dt))
+    gens(b, 0, GENS - 1)
+    b.save(str(tmp_path / "ckpt"))
+    random.seed(12345)                      # disturb the host RNGs: load() must restore them
+    np.random.seed(12345)
+    c = fresh()
+    c.load(str(tmp_path / "ckpt"))
+    assert c.generation == GENS - 1
+    gens(c, GENS - 1, GENS)
+    assert c.genomes == a.genomes
+    for m in range(POP):
+        assert torch.equal(_bits(c.base(m)), _bits(a.base(m))), m
+        assert torch.equal(_bits(c.outer_momentum(m)), _bits(a.outer_momentum(m))), m
