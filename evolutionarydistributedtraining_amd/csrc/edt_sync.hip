@@ -795,6 +795,76 @@ __global__ __launch_bounds__(kBlock) void slerp_stats_kernel(const void* v0, con
     }
 }
 
+// Speculative first pass (edt_slerp_merge_speculative): the chunk sums exactly as
+// slerp_stats_kernel forms them (same element order per thread, same FMAs, same reductions), and
+// in the same pass the lerp-branch output (1-t) v0 + t v1 (lerp_elems with the coefficients
+// slerp_coefficients gives that branch). Parents of one lineage (fine-tunes of a common base)
+// mostly have |dot| > 0.9995, where this output is final; the other segments are blended again.
+template <int IDT, int ODT>
+__global__ __launch_bounds__(kBlock) void slerp_stats_lerp_kernel(const void* v0, const void* v1, void* out,
+                                                                  const uint64_t* chunks, int64_t nchunks,
+                                                                  double* partial, const double* tvals) {
+    constexpr bool NT = EDT_NT_SLERP != 0 && IDT == EDT_BF16;
+    __shared__ double red[3][kBlock / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+        const uint64_t start = chunks[3 * c], end = start + chunks[3 * c + 1], seg = chunks[3 * c + 2];
+        const float l0 = (float)(1.0 - tvals[seg]), l1 = (float)tvals[seg];
+        double s00 = 0.0, s11 = 0.0, s01 = 0.0;
+        const uint64_t a = (start + kVec - 1) / kVec * kVec;
+        const uint64_t b = end / kVec * kVec;
+        if (a < b) {
+            for (uint64_t i = a + (uint64_t)threadIdx.x * kVec; i < b; i += (uint64_t)kBlock * kVec) {
+                float x[kVec], y[kVec], o[kVec];
+                ld<IDT, kVec, NT>(v0, i, x);
+                ld<IDT, kVec, NT>(v1, i, y);
+#pragma unroll
+                for (int j = 0; j < kVec; ++j) {
+                    const double dx = x[j], dy = y[j];
+                    s00 = __builtin_fma(dx, dx, s00);
+                    s11 = __builtin_fma(dy, dy, s11);
+                    s01 = __builtin_fma(dx, dy, s01);
+                    o[j] = l0 * x[j] + l1 * y[j];          // two rounded products, one rounded sum
+                }
+                st<ODT, kVec>(out, i, o);
+            }
+        }
+        const uint64_t h_end = a < end ? a : end;
+        const uint64_t t_beg = b > a ? b : h_end;
+        const uint64_t nh = h_end - start, nt = end - t_beg;
+        if ((uint64_t)threadIdx.x < nh + nt) {
+            const uint64_t i = threadIdx.x < nh ? start + threadIdx.x : t_beg + (threadIdx.x - nh);
+            float x[1], y[1], o[1];
+            ld<IDT, 1>(v0, i, x);
+            ld<IDT, 1>(v1, i, y);
+            const double dx = x[0], dy = y[0];
+            s00 = __builtin_fma(dx, dx, s00);
+            s11 = __builtin_fma(dy, dy, s11);
+            s01 = __builtin_fma(dx, dy, s01);
+            o[0] = l0 * x[0] + l1 * y[0];
+            st<ODT, 1>(out, i, o);
+        }
+        s00 = wave_sum(s00);
+        s11 = wave_sum(s11);
+        s01 = wave_sum(s01);
+        if (lane == 0) { red[0][wave] = s00; red[1][wave] = s11; red[2][wave] = s01; }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double acc[3];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                acc[q] = 0.0;
+#pragma unroll
+                for (int w = 0; w < kBlock / 64; ++w) acc[q] += red[q][w];
+            }
+            partial[3 * c] = acc[0];
+            partial[3 * c + 1] = acc[1];
+            partial[3 * c + 2] = acc[2];
+        }
+        __syncthreads();
+    }
+}
+
 // Fixed-order reduction of a segment's chunk sums: column q of rows [c0, c1) of a row-major table
 // with `stride` doubles per row, for the three columns (q0, q1, q2). EDT_SLERP_COEF_BLOCK = 0: one
 // wave per segment (lane-strided, then a wave sum); 1: one workgroup per segment (thread-strided,
@@ -843,7 +913,7 @@ inline unsigned coef_grid(int nseg) {
 __global__ __launch_bounds__(kBlock) void slerp_coef_kernel(const double* partial, const int32_t* first,
                                                             int nseg, const double* tvals,
                                                             float thr, float eps, float* coef,
-                                                            float* dot_out) {
+                                                            float* dot_out, int32_t* redo = nullptr) {
     const int seg = coef_segment();
     if (seg >= nseg) return;
     double sums[3];
@@ -853,14 +923,17 @@ __global__ __launch_bounds__(kBlock) void slerp_coef_kernel(const double* partia
     coef[2 * seg] = c0;
     coef[2 * seg + 1] = c1;
     if (dot_out) dot_out[seg] = dot;
+    if (redo) redo[seg] = fabsf(dot) > thr ? 0 : 1;   // the speculative lerp output stands or not
 }
 
 template <int IDT, int ODT, bool NT = (EDT_NT_SLERP != 0 && IDT == EDT_BF16)>
 __global__ __launch_bounds__(kBlock) void slerp_blend_kernel(const void* v0, const void* v1, void* out,
                                                              const uint64_t* chunks, int64_t nchunks,
-                                                             const float* coef, const uint64_t* seg_ptrs) {
+                                                             const float* coef, const uint64_t* seg_ptrs,
+                                                             const int32_t* redo = nullptr) {
     for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
         const uint64_t start = chunks[3 * c], len = chunks[3 * c + 1], seg = chunks[3 * c + 2];
+        if (redo && !redo[seg]) continue;         // speculative lerp output already final
         if (seg_ptrs) {
             v0 = reinterpret_cast<const void*>(seg_ptrs[3 * seg]);
             v1 = reinterpret_cast<const void*>(seg_ptrs[3 * seg + 1]);
@@ -1676,6 +1749,51 @@ int edt_slerp_population(const void* const* members, int nmembers, int in_dt, co
         if (rc) return rc;
     }
     return EDT_OK;
+}
+
+int edt_slerp_merge_speculative(const void* v0, const void* v1, int in_dt, void* out, int out_dt,
+                                const uint64_t* chunk_desc, int64_t nchunks, const int32_t* seg_first_chunk,
+                                int nseg, const double* t, double dot_threshold, double eps, double* partial,
+                                float* coef, float* dot_out, int32_t* redo, uint64_t n, void* stream) {
+    g_err[0] = 0;
+    if ((in_dt | out_dt) & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
+    if (nseg == 0 || nchunks == 0) return EDT_OK;
+    if (!v0 || !v1 || !out || !chunk_desc || !seg_first_chunk || !t || !partial || !coef || !redo)
+        return fail(EDT_ERR_ARG, "null buffer");
+    if (!aligned16(v0) || !aligned16(v1) || !aligned16(out))
+        return fail(EDT_ERR_ARG, "slerp buffers must be 16-byte aligned");
+    // the first pass writes `out` while the second may still need both parents
+    const uintptr_t o0 = reinterpret_cast<uintptr_t>(out), o1 = o0 + n * (out_dt == EDT_BF16 ? 2 : 4);
+    const uint64_t isz = in_dt == EDT_BF16 ? 2 : 4;
+    for (const void* p : {v0, v1}) {
+        const uintptr_t p0 = reinterpret_cast<uintptr_t>(p), p1 = p0 + n * isz;
+        if (p0 < o1 && o0 < p1) return fail(EDT_ERR_ARG, "speculative SLERP needs an output apart from the parents");
+    }
+    hipStream_t s = (hipStream_t)stream;
+    const unsigned g = slerp_grid(nchunks);
+    if (in_dt == EDT_F32 && out_dt == EDT_F32)
+        slerp_stats_lerp_kernel<EDT_F32, EDT_F32><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, partial, t);
+    else if (in_dt == EDT_F32)
+        slerp_stats_lerp_kernel<EDT_F32, EDT_BF16><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, partial, t);
+    else if (out_dt == EDT_F32)
+        slerp_stats_lerp_kernel<EDT_BF16, EDT_F32><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, partial, t);
+    else
+        slerp_stats_lerp_kernel<EDT_BF16, EDT_BF16><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, partial, t);
+    int rc = check_launch("slerp_stats_lerp_kernel");
+    if (rc) return rc;
+    slerp_coef_kernel<<<coef_grid(nseg), kBlock, 0, s>>>(partial, seg_first_chunk, nseg, t, (float)dot_threshold,
+                                                         (float)eps, coef, dot_out, redo);
+    rc = check_launch("slerp_coef_kernel");
+    if (rc) return rc;
+    if (in_dt == EDT_F32 && out_dt == EDT_F32)
+        slerp_blend_kernel<EDT_F32, EDT_F32><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, nullptr, redo);
+    else if (in_dt == EDT_F32)
+        slerp_blend_kernel<EDT_F32, EDT_BF16><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, nullptr, redo);
+    else if (out_dt == EDT_F32)
+        slerp_blend_kernel<EDT_BF16, EDT_F32><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, nullptr, redo);
+    else
+        slerp_blend_kernel<EDT_BF16, EDT_BF16><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, nullptr, redo);
+    return check_launch("slerp_blend_kernel");
 }
 
 int edt_slerp_merge_list(const void* const* v0_t, const void* const* v1_t, int in_dt, void* const* out_t,

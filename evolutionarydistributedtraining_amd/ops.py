@@ -190,10 +190,35 @@ def make_slerp_plan(seg_offsets: list[int], device: torch.device,
                      torch.empty(max(1, nseg), dtype=torch.float32, device=device), nchunks, relative)
 
 
+def _speculation_pays(plan: SlerpPlan, in_bytes: int, out_bytes: int) -> bool:
+    """Whether the speculative form is cheaper for the next merge on this plan, judged from the
+    dots the previous merge on it produced (both forms write them): with a fraction f of the
+    elements in SLERP-branch segments it moves (1 + f)(2 b_in + b_out) bytes per element against
+    4 b_in + b_out. No previous merge: speculate (EDT parents share a lineage)."""
+    if getattr(plan, "_last_thr", None) is None:
+        return True
+    import numpy as np
+    dots = plan.dots[:plan.nseg].cpu().numpy()
+    sizes = np.diff(np.asarray(plan.seg_offsets, dtype=np.int64))
+    total = max(1, int(sizes.sum()))
+    f = float(sizes[np.abs(dots) <= plan._last_thr].sum()) / total
+    return (1 + f) * (2 * in_bytes + out_bytes) < 4 * in_bytes + out_bytes
+
+
+def _overlap(a: torch.Tensor, b: torch.Tensor) -> bool:
+    a0, b0 = a.data_ptr(), b.data_ptr()
+    return a0 < b0 + b.numel() * b.element_size() and b0 < a0 + a.numel() * a.element_size()
+
+
 def slerp_arena(plan: SlerpPlan, v0: torch.Tensor, v1: torch.Tensor, out: torch.Tensor,
-                t: torch.Tensor, dot_threshold: float = 0.9995, eps: float = 1e-8) -> None:
+                t: torch.Tensor, dot_threshold: float = 0.9995, eps: float = 1e-8,
+                speculate: bool | None = None) -> None:
     """SLERP every segment of v0/v1 with its own t (float64 device tensor [nseg]) into out
-    (EDT_RL/crossover.py:11-43): chunk sums, per-segment coefficients, blend (edt_slerp_merge)."""
+    (EDT_RL/crossover.py:11-43): chunk sums, per-segment coefficients, blend (edt_slerp_merge).
+    speculate: True = edt_slerp_merge_speculative (lerp-branch output written in the stats pass,
+    only SLERP-branch segments blended again); False = the two-pass form; None = whichever the
+    previous merge on this plan says is cheaper. Bit-identical results either way; an output
+    that overlaps a parent always takes the two-pass form."""
     lib = L.lib()
     L.require_device(v0, v1, out, t)
     if v1.dtype != v0.dtype or v0.numel() != plan.seg_offsets[-1] or v1.numel() != v0.numel() \
@@ -203,10 +228,25 @@ def slerp_arena(plan: SlerpPlan, v0: torch.Tensor, v1: torch.Tensor, out: torch.
         raise L.EdtError("t must be a float64 device tensor with one value per segment")
     if plan.relative:
         raise L.EdtError("a relative (tensor-list) plan drives slerp_list, not slerp_arena")
-    L.check(lib.edt_slerp_merge(L.ptr(v0), L.ptr(v1), L.dtype_code(v0), L.ptr(out), L.dtype_code(out),
-                                L.ptr(plan.chunks), plan.nchunks, L.ptr(plan.seg_first), plan.nseg, L.ptr(t),
-                                float(dot_threshold), float(eps), L.ptr(plan.partial), L.ptr(plan.coef),
-                                L.ptr(plan.dots), L.stream_ptr(v0.device)), "edt_slerp_merge")
+    if speculate is None:
+        speculate = _speculation_pays(plan, v0.element_size(), out.element_size())
+    if speculate and (_overlap(out, v0) or _overlap(out, v1)):
+        speculate = False
+    if speculate:
+        redo = getattr(plan, "_redo", None)
+        if redo is None:
+            redo = plan._redo = torch.empty(max(1, plan.nseg), dtype=torch.int32, device=v0.device)
+        L.check(lib.edt_slerp_merge_speculative(
+            L.ptr(v0), L.ptr(v1), L.dtype_code(v0), L.ptr(out), L.dtype_code(out), L.ptr(plan.chunks), plan.nchunks,
+            L.ptr(plan.seg_first), plan.nseg, L.ptr(t), float(dot_threshold), float(eps), L.ptr(plan.partial),
+            L.ptr(plan.coef), L.ptr(plan.dots), L.ptr(redo), v0.numel(), L.stream_ptr(v0.device)),
+            "edt_slerp_merge_speculative")
+    else:
+        L.check(lib.edt_slerp_merge(L.ptr(v0), L.ptr(v1), L.dtype_code(v0), L.ptr(out), L.dtype_code(out),
+                                    L.ptr(plan.chunks), plan.nchunks, L.ptr(plan.seg_first), plan.nseg, L.ptr(t),
+                                    float(dot_threshold), float(eps), L.ptr(plan.partial), L.ptr(plan.coef),
+                                    L.ptr(plan.dots), L.stream_ptr(v0.device)), "edt_slerp_merge")
+    plan._last_thr = float(dot_threshold)
 
 
 def slerp_list(plan: SlerpPlan, v0s: list[torch.Tensor], v1s: list[torch.Tensor], outs: list[torch.Tensor],

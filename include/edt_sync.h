@@ -169,6 +169,19 @@ int edt_slerp_merge(const void* v0, const void* v1, int in_dt, void* out, int ou
                     const double* t, double dot_threshold, double eps, double* partial, float* coef,
                     float* dot_out, void* stream);
 
+/* edt_slerp_merge with a speculative first pass: the chunk sums and, in the same pass, the
+ * lerp-branch output (1-t) v0 + t v1 of every segment; the coefficients then flag (redo[s] = 1,
+ * nseg int32 of device workspace) the segments whose |dot| <= dot_threshold, and only their
+ * chunks are blended again with the SLERP coefficients. Parents of one lineage (fine-tunes of a
+ * common base: |dot| > 0.9995 on most tensors, EDT_RL/crossover.py:31-32) are merged in ONE pass
+ * over them (2 b_in + b_out per element instead of 4 b_in + b_out); segments that take the SLERP
+ * branch cost a second full pass. Outputs, sums and dots are bit-identical to edt_slerp_merge.
+ * `out` must not overlap the parents (n elements each). */
+int edt_slerp_merge_speculative(const void* v0, const void* v1, int in_dt, void* out, int out_dt,
+                                const uint64_t* chunk_desc, int64_t nchunks, const int32_t* seg_first_chunk,
+                                int nseg, const double* t, double dot_threshold, double eps, double* partial,
+                                float* coef, float* dot_out, int32_t* redo, uint64_t n, void* stream);
+
 /* Tensor-list form of edt_slerp_merge: segment i is its own tensor pair v0_t[i], v1_t[i] and is
  * written to out_t[i] (host arrays of nseg device pointers, each 16-byte aligned; NULL only for
  * empty segments), e.g. two

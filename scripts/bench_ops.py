@@ -100,21 +100,26 @@ def main():
         P = lay.total
         v0 = torch.empty(P, dtype=bf, device=dev)
         v1 = torch.empty(P, dtype=bf, device=dev)
-        step = 1 << 28
-        for s in range(0, P, step):
-            e = min(P, s + step)
-            x = torch.randn(e - s, device=dev) * 0.02
-            v0[s:e] = x.to(bf)
-            v1[s:e] = (x + torch.randn(e - s, device=dev) * 1e-3).to(bf)
-            del x
         out = torch.empty(P, dtype=bf, device=dev)
         plan = ops.make_slerp_plan(lay.offsets, dev)
         t = torch.full((len(lay),), 0.5, dtype=torch.float64, device=dev)
-        ms = timed(lambda: ops.slerp_arena(plan, v0, v1, out, t), a.iters)
-        gbs = 6 * P / ms / 1e6
-        res["slerp"] = {"P": P, "segments": len(lay), "chunks": plan.nchunks, "ms": round(ms, 3),
-                        "GBps_algorithmic": round(gbs, 1), "frac": round(gbs / PEAK, 4), "bytes_per_elem": 6,
-                        "GBps_moved_2pass": round(10 * P / ms / 1e6, 1)}
+        # far: v1 = v0 + 5 % noise (|dot| ~ 0.9988, SLERP branch everywhere);
+        # lineage: 0.5 % noise (|dot| ~ 0.99999, the lerp branch: fine-tunes of one base)
+        for parents, rel in (("far", 0.05), ("lineage", 0.005)):
+            step = 1 << 28
+            for s0 in range(0, P, step):
+                e = min(P, s0 + step)
+                x = torch.randn(e - s0, device=dev) * 0.02
+                v0[s0:e] = x.to(bf)
+                v1[s0:e] = (x + torch.randn(e - s0, device=dev) * 0.02 * rel).to(bf)
+                del x
+            for spec in (False, True):
+                ms = timed(lambda: ops.slerp_arena(plan, v0, v1, out, t, speculate=spec), a.iters)
+                gbs = 6 * P / ms / 1e6
+                res[f"slerp/{parents}/{'speculative' if spec else 'two_pass'}"] = {
+                    "P": P, "segments": len(lay), "chunks": plan.nchunks, "ms": round(ms, 3),
+                    "GBps_algorithmic": round(gbs, 1), "frac": round(gbs / PEAK, 4), "bytes_per_elem": 6,
+                    "lerp_branch_segments": int((plan.dots[:len(lay)].abs() > 0.9995).sum().item())}
     print(json.dumps(res))
 
 

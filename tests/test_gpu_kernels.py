@@ -469,6 +469,57 @@ def test_pair_merge_population_matches_per_child(dev, ops, gdt, wdt, n):
         assert not torch.isnan(m.float()).any()
 
 
+@pytest.mark.parametrize("in_dt,out_dt", [(torch.float32, torch.float32), (torch.bfloat16, torch.float32),
+                                          (torch.bfloat16, torch.bfloat16)])
+def test_slerp_speculative_matches_two_pass(dev, ops, in_dt, out_dt):
+    """edt_slerp_merge_speculative (lerp output written in the stats pass, SLERP-branch segments
+    blended again) is bit-identical to edt_slerp_merge: outputs and dots, with segments on both
+    sides of the 0.9995 threshold, ragged sizes, a zero segment; the adaptive choice picks the
+    cheaper form from the previous merge's dots; an output overlapping a parent is refused by
+    the speculative entry and handled by the two-pass form."""
+    g = torch.Generator().manual_seed(77)
+    sizes = [0, 1, 7, 33, 4096, 70_001, 0, 129, 200_003, 65_536, 131_073]
+    offs = [0]
+    for x in sizes:
+        offs.append(offs[-1] + x)
+    v0 = torch.randn(offs[-1], generator=g) * 0.02
+    v1 = v0.clone()
+    rel = [0.1, 0.001, 0.2, 0.001, 0.05, 0.005, 0.1, 0.3, 0.002, 0.02, 0.0005]   # per segment: far or near
+    for s_, r in enumerate(rel):
+        a, b = offs[s_], offs[s_ + 1]
+        v1[a:b] += torch.randn(b - a, generator=g) * 0.02 * r
+    v0[offs[7]:offs[8]] = 0
+    v0, v1 = v0.to(in_dt).to(dev), v1.to(in_dt).to(dev)
+    ts = torch.tensor([0.5, 0.0, 1.0, 0.43, 0.5, 0.7, 0.5, 0.2, 0.9, 0.3, 0.6], dtype=torch.float64).to(dev)
+    plan = ops.make_slerp_plan(offs, dev, chunk_elems=4096)
+    ref = torch.empty(offs[-1], dtype=out_dt, device=dev)
+    ops.slerp_arena(plan, v0, v1, ref, ts, speculate=False)
+    ref_dots = plan.dots.cpu().clone()
+    d = ref_dots[:len(sizes)].abs()
+    assert (d > 0.9995).any() and (d <= 0.9995).any()          # both branches present
+    got = torch.full_like(ref, float("nan"))
+    ops.slerp_arena(plan, v0, v1, got, ts, speculate=True)
+    assert torch.equal(bits(got.cpu()), bits(ref.cpu()))
+    assert torch.equal(plan.dots.cpu(), ref_dots)
+    # adaptive: here most elements sit in SLERP-branch segments -> the two-pass form pays
+    from evolutionarydistributedtraining_amd.ops import _speculation_pays
+    big_slerp = sum(x for x, r in zip(sizes, rel) if r >= 0.02) > 0.67 * offs[-1]
+    assert _speculation_pays(plan, v0.element_size(), ref.element_size()) == (not big_slerp)
+    if in_dt == out_dt:                                        # in place into parent 1: two-pass form
+        v0c = v0.clone()
+        ops.slerp_arena(plan, v0c, v1, v0c, ts, speculate=True)
+        assert torch.equal(bits(v0c.cpu()), bits(ref.cpu()))
+        from evolutionarydistributedtraining_amd import EdtError
+        from evolutionarydistributedtraining_amd import _lib as L
+        rc = L.lib().edt_slerp_merge_speculative(L.ptr(v0), L.ptr(v1), L.dtype_code(v0), L.ptr(v0), L.dtype_code(v0),
+                                                 L.ptr(plan.chunks), plan.nchunks, L.ptr(plan.seg_first), plan.nseg,
+                                                 L.ptr(ts), 0.9995, 1e-8, L.ptr(plan.partial), L.ptr(plan.coef), None,
+                                                 L.ptr(plan._redo), v0.numel(), L.stream_ptr(dev))
+        assert rc != 0
+        with pytest.raises(EdtError):
+            L.check(rc, "edt_slerp_merge_speculative")
+
+
 def test_errors_are_raised(dev, ops):
     from evolutionarydistributedtraining_amd import EdtError
     th = torch.zeros(16, device=dev)
