@@ -1044,6 +1044,8 @@ struct BlendChildren {
     const void* v1[kBlendMaxChildren];
     void* out[kBlendMaxChildren];
     const float* coef[kBlendMaxChildren];     // [nseg][2] of the child
+    const int32_t* redo[kBlendMaxChildren];   // [nseg] of the child, or null: blend every segment
+    double* partial[kBlendMaxChildren];       // [nchunks][3] of the child (speculative stats pass)
     int nchildren;
 };
 
@@ -1056,6 +1058,7 @@ __global__ __launch_bounds__(kBlock) void slerp_blend_population_kernel(BlendChi
     const int64_t c = (int64_t)((blockIdx.x / per_group) * 8 + (r % 8));
     if (c >= nchunks) return;
     const uint64_t start = chunks[3 * c], len = chunks[3 * c + 1], seg = chunks[3 * c + 2];
+    if (B.redo[child] && !B.redo[child][seg]) return;      // speculative lerp output stands
     const void* v0 = B.v0[child];
     const void* v1 = B.v1[child];
     void* out = B.out[child];
@@ -1073,6 +1076,75 @@ __global__ __launch_bounds__(kBlock) void slerp_blend_population_kernel(BlendChi
     if ((uint64_t)threadIdx.x < nh + nt) {
         const uint64_t i = threadIdx.x < nh ? start + threadIdx.x : t_beg + (threadIdx.x - nh);
         lerp_elems<IDT, ODT, EDT_F32, 1>(v0, v1, out, i, c0, c1);
+    }
+}
+
+// Speculative population pass: block (chunk, child) with the co-located placement above; each
+// forms its child's chunk sums exactly as chunk_sums() does and writes the lerp-branch output in
+// the same pass (as slerp_stats_lerp_kernel). Shared parents cross HBM once for all children.
+template <int IDT, int ODT>
+__global__ __launch_bounds__(kBlock) void slerp_pop_stats_lerp_kernel(BlendChildren B, const uint64_t* chunks,
+                                                                      int64_t nchunks, const double* tvals) {
+    __shared__ double red[3][kBlock / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t per_group = 8ull * (uint64_t)B.nchildren;
+    const uint64_t r = blockIdx.x % per_group;
+    const int child = (int)(r / 8);
+    const int64_t c = (int64_t)((blockIdx.x / per_group) * 8 + (r % 8));
+    if (c >= nchunks) return;
+    const void* v0 = B.v0[child];
+    const void* v1 = B.v1[child];
+    void* out = B.out[child];
+    const uint64_t start = chunks[3 * c], end = start + chunks[3 * c + 1], seg = chunks[3 * c + 2];
+    const float l0 = (float)(1.0 - tvals[seg]), l1 = (float)tvals[seg];
+    double s00 = 0.0, s11 = 0.0, s01 = 0.0;
+    const uint64_t a = (start + kVec - 1) / kVec * kVec;
+    const uint64_t b = end / kVec * kVec;
+    if (a < b) {
+        for (uint64_t i = a + (uint64_t)threadIdx.x * kVec; i < b; i += (uint64_t)kBlock * kVec) {
+            float x[kVec], y[kVec], o[kVec];
+            ld<IDT, kVec>(v0, i, x);
+            ld<IDT, kVec>(v1, i, y);
+#pragma unroll
+            for (int j = 0; j < kVec; ++j) {
+                const double dx = x[j], dy = y[j];
+                s00 = __builtin_fma(dx, dx, s00);
+                s11 = __builtin_fma(dy, dy, s11);
+                s01 = __builtin_fma(dx, dy, s01);
+                o[j] = l0 * x[j] + l1 * y[j];
+            }
+            st<ODT, kVec>(out, i, o);
+        }
+    }
+    const uint64_t h_end = a < end ? a : end;
+    const uint64_t t_beg = b > a ? b : h_end;
+    const uint64_t nh = h_end - start, nt = end - t_beg;
+    if ((uint64_t)threadIdx.x < nh + nt) {
+        const uint64_t i = threadIdx.x < nh ? start + threadIdx.x : t_beg + (threadIdx.x - nh);
+        float x[1], y[1], o[1];
+        ld<IDT, 1>(v0, i, x);
+        ld<IDT, 1>(v1, i, y);
+        const double dx = x[0], dy = y[0];
+        s00 = __builtin_fma(dx, dx, s00);
+        s11 = __builtin_fma(dy, dy, s11);
+        s01 = __builtin_fma(dx, dy, s01);
+        o[0] = l0 * x[0] + l1 * y[0];
+        st<ODT, 1>(out, i, o);
+    }
+    s00 = wave_sum(s00);
+    s11 = wave_sum(s11);
+    s01 = wave_sum(s01);
+    if (lane == 0) { red[0][wave] = s00; red[1][wave] = s11; red[2][wave] = s01; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double* pc = B.partial[child] + 3 * c;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            double acc = 0.0;
+#pragma unroll
+            for (int w = 0; w < kBlock / 64; ++w) acc += red[q][w];
+            pc[q] = acc;
+        }
     }
 }
 
@@ -1794,6 +1866,74 @@ int edt_slerp_merge_speculative(const void* v0, const void* v1, int in_dt, void*
     else
         slerp_blend_kernel<EDT_BF16, EDT_BF16><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, nullptr, redo);
     return check_launch("slerp_blend_kernel");
+}
+
+int edt_slerp_population_speculative(const void* const* members, int nmembers, int in_dt, const int32_t* pairs,
+                                     int npairs, void* const* outs, int out_dt, const uint64_t* chunk_desc,
+                                     int64_t nchunks, const int32_t* seg_first_chunk, int nseg, const double* t,
+                                     double dot_threshold, double eps, double* partial, float* coef,
+                                     float* dot_out, int32_t* redo, uint64_t n, void* stream) {
+    g_err[0] = 0;
+    if ((in_dt | out_dt) & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
+    if (nmembers < 1 || npairs < 0 || nseg < 0 || nchunks < 0) return fail(EDT_ERR_ARG, "bad count");
+    if (npairs == 0 || nseg == 0 || nchunks == 0) return EDT_OK;
+    if (!members || !pairs || !outs || !chunk_desc || !seg_first_chunk || !t || !partial || !coef || !redo)
+        return fail(EDT_ERR_ARG, "null buffer");
+    const uint64_t isz = in_dt == EDT_BF16 ? 2 : 4, osz = out_dt == EDT_BF16 ? 2 : 4;
+    for (int m = 0; m < nmembers; ++m)
+        if (!members[m] || !aligned16(members[m])) return fail(EDT_ERR_ARG, "member %d is null or not 16-byte aligned", m);
+    for (int q = 0; q < npairs; ++q) {
+        const int i = pairs[2 * q], j = pairs[2 * q + 1];
+        if (i < 0 || j < 0 || i >= nmembers || j >= nmembers) return fail(EDT_ERR_ARG, "pair %d: member out of range", q);
+        if (!outs[q] || !aligned16(outs[q])) return fail(EDT_ERR_ARG, "output %d is null or not 16-byte aligned", q);
+        const uintptr_t o0 = reinterpret_cast<uintptr_t>(outs[q]), o1 = o0 + n * osz;
+        for (int m = 0; m < nmembers; ++m) {           // outputs are written before the redo pass
+            const uintptr_t p0 = reinterpret_cast<uintptr_t>(members[m]), p1 = p0 + n * isz;
+            if (p0 < o1 && o0 < p1) return fail(EDT_ERR_ARG, "output %d overlaps member %d", q, m);
+        }
+    }
+    hipStream_t s = (hipStream_t)stream;
+    for (int pass = 0; pass < 2; ++pass) {
+        for (int q0 = 0; q0 < npairs; q0 += kBlendMaxChildren) {
+            BlendChildren B;
+            memset(&B, 0, sizeof(B));
+            B.nchildren = npairs - q0 < kBlendMaxChildren ? npairs - q0 : kBlendMaxChildren;
+            for (int k = 0; k < B.nchildren; ++k) {
+                const int q = q0 + k;
+                B.v0[k] = members[pairs[2 * q]];
+                B.v1[k] = members[pairs[2 * q + 1]];
+                B.out[k] = outs[q];
+                B.coef[k] = coef + 2 * (size_t)nseg * q;
+                B.redo[k] = redo + (size_t)nseg * q;
+                B.partial[k] = partial + 3 * (size_t)nchunks * q;
+            }
+            const uint64_t blocks = ((uint64_t)nchunks + 7) / 8 * 8ull * (uint64_t)B.nchildren;
+            if (blocks > 0x7fffffffull) return fail(EDT_ERR_ARG, "too many chunks for one launch");
+            const unsigned gb = (unsigned)blocks;
+#define EDT_SPEC_POP(KERNEL, ...)                                                                   \
+    do {                                                                                            \
+        if (in_dt == EDT_F32 && out_dt == EDT_F32) KERNEL<EDT_F32, EDT_F32><<<gb, kBlock, 0, s>>>(__VA_ARGS__);   \
+        else if (in_dt == EDT_F32) KERNEL<EDT_F32, EDT_BF16><<<gb, kBlock, 0, s>>>(__VA_ARGS__);                  \
+        else if (out_dt == EDT_F32) KERNEL<EDT_BF16, EDT_F32><<<gb, kBlock, 0, s>>>(__VA_ARGS__);                 \
+        else KERNEL<EDT_BF16, EDT_BF16><<<gb, kBlock, 0, s>>>(__VA_ARGS__);                                       \
+    } while (0)
+            if (pass == 0) EDT_SPEC_POP(slerp_pop_stats_lerp_kernel, B, chunk_desc, nchunks, t);
+            else EDT_SPEC_POP(slerp_blend_population_kernel, B, chunk_desc, nchunks);
+#undef EDT_SPEC_POP
+            int rc = check_launch(pass == 0 ? "slerp_pop_stats_lerp_kernel" : "slerp_blend_population_kernel");
+            if (rc) return rc;
+        }
+        if (pass == 0) {
+            for (int q = 0; q < npairs; ++q) {
+                slerp_coef_kernel<<<coef_grid(nseg), kBlock, 0, s>>>(
+                    partial + 3 * (size_t)nchunks * q, seg_first_chunk, nseg, t, (float)dot_threshold, (float)eps,
+                    coef + 2 * (size_t)nseg * q, dot_out ? dot_out + (size_t)nseg * q : nullptr, redo + (size_t)nseg * q);
+                int rc = check_launch("slerp_coef_kernel");
+                if (rc) return rc;
+            }
+        }
+    }
+    return EDT_OK;
 }
 
 int edt_slerp_merge_list(const void* const* v0_t, const void* const* v1_t, int in_dt, void* const* out_t,

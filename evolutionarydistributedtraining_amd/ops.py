@@ -278,16 +278,21 @@ def slerp_list(plan: SlerpPlan, v0s: list[torch.Tensor], v1s: list[torch.Tensor]
 
 
 def slerp_population(plan: SlerpPlan, members: list[torch.Tensor], pairs, outs: list[torch.Tensor],
-                     t: torch.Tensor, dot_threshold: float = 0.9995, eps: float = 1e-8) -> torch.Tensor:
+                     t: torch.Tensor, dot_threshold: float = 0.9995, eps: float = 1e-8,
+                     speculate: bool | None = None) -> torch.Tensor:
     """SLERP child q of members[pairs[q][0]], members[pairs[q][1]] into outs[q], for every q
-    (EDT_RL/edt.py:286-299 -> EDT_RL/crossover.py:84-135 per child), with ONE stats pass over
-    the members (their Gram matrix per chunk) instead of a stats pass per child
-    (edt_slerp_population; at most 8 members). Results are bit-identical to slerp_arena per
-    child. Returns the per-child, per-segment fp32 dots ([npairs, nseg])."""
+    (EDT_RL/edt.py:286-299 -> EDT_RL/crossover.py:84-135 per child). Two forms, bit-identical to
+    slerp_arena per child:
+      speculate=False  edt_slerp_population: ONE Gram stats pass over the (<= 8) members, then
+                       one co-located blend launch for all children;
+      speculate=True   edt_slerp_population_speculative: one co-located pass forms every child's
+                       sums and writes its lerp-branch output, then only SLERP-branch segments
+                       are blended again (parents of one lineage: a single pass);
+      None             speculate unless the previous call on this plan had half or more of its
+                       child elements in SLERP-branch segments.
+    Returns the per-child, per-segment fp32 dots ([npairs, nseg])."""
     lib = L.lib()
     M, Q = len(members), len(pairs)
-    if not 1 <= M <= 8:
-        raise L.EdtError(f"slerp_population takes 1..8 members, got {M} (use slerp_arena per child)")
     if plan.relative:
         raise L.EdtError("slerp_population runs over flat member arenas (a non-relative plan)")
     if len(outs) != Q:
@@ -299,20 +304,45 @@ def slerp_population(plan: SlerpPlan, members: list[torch.Tensor], pairs, outs: 
         raise L.EdtError("members / outputs must match the plan's layout and share one dtype each")
     if t.dtype != torch.float64 or t.numel() < plan.nseg:
         raise L.EdtError("t must be a float64 device tensor with one value per segment")
+    if speculate is None:
+        prev = getattr(plan, "_pop_dots", None)
+        if prev is None or getattr(plan, "_last_thr", None) is None:
+            speculate = True
+        else:
+            import numpy as np
+            d = prev.cpu().numpy()
+            sizes = np.diff(np.asarray(plan.seg_offsets, dtype=np.int64))
+            f = float((sizes[None, :] * (np.abs(d) <= plan._last_thr)).sum()) / max(1, int(sizes.sum()) * d.shape[0])
+            speculate = f < 0.5
+    if any(_overlap(o, m) for o in outs for m in members):
+        speculate = False
+    if not speculate and not 1 <= M <= 8:
+        raise L.EdtError(f"the Gram form takes 1..8 members, got {M}")
     dev = t.device
-    need = int(lib.edt_slerp_population_gram_doubles(M, plan.nchunks))
-    gram = getattr(plan, "_gram", None)
-    if gram is None or gram.numel() < max(1, need):
-        gram = plan._gram = torch.empty(max(1, need), dtype=torch.float64, device=dev)
     coef = torch.empty((max(1, Q), max(1, plan.nseg), 2), dtype=torch.float32, device=dev)
     dots = torch.empty((max(1, Q), max(1, plan.nseg)), dtype=torch.float32, device=dev)
     flat_pairs = (ctypes.c_int32 * max(1, 2 * Q))(*[int(x) for p in pairs for x in p])
-    L.check(lib.edt_slerp_population(L.ptr_array(members), M, L.dtype_code(in_dt), flat_pairs, Q,
-                                     L.ptr_array(outs), L.dtype_code(out_dt), L.ptr(plan.chunks), plan.nchunks,
-                                     L.ptr(plan.seg_first), plan.nseg, L.ptr(t), float(dot_threshold), float(eps),
-                                     L.ptr(gram), L.ptr(coef), L.ptr(dots), L.stream_ptr(dev)),
-            "edt_slerp_population")
-    return dots[:Q, :plan.nseg]
+    if speculate:
+        part = torch.empty(max(1, Q * plan.nchunks * 3), dtype=torch.float64, device=dev)
+        redo = torch.empty(max(1, Q * plan.nseg), dtype=torch.int32, device=dev)
+        L.check(lib.edt_slerp_population_speculative(
+            L.ptr_array(members), M, L.dtype_code(in_dt), flat_pairs, Q, L.ptr_array(outs), L.dtype_code(out_dt),
+            L.ptr(plan.chunks), plan.nchunks, L.ptr(plan.seg_first), plan.nseg, L.ptr(t), float(dot_threshold),
+            float(eps), L.ptr(part), L.ptr(coef), L.ptr(dots), L.ptr(redo), n, L.stream_ptr(dev)),
+            "edt_slerp_population_speculative")
+    else:
+        need = int(lib.edt_slerp_population_gram_doubles(M, plan.nchunks))
+        gram = getattr(plan, "_gram", None)
+        if gram is None or gram.numel() < max(1, need):
+            gram = plan._gram = torch.empty(max(1, need), dtype=torch.float64, device=dev)
+        L.check(lib.edt_slerp_population(L.ptr_array(members), M, L.dtype_code(in_dt), flat_pairs, Q,
+                                         L.ptr_array(outs), L.dtype_code(out_dt), L.ptr(plan.chunks), plan.nchunks,
+                                         L.ptr(plan.seg_first), plan.nseg, L.ptr(t), float(dot_threshold), float(eps),
+                                         L.ptr(gram), L.ptr(coef), L.ptr(dots), L.stream_ptr(dev)),
+                "edt_slerp_population")
+    plan._pop_dots = dots[:Q, :plan.nseg]
+    plan._last_thr = float(dot_threshold)
+    return plan._pop_dots
 
 
 def pair_merge_population(children, lr: float, momentum_coef: float, nesterov: bool) -> None:

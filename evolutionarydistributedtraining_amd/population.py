@@ -291,20 +291,24 @@ class ResidentPopulation:
                          self.lr, self.momentum, self.nesterov, momentum_in=ch["momentum_in"])
 
     def _slerp_children(self, pairs, got):
-        """SLERP every local child. With at most 8 distinct parent arenas on this rank (all the
-        members of a population of <= 8 on one GPU) one Gram pass over them serves every child
-        (ops.slerp_population: each member read once for the stats instead of twice per child);
-        otherwise one edt_slerp_merge per child. Bit-identical either way."""
+        """SLERP every local child in one population call (ops.slerp_population, bit-identical to
+        one edt_slerp_merge per child): shared parents are read once per pass — by the Gram stats
+        pass (<= 8 distinct parents) or the speculative co-located pass, which ops picks from the
+        previous generation's dots (parents of one lineage take the lerp branch: one pass). More
+        than 8 distinct parents: the speculative form (<= 16 local children), else per child."""
         k = self.kernels
         if self._plan is None:
             self._plan = k.make_slerp_plan(self.layout.offsets, self.device)
         local = self.local_members()
         srcs = sorted({m for c in local for m in pairs[c]})
-        if len(srcs) <= 8 and hasattr(k, "slerp_population"):
-            where = {m: q for q, m in enumerate(srcs)}
-            k.slerp_population(self._plan, [got[m][0] for m in srcs],
-                               [(where[pairs[c][0]], where[pairs[c][1]]) for c in local],
-                               [self._child[self._local(c)] for c in local], self._t, self.dot_threshold, self.eps)
+        where = {m: q for q, m in enumerate(srcs)}
+        args = (self._plan, [got[m][0] for m in srcs], [(where[pairs[c][0]], where[pairs[c][1]]) for c in local],
+                [self._child[self._local(c)] for c in local], self._t, self.dot_threshold, self.eps)
+        if hasattr(k, "slerp_population") and len(srcs) <= 8:
+            k.slerp_population(*args)
+            return
+        if hasattr(k, "slerp_population") and len(local) <= 16:
+            k.slerp_population(*args, speculate=True)
             return
         for c in local:
             i, j = pairs[c]

@@ -211,6 +211,18 @@ int edt_slerp_population(const void* const* members, int nmembers, int in_dt, co
                          const int32_t* seg_first_chunk, int nseg, const double* t, double dot_threshold,
                          double eps, double* gram, float* coef, float* dot_out, void* stream);
 
+/* edt_slerp_population with edt_slerp_merge_speculative's first pass: one co-located launch
+ * (every child of a chunk on one XCD, shared parents read once) forms each child's chunk sums and
+ * writes its lerp-branch output; per child the coefficients flag (redo: [npairs][nseg] int32) the
+ * SLERP-branch segments, which one co-located launch blends again. partial: [npairs][nchunks][3]
+ * doubles. Outputs must not overlap any member (n elements each). Bit-identical to
+ * edt_slerp_merge per child. */
+int edt_slerp_population_speculative(const void* const* members, int nmembers, int in_dt, const int32_t* pairs,
+                                     int npairs, void* const* outs, int out_dt, const uint64_t* chunk_desc,
+                                     int64_t nchunks, const int32_t* seg_first_chunk, int nseg, const double* t,
+                                     double dot_threshold, double eps, double* partial, float* coef,
+                                     float* dot_out, int32_t* redo, uint64_t n, void* stream);
+
 /* ---- misc ---- */
 const char* edt_last_error(void);
 const char* edt_version(void);

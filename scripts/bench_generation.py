@@ -39,6 +39,9 @@ def main():
     ap.add_argument("--kinds", default="sgd,slerp")
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--members", default="lineage", choices=["lineage", "random"],
+                    help="lineage: one base + 0.5 %% per-member noise (fine-tunes of a common base: the "
+                         "SLERP takes the lerp branch); random: independent members (SLERP branch)")
     a = ap.parse_args()
     from evolutionarydistributedtraining_amd.layouts import LAYOUTS
     from evolutionarydistributedtraining_amd.merge import merge_plan
@@ -46,7 +49,7 @@ def main():
     dev = torch.device("cuda:0")
     layout = LAYOUTS[a.layout]()
     n, P = layout.total, a.population
-    out = {"layout": a.layout, "params": n, "population": P, "results": {}}
+    out = {"layout": a.layout, "params": n, "population": P, "members": a.members, "results": {}}
     for kind in a.kinds.split(","):
         random.seed(0)
         if kind == "sgd":
@@ -63,8 +66,13 @@ def main():
             pop = ResidentPopulation(layout, torch.bfloat16, dev, genomes, kind="slerp", seg_t=t)
             arenas = [pop.params(m) for m in range(P)]
         g = torch.Generator(device=dev).manual_seed(1)
+        common = torch.randn(n, generator=g, device=dev) * 0.02 if a.members == "lineage" else None
         for x in arenas:
-            x.copy_(torch.randn(n, generator=g, device=dev) * 0.02)
+            if common is None:
+                x.copy_(torch.randn(n, generator=g, device=dev) * 0.02)
+            else:
+                x.copy_(common + torch.randn(n, generator=g, device=dev) * 0.02 * 0.005)
+        del common
         fitness = [float(m) for m in range(P)]
         pop.step(fitness)                      # generation 0 (first-step momentum), warm-up
         torch.cuda.synchronize()
@@ -91,7 +99,14 @@ def main():
         if kind == "sgd":
             floor = n * (len(parents) * 2 * 2 + len(donors) * 2 + P * 2 * 2)
         else:
-            floor = n * (2 * len(parents) * 2 + P * 2)    # Gram pass + blend pass, bf16 in / out
+            # two passes (Gram + blend) or, speculative, one pass + a second over the SLERP-branch
+            # share f of the elements: the cheaper of the two (the form ops picks)
+            import numpy as np
+            d = pop._plan._pop_dots.cpu().numpy()
+            sizes = np.diff(np.asarray(layout.offsets, dtype=np.int64))
+            f = float((sizes[None, :] * (np.abs(d) <= 0.9995)).sum()) / (int(sizes.sum()) * d.shape[0])
+            one = n * (len(parents) * 2 + P * 2)
+            floor = int(min(2 * n * len(parents) * 2 + n * P * 2, (1 + f) * one))
         out["results"][kind] = {
             "generation_ms": round(ms, 3), "per_child_ms": round(ms / P, 4),
             "survey_bytes": survey, "survey_TBps": round(survey / ms / 1e9, 3),

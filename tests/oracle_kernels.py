@@ -15,7 +15,7 @@ class OracleKernels:
             a, b = plan[s], plan[s + 1]
             out[a:b] = self.o.slerp(float(t[s]), v0[a:b], v1[a:b], thr, eps).to(out.dtype)
 
-    def slerp_population(self, plan, members, pairs, outs, t, thr, eps):
+    def slerp_population(self, plan, members, pairs, outs, t, thr, eps, speculate=None):
         for (i, j), out in zip(pairs, outs):
             self.slerp_arena(plan, members[i], members[j], out, t, thr, eps)
 

@@ -417,7 +417,8 @@ def test_slerp_population_matches_per_child(dev, ops, in_dt, out_dt, nmem):
     for x in sizes:
         offs.append(offs[-1] + x)
     base = torch.randn(offs[-1], generator=g) * 0.02
-    mem = [base + torch.randn(offs[-1], generator=g) * 1e-3 * (m + 1) for m in range(nmem)]
+    # members 0-2 near each other (lerp branch on most segments), the rest farther (SLERP branch)
+    mem = [base + torch.randn(offs[-1], generator=g) * (1e-5 if m < 3 else 1e-3) * (m + 1) for m in range(nmem)]
     if nmem > 1:
         mem[1][offs[4]:offs[5]] = 2 * mem[0][offs[4]:offs[5]]      # parallel -> lerp branch
     mem[0][offs[7]:offs[8]] = 0                                      # zero tensor
@@ -425,13 +426,14 @@ def test_slerp_population_matches_per_child(dev, ops, in_dt, out_dt, nmem):
     pairs = [(i % nmem, (3 * i + 1) % nmem) for i in range(max(nmem, 3))] + [(0, 0)]
     ts = torch.tensor([0.5, 0.0, 1.0, 0.43333333333333335, 0.5, 0.7, 0.5, 0.2, 0.9], dtype=torch.float64).to(dev)
     plan = ops.make_slerp_plan(offs, dev, chunk_elems=4096)
-    outs = [torch.full((offs[-1],), float("nan"), dtype=out_dt, device=dev) for _ in pairs]
-    dots = ops.slerp_population(plan, mem, pairs, outs, ts)
-    for q, (i, j) in enumerate(pairs):
-        want = torch.empty(offs[-1], dtype=out_dt, device=dev)
-        ops.slerp_arena(plan, mem[i], mem[j], want, ts)
-        assert torch.equal(bits(outs[q].cpu()), bits(want.cpu())), (q, i, j)
-        assert torch.equal(dots[q].cpu(), plan.dots.cpu()), (q, i, j)
+    for spec in (False, True):
+        outs = [torch.full((offs[-1],), float("nan"), dtype=out_dt, device=dev) for _ in pairs]
+        dots = ops.slerp_population(plan, mem, pairs, outs, ts, speculate=spec).clone()
+        for q, (i, j) in enumerate(pairs):
+            want = torch.empty(offs[-1], dtype=out_dt, device=dev)
+            ops.slerp_arena(plan, mem[i], mem[j], want, ts, speculate=False)
+            assert torch.equal(bits(outs[q].cpu()), bits(want.cpu())), (spec, q, i, j)
+            assert torch.equal(dots[q].cpu(), plan.dots[:len(sizes)].cpu()), (spec, q, i, j)
 
 
 @pytest.mark.parametrize("gdt,wdt", REGIMES)
