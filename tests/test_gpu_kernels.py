@@ -522,6 +522,44 @@ def test_slerp_speculative_matches_two_pass(dev, ops, in_dt, out_dt):
             L.check(rc, "edt_slerp_merge_speculative")
 
 
+def test_population_kernels_edges(dev, ops):
+    """Population entry points: empty arenas are a no-op, more children than one launch takes is
+    refused by the C ABI (the Python layers fall back to per-child calls), an output that is
+    also an input is refused."""
+    from evolutionarydistributedtraining_amd import EdtError
+    from evolutionarydistributedtraining_amd import _lib as L
+    bf = torch.bfloat16
+    e = torch.empty(0, dtype=bf, device=dev)
+    ops.pair_merge_population([{"b1": e, "b2": e, "m1": e, "m2": e, "out": e, "momentum": None,
+                                "momentum_in": None, "has_momentum": False}], 0.7, 0.0, False)
+    x = [torch.randn(64, device=dev).to(bf) for _ in range(4)]
+    ch = lambda out: {"b1": x[0], "b2": x[1], "m1": x[2], "m2": x[3], "out": out, "momentum": None,
+                      "momentum_in": None, "has_momentum": False}
+    with pytest.raises(EdtError):                    # 17 children: beyond one launch
+        ops.pair_merge_population([ch(torch.empty(64, dtype=bf, device=dev)) for _ in range(17)], 0.7, 0.0, False)
+    with pytest.raises(EdtError):                    # output == a parent
+        ops.pair_merge_population([ch(x[0])], 0.7, 0.0, False)
+    with pytest.raises(EdtError):                    # two children writing one buffer
+        o = torch.empty(64, dtype=bf, device=dev)
+        ops.pair_merge_population([ch(o), ch(o)], 0.7, 0.0, False)
+    plan = ops.make_slerp_plan([0, 64], dev)
+    t = torch.full((1,), 0.5, dtype=torch.float64, device=dev)
+    with pytest.raises(EdtError):                    # Gram form: at most 8 members
+        ops.slerp_population(plan, [x[0]] * 9, [(0, 1)], [torch.empty(64, dtype=bf, device=dev)], t, speculate=False)
+    with pytest.raises(EdtError):                    # speculative C entry refuses an output over a member
+        flat = (L.ctypes.c_int32 * 2)(0, 1)
+        L.check(L.lib().edt_slerp_population_speculative(
+            L.ptr_array(x[:2]), 2, 1, flat, 1, L.ptr_array([x[0]]), 1, L.ptr(plan.chunks), plan.nchunks,
+            L.ptr(plan.seg_first), 1, L.ptr(t), 0.9995, 1e-8, L.ptr(torch.empty(3 * plan.nchunks, dtype=torch.float64,
+                                                                                 device=dev)),
+            L.ptr(plan.coef), None, L.ptr(torch.empty(1, dtype=torch.int32, device=dev)), 64, L.stream_ptr(dev)),
+            "edt_slerp_population_speculative")
+    with pytest.raises(EdtError):                    # and so does the Gram form (output == member)
+        ops.slerp_population(plan, x[1:3], [(0, 1)], [x[1]], t)
+    ops.slerp_population(plan, x[1:3], [(0, 1)], [x[0]], t)  # a separate output is fine
+    torch.cuda.synchronize()
+
+
 def test_errors_are_raised(dev, ops):
     from evolutionarydistributedtraining_amd import EdtError
     th = torch.zeros(16, device=dev)
