@@ -696,43 +696,47 @@ __device__ __forceinline__ double wave_sum(double x) {
 }
 
 // Block-wide sums {v0.v0, v1.v1, v0.v1} over one chunk [start, start+len), fp64 per thread,
-// fixed reduction order (wave shuffles, then waves in order). Valid in thread 0.
-template <int IDT>
-__device__ __forceinline__ void chunk_sums(const void* v0, const void* v1, uint64_t start, uint64_t len,
-                                           double (*red)[kBlock / 64], double (&out)[3]) {
+// fixed reduction order (wave shuffles, then waves in order). Valid in thread 0. EMIT = true also
+// writes the lerp-branch output l0 v0 + l1 v1 of the chunk (two rounded fp32 products, one
+// rounded sum: lerp_elems' math) in the same pass — the speculative forms; every caller forms
+// the sums with this one loop, so their sums are bit-identical.
+template <int IDT, bool NT, bool EMIT = false, int ODT = EDT_F32>
+__device__ __forceinline__ void chunk_pass(const void* v0, const void* v1, void* out, uint64_t start, uint64_t len,
+                                           float l0, float l1, double (*red)[kBlock / 64], double (&sums)[3]) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t end = start + len;
     double s00 = 0.0, s11 = 0.0, s01 = 0.0;
     const uint64_t a = (start + kVec - 1) / kVec * kVec;      // aligned body [a, b)
     const uint64_t b = end / kVec * kVec;
-    if (a < b) {
-        for (uint64_t i = a + (uint64_t)threadIdx.x * kVec; i < b; i += (uint64_t)kBlock * kVec) {
-            float x[kVec], y[kVec];
-            ld<IDT, kVec, EDT_NT_SLERP != 0 && IDT == EDT_BF16>(v0, i, x);
-            ld<IDT, kVec, EDT_NT_SLERP != 0 && IDT == EDT_BF16>(v1, i, y);
+    auto elems = [&](auto tagN, uint64_t i) {
+        constexpr int N = decltype(tagN)::value;
+        float x[N], y[N];
+        ld<IDT, N, NT && N == kVec>(v0, i, x);
+        ld<IDT, N, NT && N == kVec>(v1, i, y);
 #pragma unroll
-            for (int j = 0; j < kVec; ++j) {
-                const double dx = x[j], dy = y[j];
-                s00 = __builtin_fma(dx, dx, s00);
-                s11 = __builtin_fma(dy, dy, s11);
-                s01 = __builtin_fma(dx, dy, s01);
-            }
+        for (int j = 0; j < N; ++j) {
+            const double dx = x[j], dy = y[j];
+            s00 = __builtin_fma(dx, dx, s00);
+            s11 = __builtin_fma(dy, dy, s11);
+            s01 = __builtin_fma(dx, dy, s01);
         }
+        if constexpr (EMIT) {
+            float o[N];
+#pragma unroll
+            for (int j = 0; j < N; ++j) o[j] = l0 * x[j] + l1 * y[j];
+            st<ODT, N>(out, i, o);
+        }
+    };
+    if (a < b) {
+        for (uint64_t i = a + (uint64_t)threadIdx.x * kVec; i < b; i += (uint64_t)kBlock * kVec)
+            elems(std::integral_constant<int, kVec>{}, i);
     }
     // head [start, min(a, end)) and tail [max(b, a), end): fewer than 16 elements
     const uint64_t h_end = a < end ? a : end;
     const uint64_t t_beg = b > a ? b : h_end;
     const uint64_t nh = h_end - start, nt = end - t_beg;
-    if ((uint64_t)threadIdx.x < nh + nt) {
-        const uint64_t i = threadIdx.x < nh ? start + threadIdx.x : t_beg + (threadIdx.x - nh);
-        float x[1], y[1];
-        ld<IDT, 1>(v0, i, x);
-        ld<IDT, 1>(v1, i, y);
-        const double dx = x[0], dy = y[0];
-        s00 = __builtin_fma(dx, dx, s00);
-        s11 = __builtin_fma(dy, dy, s11);
-        s01 = __builtin_fma(dx, dy, s01);
-    }
+    if ((uint64_t)threadIdx.x < nh + nt)
+        elems(std::integral_constant<int, 1>{}, threadIdx.x < nh ? start + threadIdx.x : t_beg + (threadIdx.x - nh));
     s00 = wave_sum(s00);
     s11 = wave_sum(s11);
     s01 = wave_sum(s01);
@@ -744,10 +748,16 @@ __device__ __forceinline__ void chunk_sums(const void* v0, const void* v1, uint6
             double acc = 0.0;
 #pragma unroll
             for (int w = 0; w < kBlock / 64; ++w) acc += red[q][w];
-            out[q] = acc;
+            sums[q] = acc;
         }
     }
     __syncthreads();
+}
+
+template <int IDT>
+__device__ __forceinline__ void chunk_sums(const void* v0, const void* v1, uint64_t start, uint64_t len,
+                                           double (*red)[kBlock / 64], double (&out)[3]) {
+    chunk_pass<IDT, EDT_NT_SLERP != 0 && IDT == EDT_BF16>(v0, v1, nullptr, start, len, 0.f, 0.f, red, out);
 }
 
 // The reference's scalar SLERP math (EDT_RL/crossover.py:24-45) from the three sums, in fp32 as
@@ -804,64 +814,17 @@ template <int IDT, int ODT>
 __global__ __launch_bounds__(kBlock) void slerp_stats_lerp_kernel(const void* v0, const void* v1, void* out,
                                                                   const uint64_t* chunks, int64_t nchunks,
                                                                   double* partial, const double* tvals) {
-    constexpr bool NT = EDT_NT_SLERP != 0 && IDT == EDT_BF16;
     __shared__ double red[3][kBlock / 64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
-        const uint64_t start = chunks[3 * c], end = start + chunks[3 * c + 1], seg = chunks[3 * c + 2];
-        const float l0 = (float)(1.0 - tvals[seg]), l1 = (float)tvals[seg];
-        double s00 = 0.0, s11 = 0.0, s01 = 0.0;
-        const uint64_t a = (start + kVec - 1) / kVec * kVec;
-        const uint64_t b = end / kVec * kVec;
-        if (a < b) {
-            for (uint64_t i = a + (uint64_t)threadIdx.x * kVec; i < b; i += (uint64_t)kBlock * kVec) {
-                float x[kVec], y[kVec], o[kVec];
-                ld<IDT, kVec, NT>(v0, i, x);
-                ld<IDT, kVec, NT>(v1, i, y);
-#pragma unroll
-                for (int j = 0; j < kVec; ++j) {
-                    const double dx = x[j], dy = y[j];
-                    s00 = __builtin_fma(dx, dx, s00);
-                    s11 = __builtin_fma(dy, dy, s11);
-                    s01 = __builtin_fma(dx, dy, s01);
-                    o[j] = l0 * x[j] + l1 * y[j];          // two rounded products, one rounded sum
-                }
-                st<ODT, kVec>(out, i, o);
-            }
-        }
-        const uint64_t h_end = a < end ? a : end;
-        const uint64_t t_beg = b > a ? b : h_end;
-        const uint64_t nh = h_end - start, nt = end - t_beg;
-        if ((uint64_t)threadIdx.x < nh + nt) {
-            const uint64_t i = threadIdx.x < nh ? start + threadIdx.x : t_beg + (threadIdx.x - nh);
-            float x[1], y[1], o[1];
-            ld<IDT, 1>(v0, i, x);
-            ld<IDT, 1>(v1, i, y);
-            const double dx = x[0], dy = y[0];
-            s00 = __builtin_fma(dx, dx, s00);
-            s11 = __builtin_fma(dy, dy, s11);
-            s01 = __builtin_fma(dx, dy, s01);
-            o[0] = l0 * x[0] + l1 * y[0];
-            st<ODT, 1>(out, i, o);
-        }
-        s00 = wave_sum(s00);
-        s11 = wave_sum(s11);
-        s01 = wave_sum(s01);
-        if (lane == 0) { red[0][wave] = s00; red[1][wave] = s11; red[2][wave] = s01; }
-        __syncthreads();
+        const uint64_t seg = chunks[3 * c + 2];
+        double sums[3];
+        chunk_pass<IDT, EDT_NT_SLERP != 0 && IDT == EDT_BF16, true, ODT>(
+            v0, v1, out, chunks[3 * c], chunks[3 * c + 1], (float)(1.0 - tvals[seg]), (float)tvals[seg], red, sums);
         if (threadIdx.x == 0) {
-            double acc[3];
-#pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                acc[q] = 0.0;
-#pragma unroll
-                for (int w = 0; w < kBlock / 64; ++w) acc[q] += red[q][w];
-            }
-            partial[3 * c] = acc[0];
-            partial[3 * c + 1] = acc[1];
-            partial[3 * c + 2] = acc[2];
+            partial[3 * c] = sums[0];
+            partial[3 * c + 1] = sums[1];
+            partial[3 * c + 2] = sums[2];
         }
-        __syncthreads();
     }
 }
 
@@ -1086,65 +1049,21 @@ template <int IDT, int ODT>
 __global__ __launch_bounds__(kBlock) void slerp_pop_stats_lerp_kernel(BlendChildren B, const uint64_t* chunks,
                                                                       int64_t nchunks, const double* tvals) {
     __shared__ double red[3][kBlock / 64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t per_group = 8ull * (uint64_t)B.nchildren;
     const uint64_t r = blockIdx.x % per_group;
     const int child = (int)(r / 8);
     const int64_t c = (int64_t)((blockIdx.x / per_group) * 8 + (r % 8));
     if (c >= nchunks) return;
-    const void* v0 = B.v0[child];
-    const void* v1 = B.v1[child];
-    void* out = B.out[child];
-    const uint64_t start = chunks[3 * c], end = start + chunks[3 * c + 1], seg = chunks[3 * c + 2];
-    const float l0 = (float)(1.0 - tvals[seg]), l1 = (float)tvals[seg];
-    double s00 = 0.0, s11 = 0.0, s01 = 0.0;
-    const uint64_t a = (start + kVec - 1) / kVec * kVec;
-    const uint64_t b = end / kVec * kVec;
-    if (a < b) {
-        for (uint64_t i = a + (uint64_t)threadIdx.x * kVec; i < b; i += (uint64_t)kBlock * kVec) {
-            float x[kVec], y[kVec], o[kVec];
-            ld<IDT, kVec>(v0, i, x);
-            ld<IDT, kVec>(v1, i, y);
-#pragma unroll
-            for (int j = 0; j < kVec; ++j) {
-                const double dx = x[j], dy = y[j];
-                s00 = __builtin_fma(dx, dx, s00);
-                s11 = __builtin_fma(dy, dy, s11);
-                s01 = __builtin_fma(dx, dy, s01);
-                o[j] = l0 * x[j] + l1 * y[j];
-            }
-            st<ODT, kVec>(out, i, o);
-        }
-    }
-    const uint64_t h_end = a < end ? a : end;
-    const uint64_t t_beg = b > a ? b : h_end;
-    const uint64_t nh = h_end - start, nt = end - t_beg;
-    if ((uint64_t)threadIdx.x < nh + nt) {
-        const uint64_t i = threadIdx.x < nh ? start + threadIdx.x : t_beg + (threadIdx.x - nh);
-        float x[1], y[1], o[1];
-        ld<IDT, 1>(v0, i, x);
-        ld<IDT, 1>(v1, i, y);
-        const double dx = x[0], dy = y[0];
-        s00 = __builtin_fma(dx, dx, s00);
-        s11 = __builtin_fma(dy, dy, s11);
-        s01 = __builtin_fma(dx, dy, s01);
-        o[0] = l0 * x[0] + l1 * y[0];
-        st<ODT, 1>(out, i, o);
-    }
-    s00 = wave_sum(s00);
-    s11 = wave_sum(s11);
-    s01 = wave_sum(s01);
-    if (lane == 0) { red[0][wave] = s00; red[1][wave] = s11; red[2][wave] = s01; }
-    __syncthreads();
+    const uint64_t seg = chunks[3 * c + 2];
+    double sums[3];
+    // default-policy loads: a parent's chunk is re-read by its other children from L2
+    chunk_pass<IDT, false, true, ODT>(B.v0[child], B.v1[child], B.out[child], chunks[3 * c], chunks[3 * c + 1],
+                                      (float)(1.0 - tvals[seg]), (float)tvals[seg], red, sums);
     if (threadIdx.x == 0) {
         double* pc = B.partial[child] + 3 * c;
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            double acc = 0.0;
-#pragma unroll
-            for (int w = 0; w < kBlock / 64; ++w) acc += red[q][w];
-            pc[q] = acc;
-        }
+        pc[0] = sums[0];
+        pc[1] = sums[1];
+        pc[2] = sums[2];
     }
 }
 
