@@ -1,0 +1,13 @@
+// edt_abi.hip — library-wide C ABI pieces: the thread-local error message and the version.
+#include "edt_common.h"
+
+namespace edt {
+thread_local char g_err[512];
+}
+
+extern "C" {
+
+const char* edt_last_error(void) { return g_err; }
+const char* edt_version(void) { return "edt_sync 0.1.0 gfx950"; }
+
+}  // extern "C"

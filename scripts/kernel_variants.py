@@ -3,7 +3,7 @@
     python scripts/kernel_variants.py --build            # here: hipcc the variants into build/variants/
     python scripts/kernel_variants.py --rounds 5         # on the GPU box: time them
 
-Each variant is the same source (evolutionarydistributedtraining_amd/csrc/edt_sync.hip) built with
+Each variant is the same sources (evolutionarydistributedtraining_amd/csrc/*.hip) built with
 different -D tunables; each is loaded as its own ctypes library and timed with HIP events on the
 1.3B-parameter, K=8 bf16-worker, fp32-master configuration of bench.py.
 """
