@@ -55,7 +55,7 @@ class ResidentPopulation:
                  kind: str = "sgd", momentum_dtype: torch.dtype | None = None, seg_t=None,
                  lr: float = 0.7, momentum: float = 0.9, nesterov: bool = True,
                  dot_threshold: float = 0.9995, eps: float = 1e-8, elitism: int = 0,
-                 group=None, kernels=None):
+                 group=None, kernels=None, keep_previous: bool = False):
         if kind not in ("sgd", "slerp"):
             raise ValueError(kind)
         if kind == "sgd":
@@ -81,6 +81,11 @@ class ResidentPopulation:
         self.genomes = [dict(g) for g in genomes]
         self.has_momentum = [False] * self.P
         self._fitness = None
+        # keep_previous: generation N-1 stays resident as members P..2P-1, so the selection can
+        # draw parents from it (EDT_LM/edt.py:226-247: tournament over current + previous)
+        self.keep_previous = keep_previous
+        self.prev_genomes = None
+        self.prev_has_momentum = [False] * self.P
         n = layout.total
         mdt = momentum_dtype or dtype
 
@@ -94,11 +99,17 @@ class ResidentPopulation:
             self._mom = [arena(mdt) if momentum else None for _ in range(self.M)]
             self._child = [arena(dtype) for _ in range(self.M)]
             self._child_mom = [arena(mdt) if momentum else None for _ in range(self.M)]
+            if keep_previous:
+                self._pbase = [arena(dtype) for _ in range(self.M)]
+                self._ptrained = [arena(dtype) for _ in range(self.M)]
+                self._pmom = [arena(mdt) if momentum else None for _ in range(self.M)]
         else:
             if seg_t is None or len(seg_t) != len(layout):
                 raise EdtError("kind='slerp' needs one t per tensor of the layout (seg_t)")
             self._params = [arena(dtype) for _ in range(self.M)]
             self._child = [arena(dtype) for _ in range(self.M)]   # RN to the member dtype (bf16: :142)
+            if keep_previous:
+                self._pparams = [arena(dtype) for _ in range(self.M)]
             self._t = torch.tensor([float(t) for t in seg_t], dtype=torch.float64).to(self.device)
             self._plan = None
         self._recv = {}
@@ -108,12 +119,13 @@ class ResidentPopulation:
         return list(range(self.rank * self.M, (self.rank + 1) * self.M))
 
     def owner(self, m: int) -> int:
-        return m // self.M
+        """Rank holding member m (m >= P: member m - P of the previous generation)."""
+        return (m % self.P) // self.M
 
     def _local(self, m):
-        if m not in self._slot:
+        if m % self.P not in self._slot or (m >= self.P and not self.keep_previous):
             raise EdtError(f"member {m} lives on rank {self.owner(m)}, not {self.rank}")
-        return self._slot[m]
+        return self._slot[m % self.P]
 
     def base(self, m: int) -> torch.Tensor:
         return self._base[self._local(m)]
@@ -155,7 +167,10 @@ class ResidentPopulation:
         sgd:   edt_sim.py:233-240: rank_based_selection of P - elitism pairs, then (elite,
                elite) pairs for the top `elitism` genomes; a population of one pairs with itself.
         slerp: EDT_RL/edt.py:267-272: roulette_wheel_selection of P pairs with
-               scale = roulette_scale(generation, max_generations) (pass `scale`)."""
+               scale = roulette_scale(generation, max_generations) (pass `scale`).
+        method="tournament_pool" (EDT_LM/edt.py:213-247, the distributed master): tournament
+               selection over this generation and the previous one (needs keep_previous=True;
+               pair indices >= P name previous-generation members), elites from this one."""
         if len(fitness) != self.P:
             raise EdtError(f"{len(fitness)} fitness values for {self.P} members")
         pairs = None
@@ -167,6 +182,8 @@ class ResidentPopulation:
                 g["model_path"] = self.model_path(m)
                 genomes.append(g)
             method = method or ("rank" if self.kind == "sgd" else "roulette")
+            if method == "tournament_pool" and not self.keep_previous:
+                raise EdtError("tournament_pool selection needs keep_previous=True")
             if self.P == 1:
                 sel = [(genomes[0], genomes[0])]
             elif method == "rank":
@@ -177,6 +194,14 @@ class ResidentPopulation:
                 sel = schedule.roulette_wheel_selection(genomes, self.P, 1.0 if scale is None else scale)
             elif method == "tournament":
                 sel = schedule.tournament_selection(genomes, self.P)
+            elif method == "tournament_pool":
+                # EDT_LM/edt.py:226-247: tournament over this generation + the previous one, then
+                # (elite, elite) pairs from this generation
+                pool = genomes + (list(self.prev_genomes) if self.prev_genomes is not None else [])
+                sel = schedule.tournament_selection(pool, self.P - self.elitism)
+                ranked = sorted(genomes, key=lambda g: g["fitness"], reverse=True)
+                sel += [(e, e) for e in ranked[:self.elitism]]
+                genomes = pool
             else:
                 raise ValueError(method)
             pairs = schedule.pair_indices(sel, genomes)
@@ -189,10 +214,11 @@ class ResidentPopulation:
         """Whose outer momentum child c inherits (EDT_LM/train/crossover.py:183-227): parent 1's
         when it has one, else parent 2's; none at generation 0; otherwise an error."""
         out = []
+        has = self.has_momentum + self.prev_has_momentum
         for i, j in pairs:
-            if self.has_momentum[i]:
+            if has[i]:
                 out.append(i)
-            elif self.has_momentum[j]:
+            elif has[j]:
                 out.append(j)
             elif self.generation == 0 or self.momentum == 0:
                 out.append(None)
@@ -201,12 +227,12 @@ class ResidentPopulation:
         return out
 
     def _payload(self, m, with_state):
-        s = self._local(m)
+        s, prev = self._local(m), m >= self.P
         if self.kind == "slerp":
-            return [self._params[s]]
-        out = [self._base[s], self._trained[s]]
+            return [(self._pparams if prev else self._params)[s]]
+        out = [(self._pbase if prev else self._base)[s], (self._ptrained if prev else self._trained)[s]]
         if with_state:
-            out.append(self._mom[s])
+            out.append((self._pmom if prev else self._mom)[s])
         return out
 
     def _recv_like(self, key, like):
@@ -217,15 +243,17 @@ class ResidentPopulation:
 
     def _exchange(self, pairs, donors):
         """Grouped send/recv of every parent a local child needs; {member: [tensors]}."""
-        owner = [self.owner(m) for m in range(self.P)]
-        have = {m: None for m in self.local_members()}
+        nmem = 2 * self.P if self.prev_genomes is not None else self.P
+        owner = [self.owner(m) for m in range(nmem)]
+        child_rank = [self.owner(c) for c in range(self.P)]
+        have = [m for m in range(nmem) if owner[m] == self.rank]
         if self.world == 1:
             return {m: self._payload(m, True) for m in have}
-        plan = schedule.exchange_plan(pairs, owner, owner)
+        plan = schedule.exchange_plan(pairs, owner, child_rank)
         mine = plan.get(self.rank, {"send": [], "recv": []})
 
         def with_state(m, dst):
-            return self.kind == "sgd" and any(donors[c] == m and owner[c] == dst for c in range(self.P))
+            return self.kind == "sgd" and any(donors[c] == m and child_rank[c] == dst for c in range(self.P))
 
         p2p = []
         for m, dst in mine["send"]:
@@ -256,12 +284,23 @@ class ResidentPopulation:
         else:
             self._sgd_children(pairs, got, donors)
         # every transfer and merge of this generation is enqueued/complete: swap the children in
-        if self.kind == "sgd":
+        # (keep_previous: the current generation becomes the previous one, whose arenas are
+        # recycled for the next children)
+        if self.kind == "sgd" and self.keep_previous:
+            self._pbase, self._base, self._child = self._base, self._child, self._pbase
+            self._ptrained, self._trained = self._trained, self._ptrained
+            if self.momentum:
+                self._pmom, self._mom, self._child_mom = self._mom, self._child_mom, self._pmom
+        elif self.kind == "sgd":
             self._base, self._child = self._child, self._base
             if self.momentum:
                 self._mom, self._child_mom = self._child_mom, self._mom
+        elif self.keep_previous:
+            self._pparams, self._params, self._child = self._params, self._child, self._pparams
         else:
             self._params, self._child = self._child, self._params
+        if self.keep_previous:
+            self.prev_has_momentum = list(self.has_momentum)
         self._genomes_after(pairs)
         if self.kind == "sgd" and self.momentum:
             self.has_momentum = [True] * self.P
@@ -315,23 +354,32 @@ class ResidentPopulation:
             k.slerp_arena(self._plan, got[i][0], got[j][0], self._child[self._local(c)], self._t,
                           self.dot_threshold, self.eps)
 
+    def _pool_genome(self, m):
+        """Genome of member m as the master sees it at selection time: current members with this
+        generation's fitness and model path, previous members (m >= P) as recorded then."""
+        if m >= self.P:
+            return dict(self.prev_genomes[m - self.P])
+        g = dict(self.genomes[m])
+        g["model_path"] = self.model_path(m)
+        if self._fitness is not None:
+            g["fitness"] = self._fitness[m]
+        return g
+
     def _genomes_after(self, pairs):
         """Child genomes (rank 0, numpy's global RNG, child order; broadcast): EDT-LM
         {"fitness": 0, "dna", "p1", "p2"} with the parents' own p1/p2 dropped
         (EDT_LM/train/crossover.py:296-309); EDT-RL {"env": {env_name, reward_dna, agents: []},
         "p1", "p2"} (EDT_RL/crossover.py:186-201; parents' p1/p2 dropped here too, so the record
-        stays one level deep)."""
+        stays one level deep). keep_previous: this generation's genomes (with fitness) become
+        the previous generation's."""
         new = None
         if self.rank == 0:
-            new = []
+            children = []
             for c, (i, j) in enumerate(pairs):
-                g1, g2 = dict(self.genomes[i]), dict(self.genomes[j])
-                for g, m in ((g1, i), (g2, j)):
+                g1, g2 = self._pool_genome(i), self._pool_genome(j)
+                for g in (g1, g2):
                     g.pop("p1", None)
                     g.pop("p2", None)
-                    g["model_path"] = self.model_path(m)
-                    if self._fitness is not None:
-                        g["fitness"] = self._fitness[m]
                 if self.kind == "sgd":
                     child = {"fitness": 0.0, "model_path": self.model_path(c, self.generation + 1),
                              "dna": uniform_dna_crossover(g1["dna"], g2["dna"]), "p1": g1, "p2": g2}
@@ -342,17 +390,28 @@ class ResidentPopulation:
                                      "reward_dna": uniform_dna_crossover(env["reward_dna"], g2["env"]["reward_dna"]),
                                      "agents": []},
                              "p1": g1, "p2": g2}
-                new.append(child)
-        self.genomes = self._sync_host(new)
+                children.append(child)
+            prev = [self._pool_genome(m) for m in range(self.P)] if self.keep_previous else None
+            new = (children, prev)
+        self.genomes, prev = self._sync_host(new)
+        if self.keep_previous:
+            self.prev_genomes = prev
 
     # ---- persistence (resume a resident run) ------------------------------------------------
     def _member_tensors(self, m):
         s = self._local(m)
         if self.kind == "slerp":
-            return [("params", self._params[s])]
+            out = [("params", self._params[s])]
+            if self.keep_previous and self.prev_genomes is not None:
+                out.append(("prev_params", self._pparams[s]))
+            return out
         out = [("base", self._base[s]), ("trained", self._trained[s])]
         if self._mom[s] is not None:
             out.append(("outer_momentum", self._mom[s]))
+        if self.keep_previous and self.prev_genomes is not None:
+            out += [("prev_base", self._pbase[s]), ("prev_trained", self._ptrained[s])]
+            if self._pmom[s] is not None:
+                out.append(("prev_outer_momentum", self._pmom[s]))
         return out
 
     def _names(self):
@@ -375,7 +434,8 @@ class ResidentPopulation:
                 write_from_arena(os.path.join(d, "model.safetensors"), self.layout, t, names)
         if self.rank == 0:
             meta = {"kind": self.kind, "population": self.P, "generation": self.generation,
-                    "genomes": self.genomes, "has_momentum": self.has_momentum}
+                    "genomes": self.genomes, "has_momentum": self.has_momentum,
+                    "prev_genomes": self.prev_genomes, "prev_has_momentum": self.prev_has_momentum}
             if rng:
                 st = random.getstate()
                 ns = np.random.get_state()
@@ -399,6 +459,9 @@ class ResidentPopulation:
         self.generation = meta["generation"]
         self.genomes = meta["genomes"]
         self.has_momentum = list(meta["has_momentum"])
+        if self.keep_previous:
+            self.prev_genomes = meta.get("prev_genomes")
+            self.prev_has_momentum = list(meta.get("prev_has_momentum") or [False] * self.P)
         names = self._names()
         for m in self.local_members():
             for tag, t in self._member_tensors(m):
