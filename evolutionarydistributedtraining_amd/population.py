@@ -368,7 +368,8 @@ class ResidentPopulation:
     def _genomes_after(self, pairs):
         """Child genomes (rank 0, numpy's global RNG, child order; broadcast): EDT-LM
         {"fitness": 0, "dna", "p1", "p2"} with the parents' own p1/p2 dropped
-        (EDT_LM/train/crossover.py:296-309); EDT-RL {"env": {env_name, reward_dna, agents: []},
+        (EDT_LM/train/crossover.py:296-309; EDT_EVOMERGE/train/crossover.py:214-227 for SLERP
+        children of DNA genomes); EDT-RL {"env": {env_name, reward_dna, agents: []},
         "p1", "p2"} (EDT_RL/crossover.py:186-201; parents' p1/p2 dropped here too, so the record
         stays one level deep). keep_previous: this generation's genomes (with fitness) become
         the previous generation's."""
@@ -380,10 +381,10 @@ class ResidentPopulation:
                 for g in (g1, g2):
                     g.pop("p1", None)
                     g.pop("p2", None)
-                if self.kind == "sgd":
+                if "env" not in g1:         # EDT-LM and EVOMERGE (SLERP children, DNA genomes)
                     child = {"fitness": 0.0, "model_path": self.model_path(c, self.generation + 1),
                              "dna": uniform_dna_crossover(g1["dna"], g2["dna"]), "p1": g1, "p2": g2}
-                else:
+                else:                           # EDT-RL: reward DNA in the env record
                     env = g1["env"]
                     child = {"model_path": self.model_path(c, self.generation + 1),
                              "env": {"env_name": env["env_name"],

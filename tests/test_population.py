@@ -399,3 +399,22 @@ def test_edt_master_tournament_pool_gpu(oracle):
     for m in range(POP):
         assert torch.equal(_bits(got[m][0]), _bits(base[m])), m
         assert torch.equal(_bits(got[m][1]), _bits(mom[m])), m
+
+
+def test_evomerge_master_genomes(oracle):
+    """EDT_EVOMERGE/edt.py: rank selection + elitism, SLERP children of DNA genomes (the
+    EVOMERGE worker writes the EDT-LM genome record, EDT_EVOMERGE/train/crossover.py:214-227)."""
+    from evolutionarydistributedtraining_amd.params import ParamLayout
+    from evolutionarydistributedtraining_amd.population import ResidentPopulation
+    from tests.oracle_kernels import OracleKernels
+    random.seed(3)
+    np.random.seed(3)
+    pop = ResidentPopulation(ParamLayout(SHAPES), torch.float32, "cpu", _genomes("sgd"), kind="slerp",
+                             seg_t=SEG_T, elitism=1, kernels=OracleKernels(oracle))
+    for m in pop.local_members():
+        pop.params(m).copy_(_init(m, ParamLayout(SHAPES).total, torch.float32))
+    pairs = pop.step(_fitness(0), method="rank")
+    assert len(pairs) == POP and pairs[-1][0] == pairs[-1][1]          # the elite self-pair
+    for c, g in enumerate(pop.genomes):
+        assert set(g) == {"fitness", "model_path", "dna", "p1", "p2"} and g["fitness"] == 0.0
+        assert g["model_path"] == f"member{c}/Gen0001"
