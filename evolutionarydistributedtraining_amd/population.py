@@ -271,9 +271,12 @@ class ResidentPopulation:
                 w.wait()
         return got
 
-    def crossover(self, pairs) -> None:
+    def crossover(self, pairs, child_hook=None) -> None:
         """Build child c of pairs[c] = (i, j) on member c's rank, for every c, then make the
-        children the population (generation + 1)."""
+        children the population (generation + 1). child_hook(c, genome), on rank 0 right after
+        child c's genome is made (in child order), is where a master does its per-child host work
+        in the reference's draw order — e.g. EDT_RL/edt.py:290-294 sets genome["env"]["agents"]
+        with random.sample after each crossover() call."""
         pairs = [tuple(p) for p in pairs]
         if len(pairs) != self.P:
             raise EdtError(f"{len(pairs)} pairs for a population of {self.P}")
@@ -301,7 +304,7 @@ class ResidentPopulation:
             self._params, self._child = self._child, self._params
         if self.keep_previous:
             self.prev_has_momentum = list(self.has_momentum)
-        self._genomes_after(pairs)
+        self._genomes_after(pairs, child_hook)
         if self.kind == "sgd" and self.momentum:
             self.has_momentum = [True] * self.P
         self.generation += 1
@@ -365,7 +368,7 @@ class ResidentPopulation:
             g["fitness"] = self._fitness[m]
         return g
 
-    def _genomes_after(self, pairs):
+    def _genomes_after(self, pairs, child_hook=None):
         """Child genomes (rank 0, numpy's global RNG, child order; broadcast): EDT-LM
         {"fitness": 0, "dna", "p1", "p2"} with the parents' own p1/p2 dropped
         (EDT_LM/train/crossover.py:296-309; EDT_EVOMERGE/train/crossover.py:214-227 for SLERP
@@ -391,6 +394,8 @@ class ResidentPopulation:
                                      "reward_dna": uniform_dna_crossover(env["reward_dna"], g2["env"]["reward_dna"]),
                                      "agents": []},
                              "p1": g1, "p2": g2}
+                if child_hook is not None:
+                    child_hook(c, child)
                 children.append(child)
             prev = [self._pool_genome(m) for m in range(self.P)] if self.keep_previous else None
             new = (children, prev)
@@ -489,8 +494,8 @@ class ResidentPopulation:
             g["dna_mutated"] = f
         return flags
 
-    def step(self, fitness: list[float], **select_kw):
+    def step(self, fitness: list[float], child_hook=None, **select_kw):
         """One generation's data path: select -> exchange -> merge -> swap. Returns the pairs."""
         pairs = self.select(fitness, **select_kw)
-        self.crossover(pairs)
+        self.crossover(pairs, child_hook)
         return pairs

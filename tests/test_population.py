@@ -76,8 +76,10 @@ def run_resident(kind, device, kernels=None):
             t.copy_((t.cpu().float() + _noise(gen, m, n)).to(dt))
         if kind == "sgd":
             pop.step(_fitness(gen))
-        else:
-            pop.step(_fitness(gen), scale=_scale(gen))
+        else:   # the RL master samples each child's opponents right after its crossover
+            pool = [f"member{m}/Gen{gen + 1:04d}/Policy" for m in range(POP)]
+            pop.step(_fitness(gen), scale=_scale(gen),
+                     child_hook=lambda c, g: g["env"].__setitem__("agents", random.sample(pool, 2)))
     out = {}
     for m in pop.local_members():
         if kind == "sgd":
@@ -144,6 +146,9 @@ def reference_flow(kind, oracle):
                                                                                 p2["env"]["reward_dna"]),
                                             "agents": []},
                                     "p1": p1, "p2": p2})
+                # EDT_RL/edt.py:290-294: opponents sampled right after each crossover()
+                pool = [f"member{m}/Gen{gen + 1:04d}/Policy" for m in range(POP)]
+                new_genomes[-1]["env"]["agents"] = random.sample(pool, 2)
             new_base.append(out)
         base, genomes = new_base, new_genomes
         if kind == "sgd":
