@@ -38,7 +38,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0        # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-XGMI_LINK_GBPS = 153.0        # per xGMI link; 7 links per GPU, one to each peer
+XGMI_LINK_GBPS = 153.6 / 2    # per xGMI link and direction (153.6 GB/s both ways); 7 links per GPU, one to each peer
 DT = {"f32": torch.float32, "bf16": torch.bfloat16}
 
 
@@ -295,7 +295,8 @@ def main():
         }
         if sharded:
             # the exchange dominates: bytes this rank puts on xGMI per step over the whole step time
-            # (the local HBM pass is inside that time), against the rank's links to its N-1 peers
+            # (the local HBM pass is inside that time), against the outbound direction of the
+            # rank's links to its N-1 peers (it receives as much at the same time)
             wire = wire_main
             achieved = wire / (ms_per_step / 1e3) / 1e9
             peak = XGMI_LINK_GBPS * (world - 1)
