@@ -67,6 +67,10 @@ def parse():
     p.add_argument("--weak-companion", type=int, default=1,
                    help="N>1: after the timed strong-scaling steps, also time W = population workers per GPU "
                         "(weak scaling) and report it beside the value as 'weak_scaling'")
+    p.add_argument("--place-candidates", type=int, default=6,
+                   help="N=1: choose the momentum buffer's HBM placement among this many allocations by "
+                        "timing the step's access pattern on each, once before the timed steps (placement.py); "
+                        "1 keeps the first allocation")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return p.parse_args()
 
@@ -207,6 +211,13 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    placement = None
+    if not sharded and args.place_candidates > 1:
+        # once per run, outside the timed region: the momentum buffer goes wherever the step's
+        # access pattern runs fastest (placement.py); every later step uses that placement
+        placement = sync.place_momentum(args.place_candidates)
+        step()
+        torch.cuda.synchronize()
 
     # fused-kernel duration, measured with HIP events on the launch stream (torch's current)
     kern_ms = None
@@ -327,6 +338,8 @@ def main():
                 ceil = algo_bytes / (probe_ms / 1e3) / 1e9
                 roofline["stream_ceiling_GBps"] = round(ceil, 1)
                 roofline["frac_of_stream_ceiling"] = round(roofline["achieved"] / ceil, 4)
+            if placement:
+                roofline["momentum_placement"] = placement
         prop = torch.cuda.get_device_properties(dev)
         out["device"] = {"name": prop.name, "arch": getattr(prop, "gcnArchName", ""),
                          "cus": prop.multi_processor_count, "hbm_gib": round(prop.total_memory / 2**30, 1)}

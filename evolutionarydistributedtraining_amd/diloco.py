@@ -187,6 +187,19 @@ class OuterSync:
         _step_flat(self.theta.flat, [w.flat for w in self.workers], self.state, self.lr,
                    self.momentum, self.nesterov)
 
+    def place_momentum(self, candidates: int = 6) -> dict:
+        """Choose where the outer momentum lives in HBM by measurement, once, for the life of
+        the run (placement.place_momentum: the step's two read-modify-write streams conflict
+        or not depending on their relative physical placement). Creates the buffer if the
+        first step has not run yet; contents and semantics are unchanged."""
+        if self.momentum == 0:
+            return {"candidates": 0, "probe_ms": [], "chosen": None}
+        from .placement import place_momentum
+        mom = self.state.buffer_for(self.theta.flat)
+        self.state.momentum, rep = place_momentum(self.theta.flat, [w.flat for w in self.workers], mom,
+                                                  candidates)
+        return rep
+
     def broadcast_(self) -> None:
         """Start every worker from the new global weights (what saving base_model to every
         worker dir does, EDT_LM/diloco.py:302-308)."""

@@ -349,3 +349,39 @@ def test_sharded_outer_step_rccl_world1(oracle, dev, tmp_path, mode, broadcast, 
         assert torch.equal(bits(sync.mom_shard[:layout.total].cpu()), bits(mom))
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("tdt", [torch.float32, torch.bfloat16])
+def test_momentum_placement_keeps_the_step_bit_identical(dev, tdt):
+    """OuterSync.place_momentum moves the momentum to the fastest of several allocations
+    (placement.py); contents and every later step stay bit-identical, exact zeros in theta
+    included (the probe kernel it times rewrites theta and momentum)."""
+    from evolutionarydistributedtraining_amd.diloco import OuterSync
+    from evolutionarydistributedtraining_amd.params import ParamArena, ParamLayout
+    layout = ParamLayout([torch.Size((1000, 1000)), torch.Size((4097,)), torch.Size((3,))], ["a", "b", "c"])
+    g = torch.Generator(device=dev).manual_seed(11)
+    theta0 = (torch.randn(layout.total, generator=g, device=dev) * 0.02).to(tdt)
+    theta0[:5000] = 0                                     # exact zeros must survive the probe
+    ws0 = [(theta0.float() + torch.randn(layout.total, generator=g, device=dev) * 1e-3).to(tdt)
+           for _ in range(3)]
+    syncs = []
+    for place in (False, True):
+        theta = ParamArena(layout, tdt, dev)
+        theta.flat.copy_(theta0)
+        workers = [ParamArena(layout, tdt, dev) for _ in ws0]
+        for w, w0 in zip(workers, ws0):
+            w.flat.copy_(w0)
+        s = OuterSync(theta, workers, 0.7, 0.9, True)
+        s.step()
+        if place:
+            before_t, before_m = theta.flat.clone(), s.state.momentum.clone()
+            rep = s.place_momentum(3)
+            assert rep["candidates"] == 3 and len(rep["probe_ms"]) == 3 and 0 <= rep["chosen"] < 3
+            assert torch.equal(theta.flat, before_t) and torch.equal(s.state.momentum, before_m)
+        s.step()
+        s.step()
+        syncs.append(s)
+    a, b = syncs
+    assert torch.equal(a.theta.flat.view(torch.int16 if tdt == torch.bfloat16 else torch.int32),
+                       b.theta.flat.view(torch.int16 if tdt == torch.bfloat16 else torch.int32))
+    assert torch.equal(a.state.momentum, b.state.momentum)
