@@ -229,9 +229,11 @@ class PopulationCrossover:
             self._bufs[key] = torch.empty(self.layout.total, dtype=dtype or self.dtype, device=self.device)
         return self._bufs[key]
 
-    def _exchange(self, pairs, payload):
-        """payload(member_is_first_parent) -> tensors this rank ships for its member; returns the
-        parents' tensor lists for this rank's child: ([...] of parent 1, [...] of parent 2)."""
+    def _exchange(self, pairs, payload, like=None):
+        """payload(member, dst) -> tensors this rank ships for its member to the rank building
+        child dst; like(src_member) -> the tensors this rank receives for that parent (shapes and
+        dtypes; default: what this rank would ship for its own member). Returns the parents'
+        tensor lists for this rank's child: ([...] of parent 1, [...] of parent 2)."""
         from .schedule import exchange_plan
         n = self.world
         if len(pairs) != n:
@@ -240,44 +242,58 @@ class PopulationCrossover:
         mine = plan[self.rank]
         ops_ = []
         for m, dst in mine["send"]:
-            i, j = pairs[dst]
-            for t in payload(m == i):
+            for t in payload(m, dst):
                 ops_.append(dist.P2POp(dist.isend, t, dst, self.group))
         i, j = pairs[self.rank]
         got = {}
         for m, src in mine["recv"]:
-            first = m == i                       # parent 1 also ships its momentum
-            like = payload(first)
-            bufs = [self._buf(("recv", first, k), t.dtype) for k, t in enumerate(like)]
+            shapes = like(m) if like is not None else payload(self.rank, self.rank)
+            bufs = [self._buf(("recv", m == i, k), t.dtype) for k, t in enumerate(shapes)]
             for b in bufs:
                 ops_.append(dist.P2POp(dist.irecv, b, src, self.group))
             got[m] = bufs
         if ops_:
             for w in dist.batch_isend_irecv(ops_):
                 w.wait()
-        par1 = payload(True) if i == self.rank else got[i]
-        par2 = payload(False) if j == self.rank else got[j]
+        par1 = payload(i, self.rank) if i == self.rank else got[i]
+        par2 = payload(j, self.rank) if j == self.rank else got[j]
         return par1, par2
 
     def slerp_step(self, member: torch.Tensor, pairs, t: torch.Tensor, out: torch.Tensor,
                    dot_threshold: float = 0.9995, eps: float = 1e-8) -> None:
         """SLERP child of pairs[rank] into `out` (EDT_RL/crossover.py:84-135 per Policy/Value;
         EDT_EVOMERGE/train/crossover.py:104-146). member: this rank's flat parameters."""
-        (p1,), (p2,) = self._exchange(pairs, lambda first: [member])
+        (p1,), (p2,) = self._exchange(pairs, lambda m, dst: [member])
         if self._plan is None:
             self._plan = self.kernels.make_slerp_plan(self.layout.offsets, self.device)
         self.kernels.slerp_arena(self._plan, p1, p2, out, t, dot_threshold, eps)
 
     def pair_merge_step(self, base: torch.Tensor, trained: torch.Tensor, momentum: torch.Tensor | None,
                         pairs, out: torch.Tensor, out_momentum: torch.Tensor | None, lr: float = 0.7,
-                        mu: float = 0.9, nesterov: bool = True, has_momentum: bool = True) -> None:
-        """EDT-LM child of pairs[rank] (EDT_LM/train/crossover.py:150-237): parent 1 ships
-        (base, trained, outer momentum) — its momentum is the one the child inherits — parent 2
-        ships (base, trained)."""
-        def payload(first):
-            return [base, trained] + ([momentum] if first and momentum is not None else [])
-        par1, par2 = self._exchange(pairs, payload)
-        if out_momentum is not None and len(par1) > 2:
-            out_momentum.copy_(par1[2])
+                        mu: float = 0.9, nesterov: bool = True, has_momentum: bool = True,
+                        generation: int = 0) -> None:
+        """EDT-LM child of pairs[rank] (EDT_LM/train/crossover.py:150-237): both parents ship
+        (base, trained); the child inherits parent 1's outer momentum when parent 1 has one, else
+        parent 2's (:183-227), and only that donor ships it. Which members have a momentum
+        (`momentum is not None and has_momentum` on their rank) is agreed first, so every rank
+        knows every message; a child with no donor past generation 0 raises NotImplementedError
+        on every rank, as the reference's crossover does (:226-227)."""
+        flags = [None] * self.world
+        dist.all_gather_object(flags, bool(has_momentum and momentum is not None), group=self.group)
+        donors = [i if flags[i] else (j if flags[j] else None) for i, j in pairs]
+        if mu != 0 and generation > 0 and any(d is None for d in donors):
+            raise NotImplementedError("Merging outer optimizer states not implemented for this case.")
+        donor = donors[self.rank]
+        if donor is not None and out_momentum is None:
+            raise ValueError("the child inherits an outer momentum: pass out_momentum")
+
+        def payload(m, dst):
+            return [base, trained] + ([momentum] if donors[dst] == m else [])
+
+        def like(m):
+            return [base, trained] + ([out_momentum] if donor == m else [])
+        par1, par2 = self._exchange(pairs, payload, like)
+        if donor is not None:
+            out_momentum.copy_((par1 if donor == pairs[self.rank][0] else par2)[2])
         self.kernels.pair_merge(par1[0], par2[0], par1[1], par2[1], out, out_momentum,
-                                has_momentum and len(par1) > 2, lr, mu, nesterov)
+                                donor is not None, lr, mu, nesterov)

@@ -131,7 +131,7 @@ def _member(r, kind):
     return base, trained, mom
 
 
-def _pop_worker(rank, world, port, pairs, outdir):
+def _pop_worker(rank, world, port, pairs, outdir, no_momentum=()):
     import torch.distributed as dist
 
     from evolutionarydistributedtraining_amd.distributed import PopulationCrossover
@@ -147,7 +147,8 @@ def _pop_worker(rank, world, port, pairs, outdir):
     pc.slerp_step(trained, pairs, t, child_slerp)
     child = torch.empty(layout.total, dtype=torch.bfloat16)
     child_mom = torch.empty_like(mom)
-    pc.pair_merge_step(base, trained, mom, pairs, child, child_mom)
+    pc.pair_merge_step(base, trained, None if rank in no_momentum else mom, pairs, child, child_mom,
+                       generation=1)
     torch.save({"slerp": child_slerp, "child": child, "mom": child_mom}, os.path.join(outdir, f"pop{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
@@ -171,6 +172,29 @@ def test_population_crossover_world3(tmp_path, oracle):
         assert torch.equal(got["slerp"], want), c
         out = torch.empty(offs[-1], dtype=torch.bfloat16)
         mom = members[i][2].clone()
+        oracle.pair_merge(members[i][0], members[j][0], members[i][1], members[j][1], out, mom, True, 0.7, 0.9, True)
+        assert torch.equal(got["child"].view(torch.int16), out.view(torch.int16)), c
+        assert torch.equal(got["mom"].view(torch.int16), mom.view(torch.int16)), c
+
+
+@pytest.mark.slow
+def test_population_crossover_parent2_momentum_world3(tmp_path, oracle):
+    """Parent 1 without an outer momentum: the child inherits parent 2's
+    (EDT_LM/train/crossover.py:183-227), shipped by parent 2's rank only."""
+    world = 3
+    pairs = [(0, 2), (1, 0), (0, 1)]          # member 0 has no momentum: donors 2, 1, 1
+    no_mom = (0,)
+    port = _free_port()
+    mp.start_processes(_pop_worker, args=(world, port, pairs, str(tmp_path), no_mom), nprocs=world,
+                       join=True, start_method="spawn")
+    from evolutionarydistributedtraining_amd.params import ParamLayout
+    offs = ParamLayout(POP_SHAPES).offsets
+    members = [_member(r, "lm") for r in range(world)]
+    for c, (i, j) in enumerate(pairs):
+        got = torch.load(tmp_path / f"pop{c}.pt", weights_only=True)
+        donor = i if i not in no_mom else j
+        out = torch.empty(offs[-1], dtype=torch.bfloat16)
+        mom = members[donor][2].clone()
         oracle.pair_merge(members[i][0], members[j][0], members[i][1], members[j][1], out, mom, True, 0.7, 0.9, True)
         assert torch.equal(got["child"].view(torch.int16), out.view(torch.int16)), c
         assert torch.equal(got["mom"].view(torch.int16), mom.view(torch.int16)), c
