@@ -36,7 +36,7 @@ import torch
 import torch.distributed as dist
 
 from . import ops as _ops
-from .diloco import OuterState, check_sgd_hparams
+from .diloco import check_sgd_hparams
 from .params import ParamArena, ParamLayout
 
 
@@ -82,7 +82,6 @@ class ShardedOuterSync:
         self.workers = [ParamArena(layout, worker_dtype, device, w[:n]) for w in self.worker_bufs]
         shard_total = sum((e - b) // self.world for b, e in self.buckets)
         self.mom_shard = torch.zeros(shard_total, dtype=theta_dtype, device=device) if momentum else None
-        self.state = OuterState()
         self.has_momentum = False
         # RCCL reduces/gathers in place; other backends (gloo, CPU tests) get separate buffers
         self.inplace = dist.get_backend(group) == "nccl"
