@@ -18,6 +18,8 @@ import torch
 
 from tests.golden_data import GOLDEN_DIR, bits, flat
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
 pytestmark = pytest.mark.gpu
 
 with open(os.path.join(GOLDEN_DIR, "manifest.json")) as _f:
@@ -574,3 +576,16 @@ def test_errors_are_raised(dev, ops):
         ops.outer_step(th.bfloat16(), [torch.zeros(16, device=dev)], None, False, 0.7, 0.0, False)
     with pytest.raises(EdtError):   # host tensors are refused: no CPU path
         ops.outer_step(torch.zeros(16), [torch.zeros(16)], None, False, 0.7, 0.0, False)
+
+
+def test_c_consumer_runs():
+    """The plain-C consumer of include/edt_sync.h (tests/c_abi/abi_consumer.c, built by build()):
+    hipMalloc'd buffers, two edt_outer_step calls on the null stream, bit-exact against the C
+    oracle, and the negative-code + edt_last_error() convention for a bad argument."""
+    import subprocess
+    exe = os.path.join(ROOT, "tests", "c_abi", "_build", "abi_consumer")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.dirname(os.path.dirname(exe))], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120, cwd="/")
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "abi consumer ok" in r.stdout

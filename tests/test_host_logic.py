@@ -142,6 +142,19 @@ def test_library_exports_every_header_symbol():
     assert lib.edt_outer_step_bytes_per_elem(0, 1, 8, 1) == 32
 
 
+def test_c_consumer_builds_and_links():
+    """tests/c_abi/abi_consumer.c includes only include/edt_sync.h (+ the HIP runtime) and links
+    against libedt_sync.so with gcc: the boundary is usable with no Python in between. Running it
+    needs a GPU (test_gpu_kernels.py::test_c_consumer_runs)."""
+    import subprocess
+    d = os.path.join(ROOT, "tests", "c_abi")
+    subprocess.run(["make", "-s", "-C", d], check=True)
+    out = subprocess.run(["ldd", os.path.join(d, "_build", "abi_consumer")], capture_output=True, text=True,
+                         check=True, cwd="/").stdout
+    assert "not found" not in out, out
+    assert "libedt_sync.so" in out and "libamdhip64" in out
+
+
 def test_chunk_table_host_function():
     import ctypes
     from evolutionarydistributedtraining_amd import _lib
