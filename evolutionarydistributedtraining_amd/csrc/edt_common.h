@@ -37,11 +37,15 @@ using edt::g_err;
 
 
 // Tunables (overridable at build time for the variant sweep in scripts/kernel_variants.py).
-// Measured on MI355X, 1.3B params x 8 bf16 workers (profiles/r01_variants.txt): 256 blocks per
-// CU (short grid-stride runs, no tail of late blocks) + non-temporal worker loads is fastest,
-// 6.78 ms = 6.21 TB/s vs 7.36 ms for 8 blocks per CU with default-policy loads.
+// Grid: one pass (EDT_BLOCKS_PER_CU 0: one 2048-element tile per workgroup, dispatched in address
+// order, so the chip's in-flight window stays one contiguous stretch of every stream). With the
+// momentum placed by measurement (placement.py) it beats 256 grid-stride blocks per CU on every
+// 1.3B regime and op (profiles/r01_oneshot.json): outer step fp32 10.74 -> 10.48 ms, bf16
+// workers 6.85 -> 6.74, all bf16 5.44 -> 5.24, pair merge 3.50 -> 3.13, lerp 1.53 -> 1.31 ms;
+// 125M equal. (Before the placement search the two were within noise, profiles/r01_variants.txt,
+// which is why 256 per CU shipped first: 6.78 ms vs 7.36 ms for 8 per CU.)
 #ifndef EDT_BLOCKS_PER_CU
-#define EDT_BLOCKS_PER_CU 256
+#define EDT_BLOCKS_PER_CU 0
 #endif
 #ifndef EDT_NT_LOADS          // non-temporal loads for the once-read bf16 worker streams
 #define EDT_NT_LOADS 1        // (fp32 streams: measured 1.6x SLOWER with nt, 17.5 vs 11.2 ms)

@@ -99,6 +99,7 @@ VARIANTS.update({"f32_nt": ["-DEDT_NT_F32=1"], "f32_bpc64": ["-DEDT_BLOCKS_PER_C
                  "f32_nt_oneshot": ["-DEDT_NT_F32=1", "-DEDT_BLOCKS_PER_CU=0"],
                  "f32_nt_ntst": ["-DEDT_NT_F32=1", "-DEDT_NT_STORES=1"],
                  "f32_nt_bpc128": ["-DEDT_NT_F32=1", "-DEDT_BLOCKS_PER_CU=128"]})
+VARIANTS.update({"default": [], "f32_ntst": ["-DEDT_NT_STORES=1"]})
 VARIANTS.update({"split0": ["-DEDT_SPLIT_HALVES=0"], "split1": ["-DEDT_SPLIT_HALVES=1"],
                  "split1_nt0": ["-DEDT_SPLIT_HALVES=1", "-DEDT_NT_LOADS=0"]})
 VARIANTS.update({f"li{i}": [f"-DEDT_LIST_ITERS={i}"] for i in (1, 2, 4, 8, 16)})
@@ -285,7 +286,7 @@ def build(names):
         print("built", out)
 
 
-def run(names, rounds, iters, layout_name, k, tdt="f32", wdt="bf16"):
+def run(names, rounds, iters, layout_name, k, tdt="f32", wdt="bf16", place=True):
     import torch
     from evolutionarydistributedtraining_amd import _lib as L
     from evolutionarydistributedtraining_amd.layouts import LAYOUTS
@@ -295,6 +296,10 @@ def run(names, rounds, iters, layout_name, k, tdt="f32", wdt="bf16"):
     theta = (torch.randn(P, device=dev) * 0.02).to(DT[tdt])
     workers = [(theta.float() + torch.randn(P, device=dev) * 1e-3).to(DT[wdt]) for _ in range(k)]
     mom = torch.zeros(P, device=dev, dtype=DT[tdt])
+    if place:       # the bench's momentum placement (placement.py), so variants compare on a good one
+        from evolutionarydistributedtraining_amd.placement import place_momentum
+        mom, rep = place_momentum(theta, workers, mom)
+        print("momentum placement", rep, flush=True)
     libs = {}
     for n in names:
         lib = ctypes.CDLL(os.path.join(VDIR, f"{n}.so"))
