@@ -43,6 +43,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ops", default="pair,slerp,lerp,outer_list")
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--slerp-chunks", default="65536",
+                    help="comma list of SLERP plan chunk sizes (elements per workgroup chunk) to time")
     ap.add_argument("--list-wdt", default="bf16", choices=["bf16", "f32"], help="outer_list worker dtype")
     a = ap.parse_args()
     from evolutionarydistributedtraining_amd import ops
@@ -101,7 +103,8 @@ def main():
         v0 = torch.empty(P, dtype=bf, device=dev)
         v1 = torch.empty(P, dtype=bf, device=dev)
         out = torch.empty(P, dtype=bf, device=dev)
-        plan = ops.make_slerp_plan(lay.offsets, dev)
+        chunk_sizes = [int(c) for c in a.slerp_chunks.split(",")]
+        plans = {c: ops.make_slerp_plan(lay.offsets, dev, chunk_elems=c) for c in chunk_sizes}
         t = torch.full((len(lay),), 0.5, dtype=torch.float64, device=dev)
         # far: v1 = v0 + 5 % noise (|dot| ~ 0.9988, SLERP branch everywhere);
         # lineage: 0.5 % noise (|dot| ~ 0.99999, the lerp branch: fine-tunes of one base)
@@ -113,10 +116,11 @@ def main():
                 v0[s0:e] = x.to(bf)
                 v1[s0:e] = (x + torch.randn(e - s0, device=dev) * 0.02 * rel).to(bf)
                 del x
-            for spec in (False, True):
+            for (c, plan), spec in ((cp, sp) for cp in plans.items() for sp in (False, True)):
                 ms = timed(lambda: ops.slerp_arena(plan, v0, v1, out, t, speculate=spec), a.iters)
                 gbs = 6 * P / ms / 1e6
-                res[f"slerp/{parents}/{'speculative' if spec else 'two_pass'}"] = {
+                tag = "" if len(plans) == 1 else f"/chunk{c}"
+                res[f"slerp/{parents}/{'speculative' if spec else 'two_pass'}{tag}"] = {
                     "P": P, "segments": len(lay), "chunks": plan.nchunks, "ms": round(ms, 3),
                     "GBps_algorithmic": round(gbs, 1), "frac": round(gbs / PEAK, 4), "bytes_per_elem": 6,
                     "lerp_branch_segments": int((plan.dots[:len(lay)].abs() > 0.9995).sum().item())}
