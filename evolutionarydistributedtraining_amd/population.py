@@ -55,13 +55,14 @@ class ResidentPopulation:
                  kind: str = "sgd", momentum_dtype: torch.dtype | None = None, seg_t=None,
                  lr: float = 0.7, momentum: float = 0.9, nesterov: bool = True,
                  dot_threshold: float = 0.9995, eps: float = 1e-8, elitism: int = 0,
-                 group=None, kernels=None, keep_previous: bool = False):
+                 group=None, kernels=None, keep_previous: bool = False, slerp_chunk: int | None = None):
         if kind not in ("sgd", "slerp"):
             raise ValueError(kind)
         if kind == "sgd":
             from .diloco import check_sgd_hparams
             check_sgd_hparams(lr, momentum, nesterov)
         self.kind = kind
+        self.slerp_chunk = slerp_chunk          # SLERP plan chunk (elements per workgroup); None: default
         self.layout = layout
         self.dtype = dtype
         self.device = torch.device(device)
@@ -340,7 +341,8 @@ class ResidentPopulation:
         than 8 distinct parents: the speculative form (<= 16 local children), else per child."""
         k = self.kernels
         if self._plan is None:
-            self._plan = k.make_slerp_plan(self.layout.offsets, self.device)
+            self._plan = k.make_slerp_plan(self.layout.offsets, self.device,
+                                           **({"chunk_elems": self.slerp_chunk} if self.slerp_chunk else {}))
         local = self.local_members()
         srcs = sorted({m for c in local for m in pairs[c]})
         where = {m: q for q, m in enumerate(srcs)}

@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--kinds", default="sgd,slerp")
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--slerp-chunk", type=int, default=None, help="SLERP plan chunk (elements per workgroup)")
     ap.add_argument("--members", default="lineage", choices=["lineage", "random"],
                     help="lineage: one base + 0.5 %% per-member noise (fine-tunes of a common base: the "
                          "SLERP takes the lerp branch); random: independent members (SLERP branch)")
@@ -63,7 +64,8 @@ def main():
                 {"value": 0.5}]}})]
             if len(t) != len(layout):
                 t = [0.5] * len(layout)
-            pop = ResidentPopulation(layout, torch.bfloat16, dev, genomes, kind="slerp", seg_t=t)
+            pop = ResidentPopulation(layout, torch.bfloat16, dev, genomes, kind="slerp", seg_t=t,
+                                     slerp_chunk=a.slerp_chunk)
             arenas = [pop.params(m) for m in range(P)]
         g = torch.Generator(device=dev).manual_seed(1)
         common = torch.randn(n, generator=g, device=dev) * 0.02 if a.members == "lineage" else None
