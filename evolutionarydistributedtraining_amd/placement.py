@@ -30,6 +30,7 @@ def probe_ms(theta: torch.Tensor, workers: list[torch.Tensor], momentum: torch.T
     n = theta.numel()
     if momentum.numel() != n or momentum.dtype != theta.dtype or any(w.numel() != n for w in workers):
         raise L.EdtError("probe operands must share theta's size (and momentum theta's dtype)")
+    workers = workers[:L.EDT_MAX_WORKERS]        # one launch's worth: the workers' placement does not matter
     arr = L.ptr_array(workers)
     st = L.stream_ptr(theta.device)
 
