@@ -114,7 +114,7 @@ def cpu_baseline(args, theta_dtype, worker_dtype, k):
 def stream_ceiling_ms(theta, workers, momentum, iters=10):
     """Median HIP-event time of edt_probe_stream over the step's own operands (None if the
     step runs without momentum: the probe always reads and writes a momentum stream)."""
-    if momentum is None or len(workers) > 32:    # the probe is one launch (<= 32 workers)
+    if momentum is None or len(workers) > 64:    # the probe is one launch (<= 64 workers)
         return None
     from evolutionarydistributedtraining_amd import _lib as L
     lib = L.lib()

@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(PKG_DIR, "libedt_sync.so")
 
 EDT_F32 = 0
 EDT_BF16 = 1
-EDT_MAX_WORKERS = 32
+EDT_MAX_WORKERS = 64
 
 _DT = {torch.float32: EDT_F32, torch.bfloat16: EDT_BF16}
 

@@ -50,7 +50,7 @@ struct TensorArgs {
     __device__ __forceinline__ const void* wp(int k) const { return w[(uint64_t)k * T + t]; }
 };
 
-// MODE_CHAIN = MODE_FUSED for populations above EDT_MAX_WORKERS: launches of <= 32 workers
+// MODE_CHAIN = MODE_FUSED for populations above EDT_MAX_WORKERS: launches of <= 64 workers
 // carry the running sum in theta's dtype (lossless: it is rounded to that dtype after every add).
 enum { MODE_FUSED = 0, MODE_PARTIAL = 1, MODE_CHAIN = 2 };
 

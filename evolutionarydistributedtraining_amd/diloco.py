@@ -19,7 +19,7 @@ import os
 import torch
 
 from . import ops
-from ._lib import EdtError
+from ._lib import EDT_MAX_WORKERS as L_MAX, EdtError
 from .params import ParamArena, ParamLayout, flat_view, pack, unpack_
 
 DILOCO_DEFAULTS = dict(lr=0.7, momentum=0.9, nesterov=True)        # EDT_LM/diloco.py:253-255
@@ -137,7 +137,7 @@ def outer_step(base_params, worker_params, state: OuterState | None = None, lr: 
     state:         the carried outer-optimiser state (None on the first generation).
     One launch either way: over the flat arenas when each list is a run of views of one arena
     (`params.arena_of_module`), else over the tensor lists themselves (`ops.outer_step_list`,
-    no packing). Only populations above 32 workers with separate tensors are packed first.
+    no packing). Only populations above 64 workers with separate tensors are packed first.
     """
     state = state or OuterState()
     base_params = list(base_params)
@@ -151,7 +151,7 @@ def outer_step(base_params, worker_params, state: OuterState | None = None, lr: 
         theta = flat_view(base_params)
         flats = [flat_view(w) for w in worker_params]
         if theta is None or any(f is None for f in flats):
-            if len(worker_params) <= 32 and base_params and all(p.is_cuda for p in base_params):
+            if len(worker_params) <= L_MAX and base_params and all(p.is_cuda for p in base_params):
                 if len({w[0].dtype for w in worker_params}) != 1:
                     raise EdtError("all trained models must share one dtype")
                 _step_list(base_params, worker_params, state, lr, momentum, nesterov)

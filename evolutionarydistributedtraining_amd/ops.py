@@ -19,7 +19,7 @@ def outer_step(theta: torch.Tensor, workers: list[torch.Tensor], momentum: torch
                has_momentum: bool, lr: float, momentum_coef: float, nesterov: bool) -> None:
     """Fused DiLoCo outer step (EDT_LM/diloco.py:238-289): theta and momentum updated in place.
 
-    theta: flat float32/bfloat16; workers: K flat tensors of one dtype (K > 32: chained launches
+    theta: flat float32/bfloat16; workers: K flat tensors of one dtype (K > 64: chained launches
     through a scratch running sum); momentum: flat, theta's dtype (required when momentum_coef != 0)."""
     lib = L.lib()
     if not workers:

@@ -36,7 +36,7 @@ enum {
     EDT_ERR_LAUNCH = -2,   /* kernel launch failed (hipGetLastError) */
 };
 
-#define EDT_MAX_WORKERS 32   /* workers consumed by one fused launch */
+#define EDT_MAX_WORKERS 64   /* workers consumed by one fused launch */
 
 /* ---- DiLoCo outer step ------------------------------------------------------------------
  * Replaces EDT_LM/diloco.py:238-289 (== EDT_LM/diloco_sim.py:233-299):
@@ -53,9 +53,9 @@ int edt_outer_step(void* theta_g, int gdt, const void* const* theta_k, int wdt, 
                    double lr, double momentum_coef, int nesterov, void* stream);
 
 /* The same step for any population size: K > EDT_MAX_WORKERS runs as consecutive launches of
- * <= 32 workers (the reference's worker order), the running sum carried in `workspace` (n
+ * <= 64 workers (the reference's worker order), the running sum carried in `workspace` (n
  * elements of theta's dtype: lossless, the sum is rounded to that dtype after every add).
- * K <= 32: identical to edt_outer_step (workspace unused, may be NULL). */
+ * K <= 64: identical to edt_outer_step (workspace unused, may be NULL). */
 int edt_outer_step_ws(void* theta_g, int gdt, const void* const* theta_k, int wdt, int K,
                       void* momentum, int has_momentum, uint64_t n, double lr, double momentum_coef,
                       int nesterov, void* workspace, void* stream);

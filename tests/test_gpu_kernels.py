@@ -183,14 +183,14 @@ REGIMES = [(torch.float32, torch.float32), (torch.float32, torch.bfloat16), (tor
 
 
 # the large size with representative populations only
-OUTER_CASES = [(n, K) for n in (1, 7, 8, 9, 4097, 1_000_003) for K in (1, 2, 3, 4, 5, 8, 16, 32, 33, 48, 64)
-               if n != 1_000_003 or K in (3, 8, 32, 48)]
+OUTER_CASES = [(n, K) for n in (1, 7, 8, 9, 4097, 1_000_003) for K in (1, 2, 3, 4, 5, 8, 16, 32, 33, 48, 64, 65, 100, 129)
+               if n != 1_000_003 or K in (3, 8, 48, 65)]
 
 
 @pytest.mark.parametrize("gdt,wdt", REGIMES)
 @pytest.mark.parametrize("n,K", OUTER_CASES)
 def test_outer_step_vs_oracle(oracle, dev, ops, gdt, wdt, K, n):
-    """K > 32 runs as chained launches carrying the running sum (edt_outer_step_ws)."""
+    """K > 64 runs as chained launches carrying the running sum (edt_outer_step_ws)."""
     theta, workers, mom = _rand_case(n, K, gdt, wdt, seed=K * 1000 + n)
     for has, (lr, mu, nest) in [(False, (0.7, 0.9, True)), (True, (0.7, 0.9, True)),
                                 (True, (0.5, 0.8, False)), (False, (1.0, 0.0, False))]:
