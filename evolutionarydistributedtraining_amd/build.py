@@ -43,5 +43,26 @@ def build_library(force: bool = False, extra_flags: list[str] | None = None, out
     return out
 
 
+COMM_SOURCE = os.path.join(CSRC, "edt_comm.cpp")
+COMM_HEADER = os.path.join(ROOT, "include", "edt_comm.h")
+COMM_OUT = os.path.join(PKG_DIR, "libedt_comm.so")
+
+
+def build_comm_library(force: bool = False) -> str:
+    """libedt_comm.so (include/edt_comm.h): RCCL behind the C ABI, host code only, linked against
+    libedt_sync.so (its kernels) and librccl; runpath $ORIGIN so the two travel together."""
+    sync = build_library()
+    deps = [COMM_SOURCE, COMM_HEADER, HEADER, sync]
+    if force or not os.path.exists(COMM_OUT) or any(os.path.getmtime(d) > os.path.getmtime(COMM_OUT) for d in deps):
+        rocm = os.path.dirname(os.path.dirname(os.path.realpath(hipcc())))
+        cmd = [hipcc(), "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-I", os.path.dirname(HEADER),
+               COMM_SOURCE, "-o", COMM_OUT + ".tmp", "-L", PKG_DIR, "-ledt_sync", "-L", os.path.join(rocm, "lib"),
+               "-lrccl", "-Wl,-rpath,$ORIGIN", "-Wl,-rpath," + os.path.join(rocm, "lib")]
+        subprocess.run(cmd, check=True)
+        os.replace(COMM_OUT + ".tmp", COMM_OUT)
+    return COMM_OUT
+
+
 if __name__ == "__main__":
     print(build_library(force=True))
+    print(build_comm_library(force=True))

@@ -1,0 +1,80 @@
+/* edt_comm.h — the cross-GPU half of the outer-loop sync behind a C ABI (libedt_comm.so):
+ * RCCL over xGMI, one communicator per rank, for hosts that do not have torch.distributed.
+ *
+ * The reference has no collectives: its gather is K x from_pretrained of the workers' checkpoints
+ * on a shared disk and its broadcast K x save_pretrained (EDT_LM/diloco.py:231-235, 302-308), and
+ * its EDT children fetch their parents' checkpoint dirs (EDT_LM/train/crossover.py:255-258).
+ * These entry points are the device-resident replacements (edt_comm_*); the
+ * Python package reaches the same RCCL through torch.distributed (distributed.py) instead.
+ *
+ * Conventions as edt_sync.h: the caller owns every buffer (device pointers), all calls are
+ * stream-ordered and asynchronous on `stream` (a hipStream_t; NULL = the null stream), and return
+ * 0 or a negative EDT_COMM_ERR_*; edt_comm_last_error() (thread-local) says why. A communicator
+ * is used by one host thread at a time.
+ */
+#ifndef EDT_COMM_H
+#define EDT_COMM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EDT_COMM_ERR_ARG (-1)
+#define EDT_COMM_ERR_RCCL (-2)
+#define EDT_COMM_ERR_HIP (-3)
+
+/* Bytes of the opaque communicator id (ncclUniqueId): rank 0 makes it, every rank passes the
+ * same bytes to edt_comm_init (the host moves them, e.g. over its own control channel). */
+uint64_t edt_comm_id_bytes(void);
+int edt_comm_unique_id(void* id_out);
+
+/* One communicator per rank: nranks ranks, this one `rank`, on the current HIP device. */
+int edt_comm_init(void** comm, const void* id, int nranks, int rank);
+int edt_comm_destroy(void* comm);
+int edt_comm_rank(const void* comm);
+int edt_comm_size(const void* comm);
+
+/* Collectives (dt: EDT_F32 = 0, EDT_BF16 = 1 as in edt_sync.h).
+ * reduce_scatter_f32: recv[0, count) = sum over ranks of send[rank * count, +count).
+ *   In place when recv == send + rank * count.
+ * all_gather:  recv[r * count, +count) = rank r's send[0, count). In place when
+ *   send == recv + rank * count.
+ * all_to_all:  recv[r * count, +count) = rank r's send[this rank * count, +count). */
+int edt_comm_reduce_scatter_f32(void* comm, const float* send, float* recv, uint64_t count_per_rank,
+                                void* stream);
+int edt_comm_all_gather(void* comm, const void* send, void* recv, uint64_t count_per_rank, int dt,
+                        void* stream);
+int edt_comm_all_to_all(void* comm, const void* send, void* recv, uint64_t count_per_rank, int dt,
+                        void* stream);
+
+/* Grouped point-to-point (the parents of each child to the rank that builds it,
+ * schedule.exchange_plan): op i sends bytes[i] from sendbufs[i] to rank send_to[i] when
+ * send_to[i] >= 0, and receives bytes[i] into recvbufs[i] from rank recv_from[i] when
+ * recv_from[i] >= 0; all nops operations form one group (no ordering deadlock). */
+int edt_comm_exchange(void* comm, const int32_t* send_to, const int32_t* recv_from,
+                      const void* const* sendbufs, void* const* recvbufs, const uint64_t* bytes,
+                      int nops, void* stream);
+
+/* The DiLoCo outer step across ranks, reduce schedule (distributed.py mode="reduce"), with the
+ * collectives on the communicator's own stream overlapping the kernels on `stream`. Per bucket
+ * [b, e) of the padded flat arena (buckets of bucket_elems, rounded to multiples of nranks * 64;
+ * n_pad a multiple of nranks * 64):
+ *   edt_delta_partial over the K_local local workers into acc[b, e)  (fp32, K_total = K_local x nranks)
+ *   reduce-scatter of acc[b, e) in place -> this rank's shard s = [b + rank*per, +per)
+ *   edt_sgd_apply on theta[s] with the momentum shard (per elements of momentum_shard, buckets
+ *   in order: the shard of rank r is n_pad / nranks elements of theta's dtype)
+ *   all-gather of theta[s] in place -> theta[b, e) on every rank.
+ * acc: n_pad fp32 elements of workspace. Returns when the work is enqueued on `stream`. */
+int edt_outer_step_sharded(void* comm, void* theta_g, int gdt, const void* const* theta_k, int wdt,
+                           int K_local, void* momentum_shard, int has_momentum, uint64_t n_pad,
+                           uint64_t bucket_elems, double lr, double momentum_coef, int nesterov,
+                           float* acc, void* stream);
+
+const char* edt_comm_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EDT_COMM_H */

@@ -385,3 +385,63 @@ def test_momentum_placement_keeps_the_step_bit_identical(dev, tdt):
     assert torch.equal(a.theta.flat.view(torch.int16 if tdt == torch.bfloat16 else torch.int32),
                        b.theta.flat.view(torch.int16 if tdt == torch.bfloat16 else torch.int32))
     assert torch.equal(a.state.momentum, b.state.momentum)
+
+
+# ------------------------------------------------------------------------------------------
+# libedt_comm.so (include/edt_comm.h) at world size 1 on the one-GPU box: the collectives are
+# identities, the sharded reduce schedule equals the single-GPU fused step bit for bit (fp32 master)
+
+def test_comm_abi_world1_collectives(dev):
+    from evolutionarydistributedtraining_amd.comm import Comm
+    c = Comm(Comm.unique_id(), 1, 0)
+    try:
+        assert (c.rank, c.size) == (0, 1)
+        g = torch.Generator(device=dev).manual_seed(5)
+        x = torch.randn(4099, generator=g, device=dev)
+        y = torch.empty_like(x)
+        c.reduce_scatter_f32(x, y)
+        torch.cuda.synchronize()
+        assert torch.equal(x, y)
+        for dt in (torch.float32, torch.bfloat16):
+            xs, ys = x.to(dt), torch.empty(4099, dtype=dt, device=dev)
+            c.all_gather(xs, ys)
+            torch.cuda.synchronize()
+            assert torch.equal(xs, ys)
+            ys.zero_()
+            c.all_to_all(xs, ys)
+            torch.cuda.synchronize()
+            assert torch.equal(xs, ys)
+        a, b = torch.arange(1000, dtype=torch.int32, device=dev), torch.zeros(1000, dtype=torch.int32, device=dev)
+        c.exchange([(0, a, 0, b)])                 # a grouped send to self and receive from self
+        torch.cuda.synchronize()
+        assert torch.equal(a, b)
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("wdt", [torch.float32, torch.bfloat16])
+def test_comm_abi_sharded_outer_step_world1(dev, wdt):
+    from evolutionarydistributedtraining_amd import ops
+    from evolutionarydistributedtraining_amd.comm import Comm
+    n, n_pad, K = 100_003, 100_032, 5                      # n_pad: a multiple of 64 (world 1)
+    g = torch.Generator(device=dev).manual_seed(9)
+    theta0 = torch.zeros(n_pad, device=dev)
+    theta0[:n] = torch.randn(n, generator=g, device=dev) * 0.02
+    workers = []
+    for _ in range(K):
+        w = torch.zeros(n_pad, dtype=wdt, device=dev)
+        w[:n] = (theta0[:n] + torch.randn(n, generator=g, device=dev) * 1e-3).to(wdt)
+        workers.append(w)
+    ref_t, ref_m = theta0.clone(), torch.zeros(n_pad, device=dev)
+    th, mom, acc = theta0.clone(), torch.zeros(n_pad, device=dev), torch.empty(n_pad, device=dev)
+    c = Comm(Comm.unique_id(), 1, 0)
+    try:
+        for has in (False, True, True):
+            ops.outer_step(ref_t, workers, ref_m, has, 0.7, 0.9, True)
+            c.outer_step_sharded(th, workers, mom, has, 0.7, 0.9, True, acc, bucket_elems=16_384)
+        torch.cuda.synchronize()
+    finally:
+        c.close()
+    assert torch.equal(th.view(torch.int32), ref_t.view(torch.int32))
+    assert torch.equal(mom.view(torch.int32), ref_m.view(torch.int32))
+    assert not th[n:].any()

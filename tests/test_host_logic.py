@@ -142,6 +142,21 @@ def test_library_exports_every_header_symbol():
     assert lib.edt_outer_step_bytes_per_elem(0, 1, 8, 1) == 32
 
 
+def test_comm_library_exports_every_header_symbol():
+    """libedt_comm.so (include/edt_comm.h: RCCL behind the C ABI) loads without a GPU and binds
+    every declared entry point; running them is the GPU tests' job."""
+    from evolutionarydistributedtraining_amd import comm
+    lib = comm.load_comm_library()
+    with open(os.path.join(ROOT, "include", "edt_comm.h")) as f:
+        header = f.read()
+    names = set(re.findall(r"^\s*(?:int|uint64_t|const char\*)\s+(edt_\w+)\s*\(", header, re.M))
+    assert len(names) == 12, names
+    assert names == {n for n, _, _ in comm.SIGNATURES}
+    for n in names:
+        assert hasattr(lib, n), n
+    assert lib.edt_comm_id_bytes() == 128
+
+
 def test_c_consumer_builds_and_links():
     """tests/c_abi/abi_consumer.c includes only include/edt_sync.h (+ the HIP runtime) and links
     against libedt_sync.so with gcc: the boundary is usable with no Python in between. Running it
