@@ -28,14 +28,15 @@ def _windows(n, count, width, seed):
     return sorted(starts) + [n - 777]          # ... and the ragged end (tail < 8 elements)
 
 
-def test_outer_step_1p3b_windows(oracle, dev):
+@pytest.mark.parametrize("wdt", [torch.bfloat16, torch.float32])   # fp32: the bench default (split halves)
+def test_outer_step_1p3b_windows(oracle, dev, wdt):
     from evolutionarydistributedtraining_amd import ops
     from evolutionarydistributedtraining_amd.layouts import gpt_1p3b
     P = gpt_1p3b().total
     K, W = 8, 4096
     gen = torch.Generator(device=dev).manual_seed(3)
     theta = torch.randn(P, device=dev, generator=gen) * 0.02
-    workers = [(theta + torch.randn(P, device=dev, generator=gen) * 1e-3).bfloat16() for _ in range(K)]
+    workers = [(theta + torch.randn(P, device=dev, generator=gen) * 1e-3).to(wdt) for _ in range(K)]
     mom = torch.randn(P, device=dev, generator=gen) * 1e-3
     wins = _windows(P, 48, W, 11)
     widths = [W] * 48 + [777]
