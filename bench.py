@@ -67,7 +67,7 @@ def parse():
     p.add_argument("--weak-companion", type=int, default=1,
                    help="N>1: after the timed strong-scaling steps, also time W = population workers per GPU "
                         "(weak scaling) and report it beside the value as 'weak_scaling'")
-    p.add_argument("--place-candidates", type=int, default=6,
+    p.add_argument("--place-candidates", type=int, default=8,
                    help="N=1: choose the momentum buffer's HBM placement among this many allocations by "
                         "timing the step's access pattern on each, once before the timed steps (placement.py); "
                         "1 keeps the first allocation")

@@ -187,7 +187,7 @@ class OuterSync:
         _step_flat(self.theta.flat, [w.flat for w in self.workers], self.state, self.lr,
                    self.momentum, self.nesterov)
 
-    def place_momentum(self, candidates: int = 6) -> dict:
+    def place_momentum(self, candidates: int = 8) -> dict:
         """Choose where the outer momentum lives in HBM by measurement, once, for the life of
         the run (placement.place_momentum: the step's two read-modify-write streams conflict
         or not depending on their relative physical placement). Creates the buffer if the

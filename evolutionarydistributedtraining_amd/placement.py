@@ -49,7 +49,7 @@ def probe_ms(theta: torch.Tensor, workers: list[torch.Tensor], momentum: torch.T
 
 
 def place_momentum(theta: torch.Tensor, workers: list[torch.Tensor], momentum: torch.Tensor,
-                   candidates: int = 6, iters: int = 3, spacer_bytes: int = 11 << 27):
+                   candidates: int = 8, iters: int = 3, spacer_bytes: int = 11 << 27):
     """Return (buffer, report): the momentum's contents in whichever of `candidates` placements
     (the current buffer + candidates - 1 fresh allocations) runs the step's access pattern
     fastest, and {"candidates", "probe_ms", "chosen"}.
