@@ -23,6 +23,10 @@ on the wire (distributed.py).
 
 Prints ONE JSON line on rank 0. Also reports the fused kernel's own duration (HIP events on the
 stream it is launched on), the HBM roofline fraction, and the CPU oracle timed on this host.
+At N=1, after the warm-up steps and before the timed ones, the momentum buffer's HBM placement is
+chosen by measurement (OuterSync.place_momentum, placement.py: the step's two read-modify-write
+streams run up to 11 % faster or slower depending on their relative physical placement); the
+candidates' probe times are in roofline.momentum_placement, and --place-candidates 1 disables it.
 """
 from __future__ import annotations
 
