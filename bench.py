@@ -219,7 +219,10 @@ def main():
     if not sharded and args.place_candidates > 1:
         # once per run, outside the timed region: the momentum buffer goes wherever the step's
         # access pattern runs fastest (placement.py); every later step uses that placement
-        placement = sync.place_momentum(args.place_candidates)
+        try:
+            placement = sync.place_momentum(args.place_candidates)
+        except Exception as e:          # a measurement extra: report it, keep the first allocation
+            placement = {"error": f"{type(e).__name__}: {e}"}
         step()
         torch.cuda.synchronize()
 
@@ -337,7 +340,11 @@ def main():
             del src, dst
             # the step's own access pattern with a trivial body (edt_probe_stream), same arenas:
             # the memory-system ceiling of this step on this device, measured after the timed steps
-            probe_ms = stream_ceiling_ms(theta.flat, [w.flat for w in workers], sync.state.momentum)
+            try:
+                probe_ms = stream_ceiling_ms(theta.flat, [w.flat for w in workers], sync.state.momentum)
+            except Exception as e:      # a measurement extra: the JSON line still prints
+                probe_ms = None
+                roofline["stream_ceiling_error"] = f"{type(e).__name__}: {e}"
             if probe_ms:
                 ceil = algo_bytes / (probe_ms / 1e3) / 1e9
                 roofline["stream_ceiling_GBps"] = round(ceil, 1)
