@@ -265,13 +265,17 @@ def main():
         # fixed, so value_N / (N value_1) isolates the cost of the xGMI exchange
         del sync, step
         torch.cuda.empty_cache()
-        w_ms, w_sched, w_wire = time_sharded(args, layout, tdt, wdt, args.population, dev, rank,
-                                             args.steps, args.warmup)
-        w_bytes = args.population * world * P * torch.finfo(wdt).bits // 8
-        weak = {"workers_per_gpu": args.population, "population": args.population * world,
-                "ms_per_step": round(w_ms, 4), "value": round(w_bytes / (w_ms / 1e3) / 1e9, 2),
-                "unit": "GB/s", "schedule": w_sched, "wire_bytes_per_rank": w_wire,
-                "note": "companion measurement after the timed strong-scaling steps; not the value"}
+        try:
+            w_ms, w_sched, w_wire = time_sharded(args, layout, tdt, wdt, args.population, dev, rank,
+                                                 args.steps, args.warmup)
+            w_bytes = args.population * world * P * torch.finfo(wdt).bits // 8
+            weak = {"workers_per_gpu": args.population, "population": args.population * world,
+                    "ms_per_step": round(w_ms, 4), "value": round(w_bytes / (w_ms / 1e3) / 1e9, 2),
+                    "unit": "GB/s", "schedule": w_sched, "wire_bytes_per_rank": w_wire,
+                    "note": "companion measurement after the timed strong-scaling steps; not the value"}
+        except torch.cuda.OutOfMemoryError as e:     # the value is already measured: report, go on
+            weak = {"error": f"OutOfMemoryError: {str(e)[:200]}"}
+            torch.cuda.empty_cache()
         sync = None
 
     if rank == 0:
