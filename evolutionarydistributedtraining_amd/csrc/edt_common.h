@@ -50,6 +50,9 @@ using edt::g_err;
 #ifndef EDT_NT_LOADS          // non-temporal loads for the once-read bf16 worker streams
 #define EDT_NT_LOADS 1        // (fp32 streams: measured 1.6x SLOWER with nt, 17.5 vs 11.2 ms)
 #endif
+#ifndef EDT_NT_RMW            // non-temporal loads for theta / momentum (read, then rewritten)
+#define EDT_NT_RMW 0
+#endif
 #ifndef EDT_NT_STORES         // non-temporal stores for theta / momentum
 #define EDT_NT_STORES 0
 #endif
@@ -276,7 +279,7 @@ inline SgdScalars make_sgd(int gdt, double lr, double mu, int has_buf, int neste
 // Loads the carried momentum buffer (issued together with the other operand loads).
 template <int GDT, int N, int H2 = 4>
 __device__ __forceinline__ void ld_momentum(const void* mom, uint64_t i, const SgdScalars& s, float (&b)[N]) {
-    if (s.use_momentum && s.has_buf) ld<GDT, N, false, H2>(mom, i, b);
+    if (s.use_momentum && s.has_buf) ld<GDT, N, (EDT_NT_RMW != 0), H2>(mom, i, b);
 }
 
 template <int GDT, int N, int H2 = 4>

@@ -60,7 +60,7 @@ enum { MODE_FUSED = 0, MODE_PARTIAL = 1, MODE_CHAIN = 2 };
 template <int GDT, int WDT, int KC, int DIV, int MODE, int N, class A, int H2 = 4>
 __device__ __forceinline__ void outer_elems(const A& a, uint64_t i) {
     float g[N], acc[N], b_in[N];
-    ld<GDT, N, false, H2>(a.theta, i, g);
+    ld<GDT, N, (EDT_NT_RMW != 0), H2>(a.theta, i, g);
     if constexpr (MODE != MODE_PARTIAL) ld_momentum<GDT, N, H2>(a.mom, i, a.sgd, b_in);
     if (MODE == MODE_PARTIAL && a.accumulate) {
         ld<EDT_F32, N, false, H2>(a.acc_out, i, acc);      // continue the running sum in worker order

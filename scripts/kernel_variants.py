@@ -99,7 +99,8 @@ VARIANTS.update({"f32_nt": ["-DEDT_NT_F32=1"], "f32_bpc64": ["-DEDT_BLOCKS_PER_C
                  "f32_nt_oneshot": ["-DEDT_NT_F32=1", "-DEDT_BLOCKS_PER_CU=0"],
                  "f32_nt_ntst": ["-DEDT_NT_F32=1", "-DEDT_NT_STORES=1"],
                  "f32_nt_bpc128": ["-DEDT_NT_F32=1", "-DEDT_BLOCKS_PER_CU=128"]})
-VARIANTS.update({"default": [], "f32_ntst": ["-DEDT_NT_STORES=1"],
+VARIANTS.update({"default": [], "f32_ntst": ["-DEDT_NT_STORES=1"], "nt_rmw": ["-DEDT_NT_RMW=1"],
+                 "nt_rmw_st": ["-DEDT_NT_RMW=1", "-DEDT_NT_STORES=1"],
                  "s_bpc1024": ["-DEDT_SLERP_BPC=1024"], "s_bpc4096": ["-DEDT_SLERP_BPC=4096"]})
 VARIANTS.update({"split0": ["-DEDT_SPLIT_HALVES=0"], "split1": ["-DEDT_SPLIT_HALVES=1"],
                  "split1_nt0": ["-DEDT_SPLIT_HALVES=1", "-DEDT_NT_LOADS=0"]})
