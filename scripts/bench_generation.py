@@ -68,13 +68,16 @@ def main():
                                      slerp_chunk=a.slerp_chunk)
             arenas = [pop.params(m) for m in range(P)]
         g = torch.Generator(device=dev).manual_seed(1)
-        common = torch.randn(n, generator=g, device=dev) * 0.02 if a.members == "lineage" else None
-        for x in arenas:
-            if common is None:
-                x.copy_(torch.randn(n, generator=g, device=dev) * 0.02)
-            else:
-                x.copy_(common + torch.randn(n, generator=g, device=dev) * 0.02 * 0.005)
-        del common
+        step = 1 << 28                      # fill in chunks: fp32 temporaries stay ~1 GiB at 7B
+        for s0 in range(0, n, step):
+            e = min(n, s0 + step)
+            common = torch.randn(e - s0, generator=g, device=dev) * 0.02 if a.members == "lineage" else None
+            for x in arenas:
+                if common is None:
+                    x[s0:e].copy_(torch.randn(e - s0, generator=g, device=dev) * 0.02)
+                else:
+                    x[s0:e].copy_(common + torch.randn(e - s0, generator=g, device=dev) * 0.02 * 0.005)
+            del common
         fitness = [float(m) for m in range(P)]
         pop.step(fitness)                      # generation 0 (first-step momentum), warm-up
         torch.cuda.synchronize()
