@@ -110,9 +110,44 @@ def cpu_baseline(args, theta_dtype, worker_dtype, k):
     times.sort()
     t = times[len(times) // 2]
     gbps = k * n * torch.finfo(worker_dtype).bits / 8 / t / 1e9
-    return {"value": round(gbps, 3), "unit": "GB/s", "cores": oracle.max_threads(), "kind": "port",
-            "sample": f"{n} elements x {k} workers (fused delta+mean+SGD, oracle/edt_oracle.c, "
-                      f"median of {len(times)} reps over {args.cpu_baseline_seconds:.0f}s)"}
+    out = {"value": round(gbps, 3), "unit": "GB/s", "cores": oracle.max_threads(), "kind": "port",
+           "sample": f"{n} elements x {k} workers (fused delta+mean+SGD, oracle/edt_oracle.c, "
+                     f"median of {len(times)} reps over {args.cpu_baseline_seconds:.0f}s)"}
+    del theta, workers, mom
+    out["reference_loop"] = reference_loop_baseline(args, theta_dtype, worker_dtype, k)
+    return out
+
+
+def reference_loop_baseline(args, theta_dtype, worker_dtype, k):
+    """The reference's outer step as it runs on its master's CPU (per-tensor torch ops + SGD,
+    restated in oracle.torch_loop_outer_step) over the first tensors of the bench layout, up to
+    the same element budget: the cost the fused kernel replaces, next to the C port above."""
+    from evolutionarydistributedtraining_amd.layouts import LAYOUTS
+    from oracle import oracle
+    shapes, total = [], 0
+    for shp in LAYOUTS[args.layout]().shapes:         # in order, skipping what would overflow
+        m = int(torch.Size(shp).numel())
+        if total + m <= args.cpu_sample_elems:
+            shapes.append(shp)
+            total += m
+    g = torch.Generator().manual_seed(2)
+    base = [(torch.randn(shp, generator=g) * 0.02).to(theta_dtype) for shp in shapes]
+    workers = [[(p.float() + torch.randn(p.shape, generator=g) * 1e-3).to(worker_dtype) for p in base]
+               for _ in range(k)]
+    opt = oracle.torch_loop_outer_step(base, workers, None, args.lr, args.momentum, bool(args.nesterov))
+    times = []
+    t_end = time.perf_counter() + args.cpu_baseline_seconds / 2
+    while time.perf_counter() < t_end or len(times) < 2:
+        t0 = time.perf_counter()
+        opt = oracle.torch_loop_outer_step(base, workers, opt, args.lr, args.momentum, bool(args.nesterov))
+        times.append(time.perf_counter() - t0)
+    times.sort()
+    t = times[len(times) // 2]
+    return {"value": round(k * total * torch.finfo(worker_dtype).bits / 8 / t / 1e9, 3), "unit": "GB/s",
+            "threads": torch.get_num_threads(),
+            "sample": f"{len(shapes)} tensors of {args.layout} in order ({total} elements) x {k} workers, "
+                      f"EDT_LM/diloco.py:238-289's per-tensor torch loop + torch.optim.SGD "
+                      f"(oracle.torch_loop_outer_step), median of {len(times)} reps"}
 
 
 def stream_ceiling_ms(theta, workers, momentum, iters=10):

@@ -186,3 +186,25 @@ def slerp_coefficients(t: float, v0, v1, dot_threshold: float = 0.9995, eps: flo
     th0 = np.arccos(dot)
     th_t = th0 * t
     return np.sin(th0 - th_t) / np.sin(th0), np.sin(th_t) / np.sin(th0), dot
+
+
+# ---- the reference's CPU loop as it runs (timing baseline, not a checker) ---------------------
+
+def torch_loop_outer_step(base_params: list[torch.Tensor], worker_params: list[list[torch.Tensor]],
+                          optimizer: torch.optim.Optimizer | None, lr: float, mu: float, nesterov: bool):
+    """The DiLoCo outer step the way EDT_LM/diloco.py:238-289 executes it on the master's CPU: per
+    parameter tensor, a running sum of (trained - base) / num_models built with torch ops (one
+    temporary per op), `p.grad = -sum`, then torch.optim.SGD (single-tensor CPU path). Restated
+    here so bench.py can time the reference's own cost profile on the GPU box's host, where the
+    reference's files are not available. Returns the optimizer (carried across calls)."""
+    K = len(worker_params)
+    for i, p in enumerate(base_params):
+        acc = torch.zeros_like(p)
+        for k in range(K):
+            acc += (worker_params[k][i] - p) / K
+        p.grad = -acc
+    if optimizer is None:
+        optimizer = torch.optim.SGD(base_params, lr=lr, momentum=mu, nesterov=nesterov)
+    optimizer.step()
+    optimizer.zero_grad()
+    return optimizer
