@@ -132,3 +132,22 @@ def test_diloco_large_bf16_parallel_tails(golden, oracle):
     assert torch.equal(bits(mom), bits(flat(golden.tlist("diloco", f"{pre}/s1/out_buf", T))))
     # and without the tail model the differences are confined to those tail elements
     assert int(tail.sum()) < 0.01 * tail.numel()
+
+
+def test_torch_loop_restatement_matches_c_oracle(oracle):
+    """oracle.torch_loop_outer_step (the reference's loop as bench.py times it on the host) computes
+    what the C oracle does, bit for bit, over two generations with the carried SGD buffer (fp32)."""
+    g = torch.Generator().manual_seed(4)
+    shapes = [(33, 7), (5,), (300,), (64, 64)]
+    K = 3
+    base = [torch.randn(s, generator=g) * 0.02 for s in shapes]
+    workers = [[p + torch.randn(p.shape, generator=g) * 1e-3 for p in base] for _ in range(K)]
+    flat = torch.cat([p.reshape(-1) for p in base])
+    wflat = [torch.cat([p.reshape(-1) for p in w]) for w in workers]
+    mom = torch.zeros_like(flat)
+    opt = None
+    for gen in range(2):
+        opt = oracle.torch_loop_outer_step(base, workers, opt, 0.7, 0.9, True)
+        oracle.outer_step(flat, wflat, mom, gen > 0, 0.7, 0.9, True)
+        got = torch.cat([p.detach().reshape(-1) for p in base])
+        assert torch.equal(got.view(torch.int32), flat.view(torch.int32)), gen
