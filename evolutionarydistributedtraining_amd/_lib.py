@@ -53,6 +53,7 @@ SIGNATURES = [
     ("edt_slerp_merge_list", _I, [ctypes.POINTER(_P), ctypes.POINTER(_P), _I, ctypes.POINTER(_P), _I, _P,
                                   ctypes.c_int64, _P, _I, _P, _D, _D, _P, _P, _P, _P, _U64, _P]),
     ("edt_slerp_population_gram_doubles", _U64, [_I, ctypes.c_int64]),
+    ("edt_slerp_population_speculative_doubles", _U64, [_I, ctypes.c_int64]),
     ("edt_slerp_population", _I, [ctypes.POINTER(_P), _I, _I, ctypes.POINTER(ctypes.c_int32), _I,
                                   ctypes.POINTER(_P), _I, _P, ctypes.c_int64, _P, _I, _P, _D, _D, _P, _P, _P,
                                   _P]),

@@ -391,7 +391,7 @@ __global__ __launch_bounds__(kBlock) void slerp_pop_stats_lerp_kernel(BlendChild
 __global__ __launch_bounds__(kBlock) void slerp_gram_coef_kernel(const double* gram, int NT, int qi, int qj, int qd,
                                                                  const int32_t* first, int nseg,
                                                                  const double* tvals, float thr, float eps,
-                                                                 float* coef, float* dot_out) {
+                                                                 float* coef, float* dot_out, int32_t* redo = nullptr) {
     const int seg = coef_segment();
     if (seg >= nseg) return;
     double sums[3];
@@ -401,6 +401,97 @@ __global__ __launch_bounds__(kBlock) void slerp_gram_coef_kernel(const double* g
     coef[2 * seg] = c0;
     coef[2 * seg + 1] = c1;
     if (dot_out) dot_out[seg] = dot;
+    if (redo) redo[seg] = fabsf(dot) > thr ? 0 : 1;   // as slerp_coef_kernel
+}
+
+// The speculative population pass in member-major form: per chunk, every distinct parent's tile
+// is loaded ONCE into registers; from it the thread accumulates the Gram sums (gram_accumulate's
+// exact FMA order, so every child's sums equal chunk_sums' on its two parents) and writes every
+// child's lerp-branch output (chunk_pass' EMIT math). A shared parent crosses HBM once for all
+// its children regardless of cache residency.
+struct PopLerp {
+    void* out[kBlendMaxChildren];
+    int32_t a[kBlendMaxChildren], b[kBlendMaxChildren];   // compact member indices of the parents
+    int n;
+};
+
+template <int M, int N>
+__device__ __forceinline__ void pick(const float (&x)[M][N], int idx, float (&y)[N]) {
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+        if (m == idx) {                 // idx is uniform across the workgroup: no divergence
+#pragma unroll
+            for (int j = 0; j < N; ++j) y[j] = x[m][j];
+        }
+}
+
+template <int IDT, int ODT, int M, int N>
+__device__ __forceinline__ void gram_lerp_elems(const Members& mem, const PopLerp& po, uint64_t i, float l0, float l1,
+                                                double (&g)[M * (M + 1) / 2]) {
+    float x[M][N];
+#pragma unroll
+    for (int m = 0; m < M; ++m) ld<IDT, N>(mem.p[m], i, x[m]);
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+#pragma unroll
+        for (int a = 0; a < M; ++a) {
+            const double da = x[a][j];
+#pragma unroll
+            for (int b = a; b < M; ++b) {
+                const double db = x[b][j];
+                g[tri_index(a, b, M)] = __builtin_fma(da, db, g[tri_index(a, b, M)]);
+            }
+        }
+    }
+    for (int q = 0; q < po.n; ++q) {
+        float u[N], v[N], o[N];
+        pick<M, N>(x, po.a[q], u);
+        pick<M, N>(x, po.b[q], v);
+#pragma unroll
+        for (int j = 0; j < N; ++j) o[j] = l0 * u[j] + l1 * v[j];
+        st<ODT, N>(po.out[q], i, o);
+    }
+}
+
+template <int IDT, int ODT, int M>
+__global__ __launch_bounds__(kBlock) void slerp_gram_lerp_kernel(Members mem, PopLerp po, const uint64_t* chunks,
+                                                                 int64_t nchunks, const double* tvals, double* gram) {
+    constexpr int NT = M * (M + 1) / 2;
+    __shared__ double red[NT][kBlock / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+        const uint64_t start = chunks[3 * c], end = start + chunks[3 * c + 1], seg = chunks[3 * c + 2];
+        const float l0 = (float)(1.0 - tvals[seg]), l1 = (float)tvals[seg];
+        double g[NT];
+#pragma unroll
+        for (int q = 0; q < NT; ++q) g[q] = 0.0;
+        const uint64_t a = (start + kVec - 1) / kVec * kVec;
+        const uint64_t b = end / kVec * kVec;
+        if (a < b) {
+            for (uint64_t i = a + (uint64_t)threadIdx.x * kVec; i < b; i += (uint64_t)kBlock * kVec)
+                gram_lerp_elems<IDT, ODT, M, kVec>(mem, po, i, l0, l1, g);
+        }
+        const uint64_t h_end = a < end ? a : end;
+        const uint64_t t_beg = b > a ? b : h_end;
+        const uint64_t nh = h_end - start, nt = end - t_beg;
+        if ((uint64_t)threadIdx.x < nh + nt) {
+            const uint64_t i = threadIdx.x < nh ? start + threadIdx.x : t_beg + (threadIdx.x - nh);
+            gram_lerp_elems<IDT, ODT, M, 1>(mem, po, i, l0, l1, g);
+        }
+#pragma unroll
+        for (int q = 0; q < NT; ++q) {
+            const double v = wave_sum(g[q]);
+            if (lane == 0) red[q][wave] = v;
+        }
+        __syncthreads();
+        if (threadIdx.x < NT) {
+            double acc = 0.0;
+#pragma unroll
+            for (int w = 0; w < kBlock / 64; ++w) acc += red[threadIdx.x][w];
+            gram[(uint64_t)c * NT + threadIdx.x] = acc;
+        }
+        __syncthreads();
+    }
 }
 
 
@@ -507,6 +598,12 @@ int edt_slerp_merge(const void* v0, const void* v1, int in_dt, void* out, int ou
     rc = edt_slerp_coef(partial, seg_first_chunk, nseg, t, dot_threshold, eps, coef, dot_out, stream);
     if (rc) return rc;
     return edt_slerp_blend(v0, v1, in_dt, out, out_dt, chunk_desc, nchunks, coef, stream);
+}
+
+uint64_t edt_slerp_population_speculative_doubles(int npairs, int64_t nchunks) {
+    if (npairs < 0 || nchunks < 0) return 0;
+    const uint64_t per = 3ull * (uint64_t)npairs > 36ull ? 3ull * (uint64_t)npairs : 36ull;   // 36: 8 x 9 / 2
+    return (uint64_t)nchunks * per;
 }
 
 uint64_t edt_slerp_population_gram_doubles(int nmembers, int64_t nchunks) {
@@ -663,7 +760,65 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
         }
     }
     hipStream_t s = (hipStream_t)stream;
-    for (int pass = 0; pass < 2; ++pass) {
+    // member-major first pass when the distinct parents fit one Gram tile (<= 8) and the children
+    // one launch (<= 16): every distinct parent read once per chunk, whatever the caches do
+    int compact[256];
+    int D = 0;
+    Members mem;
+    memset(&mem, 0, sizeof(mem));
+    bool fused = npairs <= kBlendMaxChildren && nmembers <= 256;
+    if (fused) {
+        for (int m = 0; m < nmembers; ++m) compact[m] = -1;
+        for (int q = 0; q < npairs && fused; ++q)
+            for (int e = 0; e < 2; ++e) {
+                const int m = pairs[2 * q + e];
+                if (compact[m] < 0) {
+                    if (D == kGramMaxMembers) { fused = false; break; }
+                    compact[m] = D;
+                    mem.p[D++] = members[m];
+                }
+            }
+    }
+    if (fused) {
+        PopLerp po;
+        memset(&po, 0, sizeof(po));
+        po.n = npairs;
+        for (int q = 0; q < npairs; ++q) {
+            po.out[q] = outs[q];
+            po.a[q] = compact[pairs[2 * q]];
+            po.b[q] = compact[pairs[2 * q + 1]];
+        }
+        const unsigned g = slerp_grid(nchunks);
+#define EDT_GL(M)                                                                                             \
+    case M:                                                                                                   \
+        if (in_dt == EDT_F32 && out_dt == EDT_F32)                                                            \
+            slerp_gram_lerp_kernel<EDT_F32, EDT_F32, M><<<g, kBlock, 0, s>>>(mem, po, chunk_desc, nchunks, t, partial); \
+        else if (in_dt == EDT_F32)                                                                            \
+            slerp_gram_lerp_kernel<EDT_F32, EDT_BF16, M><<<g, kBlock, 0, s>>>(mem, po, chunk_desc, nchunks, t, partial); \
+        else if (out_dt == EDT_F32)                                                                           \
+            slerp_gram_lerp_kernel<EDT_BF16, EDT_F32, M><<<g, kBlock, 0, s>>>(mem, po, chunk_desc, nchunks, t, partial); \
+        else                                                                                                  \
+            slerp_gram_lerp_kernel<EDT_BF16, EDT_BF16, M><<<g, kBlock, 0, s>>>(mem, po, chunk_desc, nchunks, t, partial); \
+        break;
+        switch (D) {
+            EDT_GL(1) EDT_GL(2) EDT_GL(3) EDT_GL(4) EDT_GL(5) EDT_GL(6) EDT_GL(7) EDT_GL(8)
+        }
+#undef EDT_GL
+        int rc = check_launch("slerp_gram_lerp_kernel");
+        if (rc) return rc;
+        const int NT = D * (D + 1) / 2;
+        for (int q = 0; q < npairs; ++q) {
+            const int i = compact[pairs[2 * q]], j = compact[pairs[2 * q + 1]];
+            const int lo = i < j ? i : j, hi = i < j ? j : i;
+            slerp_gram_coef_kernel<<<coef_grid(nseg), kBlock, 0, s>>>(
+                partial, NT, tri_index(i, i, D), tri_index(j, j, D), tri_index(lo, hi, D), seg_first_chunk, nseg, t,
+                (float)dot_threshold, (float)eps, coef + 2 * (size_t)nseg * q,
+                dot_out ? dot_out + (size_t)nseg * q : nullptr, redo + (size_t)nseg * q);
+            rc = check_launch("slerp_gram_coef_kernel");
+            if (rc) return rc;
+        }
+    }
+    for (int pass = fused ? 1 : 0; pass < 2; ++pass) {
         for (int q0 = 0; q0 < npairs; q0 += kBlendMaxChildren) {
             BlendChildren B;
             memset(&B, 0, sizeof(B));

@@ -323,7 +323,8 @@ def slerp_population(plan: SlerpPlan, members: list[torch.Tensor], pairs, outs: 
     dots = torch.empty((max(1, Q), max(1, plan.nseg)), dtype=torch.float32, device=dev)
     flat_pairs = (ctypes.c_int32 * max(1, 2 * Q))(*[int(x) for p in pairs for x in p])
     if speculate:
-        part = torch.empty(max(1, Q * plan.nchunks * 3), dtype=torch.float64, device=dev)
+        part = torch.empty(max(1, int(lib.edt_slerp_population_speculative_doubles(Q, plan.nchunks))),
+                           dtype=torch.float64, device=dev)
         redo = torch.empty(max(1, Q * plan.nseg), dtype=torch.int32, device=dev)
         L.check(lib.edt_slerp_population_speculative(
             L.ptr_array(members), M, L.dtype_code(in_dt), flat_pairs, Q, L.ptr_array(outs), L.dtype_code(out_dt),

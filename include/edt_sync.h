@@ -214,9 +214,13 @@ int edt_slerp_population(const void* const* members, int nmembers, int in_dt, co
 /* edt_slerp_population with edt_slerp_merge_speculative's first pass: one co-located launch
  * (every child of a chunk on one XCD, shared parents read once) forms each child's chunk sums and
  * writes its lerp-branch output; per child the coefficients flag (redo: [npairs][nseg] int32) the
- * SLERP-branch segments, which one co-located launch blends again. partial: [npairs][nchunks][3]
- * doubles. Outputs must not overlap any member (n elements each). Bit-identical to
- * edt_slerp_merge per child. */
+ * SLERP-branch segments, which one co-located launch blends again. When the children's distinct
+ * parents number <= 8 (and npairs <= 16) the first pass is member-major instead: one launch loads
+ * each distinct parent's tile once, forms their Gram sums and writes every child's lerp output.
+ * partial: edt_slerp_population_speculative_doubles(npairs, nchunks) doubles of workspace.
+ * Outputs must not overlap any member (n elements each). Bit-identical to edt_slerp_merge per
+ * child either way. */
+uint64_t edt_slerp_population_speculative_doubles(int npairs, int64_t nchunks);
 int edt_slerp_population_speculative(const void* const* members, int nmembers, int in_dt, const int32_t* pairs,
                                      int npairs, void* const* outs, int out_dt, const uint64_t* chunk_desc,
                                      int64_t nchunks, const int32_t* seg_first_chunk, int nseg, const double* t,
