@@ -494,6 +494,84 @@ __global__ __launch_bounds__(kBlock) void slerp_gram_lerp_kernel(Members mem, Po
     }
 }
 
+// The blends of every child in member-major form (the two-pass Gram form's second pass and the
+// speculative form's redo pass, <= 8 distinct parents): per chunk each distinct parent's tile is
+// loaded once and every child whose segment needs blending writes c0 v_i + c1 v_j from the same
+// registers (lerp_elems' math with the child's coefficients, as slerp_blend_kernel).
+struct PopBlend {
+    void* out[kBlendMaxChildren];
+    const float* coef[kBlendMaxChildren];     // [nseg][2] of the child
+    const int32_t* redo[kBlendMaxChildren];   // [nseg] of the child, or null: blend every segment
+    int32_t a[kBlendMaxChildren], b[kBlendMaxChildren];
+    int n;
+};
+
+template <int IDT, int ODT, int M, int N>
+__device__ __forceinline__ void blend_mm_elems(const Members& mem, const PopBlend& pb, uint64_t i, uint64_t seg,
+                                               uint32_t need) {
+    float x[M][N];
+#pragma unroll
+    for (int m = 0; m < M; ++m) ld<IDT, N>(mem.p[m], i, x[m]);
+    for (int q = 0; q < pb.n; ++q) {
+        if (!(need & (1u << q))) continue;
+        float u[N], v[N], o[N];
+        pick<M, N>(x, pb.a[q], u);
+        pick<M, N>(x, pb.b[q], v);
+        const float c0 = pb.coef[q][2 * seg], c1 = pb.coef[q][2 * seg + 1];
+#pragma unroll
+        for (int j = 0; j < N; ++j) o[j] = c0 * u[j] + c1 * v[j];
+        st<ODT, N>(pb.out[q], i, o);
+    }
+}
+
+template <int IDT, int ODT, int M>
+__global__ __launch_bounds__(kBlock) void slerp_blend_mm_kernel(Members mem, PopBlend pb, const uint64_t* chunks,
+                                                                int64_t nchunks) {
+    for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+        const uint64_t start = chunks[3 * c], end = start + chunks[3 * c + 1], seg = chunks[3 * c + 2];
+        uint32_t need = 0;                   // children whose output this segment still needs
+        for (int q = 0; q < pb.n; ++q)
+            if (!pb.redo[q] || pb.redo[q][seg]) need |= 1u << q;
+        if (!need) continue;                 // every child keeps its speculative lerp output
+        const uint64_t a = (start + kVec - 1) / kVec * kVec;
+        const uint64_t b = end / kVec * kVec;
+        if (a < b) {
+            for (uint64_t i = a + (uint64_t)threadIdx.x * kVec; i < b; i += (uint64_t)kBlock * kVec)
+                blend_mm_elems<IDT, ODT, M, kVec>(mem, pb, i, seg, need);
+        }
+        const uint64_t h_end = a < end ? a : end;
+        const uint64_t t_beg = b > a ? b : h_end;
+        const uint64_t nh = h_end - start, nt = end - t_beg;
+        if ((uint64_t)threadIdx.x < nh + nt) {
+            const uint64_t i = threadIdx.x < nh ? start + threadIdx.x : t_beg + (threadIdx.x - nh);
+            blend_mm_elems<IDT, ODT, M, 1>(mem, pb, i, seg, need);
+        }
+    }
+}
+
+// host: launch slerp_blend_mm_kernel over D compact parents
+inline int launch_blend_mm(const Members& mem, int D, const PopBlend& pb, int in_dt, int out_dt,
+                           const uint64_t* chunk_desc, int64_t nchunks, hipStream_t s) {
+    const unsigned g = slerp_grid(nchunks);
+#define EDT_BMM(M)                                                                                            \
+    case M:                                                                                                   \
+        if (in_dt == EDT_F32 && out_dt == EDT_F32)                                                            \
+            slerp_blend_mm_kernel<EDT_F32, EDT_F32, M><<<g, kBlock, 0, s>>>(mem, pb, chunk_desc, nchunks);    \
+        else if (in_dt == EDT_F32)                                                                            \
+            slerp_blend_mm_kernel<EDT_F32, EDT_BF16, M><<<g, kBlock, 0, s>>>(mem, pb, chunk_desc, nchunks);   \
+        else if (out_dt == EDT_F32)                                                                           \
+            slerp_blend_mm_kernel<EDT_BF16, EDT_F32, M><<<g, kBlock, 0, s>>>(mem, pb, chunk_desc, nchunks);   \
+        else                                                                                                  \
+            slerp_blend_mm_kernel<EDT_BF16, EDT_BF16, M><<<g, kBlock, 0, s>>>(mem, pb, chunk_desc, nchunks);  \
+        break;
+    switch (D) {
+        EDT_BMM(1) EDT_BMM(2) EDT_BMM(3) EDT_BMM(4) EDT_BMM(5) EDT_BMM(6) EDT_BMM(7) EDT_BMM(8)
+        default: return fail(EDT_ERR_ARG, "member-major blend over %d parents", D);
+    }
+#undef EDT_BMM
+    return check_launch("slerp_blend_mm_kernel");
+}
+
 
 
 int slerp_stats_impl(const void* v0, const void* v1, int in_dt, const uint64_t* chunk_desc, int64_t nchunks,
@@ -637,22 +715,35 @@ int edt_slerp_population(const void* const* members, int nmembers, int in_dt, co
             if (outs[q] == members[m]) return fail(EDT_ERR_ARG, "output %d aliases member %d", q, m);
     }
     hipStream_t s = (hipStream_t)stream;
+    // the Gram pass and the blends run over the distinct parents only (compact indices)
+    int compact[kGramMaxMembers];
+    int D = 0;
+    for (int m = 0; m < nmembers; ++m) compact[m] = -1;
+    memset(&mem, 0, sizeof(mem));
+    for (int q = 0; q < npairs; ++q)
+        for (int e = 0; e < 2; ++e) {
+            const int m = pairs[2 * q + e];
+            if (compact[m] < 0) {
+                compact[m] = D;
+                mem.p[D++] = members[m];
+            }
+        }
     const unsigned g = slerp_grid(nchunks);
 #define EDT_GRAM(M)                                                                                  \
     case M:                                                                                          \
         if (in_dt == EDT_F32) slerp_gram_kernel<EDT_F32, M><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, gram); \
         else slerp_gram_kernel<EDT_BF16, M><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, gram);              \
         break;
-    switch (nmembers) {
+    switch (D) {
         EDT_GRAM(1) EDT_GRAM(2) EDT_GRAM(3) EDT_GRAM(4) EDT_GRAM(5) EDT_GRAM(6) EDT_GRAM(7) EDT_GRAM(8)
     }
 #undef EDT_GRAM
     int rc = check_launch("slerp_gram_kernel");
     if (rc) return rc;
-    const int M = nmembers, NT = M * (M + 1) / 2;
+    const int M = D, NT = M * (M + 1) / 2;
     const unsigned gc = coef_grid(nseg);
     for (int q = 0; q < npairs; ++q) {
-        const int i = pairs[2 * q], j = pairs[2 * q + 1];
+        const int i = compact[pairs[2 * q]], j = compact[pairs[2 * q + 1]];
         const int lo = i < j ? i : j, hi = i < j ? j : i;
         slerp_gram_coef_kernel<<<gc, kBlock, 0, s>>>(gram, NT, tri_index(i, i, M), tri_index(j, j, M),
                                                      tri_index(lo, hi, M), seg_first_chunk, nseg, t,
@@ -661,7 +752,19 @@ int edt_slerp_population(const void* const* members, int nmembers, int in_dt, co
         rc = check_launch("slerp_gram_coef_kernel");
         if (rc) return rc;
     }
-    // the blends: every child in one co-located launch (groups of <= 16 children)
+    // the blends: member-major when the children fit one launch, else co-located groups of <= 16
+    if (npairs <= kBlendMaxChildren) {
+        PopBlend pb;
+        memset(&pb, 0, sizeof(pb));
+        pb.n = npairs;
+        for (int q = 0; q < npairs; ++q) {
+            pb.out[q] = outs[q];
+            pb.coef[q] = coef + 2 * (size_t)nseg * q;
+            pb.a[q] = compact[pairs[2 * q]];
+            pb.b[q] = compact[pairs[2 * q + 1]];
+        }
+        return launch_blend_mm(mem, D, pb, in_dt, out_dt, chunk_desc, nchunks, s);
+    }
     for (int q0 = 0; q0 < npairs; q0 += kBlendMaxChildren) {
         BlendChildren B;
         memset(&B, 0, sizeof(B));
@@ -818,7 +921,20 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
             if (rc) return rc;
         }
     }
-    for (int pass = fused ? 1 : 0; pass < 2; ++pass) {
+    if (fused) {                             // the redo blends, member-major over the same D parents
+        PopBlend pb;
+        memset(&pb, 0, sizeof(pb));
+        pb.n = npairs;
+        for (int q = 0; q < npairs; ++q) {
+            pb.out[q] = outs[q];
+            pb.coef[q] = coef + 2 * (size_t)nseg * q;
+            pb.redo[q] = redo + (size_t)nseg * q;
+            pb.a[q] = compact[pairs[2 * q]];
+            pb.b[q] = compact[pairs[2 * q + 1]];
+        }
+        return launch_blend_mm(mem, D, pb, in_dt, out_dt, chunk_desc, nchunks, s);
+    }
+    for (int pass = 0; pass < 2; ++pass) {
         for (int q0 = 0; q0 < npairs; q0 += kBlendMaxChildren) {
             BlendChildren B;
             memset(&B, 0, sizeof(B));
