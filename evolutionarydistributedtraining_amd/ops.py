@@ -288,8 +288,9 @@ def slerp_population(plan: SlerpPlan, members: list[torch.Tensor], pairs, outs: 
       speculate=True   edt_slerp_population_speculative: one co-located pass forms every child's
                        sums and writes its lerp-branch output, then only SLERP-branch segments
                        are blended again (parents of one lineage: a single pass);
-      None             speculate unless the previous call on this plan had half or more of its
-                       child elements in SLERP-branch segments.
+      None             speculate when the previous call on this plan had few enough child elements
+                       in SLERP-branch segments for the single pass to move fewer bytes
+                       (f < D b_in / (D b_in + Q b_out), D distinct parents, Q children).
     Returns the per-child, per-segment fp32 dots ([npairs, nseg])."""
     lib = L.lib()
     M, Q = len(members), len(pairs)
@@ -313,7 +314,11 @@ def slerp_population(plan: SlerpPlan, members: list[torch.Tensor], pairs, outs: 
             d = prev.cpu().numpy()
             sizes = np.diff(np.asarray(plan.seg_offsets, dtype=np.int64))
             f = float((sizes[None, :] * (np.abs(d) <= plan._last_thr)).sum()) / max(1, int(sizes.sum()) * d.shape[0])
-            speculate = f < 0.5
+            # member-major passes over D distinct parents: speculating costs (1 + f)(D b_in + Q b_out)
+            # against 2 D b_in + Q b_out for the Gram form
+            D = len({int(x) for p in pairs for x in p})
+            bi, bo = members[0].element_size(), (outs[0].element_size() if outs else members[0].element_size())
+            speculate = f < D * bi / max(1, D * bi + Q * bo)
     if any(_overlap(o, m) for o in outs for m in members):
         speculate = False
     if not speculate and not 1 <= M <= 8:
