@@ -79,7 +79,10 @@ __global__ __launch_bounds__(kBlock) void pair_kernel(PairArgs a) {
 // parent chunk crosses HBM once and its other readers hit the L2 / Infinity Cache. Per child the
 // element math is pair_elems' (bit-identical to edt_pair_merge_to).
 constexpr int kPopMaxChildren = 16;
-constexpr uint64_t kPopChunk = (uint64_t)kBlock * kVec * 4;     // 8192 elements per workgroup
+#ifndef EDT_POP_ITERS             // 8-element iterations per thread per population chunk
+#define EDT_POP_ITERS 4
+#endif
+constexpr uint64_t kPopChunk = (uint64_t)kBlock * kVec * EDT_POP_ITERS;   // 8192 elements per workgroup
 
 struct PopPairArgs {
     PairArgs c[kPopMaxChildren];

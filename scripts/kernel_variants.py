@@ -99,6 +99,7 @@ VARIANTS.update({"f32_nt": ["-DEDT_NT_F32=1"], "f32_bpc64": ["-DEDT_BLOCKS_PER_C
                  "f32_nt_oneshot": ["-DEDT_NT_F32=1", "-DEDT_BLOCKS_PER_CU=0"],
                  "f32_nt_ntst": ["-DEDT_NT_F32=1", "-DEDT_NT_STORES=1"],
                  "f32_nt_bpc128": ["-DEDT_NT_F32=1", "-DEDT_BLOCKS_PER_CU=128"]})
+VARIANTS.update({f"pop{i}": [f"-DEDT_POP_ITERS={i}"] for i in (1, 2, 8, 16)})
 VARIANTS.update({"default": [], "f32_ntst": ["-DEDT_NT_STORES=1"], "nt_rmw": ["-DEDT_NT_RMW=1"],
                  "nt_rmw_st": ["-DEDT_NT_RMW=1", "-DEDT_NT_STORES=1"],
                  "s_bpc1024": ["-DEDT_SLERP_BPC=1024"], "s_bpc4096": ["-DEDT_SLERP_BPC=4096"]})
@@ -279,6 +280,56 @@ def run_slerp_pop(names, rounds, layout_name="gpt_1p3b", P_members=8):
                      indent=1))
 
 
+def run_pair_pop(names, rounds, layout_name="gpt_1p3b"):
+    """One resident EDT-LM generation (edt_pair_merge_population, 8 children of 6 distinct parents,
+    bf16 members and momenta) per variant library."""
+    import torch
+    from evolutionarydistributedtraining_amd import _lib as L
+    from evolutionarydistributedtraining_amd.layouts import LAYOUTS
+    dev = torch.device("cuda:0")
+    n = LAYOUTS[layout_name]().total
+    bf = torch.bfloat16
+    g = torch.Generator(device=dev).manual_seed(3)
+    M = 8
+    base = [(torch.randn(n, device=dev, generator=g) * 0.02).to(bf) for _ in range(M)]
+    trained = [(b.float() + 1e-3).to(bf) for b in base]
+    moms = [(torch.randn(n, device=dev, generator=g) * 1e-3).to(bf) for _ in range(M)]
+    pairs = [(0, 1), (1, 2), (2, 0), (3, 4), (4, 5), (5, 3), (0, 3), (1, 4)]   # 6 distinct parents
+    outs = [torch.empty(n, dtype=bf, device=dev) for _ in pairs]
+    omom = [torch.empty(n, dtype=bf, device=dev) for _ in pairs]
+    C = len(pairs)
+    arr = lambda ts: (ctypes.c_void_p * C)(*[t.data_ptr() for t in ts])
+    a_b1, a_b2 = arr([base[i] for i, _ in pairs]), arr([base[j] for _, j in pairs])
+    a_m1, a_m2 = arr([trained[i] for i, _ in pairs]), arr([trained[j] for _, j in pairs])
+    a_out, a_min, a_mout = arr(outs), arr([moms[i] for i, _ in pairs]), arr(omom)
+    has = (ctypes.c_int32 * C)(*([1] * C))
+    stream = L.stream_ptr(dev)
+    cases = {}
+    for nm in names:
+        lib = ctypes.CDLL(os.path.join(VDIR, f"{nm}.so"))
+        for name, res, args in L.SIGNATURES:
+            f = getattr(lib, name)
+            f.restype, f.argtypes = res, args
+        cases[nm] = (lambda lib=lib: lib.edt_pair_merge_population(a_b1, a_b2, a_m1, a_m2, 1, a_out, 1, a_min, a_mout,
+                                                                   has, C, n, 0.7, 0.9, 1, stream))
+    times = {k: [] for k in cases}
+    for k, f in cases.items():
+        assert f() == 0
+    torch.cuda.synchronize()
+    for _ in range(rounds):
+        for k, f in cases.items():
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            assert f() == 0
+            b.record()
+            torch.cuda.synchronize()
+            times[k].append(a.elapsed_time(b))
+    floor = n * (6 * 2 * 2 + 6 * 2 + C * 2 * 2)     # distinct parents' base + trained, donor moms, children
+    res = {k: {"median_ms": round(statistics.median(v), 4),
+               "floor_TBps": round(floor / statistics.median(v) / 1e9, 3)} for k, v in times.items()}
+    print(json.dumps({"op": "pair_pop", "n": n, "variants": res}, indent=1))
+
+
 def build(names):
     from evolutionarydistributedtraining_amd.build import build_library
     os.makedirs(VDIR, exist_ok=True)
@@ -351,7 +402,7 @@ if __name__ == "__main__":
     ap.add_argument("--k", type=int, default=8)
     ap.add_argument("--tdt", default="f32")
     ap.add_argument("--wdt", default="bf16")
-    ap.add_argument("--op", default="outer", choices=["outer", "slerp", "slerp_pop", "stream", "list"])
+    ap.add_argument("--op", default="outer", choices=["outer", "slerp", "slerp_pop", "stream", "list", "pair_pop"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:
@@ -360,6 +411,8 @@ if __name__ == "__main__":
         run_stream_ops(names, a.rounds, a.iters)
     elif a.op == "list":
         run_list(names, a.rounds, a.iters, a.wdt)
+    elif a.op == "pair_pop":
+        run_pair_pop(names, a.rounds)
     elif a.op == "slerp_pop":
         run_slerp_pop(names, a.rounds)
     elif a.op == "slerp":
