@@ -113,6 +113,33 @@ __global__ __launch_bounds__(kBlock) void pair_population_kernel(PopPairArgs P) 
 }
 
 
+// The same generation with the child loop inside the thread: each thread owns an 8-element slice
+// of the arena (one-pass grid, address order) and runs pair_elems for every child on it, so a
+// parent slice shared by several children is re-read within a few instructions by the same
+// thread (an L1 hit), not by another workgroup that may run after it has left the L2.
+#ifndef EDT_POP_LOOP
+#define EDT_POP_LOOP 0
+#endif
+template <int GDT, int WDT, bool VEC>
+__global__ __launch_bounds__(kBlock) void pair_population_loop_kernel(PopPairArgs P) {
+    const uint64_t n = P.c[0].n;
+    const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if constexpr (VEC) {
+        const uint64_t nv = n / kVec;
+        if (tid < nv) {
+            for (int q = 0; q < P.nchildren; ++q) pair_elems<GDT, WDT, kVec, false>(P.c[q], tid * kVec);
+        }
+        const uint64_t t = nv * kVec + tid;
+        if (t < n) {
+            for (int q = 0; q < P.nchildren; ++q) pair_elems<GDT, WDT, 1, false>(P.c[q], t);
+        }
+    } else {
+        if (tid < n) {
+            for (int q = 0; q < P.nchildren; ++q) pair_elems<GDT, WDT, 1, false>(P.c[q], tid);
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 // lerp with a scalar t (lerp_elems in edt_common.h)
 
@@ -215,14 +242,17 @@ int edt_pair_merge_population(const void* const* b1, const void* const* b2, cons
               (!a.sgd.use_momentum || (aligned16(a.mom) && (!has || aligned16(a.mom_in))));
     }
     const uint64_t groups = (P.nchunks + 7) / 8;
-    const uint64_t blocks = groups * 8ull * (uint64_t)nchildren;
+    const uint64_t blocks = EDT_POP_LOOP ? (vec ? (n / kVec + kBlock - 1) / kBlock + 1 : (n + kBlock - 1) / kBlock)
+                                         : groups * 8ull * (uint64_t)nchildren;
     if (blocks > 0x7fffffffull) return fail(EDT_ERR_ARG, "too many elements for one launch");
     const unsigned g = (unsigned)blocks;
     hipStream_t s = (hipStream_t)stream;
 #define EDT_POP(G, W)                                                                   \
     do {                                                                                \
-        if (vec) pair_population_kernel<G, W, true><<<g, kBlock, 0, s>>>(P);            \
-        else pair_population_kernel<G, W, false><<<g, kBlock, 0, s>>>(P);               \
+        if (EDT_POP_LOOP && vec) pair_population_loop_kernel<G, W, true><<<g, kBlock, 0, s>>>(P);   \
+        else if (EDT_POP_LOOP) pair_population_loop_kernel<G, W, false><<<g, kBlock, 0, s>>>(P);   \
+        else if (vec) pair_population_kernel<G, W, true><<<g, kBlock, 0, s>>>(P);       \
+        else pair_population_kernel<G, W, false><<<g, kBlock, 0, s>>>(P);              \
     } while (0)
     if (gdt == EDT_F32 && wdt == EDT_F32) EDT_POP(EDT_F32, EDT_F32);
     else if (gdt == EDT_F32) EDT_POP(EDT_F32, EDT_BF16);
