@@ -19,28 +19,21 @@ struct PairArgs {
     SgdScalars sgd;
 };
 
-template <int GDT, int WDT, int N, bool NT = (EDT_NT_LOADS != 0 && WDT == EDT_BF16)>
-__device__ __forceinline__ void pair_elems(const PairArgs& a, uint64_t i) {
-    float base[N], b_in[N];
-    ld_momentum<GDT, N>(a.mom_in, i, a.sgd, b_in);
-    if (a.b2) {                        // run_linear_merge_5050: lerp(0.5, b1, b2) in the model dtype
-        float x[N], y[N];
-        ld<WDT, N, NT>(a.b1, i, x);
-        ld<WDT, N, NT>(a.b2, i, y);
+// The merge of one child from its already-loaded inputs (lerp base from x = b1, y = b2; trained
+// weights d1 = m1, d2 = m2; carried buffer b_in): shared by pair_elems and the member-major
+// population kernel, so both compute the same bits.
+template <int GDT, int WDT, int N>
+__device__ __forceinline__ void pair_core(const PairArgs& a, uint64_t i, float (&x)[N], float (&y)[N],
+                                          float (&d1)[N], float (&d2)[N], const float (&b_in)[N]) {
+    float base[N];
 #pragma unroll
-        for (int j = 0; j < N; ++j) { x[j] = x[j] * 0.5f; y[j] = y[j] * 0.5f; }   // (1-.5)*v0, .5*v1
-        rnd<WDT>(x);
-        rnd<WDT>(y);
+    for (int j = 0; j < N; ++j) { x[j] = x[j] * 0.5f; y[j] = y[j] * 0.5f; }   // (1-.5)*v0, .5*v1
+    rnd<WDT>(x);
+    rnd<WDT>(y);
 #pragma unroll
-        for (int j = 0; j < N; ++j) base[j] = x[j] + y[j];
-        rnd<WDT>(base);
-    } else {                           // run_sgd on an already merged base model (dtype GDT)
-        ld<GDT, N>(a.b1, i, base);
-    }
+    for (int j = 0; j < N; ++j) base[j] = x[j] + y[j];
+    rnd<WDT>(base);
     rnd<GDT>(base);                    // load_state_dict into the base model's dtype
-    float d1[N], d2[N];
-    ld<WDT, N, NT>(a.m1, i, d1);
-    ld<WDT, N, NT>(a.m2, i, d2);
 #pragma unroll
     for (int j = 0; j < N; ++j) { d1[j] = d1[j] - base[j]; d2[j] = d2[j] - base[j]; }
     rnd<GDT>(d1);
@@ -54,6 +47,42 @@ __device__ __forceinline__ void pair_elems(const PairArgs& a, uint64_t i) {
     float grad[N];
 #pragma unroll
     for (int j = 0; j < N; ++j) grad[j] = -(0.f + d1[j]);           // acc = zeros + delta
+    sgd_update<GDT, N>(base, grad, a.mom, i, a.sgd, b_in);
+    st<GDT, N>(a.out, i, base);
+}
+
+template <int GDT, int WDT, int N, bool NT = (EDT_NT_LOADS != 0 && WDT == EDT_BF16)>
+__device__ __forceinline__ void pair_elems(const PairArgs& a, uint64_t i) {
+    float b_in[N];
+    ld_momentum<GDT, N>(a.mom_in, i, a.sgd, b_in);
+    if (a.b2) {                        // run_linear_merge_5050: lerp(0.5, b1, b2) in the model dtype
+        float x[N], y[N], d1[N], d2[N];
+        ld<WDT, N, NT>(a.b1, i, x);
+        ld<WDT, N, NT>(a.b2, i, y);
+        ld<WDT, N, NT>(a.m1, i, d1);
+        ld<WDT, N, NT>(a.m2, i, d2);
+        pair_core<GDT, WDT, N>(a, i, x, y, d1, d2, b_in);
+        return;
+    }
+    float base[N];                     // run_sgd on an already merged base model (dtype GDT)
+    ld<GDT, N>(a.b1, i, base);
+    rnd<GDT>(base);
+    float d1[N], d2[N];
+    ld<WDT, N, NT>(a.m1, i, d1);
+    ld<WDT, N, NT>(a.m2, i, d2);
+#pragma unroll
+    for (int j = 0; j < N; ++j) { d1[j] = d1[j] - base[j]; d2[j] = d2[j] - base[j]; }
+    rnd<GDT>(d1);
+    rnd<GDT>(d2);
+#pragma unroll
+    for (int j = 0; j < N; ++j) d1[j] = d1[j] + d2[j];
+    rnd<GDT>(d1);
+#pragma unroll
+    for (int j = 0; j < N; ++j) d1[j] = d1[j] * 0.5f;
+    rnd<GDT>(d1);
+    float grad[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) grad[j] = -(0.f + d1[j]);
     sgd_update<GDT, N>(base, grad, a.mom, i, a.sgd, b_in);
     st<GDT, N>(a.out, i, base);
 }
@@ -113,12 +142,89 @@ __global__ __launch_bounds__(kBlock) void pair_population_kernel(PopPairArgs P) 
 }
 
 
+// Member-major form (bf16 members and momenta, <= 8 distinct parents): each thread loads every
+// distinct parent's base / trained tile and every distinct donor momentum tile of its 8-element
+// slice once (all loads in flight together), then runs pair_core for each child from those
+// registers. A shared parent crosses HBM once per slice by construction, and the children's
+// bits are pair_elems' (same pair_core).
+constexpr int kMMParents = 8;
+struct PopMM {
+    const void* b[kMMParents];
+    const void* m[kMMParents];
+    const void* mom[kMMParents];
+    int32_t ia[kPopMaxChildren], ib[kPopMaxChildren], im[kPopMaxChildren];   // im < 0: no carried buffer
+    int np, nmom;                                                             // parents, donor buffers
+};
+
+template <int D>
+__device__ __forceinline__ u32x4 pick_tile(const u32x4 (&t)[D], int idx) {
+    // a bitwise blend per slot (idx is uniform): keeps the tiles in registers, where a select
+    // chain would be folded back into a dynamically indexed array (scratch memory)
+    u32x4 r = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        const uint32_t m = 0u - (uint32_t)(d == idx);
+        r.x |= t[d].x & m;
+        r.y |= t[d].y & m;
+        r.z |= t[d].z & m;
+        r.w |= t[d].w & m;
+    }
+    return r;
+}
+
+__device__ __forceinline__ void unpack8(u32x4 w, float (&x)[8]) {
+    x[0] = bf_lo(w.x); x[1] = bf_hi(w.x); x[2] = bf_lo(w.y); x[3] = bf_hi(w.y);
+    x[4] = bf_lo(w.z); x[5] = bf_hi(w.z); x[6] = bf_lo(w.w); x[7] = bf_hi(w.w);
+}
+
+template <int D>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4)))
+void pair_population_mm_kernel(PopPairArgs P, PopMM M) {
+    const uint64_t n = P.c[0].n, nv = n / kVec;
+    const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (tid < nv) {
+        const uint64_t i = tid * kVec;
+        u32x4 tb[D], tm[D], tmo[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d)
+            if (d < M.np) {
+                tb[d] = *reinterpret_cast<const u32x4*>(static_cast<const uint16_t*>(M.b[d]) + i);
+                tm[d] = *reinterpret_cast<const u32x4*>(static_cast<const uint16_t*>(M.m[d]) + i);
+            }
+#pragma unroll
+        for (int d = 0; d < D; ++d)
+            if (d < M.nmom) tmo[d] = *reinterpret_cast<const u32x4*>(static_cast<const uint16_t*>(M.mom[d]) + i);
+#pragma unroll
+        for (int q = 0; q < kPopMaxChildren; ++q) {
+            if (q >= P.nchildren) break;
+            float x[kVec], y[kVec], d1[kVec], d2[kVec], b_in[kVec];
+            unpack8(pick_tile<D>(tb, M.ia[q]), x);
+            unpack8(pick_tile<D>(tb, M.ib[q]), y);
+            unpack8(pick_tile<D>(tm, M.ia[q]), d1);
+            unpack8(pick_tile<D>(tm, M.ib[q]), d2);
+            if (M.im[q] >= 0) unpack8(pick_tile<D>(tmo, M.im[q]), b_in);
+            else {
+#pragma unroll
+                for (int j = 0; j < kVec; ++j) b_in[j] = 0.f;
+            }
+            pair_core<EDT_BF16, EDT_BF16, kVec>(P.c[q], i, x, y, d1, d2, b_in);
+        }
+    }
+    const uint64_t t = nv * kVec + tid;                  // scalar tail (< 8 elements)
+    if (t < n)
+        for (int q = 0; q < P.nchildren; ++q) pair_elems<EDT_BF16, EDT_BF16, 1, false>(P.c[q], t);
+}
+
 // The same generation with the child loop inside the thread: each thread owns an 8-element slice
 // of the arena (one-pass grid, address order) and runs pair_elems for every child on it, so a
 // parent slice shared by several children is re-read within a few instructions by the same
 // thread (an L1 hit), not by another workgroup that may run after it has left the L2.
 #ifndef EDT_POP_LOOP
 #define EDT_POP_LOOP 0
+#endif
+#ifndef EDT_POP_MM              // member-major population kernel (bf16, <= 8 distinct parents): measured
+                                // 17.2-17.7 ms vs 15.9-16.7 co-located at 1.3B x 8 (8 parents), so off
+#define EDT_POP_MM 0
 #endif
 template <int GDT, int WDT, bool VEC>
 __global__ __launch_bounds__(kBlock) void pair_population_loop_kernel(PopPairArgs P) {
@@ -240,6 +346,59 @@ int edt_pair_merge_population(const void* const* b1, const void* const* b2, cons
         }
         vec = vec && aligned16(a.b1) && aligned16(a.b2) && aligned16(a.m1) && aligned16(a.m2) && aligned16(a.out) &&
               (!a.sgd.use_momentum || (aligned16(a.mom) && (!has || aligned16(a.mom_in))));
+    }
+    // member-major when every child merges two bf16 parents of <= 8 distinct (base, trained)
+    // pairs and the vector body applies (EDT_POP_MM, off by default: see its definition)
+    if (EDT_POP_MM && vec && gdt == EDT_BF16 && wdt == EDT_BF16) {
+        PopMM M;
+        memset(&M, 0, sizeof(M));
+        int D = 0;
+        bool ok = true;
+        auto parent = [&](const void* b, const void* m) -> int {
+            for (int d = 0; d < D; ++d)
+                if (M.b[d] == b && M.m[d] == m) return d;
+            if (D == kMMParents) return -1;
+            M.b[D] = b;
+            M.m[D] = m;
+            return D++;
+        };
+        for (int c = 0; c < nchildren && ok; ++c) {
+            const PairArgs& a = P.c[c];
+            if (!a.b2) { ok = false; break; }
+            M.ia[c] = parent(a.b1, a.m1);
+            M.ib[c] = parent(a.b2, a.m2);
+            if (M.ia[c] < 0 || M.ib[c] < 0) { ok = false; break; }
+            M.im[c] = -1;
+            if (a.sgd.use_momentum && a.sgd.has_buf) {
+                int k = 0;
+                while (k < M.nmom && M.mom[k] != a.mom_in) ++k;
+                if (k == M.nmom) {
+                    if (M.nmom == kMMParents) { ok = false; break; }
+                    M.mom[M.nmom++] = a.mom_in;
+                }
+                M.im[c] = k;
+            }
+        }
+        if (ok && D >= 1) {
+            M.np = D;
+            const uint64_t nv = n / kVec;
+            const uint64_t bl = (nv + kBlock - 1) / kBlock + 1;
+            if (bl > 0x7fffffffull) return fail(EDT_ERR_ARG, "too many elements for one launch");
+            hipStream_t s = (hipStream_t)stream;
+            const unsigned gm = (unsigned)bl;
+            if (M.nmom > D) D = M.nmom;         // tile arrays sized for parents and donors alike
+            switch (D) {
+                case 1: pair_population_mm_kernel<1><<<gm, kBlock, 0, s>>>(P, M); break;
+                case 2: pair_population_mm_kernel<2><<<gm, kBlock, 0, s>>>(P, M); break;
+                case 3: pair_population_mm_kernel<3><<<gm, kBlock, 0, s>>>(P, M); break;
+                case 4: pair_population_mm_kernel<4><<<gm, kBlock, 0, s>>>(P, M); break;
+                case 5: pair_population_mm_kernel<5><<<gm, kBlock, 0, s>>>(P, M); break;
+                case 6: pair_population_mm_kernel<6><<<gm, kBlock, 0, s>>>(P, M); break;
+                case 7: pair_population_mm_kernel<7><<<gm, kBlock, 0, s>>>(P, M); break;
+                default: pair_population_mm_kernel<8><<<gm, kBlock, 0, s>>>(P, M); break;
+            }
+            return check_launch("pair_population_mm_kernel");
+        }
     }
     const uint64_t groups = (P.nchunks + 7) / 8;
     const uint64_t blocks = EDT_POP_LOOP ? (vec ? (n / kVec + kBlock - 1) / kBlock + 1 : (n + kBlock - 1) / kBlock)
