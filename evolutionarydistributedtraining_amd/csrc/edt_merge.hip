@@ -194,9 +194,7 @@ void pair_population_mm_kernel(PopPairArgs P, PopMM M) {
 #pragma unroll
         for (int d = 0; d < D; ++d)
             if (d < M.nmom) tmo[d] = *reinterpret_cast<const u32x4*>(static_cast<const uint16_t*>(M.mom[d]) + i);
-#pragma unroll
-        for (int q = 0; q < kPopMaxChildren; ++q) {
-            if (q >= P.nchildren) break;
+        for (int q = 0; q < P.nchildren; ++q) {       // runtime child count: not unrolled
             float x[kVec], y[kVec], d1[kVec], d2[kVec], b_in[kVec];
             unpack8(pick_tile<D>(tb, M.ia[q]), x);
             unpack8(pick_tile<D>(tb, M.ib[q]), y);
