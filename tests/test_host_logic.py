@@ -245,3 +245,57 @@ def test_sgd_argument_errors_match_torch():
             torch.optim.SGD([torch.zeros(1, requires_grad=True)], lr=lr, momentum=mu, nesterov=nest)
         assert str(ours.value) == str(theirs.value)
     check_sgd_hparams(1.0, 0.0, False)        # diloco_sim.py defaults are valid
+
+
+def test_abi_error_convention_without_device():
+    """The C ABI's error convention (include/edt_sync.h: 0 or a negative EDT_ERR_*, the reason in
+    edt_last_error()) for arguments the library rejects on the host before any HIP call — the
+    reference raises at the same points (a Python exception, e.g. EDT_LM/train/crossover.py:227).
+    Pointers here are host addresses that are never dereferenced; n = 0 (empty tensors) returns 0
+    without a launch."""
+    import ctypes
+    from evolutionarydistributedtraining_amd import _lib
+    lib = _lib.load_library()
+    P = ctypes.c_void_p
+    host = (ctypes.c_uint8 * 4096)()
+    base = ctypes.addressof(host)
+    p = [P(base + 64 * i) for i in range(32)]          # distinct 16-byte aligned fake addresses
+
+    def arr(ptrs):
+        return (P * len(ptrs))(*ptrs)
+
+    def err(rc, needle):
+        msg = lib.edt_last_error().decode()
+        assert rc == -1 and needle in msg, (rc, msg)
+
+    F32, BF16 = 0, 1
+    ks = arr(p[1:9])
+    # edt_outer_step (EDT_LM/diloco.py:238-289)
+    err(lib.edt_outer_step(p[0], 5, ks, F32, 8, p[9], 1, 8, 0.7, 0.9, 1, None), "dtype")
+    err(lib.edt_outer_step(p[0], BF16, ks, F32, 8, p[9], 1, 8, 0.7, 0.9, 1, None), "dtype")  # bf16 theta, f32 workers
+    err(lib.edt_outer_step(p[0], F32, ks, F32, 0, p[9], 1, 8, 0.7, 0.9, 1, None), "worker count")
+    err(lib.edt_outer_step(p[0], F32, arr(p[:1] * 65), F32, 65, p[9], 1, 8, 0.7, 0.9, 1, None), "out of range")
+    err(lib.edt_outer_step(p[0], F32, arr([p[1], None, p[3]]), F32, 3, p[9], 1, 8, 0.7, 0.9, 1, None),
+        "theta_k[1] is null")
+    err(lib.edt_outer_step(p[0], F32, ks, F32, 8, None, 1, 8, 0.7, 0.9, 1, None), "momentum buffer is null")
+    assert lib.edt_outer_step(None, F32, ks, F32, 8, None, 0, 0, 0.7, 0.0, 0, None) == 0   # empty
+    assert lib.edt_last_error() == b""
+    # edt_pair_merge_to (EDT_LM/train/crossover.py:166-237)
+    err(lib.edt_pair_merge_to(p[1], p[2], p[3], p[4], 3, p[5], F32, p[6], p[7], 1, 8, 0.7, 0.9, 1, None), "dtype")
+    err(lib.edt_pair_merge_to(None, p[2], p[3], p[4], BF16, p[5], BF16, p[6], p[7], 1, 8, 0.7, 0.9, 1, None),
+        "null buffer")
+    err(lib.edt_pair_merge_to(p[1], p[2], p[3], p[4], BF16, p[5], BF16, None, p[7], 1, 8, 0.7, 0.9, 1, None),
+        "carried momentum is null")
+    assert lib.edt_pair_merge_to(None, None, None, None, BF16, None, BF16, None, None, 0, 0, 0.7, 0.9, 1, None) == 0
+    # edt_pair_merge_population: child count, and an output that is another child's input
+    one = arr(p[1:2])
+    err(lib.edt_pair_merge_population(one, one, one, one, BF16, one, BF16, None, None, None, 17, 8,
+                                      0.7, 0.0, 0, None), "child count")
+    b1, b2, m1, m2 = arr([p[1], p[2]]), arr([p[3], p[4]]), arr([p[5], p[6]]), arr([p[7], p[8]])
+    err(lib.edt_pair_merge_population(b1, b2, m1, m2, BF16, arr([p[9], p[1]]), BF16, None, None, None, 2, 8,
+                                      0.7, 0.0, 0, None), "child 1 writes an input of child 0")
+    err(lib.edt_pair_merge_population(b1, b2, m1, m2, BF16, arr([p[9], p[9]]), BF16, None, None, None, 2, 8,
+                                      0.7, 0.0, 0, None), "write the same buffer")
+    # edt_lerp (crossover.py:50-51): fp32 inputs computed in bf16 is not a reference combination
+    err(lib.edt_lerp(p[1], p[2], F32, p[3], F32, BF16, 8, 0.5, None), "bf16 compute of fp32")
+    err(lib.edt_lerp(p[1], None, BF16, p[3], BF16, BF16, 8, 0.5, None), "null buffer")
