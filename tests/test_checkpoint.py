@@ -82,3 +82,25 @@ def test_read_many_parallel_matches_serial(tmp_path):
     checkpoint.read_many(list(zip(dirs, arenas)), layout, threads=4, staging_bytes=4096)
     for a, w in zip(arenas, want):
         assert torch.equal(a, w)
+
+
+def test_broadcast_copies_are_independent_files(tmp_path):
+    """save_to_dirs gives every worker dir its own file with the same bytes (no hard links), so a
+    worker rewriting its checkpoint in place (save_pretrained truncates; EDT_LM/diloco.py:302-308's
+    next generation) leaves the others intact, and no temporary file is left behind."""
+    m = _tiny(torch.float32)
+    layout = ParamLayout.of_module(m)
+    flat = pack(list(m.parameters()))
+    dirs = [str(tmp_path / f"w{k}") for k in range(4)]
+    checkpoint.save_to_dirs(dirs, layout, flat)
+    files = [os.path.join(d, "model.safetensors") for d in dirs]
+    ref = open(files[0], "rb").read()
+    assert len({os.stat(f).st_ino for f in files}) == 4
+    assert all(open(f, "rb").read() == ref for f in files)
+    with open(files[1], "wb") as f:                   # an in-place rewrite of one worker's file
+        f.write(b"x")
+    assert all(open(f, "rb").read() == ref for f in files[:1] + files[2:])
+    assert not any(n.endswith(".tmp") for d in dirs for n in os.listdir(d))
+    sd = load_file(files[3])
+    for (name, _), v in zip(m.named_parameters(), layout.views(flat)):
+        assert torch.equal(sd[name], v)
