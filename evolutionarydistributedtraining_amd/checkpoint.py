@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import json
 import os
+import re
 import struct
 import threading
 
@@ -35,15 +36,31 @@ def read_header(path: str):
 
 
 def checkpoint_files(model_dir: str) -> dict[str, str]:
-    """tensor name -> file for a HF save_pretrained directory (single or sharded)."""
-    idx = os.path.join(model_dir, "model.safetensors.index.json")
-    if os.path.exists(idx):
-        with open(idx) as f:
-            wm = json.load(f)["weight_map"]
-        return {k: os.path.join(model_dir, v) for k, v in wm.items()}
+    """tensor name -> file for a HF save_pretrained directory (single or sharded). A single
+    `model.safetensors` wins over an index, as transformers resolves it: a directory holding both
+    (a sharded save overwritten by a single-file one) loads the single file."""
     path = os.path.join(model_dir, "model.safetensors")
-    header, _ = read_header(path)
-    return {k: path for k in header if k != "__metadata__"}
+    if os.path.exists(path):
+        header, _ = read_header(path)
+        return {k: path for k in header if k != "__metadata__"}
+    idx = os.path.join(model_dir, "model.safetensors.index.json")
+    with open(idx) as f:
+        wm = json.load(f)["weight_map"]
+    return {k: os.path.join(model_dir, v) for k, v in wm.items()}
+
+
+_SHARD_RE = re.compile(r"^model-\d+-of-\d+\.safetensors$")
+
+
+def remove_stale_shards(model_dir: str) -> None:
+    """Delete a sharded save's index and shard files (`model-XXXXX-of-YYYYY.safetensors`), as
+    save_pretrained cleans up weight files it is not rewriting: after a single-file save into a
+    worker dir that held the trained replica as shards, no reader can pick the stale shards."""
+    if not os.path.isdir(model_dir):
+        return
+    for f in os.listdir(model_dir):
+        if f == "model.safetensors.index.json" or _SHARD_RE.match(f):
+            os.remove(os.path.join(model_dir, f))
 
 
 class _Staging:
@@ -245,5 +262,9 @@ def save_to_dirs(dirs: list[str], layout: ParamLayout, flat: torch.Tensor, names
     host = _host_copy(flat)
     for d in dirs:
         os.makedirs(d, exist_ok=True)
+
+    def one(d):
+        _write_file(os.path.join(d, "model.safetensors"), header, host)
+        remove_stale_shards(d)        # the dir may hold the trained replica as index + shards
     with ThreadPoolExecutor(max_workers=min(len(dirs), 16)) as ex:
-        list(ex.map(lambda d: _write_file(os.path.join(d, "model.safetensors"), header, host), dirs))
+        list(ex.map(one, dirs))

@@ -184,7 +184,8 @@ void pair_population_mm_kernel(PopPairArgs P, PopMM M) {
     const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (tid < nv) {
         const uint64_t i = tid * kVec;
-        u32x4 tb[D], tm[D], tmo[D];
+        // every slot defined: pick_tile ANDs all D slots, including those past np / nmom
+        u32x4 tb[D] = {}, tm[D] = {}, tmo[D] = {};
 #pragma unroll
         for (int d = 0; d < D; ++d)
             if (d < M.np) {

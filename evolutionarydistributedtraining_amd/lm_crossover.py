@@ -177,9 +177,12 @@ def _read_parents_direct(paths, dev):
             return None
         if any(n not in have for n in layout.names):
             return None
-    dtype = next(child.parameters()).dtype
-    arena = bind_module_(child, ParamArena(layout, dtype, dev), copy=False)
-    parents = [read_into_arena(p, layout, torch.empty(layout.total, dtype=dtype, device=dev)) for p in paths]
+    # the child keeps its own dtype; the parents are always read as bf16, as the reference loads
+    # them (from_pretrained(torch_dtype=bf16), :67-70), so lerp(0.5) of the bases rounds to bf16
+    # even when from_config builds an fp32 child (the kernel takes bf16 parents + an fp32 child)
+    arena = bind_module_(child, ParamArena(layout, next(child.parameters()).dtype, dev), copy=False)
+    parents = [read_into_arena(p, layout, torch.empty(layout.total, dtype=torch.bfloat16, device=dev))
+               for p in paths]
     return child, arena, parents
 
 

@@ -120,8 +120,15 @@ def pair_merge(b1: torch.Tensor, b2: torch.Tensor | None, m1: torch.Tensor, m2: 
     n = out.numel()
     if any(t is not None and t.numel() != n for t in (b1, b2, m1, m2, momentum, momentum_in)):
         raise L.EdtError("pair-merge buffers must all have the same size")
-    if momentum_in is not None and momentum is not None and momentum_in.dtype != momentum.dtype:
-        raise L.EdtError("momentum_in and momentum must share a dtype")
+    # the kernel reads b1/b2/m2 as m1's dtype (b1 as out's when b2 is None) and both momenta as
+    # out's dtype: a mismatch would reinterpret raw bytes
+    if b2 is not None:
+        if not (b1.dtype == b2.dtype == m1.dtype == m2.dtype):
+            raise L.EdtError("b1, b2, m1 and m2 must share one dtype")
+    elif b1.dtype != out.dtype or m1.dtype != m2.dtype:
+        raise L.EdtError("with b2=None, b1 (the merged base) must have out's dtype and m1, m2 one dtype")
+    if any(t is not None and t.dtype != out.dtype for t in (momentum, momentum_in)):
+        raise L.EdtError("momentum buffers must have out's dtype")
     mom_in = momentum if momentum_in is None else momentum_in
     L.check(lib.edt_pair_merge_to(L.ptr(b1), L.ptr(b2), L.ptr(m1), L.ptr(m2), L.dtype_code(m1),
                                   L.ptr(out), L.dtype_code(out), L.ptr(mom_in), L.ptr(momentum),
@@ -371,6 +378,8 @@ def pair_merge_population(children, lr: float, momentum_coef: float, nesterov: b
             raise L.EdtError("pair-merge buffers must all have the same size")
         if any(ch[k].dtype != wdt for k in ("b1", "b2", "m1", "m2")) or ch["out"].dtype != gdt:
             raise L.EdtError("one parent dtype and one child dtype for the whole population")
+        if any(ch.get(k) is not None and ch[k].dtype != gdt for k in ("momentum", "momentum_in")):
+            raise L.EdtError("momentum buffers must have the child's dtype")
     has = (ctypes.c_int32 * C)(*[int(bool(ch.get("has_momentum"))) for ch in children])
     mom_out = [ch.get("momentum") for ch in children]
     mom_in = [ch.get("momentum_in") if ch.get("has_momentum") else None for ch in children]

@@ -104,3 +104,36 @@ def test_broadcast_copies_are_independent_files(tmp_path):
     sd = load_file(files[3])
     for (name, _), v in zip(m.named_parameters(), layout.views(flat)):
         assert torch.equal(sd[name], v)
+
+
+def test_broadcast_over_a_sharded_replica_reads_back_the_broadcast(tmp_path):
+    """A worker dir holding its trained replica as index + shards (a model too big for one
+    file) receives the new global model from save_to_dirs (EDT_LM/diloco.py:302-308): the stale
+    index and shards are removed, and reading the dir back (a restarted master, _read_parents_direct)
+    returns the broadcast weights, not the trained ones."""
+    m = _tiny(torch.float32)
+    d = tmp_path / "w0"
+    m.save_pretrained(d, max_shard_size="8KB")
+    assert os.path.exists(d / "model.safetensors.index.json")
+    layout = ParamLayout.of_module(m)
+    new = pack(list(m.parameters())) * 3 + 1
+    checkpoint.save_to_dirs([str(d)], layout, new)
+    left = sorted(os.listdir(d))
+    assert "model.safetensors.index.json" not in left
+    assert not any(f.startswith("model-") for f in left)
+    got = checkpoint.read_into_arena(str(d), layout, torch.empty(layout.total))
+    assert torch.equal(got, new)
+
+
+def test_single_file_wins_over_a_stale_index(tmp_path):
+    """checkpoint_files resolves model.safetensors before an index, as transformers does."""
+    m = _tiny(torch.float32)
+    d = tmp_path / "w"
+    m.save_pretrained(d, max_shard_size="8KB")
+    layout = ParamLayout.of_module(m)
+    new = pack(list(m.parameters())) - 5
+    checkpoint.write_from_arena(str(d / "model.safetensors"), layout, new)
+    assert os.path.exists(d / "model.safetensors.index.json")
+    assert set(checkpoint.checkpoint_files(str(d)).values()) == {str(d / "model.safetensors")}
+    got = checkpoint.read_into_arena(str(d), layout, torch.empty(layout.total))
+    assert torch.equal(got, new)
