@@ -21,6 +21,19 @@ on the wire (distributed.py).
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
+`--gpus N` without torchrun (no WORLD_SIZE in the environment) starts its own N rank processes —
+child processes of this one, before anything touches the GPU (no exec) — with RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set, waits for them and exits with their status;
+rank 0 prints the line. `--dry-run-launch` makes each rank print its environment and stop before
+device initialisation (the CPU test of the launcher).
+
+Every line carries `roofline` (the rank's local HBM kernels: at N = 1 the fused step, at N > 1 the
+schedule's kernels timed with HIP events inside the step; N > 1 adds the xGMI figure as
+`roofline.xgmi`) and `cpu_baseline` (rank 0, after the GPU phase, on the host's cores). At N = 1
+the line also carries `pair_merge` (EDT-LM child, 1.3B bf16) and `slerp_7b` (SLERP crossover of two
+7B bodies, parents of one lineage and far parents), each with its kernel time, HBM roofline and an
+oracle CPU baseline on a sample (`--ops none` drops them).
+
 Prints ONE JSON line on rank 0. Also reports the fused kernel's own duration (HIP events on the
 stream it is launched on), the HBM roofline fraction, and the CPU oracle timed on this host.
 At N=1, after the warm-up steps and before the timed ones, the momentum buffer's HBM placement is
@@ -76,7 +89,47 @@ def parse():
                         "timing the step's access pattern on each, once before the timed steps (placement.py); "
                         "1 keeps the first allocation")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    p.add_argument("--ops", default="pair_merge,slerp_7b",
+                   help="N=1: the other hot-path kernels measured after the outer step, in the same line "
+                        "('none': skip)")
+    p.add_argument("--ops-cpu-seconds", type=float, default=4.0, help="CPU baseline budget per extra op")
+    p.add_argument("--dry-run-launch", action="store_true",
+                   help="each rank prints its rank environment and exits before device init")
     return p.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """`--gpus N` without torchrun: N child processes running this script with the rank
+    environment torchrun would give them. Runs in a process that has not touched the GPU and
+    starts children (never exec). A failing rank ends the others. Returns the exit status."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    status = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc
+                for q in live:                   # a dead rank would leave the others in a collective
+                    q.terminate()
+        time.sleep(0.05)
+    return status
 
 
 def synth_population(theta: torch.Tensor, workers: list[torch.Tensor], seed: int) -> None:
@@ -150,6 +203,135 @@ def reference_loop_baseline(args, theta_dtype, worker_dtype, k):
                       f"(oracle.torch_loop_outer_step), median of {len(times)} reps"}
 
 
+def _median_time(fn, seconds):
+    fn()
+    times = []
+    t_end = time.perf_counter() + seconds
+    while time.perf_counter() < t_end or len(times) < 2:
+        t0 = time.perf_counter()
+        fn()
+        times.append(time.perf_counter() - t0)
+    times.sort()
+    return times[len(times) // 2], len(times)
+
+
+def _event_ms(fn, steps, warmup):
+    """Mean HIP-event time of `fn` (launches on torch's current stream) over `steps` calls."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    for a, b in ev:
+        a.record()
+        fn()
+        b.record()
+    torch.cuda.synchronize()
+    ts = [a.elapsed_time(b) for a, b in ev]
+    return sum(ts) / len(ts)
+
+
+def bench_pair_merge(args, dev):
+    """EDT-LM child (EDT_LM/train/crossover.py:150-237: lerp(.5) of the bases, mean of the two
+    pseudo-gradients, Nesterov SGD with the carried momentum) over the 1.3B layout, bf16 parents,
+    child and momentum: one edt_pair_merge launch, 14 algorithmic bytes per element (four parents
+    read, child written, momentum read + written)."""
+    from evolutionarydistributedtraining_amd import ops
+    from evolutionarydistributedtraining_amd.layouts import gpt_1p3b
+    from oracle import oracle
+    lay = gpt_1p3b()
+    P, bf = lay.total, torch.bfloat16
+    g = torch.Generator(device=dev).manual_seed(77)
+    b1 = (torch.randn(P, generator=g, device=dev) * 0.02).to(bf)
+    b2 = (torch.randn(P, generator=g, device=dev) * 0.02).to(bf)
+    m1 = (b1.float() + torch.randn(P, generator=g, device=dev) * 1e-3).to(bf)
+    m2 = (b2.float() + torch.randn(P, generator=g, device=dev) * 1e-3).to(bf)
+    mom = (torch.randn(P, generator=g, device=dev) * 1e-3).to(bf)
+    out = torch.empty(P, dtype=bf, device=dev)
+    ms = _event_ms(lambda: ops.pair_merge(b1, b2, m1, m2, out, mom, True, 0.7, 0.9, True), args.steps, args.warmup)
+    del b1, b2, m1, m2, mom, out
+    torch.cuda.empty_cache()
+    bpe = 14
+    gbs = bpe * P / (ms / 1e3) / 1e9
+    res = {"workload": f"EDT-LM pair merge, gpt_1p3b P={P}, bf16 parents/child/momentum, lr 0.7 mu 0.9 nesterov",
+           "kernel": "pair_kernel (edt_pair_merge_to)", "ms": round(ms, 4),
+           "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                        "frac": round(gbs / HBM_PEAK_GBPS, 4), "bytes_per_elem": bpe, "algo_bytes_per_launch": bpe * P}}
+    if args.ops_cpu_seconds > 0:
+        n = args.cpu_sample_elems
+        gc = torch.Generator().manual_seed(3)
+        xs = [(torch.randn(n, generator=gc) * 0.02).to(bf) for _ in range(4)]
+        mo = (torch.randn(n, generator=gc) * 1e-3).to(bf)
+        o = torch.empty(n, dtype=bf)
+        t, reps = _median_time(lambda: oracle.pair_merge(xs[0], xs[1], xs[2], xs[3], o, mo, True, 0.7, 0.9, True),
+                               args.ops_cpu_seconds)
+        res["cpu_baseline"] = {"value": round(bpe * n / t / 1e9, 3), "unit": "GB/s (algorithmic bytes)",
+                               "cores": oracle.max_threads(), "kind": "port",
+                               "sample": f"{n} elements (oracle/edt_oracle.c pair merge, median of {reps} reps)"}
+    return res
+
+
+def bench_slerp_7b(args, dev):
+    """SLERP crossover (EDT_RL/crossover.py:11-43 per state-dict key; EDT_EVOMERGE/train/
+    crossover.py:104-146 over Qwen2.5-7B's `model.model`) of two 7.07B-parameter bodies, bf16 in
+    and out, t = 0.5 on all 338 tensors, as ops.slerp_arena runs it (the form — speculative single
+    pass or two-pass — chosen from the previous merge's dots). 6 algorithmic bytes per element
+    (two parents read, child written). `lineage`: parents one fine-tune apart (0.5 % relative
+    difference: every tensor in the lerp branch); `far`: 5 % apart (every tensor in the SLERP
+    branch, whose dot needs a whole pass before the blend: 10 bytes moved per element)."""
+    from evolutionarydistributedtraining_amd import ops
+    from evolutionarydistributedtraining_amd.layouts import qwen2p5_7b_body
+    from oracle import oracle
+    lay = qwen2p5_7b_body()
+    P, bf = lay.total, torch.bfloat16
+    v0 = torch.empty(P, dtype=bf, device=dev)
+    v1 = torch.empty(P, dtype=bf, device=dev)
+    out = torch.empty(P, dtype=bf, device=dev)
+    plan = ops.make_slerp_plan(lay.offsets, dev)
+    t = torch.full((len(lay),), 0.5, dtype=torch.float64, device=dev)
+    g = torch.Generator(device=dev).manual_seed(11)
+    res = {"workload": f"SLERP crossover, qwen2p5_7b_body P={P} T={len(lay)}, bf16 in/out, t=0.5",
+           "kernel": "edt_slerp_merge / edt_slerp_merge_speculative"}
+    for parents, rel in (("lineage", 0.005), ("far", 0.05)):
+        step = 1 << 28
+        for s0 in range(0, P, step):
+            e = min(P, s0 + step)
+            x = torch.randn(e - s0, generator=g, device=dev) * 0.02
+            v0[s0:e] = x.to(bf)
+            v1[s0:e] = (x + torch.randn(e - s0, generator=g, device=dev) * 0.02 * rel).to(bf)
+            del x
+        plan._last_thr = None                    # a fresh pair: no previous merge to judge from
+        ms = _event_ms(lambda: ops.slerp_arena(plan, v0, v1, out, t), args.steps, max(2, args.warmup))
+        lerp_segs = int((plan.dots[:len(lay)].abs() > 0.9995).sum().item())
+        spec = ops._speculation_pays(plan, 2, 2)
+        gbs = 6 * P / (ms / 1e3) / 1e9
+        res[parents] = {"ms": round(ms, 4), "form": "speculative" if spec else "two_pass",
+                        "lerp_branch_segments": lerp_segs, "segments": len(lay),
+                        "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBPS,
+                                     "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBPS, 4), "bytes_per_elem": 6,
+                                     "algo_bytes_per_launch": 6 * P,
+                                     "moved_bytes_per_elem": 6 if spec else 10}}
+    del v0, v1, out, plan
+    torch.cuda.empty_cache()
+    if args.ops_cpu_seconds > 0:
+        # the reference's numpy SLERP (oracle.slerp restates it op for op) on the layout's first
+        # tensors up to the sample budget, far parents (the SLERP branch)
+        shapes, total = [], 0
+        for shp in lay.shapes:
+            m = int(torch.Size(shp).numel())
+            if total + m <= args.cpu_sample_elems // 4:
+                shapes.append(m)
+                total += m
+        gc = torch.Generator().manual_seed(5)
+        a = [(torch.randn(m, generator=gc) * 0.02) for m in shapes]
+        b = [(x + torch.randn(x.numel(), generator=gc) * 1e-3) for x in a]
+        tm, reps = _median_time(lambda: [oracle.slerp(0.5, x, y) for x, y in zip(a, b)], args.ops_cpu_seconds)
+        res["cpu_baseline"] = {"value": round(6 * total / tm / 1e9, 3), "unit": "GB/s (algorithmic bytes, bf16-sized)",
+                               "cores": torch.get_num_threads(), "kind": "port",
+                               "sample": f"{len(shapes)} tensors of qwen2p5_7b_body ({total} elements), "
+                                         f"EDT_RL/crossover.py:11-43's numpy SLERP (oracle.slerp), median of {reps} reps"}
+    return res
+
+
 def stream_ceiling_ms(theta, workers, momentum, iters=10):
     """Median HIP-event time of edt_probe_stream over the step's own operands (None if the
     step runs without momentum: the probe always reads and writes a momentum stream)."""
@@ -202,18 +384,27 @@ def time_sharded(args, layout, tdt, wdt, k_local, dev, rank, steps, warmup):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))       # this process never touches the GPU
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if not (world == 1 and args.gpus == 1):
-            raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch with torchrun")
-    torch.cuda.set_device(local)
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dry_run_launch:
+        print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                                          "MASTER_PORT")}), flush=True)
+        return
     sharded = world > 1 or args.sharded    # --sharded: the multi-GPU code path on one rank
+    if sharded and "MASTER_ADDR" not in os.environ:      # --gpus 1 --sharded without torchrun
+        os.environ.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
+                          MASTER_PORT=str(_free_port()))
+    torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     import torch.distributed as dist
     if sharded:
-        dist.init_process_group("nccl", device_id=dev)
+        from evolutionarydistributedtraining_amd.collectives import init_torch
+        init_torch("nccl", device_id=dev)
 
     from evolutionarydistributedtraining_amd import ops
     from evolutionarydistributedtraining_amd.layouts import LAYOUTS
@@ -245,7 +436,8 @@ def main():
         # replicas of theta must agree: rank 0's values everywhere
         dist.broadcast(sync.theta_buf, 0)
         step = sync.step
-        kernel_name = "outer_kernel" if sync.mode == "exact" else "outer_kernel(partial)"
+        kernel_name = ("outer_kernel (fused, owned shards)" if sync.mode == "exact"
+                       else "outer_kernel(partial) + sgd_apply_kernel")
 
     for _ in range(args.warmup):
         step()
@@ -261,10 +453,13 @@ def main():
         step()
         torch.cuda.synchronize()
 
-    # fused-kernel duration, measured with HIP events on the launch stream (torch's current)
+    # fused-kernel duration, measured with HIP events on the launch stream (torch's current);
+    # sharded: every local kernel of the schedule bracketed inside the step (ShardedOuterSync)
     kern_ms = None
     if not sharded:
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    else:
+        sync.kernel_events = []
 
     if sharded:
         dist.barrier()
@@ -288,6 +483,13 @@ def main():
     if not sharded:
         ks = sorted(a.elapsed_time(b) for a, b in ev)
         kern_ms = sum(ks) / len(ks)
+    else:
+        kern_ms = sum(a.elapsed_time(b) for a, b in sync.kernel_events) / args.steps
+        kern_bytes = sync.kernel_bytes()
+        sync.kernel_events = None
+        kt = torch.tensor([kern_ms], device=dev, dtype=torch.float64)     # the slowest rank's kernels
+        dist.all_reduce(kt, op=dist.ReduceOp.MAX)
+        kern_ms = kt.item()
 
     bytes_reduced = k_total * P * torch.finfo(wdt).bits // 8
     value = bytes_reduced / (ms_per_step / 1e3) / 1e9
@@ -351,16 +553,21 @@ def main():
                                        f"dp{world} {sched} (RCCL)"},
         }
         if sharded:
-            # the exchange dominates: bytes this rank puts on xGMI per step over the whole step time
-            # (the local HBM pass is inside that time), against the outbound direction of the
-            # rank's links to its N-1 peers (it receives as much at the same time)
+            # the rank's local kernels (HIP events inside the step, slowest rank) against HBM ...
+            achieved = kern_bytes / (kern_ms / 1e3) / 1e9
+            roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                        "kernel": kernel_name, "kernel_ms": round(kern_ms, 4),
+                        "algo_bytes_per_launch": kern_bytes, "schedule": sched,
+                        "note": "local kernels per rank and step (all buckets); the step itself is "
+                                "bounded by the xGMI exchange below"}
+            # ... and the exchange: bytes this rank puts on xGMI per step over the whole step time,
+            # against the outbound direction of the rank's links to its N-1 peers
             wire = wire_main
-            achieved = wire / (ms_per_step / 1e3) / 1e9
+            xa = wire / (ms_per_step / 1e3) / 1e9
             peak = XGMI_LINK_GBPS * (world - 1)
-            roofline = {"bound": "xgmi", "achieved": round(achieved, 1), "peak": peak, "unit": "GB/s",
-                        "frac": round(achieved / peak, 4) if peak else None, "traffic": None,
-                        "wire_bytes_per_rank": wire,
-                        "schedule": sched}
+            roofline["xgmi"] = {"bound": "xgmi", "achieved": round(xa, 1), "peak": peak, "unit": "GB/s",
+                                "frac": round(xa / peak, 4) if peak else None, "wire_bytes_per_rank": wire}
         if roofline:
             out["roofline"] = roofline
         if weak:
@@ -393,8 +600,23 @@ def main():
         prop = torch.cuda.get_device_properties(dev)
         out["device"] = {"name": prop.name, "arch": getattr(prop, "gcnArchName", ""),
                          "cus": prop.multi_processor_count, "hbm_gib": round(prop.total_memory / 2**30, 1)}
-        if not sharded and args.cpu_baseline_seconds > 0:
-            out["cpu_baseline"] = cpu_baseline(args, tdt, wdt, k_local)
+        if not sharded and args.ops and args.ops != "none":
+            # the other hot-path kernels, one GPU, after the outer step's arenas are freed
+            if sync is not None:
+                sync.theta = sync.workers = sync.state = None
+            theta = workers = sync = step = None
+            torch.cuda.empty_cache()
+            for name, fn in (("pair_merge", bench_pair_merge), ("slerp_7b", bench_slerp_7b)):
+                if name in args.ops:
+                    try:
+                        out[name] = fn(args, dev)
+                    except Exception as e:          # an extra: report it, keep the line
+                        out[name] = {"error": f"{type(e).__name__}: {str(e)[:300]}"}
+                        torch.cuda.empty_cache()
+        if args.cpu_baseline_seconds > 0:
+            # rank 0 after the GPU phase, on this host's cores: the whole population's step (the
+            # reference's master runs all K workers' deltas on its CPU)
+            out["cpu_baseline"] = cpu_baseline(args, tdt, wdt, k_total)
         print(json.dumps(out), flush=True)
     if sharded:
         dist.barrier()

@@ -33,9 +33,9 @@ from __future__ import annotations
 import math
 
 import torch
-import torch.distributed as dist
 
 from . import ops as _ops
+from .collectives import Collectives, TorchCollectives
 from .diloco import check_sgd_hparams
 from .params import ParamArena, ParamLayout
 
@@ -44,15 +44,17 @@ class ShardedOuterSync:
     def __init__(self, layout: ParamLayout, theta_dtype: torch.dtype, worker_dtype: torch.dtype,
                  k_local: int, device, lr: float = 0.7, momentum: float = 0.9, nesterov: bool = True,
                  mode: str = "auto", bucket_elems: int = 1 << 26, group=None, kernels=None,
-                 broadcast: str = "auto"):
+                 broadcast: str = "auto", comm: Collectives | None = None):
         if mode not in ("reduce", "exact", "auto") or broadcast not in ("theta", "workers", "auto"):
             raise ValueError((mode, broadcast))
         if mode == "reduce" and broadcast == "workers":
             raise ValueError("the reduce schedule needs the full theta replica (broadcast='theta')")
         check_sgd_hparams(lr, momentum, nesterov)
-        self.group = group
-        self.world = dist.get_world_size(group)
-        self.rank = dist.get_rank(group)
+        # the communicator seam: torch.distributed (RCCL / gloo) by default, or N virtual ranks
+        # on one device (collectives.VirtualWorld)
+        self.comm = comm or TorchCollectives(group)
+        self.world = self.comm.world
+        self.rank = self.comm.rank
         wb = torch.empty(0, dtype=worker_dtype).element_size()
         gb = torch.empty(0, dtype=theta_dtype).element_size()
         cands = {("reduce", "theta"): 4 + gb, ("exact", "theta"): k_local * wb + gb,
@@ -83,8 +85,9 @@ class ShardedOuterSync:
         shard_total = sum((e - b) // self.world for b, e in self.buckets)
         self.mom_shard = torch.zeros(shard_total, dtype=theta_dtype, device=device) if momentum else None
         self.has_momentum = False
-        # RCCL reduces/gathers in place; other backends (gloo, CPU tests) get separate buffers
-        self.inplace = dist.get_backend(group) == "nccl"
+        # RCCL (and the virtual ranks) reduce/gather in place; gloo gets separate buffers
+        self.inplace = self.comm.inplace
+        self.kernel_events = None      # a list: (start, end) HIP events around every local kernel
         if mode == "reduce":
             self.acc = torch.zeros(self.n_pad, dtype=torch.float32, device=device)
             self.acc_shard = None if self.inplace else torch.empty(shard_total, dtype=torch.float32, device=device)
@@ -97,6 +100,29 @@ class ShardedOuterSync:
         per = (e - b) // self.world
         return b + self.rank * per, b + (self.rank + 1) * per
 
+    def _launch(self, fn, *args):
+        """A local kernel, bracketed by timing events on its launch stream when
+        `kernel_events` is a list (bench.py: the per-rank HBM roofline at N > 1)."""
+        if self.kernel_events is None:
+            return fn(*args)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn(*args)
+        b.record()
+        self.kernel_events.append((a, b))
+
+    def kernel_bytes(self) -> int:
+        """Algorithmic HBM bytes of one step's local kernels on this rank (steady state:
+        momentum read + written). exact: the fused kernel over the owned shards with all K
+        workers; reduce: the partial over the whole arena + the SGD over the owned shards."""
+        wb = self.worker_bufs[0].element_size()
+        gb = self.theta_buf.element_size()
+        shard = self.n_pad // self.world
+        mom = 2 * gb if self.momentum else 0
+        if self.mode == "exact":
+            return shard * (self.k_total * wb + 2 * gb + mom)
+        return self.n_pad * (self.k_local * wb + gb + 4) + shard * (4 + 2 * gb + mom)
+
     def step(self) -> None:
         """One outer step; returns when the work is enqueued (stream-ordered, async)."""
         k = self.kernels
@@ -106,19 +132,17 @@ class ShardedOuterSync:
             # phase 1: local partial sums, reduce-scatter each bucket as soon as it is ready
             works = []
             for b, e in self.buckets:
-                k.delta_partial(self.theta_buf[b:e], [w[b:e] for w in self.worker_bufs], self.k_total,
-                                self.acc[b:e], accumulate=False)
-                works.append(dist.reduce_scatter_tensor(self._acc_out(b, e), self.acc[b:e],
-                                                        op=dist.ReduceOp.SUM, group=self.group,
-                                                        async_op=True))
+                self._launch(k.delta_partial, self.theta_buf[b:e], [w[b:e] for w in self.worker_bufs],
+                             self.k_total, self.acc[b:e], False)
+                works.append(self.comm.reduce_scatter(self._acc_out(b, e), self.acc[b:e], async_op=True))
             # phase 2: SGD on the owned shard, all-gather theta
             for (b, e), w in zip(self.buckets, works):
                 w.wait()
                 s0, s1 = self._shard(b, e)
                 per = s1 - s0
                 mom = None if self.mom_shard is None else self.mom_shard[mom_off:mom_off + per]
-                k.sgd_apply(self.theta_buf[s0:s1], self._acc_out(b, e), mom, self.has_momentum,
-                            self.lr, self.momentum, self.nesterov)
+                self._launch(k.sgd_apply, self.theta_buf[s0:s1], self._acc_out(b, e), mom, self.has_momentum,
+                             self.lr, self.momentum, self.nesterov)
                 mom_off += per
                 gathers.append(self._gather(b, e, s0, s1))
         else:
@@ -126,8 +150,7 @@ class ShardedOuterSync:
             # bucket [b, e) is already laid out [dest rank][per]); one collective per local worker
             works = []
             for b, e in self.buckets:
-                works.append([dist.all_to_all_single(self.recv[j][b:e], wb[b:e], group=self.group,
-                                                     async_op=True)
+                works.append([self.comm.all_to_all(self.recv[j][b:e], wb[b:e], async_op=True)
                               for j, wb in enumerate(self.worker_bufs)])
             # phase 2: as each bucket lands, the single-GPU fused step on the owned shard
             for (b, e), ws in zip(self.buckets, works):
@@ -139,7 +162,7 @@ class ShardedOuterSync:
                 shards = [rv[j][src] for src in range(self.world) for j in range(self.k_local)]
                 s0, s1 = self._shard(b, e)
                 mom = None if self.mom_shard is None else self.mom_shard[mom_off:mom_off + per]
-                k.outer_step(self.theta_buf[s0:s1], shards, mom, self.has_momentum, self.lr,
+                self._launch(k.outer_step, self.theta_buf[s0:s1], shards, mom, self.has_momentum, self.lr,
                              self.momentum, self.nesterov)
                 mom_off += per
                 if self.broadcast == "workers":
@@ -166,7 +189,7 @@ class ShardedOuterSync:
     def _gather(self, b, e, s0, s1):
         """All-gather the updated shards of bucket [b, e) into every rank's theta replica."""
         src = self.theta_buf[s0:s1] if self.inplace else self.theta_buf[s0:s1].clone()
-        return dist.all_gather_into_tensor(self.theta_buf[b:e], src, group=self.group, async_op=True)
+        return self.comm.all_gather(self.theta_buf[b:e], src, async_op=True)
 
     def _gather_to_workers(self, b, e, s0, s1):
         """The new theta shard of bucket [b, e), rounded to the worker dtype (torch copy_: RNE),
@@ -174,7 +197,7 @@ class ShardedOuterSync:
         w0 = self.worker_bufs[0]
         w0[s0:s1].copy_(self.theta_buf[s0:s1])
         src = w0[s0:s1] if self.inplace else w0[s0:s1].clone()
-        return dist.all_gather_into_tensor(w0[b:e], src, group=self.group, async_op=True)
+        return self.comm.all_gather(w0[b:e], src, async_op=True)
 
     def gather_theta(self) -> torch.Tensor:
         """The full master theta on every rank (with broadcast="workers" it is kept sharded;
@@ -183,7 +206,7 @@ class ShardedOuterSync:
             for b, e in self.buckets:
                 s0, s1 = self._shard(b, e)
                 src = self.theta_buf[s0:s1] if self.inplace else self.theta_buf[s0:s1].clone()
-                dist.all_gather_into_tensor(self.theta_buf[b:e], src, group=self.group)
+                self.comm.all_gather(self.theta_buf[b:e], src)
         return self.theta.flat
 
     # ---------------------------------------------------------------------------------------
@@ -212,10 +235,11 @@ class PopulationCrossover:
     directories (EDT_LM/train/crossover.py:255-258, EDT_EVOMERGE/train/crossover.py:167-168), and
     the RL master merges pairs one after another in one process (EDT_RL/edt.py:286-299)."""
 
-    def __init__(self, layout: ParamLayout, dtype: torch.dtype, device, group=None, kernels=None):
-        self.group = group
-        self.world = dist.get_world_size(group)
-        self.rank = dist.get_rank(group)
+    def __init__(self, layout: ParamLayout, dtype: torch.dtype, device, group=None, kernels=None,
+                 comm: Collectives | None = None):
+        self.comm = comm or TorchCollectives(group)
+        self.world = self.comm.world
+        self.rank = self.comm.rank
         self.kernels = kernels or _ops
         self.layout = layout
         self.device = device
@@ -242,18 +266,16 @@ class PopulationCrossover:
         ops_ = []
         for m, dst in mine["send"]:
             for t in payload(m, dst):
-                ops_.append(dist.P2POp(dist.isend, t, dst, self.group))
+                ops_.append(("send", t, dst))
         i, j = pairs[self.rank]
         got = {}
         for m, src in mine["recv"]:
             shapes = like(m) if like is not None else payload(self.rank, self.rank)
             bufs = [self._buf(("recv", m == i, k), t.dtype) for k, t in enumerate(shapes)]
             for b in bufs:
-                ops_.append(dist.P2POp(dist.irecv, b, src, self.group))
+                ops_.append(("recv", b, src))
             got[m] = bufs
-        if ops_:
-            for w in dist.batch_isend_irecv(ops_):
-                w.wait()
+        self.comm.p2p(ops_)
         par1 = payload(i, self.rank) if i == self.rank else got[i]
         par2 = payload(j, self.rank) if j == self.rank else got[j]
         return par1, par2
@@ -277,8 +299,7 @@ class PopulationCrossover:
         (`momentum is not None and has_momentum` on their rank) is agreed first, so every rank
         knows every message; a child with no donor past generation 0 raises NotImplementedError
         on every rank, as the reference's crossover does (:226-227)."""
-        flags = [None] * self.world
-        dist.all_gather_object(flags, bool(has_momentum and momentum is not None), group=self.group)
+        flags = self.comm.all_gather_object(bool(has_momentum and momentum is not None))
         donors = [i if flags[i] else (j if flags[j] else None) for i, j in pairs]
         if mu != 0 and generation > 0 and any(d is None for d in donors):
             raise NotImplementedError("Merging outer optimizer states not implemented for this case.")

@@ -55,7 +55,8 @@ class ResidentPopulation:
                  kind: str = "sgd", momentum_dtype: torch.dtype | None = None, seg_t=None,
                  lr: float = 0.7, momentum: float = 0.9, nesterov: bool = True,
                  dot_threshold: float = 0.9995, eps: float = 1e-8, elitism: int = 0,
-                 group=None, kernels=None, keep_previous: bool = False, slerp_chunk: int | None = None):
+                 group=None, kernels=None, keep_previous: bool = False, slerp_chunk: int | None = None,
+                 comm=None):
         if kind not in ("sgd", "slerp"):
             raise ValueError(kind)
         if kind == "sgd":
@@ -67,10 +68,14 @@ class ResidentPopulation:
         self.dtype = dtype
         self.device = torch.device(device)
         self.kernels = kernels or _ops
-        self.group = group
-        self.distributed = dist.is_available() and dist.is_initialized()
-        self.world = dist.get_world_size(group) if self.distributed else 1
-        self.rank = dist.get_rank(group) if self.distributed else 0
+        # the communicator seam (collectives.py): given, or torch.distributed when initialised
+        if comm is None and dist.is_available() and dist.is_initialized():
+            from .collectives import TorchCollectives
+            comm = TorchCollectives(group)
+        self.comm = comm
+        self.distributed = comm is not None
+        self.world = comm.world if comm is not None else 1
+        self.rank = comm.rank if comm is not None else 0
         self.P = len(genomes)
         if self.P == 0 or self.P % self.world:
             raise EdtError(f"population {self.P} does not split over {self.world} ranks")
@@ -155,12 +160,7 @@ class ResidentPopulation:
     def _sync_host(self, obj):
         if self.world == 1:
             return obj
-        box = [obj]
-        dist.broadcast_object_list(box, src=self.group_rank0(), group=self.group)
-        return box[0]
-
-    def group_rank0(self) -> int:
-        return dist.get_global_rank(self.group, 0) if self.group is not None else 0
+        return self.comm.broadcast_object(obj, src=0)
 
     def select(self, fitness: list[float], method: str | None = None, scale: float | None = None):
         """Parent pairs (member indices) for the next generation, chosen on rank 0.
@@ -259,17 +259,15 @@ class ResidentPopulation:
         p2p = []
         for m, dst in mine["send"]:
             for t in self._payload(m, with_state(m, dst)):
-                p2p.append(dist.P2POp(dist.isend, t, dst, self.group))
+                p2p.append(("send", t, dst))
         got = {m: self._payload(m, True) for m in have}
         like = self._payload(self.local_members()[0], self.kind == "sgd")
         for slot, (m, src) in enumerate(mine["recv"]):
             n = len(like) if with_state(m, self.rank) else (1 if self.kind == "slerp" else 2)
             bufs = [self._recv_like((slot, k), like[k]) for k in range(n)]
-            p2p.extend(dist.P2POp(dist.irecv, b, src, self.group) for b in bufs)
+            p2p.extend(("recv", b, src) for b in bufs)
             got[m] = bufs
-        if p2p:
-            for w in dist.batch_isend_irecv(p2p):
-                w.wait()
+        self.comm.p2p(p2p)
         return got
 
     def crossover(self, pairs, child_hook=None) -> None:
@@ -454,7 +452,7 @@ class ResidentPopulation:
                 json.dump(meta, f)
             os.replace(os.path.join(path, "population.json.tmp"), os.path.join(path, "population.json"))
         if self.world > 1:
-            dist.barrier(group=self.group)
+            self.comm.barrier()
 
     def load(self, path: str, rng: bool = True) -> None:
         """Restore what save() wrote (same layout, kind and population; any world size that

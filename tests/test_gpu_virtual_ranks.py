@@ -1,0 +1,113 @@
+"""The HIP kernels inside the N-rank multi-GPU schedules, on one MI355X: N virtual ranks in one
+process (collectives.VirtualWorld; one thread per rank, collectives as device copies / fp32 sums
+on the shared stream, RCCL's in-place conventions). This runs on the device exactly what each
+rank issues at N = 2 / 4 / 8 — the in-place reduce-scatter offsets, the all-to-all
+[dest rank][shard] layout, the all-gather into the worker arenas, shards that cross bucket and
+tensor ends, the n_pad tail — which the world-1 RCCL runs cannot (every collective is an
+identity there).
+
+  exact/theta, exact/workers: bit-exact with the single-GPU fused step over the whole population
+  reduce/theta:               bit-exact with the oracle's partial/SGD split summed in rank order
+                              (the virtual ranks' order), and within DESIGN §3's reassociation
+                              bound of the reference's sequential order
+  PopulationCrossover:        every child bit-identical to the single-GPU kernel on its parents
+"""
+import pytest
+import torch
+
+from evolutionarydistributedtraining_amd import ops
+from evolutionarydistributedtraining_amd.collectives import VirtualWorld
+from tests.virtual_schedules import bits, population, reduce_reference, reduce_tol, run_sharded
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+# 292,187 elements: tensors of odd sizes so shards cross tensor ends; with a bucket of 37 units
+# (unit = N x 64 elements) the buckets end mid-tensor and the last one is ragged up to n_pad
+SHAPES = [(37, 11), (5,), (1,), (256, 513), (129,), (3, 9001), (1001,), (2, 77)]
+
+
+def _fused(theta, gens):
+    th = theta.clone()
+    mom = torch.zeros_like(th)
+    for i, ws in enumerate(gens):
+        ops.outer_step(th, ws, mom, i > 0, 0.7, 0.9, True)
+    torch.cuda.synchronize()
+    return th, mom
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("mode,broadcast", [("exact", "theta"), ("exact", "workers"), ("reduce", "theta")])
+@pytest.mark.parametrize("tdt,wdt", [(torch.float32, torch.float32), (torch.float32, torch.bfloat16),
+                                     (torch.bfloat16, torch.bfloat16)])
+def test_sharded_schedule_on_virtual_ranks(oracle, world, mode, broadcast, tdt, wdt):
+    layout, theta, gens = population(SHAPES, tdt, wdt, 8, steps=2, device=DEV)
+    res = run_sharded(world, layout, tdt, wdt, theta, gens, DEV, mode=mode, broadcast=broadcast,
+                      bucket_elems=world * 64 * 37)
+    torch.cuda.synchronize()
+    n = layout.total
+    assert len(res[0]["buckets"]) >= 3 and res[0]["n_pad"] > n
+    assert (res[0]["mode"], res[0]["broadcast"]) == (mode, broadcast)
+    for r in res:
+        assert torch.equal(bits(r["theta"]), bits(res[0]["theta"]))
+    got, mom = res[0]["theta"][:n], res[0]["mom"]
+    if mode == "exact":
+        th_f, mom_f = _fused(theta, gens)
+        assert torch.equal(bits(got), bits(th_f))
+        assert torch.equal(bits(mom), bits(mom_f))
+        if broadcast == "workers":
+            want = th_f.to(wdt)
+            for r in res:
+                for w in r["workers"]:
+                    assert torch.equal(bits(w[:n]), bits(want))
+    else:
+        cpu_gens = [[w.cpu() for w in ws] for ws in gens]
+        th_rs, mom_rs = reduce_reference(oracle, theta.cpu(), cpu_gens, world)
+        assert torch.equal(bits(got.cpu()), bits(th_rs))
+        assert torch.equal(bits(mom.cpu()), bits(mom_rs))
+        th_ref = theta.cpu().clone()
+        mom_ref = torch.zeros_like(th_ref)
+        for i, ws in enumerate(cpu_gens):
+            oracle.outer_step(th_ref, ws, mom_ref, i > 0, 0.7, 0.9, True)
+        tol = reduce_tol(th_ref, mom_ref, tdt, gens=cpu_gens)
+        assert ((got.cpu().float() - th_ref.float()).abs() <= tol).all()
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_population_crossover_on_virtual_ranks(world):
+    """PopulationCrossover (one member per rank, grouped p2p of each child's parents) with the
+    HIP SLERP and pair-merge kernels: every child equals the single-GPU kernel on its parents."""
+    from evolutionarydistributedtraining_amd.distributed import PopulationCrossover
+    from evolutionarydistributedtraining_amd.params import ParamLayout
+    layout = ParamLayout([(33, 7), (5,), (3000,), (1,), (64, 65)])
+    n = layout.total
+    g = torch.Generator().manual_seed(5)
+    base = [(torch.randn(n, generator=g) * 0.02).bfloat16().to(DEV) for _ in range(world)]
+    trained = [(b.float() + torch.randn(n, generator=g).to(DEV) * 1e-3).bfloat16() for b in base]
+    mom = [(torch.randn(n, generator=g) * 1e-3).bfloat16().to(DEV) for _ in range(world)]
+    pairs = [((c * 3 + 1) % world, (c * 5 + 2) % world) for c in range(world)]
+    t = torch.tensor([0.3, 0.5, 0.9, 0.5, 0.43], dtype=torch.float64, device=DEV)
+
+    def body(comm):
+        r = comm.rank
+        pc = PopulationCrossover(layout, torch.bfloat16, DEV, comm=comm)
+        s_out = torch.empty(n, dtype=torch.float32, device=DEV)
+        pc.slerp_step(trained[r], pairs, t, s_out)
+        child = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+        cmom = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+        pc.pair_merge_step(base[r], trained[r], mom[r], pairs, child, cmom, generation=1)
+        return s_out, child, cmom
+
+    res = VirtualWorld(world).run(body)
+    torch.cuda.synchronize()
+    plan = ops.make_slerp_plan(layout.offsets, DEV)
+    for c, (i, j) in enumerate(pairs):
+        want = torch.empty(n, dtype=torch.float32, device=DEV)
+        ops.slerp_arena(plan, trained[i], trained[j], want, t, speculate=False)
+        out = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+        m_out = torch.empty_like(out)
+        ops.pair_merge(base[i], base[j], trained[i], trained[j], out, m_out, True, 0.7, 0.9, True,
+                       momentum_in=mom[i])
+        torch.cuda.synchronize()
+        assert torch.equal(res[c][0].view(torch.int32), want.view(torch.int32)), c
+        assert torch.equal(res[c][1].view(torch.int16), out.view(torch.int16)), c
+        assert torch.equal(res[c][2].view(torch.int16), m_out.view(torch.int16)), c

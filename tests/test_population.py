@@ -57,16 +57,19 @@ def _scale(gen):
     return roulette_scale(gen + 1, 10)
 
 
-def run_resident(kind, device, kernels=None):
-    """The resident population over GENS generations; returns this rank's members."""
+def run_resident(kind, device, kernels=None, comm=None):
+    """The resident population over GENS generations; returns this rank's members. comm: a
+    collectives.Collectives (virtual ranks); the host RNGs are seeded by rank 0 only (they are
+    process-global, and only rank 0 draws)."""
     from evolutionarydistributedtraining_amd.params import ParamLayout
     from evolutionarydistributedtraining_amd.population import ResidentPopulation
     layout = ParamLayout(SHAPES)
     n, dt = layout.total, _dtype(kind)
-    random.seed(7)
-    np.random.seed(7)
+    if comm is None or comm.rank == 0:
+        random.seed(7)
+        np.random.seed(7)
     pop = ResidentPopulation(layout, dt, device, _genomes(kind), kind=kind, elitism=1 if kind == "sgd" else 0,
-                             seg_t=SEG_T if kind == "slerp" else None, kernels=kernels)
+                             seg_t=SEG_T if kind == "slerp" else None, kernels=kernels, comm=comm)
     for m in pop.local_members():
         (pop.base(m) if kind == "sgd" else pop.params(m)).copy_(_init(m, n, dt))
     for gen in range(GENS):
@@ -210,6 +213,47 @@ def test_resident_world2_matches_world1(tmp_path, oracle, kind):
                 assert torch.equal(_bits(d["mom"]), _bits(mom[m])), m
             else:
                 assert torch.equal(_bits(d["params"]), _bits(base[m])), m
+
+
+def _check_world(res, world, kind, oracle, slerp_tol=None):
+    base, mom, want_genomes = reference_flow(kind, oracle)
+    per = POP // world
+    for r in range(world):
+        got, genomes = res[r]
+        assert genomes == want_genomes
+        assert sorted(got) == list(range(r * per, (r + 1) * per))
+        for m, d in got.items():
+            if kind == "sgd":
+                assert torch.equal(_bits(d["base"]), _bits(base[m])), m
+                assert torch.equal(_bits(d["mom"]), _bits(mom[m])), m
+            elif slerp_tol is None:
+                assert torch.equal(_bits(d["params"]), _bits(base[m])), m
+            else:
+                diff = (d["params"] - base[m]).abs()
+                assert (diff <= slerp_tol * base[m].abs() + 1e-8).all(), (m, diff.max().item())
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("kind", ["sgd", "slerp"])
+def test_resident_virtual_ranks_match_reference_flow(oracle, kind, world):
+    """The same generations on `world` virtual ranks (collectives.VirtualWorld, one process):
+    members spread P / world per rank, parents exchanged by the grouped p2p, genomes broadcast."""
+    from evolutionarydistributedtraining_amd.collectives import VirtualWorld
+    from tests.oracle_kernels import OracleKernels
+    res = VirtualWorld(world).run(lambda comm: run_resident(kind, "cpu", OracleKernels(oracle), comm=comm))
+    _check_world(res, world, kind, oracle)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("kind", ["sgd", "slerp"])
+def test_resident_gpu_virtual_ranks(oracle, kind, world):
+    """The HIP kernels inside the N-rank generation schedule on one MI355X (virtual ranks):
+    EDT-LM bit-exact, SLERP within the SLERP parity bar."""
+    from evolutionarydistributedtraining_amd.collectives import VirtualWorld
+    dev = torch.device("cuda:0")
+    res = VirtualWorld(world).run(lambda comm: run_resident(kind, dev, comm=comm))
+    _check_world(res, world, kind, oracle, slerp_tol=1e-5)
 
 
 def test_resident_rejects_missing_momentum(oracle):

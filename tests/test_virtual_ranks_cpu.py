@@ -1,0 +1,113 @@
+"""The multi-rank schedules on N virtual ranks in one process (collectives.VirtualWorld), CPU,
+with the oracle standing in for the HIP kernels: the same checks as the gloo world-2/3 tests
+(test_distributed_cpu.py) at world 2, 3, 4 and 8, plus the virtual communicator's own
+semantics. The GPU form (HIP kernels, one MI355X) is tests/test_gpu_virtual_ranks.py."""
+import pytest
+import torch
+
+from evolutionarydistributedtraining_amd.collectives import CommTimeout, VirtualWorld
+from tests.virtual_schedules import bits, population, reduce_reference, reduce_tol, run_sharded
+
+SHAPES = [(37, 11), (5,), (1,), (64, 33), (129,), (300,)]
+
+
+def _oracle_ref(theta, gens, tdt):
+    from oracle import oracle
+    th = theta.clone()
+    mom = torch.zeros_like(th)
+    for i, w in enumerate(gens):
+        oracle.outer_step(th, w, mom, i > 0, 0.7, 0.9, True)
+    return th, mom
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+@pytest.mark.parametrize("mode,broadcast", [("exact", "theta"), ("exact", "workers"), ("reduce", "theta")])
+@pytest.mark.parametrize("tdt,wdt", [(torch.float32, torch.float32), (torch.float32, torch.bfloat16),
+                                     (torch.bfloat16, torch.bfloat16)])
+def test_virtual_sharded_outer_step(oracle, world, mode, broadcast, tdt, wdt):
+    k_total = 8 if world != 3 else 6
+    layout, theta, gens = population(SHAPES, tdt, wdt, k_total, steps=2)
+    res = run_sharded(world, layout, tdt, wdt, theta, gens, "cpu", kernels=oracle, mode=mode,
+                      broadcast=broadcast, bucket_elems=world * 64 * 2)
+    assert len(res[0]["buckets"]) >= 3 and res[0]["n_pad"] > layout.total     # ragged tail + many buckets
+    th_ref, mom_ref = _oracle_ref(theta, gens, tdt)
+    n = layout.total
+    for r in res:
+        assert torch.equal(bits(r["theta"]), bits(res[0]["theta"]))        # every replica agrees
+    got = res[0]["theta"][:n]
+    if mode == "exact":
+        assert torch.equal(bits(got), bits(th_ref))
+        assert torch.equal(bits(res[0]["mom"]), bits(mom_ref))
+        if broadcast == "workers":
+            want = th_ref.to(wdt)
+            for r in res:
+                for w in r["workers"]:
+                    assert torch.equal(bits(w[:n]), bits(want))
+    else:
+        # bit-exact with the same op sequence in the virtual ranks' (rank-order) summation ...
+        th_rs, mom_rs = reduce_reference(oracle, theta, gens, world)
+        assert torch.equal(bits(got), bits(th_rs))
+        assert torch.equal(bits(res[0]["mom"]), bits(mom_rs))
+        # ... and within the reassociation bound of the reference's sequential order
+        assert ((got.float() - th_ref.float()).abs() <= reduce_tol(th_ref, mom_ref, tdt, gens=gens)).all()
+
+
+def test_virtual_collectives_semantics():
+    """reduce-scatter / all-gather in place (RCCL's aliasing rules), all-to-all [dest][shard],
+    grouped p2p matched in issue order, object collectives."""
+    W = 4
+
+    def body(comm):
+        r = comm.rank
+        x = torch.arange(8 * W, dtype=torch.float32) + 100 * r
+        comm.reduce_scatter(x[r * 8:(r + 1) * 8], x)                       # in place
+        rs = x[r * 8:(r + 1) * 8].clone()
+        g = torch.zeros(4 * W)
+        g[r * 4:(r + 1) * 4] = r + 1
+        comm.all_gather(g, g[r * 4:(r + 1) * 4])                            # in place
+        a_in = torch.tensor([10 * r + d for d in range(W)], dtype=torch.float32).repeat_interleave(2)
+        a_out = torch.empty_like(a_in)
+        comm.all_to_all(a_out, a_in)
+        nxt, prv = (r + 1) % W, (r - 1) % W
+        got1, got2 = torch.empty(3), torch.empty(3)
+        comm.p2p([("send", torch.full((3,), float(r)), nxt), ("send", torch.full((3,), 50. + r), nxt),
+                  ("recv", got1, prv), ("recv", got2, prv)])
+        objs = comm.all_gather_object({"r": r})
+        b = comm.broadcast_object({"v": r} if r == 2 else None, src=2)
+        comm.barrier()
+        return rs, g, a_out, got1, got2, objs, b
+
+    res = VirtualWorld(W).run(body)
+    full = sum(torch.arange(8 * W, dtype=torch.float32) + 100 * k for k in range(W))
+    for r, (rs, g, a_out, got1, got2, objs, b) in enumerate(res):
+        assert torch.equal(rs, full[r * 8:(r + 1) * 8])
+        assert torch.equal(g, torch.arange(1, W + 1, dtype=torch.float32).repeat_interleave(4))
+        assert torch.equal(a_out, torch.tensor([10 * s + r for s in range(W)], dtype=torch.float32).repeat_interleave(2))
+        assert torch.equal(got1, torch.full((3,), float((r - 1) % W)))
+        assert torch.equal(got2, torch.full((3,), 50. + (r - 1) % W))
+        assert objs == [{"r": k} for k in range(W)] and b == {"v": 2}
+
+
+def test_virtual_rank_failure_breaks_the_rendezvous():
+    """A rank that raises (or never arrives) ends every peer's wait with CommTimeout; the
+    original error is what run() re-raises — no hang."""
+    def body(comm):
+        if comm.rank == 1:
+            raise ValueError("rank 1 died")
+        comm.barrier()
+
+    with pytest.raises(ValueError, match="rank 1 died"):
+        VirtualWorld(3, timeout=30).run(body)
+
+    def mismatched(comm):
+        comm.p2p([("recv", torch.empty(2), 0)] if comm.rank == 1 else [])
+
+    with pytest.raises(Exception, match="sends nothing"):
+        VirtualWorld(2, timeout=30).run(mismatched)
+
+    def straggler(comm):
+        if comm.rank == 0:
+            comm.barrier()                     # rank 1 never joins
+
+    with pytest.raises(CommTimeout):
+        VirtualWorld(2, timeout=1).run(straggler)
