@@ -93,6 +93,8 @@ def parse():
                    help="N=1: the other hot-path kernels measured after the outer step, in the same line "
                         "('none': skip)")
     p.add_argument("--ops-cpu-seconds", type=float, default=4.0, help="CPU baseline budget per extra op")
+    p.add_argument("--bcast-compare", type=int, default=1,
+                   help="N=1: also time the step fused with the worker broadcast against step + K copies")
     p.add_argument("--dry-run-launch", action="store_true",
                    help="each rank prints its rank environment and exits before device init")
     return p.parse_args()
@@ -600,6 +602,23 @@ def main():
         prop = torch.cuda.get_device_properties(dev)
         out["device"] = {"name": prop.name, "arch": getattr(prop, "gcnArchName", ""),
                          "cus": prop.multi_processor_count, "hbm_gib": round(prop.total_memory / 2**30, 1)}
+        if not sharded and args.bcast_compare:
+            # the step with the broadcast of diloco.py:302-308 (every worker restarts from theta):
+            # fused into the kernel's pass vs the step + K device copies
+            try:
+                fused = _event_ms(lambda: sync.step(broadcast=True), args.steps, 2)
+                unfused = _event_ms(lambda: (sync.step(), sync.broadcast_()), args.steps, 2)
+                bw = torch.finfo(wdt).bits // 8
+                fb = algo_bytes + k_local * P * bw
+                out["step_with_broadcast"] = {
+                    "fused_ms": round(fused, 4), "step_plus_copies_ms": round(unfused, 4),
+                    "kernel": "outer_kernel<..., BC=true> (edt_outer_step_bcast)",
+                    "fused_roofline": {"bound": "hbm", "achieved": round(fb / (fused / 1e3) / 1e9, 1),
+                                       "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                                       "frac": round(fb / (fused / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+                                       "algo_bytes_per_launch": fb}}
+            except Exception as e:          # an extra: report it, keep the line
+                out["step_with_broadcast"] = {"error": f"{type(e).__name__}: {str(e)[:300]}"}
         if not sharded and args.ops and args.ops != "none":
             # the other hot-path kernels, one GPU, after the outer step's arenas are freed
             if sync is not None:

@@ -70,6 +70,11 @@ using edt::g_err;
 #ifndef EDT_SLERP_BPC           // workgroups per CU for the chunk-looping SLERP passes
 #define EDT_SLERP_BPC 256
 #endif
+#ifndef EDT_SLERP_GRID          // 1: the SLERP blends run one 2,048-element tile per workgroup in address
+                                // order (32 workgroups per 64 Ki chunk) and the chunk-sum passes one
+                                // workgroup per chunk; 0: grid-stride over chunks, EDT_SLERP_BPC per CU
+#define EDT_SLERP_GRID 1
+#endif
 #ifndef EDT_SLERP_COEF_BLOCK    // 1: one workgroup per segment for the chunk-sum reduction (else one wave)
 #define EDT_SLERP_COEF_BLOCK 1
 #endif
@@ -105,9 +110,31 @@ constexpr int kVec = 8;                             // elements per thread per i
 // grid cap for the grid-stride loops: 256 CUs x workgroups per CU (0 = one pass, no cap)
 constexpr uint64_t kMaxBlocks = EDT_BLOCKS_PER_CU > 0 ? 256ull * EDT_BLOCKS_PER_CU : (1ull << 31) - 1;
 
-constexpr uint64_t kSlerpMaxBlocks = 256ull * EDT_SLERP_BPC;
+constexpr uint64_t kSlerpMaxBlocks = EDT_SLERP_GRID ? (1ull << 31) - 1 : 256ull * EDT_SLERP_BPC;
+// chunk-sum passes: one workgroup per chunk (EDT_SLERP_GRID), else a grid-stride cap
 inline unsigned slerp_grid(int64_t nchunks) {
     return (unsigned)((uint64_t)nchunks < kSlerpMaxBlocks ? (uint64_t)nchunks : kSlerpMaxBlocks);
+}
+// the speculative passes (chunk sums + the lerp output in one pass) stay grid-stride: one workgroup
+// per chunk measured 9.12 ms against 8.01 ms for the 7B lineage merge (profiles/r02_slerp_grid.json)
+#ifndef EDT_SLERP_SPEC_BPC
+#define EDT_SLERP_SPEC_BPC 256
+#endif
+#ifndef EDT_SLERP_GRAM_GRID
+#define EDT_SLERP_GRAM_GRID 0
+#endif
+inline unsigned slerp_spec_grid(int64_t nchunks) {
+    const uint64_t cap = 256ull * EDT_SLERP_SPEC_BPC;
+    return (unsigned)((uint64_t)nchunks < cap ? (uint64_t)nchunks : cap);
+}
+// blend passes: tile q of chunk c is workgroup c * kTilesPerChunk + q, so the grid walks the arena
+// in address order one kTile at a time (chunks longer than kTilesPerChunk tiles loop)
+constexpr int kTile = kBlock * kVec;                 // 2,048 elements
+constexpr int kTilesPerChunk = 32;                   // the plans' default chunk: 64 Ki elements
+inline unsigned slerp_tile_grid(int64_t nchunks) {
+    if (!EDT_SLERP_GRID) return slerp_grid(nchunks);
+    const uint64_t g = (uint64_t)nchunks * kTilesPerChunk;
+    return (unsigned)(g < (1ull << 31) - 1 ? g : (1ull << 31) - 1);
 }
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));

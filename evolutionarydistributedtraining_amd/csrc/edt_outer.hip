@@ -27,6 +27,8 @@ struct OuterArgs {
     int acc_store;       // chain mode: store the running sum to acc_ws (no SGD)
     SgdScalars sgd;
     Workers w;
+    Workers bc;          // broadcast mode: round_w(theta_new) stored to these (worker dtype)
+    int nbc;
     __device__ __forceinline__ const void* wp(int k) const { return w.p[k]; }
 };
 
@@ -57,7 +59,7 @@ enum { MODE_FUSED = 0, MODE_PARTIAL = 1, MODE_CHAIN = 2 };
 // Per-element accumulation acc = sum_k round(round(w_k - g) / K) in the precision of GDT
 // (worker-major order, EDT_LM/diloco.py:243-246). MODE_PARTIAL sums the rounded quotients
 // in fp32 instead (the cross-rank sum is then an fp32 RCCL reduction).
-template <int GDT, int WDT, int KC, int DIV, int MODE, int N, class A, int H2 = 4>
+template <int GDT, int WDT, int KC, int DIV, int MODE, int N, class A, int H2 = 4, bool BC = false>
 __device__ __forceinline__ void outer_elems(const A& a, uint64_t i) {
     float g[N], acc[N], b_in[N];
     ld<GDT, N, (EDT_NT_RMW != 0), H2>(a.theta, i, g);
@@ -106,12 +108,20 @@ __device__ __forceinline__ void outer_elems(const A& a, uint64_t i) {
         for (int j = 0; j < N; ++j) grad[j] = -acc[j];               // p.grad = -avg_delta
         sgd_update<GDT, N, H2>(g, grad, a.mom, i, a.sgd, b_in);
         st<GDT, N, (EDT_NT_STORES != 0), H2>(a.theta, i, g);
+        if constexpr (BC) {
+            // the broadcast of EDT_LM/diloco.py:302-308 fused in: every destination starts the
+            // next inner loop from theta_new rounded to the worker dtype (torch copy_: RNE). A
+            // destination may be a worker this thread just read (same elements, same thread).
+#pragma unroll 4
+            for (int k = 0; k < a.nbc; ++k) st<WDT, N, (EDT_NT_STORES != 0), H2>(const_cast<void*>(a.bc.p[k]), i, g);
+        }
     }
 }
 
 // DIV = 1: true division by K (torch CPU `delta / num_models`); DIV = 0: multiply by 1/K,
 // bit-identical when K is a power of two.
-template <int GDT, int WDT, int KC, int DIV, int MODE, int N>
+// BC: also store round_w(theta_new) into a.bc (edt_outer_step_bcast).
+template <int GDT, int WDT, int KC, int DIV, int MODE, int N, bool BC = false>
 __global__ __launch_bounds__(kBlock, EDT_MIN_WAVES) void outer_kernel(OuterArgs a) {
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
     const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -120,16 +130,17 @@ __global__ __launch_bounds__(kBlock, EDT_MIN_WAVES) void outer_kernel(OuterArgs 
         constexpr int H2 = 4 * kBlock;
         const uint64_t nv = a.n / (kVec * kBlock) * kBlock;
         for (uint64_t v = tid; v < nv; v += stride)
-            outer_elems<GDT, WDT, KC, DIV, MODE, kVec, OuterArgs, H2>(a, v * kVec - 4 * threadIdx.x);
+            outer_elems<GDT, WDT, KC, DIV, MODE, kVec, OuterArgs, H2, BC>(a, v * kVec - 4 * threadIdx.x);
         for (uint64_t e = nv * kVec + tid; e < a.n; e += stride)     // scalar tail (< 8 x kBlock)
-            outer_elems<GDT, WDT, KC, DIV, MODE, 1>(a, e);
+            outer_elems<GDT, WDT, KC, DIV, MODE, 1, OuterArgs, 4, BC>(a, e);
     } else if constexpr (N == kVec) {
         const uint64_t nv = a.n / kVec;
-        for (uint64_t v = tid; v < nv; v += stride) outer_elems<GDT, WDT, KC, DIV, MODE, kVec>(a, v * kVec);
+        for (uint64_t v = tid; v < nv; v += stride)
+            outer_elems<GDT, WDT, KC, DIV, MODE, kVec, OuterArgs, 4, BC>(a, v * kVec);
         const uint64_t t = nv * kVec + tid;      // scalar tail (< 8 elements)
-        if (t < a.n) outer_elems<GDT, WDT, KC, DIV, MODE, 1>(a, t);
+        if (t < a.n) outer_elems<GDT, WDT, KC, DIV, MODE, 1, OuterArgs, 4, BC>(a, t);
     } else {
-        for (uint64_t e = tid; e < a.n; e += stride) outer_elems<GDT, WDT, KC, DIV, MODE, 1>(a, e);
+        for (uint64_t e = tid; e < a.n; e += stride) outer_elems<GDT, WDT, KC, DIV, MODE, 1, OuterArgs, 4, BC>(a, e);
     }
 }
 
@@ -300,13 +311,13 @@ __global__ __launch_bounds__(kBlock, EDT_MIN_WAVES) void probe_kernel(OuterArgs 
 // ---------------------------------------------------------------------------------------
 // launch helpers
 
-template <int GDT, int WDT, int MODE>
+template <int GDT, int WDT, int MODE, bool BC = false>
 int launch_outer_k(const OuterArgs& a, bool vec, hipStream_t s) {
     const unsigned g = grid_for(a.n, vec);
 #define EDT_LAUNCH_K(KC, DIV)                                                                    \
     do {                                                                                         \
-        if (vec) outer_kernel<GDT, WDT, KC, DIV, MODE, kVec><<<g, kBlock, 0, s>>>(a);            \
-        else outer_kernel<GDT, WDT, KC, DIV, MODE, 1><<<g, kBlock, 0, s>>>(a);                   \
+        if (vec) outer_kernel<GDT, WDT, KC, DIV, MODE, kVec, BC><<<g, kBlock, 0, s>>>(a);        \
+        else outer_kernel<GDT, WDT, KC, DIV, MODE, 1, BC><<<g, kBlock, 0, s>>>(a);               \
     } while (0)
     // compile-time worker counts for the common populations; the divisor is K_total
     if constexpr (MODE == MODE_CHAIN) {
@@ -325,11 +336,11 @@ int launch_outer_k(const OuterArgs& a, bool vec, hipStream_t s) {
     return check_launch("outer_kernel");
 }
 
-template <int MODE>
+template <int MODE, bool BC = false>
 int launch_outer(int gdt, int wdt, const OuterArgs& a, bool vec, hipStream_t s) {
-    if (gdt == EDT_F32 && wdt == EDT_F32) return launch_outer_k<EDT_F32, EDT_F32, MODE>(a, vec, s);
-    if (gdt == EDT_F32 && wdt == EDT_BF16) return launch_outer_k<EDT_F32, EDT_BF16, MODE>(a, vec, s);
-    return launch_outer_k<EDT_BF16, EDT_BF16, MODE>(a, vec, s);
+    if (gdt == EDT_F32 && wdt == EDT_F32) return launch_outer_k<EDT_F32, EDT_F32, MODE, BC>(a, vec, s);
+    if (gdt == EDT_F32 && wdt == EDT_BF16) return launch_outer_k<EDT_F32, EDT_BF16, MODE, BC>(a, vec, s);
+    return launch_outer_k<EDT_BF16, EDT_BF16, MODE, BC>(a, vec, s);
 }
 
 constexpr uint64_t kListLdsMaxTensors = 8191;          // (T + 1) x 8 B <= 64 KiB of LDS
@@ -428,6 +439,38 @@ int edt_outer_step(void* theta_g, int gdt, const void* const* theta_k, int wdt, 
     bool vec = aligned16(theta_g) && (!a.sgd.use_momentum || aligned16(momentum));
     for (int k = 0; k < K; ++k) vec = vec && aligned16(theta_k[k]);
     return launch_outer<MODE_FUSED>(gdt, wdt, a, vec, (hipStream_t)stream);
+}
+
+int edt_outer_step_bcast(void* theta_g, int gdt, const void* const* theta_k, int wdt, int K,
+                         void* momentum, int has_momentum, uint64_t n, double lr, double momentum_coef,
+                         int nesterov, void* const* bcast, int nbcast, void* stream) {
+    g_err[0] = 0;
+    if (!valid_pair(gdt, wdt)) return fail(EDT_ERR_ARG, "unsupported dtype pair (gdt/wdt)");
+    if (nbcast < 0 || nbcast > EDT_MAX_WORKERS)
+        return fail(EDT_ERR_ARG, "broadcast count %d out of range [0, %d]", nbcast, EDT_MAX_WORKERS);
+    if (nbcast == 0)
+        return edt_outer_step(theta_g, gdt, theta_k, wdt, K, momentum, has_momentum, n, lr, momentum_coef, nesterov,
+                              stream);
+    OuterArgs a;
+    int rc = fill_outer(a, theta_g, theta_k, K, K, n);
+    if (rc) return rc;
+    a.sgd = make_sgd(gdt, lr, momentum_coef, has_momentum, nesterov);
+    if (a.sgd.use_momentum && !momentum && n) return fail(EDT_ERR_ARG, "momentum buffer is null");
+    a.mom = momentum;
+    if (!bcast) return fail(EDT_ERR_ARG, "bcast is null");
+    const uintptr_t t0 = reinterpret_cast<uintptr_t>(theta_g), t1 = t0 + n * (gdt == EDT_BF16 ? 2 : 4);
+    for (int k = 0; k < nbcast; ++k) {
+        if (!bcast[k] && n) return fail(EDT_ERR_ARG, "bcast[%d] is null", k);
+        const uintptr_t b0 = reinterpret_cast<uintptr_t>(bcast[k]), b1 = b0 + n * (wdt == EDT_BF16 ? 2 : 4);
+        if (n && b0 < t1 && t0 < b1) return fail(EDT_ERR_ARG, "bcast[%d] overlaps theta_g", k);
+        a.bc.p[k] = bcast[k];
+    }
+    a.nbc = nbcast;
+    if (n == 0) return EDT_OK;
+    bool vec = aligned16(theta_g) && (!a.sgd.use_momentum || aligned16(momentum));
+    for (int k = 0; k < K; ++k) vec = vec && aligned16(theta_k[k]);
+    for (int k = 0; k < nbcast; ++k) vec = vec && aligned16(bcast[k]);
+    return launch_outer<MODE_FUSED, true>(gdt, wdt, a, vec, (hipStream_t)stream);
 }
 
 int edt_outer_step_ws(void* theta_g, int gdt, const void* const* theta_k, int wdt, int K, void* momentum,

@@ -99,6 +99,44 @@ __device__ __forceinline__ void slerp_coefficients(double s00, double s11, doubl
     }
 }
 
+// The element ranges a blend workgroup owns, as body(start, end, segment). TILES: one kTile of its
+// chunk (tiles kTilesPerChunk apart for longer chunks; grid slerp_tile_grid) — the full blends.
+// Else whole chunks, grid-stride (grid slerp_spec_grid) — the speculative redo blends, where most
+// segments are skipped and a workgroup per tile would cost more to dispatch than it saves (7B
+// lineage merge: 3.45 M empty workgroups = +1.1 ms). Tiles assume the plans' 64 Ki chunks: shorter
+// chunks stay correct, with idle workgroups.
+template <bool TILES, typename F>
+__device__ __forceinline__ void for_blend_ranges(const uint64_t* chunks, int64_t nchunks, F&& body) {
+    if constexpr (TILES && EDT_SLERP_GRID) {
+        const int64_t c = blockIdx.x / kTilesPerChunk;
+        if (c >= nchunks) return;
+        const uint64_t start = chunks[3 * c], len = chunks[3 * c + 1], seg = chunks[3 * c + 2];
+        for (uint64_t off = (uint64_t)(blockIdx.x % kTilesPerChunk) * kTile; off < len;
+             off += (uint64_t)kTilesPerChunk * kTile)
+            body(start + off, start + (off + kTile < len ? off + kTile : len), seg);
+    } else {
+        for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x)
+            body(chunks[3 * c], chunks[3 * c] + chunks[3 * c + 1], chunks[3 * c + 2]);
+    }
+}
+
+// f(N, i) over [start, end): the 16-B-aligned body in 8-element vectors (workgroup-strided), then
+// the < 16 head / tail elements one per thread.
+template <typename F>
+__device__ __forceinline__ void for_range_elems(uint64_t start, uint64_t end, F&& f) {
+    const uint64_t a = (start + kVec - 1) / kVec * kVec;
+    const uint64_t b = end / kVec * kVec;
+    if (a < b) {
+        for (uint64_t i = a + (uint64_t)threadIdx.x * kVec; i < b; i += (uint64_t)kBlock * kVec)
+            f(std::integral_constant<int, kVec>{}, i);
+    }
+    const uint64_t h_end = a < end ? a : end;
+    const uint64_t t_beg = b > a ? b : h_end;
+    const uint64_t nh = h_end - start, nt = end - t_beg;
+    if ((uint64_t)threadIdx.x < nh + nt)
+        f(std::integral_constant<int, 1>{}, threadIdx.x < nh ? start + threadIdx.x : t_beg + (threadIdx.x - nh));
+}
+
 // seg_ptrs (tensor-list form, may be null): per segment {v0, v1, out} device pointers; chunk
 // starts are then relative to their segment. Null: v0 / v1 / out are flat arenas.
 template <int IDT>
@@ -208,35 +246,27 @@ __global__ __launch_bounds__(kBlock) void slerp_coef_kernel(const double* partia
     if (redo) redo[seg] = fabsf(dot) > thr ? 0 : 1;   // the speculative lerp output stands or not
 }
 
-template <int IDT, int ODT, bool NT = (EDT_NT_SLERP != 0 && IDT == EDT_BF16)>
+template <int IDT, int ODT, bool NT = (EDT_NT_SLERP != 0 && IDT == EDT_BF16), bool TILES = true>
 __global__ __launch_bounds__(kBlock) void slerp_blend_kernel(const void* v0, const void* v1, void* out,
                                                              const uint64_t* chunks, int64_t nchunks,
                                                              const float* coef, const uint64_t* seg_ptrs,
                                                              const int32_t* redo = nullptr) {
-    for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
-        const uint64_t start = chunks[3 * c], len = chunks[3 * c + 1], seg = chunks[3 * c + 2];
-        if (redo && !redo[seg]) continue;         // speculative lerp output already final
+    for_blend_ranges<TILES>(chunks, nchunks, [&](uint64_t start, uint64_t end, uint64_t seg) {
+        if (redo && !redo[seg]) return;           // speculative lerp output already final
+        const void* a = v0;
+        const void* b = v1;
+        void* o = out;
         if (seg_ptrs) {
-            v0 = reinterpret_cast<const void*>(seg_ptrs[3 * seg]);
-            v1 = reinterpret_cast<const void*>(seg_ptrs[3 * seg + 1]);
-            out = reinterpret_cast<void*>(seg_ptrs[3 * seg + 2]);
+            a = reinterpret_cast<const void*>(seg_ptrs[3 * seg]);
+            b = reinterpret_cast<const void*>(seg_ptrs[3 * seg + 1]);
+            o = reinterpret_cast<void*>(seg_ptrs[3 * seg + 2]);
         }
-        const uint64_t end = start + len;
         const float c0 = coef[2 * seg], c1 = coef[2 * seg + 1];
-        const uint64_t a = (start + kVec - 1) / kVec * kVec;
-        const uint64_t b = end / kVec * kVec;
-        if (a < b) {
-            for (uint64_t i = a + (uint64_t)threadIdx.x * kVec; i < b; i += (uint64_t)kBlock * kVec)
-                lerp_elems<IDT, ODT, EDT_F32, kVec, NT>(v0, v1, out, i, c0, c1);
-        }
-        const uint64_t h_end = a < end ? a : end;
-        const uint64_t t_beg = b > a ? b : h_end;
-        const uint64_t nh = h_end - start, nt = end - t_beg;
-        if ((uint64_t)threadIdx.x < nh + nt) {
-            const uint64_t i = threadIdx.x < nh ? start + threadIdx.x : t_beg + (threadIdx.x - nh);
-            lerp_elems<IDT, ODT, EDT_F32, 1>(v0, v1, out, i, c0, c1);
-        }
-    }
+        for_range_elems(start, end, [&](auto tagN, uint64_t i) {
+            constexpr int N = decltype(tagN)::value;
+            lerp_elems<IDT, ODT, EDT_F32, N, NT && N == kVec>(a, b, o, i, c0, c1);
+        });
+    });
 }
 
 // ---------------------------------------------------------------------------------------
@@ -524,45 +554,37 @@ __device__ __forceinline__ void blend_mm_elems(const Members& mem, const PopBlen
     }
 }
 
-template <int IDT, int ODT, int M>
+template <int IDT, int ODT, int M, bool TILES>
 __global__ __launch_bounds__(kBlock) void slerp_blend_mm_kernel(Members mem, PopBlend pb, const uint64_t* chunks,
                                                                 int64_t nchunks) {
-    for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
-        const uint64_t start = chunks[3 * c], end = start + chunks[3 * c + 1], seg = chunks[3 * c + 2];
+    for_blend_ranges<TILES>(chunks, nchunks, [&](uint64_t start, uint64_t end, uint64_t seg) {
         uint32_t need = 0;                   // children whose output this segment still needs
         for (int q = 0; q < pb.n; ++q)
             if (!pb.redo[q] || pb.redo[q][seg]) need |= 1u << q;
-        if (!need) continue;                 // every child keeps its speculative lerp output
-        const uint64_t a = (start + kVec - 1) / kVec * kVec;
-        const uint64_t b = end / kVec * kVec;
-        if (a < b) {
-            for (uint64_t i = a + (uint64_t)threadIdx.x * kVec; i < b; i += (uint64_t)kBlock * kVec)
-                blend_mm_elems<IDT, ODT, M, kVec>(mem, pb, i, seg, need);
-        }
-        const uint64_t h_end = a < end ? a : end;
-        const uint64_t t_beg = b > a ? b : h_end;
-        const uint64_t nh = h_end - start, nt = end - t_beg;
-        if ((uint64_t)threadIdx.x < nh + nt) {
-            const uint64_t i = threadIdx.x < nh ? start + threadIdx.x : t_beg + (threadIdx.x - nh);
-            blend_mm_elems<IDT, ODT, M, 1>(mem, pb, i, seg, need);
-        }
-    }
+        if (!need) return;                   // every child keeps its speculative lerp output
+        for_range_elems(start, end, [&](auto tagN, uint64_t i) {
+            blend_mm_elems<IDT, ODT, M, decltype(tagN)::value>(mem, pb, i, seg, need);
+        });
+    });
 }
 
-// host: launch slerp_blend_mm_kernel over D compact parents
+// host: launch slerp_blend_mm_kernel over D compact parents. Grid-stride over chunks for both the
+// Gram form's blends and the speculative redo: one tile per workgroup measured 11.46-11.51 ms
+// against 10.83 ms for a 1.3B x 8 generation (the member-major body holds D parent tiles in
+// registers; profiles/r02_slerp_pop_grid.json).
 inline int launch_blend_mm(const Members& mem, int D, const PopBlend& pb, int in_dt, int out_dt,
                            const uint64_t* chunk_desc, int64_t nchunks, hipStream_t s) {
-    const unsigned g = slerp_grid(nchunks);
+    const unsigned g = slerp_spec_grid(nchunks);
 #define EDT_BMM(M)                                                                                            \
     case M:                                                                                                   \
         if (in_dt == EDT_F32 && out_dt == EDT_F32)                                                            \
-            slerp_blend_mm_kernel<EDT_F32, EDT_F32, M><<<g, kBlock, 0, s>>>(mem, pb, chunk_desc, nchunks);    \
+            slerp_blend_mm_kernel<EDT_F32, EDT_F32, M, false><<<g, kBlock, 0, s>>>(mem, pb, chunk_desc, nchunks);   \
         else if (in_dt == EDT_F32)                                                                            \
-            slerp_blend_mm_kernel<EDT_F32, EDT_BF16, M><<<g, kBlock, 0, s>>>(mem, pb, chunk_desc, nchunks);   \
+            slerp_blend_mm_kernel<EDT_F32, EDT_BF16, M, false><<<g, kBlock, 0, s>>>(mem, pb, chunk_desc, nchunks);  \
         else if (out_dt == EDT_F32)                                                                           \
-            slerp_blend_mm_kernel<EDT_BF16, EDT_F32, M><<<g, kBlock, 0, s>>>(mem, pb, chunk_desc, nchunks);   \
+            slerp_blend_mm_kernel<EDT_BF16, EDT_F32, M, false><<<g, kBlock, 0, s>>>(mem, pb, chunk_desc, nchunks);  \
         else                                                                                                  \
-            slerp_blend_mm_kernel<EDT_BF16, EDT_BF16, M><<<g, kBlock, 0, s>>>(mem, pb, chunk_desc, nchunks);  \
+            slerp_blend_mm_kernel<EDT_BF16, EDT_BF16, M, false><<<g, kBlock, 0, s>>>(mem, pb, chunk_desc, nchunks); \
         break;
     switch (D) {
         EDT_BMM(1) EDT_BMM(2) EDT_BMM(3) EDT_BMM(4) EDT_BMM(5) EDT_BMM(6) EDT_BMM(7) EDT_BMM(8)
@@ -571,8 +593,6 @@ inline int launch_blend_mm(const Members& mem, int D, const PopBlend& pb, int in
 #undef EDT_BMM
     return check_launch("slerp_blend_mm_kernel");
 }
-
-
 
 int slerp_stats_impl(const void* v0, const void* v1, int in_dt, const uint64_t* chunk_desc, int64_t nchunks,
                      double* partial, const uint64_t* seg_ptrs, void* stream) {
@@ -591,7 +611,7 @@ int slerp_blend_impl(const void* v0, const void* v1, int in_dt, void* out, int o
     if ((in_dt | out_dt) & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
     if (nchunks == 0) return EDT_OK;
     if (!chunk_desc || !coef) return fail(EDT_ERR_ARG, "null buffer");
-    const unsigned g = slerp_grid(nchunks);
+    const unsigned g = slerp_tile_grid(nchunks);
     hipStream_t s = (hipStream_t)stream;
     if (in_dt == EDT_F32 && out_dt == EDT_F32)
         slerp_blend_kernel<EDT_F32, EDT_F32><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, seg_ptrs);
@@ -728,7 +748,9 @@ int edt_slerp_population(const void* const* members, int nmembers, int in_dt, co
                 mem.p[D++] = members[m];
             }
         }
-    const unsigned g = slerp_grid(nchunks);
+    // the Gram pass (M(M+1)/2 fp64 sums per thread, low occupancy) stays grid-stride unless
+    // EDT_SLERP_GRAM_GRID: 1.3B x 8 generation 10.83 ms grid-stride vs 11.46 ms one per chunk
+    const unsigned g = EDT_SLERP_GRAM_GRID ? slerp_grid(nchunks) : slerp_spec_grid(nchunks);
 #define EDT_GRAM(M)                                                                                  \
     case M:                                                                                          \
         if (in_dt == EDT_F32) slerp_gram_kernel<EDT_F32, M><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, gram); \
@@ -812,7 +834,7 @@ int edt_slerp_merge_speculative(const void* v0, const void* v1, int in_dt, void*
         if (p0 < o1 && o0 < p1) return fail(EDT_ERR_ARG, "speculative SLERP needs an output apart from the parents");
     }
     hipStream_t s = (hipStream_t)stream;
-    const unsigned g = slerp_grid(nchunks);
+    const unsigned g = slerp_spec_grid(nchunks);
     if (in_dt == EDT_F32 && out_dt == EDT_F32)
         slerp_stats_lerp_kernel<EDT_F32, EDT_F32><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, partial, t);
     else if (in_dt == EDT_F32)
@@ -827,14 +849,16 @@ int edt_slerp_merge_speculative(const void* v0, const void* v1, int in_dt, void*
                                                          (float)eps, coef, dot_out, redo);
     rc = check_launch("slerp_coef_kernel");
     if (rc) return rc;
+    // the redo blends: grid-stride over chunks (most segments are skipped)
+    constexpr bool kNtB = EDT_NT_SLERP != 0;
     if (in_dt == EDT_F32 && out_dt == EDT_F32)
-        slerp_blend_kernel<EDT_F32, EDT_F32><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, nullptr, redo);
+        slerp_blend_kernel<EDT_F32, EDT_F32, false, false><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, nullptr, redo);
     else if (in_dt == EDT_F32)
-        slerp_blend_kernel<EDT_F32, EDT_BF16><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, nullptr, redo);
+        slerp_blend_kernel<EDT_F32, EDT_BF16, false, false><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, nullptr, redo);
     else if (out_dt == EDT_F32)
-        slerp_blend_kernel<EDT_BF16, EDT_F32><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, nullptr, redo);
+        slerp_blend_kernel<EDT_BF16, EDT_F32, kNtB, false><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, nullptr, redo);
     else
-        slerp_blend_kernel<EDT_BF16, EDT_BF16><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, nullptr, redo);
+        slerp_blend_kernel<EDT_BF16, EDT_BF16, kNtB, false><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, nullptr, redo);
     return check_launch("slerp_blend_kernel");
 }
 
@@ -891,7 +915,7 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
             po.a[q] = compact[pairs[2 * q]];
             po.b[q] = compact[pairs[2 * q + 1]];
         }
-        const unsigned g = slerp_grid(nchunks);
+        const unsigned g = slerp_spec_grid(nchunks);
 #define EDT_GL(M)                                                                                             \
     case M:                                                                                                   \
         if (in_dt == EDT_F32 && out_dt == EDT_F32)                                                            \

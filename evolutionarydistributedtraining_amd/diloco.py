@@ -101,12 +101,12 @@ class OuterState:
 
 
 def _step_flat(theta: torch.Tensor, workers: list[torch.Tensor], state: OuterState, lr: float,
-               momentum: float, nesterov: bool) -> None:
+               momentum: float, nesterov: bool, broadcast: list[torch.Tensor] | None = None) -> None:
     check_sgd_hparams(lr, momentum, nesterov)
     state.hparams = dict(lr=lr, momentum=momentum, nesterov=nesterov)
     mom = state.buffer_for(theta) if momentum != 0 else None
     has = state.has_momentum if momentum != 0 else False
-    ops.outer_step(theta, workers, mom, has, lr, momentum, nesterov)
+    ops.outer_step(theta, workers, mom, has, lr, momentum, nesterov, broadcast)
     if momentum != 0:
         state.has_momentum = True
     state.steps += 1
@@ -183,9 +183,13 @@ class OuterSync:
         self.lr, self.momentum, self.nesterov = lr, momentum, nesterov
         self.state = state or OuterState()
 
-    def step(self) -> None:
-        _step_flat(self.theta.flat, [w.flat for w in self.workers], self.state, self.lr,
-                   self.momentum, self.nesterov)
+    def step(self, broadcast: bool = False) -> None:
+        """One outer step. broadcast=True also starts every worker from the new global weights
+        (EDT_LM/diloco.py:302-308) in the same pass: each worker arena is overwritten with theta
+        rounded to its dtype right after the kernel has read it (edt_outer_step_bcast)."""
+        ws = [w.flat for w in self.workers]
+        _step_flat(self.theta.flat, ws, self.state, self.lr, self.momentum, self.nesterov,
+                   ws if broadcast else None)
 
     def place_momentum(self, candidates: int = 8) -> dict:
         """Choose where the outer momentum lives in HBM by measurement, once, for the life of
@@ -202,7 +206,8 @@ class OuterSync:
 
     def broadcast_(self) -> None:
         """Start every worker from the new global weights (what saving base_model to every
-        worker dir does, EDT_LM/diloco.py:302-308)."""
+        worker dir does, EDT_LM/diloco.py:302-308) as K device copies; step(broadcast=True) does
+        the same inside the step's pass."""
         for w in self.workers:
             w.flat.copy_(self.theta.flat)
 

@@ -162,11 +162,15 @@ class ShardedOuterSync:
                 shards = [rv[j][src] for src in range(self.world) for j in range(self.k_local)]
                 s0, s1 = self._shard(b, e)
                 mom = None if self.mom_shard is None else self.mom_shard[mom_off:mom_off + per]
+                # broadcast="workers": the HIP kernel also stores the new shard, rounded to the
+                # worker dtype, into local worker 0's arena (its bucket has been sent) — the
+                # rounding copy fused into the step
+                fused = self.broadcast == "workers" and k is _ops
                 self._launch(k.outer_step, self.theta_buf[s0:s1], shards, mom, self.has_momentum, self.lr,
-                             self.momentum, self.nesterov)
+                             self.momentum, self.nesterov, *([[self.worker_bufs[0][s0:s1]]] if fused else []))
                 mom_off += per
                 if self.broadcast == "workers":
-                    gathers.append(self._gather_to_workers(b, e, s0, s1))
+                    gathers.append(self._gather_to_workers(b, e, s0, s1, rounded=fused))
                 else:
                     gathers.append(self._gather(b, e, s0, s1))
         for g in gathers:
@@ -191,11 +195,13 @@ class ShardedOuterSync:
         src = self.theta_buf[s0:s1] if self.inplace else self.theta_buf[s0:s1].clone()
         return self.comm.all_gather(self.theta_buf[b:e], src, async_op=True)
 
-    def _gather_to_workers(self, b, e, s0, s1):
-        """The new theta shard of bucket [b, e), rounded to the worker dtype (torch copy_: RNE),
-        all-gathered into local worker 0's arena (its bucket was consumed by the all-to-all)."""
+    def _gather_to_workers(self, b, e, s0, s1, rounded=False):
+        """The new theta shard of bucket [b, e), rounded to the worker dtype (torch copy_: RNE;
+        rounded=True: the kernel already stored it), all-gathered into local worker 0's arena
+        (its bucket was consumed by the all-to-all)."""
         w0 = self.worker_bufs[0]
-        w0[s0:s1].copy_(self.theta_buf[s0:s1])
+        if not rounded:
+            w0[s0:s1].copy_(self.theta_buf[s0:s1])
         src = w0[s0:s1] if self.inplace else w0[s0:s1].clone()
         return self.comm.all_gather(w0[b:e], src, async_op=True)
 

@@ -16,21 +16,39 @@ from . import _lib as L
 
 
 def outer_step(theta: torch.Tensor, workers: list[torch.Tensor], momentum: torch.Tensor | None,
-               has_momentum: bool, lr: float, momentum_coef: float, nesterov: bool) -> None:
+               has_momentum: bool, lr: float, momentum_coef: float, nesterov: bool,
+               broadcast: list[torch.Tensor] | None = None) -> None:
     """Fused DiLoCo outer step (EDT_LM/diloco.py:238-289): theta and momentum updated in place.
 
     theta: flat float32/bfloat16; workers: K flat tensors of one dtype (K > 64: chained launches
-    through a scratch running sum); momentum: flat, theta's dtype (required when momentum_coef != 0)."""
+    through a scratch running sum); momentum: flat, theta's dtype (required when momentum_coef != 0).
+    broadcast: buffers of the workers' dtype (may be the workers themselves) that receive the new
+    theta rounded to that dtype in the same pass (edt_outer_step_bcast: the broadcast of
+    diloco.py:302-308 fused into the step, no re-read of theta per copy)."""
     lib = L.lib()
     if not workers:
         raise L.EdtError("no workers")
-    L.require_device(theta, momentum, *workers)
+    L.require_device(theta, momentum, *workers, *(broadcast or []))
     n = theta.numel()
     for w in workers:
         if w.numel() != n or w.dtype != workers[0].dtype:
             raise L.EdtError("every worker buffer must match theta's size and share one dtype")
     if momentum is not None and (momentum.numel() != n or momentum.dtype != theta.dtype):
         raise L.EdtError("momentum must have theta's size and dtype")
+    if broadcast:
+        if any(b.numel() != n or b.dtype != workers[0].dtype for b in broadcast):
+            raise L.EdtError("broadcast buffers must match theta's size and the workers' dtype")
+        if len(workers) <= L.EDT_MAX_WORKERS and len(broadcast) <= L.EDT_MAX_WORKERS:
+            L.check(lib.edt_outer_step_bcast(L.ptr(theta), L.dtype_code(theta), L.ptr_array(workers),
+                                             L.dtype_code(workers[0]), len(workers), L.ptr(momentum),
+                                             int(has_momentum), n, float(lr), float(momentum_coef),
+                                             int(nesterov), L.ptr_array(broadcast), len(broadcast),
+                                             L.stream_ptr(theta.device)), "edt_outer_step_bcast")
+            return
+        outer_step(theta, workers, momentum, has_momentum, lr, momentum_coef, nesterov)
+        for b in broadcast:
+            b.copy_(theta)
+        return
     if len(workers) <= L.EDT_MAX_WORKERS:
         L.check(lib.edt_outer_step(L.ptr(theta), L.dtype_code(theta), L.ptr_array(workers),
                                    L.dtype_code(workers[0]), len(workers), L.ptr(momentum),

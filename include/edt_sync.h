@@ -52,6 +52,17 @@ int edt_outer_step(void* theta_g, int gdt, const void* const* theta_k, int wdt, 
                    void* momentum, int has_momentum, uint64_t n,
                    double lr, double momentum_coef, int nesterov, void* stream);
 
+/* edt_outer_step fused with the broadcast of EDT_LM/diloco.py:302-308 (the new global model saved
+ * to every worker dir, from which the next inner loops start): the same step, and in the same pass
+ * theta_new rounded to the worker dtype (RNE, torch copy_) is stored into the nbcast device
+ * buffers bcast[0..nbcast) (n elements of wdt each; a buffer may be one of the theta_k, which are
+ * read before they are overwritten, element by element; none may overlap theta_g).
+ * Replaces edt_outer_step + nbcast device copies (each re-reading theta). 0 <= nbcast <= 64;
+ * nbcast = 0 is edt_outer_step. */
+int edt_outer_step_bcast(void* theta_g, int gdt, const void* const* theta_k, int wdt, int K,
+                         void* momentum, int has_momentum, uint64_t n, double lr, double momentum_coef,
+                         int nesterov, void* const* bcast, int nbcast, void* stream);
+
 /* The same step for any population size: K > EDT_MAX_WORKERS runs as consecutive launches of
  * <= 64 workers (the reference's worker order), the running sum carried in `workspace` (n
  * elements of theta's dtype: lossless, the sum is rounded to that dtype after every add).

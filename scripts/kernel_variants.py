@@ -19,7 +19,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-VDIR = os.path.join(ROOT, "build", "variants")
+VDIR = os.path.join(ROOT, "build_variants")      # travels to the GPU box (./build does not)
 
 NT = ["-DEDT_NT_LOADS=1"]
 VARIANTS = {
@@ -107,6 +107,10 @@ VARIANTS.update({"default": [], "f32_ntst": ["-DEDT_NT_STORES=1"], "nt_rmw": ["-
 VARIANTS.update({"split0": ["-DEDT_SPLIT_HALVES=0"], "split1": ["-DEDT_SPLIT_HALVES=1"],
                  "split1_nt0": ["-DEDT_SPLIT_HALVES=1", "-DEDT_NT_LOADS=0"]})
 VARIANTS.update({f"li{i}": [f"-DEDT_LIST_ITERS={i}"] for i in (1, 2, 4, 8, 16)})
+VARIANTS.update({"s_grid0": ["-DEDT_SLERP_GRID=0"], "s_grid1": ["-DEDT_SLERP_GRID=1"],
+                 "s_grid1_nt0": ["-DEDT_SLERP_GRID=1", "-DEDT_NT_SLERP=0"],
+                 "s_spec64": ["-DEDT_SLERP_SPEC_BPC=64"], "s_spec1024": ["-DEDT_SLERP_SPEC_BPC=1024"],
+                 "s_spec16": ["-DEDT_SLERP_SPEC_BPC=16"], "s_gram1": ["-DEDT_SLERP_GRAM_GRID=1"]})
 
 
 def run_list(names, rounds, iters, wdt="bf16"):
@@ -173,8 +177,10 @@ def run_list(names, rounds, iters, wdt="bf16"):
 
 
 def run_slerp(names, rounds, layout_name):
-    """Qwen2.5-7B-body-sized SLERP (bf16 in/out) per variant library: the grouped merge at
-    several group sizes, and the whole-arena three-pass form."""
+    """Qwen2.5-7B-body-sized SLERP (bf16 in/out) per variant library, each pass timed on its own
+    (stats = chunk sums, 4 B/elem read; blend = 4 B read + 2 B written; spec = the speculative
+    stats+lerp pass, 6 B/elem) and the whole merges: two-pass (far parents) and speculative
+    (lineage parents, every tensor in the lerp branch)."""
     import torch
     from evolutionarydistributedtraining_amd import _lib as L
     from evolutionarydistributedtraining_amd import ops
@@ -185,14 +191,17 @@ def run_slerp(names, rounds, layout_name):
     bf = torch.bfloat16
     v0 = torch.empty(P, dtype=bf, device=dev)
     v1 = torch.empty(P, dtype=bf, device=dev)
+    v2 = torch.empty(P, dtype=bf, device=dev)        # lineage partner of v0
     for s0 in range(0, P, 1 << 28):
         e = min(P, s0 + (1 << 28))
         x = torch.randn(e - s0, device=dev) * 0.02
         v0[s0:e] = x.to(bf)
         v1[s0:e] = (x + torch.randn(e - s0, device=dev) * 1e-3).to(bf)
+        v2[s0:e] = (x + torch.randn(e - s0, device=dev) * 1e-4).to(bf)
         del x
     out = torch.empty(P, dtype=bf, device=dev)
-    plans = {ce: ops.make_slerp_plan(lay.offsets, dev, chunk_elems=ce) for ce in (1 << 14, 1 << 16)}
+    plan = ops.make_slerp_plan(lay.offsets, dev, chunk_elems=1 << 16)
+    redo = torch.zeros(plan.nseg, dtype=torch.int32, device=dev)
     t = torch.full((len(lay),), 0.5, dtype=torch.float64, device=dev)
     stream = L.stream_ptr(dev)
     libs = {}
@@ -206,30 +215,40 @@ def run_slerp(names, rounds, layout_name):
     cases = {}
     for n in names:
         lib = libs[n]
-        for ce, plan in plans.items():
-            def three(lib=lib, plan=plan):
-                assert lib.edt_slerp_stats(P_(v0), P_(v1), 1, P_(plan.chunks), plan.nchunks, P_(plan.partial),
-                                           stream) == 0
-                assert lib.edt_slerp_coef(P_(plan.partial), P_(plan.seg_first), plan.nseg, P_(t), 0.9995, 1e-8,
-                                          P_(plan.coef), P_(plan.dots), stream) == 0
-                return lib.edt_slerp_blend(P_(v0), P_(v1), 1, P_(out), 1, P_(plan.chunks), plan.nchunks,
-                                           P_(plan.coef), stream)
-            cases[f"{n}/chunk{ce >> 10}k"] = three
+        cases[f"{n}/stats"] = (4, lambda lib=lib: lib.edt_slerp_stats(P_(v0), P_(v1), 1, P_(plan.chunks), plan.nchunks,
+                                                                       P_(plan.partial), stream))
+        cases[f"{n}/blend"] = (6, lambda lib=lib: lib.edt_slerp_blend(P_(v0), P_(v1), 1, P_(out), 1, P_(plan.chunks),
+                                                                       plan.nchunks, P_(plan.coef), stream))
+        cases[f"{n}/two_pass_far"] = (6, lambda lib=lib: lib.edt_slerp_merge(
+            P_(v0), P_(v1), 1, P_(out), 1, P_(plan.chunks), plan.nchunks, P_(plan.seg_first), plan.nseg, P_(t),
+            0.9995, 1e-8, P_(plan.partial), P_(plan.coef), P_(plan.dots), stream))
+        cases[f"{n}/speculative_lineage"] = (6, lambda lib=lib: lib.edt_slerp_merge_speculative(
+            P_(v0), P_(v2), 1, P_(out), 1, P_(plan.chunks), plan.nchunks, P_(plan.seg_first), plan.nseg, P_(t),
+            0.9995, 1e-8, P_(plan.partial), P_(plan.coef), P_(plan.dots), P_(redo), P, stream))
     times = {k: [] for k in cases}
-    for k, f in cases.items():
-        assert f() == 0
+    for k, (_, f) in cases.items():
+        assert f() == 0, k
     torch.cuda.synchronize()
     for _ in range(rounds):
-        for k, f in cases.items():
+        for k, (_, f) in cases.items():
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
             f()
             b.record()
             torch.cuda.synchronize()
             times[k].append(a.elapsed_time(b))
-    res = {k: {"median_ms": round(statistics.median(v), 3), "algo_TBps": round(6 * P / statistics.median(v) / 1e9, 3)}
-           for k, v in times.items()}
-    print(json.dumps({"layout": layout_name, "P": P, "op": "slerp", "variants": res}, indent=1))
+    res = {k: {"median_ms": round(statistics.median(v), 3),
+               "TBps": round(cases[k][0] * P / statistics.median(v) / 1e9, 3)} for k, v in times.items()}
+    # results must not depend on the grid: every variant's two-pass output is compared
+    outs = {}
+    for n in names:
+        cases[f"{n}/two_pass_far"][1]()
+        outs[n] = out.clone()
+    torch.cuda.synchronize()
+    ref = outs[names[0]]
+    res["identical_outputs"] = all(torch.equal(o.view(torch.int16), ref.view(torch.int16)) for o in outs.values())
+    print(json.dumps({"layout": layout_name, "P": P, "op": "slerp", "chunks": plan.nchunks, "variants": res},
+                     indent=1))
 
 
 def run_slerp_pop(names, rounds, layout_name="gpt_1p3b", P_members=8):
