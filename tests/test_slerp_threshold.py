@@ -1,0 +1,106 @@
+"""The SLERP branch contract at the reference's DOT_THRESHOLD = 0.9995 (EDT_RL/crossover.py:24-31),
+pinned by reference-generated cases whose true cosine sits 1e-7, 1e-6 and 1e-5 either side of it
+(tests/golden/gen_slerp_threshold.py: fp32 / bf16, 437 and 1,048,583 elements).
+
+Contract: the kernel decides the branch from ITS dot — an fp64 sum of exact
+products, normalised with fp32-rounded norms as numpy's — which is within 3e-7 of the true cosine.
+The reference decides from an fp32 dot (BLAS norms + a pairwise fp32 sum) that is off by up to
+~1e-6 at a million elements, so near the threshold the two can fall on opposite sides ("straddle";
+four of the large cases do). Then the output follows the accurate dot's branch, and differs from
+the reference's by exactly the two coefficient sets' gap: |out - ref| <= |dc0||v0| + |dc1||v1|
++ 2e-6 (|c0 v0| + |c1 v1|), dc from the two dots (fp64 formula). Where the branches agree that
+bound is the usual SLERP bar, and the lerp branch is bit-exact."""
+import json
+import math
+import os
+
+import pytest
+import torch
+from safetensors.torch import load_file
+
+from tests.golden.threshold_inputs import digest, make_pair, sample_index
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+THR = 0.9995
+
+
+def _fixture():
+    with open(os.path.join(GOLDEN, "slerp_threshold.json")) as f:
+        meta = json.load(f)
+    return meta["cases"], load_file(os.path.join(GOLDEN, "slerp_threshold.safetensors"))
+
+
+def _inputs(c, tensors):
+    if f"{c['name']}/v0" in tensors:
+        a, b = tensors[f"{c['name']}/v0"], tensors[f"{c['name']}/v1"]
+    else:
+        a, b = make_pair(c["seed"], c["n"], c["dtype"], c["noise_scale"])
+    assert digest(a, b) == c["sha256"], f"{c['name']}: rebuilt inputs differ from the generated ones"
+    return a, b
+
+
+def _coefs(t, dot):
+    """The reference's coefficient formula in fp64 for a given dot."""
+    if abs(dot) > THR:
+        return 1.0 - t, t
+    th = math.acos(dot)
+    return math.sin(th - th * t) / math.sin(th), math.sin(th * t) / math.sin(th)
+
+
+CASES, _ = _fixture()
+
+
+def test_threshold_fixture_exercises_both_sides():
+    assert sum(c["ref_lerp_branch"] != c["exact_lerp_branch"] for c in CASES) >= 2
+    assert {c["exact_lerp_branch"] for c in CASES} == {True, False}
+
+
+@pytest.mark.parametrize("c", CASES, ids=[c["name"] for c in CASES])
+def test_oracle_reproduces_reference_at_threshold(oracle, c):
+    """The numpy restatement takes the reference's branch with the reference's dot, bit for bit."""
+    _, tensors = _fixture()
+    a, b = _inputs(c, tensors)
+    idx = sample_index(c["n"])
+    for o in c["outputs"]:
+        res, dot, lerp_branch = oracle.slerp_parts(o["t"], a, b)
+        assert float(dot) == c["ref_dot"] and lerp_branch == c["ref_lerp_branch"]
+        got = torch.from_numpy(res)
+        assert torch.equal(got[idx].view(torch.int32), tensors[f"{o['key']}/out"].view(torch.int32))
+        assert float(got.double().sum()) == o["sum_f64"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c", CASES, ids=[c["name"] for c in CASES])
+def test_kernel_branch_contract_at_threshold(c):
+    from evolutionarydistributedtraining_amd import ops
+    dev = torch.device("cuda:0")
+    _, tensors = _fixture()
+    a, b = _inputs(c, tensors)
+    n = c["n"]
+    idx = sample_index(n)
+    plan = ops.make_slerp_plan([0, n], dev)
+    for o in c["outputs"]:
+        t = torch.tensor([o["t"]], dtype=torch.float64, device=dev)
+        outs = []
+        for spec in (False, True):
+            out = torch.empty(n, dtype=torch.float32, device=dev)
+            ops.slerp_arena(plan, a.to(dev), b.to(dev), out, t, speculate=spec)
+            outs.append(out.cpu())
+            dot = plan.dots[0].item()
+        assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))     # both forms agree
+        # (a) our dot is the accurate one
+        assert abs(dot - c["exact_cos"]) <= 3e-7, (dot, c["exact_cos"])
+        ours_lerp = abs(dot) > THR
+        if abs(c["exact_cos"] - THR) > 3e-7:
+            assert ours_lerp == c["exact_lerp_branch"]
+        # (b) the output is the blend of our branch, within the coefficient gap of the reference's
+        got, ref = outs[0][idx].double(), tensors[f"{o['key']}/out"].double()
+        v0, v1 = a.double()[idx], b.double()[idx]
+        c0, c1 = _coefs(o["t"], dot)
+        r0, r1 = _coefs(o["t"], c["ref_dot"])
+        bound = abs(c0 - r0) * v0.abs() + abs(c1 - r1) * v1.abs() + 2e-6 * (abs(c0) * v0.abs() + abs(c1) * v1.abs())
+        assert ((got - ref).abs() <= bound + 1e-30).all(), (c["name"], (got - ref).abs().max().item())
+        mine = c0 * v0 + c1 * v1
+        assert ((got - mine).abs() <= 2e-6 * (abs(c0) * v0.abs() + abs(c1) * v1.abs()) + 1e-30).all()
+        if ours_lerp and c["ref_lerp_branch"]:
+            assert torch.equal(outs[0][idx].view(torch.int32), tensors[f"{o['key']}/out"].view(torch.int32))
