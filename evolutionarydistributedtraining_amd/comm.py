@@ -31,8 +31,14 @@ SIGNATURES = [
                                ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_U64), _I, _P]),
     ("edt_outer_step_sharded", _I, [_P, _P, _I, ctypes.POINTER(_P), _I, _I, _P, _I, _U64, _U64, _D, _D, _I,
                                     _P, _P]),
+    ("edt_comm_abort", _I, [_P]),
+    ("edt_comm_poll", _I, [_P]),
+    ("edt_comm_wait", _I, [_P, _P, _D]),
+    ("edt_comm_set_timeout", _I, [_P, _D]),
     ("edt_comm_last_error", ctypes.c_char_p, []),
 ]
+
+ERR_ABORTED, ERR_TIMEOUT = -4, -5
 
 
 def load_comm_library():
@@ -77,6 +83,24 @@ class Comm:
         if self._h:
             _check(load_comm_library().edt_comm_destroy(self._h), "edt_comm_destroy")
             self._h = _P()
+
+    def abort(self) -> None:
+        """ncclCommAbort: outstanding collectives end; later calls fail with EDT_COMM_ERR_ABORTED."""
+        _check(load_comm_library().edt_comm_abort(self._h), "edt_comm_abort")
+
+    def poll(self) -> None:
+        """Raise EdtError if the communicator was aborted or holds an asynchronous RCCL error."""
+        _check(load_comm_library().edt_comm_poll(self._h), "edt_comm_poll")
+
+    def wait(self, device=None, timeout_s: float = 0.0) -> None:
+        """Host wait for the work on the current stream and the communicator's own; past
+        timeout_s the communicator is aborted and EdtError raised (EDT_COMM_ERR_TIMEOUT)."""
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        _check(load_comm_library().edt_comm_wait(self._h, L.stream_ptr(dev), float(timeout_s)), "edt_comm_wait")
+
+    def set_timeout(self, seconds: float) -> None:
+        """> 0: outer_step_sharded waits for its work and fails after `seconds` (edt_comm_set_timeout)."""
+        _check(load_comm_library().edt_comm_set_timeout(self._h, float(seconds)), "edt_comm_set_timeout")
 
     def _stream(self, t: torch.Tensor):
         return L.stream_ptr(t.device)

@@ -4,9 +4,11 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "edt_comm.h"
@@ -42,9 +44,54 @@ struct Comm {
     int rank = 0, nranks = 1;
     hipStream_t side = nullptr;
     std::vector<hipEvent_t> events;
+    bool aborted = false;        // edt_comm_abort (or a timeout) tore the RCCL communicator down
+    double timeout_s = 0.0;      // > 0: edt_outer_step_sharded waits for its work, bounded by this
 };
 
 Comm* as_comm(void* c) { return static_cast<Comm*>(c); }
+
+// Every entry point first: a torn-down communicator, or an asynchronous RCCL error a peer's
+// failure left behind, fails the call instead of enqueueing work that can never complete.
+int usable(Comm* c) {
+    if (!c) return fail(EDT_COMM_ERR_ARG, "null communicator");
+    if (c->aborted) return fail(EDT_COMM_ERR_ABORTED, "communicator of rank %d was aborted", c->rank);
+    ncclResult_t async = ncclSuccess;
+    ncclResult_t r = ncclCommGetAsyncError(c->nccl, &async);
+    if (r != ncclSuccess) return fail(EDT_COMM_ERR_RCCL, "ncclCommGetAsyncError: %s", ncclGetErrorString(r));
+    if (async != ncclSuccess && async != ncclInProgress)
+        return fail(EDT_COMM_ERR_RCCL, "asynchronous RCCL error on rank %d: %s", c->rank, ncclGetErrorString(async));
+    return 0;
+}
+
+void abort_comm(Comm* c) {
+    if (c && !c->aborted) {
+        (void)ncclCommAbort(c->nccl);
+        c->nccl = nullptr;
+        c->aborted = true;
+    }
+}
+
+// Host wait for `ev` (recorded after the work to wait for), polling the event and RCCL's async
+// error; past timeout_s (<= 0: none) the communicator is aborted so the stuck collectives end.
+int wait_event(Comm* c, hipEvent_t ev, double timeout_s) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        hipError_t q = hipEventQuery(ev);
+        if (q == hipSuccess) return 0;
+        if (q != hipErrorNotReady) return fail(EDT_COMM_ERR_HIP, "hipEventQuery: %s", hipGetErrorString(q));
+        if (int rc = usable(c)) {
+            abort_comm(c);
+            return rc;
+        }
+        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (timeout_s > 0 && el > timeout_s) {
+            abort_comm(c);
+            return fail(EDT_COMM_ERR_TIMEOUT, "rank %d: collectives not done after %.3f s; communicator aborted",
+                        c->rank, el);
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+}
 
 bool nccl_type(int dt, ncclDataType_t* t, uint64_t* size) {
     if (dt == EDT_F32) { *t = ncclFloat32; *size = 4; return true; }
@@ -105,7 +152,7 @@ int edt_comm_destroy(void* comm) {
     if (c->side) (void)hipStreamSynchronize(c->side);
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
     if (c->side) (void)hipStreamDestroy(c->side);
-    ncclResult_t r = ncclCommDestroy(c->nccl);
+    ncclResult_t r = c->aborted ? ncclSuccess : ncclCommDestroy(c->nccl);   // abort already freed it
     delete c;
     if (r != ncclSuccess) return fail(EDT_COMM_ERR_RCCL, "ncclCommDestroy: %s", ncclGetErrorString(r));
     return 0;
@@ -114,10 +161,39 @@ int edt_comm_destroy(void* comm) {
 int edt_comm_rank(const void* comm) { return comm ? static_cast<const Comm*>(comm)->rank : -1; }
 int edt_comm_size(const void* comm) { return comm ? static_cast<const Comm*>(comm)->nranks : -1; }
 
+int edt_comm_abort(void* comm) {
+    Comm* c = as_comm(comm);
+    if (!c) return fail(EDT_COMM_ERR_ARG, "null communicator");
+    abort_comm(c);
+    return 0;
+}
+
+int edt_comm_poll(void* comm) { return usable(as_comm(comm)); }
+
+int edt_comm_set_timeout(void* comm, double seconds) {
+    Comm* c = as_comm(comm);
+    if (!c) return fail(EDT_COMM_ERR_ARG, "null communicator");
+    if (!(seconds >= 0)) return fail(EDT_COMM_ERR_ARG, "timeout %g s", seconds);
+    c->timeout_s = seconds;
+    return 0;
+}
+
+int edt_comm_wait(void* comm, void* stream, double timeout_s) {
+    Comm* c = as_comm(comm);
+    if (int rc = usable(c)) return rc;
+    if (int rc = ensure_events(c, 1)) return rc;
+    hipEvent_t ev = c->events[0];
+    EDT_HIP(hipEventRecord(ev, static_cast<hipStream_t>(stream)));
+    if (int rc = wait_event(c, ev, timeout_s)) return rc;
+    EDT_HIP(hipEventRecord(ev, c->side));                  // and the communicator's own stream
+    return wait_event(c, ev, timeout_s);
+}
+
 int edt_comm_reduce_scatter_f32(void* comm, const float* send, float* recv, uint64_t count_per_rank,
                                 void* stream) {
     Comm* c = as_comm(comm);
-    if (!c || (count_per_rank && (!send || !recv))) return fail(EDT_COMM_ERR_ARG, "null comm or buffer");
+    if (int rc = usable(c)) return rc;
+    if (count_per_rank && (!send || !recv)) return fail(EDT_COMM_ERR_ARG, "null buffer");
     EDT_RCCL(ncclReduceScatter(send, recv, count_per_rank, ncclFloat32, ncclSum, c->nccl,
                                static_cast<hipStream_t>(stream)));
     return 0;
@@ -128,7 +204,8 @@ int edt_comm_all_gather(void* comm, const void* send, void* recv, uint64_t count
     Comm* c = as_comm(comm);
     ncclDataType_t t;
     uint64_t sz;
-    if (!c || (count_per_rank && (!send || !recv))) return fail(EDT_COMM_ERR_ARG, "null comm or buffer");
+    if (int rc = usable(c)) return rc;
+    if (count_per_rank && (!send || !recv)) return fail(EDT_COMM_ERR_ARG, "null buffer");
     if (!nccl_type(dt, &t, &sz)) return fail(EDT_COMM_ERR_ARG, "dtype %d", dt);
     EDT_RCCL(ncclAllGather(send, recv, count_per_rank, t, c->nccl, static_cast<hipStream_t>(stream)));
     return 0;
@@ -139,7 +216,8 @@ int edt_comm_all_to_all(void* comm, const void* send, void* recv, uint64_t count
     Comm* c = as_comm(comm);
     ncclDataType_t t;
     uint64_t sz;
-    if (!c || (count_per_rank && (!send || !recv))) return fail(EDT_COMM_ERR_ARG, "null comm or buffer");
+    if (int rc = usable(c)) return rc;
+    if (count_per_rank && (!send || !recv)) return fail(EDT_COMM_ERR_ARG, "null buffer");
     if (!nccl_type(dt, &t, &sz)) return fail(EDT_COMM_ERR_ARG, "dtype %d", dt);
     EDT_RCCL(ncclAllToAll(send, recv, count_per_rank, t, c->nccl, static_cast<hipStream_t>(stream)));
     return 0;
@@ -149,8 +227,9 @@ int edt_comm_exchange(void* comm, const int32_t* send_to, const int32_t* recv_fr
                       const void* const* sendbufs, void* const* recvbufs, const uint64_t* bytes,
                       int nops, void* stream) {
     Comm* c = as_comm(comm);
-    if (!c || nops < 0 || (nops && (!send_to || !recv_from || !bytes)))
-        return fail(EDT_COMM_ERR_ARG, "null comm or op arrays");
+    if (int rc = usable(c)) return rc;
+    if (nops < 0 || (nops && (!send_to || !recv_from || !bytes)))
+        return fail(EDT_COMM_ERR_ARG, "null op arrays");
     for (int i = 0; i < nops; ++i) {
         if (send_to[i] >= c->nranks || recv_from[i] >= c->nranks)
             return fail(EDT_COMM_ERR_ARG, "op %d names a rank outside [0, %d)", i, c->nranks);
@@ -180,7 +259,8 @@ int edt_outer_step_sharded(void* comm, void* theta_g, int gdt, const void* const
     Comm* c = as_comm(comm);
     ncclDataType_t gt, wt;
     uint64_t gsz, wsz;
-    if (!c || !theta_g || !theta_k || !acc) return fail(EDT_COMM_ERR_ARG, "null comm or buffer");
+    if (int rc = usable(c)) return rc;
+    if (!theta_g || !theta_k || !acc) return fail(EDT_COMM_ERR_ARG, "null buffer");
     if (!nccl_type(gdt, &gt, &gsz) || !nccl_type(wdt, &wt, &wsz)) return fail(EDT_COMM_ERR_ARG, "dtype pair %d/%d", gdt, wdt);
     if (K_local < 1 || K_local > EDT_MAX_WORKERS) return fail(EDT_COMM_ERR_ARG, "K_local %d", K_local);
     const uint64_t unit = (uint64_t)c->nranks * 64;
@@ -227,6 +307,10 @@ int edt_outer_step_sharded(void* comm, void* theta_g, int gdt, const void* const
     // the caller's stream sees the gathered theta
     EDT_HIP(hipEventRecord(c->events[2 * nb], c->side));
     EDT_HIP(hipStreamWaitEvent(s, c->events[2 * nb], 0));
+    // edt_comm_set_timeout > 0: wait here, polling RCCL's async error; a dead or stalled peer
+    // aborts the communicator after the timeout and the step returns EDT_COMM_ERR_TIMEOUT
+    // (the reference's master gives up on workers it stops hearing from, EDT_LM/diloco.py:46-71)
+    if (c->timeout_s > 0) return wait_event(c, c->events[2 * nb], c->timeout_s);
     return 0;
 }
 

@@ -815,6 +815,99 @@ int edt_slerp_population(const void* const* members, int nmembers, int in_dt, co
     return EDT_OK;
 }
 
+// ---- the three passes of edt_slerp_population as separate entries (the link-balanced sharded
+// population, distributed.ShardedSlerpPopulation: Gram sums over a rank's chunk range, then the
+// coefficients from the all-gathered table, then the blends of the rank's range) ----
+
+int edt_slerp_gram(const void* const* members, int nmembers, int in_dt, const uint64_t* chunk_desc,
+                   int64_t nchunks, double* gram, void* stream) {
+    g_err[0] = 0;
+    if (in_dt & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
+    if (nmembers < 1 || nmembers > kGramMaxMembers)
+        return fail(EDT_ERR_ARG, "member count %d out of range [1, %d]", nmembers, kGramMaxMembers);
+    if (nchunks < 0) return fail(EDT_ERR_ARG, "negative chunk count");
+    if (nchunks == 0) return EDT_OK;
+    if (!members || !chunk_desc || !gram) return fail(EDT_ERR_ARG, "null buffer");
+    Members mem;
+    memset(&mem, 0, sizeof(mem));
+    for (int m = 0; m < nmembers; ++m) {
+        if (!members[m] || !aligned16(members[m])) return fail(EDT_ERR_ARG, "member %d is null or not 16-byte aligned", m);
+        mem.p[m] = members[m];
+    }
+    hipStream_t s = (hipStream_t)stream;
+    const unsigned g = EDT_SLERP_GRAM_GRID ? slerp_grid(nchunks) : slerp_spec_grid(nchunks);
+#define EDT_GRAM1(M)                                                                                 \
+    case M:                                                                                          \
+        if (in_dt == EDT_F32) slerp_gram_kernel<EDT_F32, M><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, gram); \
+        else slerp_gram_kernel<EDT_BF16, M><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, gram);              \
+        break;
+    switch (nmembers) {
+        EDT_GRAM1(1) EDT_GRAM1(2) EDT_GRAM1(3) EDT_GRAM1(4) EDT_GRAM1(5) EDT_GRAM1(6) EDT_GRAM1(7) EDT_GRAM1(8)
+    }
+#undef EDT_GRAM1
+    return check_launch("slerp_gram_kernel");
+}
+
+int edt_slerp_gram_coef(const double* gram, int nmembers, const int32_t* pairs, int npairs,
+                        const int32_t* seg_first_chunk, int nseg, const double* t, double dot_threshold,
+                        double eps, float* coef, float* dot_out, void* stream) {
+    g_err[0] = 0;
+    if (nmembers < 1 || nmembers > kGramMaxMembers)
+        return fail(EDT_ERR_ARG, "member count %d out of range [1, %d]", nmembers, kGramMaxMembers);
+    if (npairs < 0 || nseg < 0) return fail(EDT_ERR_ARG, "negative count");
+    if (npairs == 0 || nseg == 0) return EDT_OK;
+    if (!gram || !pairs || !seg_first_chunk || !t || !coef) return fail(EDT_ERR_ARG, "null buffer");
+    const int M = nmembers, NT = M * (M + 1) / 2;
+    hipStream_t s = (hipStream_t)stream;
+    for (int q = 0; q < npairs; ++q) {
+        const int i = pairs[2 * q], j = pairs[2 * q + 1];
+        if (i < 0 || j < 0 || i >= M || j >= M) return fail(EDT_ERR_ARG, "pair %d: member out of range", q);
+        const int lo = i < j ? i : j, hi = i < j ? j : i;
+        slerp_gram_coef_kernel<<<coef_grid(nseg), kBlock, 0, s>>>(gram, NT, tri_index(i, i, M), tri_index(j, j, M),
+                                                                  tri_index(lo, hi, M), seg_first_chunk, nseg, t,
+                                                                  (float)dot_threshold, (float)eps,
+                                                                  coef + 2 * (size_t)nseg * q,
+                                                                  dot_out ? dot_out + (size_t)nseg * q : nullptr);
+        int rc = check_launch("slerp_gram_coef_kernel");
+        if (rc) return rc;
+    }
+    return EDT_OK;
+}
+
+int edt_slerp_blend_children(const void* const* members, int nmembers, int in_dt, const int32_t* pairs,
+                             int npairs, void* const* outs, int out_dt, const uint64_t* chunk_desc,
+                             int64_t nchunks, const float* coef, int nseg, void* stream) {
+    g_err[0] = 0;
+    if ((in_dt | out_dt) & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
+    if (nmembers < 1 || nmembers > kGramMaxMembers)
+        return fail(EDT_ERR_ARG, "member count %d out of range [1, %d]", nmembers, kGramMaxMembers);
+    if (npairs < 0 || npairs > kBlendMaxChildren)
+        return fail(EDT_ERR_ARG, "child count %d out of range [0, %d]", npairs, kBlendMaxChildren);
+    if (npairs == 0 || nchunks == 0) return EDT_OK;
+    if (!members || !pairs || !outs || !chunk_desc || !coef) return fail(EDT_ERR_ARG, "null buffer");
+    Members mem;
+    memset(&mem, 0, sizeof(mem));
+    for (int m = 0; m < nmembers; ++m) {
+        if (!members[m] || !aligned16(members[m])) return fail(EDT_ERR_ARG, "member %d is null or not 16-byte aligned", m);
+        mem.p[m] = members[m];
+    }
+    PopBlend pb;
+    memset(&pb, 0, sizeof(pb));
+    pb.n = npairs;
+    for (int q = 0; q < npairs; ++q) {
+        const int i = pairs[2 * q], j = pairs[2 * q + 1];
+        if (i < 0 || j < 0 || i >= nmembers || j >= nmembers) return fail(EDT_ERR_ARG, "pair %d: member out of range", q);
+        if (!outs[q] || !aligned16(outs[q])) return fail(EDT_ERR_ARG, "output %d is null or not 16-byte aligned", q);
+        for (int m = 0; m < nmembers; ++m)
+            if (outs[q] == members[m]) return fail(EDT_ERR_ARG, "output %d aliases member %d", q, m);
+        pb.out[q] = outs[q];
+        pb.coef[q] = coef + 2 * (size_t)nseg * q;
+        pb.a[q] = i;
+        pb.b[q] = j;
+    }
+    return launch_blend_mm(mem, nmembers, pb, in_dt, out_dt, chunk_desc, nchunks, (hipStream_t)stream);
+}
+
 int edt_slerp_merge_speculative(const void* v0, const void* v1, int in_dt, void* out, int out_dt,
                                 const uint64_t* chunk_desc, int64_t nchunks, const int32_t* seg_first_chunk,
                                 int nseg, const double* t, double dot_threshold, double eps, double* partial,

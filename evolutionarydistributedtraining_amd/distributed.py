@@ -323,3 +323,170 @@ class PopulationCrossover:
             out_momentum.copy_((par1 if donor == pairs[self.rank][0] else par2)[2])
         self.kernels.pair_merge(par1[0], par2[0], par1[1], par2[1], out, out_momentum,
                                 donor is not None, lr, mu, nesterov)
+
+
+class ShardedPopulationCrossover:
+    """A generation of a population of P = world members (one per GPU: BASELINE configs[4], the
+    EDT-RL / EVOMERGE population of 8 SLERP-crossed on 7B bodies across 8 GPUs; or the EDT-LM pair
+    merges), link-balanced. PopulationCrossover ships each child's two parents whole to the child's
+    rank — two full members over at most two of the GPU's seven xGMI links. Here every rank owns a
+    parameter-index shard instead (a contiguous range of whole SLERP chunks, ~1/N of the layout):
+
+      1. members -> shards: rank r sends rank s the slice of its member in s's range (grouped p2p,
+         every link busy: (N-1)/N of a member out and in per rank);
+      2. SLERP: per-chunk Gram sums of all N members over the rank's chunks (edt_slerp_gram),
+         all-gathered (nchunks x N(N+1)/2 doubles: ~31 MB at 7B), then every child's coefficients
+         (edt_slerp_gram_coef) — each chunk's sums come from the same kernel in the same order
+         wherever the chunk lives, so every child is bit-identical to edt_slerp_merge on its two
+         parents; then the rank's range of every child (edt_slerp_blend_children).
+         EDT-LM: the rank's range of every child (edt_pair_merge_population), nothing to gather;
+      3. child shards -> children: the range of child c goes to rank c.
+
+    Wire bytes per rank and generation: (N-1)/N x (member + child) (+ the donor momenta for
+    EDT-LM), spread over all N-1 links, against up to two whole members over one or two links.
+    Reference: EDT_RL/edt.py:286-299 (the master merges pair after pair), EDT_EVOMERGE/edt.py:262-280.
+    A rank's range starts at a multiple of 8 elements below its first chunk (<= 7 elements shared
+    with the previous rank), so every chunk keeps its vector alignment and hence its sums."""
+
+    def __init__(self, layout: ParamLayout, dtype: torch.dtype, device, kind: str = "slerp",
+                 out_dtype: torch.dtype | None = None, comm: Collectives | None = None, group=None,
+                 kernels=None, chunk_elems: int = 1 << 16):
+        if kind not in ("slerp", "sgd"):
+            raise ValueError(kind)
+        self.comm = comm or TorchCollectives(group)
+        self.world, self.rank = self.comm.world, self.comm.rank
+        if self.world > 8 and kind == "slerp":
+            raise ValueError("the Gram pass takes at most 8 members (one per rank)")
+        if self.world > 16:
+            raise ValueError("at most 16 children per launch")
+        self.kind, self.layout, self.device = kind, layout, torch.device(device)
+        self.dtype, self.out_dtype = dtype, out_dtype or dtype
+        self.kernels = kernels or _ops
+        import numpy as np
+        self.plan = self.kernels.make_slerp_plan(layout.offsets, self.device, chunk_elems=chunk_elems)
+        host = np.asarray(self.plan.chunks_host, dtype=np.int64).reshape(-1, 3)
+        n, N = layout.total, self.world
+        starts = host[:, 0] if len(host) else np.zeros(0, dtype=np.int64)
+        cuts = [0] + [int(np.searchsorted(starts, (r * n) // N, side="left")) for r in range(1, N)] + [len(host)]
+        self.ranges = []           # per rank: (first chunk, end chunk, base, start, end) in elements
+        for r in range(N):
+            c0, c1 = cuts[r], max(cuts[r], cuts[r + 1])
+            if c1 > c0:
+                start, end = int(host[c0, 0]), int(host[c1 - 1, 0] + host[c1 - 1, 1])
+            else:
+                start = end = int(host[c0, 0]) if c0 < len(host) else n
+            self.ranges.append((c0, c1, start // 8 * 8, start, end))
+        c0, c1, base, start, end = self.ranges[self.rank]
+        self.nloc = c1 - c0
+        self.base, self.start, self.end = base, start, end
+        loc = host[c0:c1].copy()
+        loc[:, 0] -= base
+        self.local_chunks = torch.from_numpy(loc).to(self.device) if self.device.type == "cuda" else torch.from_numpy(loc)
+        L = end - base
+        self._shard = lambda dt: torch.empty(max(L, 8), dtype=dt, device=self.device)
+        self._bufs = {}
+
+    def _buf(self, key, dt):
+        if key not in self._bufs:
+            self._bufs[key] = self._shard(dt)
+        return self._bufs[key]
+
+    def _scatter(self, tensors, tag):
+        """Every rank's tensors -> this rank's range of each: {tag, j: buffer of rank j's tensor}."""
+        ops_, got = [], {}
+        L = self.end - self.base
+        for s in range(self.world):
+            _, _, b, _, e = self.ranges[s]
+            if s != self.rank and e > b:
+                for i, t in enumerate(tensors):
+                    ops_.append(("send", t[b:e], s))
+        for j in range(self.world):
+            bufs = [self._buf((tag, i, j), t.dtype) for i, t in enumerate(tensors)]
+            got[j] = [bb[:L] for bb in bufs]
+            if j == self.rank:
+                for bb, t in zip(got[j], tensors):
+                    bb.copy_(t[self.base:self.end])
+            elif L > 0:
+                ops_.extend(("recv", bb, j) for bb in got[j])
+        self.comm.p2p(ops_)
+        return got
+
+    def _gather_children(self, shards, outs):
+        """Child q's range from every rank into outs (this rank's child): shards[q] = this rank's
+        range of child q (buffers of base..end); outs = this rank's child tensors."""
+        ops_ = []
+        off = self.start - self.base
+        for q in range(self.world):
+            for sh, out in zip(shards[q], outs):
+                if q == self.rank:
+                    out[self.start:self.end].copy_(sh[off:self.end - self.base])
+                elif self.end > self.start:
+                    ops_.append(("send", sh[off:self.end - self.base], q))
+        for j in range(self.world):
+            _, _, _, st, en = self.ranges[j]
+            if j != self.rank and en > st:
+                ops_.extend(("recv", out[st:en], j) for out in outs)
+        self.comm.p2p(ops_)
+
+    def slerp_step(self, member: torch.Tensor, pairs, t: torch.Tensor, out: torch.Tensor,
+                   dot_threshold: float = 0.9995, eps: float = 1e-8) -> torch.Tensor:
+        """Child pairs[rank] into `out`; returns the per-segment dots of every child [N, nseg]."""
+        if len(pairs) != self.world:
+            raise ValueError(f"{len(pairs)} children for {self.world} ranks")
+        k, N = self.kernels, self.world
+        sh = self._scatter([member], "m")
+        members = [sh[j][0] for j in range(N)]
+        NT = N * (N + 1) // 2
+        gram = self._bufs.get("gram")
+        if gram is None:
+            gram = self._bufs["gram"] = torch.empty((max(1, self.plan.nchunks), NT), dtype=torch.float64,
+                                                    device=self.device)
+        c0, c1 = self.ranges[self.rank][:2]
+        if self.nloc:
+            k.slerp_gram(members, self.local_chunks, self.nloc, gram[c0:c1])
+        ops_ = []                       # all-gather of the Gram rows: every rank's chunk range
+        for s in range(N):
+            if s != self.rank and self.nloc:
+                ops_.append(("send", gram[c0:c1], s))
+        for j in range(N):
+            a, b = self.ranges[j][:2]
+            if j != self.rank and b > a:
+                ops_.append(("recv", gram[a:b], j))
+        self.comm.p2p(ops_)
+        coef, dots = k.slerp_gram_coef(self.plan, gram, N, pairs, t, dot_threshold, eps)
+        outs = [self._buf(("c", q), self.out_dtype)[:self.end - self.base] for q in range(N)]
+        if self.nloc:
+            k.slerp_blend_children(members, pairs, outs, self.local_chunks, self.nloc, coef, self.plan.nseg)
+        self._gather_children([[o] for o in outs], [out])
+        return dots
+
+    def pair_merge_step(self, base: torch.Tensor, trained: torch.Tensor, momentum: torch.Tensor | None,
+                        pairs, out: torch.Tensor, out_momentum: torch.Tensor | None, lr: float = 0.7,
+                        mu: float = 0.9, nesterov: bool = True, has_momentum: bool = True,
+                        generation: int = 0) -> None:
+        """EDT-LM child pairs[rank] into out / out_momentum (EDT_LM/train/crossover.py:150-237;
+        donor = parent 1 when it has an outer momentum, else parent 2, as PopulationCrossover)."""
+        if len(pairs) != self.world:
+            raise ValueError(f"{len(pairs)} children for {self.world} ranks")
+        flags = self.comm.all_gather_object(bool(has_momentum and momentum is not None))
+        donors = [i if flags[i] else (j if flags[j] else None) for i, j in pairs]
+        if mu != 0 and generation > 0 and any(d is None for d in donors):
+            raise NotImplementedError("Merging outer optimizer states not implemented for this case.")
+        send_mom = any(d is not None for d in donors)      # some child inherits a buffer
+        if send_mom and out_momentum is None:
+            raise ValueError("the child inherits an outer momentum: pass out_momentum")
+        with_mom = out_momentum is not None                # children write one (mu != 0)
+        send = [base, trained] + ([momentum if momentum is not None else torch.zeros_like(base)] if send_mom else [])
+        sh = self._scatter(send, "p")
+        L = self.end - self.base
+        children = []
+        outs = [[self._buf(("c", q), self.out_dtype)[:L]] + ([self._buf(("cm", q), out_momentum.dtype)[:L]]
+                                                             if with_mom else []) for q in range(self.world)]
+        for q, (i, j) in enumerate(pairs):
+            d = donors[q]
+            children.append({"b1": sh[i][0], "b2": sh[j][0], "m1": sh[i][1], "m2": sh[j][1], "out": outs[q][0],
+                             "momentum": outs[q][1] if with_mom else None,
+                             "momentum_in": sh[d][2] if d is not None else None, "has_momentum": d is not None})
+        if L > 0:
+            self.kernels.pair_merge_population(children, lr, mu, nesterov)
+        self._gather_children(outs, [out] + ([out_momentum] if with_mom else []))

@@ -183,6 +183,7 @@ class SlerpPlan:
     dots: torch.Tensor            # float32 [nseg]
     nchunks: int
     relative: bool = False        # chunk starts relative to their segment (tensor-list form)
+    chunks_host: object = None    # numpy int64 [nchunks, 3]: the same table on the host
 
     @property
     def nseg(self) -> int:
@@ -212,7 +213,7 @@ def make_slerp_plan(seg_offsets: list[int], device: torch.device,
     return SlerpPlan(list(seg_offsets), chunks, seg_first,
                      torch.empty((max(1, nchunks), 3), dtype=torch.float64, device=device),
                      torch.empty((max(1, nseg), 2), dtype=torch.float32, device=device),
-                     torch.empty(max(1, nseg), dtype=torch.float32, device=device), nchunks, relative)
+                     torch.empty(max(1, nseg), dtype=torch.float32, device=device), nchunks, relative, host)
 
 
 def _speculation_pays(plan: SlerpPlan, in_bytes: int, out_bytes: int) -> bool:
@@ -408,3 +409,62 @@ def pair_merge_population(children, lr: float, momentum_coef: float, nesterov: b
         L.dtype_code(wdt), L.ptr_array([ch["out"] for ch in children]), L.dtype_code(gdt),
         arr(mom_in), arr(mom_out), has, C, n, float(lr), float(momentum_coef), int(nesterov),
         L.stream_ptr(first["out"].device)), "edt_pair_merge_population")
+
+
+# ------------------------------------------------------------------------------------------
+# the population SLERP's three passes, separately (distributed.ShardedSlerpPopulation)
+
+def slerp_gram(members: list[torch.Tensor], chunks: torch.Tensor, nchunks: int,
+               gram: torch.Tensor | None = None) -> torch.Tensor:
+    """Per-chunk Gram sums of M <= 8 member buffers over a chunk table (int64 [nchunks, 3] on the
+    device, starts relative to the buffers): float64 [nchunks, M(M+1)/2] (edt_slerp_gram)."""
+    lib = L.lib()
+    M = len(members)
+    L.require_device(*members, chunks)
+    if not 1 <= M <= 8 or any(m.dtype != members[0].dtype for m in members):
+        raise L.EdtError("slerp_gram: 1..8 members of one dtype")
+    NT = M * (M + 1) // 2
+    if gram is None:
+        gram = torch.empty((max(1, nchunks), NT), dtype=torch.float64, device=members[0].device)
+    elif gram.dtype != torch.float64 or gram.numel() < nchunks * NT:
+        raise L.EdtError("gram: float64 with nchunks x M(M+1)/2 elements")
+    L.check(lib.edt_slerp_gram(L.ptr_array(members), M, L.dtype_code(members[0]), L.ptr(chunks), nchunks,
+                               L.ptr(gram), L.stream_ptr(members[0].device)), "edt_slerp_gram")
+    return gram
+
+
+def slerp_gram_coef(plan: SlerpPlan, gram: torch.Tensor, nmembers: int, pairs, t: torch.Tensor,
+                    dot_threshold: float = 0.9995, eps: float = 1e-8):
+    """Coefficients [Q, nseg, 2] and dots [Q, nseg] of every child from a whole-layout Gram
+    table (rows = plan's chunks) (edt_slerp_gram_coef)."""
+    lib = L.lib()
+    Q = len(pairs)
+    if gram.numel() < plan.nchunks * nmembers * (nmembers + 1) // 2:
+        raise L.EdtError("gram does not cover the plan's chunks")
+    L.require_device(gram, t)
+    if t.dtype != torch.float64 or t.numel() < plan.nseg:
+        raise L.EdtError("t must be a float64 device tensor with one value per segment")
+    dev = gram.device
+    coef = torch.empty((max(1, Q), max(1, plan.nseg), 2), dtype=torch.float32, device=dev)
+    dots = torch.empty((max(1, Q), max(1, plan.nseg)), dtype=torch.float32, device=dev)
+    fp = (ctypes.c_int32 * max(1, 2 * Q))(*[int(x) for p in pairs for x in p])
+    L.check(lib.edt_slerp_gram_coef(L.ptr(gram), nmembers, fp, Q, L.ptr(plan.seg_first), plan.nseg, L.ptr(t),
+                                    float(dot_threshold), float(eps), L.ptr(coef), L.ptr(dots),
+                                    L.stream_ptr(dev)), "edt_slerp_gram_coef")
+    return coef, dots
+
+
+def slerp_blend_children(members: list[torch.Tensor], pairs, outs: list[torch.Tensor], chunks: torch.Tensor,
+                         nchunks: int, coef: torch.Tensor, nseg: int) -> None:
+    """outs[q] = c0 members[a] + c1 members[b] over a chunk table, coef [Q, nseg, 2] per child
+    (edt_slerp_blend_children; <= 8 members, <= 16 children)."""
+    lib = L.lib()
+    Q = len(pairs)
+    L.require_device(*members, *outs, chunks, coef)
+    if Q != len(outs) or coef.dtype != torch.float32 or coef.numel() < Q * nseg * 2:
+        raise L.EdtError("slerp_blend_children: one output per pair, coef [Q, nseg, 2] float32")
+    fp = (ctypes.c_int32 * max(1, 2 * Q))(*[int(x) for p in pairs for x in p])
+    L.check(lib.edt_slerp_blend_children(L.ptr_array(members), len(members), L.dtype_code(members[0]), fp, Q,
+                                         L.ptr_array(outs), L.dtype_code(outs[0]), L.ptr(chunks), nchunks,
+                                         L.ptr(coef), nseg, L.stream_ptr(members[0].device)),
+            "edt_slerp_blend_children")

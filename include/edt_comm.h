@@ -24,6 +24,8 @@ extern "C" {
 #define EDT_COMM_ERR_ARG (-1)
 #define EDT_COMM_ERR_RCCL (-2)
 #define EDT_COMM_ERR_HIP (-3)
+#define EDT_COMM_ERR_ABORTED (-4)   /* the communicator was aborted (edt_comm_abort or a timeout) */
+#define EDT_COMM_ERR_TIMEOUT (-5)   /* a bounded wait expired; the communicator is now aborted */
 
 /* Bytes of the opaque communicator id (ncclUniqueId): rank 0 makes it, every rank passes the
  * same bytes to edt_comm_init (the host moves them, e.g. over its own control channel). */
@@ -35,6 +37,25 @@ int edt_comm_init(void** comm, const void* id, int nranks, int rank);
 int edt_comm_destroy(void* comm);
 int edt_comm_rank(const void* comm);
 int edt_comm_size(const void* comm);
+
+/* Failure handling (the reference's master polls its workers over HTTP and gives up on the ones
+ * that stop answering, EDT_LM/diloco.py:46-71, diloco_sim.py:65-68; here a dead rank would
+ * otherwise leave its peers inside a collective forever):
+ *   edt_comm_abort        tear the RCCL communicator down (ncclCommAbort): outstanding collectives
+ *                         end, every later call on it returns EDT_COMM_ERR_ABORTED;
+ *                         edt_comm_destroy still frees the handle.
+ *   edt_comm_poll         0, or the asynchronous RCCL error a peer's failure left (every entry
+ *                         point checks this first and refuses to enqueue on a failed communicator).
+ *   edt_comm_wait         host wait until the work enqueued on `stream` and on the communicator's
+ *                         own stream is done, polling the async error; after timeout_s seconds
+ *                         (<= 0: no limit) the communicator is aborted -> EDT_COMM_ERR_TIMEOUT.
+ *   edt_comm_set_timeout  > 0: edt_outer_step_sharded ends with edt_comm_wait(comm, stream, s)
+ *                         (the step then returns when done, or fails after s seconds); 0 (the
+ *                         default): it returns as soon as the work is enqueued. */
+int edt_comm_abort(void* comm);
+int edt_comm_poll(void* comm);
+int edt_comm_wait(void* comm, void* stream, double timeout_s);
+int edt_comm_set_timeout(void* comm, double seconds);
 
 /* Collectives (dt: EDT_F32 = 0, EDT_BF16 = 1 as in edt_sync.h).
  * reduce_scatter_f32: recv[0, count) = sum over ranks of send[rank * count, +count).

@@ -238,6 +238,29 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
                                      double dot_threshold, double eps, double* partial, float* coef,
                                      float* dot_out, int32_t* redo, uint64_t n, void* stream);
 
+/* ---- the population SLERP's passes, separately (link-balanced sharded population) ----------
+ * edt_slerp_population = edt_slerp_gram + edt_slerp_gram_coef + edt_slerp_blend_children. Split
+ * so that the Gram sums of a rank's range of whole chunks (its parameter-index shard of all M
+ * members, EDT_RL/edt.py:286-299's population spread over the node) can be all-gathered before
+ * the coefficients: each chunk's sums are formed by the same kernel in the same order wherever
+ * the chunk lives, so the coefficients — and every child — equal edt_slerp_merge's bit for bit.
+ *   edt_slerp_gram        gram[c * NT + tri(a, b)], NT = M(M+1)/2, for the chunks of chunk_desc
+ *                         (starts relative to the member buffers); M <= 8.
+ *   edt_slerp_gram_coef   per child q = (pairs[2q], pairs[2q+1]) (member indices), per segment of
+ *                         the whole layout (seg_first_chunk indexes gram's rows): coef[q][nseg][2],
+ *                         dot_out[q][nseg] (may be NULL).
+ *   edt_slerp_blend_children  outs[q] = c0 v_a + c1 v_b over the chunks of chunk_desc, the segment
+ *                         of each chunk selecting coef[q][seg] (nseg = the row length of coef);
+ *                         <= 16 children, member-major (each member's tile read once per chunk). */
+int edt_slerp_gram(const void* const* members, int nmembers, int in_dt, const uint64_t* chunk_desc,
+                   int64_t nchunks, double* gram, void* stream);
+int edt_slerp_gram_coef(const double* gram, int nmembers, const int32_t* pairs, int npairs,
+                        const int32_t* seg_first_chunk, int nseg, const double* t, double dot_threshold,
+                        double eps, float* coef, float* dot_out, void* stream);
+int edt_slerp_blend_children(const void* const* members, int nmembers, int in_dt, const int32_t* pairs,
+                             int npairs, void* const* outs, int out_dt, const uint64_t* chunk_desc,
+                             int64_t nchunks, const float* coef, int nseg, void* stream);
+
 /* ---- misc ---- */
 const char* edt_last_error(void);
 const char* edt_version(void);

@@ -1,6 +1,7 @@
 """Test-only stand-in for the HIP kernels: the CPU oracle behind the same call surface as
 `evolutionarydistributedtraining_amd.ops` (the product default). Used to exercise the
 multi-rank host logic (gloo, CPU) and as the checker of the GPU runs."""
+import torch
 
 
 class OracleKernels:
@@ -37,3 +38,74 @@ class OracleKernels:
 
     def sgd_apply(self, theta, acc, mom, has, lr, mu, nesterov):
         self.o.sgd_apply(theta, acc, mom, has, lr, mu, nesterov)
+
+
+class ChunkGramKernels(OracleKernels):
+    """CPU stand-in for the split population-SLERP passes (edt_slerp_gram / _gram_coef /
+    _blend_children) with the same chunk-table semantics: per-chunk fp64 sums (torch, one fixed
+    order per chunk), per-segment sums over the chunks in order, the reference's scalar formula,
+    fp32 blends. Used to test the sharded schedule's data movement on CPU (gloo / virtual ranks):
+    a sharded run must equal this same arithmetic on the whole population, bit for bit."""
+
+    def make_slerp_plan(self, offsets, device, chunk_elems=1 << 16):
+        import types
+
+        import numpy as np
+        rows, first = [], []
+        for s in range(len(offsets) - 1):
+            first.append(len(rows))
+            for x in range(offsets[s], offsets[s + 1], chunk_elems):
+                rows.append((x, min(chunk_elems, offsets[s + 1] - x), s))
+        first.append(len(rows))
+        host = np.asarray(rows, dtype=np.int64).reshape(-1, 3)
+        return types.SimpleNamespace(seg_offsets=list(offsets), chunks=torch.from_numpy(host), chunks_host=host,
+                                     seg_first=first, nseg=len(offsets) - 1, nchunks=len(rows))
+
+    def slerp_gram(self, members, chunks, nchunks, gram=None):
+        M = len(members)
+        NT = M * (M + 1) // 2
+        out = torch.zeros((max(1, nchunks), NT), dtype=torch.float64) if gram is None else gram
+        for c in range(nchunks):
+            a, n = int(chunks[c, 0]), int(chunks[c, 1])
+            xs = [m[a:a + n].double() for m in members]
+            q = 0
+            for i in range(M):
+                for j in range(i, M):
+                    out[c, q] = (xs[i] * xs[j]).sum()
+                    q += 1
+        return out
+
+    def slerp_gram_coef(self, plan, gram, M, pairs, t, thr=0.9995, eps=1e-8):
+        import math
+        tri = {}
+        q = 0
+        for i in range(M):
+            for j in range(i, M):
+                tri[(i, j)] = q
+                q += 1
+        coef = torch.empty((len(pairs), plan.nseg, 2), dtype=torch.float32)
+        dots = torch.empty((len(pairs), plan.nseg), dtype=torch.float32)
+        for p, (i, j) in enumerate(pairs):
+            lo, hi = min(i, j), max(i, j)
+            for s in range(plan.nseg):
+                rows = gram[plan.seg_first[s]:plan.seg_first[s + 1]]
+                s00 = float(rows[:, tri[(i, i)]].sum())
+                s11 = float(rows[:, tri[(j, j)]].sum())
+                s01 = float(rows[:, tri[(lo, hi)]].sum())
+                n0, n1 = math.sqrt(s00), math.sqrt(s11)
+                d = s01 / ((n0 if n0 > eps else 1.0) * (n1 if n1 > eps else 1.0))
+                tt = float(t[s])
+                if abs(d) > thr:
+                    c0, c1 = 1 - tt, tt
+                else:
+                    th = math.acos(max(-1.0, min(1.0, d)))
+                    c0, c1 = math.sin(th - th * tt) / math.sin(th), math.sin(th * tt) / math.sin(th)
+                coef[p, s, 0], coef[p, s, 1], dots[p, s] = c0, c1, d
+        return coef, dots
+
+    def slerp_blend_children(self, members, pairs, outs, chunks, nchunks, coef, nseg):
+        for c in range(nchunks):
+            a, n, s = (int(x) for x in chunks[c])
+            for q, (i, j) in enumerate(pairs):
+                outs[q][a:a + n] = (coef[q, s, 0] * members[i][a:a + n].float()
+                                    + coef[q, s, 1] * members[j][a:a + n].float()).to(outs[q].dtype)

@@ -445,3 +445,39 @@ def test_comm_abi_sharded_outer_step_world1(dev, wdt):
     assert torch.equal(th.view(torch.int32), ref_t.view(torch.int32))
     assert torch.equal(mom.view(torch.int32), ref_m.view(torch.int32))
     assert not th[n:].any()
+
+
+def test_comm_abi_bounded_step_and_abort_world1(dev):
+    """The failure path of include/edt_comm.h: with a timeout set, the sharded step waits for its
+    work (polling RCCL's async error) and returns done; after edt_comm_abort every call fails
+    with a negative code and a message (EDT_COMM_ERR_ABORTED), and the handle still closes."""
+    from evolutionarydistributedtraining_amd import _lib as L
+    from evolutionarydistributedtraining_amd.comm import ERR_ABORTED, Comm, load_comm_library
+    n = 64 * 1000
+    g = torch.Generator(device=dev).manual_seed(2)
+    th = torch.randn(n, generator=g, device=dev) * 0.02
+    ws = [th + torch.randn(n, generator=g, device=dev) * 1e-3 for _ in range(3)]
+    mom, acc = torch.zeros(n, device=dev), torch.empty(n, device=dev)
+    c = Comm(Comm.unique_id(), 1, 0)
+    try:
+        c.poll()
+        c.set_timeout(60.0)
+        ref = th.clone()
+        ops_mom = torch.zeros(n, device=dev)
+        from evolutionarydistributedtraining_amd import ops
+        ops.outer_step(ref, ws, ops_mom, False, 0.7, 0.9, True)
+        c.outer_step_sharded(th, ws, mom, False, 0.7, 0.9, True, acc, bucket_elems=8192)
+        c.wait(dev, timeout_s=60.0)
+        assert torch.equal(th.view(torch.int32), ref.view(torch.int32))
+        c.abort()
+        lib = load_comm_library()
+        rc = lib.edt_comm_reduce_scatter_f32(c._h, L.ptr(acc), L.ptr(acc), n, L.stream_ptr(dev))
+        assert rc == ERR_ABORTED and b"aborted" in lib.edt_comm_last_error()
+        with pytest.raises(L.EdtError, match="aborted"):
+            c.poll()
+        with pytest.raises(L.EdtError, match="aborted"):
+            c.outer_step_sharded(th, ws, mom, True, 0.7, 0.9, True, acc, bucket_elems=8192)
+        with pytest.raises(L.EdtError, match="aborted"):
+            c.wait(dev, timeout_s=1.0)
+    finally:
+        c.close()

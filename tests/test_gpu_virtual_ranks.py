@@ -111,3 +111,68 @@ def test_population_crossover_on_virtual_ranks(world):
         assert torch.equal(res[c][0].view(torch.int32), want.view(torch.int32)), c
         assert torch.equal(res[c][1].view(torch.int16), out.view(torch.int16)), c
         assert torch.equal(res[c][2].view(torch.int16), m_out.view(torch.int16)), c
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("out_dt", [torch.float32, torch.bfloat16])
+def test_sharded_population_slerp_on_virtual_ranks(world, out_dt):
+    """The link-balanced population SLERP (each rank: a range of whole chunks of all members, Gram
+    rows all-gathered, its range of every child blended and sent to the child's rank) with the HIP
+    passes: every child bit-identical to edt_slerp_merge on its two parents, and the dots too."""
+    from evolutionarydistributedtraining_amd.distributed import ShardedPopulationCrossover
+    from evolutionarydistributedtraining_amd.params import ParamLayout
+    layout = ParamLayout([(513, 301), (7,), (1,), (131073,), (3, 1001), (64, 2049), (5,), (300_007,)])
+    n = layout.total
+    g = torch.Generator().manual_seed(8)
+    base = torch.randn(n, generator=g) * 0.02
+    members = [(base + torch.randn(n, generator=g) * 0.02 * (0.005 if r % 3 else 0.1)).bfloat16().to(DEV)
+               for r in range(world)]
+    pairs = [((3 * c + 1) % world, (5 * c + 2) % world) for c in range(world)]
+    t = torch.tensor([0.3, 0.5, 0.9, 0.5, 0.43, 0.7, 0.5, 0.6], dtype=torch.float64, device=DEV)
+
+    def body(comm):
+        sp = ShardedPopulationCrossover(layout, torch.bfloat16, DEV, kind="slerp", out_dtype=out_dt, comm=comm)
+        out = torch.full((n,), float("nan"), dtype=out_dt, device=DEV)
+        dots = sp.slerp_step(members[comm.rank], pairs, t, out)
+        return out, dots.clone()
+
+    res = VirtualWorld(world).run(body)
+    torch.cuda.synchronize()
+    plan = ops.make_slerp_plan(layout.offsets, DEV)
+    for c, (i, j) in enumerate(pairs):
+        want = torch.empty(n, dtype=out_dt, device=DEV)
+        ops.slerp_arena(plan, members[i], members[j], want, t, speculate=False)
+        torch.cuda.synchronize()
+        assert torch.equal(bits(res[c][0]), bits(want)), c
+        assert torch.equal(res[0][1][c], plan.dots[:plan.nseg]), c
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_sharded_population_pair_merge_on_virtual_ranks(world):
+    """EDT-LM children through the shards (edt_pair_merge_population on every rank's range) equal
+    edt_pair_merge per child on whole parents, child and momentum."""
+    from evolutionarydistributedtraining_amd.distributed import ShardedPopulationCrossover
+    from evolutionarydistributedtraining_amd.params import ParamLayout
+    layout = ParamLayout([(513, 301), (7,), (131073,), (5,)])
+    n = layout.total
+    g = torch.Generator().manual_seed(9)
+    base = [(torch.randn(n, generator=g) * 0.02).bfloat16().to(DEV) for _ in range(world)]
+    trained = [(b.float() + torch.randn(n, generator=g).to(DEV) * 1e-3).bfloat16() for b in base]
+    mom = [(torch.randn(n, generator=g) * 1e-3).bfloat16().to(DEV) for _ in range(world)]
+    pairs = [((3 * c + 1) % world, (5 * c + 2) % world) for c in range(world)]
+
+    def body(comm):
+        r = comm.rank
+        sp = ShardedPopulationCrossover(layout, torch.bfloat16, DEV, kind="sgd", comm=comm)
+        out, out_m = torch.empty(n, dtype=torch.bfloat16, device=DEV), torch.empty(n, dtype=torch.bfloat16, device=DEV)
+        sp.pair_merge_step(base[r], trained[r], mom[r], pairs, out, out_m, generation=1)
+        return out, out_m
+
+    res = VirtualWorld(world).run(body)
+    torch.cuda.synchronize()
+    for c, (i, j) in enumerate(pairs):
+        out, m_out = torch.empty(n, dtype=torch.bfloat16, device=DEV), torch.empty(n, dtype=torch.bfloat16, device=DEV)
+        ops.pair_merge(base[i], base[j], trained[i], trained[j], out, m_out, True, 0.7, 0.9, True, momentum_in=mom[i])
+        torch.cuda.synchronize()
+        assert torch.equal(bits(res[c][0]), bits(out)), c
+        assert torch.equal(bits(res[c][1]), bits(m_out)), c

@@ -1,0 +1,123 @@
+"""The link-balanced population crossover (distributed.ShardedPopulationCrossover) on CPU: every
+rank owns a range of whole SLERP chunks of all members, the Gram rows are all-gathered, every
+child's range is blended locally and sent to the child's rank. Virtual ranks (world 2..8) and a
+gloo world-3 run, with the CPU stand-in kernels (tests/oracle_kernels.ChunkGramKernels: same
+chunk semantics as the HIP passes): each child must equal the same arithmetic on the whole
+population, bit for bit; EDT-LM children equal the oracle pair merge. The GPU form (HIP kernels,
+against edt_slerp_merge per child) is in tests/test_gpu_virtual_ranks.py."""
+import os
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from evolutionarydistributedtraining_amd.collectives import VirtualWorld
+from evolutionarydistributedtraining_amd.params import ParamLayout
+
+SHAPES = [(33, 7), (5,), (300,), (1,), (64, 65), (3,), (1000,)]     # odd sizes: chunks off the 8-grid
+CHUNK = 256
+
+
+def _members(world, n):
+    g = torch.Generator().manual_seed(21)
+    base = torch.randn(n, generator=g) * 0.02
+    return [(base + torch.randn(n, generator=g) * 0.02 * (0.01 if r % 2 else 0.1)).bfloat16() for r in range(world)]
+
+
+def _pairs(world):
+    return [((3 * c + 1) % world, (5 * c + 2) % world) for c in range(world)]
+
+
+def _whole(kern, layout, members, pairs, t):
+    plan = kern.make_slerp_plan(layout.offsets, "cpu", chunk_elems=CHUNK)
+    M = len(members)
+    gram = kern.slerp_gram(members, plan.chunks, plan.nchunks)
+    coef, dots = kern.slerp_gram_coef(plan, gram, M, pairs, t)
+    outs = [torch.empty(layout.total, dtype=torch.float32) for _ in pairs]
+    kern.slerp_blend_children(members, pairs, outs, plan.chunks, plan.nchunks, coef, plan.nseg)
+    return outs, dots
+
+
+def _run(comm, layout, members, pairs, t, oracle, kind):
+    from evolutionarydistributedtraining_amd.distributed import ShardedPopulationCrossover
+    from tests.oracle_kernels import ChunkGramKernels
+    r = comm.rank
+    sp = ShardedPopulationCrossover(layout, torch.bfloat16, "cpu", kind=kind, out_dtype=torch.float32 if kind == "slerp"
+                                    else torch.bfloat16, comm=comm, kernels=ChunkGramKernels(oracle), chunk_elems=CHUNK)
+    if kind == "slerp":
+        out = torch.full((layout.total,), float("nan"))
+        dots = sp.slerp_step(members[r], pairs, t, out)
+        return out, dots, sp.ranges
+    g = torch.Generator().manual_seed(50 + r)
+    trained = (members[r].float() + torch.randn(layout.total, generator=g) * 1e-3).bfloat16()
+    mom = (torch.randn(layout.total, generator=g) * 1e-3).bfloat16()
+    out = torch.empty(layout.total, dtype=torch.bfloat16)
+    out_m = torch.empty_like(out)
+    sp.pair_merge_step(members[r], trained, mom if r != 0 else None, pairs, out, out_m, generation=1)
+    return out, out_m, trained, mom
+
+
+@pytest.mark.parametrize("world", [2, 3, 5, 8])
+def test_sharded_slerp_population_virtual(oracle, world):
+    from tests.oracle_kernels import ChunkGramKernels
+    layout = ParamLayout(SHAPES)
+    members = _members(world, layout.total)
+    pairs = _pairs(world)
+    t = torch.tensor([0.3, 0.5, 0.9, 0.5, 0.43, 0.7, 0.5], dtype=torch.float64)
+    res = VirtualWorld(world).run(lambda comm: _run(comm, layout, members, pairs, t, oracle, "slerp"))
+    want, wdots = _whole(ChunkGramKernels(oracle), layout, members, pairs, t)
+    ranges = res[0][2]
+    assert ranges[0][3] == 0 and ranges[-1][4] == layout.total          # the ranges tile the layout
+    assert all(ranges[r][4] == ranges[r + 1][3] for r in range(world - 1))
+    for c in range(world):
+        assert torch.equal(res[c][0].view(torch.int32), want[c].view(torch.int32)), c
+        assert torch.equal(res[c][1], wdots)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_pair_merge_population_virtual(oracle, world):
+    """EDT-LM children through the shards: the oracle's pair merge on whole members (rank 0 has no
+    outer momentum: its children take parent 2's, EDT_LM/train/crossover.py:183-227)."""
+    layout = ParamLayout(SHAPES)
+    members = _members(world, layout.total)
+    pairs = _pairs(world)
+    res = VirtualWorld(world).run(lambda comm: _run(comm, layout, members, pairs, None, oracle, "sgd"))
+    for c, (i, j) in enumerate(pairs):
+        donor = i if i != 0 else j
+        out = torch.empty(layout.total, dtype=torch.bfloat16)
+        mom = res[donor][3].clone()
+        oracle.pair_merge(members[i], members[j], res[i][2], res[j][2], out, mom, True, 0.7, 0.9, True)
+        assert torch.equal(res[c][0].view(torch.int16), out.view(torch.int16)), c
+        assert torch.equal(res[c][1].view(torch.int16), mom.view(torch.int16)), c
+
+
+def _gloo_worker(rank, world, port, outdir):
+    import torch.distributed as dist
+
+    from oracle import oracle
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from evolutionarydistributedtraining_amd.collectives import TorchCollectives
+    layout = ParamLayout(SHAPES)
+    members = _members(world, layout.total)
+    t = torch.tensor([0.3, 0.5, 0.9, 0.5, 0.43, 0.7, 0.5], dtype=torch.float64)
+    out, dots, _ = _run(TorchCollectives(), layout, members, _pairs(world), t, oracle, "slerp")
+    torch.save({"out": out, "dots": dots}, os.path.join(outdir, f"s{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.slow
+def test_sharded_slerp_population_gloo_world3(tmp_path, oracle):
+    from tests.oracle_kernels import ChunkGramKernels
+    from tests.test_distributed_cpu import _free_port
+    world = 3
+    mp.start_processes(_gloo_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    layout = ParamLayout(SHAPES)
+    t = torch.tensor([0.3, 0.5, 0.9, 0.5, 0.43, 0.7, 0.5], dtype=torch.float64)
+    want, wdots = _whole(ChunkGramKernels(oracle), layout, _members(world, layout.total), _pairs(world), t)
+    for c in range(world):
+        got = torch.load(tmp_path / f"s{c}.pt", weights_only=True)
+        assert torch.equal(got["out"].view(torch.int32), want[c].view(torch.int32)), c
+        assert torch.equal(got["dots"], wdots)
