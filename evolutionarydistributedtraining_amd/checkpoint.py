@@ -20,6 +20,7 @@ import threading
 import torch
 
 from .params import ParamLayout
+from .tracing import traced
 
 _ST_DTYPES = {"F32": torch.float32, "BF16": torch.bfloat16, "F16": torch.float16, "F64": torch.float64,
               "I64": torch.int64, "I32": torch.int32, "I16": torch.int16, "I8": torch.int8, "U8": torch.uint8,
@@ -182,6 +183,7 @@ def read_into_arena(model_dir: str, layout: ParamLayout, flat: torch.Tensor,
     return flat
 
 
+@traced("edt/checkpoint.read_many")
 def read_many(items, layout: ParamLayout, names: list[str] | None = None, threads: int = 8,
               staging_bytes: int = 64 << 20) -> None:
     """read_into_arena for several (model_dir, flat) pairs at once — the K worker checkpoints of
@@ -251,6 +253,7 @@ def write_from_arena(path: str, layout: ParamLayout, flat: torch.Tensor, names: 
     _write_file(path, _header_bytes(layout, names or layout.names, flat.dtype, metadata), _host_copy(flat))
 
 
+@traced("edt/checkpoint.save_to_dirs")
 def save_to_dirs(dirs: list[str], layout: ParamLayout, flat: torch.Tensor, names=None) -> None:
     """The broadcast edge (EDT_LM/diloco.py:302-308): the new global model to every worker dir —
     one device->host copy, then the K files written by a thread pool (as the reference's

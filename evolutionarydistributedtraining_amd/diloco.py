@@ -21,6 +21,7 @@ import torch
 from . import ops
 from ._lib import EDT_MAX_WORKERS as L_MAX, EdtError
 from .params import ParamArena, ParamLayout, flat_view, pack, unpack_
+from .tracing import traced
 
 DILOCO_DEFAULTS = dict(lr=0.7, momentum=0.9, nesterov=True)        # EDT_LM/diloco.py:253-255
 
@@ -183,6 +184,7 @@ class OuterSync:
         self.lr, self.momentum, self.nesterov = lr, momentum, nesterov
         self.state = state or OuterState()
 
+    @traced("edt/OuterSync.step")
     def step(self, broadcast: bool = False) -> None:
         """One outer step. broadcast=True also starts every worker from the new global weights
         (EDT_LM/diloco.py:302-308) in the same pass: each worker arena is overwritten with theta
@@ -266,6 +268,7 @@ class DirOuterSync:
         dt = _ST_DTYPES[metas[names[0]][1]["dtype"]]
         return ParamLayout([tuple(metas[n][1]["shape"]) for n in names], names), dt
 
+    @traced("edt/DirOuterSync.step")
     def step(self, base_dir: str, worker_dirs: list[str], out_dirs: list[str] | None = None) -> OuterState:
         import shutil
         from .checkpoint import read_many, save_to_dirs

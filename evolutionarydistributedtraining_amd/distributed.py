@@ -38,6 +38,7 @@ from . import ops as _ops
 from .collectives import Collectives, TorchCollectives
 from .diloco import check_sgd_hparams
 from .params import ParamArena, ParamLayout
+from .tracing import trange, traced
 
 
 class ShardedOuterSync:
@@ -123,8 +124,13 @@ class ShardedOuterSync:
             return shard * (self.k_total * wb + 2 * gb + mom)
         return self.n_pad * (self.k_local * wb + gb + 4) + shard * (4 + 2 * gb + mom)
 
+    @traced("edt/ShardedOuterSync.step")
     def step(self) -> None:
         """One outer step; returns when the work is enqueued (stream-ordered, async)."""
+        with trange(f"edt/sharded.{self.mode}/{self.broadcast}"):
+            self._step_body()
+
+    def _step_body(self) -> None:
         k = self.kernels
         mom_off = 0
         gathers = []
@@ -286,6 +292,7 @@ class PopulationCrossover:
         par2 = payload(j, self.rank) if j == self.rank else got[j]
         return par1, par2
 
+    @traced("edt/PopulationCrossover.slerp_step")
     def slerp_step(self, member: torch.Tensor, pairs, t: torch.Tensor, out: torch.Tensor,
                    dot_threshold: float = 0.9995, eps: float = 1e-8) -> None:
         """SLERP child of pairs[rank] into `out` (EDT_RL/crossover.py:84-135 per Policy/Value;
@@ -428,6 +435,7 @@ class ShardedPopulationCrossover:
                 ops_.extend(("recv", out[st:en], j) for out in outs)
         self.comm.p2p(ops_)
 
+    @traced("edt/ShardedPopulationCrossover.slerp_step")
     def slerp_step(self, member: torch.Tensor, pairs, t: torch.Tensor, out: torch.Tensor,
                    dot_threshold: float = 0.9995, eps: float = 1e-8) -> torch.Tensor:
         """Child pairs[rank] into `out`; returns the per-segment dots of every child [N, nseg]."""

@@ -39,6 +39,7 @@ from . import schedule
 from ._lib import EdtError
 from .merge import uniform_dna_crossover
 from .params import ParamLayout
+from .tracing import traced
 
 
 class ResidentPopulation:
@@ -162,6 +163,7 @@ class ResidentPopulation:
             return obj
         return self.comm.broadcast_object(obj, src=0)
 
+    @traced("edt/ResidentPopulation.select")
     def select(self, fitness: list[float], method: str | None = None, scale: float | None = None):
         """Parent pairs (member indices) for the next generation, chosen on rank 0.
 
@@ -270,6 +272,7 @@ class ResidentPopulation:
         self.comm.p2p(p2p)
         return got
 
+    @traced("edt/ResidentPopulation.crossover")
     def crossover(self, pairs, child_hook=None) -> None:
         """Build child c of pairs[c] = (i, j) on member c's rank, for every c, then make the
         children the population (generation + 1). child_hook(c, genome), on rank 0 right after

@@ -299,3 +299,16 @@ def test_abi_error_convention_without_device():
     # edt_lerp (crossover.py:50-51): fp32 inputs computed in bf16 is not a reference combination
     err(lib.edt_lerp(p[1], p[2], F32, p[3], F32, BF16, 8, 0.5, None), "bf16 compute of fp32")
     err(lib.edt_lerp(p[1], None, BF16, p[3], BF16, BF16, 8, 0.5, None), "null buffer")
+
+
+def test_host_code_under_asan_and_ubsan():
+    """tests/asan: the CPU oracle and the host logic of libedt_sync / libedt_comm (argument
+    validation, chunk and tensor tables, overlap checks, the comm error paths) built with
+    -fsanitize=address,undefined (host side only) and exercised without a GPU; any report fails."""
+    import subprocess
+    d = os.path.join(ROOT, "tests", "asan")
+    subprocess.run(["make", "-s", "-C", d], check=True, timeout=900)
+    p = subprocess.run([os.path.join(d, "_build", "host_checks")], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1",
+                                UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1"))
+    assert p.returncode == 0 and "host checks ok" in p.stdout, p.stderr[-3000:]
