@@ -148,61 +148,61 @@ def synth_population(theta: torch.Tensor, workers: list[torch.Tensor], seed: int
 
 
 def cpu_baseline(args, theta_dtype, worker_dtype, k):
-    """The CPU oracle (the reference's op sequence restated in C, OpenMP) on a bounded sample."""
+    """The reference's outer step as it runs on its master's CPU — EDT_LM/diloco.py:238-289's
+    per-tensor torch loop + torch.optim.SGD, restated in oracle.torch_loop_outer_step — over one
+    whole transformer block of the bench layout (every tensor shape the step meets), timed on this
+    host's cores: `value`. Beside it (`c_port`) the same op sequence as the OpenMP C oracle."""
     from oracle import oracle
+    out = reference_loop_baseline(args, theta_dtype, worker_dtype, k)
     n = args.cpu_sample_elems
     g = torch.Generator().manual_seed(1)
     theta = (torch.randn(n, generator=g) * 0.02).to(theta_dtype)
     workers = [(theta.float() + torch.randn(n, generator=g) * 1e-3).to(worker_dtype) for _ in range(k)]
     mom = torch.zeros(n, dtype=theta_dtype)
     oracle.outer_step(theta, workers, mom, False, args.lr, args.momentum, bool(args.nesterov))
-    times = []
-    t_end = time.perf_counter() + args.cpu_baseline_seconds
-    while time.perf_counter() < t_end or len(times) < 2:
-        t0 = time.perf_counter()
-        oracle.outer_step(theta, workers, mom, True, args.lr, args.momentum, bool(args.nesterov))
-        times.append(time.perf_counter() - t0)
-    times.sort()
-    t = times[len(times) // 2]
+    t, reps = _median_time(lambda: oracle.outer_step(theta, workers, mom, True, args.lr, args.momentum,
+                                                     bool(args.nesterov)), args.cpu_baseline_seconds / 2)
     gbps = k * n * torch.finfo(worker_dtype).bits / 8 / t / 1e9
-    out = {"value": round(gbps, 3), "unit": "GB/s", "cores": oracle.max_threads(), "kind": "port",
-           "sample": f"{n} elements x {k} workers (fused delta+mean+SGD, oracle/edt_oracle.c, "
-                     f"median of {len(times)} reps over {args.cpu_baseline_seconds:.0f}s)"}
-    del theta, workers, mom
-    out["reference_loop"] = reference_loop_baseline(args, theta_dtype, worker_dtype, k)
+    out["c_port"] = {"value": round(gbps, 3), "unit": "GB/s", "cores": oracle.max_threads(), "kind": "port",
+                     "sample": f"{n} elements x {k} workers (fused delta+mean+SGD, oracle/edt_oracle.c, "
+                               f"median of {reps} reps)"}
     return out
 
 
+def _block_sample(layout, budget):
+    """The tensors of the layout's first transformer block (names with '.0.'), else the first
+    tensors in order within the budget: a sample with every shape of the step."""
+    idx = [i for i, nm in enumerate(layout.names or []) if ".0." in nm]
+    if not idx or sum(layout.numels[i] for i in idx) > budget:
+        idx, tot = [], 0
+        for i, m in enumerate(layout.numels):
+            if tot + m <= budget:
+                idx.append(i)
+                tot += m
+    return [layout.shapes[i] for i in idx], [layout.names[i] if layout.names else str(i) for i in idx]
+
+
 def reference_loop_baseline(args, theta_dtype, worker_dtype, k):
-    """The reference's outer step as it runs on its master's CPU (per-tensor torch ops + SGD,
-    restated in oracle.torch_loop_outer_step) over the first tensors of the bench layout, up to
-    the same element budget: the cost the fused kernel replaces, next to the C port above."""
     from evolutionarydistributedtraining_amd.layouts import LAYOUTS
     from oracle import oracle
-    shapes, total = [], 0
-    for shp in LAYOUTS[args.layout]().shapes:         # in order, skipping what would overflow
-        m = int(torch.Size(shp).numel())
-        if total + m <= args.cpu_sample_elems:
-            shapes.append(shp)
-            total += m
+    lay = LAYOUTS[args.layout]()
+    shapes, names = _block_sample(lay, 4 * args.cpu_sample_elems)
+    total = sum(int(torch.Size(s).numel()) for s in shapes)
     g = torch.Generator().manual_seed(2)
     base = [(torch.randn(shp, generator=g) * 0.02).to(theta_dtype) for shp in shapes]
     workers = [[(p.float() + torch.randn(p.shape, generator=g) * 1e-3).to(worker_dtype) for p in base]
                for _ in range(k)]
-    opt = oracle.torch_loop_outer_step(base, workers, None, args.lr, args.momentum, bool(args.nesterov))
-    times = []
-    t_end = time.perf_counter() + args.cpu_baseline_seconds / 2
-    while time.perf_counter() < t_end or len(times) < 2:
-        t0 = time.perf_counter()
-        opt = oracle.torch_loop_outer_step(base, workers, opt, args.lr, args.momentum, bool(args.nesterov))
-        times.append(time.perf_counter() - t0)
-    times.sort()
-    t = times[len(times) // 2]
+    state = {"opt": oracle.torch_loop_outer_step(base, workers, None, args.lr, args.momentum, bool(args.nesterov))}
+
+    def rep():
+        state["opt"] = oracle.torch_loop_outer_step(base, workers, state["opt"], args.lr, args.momentum,
+                                                    bool(args.nesterov))
+    t, reps = _median_time(rep, args.cpu_baseline_seconds / 2)
     return {"value": round(k * total * torch.finfo(worker_dtype).bits / 8 / t / 1e9, 3), "unit": "GB/s",
-            "threads": torch.get_num_threads(),
-            "sample": f"{len(shapes)} tensors of {args.layout} in order ({total} elements) x {k} workers, "
-                      f"EDT_LM/diloco.py:238-289's per-tensor torch loop + torch.optim.SGD "
-                      f"(oracle.torch_loop_outer_step), median of {len(times)} reps"}
+            "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"{len(shapes)} tensors of {args.layout} ({names[0]} .. {names[-1]}, {total} elements) x {k} "
+                      f"workers, EDT_LM/diloco.py:238-289's per-tensor torch loop + torch.optim.SGD "
+                      f"(oracle.torch_loop_outer_step), median of {reps} reps"}
 
 
 def _median_time(fn, seconds):

@@ -130,7 +130,10 @@ inline unsigned slerp_spec_grid(int64_t nchunks) {
 // blend passes: tile q of chunk c is workgroup c * kTilesPerChunk + q, so the grid walks the arena
 // in address order one kTile at a time (chunks longer than kTilesPerChunk tiles loop)
 constexpr int kTile = kBlock * kVec;                 // 2,048 elements
-constexpr int kTilesPerChunk = 32;                   // the plans' default chunk: 64 Ki elements
+#ifndef EDT_SLERP_TPC
+#define EDT_SLERP_TPC 32
+#endif
+constexpr int kTilesPerChunk = EDT_SLERP_TPC;        // the plans' default chunk: 64 Ki elements
 inline unsigned slerp_tile_grid(int64_t nchunks) {
     if (!EDT_SLERP_GRID) return slerp_grid(nchunks);
     const uint64_t g = (uint64_t)nchunks * kTilesPerChunk;

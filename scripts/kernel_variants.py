@@ -110,7 +110,11 @@ VARIANTS.update({f"li{i}": [f"-DEDT_LIST_ITERS={i}"] for i in (1, 2, 4, 8, 16)})
 VARIANTS.update({"s_grid0": ["-DEDT_SLERP_GRID=0"], "s_grid1": ["-DEDT_SLERP_GRID=1"],
                  "s_grid1_nt0": ["-DEDT_SLERP_GRID=1", "-DEDT_NT_SLERP=0"],
                  "s_spec64": ["-DEDT_SLERP_SPEC_BPC=64"], "s_spec1024": ["-DEDT_SLERP_SPEC_BPC=1024"],
-                 "s_spec16": ["-DEDT_SLERP_SPEC_BPC=16"], "s_gram1": ["-DEDT_SLERP_GRAM_GRID=1"]})
+                 "s_spec16": ["-DEDT_SLERP_SPEC_BPC=16"], "s_gram1": ["-DEDT_SLERP_GRAM_GRID=1"],
+                 "s_tile2k": ["-DEDT_SLERP_TPC=1", "-DEDT_SLERP_SPEC_BPC=1048576"],
+                 "s_tile4k": ["-DEDT_SLERP_TPC=2", "-DEDT_SLERP_SPEC_BPC=1048576"],
+                 "s_tile8k": ["-DEDT_SLERP_TPC=4", "-DEDT_SLERP_SPEC_BPC=1048576"],
+                 "s_tile16k": ["-DEDT_SLERP_TPC=8", "-DEDT_SLERP_SPEC_BPC=1048576"]})
 
 
 def run_list(names, rounds, iters, wdt="bf16"):
@@ -200,7 +204,7 @@ def run_slerp(names, rounds, layout_name):
         v2[s0:e] = (x + torch.randn(e - s0, device=dev) * 1e-4).to(bf)
         del x
     out = torch.empty(P, dtype=bf, device=dev)
-    plan = ops.make_slerp_plan(lay.offsets, dev, chunk_elems=1 << 16)
+    plan = ops.make_slerp_plan(lay.offsets, dev, chunk_elems=int(os.environ.get("EDT_VARIANT_CHUNK", 1 << 16)))
     redo = torch.zeros(plan.nseg, dtype=torch.int32, device=dev)
     t = torch.full((len(lay),), 0.5, dtype=torch.float64, device=dev)
     stream = L.stream_ptr(dev)
