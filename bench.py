@@ -232,6 +232,15 @@ def _event_ms(fn, steps, warmup):
     return sum(ts) / len(ts)
 
 
+def _pmc_traffic(args, key):
+    """HBM bytes per launch from the committed PMC summary (scripts/profile_pmc_ops.sh), or None."""
+    try:
+        with open(args.traffic_json) as f:
+            return json.load(f).get(key, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
 def bench_pair_merge(args, dev):
     """EDT-LM child (EDT_LM/train/crossover.py:150-237: lerp(.5) of the bases, mean of the two
     pseudo-gradients, Nesterov SGD with the carried momentum) over the 1.3B layout, bf16 parents,
@@ -257,7 +266,8 @@ def bench_pair_merge(args, dev):
     res = {"workload": f"EDT-LM pair merge, gpt_1p3b P={P}, bf16 parents/child/momentum, lr 0.7 mu 0.9 nesterov",
            "kernel": "pair_kernel (edt_pair_merge_to)", "ms": round(ms, 4),
            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                        "frac": round(gbs / HBM_PEAK_GBPS, 4), "bytes_per_elem": bpe, "algo_bytes_per_launch": bpe * P}}
+                        "frac": round(gbs / HBM_PEAK_GBPS, 4), "bytes_per_elem": bpe, "algo_bytes_per_launch": bpe * P,
+                        "traffic": _pmc_traffic(args, "pair_merge/gpt_1p3b/bf16")}}
     if args.ops_cpu_seconds > 0:
         n = args.cpu_sample_elems
         gc = torch.Generator().manual_seed(3)
@@ -311,7 +321,8 @@ def bench_slerp_7b(args, dev):
                         "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBPS,
                                      "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBPS, 4), "bytes_per_elem": 6,
                                      "algo_bytes_per_launch": 6 * P,
-                                     "moved_bytes_per_elem": 6 if spec else 10}}
+                                     "moved_bytes_per_elem": 6 if spec else 10,
+                                     "traffic": _pmc_traffic(args, f"slerp_7b/{parents}")}}
     del v0, v1, out, plan
     torch.cuda.empty_cache()
     if args.ops_cpu_seconds > 0:
