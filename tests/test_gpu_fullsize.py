@@ -173,3 +173,83 @@ def test_cross_stream_ordering(dev):
         ops.outer_step(th, dst, None, False, 1.0, 0.0, False)
     torch.cuda.synchronize()
     assert torch.equal(bits(th.cpu()), bits(ref_t.cpu()))
+
+
+def test_sharded_schedule_1p3b_virtual_world8(dev):
+    """BASELINE's "1.3B, 8 workers over 8 GPUs" schedule at full size on one GPU: 8 virtual ranks
+    (collectives.VirtualWorld), one bf16 worker each, fp32 master, exact/workers (what `auto` picks
+    at N = 8) over 64 Mi-element buckets, two steps: the gathered master, the momentum and every
+    rank's worker (the new theta rounded to bf16) bit-exact with the single-GPU fused step over the
+    whole population."""
+    from evolutionarydistributedtraining_amd import ops
+    from evolutionarydistributedtraining_amd.collectives import VirtualWorld
+    from evolutionarydistributedtraining_amd.distributed import ShardedOuterSync
+    from evolutionarydistributedtraining_amd.layouts import gpt_1p3b
+    lay = gpt_1p3b()
+    P, N = lay.total, 8
+    gen = torch.Generator(device=dev).manual_seed(12)
+    theta0 = torch.randn(P, device=dev, generator=gen) * 0.02
+    gens = [[(theta0 + torch.randn(P, device=dev, generator=gen) * 1e-3 * (s + 1)).bfloat16() for _ in range(N)]
+            for s in range(2)]
+    th, mom = theta0.clone(), torch.zeros(P, device=dev)
+    for i, ws in enumerate(gens):
+        ops.outer_step(th, ws, mom, i > 0, 0.7, 0.9, True)
+    want_w = th.bfloat16()
+
+    def body(comm):
+        s = ShardedOuterSync(lay, torch.float32, torch.bfloat16, 1, dev, comm=comm)
+        assert (s.mode, s.broadcast) == ("exact", "workers")
+        s.theta.flat.copy_(theta0)
+        for ws in gens:
+            s.workers[0].flat.copy_(ws[comm.rank])
+            s.step()
+        ok_w = bool(torch.equal(s.workers[0].flat.view(torch.int16), want_w.view(torch.int16)))
+        full = s.gather_theta()
+        ok_t = bool(torch.equal(full.view(torch.int32), th.view(torch.int32)))
+        # the rank's momentum shards against the fused step's buffer, bucket by bucket
+        off, ok_m = 0, True
+        for b, e in s.buckets:
+            s0, s1 = s._shard(b, e)
+            m = s.mom_shard[off:off + (s1 - s0)]
+            hi = min(s1, P)
+            if hi > s0:
+                ok_m &= bool(torch.equal(m[:hi - s0].view(torch.int32), mom[s0:hi].view(torch.int32)))
+            off += s1 - s0
+        torch.cuda.synchronize()
+        return ok_t, ok_m, ok_w
+
+    res = VirtualWorld(N, timeout=600).run(body)
+    assert all(all(r) for r in res), res
+
+
+def test_sharded_population_1p3b_virtual_world8(dev):
+    """BASELINE configs[4]'s link-balanced population at 1.3B on one GPU: 8 virtual ranks, 8 bf16
+    members, every child bit-identical to edt_slerp_merge on its two parents."""
+    from evolutionarydistributedtraining_amd import ops
+    from evolutionarydistributedtraining_amd.collectives import VirtualWorld
+    from evolutionarydistributedtraining_amd.distributed import ShardedPopulationCrossover
+    from evolutionarydistributedtraining_amd.layouts import gpt_1p3b
+    lay = gpt_1p3b()
+    P, N = lay.total, 8
+    gen = torch.Generator(device=dev).manual_seed(13)
+    base = torch.randn(P, device=dev, generator=gen) * 0.02
+    members = [(base + torch.randn(P, device=dev, generator=gen) * 0.02 * (0.005 if m % 2 else 0.05)).bfloat16()
+               for m in range(N)]
+    del base
+    pairs = [((3 * c + 1) % N, (5 * c + 2) % N) for c in range(N)]
+    t = torch.full((len(lay),), 0.5, dtype=torch.float64, device=dev)
+
+    def body(comm):
+        sp = ShardedPopulationCrossover(lay, torch.bfloat16, dev, comm=comm)
+        out = torch.empty(P, dtype=torch.bfloat16, device=dev)
+        sp.slerp_step(members[comm.rank], pairs, t, out)
+        torch.cuda.synchronize()
+        return out
+
+    res = VirtualWorld(N, timeout=600).run(body)
+    plan = ops.make_slerp_plan(lay.offsets, dev)
+    want = torch.empty(P, dtype=torch.bfloat16, device=dev)
+    for c, (i, j) in enumerate(pairs):
+        ops.slerp_arena(plan, members[i], members[j], want, t, speculate=False)
+        torch.cuda.synchronize()
+        assert torch.equal(res[c].view(torch.int16), want.view(torch.int16)), c
