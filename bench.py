@@ -89,9 +89,9 @@ def parse():
                         "timing the step's access pattern on each, once before the timed steps (placement.py); "
                         "1 keeps the first allocation")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
-    p.add_argument("--ops", default="pair_merge,slerp_7b",
-                   help="N=1: the other hot-path kernels measured after the outer step, in the same line "
-                        "('none': skip)")
+    p.add_argument("--ops", default="pair_merge,slerp_7b,population_7b",
+                   help="the other hot-path measurements in the same line ('none': skip): N=1 pair_merge, "
+                        "slerp_7b; N>1 population_7b (BASELINE configs[4] across the N GPUs)")
     p.add_argument("--ops-cpu-seconds", type=float, default=4.0, help="CPU baseline budget per extra op")
     p.add_argument("--bcast-compare", type=int, default=1,
                    help="N=1: also time the step fused with the worker broadcast against step + K copies")
@@ -345,6 +345,55 @@ def bench_slerp_7b(args, dev):
     return res
 
 
+def bench_population(args, dev, comm, layout_name="qwen2p5_7b_body"):
+    """BASELINE configs[4] at N > 1: a population of N members (one 7.07B bf16 body per GPU,
+    qwen2p5_7b_body) SLERP-crossed into N children (t = 0.5, far parents: the SLERP branch), timed
+    link-balanced (distributed.ShardedPopulationCrossover: chunk-range shards of every member,
+    Gram rows all-gathered, children gathered back) and per child (PopulationCrossover: each
+    child's two parents shipped whole). Max over ranks; every rank of `comm` takes part."""
+    from evolutionarydistributedtraining_amd.distributed import PopulationCrossover, ShardedPopulationCrossover
+    from evolutionarydistributedtraining_amd.layouts import LAYOUTS
+    lay = LAYOUTS[layout_name]()
+    rank, world = comm.rank, comm.world
+    P, bf = lay.total, torch.bfloat16
+    g = torch.Generator(device=dev).manual_seed(100 + rank)
+    member = torch.empty(P, dtype=bf, device=dev)
+    for s0 in range(0, P, 1 << 28):
+        e = min(P, s0 + (1 << 28))
+        member[s0:e] = (torch.randn(e - s0, generator=g, device=dev) * 0.02).to(bf)
+    out = torch.empty(P, dtype=bf, device=dev)
+    t = torch.full((len(lay),), 0.5, dtype=torch.float64, device=dev)
+    pairs = [((3 * c + 1) % world, (5 * c + 2) % world) for c in range(world)]
+    res = {"workload": f"SLERP population of {world} x {layout_name} (P={P}, bf16), one member per GPU",
+           "pairs": pairs}
+
+    def timed(step, n):
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize()
+        comm.barrier()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            step()
+        torch.cuda.synchronize()
+        comm.barrier()
+        return max(comm.all_gather_object((time.perf_counter() - t0) / n * 1e3))
+    sp = ShardedPopulationCrossover(lay, bf, dev, kind="slerp", comm=comm)
+    ms = timed(lambda: sp.slerp_step(member, pairs, t, out), max(3, args.steps // 4))
+    wire = 2 * (world - 1) * (P * 2 // world)            # members out + children out, per rank
+    peak = XGMI_LINK_GBPS * (world - 1)
+    res["sharded"] = {"ms": round(ms, 3), "wire_bytes_per_rank": wire,
+                      "xgmi": {"achieved": round(wire / (ms / 1e3) / 1e9, 1), "peak": peak, "unit": "GB/s",
+                               "frac": round(wire / (ms / 1e3) / 1e9 / peak, 4)}}
+    del sp
+    torch.cuda.empty_cache()
+    pc = PopulationCrossover(lay, bf, dev, comm=comm)
+    res["per_child"] = {"ms": round(timed(lambda: pc.slerp_step(member, pairs, t, out), 3), 3)}
+    del pc, member, out
+    torch.cuda.empty_cache()
+    return res
+
+
 def stream_ceiling_ms(theta, workers, momentum, iters=10):
     """Median HIP-event time of edt_probe_stream over the step's own operands (None if the
     step runs without momentum: the probe always reads and writes a momentum stream)."""
@@ -527,6 +576,17 @@ def main():
             weak = {"error": f"OutOfMemoryError: {str(e)[:200]}"}
             torch.cuda.empty_cache()
         sync = None
+    population = None
+    if sharded and world > 1 and "population_7b" in args.ops:
+        # configs[4] on the same node, after the DiLoCo measurements (every rank takes part)
+        sync = step = None
+        torch.cuda.empty_cache()
+        try:
+            from evolutionarydistributedtraining_amd.collectives import TorchCollectives
+            population = bench_population(args, dev, TorchCollectives())
+        except torch.cuda.OutOfMemoryError as e:
+            population = {"error": f"OutOfMemoryError: {str(e)[:200]}"}
+            torch.cuda.empty_cache()
 
     if rank == 0:
         bg = torch.finfo(tdt).bits // 8
@@ -585,6 +645,8 @@ def main():
             out["roofline"] = roofline
         if weak:
             out["weak_scaling"] = weak
+        if population:
+            out["population_slerp_7b"] = population
         if not sharded:   # what a plain device-to-device copy reaches on this device, same process
             src = torch.empty(1 << 29, dtype=torch.float32, device=dev)
             dst = torch.empty_like(src)

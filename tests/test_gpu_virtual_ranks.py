@@ -176,3 +176,17 @@ def test_sharded_population_pair_merge_on_virtual_ranks(world):
         torch.cuda.synchronize()
         assert torch.equal(bits(res[c][0]), bits(out)), c
         assert torch.equal(bits(res[c][1]), bits(m_out)), c
+
+
+def test_bench_population_measurement_on_virtual_ranks():
+    """bench.py's N > 1 configs[4] measurement (bench_population) runs its schedule end to end
+    through a communicator: here 4 virtual ranks on the 125M layout (the driver's 8-GPU run uses
+    RCCL and the 7B body)."""
+    import types
+
+    import bench
+    args = types.SimpleNamespace(steps=4)
+    res = VirtualWorld(4).run(lambda comm: bench.bench_population(args, DEV, comm, "gpt2_small"))
+    for r in res:
+        assert r["sharded"]["ms"] > 0 and r["per_child"]["ms"] > 0
+        assert r["sharded"]["wire_bytes_per_rank"] == 2 * 3 * (124439808 * 2 // 4)
