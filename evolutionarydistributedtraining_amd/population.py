@@ -57,7 +57,7 @@ class ResidentPopulation:
                  lr: float = 0.7, momentum: float = 0.9, nesterov: bool = True,
                  dot_threshold: float = 0.9995, eps: float = 1e-8, elitism: int = 0,
                  group=None, kernels=None, keep_previous: bool = False, slerp_chunk: int | None = None,
-                 comm=None):
+                 comm=None, exchange: str = "per_child"):
         if kind not in ("sgd", "slerp"):
             raise ValueError(kind)
         if kind == "sgd":
@@ -81,6 +81,15 @@ class ResidentPopulation:
         if self.P == 0 or self.P % self.world:
             raise EdtError(f"population {self.P} does not split over {self.world} ranks")
         self.M = self.P // self.world
+        # exchange="sharded": one member per rank, the generation's data path link-balanced
+        # (distributed.ShardedPopulationCrossover: chunk-range shards of every member, children
+        # gathered back) instead of shipping each child's two parents whole
+        if exchange not in ("per_child", "sharded"):
+            raise ValueError(exchange)
+        if exchange == "sharded" and (self.M != 1 or keep_previous or comm is None):
+            raise EdtError("exchange='sharded' needs one member per rank, a communicator, no keep_previous")
+        self.exchange = exchange
+        self._sharded = None
         self.lr, self.momentum, self.nesterov = lr, momentum, nesterov
         self.dot_threshold, self.eps = dot_threshold, eps
         self.elitism = elitism
@@ -283,11 +292,14 @@ class ResidentPopulation:
         if len(pairs) != self.P:
             raise EdtError(f"{len(pairs)} pairs for a population of {self.P}")
         donors = self._donors(pairs) if self.kind == "sgd" else [None] * self.P
-        got = self._exchange(pairs, donors)
-        if self.kind == "slerp":
-            self._slerp_children(pairs, got)
+        if self.exchange == "sharded":
+            self._sharded_children(pairs)
         else:
-            self._sgd_children(pairs, got, donors)
+            got = self._exchange(pairs, donors)
+            if self.kind == "slerp":
+                self._slerp_children(pairs, got)
+            else:
+                self._sgd_children(pairs, got, donors)
         # every transfer and merge of this generation is enqueued/complete: swap the children in
         # (keep_previous: the current generation becomes the previous one, whose arenas are
         # recycled for the next children)
@@ -359,6 +371,23 @@ class ResidentPopulation:
             i, j = pairs[c]
             k.slerp_arena(self._plan, got[i][0], got[j][0], self._child[self._local(c)], self._t,
                           self.dot_threshold, self.eps)
+
+    def _sharded_children(self, pairs):
+        """This rank's child through the link-balanced schedule (bit-identical to the per-child
+        kernels)."""
+        from .distributed import ShardedPopulationCrossover
+        if self._sharded is None:
+            self._sharded = ShardedPopulationCrossover(self.layout, self.dtype, self.device, kind=self.kind,
+                                                       comm=self.comm, kernels=self.kernels,
+                                                       chunk_elems=self.slerp_chunk or (1 << 16))
+        m = self.rank
+        if self.kind == "slerp":
+            self._sharded.slerp_step(self._params[0], pairs, self._t, self._child[0], self.dot_threshold, self.eps)
+            return
+        has = self.has_momentum[m] and self.momentum != 0
+        self._sharded.pair_merge_step(self._base[0], self._trained[0], self._mom[0] if has else None, pairs,
+                                      self._child[0], self._child_mom[0], self.lr, self.momentum, self.nesterov,
+                                      has_momentum=has, generation=self.generation)
 
     def _pool_genome(self, m):
         """Genome of member m as the master sees it at selection time: current members with this

@@ -57,7 +57,7 @@ def _scale(gen):
     return roulette_scale(gen + 1, 10)
 
 
-def run_resident(kind, device, kernels=None, comm=None):
+def run_resident(kind, device, kernels=None, comm=None, exchange="per_child"):
     """The resident population over GENS generations; returns this rank's members. comm: a
     collectives.Collectives (virtual ranks); the host RNGs are seeded by rank 0 only (they are
     process-global, and only rank 0 draws)."""
@@ -69,7 +69,8 @@ def run_resident(kind, device, kernels=None, comm=None):
         random.seed(7)
         np.random.seed(7)
     pop = ResidentPopulation(layout, dt, device, _genomes(kind), kind=kind, elitism=1 if kind == "sgd" else 0,
-                             seg_t=SEG_T if kind == "slerp" else None, kernels=kernels, comm=comm)
+                             seg_t=SEG_T if kind == "slerp" else None, kernels=kernels, comm=comm,
+                             exchange=exchange)
     for m in pop.local_members():
         (pop.base(m) if kind == "sgd" else pop.params(m)).copy_(_init(m, n, dt))
     for gen in range(GENS):
@@ -242,6 +243,27 @@ def test_resident_virtual_ranks_match_reference_flow(oracle, kind, world):
     from tests.oracle_kernels import OracleKernels
     res = VirtualWorld(world).run(lambda comm: run_resident(kind, "cpu", OracleKernels(oracle), comm=comm))
     _check_world(res, world, kind, oracle)
+
+
+def test_resident_sharded_exchange_virtual_ranks(oracle):
+    """exchange="sharded" (one member per rank, link-balanced) on 4 virtual ranks, EDT-LM: the
+    same members, momenta and genomes as the reference flow, bit for bit."""
+    from evolutionarydistributedtraining_amd.collectives import VirtualWorld
+    from tests.oracle_kernels import ChunkGramKernels
+    res = VirtualWorld(POP).run(lambda comm: run_resident("sgd", "cpu", ChunkGramKernels(oracle), comm=comm,
+                                                          exchange="sharded"))
+    _check_world(res, POP, "sgd", oracle)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["sgd", "slerp"])
+def test_resident_gpu_sharded_exchange(oracle, kind):
+    """exchange="sharded" with the HIP kernels on 4 virtual ranks: EDT-LM bit-exact, SLERP within
+    the SLERP bar of the reference flow."""
+    from evolutionarydistributedtraining_amd.collectives import VirtualWorld
+    dev = torch.device("cuda:0")
+    res = VirtualWorld(POP).run(lambda comm: run_resident(kind, dev, comm=comm, exchange="sharded"))
+    _check_world(res, POP, kind, oracle, slerp_tol=1e-5)
 
 
 @pytest.mark.gpu
