@@ -30,6 +30,8 @@ SIGNATURES = [
     ("edt_outer_step", _I, [_P, _I, ctypes.POINTER(_P), _I, _I, _P, _I, _U64, _D, _D, _I, _P]),
     ("edt_outer_step_bcast", _I, [_P, _I, ctypes.POINTER(_P), _I, _I, _P, _I, _U64, _D, _D, _I,
                                   ctypes.POINTER(_P), _I, _P]),
+    ("edt_outer_step_tail", _I, [_P, _I, ctypes.POINTER(_P), _I, _I, _P, _I, _U64, _D, _D, _I, _P, _P]),
+    ("edt_pair_merge_tail", _I, [_P, _P, _P, _P, _I, _P, _I, _P, _P, _I, _U64, _D, _D, _I, _P, _P]),
     ("edt_outer_step_ws", _I, [_P, _I, ctypes.POINTER(_P), _I, _I, _P, _I, _U64, _D, _D, _I, _P, _P]),
     ("edt_outer_list_workspace_bytes", _U64, [_I, _I]),
     ("edt_outer_step_list", _I, [ctypes.POINTER(_P), _I, ctypes.POINTER(_P), _I, _I, ctypes.POINTER(_P), _I,

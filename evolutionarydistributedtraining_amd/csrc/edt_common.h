@@ -290,6 +290,10 @@ struct SgdScalars {
     int use_momentum;  // momentum != 0
     int has_buf;       // momentum buffer carried from a previous step
     int nesterov;
+    // bf16 only, may be null: 1 bit per element (bit i & 7 of byte i >> 3, flat-arena index) set
+    // where the reference's torch CPU kernels take their scalar tail, whose add(x, y, alpha) rounds
+    // twice: round(x + round(alpha * y)) instead of one FMA (edt_outer_step_tail, edt_pair_merge_tail)
+    const uint8_t* tail;
 };
 
 inline SgdScalars make_sgd(int gdt, double lr, double mu, int has_buf, int nesterov) {
@@ -300,6 +304,7 @@ inline SgdScalars make_sgd(int gdt, double lr, double mu, int has_buf, int neste
     s.use_momentum = mu != 0.0;
     s.has_buf = has_buf;
     s.nesterov = nesterov;
+    s.tail = nullptr;
     return s;
 }
 
@@ -312,9 +317,21 @@ __device__ __forceinline__ void ld_momentum(const void* mom, uint64_t i, const S
     if (s.use_momentum && s.has_buf) ld<GDT, N, (EDT_NT_RMW != 0), H2>(mom, i, b);
 }
 
+// add(x, y, alpha) in bf16 where the tail bit is set: torch CPU's scalar form, alpha * y rounded
+// to bf16 before the add (the vectorised form is one fp32 FMA; the caller rounds the sum)
+__device__ __forceinline__ float tail_add(float x, float a, float y) {
+    float p[1] = {a * y};
+    rnd<EDT_BF16>(p);
+    return x + p[0];
+}
+
 template <int GDT, int N, int H2 = 4>
 __device__ __forceinline__ void sgd_update(float (&theta)[N], const float (&grad)[N], void* mom,
                                            uint64_t i, const SgdScalars& s, const float (&b_in)[N]) {
+    uint32_t tb = 0;                   // scalar-tail bits of elements i .. i + N - 1
+    if constexpr (GDT == EDT_BF16 && H2 == 4 && (N == 8 || N == 1)) {
+        if (s.tail) tb = N == 8 ? (uint32_t)s.tail[i >> 3] : ((uint32_t)s.tail[i >> 3] >> (i & 7)) & 1u;
+    }
     float u[N];
     if (s.use_momentum) {
         float b[N];
@@ -332,7 +349,8 @@ __device__ __forceinline__ void sgd_update(float (&theta)[N], const float (&grad
         st<GDT, N, (EDT_NT_STORES != 0), H2>(mom, i, b);
         if (s.nesterov) {
 #pragma unroll
-            for (int j = 0; j < N; ++j) u[j] = __builtin_fmaf(s.alpha_mu, b[j], grad[j]);
+            for (int j = 0; j < N; ++j)
+                u[j] = (tb >> j) & 1u ? tail_add(grad[j], s.alpha_mu, b[j]) : __builtin_fmaf(s.alpha_mu, b[j], grad[j]);
             rnd<GDT>(u);
         } else {
 #pragma unroll
@@ -343,7 +361,8 @@ __device__ __forceinline__ void sgd_update(float (&theta)[N], const float (&grad
         for (int j = 0; j < N; ++j) u[j] = grad[j];
     }
 #pragma unroll
-    for (int j = 0; j < N; ++j) theta[j] = __builtin_fmaf(s.alpha_nlr, u[j], theta[j]);
+    for (int j = 0; j < N; ++j)
+        theta[j] = (tb >> j) & 1u ? tail_add(theta[j], s.alpha_nlr, u[j]) : __builtin_fmaf(s.alpha_nlr, u[j], theta[j]);
     rnd<GDT>(theta);
 }
 

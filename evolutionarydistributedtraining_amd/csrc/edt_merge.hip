@@ -276,9 +276,22 @@ int edt_pair_merge(const void* b1, const void* b2, const void* m1, const void* m
                              momentum_coef, nesterov, stream);
 }
 
+int edt_pair_merge_tail(const void* b1, const void* b2, const void* m1, const void* m2, int wdt,
+                        void* theta_out, int gdt, const void* momentum_in, void* momentum, int has_momentum,
+                        uint64_t n, double lr, double momentum_coef, int nesterov, const uint8_t* tail_bits,
+                        void* stream);
+
 int edt_pair_merge_to(const void* b1, const void* b2, const void* m1, const void* m2, int wdt,
                       void* theta_out, int gdt, const void* momentum_in, void* momentum, int has_momentum,
                       uint64_t n, double lr, double momentum_coef, int nesterov, void* stream) {
+    return edt_pair_merge_tail(b1, b2, m1, m2, wdt, theta_out, gdt, momentum_in, momentum, has_momentum, n, lr,
+                               momentum_coef, nesterov, nullptr, stream);
+}
+
+int edt_pair_merge_tail(const void* b1, const void* b2, const void* m1, const void* m2, int wdt,
+                        void* theta_out, int gdt, const void* momentum_in, void* momentum, int has_momentum,
+                        uint64_t n, double lr, double momentum_coef, int nesterov, const uint8_t* tail_bits,
+                        void* stream) {
     g_err[0] = 0;
     if (!valid_pair(gdt, wdt)) return fail(EDT_ERR_ARG, "unsupported dtype pair (gdt/wdt)");
     if (n == 0) return EDT_OK;
@@ -287,6 +300,7 @@ int edt_pair_merge_to(const void* b1, const void* b2, const void* m1, const void
     a.b1 = b1; a.b2 = b2; a.m1 = m1; a.m2 = m2; a.out = theta_out; a.mom = momentum; a.n = n;
     a.mom_in = momentum_in;
     a.sgd = make_sgd(gdt, lr, momentum_coef, has_momentum, nesterov);
+    if (gdt == EDT_BF16) a.sgd.tail = tail_bits;    // fp32: nothing to emulate
     if (a.sgd.use_momentum && !momentum) return fail(EDT_ERR_ARG, "momentum buffer is null");
     if (a.sgd.use_momentum && has_momentum && !momentum_in) return fail(EDT_ERR_ARG, "carried momentum is null");
     const bool vec = aligned16(b1) && (!b2 || aligned16(b2)) && aligned16(m1) && aligned16(m2) &&

@@ -441,6 +441,24 @@ int edt_outer_step(void* theta_g, int gdt, const void* const* theta_k, int wdt, 
     return launch_outer<MODE_FUSED>(gdt, wdt, a, vec, (hipStream_t)stream);
 }
 
+int edt_outer_step_tail(void* theta_g, int gdt, const void* const* theta_k, int wdt, int K,
+                        void* momentum, int has_momentum, uint64_t n, double lr, double momentum_coef,
+                        int nesterov, const uint8_t* tail_bits, void* stream) {
+    g_err[0] = 0;
+    if (!valid_pair(gdt, wdt)) return fail(EDT_ERR_ARG, "unsupported dtype pair (gdt/wdt)");
+    OuterArgs a;
+    int rc = fill_outer(a, theta_g, theta_k, K, K, n);
+    if (rc) return rc;
+    a.sgd = make_sgd(gdt, lr, momentum_coef, has_momentum, nesterov);
+    if (a.sgd.use_momentum && !momentum && n) return fail(EDT_ERR_ARG, "momentum buffer is null");
+    a.mom = momentum;
+    if (gdt == EDT_BF16) a.sgd.tail = tail_bits;    // fp32: torch's tails are FMAs too, nothing to emulate
+    if (n == 0) return EDT_OK;
+    bool vec = aligned16(theta_g) && (!a.sgd.use_momentum || aligned16(momentum));
+    for (int k = 0; k < K; ++k) vec = vec && aligned16(theta_k[k]);
+    return launch_outer<MODE_FUSED>(gdt, wdt, a, vec, (hipStream_t)stream);
+}
+
 int edt_outer_step_bcast(void* theta_g, int gdt, const void* const* theta_k, int wdt, int K,
                          void* momentum, int has_momentum, uint64_t n, double lr, double momentum_coef,
                          int nesterov, void* const* bcast, int nbcast, void* stream) {

@@ -101,13 +101,29 @@ class OuterState:
         return st
 
 
+def _tail_bits(cpu_tails, numels, device):
+    """cpu_tails = (vec_elems, num_threads) of the reference's host -> the device bitmask of its
+    torch scalar-tail elements (torchcompat), or None."""
+    if cpu_tails is None:
+        return None
+    from .torchcompat import torch_cpu_tail_bits
+    vec, threads = cpu_tails
+    return torch_cpu_tail_bits(numels, vec_elems=vec, num_threads=threads, device=device)
+
+
 def _step_flat(theta: torch.Tensor, workers: list[torch.Tensor], state: OuterState, lr: float,
-               momentum: float, nesterov: bool, broadcast: list[torch.Tensor] | None = None) -> None:
+               momentum: float, nesterov: bool, broadcast: list[torch.Tensor] | None = None,
+               tail_bits: torch.Tensor | None = None) -> None:
     check_sgd_hparams(lr, momentum, nesterov)
     state.hparams = dict(lr=lr, momentum=momentum, nesterov=nesterov)
     mom = state.buffer_for(theta) if momentum != 0 else None
     has = state.has_momentum if momentum != 0 else False
-    ops.outer_step(theta, workers, mom, has, lr, momentum, nesterov, broadcast)
+    if tail_bits is not None and broadcast:              # the tail form has no fused broadcast
+        ops.outer_step(theta, workers, mom, has, lr, momentum, nesterov, tail_bits=tail_bits)
+        for b in broadcast:
+            b.copy_(theta)
+    else:
+        ops.outer_step(theta, workers, mom, has, lr, momentum, nesterov, broadcast, tail_bits=tail_bits)
     if momentum != 0:
         state.has_momentum = True
     state.steps += 1
@@ -129,7 +145,7 @@ def _step_list(thetas: list[torch.Tensor], workers: list[list[torch.Tensor]], st
 
 
 def outer_step(base_params, worker_params, state: OuterState | None = None, lr: float = 0.7,
-               momentum: float = 0.9, nesterov: bool = True) -> OuterState:
+               momentum: float = 0.9, nesterov: bool = True, cpu_tails: tuple[int, int] | None = None) -> OuterState:
     """Drop-in for EDT_LM/diloco.py:238-289 on device-resident parameters.
 
     base_params:   list of the global model's parameters (`list(base_model.parameters())`),
@@ -139,6 +155,9 @@ def outer_step(base_params, worker_params, state: OuterState | None = None, lr: 
     One launch either way: over the flat arenas when each list is a run of views of one arena
     (`params.arena_of_module`), else over the tensor lists themselves (`ops.outer_step_list`,
     no packing). Only populations above 64 workers with separate tensors are packed first.
+    cpu_tails = (Vec::size(), torch threads) of the reference's master, e.g. (32, 8): bf16 results
+    bit-exact with the reference run there, torch's scalar tails included (torchcompat; flat form,
+    separate tensors are packed).
     """
     state = state or OuterState()
     base_params = list(base_params)
@@ -152,7 +171,7 @@ def outer_step(base_params, worker_params, state: OuterState | None = None, lr: 
         theta = flat_view(base_params)
         flats = [flat_view(w) for w in worker_params]
         if theta is None or any(f is None for f in flats):
-            if len(worker_params) <= L_MAX and base_params and all(p.is_cuda for p in base_params):
+            if cpu_tails is None and len(worker_params) <= L_MAX and base_params and all(p.is_cuda for p in base_params):
                 if len({w[0].dtype for w in worker_params}) != 1:
                     raise EdtError("all trained models must share one dtype")
                 _step_list(base_params, worker_params, state, lr, momentum, nesterov)
@@ -164,7 +183,8 @@ def outer_step(base_params, worker_params, state: OuterState | None = None, lr: 
         wdt = {f.dtype for f in flats}
         if len(wdt) != 1:
             raise EdtError("all trained models must share one dtype")
-        _step_flat(theta, flats, state, lr, momentum, nesterov)
+        _step_flat(theta, flats, state, lr, momentum, nesterov,
+                   tail_bits=_tail_bits(cpu_tails, [p.numel() for p in base_params], theta.device))
         if copied:
             unpack_(theta, base_params)
     return state
@@ -178,11 +198,14 @@ class OuterSync:
     """
 
     def __init__(self, theta: ParamArena, workers: list[ParamArena], lr: float = 0.7,
-                 momentum: float = 0.9, nesterov: bool = True, state: OuterState | None = None):
+                 momentum: float = 0.9, nesterov: bool = True, state: OuterState | None = None,
+                 cpu_tails: tuple[int, int] | None = None):
         self.theta = theta
         self.workers = workers
         self.lr, self.momentum, self.nesterov = lr, momentum, nesterov
         self.state = state or OuterState()
+        # (Vec::size(), threads) of the reference's host: its bf16 scalar tails (outer_step's doc)
+        self.tail_bits = _tail_bits(cpu_tails, theta.layout.numels, theta.flat.device)
 
     @traced("edt/OuterSync.step")
     def step(self, broadcast: bool = False) -> None:
@@ -191,7 +214,7 @@ class OuterSync:
         rounded to its dtype right after the kernel has read it (edt_outer_step_bcast)."""
         ws = [w.flat for w in self.workers]
         _step_flat(self.theta.flat, ws, self.state, self.lr, self.momentum, self.nesterov,
-                   ws if broadcast else None)
+                   ws if broadcast else None, tail_bits=self.tail_bits)
 
     def place_momentum(self, candidates: int = 8) -> dict:
         """Choose where the outer momentum lives in HBM by measurement, once, for the life of

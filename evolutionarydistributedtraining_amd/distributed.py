@@ -45,7 +45,8 @@ class ShardedOuterSync:
     def __init__(self, layout: ParamLayout, theta_dtype: torch.dtype, worker_dtype: torch.dtype,
                  k_local: int, device, lr: float = 0.7, momentum: float = 0.9, nesterov: bool = True,
                  mode: str = "auto", bucket_elems: int = 1 << 26, group=None, kernels=None,
-                 broadcast: str = "auto", comm: Collectives | None = None):
+                 broadcast: str = "auto", comm: Collectives | None = None,
+                 cpu_tails: tuple[int, int] | None = None):
         if mode not in ("reduce", "exact", "auto") or broadcast not in ("theta", "workers", "auto"):
             raise ValueError((mode, broadcast))
         if mode == "reduce" and broadcast == "workers":
@@ -89,6 +90,13 @@ class ShardedOuterSync:
         # RCCL (and the virtual ranks) reduce/gather in place; gloo gets separate buffers
         self.inplace = self.comm.inplace
         self.kernel_events = None      # a list: (start, end) HIP events around every local kernel
+        # (Vec::size(), threads) of the reference's host: exact mode reproduces its bf16 scalar tails
+        # (diloco.outer_step's cpu_tails; the reduce mode reassociates the sum anyway)
+        self.tail_bits = None
+        if cpu_tails is not None and mode == "exact" and self.kernels is _ops:
+            from .torchcompat import torch_cpu_tail_bits
+            self.tail_bits = torch_cpu_tail_bits(list(layout.numels) + [self.n_pad - n], vec_elems=cpu_tails[0],
+                                                 num_threads=cpu_tails[1], device=device)
         if mode == "reduce":
             self.acc = torch.zeros(self.n_pad, dtype=torch.float32, device=device)
             self.acc_shard = None if self.inplace else torch.empty(shard_total, dtype=torch.float32, device=device)
@@ -171,8 +179,13 @@ class ShardedOuterSync:
                 # broadcast="workers": the HIP kernel also stores the new shard, rounded to the
                 # worker dtype, into local worker 0's arena (its bucket has been sent) — the
                 # rounding copy fused into the step
-                fused = self.broadcast == "workers" and k is _ops
-                self._launch(k.outer_step, self.theta_buf[s0:s1], shards, mom, self.has_momentum, self.lr,
+                fused = self.broadcast == "workers" and k is _ops and self.tail_bits is None
+                if self.tail_bits is not None:     # shards start at multiples of 64: whole bytes
+                    import functools
+                    fn = functools.partial(k.outer_step, tail_bits=self.tail_bits[s0 // 8:(s1 + 7) // 8])
+                else:
+                    fn = k.outer_step
+                self._launch(fn, self.theta_buf[s0:s1], shards, mom, self.has_momentum, self.lr,
                              self.momentum, self.nesterov, *([[self.worker_bufs[0][s0:s1]]] if fused else []))
                 mom_off += per
                 if self.broadcast == "workers":

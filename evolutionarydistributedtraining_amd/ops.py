@@ -17,14 +17,17 @@ from . import _lib as L
 
 def outer_step(theta: torch.Tensor, workers: list[torch.Tensor], momentum: torch.Tensor | None,
                has_momentum: bool, lr: float, momentum_coef: float, nesterov: bool,
-               broadcast: list[torch.Tensor] | None = None) -> None:
+               broadcast: list[torch.Tensor] | None = None, tail_bits: torch.Tensor | None = None) -> None:
     """Fused DiLoCo outer step (EDT_LM/diloco.py:238-289): theta and momentum updated in place.
 
     theta: flat float32/bfloat16; workers: K flat tensors of one dtype (K > 64: chained launches
     through a scratch running sum); momentum: flat, theta's dtype (required when momentum_coef != 0).
     broadcast: buffers of the workers' dtype (may be the workers themselves) that receive the new
     theta rounded to that dtype in the same pass (edt_outer_step_bcast: the broadcast of
-    diloco.py:302-308 fused into the step, no re-read of theta per copy)."""
+    diloco.py:302-308 fused into the step, no re-read of theta per copy).
+    tail_bits: torchcompat.torch_cpu_tail_bits of the reference's host (uint8 device bitmask of the
+    arena): bf16 elements on torch CPU's scalar tails round add(alpha) twice, as the reference does
+    there (edt_outer_step_tail)."""
     lib = L.lib()
     if not workers:
         raise L.EdtError("no workers")
@@ -48,6 +51,17 @@ def outer_step(theta: torch.Tensor, workers: list[torch.Tensor], momentum: torch
         outer_step(theta, workers, momentum, has_momentum, lr, momentum_coef, nesterov)
         for b in broadcast:
             b.copy_(theta)
+        return
+    if tail_bits is not None:
+        L.require_device(tail_bits)
+        if broadcast or len(workers) > L.EDT_MAX_WORKERS:
+            raise L.EdtError("tail emulation runs in the plain fused step (<= 64 workers, no broadcast)")
+        if tail_bits.dtype != torch.uint8 or tail_bits.numel() * 8 < n:
+            raise L.EdtError("tail_bits: uint8 with one bit per element")
+        L.check(lib.edt_outer_step_tail(L.ptr(theta), L.dtype_code(theta), L.ptr_array(workers),
+                                        L.dtype_code(workers[0]), len(workers), L.ptr(momentum),
+                                        int(has_momentum), n, float(lr), float(momentum_coef), int(nesterov),
+                                        L.ptr(tail_bits), L.stream_ptr(theta.device)), "edt_outer_step_tail")
         return
     if len(workers) <= L.EDT_MAX_WORKERS:
         L.check(lib.edt_outer_step(L.ptr(theta), L.dtype_code(theta), L.ptr_array(workers),
@@ -128,7 +142,8 @@ def sgd_apply(theta: torch.Tensor, acc: torch.Tensor, momentum: torch.Tensor | N
 
 def pair_merge(b1: torch.Tensor, b2: torch.Tensor | None, m1: torch.Tensor, m2: torch.Tensor,
                out: torch.Tensor, momentum: torch.Tensor | None, has_momentum: bool, lr: float,
-               momentum_coef: float, nesterov: bool, momentum_in: torch.Tensor | None = None) -> None:
+               momentum_coef: float, nesterov: bool, momentum_in: torch.Tensor | None = None,
+               tail_bits: torch.Tensor | None = None) -> None:
     """EDT child = SGD step of lerp(.5, b1, b2) towards m1, m2 (EDT_LM/train/crossover.py:150-230).
     b2 None: b1 is the already merged base (dtype of `out`). momentum is updated in place, or,
     with `momentum_in` (the donor parent's buffer, left intact), written fresh
@@ -148,10 +163,14 @@ def pair_merge(b1: torch.Tensor, b2: torch.Tensor | None, m1: torch.Tensor, m2: 
     if any(t is not None and t.dtype != out.dtype for t in (momentum, momentum_in)):
         raise L.EdtError("momentum buffers must have out's dtype")
     mom_in = momentum if momentum_in is None else momentum_in
-    L.check(lib.edt_pair_merge_to(L.ptr(b1), L.ptr(b2), L.ptr(m1), L.ptr(m2), L.dtype_code(m1),
-                                  L.ptr(out), L.dtype_code(out), L.ptr(mom_in), L.ptr(momentum),
-                                  int(has_momentum), n, float(lr), float(momentum_coef), int(nesterov),
-                                  L.stream_ptr(out.device)), "edt_pair_merge_to")
+    if tail_bits is not None:
+        L.require_device(tail_bits)
+        if tail_bits.dtype != torch.uint8 or tail_bits.numel() * 8 < n:
+            raise L.EdtError("tail_bits: uint8 with one bit per element")
+    L.check(lib.edt_pair_merge_tail(L.ptr(b1), L.ptr(b2), L.ptr(m1), L.ptr(m2), L.dtype_code(m1),
+                                    L.ptr(out), L.dtype_code(out), L.ptr(mom_in), L.ptr(momentum),
+                                    int(has_momentum), n, float(lr), float(momentum_coef), int(nesterov),
+                                    L.ptr(tail_bits), L.stream_ptr(out.device)), "edt_pair_merge_tail")
 
 
 def lerp(t: float, v0: torch.Tensor, v1: torch.Tensor, out: torch.Tensor | None = None,

@@ -63,6 +63,23 @@ int edt_outer_step_bcast(void* theta_g, int gdt, const void* const* theta_k, int
                          void* momentum, int has_momentum, uint64_t n, double lr, double momentum_coef,
                          int nesterov, void* const* bcast, int nbcast, void* stream);
 
+/* Bit-exact with the reference on a given host: torch's CPU kernels run add(x, y, alpha) as one
+ * FMA on their vectorised path but as round(x + round(alpha * y)) on the scalar tail of every
+ * contiguous run (the last numel % Vec::size() elements of each at::parallel_for chunk; Vec::size()
+ * = 32 bf16 on AVX-512, 16 on AVX2), which differ in bf16 (EDT_LM/diloco.py:252-289's SGD:
+ * grad.add(buf, alpha=mu), param.add_(grad, alpha=-lr)). edt_outer_step / edt_pair_merge_to compute
+ * the vectorised form on every element; these variants take the tail elements of the reference's
+ * host as a bitmask (device, 1 bit per element of the flat arena, bit i & 7 of byte i >> 3; built
+ * from the layout, the host's vector width and its thread count) and round those twice. Ignored
+ * for fp32 (torch's fp32 tails are FMAs too). tail_bits NULL = the plain functions. */
+int edt_outer_step_tail(void* theta_g, int gdt, const void* const* theta_k, int wdt, int K,
+                        void* momentum, int has_momentum, uint64_t n, double lr, double momentum_coef,
+                        int nesterov, const uint8_t* tail_bits, void* stream);
+int edt_pair_merge_tail(const void* b1, const void* b2, const void* m1, const void* m2, int wdt,
+                        void* theta_out, int gdt, const void* momentum_in, void* momentum_out,
+                        int has_momentum, uint64_t n, double lr, double momentum_coef, int nesterov,
+                        const uint8_t* tail_bits, void* stream);
+
 /* The same step for any population size: K > EDT_MAX_WORKERS runs as consecutive launches of
  * <= 64 workers (the reference's worker order), the running sum carried in `workspace` (n
  * elements of theta's dtype: lossless, the sum is rounded to that dtype after every add).

@@ -591,3 +591,99 @@ def test_c_consumer_runs():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120, cwd="/")
     assert r.returncode == 0, r.stdout + r.stderr
     assert "abi consumer ok" in r.stdout
+
+
+# ------------------------------------------------------------------------------------------
+# torch CPU scalar-tail emulation (edt_outer_step_tail / edt_pair_merge_tail): with the reference
+# host's tail elements, the bf16 regime is bit-exact with the reference on EVERY element
+
+def _tail_bits(numels, dev, threads=1, vec=32):
+    from evolutionarydistributedtraining_amd.torchcompat import torch_cpu_tail_bits
+    return torch_cpu_tail_bits(numels, vec_elems=vec, num_threads=threads, device=dev)
+
+
+@pytest.mark.parametrize("idx", range(len(_M["diloco"])))
+def test_diloco_golden_bit_exact_with_tails(golden, dev, ops, idx):
+    c = golden.diloco_cases()[idx]
+    T = len(c["shapes"])
+    numels = [int(torch.Size(s).numel()) for s in c["shapes"]]
+    tb = _tail_bits(numels, dev)
+    prev_buf = None
+    for step in c["steps"]:
+        pre = step["prefix"]
+        theta = flat(golden.tlist("diloco", f"{pre}/base", T)).contiguous()
+        workers = [flat(golden.tlist("diloco", f"{pre}/worker{k}", T)).contiguous() for k in range(c["K"])]
+        mu = c["momentum"]
+        mom = None if mu == 0 else (torch.zeros_like(theta) if prev_buf is None else prev_buf.clone())
+        has = mu != 0 and prev_buf is not None
+        th_d, mom_d = theta.to(dev), None if mom is None else mom.to(dev)
+        ops.outer_step(th_d, [w.to(dev) for w in workers], mom_d, has, c["lr"], mu, c["nesterov"], tail_bits=tb)
+        want = flat(golden.tlist("diloco", f"{pre}/out_theta", T))
+        assert torch.equal(bits(th_d.cpu()), bits(want)), pre           # every element, every regime
+        if step["has_out_buf"]:
+            prev_buf = mom_d.cpu()
+            assert torch.equal(bits(prev_buf), bits(flat(golden.tlist("diloco", f"{pre}/out_buf", T))))
+
+
+def test_diloco_large_golden_bit_exact_with_parallel_tails(golden, dev, ops):
+    """The golden case whose tensors exceed torch's parallel grain, generated with torch's thread
+    count of the generating host: a tail at the end of every parallel chunk, reproduced exactly."""
+    c = golden.manifest["diloco_large"]
+    T = len(c["shapes"])
+    numels = [int(torch.Size(s).numel()) for s in c["shapes"]]
+    tb = _tail_bits(numels, dev, threads=c["torch_num_threads"])
+    pre = c["name"]
+    theta = flat(golden.tlist("diloco", f"{pre}/s0/base", T)).contiguous().to(dev)
+    mom = torch.zeros_like(theta)
+    for step in (0, 1):
+        ws = [flat(golden.tlist("diloco", f"{pre}/s{step}/worker{k}", T)).contiguous().to(dev) for k in range(c["K"])]
+        ops.outer_step(theta, ws, mom, step == 1, c["lr"], c["momentum"], c["nesterov"], tail_bits=tb)
+        assert torch.equal(bits(theta.cpu()), bits(flat(golden.tlist("diloco", f"{pre}/s{step}/out_theta", T)))), step
+    assert torch.equal(bits(mom.cpu()), bits(flat(golden.tlist("diloco", f"{pre}/s1/out_buf", T))))
+
+
+@pytest.mark.parametrize("idx", range(len(_M["pair_merge"])))
+def test_pair_merge_golden_bit_exact_with_tails(golden, dev, ops, idx):
+    from tests.test_oracle_golden import pair_inputs
+    c = golden.pair_cases()[idx]
+    p = pair_inputs(golden, c)
+    tb = _tail_bits([int(torch.Size(s).numel()) for s in c["shapes"]], dev)
+    n = p["b1"].numel()
+    out_d = torch.empty(n, dtype=p["bdt"], device=dev)
+    mom_d = None if p["mom"] is None else p["mom"].to(dev)
+    ops.pair_merge(p["b1"].to(dev), p["b2"].to(dev), p["m1"].to(dev), p["m2"].to(dev), out_d, mom_d,
+                   p["has"], p["lr"], p["mu"], p["nesterov"], tail_bits=tb)
+    assert torch.equal(bits(out_d.cpu()), bits(p["want_theta"])), c["name"]
+    if p["want_buf"] is not None:
+        assert torch.equal(bits(mom_d.cpu()), bits(p["want_buf"].to(p["bdt"])))
+
+
+@pytest.mark.parametrize("threads,vec", [(1, 32), (3, 32), (8, 16), (16, 32)])
+def test_tail_emulation_vs_oracle(oracle, dev, ops, threads, vec):
+    """Random bf16 layouts (odd sizes, tensors above the parallel grain): the kernels with a host's
+    tail bits equal the oracle with the same host's tail mask, bit for bit; vector and scalar
+    (misaligned) bodies."""
+    from evolutionarydistributedtraining_amd.torchcompat import torch_cpu_tail_bits
+    numels = [70_001, 5, 31, 257 * 160, 33, 100_003]
+    n = sum(numels)
+    mask = oracle.torch_cpu_tail_mask(numels, vec_elems=vec, num_threads=threads)
+    tb = torch_cpu_tail_bits(numels, vec_elems=vec, num_threads=threads, device=dev)
+    g = torch.Generator().manual_seed(threads * 100 + vec)
+    theta = (torch.randn(n, generator=g) * 0.02).bfloat16()
+    ws = [(theta.float() + torch.randn(n, generator=g) * 1e-3).bfloat16() for _ in range(3)]
+    mom = (torch.randn(n, generator=g) * 1e-3).bfloat16()
+    th_d, m_d = theta.to(dev), mom.to(dev)
+    ops.outer_step(th_d, [w.to(dev) for w in ws], m_d, True, 0.7, 0.9, True, tail_bits=tb)
+    th, m = theta.clone(), mom.clone()
+    oracle.outer_step(th, ws, m, True, 0.7, 0.9, True, mask)
+    assert torch.equal(bits(th_d.cpu()), bits(th)) and torch.equal(bits(m_d.cpu()), bits(m))
+    assert int(mask.sum()) > 0
+    # pair merge, bases merged in the kernel (b2 given)
+    out_d = torch.empty(n, dtype=torch.bfloat16, device=dev)
+    mom2_d = mom.to(dev)
+    ops.pair_merge(ws[0].to(dev), ws[1].to(dev), ws[2].to(dev), theta.to(dev), out_d, mom2_d, True, 0.7, 0.9, True,
+                   tail_bits=tb)
+    out = torch.empty(n, dtype=torch.bfloat16)
+    m2 = mom.clone()
+    oracle.pair_merge(ws[0], ws[1], ws[2], theta, out, m2, True, 0.7, 0.9, True, tail=mask)
+    assert torch.equal(bits(out_d.cpu()), bits(out)) and torch.equal(bits(mom2_d.cpu()), bits(m2))

@@ -481,3 +481,22 @@ def test_comm_abi_bounded_step_and_abort_world1(dev):
             c.wait(dev, timeout_s=1.0)
     finally:
         c.close()
+
+
+def test_outer_step_surface_cpu_tails_bit_exact_with_reference(golden, dev):
+    """diloco.outer_step(..., cpu_tails=(32, threads)) on the golden case generated with torch's
+    parallel chunks (separate parameter tensors, as list(model.parameters())): the reference's
+    bf16 output and momentum, bit for bit."""
+    from evolutionarydistributedtraining_amd.diloco import outer_step
+    from tests.golden_data import bits, flat
+    c = golden.manifest["diloco_large"]
+    T = len(c["shapes"])
+    pre = c["name"]
+    base = [t.clone().to(dev) for t in golden.tlist("diloco", f"{pre}/s0/base", T)]
+    state = None
+    for step in (0, 1):
+        ws = [[t.to(dev) for t in golden.tlist("diloco", f"{pre}/s{step}/worker{k}", T)] for k in range(c["K"])]
+        state = outer_step(base, ws, state, c["lr"], c["momentum"], c["nesterov"],
+                           cpu_tails=(32, c["torch_num_threads"]))
+        got = flat([t.cpu() for t in base])
+        assert torch.equal(bits(got), bits(flat(golden.tlist("diloco", f"{pre}/s{step}/out_theta", T)))), step

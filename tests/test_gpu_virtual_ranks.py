@@ -190,3 +190,38 @@ def test_bench_population_measurement_on_virtual_ranks():
     for r in res:
         assert r["sharded"]["ms"] > 0 and r["per_child"]["ms"] > 0
         assert r["sharded"]["wire_bytes_per_rank"] == 2 * 3 * (124439808 * 2 // 4)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_sharded_exact_with_torch_tails(world):
+    """exact mode with cpu_tails (the reference host's bf16 scalar tails): every rank's shard step
+    takes its slice of the tail bitmask, and the gathered master equals the single-GPU fused step
+    with the same bits."""
+    from evolutionarydistributedtraining_amd.torchcompat import torch_cpu_tail_bits
+    layout, theta, gens = population(SHAPES, torch.bfloat16, torch.bfloat16, 8, steps=2, device=DEV)
+    tb = torch_cpu_tail_bits(layout.numels, vec_elems=32, num_threads=8, device=DEV)
+    th, mom = theta.clone(), torch.zeros_like(theta)
+    for i, ws in enumerate(gens):
+        ops.outer_step(th, ws, mom, i > 0, 0.7, 0.9, True, tail_bits=tb)
+    from evolutionarydistributedtraining_amd.distributed import ShardedOuterSync
+    k_local = 8 // world
+
+    def body(comm):
+        s = ShardedOuterSync(layout, torch.bfloat16, torch.bfloat16, k_local, DEV, mode="exact", broadcast="theta",
+                             bucket_elems=world * 64 * 37, comm=comm, cpu_tails=(32, 8))
+        s.theta.flat.copy_(theta)
+        for ws in gens:
+            for j, a in enumerate(s.workers):
+                a.flat.copy_(ws[comm.rank * k_local + j])
+            s.step()
+        return s.gather_theta().clone()
+
+    res = VirtualWorld(world).run(body)
+    torch.cuda.synchronize()
+    for r in res:
+        assert torch.equal(bits(r), bits(th))
+    plain = theta.clone()
+    m2 = torch.zeros_like(theta)
+    for i, ws in enumerate(gens):
+        ops.outer_step(plain, ws, m2, i > 0, 0.7, 0.9, True)
+    assert not torch.equal(bits(plain), bits(th))      # the tails do change bits here

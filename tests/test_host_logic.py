@@ -312,3 +312,17 @@ def test_host_code_under_asan_and_ubsan():
                        env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1",
                                 UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1"))
     assert p.returncode == 0 and "host checks ok" in p.stdout, p.stderr[-3000:]
+
+
+@pytest.mark.parametrize("threads,vec", [(1, 32), (3, 32), (8, 16), (64, 32)])
+def test_torch_tail_bits_match_the_oracle_mask(oracle, threads, vec):
+    """torchcompat.torch_cpu_tail_bits (the product's restatement of torch's vectorized_loop /
+    parallel_for tails, for edt_outer_step_tail) packs exactly the oracle's tail mask."""
+    import numpy as np
+
+    from evolutionarydistributedtraining_amd.torchcompat import torch_cpu_tail_bits
+    numels = [70_001, 5, 0, 31, 257 * 160, 33, 1_000_003, 1]
+    mask = oracle.torch_cpu_tail_mask(numels, vec_elems=vec, num_threads=threads).numpy()
+    bits = torch_cpu_tail_bits(numels, vec_elems=vec, num_threads=threads).numpy()
+    got = np.unpackbits(bits, bitorder="little")[:mask.size]
+    assert np.array_equal(got, mask) and not np.unpackbits(bits, bitorder="little")[mask.size:].any()
