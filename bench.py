@@ -457,6 +457,11 @@ def main():
         print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
                                                           "MASTER_PORT")}), flush=True)
         return
+    # stdout carries exactly one JSON line (rank 0): everything else the libraries print on fd 1
+    # (RCCL's version banner at communicator init, ROCm notices) is sent to stderr
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     sharded = world > 1 or args.sharded    # --sharded: the multi-GPU code path on one rank
     if sharded and "MASTER_ADDR" not in os.environ:      # --gpus 1 --sharded without torchrun
         os.environ.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
@@ -709,7 +714,7 @@ def main():
             # rank 0 after the GPU phase, on this host's cores: the whole population's step (the
             # reference's master runs all K workers' deltas on its CPU)
             out["cpu_baseline"] = cpu_baseline(args, tdt, wdt, k_total)
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     if sharded:
         dist.barrier()
         dist.destroy_process_group()
