@@ -72,7 +72,7 @@ def parse():
     p.add_argument("--lr", type=float, default=0.7)
     p.add_argument("--momentum", type=float, default=0.9)
     p.add_argument("--nesterov", type=int, default=1)
-    p.add_argument("--mode", default="auto", choices=["reduce", "exact", "auto"])
+    p.add_argument("--mode", default="auto", choices=["reduce", "reduce_ordered", "exact", "auto"])
     p.add_argument("--broadcast", default="auto", choices=["theta", "workers", "auto"],
                    help="N>1: all-gather the fp32 theta replica, or the new theta rounded into the "
                         "worker arenas (fp32 master kept sharded)")
@@ -503,8 +503,9 @@ def main():
         # replicas of theta must agree: rank 0's values everywhere
         dist.broadcast(sync.theta_buf, 0)
         step = sync.step
-        kernel_name = ("outer_kernel (fused, owned shards)" if sync.mode == "exact"
-                       else "outer_kernel(partial) + sgd_apply_kernel")
+        kernel_name = {"exact": "outer_kernel (fused, owned shards)",
+                       "reduce": "outer_kernel(partial) + sgd_apply_kernel",
+                       "reduce_ordered": "outer_kernel(partial) + sgd_apply_sum_kernel"}[sync.mode]
 
     for _ in range(args.warmup):
         step()

@@ -38,6 +38,7 @@ SIGNATURES = [
                                  ctypes.POINTER(_U64), _I, _D, _D, _I, _P, _U64, _P]),
     ("edt_delta_partial", _I, [_P, _I, ctypes.POINTER(_P), _I, _I, _I, _U64, _P, _I, _P]),
     ("edt_sgd_apply", _I, [_P, _I, _P, _P, _I, _U64, _D, _D, _I, _P]),
+    ("edt_sgd_apply_sum", _I, [_P, _I, ctypes.POINTER(_P), _I, _P, _I, _U64, _D, _D, _I, _P]),
     ("edt_pair_merge", _I, [_P, _P, _P, _P, _I, _P, _I, _P, _I, _U64, _D, _D, _I, _P]),
     ("edt_pair_merge_to", _I, [_P, _P, _P, _P, _I, _P, _I, _P, _P, _I, _U64, _D, _D, _I, _P]),
     ("edt_pair_merge_population", _I, [ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_P),

@@ -264,6 +264,49 @@ __global__ __launch_bounds__(kBlock) void sgd_apply_kernel(void* theta, const fl
 }
 
 
+// SGD from N per-rank fp32 partial sums of the same shard, summed in rank order (the sharded
+// step's "reduce_ordered" schedule: an all-to-all delivers every rank's partial of the owned
+// shard, so the cross-rank sum has one fixed order whatever the collective library does).
+struct Partials {
+    const float* p[EDT_MAX_WORKERS];
+};
+
+template <int GDT, int N>
+__global__ __launch_bounds__(kBlock) void sgd_apply_sum_kernel(void* theta, Partials P, int np, void* mom,
+                                                               uint64_t n, SgdScalars s) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    auto elems = [&](auto tagN, uint64_t i) {
+        constexpr int M = decltype(tagN)::value;
+        float g[M], a[M], grad[M], b_in[M];
+        ld<GDT, M>(theta, i, g);
+        ld_momentum<GDT, M>(mom, i, s, b_in);
+        ld<EDT_F32, M>(P.p[0], i, a);
+        for (int r = 1; r < np; ++r) {              // rank order
+            float x[M];
+            ld<EDT_F32, M>(P.p[r], i, x);
+#pragma unroll
+            for (int j = 0; j < M; ++j) a[j] = a[j] + x[j];
+        }
+        rnd<GDT>(a);
+#pragma unroll
+        for (int j = 0; j < M; ++j) grad[j] = -a[j];
+        sgd_update<GDT, M>(g, grad, mom, i, s, b_in);
+        st<GDT, M>(theta, i, g);
+    };
+    using V8 = std::integral_constant<int, kVec>;
+    using V1 = std::integral_constant<int, 1>;
+    if constexpr (N == kVec) {
+        const uint64_t nv = n / kVec;
+        for (uint64_t v = tid; v < nv; v += stride) elems(V8{}, v * kVec);
+        const uint64_t t = nv * kVec + tid;
+        if (t < n) elems(V1{}, t);
+    } else {
+        for (uint64_t e = tid; e < n; e += stride) elems(V1{}, e);
+    }
+}
+
+
 // ---------------------------------------------------------------------------------------
 // Diagnostic: the fused step's access pattern (same operands, loads, stores, cache policy, grid)
 // with a trivial body. Its time is the memory-system ceiling of the step on the device at hand:
@@ -617,6 +660,36 @@ int edt_delta_partial(const void* theta_g, int gdt, const void* const* theta_k, 
     bool vec = aligned16(theta_g) && aligned16(acc_f32);
     for (int k = 0; k < K_local; ++k) vec = vec && aligned16(theta_k[k]);
     return launch_outer<MODE_PARTIAL>(gdt, wdt, a, vec, (hipStream_t)stream);
+}
+
+int edt_sgd_apply_sum(void* theta_g, int gdt, const float* const* acc_f32, int nacc, void* momentum,
+                      int has_momentum, uint64_t n, double lr, double momentum_coef, int nesterov, void* stream) {
+    g_err[0] = 0;
+    if (gdt != EDT_F32 && gdt != EDT_BF16) return fail(EDT_ERR_ARG, "unsupported dtype");
+    if (nacc < 1 || nacc > EDT_MAX_WORKERS) return fail(EDT_ERR_ARG, "partial count %d out of range [1, %d]", nacc,
+                                                         EDT_MAX_WORKERS);
+    if (n == 0) return EDT_OK;
+    if (!theta_g || !acc_f32) return fail(EDT_ERR_ARG, "null buffer");
+    SgdScalars s = make_sgd(gdt, lr, momentum_coef, has_momentum, nesterov);
+    if (s.use_momentum && !momentum) return fail(EDT_ERR_ARG, "momentum buffer is null");
+    Partials P;
+    memset(&P, 0, sizeof(P));
+    bool vec = aligned16(theta_g) && (!s.use_momentum || aligned16(momentum));
+    for (int r = 0; r < nacc; ++r) {
+        if (!acc_f32[r]) return fail(EDT_ERR_ARG, "acc_f32[%d] is null", r);
+        P.p[r] = acc_f32[r];
+        vec = vec && aligned16(acc_f32[r]);
+    }
+    const unsigned g = grid_for(n, vec);
+    hipStream_t st = (hipStream_t)stream;
+    if (gdt == EDT_F32) {
+        if (vec) sgd_apply_sum_kernel<EDT_F32, kVec><<<g, kBlock, 0, st>>>(theta_g, P, nacc, momentum, n, s);
+        else sgd_apply_sum_kernel<EDT_F32, 1><<<g, kBlock, 0, st>>>(theta_g, P, nacc, momentum, n, s);
+    } else {
+        if (vec) sgd_apply_sum_kernel<EDT_BF16, kVec><<<g, kBlock, 0, st>>>(theta_g, P, nacc, momentum, n, s);
+        else sgd_apply_sum_kernel<EDT_BF16, 1><<<g, kBlock, 0, st>>>(theta_g, P, nacc, momentum, n, s);
+    }
+    return check_launch("sgd_apply_sum_kernel");
 }
 
 int edt_sgd_apply(void* theta_g, int gdt, const float* acc_f32, void* momentum, int has_momentum,

@@ -47,10 +47,10 @@ class ShardedOuterSync:
                  mode: str = "auto", bucket_elems: int = 1 << 26, group=None, kernels=None,
                  broadcast: str = "auto", comm: Collectives | None = None,
                  cpu_tails: tuple[int, int] | None = None):
-        if mode not in ("reduce", "exact", "auto") or broadcast not in ("theta", "workers", "auto"):
+        if mode not in ("reduce", "reduce_ordered", "exact", "auto") or broadcast not in ("theta", "workers", "auto"):
             raise ValueError((mode, broadcast))
-        if mode == "reduce" and broadcast == "workers":
-            raise ValueError("the reduce schedule needs the full theta replica (broadcast='theta')")
+        if mode.startswith("reduce") and broadcast == "workers":
+            raise ValueError("the reduce schedules need the full theta replica (broadcast='theta')")
         check_sgd_hparams(lr, momentum, nesterov)
         # the communicator seam: torch.distributed (RCCL / gloo) by default, or N virtual ranks
         # on one device (collectives.VirtualWorld)
@@ -59,12 +59,14 @@ class ShardedOuterSync:
         self.rank = self.comm.rank
         wb = torch.empty(0, dtype=worker_dtype).element_size()
         gb = torch.empty(0, dtype=theta_dtype).element_size()
-        cands = {("reduce", "theta"): 4 + gb, ("exact", "theta"): k_local * wb + gb,
-                 ("exact", "workers"): (k_local + 1) * wb}
+        cands = {("reduce", "theta"): 4 + gb, ("reduce_ordered", "theta"): 4 + gb,
+                 ("exact", "theta"): k_local * wb + gb, ("exact", "workers"): (k_local + 1) * wb}
         cands = {key: v for key, v in cands.items()
                  if mode in ("auto", key[0]) and broadcast in ("auto", key[1])}
-        # fewest wire bytes per element; ties go to the bit-exact schedule
-        mode, broadcast = min(cands, key=lambda key: (cands[key], key[0] != "exact", key[1] != "workers"))
+        # fewest wire bytes per element; ties go to the bit-exact schedule, then to the one whose
+        # cross-rank sum has a fixed order (reduce_ordered) over RCCL's own (reduce)
+        pref = {"exact": 0, "reduce_ordered": 1, "reduce": 2}
+        mode, broadcast = min(cands, key=lambda key: (cands[key], pref[key[0]], key[1] != "workers"))
         self.kernels = kernels or _ops
         self.mode = mode
         self.broadcast = broadcast
@@ -100,6 +102,10 @@ class ShardedOuterSync:
         if mode == "reduce":
             self.acc = torch.zeros(self.n_pad, dtype=torch.float32, device=device)
             self.acc_shard = None if self.inplace else torch.empty(shard_total, dtype=torch.float32, device=device)
+        elif mode == "reduce_ordered":
+            # partials laid out [dest rank][shard] per bucket, received as [src rank][shard]
+            self.acc = torch.zeros(self.n_pad, dtype=torch.float32, device=device)
+            self.acc_recv = torch.zeros(self.n_pad, dtype=torch.float32, device=device)
         else:
             # recv[j][b:e] viewed [src rank][per]: local worker j of every rank, this rank's shard
             self.recv = [torch.empty(self.n_pad, dtype=worker_dtype, device=device) for _ in range(k_local)]
@@ -130,6 +136,8 @@ class ShardedOuterSync:
         mom = 2 * gb if self.momentum else 0
         if self.mode == "exact":
             return shard * (self.k_total * wb + 2 * gb + mom)
+        if self.mode == "reduce_ordered":
+            return self.n_pad * (self.k_local * wb + gb + 4) + shard * (4 * self.world + 2 * gb + mom)
         return self.n_pad * (self.k_local * wb + gb + 4) + shard * (4 + 2 * gb + mom)
 
     @traced("edt/ShardedOuterSync.step")
@@ -157,6 +165,24 @@ class ShardedOuterSync:
                 mom = None if self.mom_shard is None else self.mom_shard[mom_off:mom_off + per]
                 self._launch(k.sgd_apply, self.theta_buf[s0:s1], self._acc_out(b, e), mom, self.has_momentum,
                              self.lr, self.momentum, self.nesterov)
+                mom_off += per
+                gathers.append(self._gather(b, e, s0, s1))
+        elif self.mode == "reduce_ordered":
+            # phase 1: local partials, each bucket's all-to-all as soon as it is ready (the partial
+            # of bucket [b, e) is laid out [dest rank][shard]; it arrives as [src rank][shard])
+            works = []
+            for b, e in self.buckets:
+                self._launch(k.delta_partial, self.theta_buf[b:e], [w[b:e] for w in self.worker_bufs],
+                             self.k_total, self.acc[b:e], False)
+                works.append(self.comm.all_to_all(self.acc_recv[b:e], self.acc[b:e], async_op=True))
+            # phase 2: the owned shard's N partials summed in rank order + SGD, then the all-gather
+            for (b, e), w in zip(self.buckets, works):
+                w.wait()
+                s0, s1 = self._shard(b, e)
+                per = s1 - s0
+                parts = list(self.acc_recv[b:e].view(self.world, per))
+                mom = None if self.mom_shard is None else self.mom_shard[mom_off:mom_off + per]
+                self._launch(self._sgd_sum, self.theta_buf[s0:s1], parts, mom)
                 mom_off += per
                 gathers.append(self._gather(b, e, s0, s1))
         else:
@@ -199,6 +225,17 @@ class ShardedOuterSync:
                 w.copy_(self.worker_bufs[0])
         if self.momentum:
             self.has_momentum = True
+
+    def _sgd_sum(self, theta, parts, mom):
+        """SGD from the shard's per-rank partials, summed in rank order."""
+        k = self.kernels
+        if hasattr(k, "sgd_apply_sum"):
+            k.sgd_apply_sum(theta, parts, mom, self.has_momentum, self.lr, self.momentum, self.nesterov)
+            return
+        total = parts[0].clone()             # stand-in kernels (CPU tests): the same order in torch
+        for p in parts[1:]:
+            total.add_(p)
+        k.sgd_apply(theta, total, mom, self.has_momentum, self.lr, self.momentum, self.nesterov)
 
     def _acc_out(self, b, e):
         """Reduce-scatter destination for bucket [b, e): this rank's slice of the acc buffer
@@ -244,7 +281,7 @@ class ShardedOuterSync:
         f = (self.world - 1) / self.world
         bg = self.theta_buf.element_size()
         wb = self.worker_bufs[0].element_size()
-        if self.mode == "reduce":
+        if self.mode.startswith("reduce"):
             return int(f * self.n_pad * (4 + bg))
         return int(f * self.n_pad * (self.k_local * wb + (wb if self.broadcast == "workers" else bg)))
 

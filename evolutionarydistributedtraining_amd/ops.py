@@ -140,6 +140,19 @@ def sgd_apply(theta: torch.Tensor, acc: torch.Tensor, momentum: torch.Tensor | N
                               int(nesterov), L.stream_ptr(theta.device)), "edt_sgd_apply")
 
 
+def sgd_apply_sum(theta: torch.Tensor, accs: list[torch.Tensor], momentum: torch.Tensor | None,
+                  has_momentum: bool, lr: float, momentum_coef: float, nesterov: bool) -> None:
+    """grad = -round(((acc_0 + acc_1) + ...)) in that order (fp32), then the SGD step on theta
+    (edt_sgd_apply_sum: the reduce_ordered schedule's per-shard step)."""
+    lib = L.lib()
+    L.require_device(theta, momentum, *accs)
+    if not accs or any(a.dtype != torch.float32 or a.numel() != theta.numel() for a in accs):
+        raise L.EdtError("accs: fp32 buffers of theta's size")
+    L.check(lib.edt_sgd_apply_sum(L.ptr(theta), L.dtype_code(theta), L.ptr_array(accs), len(accs), L.ptr(momentum),
+                                  int(has_momentum), theta.numel(), float(lr), float(momentum_coef), int(nesterov),
+                                  L.stream_ptr(theta.device)), "edt_sgd_apply_sum")
+
+
 def pair_merge(b1: torch.Tensor, b2: torch.Tensor | None, m1: torch.Tensor, m2: torch.Tensor,
                out: torch.Tensor, momentum: torch.Tensor | None, has_momentum: bool, lr: float,
                momentum_coef: float, nesterov: bool, momentum_in: torch.Tensor | None = None,

@@ -119,6 +119,13 @@ int edt_delta_partial(const void* theta_g, int gdt, const void* const* theta_k, 
 int edt_sgd_apply(void* theta_g, int gdt, const float* acc_f32, void* momentum, int has_momentum,
                   uint64_t n, double lr, double momentum_coef, int nesterov, void* stream);
 
+/* SGD on a shard from nacc per-rank fp32 partial sums of it (acc_f32[0..nacc), device pointers,
+ * n elements each), summed in that order: grad = -round_g(((acc_0 + acc_1) + ...) + acc_{nacc-1}).
+ * The sharded step's reduce_ordered schedule (all-to-all of the partials, then this): the
+ * cross-rank sum has one fixed order, independent of the collective library's algorithm. */
+int edt_sgd_apply_sum(void* theta_g, int gdt, const float* const* acc_f32, int nacc, void* momentum,
+                      int has_momentum, uint64_t n, double lr, double momentum_coef, int nesterov, void* stream);
+
 /* ---- EDT pairwise merge -------------------------------------------------------------------
  * Replaces EDT_LM/train/crossover.py:150-163 + 166-230 for one child:
  *   B = lerp(0.5, b1, b2)                         (run_linear_merge_5050, in the model dtype wdt)

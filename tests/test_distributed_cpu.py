@@ -76,7 +76,8 @@ def _ulp(x, dt):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("mode,broadcast", [("exact", "theta"), ("exact", "workers"), ("reduce", "theta")])
+@pytest.mark.parametrize("mode,broadcast", [("exact", "theta"), ("exact", "workers"), ("reduce", "theta"),
+                                            ("reduce_ordered", "theta")])
 @pytest.mark.parametrize("tdt,wdt", [(torch.float32, torch.bfloat16), (torch.bfloat16, torch.bfloat16)])
 def test_sharded_outer_step_world2(tmp_path, oracle, mode, broadcast, tdt, wdt):
     port = _free_port()
@@ -98,7 +99,12 @@ def test_sharded_outer_step_world2(tmp_path, oracle, mode, broadcast, tdt, wdt):
             off[r] += per
     mom = mom[:n]
     bits = (lambda t: t.view(torch.int32)) if tdt == torch.float32 else (lambda t: t.view(torch.int16))
-    if mode == "exact":
+    if mode == "reduce_ordered":         # the cross-rank sum in rank order: one fixed result
+        from tests.virtual_schedules import reduce_reference
+        _, theta0, steps = _population(tdt, wdt)
+        th_rs, mom_rs = reduce_reference(oracle, theta0, steps, WORLD)
+        assert torch.equal(bits(got), bits(th_rs)) and torch.equal(bits(mom), bits(mom_rs))
+    elif mode == "exact":
         assert torch.equal(bits(got), bits(th_ref))
         assert torch.equal(bits(mom), bits(mom_ref))
         if broadcast == "workers":       # every local worker now starts from round_w(theta)

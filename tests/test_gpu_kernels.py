@@ -687,3 +687,23 @@ def test_tail_emulation_vs_oracle(oracle, dev, ops, threads, vec):
     m2 = mom.clone()
     oracle.pair_merge(ws[0], ws[1], ws[2], theta, out, m2, True, 0.7, 0.9, True, tail=mask)
     assert torch.equal(bits(out_d.cpu()), bits(out)) and torch.equal(bits(mom2_d.cpu()), bits(m2))
+
+
+@pytest.mark.parametrize("gdt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("nacc,off", [(1, 0), (3, 0), (8, 1)])
+def test_sgd_apply_sum_vs_oracle(oracle, dev, ops, gdt, nacc, off):
+    """edt_sgd_apply_sum (reduce_ordered's per-shard step): the partials summed in the given order
+    in fp32, then the oracle's SGD from that sum, bit for bit; vector and scalar (misaligned) bodies."""
+    n = 50_003
+    g = torch.Generator().manual_seed(nacc + off)
+    theta = (torch.randn(n + off, generator=g) * 0.02).to(gdt)
+    mom = (torch.randn(n + off, generator=g) * 1e-3).to(gdt)
+    accs = [torch.randn(n + off, generator=g) * 1e-4 for _ in range(nacc)]
+    th_d, m_d = theta.to(dev)[off:], mom.to(dev)[off:]
+    ops.sgd_apply_sum(th_d, [a.to(dev)[off:] for a in accs], m_d, True, 0.7, 0.9, True)
+    total = accs[0][off:].clone()
+    for a in accs[1:]:
+        total.add_(a[off:])
+    th, m = theta[off:].clone(), mom[off:].clone()
+    oracle.sgd_apply(th, total, m, True, 0.7, 0.9, True)
+    assert torch.equal(bits(th_d.cpu()), bits(th)) and torch.equal(bits(m_d.cpu()), bits(m))

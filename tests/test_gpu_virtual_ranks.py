@@ -36,7 +36,8 @@ def _fused(theta, gens):
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])
-@pytest.mark.parametrize("mode,broadcast", [("exact", "theta"), ("exact", "workers"), ("reduce", "theta")])
+@pytest.mark.parametrize("mode,broadcast", [("exact", "theta"), ("exact", "workers"), ("reduce", "theta"),
+                                            ("reduce_ordered", "theta")])
 @pytest.mark.parametrize("tdt,wdt", [(torch.float32, torch.float32), (torch.float32, torch.bfloat16),
                                      (torch.bfloat16, torch.bfloat16)])
 def test_sharded_schedule_on_virtual_ranks(oracle, world, mode, broadcast, tdt, wdt):

@@ -21,7 +21,8 @@ def _oracle_ref(theta, gens, tdt):
 
 
 @pytest.mark.parametrize("world", [2, 3, 4, 8])
-@pytest.mark.parametrize("mode,broadcast", [("exact", "theta"), ("exact", "workers"), ("reduce", "theta")])
+@pytest.mark.parametrize("mode,broadcast", [("exact", "theta"), ("exact", "workers"), ("reduce", "theta"),
+                                            ("reduce_ordered", "theta")])
 @pytest.mark.parametrize("tdt,wdt", [(torch.float32, torch.float32), (torch.float32, torch.bfloat16),
                                      (torch.bfloat16, torch.bfloat16)])
 def test_virtual_sharded_outer_step(oracle, world, mode, broadcast, tdt, wdt):
