@@ -169,6 +169,18 @@ def cpu_baseline(args, theta_dtype, worker_dtype, k):
     return out
 
 
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
 def _block_sample(layout, budget):
     """The tensors of the layout's first transformer block (names with '.0.'), else the first
     tensors in order within the budget: a sample with every shape of the step."""
@@ -199,7 +211,8 @@ def reference_loop_baseline(args, theta_dtype, worker_dtype, k):
                                                     bool(args.nesterov))
     t, reps = _median_time(rep, args.cpu_baseline_seconds / 2)
     return {"value": round(k * total * torch.finfo(worker_dtype).bits / 8 / t / 1e9, 3), "unit": "GB/s",
-            "cores": torch.get_num_threads(), "kind": "port",
+            "cores": torch.get_num_threads(), "kind": "port", "cpu_model": _cpu_model(),
+            "host_cpus_visible": os.cpu_count(),
             "sample": f"{len(shapes)} tensors of {args.layout} ({names[0]} .. {names[-1]}, {total} elements) x {k} "
                       f"workers, EDT_LM/diloco.py:238-289's per-tensor torch loop + torch.optim.SGD "
                       f"(oracle.torch_loop_outer_step), median of {reps} reps"}
