@@ -137,3 +137,22 @@ def test_single_file_wins_over_a_stale_index(tmp_path):
     assert set(checkpoint.checkpoint_files(str(d)).values()) == {str(d / "model.safetensors")}
     got = checkpoint.read_into_arena(str(d), layout, torch.empty(layout.total))
     assert torch.equal(got, new)
+
+
+def test_split_readers_and_threaded_writes(tmp_path):
+    """read_many with fewer checkpoints than readers cuts each checkpoint into tensor ranges (one
+    reader each); the threaded pwrite writer produces the same file as a single write."""
+    m = _tiny(torch.bfloat16)
+    m.save_pretrained(tmp_path / "a", max_shard_size="8KB")
+    layout = ParamLayout.of_module(m)
+    want = pack(list(m.parameters()))
+    got = torch.full((layout.total,), float("nan"), dtype=torch.bfloat16)
+    checkpoint.read_many([(str(tmp_path / "a"), got)], layout, threads=5, staging_bytes=4096)
+    assert torch.equal(got, want)
+    header = checkpoint._header_bytes(layout, layout.names, want.dtype, None)
+    checkpoint._write_file(str(tmp_path / "one.safetensors"), header, want, threads=1)
+    checkpoint._write_file(str(tmp_path / "many.safetensors"), header, want, threads=7, min_bytes=0)
+    assert (tmp_path / "one.safetensors").read_bytes() == (tmp_path / "many.safetensors").read_bytes()
+    sd = load_file(str(tmp_path / "many.safetensors"))
+    for (name, _), v in zip(m.named_parameters(), layout.views(want)):
+        assert torch.equal(sd[name], v)
