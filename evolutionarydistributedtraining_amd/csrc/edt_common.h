@@ -134,6 +134,9 @@ constexpr int kTile = kBlock * kVec;                 // 2,048 elements
 #define EDT_SLERP_TPC 32
 #endif
 constexpr int kTilesPerChunk = EDT_SLERP_TPC;        // the plans' default chunk: 64 Ki elements
+#ifndef EDT_SLERP_BLEND_REV     // 1: the tile grid walks the arena from its end (probe: does the blend
+#define EDT_SLERP_BLEND_REV 0   // re-read what the stats pass left in the Infinity Cache last?)
+#endif
 inline unsigned slerp_tile_grid(int64_t nchunks) {
     if (!EDT_SLERP_GRID) return slerp_grid(nchunks);
     const uint64_t g = (uint64_t)nchunks * kTilesPerChunk;

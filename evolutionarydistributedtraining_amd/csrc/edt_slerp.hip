@@ -108,10 +108,11 @@ __device__ __forceinline__ void slerp_coefficients(double s00, double s11, doubl
 template <bool TILES, typename F>
 __device__ __forceinline__ void for_blend_ranges(const uint64_t* chunks, int64_t nchunks, F&& body) {
     if constexpr (TILES && EDT_SLERP_GRID) {
-        const int64_t c = blockIdx.x / kTilesPerChunk;
+        const uint64_t b = EDT_SLERP_BLEND_REV ? gridDim.x - 1 - blockIdx.x : blockIdx.x;
+        const int64_t c = (int64_t)(b / kTilesPerChunk);
         if (c >= nchunks) return;
         const uint64_t start = chunks[3 * c], len = chunks[3 * c + 1], seg = chunks[3 * c + 2];
-        for (uint64_t off = (uint64_t)(blockIdx.x % kTilesPerChunk) * kTile; off < len;
+        for (uint64_t off = (b % kTilesPerChunk) * kTile; off < len;
              off += (uint64_t)kTilesPerChunk * kTile)
             body(start + off, start + (off + kTile < len ? off + kTile : len), seg);
     } else {

@@ -115,6 +115,8 @@ VARIANTS.update({"s_grid0": ["-DEDT_SLERP_GRID=0"], "s_grid1": ["-DEDT_SLERP_GRI
                  "s_tile4k": ["-DEDT_SLERP_TPC=2", "-DEDT_SLERP_SPEC_BPC=1048576"],
                  "s_tile8k": ["-DEDT_SLERP_TPC=4", "-DEDT_SLERP_SPEC_BPC=1048576"],
                  "s_tile16k": ["-DEDT_SLERP_TPC=8", "-DEDT_SLERP_SPEC_BPC=1048576"]})
+VARIANTS.update({"s_nt0": ["-DEDT_NT_SLERP=0"], "s_rev": ["-DEDT_SLERP_BLEND_REV=1"],
+                 "s_rev_nt0": ["-DEDT_SLERP_BLEND_REV=1", "-DEDT_NT_SLERP=0"]})
 
 
 def run_list(names, rounds, iters, wdt="bf16"):
