@@ -1,0 +1,167 @@
+"""BASELINE.json's multi-GPU configs at their named sizes, run as virtual ranks on one MI355X
+(collectives.VirtualWorld: N logical ranks in one process, collectives as device copies), so the
+HIP kernels run inside the exact schedules the driver's 8-GPU bench launches over RCCL:
+
+  configs[2]  125M-param LM (gpt2_small), 8 workers = 8 GPUs, fp32: every schedule (exact,
+              reduce_ordered, reduce) against the single-GPU fused step over the whole population
+  configs[3]  1.3B-param LM, 8 workers over 8 GPUs, bf16 params (theta, momentum and workers bf16)
+  configs[4]  the 7.07B Qwen2.5 body population crossover (link-balanced), at world 2 (8 members of
+              7B plus their children and shards exceed one GPU's 288 GB; the schedule's world-8
+              form runs at 1.3B in test_gpu_fullsize.py)
+
+Reference semantics: EDT_LM/diloco.py:238-289 (outer step), EDT_RL/crossover.py:11-43 (SLERP)."""
+from __future__ import annotations
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    return torch.device("cuda:0")
+
+
+def _population(P, K, steps, seed, wdt, dev):
+    gen = torch.Generator(device=dev).manual_seed(seed)
+    theta0 = torch.randn(P, device=dev, generator=gen) * 0.02
+    gens = [[(theta0 + torch.randn(P, device=dev, generator=gen) * 1e-3 * (s + 1)).to(wdt) for _ in range(K)]
+            for s in range(steps)]
+    return theta0, gens
+
+
+def _run(lay, tdt, wdt, theta0, gens, dev, mode, broadcast, world=8):
+    from evolutionarydistributedtraining_amd.collectives import VirtualWorld
+    from evolutionarydistributedtraining_amd.distributed import ShardedOuterSync
+    k_local = len(gens[0]) // world
+
+    def body(comm):
+        s = ShardedOuterSync(lay, tdt, wdt, k_local, dev, mode=mode, broadcast=broadcast, comm=comm)
+        s.theta.flat.copy_(theta0.to(tdt))
+        for ws in gens:
+            for j, arena in enumerate(s.workers):
+                arena.flat.copy_(ws[comm.rank * k_local + j])
+            s.step()
+        theta = s.gather_theta().clone()
+        mom = []
+        off = 0
+        for b, e in s.buckets:
+            s0, s1 = s._shard(b, e)
+            mom.append((s0, s1, s.mom_shard[off:off + (s1 - s0)].clone()))
+            off += s1 - s0
+        torch.cuda.synchronize()
+        return theta, mom, (s.mode, s.broadcast)
+
+    return VirtualWorld(world, timeout=600).run(body)
+
+
+def _mom_equal(mom_parts, want, P):
+    for s0, s1, m in mom_parts:
+        hi = min(s1, P)
+        if hi > s0 and not torch.equal(m[:hi - s0].view(torch.int16 if m.dtype == torch.bfloat16 else torch.int32),
+                                       want[s0:hi].view(torch.int16 if want.dtype == torch.bfloat16 else torch.int32)):
+            return False
+    return True
+
+
+def test_config2_125m_fp32_world8_every_schedule(dev):
+    """configs[2]: exact bit-exact with the fused step; reduce_ordered bit-exact with the rank-order
+    sum of the ranks' fp32 partials (edt_delta_partial per rank + edt_sgd_apply_sum); reduce within
+    the reassociation bound of DESIGN §3 against the fused step."""
+    from evolutionarydistributedtraining_amd import ops
+    from evolutionarydistributedtraining_amd.layouts import gpt2_small
+    from tests.virtual_schedules import reduce_tol
+    lay = gpt2_small()
+    P, K, f32 = lay.total, 8, torch.float32
+    theta0, gens = _population(P, K, 2, 21, f32, dev)
+    th, mom = theta0.clone(), torch.zeros(P, device=dev)
+    for i, ws in enumerate(gens):
+        ops.outer_step(th, ws, mom, i > 0, 0.7, 0.9, True)
+    # the rank-order reference of reduce_ordered (one worker per rank)
+    th_o, mom_o = theta0.clone(), torch.zeros(P, device=dev)
+    for i, ws in enumerate(gens):
+        accs = [torch.empty(P, device=dev) for _ in range(K)]
+        for r in range(K):
+            ops.delta_partial(th_o, [ws[r]], K, accs[r], False)
+        ops.sgd_apply_sum(th_o, accs, mom_o, i > 0, 0.7, 0.9, True)
+        del accs
+    torch.cuda.synchronize()
+
+    for mode in ("exact", "reduce_ordered"):
+        res = _run(lay, f32, f32, theta0, gens, dev, mode, "theta")
+        want_t, want_m = (th, mom) if mode == "exact" else (th_o, mom_o)
+        for r, (theta, mom_parts, sched) in enumerate(res):
+            assert sched == (mode, "theta")
+            assert torch.equal(theta.view(torch.int32), want_t.view(torch.int32)), (mode, r)
+            assert _mom_equal(mom_parts, want_m, P), (mode, r)
+        del res
+    res = _run(lay, f32, f32, theta0, gens, dev, "reduce", "theta")
+    tol = reduce_tol(th, mom, f32, gens=gens)
+    for theta, _, sched in res:
+        assert sched == ("reduce", "theta")
+        assert bool(((theta - th).abs() <= tol).all())
+
+
+def test_config3_1p3b_all_bf16_world8(dev):
+    """configs[3] ("bf16 params"): bf16 theta, momentum and workers, one worker per virtual rank,
+    the schedule `auto` picks; the new theta and momentum bit-exact with the fused single-GPU step
+    (both in torch's vectorised bf16 semantics)."""
+    from evolutionarydistributedtraining_amd import ops
+    from evolutionarydistributedtraining_amd.layouts import gpt_1p3b
+    lay = gpt_1p3b()
+    P, K, bf = lay.total, 8, torch.bfloat16
+    theta0, gens = _population(P, K, 2, 31, bf, dev)
+    th, mom = theta0.to(bf), torch.zeros(P, dtype=bf, device=dev)
+    for i, ws in enumerate(gens):
+        ops.outer_step(th, ws, mom, i > 0, 0.7, 0.9, True)
+    torch.cuda.synchronize()
+    res = _run(lay, bf, bf, theta0, gens, dev, "auto", "auto")
+    for r, (theta, mom_parts, sched) in enumerate(res):
+        assert sched[0] in ("exact", "reduce_ordered", "reduce")
+        if sched[0] == "exact":
+            assert torch.equal(theta.view(torch.int16), th.view(torch.int16)), r
+            assert _mom_equal(mom_parts, mom, P), r
+        else:   # a reassociating schedule: the bound instead
+            from tests.virtual_schedules import reduce_tol
+            assert bool(((theta.float() - th.float()).abs() <= reduce_tol(th, mom, bf, gens=gens)).all()), r
+
+
+def test_config4_7b_population_world2(dev):
+    """configs[4] at the 7.07B Qwen2.5 body: 2 virtual ranks, one bf16 member each, far parents
+    (the SLERP branch) and a self-pair; every child bit-identical to edt_slerp_merge on its two
+    parents."""
+    from evolutionarydistributedtraining_amd import ops
+    from evolutionarydistributedtraining_amd.collectives import VirtualWorld
+    from evolutionarydistributedtraining_amd.distributed import ShardedPopulationCrossover
+    from evolutionarydistributedtraining_amd.layouts import qwen2p5_7b_body
+    lay = qwen2p5_7b_body()
+    P, N, bf = lay.total, 2, torch.bfloat16
+    gen = torch.Generator(device=dev).manual_seed(41)
+    members = []
+    for m in range(N):
+        x = torch.empty(P, dtype=bf, device=dev)
+        for s in range(0, P, 1 << 28):
+            e = min(P, s + (1 << 28))
+            x[s:e] = (torch.randn(e - s, device=dev, generator=gen) * 0.02).to(bf)
+        members.append(x)
+    pairs = [(0, 1), (1, 1)]
+    t = torch.rand(len(lay), dtype=torch.float64, device=dev, generator=gen)
+
+    def body(comm):
+        sp = ShardedPopulationCrossover(lay, bf, dev, comm=comm)
+        out = torch.empty(P, dtype=bf, device=dev)
+        sp.slerp_step(members[comm.rank], pairs, t, out)
+        torch.cuda.synchronize()
+        del sp
+        return out
+
+    res = VirtualWorld(N, timeout=600).run(body)
+    plan = ops.make_slerp_plan(lay.offsets, dev)
+    want = torch.empty(P, dtype=bf, device=dev)
+    for c, (i, j) in enumerate(pairs):
+        ops.slerp_arena(plan, members[i], members[j], want, t, speculate=False)
+        torch.cuda.synchronize()
+        assert torch.equal(res[c].view(torch.int16), want.view(torch.int16)), c
