@@ -9,7 +9,10 @@ disk (EDT_LM/diloco.py:231-235 gather, :302-308 broadcast; EDT_EVOMERGE/train/cr
   slerp   one SLERP child of two 7.07B bf16 bodies: both parents read into arenas -> slerp_arena
           -> the child written (write_from_arena).
 Files go to a scratch dir (page cache warm after writing: the best case of a shared disk) and are
-deleted at the end. Rates are of the files' bytes.
+deleted at the end. Rates are of the files' bytes. Before each timed phase the page cache's dirty
+pages are flushed (os.sync(), untimed, its duration reported): otherwise a write phase pays for the
+write-back of the files created just before it, and the figures track the file system's flusher,
+not the path.
 
     python scripts/e2e_checkpoint_large.py --dir /path/with/80GB
 """
@@ -38,7 +41,13 @@ def _fill(flat, seed, base=None, scale=0.02):
         flat[s:e] = x.to(flat.dtype)
 
 
+SYNCS = []
+
+
 def _sync_time(fn):
+    t0 = time.perf_counter()
+    os.sync()                     # untimed: flush the dirty pages earlier phases left
+    SYNCS.append(round(time.perf_counter() - t0, 2))
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     out = fn()
@@ -136,10 +145,11 @@ def main():
     os.makedirs(a.dir, exist_ok=True)
     try:
         if "diloco" in a.what:
-            print(json.dumps({"diloco": diloco(a, dev, a.dir)}), flush=True)
+            print(json.dumps({"diloco": diloco(a, dev, a.dir), "os_sync_s_before_phases": SYNCS[:]}), flush=True)
+            SYNCS.clear()
             torch.cuda.empty_cache()
         if "slerp" in a.what:
-            print(json.dumps({"slerp": slerp(a, dev, a.dir)}), flush=True)
+            print(json.dumps({"slerp": slerp(a, dev, a.dir), "os_sync_s_before_phases": SYNCS[:]}), flush=True)
     finally:
         shutil.rmtree(a.dir, ignore_errors=True)
 
