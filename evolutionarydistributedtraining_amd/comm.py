@@ -31,6 +31,8 @@ SIGNATURES = [
                                ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_U64), _I, _P]),
     ("edt_outer_step_sharded", _I, [_P, _P, _I, ctypes.POINTER(_P), _I, _I, _P, _I, _U64, _U64, _D, _D, _I,
                                     _P, _P]),
+    ("edt_outer_step_sharded_ordered", _I, [_P, _P, _I, ctypes.POINTER(_P), _I, _I, _P, _I, _U64, _U64, _D, _D,
+                                            _I, _P, _P, _P]),
     ("edt_comm_abort", _I, [_P]),
     ("edt_comm_poll", _I, [_P]),
     ("edt_comm_wait", _I, [_P, _P, _D]),
@@ -159,3 +161,20 @@ class Comm:
             self._h, L.ptr(theta), L.dtype_code(theta), L.ptr_array(workers), L.dtype_code(workers[0]), len(workers),
             L.ptr(momentum_shard) if momentum_shard is not None else None, int(has_momentum), n, bucket_elems,
             float(lr), float(momentum_coef), int(nesterov), L.ptr(acc), self._stream(theta)), "edt_outer_step_sharded")
+
+    def outer_step_sharded_ordered(self, theta: torch.Tensor, workers: list[torch.Tensor],
+                                   momentum_shard: torch.Tensor | None, has_momentum: bool, lr: float,
+                                   momentum_coef: float, nesterov: bool, acc: torch.Tensor, recv: torch.Tensor,
+                                   bucket_elems: int = 1 << 26) -> None:
+        """edt_outer_step_sharded_ordered (the reduce_ordered schedule): as outer_step_sharded,
+        plus `recv`, a second n_pad fp32 workspace the partials' all-to-all lands in."""
+        n = theta.numel()
+        L.require_device(theta, acc, recv, *workers, *([momentum_shard] if momentum_shard is not None else []))
+        if any(w.numel() != n or w.dtype != workers[0].dtype for w in workers) or acc.numel() != n \
+                or acc.dtype != torch.float32 or recv.numel() != n or recv.dtype != torch.float32:
+            raise L.EdtError("workers / acc / recv must match the padded theta")
+        _check(load_comm_library().edt_outer_step_sharded_ordered(
+            self._h, L.ptr(theta), L.dtype_code(theta), L.ptr_array(workers), L.dtype_code(workers[0]), len(workers),
+            L.ptr(momentum_shard) if momentum_shard is not None else None, int(has_momentum), n, bucket_elems,
+            float(lr), float(momentum_coef), int(nesterov), L.ptr(acc), L.ptr(recv), self._stream(theta)),
+            "edt_outer_step_sharded_ordered")

@@ -1,6 +1,6 @@
 // edt_comm.cpp — RCCL (over xGMI) behind the C ABI of include/edt_comm.h, and the bucketed
-// DiLoCo reduce schedule in C (the same schedule as distributed.py mode="reduce"): host code only,
-// the kernels are libedt_sync's edt_delta_partial / edt_sgd_apply.
+// DiLoCo schedules in C (distributed.py mode="reduce" and "reduce_ordered"): host code only, the
+// kernels are libedt_sync's edt_delta_partial / edt_sgd_apply / edt_sgd_apply_sum.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -310,6 +310,69 @@ int edt_outer_step_sharded(void* comm, void* theta_g, int gdt, const void* const
     // edt_comm_set_timeout > 0: wait here, polling RCCL's async error; a dead or stalled peer
     // aborts the communicator after the timeout and the step returns EDT_COMM_ERR_TIMEOUT
     // (the reference's master gives up on workers it stops hearing from, EDT_LM/diloco.py:46-71)
+    if (c->timeout_s > 0) return wait_event(c, c->events[2 * nb], c->timeout_s);
+    return 0;
+}
+
+int edt_outer_step_sharded_ordered(void* comm, void* theta_g, int gdt, const void* const* theta_k, int wdt,
+                                   int K_local, void* momentum_shard, int has_momentum, uint64_t n_pad,
+                                   uint64_t bucket_elems, double lr, double momentum_coef, int nesterov,
+                                   float* acc, float* recv, void* stream) {
+    Comm* c = as_comm(comm);
+    ncclDataType_t gt, wt;
+    uint64_t gsz, wsz;
+    if (int rc = usable(c)) return rc;
+    if (!theta_g || !theta_k || !acc || !recv) return fail(EDT_COMM_ERR_ARG, "null buffer");
+    if (recv == acc) return fail(EDT_COMM_ERR_ARG, "recv must not alias acc (the all-to-all is out of place)");
+    if (!nccl_type(gdt, &gt, &gsz) || !nccl_type(wdt, &wt, &wsz)) return fail(EDT_COMM_ERR_ARG, "dtype pair %d/%d", gdt, wdt);
+    if (K_local < 1 || K_local > EDT_MAX_WORKERS) return fail(EDT_COMM_ERR_ARG, "K_local %d", K_local);
+    if (c->nranks > EDT_MAX_WORKERS) return fail(EDT_COMM_ERR_ARG, "%d ranks: at most %d partials per shard", c->nranks,
+                                                 EDT_MAX_WORKERS);
+    const uint64_t unit = (uint64_t)c->nranks * 64;
+    if (n_pad % unit) return fail(EDT_COMM_ERR_ARG, "n_pad %llu is not a multiple of nranks x 64",
+                                  (unsigned long long)n_pad);
+    if (momentum_coef != 0 && !momentum_shard) return fail(EDT_COMM_ERR_ARG, "momentum shard is null");
+    uint64_t bucket = bucket_elems / unit * unit;
+    if (bucket < unit) bucket = unit;
+    if (bucket > n_pad) bucket = n_pad;
+    const uint64_t nb = n_pad ? (n_pad + bucket - 1) / bucket : 0;
+    if (int rc = ensure_events(c, 2 * nb + 1)) return rc;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int K_total = K_local * c->nranks;
+    char* th = static_cast<char*>(theta_g);
+    std::vector<const void*> wb(K_local);
+    // phase 1: per bucket the local fp32 partial on `stream` (laid out [dest rank][shard]), then
+    // its all-to-all on the side stream: recv[b, e) arrives as [src rank][shard]
+    for (uint64_t i = 0; i < nb; ++i) {
+        const uint64_t b = i * bucket, e = b + bucket < n_pad ? b + bucket : n_pad, per = (e - b) / c->nranks;
+        for (int k = 0; k < K_local; ++k) wb[k] = static_cast<const char*>(theta_k[k]) + b * wsz;
+        int rc = edt_delta_partial(th + b * gsz, gdt, wb.data(), wdt, K_local, K_total, e - b, acc + b, 0, s);
+        if (rc) return fail(EDT_COMM_ERR_ARG, "edt_delta_partial: %s", edt_last_error());
+        EDT_HIP(hipEventRecord(c->events[2 * i], s));
+        EDT_HIP(hipStreamWaitEvent(c->side, c->events[2 * i], 0));
+        EDT_RCCL(ncclAllToAll(acc + b, recv + b, per, ncclFloat32, c->nccl, c->side));
+        EDT_HIP(hipEventRecord(c->events[2 * i + 1], c->side));
+    }
+    // phase 2: the owned shard's N partials summed in rank order + SGD (edt_sgd_apply_sum), then
+    // the shard's all-gather — the cross-rank sum has one order whatever RCCL's algorithm
+    std::vector<const float*> parts(c->nranks);
+    uint64_t mom_off = 0;
+    for (uint64_t i = 0; i < nb; ++i) {
+        const uint64_t b = i * bucket, e = b + bucket < n_pad ? b + bucket : n_pad, per = (e - b) / c->nranks;
+        const uint64_t s0 = b + (uint64_t)c->rank * per;
+        for (int r = 0; r < c->nranks; ++r) parts[r] = recv + b + (uint64_t)r * per;
+        EDT_HIP(hipStreamWaitEvent(s, c->events[2 * i + 1], 0));
+        void* mom = momentum_shard ? static_cast<char*>(momentum_shard) + mom_off * gsz : nullptr;
+        int rc = edt_sgd_apply_sum(th + s0 * gsz, gdt, parts.data(), c->nranks, momentum_coef != 0 ? mom : nullptr,
+                                   has_momentum, per, lr, momentum_coef, nesterov, s);
+        if (rc) return fail(EDT_COMM_ERR_ARG, "edt_sgd_apply_sum: %s", edt_last_error());
+        mom_off += per;
+        EDT_HIP(hipEventRecord(c->events[2 * i], s));
+        EDT_HIP(hipStreamWaitEvent(c->side, c->events[2 * i], 0));
+        EDT_RCCL(ncclAllGather(th + s0 * gsz, th + b * gsz, per, gt, c->nccl, c->side));
+    }
+    EDT_HIP(hipEventRecord(c->events[2 * nb], c->side));
+    EDT_HIP(hipStreamWaitEvent(s, c->events[2 * nb], 0));
     if (c->timeout_s > 0) return wait_event(c, c->events[2 * nb], c->timeout_s);
     return 0;
 }

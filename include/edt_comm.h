@@ -93,6 +93,18 @@ int edt_outer_step_sharded(void* comm, void* theta_g, int gdt, const void* const
                            uint64_t bucket_elems, double lr, double momentum_coef, int nesterov,
                            float* acc, void* stream);
 
+/* The same step, reduce_ordered schedule (distributed.py mode="reduce_ordered"): per bucket the
+ * local fp32 partial into acc[b, e) (laid out [dest rank][shard]), an all-to-all into recv[b, e)
+ * ([src rank][shard]), then edt_sgd_apply_sum on the owned shard with the nranks partials in rank
+ * order, then the all-gather. The cross-rank sum has one fixed order whatever RCCL's algorithm
+ * or topology: the result is reproducible run to run. Same wire bytes as the reduce schedule.
+ * recv: n_pad fp32 elements of workspace, distinct from acc. nranks <= EDT_MAX_WORKERS.
+ * Replaces the same block as edt_outer_step_sharded (EDT_LM/diloco.py:238-289). */
+int edt_outer_step_sharded_ordered(void* comm, void* theta_g, int gdt, const void* const* theta_k, int wdt,
+                                   int K_local, void* momentum_shard, int has_momentum, uint64_t n_pad,
+                                   uint64_t bucket_elems, double lr, double momentum_coef, int nesterov,
+                                   float* acc, float* recv, void* stream);
+
 const char* edt_comm_last_error(void);
 
 #ifdef __cplusplus

@@ -420,7 +420,11 @@ def test_comm_abi_world1_collectives(dev):
 
 
 @pytest.mark.parametrize("wdt", [torch.float32, torch.bfloat16])
-def test_comm_abi_sharded_outer_step_world1(dev, wdt):
+@pytest.mark.parametrize("ordered", [False, True])
+def test_comm_abi_sharded_outer_step_world1(dev, wdt, ordered):
+    """edt_outer_step_sharded (reduce) and edt_outer_step_sharded_ordered (reduce_ordered: the
+    partials' all-to-all + edt_sgd_apply_sum) at world 1: bit-exact with the fused step over the
+    whole population, over several buckets and a padded tail."""
     from evolutionarydistributedtraining_amd import ops
     from evolutionarydistributedtraining_amd.comm import Comm
     n, n_pad, K = 100_003, 100_032, 5                      # n_pad: a multiple of 64 (world 1)
@@ -434,11 +438,15 @@ def test_comm_abi_sharded_outer_step_world1(dev, wdt):
         workers.append(w)
     ref_t, ref_m = theta0.clone(), torch.zeros(n_pad, device=dev)
     th, mom, acc = theta0.clone(), torch.zeros(n_pad, device=dev), torch.empty(n_pad, device=dev)
+    recv = torch.empty(n_pad, device=dev)
     c = Comm(Comm.unique_id(), 1, 0)
     try:
         for has in (False, True, True):
             ops.outer_step(ref_t, workers, ref_m, has, 0.7, 0.9, True)
-            c.outer_step_sharded(th, workers, mom, has, 0.7, 0.9, True, acc, bucket_elems=16_384)
+            if ordered:
+                c.outer_step_sharded_ordered(th, workers, mom, has, 0.7, 0.9, True, acc, recv, bucket_elems=16_384)
+            else:
+                c.outer_step_sharded(th, workers, mom, has, 0.7, 0.9, True, acc, bucket_elems=16_384)
         torch.cuda.synchronize()
     finally:
         c.close()
