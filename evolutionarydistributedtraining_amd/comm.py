@@ -33,6 +33,8 @@ SIGNATURES = [
                                     _P, _P]),
     ("edt_outer_step_sharded_ordered", _I, [_P, _P, _I, ctypes.POINTER(_P), _I, _I, _P, _I, _U64, _U64, _D, _D,
                                             _I, _P, _P, _P]),
+    ("edt_outer_step_sharded_exact", _I, [_P, _P, _I, ctypes.POINTER(_P), _I, _I, _P, _I, _U64, _U64, _D, _D,
+                                          _I, ctypes.POINTER(_P), _P]),
     ("edt_comm_abort", _I, [_P]),
     ("edt_comm_poll", _I, [_P]),
     ("edt_comm_wait", _I, [_P, _P, _D]),
@@ -178,3 +180,19 @@ class Comm:
             L.ptr(momentum_shard) if momentum_shard is not None else None, int(has_momentum), n, bucket_elems,
             float(lr), float(momentum_coef), int(nesterov), L.ptr(acc), L.ptr(recv), self._stream(theta)),
             "edt_outer_step_sharded_ordered")
+
+    def outer_step_sharded_exact(self, theta: torch.Tensor, workers: list[torch.Tensor],
+                                 momentum_shard: torch.Tensor | None, has_momentum: bool, lr: float,
+                                 momentum_coef: float, nesterov: bool, recv: list[torch.Tensor],
+                                 bucket_elems: int = 1 << 26) -> None:
+        """edt_outer_step_sharded_exact (the exact schedule, theta broadcast): recv holds one
+        padded buffer of the workers' dtype per local worker, where their all-to-alls land."""
+        n = theta.numel()
+        L.require_device(theta, *workers, *recv, *([momentum_shard] if momentum_shard is not None else []))
+        if len(recv) != len(workers) or any(t.numel() != n or t.dtype != workers[0].dtype for t in workers + recv):
+            raise L.EdtError("workers / recv must match the padded theta, one receive buffer per worker")
+        _check(load_comm_library().edt_outer_step_sharded_exact(
+            self._h, L.ptr(theta), L.dtype_code(theta), L.ptr_array(workers), L.dtype_code(workers[0]), len(workers),
+            L.ptr(momentum_shard) if momentum_shard is not None else None, int(has_momentum), n, bucket_elems,
+            float(lr), float(momentum_coef), int(nesterov), L.ptr_array(recv), self._stream(theta)),
+            "edt_outer_step_sharded_exact")

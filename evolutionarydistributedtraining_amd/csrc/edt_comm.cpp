@@ -1,6 +1,7 @@
 // edt_comm.cpp — RCCL (over xGMI) behind the C ABI of include/edt_comm.h, and the bucketed
-// DiLoCo schedules in C (distributed.py mode="reduce" and "reduce_ordered"): host code only, the
-// kernels are libedt_sync's edt_delta_partial / edt_sgd_apply / edt_sgd_apply_sum.
+// DiLoCo schedules in C (distributed.py mode="reduce", "reduce_ordered" and "exact"): host code
+// only, the kernels are libedt_sync's edt_delta_partial / edt_sgd_apply / edt_sgd_apply_sum /
+// edt_outer_step.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -366,6 +367,79 @@ int edt_outer_step_sharded_ordered(void* comm, void* theta_g, int gdt, const voi
         int rc = edt_sgd_apply_sum(th + s0 * gsz, gdt, parts.data(), c->nranks, momentum_coef != 0 ? mom : nullptr,
                                    has_momentum, per, lr, momentum_coef, nesterov, s);
         if (rc) return fail(EDT_COMM_ERR_ARG, "edt_sgd_apply_sum: %s", edt_last_error());
+        mom_off += per;
+        EDT_HIP(hipEventRecord(c->events[2 * i], s));
+        EDT_HIP(hipStreamWaitEvent(c->side, c->events[2 * i], 0));
+        EDT_RCCL(ncclAllGather(th + s0 * gsz, th + b * gsz, per, gt, c->nccl, c->side));
+    }
+    EDT_HIP(hipEventRecord(c->events[2 * nb], c->side));
+    EDT_HIP(hipStreamWaitEvent(s, c->events[2 * nb], 0));
+    if (c->timeout_s > 0) return wait_event(c, c->events[2 * nb], c->timeout_s);
+    return 0;
+}
+
+int edt_outer_step_sharded_exact(void* comm, void* theta_g, int gdt, const void* const* theta_k, int wdt,
+                                 int K_local, void* momentum_shard, int has_momentum, uint64_t n_pad,
+                                 uint64_t bucket_elems, double lr, double momentum_coef, int nesterov,
+                                 void* const* recv, void* stream) {
+    Comm* c = as_comm(comm);
+    ncclDataType_t gt, wt;
+    uint64_t gsz, wsz;
+    if (int rc = usable(c)) return rc;
+    if (!theta_g || !theta_k || !recv) return fail(EDT_COMM_ERR_ARG, "null buffer");
+    if (!nccl_type(gdt, &gt, &gsz) || !nccl_type(wdt, &wt, &wsz)) return fail(EDT_COMM_ERR_ARG, "dtype pair %d/%d", gdt, wdt);
+    if (K_local < 1 || (int64_t)K_local * c->nranks > EDT_MAX_WORKERS)
+        return fail(EDT_COMM_ERR_ARG, "K_local %d x %d ranks: the fused step takes at most %d workers", K_local,
+                    c->nranks, EDT_MAX_WORKERS);
+    for (int j = 0; j < K_local; ++j)
+        if (!theta_k[j] || !recv[j]) return fail(EDT_COMM_ERR_ARG, "worker %d: null arena or receive buffer", j);
+    const uint64_t unit = (uint64_t)c->nranks * 64;
+    if (n_pad % unit) return fail(EDT_COMM_ERR_ARG, "n_pad %llu is not a multiple of nranks x 64",
+                                  (unsigned long long)n_pad);
+    if (momentum_coef != 0 && !momentum_shard) return fail(EDT_COMM_ERR_ARG, "momentum shard is null");
+    uint64_t bucket = bucket_elems / unit * unit;
+    if (bucket < unit) bucket = unit;
+    if (bucket > n_pad) bucket = n_pad;
+    const uint64_t nb = n_pad ? (n_pad + bucket - 1) / bucket : 0;
+    if (int rc = ensure_events(c, 2 * nb + 2)) return rc;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int K_total = K_local * c->nranks;
+    char* th = static_cast<char*>(theta_g);
+    // phase 1 (side stream, after the caller's work on the arenas): every bucket's all-to-all, one
+    // per local worker, straight from the arenas — a worker's bucket is already laid out
+    // [dest rank][shard] and arrives in recv[j] as [src rank][shard]
+    EDT_HIP(hipEventRecord(c->events[2 * nb + 1], s));
+    EDT_HIP(hipStreamWaitEvent(c->side, c->events[2 * nb + 1], 0));
+    for (uint64_t i = 0; i < nb; ++i) {
+        const uint64_t b = i * bucket, e = b + bucket < n_pad ? b + bucket : n_pad, per = (e - b) / c->nranks;
+        EDT_RCCL(ncclGroupStart());
+        for (int j = 0; j < K_local; ++j) {
+            ncclResult_t r = ncclAllToAll(static_cast<const char*>(theta_k[j]) + b * wsz,
+                                          static_cast<char*>(recv[j]) + b * wsz, per, wt, c->nccl, c->side);
+            if (r != ncclSuccess) {
+                (void)ncclGroupEnd();
+                return fail(EDT_COMM_ERR_RCCL, "ncclAllToAll worker %d: %s", j, ncclGetErrorString(r));
+            }
+        }
+        EDT_RCCL(ncclGroupEnd());
+        EDT_HIP(hipEventRecord(c->events[2 * i + 1], c->side));
+    }
+    // phase 2: as each bucket lands, the single-GPU fused step on the owned shard with the K_total
+    // workers in the reference's order (global worker k = src rank x K_local + j): bit-exact with
+    // edt_outer_step over the whole population; then the shard's all-gather into theta
+    std::vector<const void*> shards(K_total);
+    uint64_t mom_off = 0;
+    for (uint64_t i = 0; i < nb; ++i) {
+        const uint64_t b = i * bucket, e = b + bucket < n_pad ? b + bucket : n_pad, per = (e - b) / c->nranks;
+        const uint64_t s0 = b + (uint64_t)c->rank * per;
+        for (int src = 0; src < c->nranks; ++src)
+            for (int j = 0; j < K_local; ++j)
+                shards[src * K_local + j] = static_cast<const char*>(recv[j]) + (b + (uint64_t)src * per) * wsz;
+        EDT_HIP(hipStreamWaitEvent(s, c->events[2 * i + 1], 0));
+        void* mom = momentum_shard ? static_cast<char*>(momentum_shard) + mom_off * gsz : nullptr;
+        int rc = edt_outer_step(th + s0 * gsz, gdt, shards.data(), wdt, K_total, momentum_coef != 0 ? mom : nullptr,
+                                has_momentum, per, lr, momentum_coef, nesterov, s);
+        if (rc) return fail(EDT_COMM_ERR_ARG, "edt_outer_step: %s", edt_last_error());
         mom_off += per;
         EDT_HIP(hipEventRecord(c->events[2 * i], s));
         EDT_HIP(hipStreamWaitEvent(c->side, c->events[2 * i], 0));

@@ -105,6 +105,19 @@ int edt_outer_step_sharded_ordered(void* comm, void* theta_g, int gdt, const voi
                                    uint64_t bucket_elems, double lr, double momentum_coef, int nesterov,
                                    float* acc, float* recv, void* stream);
 
+/* The same step, exact schedule (distributed.py mode="exact", broadcast="theta"): per bucket one
+ * all-to-all per local worker straight from the worker arenas into recv[j] (a worker's bucket is
+ * already laid out [dest rank][shard]; it arrives as [src rank][shard]), then edt_outer_step on
+ * the owned shard with the K_local x nranks workers in the reference's order (global worker
+ * k = src rank x K_local + j) — bit-exact with edt_outer_step over the whole population — then
+ * the shard's all-gather into theta_g. Wire bytes per rank (nranks-1)/nranks x n_pad x
+ * (K_local x wdt + gdt bytes): fewer than the reduce schedules when K_local x wdt bytes < 4.
+ * recv: K_local device buffers of n_pad elements of wdt. K_local x nranks <= EDT_MAX_WORKERS. */
+int edt_outer_step_sharded_exact(void* comm, void* theta_g, int gdt, const void* const* theta_k, int wdt,
+                                 int K_local, void* momentum_shard, int has_momentum, uint64_t n_pad,
+                                 uint64_t bucket_elems, double lr, double momentum_coef, int nesterov,
+                                 void* const* recv, void* stream);
+
 const char* edt_comm_last_error(void);
 
 #ifdef __cplusplus

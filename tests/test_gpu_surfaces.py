@@ -420,10 +420,11 @@ def test_comm_abi_world1_collectives(dev):
 
 
 @pytest.mark.parametrize("wdt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("ordered", [False, True])
-def test_comm_abi_sharded_outer_step_world1(dev, wdt, ordered):
-    """edt_outer_step_sharded (reduce) and edt_outer_step_sharded_ordered (reduce_ordered: the
-    partials' all-to-all + edt_sgd_apply_sum) at world 1: bit-exact with the fused step over the
+@pytest.mark.parametrize("schedule", ["reduce", "ordered", "exact"])
+def test_comm_abi_sharded_outer_step_world1(dev, wdt, schedule):
+    """edt_outer_step_sharded (reduce), edt_outer_step_sharded_ordered (reduce_ordered: the
+    partials' all-to-all + edt_sgd_apply_sum) and edt_outer_step_sharded_exact (the workers'
+    all-to-all + the fused step per shard) at world 1: bit-exact with the fused step over the
     whole population, over several buckets and a padded tail."""
     from evolutionarydistributedtraining_amd import ops
     from evolutionarydistributedtraining_amd.comm import Comm
@@ -439,12 +440,15 @@ def test_comm_abi_sharded_outer_step_world1(dev, wdt, ordered):
     ref_t, ref_m = theta0.clone(), torch.zeros(n_pad, device=dev)
     th, mom, acc = theta0.clone(), torch.zeros(n_pad, device=dev), torch.empty(n_pad, device=dev)
     recv = torch.empty(n_pad, device=dev)
+    recv_w = [torch.empty(n_pad, dtype=wdt, device=dev) for _ in range(K)]
     c = Comm(Comm.unique_id(), 1, 0)
     try:
         for has in (False, True, True):
             ops.outer_step(ref_t, workers, ref_m, has, 0.7, 0.9, True)
-            if ordered:
+            if schedule == "ordered":
                 c.outer_step_sharded_ordered(th, workers, mom, has, 0.7, 0.9, True, acc, recv, bucket_elems=16_384)
+            elif schedule == "exact":
+                c.outer_step_sharded_exact(th, workers, mom, has, 0.7, 0.9, True, recv_w, bucket_elems=16_384)
             else:
                 c.outer_step_sharded(th, workers, mom, has, 0.7, 0.9, True, acc, bucket_elems=16_384)
         torch.cuda.synchronize()

@@ -150,7 +150,7 @@ def test_comm_library_exports_every_header_symbol():
     with open(os.path.join(ROOT, "include", "edt_comm.h")) as f:
         header = f.read()
     names = set(re.findall(r"^\s*(?:int|uint64_t|const char\*)\s+(edt_\w+)\s*\(", header, re.M))
-    assert len(names) == 17, names
+    assert len(names) == 18, names
     assert names == {n for n, _, _ in comm.SIGNATURES}
     for n in names:
         assert hasattr(lib, n), n
