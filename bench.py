@@ -591,8 +591,8 @@ def main():
                     "ms_per_step": round(w_ms, 4), "value": round(w_bytes / (w_ms / 1e3) / 1e9, 2),
                     "unit": "GB/s", "schedule": w_sched, "wire_bytes_per_rank": w_wire,
                     "note": "companion measurement after the timed strong-scaling steps; not the value"}
-        except torch.cuda.OutOfMemoryError as e:     # the value is already measured: report, go on
-            weak = {"error": f"OutOfMemoryError: {str(e)[:200]}"}
+        except Exception as e:     # the value is already measured: report, go on
+            weak = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
             torch.cuda.empty_cache()
         sync = None
     population = None
@@ -603,8 +603,8 @@ def main():
         try:
             from evolutionarydistributedtraining_amd.collectives import TorchCollectives
             population = bench_population(args, dev, TorchCollectives())
-        except torch.cuda.OutOfMemoryError as e:
-            population = {"error": f"OutOfMemoryError: {str(e)[:200]}"}
+        except Exception as e:     # an extra after the value: report it, keep the line
+            population = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
             torch.cuda.empty_cache()
 
     if rank == 0:
