@@ -179,6 +179,10 @@ static void comm_host_paths(void) {
     EXPECT(edt_comm_reduce_scatter_f32(NULL, NULL, NULL, 4, NULL) == EDT_COMM_ERR_ARG);
     EXPECT(edt_outer_step_sharded(NULL, NULL, 0, NULL, 0, 1, NULL, 0, 64, 64, 0.7, 0.9, 1, NULL, NULL) ==
            EDT_COMM_ERR_ARG);
+    EXPECT(edt_outer_step_sharded_ordered(NULL, NULL, 0, NULL, 0, 1, NULL, 0, 64, 64, 0.7, 0.9, 1, NULL, NULL,
+                                          NULL) == EDT_COMM_ERR_ARG);
+    EXPECT(edt_outer_step_sharded_exact(NULL, NULL, 0, NULL, 0, 1, NULL, 0, 64, 64, 0.7, 0.9, 1, NULL, NULL) ==
+           EDT_COMM_ERR_ARG);
     EXPECT(edt_comm_last_error()[0] != 0);
     char id[128];
     void* comm = NULL;
