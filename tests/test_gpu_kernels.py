@@ -593,6 +593,21 @@ def test_c_consumer_runs():
     assert "abi consumer ok" in r.stdout
 
 
+def test_c_comm_consumer_runs():
+    """The plain-C multi-GPU master over include/edt_comm.h (tests/c_abi/comm_consumer.c) at world
+    size 1: unique id, init, two outer steps with each of the three sharded schedules (reduce,
+    reduce_ordered, exact) bit-exact against the C oracle, then the abort path."""
+    import subprocess
+    exe = os.path.join(ROOT, "tests", "c_abi", "_build", "comm_consumer")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.dirname(os.path.dirname(exe))], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120, cwd="/")
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "comm consumer ok" in r.stdout
+    for name in ("reduce", "reduce_ordered", "exact"):
+        assert f"{name}: bit-exact with the oracle" in r.stdout
+
+
 # ------------------------------------------------------------------------------------------
 # torch CPU scalar-tail emulation (edt_outer_step_tail / edt_pair_merge_tail): with the reference
 # host's tail elements, the bf16 regime is bit-exact with the reference on EVERY element

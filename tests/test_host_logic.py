@@ -168,6 +168,11 @@ def test_c_consumer_builds_and_links():
                          check=True, cwd="/").stdout
     assert "not found" not in out, out
     assert "libedt_sync.so" in out and "libamdhip64" in out
+    # the plain-C multi-GPU master (include/edt_comm.h): libedt_comm.so and RCCL behind it
+    out = subprocess.run(["ldd", os.path.join(d, "_build", "comm_consumer")], capture_output=True, text=True,
+                         check=True, cwd="/").stdout
+    assert "not found" not in out, out
+    assert "libedt_comm.so" in out and "librccl" in out
 
 
 def test_chunk_table_host_function():
