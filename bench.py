@@ -93,6 +93,9 @@ def parse():
                    help="the other hot-path measurements in the same line ('none': skip): N=1 pair_merge, "
                         "slerp_7b; N>1 population_7b (BASELINE configs[4] across the N GPUs)")
     p.add_argument("--ops-cpu-seconds", type=float, default=4.0, help="CPU baseline budget per extra op")
+    p.add_argument("--population-groups", type=int, default=4,
+                   help="N>1 population_7b: also time the link-balanced crossover with its exchanges "
+                        "pipelined over this many chunk groups per rank (1: only the unpipelined form)")
     p.add_argument("--bcast-compare", type=int, default=1,
                    help="N=1: also time the step fused with the worker broadcast against step + K copies")
     p.add_argument("--dry-run-launch", action="store_true",
@@ -362,8 +365,9 @@ def bench_population(args, dev, comm, layout_name="qwen2p5_7b_body"):
     """BASELINE configs[4] at N > 1: a population of N members (one 7.07B bf16 body per GPU,
     qwen2p5_7b_body) SLERP-crossed into N children (t = 0.5, far parents: the SLERP branch), timed
     link-balanced (distributed.ShardedPopulationCrossover: chunk-range shards of every member,
-    Gram rows all-gathered, children gathered back) and per child (PopulationCrossover: each
-    child's two parents shipped whole). Max over ranks; every rank of `comm` takes part."""
+    Gram rows all-gathered, children gathered back), the same with its exchanges pipelined over
+    chunk groups (`sharded_pipelined`), and per child (PopulationCrossover: each child's two parents
+    shipped whole). Max over ranks; every rank of `comm` takes part."""
     from evolutionarydistributedtraining_amd.distributed import PopulationCrossover, ShardedPopulationCrossover
     from evolutionarydistributedtraining_amd.layouts import LAYOUTS
     lay = LAYOUTS[layout_name]()
@@ -391,15 +395,18 @@ def bench_population(args, dev, comm, layout_name="qwen2p5_7b_body"):
         torch.cuda.synchronize()
         comm.barrier()
         return max(comm.all_gather_object((time.perf_counter() - t0) / n * 1e3))
-    sp = ShardedPopulationCrossover(lay, bf, dev, kind="slerp", comm=comm)
-    ms = timed(lambda: sp.slerp_step(member, pairs, t, out), max(3, args.steps // 4))
     wire = 2 * (world - 1) * (P * 2 // world)            # members out + children out, per rank
     peak = XGMI_LINK_GBPS * (world - 1)
-    res["sharded"] = {"ms": round(ms, 3), "wire_bytes_per_rank": wire,
-                      "xgmi": {"achieved": round(wire / (ms / 1e3) / 1e9, 1), "peak": peak, "unit": "GB/s",
-                               "frac": round(wire / (ms / 1e3) / 1e9 / peak, 4)}}
-    del sp
-    torch.cuda.empty_cache()
+    for key, groups in (("sharded", 1), ("sharded_pipelined", args.population_groups)):
+        if groups < 1 or (key == "sharded_pipelined" and groups == 1):
+            continue
+        sp = ShardedPopulationCrossover(lay, bf, dev, kind="slerp", comm=comm, groups=groups)
+        ms = timed(lambda: sp.slerp_step(member, pairs, t, out), max(3, args.steps // 4))
+        res[key] = {"ms": round(ms, 3), "groups": groups, "wire_bytes_per_rank": wire,
+                    "xgmi": {"achieved": round(wire / (ms / 1e3) / 1e9, 1), "peak": peak, "unit": "GB/s",
+                             "frac": round(wire / (ms / 1e3) / 1e9 / peak, 4)}}
+        del sp
+        torch.cuda.empty_cache()
     pc = PopulationCrossover(lay, bf, dev, comm=comm)
     res["per_child"] = {"ms": round(timed(lambda: pc.slerp_step(member, pairs, t, out), 3), 3)}
     del pc, member, out

@@ -44,6 +44,18 @@ class _Done:
         return True
 
 
+class _Works:
+    """Several handles waited as one."""
+
+    def __init__(self, works):
+        self.works = works
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        return True
+
+
 class _TorchWork:
     """RCCL: wait() only orders the current stream after the collective (a host-blocking
     wait with a timeout would serialise the bucket pipeline); its timeout is the RCCL
@@ -78,9 +90,10 @@ class Collectives:
     def all_to_all(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
         raise NotImplementedError
 
-    def p2p(self, ops: list[tuple[str, torch.Tensor, int]]) -> None:
+    def p2p(self, ops: list[tuple[str, torch.Tensor, int]], async_op: bool = False):
         """A grouped exchange: ("send" | "recv", tensor, peer rank); returns when all are done
-        (stream-ordered for device backends)."""
+        (stream-ordered for device backends), or with async_op a handle whose wait() orders the
+        current stream after it (several exchanges can then be in flight at once)."""
         raise NotImplementedError
 
     def all_gather_object(self, obj) -> list:
@@ -132,13 +145,16 @@ class TorchCollectives(Collectives):
     def _global(self, r):
         return r if self.group is None else self.dist.get_global_rank(self.group, r)
 
-    def p2p(self, ops):
+    def p2p(self, ops, async_op=False):
         d = self.dist
         reqs = [d.P2POp(d.isend if kind == "send" else d.irecv, t, self._global(peer), self.group)
                 for kind, t, peer in ops]
-        if reqs:
-            for w in d.batch_isend_irecv(reqs):
-                _TorchWork(w, self.timeout, self.inplace).wait()
+        works = [_TorchWork(w, self.timeout, self.inplace) for w in d.batch_isend_irecv(reqs)] if reqs else []
+        handle = _Works(works)
+        if async_op:
+            return handle
+        handle.wait()
+        return _Done()
 
     def all_gather_object(self, obj):
         out = [None] * self.world
@@ -275,7 +291,7 @@ class VirtualCollectives(Collectives):
         self.vw.rendezvous(self.rank, (out, inp), combine)
         return _Done()
 
-    def p2p(self, ops):
+    def p2p(self, ops, async_op=False):
         for kind, _, peer in ops:
             if kind not in ("send", "recv") or not 0 <= peer < self.world:
                 raise EdtError(f"bad p2p op {kind} to {peer}")
@@ -300,6 +316,7 @@ class VirtualCollectives(Collectives):
             if left:
                 raise EdtError(f"virtual p2p: unmatched sends {left}")
         self.vw.rendezvous(self.rank, list(ops), combine)
+        return _Done()
 
     def all_gather_object(self, obj):
         return copy.deepcopy(self.vw.rendezvous(self.rank, obj, lambda items: list(items)))

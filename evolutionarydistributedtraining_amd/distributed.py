@@ -403,11 +403,17 @@ class ShardedPopulationCrossover:
     EDT-LM), spread over all N-1 links, against up to two whole members over one or two links.
     Reference: EDT_RL/edt.py:286-299 (the master merges pair after pair), EDT_EVOMERGE/edt.py:262-280.
     A rank's range starts at a multiple of 8 elements below its first chunk (<= 7 elements shared
-    with the previous rank), so every chunk keeps its vector alignment and hence its sums."""
+    with the previous rank), so every chunk keeps its vector alignment and hence its sums.
+
+    groups > 1 (SLERP): every rank's range is cut into that many groups of whole chunks and the
+    exchanges run per group, all of a phase's groups in flight at once: the Gram pass of group g
+    starts as soon as g's member slices have landed (while later groups are still on the links),
+    and group g of the children leaves as soon as its blend is done (while later groups blend).
+    Same bytes, same kernels on the same chunks: the children are bit-identical to groups = 1."""
 
     def __init__(self, layout: ParamLayout, dtype: torch.dtype, device, kind: str = "slerp",
                  out_dtype: torch.dtype | None = None, comm: Collectives | None = None, group=None,
-                 kernels=None, chunk_elems: int = 1 << 16):
+                 kernels=None, chunk_elems: int = 1 << 16, groups: int = 1):
         if kind not in ("slerp", "sgd"):
             raise ValueError(kind)
         self.comm = comm or TorchCollectives(group)
@@ -433,6 +439,22 @@ class ShardedPopulationCrossover:
             else:
                 start = end = int(host[c0, 0]) if c0 < len(host) else n
             self.ranges.append((c0, c1, start // 8 * 8, start, end))
+        if groups < 1:
+            raise ValueError(groups)
+        # per rank: its chunk range in `groups` contiguous groups (fewer when it has fewer chunks),
+        # each (first chunk, end chunk, lo, hi) with [lo, hi) the elements a group carries: the
+        # first group from the rank's aligned base, the others from their first chunk's start
+        self.granges = []
+        for r in range(N):
+            a, b, rbase = self.ranges[r][0], self.ranges[r][1], self.ranges[r][2]
+            G = min(groups, b - a)
+            gl = []
+            for g in range(G):
+                g0, g1 = a + (b - a) * g // G, a + (b - a) * (g + 1) // G
+                lo = rbase if g == 0 else int(host[g0, 0])
+                gl.append((g0, g1, lo, int(host[g1 - 1, 0] + host[g1 - 1, 1])))
+            self.granges.append(gl)
+        self.groups = groups
         c0, c1, base, start, end = self.ranges[self.rank]
         self.nloc = c1 - c0
         self.base, self.start, self.end = base, start, end
@@ -485,6 +507,47 @@ class ShardedPopulationCrossover:
                 ops_.extend(("recv", out[st:en], j) for out in outs)
         self.comm.p2p(ops_)
 
+    def _scatter_groups(self, member, tag):
+        """_scatter of one tensor, one grouped exchange per chunk group, all issued at once.
+        Returns (buffers per rank j, one handle per group)."""
+        L = self.end - self.base
+        got = {j: self._buf((tag, 0, j), member.dtype)[:L] for j in range(self.world)}
+        mine = self.granges[self.rank]
+        handles = []
+        for g in range(self.groups):
+            ops_ = []
+            for s_ in range(self.world):
+                if s_ != self.rank and g < len(self.granges[s_]):
+                    _, _, lo, hi = self.granges[s_][g]
+                    ops_.append(("send", member[lo:hi], s_))
+            if g < len(mine):
+                _, _, lo, hi = mine[g]
+                ops_.extend(("recv", got[j][lo - self.base:hi - self.base], j)
+                            for j in range(self.world) if j != self.rank)
+            handles.append(self.comm.p2p(ops_, async_op=True))
+        got[self.rank].copy_(member[self.base:self.end])
+        return got, handles
+
+    def _gather_group(self, g, outs, out):
+        """Group g of this rank's range of every child q to rank q, and group g of every other
+        rank's range of this rank's child into `out` (issued, not waited)."""
+        ops_ = []
+        mine = self.granges[self.rank]
+        if g < len(mine):
+            _, _, lo, hi = mine[g]
+            lo = max(lo, self.start)
+            for q in range(self.world):
+                if q == self.rank:
+                    out[lo:hi].copy_(outs[q][lo - self.base:hi - self.base])
+                else:
+                    ops_.append(("send", outs[q][lo - self.base:hi - self.base], q))
+        for j in range(self.world):
+            if j != self.rank and g < len(self.granges[j]):
+                _, _, lo, hi = self.granges[j][g]
+                lo = max(lo, self.ranges[j][3])
+                ops_.append(("recv", out[lo:hi], j))
+        return self.comm.p2p(ops_, async_op=True)
+
     @traced("edt/ShardedPopulationCrossover.slerp_step")
     def slerp_step(self, member: torch.Tensor, pairs, t: torch.Tensor, out: torch.Tensor,
                    dot_threshold: float = 0.9995, eps: float = 1e-8) -> torch.Tensor:
@@ -492,16 +555,26 @@ class ShardedPopulationCrossover:
         if len(pairs) != self.world:
             raise ValueError(f"{len(pairs)} children for {self.world} ranks")
         k, N = self.kernels, self.world
-        sh = self._scatter([member], "m")
-        members = [sh[j][0] for j in range(N)]
         NT = N * (N + 1) // 2
         gram = self._bufs.get("gram")
         if gram is None:
             gram = self._bufs["gram"] = torch.empty((max(1, self.plan.nchunks), NT), dtype=torch.float64,
                                                     device=self.device)
         c0, c1 = self.ranges[self.rank][:2]
-        if self.nloc:
-            k.slerp_gram(members, self.local_chunks, self.nloc, gram[c0:c1])
+        mine = self.granges[self.rank]
+        if self.groups > 1:
+            sh, handles = self._scatter_groups(member, "m")
+            members = [sh[j] for j in range(N)]
+            for g, h in enumerate(handles):
+                h.wait()
+                if g < len(mine):
+                    g0, g1 = mine[g][0] - c0, mine[g][1] - c0
+                    k.slerp_gram(members, self.local_chunks[g0:g1], g1 - g0, gram[c0 + g0:c0 + g1])
+        else:
+            sh = self._scatter([member], "m")
+            members = [sh[j][0] for j in range(N)]
+            if self.nloc:
+                k.slerp_gram(members, self.local_chunks, self.nloc, gram[c0:c1])
         ops_ = []                       # all-gather of the Gram rows: every rank's chunk range
         for s in range(N):
             if s != self.rank and self.nloc:
@@ -513,6 +586,17 @@ class ShardedPopulationCrossover:
         self.comm.p2p(ops_)
         coef, dots = k.slerp_gram_coef(self.plan, gram, N, pairs, t, dot_threshold, eps)
         outs = [self._buf(("c", q), self.out_dtype)[:self.end - self.base] for q in range(N)]
+        if self.groups > 1:
+            handles = []
+            for g in range(self.groups):
+                if g < len(mine):
+                    g0, g1 = mine[g][0] - c0, mine[g][1] - c0
+                    k.slerp_blend_children(members, pairs, outs, self.local_chunks[g0:g1], g1 - g0, coef,
+                                           self.plan.nseg)
+                handles.append(self._gather_group(g, outs, out))
+            for h in handles:
+                h.wait()
+            return dots
         if self.nloc:
             k.slerp_blend_children(members, pairs, outs, self.local_chunks, self.nloc, coef, self.plan.nseg)
         self._gather_children([[o] for o in outs], [out])

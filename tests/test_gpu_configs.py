@@ -129,7 +129,8 @@ def test_config3_1p3b_all_bf16_world8(dev):
             assert bool(((theta.float() - th.float()).abs() <= reduce_tol(th, mom, bf, gens=gens)).all()), r
 
 
-def test_config4_7b_population_world2(dev):
+@pytest.mark.parametrize("groups", [1, 4])
+def test_config4_7b_population_world2(dev, groups):
     """configs[4] at the 7.07B Qwen2.5 body: 2 virtual ranks, one bf16 member each, far parents
     (the SLERP branch) and a self-pair; every child bit-identical to edt_slerp_merge on its two
     parents."""
@@ -151,7 +152,7 @@ def test_config4_7b_population_world2(dev):
     t = torch.rand(len(lay), dtype=torch.float64, device=dev, generator=gen)
 
     def body(comm):
-        sp = ShardedPopulationCrossover(lay, bf, dev, comm=comm)
+        sp = ShardedPopulationCrossover(lay, bf, dev, comm=comm, groups=groups)
         out = torch.empty(P, dtype=bf, device=dev)
         sp.slerp_step(members[comm.rank], pairs, t, out)
         torch.cuda.synchronize()

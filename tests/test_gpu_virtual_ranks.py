@@ -116,7 +116,8 @@ def test_population_crossover_on_virtual_ranks(world):
 
 @pytest.mark.parametrize("world", [2, 4, 8])
 @pytest.mark.parametrize("out_dt", [torch.float32, torch.bfloat16])
-def test_sharded_population_slerp_on_virtual_ranks(world, out_dt):
+@pytest.mark.parametrize("groups", [1, 3])
+def test_sharded_population_slerp_on_virtual_ranks(world, out_dt, groups):
     """The link-balanced population SLERP (each rank: a range of whole chunks of all members, Gram
     rows all-gathered, its range of every child blended and sent to the child's rank) with the HIP
     passes: every child bit-identical to edt_slerp_merge on its two parents, and the dots too."""
@@ -132,7 +133,8 @@ def test_sharded_population_slerp_on_virtual_ranks(world, out_dt):
     t = torch.tensor([0.3, 0.5, 0.9, 0.5, 0.43, 0.7, 0.5, 0.6], dtype=torch.float64, device=DEV)
 
     def body(comm):
-        sp = ShardedPopulationCrossover(layout, torch.bfloat16, DEV, kind="slerp", out_dtype=out_dt, comm=comm)
+        sp = ShardedPopulationCrossover(layout, torch.bfloat16, DEV, kind="slerp", out_dtype=out_dt, comm=comm,
+                                        groups=groups)
         out = torch.full((n,), float("nan"), dtype=out_dt, device=DEV)
         dots = sp.slerp_step(members[comm.rank], pairs, t, out)
         return out, dots.clone()
@@ -186,10 +188,11 @@ def test_bench_population_measurement_on_virtual_ranks():
     import types
 
     import bench
-    args = types.SimpleNamespace(steps=4)
+    args = types.SimpleNamespace(steps=4, population_groups=4)
     res = VirtualWorld(4).run(lambda comm: bench.bench_population(args, DEV, comm, "gpt2_small"))
     for r in res:
         assert r["sharded"]["ms"] > 0 and r["per_child"]["ms"] > 0
+        assert r["sharded_pipelined"]["ms"] > 0 and r["sharded_pipelined"]["groups"] == 4
         assert r["sharded"]["wire_bytes_per_rank"] == 2 * 3 * (124439808 * 2 // 4)
 
 

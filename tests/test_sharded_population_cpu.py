@@ -38,12 +38,13 @@ def _whole(kern, layout, members, pairs, t):
     return outs, dots
 
 
-def _run(comm, layout, members, pairs, t, oracle, kind):
+def _run(comm, layout, members, pairs, t, oracle, kind, groups=1):
     from evolutionarydistributedtraining_amd.distributed import ShardedPopulationCrossover
     from tests.oracle_kernels import ChunkGramKernels
     r = comm.rank
     sp = ShardedPopulationCrossover(layout, torch.bfloat16, "cpu", kind=kind, out_dtype=torch.float32 if kind == "slerp"
-                                    else torch.bfloat16, comm=comm, kernels=ChunkGramKernels(oracle), chunk_elems=CHUNK)
+                                    else torch.bfloat16, comm=comm, kernels=ChunkGramKernels(oracle), chunk_elems=CHUNK,
+                                    groups=groups)
     if kind == "slerp":
         out = torch.full((layout.total,), float("nan"))
         dots = sp.slerp_step(members[r], pairs, t, out)
@@ -58,13 +59,14 @@ def _run(comm, layout, members, pairs, t, oracle, kind):
 
 
 @pytest.mark.parametrize("world", [2, 3, 5, 8])
-def test_sharded_slerp_population_virtual(oracle, world):
+@pytest.mark.parametrize("groups", [1, 2, 5])     # 5: more groups than some ranks have chunks
+def test_sharded_slerp_population_virtual(oracle, world, groups):
     from tests.oracle_kernels import ChunkGramKernels
     layout = ParamLayout(SHAPES)
     members = _members(world, layout.total)
     pairs = _pairs(world)
     t = torch.tensor([0.3, 0.5, 0.9, 0.5, 0.43, 0.7, 0.5], dtype=torch.float64)
-    res = VirtualWorld(world).run(lambda comm: _run(comm, layout, members, pairs, t, oracle, "slerp"))
+    res = VirtualWorld(world).run(lambda comm: _run(comm, layout, members, pairs, t, oracle, "slerp", groups))
     want, wdots = _whole(ChunkGramKernels(oracle), layout, members, pairs, t)
     ranges = res[0][2]
     assert ranges[0][3] == 0 and ranges[-1][4] == layout.total          # the ranges tile the layout
@@ -91,7 +93,7 @@ def test_sharded_pair_merge_population_virtual(oracle, world):
         assert torch.equal(res[c][1].view(torch.int16), mom.view(torch.int16)), c
 
 
-def _gloo_worker(rank, world, port, outdir):
+def _gloo_worker(rank, world, port, outdir, groups=1):
     import torch.distributed as dist
 
     from oracle import oracle
@@ -101,18 +103,19 @@ def _gloo_worker(rank, world, port, outdir):
     layout = ParamLayout(SHAPES)
     members = _members(world, layout.total)
     t = torch.tensor([0.3, 0.5, 0.9, 0.5, 0.43, 0.7, 0.5], dtype=torch.float64)
-    out, dots, _ = _run(TorchCollectives(), layout, members, _pairs(world), t, oracle, "slerp")
+    out, dots, _ = _run(TorchCollectives(), layout, members, _pairs(world), t, oracle, "slerp", groups)
     torch.save({"out": out, "dots": dots}, os.path.join(outdir, f"s{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
 
 @pytest.mark.slow
-def test_sharded_slerp_population_gloo_world3(tmp_path, oracle):
+@pytest.mark.parametrize("groups", [1, 3])        # 3: the pipelined exchanges, async gloo p2p batches
+def test_sharded_slerp_population_gloo_world3(tmp_path, oracle, groups):
     from tests.oracle_kernels import ChunkGramKernels
     from tests.test_distributed_cpu import _free_port
     world = 3
-    mp.start_processes(_gloo_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+    mp.start_processes(_gloo_worker, args=(world, _free_port(), str(tmp_path), groups), nprocs=world, join=True,
                        start_method="spawn")
     layout = ParamLayout(SHAPES)
     t = torch.tensor([0.3, 0.5, 0.9, 0.5, 0.43, 0.7, 0.5], dtype=torch.float64)
