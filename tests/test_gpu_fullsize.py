@@ -2,7 +2,8 @@
 
 * element locality: the outer step / pair merge / lerp are element-wise, so any window of the
   1.3B-parameter arena (beyond 2^31 elements' worth of bytes: 64-bit indexing) can be checked
-  against the oracle on its own — random windows plus the arena's ragged end;
+  against the oracle on its own — random windows plus the arena's ragged end; and arenas of
+  2^32 + 4099 elements (beyond a 32-bit element index) on windows straddling 2^31 and 2^32;
 * SLERP on the Qwen2.5-7B body layout (7.07B elements, 338 segments): small segments checked
   whole against the oracle; every segment's dot against an independent fp64 torch reduction;
 * hipGraph capture/replay and cross-stream ordering give the same bits as eager launches.
@@ -73,6 +74,65 @@ def test_pair_merge_1p3b_windows(oracle, dev):
                           0.7, 0.9, True)
         assert torch.equal(bits(out[s:s + w].cpu()), bits(o)), s
         assert torch.equal(bits(mom[s:s + w].cpu()), bits(m)), s
+
+
+def _fill(n, dev, gen, scale, dtype, base=None):
+    out = torch.empty(n, dtype=dtype, device=dev)
+    for a in range(0, n, 1 << 28):
+        b = min(n, a + (1 << 28))
+        x = torch.randn(b - a, device=dev, generator=gen) * scale
+        if base is not None:
+            x += base[a:b].float()
+        out[a:b] = x.to(dtype)
+    return out
+
+
+def test_element_counts_beyond_2_32(oracle, dev):
+    """The maximum-size edge: arenas of 2^32 + 4099 elements (more than a 32-bit element index
+    holds, as the 7B body's 7.07B elements do): the outer step (fp32 theta + momentum, two bf16
+    workers), the pair merge and lerp (bf16), checked against the oracle on windows straddling
+    2^31 and 2^32 elements and on the ragged end."""
+    from evolutionarydistributedtraining_amd import ops
+    n = (1 << 32) + 4099
+    gen = torch.Generator(device=dev).manual_seed(17)
+    bf = torch.bfloat16
+    W = 4096
+    wins = [0, (1 << 31) - W // 2, (1 << 32) - W // 2, (1 << 32) - 8, n - W, n - 777]
+    widths = [min(W, n - s) for s in wins]
+    # the outer step
+    theta = _fill(n, dev, gen, 0.02, torch.float32)
+    workers = [_fill(n, dev, gen, 1e-3, bf, base=theta) for _ in range(2)]
+    mom = _fill(n, dev, gen, 1e-3, torch.float32)
+    before = [(theta[s:s + w].cpu(), [x[s:s + w].cpu() for x in workers], mom[s:s + w].cpu())
+              for s, w in zip(wins, widths)]
+    ops.outer_step(theta, workers, mom, True, 0.7, 0.9, True)
+    torch.cuda.synchronize()
+    for (s, w), (th, ws, m) in zip(zip(wins, widths), before):
+        oracle.outer_step(th, ws, m, True, 0.7, 0.9, True)
+        assert torch.equal(bits(theta[s:s + w].cpu()), bits(th)), s
+        assert torch.equal(bits(mom[s:s + w].cpu()), bits(m)), s
+    del theta, mom, before
+    torch.cuda.empty_cache()
+    # the pair merge (the two workers as bases, trained copies + a bf16 momentum) and lerp
+    b1, b2 = workers
+    m1 = _fill(n, dev, gen, 1e-3, bf, base=b1)
+    m2 = _fill(n, dev, gen, 1e-3, bf, base=b2)
+    pm = _fill(n, dev, gen, 1e-3, bf)
+    out = torch.empty(n, dtype=bf, device=dev)
+    pm_before = [pm[s:s + w].cpu() for s, w in zip(wins, widths)]
+    ops.pair_merge(b1, b2, m1, m2, out, pm, True, 0.7, 0.9, True)
+    torch.cuda.synchronize()
+    for (s, w), m in zip(zip(wins, widths), pm_before):
+        o = torch.empty(w, dtype=bf)
+        oracle.pair_merge(b1[s:s + w].cpu(), b2[s:s + w].cpu(), m1[s:s + w].cpu(), m2[s:s + w].cpu(), o, m, True,
+                          0.7, 0.9, True)
+        assert torch.equal(bits(out[s:s + w].cpu()), bits(o)), s
+        assert torch.equal(bits(pm[s:s + w].cpu()), bits(m)), s
+    ops.lerp(0.3, b1, b2, out)
+    torch.cuda.synchronize()
+    for s, w in zip(wins, widths):
+        want = oracle.lerp(0.3, b1[s:s + w].cpu(), b2[s:s + w].cpu())
+        assert torch.equal(bits(out[s:s + w].cpu()), bits(want)), s
 
 
 def test_slerp_qwen7b_body(oracle, dev):
