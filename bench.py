@@ -338,6 +338,9 @@ def bench_slerp_7b(args, dev):
                                      "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBPS, 4), "bytes_per_elem": 6,
                                      "algo_bytes_per_launch": 6 * P,
                                      "moved_bytes_per_elem": 6 if spec else 10,
+                                     # the form's own bytes (two-pass: both parents read twice)
+                                     # over the time: its streaming rate against the same peak
+                                     "moved_frac": round((6 if spec else 10) * P / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
                                      "traffic": _pmc_traffic(args, f"slerp_7b/{parents}")}}
     del v0, v1, out, plan
     torch.cuda.empty_cache()
