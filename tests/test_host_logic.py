@@ -331,3 +331,18 @@ def test_torch_tail_bits_match_the_oracle_mask(oracle, threads, vec):
     bits = torch_cpu_tail_bits(numels, vec_elems=vec, num_threads=threads).numpy()
     got = np.unpackbits(bits, bitorder="little")[:mask.size]
     assert np.array_equal(got, mask) and not np.unpackbits(bits, bitorder="little")[mask.size:].any()
+
+
+def test_examples_import_and_model_runs_on_cpu():
+    """examples/diloco_sim.py and examples/edt_sim.py import without a GPU; the tiny LM and its
+    synthetic batches run on the CPU (the simulations themselves are GPU tests, test_gpu_sim.py)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "examples"))
+    import diloco_sim
+    import edt_sim  # noqa: F401
+    m = diloco_sim.TinyLM()
+    x = diloco_sim.batch(0, "cpu", size=2)
+    assert x.shape == (2, diloco_sim.CTX) and int(x.max()) < diloco_sim.VOCAB
+    assert bool((x[:, 1:] == (3 * x[:, :-1] + 1) % diloco_sim.VOCAB).all())
+    loss = diloco_sim.loss_of(m, x)
+    assert loss.ndim == 0 and float(loss) > 0
