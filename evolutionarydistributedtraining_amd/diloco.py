@@ -136,7 +136,13 @@ def _step_list(thetas: list[torch.Tensor], workers: list[list[torch.Tensor]], st
     moms = None
     if momentum != 0:
         flat = state.buffer_for(thetas[0], sum(t.numel() for t in thetas))
-        moms = ParamLayout.of(thetas).views(flat)
+        shapes = [t.shape for t in thetas]
+        cached = getattr(state, "_list_views", None)      # the per-tensor views of the buffer,
+        if cached is not None and cached[0] is flat and cached[1] == shapes:   # kept across calls
+            moms = cached[2]
+        else:
+            moms = ParamLayout.of(thetas).views(flat)
+            state._list_views = (flat, shapes, moms)
     ops.outer_step_list(thetas, workers, moms, state.has_momentum if momentum != 0 else False,
                         lr, momentum, nesterov)
     if momentum != 0:
@@ -164,8 +170,9 @@ def outer_step(base_params, worker_params, state: OuterState | None = None, lr: 
     worker_params = [list(w) for w in worker_params]
     if not worker_params:
         raise EdtError("no trained models")
+    shapes = [p.shape for p in base_params]
     for w in worker_params:
-        if len(w) != len(base_params) or any(a.shape != b.shape for a, b in zip(w, base_params)):
+        if [a.shape for a in w] != shapes:
             raise EdtError("trained model parameters do not match the base model")
     with torch.no_grad():
         theta = flat_view(base_params)

@@ -88,29 +88,45 @@ def outer_step_list(thetas: list[torch.Tensor], workers: list[list[torch.Tensor]
         raise L.EdtError("no workers")
     if K > L.EDT_MAX_WORKERS:
         raise L.EdtError(f"tensor-list step takes at most {L.EDT_MAX_WORKERS} workers")
-    flat_w = [t for w in workers for t in w]
-    L.require_device(*thetas, *flat_w, *(momenta or []))
     if any(len(w) != T for w in workers):
         raise L.EdtError("every worker needs one tensor per parameter")
-    gdt, wdt = thetas[0].dtype, workers[0][0].dtype if T else thetas[0].dtype
-    for t in range(T):
-        n = thetas[t].numel()
-        if thetas[t].dtype != gdt:
-            raise L.EdtError("all parameters of the base model must share one dtype")
-        for w in workers:
-            if w[t].numel() != n or w[t].dtype != wdt:
-                raise L.EdtError(f"worker tensor {t} does not match the base parameter")
-        if momenta is not None and (momenta[t].numel() != n or momenta[t].dtype != gdt):
-            raise L.EdtError(f"momentum tensor {t} must match the parameter's size and dtype")
     if momentum_coef != 0 and momenta is None:
         raise L.EdtError("momentum tensors are required when momentum != 0")
+    if momenta is not None and len(momenta) != T:
+        raise L.EdtError("one momentum tensor per parameter")
     if T == 0:
         return
-    numel = (ctypes.c_uint64 * T)(*[t.numel() for t in thetas])
+    # one comprehension per property over all T x (K + 2) tensors (the drop-in path sees
+    # model.parameters() lists: hundreds of tensors per model, so per-tensor Python matters)
+    flat_w = [t for w in workers for t in w]
+    every = thetas + flat_w + (list(momenta) if momenta is not None else [])
+    if not all([t.is_cuda for t in every]):
+        raise L.EdtError("outer-loop sync operands must be device-resident (HBM) tensors")
+    if not all([t.is_contiguous() for t in every]):
+        raise L.EdtError("outer-loop sync operands must be contiguous")
+    if len({t.get_device() for t in every}) != 1:
+        raise L.EdtError("operands on different devices")
+    gdt, wdt = thetas[0].dtype, workers[0][0].dtype
+    if {t.dtype for t in thetas} != {gdt}:
+        raise L.EdtError("all parameters of the base model must share one dtype")
+    if {t.dtype for t in flat_w} != {wdt}:
+        raise L.EdtError("every worker tensor must share the workers' dtype")
+    numels = [t.numel() for t in thetas]
+    for k, w in enumerate(workers):
+        if [t.numel() for t in w] != numels:
+            bad = next(t for t in range(T) if w[t].numel() != numels[t])
+            raise L.EdtError(f"worker tensor {bad} does not match the base parameter")
+    if momenta is not None:
+        if [t.numel() for t in momenta] != numels or {t.dtype for t in momenta} != {gdt}:
+            raise L.EdtError("momentum tensors must match the parameters' sizes and dtype")
+    numel = (ctypes.c_uint64 * T)(*numels)
     nbytes = lib.edt_outer_list_workspace_bytes(T, K)
     ws = torch.empty(nbytes, dtype=torch.uint8, device=thetas[0].device)
-    L.check(lib.edt_outer_step_list(L.ptr_array(thetas), L.dtype_code(gdt), L.ptr_array(flat_w),
-                                    L.dtype_code(wdt), K, L.ptr_array(momenta) if momenta is not None else None,
+    P_ = ctypes.c_void_p
+    th_arr = (P_ * T)(*[t.data_ptr() for t in thetas])
+    w_arr = (P_ * len(flat_w))(*[t.data_ptr() for t in flat_w])
+    m_arr = (P_ * T)(*[t.data_ptr() for t in momenta]) if momenta is not None else None
+    L.check(lib.edt_outer_step_list(th_arr, L.dtype_code(gdt), w_arr, L.dtype_code(wdt), K, m_arr,
                                     int(has_momentum), numel, T, float(lr), float(momentum_coef), int(nesterov),
                                     L.ptr(ws), nbytes, L.stream_ptr(thetas[0].device)), "edt_outer_step_list")
 
