@@ -3,28 +3,33 @@
 The reference has no collectives: its "gather" is K x `from_pretrained` of the workers'
 checkpoints on a shared disk and its "broadcast" is K x `save_pretrained` (EDT_LM/diloco.py:
 231-235, 302-308). Here the population is resident in HBM across the node and the cross-replica
-mean is a real exchange step. Two schedules, both bucketed so RCCL traffic on the comm stream
+mean is a real exchange step. Three schedules, all bucketed so RCCL traffic on the comm stream
 overlaps the HBM-bound kernels on the compute stream:
 
-  mode="reduce"  each rank fuses its local workers into an fp32 partial sum (edt_delta_partial),
-                 reduce-scatter(sum, fp32) -> SGD on the owned shard (momentum sharded 1/N,
-                 edt_sgd_apply) -> all-gather of theta. Wire bytes per rank and step:
-                 (N-1)/N * P * (4 + b_g). Summation order across ranks differs from the
-                 reference's sequential order: fp32 <= 2 ulp, bf16 <= 1 bf16 ulp.
-  mode="exact"   all-to-all of the raw worker shards to their owners, then the single-GPU fused
-                 kernel on each shard (the reference's worker order, bit-exact), all-gather of
-                 theta. Wire bytes: (N-1)/N * P * (K_local * b_w + b_g).
-  broadcast      what the all-gather delivers to every rank. "theta": the full master replica
-                 (theta's dtype). "workers" (exact mode only): the new theta rounded to the worker
-                 dtype, straight into every local worker arena — the start of the next inner
-                 loop, which is all the reference ships to the workers (diloco.py:302-308 saves
-                 the base to every worker dir; the bf16 workers load it rounded). The fp32 master
-                 then stays sharded (each rank updates only the shard it owns; `gather_theta()`
-                 assembles it on demand, e.g. for a checkpoint). Wire bytes:
-                 (N-1)/N * P * (K_local + 1) * b_w.
-  mode="auto" / broadcast="auto" (defaults) pick the combination with the fewest wire bytes:
-  at K = 8 bf16 workers, fp32 theta: N = 2 reduce/theta (8 B/elem), N = 4 and 8 exact/workers
-  (6 and 4 B/elem).
+  mode="reduce"          each rank fuses its local workers into an fp32 partial sum
+                         (edt_delta_partial), reduce-scatter(sum, fp32) -> SGD on the owned shard
+                         (momentum sharded 1/N, edt_sgd_apply) -> all-gather of theta. Wire bytes
+                         per rank and step: (N-1)/N * P * (4 + b_g). The cross-rank sum is RCCL's
+                         (its order depends on the algorithm RCCL picks); within DESIGN §3's bound of
+                         the reference's sequential order.
+  mode="reduce_ordered"  the same partials, an all-to-all of them instead of the reduce-scatter,
+                         then edt_sgd_apply_sum: the owned shard's N partials summed in rank order
+                         + SGD. Same wire bytes as reduce; one fixed summation order whatever RCCL
+                         does (reproducible run to run, bit-exact with the oracle's split).
+  mode="exact"           all-to-all of the raw worker shards to their owners, then the single-GPU
+                         fused kernel on each shard (the reference's worker order, bit-exact),
+                         all-gather of theta. Wire bytes: (N-1)/N * P * (K_local * b_w + b_g).
+  broadcast              what the all-gather delivers to every rank. "theta": the full master
+                         replica (theta's dtype). "workers" (exact mode only): the new theta rounded
+                         to the worker dtype, straight into every local worker arena — the start of
+                         the next inner loop, which is all the reference ships to the workers
+                         (diloco.py:302-308 saves the base to every worker dir; the bf16 workers load
+                         it rounded). The fp32 master then stays sharded (`gather_theta()` assembles
+                         it on demand, e.g. for a checkpoint). Wire bytes: (N-1)/N * P * (K_local + 1) * b_w.
+  mode="auto" / broadcast="auto" (defaults) pick the combination with the fewest wire bytes,
+  ties to exact, then reduce_ordered: at K = 8 bf16 workers, fp32 theta: N = 2 reduce_ordered/theta
+  (8 B/elem), N = 4 and 8 exact/workers (6 and 4 B/elem); all fp32: N = 2 and 4 reduce_ordered,
+  N = 8 exact.
 
 Every rank holds 1/N of the momentum and owns contiguous shards of every bucket.
 """
