@@ -286,43 +286,69 @@ def _write_file(path: str, header: bytes, host: torch.Tensor, threads: int = 1, 
     os.replace(tmp, path)
 
 
-def _stream_write(path: str, header: bytes, flat: torch.Tensor, staging_bytes: int) -> None:
-    """header + the device arena's bytes to path (via path.tmp, renamed when complete) through a
-    pooled pinned staging pair: the D2H of chunk i+1 runs on the staging copy stream (after the
-    caller's stream, so every kernel that produced `flat` has finished) while chunk i is written."""
+def _stream_write(path: str, header: bytes, flat: torch.Tensor, staging_bytes: int, writers: int = 1) -> None:
+    """header + the device arena's bytes to path (via path.tmp, renamed when complete) through
+    pooled pinned staging pairs: the D2H of a writer's next chunk runs on its staging copy stream
+    (after the caller's stream, so every kernel that produced `flat` has finished) while its
+    current chunk is written. writers > 1: that many threads, each with its own staging pair and
+    copy stream, take every writers-th chunk and write it at its own offset (os.pwrite releases
+    the GIL), so page-cache copies of several chunks proceed at once."""
+    from concurrent.futures import ThreadPoolExecutor
     dev = flat.device
     data = flat.view(torch.uint8)
     n = data.numel()
-    stage = _acquire_stage(staging_bytes, dev)
-    stage.stream.wait_stream(torch.cuda.current_stream(dev))
+    caller = torch.cuda.current_stream(dev)
+    chunks = list(range(0, n, staging_bytes))
+    writers = max(1, min(writers, len(chunks)))
     tmp = path + ".tmp"
-    try:
-        with open(tmp, "wb") as f:
-            f.write(header)
+    fd = os.open(tmp, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+    hl = len(header)
+
+    def writer(w):
+        torch.cuda.set_device(dev)
+        stage = _acquire_stage(staging_bytes, dev)
+        try:
+            stage.stream.wait_stream(caller)
+            mine = chunks[w::writers]
             pending = []
 
             def issue(s0):
                 i, buf = stage.next()        # its previous chunk was written two steps ago
-                s1 = min(n, s0 + buf.numel())
+                nb = min(n, s0 + staging_bytes) - s0
                 with torch.cuda.stream(stage.stream):
-                    buf[:s1 - s0].copy_(data[s0:s1], non_blocking=True)
+                    buf[:nb].copy_(data[s0:s0 + nb], non_blocking=True)
                 stage.record(i)
-                pending.append((i, buf, s1 - s0))
-                return s1
-            nxt = issue(0) if n else 0
-            while pending:
-                if nxt < n:
-                    nxt = issue(nxt)
-                i, buf, nb = pending.pop(0)
+                pending.append((i, buf, s0, nb))
+            k = 0
+            while pending or k < len(mine):
+                while k < len(mine) and len(pending) < 2:
+                    issue(mine[k])
+                    k += 1
+                i, buf, s0, nb = pending.pop(0)
                 stage.events[i].synchronize()
-                f.write(memoryview(buf[:nb].numpy()))
+                mv = memoryview(buf[:nb].numpy())
+                done = 0
+                while done < nb:
+                    done += os.pwrite(fd, mv[done:], hl + s0 + done)
+        finally:
+            _release_stage(stage)
+    try:
+        done = 0
+        while done < hl:
+            done += os.pwrite(fd, header[done:], done)
+        if writers == 1:
+            writer(0)
+        else:
+            with ThreadPoolExecutor(max_workers=writers) as ex:
+                list(ex.map(writer, range(writers)))
     finally:
-        _release_stage(stage)
+        os.close(fd)
     os.replace(tmp, path)
 
 
 def write_from_arena(path: str, layout: ParamLayout, flat: torch.Tensor, names: list[str] | None = None,
-                     metadata: dict | None = None, threads: int = 1, staging_bytes: int = 64 << 20) -> None:
+                     metadata: dict | None = None, threads: int = 1, staging_bytes: int = 64 << 20,
+                     writers: int = 1) -> None:
     """Write `flat` as a .safetensors file (tensors in layout order, one contiguous data section).
     A device arena streams through a pooled pinned staging pair (`staging_bytes` each), its D2H
     overlapping the writes: no whole-arena pinned buffer (pinning 14 GB for a 7B child costs
@@ -333,7 +359,7 @@ def write_from_arena(path: str, layout: ParamLayout, flat: torch.Tensor, names: 
     if flat.device.type == "cuda":
         if not flat.is_contiguous():
             raise ValueError("write_from_arena needs a contiguous arena")
-        _stream_write(path, header, flat, staging_bytes)
+        _stream_write(path, header, flat, staging_bytes, writers)
     else:
         _write_file(path, header, flat.contiguous(), threads)
 

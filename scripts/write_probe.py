@@ -10,8 +10,11 @@ writes fastest.
   write_pageable   one write() of the pageable buffer
   chunked_C        2 pinned staging buffers of C bytes: D2H of chunk i+1 on a copy stream while
                    chunk i is written (pinning the staging pair included, as a fresh process pays it)
+  --ab R           R interleaved rounds from a clean page cache (os.sync() first): one write of a
+                   cached pinned whole copy, chunked_C, and checkpoint._stream_write with each of
+                   `--writers` writer threads
 
-    python scripts/write_probe.py [--dir DIR] [--chunks 268435456,1073741824] [--ab 3]
+    python scripts/write_probe.py [--dir DIR] [--chunks 268435456,1073741824] [--ab 3 --writers 1,2,4]
 """
 from __future__ import annotations
 
@@ -68,23 +71,8 @@ def _chunked(path, hdr, xb, nbytes, c):
             f.write(memoryview(bufs[i % 2][:sizes[i]].numpy()))
 
 
-def main():
-    from evolutionarydistributedtraining_amd import checkpoint
-    from evolutionarydistributedtraining_amd.layouts import qwen2p5_7b_body
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--dir", default=os.path.join(os.getcwd(), "write_probe_tmp"))
-    ap.add_argument("--chunks", default=str(256 << 20) + "," + str(1 << 30))
-    ap.add_argument("--ab", type=int, default=0, help="interleaved A/B repetitions after os.sync()")
-    a = ap.parse_args()
-    os.makedirs(a.dir, exist_ok=True)
-    lay = qwen2p5_7b_body()
-    P = lay.total
-    nbytes = 2 * P
-    x = torch.empty(P, dtype=torch.bfloat16, device="cuda")
-    x.fill_(0.5)
-    hdr = checkpoint._header_bytes(lay, lay.names, x.dtype, None)
-    path = os.path.join(a.dir, "child.safetensors")
-    res = {"bytes": nbytes}
+def _phases(a, checkpoint, lay, x, hdr, path, nbytes, res):
+    P = x.numel()
 
     def rate(t):
         return {"s": round(t, 3), "GBps": round(nbytes / t / 1e9, 2)}
@@ -111,28 +99,57 @@ def main():
     t, _ = _t(lambda: checkpoint.write_from_arena(path, lay, x))
     res["write_from_arena_first"] = rate(t)
     t, _ = _t(lambda: checkpoint.write_from_arena(path, lay, x))
-    res["write_from_arena_cached_pin"] = rate(t)
+    res["write_from_arena_again"] = rate(t)
     os.remove(path)
+
+
+def _ab(a, checkpoint, x, hdr, path, nbytes, res):
+    """Interleaved rounds from a clean page cache (os.sync() first, its time reported)."""
+    xb = x.view(torch.uint8)
+    forms = {"whole_cached_pin": lambda: checkpoint._write_file(path, hdr, checkpoint._host_copy(x))}
+    for c in [int(v) for v in a.chunks.split(",")]:
+        forms[f"chunked_{c >> 20}MiB"] = lambda c=c: _chunked(path, hdr, xb, nbytes, c)
+    for w in [int(v) for v in a.writers.split(",") if v]:
+        forms[f"stream_64MiB_w{w}"] = lambda w=w: checkpoint._stream_write(path, hdr, x, 64 << 20, w)
+    ab = {k: [] for k in forms}
+    syncs = []
+    for _ in range(a.ab):
+        for k, fn in forms.items():
+            t0 = time.perf_counter()
+            os.sync()
+            syncs.append(round(time.perf_counter() - t0, 2))
+            t, _ = _t(fn)
+            ab[k].append(round(t, 3))
+            if os.path.exists(path):
+                os.remove(path)
+            print(k, ab[k][-1], file=sys.stderr, flush=True)
+    res["ab_seconds"] = ab
+    res["ab_sync_seconds"] = syncs
+
+
+def main():
+    from evolutionarydistributedtraining_amd import checkpoint
+    from evolutionarydistributedtraining_amd.layouts import qwen2p5_7b_body
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--dir", default=os.path.join(os.getcwd(), "write_probe_tmp"))
+    ap.add_argument("--chunks", default=str(256 << 20) + "," + str(1 << 30))
+    ap.add_argument("--ab", type=int, default=0, help="interleaved A/B repetitions after os.sync()")
+    ap.add_argument("--writers", default="", help="--ab: also checkpoint._stream_write with these writer counts")
+    ap.add_argument("--skip-phases", action="store_true", help="only the --ab comparison")
+    a = ap.parse_args()
+    os.makedirs(a.dir, exist_ok=True)
+    lay = qwen2p5_7b_body()
+    P = lay.total
+    nbytes = 2 * P
+    x = torch.empty(P, dtype=torch.bfloat16, device="cuda")
+    x.fill_(0.5)
+    hdr = checkpoint._header_bytes(lay, lay.names, x.dtype, None)
+    path = os.path.join(a.dir, "child.safetensors")
+    res = {"bytes": nbytes}
+    if not a.skip_phases:
+        _phases(a, checkpoint, lay, x, hdr, path, nbytes, res)
     if a.ab:
-        # A/B from a clean page cache each time (os.sync() first, its time reported): the whole
-        # buffer (pinned buffer cached) against chunked streaming, interleaved
-        forms = {"whole_cached_pin": lambda: checkpoint.write_from_arena(path, lay, x)}
-        for c in [int(v) for v in a.chunks.split(",")]:
-            forms[f"chunked_{c >> 20}MiB"] = lambda c=c: _chunked(path, hdr, xb, nbytes, c)
-        ab = {k: [] for k in forms}
-        syncs = []
-        for _ in range(a.ab):
-            for k, fn in forms.items():
-                t0 = time.perf_counter()
-                os.sync()
-                syncs.append(round(time.perf_counter() - t0, 2))
-                t, _ = _t(fn)
-                ab[k].append(round(t, 3))
-                if os.path.exists(path):
-                    os.remove(path)
-                print(k, ab[k][-1], file=sys.stderr, flush=True)
-        res["ab_seconds"] = ab
-        res["ab_sync_seconds"] = syncs
+        _ab(a, checkpoint, x, hdr, path, nbytes, res)
     os.rmdir(a.dir)
     print(json.dumps(res), flush=True)
 
