@@ -1,0 +1,88 @@
+"""Differential fuzzing of the HIP kernels against the oracle (hypothesis): random sizes (odd,
+tiny, vector-boundary), populations, dtype regimes and — what the fixed-parameter tests do not
+vary — arbitrary outer-optimiser scalars (lr, momentum, Nesterov, first step or carried buffer) and
+lerp weights. The scalars are where the reference's conversions bite: torch rounds `alpha` to
+bf16 for bf16 tensors, `mul_(s)` keeps the fp32 scalar, `/ K` is a true division, so a
+kernel that folded or rounded a scalar differently would show up here on some draw. Every case is
+bit-exact. Reference: EDT_LM/diloco.py:238-289, EDT_LM/train/crossover.py:50-51,150-237."""
+import pytest
+import torch
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
+
+from tests.golden_data import bits
+
+pytestmark = pytest.mark.gpu
+
+REGIMES = [(torch.float32, torch.float32), (torch.float32, torch.bfloat16), (torch.bfloat16, torch.bfloat16)]
+FUZZ = settings(max_examples=200, deadline=None, derandomize=True,
+                suppress_health_check=[HealthCheck.function_scoped_fixture, HealthCheck.too_slow])
+
+sizes = st.one_of(st.integers(1, 40), st.integers(1, 5000), st.sampled_from([7, 8, 9, 2047, 2048, 2049, 4097]))
+scalars = st.floats(min_value=1e-4, max_value=2.0, allow_nan=False, allow_infinity=False)
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    return torch.device("cuda:0")
+
+
+@FUZZ
+@given(n=sizes, K=st.integers(1, 12), regime=st.sampled_from(REGIMES), lr=scalars,
+       mu=st.one_of(st.just(0.0), st.floats(0.0, 0.999)), nesterov=st.booleans(), has=st.booleans(),
+       seed=st.integers(0, 2**31 - 1))
+def test_outer_step_fuzz(oracle, dev, n, K, regime, lr, mu, nesterov, has, seed):
+    from evolutionarydistributedtraining_amd import ops
+    gdt, wdt = regime
+    if nesterov and mu == 0:
+        nesterov = False                     # torch.optim.SGD rejects Nesterov without momentum
+    g = torch.Generator().manual_seed(seed)
+    theta = (torch.randn(n, generator=g) * 0.02).to(gdt)
+    workers = [(theta.float() + torch.randn(n, generator=g) * 1e-3).to(wdt) for _ in range(K)]
+    mom = (torch.randn(n, generator=g) * 1e-3).to(gdt)
+    th_d, m_d = theta.to(dev), mom.to(dev)
+    ops.outer_step(th_d, [w.to(dev) for w in workers], m_d if mu else None, has, lr, mu, nesterov)
+    oracle.outer_step(theta, workers, mom if mu else None, has, lr, mu, nesterov)
+    assert torch.equal(bits(th_d.cpu()), bits(theta))
+    if mu:
+        assert torch.equal(bits(m_d.cpu()), bits(mom))
+
+
+@FUZZ
+@given(n=sizes, lr=scalars, mu=st.one_of(st.just(0.0), st.floats(0.0, 0.999)), nesterov=st.booleans(),
+       has=st.booleans(), regime=st.sampled_from([(torch.bfloat16, torch.bfloat16), (torch.float32, torch.float32),
+                                                  (torch.float32, torch.bfloat16)]),
+       seed=st.integers(0, 2**31 - 1))
+def test_pair_merge_fuzz(oracle, dev, n, lr, mu, nesterov, has, regime, seed):
+    from evolutionarydistributedtraining_amd import ops
+    gdt, wdt = regime
+    if nesterov and mu == 0:
+        nesterov = False
+    g = torch.Generator().manual_seed(seed)
+    b1, b2 = [(torch.randn(n, generator=g) * 0.02).to(wdt) for _ in range(2)]
+    m1 = (b1.float() + torch.randn(n, generator=g) * 1e-3).to(wdt)
+    m2 = (b2.float() + torch.randn(n, generator=g) * 1e-3).to(wdt)
+    mom = (torch.randn(n, generator=g) * 1e-3).to(gdt)
+    out_d = torch.empty(n, dtype=gdt, device=dev)
+    mom_d = mom.to(dev)
+    ops.pair_merge(b1.to(dev), b2.to(dev), m1.to(dev), m2.to(dev), out_d, mom_d if mu else None, has, lr, mu,
+                   nesterov)
+    out = torch.empty(n, dtype=gdt)
+    oracle.pair_merge(b1, b2, m1, m2, out, mom if mu else None, has, lr, mu, nesterov)
+    assert torch.equal(bits(out_d.cpu()), bits(out))
+    if mu:
+        assert torch.equal(bits(mom_d.cpu()), bits(mom))
+
+
+@FUZZ
+@given(n=sizes, t=st.floats(0.0, 1.0), dt=st.sampled_from([torch.float32, torch.bfloat16]),
+       seed=st.integers(0, 2**31 - 1))
+def test_lerp_fuzz(oracle, dev, n, t, dt, seed):
+    from evolutionarydistributedtraining_amd import ops
+    g = torch.Generator().manual_seed(seed)
+    v0, v1 = [(torch.randn(n, generator=g) * 0.02).to(dt) for _ in range(2)]
+    got = ops.lerp(t, v0.to(dev), v1.to(dev))
+    want = oracle.lerp(t, v0, v1)
+    assert torch.equal(bits(got.cpu()), bits(want))
