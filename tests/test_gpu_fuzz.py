@@ -86,3 +86,44 @@ def test_lerp_fuzz(oracle, dev, n, t, dt, seed):
     got = ops.lerp(t, v0.to(dev), v1.to(dev))
     want = oracle.lerp(t, v0, v1)
     assert torch.equal(bits(got.cpu()), bits(want))
+
+
+@FUZZ
+@given(sizes_=st.lists(st.integers(0, 3000), min_size=1, max_size=5),
+       ts=st.lists(st.floats(0.0, 1.0), min_size=5, max_size=5),
+       spread=st.sampled_from([1e-4, 0.01, 0.05, 0.5, 2.0]), seed=st.integers(0, 2**31 - 1),
+       speculate=st.booleans())
+def test_slerp_fuzz(oracle, dev, sizes_, ts, spread, seed, speculate):
+    """Multi-tensor SLERP (EDT_RL/crossover.py:11-43) over random segment sizes (empty included),
+    per-segment t and parent distances from lineage (lerp branch) to far (SLERP branch), both
+    kernel forms: per segment the branch agrees with the oracle's (fp32) dot away from the
+    threshold, the lerp branch is bit-exact, and the SLERP branch is within the golden bar."""
+    from evolutionarydistributedtraining_amd import ops
+    g = torch.Generator().manual_seed(seed)
+    offs = [0]
+    for s in sizes_:
+        offs.append(offs[-1] + s)
+    n = offs[-1]
+    v0 = torch.randn(n, generator=g) * 0.02
+    v1 = v0 + torch.randn(n, generator=g) * 0.02 * spread
+    t = torch.tensor(ts[:len(sizes_)], dtype=torch.float64)
+    plan = ops.make_slerp_plan(offs, dev, chunk_elems=1024)
+    out_d = torch.empty(max(n, 1), dtype=torch.float32, device=dev)[:n]
+    ops.slerp_arena(plan, v0.to(dev), v1.to(dev), out_d, t.to(dev), speculate=speculate)
+    got = out_d.cpu()
+    for s in range(len(sizes_)):
+        a, b = offs[s], offs[s + 1]
+        if b == a:
+            continue
+        want = oracle.slerp(float(t[s]), v0[a:b], v1[a:b]).float()
+        c0, c1, dot = oracle.slerp_coefficients(float(t[s]), v0[a:b], v1[a:b])
+        if abs(abs(float(dot)) - 0.9995) < 1e-5:
+            continue                                     # the threshold contract's own tests
+        err = (got[a:b] - want).abs()
+        assert (err <= _tol(c0, c1, v0[a:b], v1[a:b])).all(), (s, err.max().item())
+        if abs(float(dot)) > 0.9995:
+            assert torch.equal(bits(got[a:b]), bits(want)), s
+
+
+def _tol(c0, c1, v0, v1):
+    return 2e-6 * (abs(float(c0)) * v0.float().abs() + abs(float(c1)) * v1.float().abs()) + 1e-30
