@@ -112,3 +112,43 @@ def test_virtual_rank_failure_breaks_the_rendezvous():
 
     with pytest.raises(CommTimeout):
         VirtualWorld(2, timeout=1).run(straggler)
+
+
+from hypothesis import HealthCheck, given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+
+@settings(max_examples=40, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.function_scoped_fixture, HealthCheck.too_slow])
+@given(world=st.integers(1, 5), k_local=st.integers(1, 3),
+       shapes=st.lists(st.one_of(st.tuples(st.integers(1, 300)), st.tuples(st.integers(1, 40), st.integers(1, 40))),
+                       min_size=1, max_size=6),
+       units=st.integers(1, 9), mode=st.sampled_from(["exact", "reduce", "reduce_ordered"]),
+       workers_bcast=st.booleans(), dts=st.sampled_from([(torch.float32, torch.float32),
+                                                         (torch.float32, torch.bfloat16),
+                                                         (torch.bfloat16, torch.bfloat16)]))
+def test_virtual_sharded_fuzz(oracle, world, k_local, shapes, units, mode, workers_bcast, dts):
+    """Random worlds, populations, layouts and bucket sizes (bucket_elems = units x world x 64, so
+    buckets end anywhere relative to tensors and to the padded tail): exact is bit-exact with the
+    oracle's single fused step over the whole population, the reduce schedules with the rank-order
+    reference; every rank's replica agrees."""
+    tdt, wdt = dts
+    broadcast = "workers" if workers_bcast and mode == "exact" else "theta"
+    k_total = k_local * world
+    layout, theta, gens = population(shapes, tdt, wdt, k_total, steps=2, seed=world * 31 + units)
+    res = run_sharded(world, layout, tdt, wdt, theta, gens, "cpu", kernels=oracle, mode=mode,
+                      broadcast=broadcast, bucket_elems=units * world * 64)
+    n = layout.total
+    for r in res:
+        assert torch.equal(bits(r["theta"]), bits(res[0]["theta"]))
+    got = res[0]["theta"][:n]
+    if mode == "exact":
+        th_ref, mom_ref = _oracle_ref(theta, gens, tdt)
+    else:
+        th_ref, mom_ref = reduce_reference(oracle, theta, gens, world)
+    assert torch.equal(bits(got), bits(th_ref))
+    assert torch.equal(bits(res[0]["mom"]), bits(mom_ref))
+    if broadcast == "workers":
+        for r in res:
+            for w in r["workers"]:
+                assert torch.equal(bits(w[:n]), bits(th_ref.to(wdt)))
