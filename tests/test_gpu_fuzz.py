@@ -127,3 +127,44 @@ def test_slerp_fuzz(oracle, dev, sizes_, ts, spread, seed, speculate):
 
 def _tol(c0, c1, v0, v1):
     return 2e-6 * (abs(float(c0)) * v0.float().abs() + abs(float(c1)) * v1.float().abs()) + 1e-30
+
+
+@settings(max_examples=30, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.function_scoped_fixture, HealthCheck.too_slow])
+@given(world=st.integers(1, 8), k_local=st.integers(1, 3),
+       shapes=st.lists(st.one_of(st.tuples(st.integers(1, 5000)), st.tuples(st.integers(1, 70), st.integers(1, 70))),
+                       min_size=1, max_size=6),
+       units=st.integers(1, 9), mode=st.sampled_from(["exact", "reduce_ordered"]), workers_bcast=st.booleans(),
+       dts=st.sampled_from(REGIMES))
+def test_sharded_schedules_fuzz_on_virtual_ranks(dev, world, k_local, shapes, units, mode, workers_bcast, dts):
+    """The HIP kernels inside the sharded schedules on random virtual worlds, layouts and bucket
+    sizes: exact (either broadcast) bit-exact with the fused single-GPU step over the whole
+    population; reduce_ordered bit-exact with per-rank edt_delta_partial + edt_sgd_apply_sum."""
+    from evolutionarydistributedtraining_amd import ops
+    from tests.virtual_schedules import population, run_sharded
+    tdt, wdt = dts
+    broadcast = "workers" if workers_bcast and mode == "exact" else "theta"
+    k_total = k_local * world
+    layout, theta, gens = population(shapes, tdt, wdt, k_total, steps=2, seed=world * 7 + units, device=dev)
+    res = run_sharded(world, layout, tdt, wdt, theta, gens, dev, mode=mode, broadcast=broadcast,
+                      bucket_elems=units * world * 64)
+    n = layout.total
+    th, mom = theta.clone(), torch.zeros(n, dtype=tdt, device=dev)
+    for i, ws in enumerate(gens):
+        if mode == "exact":
+            ops.outer_step(th, ws, mom, i > 0, 0.7, 0.9, True)
+        else:
+            accs = []
+            for r in range(world):
+                acc = torch.empty(n, device=dev)
+                ops.delta_partial(th, ws[r * k_local:(r + 1) * k_local], k_total, acc, False)
+                accs.append(acc)
+            ops.sgd_apply_sum(th, accs, mom, i > 0, 0.7, 0.9, True)
+    torch.cuda.synchronize()
+    for r in res:
+        assert torch.equal(bits(r["theta"][:n].cpu()), bits(th.cpu())), r
+    assert torch.equal(bits(res[0]["mom"].cpu()), bits(mom.cpu()))
+    if broadcast == "workers":
+        for r in res:
+            for w in r["workers"]:
+                assert torch.equal(bits(w[:n].cpu()), bits(th.to(wdt).cpu()))
