@@ -124,3 +124,35 @@ def test_sharded_slerp_population_gloo_world3(tmp_path, oracle, groups):
         got = torch.load(tmp_path / f"s{c}.pt", weights_only=True)
         assert torch.equal(got["out"].view(torch.int32), want[c].view(torch.int32)), c
         assert torch.equal(got["dots"], wdots)
+
+
+from hypothesis import HealthCheck, given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+
+@settings(max_examples=40, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.function_scoped_fixture, HealthCheck.too_slow])
+@given(world=st.integers(1, 8), groups=st.integers(1, 4),
+       shapes=st.lists(st.one_of(st.tuples(st.integers(1, 900)), st.tuples(st.integers(1, 30), st.integers(1, 30))),
+                       min_size=1, max_size=7),
+       seed=st.integers(0, 2**31 - 1))
+def test_sharded_slerp_population_fuzz(oracle, world, groups, shapes, seed):
+    """Random layouts (tensor sizes off the 8-element grid, so rank ranges start mid-vector and
+    share up to 7 elements with the previous rank), worlds and pipeline groups: every child equals
+    the whole-population arithmetic bit for bit, and the ranks' ranges tile the layout."""
+    from tests.oracle_kernels import ChunkGramKernels
+    layout = ParamLayout(shapes)
+    g = torch.Generator().manual_seed(seed)
+    base = torch.randn(layout.total, generator=g) * 0.02
+    members = [(base + torch.randn(layout.total, generator=g) * 0.02 * (0.01 if r % 2 else 0.1)).bfloat16()
+               for r in range(world)]
+    pairs = _pairs(world)
+    t = torch.rand(len(shapes), generator=g, dtype=torch.float64)
+    res = VirtualWorld(world).run(lambda comm: _run(comm, layout, members, pairs, t, oracle, "slerp", groups))
+    want, wdots = _whole(ChunkGramKernels(oracle), layout, members, pairs, t)
+    ranges = res[0][2]
+    assert ranges[0][3] == 0 and ranges[-1][4] == layout.total
+    assert all(ranges[r][4] == ranges[r + 1][3] for r in range(world - 1))
+    for c in range(world):
+        assert torch.equal(res[c][0].view(torch.int32), want[c].view(torch.int32)), c
+        assert torch.equal(res[c][1], wdots)
