@@ -168,3 +168,43 @@ def test_sharded_schedules_fuzz_on_virtual_ranks(dev, world, k_local, shapes, un
         for r in res:
             for w in r["workers"]:
                 assert torch.equal(bits(w[:n].cpu()), bits(th.to(wdt).cpu()))
+
+
+@settings(max_examples=25, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.function_scoped_fixture, HealthCheck.too_slow])
+@given(world=st.integers(1, 8), groups=st.integers(1, 4),
+       shapes=st.lists(st.one_of(st.tuples(st.integers(1, 20000)), st.tuples(st.integers(1, 90), st.integers(1, 90))),
+                       min_size=1, max_size=7),
+       seed=st.integers(0, 2**31 - 1))
+def test_sharded_population_fuzz_on_virtual_ranks(dev, world, groups, shapes, seed):
+    """The link-balanced population crossover with the HIP Gram / coefficient / blend passes on
+    random layouts (1,024-element chunks: many chunks per rank, ranges starting off the vector
+    grid), worlds and pipeline groups: every child bit-identical to edt_slerp_merge on its two
+    parents with the same chunk table."""
+    from evolutionarydistributedtraining_amd import ops
+    from evolutionarydistributedtraining_amd.collectives import VirtualWorld
+    from evolutionarydistributedtraining_amd.distributed import ShardedPopulationCrossover
+    from evolutionarydistributedtraining_amd.params import ParamLayout
+    layout = ParamLayout(shapes)
+    n = layout.total
+    g = torch.Generator().manual_seed(seed)
+    base = torch.randn(n, generator=g) * 0.02
+    members = [(base + torch.randn(n, generator=g) * 0.02 * (0.005 if r % 2 else 0.1)).bfloat16().to(dev)
+               for r in range(world)]
+    pairs = [((3 * c + 1) % world, (5 * c + 2) % world) for c in range(world)]
+    t = torch.rand(len(shapes), generator=g, dtype=torch.float64).to(dev)
+
+    def body(comm):
+        sp = ShardedPopulationCrossover(layout, torch.bfloat16, dev, comm=comm, chunk_elems=1024, groups=groups)
+        out = torch.empty(n, dtype=torch.bfloat16, device=dev)
+        sp.slerp_step(members[comm.rank], pairs, t, out)
+        torch.cuda.synchronize()
+        return out
+
+    res = VirtualWorld(world).run(body)
+    plan = ops.make_slerp_plan(layout.offsets, dev, chunk_elems=1024)
+    want = torch.empty(n, dtype=torch.bfloat16, device=dev)
+    for c, (i, j) in enumerate(pairs):
+        ops.slerp_arena(plan, members[i], members[j], want, t, speculate=False)
+        torch.cuda.synchronize()
+        assert torch.equal(res[c].view(torch.int16), want.view(torch.int16)), c
