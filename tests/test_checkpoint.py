@@ -156,3 +156,58 @@ def test_split_readers_and_threaded_writes(tmp_path):
     sd = load_file(str(tmp_path / "many.safetensors"))
     for (name, _), v in zip(m.named_parameters(), layout.views(want)):
         assert torch.equal(sd[name], v)
+
+
+from hypothesis import HealthCheck, given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+
+def _write_sharded(d, names, tensors, cuts):
+    """A HF-style sharded checkpoint written by hand: files split at `cuts` (tensor indices),
+    tensors stored in a shuffled order inside each file, plus model.safetensors.index.json."""
+    import json
+    import random
+
+    from safetensors.torch import save_file
+    os.makedirs(d, exist_ok=True)
+    bounds = [0] + sorted(set(cuts)) + [len(names)]
+    nf = len(bounds) - 1
+    wmap = {}
+    rng = random.Random(len(names) * 7 + nf)
+    for f in range(nf):
+        idx = list(range(bounds[f], bounds[f + 1]))
+        rng.shuffle(idx)
+        fname = f"model-{f + 1:05d}-of-{nf:05d}.safetensors"
+        save_file({names[i]: tensors[i].contiguous() for i in idx}, os.path.join(d, fname))
+        for i in idx:
+            wmap[names[i]] = fname
+    with open(os.path.join(d, "model.safetensors.index.json"), "w") as fh:
+        json.dump({"metadata": {}, "weight_map": wmap}, fh)
+
+
+@settings(max_examples=40, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.function_scoped_fixture, HealthCheck.too_slow])
+@given(shapes=st.lists(st.one_of(st.tuples(st.integers(1, 5000)), st.tuples(st.integers(1, 60), st.integers(1, 60))),
+                       min_size=1, max_size=9),
+       ckpt_dt=st.sampled_from([torch.float32, torch.bfloat16]), arena_dt=st.sampled_from([torch.float32, torch.bfloat16]),
+       cuts=st.lists(st.integers(1, 8), max_size=3), staging=st.sampled_from([64, 4096, 1 << 20]),
+       threads=st.integers(1, 8), copies=st.integers(1, 3), seed=st.integers(0, 2**31 - 1))
+def test_reader_fuzz(tmp_path_factory, shapes, ckpt_dt, arena_dt, cuts, staging, threads, copies, seed):
+    """read_into_arena / read_many over random layouts, shard splits, in-file tensor orders, dtype
+    conversions (torch copy_ rounding, as load_state_dict does), staging sizes smaller than one
+    tensor, and reader counts (one checkpoint split over several readers): every arena equals the
+    tensors packed in layout order."""
+    d0 = str(tmp_path_factory.mktemp("ck"))
+    g = torch.Generator().manual_seed(seed)
+    names = [f"layers.{i}.w" for i in range(len(shapes))]
+    layout = ParamLayout([torch.Size(s) for s in shapes], names)
+    items, want = [], []
+    for c in range(copies):
+        ts = [(torch.randn(s, generator=g) * 0.02).to(ckpt_dt) for s in shapes]
+        d = os.path.join(d0, f"m{c}")
+        _write_sharded(d, names, ts, [k for k in cuts if k < len(shapes)])
+        items.append((d, torch.full((layout.total,), float("nan"), dtype=arena_dt)))
+        want.append(torch.cat([t.reshape(-1).to(arena_dt) for t in ts]))
+    checkpoint.read_many(items, layout, threads=threads, staging_bytes=staging)
+    for (_, flat), w in zip(items, want):
+        assert torch.equal(flat, w)
