@@ -93,6 +93,9 @@ def parse():
                    help="the other hot-path measurements in the same line ('none': skip): N=1 pair_merge, "
                         "slerp_7b; N>1 population_7b (BASELINE configs[4] across the N GPUs)")
     p.add_argument("--ops-cpu-seconds", type=float, default=4.0, help="CPU baseline budget per extra op")
+    p.add_argument("--compare-schedules", type=int, default=1,
+                   help="N>1: after the value, also time the other sharded schedules (exact/workers, "
+                        "exact/theta, reduce_ordered, reduce) and report them as 'other_schedules'")
     p.add_argument("--population-groups", type=int, default=4,
                    help="N>1 population_7b: also time the link-balanced crossover with its exchanges "
                         "pipelined over this many chunk groups per rank (1: only the unpipelined form)")
@@ -439,14 +442,15 @@ def stream_ceiling_ms(theta, workers, momentum, iters=10):
     return ts[len(ts) // 2]
 
 
-def time_sharded(args, layout, tdt, wdt, k_local, dev, rank, steps, warmup):
+def time_sharded(args, layout, tdt, wdt, k_local, dev, rank, steps, warmup, mode=None, broadcast=None):
     """Build a ShardedOuterSync with k_local workers per rank, warm it up and time `steps` steps
     (barrier + synchronize on both sides, max over ranks). Returns (ms_per_step, mode/broadcast,
     wire bytes per rank); frees the arenas."""
     import torch.distributed as dist
     from evolutionarydistributedtraining_amd.distributed import ShardedOuterSync
     sync = ShardedOuterSync(layout, tdt, wdt, k_local, dev, args.lr, args.momentum, bool(args.nesterov),
-                            mode=args.mode, bucket_elems=args.bucket_elems, broadcast=args.broadcast)
+                            mode=mode or args.mode, bucket_elems=args.bucket_elems,
+                            broadcast=broadcast or args.broadcast)
     synth_population(sync.theta.flat, [w.flat for w in sync.workers], seed=4321 + 7919 * rank)
     dist.broadcast(sync.theta_buf, 0)
     for _ in range(warmup):
@@ -605,6 +609,24 @@ def main():
             weak = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
             torch.cuda.empty_cache()
         sync = None
+    schedules = None
+    if sharded and world > 1 and args.compare_schedules:
+        # every schedule the strong-scaling population can run, same steps, after the value: the
+        # data to tune mode="auto" on this node (outside the reported value)
+        sync = step = None
+        torch.cuda.empty_cache()
+        schedules = {}
+        for m, b in (("exact", "workers"), ("exact", "theta"), ("reduce_ordered", "theta"), ("reduce", "theta")):
+            if f"{m}/{b}" == sched:
+                continue
+            try:
+                ms_, name, wire_ = time_sharded(args, layout, tdt, wdt, k_local, dev, rank, args.steps,
+                                                args.warmup, mode=m, broadcast=b)
+                schedules[name] = {"ms_per_step": round(ms_, 4), "wire_bytes_per_rank": wire_,
+                                   "value": round(bytes_reduced / (ms_ / 1e3) / 1e9, 2)}
+            except Exception as e:     # an extra after the value: report it, keep the line
+                schedules[f"{m}/{b}"] = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
+                torch.cuda.empty_cache()
     population = None
     if sharded and world > 1 and "population_7b" in args.ops:
         # configs[4] on the same node, after the DiLoCo measurements (every rank takes part)
@@ -674,6 +696,8 @@ def main():
             out["roofline"] = roofline
         if weak:
             out["weak_scaling"] = weak
+        if schedules:
+            out["other_schedules"] = schedules
         if population:
             out["population_slerp_7b"] = population
         if not sharded:   # what a plain device-to-device copy reaches on this device, same process
