@@ -57,7 +57,7 @@ class ResidentPopulation:
                  lr: float = 0.7, momentum: float = 0.9, nesterov: bool = True,
                  dot_threshold: float = 0.9995, eps: float = 1e-8, elitism: int = 0,
                  group=None, kernels=None, keep_previous: bool = False, slerp_chunk: int | None = None,
-                 comm=None, exchange: str = "per_child"):
+                 comm=None, exchange: str = "per_child", exchange_groups: int = 1):
         if kind not in ("sgd", "slerp"):
             raise ValueError(kind)
         if kind == "sgd":
@@ -89,6 +89,7 @@ class ResidentPopulation:
         if exchange == "sharded" and (self.M != 1 or keep_previous or comm is None):
             raise EdtError("exchange='sharded' needs one member per rank, a communicator, no keep_previous")
         self.exchange = exchange
+        self.exchange_groups = exchange_groups      # sharded SLERP: exchanges pipelined over chunk groups
         self._sharded = None
         self.lr, self.momentum, self.nesterov = lr, momentum, nesterov
         self.dot_threshold, self.eps = dot_threshold, eps
@@ -379,7 +380,8 @@ class ResidentPopulation:
         if self._sharded is None:
             self._sharded = ShardedPopulationCrossover(self.layout, self.dtype, self.device, kind=self.kind,
                                                        comm=self.comm, kernels=self.kernels,
-                                                       chunk_elems=self.slerp_chunk or (1 << 16))
+                                                       chunk_elems=self.slerp_chunk or (1 << 16),
+                                                       groups=self.exchange_groups)
         m = self.rank
         if self.kind == "slerp":
             self._sharded.slerp_step(self._params[0], pairs, self._t, self._child[0], self.dot_threshold, self.eps)

@@ -57,7 +57,7 @@ def _scale(gen):
     return roulette_scale(gen + 1, 10)
 
 
-def run_resident(kind, device, kernels=None, comm=None, exchange="per_child"):
+def run_resident(kind, device, kernels=None, comm=None, exchange="per_child", exchange_groups=1):
     """The resident population over GENS generations; returns this rank's members. comm: a
     collectives.Collectives (virtual ranks); the host RNGs are seeded by rank 0 only (they are
     process-global, and only rank 0 draws)."""
@@ -70,7 +70,7 @@ def run_resident(kind, device, kernels=None, comm=None, exchange="per_child"):
         np.random.seed(7)
     pop = ResidentPopulation(layout, dt, device, _genomes(kind), kind=kind, elitism=1 if kind == "sgd" else 0,
                              seg_t=SEG_T if kind == "slerp" else None, kernels=kernels, comm=comm,
-                             exchange=exchange)
+                             exchange=exchange, exchange_groups=exchange_groups)
     for m in pop.local_members():
         (pop.base(m) if kind == "sgd" else pop.params(m)).copy_(_init(m, n, dt))
     for gen in range(GENS):
@@ -256,13 +256,14 @@ def test_resident_sharded_exchange_virtual_ranks(oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind", ["sgd", "slerp"])
-def test_resident_gpu_sharded_exchange(oracle, kind):
+@pytest.mark.parametrize("kind,groups", [("sgd", 1), ("slerp", 1), ("slerp", 3)])
+def test_resident_gpu_sharded_exchange(oracle, kind, groups):
     """exchange="sharded" with the HIP kernels on 4 virtual ranks: EDT-LM bit-exact, SLERP within
-    the SLERP bar of the reference flow."""
+    the SLERP bar of the reference flow (also with the exchanges pipelined over 3 chunk groups)."""
     from evolutionarydistributedtraining_amd.collectives import VirtualWorld
     dev = torch.device("cuda:0")
-    res = VirtualWorld(POP).run(lambda comm: run_resident(kind, dev, comm=comm, exchange="sharded"))
+    res = VirtualWorld(POP).run(lambda comm: run_resident(kind, dev, comm=comm, exchange="sharded",
+                                                          exchange_groups=groups))
     _check_world(res, POP, kind, oracle, slerp_tol=1e-5)
 
 
