@@ -305,7 +305,10 @@ def _stream_write(path: str, header: bytes, flat: torch.Tensor, staging_bytes: i
     hl = len(header)
 
     def writer(w):
-        torch.cuda.set_device(dev)
+        with torch.cuda.device(dev):        # restores the caller's current device afterwards
+            _write_chunks(w)
+
+    def _write_chunks(w):
         stage = _acquire_stage(staging_bytes, dev)
         try:
             stage.stream.wait_stream(caller)
