@@ -27,6 +27,10 @@ WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set, waits for them and exits w
 rank 0 prints the line. `--dry-run-launch` makes each rank print its environment and stop before
 device initialisation (the CPU test of the launcher).
 
+N>1 lines also carry, after the value: `weak_scaling` (population 8 per GPU), `other_schedules`
+(every other sharded schedule, timed the same way), `baseline_configs` (BASELINE configs[2]: 125M
+fp32 and configs[3]: 1.3B bf16, same population split) and `population_slerp_7b` (configs[4]).
+
 Every line carries `roofline` (the rank's local HBM kernels: at N = 1 the fused step, at N > 1 the
 schedule's kernels timed with HIP events inside the step; N > 1 adds the xGMI figure as
 `roofline.xgmi`) and `cpu_baseline` (rank 0, after the GPU phase, on the host's cores). At N = 1
@@ -96,6 +100,9 @@ def parse():
     p.add_argument("--compare-schedules", type=int, default=1,
                    help="N>1: after the value, also time the other sharded schedules (exact/workers, "
                         "exact/theta, reduce_ordered, reduce) and report them as 'other_schedules'")
+    p.add_argument("--config-companions", type=int, default=1,
+                   help="N>1: after the value, also time BASELINE configs[2] (125M fp32) and configs[3] "
+                        "(1.3B bf16) with the same population split ('baseline_configs')")
     p.add_argument("--population-groups", type=int, default=4,
                    help="N>1 population_7b: also time the link-balanced crossover with its exchanges "
                         "pipelined over this many chunk groups per rank (1: only the unpipelined form)")
@@ -610,7 +617,7 @@ def main():
             torch.cuda.empty_cache()
         sync = None
     schedules = None
-    if sharded and world > 1 and args.compare_schedules:
+    if sharded and args.compare_schedules:          # (world 1: the --sharded rehearsal)
         # every schedule the strong-scaling population can run, same steps, after the value: the
         # data to tune mode="auto" on this node (outside the reported value)
         sync = step = None
@@ -626,6 +633,27 @@ def main():
                                    "value": round(bytes_reduced / (ms_ / 1e3) / 1e9, 2)}
             except Exception as e:     # an extra after the value: report it, keep the line
                 schedules[f"{m}/{b}"] = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
+                torch.cuda.empty_cache()
+    configs = None
+    if sharded and args.config_companions:          # (world 1: the --sharded rehearsal)
+        # BASELINE's other multi-GPU DiLoCo configs on the same node, after the value: configs[2]
+        # (125M, 8 workers = 8 GPUs, fp32 as the reference computes) and configs[3] (1.3B, 8
+        # workers over the GPUs, bf16 params); same population split, the schedule auto picks
+        sync = step = None
+        torch.cuda.empty_cache()
+        configs = {}
+        for key, lname, cdt in (("configs2_125m_fp32", "gpt2_small", torch.float32),
+                                ("configs3_1p3b_bf16", "gpt_1p3b", torch.bfloat16)):
+            try:
+                lay_c = LAYOUTS[lname]()
+                ms_, name, wire_ = time_sharded(args, lay_c, cdt, cdt, k_local, dev, rank, args.steps, args.warmup)
+                b_c = k_total * lay_c.total * torch.finfo(cdt).bits // 8
+                configs[key] = {"layout": lname, "params": lay_c.total, "dtype": "f32" if cdt == torch.float32 else "bf16",
+                                "population": k_total, "workers_per_gpu": k_local, "schedule": name,
+                                "ms_per_step": round(ms_, 4), "value": round(b_c / (ms_ / 1e3) / 1e9, 2),
+                                "unit": "GB/s", "wire_bytes_per_rank": wire_}
+            except Exception as e:     # an extra after the value: report it, keep the line
+                configs[key] = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
                 torch.cuda.empty_cache()
     population = None
     if sharded and world > 1 and "population_7b" in args.ops:
@@ -698,6 +726,8 @@ def main():
             out["weak_scaling"] = weak
         if schedules:
             out["other_schedules"] = schedules
+        if configs:
+            out["baseline_configs"] = configs
         if population:
             out["population_slerp_7b"] = population
         if not sharded:   # what a plain device-to-device copy reaches on this device, same process
