@@ -34,7 +34,8 @@ fp32 and configs[3]: 1.3B bf16, same population split) and `population_slerp_7b`
 Every line carries `roofline` (the rank's local HBM kernels: at N = 1 the fused step, at N > 1 the
 schedule's kernels timed with HIP events inside the step; N > 1 adds the xGMI figure as
 `roofline.xgmi`) and `cpu_baseline` (rank 0, after the GPU phase, on the host's cores). At N = 1
-the line also carries `pair_merge` (EDT-LM child, 1.3B bf16) and `slerp_7b` (SLERP crossover of two
+the line also carries `configs1_125m` (BASELINE configs[1]: the 125M x 8 resident population,
+fp32), `pair_merge` (EDT-LM child, 1.3B bf16) and `slerp_7b` (SLERP crossover of two
 7B bodies, parents of one lineage and far parents), each with its kernel time, HBM roofline and an
 oracle CPU baseline on a sample (`--ops none` drops them).
 
@@ -93,9 +94,10 @@ def parse():
                         "timing the step's access pattern on each, once before the timed steps (placement.py); "
                         "1 keeps the first allocation")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
-    p.add_argument("--ops", default="pair_merge,slerp_7b,population_7b",
-                   help="the other hot-path measurements in the same line ('none': skip): N=1 pair_merge, "
-                        "slerp_7b; N>1 population_7b (BASELINE configs[4] across the N GPUs)")
+    p.add_argument("--ops", default="configs1_125m,pair_merge,slerp_7b,population_7b",
+                   help="the other hot-path measurements in the same line ('none': skip): N=1 configs1_125m "
+                        "(BASELINE configs[1]: 125M x 8 resident), pair_merge, slerp_7b; N>1 population_7b "
+                        "(BASELINE configs[4] across the N GPUs)")
     p.add_argument("--ops-cpu-seconds", type=float, default=4.0, help="CPU baseline budget per extra op")
     p.add_argument("--compare-schedules", type=int, default=1,
                    help="N>1: after the value, also time the other sharded schedules (exact/workers, "
@@ -265,6 +267,37 @@ def _pmc_traffic(args, key):
             return json.load(f).get(key, {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None
+
+
+def bench_config1(args, dev):
+    """BASELINE configs[1] — the configuration the metric is quoted on: a 125M-param LM
+    (gpt2_small, 148 tensors) with an 8-worker population resident on one GPU, fp32 (as the
+    reference computes the outer step), Nesterov SGD with the carried buffer; the momentum placed
+    by measurement as for the main line. value = 8 x P x 4 bytes reduced per step."""
+    from evolutionarydistributedtraining_amd.diloco import OuterSync
+    from evolutionarydistributedtraining_amd.layouts import gpt2_small
+    from evolutionarydistributedtraining_amd.params import ParamArena
+    lay = gpt2_small()
+    P, K = lay.total, 8
+    theta = ParamArena(lay, torch.float32, dev)
+    workers = [ParamArena(lay, torch.float32, dev) for _ in range(K)]
+    synth_population(theta.flat, [w.flat for w in workers], seed=1234)
+    sync = OuterSync(theta, workers, args.lr, args.momentum, bool(args.nesterov))
+    sync.step()
+    torch.cuda.synchronize()
+    if args.place_candidates > 1:
+        sync.place_momentum(args.place_candidates)
+    ms = _event_ms(sync.step, max(args.steps, 20), args.warmup)
+    per_elem = K * 4 + 16
+    gbs = per_elem * P / (ms / 1e3) / 1e9
+    del sync, theta, workers
+    torch.cuda.empty_cache()
+    return {"workload": f"DiLoCo outer step, gpt2_small P={P} T={len(lay)}, population {K} fp32 workers resident, "
+                        f"fp32 theta+momentum, lr {args.lr} mu {args.momentum} nesterov {bool(args.nesterov)}",
+            "ms_per_step": round(ms, 4), "value": round(K * P * 4 / (ms / 1e3) / 1e9, 2), "unit": "GB/s",
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(gbs / HBM_PEAK_GBPS, 4), "bytes_per_elem": per_elem,
+                         "algo_bytes_per_launch": per_elem * P}}
 
 
 def bench_pair_merge(args, dev):
@@ -781,7 +814,8 @@ def main():
                 sync.theta = sync.workers = sync.state = None
             theta = workers = sync = step = None
             torch.cuda.empty_cache()
-            for name, fn in (("pair_merge", bench_pair_merge), ("slerp_7b", bench_slerp_7b)):
+            for name, fn in (("configs1_125m", bench_config1), ("pair_merge", bench_pair_merge),
+                             ("slerp_7b", bench_slerp_7b)):
                 if name in args.ops:
                     try:
                         out[name] = fn(args, dev)
