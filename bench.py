@@ -30,6 +30,8 @@ device initialisation (the CPU test of the launcher).
 N>1 lines also carry, after the value: `weak_scaling` (population 8 per GPU), `other_schedules`
 (every other sharded schedule, timed the same way), `baseline_configs` (BASELINE configs[2]: 125M
 fp32 and configs[3]: 1.3B bf16, same population split) and `population_slerp_7b` (configs[4]).
+On that path rank 0 times its CPU baseline right after the value, and the extras run under
+`--extras-deadline` seconds (ExtrasDeadline): if they hang, the line still prints with the value.
 
 Every line carries `roofline` (the rank's local HBM kernels: at N = 1 the fused step, at N > 1 the
 schedule's kernels timed with HIP events inside the step; N > 1 adds the xGMI figure as
@@ -112,7 +114,58 @@ def parse():
                    help="N=1: also time the step fused with the worker broadcast against step + K copies")
     p.add_argument("--dry-run-launch", action="store_true",
                    help="each rank prints its rank environment and exits before device init")
+    p.add_argument("--extras-deadline", type=float, default=300.0,
+                   help="multi-GPU path: seconds allowed for everything after the value (companions, other "
+                        "schedules, BASELINE configs, population); past it rank 0 prints the line with what "
+                        "it has and every rank exits (0: no deadline)")
     return p.parse_args()
+
+
+class ExtrasDeadline:
+    """The multi-GPU line's safety net. The value is measured first; the extras after it (weak
+    companion, other schedules, BASELINE configs, the population crossover) put more collectives
+    and point-to-point exchanges on the node. If they have not finished `seconds` after they
+    start — a peer died or an exchange never completes — rank 0 prints the line it has (value,
+    rooflines, cpu_baseline and every extra that finished, plus `extras_deadline`) and every rank
+    exits, so a hang in an extra can never cost the measured value. `emit()` prints the line
+    exactly once, whichever thread gets there first."""
+
+    def __init__(self, seconds: float, rank: int, out: dict | None, json_out, exit_fn=None):
+        import threading
+        self.seconds, self.rank, self.out, self.json_out = seconds, rank, out, json_out
+        self.exit_fn = exit_fn or os._exit
+        self.lock = threading.Lock()
+        self.printed = False
+        self.fired = False
+        self.timer = None
+        if seconds > 0:
+            self.timer = threading.Timer(seconds, self._fire)
+            self.timer.daemon = True
+            self.timer.start()
+
+    def emit(self, extra: dict | None = None) -> bool:
+        """Rank 0: print the line (a snapshot of `out` + `extra`) unless it already has been."""
+        with self.lock:
+            if self.printed or self.rank != 0 or self.out is None:
+                return False
+            line = dict(self.out)
+            line.update(extra or {})
+            print(json.dumps(line), file=self.json_out, flush=True)
+            self.printed = True
+            return True
+
+    def _fire(self):
+        self.fired = True
+        pending = [k for k in ("weak_scaling", "other_schedules", "baseline_configs", "population_slerp_7b")
+                   if self.out is not None and k not in self.out]
+        self.emit({"extras_deadline": {"seconds": self.seconds, "unfinished_or_skipped": pending,
+                                       "note": "the extras after the value did not finish in time; the "
+                                               "value and what finished are reported, every rank exits"}})
+        self.exit_fn(0)
+
+    def cancel(self):
+        if self.timer is not None:
+            self.timer.cancel()
 
 
 def _free_port() -> int:
@@ -628,84 +681,17 @@ def main():
 
     bytes_reduced = k_total * P * torch.finfo(wdt).bits // 8
     value = bytes_reduced / (ms_per_step / 1e3) / 1e9
-
     sched = f"{sync.mode}/{sync.broadcast}" if sharded else None
     wire_main = sync.wire_bytes() if sharded else None
-    weak = None
-    if sharded and scaling == "strong" and args.weak_companion:     # (world 1: --sharded rehearsal)
-        # the same schedule with the N = 1 population on EVERY rank (population x N): per-GPU work
-        # fixed, so value_N / (N value_1) isolates the cost of the xGMI exchange
-        del sync, step
-        torch.cuda.empty_cache()
-        try:
-            w_ms, w_sched, w_wire = time_sharded(args, layout, tdt, wdt, args.population, dev, rank,
-                                                 args.steps, args.warmup)
-            w_bytes = args.population * world * P * torch.finfo(wdt).bits // 8
-            weak = {"workers_per_gpu": args.population, "population": args.population * world,
-                    "ms_per_step": round(w_ms, 4), "value": round(w_bytes / (w_ms / 1e3) / 1e9, 2),
-                    "unit": "GB/s", "schedule": w_sched, "wire_bytes_per_rank": w_wire,
-                    "note": "companion measurement after the timed strong-scaling steps; not the value"}
-        except Exception as e:     # the value is already measured: report, go on
-            weak = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
-            torch.cuda.empty_cache()
-        sync = None
-    schedules = None
-    if sharded and args.compare_schedules:          # (world 1: the --sharded rehearsal)
-        # every schedule the strong-scaling population can run, same steps, after the value: the
-        # data to tune mode="auto" on this node (outside the reported value)
-        sync = step = None
-        torch.cuda.empty_cache()
-        schedules = {}
-        for m, b in (("exact", "workers"), ("exact", "theta"), ("reduce_ordered", "theta"), ("reduce", "theta")):
-            if f"{m}/{b}" == sched:
-                continue
-            try:
-                ms_, name, wire_ = time_sharded(args, layout, tdt, wdt, k_local, dev, rank, args.steps,
-                                                args.warmup, mode=m, broadcast=b)
-                schedules[name] = {"ms_per_step": round(ms_, 4), "wire_bytes_per_rank": wire_,
-                                   "value": round(bytes_reduced / (ms_ / 1e3) / 1e9, 2)}
-            except Exception as e:     # an extra after the value: report it, keep the line
-                schedules[f"{m}/{b}"] = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
-                torch.cuda.empty_cache()
-    configs = None
-    if sharded and args.config_companions:          # (world 1: the --sharded rehearsal)
-        # BASELINE's other multi-GPU DiLoCo configs on the same node, after the value: configs[2]
-        # (125M, 8 workers = 8 GPUs, fp32 as the reference computes) and configs[3] (1.3B, 8
-        # workers over the GPUs, bf16 params); same population split, the schedule auto picks
-        sync = step = None
-        torch.cuda.empty_cache()
-        configs = {}
-        for key, lname, cdt in (("configs2_125m_fp32", "gpt2_small", torch.float32),
-                                ("configs3_1p3b_bf16", "gpt_1p3b", torch.bfloat16)):
-            try:
-                lay_c = LAYOUTS[lname]()
-                ms_, name, wire_ = time_sharded(args, lay_c, cdt, cdt, k_local, dev, rank, args.steps, args.warmup)
-                b_c = k_total * lay_c.total * torch.finfo(cdt).bits // 8
-                configs[key] = {"layout": lname, "params": lay_c.total, "dtype": "f32" if cdt == torch.float32 else "bf16",
-                                "population": k_total, "workers_per_gpu": k_local, "schedule": name,
-                                "ms_per_step": round(ms_, 4), "value": round(b_c / (ms_ / 1e3) / 1e9, 2),
-                                "unit": "GB/s", "wire_bytes_per_rank": wire_}
-            except Exception as e:     # an extra after the value: report it, keep the line
-                configs[key] = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
-                torch.cuda.empty_cache()
-    population = None
-    if sharded and world > 1 and "population_7b" in args.ops:
-        # configs[4] on the same node, after the DiLoCo measurements (every rank takes part)
-        sync = step = None
-        torch.cuda.empty_cache()
-        try:
-            from evolutionarydistributedtraining_amd.collectives import TorchCollectives
-            population = bench_population(args, dev, TorchCollectives())
-        except Exception as e:     # an extra after the value: report it, keep the line
-            population = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
-            torch.cuda.empty_cache()
 
+    # rank 0's line, built as soon as the value is measured; the extras below add to it
+    out = None
+    roofline = None
     if rank == 0:
         bg = torch.finfo(tdt).bits // 8
         bw = torch.finfo(wdt).bits // 8
         per_elem = k_local * bw + 2 * bg + (2 * bg if args.momentum else 0)
         algo_bytes = per_elem * P                       # one launch, steady state (carried buffer)
-        roofline = None
         if not sharded:
             achieved = algo_bytes / (kern_ms / 1e3) / 1e9
             traffic = None
@@ -721,6 +707,22 @@ def main():
                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                         "kernel": kernel_name, "kernel_ms": round(kern_ms, 4),
                         "bytes_per_elem": per_elem, "algo_bytes_per_launch": algo_bytes}
+        else:
+            # the rank's local kernels (HIP events inside the step, slowest rank) against HBM ...
+            achieved = kern_bytes / (kern_ms / 1e3) / 1e9
+            roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                        "kernel": kernel_name, "kernel_ms": round(kern_ms, 4),
+                        "algo_bytes_per_launch": kern_bytes, "schedule": sched,
+                        "note": "local kernels per rank and step (all buckets); the step itself is "
+                                "bounded by the xGMI exchange below"}
+            # ... and the exchange: bytes this rank puts on xGMI per step over the whole step time,
+            # against the outbound direction of the rank's links to its N-1 peers
+            xa = wire_main / (ms_per_step / 1e3) / 1e9
+            peak = XGMI_LINK_GBPS * (world - 1)
+            roofline["xgmi"] = {"bound": "xgmi", "achieved": round(xa, 1), "peak": peak, "unit": "GB/s",
+                                "frac": round(xa / peak, 4) if peak else None, "wire_bytes_per_rank": wire_main}
+        prop = torch.cuda.get_device_properties(dev)
         out = {
             "metric": "GB/s of param bytes reduced per outer step (device-resident), 1/2/4/8 GPUs",
             "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
@@ -736,69 +738,120 @@ def main():
                        "theta_dtype": args.theta_dtype,
                        "parallelism": "single GPU" if not sharded else
                                        f"dp{world} {sched} (RCCL)"},
+            "roofline": roofline,
+            "device": {"name": prop.name, "arch": getattr(prop, "gcnArchName", ""),
+                       "cus": prop.multi_processor_count, "hbm_gib": round(prop.total_memory / 2**30, 1)},
         }
-        if sharded:
-            # the rank's local kernels (HIP events inside the step, slowest rank) against HBM ...
-            achieved = kern_bytes / (kern_ms / 1e3) / 1e9
-            roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                        "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
-                        "kernel": kernel_name, "kernel_ms": round(kern_ms, 4),
-                        "algo_bytes_per_launch": kern_bytes, "schedule": sched,
-                        "note": "local kernels per rank and step (all buckets); the step itself is "
-                                "bounded by the xGMI exchange below"}
-            # ... and the exchange: bytes this rank puts on xGMI per step over the whole step time,
-            # against the outbound direction of the rank's links to its N-1 peers
-            wire = wire_main
-            xa = wire / (ms_per_step / 1e3) / 1e9
-            peak = XGMI_LINK_GBPS * (world - 1)
-            roofline["xgmi"] = {"bound": "xgmi", "achieved": round(xa, 1), "peak": peak, "unit": "GB/s",
-                                "frac": round(xa / peak, 4) if peak else None, "wire_bytes_per_rank": wire}
-        if roofline:
-            out["roofline"] = roofline
-        if weak:
-            out["weak_scaling"] = weak
-        if schedules:
-            out["other_schedules"] = schedules
-        if configs:
-            out["baseline_configs"] = configs
-        if population:
-            out["population_slerp_7b"] = population
-        if not sharded:   # what a plain device-to-device copy reaches on this device, same process
-            src = torch.empty(1 << 29, dtype=torch.float32, device=dev)
-            dst = torch.empty_like(src)
-            dst.copy_(src)
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record()
-            for _ in range(5):
-                dst.copy_(src)
-            b.record()
-            torch.cuda.synchronize()
-            roofline["device_copy_GBps"] = round(5 * 2 * src.numel() * 4 / (a.elapsed_time(b) / 1e3) / 1e9, 1)
-            del src, dst
-            # the step's own access pattern with a trivial body (edt_probe_stream), same arenas:
-            # the memory-system ceiling of this step on this device, measured after the timed steps
+
+    deadline = None
+    if sharded:
+        # multi-GPU path: rank 0 times the CPU baseline first (the other ranks wait at the barrier),
+        # then every extra runs under the deadline, so neither can be lost to a hang in an extra
+        if rank == 0 and args.cpu_baseline_seconds > 0:
+            out["cpu_baseline"] = cpu_baseline(args, tdt, wdt, k_total)
+        dist.barrier()
+        deadline = ExtrasDeadline(args.extras_deadline, rank, out, json_out)
+        sync = step = None
+        torch.cuda.empty_cache()
+        if scaling == "strong" and args.weak_companion:     # (world 1: --sharded rehearsal)
+            # the same schedule with the N = 1 population on EVERY rank (population x N): per-GPU
+            # work fixed, so value_N / (N value_1) isolates the cost of the xGMI exchange
             try:
-                probe_ms = stream_ceiling_ms(theta.flat, [w.flat for w in workers], sync.state.momentum)
-            except Exception as e:      # a measurement extra: the JSON line still prints
-                probe_ms = None
-                roofline["stream_ceiling_error"] = f"{type(e).__name__}: {e}"
-            if probe_ms:
-                ceil = algo_bytes / (probe_ms / 1e3) / 1e9
-                roofline["stream_ceiling_GBps"] = round(ceil, 1)
-                roofline["frac_of_stream_ceiling"] = round(roofline["achieved"] / ceil, 4)
-            if placement:
-                roofline["momentum_placement"] = placement
-        prop = torch.cuda.get_device_properties(dev)
-        out["device"] = {"name": prop.name, "arch": getattr(prop, "gcnArchName", ""),
-                         "cus": prop.multi_processor_count, "hbm_gib": round(prop.total_memory / 2**30, 1)}
-        if not sharded and args.bcast_compare:
+                w_ms, w_sched, w_wire = time_sharded(args, layout, tdt, wdt, args.population, dev, rank,
+                                                     args.steps, args.warmup)
+                w_bytes = args.population * world * P * torch.finfo(wdt).bits // 8
+                weak = {"workers_per_gpu": args.population, "population": args.population * world,
+                        "ms_per_step": round(w_ms, 4), "value": round(w_bytes / (w_ms / 1e3) / 1e9, 2),
+                        "unit": "GB/s", "schedule": w_sched, "wire_bytes_per_rank": w_wire,
+                        "note": "companion measurement after the timed strong-scaling steps; not the value"}
+            except Exception as e:     # the value is already measured: report, go on
+                weak = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
+                torch.cuda.empty_cache()
+            if out is not None:
+                out["weak_scaling"] = weak
+        if args.compare_schedules:
+            # every schedule the strong-scaling population can run, same steps, after the value: the
+            # data to tune mode="auto" on this node (outside the reported value)
+            schedules = {}
+            for m, b in (("exact", "workers"), ("exact", "theta"), ("reduce_ordered", "theta"), ("reduce", "theta")):
+                if f"{m}/{b}" == sched:
+                    continue
+                try:
+                    ms_, name, wire_ = time_sharded(args, layout, tdt, wdt, k_local, dev, rank, args.steps,
+                                                    args.warmup, mode=m, broadcast=b)
+                    schedules[name] = {"ms_per_step": round(ms_, 4), "wire_bytes_per_rank": wire_,
+                                       "value": round(bytes_reduced / (ms_ / 1e3) / 1e9, 2)}
+                except Exception as e:     # an extra after the value: report it, keep the line
+                    schedules[f"{m}/{b}"] = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
+                    torch.cuda.empty_cache()
+            if out is not None:
+                out["other_schedules"] = schedules
+        if args.config_companions:
+            # BASELINE's other multi-GPU DiLoCo configs on the same node, after the value: configs[2]
+            # (125M, 8 workers = 8 GPUs, fp32 as the reference computes) and configs[3] (1.3B, 8
+            # workers over the GPUs, bf16 params); same population split, the schedule auto picks
+            configs = {}
+            for key, lname, cdt in (("configs2_125m_fp32", "gpt2_small", torch.float32),
+                                    ("configs3_1p3b_bf16", "gpt_1p3b", torch.bfloat16)):
+                try:
+                    lay_c = LAYOUTS[lname]()
+                    ms_, name, wire_ = time_sharded(args, lay_c, cdt, cdt, k_local, dev, rank, args.steps,
+                                                    args.warmup)
+                    b_c = k_total * lay_c.total * torch.finfo(cdt).bits // 8
+                    configs[key] = {"layout": lname, "params": lay_c.total,
+                                    "dtype": "f32" if cdt == torch.float32 else "bf16",
+                                    "population": k_total, "workers_per_gpu": k_local, "schedule": name,
+                                    "ms_per_step": round(ms_, 4), "value": round(b_c / (ms_ / 1e3) / 1e9, 2),
+                                    "unit": "GB/s", "wire_bytes_per_rank": wire_}
+                except Exception as e:     # an extra after the value: report it, keep the line
+                    configs[key] = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
+                    torch.cuda.empty_cache()
+            if out is not None:
+                out["baseline_configs"] = configs
+        if world > 1 and "population_7b" in args.ops:
+            # configs[4] on the same node, after the DiLoCo measurements (every rank takes part)
+            try:
+                from evolutionarydistributedtraining_amd.collectives import TorchCollectives
+                population = bench_population(args, dev, TorchCollectives())
+            except Exception as e:     # an extra after the value: report it, keep the line
+                population = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
+                torch.cuda.empty_cache()
+            if out is not None:
+                out["population_slerp_7b"] = population
+
+    if rank == 0 and not sharded:
+        # what a plain device-to-device copy reaches on this device, same process
+        src = torch.empty(1 << 29, dtype=torch.float32, device=dev)
+        dst = torch.empty_like(src)
+        dst.copy_(src)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(5):
+            dst.copy_(src)
+        b.record()
+        torch.cuda.synchronize()
+        roofline["device_copy_GBps"] = round(5 * 2 * src.numel() * 4 / (a.elapsed_time(b) / 1e3) / 1e9, 1)
+        del src, dst
+        # the step's own access pattern with a trivial body (edt_probe_stream), same arenas:
+        # the memory-system ceiling of this step on this device, measured after the timed steps
+        try:
+            probe_ms = stream_ceiling_ms(theta.flat, [w.flat for w in workers], sync.state.momentum)
+        except Exception as e:      # a measurement extra: the JSON line still prints
+            probe_ms = None
+            roofline["stream_ceiling_error"] = f"{type(e).__name__}: {e}"
+        if probe_ms:
+            ceil = algo_bytes / (probe_ms / 1e3) / 1e9
+            roofline["stream_ceiling_GBps"] = round(ceil, 1)
+            roofline["frac_of_stream_ceiling"] = round(roofline["achieved"] / ceil, 4)
+        if placement:
+            roofline["momentum_placement"] = placement
+        if args.bcast_compare:
             # the step with the broadcast of diloco.py:302-308 (every worker restarts from theta):
             # fused into the kernel's pass vs the step + K device copies
             try:
                 fused = _event_ms(lambda: sync.step(broadcast=True), args.steps, 2)
                 unfused = _event_ms(lambda: (sync.step(), sync.broadcast_()), args.steps, 2)
-                bw = torch.finfo(wdt).bits // 8
-                fb = algo_bytes + k_local * P * bw
+                fb = algo_bytes + k_local * P * (torch.finfo(wdt).bits // 8)
                 out["step_with_broadcast"] = {
                     "fused_ms": round(fused, 4), "step_plus_copies_ms": round(unfused, 4),
                     "kernel": "outer_kernel<..., BC=true> (edt_outer_step_bcast)",
@@ -808,10 +861,9 @@ def main():
                                        "algo_bytes_per_launch": fb}}
             except Exception as e:          # an extra: report it, keep the line
                 out["step_with_broadcast"] = {"error": f"{type(e).__name__}: {str(e)[:300]}"}
-        if not sharded and args.ops and args.ops != "none":
+        if args.ops and args.ops != "none":
             # the other hot-path kernels, one GPU, after the outer step's arenas are freed
-            if sync is not None:
-                sync.theta = sync.workers = sync.state = None
+            sync.theta = sync.workers = sync.state = None
             theta = workers = sync = step = None
             torch.cuda.empty_cache()
             for name, fn in (("configs1_125m", bench_config1), ("pair_merge", bench_pair_merge),
@@ -826,11 +878,14 @@ def main():
             # rank 0 after the GPU phase, on this host's cores: the whole population's step (the
             # reference's master runs all K workers' deltas on its CPU)
             out["cpu_baseline"] = cpu_baseline(args, tdt, wdt, k_total)
-        print(json.dumps(out), file=json_out, flush=True)
-    if sharded:
-        dist.barrier()
-        dist.destroy_process_group()
-
+    if deadline is None:
+        if rank == 0:
+            print(json.dumps(out), file=json_out, flush=True)
+        return
+    deadline.emit()
+    dist.barrier()          # still under the deadline: a rank stuck in an extra cannot hang the exit
+    deadline.cancel()
+    dist.destroy_process_group()
 
 if __name__ == "__main__":
     main()
