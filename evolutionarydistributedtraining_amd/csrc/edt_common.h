@@ -110,6 +110,26 @@ constexpr int kVec = 8;                             // elements per thread per i
 // grid cap for the grid-stride loops: 256 CUs x workgroups per CU (0 = one pass, no cap)
 constexpr uint64_t kMaxBlocks = EDT_BLOCKS_PER_CU > 0 ? 256ull * EDT_BLOCKS_PER_CU : (1ull << 31) - 1;
 
+// XCD-aware block order for the one-pass stream kernels (outer_kernel, pair_kernel). Workgroups
+// are dispatched round-robin over the 8 XCDs (block b on XCD b % 8), so by default the XCDs
+// interleave at one tile. EDT_XCD_RUN = M > 0 permutes the blocks so each XCD streams runs of M
+// consecutive tiles (M = -1: one contiguous 1/8 of the arena per XCD). A permutation of
+// [0, gridDim): every tile is still processed exactly once, by one workgroup.
+#ifndef EDT_XCD_RUN
+#define EDT_XCD_RUN 0
+#endif
+__device__ __forceinline__ uint64_t xcd_block(uint64_t b, uint64_t G) {
+    if constexpr (EDT_XCD_RUN == 0) {
+        return b;
+    } else {
+        const uint64_t M = EDT_XCD_RUN > 0 ? (uint64_t)EDT_XCD_RUN : G / 8;
+        const uint64_t span = 8 * M;                 // blocks per group: M tiles on each XCD
+        if (M == 0 || b >= G / span * span) return b;    // the ragged last group keeps its order
+        const uint64_t g = b / span, x = b % 8, j = (b / 8) % M;
+        return g * span + x * M + j;
+    }
+}
+
 constexpr uint64_t kSlerpMaxBlocks = EDT_SLERP_GRID ? (1ull << 31) - 1 : 256ull * EDT_SLERP_BPC;
 // chunk-sum passes: one workgroup per chunk (EDT_SLERP_GRID), else a grid-stride cap
 inline unsigned slerp_grid(int64_t nchunks) {

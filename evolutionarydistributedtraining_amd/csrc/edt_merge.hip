@@ -90,7 +90,7 @@ __device__ __forceinline__ void pair_elems(const PairArgs& a, uint64_t i) {
 template <int GDT, int WDT, int N>
 __global__ __launch_bounds__(kBlock) void pair_kernel(PairArgs a) {
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-    const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t tid = xcd_block(blockIdx.x, gridDim.x) * kBlock + threadIdx.x;
     if constexpr (N == kVec) {
         const uint64_t nv = a.n / kVec;
         for (uint64_t v = tid; v < nv; v += stride) pair_elems<GDT, WDT, kVec>(a, v * kVec);

@@ -124,7 +124,7 @@ __device__ __forceinline__ void outer_elems(const A& a, uint64_t i) {
 template <int GDT, int WDT, int KC, int DIV, int MODE, int N, bool BC = false>
 __global__ __launch_bounds__(kBlock, EDT_MIN_WAVES) void outer_kernel(OuterArgs a) {
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-    const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t tid = xcd_block(blockIdx.x, gridDim.x) * kBlock + threadIdx.x;
     if constexpr (N == kVec && split_halves<GDT, WDT>()) {
         // tiles of kBlock x 8 elements; thread t owns [4t, 4t+4) and [4(kBlock+t), +4) of a tile
         constexpr int H2 = 4 * kBlock;

@@ -46,6 +46,9 @@ SLERP_VARIANTS = {"s_default": [],
                   "s_nt_coefblk": ["-DEDT_NT_SLERP=1", "-DEDT_SLERP_COEF_BLOCK=1"],
                   "s_bpc32_nt": ["-DEDT_SLERP_BPC=32", "-DEDT_NT_SLERP=1"],
                   "s_bpc8_nt": ["-DEDT_SLERP_BPC=8", "-DEDT_NT_SLERP=1"]}
+# XCD-aware block order (edt_common.h xcd_block): runs of M consecutive tiles per XCD
+VARIANTS.update({f"xcd{m}": [f"-DEDT_XCD_RUN={m}"] for m in (2, 8, 64, 512)})
+VARIANTS["xcd_full"] = ["-DEDT_XCD_RUN=-1"]
 VARIANTS.update({"lerp_nt": ["-DEDT_NT_LERP=1"], "nt0": ["-DEDT_NT_LOADS=0"],
                  "bpc32_nt0": ["-DEDT_BLOCKS_PER_CU=32", "-DEDT_NT_LOADS=0"]})
 
