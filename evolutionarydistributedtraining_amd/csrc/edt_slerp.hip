@@ -662,6 +662,7 @@ int64_t edt_slerp_make_chunks(const uint64_t* seg_offsets, int nseg, uint32_t ch
 int edt_slerp_stats(const void* v0, const void* v1, int in_dt, const uint64_t* chunk_desc, int64_t nchunks,
                     double* partial, void* stream) {
     g_err[0] = 0;
+    if (nchunks < 0) return fail(EDT_ERR_ARG, "negative chunk count");
     if (nchunks == 0) return EDT_OK;
     if (!v0 || !v1) return fail(EDT_ERR_ARG, "null buffer");
     if (!aligned16(v0) || !aligned16(v1)) return fail(EDT_ERR_ARG, "slerp inputs must be 16-byte aligned");
@@ -671,6 +672,7 @@ int edt_slerp_stats(const void* v0, const void* v1, int in_dt, const uint64_t* c
 int edt_slerp_coef(const double* partial, const int32_t* seg_first_chunk, int nseg, const double* t,
                    double dot_threshold, double eps, float* coef, float* dot_out, void* stream) {
     g_err[0] = 0;
+    if (nseg < 0) return fail(EDT_ERR_ARG, "negative segment count");
     if (nseg == 0) return EDT_OK;
     if (!partial || !seg_first_chunk || !t || !coef) return fail(EDT_ERR_ARG, "null buffer");
     const unsigned g = coef_grid(nseg);
@@ -682,6 +684,7 @@ int edt_slerp_coef(const double* partial, const int32_t* seg_first_chunk, int ns
 int edt_slerp_blend(const void* v0, const void* v1, int in_dt, void* out, int out_dt, const uint64_t* chunk_desc,
                     int64_t nchunks, const float* coef, void* stream) {
     g_err[0] = 0;
+    if (nchunks < 0) return fail(EDT_ERR_ARG, "negative chunk count");
     if (nchunks == 0) return EDT_OK;
     if (!v0 || !v1 || !out) return fail(EDT_ERR_ARG, "null buffer");
     if (!aligned16(v0) || !aligned16(v1) || !aligned16(out))
@@ -884,6 +887,7 @@ int edt_slerp_blend_children(const void* const* members, int nmembers, int in_dt
         return fail(EDT_ERR_ARG, "member count %d out of range [1, %d]", nmembers, kGramMaxMembers);
     if (npairs < 0 || npairs > kBlendMaxChildren)
         return fail(EDT_ERR_ARG, "child count %d out of range [0, %d]", npairs, kBlendMaxChildren);
+    if (nchunks < 0 || nseg < 0) return fail(EDT_ERR_ARG, "negative count");
     if (npairs == 0 || nchunks == 0) return EDT_OK;
     if (!members || !pairs || !outs || !chunk_desc || !coef) return fail(EDT_ERR_ARG, "null buffer");
     Members mem;
@@ -915,6 +919,7 @@ int edt_slerp_merge_speculative(const void* v0, const void* v1, int in_dt, void*
                                 float* coef, float* dot_out, int32_t* redo, uint64_t n, void* stream) {
     g_err[0] = 0;
     if ((in_dt | out_dt) & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
+    if (nseg < 0 || nchunks < 0) return fail(EDT_ERR_ARG, "negative count");
     if (nseg == 0 || nchunks == 0) return EDT_OK;
     if (!v0 || !v1 || !out || !chunk_desc || !seg_first_chunk || !t || !partial || !coef || !redo)
         return fail(EDT_ERR_ARG, "null buffer");
@@ -1100,7 +1105,7 @@ int edt_slerp_merge_list(const void* const* v0_t, const void* const* v1_t, int i
                          int nseg, const double* t, double dot_threshold, double eps, double* partial, float* coef,
                          float* dot_out, void* workspace, uint64_t workspace_bytes, void* stream) {
     g_err[0] = 0;
-    if (nseg < 0) return fail(EDT_ERR_ARG, "segment count %d < 0", nseg);
+    if (nseg < 0 || nchunks < 0) return fail(EDT_ERR_ARG, "negative count (segments %d, chunks %lld)", nseg, (long long)nchunks);
     if (nseg == 0 || nchunks == 0) return EDT_OK;
     if (!v0_t || !v1_t || !out_t) return fail(EDT_ERR_ARG, "null tensor table");
     const uint64_t need = 3ull * sizeof(uint64_t) * (uint64_t)nseg;

@@ -304,6 +304,18 @@ def test_abi_error_convention_without_device():
     # edt_lerp (crossover.py:50-51): fp32 inputs computed in bf16 is not a reference combination
     err(lib.edt_lerp(p[1], p[2], F32, p[3], F32, BF16, 8, 0.5, None), "bf16 compute of fp32")
     err(lib.edt_lerp(p[1], None, BF16, p[3], BF16, BF16, 8, 0.5, None), "null buffer")
+    # the split SLERP passes and the one-call forms (EDT_RL/crossover.py:11-43): negative chunk /
+    # segment counts are rejected before any grid is sized from them
+    err(lib.edt_slerp_stats(p[1], p[2], BF16, p[3], -1, p[4], None), "negative")
+    err(lib.edt_slerp_coef(p[1], p[2], -2, p[3], 0.9995, 1e-8, p[4], None, None), "negative")
+    err(lib.edt_slerp_blend(p[1], p[2], BF16, p[3], BF16, p[4], -1, p[5], None), "negative")
+    err(lib.edt_slerp_merge(p[1], p[2], BF16, p[3], BF16, p[4], -1, p[5], 1, p[6], 0.9995, 1e-8, p[7], p[8],
+                            None, None), "negative")
+    err(lib.edt_slerp_merge_speculative(p[1], p[2], BF16, p[3], BF16, p[4], -1, p[5], 1, p[6], 0.9995, 1e-8,
+                                        p[7], p[8], None, p[9], 8, None), "negative")
+    err(lib.edt_slerp_blend_children(arr(p[1:3]), 2, BF16, (ctypes.c_int32 * 2)(0, 1), 1, arr(p[5:6]), BF16, p[6],
+                                     -1, p[7], 1, None), "negative")
+    assert lib.edt_slerp_stats(p[1], p[2], BF16, p[3], 0, p[4], None) == 0          # no chunks: nothing to do
 
 
 def test_host_code_under_asan_and_ubsan():
