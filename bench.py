@@ -35,7 +35,8 @@ On that path rank 0 times its CPU baseline right after the value, and the extras
 
 Every line carries `roofline` (the rank's local HBM kernels: at N = 1 the fused step, at N > 1 the
 schedule's kernels timed with HIP events inside the step; N > 1 adds the xGMI figure as
-`roofline.xgmi`) and `cpu_baseline` (rank 0, after the GPU phase, on the host's cores). At N = 1
+`roofline.xgmi`) and `cpu_baseline` (rank 0, on the host's cores: at N = 1 after the GPU phase, at
+N > 1 right after the timed steps). At N = 1
 the line also carries `configs1_125m` (BASELINE configs[1]: the 125M x 8 resident population,
 fp32), `pair_merge` (EDT-LM child, 1.3B bf16) and `slerp_7b` (SLERP crossover of two
 7B bodies, parents of one lineage and far parents), each with its kernel time, HBM roofline and an
@@ -114,6 +115,8 @@ def parse():
                    help="N=1: also time the step fused with the worker broadcast against step + K copies")
     p.add_argument("--dry-run-launch", action="store_true",
                    help="each rank prints its rank environment and exits before device init")
+    p.add_argument("--dry-run-sleep", type=float, default=0.0,
+                   help="with --dry-run-launch: each rank then sleeps this long (launcher signal tests)")
     p.add_argument("--extras-deadline", type=float, default=300.0,
                    help="multi-GPU path: seconds allowed for everything after the value (companions, other "
                         "schedules, BASELINE configs, population); past it rank 0 prints the line with what "
@@ -178,14 +181,39 @@ def _free_port() -> int:
 def launch_ranks(n: int) -> int:
     """`--gpus N` without torchrun: N child processes running this script with the rank
     environment torchrun would give them. Runs in a process that has not touched the GPU and
-    starts children (never exec). A failing rank ends the others. Returns the exit status."""
+    starts children (never exec). A failing rank ends the others; a launcher stopped by SIGTERM /
+    SIGINT / SIGHUP passes the signal on to its ranks and waits for them, and a launcher killed
+    outright takes them with it (PR_SET_PDEATHSIG), so no rank outlives a timed-out run holding
+    its GPU. Returns the exit status."""
+    import signal
     import subprocess
     port = _free_port()
     procs = []
+
+    def die_with_parent():              # in the child before exec: SIGTERM when this launcher dies
+        try:
+            import ctypes
+            ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGTERM)    # PR_SET_PDEATHSIG
+        except OSError:
+            pass
+
+    def forward(signum, _frame):        # a launcher stopped by a signal stops its ranks first
+        for q in procs:
+            if q.poll() is None:
+                q.send_signal(signum)
+        for q in procs:
+            try:
+                q.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                q.kill()
+        sys.exit(128 + signum)
+    for sig in (signal.SIGTERM, signal.SIGINT, signal.SIGHUP):
+        signal.signal(sig, forward)
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env,
+                                      preexec_fn=die_with_parent))
     status = 0
     live = list(procs)
     while live:
@@ -574,8 +602,9 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     if args.dry_run_launch:
-        print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
-                                                          "MASTER_PORT")}), flush=True)
+        print(json.dumps({**{k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                                             "MASTER_PORT")}, "PID": os.getpid()}), flush=True)
+        time.sleep(args.dry_run_sleep)
         return
     # stdout carries exactly one JSON line (rank 0): everything else the libraries print on fd 1
     # (RCCL's version banner at communicator init, ROCm notices) is sent to stderr

@@ -37,3 +37,35 @@ def test_bench_launcher_propagates_a_rank_failure():
                        capture_output=True, text=True, env=env, timeout=300)
     assert p.returncode != 0
     assert p.stderr.count("Traceback") >= 1
+
+
+def _alive(pid):
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    with open(f"/proc/{pid}/stat") as f:          # a zombie is gone for our purpose
+        return f.read().split(")")[-1].split()[0] != "Z"
+
+
+@pytest.mark.parametrize("how", ["term", "kill"])
+def test_bench_launcher_takes_its_ranks_down(how):
+    """A launcher stopped by SIGTERM forwards it and waits for its ranks; one killed outright
+    (SIGKILL: no handler runs) still takes them with it (PR_SET_PDEATHSIG). Either way no rank is
+    left running, as a timed-out driver run must not leave ranks holding GPUs."""
+    import signal
+    import time
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                           "MASTER_PORT")}
+    p = subprocess.Popen([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run-launch",
+                          "--dry-run-sleep", "120"], stdout=subprocess.PIPE, text=True, env=env)
+    pids = [json.loads(p.stdout.readline())["PID"] for _ in range(2)]
+    assert all(_alive(q) for q in pids)
+    p.send_signal(signal.SIGTERM if how == "term" else signal.SIGKILL)
+    p.wait(timeout=60)
+    deadline = time.time() + 30
+    while time.time() < deadline and any(_alive(q) for q in pids):
+        time.sleep(0.1)
+    assert not any(_alive(q) for q in pids)
+    if how == "term":
+        assert p.returncode == 128 + signal.SIGTERM
