@@ -103,14 +103,47 @@ __global__ __launch_bounds__(256) void step10_kernel(Ptrs p, float* theta, float
     }
 }
 
+// theta and momentum interleaved per tile in ONE buffer (tile t: 2,048 theta floats then 2,048
+// momentum floats): the two read-modify-write streams always sit side by side in HBM, whatever
+// the allocation — does that make the step's rate independent of placement?
+template <bool NT>
+__global__ __launch_bounds__(256) void step10_il_kernel(Ptrs p, float* tm, uint64_t n) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const uint64_t i = idx(h);
+        if (i + 4 > n) continue;
+        const uint64_t j = (uint64_t)blockIdx.x * 4096 + (uint64_t)h * 1024 + (uint64_t)threadIdx.x * 4;
+        f4 x[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x[k] = ld4<NT>(p.in[k] + i);
+        f4 th = *reinterpret_cast<const f4*>(tm + j);
+        f4 m = *reinterpret_cast<const f4*>(tm + j + 2048);
+        f4 d = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) d += x[k] - th;
+        m = 0.9f * m + d * 0.125f;
+        *reinterpret_cast<f4*>(tm + j + 2048) = m;
+        *reinterpret_cast<f4*>(tm + j) = th + 0.7f * m;
+    }
+}
+
 int main(int argc, char** argv) {
     const uint64_t n = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 1315723264ull;
     const uint64_t bytes = n * 4;
+    // argv[2]: MiB of spacer allocated between theta and momentum (shifts their relative placement)
+    const uint64_t spacer = argc > 2 ? std::strtoull(argv[2], nullptr, 10) << 20 : 0;
+    const bool only_step = argc > 3;       // argv[3] present: only the two step kernels
     std::vector<float*> bufs(11);
-    for (auto& b : bufs) {
-        CHECK(hipMalloc(&b, bytes));
-        CHECK(hipMemset(b, 0, bytes));
+    float* gap = nullptr;
+    for (int q = 0; q < 11; ++q) {
+        if (q == 9 && spacer) CHECK(hipMalloc(&gap, spacer));
+        CHECK(hipMalloc(&bufs[q], bytes));
+        CHECK(hipMemset(bufs[q], 0, bytes));
     }
+    float* tm = nullptr;
+    const uint64_t grid_tiles = (n + 2047) / 2048;
+    CHECK(hipMalloc(&tm, grid_tiles * 4096 * 4));
+    CHECK(hipMemset(tm, 0, grid_tiles * 4096 * 4));
     Ptrs p;
     for (int k = 0; k < 8; ++k) p.in[k] = bufs[k];
     float* theta = bufs[8];
@@ -140,6 +173,13 @@ int main(int argc, char** argv) {
         std::fflush(stdout);
     };
     const double B = (double)bytes;
+    if (only_step) {
+        for (int r = 0; r < 3; ++r) {
+            time("step10", 12 * B, [&] { step10_kernel<false><<<grid, 256>>>(p, theta, mom, n); });
+            time("step10_il", 12 * B, [&] { step10_il_kernel<false><<<grid, 256>>>(p, tm, n); });
+        }
+        return 0;
+    }
     time("copy", 2 * B, [&] { copy_kernel<false><<<grid, 256>>>(bufs[0], out, n); });
     time("copy_nt", 2 * B, [&] { copy_kernel<true><<<grid, 256>>>(bufs[0], out, n); });
     time("read8", 8 * B, [&] { read8_kernel<false, false><<<grid, 256>>>(p, out, n); });
@@ -148,7 +188,10 @@ int main(int argc, char** argv) {
     time("read8w1_nt", 9 * B, [&] { read8_kernel<true, true><<<grid, 256>>>(p, out, n); });
     time("step10", 12 * B, [&] { step10_kernel<false><<<grid, 256>>>(p, theta, mom, n); });
     time("step10_nt", 12 * B, [&] { step10_kernel<true><<<grid, 256>>>(p, theta, mom, n); });
+    time("step10_il", 12 * B, [&] { step10_il_kernel<false><<<grid, 256>>>(p, tm, n); });
     CHECK(hipGetLastError());
     for (auto& x : bufs) CHECK(hipFree(x));
+    CHECK(hipFree(tm));
+    if (gap) CHECK(hipFree(gap));
     return 0;
 }
