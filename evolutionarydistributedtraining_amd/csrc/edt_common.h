@@ -140,6 +140,9 @@ inline unsigned slerp_grid(int64_t nchunks) {
 #ifndef EDT_SLERP_SPEC_BPC
 #define EDT_SLERP_SPEC_BPC 256
 #endif
+#ifndef EDT_SLERP_SPEC_CONTIG       // speculative pass: k > 0 = k consecutive chunks per workgroup
+#define EDT_SLERP_SPEC_CONTIG 0     // (address order); 0 = grid-stride over EDT_SLERP_SPEC_BPC per CU
+#endif
 #ifndef EDT_SLERP_GRAM_GRID
 #define EDT_SLERP_GRAM_GRID 0
 #endif

@@ -173,7 +173,13 @@ __global__ __launch_bounds__(kBlock) void slerp_stats_lerp_kernel(const void* v0
                                                                   const uint64_t* chunks, int64_t nchunks,
                                                                   double* partial, const double* tvals) {
     __shared__ double red[3][kBlock / 64];
-    for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    // EDT_SLERP_SPEC_CONTIG = k > 0: workgroup b takes chunks [b k, b k + k) (address order);
+    // 0: grid-stride. Either way each chunk's sums come from one workgroup in the same order.
+    const int64_t c_first = EDT_SLERP_SPEC_CONTIG > 0 ? (int64_t)blockIdx.x * EDT_SLERP_SPEC_CONTIG : (int64_t)blockIdx.x;
+    const int64_t c_step = EDT_SLERP_SPEC_CONTIG > 0 ? 1 : (int64_t)gridDim.x;
+    const int64_t c_end = EDT_SLERP_SPEC_CONTIG > 0 ? (c_first + EDT_SLERP_SPEC_CONTIG < nchunks
+                                                        ? c_first + EDT_SLERP_SPEC_CONTIG : nchunks) : nchunks;
+    for (int64_t c = c_first; c < c_end; c += c_step) {
         const uint64_t seg = chunks[3 * c + 2];
         double sums[3];
         chunk_pass<IDT, EDT_NT_SLERP != 0 && IDT == EDT_BF16, true, ODT>(
@@ -933,7 +939,8 @@ int edt_slerp_merge_speculative(const void* v0, const void* v1, int in_dt, void*
         if (p0 < o1 && o0 < p1) return fail(EDT_ERR_ARG, "speculative SLERP needs an output apart from the parents");
     }
     hipStream_t s = (hipStream_t)stream;
-    const unsigned g = slerp_spec_grid(nchunks);
+    const unsigned g = EDT_SLERP_SPEC_CONTIG > 0 ? (unsigned)((nchunks + EDT_SLERP_SPEC_CONTIG - 1) / EDT_SLERP_SPEC_CONTIG)
+                                                 : slerp_spec_grid(nchunks);
     if (in_dt == EDT_F32 && out_dt == EDT_F32)
         slerp_stats_lerp_kernel<EDT_F32, EDT_F32><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, partial, t);
     else if (in_dt == EDT_F32)

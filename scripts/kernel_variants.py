@@ -49,6 +49,9 @@ SLERP_VARIANTS = {"s_default": [],
 # XCD-aware block order (edt_common.h xcd_block): runs of M consecutive tiles per XCD
 VARIANTS.update({f"xcd{m}": [f"-DEDT_XCD_RUN={m}"] for m in (2, 8, 64, 512)})
 VARIANTS["xcd_full"] = ["-DEDT_XCD_RUN=-1"]
+# speculative SLERP pass: k consecutive chunks per workgroup in address order (EDT_SLERP_SPEC_CONTIG)
+VARIANTS.update({f"spec_c{k}": [f"-DEDT_SLERP_SPEC_CONTIG={k}"] for k in (1, 2, 3, 4)})
+VARIANTS.update({f"spec_b{b}": [f"-DEDT_SLERP_SPEC_BPC={b}"] for b in (32, 64, 128, 192)})
 VARIANTS.update({"lerp_nt": ["-DEDT_NT_LERP=1"], "nt0": ["-DEDT_NT_LOADS=0"],
                  "bpc32_nt0": ["-DEDT_BLOCKS_PER_CU=32", "-DEDT_NT_LOADS=0"]})
 
