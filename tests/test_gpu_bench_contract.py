@@ -1,0 +1,69 @@
+"""bench.py's output contract, checked on the device: ONE JSON line on stdout with the fields the
+driver parses (metric / value / unit / n_gpus / steps / warmup / ms_per_step / higher_is_better /
+scaling / vs_baseline / dtype / data / config), plus the `roofline` object (bound, achieved, peak,
+unit, frac = achieved / peak, traffic) and the `cpu_baseline` object (value, unit, cores, kind,
+sample) — for the single-GPU line and for the multi-GPU code path at world 1 (`--sharded`, which
+adds roofline.xgmi). Small layout and short budgets: the contract, not the numbers."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TOP = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+       "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"}
+
+
+def _run(*extra):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                           "MASTER_PORT")}
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--layout", "gpt2_small", "--steps", "3", "--warmup", "1",
+           "--cpu-baseline-seconds", "0.4", "--cpu-sample-elems", str(1 << 18), "--ops-cpu-seconds", "0.2", *extra]
+    p = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=110)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, p.stdout              # stdout carries exactly the one JSON line
+    return json.loads(lines[0])
+
+
+def _check_common(d, n_gpus):
+    assert TOP <= set(d), TOP - set(d)
+    assert d["metric"] == "GB/s of param bytes reduced per outer step (device-resident), 1/2/4/8 GPUs"
+    assert d["unit"] == "GB/s" and d["n_gpus"] == n_gpus and d["steps"] == 3 and d["warmup"] == 1
+    assert d["higher_is_better"] is True and d["scaling"] in ("strong", "weak") and d["vs_baseline"] is None
+    assert d["value"] > 0 and d["ms_per_step"] > 0 and d["dtype"] in ("f32", "bf16")
+    assert "synthetic" in d["data"] and "workload" in d["config"]
+    P = d["config"]["params"]
+    # value = K x P x bytes per worker element over the step time
+    bw = 4 if d["config"]["worker_dtype"] == "f32" else 2
+    assert d["value"] == pytest.approx(d["config"]["population"] * P * bw / (d["ms_per_step"] / 1e3) / 1e9, rel=2e-3)
+    r = d["roofline"]
+    assert {"bound", "achieved", "peak", "unit", "frac", "traffic"} <= set(r)
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert r["frac"] == pytest.approx(r["achieved"] / r["peak"], abs=1e-3) and 0 < r["frac"] < 1
+    c = d["cpu_baseline"]
+    assert {"value", "unit", "cores", "kind", "sample"} <= set(c) and c["kind"] in ("port", "reference")
+    assert c["value"] > 0 and c["cores"] >= 1 and c["sample"]
+
+
+def test_single_gpu_line():
+    d = _run("--place-candidates", "2", "--ops", "none", "--bcast-compare", "0")
+    _check_common(d, 1)
+    assert d["config"]["parallelism"] == "single GPU"
+    assert d["roofline"]["kernel_ms"] <= d["ms_per_step"] * 1.05
+
+
+def test_multi_gpu_path_line_at_world_1():
+    d = _run("--gpus", "1", "--sharded", "--compare-schedules", "0", "--config-companions", "0")
+    _check_common(d, 1)
+    assert "RCCL" in d["config"]["parallelism"]
+    x = d["roofline"]["xgmi"]
+    assert x["bound"] == "xgmi" and "wire_bytes_per_rank" in x
+    assert "weak_scaling" in d and "extras_deadline" not in d
