@@ -701,6 +701,15 @@ int edt_slerp_blend(const void* v0, const void* v1, int in_dt, void* out, int ou
 int edt_slerp_merge(const void* v0, const void* v1, int in_dt, void* out, int out_dt, const uint64_t* chunk_desc,
                     int64_t nchunks, const int32_t* seg_first_chunk, int nseg, const double* t, double dot_threshold,
                     double eps, double* partial, float* coef, float* dot_out, void* stream) {
+    // every argument of the three passes checked before the first launch: a rejected call does nothing
+    g_err[0] = 0;
+    if ((in_dt | out_dt) & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
+    if (nchunks < 0 || nseg < 0) return fail(EDT_ERR_ARG, "negative count");
+    if (nchunks > 0 && (!v0 || !v1 || !out || !chunk_desc || !partial || !coef))
+        return fail(EDT_ERR_ARG, "null buffer");
+    if (nseg > 0 && (!seg_first_chunk || !t || !partial || !coef)) return fail(EDT_ERR_ARG, "null buffer");
+    if (nchunks > 0 && (!aligned16(v0) || !aligned16(v1) || !aligned16(out)))
+        return fail(EDT_ERR_ARG, "slerp buffers must be 16-byte aligned");
     int rc = edt_slerp_stats(v0, v1, in_dt, chunk_desc, nchunks, partial, stream);
     if (rc) return rc;
     rc = edt_slerp_coef(partial, seg_first_chunk, nseg, t, dot_threshold, eps, coef, dot_out, stream);
@@ -1112,9 +1121,11 @@ int edt_slerp_merge_list(const void* const* v0_t, const void* const* v1_t, int i
                          int nseg, const double* t, double dot_threshold, double eps, double* partial, float* coef,
                          float* dot_out, void* workspace, uint64_t workspace_bytes, void* stream) {
     g_err[0] = 0;
+    if ((in_dt | out_dt) & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
     if (nseg < 0 || nchunks < 0) return fail(EDT_ERR_ARG, "negative count (segments %d, chunks %lld)", nseg, (long long)nchunks);
     if (nseg == 0 || nchunks == 0) return EDT_OK;
     if (!v0_t || !v1_t || !out_t) return fail(EDT_ERR_ARG, "null tensor table");
+    if (!chunk_desc || !seg_first_chunk || !t || !partial || !coef) return fail(EDT_ERR_ARG, "null buffer");
     const uint64_t need = 3ull * sizeof(uint64_t) * (uint64_t)nseg;
     if (!workspace || workspace_bytes < need)
         return fail(EDT_ERR_ARG, "workspace of %llu bytes needed", (unsigned long long)need);
