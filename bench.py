@@ -131,7 +131,11 @@ class ExtrasDeadline:
     start — a peer died or an exchange never completes — rank 0 prints the line it has (value,
     rooflines, cpu_baseline and every extra that finished, plus `extras_deadline`) and every rank
     exits, so a hang in an extra can never cost the measured value. `emit()` prints the line
-    exactly once, whichever thread gets there first."""
+    exactly once, whichever thread gets there first. The exit status is EXIT_STATUS (3), not 0: a
+    hung collective or a dead peer must read as a failed run to launch_ranks and any harness, with
+    the measured line still printed first."""
+
+    EXIT_STATUS = 3
 
     def __init__(self, seconds: float, rank: int, out: dict | None, json_out, exit_fn=None):
         import threading
@@ -163,8 +167,9 @@ class ExtrasDeadline:
                    if self.out is not None and k not in self.out]
         self.emit({"extras_deadline": {"seconds": self.seconds, "unfinished_or_skipped": pending,
                                        "note": "the extras after the value did not finish in time; the "
-                                               "value and what finished are reported, every rank exits"}})
-        self.exit_fn(0)
+                                               "value and what finished are reported, every rank exits "
+                                               "with status 3"}})
+        self.exit_fn(self.EXIT_STATUS)
 
     def cancel(self):
         if self.timer is not None:

@@ -67,13 +67,22 @@ using edt::g_err;
 #ifndef EDT_NT_SLERP            // non-temporal loads of the SLERP parents (stats and blend passes)
 #define EDT_NT_SLERP 1
 #endif
-#ifndef EDT_SLERP_BPC           // workgroups per CU for the chunk-looping SLERP passes
+#ifndef EDT_SLERP_BPC           // workgroups per CU for the grid-stride SLERP passes (redo / member-major blends)
 #define EDT_SLERP_BPC 256
 #endif
 #ifndef EDT_SLERP_GRID          // 1: the SLERP blends run one 2,048-element tile per workgroup in address
-                                // order (32 workgroups per 64 Ki chunk) and the chunk-sum passes one
-                                // workgroup per chunk; 0: grid-stride over chunks, EDT_SLERP_BPC per CU
+                                // order (32 workgroups per 64 Ki chunk); 0: grid-stride over chunks,
+                                // EDT_SLERP_BPC per CU
 #define EDT_SLERP_GRID 1
+#endif
+#ifndef EDT_SLERP_WAVE_ITERS    // 8-element vectors per lane in one wave tile of the chunk sums
+#define EDT_SLERP_WAVE_ITERS 4
+#endif
+#ifndef EDT_SLERP_SLOTS         // wave slots per chunk for the chunk sums (edt_slerp.hip: the canonical
+#define EDT_SLERP_SLOTS (128 / EDT_SLERP_WAVE_ITERS)   // order; slots x wave tiles = the plans' 64 Ki chunks)
+#endif
+#ifndef EDT_SLERP_SUMS_BPC      // chunk-sum passes: 0 = one workgroup per (chunk, slot group) in address
+#define EDT_SLERP_SUMS_BPC 0    // order; k > 0 = k workgroups per CU striding over those units
 #endif
 #ifndef EDT_SLERP_COEF_BLOCK    // 1: one workgroup per segment for the chunk-sum reduction (else one wave)
 #define EDT_SLERP_COEF_BLOCK 1
@@ -107,8 +116,11 @@ constexpr bool split_halves() {
 
 constexpr int kBlock = 256;                         // 4 waves
 constexpr int kVec = 8;                             // elements per thread per iteration
-// grid cap for the grid-stride loops: 256 CUs x workgroups per CU (0 = one pass, no cap)
-constexpr uint64_t kMaxBlocks = EDT_BLOCKS_PER_CU > 0 ? 256ull * EDT_BLOCKS_PER_CU : (1ull << 31) - 1;
+// HIP's dispatch limit: at most 2^32 - 1 work-items per grid dimension, i.e. 16,777,215 workgroups
+// of kBlock threads. Every grid below is capped there and the kernels grid-stride past it.
+constexpr uint64_t kGridBlockCap = 0xffffffffull / kBlock;
+// grid cap for the grid-stride loops: 256 CUs x workgroups per CU (0 = one pass up to the dispatch cap)
+constexpr uint64_t kMaxBlocks = EDT_BLOCKS_PER_CU > 0 ? 256ull * EDT_BLOCKS_PER_CU : kGridBlockCap;
 
 // XCD-aware block order for the one-pass stream kernels (outer_kernel, pair_kernel). Workgroups
 // are dispatched round-robin over the 8 XCDs (block b on XCD b % 8), so by default the XCDs
@@ -130,21 +142,14 @@ __device__ __forceinline__ uint64_t xcd_block(uint64_t b, uint64_t G) {
     }
 }
 
-constexpr uint64_t kSlerpMaxBlocks = EDT_SLERP_GRID ? (1ull << 31) - 1 : 256ull * EDT_SLERP_BPC;
-// chunk-sum passes: one workgroup per chunk (EDT_SLERP_GRID), else a grid-stride cap
+constexpr uint64_t kSlerpMaxBlocks = EDT_SLERP_GRID ? kGridBlockCap : 256ull * EDT_SLERP_BPC;
 inline unsigned slerp_grid(int64_t nchunks) {
     return (unsigned)((uint64_t)nchunks < kSlerpMaxBlocks ? (uint64_t)nchunks : kSlerpMaxBlocks);
 }
-// the speculative passes (chunk sums + the lerp output in one pass) stay grid-stride: one workgroup
-// per chunk measured 9.12 ms against 8.01 ms for the 7B lineage merge (profiles/r02_slerp_grid.json)
+// the passes that skip most chunks (the speculative redo blends) or hold several parents' tiles in
+// registers (the member-major blends) stay grid-stride over chunks, EDT_SLERP_SPEC_BPC per CU
 #ifndef EDT_SLERP_SPEC_BPC
 #define EDT_SLERP_SPEC_BPC 256
-#endif
-#ifndef EDT_SLERP_SPEC_CONTIG       // speculative pass: k > 0 = k consecutive chunks per workgroup
-#define EDT_SLERP_SPEC_CONTIG 0     // (address order); 0 = grid-stride over EDT_SLERP_SPEC_BPC per CU
-#endif
-#ifndef EDT_SLERP_GRAM_GRID
-#define EDT_SLERP_GRAM_GRID 0
 #endif
 inline unsigned slerp_spec_grid(int64_t nchunks) {
     const uint64_t cap = 256ull * EDT_SLERP_SPEC_BPC;
@@ -162,8 +167,8 @@ constexpr int kTilesPerChunk = EDT_SLERP_TPC;        // the plans' default chunk
 #endif
 inline unsigned slerp_tile_grid(int64_t nchunks) {
     if (!EDT_SLERP_GRID) return slerp_grid(nchunks);
-    const uint64_t g = (uint64_t)nchunks * kTilesPerChunk;
-    return (unsigned)(g < (1ull << 31) - 1 ? g : (1ull << 31) - 1);
+    const uint64_t g = (uint64_t)nchunks * kTilesPerChunk;    // past the cap, for_blend_ranges grid-strides
+    return (unsigned)(g < kGridBlockCap ? g : kGridBlockCap);
 }
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));

@@ -396,7 +396,7 @@ int edt_pair_merge_population(const void* const* b1, const void* const* b2, cons
             M.np = D;
             const uint64_t nv = n / kVec;
             const uint64_t bl = (nv + kBlock - 1) / kBlock + 1;
-            if (bl > 0x7fffffffull) return fail(EDT_ERR_ARG, "too many elements for one launch");
+            if (bl > kGridBlockCap) return fail(EDT_ERR_ARG, "too many elements for one launch");
             hipStream_t s = (hipStream_t)stream;
             const unsigned gm = (unsigned)bl;
             if (M.nmom > D) D = M.nmom;         // tile arrays sized for parents and donors alike
@@ -416,7 +416,7 @@ int edt_pair_merge_population(const void* const* b1, const void* const* b2, cons
     const uint64_t groups = (P.nchunks + 7) / 8;
     const uint64_t blocks = EDT_POP_LOOP ? (vec ? (n / kVec + kBlock - 1) / kBlock + 1 : (n + kBlock - 1) / kBlock)
                                          : groups * 8ull * (uint64_t)nchildren;
-    if (blocks > 0x7fffffffull) return fail(EDT_ERR_ARG, "too many elements for one launch");
+    if (blocks > kGridBlockCap) return fail(EDT_ERR_ARG, "too many elements for one launch");
     const unsigned g = (unsigned)blocks;
     hipStream_t s = (hipStream_t)stream;
 #define EDT_POP(G, W)                                                                   \

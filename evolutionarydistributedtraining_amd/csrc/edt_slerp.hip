@@ -14,24 +14,97 @@ __device__ __forceinline__ double wave_sum(double x) {
     return x;
 }
 
-// Block-wide sums {v0.v0, v1.v1, v0.v1} over one chunk [start, start+len), fp64 per thread,
-// fixed reduction order (wave shuffles, then waves in order). Valid in thread 0. EMIT = true also
-// writes the lerp-branch output l0 v0 + l1 v1 of the chunk (two rounded fp32 products, one
-// rounded sum: lerp_elems' math) in the same pass — the speculative forms; every caller forms
-// the sums with this one loop, so their sums are bit-identical.
-template <int IDT, bool NT, bool EMIT = false, int ODT = EDT_F32>
-__device__ __forceinline__ void chunk_pass(const void* v0, const void* v1, void* out, uint64_t start, uint64_t len,
-                                           float l0, float l1, double (*red)[kBlock / 64], double (&sums)[3]) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+// ---- the chunk sums' canonical order (every form: pair, speculative, Gram, sharded) --------------
+// A chunk's sums are formed by kSlots independent WAVE SLOTS, with no workgroup barrier anywhere:
+// slot j takes the wave tiles j, j + kSlots, ... of the chunk's 16-B-aligned body (kWaveTile
+// elements each: kWaveIters lane-contiguous 8-element vectors per lane, 1 KiB per wave access for
+// bf16), slot 0 also the < 16 head / tail elements (one per lane); per lane the products are
+// accumulated in element order by fp64 FMAs, the wave butterfly leaves the slot's totals in every
+// lane, and the slot rows go to a scratch table. slot_reduce_kernel then sums each chunk's kSlots
+// rows in slot order into the chunk row. The sum kernels run one workgroup per (chunk, group of
+// kBlock / 64 slots) in address order — the one-pass grid of the stream kernels, the chip's
+// in-flight window one contiguous stretch of every operand — where the previous form (one
+// workgroup per chunk, grid-stride, an LDS block reduction behind two barriers per chunk) kept
+// 65,536 far-apart chunks in flight and ran the 7B speculative pass at 7.1-8.3 ms depending on
+// the allocation against lerp's steady 7.0 ms on the same bytes (profiles/r03_*).
+constexpr int kSlots = EDT_SLERP_SLOTS;                       // slot rows per chunk
+constexpr int kWaveIters = EDT_SLERP_WAVE_ITERS;              // 8-element vectors per lane per tile
+constexpr int kWaveTile = 64 * kVec * kWaveIters;             // 2,048 elements
+constexpr int kWavesPerBlock = kBlock / 64;
+constexpr int kSlotGroups = kSlots / kWavesPerBlock;          // workgroups per chunk
+static_assert(kSlots % kWavesPerBlock == 0, "slots come in whole workgroups");
+
+inline unsigned slot_grid(int64_t nchunks) {                  // one workgroup per (chunk, slot group)
+    const uint64_t g = (uint64_t)nchunks * kSlotGroups;
+    const uint64_t cap = EDT_SLERP_SUMS_BPC > 0 ? 256ull * EDT_SLERP_SUMS_BPC : kGridBlockCap;
+    return (unsigned)(g < cap ? g : cap);
+}
+
+// The traversal of one wave slot over chunk [start, start + len): tile(i, b) for each of the
+// lane's wave tiles (first vector i; vectors i + k * 64 * kVec for k < kWaveIters while < b), then
+// elem(i) for the head / tail element slot 0's lane takes. Callers accumulate in exactly this order.
+template <typename Tile, typename Elem>
+__device__ __forceinline__ void for_slot(uint64_t start, uint64_t len, int slot, Tile&& tile, Elem&& elem) {
+    const uint64_t lane = threadIdx.x & 63;
     const uint64_t end = start + len;
-    double s00 = 0.0, s11 = 0.0, s01 = 0.0;
     const uint64_t a = (start + kVec - 1) / kVec * kVec;      // aligned body [a, b)
     const uint64_t b = end / kVec * kVec;
-    auto elems = [&](auto tagN, uint64_t i) {
+    if (a < b) {
+        for (uint64_t i = a + (uint64_t)slot * kWaveTile + lane * kVec; i < b; i += (uint64_t)kSlots * kWaveTile)
+            tile(i, b);
+    }
+    if (slot == 0) {
+        const uint64_t h_end = a < end ? a : end;
+        const uint64_t t_beg = b > a ? b : h_end;
+        const uint64_t nh = h_end - start, nt = end - t_beg;
+        if (lane < nh + nt) elem(lane < nh ? start + lane : t_beg + (lane - nh));
+    }
+}
+
+// A wave's W totals (identical in every lane after the butterfly) as one contiguous store of W
+// doubles by lanes 0 .. W-1.
+template <int W>
+__device__ __forceinline__ void store_slot_row(double* row, const double (&v)[W]) {
+    const int lane = threadIdx.x & 63;
+    double x = 0.0;
+#pragma unroll
+    for (int q = 0; q < W; ++q)
+        if (lane == q) x = v[q];
+    if (lane < W) row[lane] = x;
+}
+
+// Chunk rows from the slot rows: rows[c][q] = sum over s in slot order of slots[c][s][q].
+__global__ __launch_bounds__(kBlock) void slot_reduce_kernel(const double* __restrict__ slots, int W,
+                                                             int64_t nchunks, double* __restrict__ rows) {
+    const uint64_t n = (uint64_t)nchunks * (uint64_t)W;
+    for (uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x; k < n; k += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t c = k / (uint64_t)W, q = k % (uint64_t)W;
+        const double* p = slots + c * kSlots * (uint64_t)W + q;
+        double acc = 0.0;
+#pragma unroll 8
+        for (int s = 0; s < kSlots; ++s) acc += p[(uint64_t)s * W];
+        rows[k] = acc;
+    }
+}
+
+inline int launch_slot_reduce(const double* slots, int W, int64_t nchunks, double* rows, hipStream_t s) {
+    const uint64_t n = (uint64_t)nchunks * (uint64_t)W;
+    uint64_t g = (n + kBlock - 1) / kBlock;
+    if (g < 1) g = 1;
+    if (g > 4096) g = 4096;
+    slot_reduce_kernel<<<(unsigned)g, kBlock, 0, s>>>(slots, W, nchunks, rows);
+    return check_launch("slot_reduce_kernel");
+}
+
+// One wave slot of a pair's sums {v0.v0, v1.v1, v0.v1} (fp64, canonical order). EMIT = true also
+// writes the lerp-branch output l0 v0 + l1 v1 of the slot's elements (two rounded fp32 products,
+// one rounded sum: lerp_elems' math) in the same pass — the speculative forms.
+template <int IDT, bool NT, bool EMIT, int ODT>
+__device__ __forceinline__ void pair_slot(const void* v0, const void* v1, void* out, uint64_t start, uint64_t len,
+                                          int slot, float l0, float l1, double (&sums)[3]) {
+    double s00 = 0.0, s11 = 0.0, s01 = 0.0;
+    auto acc = [&](auto tagN, const float* x, const float* y) {
         constexpr int N = decltype(tagN)::value;
-        float x[N], y[N];
-        ld<IDT, N, NT && N == kVec>(v0, i, x);
-        ld<IDT, N, NT && N == kVec>(v1, i, y);
 #pragma unroll
         for (int j = 0; j < N; ++j) {
             const double dx = x[j], dy = y[j];
@@ -39,54 +112,50 @@ __device__ __forceinline__ void chunk_pass(const void* v0, const void* v1, void*
             s11 = __builtin_fma(dy, dy, s11);
             s01 = __builtin_fma(dx, dy, s01);
         }
-        if constexpr (EMIT) {
-            float o[N];
-#pragma unroll
-            for (int j = 0; j < N; ++j) o[j] = l0 * x[j] + l1 * y[j];
-            st<ODT, N>(out, i, o);
-        }
     };
-    if (a < b) {
-        for (uint64_t i = a + (uint64_t)threadIdx.x * kVec; i < b; i += (uint64_t)kBlock * kVec)
-            elems(std::integral_constant<int, kVec>{}, i);
-    }
-    // head [start, min(a, end)) and tail [max(b, a), end): fewer than 16 elements
-    const uint64_t h_end = a < end ? a : end;
-    const uint64_t t_beg = b > a ? b : h_end;
-    const uint64_t nh = h_end - start, nt = end - t_beg;
-    if ((uint64_t)threadIdx.x < nh + nt)
-        elems(std::integral_constant<int, 1>{}, threadIdx.x < nh ? start + threadIdx.x : t_beg + (threadIdx.x - nh));
-    s00 = wave_sum(s00);
-    s11 = wave_sum(s11);
-    s01 = wave_sum(s01);
-    if (lane == 0) { red[0][wave] = s00; red[1][wave] = s11; red[2][wave] = s01; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
+    for_slot(start, len, slot,
+        [&](uint64_t i0, uint64_t b) {
+            float x[kWaveIters][kVec], y[kWaveIters][kVec];
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            double acc = 0.0;
+            for (int k = 0; k < kWaveIters; ++k) {           // every load of the tile issued first
+                const uint64_t i = i0 + (uint64_t)k * 64 * kVec;
+                if (i < b) {
+                    ld<IDT, kVec, NT>(v0, i, x[k]);
+                    ld<IDT, kVec, NT>(v1, i, y[k]);
+                }
+            }
 #pragma unroll
-            for (int w = 0; w < kBlock / 64; ++w) acc += red[q][w];
-            sums[q] = acc;
-        }
-    }
-    __syncthreads();
+            for (int k = 0; k < kWaveIters; ++k) {
+                const uint64_t i = i0 + (uint64_t)k * 64 * kVec;
+                if (i < b) {
+                    acc(std::integral_constant<int, kVec>{}, x[k], y[k]);
+                    if constexpr (EMIT) {
+                        float o[kVec];
+#pragma unroll
+                        for (int j = 0; j < kVec; ++j) o[j] = l0 * x[k][j] + l1 * y[k][j];
+                        st<ODT, kVec>(out, i, o);
+                    }
+                }
+            }
+        },
+        [&](uint64_t i) {
+            float x[1], y[1];
+            ld<IDT, 1>(v0, i, x);
+            ld<IDT, 1>(v1, i, y);
+            acc(std::integral_constant<int, 1>{}, x, y);
+            if constexpr (EMIT) {
+                float o[1] = {l0 * x[0] + l1 * y[0]};
+                st<ODT, 1>(out, i, o);
+            }
+        });
+    sums[0] = wave_sum(s00);
+    sums[1] = wave_sum(s11);
+    sums[2] = wave_sum(s01);
 }
 
-template <int IDT>
-__device__ __forceinline__ void chunk_sums(const void* v0, const void* v1, uint64_t start, uint64_t len,
-                                           double (*red)[kBlock / 64], double (&out)[3]) {
-    chunk_pass<IDT, EDT_NT_SLERP != 0 && IDT == EDT_BF16>(v0, v1, nullptr, start, len, 0.f, 0.f, red, out);
-}
-
-// The reference's scalar SLERP math (EDT_RL/crossover.py:24-45) from the three sums, in fp32 as
+// The reference's branch and coefficients (EDT_RL/crossover.py:31-45) for an fp32 dot, in fp32 as
 // numpy does it for float32 scalars (NEP 50: python floats enter as fp32).
-__device__ __forceinline__ void slerp_coefficients(double s00, double s11, double s01, double t, float thr,
-                                                   float eps, float& c0, float& c1, float& dot) {
-    const float n0 = (float)sqrt(s00), n1 = (float)sqrt(s11);      // np.linalg.norm (fp32)
-    const double d0 = n0 > eps ? (double)n0 : 1.0;                  // normalize() divides only if > eps
-    const double d1 = n1 > eps ? (double)n1 : 1.0;
-    dot = (float)(s01 / (d0 * d1));
+__device__ __forceinline__ void coefficients_from_dot(float dot, double t, float thr, float& c0, float& c1) {
     if (fabsf(dot) > thr) {                                         // lerp on the originals
         c0 = (float)(1.0 - t);
         c1 = (float)t;
@@ -99,6 +168,16 @@ __device__ __forceinline__ void slerp_coefficients(double s00, double s11, doubl
     }
 }
 
+// The reference's scalar SLERP math (EDT_RL/crossover.py:24-45) from the three sums.
+__device__ __forceinline__ void slerp_coefficients(double s00, double s11, double s01, double t, float thr,
+                                                   float eps, float& c0, float& c1, float& dot) {
+    const float n0 = (float)sqrt(s00), n1 = (float)sqrt(s11);      // np.linalg.norm (fp32)
+    const double d0 = n0 > eps ? (double)n0 : 1.0;                  // normalize() divides only if > eps
+    const double d1 = n1 > eps ? (double)n1 : 1.0;
+    dot = (float)(s01 / (d0 * d1));
+    coefficients_from_dot(dot, t, thr, c0, c1);
+}
+
 // The element ranges a blend workgroup owns, as body(start, end, segment). TILES: one kTile of its
 // chunk (tiles kTilesPerChunk apart for longer chunks; grid slerp_tile_grid) — the full blends.
 // Else whole chunks, grid-stride (grid slerp_spec_grid) — the speculative redo blends, where most
@@ -108,13 +187,16 @@ __device__ __forceinline__ void slerp_coefficients(double s00, double s11, doubl
 template <bool TILES, typename F>
 __device__ __forceinline__ void for_blend_ranges(const uint64_t* chunks, int64_t nchunks, F&& body) {
     if constexpr (TILES && EDT_SLERP_GRID) {
-        const uint64_t b = EDT_SLERP_BLEND_REV ? gridDim.x - 1 - blockIdx.x : blockIdx.x;
-        const int64_t c = (int64_t)(b / kTilesPerChunk);
-        if (c >= nchunks) return;
-        const uint64_t start = chunks[3 * c], len = chunks[3 * c + 1], seg = chunks[3 * c + 2];
-        for (uint64_t off = (b % kTilesPerChunk) * kTile; off < len;
-             off += (uint64_t)kTilesPerChunk * kTile)
-            body(start + off, start + (off + kTile < len ? off + kTile : len), seg);
+        // one tile per workgroup; a grid capped at kGridBlockCap strides over the rest
+        const uint64_t total = (uint64_t)nchunks * kTilesPerChunk;
+        for (uint64_t b0 = blockIdx.x; b0 < total; b0 += gridDim.x) {
+            const uint64_t b = EDT_SLERP_BLEND_REV ? total - 1 - b0 : b0;
+            const int64_t c = (int64_t)(b / kTilesPerChunk);
+            const uint64_t start = chunks[3 * c], len = chunks[3 * c + 1], seg = chunks[3 * c + 2];
+            for (uint64_t off = (b % kTilesPerChunk) * kTile; off < len;
+                 off += (uint64_t)kTilesPerChunk * kTile)
+                body(start + off, start + (off + kTile < len ? off + kTile : len), seg);
+        }
     } else {
         for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x)
             body(chunks[3 * c], chunks[3 * c] + chunks[3 * c + 1], chunks[3 * c + 2]);
@@ -138,58 +220,61 @@ __device__ __forceinline__ void for_range_elems(uint64_t start, uint64_t end, F&
         f(std::integral_constant<int, 1>{}, threadIdx.x < nh ? start + threadIdx.x : t_beg + (threadIdx.x - nh));
 }
 
-// seg_ptrs (tensor-list form, may be null): per segment {v0, v1, out} device pointers; chunk
-// starts are then relative to their segment. Null: v0 / v1 / out are flat arenas.
-template <int IDT>
-__global__ __launch_bounds__(kBlock) void slerp_stats_kernel(const void* v0, const void* v1,
-                                                             const uint64_t* chunks, int64_t nchunks,
-                                                             double* partial, const uint64_t* seg_ptrs) {
-    __shared__ double red[3][kBlock / 64];
-    for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
-        double sums[3];
+// The pair sums' slot rows (slots[c][slot][3]), one workgroup per (chunk, slot group), address
+// order. seg_ptrs (tensor-list form, may be null): per segment {v0, v1, out} device pointers;
+// chunk starts are then relative to their segment. Null: v0 / v1 / out are flat arenas.
+// EMIT (the speculative first pass, edt_slerp_merge_speculative): the same sums, and in the same
+// pass the lerp-branch output (1-t) v0 + t v1 with the coefficients slerp_coefficients gives that
+// branch. Parents of one lineage (fine-tunes of a common base) mostly have |dot| > 0.9995, where
+// this output is final; the other segments are blended again.
+template <int IDT, bool EMIT, int ODT>
+__global__ __launch_bounds__(kBlock) void pair_sums_kernel(const void* v0, const void* v1, void* out,
+                                                           const uint64_t* chunks, int64_t nchunks, double* slots,
+                                                           const double* tvals, const uint64_t* seg_ptrs) {
+    constexpr bool NT = EDT_NT_SLERP != 0 && IDT == EDT_BF16;
+    const int wave = threadIdx.x >> 6;
+    const uint64_t units = (uint64_t)nchunks * kSlotGroups;
+    for (uint64_t u = blockIdx.x; u < units; u += gridDim.x) {
+        const uint64_t c = u / kSlotGroups;
+        const int slot = (int)(u % kSlotGroups) * kWavesPerBlock + wave;
+        const uint64_t seg = chunks[3 * c + 2];
         const void* a = v0;
         const void* b = v1;
+        void* o = out;
         if (seg_ptrs) {
-            const uint64_t seg = chunks[3 * c + 2];
             a = reinterpret_cast<const void*>(seg_ptrs[3 * seg]);
             b = reinterpret_cast<const void*>(seg_ptrs[3 * seg + 1]);
+            o = reinterpret_cast<void*>(seg_ptrs[3 * seg + 2]);
         }
-        chunk_sums<IDT>(a, b, chunks[3 * c], chunks[3 * c + 1], red, sums);
-        if (threadIdx.x == 0) {
-            partial[3 * c] = sums[0];
-            partial[3 * c + 1] = sums[1];
-            partial[3 * c + 2] = sums[2];
+        float l0 = 0.f, l1 = 0.f;
+        if constexpr (EMIT) {
+            l0 = (float)(1.0 - tvals[seg]);
+            l1 = (float)tvals[seg];
         }
+        double sums[3];
+        pair_slot<IDT, NT, EMIT, ODT>(a, b, o, chunks[3 * c], chunks[3 * c + 1], slot, l0, l1, sums);
+        store_slot_row<3>(slots + (c * kSlots + (uint64_t)slot) * 3, sums);
     }
 }
 
-// Speculative first pass (edt_slerp_merge_speculative): the chunk sums exactly as
-// slerp_stats_kernel forms them (same element order per thread, same FMAs, same reductions), and
-// in the same pass the lerp-branch output (1-t) v0 + t v1 (lerp_elems with the coefficients
-// slerp_coefficients gives that branch). Parents of one lineage (fine-tunes of a common base)
-// mostly have |dot| > 0.9995, where this output is final; the other segments are blended again.
-template <int IDT, int ODT>
-__global__ __launch_bounds__(kBlock) void slerp_stats_lerp_kernel(const void* v0, const void* v1, void* out,
-                                                                  const uint64_t* chunks, int64_t nchunks,
-                                                                  double* partial, const double* tvals) {
-    __shared__ double red[3][kBlock / 64];
-    // EDT_SLERP_SPEC_CONTIG = k > 0: workgroup b takes chunks [b k, b k + k) (address order);
-    // 0: grid-stride. Either way each chunk's sums come from one workgroup in the same order.
-    const int64_t c_first = EDT_SLERP_SPEC_CONTIG > 0 ? (int64_t)blockIdx.x * EDT_SLERP_SPEC_CONTIG : (int64_t)blockIdx.x;
-    const int64_t c_step = EDT_SLERP_SPEC_CONTIG > 0 ? 1 : (int64_t)gridDim.x;
-    const int64_t c_end = EDT_SLERP_SPEC_CONTIG > 0 ? (c_first + EDT_SLERP_SPEC_CONTIG < nchunks
-                                                        ? c_first + EDT_SLERP_SPEC_CONTIG : nchunks) : nchunks;
-    for (int64_t c = c_first; c < c_end; c += c_step) {
-        const uint64_t seg = chunks[3 * c + 2];
-        double sums[3];
-        chunk_pass<IDT, EDT_NT_SLERP != 0 && IDT == EDT_BF16, true, ODT>(
-            v0, v1, out, chunks[3 * c], chunks[3 * c + 1], (float)(1.0 - tvals[seg]), (float)tvals[seg], red, sums);
-        if (threadIdx.x == 0) {
-            partial[3 * c] = sums[0];
-            partial[3 * c + 1] = sums[1];
-            partial[3 * c + 2] = sums[2];
-        }
-    }
+// host: the pair sums into partial (rows [nchunks][3], then the slot scratch), EMIT optional
+int pair_sums(const void* v0, const void* v1, int in_dt, void* out, int out_dt, bool emit,
+              const uint64_t* chunk_desc, int64_t nchunks, double* partial, const double* t,
+              const uint64_t* seg_ptrs, hipStream_t s) {
+    double* slots = partial + 3 * (uint64_t)nchunks;
+    const unsigned g = slot_grid(nchunks);
+#define EDT_PS(I, E, O) pair_sums_kernel<I, E, O><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, slots, t, seg_ptrs)
+    if (!emit) {
+        if (in_dt == EDT_F32) EDT_PS(EDT_F32, false, EDT_F32);
+        else EDT_PS(EDT_BF16, false, EDT_F32);
+    } else if (in_dt == EDT_F32 && out_dt == EDT_F32) EDT_PS(EDT_F32, true, EDT_F32);
+    else if (in_dt == EDT_F32) EDT_PS(EDT_F32, true, EDT_BF16);
+    else if (out_dt == EDT_F32) EDT_PS(EDT_BF16, true, EDT_F32);
+    else EDT_PS(EDT_BF16, true, EDT_BF16);
+#undef EDT_PS
+    int rc = check_launch(emit ? "pair_sums_kernel (speculative)" : "pair_sums_kernel");
+    if (rc) return rc;
+    return launch_slot_reduce(slots, 3, nchunks, partial, s);
 }
 
 // Fixed-order reduction of a segment's chunk sums: column q of rows [c0, c1) of a row-major table
@@ -281,9 +366,9 @@ __global__ __launch_bounds__(kBlock) void slerp_blend_kernel(const void* v0, con
 // generation): ONE pass over the M <= 8 members per chunk forms every member's squared norm and
 // every pair's dot — the upper triangle of the Gram matrix, M(M+1)/2 fp64 sums per chunk — where
 // per-child stats passes would read each child's two parents. A child's (|vi|^2, |vj|^2, vi.vj)
-// are then read out of it. Every sum is bit-identical to chunk_sums() on (vi, vj): the same
-// per-thread FMA sequence in element order (an FMA's product is exact, so vi*vj == vj*vi), the
-// same wave and block reductions; the coefficients therefore equal edt_slerp_merge's.
+// are then read out of it. Every sum is bit-identical to pair_slot() on (vi, vj): the same wave
+// slots, the same per-lane FMA sequence in element order (an FMA's product is exact, so vi*vj ==
+// vj*vi), the same butterfly and slot reduction; the coefficients therefore equal edt_slerp_merge's.
 
 constexpr int kGramMaxMembers = 8;
 struct Members {
@@ -294,11 +379,8 @@ __host__ __device__ constexpr int tri_index(int a, int b, int M) {   // a <= b <
     return a * M - a * (a - 1) / 2 + (b - a);
 }
 
-template <int IDT, int M, int N>
-__device__ __forceinline__ void gram_accumulate(const Members& mem, uint64_t i, double (&g)[M * (M + 1) / 2]) {
-    float x[M][N];
-#pragma unroll
-    for (int m = 0; m < M; ++m) ld<IDT, N>(mem.p[m], i, x[m]);   // default policy: measured faster here
+template <int M, int N>
+__device__ __forceinline__ void gram_fma(const float (&x)[M][N], double (&g)[M * (M + 1) / 2]) {
 #pragma unroll
     for (int j = 0; j < N; ++j) {
 #pragma unroll
@@ -313,44 +395,116 @@ __device__ __forceinline__ void gram_accumulate(const Members& mem, uint64_t i, 
     }
 }
 
-template <int IDT, int M>
-__global__ __launch_bounds__(kBlock) void slerp_gram_kernel(Members mem, const uint64_t* chunks, int64_t nchunks,
-                                                            double* gram) {
+// The lerp-branch outputs of the children from the parents' registers (PopLerp below).
+struct PopLerp {
+    void* out[16];
+    int32_t a[16], b[16];      // compact member indices of the parents
+    int n;
+};
+
+template <int M, int N>
+__device__ __forceinline__ void pick(const float (&x)[M][N], int idx, float (&y)[N]) {
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+        if (m == idx) {                 // idx is uniform across the workgroup: no divergence
+#pragma unroll
+            for (int j = 0; j < N; ++j) y[j] = x[m][j];
+        }
+}
+
+template <int ODT, int M, int N>
+__device__ __forceinline__ void emit_children(const PopLerp& po, const float (&x)[M][N], uint64_t i, float l0, float l1) {
+    for (int q = 0; q < po.n; ++q) {
+        float u[N], v[N], o[N];
+        pick<M, N>(x, po.a[q], u);
+        pick<M, N>(x, po.b[q], v);
+#pragma unroll
+        for (int j = 0; j < N; ++j) o[j] = l0 * u[j] + l1 * v[j];
+        st<ODT, N>(po.out[q], i, o);
+    }
+}
+
+// Gram slot rows (slots[c][slot][M(M+1)/2]), one workgroup per (chunk, slot group), address order.
+// EMIT (the member-major speculative pass, edt_slerp_population_speculative): each distinct parent's
+// vector is loaded ONCE into registers, its Gram sums accumulated and every child's lerp-branch
+// output written from the same registers — a shared parent crosses HBM once for all its children.
+template <int IDT, int M, bool EMIT, int ODT>
+__global__ __launch_bounds__(kBlock) void slerp_gram_kernel(Members mem, PopLerp po, const uint64_t* chunks,
+                                                            int64_t nchunks, const double* tvals, double* slots) {
     constexpr int NT = M * (M + 1) / 2;
-    __shared__ double red[NT][kBlock / 64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
-        const uint64_t start = chunks[3 * c], end = start + chunks[3 * c + 1];
+    const int wave = threadIdx.x >> 6;
+    const uint64_t units = (uint64_t)nchunks * kSlotGroups;
+    for (uint64_t u = blockIdx.x; u < units; u += gridDim.x) {
+        const uint64_t c = u / kSlotGroups;
+        const int slot = (int)(u % kSlotGroups) * kWavesPerBlock + wave;
+        float l0 = 0.f, l1 = 0.f;
+        if constexpr (EMIT) {
+            const uint64_t seg = chunks[3 * c + 2];
+            l0 = (float)(1.0 - tvals[seg]);
+            l1 = (float)tvals[seg];
+        }
         double g[NT];
 #pragma unroll
         for (int q = 0; q < NT; ++q) g[q] = 0.0;
-        const uint64_t a = (start + kVec - 1) / kVec * kVec;
-        const uint64_t b = end / kVec * kVec;
-        if (a < b) {
-            for (uint64_t i = a + (uint64_t)threadIdx.x * kVec; i < b; i += (uint64_t)kBlock * kVec)
-                gram_accumulate<IDT, M, kVec>(mem, i, g);
-        }
-        const uint64_t h_end = a < end ? a : end;
-        const uint64_t t_beg = b > a ? b : h_end;
-        const uint64_t nh = h_end - start, nt = end - t_beg;
-        if ((uint64_t)threadIdx.x < nh + nt) {
-            const uint64_t i = threadIdx.x < nh ? start + threadIdx.x : t_beg + (threadIdx.x - nh);
-            gram_accumulate<IDT, M, 1>(mem, i, g);
-        }
+        for_slot(chunks[3 * c], chunks[3 * c + 1], slot,
+            [&](uint64_t i0, uint64_t b) {
+                // M <= 4: the tile's vectors unrolled; more members: one vector at a time (the
+                // member tiles and M(M+1)/2 accumulators already fill the register file)
+#pragma unroll(M <= 4 ? kWaveIters : 1)
+                for (int k = 0; k < kWaveIters; ++k) {
+                    const uint64_t i = i0 + (uint64_t)k * 64 * kVec;
+                    if (i < b) {
+                        float x[M][kVec];
 #pragma unroll
-        for (int q = 0; q < NT; ++q) {
-            const double v = wave_sum(g[q]);
-            if (lane == 0) red[q][wave] = v;
-        }
-        __syncthreads();
-        if (threadIdx.x < NT) {
-            double acc = 0.0;
+                        for (int m = 0; m < M; ++m) ld<IDT, kVec>(mem.p[m], i, x[m]);   // default policy
+                        gram_fma<M, kVec>(x, g);
+                        if constexpr (EMIT) emit_children<ODT, M, kVec>(po, x, i, l0, l1);
+                    }
+                }
+            },
+            [&](uint64_t i) {
+                float x[M][1];
 #pragma unroll
-            for (int w = 0; w < kBlock / 64; ++w) acc += red[threadIdx.x][w];
-            gram[(uint64_t)c * NT + threadIdx.x] = acc;
-        }
-        __syncthreads();
+                for (int m = 0; m < M; ++m) ld<IDT, 1>(mem.p[m], i, x[m]);
+                gram_fma<M, 1>(x, g);
+                if constexpr (EMIT) emit_children<ODT, M, 1>(po, x, i, l0, l1);
+            });
+#pragma unroll
+        for (int q = 0; q < NT; ++q) g[q] = wave_sum(g[q]);
+        store_slot_row<NT>(slots + (c * kSlots + (uint64_t)slot) * NT, g);
     }
+}
+
+// host: the Gram sums of D compact members into gram (rows [nchunks][NT], then the slot scratch);
+// po != null: the member-major speculative pass (children's lerp-branch outputs written too)
+inline int gram_sums(const Members& mem, int D, const PopLerp* po, int in_dt, int out_dt, const uint64_t* chunk_desc,
+                     int64_t nchunks, const double* t, double* gram, hipStream_t s) {
+    const int NT = D * (D + 1) / 2;
+    double* slots = gram + (uint64_t)nchunks * NT;
+    const unsigned g = slot_grid(nchunks);
+    PopLerp none;
+    memset(&none, 0, sizeof(none));
+    const PopLerp& P = po ? *po : none;
+#define EDT_GS(I, M, E, O) slerp_gram_kernel<I, M, E, O><<<g, kBlock, 0, s>>>(mem, P, chunk_desc, nchunks, t, slots)
+#define EDT_GM(M)                                                                      \
+    case M:                                                                            \
+        if (!po) {                                                                     \
+            if (in_dt == EDT_F32) EDT_GS(EDT_F32, M, false, EDT_F32);                  \
+            else EDT_GS(EDT_BF16, M, false, EDT_F32);                                  \
+        } else if (in_dt == EDT_F32 && out_dt == EDT_F32) EDT_GS(EDT_F32, M, true, EDT_F32);   \
+        else if (in_dt == EDT_F32) EDT_GS(EDT_F32, M, true, EDT_BF16);                 \
+        else if (out_dt == EDT_F32) EDT_GS(EDT_BF16, M, true, EDT_F32);                \
+        else EDT_GS(EDT_BF16, M, true, EDT_BF16);                                      \
+        break;
+    switch (D) {
+        EDT_GM(1) EDT_GM(2) EDT_GM(3) EDT_GM(4) EDT_GM(5) EDT_GM(6) EDT_GM(7) EDT_GM(8)
+        default: return fail(EDT_ERR_ARG, "Gram pass over %d members", D);
+    }
+#undef EDT_GM
+#undef EDT_GS
+    int rc = check_launch(po ? "slerp_gram_kernel (speculative)" : "slerp_gram_kernel");
+    if (rc) return rc;
+    return launch_slot_reduce(slots, NT, nchunks, gram, s);
 }
 
 // The blends of every child in one launch, with pair_population_kernel's placement: the
@@ -364,7 +518,7 @@ struct BlendChildren {
     void* out[kBlendMaxChildren];
     const float* coef[kBlendMaxChildren];     // [nseg][2] of the child
     const int32_t* redo[kBlendMaxChildren];   // [nseg] of the child, or null: blend every segment
-    double* partial[kBlendMaxChildren];       // [nchunks][3] of the child (speculative stats pass)
+    double* slots[kBlendMaxChildren];         // [nchunks][kSlots][3] of the child (speculative stats pass)
     int nchildren;
 };
 
@@ -398,29 +552,27 @@ __global__ __launch_bounds__(kBlock) void slerp_blend_population_kernel(BlendChi
     }
 }
 
-// Speculative population pass: block (chunk, child) with the co-located placement above; each
-// forms its child's chunk sums exactly as chunk_sums() does and writes the lerp-branch output in
-// the same pass (as slerp_stats_lerp_kernel). Shared parents cross HBM once for all children.
+// Speculative population pass for more than 8 distinct parents: block (unit, child) with the
+// co-located placement above, a unit being one (chunk, slot group): the blocks of every child for
+// one unit carry the same blockIdx % 8 (one XCD, one L2). Each forms its child's slot rows exactly
+// as pair_slot() does and writes the lerp-branch output in the same pass (as the speculative pair
+// pass). Shared parents cross HBM once for all children.
 template <int IDT, int ODT>
 __global__ __launch_bounds__(kBlock) void slerp_pop_stats_lerp_kernel(BlendChildren B, const uint64_t* chunks,
                                                                       int64_t nchunks, const double* tvals) {
-    __shared__ double red[3][kBlock / 64];
     const uint64_t per_group = 8ull * (uint64_t)B.nchildren;
     const uint64_t r = blockIdx.x % per_group;
     const int child = (int)(r / 8);
-    const int64_t c = (int64_t)((blockIdx.x / per_group) * 8 + (r % 8));
-    if (c >= nchunks) return;
+    const uint64_t u = (blockIdx.x / per_group) * 8 + (r % 8);
+    if (u >= (uint64_t)nchunks * kSlotGroups) return;
+    const uint64_t c = u / kSlotGroups;
+    const int slot = (int)(u % kSlotGroups) * kWavesPerBlock + (int)(threadIdx.x >> 6);
     const uint64_t seg = chunks[3 * c + 2];
     double sums[3];
     // default-policy loads: a parent's chunk is re-read by its other children from L2
-    chunk_pass<IDT, false, true, ODT>(B.v0[child], B.v1[child], B.out[child], chunks[3 * c], chunks[3 * c + 1],
-                                      (float)(1.0 - tvals[seg]), (float)tvals[seg], red, sums);
-    if (threadIdx.x == 0) {
-        double* pc = B.partial[child] + 3 * c;
-        pc[0] = sums[0];
-        pc[1] = sums[1];
-        pc[2] = sums[2];
-    }
+    pair_slot<IDT, false, true, ODT>(B.v0[child], B.v1[child], B.out[child], chunks[3 * c], chunks[3 * c + 1], slot,
+                                     (float)(1.0 - tvals[seg]), (float)tvals[seg], sums);
+    store_slot_row<3>(B.slots[child] + (c * kSlots + (uint64_t)slot) * 3, sums);
 }
 
 // Per segment for the pair (i, j): slerp_coef_kernel's reduction over the chunks, reading the
@@ -439,96 +591,6 @@ __global__ __launch_bounds__(kBlock) void slerp_gram_coef_kernel(const double* g
     coef[2 * seg + 1] = c1;
     if (dot_out) dot_out[seg] = dot;
     if (redo) redo[seg] = fabsf(dot) > thr ? 0 : 1;   // as slerp_coef_kernel
-}
-
-// The speculative population pass in member-major form: per chunk, every distinct parent's tile
-// is loaded ONCE into registers; from it the thread accumulates the Gram sums (gram_accumulate's
-// exact FMA order, so every child's sums equal chunk_sums' on its two parents) and writes every
-// child's lerp-branch output (chunk_pass' EMIT math). A shared parent crosses HBM once for all
-// its children regardless of cache residency.
-struct PopLerp {
-    void* out[kBlendMaxChildren];
-    int32_t a[kBlendMaxChildren], b[kBlendMaxChildren];   // compact member indices of the parents
-    int n;
-};
-
-template <int M, int N>
-__device__ __forceinline__ void pick(const float (&x)[M][N], int idx, float (&y)[N]) {
-#pragma unroll
-    for (int m = 0; m < M; ++m)
-        if (m == idx) {                 // idx is uniform across the workgroup: no divergence
-#pragma unroll
-            for (int j = 0; j < N; ++j) y[j] = x[m][j];
-        }
-}
-
-template <int IDT, int ODT, int M, int N>
-__device__ __forceinline__ void gram_lerp_elems(const Members& mem, const PopLerp& po, uint64_t i, float l0, float l1,
-                                                double (&g)[M * (M + 1) / 2]) {
-    float x[M][N];
-#pragma unroll
-    for (int m = 0; m < M; ++m) ld<IDT, N>(mem.p[m], i, x[m]);
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-#pragma unroll
-        for (int a = 0; a < M; ++a) {
-            const double da = x[a][j];
-#pragma unroll
-            for (int b = a; b < M; ++b) {
-                const double db = x[b][j];
-                g[tri_index(a, b, M)] = __builtin_fma(da, db, g[tri_index(a, b, M)]);
-            }
-        }
-    }
-    for (int q = 0; q < po.n; ++q) {
-        float u[N], v[N], o[N];
-        pick<M, N>(x, po.a[q], u);
-        pick<M, N>(x, po.b[q], v);
-#pragma unroll
-        for (int j = 0; j < N; ++j) o[j] = l0 * u[j] + l1 * v[j];
-        st<ODT, N>(po.out[q], i, o);
-    }
-}
-
-template <int IDT, int ODT, int M>
-__global__ __launch_bounds__(kBlock) void slerp_gram_lerp_kernel(Members mem, PopLerp po, const uint64_t* chunks,
-                                                                 int64_t nchunks, const double* tvals, double* gram) {
-    constexpr int NT = M * (M + 1) / 2;
-    __shared__ double red[NT][kBlock / 64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
-        const uint64_t start = chunks[3 * c], end = start + chunks[3 * c + 1], seg = chunks[3 * c + 2];
-        const float l0 = (float)(1.0 - tvals[seg]), l1 = (float)tvals[seg];
-        double g[NT];
-#pragma unroll
-        for (int q = 0; q < NT; ++q) g[q] = 0.0;
-        const uint64_t a = (start + kVec - 1) / kVec * kVec;
-        const uint64_t b = end / kVec * kVec;
-        if (a < b) {
-            for (uint64_t i = a + (uint64_t)threadIdx.x * kVec; i < b; i += (uint64_t)kBlock * kVec)
-                gram_lerp_elems<IDT, ODT, M, kVec>(mem, po, i, l0, l1, g);
-        }
-        const uint64_t h_end = a < end ? a : end;
-        const uint64_t t_beg = b > a ? b : h_end;
-        const uint64_t nh = h_end - start, nt = end - t_beg;
-        if ((uint64_t)threadIdx.x < nh + nt) {
-            const uint64_t i = threadIdx.x < nh ? start + threadIdx.x : t_beg + (threadIdx.x - nh);
-            gram_lerp_elems<IDT, ODT, M, 1>(mem, po, i, l0, l1, g);
-        }
-#pragma unroll
-        for (int q = 0; q < NT; ++q) {
-            const double v = wave_sum(g[q]);
-            if (lane == 0) red[q][wave] = v;
-        }
-        __syncthreads();
-        if (threadIdx.x < NT) {
-            double acc = 0.0;
-#pragma unroll
-            for (int w = 0; w < kBlock / 64; ++w) acc += red[threadIdx.x][w];
-            gram[(uint64_t)c * NT + threadIdx.x] = acc;
-        }
-        __syncthreads();
-    }
 }
 
 // The blends of every child in member-major form (the two-pass Gram form's second pass and the
@@ -606,11 +668,8 @@ int slerp_stats_impl(const void* v0, const void* v1, int in_dt, const uint64_t* 
     if (in_dt & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
     if (nchunks == 0) return EDT_OK;
     if (!chunk_desc || !partial) return fail(EDT_ERR_ARG, "null buffer");
-    const unsigned g = slerp_grid(nchunks);
-    hipStream_t s = (hipStream_t)stream;
-    if (in_dt == EDT_F32) slerp_stats_kernel<EDT_F32><<<g, kBlock, 0, s>>>(v0, v1, chunk_desc, nchunks, partial, seg_ptrs);
-    else slerp_stats_kernel<EDT_BF16><<<g, kBlock, 0, s>>>(v0, v1, chunk_desc, nchunks, partial, seg_ptrs);
-    return check_launch("slerp_stats_kernel");
+    return pair_sums(v0, v1, in_dt, nullptr, EDT_F32, false, chunk_desc, nchunks, partial, nullptr, seg_ptrs,
+                     (hipStream_t)stream);
 }
 
 int slerp_blend_impl(const void* v0, const void* v1, int in_dt, void* out, int out_dt, const uint64_t* chunk_desc,
@@ -635,6 +694,312 @@ int slerp_blend_impl(const void* v0, const void* v1, int in_dt, void* out, int o
     return check_launch("slerp_blend_kernel");
 }
 
+
+// ---------------------------------------------------------------------------------------
+// Reference-dot mode (opt-in): the reference's own fp32 dot of EDT_RL/crossover.py:20-29 restated
+// bit for bit on the device (oracle/edt_oracle.c, pinned on numpy 2.2 / OpenBLAS 0.3.29 SkylakeX):
+//   norm  = sqrt(sdot(v, v)): `threads` OpenBLAS level-1 chunks (ceil(rest / threads left)), each
+//           64 fp32 FMA chains over 64-element blocks (chain L takes elements 64k + L), folded to
+//           32, the 32-element remainder block, ((a0 + a1) + a2) + a3, the halves and two hadds,
+//           then the < 32 tail in double; chunks added in order in double, rounded each time;
+//   dot   = np.sum((v0 / n0) * (v1 / n1)): 8192-element buffers, each summed pairwise (blocks of
+//           <= 128 with 8 accumulators, else halves cut at a multiple of 8), added in order to a
+//           float starting at 0.
+// The fp64 dot of the chunk sums stays the default; this mode replaces it where the caller's
+// flags say so (e.g. segments whose fp64 dot lies near DOT_THRESHOLD, where the two can take
+// different branches). The FMA chains are sequential by definition, so one workgroup streams a
+// segment chunk through LDS to one compute wave: a parity mode, not a fast path.
+
+constexpr int kRefThreads = 1024;                      // workgroup of the norm pass
+constexpr int kRefPer = 16;                            // elements staged per thread per stage
+constexpr int kRefStage = kRefThreads * kRefPer;       // 16,384 elements (64 KiB of fp32)
+constexpr int kRefBuf = 8192;                          // numpy's ufunc buffer
+
+// segment s of a chunk table: [start, end) (relative to the segment's buffers when seg_ptrs)
+__device__ __forceinline__ void ref_segment(const uint64_t* chunks, const int32_t* first, int s, uint64_t& a,
+                                            uint64_t& e) {
+    const int c0 = first[s], c1 = first[s + 1];
+    a = e = 0;
+    if (c1 > c0) {
+        a = chunks[3 * (uint64_t)c0];
+        e = chunks[3 * (uint64_t)(c1 - 1)] + chunks[3 * (uint64_t)(c1 - 1) + 1];
+    }
+}
+
+// OpenBLAS's level-1 split: chunk t of `threads` over n elements -> [off, off + len)
+__device__ __forceinline__ void ref_split(uint64_t n, int threads, int t, uint64_t& off, uint64_t& len) {
+    uint64_t rest = n;
+    off = 0;
+    len = 0;
+    for (int c = 0; c <= t && rest > 0; ++c) {
+        uint64_t w = (rest + (uint64_t)(threads - c) - 1) / (uint64_t)(threads - c);
+        if (w > rest) w = rest;
+        if (c == t) {
+            len = w;
+            return;
+        }
+        off += w;
+        rest -= w;
+    }
+}
+
+template <int IDT>
+__device__ __forceinline__ float ref_load(const void* p, uint64_t i) {
+    float x[1];
+    ld<IDT, 1>(p, i, x);
+    return x[0];
+}
+
+// Pass 1: block -> (segment s, vector w in {v0, v1}, thread chunk t); part[(2 s + w) threads + t] =
+// that chunk's sdot(v, v) as OpenBLAS returns it to its combiner (double).
+template <int IDT>
+__global__ __launch_bounds__(kRefThreads) void refdot_norm_kernel(const void* v0, const void* v1,
+                                                                  const uint64_t* chunks, const int32_t* first,
+                                                                  int nseg, const int32_t* flag, int threads,
+                                                                  const uint64_t* seg_ptrs, double* part) {
+    const int s = (int)(blockIdx.x / (2u * (unsigned)threads));
+    const int w = (int)((blockIdx.x / (unsigned)threads) % 2u);
+    const int t = (int)(blockIdx.x % (unsigned)threads);
+    if (s >= nseg || (flag && !flag[s])) return;
+    uint64_t a, e;
+    ref_segment(chunks, first, s, a, e);
+    const void* v = w ? v1 : v0;
+    if (seg_ptrs) v = reinterpret_cast<const void*>(seg_ptrs[3 * (uint64_t)s + w]);
+    uint64_t off, len;
+    ref_split(e - a, threads, t, off, len);
+    const uint64_t base = a + off;
+    const uint64_t n1 = len & ~(uint64_t)31, n64 = n1 & ~(uint64_t)63;
+    __shared__ float buf[2][kRefStage];
+    __shared__ float red[64];
+    const int tid = threadIdx.x, lane = tid & 63;
+    float acc = 0.f;                                     // wave 0: chain `lane`
+    const uint64_t nst = (n64 + kRefStage - 1) / kRefStage;
+    float r[kRefPer];
+    auto fetch = [&](uint64_t st) {
+#pragma unroll
+        for (int q = 0; q < kRefPer; ++q) {
+            const uint64_t i = st * kRefStage + (uint64_t)q * kRefThreads + (uint64_t)tid;
+            r[q] = i < n64 ? ref_load<IDT>(v, base + i) : 0.f;
+        }
+    };
+    auto put = [&](int b) {
+#pragma unroll
+        for (int q = 0; q < kRefPer; ++q) buf[b][q * kRefThreads + tid] = r[q];
+    };
+    if (nst > 0) {
+        fetch(0);
+        put(0);
+    }
+    __syncthreads();
+    for (uint64_t st = 0; st < nst; ++st) {
+        if (st + 1 < nst) fetch(st + 1);                 // the next stage's loads in flight ...
+        if (tid < 64) {                                  // ... while wave 0 runs this stage's chains
+            const uint64_t m = (n64 - st * kRefStage < (uint64_t)kRefStage ? n64 - st * kRefStage : kRefStage) / 64;
+            const float* bb = buf[st & 1];
+            for (uint64_t k = 0; k < m; ++k) {
+                const float x = bb[k * 64 + lane];
+                acc = __builtin_fmaf(x, x, acc);
+            }
+        }
+        if (st + 1 < nst) put((int)((st + 1) & 1));      // buffer last read in stage st - 1
+        __syncthreads();
+    }
+    if (tid < 64) red[lane] = acc;
+    __syncthreads();
+    if (tid == 0) {
+        double d = 0.0;
+        if (n1) {
+            float a8[4][8];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int l = 0; l < 8; ++l) a8[j][l] = red[16 * j + l] + red[16 * j + l + 8];
+            if (n1 > n64)                                // the 32-element remainder block
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int l = 0; l < 8; ++l) {
+                        const float x = ref_load<IDT>(v, base + n64 + 8 * j + l);
+                        a8[j][l] = __builtin_fmaf(x, x, a8[j][l]);
+                    }
+            float sl[8], h[4];
+#pragma unroll
+            for (int l = 0; l < 8; ++l) sl[l] = ((a8[0][l] + a8[1][l]) + a8[2][l]) + a8[3][l];
+#pragma unroll
+            for (int l = 0; l < 4; ++l) h[l] = sl[l] + sl[l + 4];
+            d = (double)((h[0] + h[1]) + (h[2] + h[3]));
+        }
+        for (uint64_t i = n1; i < len; ++i) {
+            const float x = ref_load<IDT>(v, base + i);
+            d += (double)(x * x);
+        }
+        part[(2 * (uint64_t)s + w) * (uint64_t)threads + t] = d;
+    }
+}
+
+// The norm of (segment s, vector w) from the chunk results, as np.linalg.norm returns it.
+__device__ __forceinline__ float ref_norm(const double* part, int s, int w, int threads) {
+    const double* p = part + (2 * (uint64_t)s + w) * (uint64_t)threads;
+    float dot;
+    if (threads <= 1) {
+        dot = (float)p[0];
+    } else {
+        dot = 0.f;
+        for (int t = 0; t < threads; ++t) dot = (float)((double)dot + p[t]);
+    }
+    return __fsqrt_rn(dot);
+}
+
+template <int IDT>
+struct RefProd {                                         // element i of (v0 / n0) * (v1 / n1)
+    const void* a;
+    const void* b;
+    float n0, n1;
+    bool d0, d1;                                         // normalize() divides only if norm > eps
+    __device__ __forceinline__ float operator()(uint64_t i) const {
+        float x = ref_load<IDT>(a, i), y = ref_load<IDT>(b, i);
+        if (d0) x = __fdiv_rn(x, n0);
+        if (d1) y = __fdiv_rn(y, n1);
+        return x * y;
+    }
+};
+
+template <typename P>
+__device__ __forceinline__ float np_leaf(const P& p, uint64_t o, uint64_t n) {
+    if (n < 8) {
+        float r = 0.f;
+        for (uint64_t i = 0; i < n; ++i) r += p(o + i);
+        return r;
+    }
+    float r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = p(o + j);
+    uint64_t i = 8;
+    for (; i < n - (n % 8); i += 8)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] += p(o + i + j);
+    float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res += p(o + i);
+    return res;
+}
+
+// numpy's pairwise_sum over [o, o + n), n <= 8192, on one lane (explicit stack, depth <= 7).
+template <typename P>
+__device__ float np_pairwise_serial(const P& p, uint64_t o, uint64_t n) {
+    uint64_t so[12], sn[12];
+    float sl[12];
+    int stage[12];
+    int sp = 0;
+    so[0] = o;
+    sn[0] = n;
+    stage[0] = 0;
+    float ret = 0.f;
+    for (;;) {
+        const uint64_t fo = so[sp], fn = sn[sp];
+        uint64_t h = fn / 2;
+        h -= h % 8;
+        bool done = false;
+        if (stage[sp] == 0) {
+            if (fn <= 128) {
+                ret = np_leaf(p, fo, fn);
+                done = true;
+            } else {
+                stage[sp] = 1;
+                so[sp + 1] = fo;
+                sn[sp + 1] = h;
+                stage[sp + 1] = 0;
+                ++sp;
+            }
+        } else if (stage[sp] == 1) {
+            sl[sp] = ret;
+            stage[sp] = 2;
+            so[sp + 1] = fo + h;
+            sn[sp + 1] = fn - h;
+            stage[sp + 1] = 0;
+            ++sp;
+        } else {
+            ret = sl[sp] + ret;
+            done = true;
+        }
+        if (done) {
+            if (sp == 0) return ret;
+            --sp;
+        }
+    }
+}
+
+// Pass 2: one wave per 8192-element buffer of a flagged segment (buffer q of chunk c; chunks are
+// whole multiples of it inside their segment): a full buffer is numpy's perfect pairwise tree —
+// lane L the 128-element leaf L, the xor butterfly the levels above it in order — a partial one
+// (the segment's last) runs the recursion on lane 0. bsum[c * bpc + q] = the buffer's sum.
+template <int IDT>
+__global__ __launch_bounds__(kBlock) void refdot_sum_kernel(const void* v0, const void* v1, const uint64_t* chunks,
+                                                            int64_t nchunks, const int32_t* first, const int32_t* flag,
+                                                            int threads, float eps, const uint64_t* seg_ptrs,
+                                                            const double* part, int bpc, float* bsum) {
+    const uint64_t u = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (u >= (uint64_t)nchunks * (uint64_t)bpc) return;
+    const uint64_t c = u / (uint64_t)bpc, q = u % (uint64_t)bpc;
+    const int s = (int)chunks[3 * c + 2];
+    if (flag && !flag[s]) return;
+    const uint64_t cs = chunks[3 * c], cl = chunks[3 * c + 1];
+    if (q * kRefBuf >= cl) return;
+    const uint64_t o = cs + q * kRefBuf;
+    const uint64_t n = cl - q * kRefBuf < (uint64_t)kRefBuf ? cl - q * kRefBuf : (uint64_t)kRefBuf;
+    RefProd<IDT> p;
+    p.a = seg_ptrs ? reinterpret_cast<const void*>(seg_ptrs[3 * (uint64_t)s]) : v0;
+    p.b = seg_ptrs ? reinterpret_cast<const void*>(seg_ptrs[3 * (uint64_t)s + 1]) : v1;
+    p.n0 = ref_norm(part, s, 0, threads);
+    p.n1 = ref_norm(part, s, 1, threads);
+    p.d0 = p.n0 > eps;
+    p.d1 = p.n1 > eps;
+    if (n == (uint64_t)kRefBuf) {
+        float x = np_leaf(p, o + 128 * (uint64_t)lane, 128);
+#pragma unroll
+        for (int m = 1; m < 64; m <<= 1) x += __shfl_xor(x, m, 64);
+        if (lane == 0) bsum[u] = x;
+    } else if (lane == 0) {
+        bsum[u] = np_pairwise_serial(p, o, n);
+    }
+}
+
+// Pass 3: per flagged segment, the buffers' sums added in order to a float starting at 0.
+__global__ __launch_bounds__(kBlock) void refdot_total_kernel(const uint64_t* chunks, const int32_t* first, int nseg,
+                                                              const int32_t* flag, int bpc, const float* bsum,
+                                                              float* ref_dot) {
+    const int s = (int)(blockIdx.x * kBlock + threadIdx.x);
+    if (s >= nseg || (flag && !flag[s])) return;
+    float r = 0.f;
+    for (int c = first[s]; c < first[s + 1]; ++c) {
+        const uint64_t cl = chunks[3 * (uint64_t)c + 1];
+        for (int q = 0; q < bpc && (uint64_t)q * kRefBuf < cl; ++q) r += bsum[(uint64_t)c * bpc + q];
+    }
+    ref_dot[s] = r;
+}
+
+// Flags: segments whose dot lies within `band` of the threshold (|dot| in [thr - band, thr + band]);
+// band < 0: every segment.
+__global__ __launch_bounds__(kBlock) void refdot_flag_kernel(const float* dots, int nseg, float thr, float band,
+                                                             int32_t* flag) {
+    const int s = (int)(blockIdx.x * kBlock + threadIdx.x);
+    if (s >= nseg) return;
+    flag[s] = band < 0.f || fabsf(fabsf(dots[s]) - thr) <= band ? 1 : 0;
+}
+
+// Coefficients of the flagged segments from the reference dot (slerp_coefficients' scalar math).
+__global__ __launch_bounds__(kBlock) void refdot_coef_kernel(const float* ref_dot, const int32_t* flag, int nseg,
+                                                             const double* tvals, float thr, float* coef,
+                                                             float* dot_out) {
+    const int s = (int)(blockIdx.x * kBlock + threadIdx.x);
+    if (s >= nseg || (flag && !flag[s])) return;
+    const float dot = ref_dot[s];
+    float c0, c1;
+    coefficients_from_dot(dot, tvals[s], thr, c0, c1);
+    coef[2 * s] = c0;
+    coef[2 * s + 1] = c1;
+    if (dot_out) dot_out[s] = dot;
+}
 
 }  // namespace
 
@@ -717,15 +1082,20 @@ int edt_slerp_merge(const void* v0, const void* v1, int in_dt, void* out, int ou
     return edt_slerp_blend(v0, v1, in_dt, out, out_dt, chunk_desc, nchunks, coef, stream);
 }
 
+uint64_t edt_slerp_sums_doubles(int width, int64_t nchunks) {
+    if (width < 1 || nchunks < 0) return 0;
+    return (uint64_t)nchunks * (uint64_t)width * (1ull + (uint64_t)kSlots);
+}
+
 uint64_t edt_slerp_population_speculative_doubles(int npairs, int64_t nchunks) {
     if (npairs < 0 || nchunks < 0) return 0;
     const uint64_t per = 3ull * (uint64_t)npairs > 36ull ? 3ull * (uint64_t)npairs : 36ull;   // 36: 8 x 9 / 2
-    return (uint64_t)nchunks * per;
+    return (uint64_t)nchunks * per * (1ull + (uint64_t)kSlots);
 }
 
 uint64_t edt_slerp_population_gram_doubles(int nmembers, int64_t nchunks) {
     if (nmembers < 1 || nmembers > kGramMaxMembers || nchunks < 0) return 0;
-    return (uint64_t)nchunks * (uint64_t)(nmembers * (nmembers + 1) / 2);
+    return edt_slerp_sums_doubles(nmembers * (nmembers + 1) / 2, nchunks);
 }
 
 int edt_slerp_population(const void* const* members, int nmembers, int in_dt, const int32_t* pairs, int npairs,
@@ -767,19 +1137,7 @@ int edt_slerp_population(const void* const* members, int nmembers, int in_dt, co
                 mem.p[D++] = members[m];
             }
         }
-    // the Gram pass (M(M+1)/2 fp64 sums per thread, low occupancy) stays grid-stride unless
-    // EDT_SLERP_GRAM_GRID: 1.3B x 8 generation 10.83 ms grid-stride vs 11.46 ms one per chunk
-    const unsigned g = EDT_SLERP_GRAM_GRID ? slerp_grid(nchunks) : slerp_spec_grid(nchunks);
-#define EDT_GRAM(M)                                                                                  \
-    case M:                                                                                          \
-        if (in_dt == EDT_F32) slerp_gram_kernel<EDT_F32, M><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, gram); \
-        else slerp_gram_kernel<EDT_BF16, M><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, gram);              \
-        break;
-    switch (D) {
-        EDT_GRAM(1) EDT_GRAM(2) EDT_GRAM(3) EDT_GRAM(4) EDT_GRAM(5) EDT_GRAM(6) EDT_GRAM(7) EDT_GRAM(8)
-    }
-#undef EDT_GRAM
-    int rc = check_launch("slerp_gram_kernel");
+    int rc = gram_sums(mem, D, nullptr, in_dt, out_dt, chunk_desc, nchunks, nullptr, gram, s);
     if (rc) return rc;
     const int M = D, NT = M * (M + 1) / 2;
     const unsigned gc = coef_grid(nseg);
@@ -818,7 +1176,7 @@ int edt_slerp_population(const void* const* members, int nmembers, int in_dt, co
             B.coef[k] = coef + 2 * (size_t)nseg * q;
         }
         const uint64_t blocks = ((uint64_t)nchunks + 7) / 8 * 8ull * (uint64_t)B.nchildren;
-        if (blocks > 0x7fffffffull) return fail(EDT_ERR_ARG, "too many chunks for one launch");
+        if (blocks > kGridBlockCap) return fail(EDT_ERR_ARG, "too many chunks for one launch");
         const unsigned gb = (unsigned)blocks;
         if (in_dt == EDT_F32 && out_dt == EDT_F32)
             slerp_blend_population_kernel<EDT_F32, EDT_F32><<<gb, kBlock, 0, s>>>(B, chunk_desc, nchunks);
@@ -853,18 +1211,7 @@ int edt_slerp_gram(const void* const* members, int nmembers, int in_dt, const ui
         if (!members[m] || !aligned16(members[m])) return fail(EDT_ERR_ARG, "member %d is null or not 16-byte aligned", m);
         mem.p[m] = members[m];
     }
-    hipStream_t s = (hipStream_t)stream;
-    const unsigned g = EDT_SLERP_GRAM_GRID ? slerp_grid(nchunks) : slerp_spec_grid(nchunks);
-#define EDT_GRAM1(M)                                                                                 \
-    case M:                                                                                          \
-        if (in_dt == EDT_F32) slerp_gram_kernel<EDT_F32, M><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, gram); \
-        else slerp_gram_kernel<EDT_BF16, M><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, gram);              \
-        break;
-    switch (nmembers) {
-        EDT_GRAM1(1) EDT_GRAM1(2) EDT_GRAM1(3) EDT_GRAM1(4) EDT_GRAM1(5) EDT_GRAM1(6) EDT_GRAM1(7) EDT_GRAM1(8)
-    }
-#undef EDT_GRAM1
-    return check_launch("slerp_gram_kernel");
+    return gram_sums(mem, nmembers, nullptr, in_dt, EDT_F32, chunk_desc, nchunks, nullptr, gram, (hipStream_t)stream);
 }
 
 int edt_slerp_gram_coef(const double* gram, int nmembers, const int32_t* pairs, int npairs,
@@ -948,23 +1295,14 @@ int edt_slerp_merge_speculative(const void* v0, const void* v1, int in_dt, void*
         if (p0 < o1 && o0 < p1) return fail(EDT_ERR_ARG, "speculative SLERP needs an output apart from the parents");
     }
     hipStream_t s = (hipStream_t)stream;
-    const unsigned g = EDT_SLERP_SPEC_CONTIG > 0 ? (unsigned)((nchunks + EDT_SLERP_SPEC_CONTIG - 1) / EDT_SLERP_SPEC_CONTIG)
-                                                 : slerp_spec_grid(nchunks);
-    if (in_dt == EDT_F32 && out_dt == EDT_F32)
-        slerp_stats_lerp_kernel<EDT_F32, EDT_F32><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, partial, t);
-    else if (in_dt == EDT_F32)
-        slerp_stats_lerp_kernel<EDT_F32, EDT_BF16><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, partial, t);
-    else if (out_dt == EDT_F32)
-        slerp_stats_lerp_kernel<EDT_BF16, EDT_F32><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, partial, t);
-    else
-        slerp_stats_lerp_kernel<EDT_BF16, EDT_BF16><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, partial, t);
-    int rc = check_launch("slerp_stats_lerp_kernel");
+    int rc = pair_sums(v0, v1, in_dt, out, out_dt, true, chunk_desc, nchunks, partial, t, nullptr, s);
     if (rc) return rc;
     slerp_coef_kernel<<<coef_grid(nseg), kBlock, 0, s>>>(partial, seg_first_chunk, nseg, t, (float)dot_threshold,
                                                          (float)eps, coef, dot_out, redo);
     rc = check_launch("slerp_coef_kernel");
     if (rc) return rc;
     // the redo blends: grid-stride over chunks (most segments are skipped)
+    const unsigned g = slerp_spec_grid(nchunks);
     constexpr bool kNtB = EDT_NT_SLERP != 0;
     if (in_dt == EDT_F32 && out_dt == EDT_F32)
         slerp_blend_kernel<EDT_F32, EDT_F32, false, false><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, nullptr, redo);
@@ -1030,23 +1368,7 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
             po.a[q] = compact[pairs[2 * q]];
             po.b[q] = compact[pairs[2 * q + 1]];
         }
-        const unsigned g = slerp_spec_grid(nchunks);
-#define EDT_GL(M)                                                                                             \
-    case M:                                                                                                   \
-        if (in_dt == EDT_F32 && out_dt == EDT_F32)                                                            \
-            slerp_gram_lerp_kernel<EDT_F32, EDT_F32, M><<<g, kBlock, 0, s>>>(mem, po, chunk_desc, nchunks, t, partial); \
-        else if (in_dt == EDT_F32)                                                                            \
-            slerp_gram_lerp_kernel<EDT_F32, EDT_BF16, M><<<g, kBlock, 0, s>>>(mem, po, chunk_desc, nchunks, t, partial); \
-        else if (out_dt == EDT_F32)                                                                           \
-            slerp_gram_lerp_kernel<EDT_BF16, EDT_F32, M><<<g, kBlock, 0, s>>>(mem, po, chunk_desc, nchunks, t, partial); \
-        else                                                                                                  \
-            slerp_gram_lerp_kernel<EDT_BF16, EDT_BF16, M><<<g, kBlock, 0, s>>>(mem, po, chunk_desc, nchunks, t, partial); \
-        break;
-        switch (D) {
-            EDT_GL(1) EDT_GL(2) EDT_GL(3) EDT_GL(4) EDT_GL(5) EDT_GL(6) EDT_GL(7) EDT_GL(8)
-        }
-#undef EDT_GL
-        int rc = check_launch("slerp_gram_lerp_kernel");
+        int rc = gram_sums(mem, D, &po, in_dt, out_dt, chunk_desc, nchunks, t, partial, s);
         if (rc) return rc;
         const int NT = D * (D + 1) / 2;
         for (int q = 0; q < npairs; ++q) {
@@ -1085,10 +1407,12 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
                 B.out[k] = outs[q];
                 B.coef[k] = coef + 2 * (size_t)nseg * q;
                 B.redo[k] = redo + (size_t)nseg * q;
-                B.partial[k] = partial + 3 * (size_t)nchunks * q;
+                B.slots[k] = partial + 3 * (size_t)nchunks * npairs + 3 * (size_t)kSlots * nchunks * q;
             }
-            const uint64_t blocks = ((uint64_t)nchunks + 7) / 8 * 8ull * (uint64_t)B.nchildren;
-            if (blocks > 0x7fffffffull) return fail(EDT_ERR_ARG, "too many chunks for one launch");
+            // pass 0: one block per (unit = chunk x slot group, child); pass 1: per (chunk, child)
+            const uint64_t units = pass == 0 ? (uint64_t)nchunks * kSlotGroups : (uint64_t)nchunks;
+            const uint64_t blocks = (units + 7) / 8 * 8ull * (uint64_t)B.nchildren;
+            if (blocks > kGridBlockCap) return fail(EDT_ERR_ARG, "too many chunks for one launch");
             const unsigned gb = (unsigned)blocks;
 #define EDT_SPEC_POP(KERNEL, ...)                                                                   \
     do {                                                                                            \
@@ -1105,10 +1429,13 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
         }
         if (pass == 0) {
             for (int q = 0; q < npairs; ++q) {
+                int rc = launch_slot_reduce(partial + 3 * (size_t)nchunks * npairs + 3 * (size_t)kSlots * nchunks * q, 3,
+                                            nchunks, partial + 3 * (size_t)nchunks * q, s);
+                if (rc) return rc;
                 slerp_coef_kernel<<<coef_grid(nseg), kBlock, 0, s>>>(
                     partial + 3 * (size_t)nchunks * q, seg_first_chunk, nseg, t, (float)dot_threshold, (float)eps,
                     coef + 2 * (size_t)nseg * q, dot_out ? dot_out + (size_t)nseg * q : nullptr, redo + (size_t)nseg * q);
-                int rc = check_launch("slerp_coef_kernel");
+                rc = check_launch("slerp_coef_kernel");
                 if (rc) return rc;
             }
         }
@@ -1151,5 +1478,92 @@ int edt_slerp_merge_list(const void* const* v0_t, const void* const* v1_t, int i
     return slerp_blend_impl(nullptr, nullptr, in_dt, nullptr, out_dt, chunk_desc, nchunks, coef, seg_ptrs, stream);
 }
 
+
+// ---- reference-dot mode (include/edt_sync.h) ----
+
+uint64_t edt_slerp_refdot_workspace_bytes(int nseg, int64_t nchunks, uint32_t chunk_elems, int threads) {
+    if (nseg < 0 || nchunks < 0 || threads < 1 || chunk_elems == 0 || chunk_elems % kRefBuf) return 0;
+    const uint64_t bpc = chunk_elems / kRefBuf;
+    return 8ull * 2 * (uint64_t)(nseg > 0 ? nseg : 1) * (uint64_t)threads + 4ull * (uint64_t)(nchunks > 0 ? nchunks : 1) * bpc;
+}
+
+int edt_slerp_refdot_flags(const float* dots, int nseg, double dot_threshold, double band, int32_t* flag,
+                           void* stream) {
+    g_err[0] = 0;
+    if (nseg < 0) return fail(EDT_ERR_ARG, "negative segment count");
+    if (nseg == 0) return EDT_OK;
+    if (!dots || !flag) return fail(EDT_ERR_ARG, "null buffer");
+    refdot_flag_kernel<<<(unsigned)((nseg + kBlock - 1) / kBlock), kBlock, 0, (hipStream_t)stream>>>(
+        dots, nseg, (float)dot_threshold, (float)band, flag);
+    return check_launch("refdot_flag_kernel");
+}
+
+static int refdot_impl(const void* v0, const void* v1, int in_dt, const uint64_t* chunk_desc, int64_t nchunks,
+                       const int32_t* seg_first_chunk, int nseg, uint32_t chunk_elems, const int32_t* flag,
+                       int threads, double eps, float* ref_dot, void* workspace, uint64_t workspace_bytes,
+                       const uint64_t* seg_ptrs, void* stream) {
+    if (in_dt & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
+    if (nseg < 0 || nchunks < 0) return fail(EDT_ERR_ARG, "negative count");
+    if (threads < 1 || threads > 256) return fail(EDT_ERR_ARG, "BLAS thread count %d out of range [1, 256]", threads);
+    if (chunk_elems == 0 || chunk_elems % kRefBuf)
+        return fail(EDT_ERR_ARG, "reference-dot mode needs chunks of a multiple of %d elements (got %u)", kRefBuf,
+                    chunk_elems);
+    if (nseg == 0) return EDT_OK;
+    if (!chunk_desc || !seg_first_chunk || !ref_dot || !workspace) return fail(EDT_ERR_ARG, "null buffer");
+    if (!seg_ptrs && (!v0 || !v1)) return fail(EDT_ERR_ARG, "null buffer");
+    const uint64_t need = edt_slerp_refdot_workspace_bytes(nseg, nchunks, chunk_elems, threads);
+    if (workspace_bytes < need) return fail(EDT_ERR_ARG, "workspace of %llu bytes needed", (unsigned long long)need);
+    if (reinterpret_cast<uintptr_t>(workspace) & 7u) return fail(EDT_ERR_ARG, "workspace must be 8-byte aligned");
+    hipStream_t s = (hipStream_t)stream;
+    double* part = static_cast<double*>(workspace);
+    float* bsum = reinterpret_cast<float*>(part + 2 * (uint64_t)nseg * (uint64_t)threads);
+    const int bpc = (int)(chunk_elems / kRefBuf);
+    const uint64_t gn = 2ull * (uint64_t)nseg * (uint64_t)threads;
+    if (gn > kGridBlockCap) return fail(EDT_ERR_ARG, "too many segments x threads");
+    if (in_dt == EDT_F32)
+        refdot_norm_kernel<EDT_F32><<<(unsigned)gn, kRefThreads, 0, s>>>(v0, v1, chunk_desc, seg_first_chunk, nseg, flag,
+                                                                         threads, seg_ptrs, part);
+    else
+        refdot_norm_kernel<EDT_BF16><<<(unsigned)gn, kRefThreads, 0, s>>>(v0, v1, chunk_desc, seg_first_chunk, nseg,
+                                                                          flag, threads, seg_ptrs, part);
+    int rc = check_launch("refdot_norm_kernel");
+    if (rc) return rc;
+    if (nchunks > 0) {
+        const uint64_t waves = (uint64_t)nchunks * (uint64_t)bpc;
+        const uint64_t gs = (waves + kBlock / 64 - 1) / (kBlock / 64);
+        if (gs > kGridBlockCap) return fail(EDT_ERR_ARG, "too many chunks for one launch");
+        if (in_dt == EDT_F32)
+            refdot_sum_kernel<EDT_F32><<<(unsigned)gs, kBlock, 0, s>>>(v0, v1, chunk_desc, nchunks, seg_first_chunk, flag,
+                                                                        threads, (float)eps, seg_ptrs, part, bpc, bsum);
+        else
+            refdot_sum_kernel<EDT_BF16><<<(unsigned)gs, kBlock, 0, s>>>(v0, v1, chunk_desc, nchunks, seg_first_chunk,
+                                                                         flag, threads, (float)eps, seg_ptrs, part, bpc,
+                                                                         bsum);
+        rc = check_launch("refdot_sum_kernel");
+        if (rc) return rc;
+    }
+    refdot_total_kernel<<<(unsigned)((nseg + kBlock - 1) / kBlock), kBlock, 0, s>>>(chunk_desc, seg_first_chunk, nseg,
+                                                                                    flag, bpc, bsum, ref_dot);
+    return check_launch("refdot_total_kernel");
+}
+
+int edt_slerp_refdot(const void* v0, const void* v1, int in_dt, const uint64_t* chunk_desc, int64_t nchunks,
+                     const int32_t* seg_first_chunk, int nseg, uint32_t chunk_elems, const int32_t* flag, int threads,
+                     double eps, float* ref_dot, void* workspace, uint64_t workspace_bytes, void* stream) {
+    g_err[0] = 0;
+    return refdot_impl(v0, v1, in_dt, chunk_desc, nchunks, seg_first_chunk, nseg, chunk_elems, flag, threads, eps,
+                       ref_dot, workspace, workspace_bytes, nullptr, stream);
+}
+
+int edt_slerp_refdot_coef(const float* ref_dot, const int32_t* flag, int nseg, const double* t, double dot_threshold,
+                          float* coef, float* dot_out, void* stream) {
+    g_err[0] = 0;
+    if (nseg < 0) return fail(EDT_ERR_ARG, "negative segment count");
+    if (nseg == 0) return EDT_OK;
+    if (!ref_dot || !t || !coef) return fail(EDT_ERR_ARG, "null buffer");
+    refdot_coef_kernel<<<(unsigned)((nseg + kBlock - 1) / kBlock), kBlock, 0, (hipStream_t)stream>>>(
+        ref_dot, flag, nseg, t, (float)dot_threshold, coef, dot_out);
+    return check_launch("refdot_coef_kernel");
+}
 
 }  // extern "C"

@@ -270,11 +270,17 @@ class DirOuterSync:
     state_path: the outer optimiser's state file (torch `SGD.state_dict()` format, as
     `outer_optim.pt`): loaded before the first step when it exists and rewritten after every step,
     so a restarted master resumes the momentum carry (the reference keeps it in RAM only,
-    EDT_LM/diloco.py:100)."""
+    EDT_LM/diloco.py:100).
+    carry_inner_state: EDT_LM/diloco.py:295-300 — before the new weights are written, each
+    worker's previous-generation `optimizer.pt` / `scheduler.pt` (step(prev_dirs=...), GenN of
+    every machine) is copied over the one its inner loop left in its GenN+1 dir, where it exists,
+    so the next inner loop resumes the inner optimiser as the reference's does."""
+
+    INNER_STATE_FILES = ("optimizer.pt", "scheduler.pt")
 
     def __init__(self, device=None, theta_dtype=None, worker_dtype=None, names=None,
                  lr=0.7, momentum=0.9, nesterov=True, state: OuterState | None = None,
-                 state_path: str | None = None):
+                 state_path: str | None = None, carry_inner_state: bool = False):
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.theta_dtype, self.worker_dtype, self.names = theta_dtype, worker_dtype, names
         self.lr, self.momentum, self.nesterov = lr, momentum, nesterov
@@ -284,6 +290,7 @@ class DirOuterSync:
         self.workers: list[ParamArena] = []
         self._written: set[str] = set()     # dirs holding the resident theta (last step's output)
         self.state_path = state_path
+        self.carry_inner_state = carry_inner_state
 
     def _layout_from(self, model_dir):
         from .checkpoint import checkpoint_files, read_header, _ST_DTYPES
@@ -299,9 +306,16 @@ class DirOuterSync:
         return ParamLayout([tuple(metas[n][1]["shape"]) for n in names], names), dt
 
     @traced("edt/DirOuterSync.step")
-    def step(self, base_dir: str, worker_dirs: list[str], out_dirs: list[str] | None = None) -> OuterState:
+    def step(self, base_dir: str, worker_dirs: list[str], out_dirs: list[str] | None = None,
+             prev_dirs: list[str] | None = None) -> OuterState:
+        """base_dir: GenN of worker 0 (the base); worker_dirs: GenN+1 of every worker (trained);
+        out_dirs: where the new weights go (default: worker_dirs, as the reference); prev_dirs:
+        GenN of every worker, whose inner optimiser / scheduler files are carried into
+        worker_dirs when carry_inner_state is set (EDT_LM/diloco.py:295-300)."""
         import shutil
         from .checkpoint import read_many, save_to_dirs
+        if self.carry_inner_state and (prev_dirs is None or len(prev_dirs) != len(worker_dirs)):
+            raise ValueError("carry_inner_state needs prev_dirs: the previous generation dir of every worker")
         if self.layout is None:
             self.layout, ckpt_dt = self._layout_from(base_dir)
             self.theta_dtype = self.theta_dtype or ckpt_dt
@@ -318,6 +332,12 @@ class DirOuterSync:
         _step_flat(self.theta.flat, [w.flat for w in self.workers[:len(worker_dirs)]], self.state,
                    self.lr, self.momentum, self.nesterov)
         out_dirs = worker_dirs if out_dirs is None else out_dirs
+        if self.carry_inner_state:          # diloco.py:295-300, before the model write as there
+            for source, target in zip(prev_dirs, worker_dirs):
+                for fname in self.INNER_STATE_FILES:
+                    src = os.path.join(source, fname)
+                    if os.path.exists(src):
+                        shutil.copy(src, os.path.join(target, fname))
         save_to_dirs(out_dirs, self.layout, self.theta.flat)
         if self.state_path:                  # durable carry: write-then-rename
             self.state.save(self.state_path + ".tmp", self.layout)

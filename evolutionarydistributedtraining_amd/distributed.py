@@ -40,6 +40,7 @@ import math
 import torch
 
 from . import ops as _ops
+from ._lib import EdtError
 from .collectives import Collectives, TorchCollectives
 from .diloco import check_sgd_hparams
 from .params import ParamArena, ParamLayout
@@ -467,12 +468,12 @@ class ShardedPopulationCrossover:
         loc[:, 0] -= base
         self.local_chunks = torch.from_numpy(loc).to(self.device) if self.device.type == "cuda" else torch.from_numpy(loc)
         L = end - base
-        self._shard = lambda dt: torch.empty(max(L, 8), dtype=dt, device=self.device)
+        self._shard_len = max(L, 8)     # no closure over self: the buffers go with the object
         self._bufs = {}
 
     def _buf(self, key, dt):
         if key not in self._bufs:
-            self._bufs[key] = self._shard(dt)
+            self._bufs[key] = torch.empty(self._shard_len, dtype=dt, device=self.device)
         return self._bufs[key]
 
     def _scatter(self, tensors, tag):
@@ -615,15 +616,24 @@ class ShardedPopulationCrossover:
         donor = parent 1 when it has an outer momentum, else parent 2, as PopulationCrossover)."""
         if len(pairs) != self.world:
             raise ValueError(f"{len(pairs)} children for {self.world} ranks")
-        flags = self.comm.all_gather_object(bool(has_momentum and momentum is not None))
+        # each rank's momentum flag and the dtypes its momentum buffers would travel in: every rank
+        # sizes its p2p buffers from its own send list, so a dtype that differs across ranks would
+        # post sends and receives of different byte counts — refused on every rank instead
+        has = bool(has_momentum and momentum is not None)
+        mdt = str(out_momentum.dtype) if out_momentum is not None else None
+        info = self.comm.all_gather_object((has, mdt, str(momentum.dtype) if has else None))
+        flags = [f for f, _, _ in info]
         donors = [i if flags[i] else (j if flags[j] else None) for i, j in pairs]
         if mu != 0 and generation > 0 and any(d is None for d in donors):
             raise NotImplementedError("Merging outer optimizer states not implemented for this case.")
         send_mom = any(d is not None for d in donors)      # some child inherits a buffer
-        if send_mom and out_momentum is None:
-            raise ValueError("the child inherits an outer momentum: pass out_momentum")
+        if send_mom and any(m is None for _, m, _ in info):     # on every rank, not just the one missing it
+            raise ValueError("the child inherits an outer momentum: pass out_momentum on every rank")
+        if send_mom and (len({m for _, m, _ in info}) != 1 or any(d not in (None, info[0][1]) for _, _, d in info)):
+            raise EdtError(f"outer momentum dtypes differ across ranks or from the child's: {info}")
         with_mom = out_momentum is not None                # children write one (mu != 0)
-        send = [base, trained] + ([momentum if momentum is not None else torch.zeros_like(base)] if send_mom else [])
+        stand_in = (lambda: torch.zeros_like(base, dtype=out_momentum.dtype)) if send_mom else None
+        send = [base, trained] + ([momentum if has else stand_in()] if send_mom else [])
         sh = self._scatter(send, "p")
         L = self.end - self.base
         children = []

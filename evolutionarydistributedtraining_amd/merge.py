@@ -140,6 +140,19 @@ def _compute_device(*tensors) -> torch.device:
 
 _plans: dict = {}
 
+# The SLERP branch-decision mode of every merge below (and so of the rl / evomerge surfaces):
+# None = the kernels' fp64 dot; an ops.RefDot = the reference host's own fp32 dot,
+# bit for bit, on the segments it flags (set_reference_dot).
+_ref_dot = None
+
+
+def set_reference_dot(ref=None):
+    """Decide the SLERP branch as the reference host does (ops.RefDot(threads, band)), or from the
+    accurate fp64 dot (None, the default). Returns the previous setting."""
+    global _ref_dot
+    prev, _ref_dot = _ref_dot, ref
+    return prev
+
 
 def _plan_for(offsets, device, relative=False):
     key = (tuple(offsets), str(device), relative)
@@ -216,7 +229,8 @@ def slerp_tensors(pairs, ts, out_dtype=torch.float32, device=None, dot_threshold
         dts = {o.dtype for o in out}
         out_dtype = out[0].dtype if len(dts) == 1 else torch.float32   # mixed: round once, in copy_
     tt = torch.tensor([float(t) for t in ts], dtype=torch.float64).to(dev)
-    if all(a.dtype == in_dt and b.dtype == in_dt for a, b in pairs) and _listable([t for p in pairs for t in p], dev):
+    if _ref_dot is None and all(a.dtype == in_dt and b.dtype == in_dt for a, b in pairs) \
+            and _listable([t for p in pairs for t in p], dev):
         outs = out
         if outs is None:
             outs = [torch.empty(a.shape, dtype=out_dtype, device=dev) for a, _ in pairs]
@@ -233,7 +247,7 @@ def slerp_tensors(pairs, ts, out_dtype=torch.float32, device=None, dot_threshold
         v1[s:e].copy_(b.detach().reshape(-1))
     res = torch.empty(total, dtype=out_dtype, device=dev)
     plan = _plan_for(offsets, dev)
-    ops.slerp_arena(plan, v0, v1, res, tt, dot_threshold, eps)
+    ops.slerp_arena(plan, v0, v1, res, tt, dot_threshold, eps, ref_dot=_ref_dot)
     views = [res[s:e].view(a.shape) for (a, _), s, e in zip(pairs, offsets[:-1], offsets[1:])]
     if out is None:
         return views

@@ -27,7 +27,8 @@ def outer_step(theta: torch.Tensor, workers: list[torch.Tensor], momentum: torch
     diloco.py:302-308 fused into the step, no re-read of theta per copy).
     tail_bits: torchcompat.torch_cpu_tail_bits of the reference's host (uint8 device bitmask of the
     arena): bf16 elements on torch CPU's scalar tails round add(alpha) twice, as the reference does
-    there (edt_outer_step_tail)."""
+    there (edt_outer_step_tail); with a broadcast too, the tail step runs and then each broadcast
+    buffer is copied from theta."""
     lib = L.lib()
     if not workers:
         raise L.EdtError("no workers")
@@ -38,9 +39,23 @@ def outer_step(theta: torch.Tensor, workers: list[torch.Tensor], momentum: torch
             raise L.EdtError("every worker buffer must match theta's size and share one dtype")
     if momentum is not None and (momentum.numel() != n or momentum.dtype != theta.dtype):
         raise L.EdtError("momentum must have theta's size and dtype")
+    if broadcast and any(b.numel() != n or b.dtype != workers[0].dtype for b in broadcast):
+        raise L.EdtError("broadcast buffers must match theta's size and the workers' dtype")
+    if tail_bits is not None:
+        # checked first: the tail emulation is never dropped because a broadcast was asked for
+        L.require_device(tail_bits)
+        if len(workers) > L.EDT_MAX_WORKERS:
+            raise L.EdtError("tail emulation runs in the plain fused step (<= 64 workers)")
+        if tail_bits.dtype != torch.uint8 or tail_bits.numel() * 8 < n:
+            raise L.EdtError("tail_bits: uint8 with one bit per element")
+        L.check(lib.edt_outer_step_tail(L.ptr(theta), L.dtype_code(theta), L.ptr_array(workers),
+                                        L.dtype_code(workers[0]), len(workers), L.ptr(momentum),
+                                        int(has_momentum), n, float(lr), float(momentum_coef), int(nesterov),
+                                        L.ptr(tail_bits), L.stream_ptr(theta.device)), "edt_outer_step_tail")
+        for b in broadcast or []:          # the broadcast after the step, as diloco._step_flat does
+            b.copy_(theta)
+        return
     if broadcast:
-        if any(b.numel() != n or b.dtype != workers[0].dtype for b in broadcast):
-            raise L.EdtError("broadcast buffers must match theta's size and the workers' dtype")
         if len(workers) <= L.EDT_MAX_WORKERS and len(broadcast) <= L.EDT_MAX_WORKERS:
             L.check(lib.edt_outer_step_bcast(L.ptr(theta), L.dtype_code(theta), L.ptr_array(workers),
                                              L.dtype_code(workers[0]), len(workers), L.ptr(momentum),
@@ -51,17 +66,6 @@ def outer_step(theta: torch.Tensor, workers: list[torch.Tensor], momentum: torch
         outer_step(theta, workers, momentum, has_momentum, lr, momentum_coef, nesterov)
         for b in broadcast:
             b.copy_(theta)
-        return
-    if tail_bits is not None:
-        L.require_device(tail_bits)
-        if broadcast or len(workers) > L.EDT_MAX_WORKERS:
-            raise L.EdtError("tail emulation runs in the plain fused step (<= 64 workers, no broadcast)")
-        if tail_bits.dtype != torch.uint8 or tail_bits.numel() * 8 < n:
-            raise L.EdtError("tail_bits: uint8 with one bit per element")
-        L.check(lib.edt_outer_step_tail(L.ptr(theta), L.dtype_code(theta), L.ptr_array(workers),
-                                        L.dtype_code(workers[0]), len(workers), L.ptr(momentum),
-                                        int(has_momentum), n, float(lr), float(momentum_coef), int(nesterov),
-                                        L.ptr(tail_bits), L.stream_ptr(theta.device)), "edt_outer_step_tail")
         return
     if len(workers) <= L.EDT_MAX_WORKERS:
         L.check(lib.edt_outer_step(L.ptr(theta), L.dtype_code(theta), L.ptr_array(workers),
@@ -226,12 +230,13 @@ class SlerpPlan:
     seg_offsets: list[int]
     chunks: torch.Tensor          # int64 [nchunks, 3] = start, length, segment
     seg_first: torch.Tensor       # int32 [nseg + 1]
-    partial: torch.Tensor         # float64 [nchunks, 3] workspace
+    partial: torch.Tensor         # float64 workspace: chunk rows [nchunks, 3], then the slot scratch
     coef: torch.Tensor            # float32 [nseg, 2]
     dots: torch.Tensor            # float32 [nseg]
     nchunks: int
     relative: bool = False        # chunk starts relative to their segment (tensor-list form)
     chunks_host: object = None    # numpy int64 [nchunks, 3]: the same table on the host
+    chunk_elems: int = 1 << 16
 
     @property
     def nseg(self) -> int:
@@ -259,9 +264,48 @@ def make_slerp_plan(seg_offsets: list[int], device: torch.device,
     chunks = torch.from_numpy(host).to(device)
     seg_first = torch.tensor(list(first), dtype=torch.int32).to(device)
     return SlerpPlan(list(seg_offsets), chunks, seg_first,
-                     torch.empty((max(1, nchunks), 3), dtype=torch.float64, device=device),
+                     torch.empty(max(1, int(lib.edt_slerp_sums_doubles(3, nchunks))), dtype=torch.float64,
+                                 device=device),
                      torch.empty((max(1, nseg), 2), dtype=torch.float32, device=device),
-                     torch.empty(max(1, nseg), dtype=torch.float32, device=device), nchunks, relative, host)
+                     torch.empty(max(1, nseg), dtype=torch.float32, device=device), nchunks, relative, host,
+                     int(chunk_elems))
+
+
+@dataclass(frozen=True)
+class RefDot:
+    """Reference-dot mode for the SLERP branch decision (include/edt_sync.h, edt_slerp_refdot):
+    segments whose fp64 dot lies within `band` of DOT_THRESHOLD (band < 0: every segment) take the
+    reference's own fp32 dot — BLAS sdot norms + numpy's pairwise sum, restated bit for bit for
+    the reference host's numpy / OpenBLAS (`threads` = OpenBLAS's thread count for sdot there; 1 on
+    the pinned host) — and the branch and coefficients that follow from it. Without it (the
+    default) the kernels decide from their fp64 dot, the accurate one."""
+    threads: int = 1
+    band: float = -1.0
+
+
+def _refdot_pass(plan: SlerpPlan, v0: torch.Tensor, v1: torch.Tensor, t: torch.Tensor, dot_threshold: float,
+                 eps: float, ref: RefDot) -> None:
+    """After edt_slerp_coef: flag segments, recompute their dot the reference's way, overwrite
+    their coefficients and dots (plan.coef / plan.dots)."""
+    lib = L.lib()
+    dev, st = v0.device, L.stream_ptr(v0.device)
+    need = int(lib.edt_slerp_refdot_workspace_bytes(plan.nseg, plan.nchunks, plan.chunk_elems, int(ref.threads)))
+    if need == 0:
+        raise L.EdtError(f"reference-dot mode needs chunks of a multiple of 8192 elements (plan: {plan.chunk_elems})")
+    ws = getattr(plan, "_refdot_ws", None)
+    if ws is None or ws.numel() * 8 < need:
+        ws = plan._refdot_ws = torch.empty((need + 7) // 8, dtype=torch.float64, device=dev)
+        plan._refdot_flag = torch.empty(max(1, plan.nseg), dtype=torch.int32, device=dev)
+        plan._refdot_val = torch.empty(max(1, plan.nseg), dtype=torch.float32, device=dev)
+    L.check(lib.edt_slerp_refdot_flags(L.ptr(plan.dots), plan.nseg, float(dot_threshold), float(ref.band),
+                                       L.ptr(plan._refdot_flag), st), "edt_slerp_refdot_flags")
+    L.check(lib.edt_slerp_refdot(L.ptr(v0), L.ptr(v1), L.dtype_code(v0), L.ptr(plan.chunks), plan.nchunks,
+                                 L.ptr(plan.seg_first), plan.nseg, plan.chunk_elems, L.ptr(plan._refdot_flag),
+                                 int(ref.threads), float(eps), L.ptr(plan._refdot_val), L.ptr(ws), ws.numel() * 8, st),
+            "edt_slerp_refdot")
+    L.check(lib.edt_slerp_refdot_coef(L.ptr(plan._refdot_val), L.ptr(plan._refdot_flag), plan.nseg, L.ptr(t),
+                                      float(dot_threshold), L.ptr(plan.coef), L.ptr(plan.dots), st),
+            "edt_slerp_refdot_coef")
 
 
 def _speculation_pays(plan: SlerpPlan, in_bytes: int, out_bytes: int) -> bool:
@@ -286,13 +330,14 @@ def _overlap(a: torch.Tensor, b: torch.Tensor) -> bool:
 
 def slerp_arena(plan: SlerpPlan, v0: torch.Tensor, v1: torch.Tensor, out: torch.Tensor,
                 t: torch.Tensor, dot_threshold: float = 0.9995, eps: float = 1e-8,
-                speculate: bool | None = None) -> None:
+                speculate: bool | None = None, ref_dot: RefDot | None = None) -> None:
     """SLERP every segment of v0/v1 with its own t (float64 device tensor [nseg]) into out
     (EDT_RL/crossover.py:11-43): chunk sums, per-segment coefficients, blend (edt_slerp_merge).
     speculate: True = edt_slerp_merge_speculative (lerp-branch output written in the stats pass,
     only SLERP-branch segments blended again); False = the two-pass form; None = whichever the
     previous merge on this plan says is cheaper. Bit-identical results either way; an output
-    that overlaps a parent always takes the two-pass form."""
+    that overlaps a parent always takes the two-pass form. ref_dot (RefDot): the reference-dot
+    mode, always the split two-pass form: stats -> coef -> refdot -> blend."""
     lib = L.lib()
     L.require_device(v0, v1, out, t)
     if v1.dtype != v0.dtype or v0.numel() != plan.seg_offsets[-1] or v1.numel() != v0.numel() \
@@ -302,6 +347,18 @@ def slerp_arena(plan: SlerpPlan, v0: torch.Tensor, v1: torch.Tensor, out: torch.
         raise L.EdtError("t must be a float64 device tensor with one value per segment")
     if plan.relative:
         raise L.EdtError("a relative (tensor-list) plan drives slerp_list, not slerp_arena")
+    if ref_dot is not None:
+        st = L.stream_ptr(v0.device)
+        L.check(lib.edt_slerp_stats(L.ptr(v0), L.ptr(v1), L.dtype_code(v0), L.ptr(plan.chunks), plan.nchunks,
+                                    L.ptr(plan.partial), st), "edt_slerp_stats")
+        L.check(lib.edt_slerp_coef(L.ptr(plan.partial), L.ptr(plan.seg_first), plan.nseg, L.ptr(t),
+                                   float(dot_threshold), float(eps), L.ptr(plan.coef), L.ptr(plan.dots), st),
+                "edt_slerp_coef")
+        _refdot_pass(plan, v0, v1, t, dot_threshold, eps, ref_dot)
+        L.check(lib.edt_slerp_blend(L.ptr(v0), L.ptr(v1), L.dtype_code(v0), L.ptr(out), L.dtype_code(out),
+                                    L.ptr(plan.chunks), plan.nchunks, L.ptr(plan.coef), st), "edt_slerp_blend")
+        plan._last_thr = float(dot_threshold)
+        return
     if speculate is None:
         speculate = _speculation_pays(plan, v0.element_size(), out.element_size())
     if speculate and (_overlap(out, v0) or _overlap(out, v1)):
@@ -465,19 +522,28 @@ def pair_merge_population(children, lr: float, momentum_coef: float, nesterov: b
 def slerp_gram(members: list[torch.Tensor], chunks: torch.Tensor, nchunks: int,
                gram: torch.Tensor | None = None) -> torch.Tensor:
     """Per-chunk Gram sums of M <= 8 member buffers over a chunk table (int64 [nchunks, 3] on the
-    device, starts relative to the buffers): float64 [nchunks, M(M+1)/2] (edt_slerp_gram)."""
+    device, starts relative to the buffers): float64 [nchunks, M(M+1)/2] (edt_slerp_gram). `gram`
+    (optional) receives the rows; its first nchunks x M(M+1)/2 elements are written."""
     lib = L.lib()
     M = len(members)
     L.require_device(*members, chunks)
     if not 1 <= M <= 8 or any(m.dtype != members[0].dtype for m in members):
         raise L.EdtError("slerp_gram: 1..8 members of one dtype")
     NT = M * (M + 1) // 2
-    if gram is None:
-        gram = torch.empty((max(1, nchunks), NT), dtype=torch.float64, device=members[0].device)
-    elif gram.dtype != torch.float64 or gram.numel() < nchunks * NT:
+    need = max(1, int(lib.edt_slerp_population_gram_doubles(M, nchunks)))
+    if gram is not None and (gram.dtype != torch.float64 or gram.numel() < nchunks * NT):
         raise L.EdtError("gram: float64 with nchunks x M(M+1)/2 elements")
+    # the kernel needs the rows plus its slot scratch behind them; a smaller (or non-contiguous)
+    # `gram` — e.g. a rank's rows of the whole table — gets its rows copied from a full-size buffer
+    direct = gram is not None and gram.is_contiguous() and gram.numel() >= need
+    work = gram if direct else torch.empty(need, dtype=torch.float64, device=members[0].device)
     L.check(lib.edt_slerp_gram(L.ptr_array(members), M, L.dtype_code(members[0]), L.ptr(chunks), nchunks,
-                               L.ptr(gram), L.stream_ptr(members[0].device)), "edt_slerp_gram")
+                               L.ptr(work), L.stream_ptr(members[0].device)), "edt_slerp_gram")
+    rows = work.view(-1)[:nchunks * NT].view(nchunks, NT) if not direct else gram
+    if gram is None:
+        return rows
+    if not direct:
+        gram.view(-1)[:nchunks * NT].copy_(rows.view(-1))
     return gram
 
 

@@ -177,6 +177,14 @@ int64_t edt_slerp_make_chunks(const uint64_t* seg_offsets_host, int nseg, uint32
                               uint64_t* chunk_desc_host, int64_t max_chunks,
                               int32_t* seg_first_chunk_host);
 
+/* Chunk-sum tables. Every chunk's fp64 sums are formed in one canonical order by wave slots with
+ * no workgroup barrier (edt_slerp.hip): a table of W sums per chunk therefore needs
+ * edt_slerp_sums_doubles(W, nchunks) doubles — the chunk rows [nchunks][W] first (what the
+ * coefficient passes read and what a caller may copy or all-gather), then the slot scratch the
+ * sum pass fills and folds into the rows. Every `partial` of the pair forms below holds
+ * edt_slerp_sums_doubles(3, nchunks) doubles. */
+uint64_t edt_slerp_sums_doubles(int width, int64_t nchunks);
+
 /* Pass 1: per-chunk sums  partial[c] = { sum v0^2, sum v1^2, sum v0*v1 }  (fp64). */
 int edt_slerp_stats(const void* v0, const void* v1, int in_dt, const uint64_t* chunk_desc,
                     int64_t nchunks, double* partial, void* stream);
@@ -262,6 +270,32 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
                                      double dot_threshold, double eps, double* partial, float* coef,
                                      float* dot_out, int32_t* redo, uint64_t n, void* stream);
 
+/* ---- reference-dot mode (opt-in; EDT_RL/crossover.py:20-31 on the reference host) -------------
+ * The default coefficients come from an fp64 dot of the chunk sums (within ~3e-7 of the true
+ * cosine). The reference decides its branch from an fp32 dot whose error grows with the tensor
+ * (BLAS sdot norms, then numpy's pairwise sum of the normalised products), so near
+ * DOT_THRESHOLD the two can take different branches. This mode recomputes, for the flagged
+ * segments, the reference's own fp32 dot bit for bit (restated and pinned in oracle/edt_oracle.c:
+ * numpy 2.2 with OpenBLAS 0.3.29's SkylakeX sdot; `threads` = OpenBLAS's thread count for sdot
+ * on the reference host, 1 on the pinned host) and the coefficients from it:
+ *   edt_slerp_refdot_flags  flag[s] = 1 where | |dots[s]| - dot_threshold | <= band (band < 0: all)
+ *   edt_slerp_refdot        ref_dot[s] for every flagged segment (flag NULL: all); chunks of the
+ *                           plan (chunk_elems, a multiple of 8192); workspace (device, 8-byte
+ *                           aligned): edt_slerp_refdot_workspace_bytes(...)
+ *   edt_slerp_refdot_coef   coef / dot_out of the flagged segments from ref_dot (the branch and the
+ *                           fp32 SLERP coefficients of edt_slerp_coef)
+ * Order: edt_slerp_stats -> edt_slerp_coef -> flags -> refdot -> refdot_coef -> edt_slerp_blend.
+ * The norms are sequential FMA chains by definition (one workgroup per segment and BLAS thread):
+ * a parity mode, tens of ms for a 545M-element tensor. */
+uint64_t edt_slerp_refdot_workspace_bytes(int nseg, int64_t nchunks, uint32_t chunk_elems, int threads);
+int edt_slerp_refdot_flags(const float* dots, int nseg, double dot_threshold, double band, int32_t* flag,
+                           void* stream);
+int edt_slerp_refdot(const void* v0, const void* v1, int in_dt, const uint64_t* chunk_desc, int64_t nchunks,
+                     const int32_t* seg_first_chunk, int nseg, uint32_t chunk_elems, const int32_t* flag, int threads,
+                     double eps, float* ref_dot, void* workspace, uint64_t workspace_bytes, void* stream);
+int edt_slerp_refdot_coef(const float* ref_dot, const int32_t* flag, int nseg, const double* t, double dot_threshold,
+                          float* coef, float* dot_out, void* stream);
+
 /* ---- the population SLERP's passes, separately (link-balanced sharded population) ----------
  * edt_slerp_population = edt_slerp_gram + edt_slerp_gram_coef + edt_slerp_blend_children. Split
  * so that the Gram sums of a rank's range of whole chunks (its parameter-index shard of all M
@@ -269,6 +303,7 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
  * the coefficients: each chunk's sums are formed by the same kernel in the same order wherever
  * the chunk lives, so the coefficients — and every child — equal edt_slerp_merge's bit for bit.
  *   edt_slerp_gram        gram[c * NT + tri(a, b)], NT = M(M+1)/2, for the chunks of chunk_desc
+ *                         (gram: edt_slerp_population_gram_doubles(M, nchunks) doubles, rows first)
  *                         (starts relative to the member buffers); M <= 8.
  *   edt_slerp_gram_coef   per child q = (pairs[2q], pairs[2q+1]) (member indices), per segment of
  *                         the whole layout (seg_first_chunk indexes gram's rows): coef[q][nseg][2],

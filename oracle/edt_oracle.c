@@ -28,6 +28,7 @@
  */
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 enum { OR_F32 = 0, OR_BF16 = 1 };
@@ -229,4 +230,122 @@ int oracle_max_threads(void) {
 #else
     return 1;
 #endif
+}
+
+/* ---- the reference's SLERP dot (EDT_RL/crossover.py:20-29), restated bit for bit ------------
+ * dot = np.sum(normalize(v0) * normalize(v1)) on float32 arrays, normalize(v) = v / ||v|| when
+ * ||v|| > eps (:57-61), ||v|| = np.linalg.norm = sqrt(v.ravel().dot(v.ravel())):
+ *   * v.dot(v) is BLAS sdot. numpy 2.2's wheel bundles OpenBLAS 0.3.29 (scipy-openblas, DYNAMIC_ARCH),
+ *     which on this host runs its SkylakeX kernel (threadpoolctl: architecture "SkylakeX"): for the
+ *     first n1 = n & -32 elements, 4 x 16 fp32 lanes accumulate with FMA over 64-element blocks
+ *     (lane L takes elements 64k + L), fold to 4 x 8 lanes (acc[L] + acc[L + 8] per zmm), the
+ *     32-element remainder block (if any) into those with FMA, then ((a0 + a1) + a2) + a3 per lane,
+ *     the two 128-bit halves added and two hadds; the n - n1 tail elements are added one by one
+ *     as fp32 products into a double accumulator, and the result is returned as float. With
+ *     `threads` > 1 the vector is cut into OpenBLAS's level-1 chunks (ceil(rest / threads left))
+ *     and the chunk results are added in order in double, rounding to float after each add.
+ *     Pinned on this host (tests/test_refdot_cpu.py): threads = 1 at every size tested (up to 67M
+ *     elements) reproduces x.dot(x) bit for bit; threads > 1 is the library's published split,
+ *     unpinned here.
+ *   * np.sum over a contiguous float32 array: the ufunc reduction walks it in buffers of 8192
+ *     elements; each buffer is summed pairwise (numpy's pairwise_sum: blocks of <= 128 with 8
+ *     accumulators, else halves cut at a multiple of 8) and added to a float running sum that
+ *     starts at 0 (the add identity). Pinned the same way.
+ * The reference's threshold test `np.abs(dot) > 0.9995` compares in float32 (NEP 50). */
+static float sdot_k16(int64_t n, const float* x, const float* y) {
+    float a5[4][16], a[4][8];
+    memset(a5, 0, sizeof(a5));
+    int64_t i = 0;
+    const int64_t n64 = n & ~(int64_t)63;
+    for (; i < n64; i += 64)
+        for (int j = 0; j < 4; ++j)
+            for (int l = 0; l < 16; ++l) a5[j][l] = fmaf(x[i + 16 * j + l], y[i + 16 * j + l], a5[j][l]);
+    for (int j = 0; j < 4; ++j)
+        for (int l = 0; l < 8; ++l) a[j][l] = a5[j][l] + a5[j][l + 8];
+    for (; i < n; i += 32)
+        for (int j = 0; j < 4; ++j)
+            for (int l = 0; l < 8; ++l) a[j][l] = fmaf(x[i + 8 * j + l], y[i + 8 * j + l], a[j][l]);
+    float s[8], h[4];
+    for (int l = 0; l < 8; ++l) s[l] = ((a[0][l] + a[1][l]) + a[2][l]) + a[3][l];
+    for (int l = 0; l < 4; ++l) h[l] = s[l] + s[l + 4];
+    return (h[0] + h[1]) + (h[2] + h[3]);
+}
+
+static double sdot_chunk(int64_t n, const float* x, const float* y) {
+    const int64_t n1 = n & ~(int64_t)31;
+    double d = n1 ? (double)sdot_k16(n1, x, y) : 0.0;
+    for (int64_t i = n1; i < n; ++i) d += (double)(y[i] * x[i]);
+    return d;
+}
+
+float oracle_ref_sdot(const float* x, const float* y, int64_t n, int threads) {
+    if (n <= 0) return 0.f;
+    if (threads <= 1) return (float)sdot_chunk(n, x, y);
+    float dot = 0.f;
+    int64_t rest = n, off = 0;
+    for (int c = 0; rest > 0; ++c) {
+        int64_t w = (rest + threads - c - 1) / (threads - c);
+        if (w > rest) w = rest;
+        dot = (float)((double)dot + sdot_chunk(w, x + off, y + off));
+        rest -= w;
+        off += w;
+    }
+    return dot;
+}
+
+static float np_pairwise(const float* a, int64_t n) {
+    if (n < 8) {
+        float r = 0.f;
+        for (int64_t i = 0; i < n; ++i) r += a[i];
+        return r;
+    }
+    if (n <= 128) {
+        float r[8];
+        for (int j = 0; j < 8; ++j) r[j] = a[j];
+        int64_t i;
+        for (i = 8; i < n - (n % 8); i += 8)
+            for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+        float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < n; ++i) res += a[i];
+        return res;
+    }
+    int64_t n2 = n / 2;
+    n2 -= n2 % 8;
+    return np_pairwise(a, n2) + np_pairwise(a + n2, n - n2);
+}
+
+float oracle_np_sum_f32(const float* a, int64_t n) {
+    float r = 0.f;
+    for (int64_t o = 0; o < n; o += 8192) r += np_pairwise(a + o, n - o < 8192 ? n - o : 8192);
+    return r;
+}
+
+/* The whole dot of EDT_RL/crossover.py:20-29 for inputs of dtype dt (bf16 widened to fp32 first,
+ * as `.float().numpy()`); also returns the two fp32 norms. */
+int oracle_ref_slerp_dot(const void* v0, const void* v1, int dt, int64_t n, int threads, float eps, float* dot,
+                         float* norm0, float* norm1) {
+    float* a = (float*)malloc(sizeof(float) * (size_t)(n > 0 ? n : 1));
+    float* b = (float*)malloc(sizeof(float) * (size_t)(n > 0 ? n : 1));
+    if (!a || !b) {
+        free(a);
+        free(b);
+        return -1;
+    }
+    for (int64_t i = 0; i < n; ++i) {
+        a[i] = load(v0, dt, (uint64_t)i);
+        b[i] = load(v1, dt, (uint64_t)i);
+    }
+    const float n0 = sqrtf(oracle_ref_sdot(a, a, n, threads));
+    const float n1 = sqrtf(oracle_ref_sdot(b, b, n, threads));
+    for (int64_t i = 0; i < n; ++i) {
+        const float x = n0 > eps ? a[i] / n0 : a[i];
+        const float y = n1 > eps ? b[i] / n1 : b[i];
+        a[i] = x * y;
+    }
+    *dot = oracle_np_sum_f32(a, n);
+    if (norm0) *norm0 = n0;
+    if (norm1) *norm1 = n1;
+    free(a);
+    free(b);
+    return 0;
 }

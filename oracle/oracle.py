@@ -50,8 +50,15 @@ def lib() -> ctypes.CDLL:
         l.oracle_delta_partial.argtypes = [_P, _I, ctypes.POINTER(_P), _I, _I, _I, _U64, _P, _I]
         l.oracle_sgd_apply.argtypes = [_P, _I, _P, _P, _I, _U64, _D, _D, _I]
         l.oracle_max_threads.argtypes = []
+        l.oracle_ref_sdot.argtypes = [_P, _P, ctypes.c_int64, _I]
+        l.oracle_ref_sdot.restype = ctypes.c_float
+        l.oracle_np_sum_f32.argtypes = [_P, ctypes.c_int64]
+        l.oracle_np_sum_f32.restype = ctypes.c_float
+        l.oracle_ref_slerp_dot.argtypes = [_P, _P, _I, ctypes.c_int64, _I, ctypes.c_float,
+                                           ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
+                                           ctypes.POINTER(ctypes.c_float)]
         for f in (l.oracle_outer_step, l.oracle_pair_merge, l.oracle_lerp, l.oracle_max_threads,
-                  l.oracle_delta_partial, l.oracle_sgd_apply):
+                  l.oracle_delta_partial, l.oracle_sgd_apply, l.oracle_ref_slerp_dot):
             f.restype = _I
         _lib = l
     return _lib
@@ -169,6 +176,30 @@ def slerp_parts(t: float, v0, v1, dot_threshold: float = 0.9995, eps: float = 1e
     s0 = np.sin(th0 - th_t) / np.sin(th0)
     s1 = np.sin(th_t) / np.sin(th0)
     return s0 * a + s1 * b, dot, False
+
+
+def ref_sdot(x: np.ndarray, y: np.ndarray, threads: int = 1) -> np.float32:
+    """BLAS sdot as the reference host's numpy runs it (edt_oracle.c: OpenBLAS 0.3.29 SkylakeX)."""
+    x = np.ascontiguousarray(x, dtype=np.float32).ravel()
+    y = np.ascontiguousarray(y, dtype=np.float32).ravel()
+    return np.float32(lib().oracle_ref_sdot(x.ctypes.data, y.ctypes.data, x.size, threads))
+
+
+def np_sum_f32(a: np.ndarray) -> np.float32:
+    """np.sum of a contiguous float32 array (8192-element buffers, pairwise inside), restated."""
+    a = np.ascontiguousarray(a, dtype=np.float32).ravel()
+    return np.float32(lib().oracle_np_sum_f32(a.ctypes.data, a.size))
+
+
+def ref_slerp_dot(v0, v1, threads: int = 1, eps: float = 1e-8):
+    """(dot, norm0, norm1) of EDT_RL/crossover.py:20-29 from the restatement (no numpy reduction):
+    what the reference's own numpy computes on a host with this BLAS model."""
+    a, b = _cpu(torch.as_tensor(v0)).reshape(-1), _cpu(torch.as_tensor(v1)).reshape(-1)
+    d, n0, n1 = ctypes.c_float(), ctypes.c_float(), ctypes.c_float()
+    rc = lib().oracle_ref_slerp_dot(a.data_ptr(), b.data_ptr(), _DT[a.dtype], a.numel(), threads, eps,
+                                    ctypes.byref(d), ctypes.byref(n0), ctypes.byref(n1))
+    assert rc == 0, rc
+    return np.float32(d.value), np.float32(n0.value), np.float32(n1.value)
 
 
 def slerp(t: float, v0, v1, dot_threshold: float = 0.9995, eps: float = 1e-8) -> torch.Tensor:

@@ -1,0 +1,38 @@
+"""Build-time variants of the chunk-sum passes (edt_slerp.hip wave slots) into variants_slerp/,
+for scripts/slerp_spec_probe.py --variants variants_slerp (timed beside the in-tree library).
+
+    python scripts/build_slerp_variants.py [name ...]
+"""
+import os
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+OUT = os.path.join(ROOT, "variants_slerp")
+
+VARIANTS = {
+    "it1": ["-DEDT_SLERP_WAVE_ITERS=1"],
+    "it2": ["-DEDT_SLERP_WAVE_ITERS=2"],
+    "it8": ["-DEDT_SLERP_WAVE_ITERS=8"],
+    "it4_bpc16": ["-DEDT_SLERP_SUMS_BPC=16"],
+    "it4_bpc64": ["-DEDT_SLERP_SUMS_BPC=64"],
+    "it4_nont": ["-DEDT_NT_SLERP=0"],
+}
+
+
+def main():
+    from evolutionarydistributedtraining_amd.build import build_library
+    names = sys.argv[1:] or list(VARIANTS)
+    os.makedirs(OUT, exist_ok=True)
+    for f in os.listdir(OUT):
+        if f.endswith(".so") and f[3:-3] not in names:
+            os.remove(os.path.join(OUT, f))
+    with ThreadPoolExecutor(3) as ex:
+        list(ex.map(lambda n: build_library(force=True, extra_flags=VARIANTS[n], out=os.path.join(OUT, f"lib{n}.so")),
+                    names))
+    print("built", names)
+
+
+if __name__ == "__main__":
+    main()

@@ -24,3 +24,19 @@ def oracle():
     from oracle import oracle as o
     o.build()
     return o
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _release_device_memory():
+    """After each test module: collect cycles and hand the caching allocator's blocks back, so a
+    module that filled HBM (the 7B populations) cannot starve the next one."""
+    yield
+    import gc
+    gc.collect()
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+    except Exception:       # noqa: BLE001 - best effort, never fails a test
+        pass

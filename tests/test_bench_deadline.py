@@ -1,6 +1,7 @@
 """bench.py's multi-GPU safety net (ExtrasDeadline): the line is printed exactly once, by rank 0,
 with the value and every extra that finished, whether the extras complete or hang past the
-deadline; other ranks print nothing; the deadline makes every rank exit."""
+deadline; other ranks print nothing; the deadline makes every rank exit with a non-zero status
+(a hang must read as a failed run)."""
 import io
 import json
 import os
@@ -22,9 +23,10 @@ def _line(buf):
 
 def test_deadline_fires_once_with_the_value_and_finished_extras():
     out = {"value": 123.0, "cpu_baseline": {"value": 1.0}, "weak_scaling": {"ms_per_step": 2.0}}
-    buf, exited = io.StringIO(), threading.Event()
-    d = bench.ExtrasDeadline(0.2, 0, out, buf, exit_fn=lambda code: exited.set())
+    buf, exited, codes = io.StringIO(), threading.Event(), []
+    d = bench.ExtrasDeadline(0.2, 0, out, buf, exit_fn=lambda code: (codes.append(code), exited.set()))
     assert exited.wait(5)
+    assert codes == [3]
     line = _line(buf)
     assert line["value"] == 123.0 and line["weak_scaling"] == {"ms_per_step": 2.0}
     assert line["extras_deadline"]["unfinished_or_skipped"] == ["other_schedules", "baseline_configs",
@@ -47,9 +49,10 @@ def test_extras_in_time_print_one_line_and_cancel():
 
 
 def test_other_ranks_never_print_but_exit_on_the_deadline():
-    buf, exited = io.StringIO(), threading.Event()
-    d = bench.ExtrasDeadline(0.1, 3, None, buf, exit_fn=lambda code: exited.set())
+    buf, exited, codes = io.StringIO(), threading.Event(), []
+    d = bench.ExtrasDeadline(0.1, 3, None, buf, exit_fn=lambda code: (codes.append(code), exited.set()))
     assert exited.wait(5)
+    assert codes == [3]
     assert d.emit() is False and buf.getvalue() == ""
 
 

@@ -156,3 +156,38 @@ def test_sharded_slerp_population_fuzz(oracle, world, groups, shapes, seed):
     for c in range(world):
         assert torch.equal(res[c][0].view(torch.int32), want[c].view(torch.int32)), c
         assert torch.equal(res[c][1], wdots)
+
+
+def _pm_dtypes(comm, layout, members, pairs, oracle, mom_dt, out_mom_dt, no_mom_rank):
+    from evolutionarydistributedtraining_amd.distributed import ShardedPopulationCrossover
+    from tests.oracle_kernels import ChunkGramKernels
+    r = comm.rank
+    sp = ShardedPopulationCrossover(layout, torch.bfloat16, "cpu", kind="sgd", comm=comm,
+                                    kernels=ChunkGramKernels(oracle), chunk_elems=CHUNK)
+    g = torch.Generator().manual_seed(60 + r)
+    trained = (members[r].float() + torch.randn(layout.total, generator=g) * 1e-3).bfloat16()
+    mom = (torch.randn(layout.total, generator=g) * 1e-3).to(mom_dt[r])
+    out = torch.empty(layout.total, dtype=torch.bfloat16)
+    out_m = torch.empty(layout.total, dtype=out_mom_dt[r])
+    try:
+        sp.pair_merge_step(members[r], trained, None if r == no_mom_rank else mom, pairs, out, out_m, generation=1)
+    except Exception as e:          # noqa: BLE001 - the refusal is the result
+        return type(e).__name__
+    return "ok"
+
+
+def test_sharded_pair_merge_momentum_dtype_mismatch_refused_on_every_rank(oracle):
+    """A momentum dtype that differs across ranks (or from the children's) would post p2p sends and
+    receives of different byte counts (a hang under RCCL): every rank refuses it before any
+    exchange, including the rank whose own buffers agree."""
+    world = 2
+    layout = ParamLayout(SHAPES)
+    members = _members(world, layout.total)
+    pairs = _pairs(world)
+    f32, bf = torch.float32, torch.bfloat16
+    res = VirtualWorld(world).run(lambda comm: _pm_dtypes(comm, layout, members, pairs, oracle,
+                                                          [bf, f32], [bf, f32], 0))
+    assert res == ["EdtError", "EdtError"], res
+    res = VirtualWorld(world).run(lambda comm: _pm_dtypes(comm, layout, members, pairs, oracle,
+                                                          [bf, bf], [bf, bf], 0))
+    assert res == ["ok", "ok"], res
