@@ -67,7 +67,7 @@ XGMI_LINK_GBPS = 153.6 / 2    # per xGMI link and direction (153.6 GB/s both way
 DT = {"f32": torch.float32, "bf16": torch.bfloat16}
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
@@ -121,7 +121,49 @@ def parse():
                    help="multi-GPU path: seconds allowed for everything after the value (companions, other "
                         "schedules, BASELINE configs, population); past it rank 0 prints the line with what "
                         "it has and every rank exits (0: no deadline)")
-    return p.parse_args()
+    p.add_argument("--config-layouts", default="configs2_125m_fp32=gpt2_small:f32,configs3_1p3b_bf16=gpt_1p3b:bf16",
+                   help="N>1 baseline_configs: key=layout:dtype,... (BASELINE configs[2] and [3])")
+    p.add_argument("--population-layout", default="qwen2p5_7b_body",
+                   help="N>1 population_slerp_7b: the member layout (BASELINE configs[4]: the 7.07B body)")
+    return p.parse_args(argv)
+
+
+class _HostEvent:
+    """A host-clock stand-in for a timing event (the CPU rehearsal of the N > 1 line)."""
+
+    def record(self, stream=None):
+        self.t = time.perf_counter()
+
+    def elapsed_time(self, other) -> float:
+        return (other.t - self.t) * 1e3
+
+
+class Runtime:
+    """The device plumbing of the timed loops: a HIP device (streams, HIP events, the caching
+    allocator), or the host (tests/test_bench_rehearsal.py runs the whole N > 1 line on gloo with
+    CPU stand-in kernels, so the driver's first 8-GPU run meets no untried host code)."""
+
+    def __init__(self, dev):
+        self.dev = torch.device(dev)
+        self.gpu = self.dev.type == "cuda"
+
+    def sync(self):
+        if self.gpu:
+            torch.cuda.synchronize(self.dev)
+
+    def event(self):
+        return torch.cuda.Event(enable_timing=True) if self.gpu else _HostEvent()
+
+    def empty_cache(self):
+        if self.gpu:
+            torch.cuda.empty_cache()
+
+    def device_info(self) -> dict:
+        if not self.gpu:
+            return {"name": "host (rehearsal)", "arch": "cpu", "cus": os.cpu_count(), "hbm_gib": None}
+        prop = torch.cuda.get_device_properties(self.dev)
+        return {"name": prop.name, "arch": getattr(prop, "gcnArchName", ""),
+                "cus": prop.multi_processor_count, "hbm_gib": round(prop.total_memory / 2**30, 1)}
 
 
 class ExtrasDeadline:
@@ -248,6 +290,22 @@ def synth_population(theta: torch.Tensor, workers: list[torch.Tensor], seed: int
             w[a:b].copy_(t + torch.randn(b - a, generator=g, device=theta.device) * 1e-3)
 
 
+def synth_sharded(theta: torch.Tensor, workers: list[torch.Tensor], rank: int) -> None:
+    """The N > 1 population: theta from one seed on every rank (the replicas agree without a
+    broadcast), this rank's workers = theta + N(0, 1e-3^2) from a per-rank seed."""
+    dev = theta.device
+    gt = torch.Generator(device=dev).manual_seed(1234)
+    gw = torch.Generator(device=dev).manual_seed(4321 + 7919 * rank)
+    chunk = 1 << 26
+    n = theta.numel()
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        t = torch.randn(b - a, generator=gt, device=dev) * 0.02
+        theta[a:b].copy_(t)
+        for w in workers:
+            w[a:b].copy_(t + torch.randn(b - a, generator=gw, device=dev) * 1e-3)
+
+
 def cpu_baseline(args, theta_dtype, worker_dtype, k):
     """The reference's outer step as it runs on its master's CPU — EDT_LM/diloco.py:238-289's
     per-tensor torch loop + torch.optim.SGD, restated in oracle.torch_loop_outer_step — over one
@@ -346,13 +404,29 @@ def _event_ms(fn, steps, warmup):
     return sum(ts) / len(ts)
 
 
-def _pmc_traffic(args, key):
-    """HBM bytes per launch from the committed PMC summary (scripts/profile_pmc_ops.sh), or None."""
+def _pmc_traffic(args, key, with_note=False):
+    """HBM bytes per launch from the committed PMC summary (scripts/profile_pmc.sh,
+    scripts/profile_pmc_ops.sh), or None. An entry counts only when its `lib_sha256` stamp is the
+    library loaded in this process: counters measured on other kernels are never carried into the
+    line (the reason is returned beside it with with_note=True)."""
+    from evolutionarydistributedtraining_amd import _lib as L
+    value, note = None, None
     try:
         with open(args.traffic_json) as f:
-            return json.load(f).get(key, {}).get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        return None
+            entry = json.load(f).get(key)
+    except (OSError, ValueError) as e:
+        entry, note = None, f"no PMC summary ({type(e).__name__})"
+    if entry is not None:
+        stamp, here = entry.get("lib_sha256"), L.library_sha256()
+        if stamp and stamp == here:
+            value = entry.get("hbm_bytes_per_launch")
+            note = f"PMC passes on this build (lib_sha256 {here[:12]}), {os.path.basename(args.traffic_json)}"
+        else:
+            note = (f"stale: the PMC entry was measured on build {str(stamp)[:12]}, this process loaded "
+                    f"{str(here)[:12]}; re-collect with scripts/profile_pmc*.sh")
+    elif note is None:
+        note = f"no PMC entry for {key}"
+    return (value, note) if with_note else value
 
 
 def bench_config1(args, dev):
@@ -412,7 +486,8 @@ def bench_pair_merge(args, dev):
            "kernel": "pair_kernel (edt_pair_merge_to)", "ms": round(ms, 4),
            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                         "frac": round(gbs / HBM_PEAK_GBPS, 4), "bytes_per_elem": bpe, "algo_bytes_per_launch": bpe * P,
-                        "traffic": _pmc_traffic(args, "pair_merge/gpt_1p3b/bf16")}}
+                        "traffic": _pmc_traffic(args, "pair_merge/gpt_1p3b/bf16"),
+                        "traffic_source": _pmc_traffic(args, "pair_merge/gpt_1p3b/bf16", with_note=True)[1]}}
     if args.ops_cpu_seconds > 0:
         n = args.cpu_sample_elems
         gc = torch.Generator().manual_seed(3)
@@ -470,7 +545,8 @@ def bench_slerp_7b(args, dev):
                                      # the form's own bytes (two-pass: both parents read twice)
                                      # over the time: its streaming rate against the same peak
                                      "moved_frac": round((6 if spec else 10) * P / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
-                                     "traffic": _pmc_traffic(args, f"slerp_7b/{parents}")}}
+                                     "traffic": _pmc_traffic(args, f"slerp_7b/{parents}"),
+                                     "traffic_source": _pmc_traffic(args, f"slerp_7b/{parents}", with_note=True)[1]}}
     del v0, v1, out, plan
     torch.cuda.empty_cache()
     if args.ops_cpu_seconds > 0:
@@ -493,17 +569,18 @@ def bench_slerp_7b(args, dev):
     return res
 
 
-def bench_population(args, dev, comm, layout_name="qwen2p5_7b_body"):
+def bench_population(args, rt, comm, kernels=None, layout_name="qwen2p5_7b_body"):
     """BASELINE configs[4] at N > 1: a population of N members (one 7.07B bf16 body per GPU,
     qwen2p5_7b_body) SLERP-crossed into N children (t = 0.5, far parents: the SLERP branch), timed
     link-balanced (distributed.ShardedPopulationCrossover: chunk-range shards of every member,
     Gram rows all-gathered, children gathered back), the same with its exchanges pipelined over
     chunk groups (`sharded_pipelined`), and per child (PopulationCrossover: each child's two parents
-    shipped whole). Max over ranks; every rank of `comm` takes part."""
+    shipped whole). Max over ranks; every rank of `comm` takes part. `kernels`: the product ops
+    (default) or a host stand-in (the CPU rehearsal)."""
     from evolutionarydistributedtraining_amd.distributed import PopulationCrossover, ShardedPopulationCrossover
     from evolutionarydistributedtraining_amd.layouts import LAYOUTS
     lay = LAYOUTS[layout_name]()
-    rank, world = comm.rank, comm.world
+    rank, world, dev = comm.rank, comm.world, rt.dev
     P, bf = lay.total, torch.bfloat16
     g = torch.Generator(device=dev).manual_seed(100 + rank)
     member = torch.empty(P, dtype=bf, device=dev)
@@ -519,12 +596,12 @@ def bench_population(args, dev, comm, layout_name="qwen2p5_7b_body"):
     def timed(step, n):
         for _ in range(2):
             step()
-        torch.cuda.synchronize()
+        rt.sync()
         comm.barrier()
         t0 = time.perf_counter()
         for _ in range(n):
             step()
-        torch.cuda.synchronize()
+        rt.sync()
         comm.barrier()
         return max(comm.all_gather_object((time.perf_counter() - t0) / n * 1e3))
     wire = 2 * (world - 1) * (P * 2 // world)            # members out + children out, per rank
@@ -532,17 +609,17 @@ def bench_population(args, dev, comm, layout_name="qwen2p5_7b_body"):
     for key, groups in (("sharded", 1), ("sharded_pipelined", args.population_groups)):
         if groups < 1 or (key == "sharded_pipelined" and groups == 1):
             continue
-        sp = ShardedPopulationCrossover(lay, bf, dev, kind="slerp", comm=comm, groups=groups)
+        sp = ShardedPopulationCrossover(lay, bf, dev, kind="slerp", comm=comm, groups=groups, kernels=kernels)
         ms = timed(lambda: sp.slerp_step(member, pairs, t, out), max(3, args.steps // 4))
         res[key] = {"ms": round(ms, 3), "groups": groups, "wire_bytes_per_rank": wire,
                     "xgmi": {"achieved": round(wire / (ms / 1e3) / 1e9, 1), "peak": peak, "unit": "GB/s",
-                             "frac": round(wire / (ms / 1e3) / 1e9 / peak, 4)}}
+                             "frac": round(wire / (ms / 1e3) / 1e9 / peak, 4) if peak else None}}
         del sp
-        torch.cuda.empty_cache()
-    pc = PopulationCrossover(lay, bf, dev, comm=comm)
+        rt.empty_cache()
+    pc = PopulationCrossover(lay, bf, dev, comm=comm, kernels=kernels)
     res["per_child"] = {"ms": round(timed(lambda: pc.slerp_step(member, pairs, t, out), 3), 3)}
     del pc, member, out
-    torch.cuda.empty_cache()
+    rt.empty_cache()
     return res
 
 
@@ -568,33 +645,195 @@ def stream_ceiling_ms(theta, workers, momentum, iters=10):
     return ts[len(ts) // 2]
 
 
-def time_sharded(args, layout, tdt, wdt, k_local, dev, rank, steps, warmup, mode=None, broadcast=None):
+def time_sharded(args, layout, tdt, wdt, k_local, rt, comm, kernels, steps, warmup, mode=None, broadcast=None):
     """Build a ShardedOuterSync with k_local workers per rank, warm it up and time `steps` steps
     (barrier + synchronize on both sides, max over ranks). Returns (ms_per_step, mode/broadcast,
     wire bytes per rank); frees the arenas."""
-    import torch.distributed as dist
     from evolutionarydistributedtraining_amd.distributed import ShardedOuterSync
-    sync = ShardedOuterSync(layout, tdt, wdt, k_local, dev, args.lr, args.momentum, bool(args.nesterov),
+    sync = ShardedOuterSync(layout, tdt, wdt, k_local, rt.dev, args.lr, args.momentum, bool(args.nesterov),
                             mode=mode or args.mode, bucket_elems=args.bucket_elems,
-                            broadcast=broadcast or args.broadcast)
-    synth_population(sync.theta.flat, [w.flat for w in sync.workers], seed=4321 + 7919 * rank)
-    dist.broadcast(sync.theta_buf, 0)
+                            broadcast=broadcast or args.broadcast, comm=comm, kernels=kernels)
+    synth_sharded(sync.theta.flat, [w.flat for w in sync.workers], comm.rank)
     for _ in range(warmup):
         sync.step()
-    torch.cuda.synchronize()
-    dist.barrier()
-    torch.cuda.synchronize()
+    rt.sync()
+    comm.barrier()
+    rt.sync()
     t0 = time.perf_counter()
     for _ in range(steps):
         sync.step()
-    torch.cuda.synchronize()
-    dist.barrier()
-    t = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    res = (t.item() / steps * 1e3, f"{sync.mode}/{sync.broadcast}", sync.wire_bytes())
+    rt.sync()
+    comm.barrier()
+    elapsed = max(comm.all_gather_object(time.perf_counter() - t0))
+    res = (elapsed / steps * 1e3, f"{sync.mode}/{sync.broadcast}", sync.wire_bytes())
     del sync
-    torch.cuda.empty_cache()
+    rt.empty_cache()
     return res
+
+
+def run_sharded(args, comm, rt, json_out, kernels=None, exit_fn=None) -> dict | None:
+    """The N > 1 line (and `--gpus 1 --sharded`): the sharded outer step over `comm`, timed; the
+    line built on rank 0 (value, local-kernel HBM roofline + the xGMI figure, the CPU baseline);
+    then the extras under the deadline (weak companion, other schedules, BASELINE configs[2]/[3],
+    configs[4]'s population); rank 0 prints ONE line. `comm`: the collectives.Collectives seam
+    (RCCL here; gloo in tests/test_bench_rehearsal.py), `rt`: Runtime, `kernels`: the product ops
+    (None) or a host stand-in. Returns rank 0's line."""
+    from evolutionarydistributedtraining_amd.distributed import ShardedOuterSync
+    from evolutionarydistributedtraining_amd.layouts import LAYOUTS
+    rank, world = comm.rank, comm.world
+    layout = LAYOUTS[args.layout]()
+    tdt, wdt = DT[args.theta_dtype], DT[args.worker_dtype]
+    if args.workers_per_gpu:
+        k_local, scaling = args.workers_per_gpu, "weak"
+    else:
+        if args.population % world:
+            raise SystemExit(f"population {args.population} does not split over {world} GPUs")
+        k_local, scaling = args.population // world, "strong"
+    k_total = k_local * world
+    P = layout.total
+    sync = ShardedOuterSync(layout, tdt, wdt, k_local, rt.dev, args.lr, args.momentum, bool(args.nesterov),
+                            mode=args.mode, bucket_elems=args.bucket_elems, broadcast=args.broadcast,
+                            comm=comm, kernels=kernels)
+    sync.event_factory = rt.event
+    synth_sharded(sync.theta.flat, [w.flat for w in sync.workers], rank)
+    kernel_name = {"exact": "outer_kernel (fused, owned shards)",
+                   "reduce": "outer_kernel(partial) + sgd_apply_kernel",
+                   "reduce_ordered": "outer_kernel(partial) + sgd_apply_sum_kernel"}[sync.mode]
+    for _ in range(args.warmup):
+        sync.step()
+    rt.sync()
+    sync.kernel_events = []          # every local kernel of the schedule, bracketed inside the step
+    comm.barrier()
+    rt.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sync.step()
+    rt.sync()
+    comm.barrier()
+    elapsed = max(comm.all_gather_object(time.perf_counter() - t0))
+    ms_per_step = elapsed / args.steps * 1e3
+    kern_ms = max(comm.all_gather_object(sum(a.elapsed_time(b) for a, b in sync.kernel_events) / args.steps))
+    kern_bytes = sync.kernel_bytes()
+    sync.kernel_events = None
+    bytes_reduced = k_total * P * torch.finfo(wdt).bits // 8
+    value = bytes_reduced / (ms_per_step / 1e3) / 1e9
+    sched = f"{sync.mode}/{sync.broadcast}"
+    wire_main = sync.wire_bytes()
+
+    out = None
+    if rank == 0:
+        # the rank's local kernels (HIP events inside the step, slowest rank) against HBM ...
+        achieved = kern_bytes / (kern_ms / 1e3) / 1e9
+        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                    "traffic_note": "no PMC collection on the multi-GPU path",
+                    "kernel": kernel_name, "kernel_ms": round(kern_ms, 4),
+                    "algo_bytes_per_launch": kern_bytes, "schedule": sched,
+                    "note": "local kernels per rank and step (all buckets); the step itself is "
+                            "bounded by the xGMI exchange below"}
+        # ... and the exchange: bytes this rank puts on xGMI per step over the whole step time,
+        # against the outbound direction of the rank's links to its N-1 peers
+        xa = wire_main / (ms_per_step / 1e3) / 1e9
+        peak = XGMI_LINK_GBPS * (world - 1)
+        roofline["xgmi"] = {"bound": "xgmi", "achieved": round(xa, 1), "peak": peak, "unit": "GB/s",
+                            "frac": round(xa / peak, 4) if peak else None, "wire_bytes_per_rank": wire_main}
+        out = {
+            "metric": "GB/s of param bytes reduced per outer step (device-resident), 1/2/4/8 GPUs",
+            "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": scaling, "vs_baseline": None, "dtype": "f32" if tdt == torch.float32 else "bf16",
+            "data": "synthetic (theta ~ N(0,.02^2) from one seed on every rank, worker = theta + N(0,1e-3^2) "
+                    "from a per-rank seed, on device)",
+            "config": {"workload": f"DiLoCo outer step, {args.layout} P={P} T={len(layout)}, "
+                                   f"population {k_total} ({k_local} {args.worker_dtype} workers resident per GPU), "
+                                   f"{args.theta_dtype} theta+momentum, lr {args.lr} mu {args.momentum} "
+                                   f"nesterov {bool(args.nesterov)}",
+                       "params": P, "tensors": len(layout), "workers_per_gpu": k_local,
+                       "population": k_total, "worker_dtype": args.worker_dtype,
+                       "theta_dtype": args.theta_dtype, "parallelism": f"dp{world} {sched} (RCCL)"},
+            "roofline": roofline,
+            "device": rt.device_info(),
+        }
+        # rank 0 times the CPU baseline first (the other ranks wait at the barrier), then every
+        # extra runs under the deadline, so neither can be lost to a hang in an extra
+        if args.cpu_baseline_seconds > 0:
+            try:
+                out["cpu_baseline"] = cpu_baseline(args, tdt, wdt, k_total)
+            except Exception as e:     # the value is measured: report the failure, keep the line
+                out["cpu_baseline"] = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
+    comm.barrier()
+    deadline = ExtrasDeadline(args.extras_deadline, rank, out, json_out, exit_fn=exit_fn)
+    sync = None
+    rt.empty_cache()
+    if scaling == "strong" and args.weak_companion:     # (world 1: --sharded rehearsal)
+        # the same schedule with the N = 1 population on EVERY rank (population x N): per-GPU
+        # work fixed, so value_N / (N value_1) isolates the cost of the xGMI exchange
+        try:
+            w_ms, w_sched, w_wire = time_sharded(args, layout, tdt, wdt, args.population, rt, comm, kernels,
+                                                 args.steps, args.warmup)
+            w_bytes = args.population * world * P * torch.finfo(wdt).bits // 8
+            weak = {"workers_per_gpu": args.population, "population": args.population * world,
+                    "ms_per_step": round(w_ms, 4), "value": round(w_bytes / (w_ms / 1e3) / 1e9, 2),
+                    "unit": "GB/s", "schedule": w_sched, "wire_bytes_per_rank": w_wire,
+                    "note": "companion measurement after the timed strong-scaling steps; not the value"}
+        except Exception as e:     # the value is already measured: report, go on
+            weak = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
+            rt.empty_cache()
+        if out is not None:
+            out["weak_scaling"] = weak
+    if args.compare_schedules:
+        # every schedule the strong-scaling population can run, same steps, after the value: the
+        # data to tune mode="auto" on this node (outside the reported value)
+        schedules = {}
+        for m, b in (("exact", "workers"), ("exact", "theta"), ("reduce_ordered", "theta"), ("reduce", "theta")):
+            if f"{m}/{b}" == sched:
+                continue
+            try:
+                ms_, name, wire_ = time_sharded(args, layout, tdt, wdt, k_local, rt, comm, kernels, args.steps,
+                                                args.warmup, mode=m, broadcast=b)
+                schedules[name] = {"ms_per_step": round(ms_, 4), "wire_bytes_per_rank": wire_,
+                                   "value": round(bytes_reduced / (ms_ / 1e3) / 1e9, 2)}
+            except Exception as e:     # an extra after the value: report it, keep the line
+                schedules[f"{m}/{b}"] = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
+                rt.empty_cache()
+        if out is not None:
+            out["other_schedules"] = schedules
+    if args.config_companions:
+        # BASELINE's other multi-GPU DiLoCo configs on the same node, after the value: configs[2]
+        # (125M, 8 workers = 8 GPUs, fp32 as the reference computes) and configs[3] (1.3B, 8
+        # workers over the GPUs, bf16 params); same population split, the schedule auto picks
+        configs = {}
+        for item in args.config_layouts.split(","):
+            key, spec = item.split("=")
+            lname, cname = spec.split(":")
+            cdt = DT[cname]
+            try:
+                lay_c = LAYOUTS[lname]()
+                ms_, name, wire_ = time_sharded(args, lay_c, cdt, cdt, k_local, rt, comm, kernels, args.steps,
+                                                args.warmup)
+                b_c = k_total * lay_c.total * torch.finfo(cdt).bits // 8
+                configs[key] = {"layout": lname, "params": lay_c.total, "dtype": cname,
+                                "population": k_total, "workers_per_gpu": k_local, "schedule": name,
+                                "ms_per_step": round(ms_, 4), "value": round(b_c / (ms_ / 1e3) / 1e9, 2),
+                                "unit": "GB/s", "wire_bytes_per_rank": wire_}
+            except Exception as e:     # an extra after the value: report it, keep the line
+                configs[key] = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
+                rt.empty_cache()
+        if out is not None:
+            out["baseline_configs"] = configs
+    if world > 1 and "population_7b" in args.ops:
+        # configs[4] on the same node, after the DiLoCo measurements (every rank takes part)
+        try:
+            population = bench_population(args, rt, comm, kernels, layout_name=args.population_layout)
+        except Exception as e:     # an extra after the value: report it, keep the line
+            population = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
+            rt.empty_cache()
+        if out is not None:
+            out["population_slerp_7b"] = population
+    deadline.emit()
+    comm.barrier()          # still under the deadline: a rank stuck in an extra cannot hang the exit
+    deadline.cancel()
+    return out
 
 
 def main():
@@ -622,50 +861,40 @@ def main():
                           MASTER_PORT=str(_free_port()))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    import torch.distributed as dist
+    rt = Runtime(dev)
     if sharded:
-        from evolutionarydistributedtraining_amd.collectives import init_torch
+        import torch.distributed as dist
+        from evolutionarydistributedtraining_amd.collectives import TorchCollectives, init_torch
         init_torch("nccl", device_id=dev)
+        run_sharded(args, TorchCollectives(), rt, json_out)
+        dist.destroy_process_group()
+        return
 
-    from evolutionarydistributedtraining_amd import ops
     from evolutionarydistributedtraining_amd.layouts import LAYOUTS
     from evolutionarydistributedtraining_amd.diloco import OuterSync
     from evolutionarydistributedtraining_amd.params import ParamArena
 
     layout = LAYOUTS[args.layout]()
     tdt, wdt = DT[args.theta_dtype], DT[args.worker_dtype]
-    if args.workers_per_gpu:
-        k_local, scaling = args.workers_per_gpu, "weak"
-    else:
-        if args.population % world:
-            raise SystemExit(f"population {args.population} does not split over {world} GPUs")
-        k_local, scaling = args.population // world, "strong"
-    k_total = k_local * world
+    k_local = args.workers_per_gpu or args.population
+    scaling = "weak" if args.workers_per_gpu else "strong"
+    k_total = k_local
     P = layout.total
-    if not sharded:
-        theta = ParamArena(layout, tdt, dev)
-        workers = [ParamArena(layout, wdt, dev) for _ in range(k_local)]
-        synth_population(theta.flat, [w.flat for w in workers], seed=1234)
-        sync = OuterSync(theta, workers, args.lr, args.momentum, bool(args.nesterov))
-        step = sync.step
-        kernel_name = "outer_kernel"
-    else:
-        from evolutionarydistributedtraining_amd.distributed import ShardedOuterSync
-        sync = ShardedOuterSync(layout, tdt, wdt, k_local, dev, args.lr, args.momentum, bool(args.nesterov),
-                                mode=args.mode, bucket_elems=args.bucket_elems, broadcast=args.broadcast)
-        synth_population(sync.theta.flat, [w.flat for w in sync.workers], seed=1234 + 7919 * rank)
-        # replicas of theta must agree: rank 0's values everywhere
-        dist.broadcast(sync.theta_buf, 0)
-        step = sync.step
-        kernel_name = {"exact": "outer_kernel (fused, owned shards)",
-                       "reduce": "outer_kernel(partial) + sgd_apply_kernel",
-                       "reduce_ordered": "outer_kernel(partial) + sgd_apply_sum_kernel"}[sync.mode]
+    theta = ParamArena(layout, tdt, dev)
+    workers = [ParamArena(layout, wdt, dev) for _ in range(k_local)]
+    synth_population(theta.flat, [w.flat for w in workers], seed=1234)
+    sync = OuterSync(theta, workers, args.lr, args.momentum, bool(args.nesterov))
+    step = sync.step
+    kernel_name = "outer_kernel"
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     placement = None
-    if not sharded and args.place_candidates > 1:
+    # the fused step on the first allocation, before any placement search: what the drop-in list
+    # path and any first-allocation user get, reported beside the placed value
+    unplaced_ms = _event_ms(step, 5, 0)
+    if args.place_candidates > 1:
         # once per run, outside the timed region: the momentum buffer goes wherever the step's
         # access pattern runs fastest (placement.py); every later step uses that placement
         try:
@@ -675,251 +904,117 @@ def main():
         step()
         torch.cuda.synchronize()
 
-    # fused-kernel duration, measured with HIP events on the launch stream (torch's current);
-    # sharded: every local kernel of the schedule bracketed inside the step (ShardedOuterSync)
-    kern_ms = None
-    if not sharded:
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    else:
-        sync.kernel_events = []
-
-    if sharded:
-        dist.barrier()
+    # fused-kernel duration, measured with HIP events on the launch stream (torch's current)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        if not sharded:
-            ev[i][0].record()
+        ev[i][0].record()
         step()
-        if not sharded:
-            ev[i][1].record()
+        ev[i][1].record()
     torch.cuda.synchronize()
-    if sharded:
-        dist.barrier()
     elapsed = time.perf_counter() - t0
-    if sharded:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
     ms_per_step = elapsed / args.steps * 1e3
-    if not sharded:
-        ks = sorted(a.elapsed_time(b) for a, b in ev)
-        kern_ms = sum(ks) / len(ks)
-    else:
-        kern_ms = sum(a.elapsed_time(b) for a, b in sync.kernel_events) / args.steps
-        kern_bytes = sync.kernel_bytes()
-        sync.kernel_events = None
-        kt = torch.tensor([kern_ms], device=dev, dtype=torch.float64)     # the slowest rank's kernels
-        dist.all_reduce(kt, op=dist.ReduceOp.MAX)
-        kern_ms = kt.item()
+    ks = sorted(a.elapsed_time(b) for a, b in ev)
+    kern_ms = sum(ks) / len(ks)
 
     bytes_reduced = k_total * P * torch.finfo(wdt).bits // 8
     value = bytes_reduced / (ms_per_step / 1e3) / 1e9
-    sched = f"{sync.mode}/{sync.broadcast}" if sharded else None
-    wire_main = sync.wire_bytes() if sharded else None
-
-    # rank 0's line, built as soon as the value is measured; the extras below add to it
-    out = None
-    roofline = None
-    if rank == 0:
-        bg = torch.finfo(tdt).bits // 8
-        bw = torch.finfo(wdt).bits // 8
-        per_elem = k_local * bw + 2 * bg + (2 * bg if args.momentum else 0)
-        algo_bytes = per_elem * P                       # one launch, steady state (carried buffer)
-        if not sharded:
-            achieved = algo_bytes / (kern_ms / 1e3) / 1e9
-            traffic = None
-            if os.path.exists(args.traffic_json):
-                try:
-                    with open(args.traffic_json) as f:
-                        tj = json.load(f)
-                    key = f"{args.layout}/K{k_local}/{args.theta_dtype}-{args.worker_dtype}"
-                    traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
-                except (OSError, ValueError):
-                    traffic = None
-            roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
-                        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                        "kernel": kernel_name, "kernel_ms": round(kern_ms, 4),
-                        "bytes_per_elem": per_elem, "algo_bytes_per_launch": algo_bytes}
-        else:
-            # the rank's local kernels (HIP events inside the step, slowest rank) against HBM ...
-            achieved = kern_bytes / (kern_ms / 1e3) / 1e9
-            roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                        "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
-                        "kernel": kernel_name, "kernel_ms": round(kern_ms, 4),
-                        "algo_bytes_per_launch": kern_bytes, "schedule": sched,
-                        "note": "local kernels per rank and step (all buckets); the step itself is "
-                                "bounded by the xGMI exchange below"}
-            # ... and the exchange: bytes this rank puts on xGMI per step over the whole step time,
-            # against the outbound direction of the rank's links to its N-1 peers
-            xa = wire_main / (ms_per_step / 1e3) / 1e9
-            peak = XGMI_LINK_GBPS * (world - 1)
-            roofline["xgmi"] = {"bound": "xgmi", "achieved": round(xa, 1), "peak": peak, "unit": "GB/s",
-                                "frac": round(xa / peak, 4) if peak else None, "wire_bytes_per_rank": wire_main}
-        prop = torch.cuda.get_device_properties(dev)
-        out = {
-            "metric": "GB/s of param bytes reduced per outer step (device-resident), 1/2/4/8 GPUs",
-            "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": scaling, "vs_baseline": None, "dtype": "f32" if tdt == torch.float32 else "bf16",
-            "data": "synthetic (theta ~ N(0,.02^2), worker = theta + N(0,1e-3^2), seeded on device)",
-            "config": {"workload": f"DiLoCo outer step, {args.layout} P={P} T={len(layout)}, "
-                                   f"population {k_total} ({k_local} {args.worker_dtype} workers resident per GPU), "
-                                   f"{args.theta_dtype} theta+momentum, lr {args.lr} mu {args.momentum} "
-                                   f"nesterov {bool(args.nesterov)}",
-                       "params": P, "tensors": len(layout), "workers_per_gpu": k_local,
-                       "population": k_total, "worker_dtype": args.worker_dtype,
-                       "theta_dtype": args.theta_dtype,
-                       "parallelism": "single GPU" if not sharded else
-                                       f"dp{world} {sched} (RCCL)"},
-            "roofline": roofline,
-            "device": {"name": prop.name, "arch": getattr(prop, "gcnArchName", ""),
-                       "cus": prop.multi_processor_count, "hbm_gib": round(prop.total_memory / 2**30, 1)},
-        }
-
-    deadline = None
-    if sharded:
-        # multi-GPU path: rank 0 times the CPU baseline first (the other ranks wait at the barrier),
-        # then every extra runs under the deadline, so neither can be lost to a hang in an extra
-        if rank == 0 and args.cpu_baseline_seconds > 0:
-            out["cpu_baseline"] = cpu_baseline(args, tdt, wdt, k_total)
-        dist.barrier()
-        deadline = ExtrasDeadline(args.extras_deadline, rank, out, json_out)
-        sync = step = None
-        torch.cuda.empty_cache()
-        if scaling == "strong" and args.weak_companion:     # (world 1: --sharded rehearsal)
-            # the same schedule with the N = 1 population on EVERY rank (population x N): per-GPU
-            # work fixed, so value_N / (N value_1) isolates the cost of the xGMI exchange
-            try:
-                w_ms, w_sched, w_wire = time_sharded(args, layout, tdt, wdt, args.population, dev, rank,
-                                                     args.steps, args.warmup)
-                w_bytes = args.population * world * P * torch.finfo(wdt).bits // 8
-                weak = {"workers_per_gpu": args.population, "population": args.population * world,
-                        "ms_per_step": round(w_ms, 4), "value": round(w_bytes / (w_ms / 1e3) / 1e9, 2),
-                        "unit": "GB/s", "schedule": w_sched, "wire_bytes_per_rank": w_wire,
-                        "note": "companion measurement after the timed strong-scaling steps; not the value"}
-            except Exception as e:     # the value is already measured: report, go on
-                weak = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
-                torch.cuda.empty_cache()
-            if out is not None:
-                out["weak_scaling"] = weak
-        if args.compare_schedules:
-            # every schedule the strong-scaling population can run, same steps, after the value: the
-            # data to tune mode="auto" on this node (outside the reported value)
-            schedules = {}
-            for m, b in (("exact", "workers"), ("exact", "theta"), ("reduce_ordered", "theta"), ("reduce", "theta")):
-                if f"{m}/{b}" == sched:
-                    continue
-                try:
-                    ms_, name, wire_ = time_sharded(args, layout, tdt, wdt, k_local, dev, rank, args.steps,
-                                                    args.warmup, mode=m, broadcast=b)
-                    schedules[name] = {"ms_per_step": round(ms_, 4), "wire_bytes_per_rank": wire_,
-                                       "value": round(bytes_reduced / (ms_ / 1e3) / 1e9, 2)}
-                except Exception as e:     # an extra after the value: report it, keep the line
-                    schedules[f"{m}/{b}"] = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
-                    torch.cuda.empty_cache()
-            if out is not None:
-                out["other_schedules"] = schedules
-        if args.config_companions:
-            # BASELINE's other multi-GPU DiLoCo configs on the same node, after the value: configs[2]
-            # (125M, 8 workers = 8 GPUs, fp32 as the reference computes) and configs[3] (1.3B, 8
-            # workers over the GPUs, bf16 params); same population split, the schedule auto picks
-            configs = {}
-            for key, lname, cdt in (("configs2_125m_fp32", "gpt2_small", torch.float32),
-                                    ("configs3_1p3b_bf16", "gpt_1p3b", torch.bfloat16)):
-                try:
-                    lay_c = LAYOUTS[lname]()
-                    ms_, name, wire_ = time_sharded(args, lay_c, cdt, cdt, k_local, dev, rank, args.steps,
-                                                    args.warmup)
-                    b_c = k_total * lay_c.total * torch.finfo(cdt).bits // 8
-                    configs[key] = {"layout": lname, "params": lay_c.total,
-                                    "dtype": "f32" if cdt == torch.float32 else "bf16",
-                                    "population": k_total, "workers_per_gpu": k_local, "schedule": name,
-                                    "ms_per_step": round(ms_, 4), "value": round(b_c / (ms_ / 1e3) / 1e9, 2),
-                                    "unit": "GB/s", "wire_bytes_per_rank": wire_}
-                except Exception as e:     # an extra after the value: report it, keep the line
-                    configs[key] = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
-                    torch.cuda.empty_cache()
-            if out is not None:
-                out["baseline_configs"] = configs
-        if world > 1 and "population_7b" in args.ops:
-            # configs[4] on the same node, after the DiLoCo measurements (every rank takes part)
-            try:
-                from evolutionarydistributedtraining_amd.collectives import TorchCollectives
-                population = bench_population(args, dev, TorchCollectives())
-            except Exception as e:     # an extra after the value: report it, keep the line
-                population = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
-                torch.cuda.empty_cache()
-            if out is not None:
-                out["population_slerp_7b"] = population
-
-    if rank == 0 and not sharded:
-        # what a plain device-to-device copy reaches on this device, same process
-        src = torch.empty(1 << 29, dtype=torch.float32, device=dev)
-        dst = torch.empty_like(src)
-        dst.copy_(src)
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record()
-        for _ in range(5):
-            dst.copy_(src)
-        b.record()
-        torch.cuda.synchronize()
-        roofline["device_copy_GBps"] = round(5 * 2 * src.numel() * 4 / (a.elapsed_time(b) / 1e3) / 1e9, 1)
-        del src, dst
-        # the step's own access pattern with a trivial body (edt_probe_stream), same arenas:
-        # the memory-system ceiling of this step on this device, measured after the timed steps
-        try:
-            probe_ms = stream_ceiling_ms(theta.flat, [w.flat for w in workers], sync.state.momentum)
-        except Exception as e:      # a measurement extra: the JSON line still prints
-            probe_ms = None
-            roofline["stream_ceiling_error"] = f"{type(e).__name__}: {e}"
-        if probe_ms:
-            ceil = algo_bytes / (probe_ms / 1e3) / 1e9
-            roofline["stream_ceiling_GBps"] = round(ceil, 1)
-            roofline["frac_of_stream_ceiling"] = round(roofline["achieved"] / ceil, 4)
-        if placement:
-            roofline["momentum_placement"] = placement
-        if args.bcast_compare:
-            # the step with the broadcast of diloco.py:302-308 (every worker restarts from theta):
-            # fused into the kernel's pass vs the step + K device copies
-            try:
-                fused = _event_ms(lambda: sync.step(broadcast=True), args.steps, 2)
-                unfused = _event_ms(lambda: (sync.step(), sync.broadcast_()), args.steps, 2)
-                fb = algo_bytes + k_local * P * (torch.finfo(wdt).bits // 8)
-                out["step_with_broadcast"] = {
-                    "fused_ms": round(fused, 4), "step_plus_copies_ms": round(unfused, 4),
-                    "kernel": "outer_kernel<..., BC=true> (edt_outer_step_bcast)",
-                    "fused_roofline": {"bound": "hbm", "achieved": round(fb / (fused / 1e3) / 1e9, 1),
-                                       "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                                       "frac": round(fb / (fused / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
-                                       "algo_bytes_per_launch": fb}}
-            except Exception as e:          # an extra: report it, keep the line
-                out["step_with_broadcast"] = {"error": f"{type(e).__name__}: {str(e)[:300]}"}
-        if args.ops and args.ops != "none":
-            # the other hot-path kernels, one GPU, after the outer step's arenas are freed
-            sync.theta = sync.workers = sync.state = None
-            theta = workers = sync = step = None
-            torch.cuda.empty_cache()
-            for name, fn in (("configs1_125m", bench_config1), ("pair_merge", bench_pair_merge),
-                             ("slerp_7b", bench_slerp_7b)):
-                if name in args.ops:
-                    try:
-                        out[name] = fn(args, dev)
-                    except Exception as e:          # an extra: report it, keep the line
-                        out[name] = {"error": f"{type(e).__name__}: {str(e)[:300]}"}
-                        torch.cuda.empty_cache()
-        if args.cpu_baseline_seconds > 0:
-            # rank 0 after the GPU phase, on this host's cores: the whole population's step (the
-            # reference's master runs all K workers' deltas on its CPU)
-            out["cpu_baseline"] = cpu_baseline(args, tdt, wdt, k_total)
-    if deadline is None:
-        if rank == 0:
-            print(json.dumps(out), file=json_out, flush=True)
+    if rank != 0:
         return
-    deadline.emit()
-    dist.barrier()          # still under the deadline: a rank stuck in an extra cannot hang the exit
-    deadline.cancel()
-    dist.destroy_process_group()
+    bg = torch.finfo(tdt).bits // 8
+    bw = torch.finfo(wdt).bits // 8
+    per_elem = k_local * bw + 2 * bg + (2 * bg if args.momentum else 0)
+    algo_bytes = per_elem * P                       # one launch, steady state (carried buffer)
+    achieved = algo_bytes / (kern_ms / 1e3) / 1e9
+    traffic, traffic_note = _pmc_traffic(args, f"{args.layout}/K{k_local}/{args.theta_dtype}-{args.worker_dtype}",
+                                         with_note=True)
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                "traffic_source": traffic_note,
+                "kernel": kernel_name, "kernel_ms": round(kern_ms, 4),
+                "bytes_per_elem": per_elem, "algo_bytes_per_launch": algo_bytes}
+    out = {
+        "metric": "GB/s of param bytes reduced per outer step (device-resident), 1/2/4/8 GPUs",
+        "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+        "scaling": scaling, "vs_baseline": None, "dtype": "f32" if tdt == torch.float32 else "bf16",
+        "data": "synthetic (theta ~ N(0,.02^2), worker = theta + N(0,1e-3^2), seeded on device)",
+        "config": {"workload": f"DiLoCo outer step, {args.layout} P={P} T={len(layout)}, "
+                               f"population {k_total} ({k_local} {args.worker_dtype} workers resident per GPU), "
+                               f"{args.theta_dtype} theta+momentum, lr {args.lr} mu {args.momentum} "
+                               f"nesterov {bool(args.nesterov)}",
+                   "params": P, "tensors": len(layout), "workers_per_gpu": k_local,
+                   "population": k_total, "worker_dtype": args.worker_dtype,
+                   "theta_dtype": args.theta_dtype, "parallelism": "single GPU"},
+        "roofline": roofline,
+        "device": rt.device_info(),
+    }
+
+    # what a plain device-to-device copy reaches on this device, same process
+    src = torch.empty(1 << 29, dtype=torch.float32, device=dev)
+    dst = torch.empty_like(src)
+    dst.copy_(src)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(5):
+        dst.copy_(src)
+    b.record()
+    torch.cuda.synchronize()
+    roofline["device_copy_GBps"] = round(5 * 2 * src.numel() * 4 / (a.elapsed_time(b) / 1e3) / 1e9, 1)
+    del src, dst
+    # the step's own access pattern with a trivial body (edt_probe_stream), same arenas:
+    # the memory-system ceiling of this step on this device, measured after the timed steps
+    try:
+        probe_ms = stream_ceiling_ms(theta.flat, [w.flat for w in workers], sync.state.momentum)
+    except Exception as e:      # a measurement extra: the JSON line still prints
+        probe_ms = None
+        roofline["stream_ceiling_error"] = f"{type(e).__name__}: {e}"
+    if probe_ms:
+        ceil = algo_bytes / (probe_ms / 1e3) / 1e9
+        roofline["stream_ceiling_GBps"] = round(ceil, 1)
+        roofline["frac_of_stream_ceiling"] = round(roofline["achieved"] / ceil, 4)
+    roofline["unplaced_ms"] = round(unplaced_ms, 4)
+    roofline["unplaced_frac"] = round(algo_bytes / (unplaced_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)
+    roofline["unplaced_note"] = ("the fused step (HIP events, 5 launches) on the momentum's first allocation, "
+                                 "before the placement search; kernel_ms is after it")
+    if placement:
+        roofline["momentum_placement"] = placement
+    if args.bcast_compare:
+        # the step with the broadcast of diloco.py:302-308 (every worker restarts from theta):
+        # fused into the kernel's pass vs the step + K device copies
+        try:
+            fused = _event_ms(lambda: sync.step(broadcast=True), args.steps, 2)
+            unfused = _event_ms(lambda: (sync.step(), sync.broadcast_()), args.steps, 2)
+            fb = algo_bytes + k_local * P * (torch.finfo(wdt).bits // 8)
+            out["step_with_broadcast"] = {
+                "fused_ms": round(fused, 4), "step_plus_copies_ms": round(unfused, 4),
+                "kernel": "outer_kernel<..., BC=true> (edt_outer_step_bcast)",
+                "fused_roofline": {"bound": "hbm", "achieved": round(fb / (fused / 1e3) / 1e9, 1),
+                                   "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                                   "frac": round(fb / (fused / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+                                   "algo_bytes_per_launch": fb}}
+        except Exception as e:          # an extra: report it, keep the line
+            out["step_with_broadcast"] = {"error": f"{type(e).__name__}: {str(e)[:300]}"}
+    if args.ops and args.ops != "none":
+        # the other hot-path kernels, one GPU, after the outer step's arenas are freed
+        sync.theta = sync.workers = sync.state = None
+        theta = workers = sync = step = None
+        torch.cuda.empty_cache()
+        for name, fn in (("configs1_125m", bench_config1), ("pair_merge", bench_pair_merge),
+                         ("slerp_7b", bench_slerp_7b)):
+            if name in args.ops:
+                try:
+                    out[name] = fn(args, dev)
+                except Exception as e:          # an extra: report it, keep the line
+                    out[name] = {"error": f"{type(e).__name__}: {str(e)[:300]}"}
+                    torch.cuda.empty_cache()
+    if args.cpu_baseline_seconds > 0:
+        # rank 0 after the GPU phase, on this host's cores: the whole population's step (the
+        # reference's master runs all K workers' deltas on its CPU)
+        out["cpu_baseline"] = cpu_baseline(args, tdt, wdt, k_total)
+    print(json.dumps(out), file=json_out, flush=True)
+
 
 if __name__ == "__main__":
     main()

@@ -87,6 +87,22 @@ class EdtError(RuntimeError):
     """A C-ABI call returned a negative status (message from edt_last_error())."""
 
 
+_sha_cache: dict = {}
+
+
+def library_sha256(path: str = LIB_PATH) -> str | None:
+    """sha256 of the library file: the build stamp that ties a profile (profiles/pmc_traffic.json)
+    to the exact kernels it was measured on."""
+    if path not in _sha_cache:
+        import hashlib
+        try:
+            with open(path, "rb") as f:
+                _sha_cache[path] = hashlib.sha256(f.read()).hexdigest()
+        except OSError:
+            return None
+    return _sha_cache[path]
+
+
 def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     """Load and bind the shared object (no GPU needed). Raises if it is missing."""
     global _lib

@@ -47,6 +47,10 @@ from .params import ParamArena, ParamLayout
 from .tracing import trange, traced
 
 
+def _timing_event():
+    return torch.cuda.Event(enable_timing=True)
+
+
 class ShardedOuterSync:
     def __init__(self, layout: ParamLayout, theta_dtype: torch.dtype, worker_dtype: torch.dtype,
                  k_local: int, device, lr: float = 0.7, momentum: float = 0.9, nesterov: bool = True,
@@ -98,6 +102,7 @@ class ShardedOuterSync:
         # RCCL (and the virtual ranks) reduce/gather in place; gloo gets separate buffers
         self.inplace = self.comm.inplace
         self.kernel_events = None      # a list: (start, end) HIP events around every local kernel
+        self.event_factory = _timing_event   # bench.py's host rehearsal swaps in host-clock events
         # (Vec::size(), threads) of the reference's host: exact mode reproduces its bf16 scalar tails
         # (diloco.outer_step's cpu_tails; the reduce mode reassociates the sum anyway)
         self.tail_bits = None
@@ -126,7 +131,7 @@ class ShardedOuterSync:
         `kernel_events` is a list (bench.py: the per-rank HBM roofline at N > 1)."""
         if self.kernel_events is None:
             return fn(*args)
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a, b = self.event_factory(), self.event_factory()
         a.record()
         fn(*args)
         b.record()

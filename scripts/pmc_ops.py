@@ -39,8 +39,8 @@ def main():
     if pm:
         pm.update(algorithmic_bytes=14 * P1, correction="FETCH_SIZE x2 (16 B/lane bf16 loads), WRITE_SIZE x1")
         out["pair_merge/gpt_1p3b/bf16"] = pm
-    spec = traffic("slerp_stats_lerp_kernel")
-    stats = traffic("slerp_stats_kernel")
+    spec = traffic("pair_sums_kernel<1, true")
+    stats = traffic("pair_sums_kernel<1, false")
     blend = traffic("slerp_blend_kernel<1, 1, true, true>")
     if spec:
         out["slerp_7b/lineage"] = {"passes": [spec], "hbm_bytes_per_launch": spec["hbm_bytes_per_launch"],
@@ -51,6 +51,9 @@ def main():
                                "hbm_bytes_per_launch": stats["hbm_bytes_per_launch"] + blend["hbm_bytes_per_launch"],
                                "algorithmic_bytes": 6 * P7, "moved_bytes": 10 * P7,
                                "note": "two-pass: chunk sums (4 B/elem read) + blend (4 B read, 2 B written)"}
+    from evolutionarydistributedtraining_amd._lib import library_sha256
+    for rec in out.values():
+        rec["lib_sha256"] = library_sha256()      # the build these counters were measured on
     with open(os.path.join(root, "pmc_ops_traffic.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))

@@ -63,6 +63,8 @@ def main():
     else:
         rec["hbm_bytes_per_launch"] = int(2 * f_kib * 1024 + w_kib * 1024)
         rec["correction"] = "FETCH_SIZE x2 (gfx950 16B/lane streaming read), WRITE_SIZE x1; KiB -> bytes"
+    from evolutionarydistributedtraining_amd._lib import library_sha256
+    rec["lib_sha256"] = library_sha256()          # the build these counters were measured on
     out = {f"{layout}/K{k}/{tdt}-{wdt}": rec}
     with open(os.path.join(root, "pmc_traffic.json"), "w") as f:
         json.dump(out, f, indent=1)

@@ -10,6 +10,10 @@
 //   w1nb        w1 without the butterfly: lane 0 stores its own sums (what the reduction costs)
 //   w1tab       w1 with the tile's start read from a 24-B-per-chunk table first (the chunk lookup)
 //   s1 / s4     read-only sums (the two-pass stats), 1 or 4 vectors per lane
+//   w1ns        w1 with the row store skipped (stored only if a sum were NaN): the second write stream
+//   w1lo        fp64 sums per lane, no butterfly, no store (NaN-guarded): the per-lane math alone
+//   lerp4       lerp with 4 vectors per lane
+//   w4plain     w4 with default-policy loads
 //
 //   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -o scripts/_spec_probe scripts/spec_probe.hip
 //   scripts/_spec_probe [n_elements] [rounds]
@@ -55,9 +59,10 @@ __device__ __forceinline__ float wsumf(float x) {
     return x;
 }
 
-// MODE: 0 lerp, 1 fp64 sums + butterfly, 2 fp32 sums + butterfly, 3 fp64 no butterfly, 4 = 1 + table
-// EMIT: write the lerp output; IT: vectors per lane
-template <int MODE, bool EMIT, int IT>
+// MODE: 0 lerp, 1 fp64 sums + butterfly, 2 fp32 sums + butterfly, 3 fp64 no butterfly, 4 = 1 + table,
+// 5 = 1 with the row store NaN-guarded, 6 = per-lane fp64 sums NaN-guarded (no butterfly)
+// EMIT: write the lerp output; IT: vectors per lane; NTL: non-temporal loads
+template <int MODE, bool EMIT, int IT, bool NTL = true>
 __global__ __launch_bounds__(256) void k(const uint16_t* __restrict__ a, const uint16_t* __restrict__ b,
                                          uint16_t* __restrict__ o, uint64_t n, const uint64_t* __restrict__ tab,
                                          double* __restrict__ rows) {
@@ -70,8 +75,13 @@ __global__ __launch_bounds__(256) void k(const uint16_t* __restrict__ a, const u
     for (int k = 0; k < IT; ++k) {
         const uint64_t i = wbase + (uint64_t)k * 512;
         if (i + 8 <= n) {
-            wa[k] = __builtin_nontemporal_load(reinterpret_cast<const u4*>(a + i));
-            wb[k] = __builtin_nontemporal_load(reinterpret_cast<const u4*>(b + i));
+            if constexpr (NTL) {
+                wa[k] = __builtin_nontemporal_load(reinterpret_cast<const u4*>(a + i));
+                wb[k] = __builtin_nontemporal_load(reinterpret_cast<const u4*>(b + i));
+            } else {
+                wa[k] = *reinterpret_cast<const u4*>(a + i);
+                wb[k] = *reinterpret_cast<const u4*>(b + i);
+            }
         } else {
             wa[k] = wb[k] = (u4){0, 0, 0, 0};
         }
@@ -117,6 +127,10 @@ __global__ __launch_bounds__(256) void k(const uint16_t* __restrict__ a, const u
         if (lane == 0) { rows[row] = s00; rows[row + 1] = s11; rows[row + 2] = s01; }
         return;
     }
+    if constexpr (MODE == 6) {
+        if (s00 != s00 || s11 != s11 || s01 != s01) rows[row] = s00;
+        return;
+    }
     double v;
     if constexpr (MODE == 2) {
         const float a0 = wsumf(f00), a1 = wsumf(f11), a2 = wsumf(f01);
@@ -124,6 +138,10 @@ __global__ __launch_bounds__(256) void k(const uint16_t* __restrict__ a, const u
     } else {
         const double a0 = wsum(s00), a1 = wsum(s11), a2 = wsum(s01);
         v = lane == 0 ? a0 : lane == 1 ? a1 : a2;
+    }
+    if constexpr (MODE == 5) {
+        if (v != v) rows[row + lane] = v;
+        return;
     }
     if (lane < 3) rows[row + lane] = v;
 }
@@ -156,6 +174,11 @@ int main(int argc, char** argv) {
         {"w1tab", 6, [&] { k<4, true, 1><<<g1, 256>>>(a, b, o, n, tab, rows); }},
         {"s1", 4, [&] { k<1, false, 1><<<g1, 256>>>(a, b, o, n, tab, rows); }},
         {"s4", 4, [&] { k<1, false, 4><<<g4, 256>>>(a, b, o, n, tab, rows); }},
+        {"w1ns", 6, [&] { k<5, true, 1><<<g1, 256>>>(a, b, o, n, tab, rows); }},
+        {"w1lo", 6, [&] { k<6, true, 1><<<g1, 256>>>(a, b, o, n, tab, rows); }},
+        {"lerp4", 6, [&] { k<0, true, 4><<<g4, 256>>>(a, b, o, n, tab, rows); }},
+        {"w4plain", 6, [&] { k<1, true, 4, false><<<g4, 256>>>(a, b, o, n, tab, rows); }},
+        {"lerp_plain", 6, [&] { k<0, true, 1, false><<<g1, 256>>>(a, b, o, n, tab, rows); }},
     };
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));

@@ -1,0 +1,125 @@
+"""The whole N > 1 bench line rehearsed on the CPU, so the driver's first multi-GPU run cannot die in
+untried host code (EDT_LM/diloco.py:231-235,302-308 is the exchange it replaces).
+
+bench.run_sharded — the function `python bench.py --gpus N` runs on every rank — driven here over
+gloo at world 2 and 4 by real rank processes (the same environment the launcher gives them), with
+the CPU stand-in kernels injected by this test (tests/oracle_kernels.py; the product ops stay the
+default in bench.py) and tiny layouts registered for the run. Every extra runs: the weak
+companion, the other schedules, BASELINE configs[2]/[3] (tiny layouts here) and configs[4]'s
+population crossover; and the extras deadline fires on a rank that hangs, which must still print
+the line with the value and exit non-zero."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+LAYOUTS = {"rehearsal_main": [(64, 33), (257,), (31, 17), (1000,)],
+           "rehearsal_c2": [(40, 24), (24,), (333,)],
+           "rehearsal_c3": [(128, 9), (77,)],
+           "rehearsal_pop": [(300,), (17, 19), (1024,)]}
+ARGS = ["--layout", "rehearsal_main", "--population", "4", "--steps", "2", "--warmup", "1",
+        "--cpu-baseline-seconds", "0.2", "--cpu-sample-elems", "4096", "--bucket-elems", "2048",
+        "--config-layouts", "configs2_125m_fp32=rehearsal_c2:f32,configs3_1p3b_bf16=rehearsal_c3:bf16",
+        "--population-layout", "rehearsal_pop", "--population-groups", "2"]
+
+
+def _rank_main():
+    """One rank (launched by _launch with the torchrun-style environment)."""
+    import time
+
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    import bench
+    from evolutionarydistributedtraining_amd.collectives import TorchCollectives
+    from evolutionarydistributedtraining_amd.layouts import LAYOUTS as REG
+    from evolutionarydistributedtraining_amd.params import ParamLayout
+    from oracle import oracle
+    from tests.oracle_kernels import ChunkGramKernels, OracleKernels
+    for name, shapes in LAYOUTS.items():
+        REG[name] = lambda shapes=shapes: ParamLayout(shapes)
+    hang_rank = int(os.environ.get("REHEARSAL_HANG_RANK", "-1"))
+
+    class Kernels(ChunkGramKernels):
+        def slerp_arena(self, plan, v0, v1, out, t, thr=0.9995, eps=1e-8, **kw):
+            OracleKernels.slerp_arena(self, getattr(plan, "seg_offsets", plan), v0, v1, out, t, thr, eps)
+
+        def slerp_gram(self, members, chunks, nchunks, gram=None):
+            if dist.get_rank() == hang_rank:
+                time.sleep(120)                  # a peer that never answers: the deadline must fire
+            return super().slerp_gram(members, chunks, nchunks, gram)
+
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=int(os.environ["RANK"]), world_size=int(os.environ["WORLD_SIZE"]))
+    args = bench.parse(json.loads(os.environ["REHEARSAL_ARGS"]))
+    bench.run_sharded(args, TorchCollectives(), bench.Runtime("cpu"), sys.stdout, kernels=Kernels(oracle))
+    dist.destroy_process_group()
+
+
+def _launch(world, extra=(), hang_rank=-1, timeout=240):
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), REHEARSAL_ARGS=json.dumps(ARGS + ["--gpus", str(world)] + list(extra)),
+                   REHEARSAL_HANG_RANK=str(hang_rank), OMP_NUM_THREADS="2")
+        procs.append(subprocess.Popen([sys.executable, "-c", "from tests.test_bench_rehearsal import _rank_main; "
+                                       "_rank_main()"], cwd=ROOT, env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = []
+    try:
+        for p in procs:
+            o, e = p.communicate(timeout=timeout)
+            outs.append((p.returncode, o, e))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    lines = [l for l in outs[0][1].splitlines() if l.startswith("{")]
+    return outs, lines
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_line_at_world(world):
+    outs, lines = _launch(world)
+    assert all(rc == 0 for rc, _, _ in outs), [(rc, e[-2000:]) for rc, _, e in outs]
+    assert len(lines) == 1, outs[0][1][-2000:]
+    for rc, o, _ in outs[1:]:
+        assert not [l for l in o.splitlines() if l.startswith("{")]        # only rank 0 prints
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == world and d["value"] > 0 and d["ms_per_step"] > 0
+    assert d["roofline"]["xgmi"]["wire_bytes_per_rank"] > 0
+    assert d["roofline"]["kernel_ms"] > 0 and d["roofline"]["algo_bytes_per_launch"] > 0
+    assert d["cpu_baseline"]["value"] > 0 and "c_port" in d["cpu_baseline"]
+    for key in ("weak_scaling", "other_schedules", "baseline_configs", "population_slerp_7b"):
+        assert key in d, key
+    assert "error" not in d["weak_scaling"], d["weak_scaling"]
+    assert len(d["other_schedules"]) == 3 and all("error" not in v for v in d["other_schedules"].values()), \
+        d["other_schedules"]
+    assert set(d["baseline_configs"]) == {"configs2_125m_fp32", "configs3_1p3b_bf16"}
+    assert all("error" not in v for v in d["baseline_configs"].values()), d["baseline_configs"]
+    pop = d["population_slerp_7b"]
+    assert "error" not in pop and {"sharded", "sharded_pipelined", "per_child"} <= set(pop), pop
+    assert pop["sharded"]["wire_bytes_per_rank"] > 0
+    assert "extras_deadline" not in d
+
+
+@pytest.mark.slow
+def test_bench_line_deadline_fires_on_a_hung_rank():
+    """Rank 0 hangs inside the population crossover (the last extra): the deadline prints the line
+    with the value and every finished extra, names the unfinished one, and every rank exits 3."""
+    outs, lines = _launch(2, extra=["--extras-deadline", "20"], hang_rank=0)
+    assert [rc for rc, _, _ in outs] == [3, 3], [(rc, e[-1500:]) for rc, _, e in outs]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["value"] > 0 and d["cpu_baseline"]["value"] > 0
+    assert {"weak_scaling", "other_schedules", "baseline_configs"} <= set(d)
+    assert d["extras_deadline"]["unfinished_or_skipped"] == ["population_slerp_7b"]
