@@ -550,22 +550,23 @@ def bench_slerp_7b(args, dev):
     del v0, v1, out, plan
     torch.cuda.empty_cache()
     if args.ops_cpu_seconds > 0:
-        # the reference's numpy SLERP (oracle.slerp restates it op for op) on the layout's first
-        # tensors up to the sample budget, far parents (the SLERP branch)
-        shapes, total = [], 0
-        for shp in lay.shapes:
-            m = int(torch.Size(shp).numel())
-            if total + m <= args.cpu_sample_elems // 4:
-                shapes.append(m)
-                total += m
+        # the reference's numpy SLERP (oracle.slerp restates it op for op) over one whole
+        # transformer block of the layout (layer 0: the attention projections, the three 67.9M-
+        # element MLP matrices, the norms and biases — every tensor shape of the merge, the large
+        # ones dominating as in the 7B body), far parents (the SLERP branch)
+        shapes, names = _block_sample(lay, 300_000_000)
+        sizes = [int(torch.Size(shp).numel()) for shp in shapes]
+        total = sum(sizes)
         gc = torch.Generator().manual_seed(5)
-        a = [(torch.randn(m, generator=gc) * 0.02) for m in shapes]
+        a = [(torch.randn(m, generator=gc) * 0.02) for m in sizes]
         b = [(x + torch.randn(x.numel(), generator=gc) * 1e-3) for x in a]
         tm, reps = _median_time(lambda: [oracle.slerp(0.5, x, y) for x, y in zip(a, b)], args.ops_cpu_seconds)
+        del a, b
         res["cpu_baseline"] = {"value": round(6 * total / tm / 1e9, 3), "unit": "GB/s (algorithmic bytes, bf16-sized)",
                                "cores": torch.get_num_threads(), "kind": "port",
-                               "sample": f"{len(shapes)} tensors of qwen2p5_7b_body ({total} elements), "
-                                         f"EDT_RL/crossover.py:11-43's numpy SLERP (oracle.slerp), median of {reps} reps"}
+                               "sample": f"{len(sizes)} tensors of qwen2p5_7b_body layer 0 ({names[0]} .. {names[-1]}, "
+                                         f"{total} elements, largest {max(sizes)}), EDT_RL/crossover.py:11-43's numpy "
+                                         f"SLERP (oracle.slerp), median of {reps} reps"}
     return res
 
 

@@ -15,45 +15,59 @@ __device__ __forceinline__ double wave_sum(double x) {
 }
 
 // ---- the chunk sums' canonical order (every form: pair, speculative, Gram, sharded) --------------
-// A chunk's sums are formed by kSlots independent WAVE SLOTS, with no workgroup barrier anywhere:
-// slot j takes the wave tiles j, j + kSlots, ... of the chunk's 16-B-aligned body (kWaveTile
-// elements each: kWaveIters lane-contiguous 8-element vectors per lane, 1 KiB per wave access for
-// bf16), slot 0 also the < 16 head / tail elements (one per lane); per lane the products are
-// accumulated in element order by fp64 FMAs, the wave butterfly leaves the slot's totals in every
-// lane, and the slot rows go to a scratch table. slot_reduce_kernel then sums each chunk's kSlots
-// rows in slot order into the chunk row. The sum kernels run one workgroup per (chunk, group of
-// kBlock / 64 slots) in address order — the one-pass grid of the stream kernels, the chip's
-// in-flight window one contiguous stretch of every operand — where the previous form (one
-// workgroup per chunk, grid-stride, an LDS block reduction behind two barriers per chunk) kept
-// 65,536 far-apart chunks in flight and ran the 7B speculative pass at 7.1-8.3 ms depending on
-// the allocation against lerp's steady 7.0 ms on the same bytes (profiles/r03_*).
-constexpr int kSlots = EDT_SLERP_SLOTS;                       // slot rows per chunk
-constexpr int kWaveIters = EDT_SLERP_WAVE_ITERS;              // 8-element vectors per lane per tile
-constexpr int kWaveTile = 64 * kVec * kWaveIters;             // 2,048 elements
+// A chunk [start, start + len) (len <= 64 Ki) is cut into kTileSlots = 128 tiles of its 16-B-aligned
+// body [a, b): tile j holds, on lane l, the 8 elements at a + 512 j + 8 l (when below b); tile 0's
+// lanes also take the < 16 head / tail elements (lane l the l-th of them) after their vector. Per
+// lane the products are accumulated in element order by fp64 FMAs; the wave's xor butterfly
+// (wave_sum) gives the TILE SUM; the chunk's sum is the perfect binary tree over its 128 tile sums
+// in order, adjacent pairs first ((t0 + t1) + (t2 + t3)) + ..., empty tiles 0.0. Every kernel forms
+// complete subtrees — one tile per wave (a level-0 row), four tiles per wave combined in registers
+// (level 2), sixteen per workgroup combined in LDS (level 4) — and writes them as rows;
+// tree_reduce_kernel finishes each chunk's tree from its rows. So every form's per-chunk sums are
+// bit-identical whatever the work split, with no workgroup barrier in the pair passes.
+//
+// Why this shape (profiles/r03_spec_probe*.json, scripts/spec_probe.hip on the 7B body): the
+// speculative pass is lerp's stream (2 reads + 1 write per element) plus the sums; one tile per wave
+// in address order — lerp's own grid — costs nothing measurable for the fp64 math and butterflies
+// (6.94 ms vs lerp 6.92 with the row store removed); what does cost is the rows' second write
+// stream: 24-B rows scattered over the table +11 %, whole lines +1-3 %, and rows placed XCD-major
+// (each XCD's workgroups write one contiguous stretch, so its L2 writes back whole lines) +1.3 %.
+// The previous form (one workgroup per 64 Ki chunk, grid-stride, an LDS block reduction per chunk)
+// ran 7.1-8.3 ms depending on the allocation.
+constexpr int kTileElems = 64 * kVec;                         // 512
+constexpr int kTileSlots = 128;                               // tiles per chunk: chunks <= 64 Ki
+constexpr uint32_t kMaxChunkElems = (uint32_t)kTileSlots * kTileElems;
 constexpr int kWavesPerBlock = kBlock / 64;
-constexpr int kSlotGroups = kSlots / kWavesPerBlock;          // workgroups per chunk
-static_assert(kSlots % kWavesPerBlock == 0, "slots come in whole workgroups");
+// the row levels the kernels write: pair passes one tile per wave (level 0; the read-only stats
+// pass four per wave, level 2), the Gram passes sixteen per workgroup (level 4)
+constexpr int kPairRows = kTileSlots;                         // rows per chunk, level 0
+constexpr int kGramRows = kTileSlots / 16;                    // rows per chunk, level 4
 
-inline unsigned slot_grid(int64_t nchunks) {                  // one workgroup per (chunk, slot group)
-    const uint64_t g = (uint64_t)nchunks * kSlotGroups;
-    const uint64_t cap = EDT_SLERP_SUMS_BPC > 0 ? 256ull * EDT_SLERP_SUMS_BPC : kGridBlockCap;
-    return (unsigned)(g < cap ? g : cap);
+// One-pass grids of `units` workgroups in address order (a unit = a fixed set of a chunk's tiles);
+// past the dispatch cap (a multiple of 8, so blockIdx % 8 stays the unit's XCD) they stride.
+constexpr uint64_t kUnitGridCap = kGridBlockCap / 8 * 8;
+inline unsigned unit_grid(uint64_t units) {
+    return (unsigned)(units < kUnitGridCap ? (units ? units : 1) : kUnitGridCap);
 }
 
-// The traversal of one wave slot over chunk [start, start + len): tile(i, b) for each of the
-// lane's wave tiles (first vector i; vectors i + k * 64 * kVec for k < kWaveIters while < b), then
-// elem(i) for the head / tail element slot 0's lane takes. Callers accumulate in exactly this order.
-template <typename Tile, typename Elem>
-__device__ __forceinline__ void for_slot(uint64_t start, uint64_t len, int slot, Tile&& tile, Elem&& elem) {
+// Where unit u's rows go: XCD-major — the units one XCD runs (u % 8 equal) are contiguous, so each
+// XCD's L2 fills whole lines of the row table before writing them back.
+__host__ __device__ __forceinline__ uint64_t unit_slot(uint64_t u, uint64_t units) {
+    const uint64_t per = (units + 7) / 8;
+    return (u % 8) * per + u / 8;
+}
+
+// The lane's share of tile j of chunk [start, start + len): vec(i) for its 8-element vector (when
+// inside the aligned body), then (tile 0) elem(i) for its head / tail element.
+template <typename Vec, typename Elem>
+__device__ __forceinline__ void for_tile(uint64_t start, uint64_t len, int j, Vec&& vec, Elem&& elem) {
     const uint64_t lane = threadIdx.x & 63;
     const uint64_t end = start + len;
     const uint64_t a = (start + kVec - 1) / kVec * kVec;      // aligned body [a, b)
     const uint64_t b = end / kVec * kVec;
-    if (a < b) {
-        for (uint64_t i = a + (uint64_t)slot * kWaveTile + lane * kVec; i < b; i += (uint64_t)kSlots * kWaveTile)
-            tile(i, b);
-    }
-    if (slot == 0) {
+    const uint64_t i = a + (uint64_t)j * kTileElems + lane * kVec;
+    if (a < b && i < b) vec(i);
+    if (j == 0) {
         const uint64_t h_end = a < end ? a : end;
         const uint64_t t_beg = b > a ? b : h_end;
         const uint64_t nh = h_end - start, nt = end - t_beg;
@@ -64,7 +78,7 @@ __device__ __forceinline__ void for_slot(uint64_t start, uint64_t len, int slot,
 // A wave's W totals (identical in every lane after the butterfly) as one contiguous store of W
 // doubles by lanes 0 .. W-1.
 template <int W>
-__device__ __forceinline__ void store_slot_row(double* row, const double (&v)[W]) {
+__device__ __forceinline__ void store_row(double* row, const double (&v)[W]) {
     const int lane = threadIdx.x & 63;
     double x = 0.0;
 #pragma unroll
@@ -73,76 +87,80 @@ __device__ __forceinline__ void store_slot_row(double* row, const double (&v)[W]
     if (lane < W) row[lane] = x;
 }
 
-// Chunk rows from the slot rows: rows[c][q] = sum over s in slot order of slots[c][s][q].
-__global__ __launch_bounds__(kBlock) void slot_reduce_kernel(const double* __restrict__ slots, int W,
-                                                             int64_t nchunks, double* __restrict__ rows) {
-    const uint64_t n = (uint64_t)nchunks * (uint64_t)W;
-    for (uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x; k < n; k += (uint64_t)gridDim.x * kBlock) {
-        const uint64_t c = k / (uint64_t)W, q = k % (uint64_t)W;
-        const double* p = slots + c * kSlots * (uint64_t)W + q;
-        double acc = 0.0;
-#pragma unroll 8
-        for (int s = 0; s < kSlots; ++s) acc += p[(uint64_t)s * W];
-        rows[k] = acc;
+// Per chunk, one wave: the chunk's W sums from its `nrows` rows (level log2(128 / nrows)), as the
+// perfect tree's upper levels — each lane combines its consecutive rows, then the ascending xor
+// butterfly (1, 2, 4, ...) pairs adjacent subtrees level by level. Rows of chunk c: unit
+// u = c * upc + r / rpu at row table slot unit_slot(u, nchunks * upc) * rpu + r % rpu.
+__global__ __launch_bounds__(kBlock) void tree_reduce_kernel(const double* __restrict__ rows, int W, int nrows,
+                                                             int upc, int rpu, int64_t nchunks,
+                                                             double* __restrict__ out) {
+    const uint64_t c = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (c >= (uint64_t)nchunks) return;
+    const uint64_t units = (uint64_t)nchunks * (uint64_t)upc;
+    const int per_lane = nrows > 64 ? nrows / 64 : 1;
+    const int lanes = nrows > 64 ? 64 : nrows;
+    for (int q = 0; q < W; ++q) {
+        double x = 0.0;
+        if (lane < lanes) {
+            for (int k = 0; k < per_lane; ++k) {              // per_lane is 1 or 2: a pair's sum
+                const int r = lane * per_lane + k;
+                const uint64_t u = c * (uint64_t)upc + (uint64_t)(r / rpu);
+                const double v = rows[(unit_slot(u, units) * (uint64_t)rpu + (uint64_t)(r % rpu)) * (uint64_t)W + q];
+                x = k == 0 ? v : x + v;
+            }
+        }
+        for (int o = 1; o < lanes; o <<= 1) x += __shfl_xor(x, o, 64);
+        if (lane == 0) out[c * (uint64_t)W + q] = x;
     }
 }
 
-inline int launch_slot_reduce(const double* slots, int W, int64_t nchunks, double* rows, hipStream_t s) {
-    const uint64_t n = (uint64_t)nchunks * (uint64_t)W;
-    uint64_t g = (n + kBlock - 1) / kBlock;
-    if (g < 1) g = 1;
-    if (g > 4096) g = 4096;
-    slot_reduce_kernel<<<(unsigned)g, kBlock, 0, s>>>(slots, W, nchunks, rows);
-    return check_launch("slot_reduce_kernel");
+inline int launch_tree_reduce(const double* rows, int W, int nrows, int upc, int rpu, int64_t nchunks, double* out,
+                              hipStream_t s) {
+    if (nchunks <= 0) return EDT_OK;
+    const uint64_t g = ((uint64_t)nchunks + kWavesPerBlock - 1) / kWavesPerBlock;
+    if (g > kGridBlockCap) return fail(EDT_ERR_ARG, "too many chunks for one launch");
+    tree_reduce_kernel<<<(unsigned)g, kBlock, 0, s>>>(rows, W, nrows, upc, rpu, nchunks, out);
+    return check_launch("tree_reduce_kernel");
 }
 
-// One wave slot of a pair's sums {v0.v0, v1.v1, v0.v1} (fp64, canonical order). EMIT = true also
-// writes the lerp-branch output l0 v0 + l1 v1 of the slot's elements (two rounded fp32 products,
-// one rounded sum: lerp_elems' math) in the same pass — the speculative forms.
+// The fp64 FMAs of a pair's sums {v0.v0, v1.v1, v0.v1} over N elements (canonical per-lane order).
+template <int N>
+__device__ __forceinline__ void pair_fma(const float* x, const float* y, double& s00, double& s11, double& s01) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        const double dx = x[j], dy = y[j];
+        s00 = __builtin_fma(dx, dx, s00);
+        s11 = __builtin_fma(dy, dy, s11);
+        s01 = __builtin_fma(dx, dy, s01);
+    }
+}
+
+// Tile j's pair sums (the tile sum in every lane). EMIT = true also writes the lerp-branch output
+// l0 v0 + l1 v1 of the tile (two rounded fp32 products, one rounded sum: lerp_elems' math) — the
+// speculative forms.
 template <int IDT, bool NT, bool EMIT, int ODT>
-__device__ __forceinline__ void pair_slot(const void* v0, const void* v1, void* out, uint64_t start, uint64_t len,
-                                          int slot, float l0, float l1, double (&sums)[3]) {
+__device__ __forceinline__ void pair_tile(const void* v0, const void* v1, void* out, uint64_t start, uint64_t len,
+                                          int j, float l0, float l1, double (&sums)[3]) {
     double s00 = 0.0, s11 = 0.0, s01 = 0.0;
-    auto acc = [&](auto tagN, const float* x, const float* y) {
-        constexpr int N = decltype(tagN)::value;
+    for_tile(start, len, j,
+        [&](uint64_t i) {
+            float x[kVec], y[kVec];
+            ld<IDT, kVec, NT>(v0, i, x);
+            ld<IDT, kVec, NT>(v1, i, y);
+            pair_fma<kVec>(x, y, s00, s11, s01);
+            if constexpr (EMIT) {
+                float o[kVec];
 #pragma unroll
-        for (int j = 0; j < N; ++j) {
-            const double dx = x[j], dy = y[j];
-            s00 = __builtin_fma(dx, dx, s00);
-            s11 = __builtin_fma(dy, dy, s11);
-            s01 = __builtin_fma(dx, dy, s01);
-        }
-    };
-    for_slot(start, len, slot,
-        [&](uint64_t i0, uint64_t b) {
-            float x[kWaveIters][kVec], y[kWaveIters][kVec];
-#pragma unroll
-            for (int k = 0; k < kWaveIters; ++k) {           // every load of the tile issued first
-                const uint64_t i = i0 + (uint64_t)k * 64 * kVec;
-                if (i < b) {
-                    ld<IDT, kVec, NT>(v0, i, x[k]);
-                    ld<IDT, kVec, NT>(v1, i, y[k]);
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < kWaveIters; ++k) {
-                const uint64_t i = i0 + (uint64_t)k * 64 * kVec;
-                if (i < b) {
-                    acc(std::integral_constant<int, kVec>{}, x[k], y[k]);
-                    if constexpr (EMIT) {
-                        float o[kVec];
-#pragma unroll
-                        for (int j = 0; j < kVec; ++j) o[j] = l0 * x[k][j] + l1 * y[k][j];
-                        st<ODT, kVec>(out, i, o);
-                    }
-                }
+                for (int e = 0; e < kVec; ++e) o[e] = l0 * x[e] + l1 * y[e];
+                st<ODT, kVec>(out, i, o);
             }
         },
         [&](uint64_t i) {
             float x[1], y[1];
             ld<IDT, 1>(v0, i, x);
             ld<IDT, 1>(v1, i, y);
-            acc(std::integral_constant<int, 1>{}, x, y);
+            pair_fma<1>(x, y, s00, s11, s01);
             if constexpr (EMIT) {
                 float o[1] = {l0 * x[0] + l1 * y[0]};
                 st<ODT, 1>(out, i, o);
@@ -151,6 +169,51 @@ __device__ __forceinline__ void pair_slot(const void* v0, const void* v1, void* 
     sums[0] = wave_sum(s00);
     sums[1] = wave_sum(s11);
     sums[2] = wave_sum(s01);
+}
+
+// Tiles 4 m .. 4 m + 3 of a chunk by one wave, read-only (the two-pass stats): the four tiles'
+// loads issued together, each tile's sums and butterfly as pair_tile's, combined in registers as
+// the tree does: (t0 + t1) + (t2 + t3) — a level-2 row.
+template <int IDT, bool NT>
+__device__ __forceinline__ void pair_tiles4(const void* v0, const void* v1, uint64_t start, uint64_t len, int m,
+                                            double (&sums)[3]) {
+    const uint64_t lane = threadIdx.x & 63;
+    const uint64_t end = start + len;
+    const uint64_t a = (start + kVec - 1) / kVec * kVec;
+    const uint64_t b = end / kVec * kVec;
+    float x[4][kVec], y[4][kVec];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint64_t i = a + (uint64_t)(4 * m + k) * kTileElems + lane * kVec;
+        if (a < b && i < b) {
+            ld<IDT, kVec, NT>(v0, i, x[k]);
+            ld<IDT, kVec, NT>(v1, i, y[k]);
+        }
+    }
+    double t[4][3];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        double s00 = 0.0, s11 = 0.0, s01 = 0.0;
+        const uint64_t i = a + (uint64_t)(4 * m + k) * kTileElems + lane * kVec;
+        if (a < b && i < b) pair_fma<kVec>(x[k], y[k], s00, s11, s01);
+        if (4 * m + k == 0) {                                // tile 0's head / tail elements
+            const uint64_t h_end = a < end ? a : end;
+            const uint64_t t_beg = b > a ? b : h_end;
+            const uint64_t nh = h_end - start, nt = end - t_beg;
+            if (lane < nh + nt) {
+                const uint64_t e = lane < nh ? start + lane : t_beg + (lane - nh);
+                float xe[1], ye[1];
+                ld<IDT, 1>(v0, e, xe);
+                ld<IDT, 1>(v1, e, ye);
+                pair_fma<1>(xe, ye, s00, s11, s01);
+            }
+        }
+        t[k][0] = wave_sum(s00);
+        t[k][1] = wave_sum(s11);
+        t[k][2] = wave_sum(s01);
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) sums[q] = (t[0][q] + t[1][q]) + (t[2][q] + t[3][q]);
 }
 
 // The reference's branch and coefficients (EDT_RL/crossover.py:31-45) for an fp32 dot, in fp32 as
@@ -220,23 +283,25 @@ __device__ __forceinline__ void for_range_elems(uint64_t start, uint64_t end, F&
         f(std::integral_constant<int, 1>{}, threadIdx.x < nh ? start + threadIdx.x : t_beg + (threadIdx.x - nh));
 }
 
-// The pair sums' slot rows (slots[c][slot][3]), one workgroup per (chunk, slot group), address
-// order. seg_ptrs (tensor-list form, may be null): per segment {v0, v1, out} device pointers;
-// chunk starts are then relative to their segment. Null: v0 / v1 / out are flat arenas.
-// EMIT (the speculative first pass, edt_slerp_merge_speculative): the same sums, and in the same
-// pass the lerp-branch output (1-t) v0 + t v1 with the coefficients slerp_coefficients gives that
-// branch. Parents of one lineage (fine-tunes of a common base) mostly have |dot| > 0.9995, where
-// this output is final; the other segments are blended again.
+// The pair sums' rows, one workgroup per unit in address order (unit_slot: XCD-major rows).
+// EMIT (the speculative first pass, edt_slerp_merge_speculative): unit = 4 tiles, one per wave
+// (level-0 rows), lerp's own grid; the lerp-branch output (1-t) v0 + t v1 with the coefficients
+// slerp_coefficients gives that branch is written in the same pass. Parents of one lineage
+// (fine-tunes of a common base) mostly have |dot| > 0.9995, where this output is final; the other
+// segments are blended again. Read-only (the two-pass stats): unit = 16 tiles, four per wave
+// (level-2 rows). seg_ptrs (tensor-list form, may be null): per segment {v0, v1, out} device
+// pointers; chunk starts are then relative to their segment. Null: flat arenas.
 template <int IDT, bool EMIT, int ODT>
 __global__ __launch_bounds__(kBlock) void pair_sums_kernel(const void* v0, const void* v1, void* out,
-                                                           const uint64_t* chunks, int64_t nchunks, double* slots,
+                                                           const uint64_t* chunks, int64_t nchunks, double* rows,
                                                            const double* tvals, const uint64_t* seg_ptrs) {
     constexpr bool NT = EDT_NT_SLERP != 0 && IDT == EDT_BF16;
+    constexpr int upc = EMIT ? kTileSlots / 4 : kTileSlots / 16;          // units per chunk
     const int wave = threadIdx.x >> 6;
-    const uint64_t units = (uint64_t)nchunks * kSlotGroups;
+    const uint64_t units = (uint64_t)nchunks * upc;
     for (uint64_t u = blockIdx.x; u < units; u += gridDim.x) {
-        const uint64_t c = u / kSlotGroups;
-        const int slot = (int)(u % kSlotGroups) * kWavesPerBlock + wave;
+        const uint64_t c = u / upc;
+        const int g = (int)(u % upc);
         const uint64_t seg = chunks[3 * c + 2];
         const void* a = v0;
         const void* b = v1;
@@ -246,24 +311,25 @@ __global__ __launch_bounds__(kBlock) void pair_sums_kernel(const void* v0, const
             b = reinterpret_cast<const void*>(seg_ptrs[3 * seg + 1]);
             o = reinterpret_cast<void*>(seg_ptrs[3 * seg + 2]);
         }
-        float l0 = 0.f, l1 = 0.f;
-        if constexpr (EMIT) {
-            l0 = (float)(1.0 - tvals[seg]);
-            l1 = (float)tvals[seg];
-        }
         double sums[3];
-        pair_slot<IDT, NT, EMIT, ODT>(a, b, o, chunks[3 * c], chunks[3 * c + 1], slot, l0, l1, sums);
-        store_slot_row<3>(slots + (c * kSlots + (uint64_t)slot) * 3, sums);
+        if constexpr (EMIT) {
+            pair_tile<IDT, NT, true, ODT>(a, b, o, chunks[3 * c], chunks[3 * c + 1], 4 * g + wave,
+                                          (float)(1.0 - tvals[seg]), (float)tvals[seg], sums);
+        } else {
+            pair_tiles4<IDT, NT>(a, b, chunks[3 * c], chunks[3 * c + 1], 4 * g + wave, sums);
+        }
+        store_row<3>(rows + (unit_slot(u, units) * kWavesPerBlock + wave) * 3, sums);
     }
 }
 
-// host: the pair sums into partial (rows [nchunks][3], then the slot scratch), EMIT optional
+// host: the pair sums into partial (chunk rows [nchunks][3], then the row scratch), EMIT optional
 int pair_sums(const void* v0, const void* v1, int in_dt, void* out, int out_dt, bool emit,
               const uint64_t* chunk_desc, int64_t nchunks, double* partial, const double* t,
               const uint64_t* seg_ptrs, hipStream_t s) {
-    double* slots = partial + 3 * (uint64_t)nchunks;
-    const unsigned g = slot_grid(nchunks);
-#define EDT_PS(I, E, O) pair_sums_kernel<I, E, O><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, slots, t, seg_ptrs)
+    double* rows = partial + 3 * (uint64_t)nchunks;
+    const int upc = emit ? kTileSlots / 4 : kTileSlots / 16;
+    const unsigned g = unit_grid((uint64_t)nchunks * upc);
+#define EDT_PS(I, E, O) pair_sums_kernel<I, E, O><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, rows, t, seg_ptrs)
     if (!emit) {
         if (in_dt == EDT_F32) EDT_PS(EDT_F32, false, EDT_F32);
         else EDT_PS(EDT_BF16, false, EDT_F32);
@@ -274,7 +340,8 @@ int pair_sums(const void* v0, const void* v1, int in_dt, void* out, int out_dt, 
 #undef EDT_PS
     int rc = check_launch(emit ? "pair_sums_kernel (speculative)" : "pair_sums_kernel");
     if (rc) return rc;
-    return launch_slot_reduce(slots, 3, nchunks, partial, s);
+    // rows per chunk: 128 (level 0, one per unit's wave) or 32 (level 2)
+    return launch_tree_reduce(rows, 3, upc * kWavesPerBlock, upc, kWavesPerBlock, nchunks, partial, s);
 }
 
 // Fixed-order reduction of a segment's chunk sums: column q of rows [c0, c1) of a row-major table
@@ -424,68 +491,85 @@ __device__ __forceinline__ void emit_children(const PopLerp& po, const float (&x
     }
 }
 
-// Gram slot rows (slots[c][slot][M(M+1)/2]), one workgroup per (chunk, slot group), address order.
-// EMIT (the member-major speculative pass, edt_slerp_population_speculative): each distinct parent's
-// vector is loaded ONCE into registers, its Gram sums accumulated and every child's lerp-branch
-// output written from the same registers — a shared parent crosses HBM once for all its children.
+// Gram rows (level 4), one workgroup per unit of 16 tiles in address order: wave w takes tiles
+// 16 g + 4 w .. + 3 one after the other (one vector per member per lane: M loads in flight), each
+// tile's sums butterflied as pair_tile's and parked in LDS; after the barrier wave 0's lanes
+// (one per sum) combine the 16 tile sums as the tree does and store the unit's row (unit_slot).
+// EMIT (the member-major speculative pass, edt_slerp_population_speculative): each distinct
+// parent's vector is loaded ONCE into registers, its Gram sums accumulated and every child's
+// lerp-branch output written from the same registers — a shared parent crosses HBM once for all
+// its children.
 template <int IDT, int M, bool EMIT, int ODT>
 __global__ __launch_bounds__(kBlock) void slerp_gram_kernel(Members mem, PopLerp po, const uint64_t* chunks,
-                                                            int64_t nchunks, const double* tvals, double* slots) {
+                                                            int64_t nchunks, const double* tvals, double* rows) {
     constexpr int NT = M * (M + 1) / 2;
-    const int wave = threadIdx.x >> 6;
-    const uint64_t units = (uint64_t)nchunks * kSlotGroups;
+    constexpr int upc = kTileSlots / 16;
+    __shared__ double ts[16][NT];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t units = (uint64_t)nchunks * upc;
     for (uint64_t u = blockIdx.x; u < units; u += gridDim.x) {
-        const uint64_t c = u / kSlotGroups;
-        const int slot = (int)(u % kSlotGroups) * kWavesPerBlock + wave;
+        const uint64_t c = u / upc;
+        const int g = (int)(u % upc);
+        const uint64_t start = chunks[3 * c], len = chunks[3 * c + 1];
         float l0 = 0.f, l1 = 0.f;
         if constexpr (EMIT) {
             const uint64_t seg = chunks[3 * c + 2];
             l0 = (float)(1.0 - tvals[seg]);
             l1 = (float)tvals[seg];
         }
-        double g[NT];
+#pragma unroll(M <= 2 ? 4 : 1)
+        for (int k = 0; k < 4; ++k) {
+            const int j = 16 * g + 4 * wave + k;
+            double gs[NT];
 #pragma unroll
-        for (int q = 0; q < NT; ++q) g[q] = 0.0;
-        for_slot(chunks[3 * c], chunks[3 * c + 1], slot,
-            [&](uint64_t i0, uint64_t b) {
-                // M <= 4: the tile's vectors unrolled; more members: one vector at a time (the
-                // member tiles and M(M+1)/2 accumulators already fill the register file)
-#pragma unroll(M <= 4 ? kWaveIters : 1)
-                for (int k = 0; k < kWaveIters; ++k) {
-                    const uint64_t i = i0 + (uint64_t)k * 64 * kVec;
-                    if (i < b) {
-                        float x[M][kVec];
+            for (int q = 0; q < NT; ++q) gs[q] = 0.0;
+            for_tile(start, len, j,
+                [&](uint64_t i) {
+                    float x[M][kVec];
 #pragma unroll
-                        for (int m = 0; m < M; ++m) ld<IDT, kVec>(mem.p[m], i, x[m]);   // default policy
-                        gram_fma<M, kVec>(x, g);
-                        if constexpr (EMIT) emit_children<ODT, M, kVec>(po, x, i, l0, l1);
-                    }
-                }
-            },
-            [&](uint64_t i) {
-                float x[M][1];
+                    for (int m = 0; m < M; ++m) ld<IDT, kVec>(mem.p[m], i, x[m]);   // default policy
+                    gram_fma<M, kVec>(x, gs);
+                    if constexpr (EMIT) emit_children<ODT, M, kVec>(po, x, i, l0, l1);
+                },
+                [&](uint64_t i) {
+                    float x[M][1];
 #pragma unroll
-                for (int m = 0; m < M; ++m) ld<IDT, 1>(mem.p[m], i, x[m]);
-                gram_fma<M, 1>(x, g);
-                if constexpr (EMIT) emit_children<ODT, M, 1>(po, x, i, l0, l1);
-            });
+                    for (int m = 0; m < M; ++m) ld<IDT, 1>(mem.p[m], i, x[m]);
+                    gram_fma<M, 1>(x, gs);
+                    if constexpr (EMIT) emit_children<ODT, M, 1>(po, x, i, l0, l1);
+                });
 #pragma unroll
-        for (int q = 0; q < NT; ++q) g[q] = wave_sum(g[q]);
-        store_slot_row<NT>(slots + (c * kSlots + (uint64_t)slot) * NT, g);
+            for (int q = 0; q < NT; ++q) gs[q] = wave_sum(gs[q]);
+            double v = 0.0;
+#pragma unroll
+            for (int q = 0; q < NT; ++q)
+                if (lane == q) v = gs[q];
+            if (lane < NT) ts[4 * wave + k][lane] = v;
+        }
+        __syncthreads();
+        if (wave == 0 && lane < NT) {
+            double t8[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) t8[i] = ts[2 * i][lane] + ts[2 * i + 1][lane];
+            const double q0 = (t8[0] + t8[1]) + (t8[2] + t8[3]), q1 = (t8[4] + t8[5]) + (t8[6] + t8[7]);
+            rows[unit_slot(u, units) * NT + lane] = q0 + q1;
+        }
+        __syncthreads();
     }
 }
 
-// host: the Gram sums of D compact members into gram (rows [nchunks][NT], then the slot scratch);
-// po != null: the member-major speculative pass (children's lerp-branch outputs written too)
+// host: the Gram sums of D compact members into gram (chunk rows [nchunks][NT], then the row
+// scratch); po != null: the member-major speculative pass (children's lerp-branch outputs too)
 inline int gram_sums(const Members& mem, int D, const PopLerp* po, int in_dt, int out_dt, const uint64_t* chunk_desc,
                      int64_t nchunks, const double* t, double* gram, hipStream_t s) {
     const int NT = D * (D + 1) / 2;
-    double* slots = gram + (uint64_t)nchunks * NT;
-    const unsigned g = slot_grid(nchunks);
+    double* rows = gram + (uint64_t)nchunks * NT;
+    constexpr int upc = kTileSlots / 16;
+    const unsigned g = unit_grid((uint64_t)nchunks * upc);
     PopLerp none;
     memset(&none, 0, sizeof(none));
     const PopLerp& P = po ? *po : none;
-#define EDT_GS(I, M, E, O) slerp_gram_kernel<I, M, E, O><<<g, kBlock, 0, s>>>(mem, P, chunk_desc, nchunks, t, slots)
+#define EDT_GS(I, M, E, O) slerp_gram_kernel<I, M, E, O><<<g, kBlock, 0, s>>>(mem, P, chunk_desc, nchunks, t, rows)
 #define EDT_GM(M)                                                                      \
     case M:                                                                            \
         if (!po) {                                                                     \
@@ -504,7 +588,7 @@ inline int gram_sums(const Members& mem, int D, const PopLerp* po, int in_dt, in
 #undef EDT_GS
     int rc = check_launch(po ? "slerp_gram_kernel (speculative)" : "slerp_gram_kernel");
     if (rc) return rc;
-    return launch_slot_reduce(slots, NT, nchunks, gram, s);
+    return launch_tree_reduce(rows, NT, kGramRows, upc, 1, nchunks, gram, s);
 }
 
 // The blends of every child in one launch, with pair_population_kernel's placement: the
@@ -518,7 +602,7 @@ struct BlendChildren {
     void* out[kBlendMaxChildren];
     const float* coef[kBlendMaxChildren];     // [nseg][2] of the child
     const int32_t* redo[kBlendMaxChildren];   // [nseg] of the child, or null: blend every segment
-    double* slots[kBlendMaxChildren];         // [nchunks][kSlots][3] of the child (speculative stats pass)
+    double* slots[kBlendMaxChildren];         // the child's level-0 rows (speculative stats pass)
     int nchildren;
 };
 
@@ -553,26 +637,29 @@ __global__ __launch_bounds__(kBlock) void slerp_blend_population_kernel(BlendChi
 }
 
 // Speculative population pass for more than 8 distinct parents: block (unit, child) with the
-// co-located placement above, a unit being one (chunk, slot group): the blocks of every child for
-// one unit carry the same blockIdx % 8 (one XCD, one L2). Each forms its child's slot rows exactly
-// as pair_slot() does and writes the lerp-branch output in the same pass (as the speculative pair
-// pass). Shared parents cross HBM once for all children.
+// co-located placement above, a unit being 4 tiles of a chunk (one per wave): the blocks of every
+// child for one unit carry the same blockIdx % 8 (one XCD, one L2). Each forms its child's tile
+// sums exactly as pair_tile() does (level-0 rows, the child's own row table) and writes the
+// lerp-branch output in the same pass. Shared parents cross HBM once for all children.
 template <int IDT, int ODT>
 __global__ __launch_bounds__(kBlock) void slerp_pop_stats_lerp_kernel(BlendChildren B, const uint64_t* chunks,
                                                                       int64_t nchunks, const double* tvals) {
+    constexpr int upc = kTileSlots / 4;
     const uint64_t per_group = 8ull * (uint64_t)B.nchildren;
     const uint64_t r = blockIdx.x % per_group;
     const int child = (int)(r / 8);
     const uint64_t u = (blockIdx.x / per_group) * 8 + (r % 8);
-    if (u >= (uint64_t)nchunks * kSlotGroups) return;
-    const uint64_t c = u / kSlotGroups;
-    const int slot = (int)(u % kSlotGroups) * kWavesPerBlock + (int)(threadIdx.x >> 6);
+    const uint64_t units = (uint64_t)nchunks * upc;
+    if (u >= units) return;
+    const uint64_t c = u / upc;
+    const int wave = (int)(threadIdx.x >> 6);
     const uint64_t seg = chunks[3 * c + 2];
     double sums[3];
     // default-policy loads: a parent's chunk is re-read by its other children from L2
-    pair_slot<IDT, false, true, ODT>(B.v0[child], B.v1[child], B.out[child], chunks[3 * c], chunks[3 * c + 1], slot,
-                                     (float)(1.0 - tvals[seg]), (float)tvals[seg], sums);
-    store_slot_row<3>(B.slots[child] + (c * kSlots + (uint64_t)slot) * 3, sums);
+    pair_tile<IDT, false, true, ODT>(B.v0[child], B.v1[child], B.out[child], chunks[3 * c], chunks[3 * c + 1],
+                                     (int)(u % upc) * kWavesPerBlock + wave, (float)(1.0 - tvals[seg]),
+                                     (float)tvals[seg], sums);
+    store_row<3>(B.slots[child] + (unit_slot(u, units) * kWavesPerBlock + wave) * 3, sums);
 }
 
 // Per segment for the pair (i, j): slerp_coef_kernel's reduction over the chunks, reading the
@@ -1028,6 +1115,8 @@ int64_t edt_slerp_make_chunks(const uint64_t* seg_offsets, int nseg, uint32_t ch
                               uint64_t* chunk_desc, int64_t max_chunks, int32_t* seg_first_chunk) {
     g_err[0] = 0;
     if (nseg < 0 || !seg_offsets || chunk_elems == 0) return fail(EDT_ERR_ARG, "bad segment table");
+    if (chunk_elems > kMaxChunkElems)       // the sums' canonical tree spans 128 tiles of 512
+        return fail(EDT_ERR_ARG, "chunk_elems %u above %u", chunk_elems, kMaxChunkElems);
     int64_t c = 0;
     for (int s = 0; s < nseg; ++s) {
         if (seg_first_chunk) seg_first_chunk[s] = (int32_t)c;
@@ -1102,14 +1191,19 @@ int edt_slerp_merge(const void* v0, const void* v1, int in_dt, void* out, int ou
 }
 
 uint64_t edt_slerp_sums_doubles(int width, int64_t nchunks) {
+    // the chunk rows + the largest row scratch a pass writes for this width: level-0 rows (one per
+    // tile) for the pair passes (width 3), level-4 rows for the Gram passes
     if (width < 1 || nchunks < 0) return 0;
-    return (uint64_t)nchunks * (uint64_t)width * (1ull + (uint64_t)kSlots);
+    const uint64_t rows = width <= 3 ? kPairRows : kGramRows;
+    return (uint64_t)nchunks * (uint64_t)width * (1ull + rows);
 }
 
 uint64_t edt_slerp_population_speculative_doubles(int npairs, int64_t nchunks) {
     if (npairs < 0 || nchunks < 0) return 0;
-    const uint64_t per = 3ull * (uint64_t)npairs > 36ull ? 3ull * (uint64_t)npairs : 36ull;   // 36: 8 x 9 / 2
-    return (uint64_t)nchunks * per * (1ull + (uint64_t)kSlots);
+    // co-located per-child form: each child's chunk rows + level-0 rows; member-major: <= 36 Gram sums
+    const uint64_t pair = 3ull * (uint64_t)npairs * (1ull + kPairRows);
+    const uint64_t gram = 36ull * (1ull + kGramRows);                    // 36: 8 x 9 / 2
+    return (uint64_t)nchunks * (pair > gram ? pair : gram);
 }
 
 uint64_t edt_slerp_population_gram_doubles(int nmembers, int64_t nchunks) {
@@ -1426,10 +1520,10 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
                 B.out[k] = outs[q];
                 B.coef[k] = coef + 2 * (size_t)nseg * q;
                 B.redo[k] = redo + (size_t)nseg * q;
-                B.slots[k] = partial + 3 * (size_t)nchunks * npairs + 3 * (size_t)kSlots * nchunks * q;
+                B.slots[k] = partial + 3 * (size_t)nchunks * npairs + 3 * (size_t)kPairRows * nchunks * q;
             }
             // pass 0: one block per (unit = chunk x slot group, child); pass 1: per (chunk, child)
-            const uint64_t units = pass == 0 ? (uint64_t)nchunks * kSlotGroups : (uint64_t)nchunks;
+            const uint64_t units = pass == 0 ? (uint64_t)nchunks * (kTileSlots / 4) : (uint64_t)nchunks;
             const uint64_t blocks = (units + 7) / 8 * 8ull * (uint64_t)B.nchildren;
             if (blocks > kGridBlockCap) return fail(EDT_ERR_ARG, "too many chunks for one launch");
             const unsigned gb = (unsigned)blocks;
@@ -1448,8 +1542,9 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
         }
         if (pass == 0) {
             for (int q = 0; q < npairs; ++q) {
-                int rc = launch_slot_reduce(partial + 3 * (size_t)nchunks * npairs + 3 * (size_t)kSlots * nchunks * q, 3,
-                                            nchunks, partial + 3 * (size_t)nchunks * q, s);
+                int rc = launch_tree_reduce(partial + 3 * (size_t)nchunks * npairs + 3 * (size_t)kPairRows * nchunks * q, 3,
+                                            kPairRows, kTileSlots / 4, kWavesPerBlock, nchunks,
+                                            partial + 3 * (size_t)nchunks * q, s);
                 if (rc) return rc;
                 slerp_coef_kernel<<<coef_grid(nseg), kBlock, 0, s>>>(
                     partial + 3 * (size_t)nchunks * q, seg_first_chunk, nseg, t, (float)dot_threshold, (float)eps,

@@ -171,7 +171,8 @@ int edt_lerp(const void* v0, const void* v1, int in_dt, void* out, int out_dt, i
  * [seg_offsets[s], seg_offsets[s+1]). Work is cut into chunks that never cross a segment.
  *
  * edt_slerp_make_chunks (HOST function): fills chunk_desc (3 uint64 per chunk:
- *   start, length, segment) and seg_first_chunk (nseg+1) for chunk length `chunk_elems`;
+ *   start, length, segment) and seg_first_chunk (nseg+1) for chunk length `chunk_elems`
+ *   (<= 65536: a chunk's sums are a fixed tree over at most 128 tiles of 512 elements);
  *   returns the chunk count, or the required count (negated - 1) if max_chunks is too small. */
 int64_t edt_slerp_make_chunks(const uint64_t* seg_offsets_host, int nseg, uint32_t chunk_elems,
                               uint64_t* chunk_desc_host, int64_t max_chunks,

@@ -14,6 +14,10 @@
 //   w1lo        fp64 sums per lane, no butterfly, no store (NaN-guarded): the per-lane math alone
 //   lerp4       lerp with 4 vectors per lane
 //   w4plain     w4 with default-policy loads
+//   w1p128 / w4p128 / w4p64   the row padded to a whole 128-B (64-B) line, written by one wave
+//   w4p128nt    the same with a non-temporal row store
+//   w1x / w4x   rows placed XCD-major (the rows of the workgroups one XCD runs are contiguous, so
+//               its L2 fills whole lines before writing back)
 //
 //   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -o scripts/_spec_probe scripts/spec_probe.hip
 //   scripts/_spec_probe [n_elements] [rounds]
@@ -60,7 +64,9 @@ __device__ __forceinline__ float wsumf(float x) {
 }
 
 // MODE: 0 lerp, 1 fp64 sums + butterfly, 2 fp32 sums + butterfly, 3 fp64 no butterfly, 4 = 1 + table,
-// 5 = 1 with the row store NaN-guarded, 6 = per-lane fp64 sums NaN-guarded (no butterfly)
+// 5 = 1 with the row store NaN-guarded, 6 = per-lane fp64 sums NaN-guarded (no butterfly),
+// 7 / 8 = 1 with the row padded to 16 / 8 doubles (a whole 128-B / 64-B line per wave), 9 = 7 + nt store,
+// 10 = 1 with XCD-major row placement
 // EMIT: write the lerp output; IT: vectors per lane; NTL: non-temporal loads
 template <int MODE, bool EMIT, int IT, bool NTL = true>
 __global__ __launch_bounds__(256) void k(const uint16_t* __restrict__ a, const uint16_t* __restrict__ b,
@@ -143,6 +149,22 @@ __global__ __launch_bounds__(256) void k(const uint16_t* __restrict__ a, const u
         if (v != v) rows[row + lane] = v;
         return;
     }
+    if constexpr (MODE == 7 || MODE == 8 || MODE == 9) {
+        constexpr int W = MODE == 8 ? 8 : 16;
+        const uint64_t prow = ((uint64_t)blockIdx.x * 4 + wave) * W;
+        const double pv = lane < 3 ? v : 0.0;
+        if (lane < W) {
+            if constexpr (MODE == 9) __builtin_nontemporal_store(pv, rows + prow + lane);
+            else rows[prow + lane] = pv;
+        }
+        return;
+    }
+    if constexpr (MODE == 10) {
+        const uint64_t G = gridDim.x, b = blockIdx.x, per = (G + 7) / 8;
+        const uint64_t xrow = ((b % 8) * per + b / 8) * 4 + wave;
+        if (lane < 3) rows[xrow * 3 + lane] = v;
+        return;
+    }
     if (lane < 3) rows[row + lane] = v;
 }
 
@@ -158,7 +180,7 @@ int main(int argc, char** argv) {
     CHECK(hipMemset(a, 0x3c, n * 2));
     CHECK(hipMemset(b, 0x3d, n * 2));
     const uint64_t tiles1 = (n + 2047) / 2048, tiles4 = (n + 8191) / 8192;
-    CHECK(hipMalloc(&rows, tiles1 * 4 * 3 * 8));
+    CHECK(hipMalloc(&rows, tiles1 * 4 * 16 * 8));
     std::vector<uint64_t> ht(3 * tiles1);
     for (uint64_t t = 0; t < tiles1; ++t) { ht[3 * t] = t * 2048; ht[3 * t + 1] = 2048; ht[3 * t + 2] = 0; }
     CHECK(hipMalloc(&tab, ht.size() * 8));
@@ -179,6 +201,15 @@ int main(int argc, char** argv) {
         {"lerp4", 6, [&] { k<0, true, 4><<<g4, 256>>>(a, b, o, n, tab, rows); }},
         {"w4plain", 6, [&] { k<1, true, 4, false><<<g4, 256>>>(a, b, o, n, tab, rows); }},
         {"lerp_plain", 6, [&] { k<0, true, 1, false><<<g1, 256>>>(a, b, o, n, tab, rows); }},
+        {"w1p128", 6, [&] { k<7, true, 1><<<g1, 256>>>(a, b, o, n, tab, rows); }},
+        {"w4p128", 6, [&] { k<7, true, 4><<<g4, 256>>>(a, b, o, n, tab, rows); }},
+        {"w4p64", 6, [&] { k<8, true, 4><<<g4, 256>>>(a, b, o, n, tab, rows); }},
+        {"w4p128nt", 6, [&] { k<9, true, 4><<<g4, 256>>>(a, b, o, n, tab, rows); }},
+        {"s4p128", 4, [&] { k<7, false, 4><<<g4, 256>>>(a, b, o, n, tab, rows); }},
+        {"w1x", 6, [&] { k<10, true, 1><<<g1, 256>>>(a, b, o, n, tab, rows); }},
+        {"w4x", 6, [&] { k<10, true, 4><<<g4, 256>>>(a, b, o, n, tab, rows); }},
+        {"w2x", 6, [&] { k<10, true, 2><<<(unsigned)((n + 4095) / 4096), 256>>>(a, b, o, n, tab, rows); }},
+        {"s4x", 4, [&] { k<10, false, 4><<<g4, 256>>>(a, b, o, n, tab, rows); }},
     };
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
