@@ -274,13 +274,17 @@ class DirOuterSync:
     carry_inner_state: EDT_LM/diloco.py:295-300 — before the new weights are written, each
     worker's previous-generation `optimizer.pt` / `scheduler.pt` (step(prev_dirs=...), GenN of
     every machine) is copied over the one its inner loop left in its GenN+1 dir, where it exists,
-    so the next inner loop resumes the inner optimiser as the reference's does."""
+    so the next inner loop resumes the inner optimiser as the reference's does.
+    place_momentum: after the first step, choose the outer momentum's HBM placement by measurement
+    once (OuterSync.place_momentum; 0 = keep the first allocation). The θ and worker arenas stay
+    resident across generations here, so the choice holds for the rest of the run — the drop-in
+    form of the resident flow's placement."""
 
     INNER_STATE_FILES = ("optimizer.pt", "scheduler.pt")
 
     def __init__(self, device=None, theta_dtype=None, worker_dtype=None, names=None,
                  lr=0.7, momentum=0.9, nesterov=True, state: OuterState | None = None,
-                 state_path: str | None = None, carry_inner_state: bool = False):
+                 state_path: str | None = None, carry_inner_state: bool = False, place_momentum: int = 0):
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.theta_dtype, self.worker_dtype, self.names = theta_dtype, worker_dtype, names
         self.lr, self.momentum, self.nesterov = lr, momentum, nesterov
@@ -291,6 +295,8 @@ class DirOuterSync:
         self._written: set[str] = set()     # dirs holding the resident theta (last step's output)
         self.state_path = state_path
         self.carry_inner_state = carry_inner_state
+        self.place_candidates = place_momentum
+        self.placement = None             # the placement search's report, once it has run
 
     def _layout_from(self, model_dir):
         from .checkpoint import checkpoint_files, read_header, _ST_DTYPES
@@ -329,8 +335,13 @@ class DirOuterSync:
         if os.path.abspath(base_dir) not in self._written:   # else theta is already resident
             items.insert(0, (base_dir, self.theta.flat))
         read_many(items, self.layout, self.names)        # the K + 1 checkpoints read in parallel
-        _step_flat(self.theta.flat, [w.flat for w in self.workers[:len(worker_dirs)]], self.state,
-                   self.lr, self.momentum, self.nesterov)
+        workers = [w.flat for w in self.workers[:len(worker_dirs)]]
+        _step_flat(self.theta.flat, workers, self.state, self.lr, self.momentum, self.nesterov)
+        if self.place_candidates > 1 and self.placement is None and self.momentum != 0 \
+                and self.theta.flat.device.type == "cuda":
+            from .placement import place_momentum
+            self.state.momentum, self.placement = place_momentum(self.theta.flat, workers, self.state.momentum,
+                                                                 self.place_candidates)
         out_dirs = worker_dirs if out_dirs is None else out_dirs
         if self.carry_inner_state:          # diloco.py:295-300, before the model write as there
             for source, target in zip(prev_dirs, worker_dirs):

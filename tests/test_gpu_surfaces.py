@@ -316,6 +316,51 @@ def test_dir_outer_sync_two_generations(oracle, dev, tmp_path):
     assert torch.equal(bits(sync.state.momentum.cpu()), bits(mom))
 
 
+def test_dir_outer_sync_placed_momentum_and_inner_state_carry(oracle, dev, tmp_path):
+    """DirOuterSync(place_momentum=8, carry_inner_state=True): the momentum moved once after the
+    first step (resident arenas, so the placement holds), every later generation bit-identical to
+    the oracle; each GenN+1 dir ends with its machine's GenN optimizer.pt / scheduler.pt
+    (EDT_LM/diloco.py:295-300)."""
+    from transformers import LlamaForCausalLM
+    from evolutionarydistributedtraining_amd.diloco import DirOuterSync
+    from evolutionarydistributedtraining_amd.params import ParamLayout, pack
+    K = 2
+    base = _llama([p.detach() for p in _llama([]).parameters()], torch.bfloat16)
+    g = torch.Generator().manual_seed(22)
+    with torch.no_grad():
+        for p in base.parameters():
+            p.copy_(torch.randn(p.shape, generator=g) * 0.02)
+    layout = ParamLayout.of_module(base)
+    for k in range(K):
+        base.save_pretrained(tmp_path / f"w{k}" / "Gen0000")
+        (tmp_path / f"w{k}" / "Gen0000" / "optimizer.pt").write_bytes(f"opt w{k} g0".encode())
+        (tmp_path / f"w{k}" / "Gen0000" / "scheduler.pt").write_bytes(f"sch w{k} g0".encode())
+    sync = DirOuterSync(device=dev, names=layout.names, lr=0.7, momentum=0.9, nesterov=True,
+                        carry_inner_state=True, place_momentum=8)
+    theta = pack(list(base.parameters()))
+    mom = torch.zeros_like(theta)
+    prev = [str(tmp_path / f"w{k}" / "Gen0000") for k in range(K)]
+    for gen in range(3):
+        dirs, workers = [], []
+        for k in range(K):
+            d = tmp_path / f"w{k}" / f"Gen{gen + 1:04d}"
+            m = _llama([(t.float() + torch.randn(t.shape, generator=g) * 1e-3).bfloat16()
+                        for t in layout.views(theta)])
+            m.save_pretrained(d)
+            (d / "optimizer.pt").write_bytes(f"opt w{k} g{gen + 1}".encode())
+            dirs.append(str(d))
+            workers.append(pack(list(m.parameters())))
+        sync.step(prev[0], dirs, prev_dirs=prev)
+        oracle.outer_step(theta, workers, mom, gen > 0, 0.7, 0.9, True)
+        for k, d in enumerate(dirs):
+            got = LlamaForCausalLM.from_pretrained(d, dtype=torch.bfloat16)
+            assert torch.equal(bits(pack(list(got.parameters()))), bits(theta)), (gen, d)
+            assert (tmp_path / f"w{k}" / f"Gen{gen + 1:04d}" / "optimizer.pt").read_bytes() == f"opt w{k} g0".encode()
+        assert sync.placement is not None and sync.placement["candidates"] >= 1
+        prev = dirs
+    assert torch.equal(bits(sync.state.momentum.cpu()), bits(mom))
+
+
 @pytest.mark.parametrize("wdt", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("mode,broadcast", [("reduce", "theta"), ("exact", "theta"), ("exact", "workers")])
 def test_sharded_outer_step_rccl_world1(oracle, dev, tmp_path, mode, broadcast, wdt):

@@ -9,7 +9,13 @@ The reference decides from an fp32 dot (BLAS norms + a pairwise fp32 sum) that i
 four of the large cases do). Then the output follows the accurate dot's branch, and differs from
 the reference's by exactly the two coefficient sets' gap: |out - ref| <= |dc0||v0| + |dc1||v1|
 + 2e-6 (|c0 v0| + |c1 v1|), dc from the two dots (fp64 formula). Where the branches agree that
-bound is the usual SLERP bar, and the lerp branch is bit-exact."""
+bound is the usual SLERP bar, and the lerp branch is bit-exact.
+
+That is the DEFAULT path's contract. Parity with the reference's own branch decision is the
+reference-dot mode (ops.RefDot, merge.set_reference_dot): the device recomputes the reference's
+fp32 dot bit for bit, so all 24 cases take the reference's branch and every output is within the
+ordinary 2e-6 SLERP bar of the reference's (lerp branch bit for bit) —
+tests/test_gpu_refdot.py::test_refdot_mode_takes_the_reference_branch_at_threshold."""
 import json
 import math
 import os
