@@ -124,9 +124,48 @@ inline int launch_tree_reduce(const double* rows, int W, int nrows, int upc, int
     return check_launch("tree_reduce_kernel");
 }
 
+// 8 consecutive elements held as loaded (bf16: one 16-B word, unpacked per element on use), so a
+// wave keeps several vectors in flight on few registers.
+template <int IDT>
+struct Raw8;
+template <>
+struct Raw8<EDT_BF16> {
+    u32x4 w;
+    __device__ __forceinline__ float operator[](int j) const {
+        const uint32_t x = (j >> 1) == 0 ? w.x : (j >> 1) == 1 ? w.y : (j >> 1) == 2 ? w.z : w.w;
+        return (j & 1) ? bf_hi(x) : bf_lo(x);
+    }
+};
+template <>
+struct Raw8<EDT_F32> {
+    f32x4 lo, hi;
+    __device__ __forceinline__ float operator[](int j) const {
+        const f32x4& v = j < 4 ? lo : hi;
+        return (j & 3) == 0 ? v.x : (j & 3) == 1 ? v.y : (j & 3) == 2 ? v.z : v.w;
+    }
+};
+
+struct Raw1 {                                        // one element, the same indexing
+    float v[1];
+    __device__ __forceinline__ float operator[](int) const { return v[0]; }
+};
+
+template <int IDT, bool NT>
+__device__ __forceinline__ Raw8<IDT> ld_raw(const void* p, uint64_t i) {
+    Raw8<IDT> r;
+    if constexpr (IDT == EDT_BF16) {
+        r.w = vload<u32x4, NT>(reinterpret_cast<const u32x4*>(static_cast<const uint16_t*>(p) + i));
+    } else {
+        const float* q = static_cast<const float*>(p) + i;
+        r.lo = vload<f32x4, NT>(reinterpret_cast<const f32x4*>(q));
+        r.hi = vload<f32x4, NT>(reinterpret_cast<const f32x4*>(q + 4));
+    }
+    return r;
+}
+
 // The fp64 FMAs of a pair's sums {v0.v0, v1.v1, v0.v1} over N elements (canonical per-lane order).
-template <int N>
-__device__ __forceinline__ void pair_fma(const float* x, const float* y, double& s00, double& s11, double& s01) {
+template <int N, typename X, typename Y>
+__device__ __forceinline__ void pair_fma(const X& x, const Y& y, double& s00, double& s11, double& s01) {
 #pragma unroll
     for (int j = 0; j < N; ++j) {
         const double dx = x[j], dy = y[j];
@@ -136,6 +175,19 @@ __device__ __forceinline__ void pair_fma(const float* x, const float* y, double&
     }
 }
 
+// Tile 0's head / tail element of this lane, if any: elem(i).
+template <typename Elem>
+__device__ __forceinline__ void tile0_edge(uint64_t start, uint64_t len, Elem&& elem) {
+    const uint64_t lane = threadIdx.x & 63;
+    const uint64_t end = start + len;
+    const uint64_t a = (start + kVec - 1) / kVec * kVec;
+    const uint64_t b = end / kVec * kVec;
+    const uint64_t h_end = a < end ? a : end;
+    const uint64_t t_beg = b > a ? b : h_end;
+    const uint64_t nh = h_end - start, nt = end - t_beg;
+    if (lane < nh + nt) elem(lane < nh ? start + lane : t_beg + (lane - nh));
+}
+
 // Tile j's pair sums (the tile sum in every lane). EMIT = true also writes the lerp-branch output
 // l0 v0 + l1 v1 of the tile (two rounded fp32 products, one rounded sum: lerp_elems' math) — the
 // speculative forms.
@@ -143,27 +195,27 @@ template <int IDT, bool NT, bool EMIT, int ODT>
 __device__ __forceinline__ void pair_tile(const void* v0, const void* v1, void* out, uint64_t start, uint64_t len,
                                           int j, float l0, float l1, double (&sums)[3]) {
     double s00 = 0.0, s11 = 0.0, s01 = 0.0;
-    for_tile(start, len, j,
-        [&](uint64_t i) {
-            float x[kVec], y[kVec];
-            ld<IDT, kVec, NT>(v0, i, x);
-            ld<IDT, kVec, NT>(v1, i, y);
-            pair_fma<kVec>(x, y, s00, s11, s01);
-            if constexpr (EMIT) {
-                float o[kVec];
+    const uint64_t a = (start + kVec - 1) / kVec * kVec, b = (start + len) / kVec * kVec;
+    const uint64_t i = a + (uint64_t)j * kTileElems + (uint64_t)(threadIdx.x & 63) * kVec;
+    if (a < b && i < b) {
+        const Raw8<IDT> x = ld_raw<IDT, NT>(v0, i), y = ld_raw<IDT, NT>(v1, i);
+        pair_fma<kVec>(x, y, s00, s11, s01);
+        if constexpr (EMIT) {
+            float o[kVec];
 #pragma unroll
-                for (int e = 0; e < kVec; ++e) o[e] = l0 * x[e] + l1 * y[e];
-                st<ODT, kVec>(out, i, o);
-            }
-        },
-        [&](uint64_t i) {
+            for (int e = 0; e < kVec; ++e) o[e] = l0 * x[e] + l1 * y[e];
+            st<ODT, kVec>(out, i, o);
+        }
+    }
+    if (j == 0)
+        tile0_edge(start, len, [&](uint64_t e) {
             float x[1], y[1];
-            ld<IDT, 1>(v0, i, x);
-            ld<IDT, 1>(v1, i, y);
+            ld<IDT, 1>(v0, e, x);
+            ld<IDT, 1>(v1, e, y);
             pair_fma<1>(x, y, s00, s11, s01);
             if constexpr (EMIT) {
                 float o[1] = {l0 * x[0] + l1 * y[0]};
-                st<ODT, 1>(out, i, o);
+                st<ODT, 1>(out, e, o);
             }
         });
     sums[0] = wave_sum(s00);
@@ -177,37 +229,29 @@ __device__ __forceinline__ void pair_tile(const void* v0, const void* v1, void* 
 template <int IDT, bool NT>
 __device__ __forceinline__ void pair_tiles4(const void* v0, const void* v1, uint64_t start, uint64_t len, int m,
                                             double (&sums)[3]) {
-    const uint64_t lane = threadIdx.x & 63;
-    const uint64_t end = start + len;
-    const uint64_t a = (start + kVec - 1) / kVec * kVec;
-    const uint64_t b = end / kVec * kVec;
-    float x[4][kVec], y[4][kVec];
+    const uint64_t a = (start + kVec - 1) / kVec * kVec, b = (start + len) / kVec * kVec;
+    const uint64_t i0 = a + (uint64_t)(4 * m) * kTileElems + (uint64_t)(threadIdx.x & 63) * kVec;
+    Raw8<IDT> x[4], y[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const uint64_t i = a + (uint64_t)(4 * m + k) * kTileElems + lane * kVec;
+        const uint64_t i = i0 + (uint64_t)k * kTileElems;
         if (a < b && i < b) {
-            ld<IDT, kVec, NT>(v0, i, x[k]);
-            ld<IDT, kVec, NT>(v1, i, y[k]);
+            x[k] = ld_raw<IDT, NT>(v0, i);
+            y[k] = ld_raw<IDT, NT>(v1, i);
         }
     }
     double t[4][3];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         double s00 = 0.0, s11 = 0.0, s01 = 0.0;
-        const uint64_t i = a + (uint64_t)(4 * m + k) * kTileElems + lane * kVec;
-        if (a < b && i < b) pair_fma<kVec>(x[k], y[k], s00, s11, s01);
-        if (4 * m + k == 0) {                                // tile 0's head / tail elements
-            const uint64_t h_end = a < end ? a : end;
-            const uint64_t t_beg = b > a ? b : h_end;
-            const uint64_t nh = h_end - start, nt = end - t_beg;
-            if (lane < nh + nt) {
-                const uint64_t e = lane < nh ? start + lane : t_beg + (lane - nh);
+        if (a < b && i0 + (uint64_t)k * kTileElems < b) pair_fma<kVec>(x[k], y[k], s00, s11, s01);
+        if (4 * m + k == 0)
+            tile0_edge(start, len, [&](uint64_t e) {
                 float xe[1], ye[1];
                 ld<IDT, 1>(v0, e, xe);
                 ld<IDT, 1>(v1, e, ye);
                 pair_fma<1>(xe, ye, s00, s11, s01);
-            }
-        }
+            });
         t[k][0] = wave_sum(s00);
         t[k][1] = wave_sum(s11);
         t[k][2] = wave_sum(s01);
@@ -294,12 +338,14 @@ __device__ __forceinline__ void for_range_elems(uint64_t start, uint64_t end, F&
 template <int IDT, bool EMIT, int ODT>
 __global__ __launch_bounds__(kBlock) void pair_sums_kernel(const void* v0, const void* v1, void* out,
                                                            const uint64_t* chunks, int64_t nchunks, double* rows,
-                                                           const double* tvals, const uint64_t* seg_ptrs) {
+                                                           const double* tvals, const uint64_t* seg_ptrs, uint64_t u0) {
     constexpr bool NT = EDT_NT_SLERP != 0 && IDT == EDT_BF16;
     constexpr int upc = EMIT ? kTileSlots / 4 : kTileSlots / 16;          // units per chunk
     const int wave = threadIdx.x >> 6;
     const uint64_t units = (uint64_t)nchunks * upc;
-    for (uint64_t u = blockIdx.x; u < units; u += gridDim.x) {
+    {   // one unit per workgroup (no grid-stride loop: it costs registers, i.e. occupancy)
+        const uint64_t u = u0 + blockIdx.x;
+        if (u >= units) return;
         const uint64_t c = u / upc;
         const int g = (int)(u % upc);
         const uint64_t seg = chunks[3 * c + 2];
@@ -328,18 +374,21 @@ int pair_sums(const void* v0, const void* v1, int in_dt, void* out, int out_dt, 
               const uint64_t* seg_ptrs, hipStream_t s) {
     double* rows = partial + 3 * (uint64_t)nchunks;
     const int upc = emit ? kTileSlots / 4 : kTileSlots / 16;
-    const unsigned g = unit_grid((uint64_t)nchunks * upc);
-#define EDT_PS(I, E, O) pair_sums_kernel<I, E, O><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, rows, t, seg_ptrs)
-    if (!emit) {
-        if (in_dt == EDT_F32) EDT_PS(EDT_F32, false, EDT_F32);
-        else EDT_PS(EDT_BF16, false, EDT_F32);
-    } else if (in_dt == EDT_F32 && out_dt == EDT_F32) EDT_PS(EDT_F32, true, EDT_F32);
-    else if (in_dt == EDT_F32) EDT_PS(EDT_F32, true, EDT_BF16);
-    else if (out_dt == EDT_F32) EDT_PS(EDT_BF16, true, EDT_F32);
-    else EDT_PS(EDT_BF16, true, EDT_BF16);
+    const uint64_t units = (uint64_t)nchunks * upc;
+    for (uint64_t u0 = 0; u0 < units; u0 += kUnitGridCap) {       // > 16.7M units: several launches
+        const unsigned g = unit_grid(units - u0);
+#define EDT_PS(I, E, O) pair_sums_kernel<I, E, O><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, rows, t, seg_ptrs, u0)
+        if (!emit) {
+            if (in_dt == EDT_F32) EDT_PS(EDT_F32, false, EDT_F32);
+            else EDT_PS(EDT_BF16, false, EDT_F32);
+        } else if (in_dt == EDT_F32 && out_dt == EDT_F32) EDT_PS(EDT_F32, true, EDT_F32);
+        else if (in_dt == EDT_F32) EDT_PS(EDT_F32, true, EDT_BF16);
+        else if (out_dt == EDT_F32) EDT_PS(EDT_BF16, true, EDT_F32);
+        else EDT_PS(EDT_BF16, true, EDT_BF16);
 #undef EDT_PS
-    int rc = check_launch(emit ? "pair_sums_kernel (speculative)" : "pair_sums_kernel");
-    if (rc) return rc;
+        int rc = check_launch(emit ? "pair_sums_kernel (speculative)" : "pair_sums_kernel");
+        if (rc) return rc;
+    }
     // rows per chunk: 128 (level 0, one per unit's wave) or 32 (level 2)
     return launch_tree_reduce(rows, 3, upc * kWavesPerBlock, upc, kWavesPerBlock, nchunks, partial, s);
 }
@@ -446,8 +495,8 @@ __host__ __device__ constexpr int tri_index(int a, int b, int M) {   // a <= b <
     return a * M - a * (a - 1) / 2 + (b - a);
 }
 
-template <int M, int N>
-__device__ __forceinline__ void gram_fma(const float (&x)[M][N], double (&g)[M * (M + 1) / 2]) {
+template <int M, int N, typename X>
+__device__ __forceinline__ void gram_fma(const X (&x)[M], double (&g)[M * (M + 1) / 2]) {
 #pragma unroll
     for (int j = 0; j < N; ++j) {
 #pragma unroll
@@ -479,12 +528,20 @@ __device__ __forceinline__ void pick(const float (&x)[M][N], int idx, float (&y)
         }
 }
 
-template <int ODT, int M, int N>
-__device__ __forceinline__ void emit_children(const PopLerp& po, const float (&x)[M][N], uint64_t i, float l0, float l1) {
+template <int M, typename X>
+__device__ __forceinline__ X pick_one(const X (&x)[M], int idx) {
+    X y = x[0];
+#pragma unroll
+    for (int m = 1; m < M; ++m)
+        if (m == idx) y = x[m];          // idx is uniform across the workgroup: no divergence
+    return y;
+}
+
+template <int ODT, int M, int N, typename X>
+__device__ __forceinline__ void emit_children(const PopLerp& po, const X (&x)[M], uint64_t i, float l0, float l1) {
     for (int q = 0; q < po.n; ++q) {
-        float u[N], v[N], o[N];
-        pick<M, N>(x, po.a[q], u);
-        pick<M, N>(x, po.b[q], v);
+        const X u = pick_one<M>(x, po.a[q]), v = pick_one<M>(x, po.b[q]);
+        float o[N];
 #pragma unroll
         for (int j = 0; j < N; ++j) o[j] = l0 * u[j] + l1 * v[j];
         st<ODT, N>(po.out[q], i, o);
@@ -501,13 +558,16 @@ __device__ __forceinline__ void emit_children(const PopLerp& po, const float (&x
 // its children.
 template <int IDT, int M, bool EMIT, int ODT>
 __global__ __launch_bounds__(kBlock) void slerp_gram_kernel(Members mem, PopLerp po, const uint64_t* chunks,
-                                                            int64_t nchunks, const double* tvals, double* rows) {
+                                                            int64_t nchunks, const double* tvals, double* rows,
+                                                            uint64_t u0) {
     constexpr int NT = M * (M + 1) / 2;
     constexpr int upc = kTileSlots / 16;
     __shared__ double ts[16][NT];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t units = (uint64_t)nchunks * upc;
-    for (uint64_t u = blockIdx.x; u < units; u += gridDim.x) {
+    {   // one unit per workgroup
+        const uint64_t u = u0 + blockIdx.x;
+        if (u >= units) return;
         const uint64_t c = u / upc;
         const int g = (int)(u % upc);
         const uint64_t start = chunks[3 * c], len = chunks[3 * c + 1];
@@ -525,16 +585,16 @@ __global__ __launch_bounds__(kBlock) void slerp_gram_kernel(Members mem, PopLerp
             for (int q = 0; q < NT; ++q) gs[q] = 0.0;
             for_tile(start, len, j,
                 [&](uint64_t i) {
-                    float x[M][kVec];
+                    Raw8<IDT> x[M];
 #pragma unroll
-                    for (int m = 0; m < M; ++m) ld<IDT, kVec>(mem.p[m], i, x[m]);   // default policy
+                    for (int m = 0; m < M; ++m) x[m] = ld_raw<IDT, false>(mem.p[m], i);   // default policy
                     gram_fma<M, kVec>(x, gs);
                     if constexpr (EMIT) emit_children<ODT, M, kVec>(po, x, i, l0, l1);
                 },
                 [&](uint64_t i) {
-                    float x[M][1];
+                    Raw1 x[M];
 #pragma unroll
-                    for (int m = 0; m < M; ++m) ld<IDT, 1>(mem.p[m], i, x[m]);
+                    for (int m = 0; m < M; ++m) ld<IDT, 1>(mem.p[m], i, x[m].v);
                     gram_fma<M, 1>(x, gs);
                     if constexpr (EMIT) emit_children<ODT, M, 1>(po, x, i, l0, l1);
                 });
@@ -554,7 +614,6 @@ __global__ __launch_bounds__(kBlock) void slerp_gram_kernel(Members mem, PopLerp
             const double q0 = (t8[0] + t8[1]) + (t8[2] + t8[3]), q1 = (t8[4] + t8[5]) + (t8[6] + t8[7]);
             rows[unit_slot(u, units) * NT + lane] = q0 + q1;
         }
-        __syncthreads();
     }
 }
 
@@ -565,11 +624,13 @@ inline int gram_sums(const Members& mem, int D, const PopLerp* po, int in_dt, in
     const int NT = D * (D + 1) / 2;
     double* rows = gram + (uint64_t)nchunks * NT;
     constexpr int upc = kTileSlots / 16;
-    const unsigned g = unit_grid((uint64_t)nchunks * upc);
+    const uint64_t units = (uint64_t)nchunks * upc;
     PopLerp none;
     memset(&none, 0, sizeof(none));
     const PopLerp& P = po ? *po : none;
-#define EDT_GS(I, M, E, O) slerp_gram_kernel<I, M, E, O><<<g, kBlock, 0, s>>>(mem, P, chunk_desc, nchunks, t, rows)
+    for (uint64_t u0 = 0; u0 < units; u0 += kUnitGridCap) {
+    const unsigned g = unit_grid(units - u0);
+#define EDT_GS(I, M, E, O) slerp_gram_kernel<I, M, E, O><<<g, kBlock, 0, s>>>(mem, P, chunk_desc, nchunks, t, rows, u0)
 #define EDT_GM(M)                                                                      \
     case M:                                                                            \
         if (!po) {                                                                     \
@@ -588,6 +649,7 @@ inline int gram_sums(const Members& mem, int D, const PopLerp* po, int in_dt, in
 #undef EDT_GS
     int rc = check_launch(po ? "slerp_gram_kernel (speculative)" : "slerp_gram_kernel");
     if (rc) return rc;
+    }
     return launch_tree_reduce(rows, NT, kGramRows, upc, 1, nchunks, gram, s);
 }
 

@@ -189,7 +189,8 @@ def test_bench_population_measurement_on_virtual_ranks():
 
     import bench
     args = types.SimpleNamespace(steps=4, population_groups=4)
-    res = VirtualWorld(4).run(lambda comm: bench.bench_population(args, DEV, comm, "gpt2_small"))
+    res = VirtualWorld(4).run(lambda comm: bench.bench_population(args, bench.Runtime(DEV), comm,
+                                                                  layout_name="gpt2_small"))
     for r in res:
         assert r["sharded"]["ms"] > 0 and r["per_child"]["ms"] > 0
         assert r["sharded_pipelined"]["ms"] > 0 and r["sharded_pipelined"]["groups"] == 4
