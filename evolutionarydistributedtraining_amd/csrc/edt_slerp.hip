@@ -14,6 +14,108 @@ __device__ __forceinline__ double wave_sum(double x) {
     return x;
 }
 
+// ---- the tile butterfly without LDS ------------------------------------------------------------
+// wave_sum's descending xor butterfly (x_l += x_{l ^ o}, o = 32 .. 1) bit for bit, on the VALU:
+// __shfl_xor is a ds_bpermute through the LDS crossbar (two per double and level), which on the
+// Gram pass (36 sums per tile) cost more than streaming its members. Levels 32 / 16 use gfx950's
+// v_permlane32_swap / v_permlane16_swap, levels 8 .. 1 DPP moves (row_ror:8; half-mirror after a
+// quad reverse = xor 4; quad_perm xor 2 / xor 1). fp64 addition is commutative, so a lane forming
+// partner + self instead of self + partner gets the same bits.
+//
+// Several values at once are TRANSPOSED at levels 32 and 16 (the swap exchanges half the values):
+// for values A = v[k], B = v[h + k] a lane whose level bit is clear keeps A's pair sum, the other
+// lane B's — the same pair sums the per-value butterfly forms, one swap + one add per pair instead
+// of per value. After both levels, row r = lane / 16 holds N2 of the N values (index: red_index),
+// and the remaining levels run on those alone.
+__device__ __forceinline__ double join_d(uint32_t lo, uint32_t hi) {
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+template <int LVL>
+__device__ __forceinline__ double swap_sum(double x, double y) {
+    const uint64_t bx = (uint64_t)__double_as_longlong(x), by = (uint64_t)__double_as_longlong(y);
+    if constexpr (LVL == 32) {
+        const auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)bx, (uint32_t)by, false, false);
+        const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)(bx >> 32), (uint32_t)(by >> 32), false, false);
+        return join_d(lo[0], hi[0]) + join_d(lo[1], hi[1]);
+    } else {
+        static_assert(LVL == 16, "swap levels are 32 and 16");
+        const auto lo = __builtin_amdgcn_permlane16_swap((uint32_t)bx, (uint32_t)by, false, false);
+        const auto hi = __builtin_amdgcn_permlane16_swap((uint32_t)(bx >> 32), (uint32_t)(by >> 32), false, false);
+        return join_d(lo[0], hi[0]) + join_d(lo[1], hi[1]);
+    }
+}
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double x) {
+    const uint64_t b = (uint64_t)__double_as_longlong(x);
+    return join_d((uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)b, CTRL, 0xf, 0xf, false),
+                  (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(b >> 32), CTRL, 0xf, 0xf, false));
+}
+
+// levels 8, 4, 2, 1 of the butterfly (within each row of 16 lanes)
+__device__ __forceinline__ double row_butterfly(double x) {
+    x += dpp_d<0x128>(x);                 // row_ror:8       = lane ^ 8
+    x += dpp_d<0x141>(dpp_d<0x1B>(x));    // half-mirror (lane ^ 7) of quad_perm [3,2,1,0] (lane ^ 3)
+    x += dpp_d<0x4E>(x);                  // quad_perm [2,3,0,1] = lane ^ 2
+    x += dpp_d<0xB1>(x);                  // quad_perm [1,0,3,2] = lane ^ 1
+    return x;
+}
+
+template <int N>
+struct Red {
+    static constexpr int H1 = N / 2, N1 = H1 + (N & 1);       // after level 32
+    static constexpr int H2 = N1 / 2, N2 = H2 + (N1 & 1);     // after level 16: values per row
+};
+
+// N tile sums at once: r[s] on lane l = the butterfly total of value red_index<N>(s, l)
+template <int N>
+__device__ __forceinline__ void tile_reduce(const double (&v)[N], double (&r)[Red<N>::N2]) {
+    constexpr int H1 = Red<N>::H1, N1 = Red<N>::N1, H2 = Red<N>::H2, N2 = Red<N>::N2;
+    double r1[N1];
+#pragma unroll
+    for (int k = 0; k < H1; ++k) r1[k] = swap_sum<32>(v[k], v[H1 + k]);
+    if constexpr (N & 1) r1[H1] = swap_sum<32>(v[N - 1], v[N - 1]);
+#pragma unroll
+    for (int k = 0; k < H2; ++k) r[k] = swap_sum<16>(r1[k], r1[H2 + k]);
+    if constexpr (N1 & 1) r[H2] = swap_sum<16>(r1[N1 - 1], r1[N1 - 1]);
+#pragma unroll
+    for (int s = 0; s < N2; ++s) r[s] = row_butterfly(r[s]);
+}
+
+// Which value slot s of lane `lane` holds after tile_reduce<N>, and whether this lane is the one
+// writer of it (a leftover value at an odd level is held by both halves).
+template <int N>
+__device__ __forceinline__ int red_index(int s, int lane, bool& owner) {
+    constexpr int H1 = Red<N>::H1, N1 = Red<N>::N1, H2 = Red<N>::H2;
+    const bool b5 = (lane >> 5) & 1, b4 = (lane >> 4) & 1;
+    owner = true;
+    int s1;
+    if (s < H2) {
+        s1 = b4 ? H2 + s : s;
+    } else {
+        s1 = N1 - 1;
+        owner = !b4;
+    }
+    if (s1 < H1) return b5 ? H1 + s1 : s1;
+    owner = owner && !b5;
+    return N - 1;
+}
+
+// Lane l writes, when it owns one, the value slot (l % 16) holds: store(index, value).
+template <int N, typename Store>
+__device__ __forceinline__ void red_store(const double (&r)[Red<N>::N2], Store&& store) {
+    const int lane = threadIdx.x & 63, s = lane & 15;
+    if (s >= Red<N>::N2) return;
+    double x = r[0];
+#pragma unroll
+    for (int q = 1; q < Red<N>::N2; ++q)
+        if (s == q) x = r[q];
+    bool owner;
+    const int idx = red_index<N>(s, lane, owner);
+    if (owner) store(idx, x);
+}
+
 // ---- the chunk sums' canonical order (every form: pair, speculative, Gram, sharded) --------------
 // A chunk [start, start + len) (len <= 64 Ki) is cut into kTileSlots = 128 tiles of its 16-B-aligned
 // body [a, b): tile j holds, on lane l, the 8 elements at a + 512 j + 8 l (when below b); tile 0's
@@ -73,18 +175,6 @@ __device__ __forceinline__ void for_tile(uint64_t start, uint64_t len, int j, Ve
         const uint64_t nh = h_end - start, nt = end - t_beg;
         if (lane < nh + nt) elem(lane < nh ? start + lane : t_beg + (lane - nh));
     }
-}
-
-// A wave's W totals (identical in every lane after the butterfly) as one contiguous store of W
-// doubles by lanes 0 .. W-1.
-template <int W>
-__device__ __forceinline__ void store_row(double* row, const double (&v)[W]) {
-    const int lane = threadIdx.x & 63;
-    double x = 0.0;
-#pragma unroll
-    for (int q = 0; q < W; ++q)
-        if (lane == q) x = v[q];
-    if (lane < W) row[lane] = x;
 }
 
 // Per chunk, one wave: the chunk's W sums from its `nrows` rows (level log2(128 / nrows)), as the
@@ -188,12 +278,12 @@ __device__ __forceinline__ void tile0_edge(uint64_t start, uint64_t len, Elem&& 
     if (lane < nh + nt) elem(lane < nh ? start + lane : t_beg + (lane - nh));
 }
 
-// Tile j's pair sums (the tile sum in every lane). EMIT = true also writes the lerp-branch output
-// l0 v0 + l1 v1 of the tile (two rounded fp32 products, one rounded sum: lerp_elems' math) — the
-// speculative forms.
+// Tile j's pair sums, stored as the row {v0.v0, v1.v1, v0.v1} at `row` (level 0). EMIT = true also
+// writes the lerp-branch output l0 v0 + l1 v1 of the tile (two rounded fp32 products, one rounded
+// sum: lerp_elems' math) — the speculative forms.
 template <int IDT, bool NT, bool EMIT, int ODT>
 __device__ __forceinline__ void pair_tile(const void* v0, const void* v1, void* out, uint64_t start, uint64_t len,
-                                          int j, float l0, float l1, double (&sums)[3]) {
+                                          int j, float l0, float l1, double* row) {
     double s00 = 0.0, s11 = 0.0, s01 = 0.0;
     const uint64_t a = (start + kVec - 1) / kVec * kVec, b = (start + len) / kVec * kVec;
     const uint64_t i = a + (uint64_t)j * kTileElems + (uint64_t)(threadIdx.x & 63) * kVec;
@@ -218,17 +308,19 @@ __device__ __forceinline__ void pair_tile(const void* v0, const void* v1, void* 
                 st<ODT, 1>(out, e, o);
             }
         });
-    sums[0] = wave_sum(s00);
-    sums[1] = wave_sum(s11);
-    sums[2] = wave_sum(s01);
+    const double v[3] = {s00, s11, s01};
+    double r[Red<3>::N2];
+    tile_reduce<3>(v, r);
+    red_store<3>(r, [&](int q, double x) { row[q] = x; });
 }
 
 // Tiles 4 m .. 4 m + 3 of a chunk by one wave, read-only (the two-pass stats): the four tiles'
-// loads issued together, each tile's sums and butterfly as pair_tile's, combined in registers as
-// the tree does: (t0 + t1) + (t2 + t3) — a level-2 row.
+// loads issued together, each tile's sums and butterfly as pair_tile's (the 12 values transposed
+// together: row r of the wave ends with tile r's three sums), combined as the tree does —
+// (t0 + t1) + (t2 + t3) by the level-16 and level-32 swaps — and stored as a level-2 row.
 template <int IDT, bool NT>
 __device__ __forceinline__ void pair_tiles4(const void* v0, const void* v1, uint64_t start, uint64_t len, int m,
-                                            double (&sums)[3]) {
+                                            double* row) {
     const uint64_t a = (start + kVec - 1) / kVec * kVec, b = (start + len) / kVec * kVec;
     const uint64_t i0 = a + (uint64_t)(4 * m) * kTileElems + (uint64_t)(threadIdx.x & 63) * kVec;
     Raw8<IDT> x[4], y[4];
@@ -240,7 +332,7 @@ __device__ __forceinline__ void pair_tiles4(const void* v0, const void* v1, uint
             y[k] = ld_raw<IDT, NT>(v1, i);
         }
     }
-    double t[4][3];
+    double t[12];                                    // tile-major: t[3 k + q]
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         double s00 = 0.0, s11 = 0.0, s01 = 0.0;
@@ -252,12 +344,22 @@ __device__ __forceinline__ void pair_tiles4(const void* v0, const void* v1, uint
                 ld<IDT, 1>(v1, e, ye);
                 pair_fma<1>(xe, ye, s00, s11, s01);
             });
-        t[k][0] = wave_sum(s00);
-        t[k][1] = wave_sum(s11);
-        t[k][2] = wave_sum(s01);
+        t[3 * k] = s00;
+        t[3 * k + 1] = s11;
+        t[3 * k + 2] = s01;
     }
+    double r[Red<12>::N2];                           // row r: tile r's three sums (red_index)
+    tile_reduce<12>(t, r);
 #pragma unroll
-    for (int q = 0; q < 3; ++q) sums[q] = (t[0][q] + t[1][q]) + (t[2][q] + t[3][q]);
+    for (int q = 0; q < 3; ++q) {
+        const double p = swap_sum<16>(r[q], r[q]);        // rows 0 / 2: t0 + t1 / t2 + t3
+        r[q] = swap_sum<32>(p, p);                         // (t0 + t1) + (t2 + t3)
+    }
+    const int lane = threadIdx.x & 63;
+    double x0 = r[0];
+    if (lane == 1) x0 = r[1];
+    if (lane == 2) x0 = r[2];
+    if (lane < 3) row[lane] = x0;
 }
 
 // The reference's branch and coefficients (EDT_RL/crossover.py:31-45) for an fp32 dot, in fp32 as
@@ -357,14 +459,13 @@ __global__ __launch_bounds__(kBlock) void pair_sums_kernel(const void* v0, const
             b = reinterpret_cast<const void*>(seg_ptrs[3 * seg + 1]);
             o = reinterpret_cast<void*>(seg_ptrs[3 * seg + 2]);
         }
-        double sums[3];
+        double* row = rows + (unit_slot(u, units) * kWavesPerBlock + wave) * 3;
         if constexpr (EMIT) {
             pair_tile<IDT, NT, true, ODT>(a, b, o, chunks[3 * c], chunks[3 * c + 1], 4 * g + wave,
-                                          (float)(1.0 - tvals[seg]), (float)tvals[seg], sums);
+                                          (float)(1.0 - tvals[seg]), (float)tvals[seg], row);
         } else {
-            pair_tiles4<IDT, NT>(a, b, chunks[3 * c], chunks[3 * c + 1], 4 * g + wave, sums);
+            pair_tiles4<IDT, NT>(a, b, chunks[3 * c], chunks[3 * c + 1], 4 * g + wave, row);
         }
-        store_row<3>(rows + (unit_slot(u, units) * kWavesPerBlock + wave) * 3, sums);
     }
 }
 
@@ -598,13 +699,9 @@ __global__ __launch_bounds__(kBlock) void slerp_gram_kernel(Members mem, PopLerp
                     gram_fma<M, 1>(x, gs);
                     if constexpr (EMIT) emit_children<ODT, M, 1>(po, x, i, l0, l1);
                 });
-#pragma unroll
-            for (int q = 0; q < NT; ++q) gs[q] = wave_sum(gs[q]);
-            double v = 0.0;
-#pragma unroll
-            for (int q = 0; q < NT; ++q)
-                if (lane == q) v = gs[q];
-            if (lane < NT) ts[4 * wave + k][lane] = v;
+            double r[Red<NT>::N2];
+            tile_reduce<NT>(gs, r);
+            red_store<NT>(r, [&](int q, double x) { ts[4 * wave + k][q] = x; });
         }
         __syncthreads();
         if (wave == 0 && lane < NT) {
@@ -716,12 +813,10 @@ __global__ __launch_bounds__(kBlock) void slerp_pop_stats_lerp_kernel(BlendChild
     const uint64_t c = u / upc;
     const int wave = (int)(threadIdx.x >> 6);
     const uint64_t seg = chunks[3 * c + 2];
-    double sums[3];
     // default-policy loads: a parent's chunk is re-read by its other children from L2
     pair_tile<IDT, false, true, ODT>(B.v0[child], B.v1[child], B.out[child], chunks[3 * c], chunks[3 * c + 1],
                                      (int)(u % upc) * kWavesPerBlock + wave, (float)(1.0 - tvals[seg]),
-                                     (float)tvals[seg], sums);
-    store_row<3>(B.slots[child] + (unit_slot(u, units) * kWavesPerBlock + wave) * 3, sums);
+                                     (float)tvals[seg], B.slots[child] + (unit_slot(u, units) * kWavesPerBlock + wave) * 3);
 }
 
 // Per segment for the pair (i, j): slerp_coef_kernel's reduction over the chunks, reading the

@@ -105,6 +105,10 @@ class ResidentPopulation:
         self.prev_has_momentum = [False] * self.P
         n = layout.total
         mdt = momentum_dtype or dtype
+        if mdt != dtype:
+            # the pair merge writes the child momentum in the child's dtype (edt_pair_merge,
+            # ops.pair_merge checks it), so a separate momentum dtype could never cross over
+            raise EdtError(f"momentum_dtype {mdt} must equal the member dtype {dtype}")
 
         def arena(dt):
             return torch.zeros(n, dtype=dt, device=self.device)

@@ -202,6 +202,48 @@ def ref_slerp_dot(v0, v1, threads: int = 1, eps: float = 1e-8):
     return np.float32(d.value), np.float32(n0.value), np.float32(n1.value)
 
 
+def canonical_chunk_sums(v0, v1, chunks) -> np.ndarray:
+    """The product's fp64 chunk sums {v0.v0, v1.v1, v0.v1} [nchunks, 3] in its documented canonical
+    order (edt_slerp.hip, "the chunk sums' canonical order") — not the reference's
+    order (it sums in fp32 with numpy): this pins that every kernel form computes exactly the
+    order the design states. Per chunk [start, start + len): the 8-aligned body in 128 tiles of
+    64 lanes x 8 elements, each lane an fp64 FMA chain in element order (a float32 product is exact
+    in fp64, so s + x * x here rounds once, as the FMA does); tile 0's lanes then take the head /
+    tail elements; the descending xor butterfly (32 .. 1) per tile; the perfect binary tree over the
+    128 tile sums, adjacent pairs first."""
+    x = _cpu(torch.as_tensor(v0)).reshape(-1).float().numpy().astype(np.float64)
+    y = _cpu(torch.as_tensor(v1)).reshape(-1).float().numpy().astype(np.float64)
+    chunks = np.asarray(chunks, dtype=np.int64).reshape(-1, 3)
+    out = np.zeros((len(chunks), 3))
+    lanes = np.arange(64)
+    for c, (start, ln, _) in enumerate(chunks):
+        end = start + ln
+        a, b = (start + 7) // 8 * 8, end // 8 * 8
+        P = np.zeros((3, 128, 64))
+        if a < b:
+            X, Y = np.zeros(128 * 512), np.zeros(128 * 512)
+            X[:b - a], Y[:b - a] = x[a:b], y[a:b]
+            X, Y = X.reshape(128, 64, 8), Y.reshape(128, 64, 8)
+            for e in range(8):
+                xe, ye = X[:, :, e], Y[:, :, e]
+                P[0] = P[0] + xe * xe
+                P[1] = P[1] + ye * ye
+                P[2] = P[2] + xe * ye
+        h_end = min(a, end)
+        t_beg = b if b > a else h_end
+        nh, nt = h_end - start, end - t_beg
+        for lane in range(nh + nt):
+            i = start + lane if lane < nh else t_beg + lane - nh
+            P[:, 0, lane] = P[:, 0, lane] + np.array([x[i] * x[i], y[i] * y[i], x[i] * y[i]])
+        for o in (32, 16, 8, 4, 2, 1):
+            P = P + P[:, :, lanes ^ o]
+        T = P[:, :, 0]
+        while T.shape[1] > 1:
+            T = T[:, 0::2] + T[:, 1::2]
+        out[c] = T[:, 0]
+    return out
+
+
 def slerp(t: float, v0, v1, dot_threshold: float = 0.9995, eps: float = 1e-8) -> torch.Tensor:
     res, _, _ = slerp_parts(t, v0, v1, dot_threshold, eps)
     return torch.from_numpy(np.ascontiguousarray(res))
