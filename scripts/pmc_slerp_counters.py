@@ -1,0 +1,52 @@
+"""Summarise scripts/pmc_slerp_counters.sh: per kernel (lerp, speculative pass, two-pass stats and
+blend) the median of every counter over its launches, plus the ratios the verdict asked for —
+waves per CU and occupancy (SQ_WAVE_CYCLES counts quad-cycles: x4 / GRBM_GUI_ACTIVE / 256 CUs),
+the share of wave time parked (SQ_WAIT_ANY) vs issuing, and write combining (64-B write requests
+of all write requests at the memory side).
+
+    python scripts/pmc_slerp_counters.py gpurun_out/<tag>/counters
+"""
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+
+KERNELS = {"lerp": "lerp_kernel<1, 1, 1, 8>", "speculative": "pair_sums_kernel<1, true, 1>",
+           "stats": "pair_sums_kernel<1, false", "blend": "slerp_blend_kernel<1, 1, true, true>",
+           "tree_reduce": "tree_reduce_kernel"}
+CUS = 256
+
+
+def main():
+    root = sys.argv[1]
+    vals = {k: {} for k in KERNELS}
+    for path in glob.glob(os.path.join(root, "*", "**", "*counter_collection.csv"), recursive=True):
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                name = row.get("Kernel_Name", "")
+                for k, sub in KERNELS.items():
+                    if sub in name:
+                        vals[k].setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
+    out = {}
+    for k, cs in vals.items():
+        med = {c: statistics.median(v) for c, v in cs.items()}
+        rec = {"launches": max((len(v) for v in cs.values()), default=0), "counters": med}
+        g = med.get("GRBM_GUI_ACTIVE")
+        if g and "SQ_WAVE_CYCLES" in med:
+            rec["mean_waves_per_cu"] = round(4 * med["SQ_WAVE_CYCLES"] / g / CUS, 2)
+            rec["occupancy_of_32_waves_per_cu"] = round(4 * med["SQ_WAVE_CYCLES"] / g / CUS / 32, 3)
+        if "SQ_WAVE_CYCLES" in med and "SQ_WAIT_ANY" in med:
+            rec["wave_time_parked"] = round(med["SQ_WAIT_ANY"] / med["SQ_WAVE_CYCLES"], 3)
+            rec["wave_time_issuing"] = round(med.get("SQ_ACTIVE_INST_ANY", 0) / med["SQ_WAVE_CYCLES"], 3)
+        if med.get("TCC_EA0_WRREQ_sum"):
+            rec["write_requests_64B_share"] = round(med.get("TCC_EA0_WRREQ_64B_sum", 0) / med["TCC_EA0_WRREQ_sum"], 3)
+        out[k] = rec
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from evolutionarydistributedtraining_amd._lib import library_sha256
+    print(json.dumps({"probe": "pmc_slerp_counters", "lib_sha256": library_sha256(), "kernels": out}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
