@@ -75,14 +75,8 @@ using edt::g_err;
                                 // EDT_SLERP_BPC per CU
 #define EDT_SLERP_GRID 1
 #endif
-#ifndef EDT_SLERP_WAVE_ITERS    // 8-element vectors per lane in one wave tile of the chunk sums
-#define EDT_SLERP_WAVE_ITERS 4
-#endif
-#ifndef EDT_SLERP_SLOTS         // wave slots per chunk for the chunk sums (edt_slerp.hip: the canonical
-#define EDT_SLERP_SLOTS (128 / EDT_SLERP_WAVE_ITERS)   // order; slots x wave tiles = the plans' 64 Ki chunks)
-#endif
-#ifndef EDT_SLERP_SUMS_BPC      // chunk-sum passes: 0 = one workgroup per (chunk, slot group) in address
-#define EDT_SLERP_SUMS_BPC 0    // order; k > 0 = k workgroups per CU striding over those units
+#ifndef EDT_SLERP_STATS_TPW     // 512-element tiles per wave in the read-only chunk-sum pass (4, 8 or 16;
+#define EDT_SLERP_STATS_TPW 4   // the sums' order is the same for every value: edt_slerp.hip)
 #endif
 #ifndef EDT_SLERP_COEF_BLOCK    // 1: one workgroup per segment for the chunk-sum reduction (else one wave)
 #define EDT_SLERP_COEF_BLOCK 1

@@ -141,9 +141,10 @@ constexpr int kTileSlots = 128;                               // tiles per chunk
 constexpr uint32_t kMaxChunkElems = (uint32_t)kTileSlots * kTileElems;
 constexpr int kWavesPerBlock = kBlock / 64;
 // the row levels the kernels write: pair passes one tile per wave (level 0; the read-only stats
-// pass four per wave, level 2), the Gram passes sixteen per workgroup (level 4)
+// pass kStatsTPW per wave, level log2 kStatsTPW), the Gram passes sixteen per workgroup (level 4)
 constexpr int kPairRows = kTileSlots;                         // rows per chunk, level 0
 constexpr int kGramRows = kTileSlots / 16;                    // rows per chunk, level 4
+constexpr int kStatsTPW = EDT_SLERP_STATS_TPW;                // tiles per wave of the read-only pass
 
 // One-pass grids of `units` workgroups in address order (a unit = a fixed set of a chunk's tiles);
 // past the dispatch cap (a multiple of 8, so blockIdx % 8 stays the unit's XCD) they stride.
@@ -314,30 +315,33 @@ __device__ __forceinline__ void pair_tile(const void* v0, const void* v1, void* 
     red_store<3>(r, [&](int q, double x) { row[q] = x; });
 }
 
-// Tiles 4 m .. 4 m + 3 of a chunk by one wave, read-only (the two-pass stats): the four tiles'
-// loads issued together, each tile's sums and butterfly as pair_tile's (the 12 values transposed
-// together: row r of the wave ends with tile r's three sums), combined as the tree does —
-// (t0 + t1) + (t2 + t3) by the level-16 and level-32 swaps — and stored as a level-2 row.
-template <int IDT, bool NT>
-__device__ __forceinline__ void pair_tiles4(const void* v0, const void* v1, uint64_t start, uint64_t len, int m,
-                                            double* row) {
+// Tiles T m .. T m + T - 1 of a chunk by one wave, read-only (the two-pass stats; T = 4, 8, 16):
+// the T tiles' loads issued together, each tile's sums and butterfly as pair_tile's (the 3 T values
+// transposed together: row r of the wave ends with tiles K r .. K r + K - 1, K = T / 4), then the
+// tree over the T tile sums in registers — within a row, then rows 0 + 1 and 2 + 3 by the level-16
+// swap, then the two halves by the level-32 swap — stored as one row of level log2 T.
+template <int IDT, bool NT, int T>
+__device__ __forceinline__ void pair_tiles(const void* v0, const void* v1, uint64_t start, uint64_t len, int m,
+                                           double* row) {
+    static_assert(T == 4 || T == 8 || T == 16, "tiles per wave");
+    constexpr int K = T / 4;
     const uint64_t a = (start + kVec - 1) / kVec * kVec, b = (start + len) / kVec * kVec;
-    const uint64_t i0 = a + (uint64_t)(4 * m) * kTileElems + (uint64_t)(threadIdx.x & 63) * kVec;
-    Raw8<IDT> x[4], y[4];
+    const uint64_t i0 = a + (uint64_t)(T * m) * kTileElems + (uint64_t)(threadIdx.x & 63) * kVec;
+    Raw8<IDT> x[T], y[T];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < T; ++k) {
         const uint64_t i = i0 + (uint64_t)k * kTileElems;
         if (a < b && i < b) {
             x[k] = ld_raw<IDT, NT>(v0, i);
             y[k] = ld_raw<IDT, NT>(v1, i);
         }
     }
-    double t[12];                                    // tile-major: t[3 k + q]
+    double t[3 * T];                                 // tile-major: t[3 k + q]
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < T; ++k) {
         double s00 = 0.0, s11 = 0.0, s01 = 0.0;
         if (a < b && i0 + (uint64_t)k * kTileElems < b) pair_fma<kVec>(x[k], y[k], s00, s11, s01);
-        if (4 * m + k == 0)
+        if (T * m + k == 0)
             tile0_edge(start, len, [&](uint64_t e) {
                 float xe[1], ye[1];
                 ld<IDT, 1>(v0, e, xe);
@@ -348,17 +352,20 @@ __device__ __forceinline__ void pair_tiles4(const void* v0, const void* v1, uint
         t[3 * k + 1] = s11;
         t[3 * k + 2] = s01;
     }
-    double r[Red<12>::N2];                           // row r: tile r's three sums (red_index)
-    tile_reduce<12>(t, r);
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-        const double p = swap_sum<16>(r[q], r[q]);        // rows 0 / 2: t0 + t1 / t2 + t3
-        r[q] = swap_sum<32>(p, p);                         // (t0 + t1) + (t2 + t3)
-    }
+    static_assert(Red<3 * T>::N2 == 3 * K, "row layout");
+    double r[3 * K];                                 // row r: tiles K r + j at r[3 j + q] (red_index)
+    tile_reduce<3 * T>(t, r);
+    auto total = [&](int q) {                        // q is a constant after inlining
+        double v;
+        if constexpr (K == 1) v = r[q];
+        else if constexpr (K == 2) v = r[q] + r[3 + q];
+        else v = (r[q] + r[3 + q]) + (r[6 + q] + r[9 + q]);
+        const double p = swap_sum<16>(v, v);              // rows 0 / 2: the first / second quarter pairs
+        return swap_sum<32>(p, p);                        // the two halves
+    };
+    const double s0 = total(0), s1 = total(1), s2 = total(2);
     const int lane = threadIdx.x & 63;
-    double x0 = r[0];
-    if (lane == 1) x0 = r[1];
-    if (lane == 2) x0 = r[2];
+    const double x0 = lane == 0 ? s0 : lane == 1 ? s1 : s2;
     if (lane < 3) row[lane] = x0;
 }
 
@@ -434,15 +441,15 @@ __device__ __forceinline__ void for_range_elems(uint64_t start, uint64_t end, F&
 // (level-0 rows), lerp's own grid; the lerp-branch output (1-t) v0 + t v1 with the coefficients
 // slerp_coefficients gives that branch is written in the same pass. Parents of one lineage
 // (fine-tunes of a common base) mostly have |dot| > 0.9995, where this output is final; the other
-// segments are blended again. Read-only (the two-pass stats): unit = 16 tiles, four per wave
-// (level-2 rows). seg_ptrs (tensor-list form, may be null): per segment {v0, v1, out} device
+// segments are blended again. Read-only (the two-pass stats): unit = 4 kStatsTPW tiles,
+// kStatsTPW per wave (rows of level log2 kStatsTPW). seg_ptrs (tensor-list form, may be null): per segment {v0, v1, out} device
 // pointers; chunk starts are then relative to their segment. Null: flat arenas.
 template <int IDT, bool EMIT, int ODT>
 __global__ __launch_bounds__(kBlock) void pair_sums_kernel(const void* v0, const void* v1, void* out,
                                                            const uint64_t* chunks, int64_t nchunks, double* rows,
                                                            const double* tvals, const uint64_t* seg_ptrs, uint64_t u0) {
     constexpr bool NT = EDT_NT_SLERP != 0 && IDT == EDT_BF16;
-    constexpr int upc = EMIT ? kTileSlots / 4 : kTileSlots / 16;          // units per chunk
+    constexpr int upc = EMIT ? kTileSlots / 4 : kTileSlots / (4 * kStatsTPW);   // units per chunk
     const int wave = threadIdx.x >> 6;
     const uint64_t units = (uint64_t)nchunks * upc;
     {   // one unit per workgroup (no grid-stride loop: it costs registers, i.e. occupancy)
@@ -464,7 +471,7 @@ __global__ __launch_bounds__(kBlock) void pair_sums_kernel(const void* v0, const
             pair_tile<IDT, NT, true, ODT>(a, b, o, chunks[3 * c], chunks[3 * c + 1], 4 * g + wave,
                                           (float)(1.0 - tvals[seg]), (float)tvals[seg], row);
         } else {
-            pair_tiles4<IDT, NT>(a, b, chunks[3 * c], chunks[3 * c + 1], 4 * g + wave, row);
+            pair_tiles<IDT, NT, kStatsTPW>(a, b, chunks[3 * c], chunks[3 * c + 1], 4 * g + wave, row);
         }
     }
 }
@@ -474,7 +481,7 @@ int pair_sums(const void* v0, const void* v1, int in_dt, void* out, int out_dt, 
               const uint64_t* chunk_desc, int64_t nchunks, double* partial, const double* t,
               const uint64_t* seg_ptrs, hipStream_t s) {
     double* rows = partial + 3 * (uint64_t)nchunks;
-    const int upc = emit ? kTileSlots / 4 : kTileSlots / 16;
+    const int upc = emit ? kTileSlots / 4 : kTileSlots / (4 * kStatsTPW);
     const uint64_t units = (uint64_t)nchunks * upc;
     for (uint64_t u0 = 0; u0 < units; u0 += kUnitGridCap) {       // > 16.7M units: several launches
         const unsigned g = unit_grid(units - u0);
@@ -490,7 +497,7 @@ int pair_sums(const void* v0, const void* v1, int in_dt, void* out, int out_dt, 
         int rc = check_launch(emit ? "pair_sums_kernel (speculative)" : "pair_sums_kernel");
         if (rc) return rc;
     }
-    // rows per chunk: 128 (level 0, one per unit's wave) or 32 (level 2)
+    // rows per chunk: 128 (level 0, one per unit's wave) or 128 / kStatsTPW
     return launch_tree_reduce(rows, 3, upc * kWavesPerBlock, upc, kWavesPerBlock, nchunks, partial, s);
 }
 

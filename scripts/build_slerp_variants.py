@@ -1,4 +1,4 @@
-"""Build-time variants of the chunk-sum passes (edt_slerp.hip wave slots) into variants_slerp/,
+"""Build-time variants of the chunk-sum passes (edt_slerp.hip) into variants_slerp/,
 for scripts/slerp_spec_probe.py --variants variants_slerp (timed beside the in-tree library).
 
     python scripts/build_slerp_variants.py [name ...]
@@ -12,12 +12,9 @@ sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "variants_slerp")
 
 VARIANTS = {
-    "it1": ["-DEDT_SLERP_WAVE_ITERS=1"],
-    "it2": ["-DEDT_SLERP_WAVE_ITERS=2"],
-    "it8": ["-DEDT_SLERP_WAVE_ITERS=8"],
-    "it4_bpc16": ["-DEDT_SLERP_SUMS_BPC=16"],
-    "it4_bpc64": ["-DEDT_SLERP_SUMS_BPC=64"],
-    "it4_nont": ["-DEDT_NT_SLERP=0"],
+    "tpw8": ["-DEDT_SLERP_STATS_TPW=8"],
+    "tpw16": ["-DEDT_SLERP_STATS_TPW=16"],
+    "nont": ["-DEDT_NT_SLERP=0"],
 }
 
 

@@ -8,7 +8,8 @@ EDT_RECORD_DIR=$OUT timeout -k 10 1000 python -u -m pytest tests -x -q -m gpu --
     ${PYTEST_ARGS:-} > $OUT/pytest_gpu.log 2>&1; s=$?
 tail -6 $OUT/pytest_gpu.log; [ $s -le 1 ] || exit $s
 for far in "" "--far"; do
-  timeout -k 10 300 python scripts/slerp_spec_probe.py --rounds 5 $far >> $OUT/probe.jsonl 2>> $OUT/probe.err || exit 3
+  V=""; [ -d variants_slerp ] && V="--variants variants_slerp"      # build-time variants, if built
+  timeout -k 10 300 python scripts/slerp_spec_probe.py --rounds 5 $far $V >> $OUT/probe.jsonl 2>> $OUT/probe.err || exit 3
 done
 cat $OUT/probe.jsonl
 (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
