@@ -156,6 +156,9 @@ constexpr int kTile = kBlock * kVec;                 // 2,048 elements
 #define EDT_SLERP_TPC 32
 #endif
 constexpr int kTilesPerChunk = EDT_SLERP_TPC;        // the plans' default chunk: 64 Ki elements
+#ifndef EDT_SLERP_BLEND_TILE    // 1: the full SLERP blend on the speculative pass's one-shot unit grid
+#define EDT_SLERP_BLEND_TILE 1  // (slerp_blend_tile_kernel); 0: slerp_blend_kernel's tile grid
+#endif
 #ifndef EDT_SLERP_BLEND_REV     // 1: the tile grid walks the arena from its end (probe: does the blend
 #define EDT_SLERP_BLEND_REV 0   // re-read what the stats pass left in the Infinity Cache last?)
 #endif

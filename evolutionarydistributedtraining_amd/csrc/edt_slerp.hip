@@ -447,8 +447,10 @@ __device__ __forceinline__ void for_range_elems(uint64_t start, uint64_t end, F&
 template <int IDT, bool EMIT, int ODT>
 __global__ __launch_bounds__(kBlock) void pair_sums_kernel(const void* v0, const void* v1, void* out,
                                                            const uint64_t* chunks, int64_t nchunks, double* rows,
-                                                           const double* tvals, const uint64_t* seg_ptrs, uint64_t u0) {
+                                                           const double* tvals, const uint64_t* seg_ptrs, uint64_t u0,
+                                                           int32_t* zero_word) {
     constexpr bool NT = EDT_NT_SLERP != 0 && IDT == EDT_BF16;
+    if (zero_word && u0 == 0 && blockIdx.x == 0 && threadIdx.x == 0) *zero_word = 0;   // the any-redo flag
     constexpr int upc = EMIT ? kTileSlots / 4 : kTileSlots / (4 * kStatsTPW);   // units per chunk
     const int wave = threadIdx.x >> 6;
     const uint64_t units = (uint64_t)nchunks * upc;
@@ -479,13 +481,13 @@ __global__ __launch_bounds__(kBlock) void pair_sums_kernel(const void* v0, const
 // host: the pair sums into partial (chunk rows [nchunks][3], then the row scratch), EMIT optional
 int pair_sums(const void* v0, const void* v1, int in_dt, void* out, int out_dt, bool emit,
               const uint64_t* chunk_desc, int64_t nchunks, double* partial, const double* t,
-              const uint64_t* seg_ptrs, hipStream_t s) {
+              const uint64_t* seg_ptrs, hipStream_t s, int32_t* zero_word = nullptr) {
     double* rows = partial + 3 * (uint64_t)nchunks;
     const int upc = emit ? kTileSlots / 4 : kTileSlots / (4 * kStatsTPW);
     const uint64_t units = (uint64_t)nchunks * upc;
     for (uint64_t u0 = 0; u0 < units; u0 += kUnitGridCap) {       // > 16.7M units: several launches
         const unsigned g = unit_grid(units - u0);
-#define EDT_PS(I, E, O) pair_sums_kernel<I, E, O><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, rows, t, seg_ptrs, u0)
+#define EDT_PS(I, E, O) pair_sums_kernel<I, E, O><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, rows, t, seg_ptrs, u0, zero_word)
         if (!emit) {
             if (in_dt == EDT_F32) EDT_PS(EDT_F32, false, EDT_F32);
             else EDT_PS(EDT_BF16, false, EDT_F32);
@@ -549,7 +551,8 @@ inline unsigned coef_grid(int nseg) {
 __global__ __launch_bounds__(kBlock) void slerp_coef_kernel(const double* partial, const int32_t* first,
                                                             int nseg, const double* tvals,
                                                             float thr, float eps, float* coef,
-                                                            float* dot_out, int32_t* redo = nullptr) {
+                                                            float* dot_out, int32_t* redo = nullptr,
+                                                            int32_t* any_redo = nullptr) {
     const int seg = coef_segment();
     if (seg >= nseg) return;
     double sums[3];
@@ -559,14 +562,20 @@ __global__ __launch_bounds__(kBlock) void slerp_coef_kernel(const double* partia
     coef[2 * seg] = c0;
     coef[2 * seg + 1] = c1;
     if (dot_out) dot_out[seg] = dot;
-    if (redo) redo[seg] = fabsf(dot) > thr ? 0 : 1;   // the speculative lerp output stands or not
+    if (redo) {                                       // the speculative lerp output stands or not
+        const int32_t r = fabsf(dot) > thr ? 0 : 1;
+        redo[seg] = r;
+        if (r && any_redo) *any_redo = 1;             // every writer stores the same 1
+    }
 }
 
 template <int IDT, int ODT, bool NT = (EDT_NT_SLERP != 0 && IDT == EDT_BF16), bool TILES = true>
 __global__ __launch_bounds__(kBlock) void slerp_blend_kernel(const void* v0, const void* v1, void* out,
                                                              const uint64_t* chunks, int64_t nchunks,
                                                              const float* coef, const uint64_t* seg_ptrs,
-                                                             const int32_t* redo = nullptr) {
+                                                             const int32_t* redo = nullptr,
+                                                             const int32_t* any_redo = nullptr) {
+    if (any_redo && *any_redo == 0) return;       // no segment to blend again: the whole grid exits
     for_blend_ranges<TILES>(chunks, nchunks, [&](uint64_t start, uint64_t end, uint64_t seg) {
         if (redo && !redo[seg]) return;           // speculative lerp output already final
         const void* a = v0;
@@ -583,6 +592,50 @@ __global__ __launch_bounds__(kBlock) void slerp_blend_kernel(const void* v0, con
             lerp_elems<IDT, ODT, EDT_F32, N, NT && N == kVec>(a, b, o, i, c0, c1);
         });
     });
+}
+
+// The full blend (the two-pass form's second pass) on the speculative pass's grid: one workgroup
+// per unit of 4 tiles in address order (one-shot, no grid-stride loop), wave w the unit's tile
+// j = 4 g + w (for_tile's lane mapping; tile 0 also takes the head / tail elements). The chunk row
+// is read once, the parents' vectors are loaded before the segment's coefficients, so the data
+// loads wait on one dependent read, not three (slerp_blend_kernel's tile form: 7.52 ms against
+// lerp's 7.04 on the 7B body, r3 counters — 36 % more wave-cycles, 2.5x the VMEM reads).
+// lerp_elems' math: two rounded fp32 products, one rounded sum.
+template <int IDT, int ODT, bool NT>
+__global__ __launch_bounds__(kBlock) void slerp_blend_tile_kernel(const void* __restrict__ v0,
+                                                                  const void* __restrict__ v1,
+                                                                  void* __restrict__ out,
+                                                                  const uint64_t* __restrict__ chunks, int64_t nchunks,
+                                                                  const float* __restrict__ coef,
+                                                                  const uint64_t* __restrict__ seg_ptrs, uint64_t u0) {
+    constexpr int upc = kTileSlots / kWavesPerBlock;
+    const uint64_t u = u0 + blockIdx.x;
+    if (u >= (uint64_t)nchunks * upc) return;
+    const uint64_t c = u / upc;
+    const int j = (int)(u % upc) * kWavesPerBlock + (int)(threadIdx.x >> 6);
+    const uint64_t start = chunks[3 * c], len = chunks[3 * c + 1], seg = chunks[3 * c + 2];
+    const void* a = v0;
+    const void* b = v1;
+    void* o = out;
+    if (seg_ptrs) {
+        a = reinterpret_cast<const void*>(seg_ptrs[3 * seg]);
+        b = reinterpret_cast<const void*>(seg_ptrs[3 * seg + 1]);
+        o = reinterpret_cast<void*>(seg_ptrs[3 * seg + 2]);
+    }
+    const uint64_t A = (start + kVec - 1) / kVec * kVec, B = (start + len) / kVec * kVec;
+    const uint64_t i = A + (uint64_t)j * kTileElems + (uint64_t)(threadIdx.x & 63) * kVec;
+    if (A < B && i < B) {
+        const Raw8<IDT> x = ld_raw<IDT, NT>(a, i), y = ld_raw<IDT, NT>(b, i);
+        const float c0 = coef[2 * seg], c1 = coef[2 * seg + 1];
+        float r[kVec];
+#pragma unroll
+        for (int e = 0; e < kVec; ++e) r[e] = c0 * x[e] + c1 * y[e];
+        st<ODT, kVec>(o, i, r);
+    }
+    if (j == 0)
+        tile0_edge(start, len, [&](uint64_t e) {
+            lerp_elems<IDT, ODT, EDT_F32, 1>(a, b, o, e, coef[2 * seg], coef[2 * seg + 1]);
+        });
 }
 
 // ---------------------------------------------------------------------------------------
@@ -928,8 +981,26 @@ int slerp_blend_impl(const void* v0, const void* v1, int in_dt, void* out, int o
     if ((in_dt | out_dt) & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
     if (nchunks == 0) return EDT_OK;
     if (!chunk_desc || !coef) return fail(EDT_ERR_ARG, "null buffer");
-    const unsigned g = slerp_tile_grid(nchunks);
     hipStream_t s = (hipStream_t)stream;
+    if (EDT_SLERP_BLEND_TILE) {
+        constexpr bool kNt = EDT_NT_SLERP != 0;
+        const uint64_t units = (uint64_t)nchunks * (kTileSlots / kWavesPerBlock);
+        for (uint64_t u0 = 0; u0 < units; u0 += kUnitGridCap) {
+            const unsigned g = unit_grid(units - u0);
+#define EDT_BT(I, O, N) slerp_blend_tile_kernel<I, O, N><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, seg_ptrs, u0)
+            if (in_dt == EDT_F32 && out_dt == EDT_F32) EDT_BT(EDT_F32, EDT_F32, false);
+            else if (in_dt == EDT_F32) EDT_BT(EDT_F32, EDT_BF16, false);
+            else if (out_dt == EDT_F32 && nt) EDT_BT(EDT_BF16, EDT_F32, kNt);
+            else if (out_dt == EDT_F32) EDT_BT(EDT_BF16, EDT_F32, false);
+            else if (nt) EDT_BT(EDT_BF16, EDT_BF16, kNt);
+            else EDT_BT(EDT_BF16, EDT_BF16, false);
+#undef EDT_BT
+            int rc = check_launch("slerp_blend_tile_kernel");
+            if (rc) return rc;
+        }
+        return EDT_OK;
+    }
+    const unsigned g = slerp_tile_grid(nchunks);
     if (in_dt == EDT_F32 && out_dt == EDT_F32)
         slerp_blend_kernel<EDT_F32, EDT_F32><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, seg_ptrs);
     else if (in_dt == EDT_F32)
@@ -1357,9 +1428,10 @@ int edt_slerp_merge(const void* v0, const void* v1, int in_dt, void* out, int ou
 uint64_t edt_slerp_sums_doubles(int width, int64_t nchunks) {
     // the chunk rows + the largest row scratch a pass writes for this width: level-0 rows (one per
     // tile) for the pair passes (width 3), level-4 rows for the Gram passes
+    // (width 3: plus one double at the end, the speculative pass's any-redo flag)
     if (width < 1 || nchunks < 0) return 0;
     const uint64_t rows = width <= 3 ? kPairRows : kGramRows;
-    return (uint64_t)nchunks * (uint64_t)width * (1ull + rows);
+    return (uint64_t)nchunks * (uint64_t)width * (1ull + rows) + (width <= 3 ? 1 : 0);
 }
 
 uint64_t edt_slerp_population_speculative_doubles(int npairs, int64_t nchunks) {
@@ -1572,23 +1644,26 @@ int edt_slerp_merge_speculative(const void* v0, const void* v1, int in_dt, void*
         if (p0 < o1 && o0 < p1) return fail(EDT_ERR_ARG, "speculative SLERP needs an output apart from the parents");
     }
     hipStream_t s = (hipStream_t)stream;
-    int rc = pair_sums(v0, v1, in_dt, out, out_dt, true, chunk_desc, nchunks, partial, t, nullptr, s);
+    // the any-redo flag: the last double of the workspace (edt_slerp_sums_doubles), zeroed by the
+    // first pass, set by the coefficient kernel when some segment takes the SLERP branch
+    int32_t* any = reinterpret_cast<int32_t*>(partial + edt_slerp_sums_doubles(3, nchunks) - 1);
+    int rc = pair_sums(v0, v1, in_dt, out, out_dt, true, chunk_desc, nchunks, partial, t, nullptr, s, any);
     if (rc) return rc;
     slerp_coef_kernel<<<coef_grid(nseg), kBlock, 0, s>>>(partial, seg_first_chunk, nseg, t, (float)dot_threshold,
-                                                         (float)eps, coef, dot_out, redo);
+                                                         (float)eps, coef, dot_out, redo, any);
     rc = check_launch("slerp_coef_kernel");
     if (rc) return rc;
     // the redo blends: grid-stride over chunks (most segments are skipped)
     const unsigned g = slerp_spec_grid(nchunks);
     constexpr bool kNtB = EDT_NT_SLERP != 0;
     if (in_dt == EDT_F32 && out_dt == EDT_F32)
-        slerp_blend_kernel<EDT_F32, EDT_F32, false, false><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, nullptr, redo);
+        slerp_blend_kernel<EDT_F32, EDT_F32, false, false><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, nullptr, redo, any);
     else if (in_dt == EDT_F32)
-        slerp_blend_kernel<EDT_F32, EDT_BF16, false, false><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, nullptr, redo);
+        slerp_blend_kernel<EDT_F32, EDT_BF16, false, false><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, nullptr, redo, any);
     else if (out_dt == EDT_F32)
-        slerp_blend_kernel<EDT_BF16, EDT_F32, kNtB, false><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, nullptr, redo);
+        slerp_blend_kernel<EDT_BF16, EDT_F32, kNtB, false><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, nullptr, redo, any);
     else
-        slerp_blend_kernel<EDT_BF16, EDT_BF16, kNtB, false><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, nullptr, redo);
+        slerp_blend_kernel<EDT_BF16, EDT_BF16, kNtB, false><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, nullptr, redo, any);
     return check_launch("slerp_blend_kernel");
 }
 

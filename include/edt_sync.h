@@ -178,12 +178,13 @@ int64_t edt_slerp_make_chunks(const uint64_t* seg_offsets_host, int nseg, uint32
                               uint64_t* chunk_desc_host, int64_t max_chunks,
                               int32_t* seg_first_chunk_host);
 
-/* Chunk-sum tables. Every chunk's fp64 sums are formed in one canonical order by wave slots with
- * no workgroup barrier (edt_slerp.hip): a table of W sums per chunk therefore needs
- * edt_slerp_sums_doubles(W, nchunks) doubles — the chunk rows [nchunks][W] first (what the
- * coefficient passes read and what a caller may copy or all-gather), then the slot scratch the
- * sum pass fills and folds into the rows. Every `partial` of the pair forms below holds
- * edt_slerp_sums_doubles(3, nchunks) doubles. */
+/* Chunk-sum tables. Every chunk's fp64 sums are formed in one canonical order (edt_slerp.hip:
+ * per-lane FMA chains over 512-element tiles, the wave butterfly, a perfect binary tree over the
+ * tiles), written as partial-tree rows with no workgroup barrier: a table of W sums per chunk
+ * therefore needs edt_slerp_sums_doubles(W, nchunks) doubles — the chunk rows [nchunks][W] first
+ * (what the coefficient passes read and what a caller may copy or all-gather), then the row
+ * scratch the sum pass fills and folds into the rows (W = 3: and one flag word at the end). Every
+ * `partial` of the pair forms below holds edt_slerp_sums_doubles(3, nchunks) doubles. */
 uint64_t edt_slerp_sums_doubles(int width, int64_t nchunks);
 
 /* Pass 1: per-chunk sums  partial[c] = { sum v0^2, sum v1^2, sum v0*v1 }  (fp64). */

@@ -15,6 +15,7 @@ VARIANTS = {
     "tpw8": ["-DEDT_SLERP_STATS_TPW=8"],
     "tpw16": ["-DEDT_SLERP_STATS_TPW=16"],
     "nont": ["-DEDT_NT_SLERP=0"],
+    "blendold": ["-DEDT_SLERP_BLEND_TILE=0"],
 }
 
 
