@@ -75,8 +75,12 @@ using edt::g_err;
                                 // EDT_SLERP_BPC per CU
 #define EDT_SLERP_GRID 1
 #endif
-#ifndef EDT_SLERP_STATS_TPW     // 512-element tiles per wave in the read-only chunk-sum pass (4, 8 or 16;
-#define EDT_SLERP_STATS_TPW 4   // the sums' order is the same for every value: edt_slerp.hip)
+// 512-element tiles per wave in the read-only chunk-sum pass (4, 8 or 16; the sums' order is the
+// same for every value, edt_slerp.hip). 7B body, bf16, one box (profiles/r03_slerp_stats_tpw.jsonl):
+// 4.44 / 4.21 / 4.09 ms for 4 / 8 / 16 — a read-only stream wants many bytes in flight per wave
+// (16: 142 VGPRs, 3 waves per SIMD, 256 B per lane outstanding).
+#ifndef EDT_SLERP_STATS_TPW
+#define EDT_SLERP_STATS_TPW 16
 #endif
 #ifndef EDT_SLERP_COEF_BLOCK    // 1: one workgroup per segment for the chunk-sum reduction (else one wave)
 #define EDT_SLERP_COEF_BLOCK 1

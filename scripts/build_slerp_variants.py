@@ -12,8 +12,8 @@ sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "variants_slerp")
 
 VARIANTS = {
+    "tpw4": ["-DEDT_SLERP_STATS_TPW=4"],
     "tpw8": ["-DEDT_SLERP_STATS_TPW=8"],
-    "tpw16": ["-DEDT_SLERP_STATS_TPW=16"],
     "nont": ["-DEDT_NT_SLERP=0"],
     "blendold": ["-DEDT_SLERP_BLEND_TILE=0"],
 }

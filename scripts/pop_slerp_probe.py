@@ -1,0 +1,83 @@
+"""BASELINE configs[4] on one MI355X, timed warm: a resident population of 8 Qwen2.5-7B bodies (bf16)
+SLERP-crossed into 8 children (edt_slerp_population*), in each kernel form:
+lineage members and independent members, each through both forms (ops.slerp_population with
+speculate=True: one co-located pass + SLERP-branch redo; False: the Gram stats pass + member-major
+blends) — `--rounds` generations after one warm-up each, HIP events around each generation.
+Run under rocprofv3 --kernel-trace --stats for the per-kernel split.
+
+    python scripts/pop_slerp_probe.py [--rounds 3]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+BF = torch.bfloat16
+
+
+def fill(dst, gen, scale, base=None, rel=0.0):
+    step = 1 << 28
+    for s in range(0, dst.numel(), step):
+        e = min(dst.numel(), s + step)
+        x = torch.randn(e - s, device=dst.device, generator=gen) * scale
+        if base is not None:
+            x = base[s:e].float() + x * rel
+        dst[s:e] = x.to(dst.dtype)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=3)
+    a = ap.parse_args()
+    from evolutionarydistributedtraining_amd import ops
+    from evolutionarydistributedtraining_amd.layouts import qwen2p5_7b_body
+    dev = torch.device("cuda:0")
+    lay = qwen2p5_7b_body()
+    P, N = lay.total, 8
+    gen = torch.Generator(device=dev).manual_seed(4)
+    members = [torch.empty(P, dtype=BF, device=dev) for _ in range(N)]
+    outs = [torch.empty(P, dtype=BF, device=dev) for _ in range(N)]
+    t = torch.rand(len(lay), dtype=torch.float64, generator=torch.Generator().manual_seed(4)).to(dev)
+    plan = ops.make_slerp_plan(lay.offsets, dev)
+    pairs = [((3 * c + 1) % N, (5 * c + 2) % N) for c in range(N)]
+    s = torch.cuda.current_stream(dev)
+    res = {}
+
+    def run(name, speculate):
+        ts = []
+        for r in range(a.rounds + 1):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            dots = ops.slerp_population(plan, members, pairs, outs, t, speculate=speculate)
+            e1.record(s)
+            torch.cuda.synchronize()
+            if r:
+                ts.append(e0.elapsed_time(e1))
+        slerp_share = float((dots.abs() <= 0.9995).float().mean())
+        res[name] = {"median_ms": round(statistics.median(ts), 3), "min_ms": round(min(ts), 3),
+                     "children": N, "distinct_parents": len({m for p in pairs for m in p}),
+                     "slerp_branch_segment_share": round(slerp_share, 3),
+                     "GBps_algorithmic": round(2 * P * (len({m for p in pairs for m in p}) + N)
+                                               / statistics.median(ts) / 1e6, 1)}
+        print(name, res[name], flush=True)
+
+    base = torch.empty(P, dtype=BF, device=dev)
+    fill(base, gen, 0.02)
+    for m in members:
+        fill(m, gen, 0.02, base=base, rel=0.005)       # one lineage: every segment in the lerp branch
+    del base
+    run("lineage_speculative", True)
+    run("lineage_gram_two_pass", False)
+    for m in members:
+        fill(m, gen, 0.02)                             # independent members: the SLERP branch
+    run("independent_speculative_redo", True)
+    run("independent_gram_two_pass", False)
+    print(json.dumps({"probe": "pop_slerp", "elements_per_member": P, "results": res}))
+
+
+if __name__ == "__main__":
+    main()
