@@ -82,6 +82,9 @@ using edt::g_err;
 #ifndef EDT_SLERP_STATS_TPW
 #define EDT_SLERP_STATS_TPW 16
 #endif
+#ifndef EDT_SLERP_POP_FUSED     // speculative population pass: 1 = member-major Gram pass when the distinct
+#define EDT_SLERP_POP_FUSED 1   // parents fit one tile (<= 8); 0 = always the co-located per-child pass
+#endif
 #ifndef EDT_SLERP_COEF_BLOCK    // 1: one workgroup per segment for the chunk-sum reduction (else one wave)
 #define EDT_SLERP_COEF_BLOCK 1
 #endif

@@ -102,18 +102,19 @@ __device__ __forceinline__ int red_index(int s, int lane, bool& owner) {
     return N - 1;
 }
 
-// Lane l writes, when it owns one, the value slot (l % 16) holds: store(index, value).
+// Lane l writes, when it owns one, the value slot (l % 16) holds: store(index, value). One
+// predicated store per slot (a register chosen by lane would be an indexed private array: scratch).
 template <int N, typename Store>
 __device__ __forceinline__ void red_store(const double (&r)[Red<N>::N2], Store&& store) {
     const int lane = threadIdx.x & 63, s = lane & 15;
-    if (s >= Red<N>::N2) return;
-    double x = r[0];
 #pragma unroll
-    for (int q = 1; q < Red<N>::N2; ++q)
-        if (s == q) x = r[q];
-    bool owner;
-    const int idx = red_index<N>(s, lane, owner);
-    if (owner) store(idx, x);
+    for (int q = 0; q < Red<N>::N2; ++q) {
+        if (s == q) {
+            bool owner;
+            const int idx = red_index<N>(q, lane, owner);
+            if (owner) store(idx, r[q]);
+        }
+    }
 }
 
 // ---- the chunk sums' canonical order (every form: pair, speculative, Gram, sharded) --------------
@@ -1698,7 +1699,7 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
     int D = 0;
     Members mem;
     memset(&mem, 0, sizeof(mem));
-    bool fused = npairs <= kBlendMaxChildren && nmembers <= 256;
+    bool fused = EDT_SLERP_POP_FUSED && npairs <= kBlendMaxChildren && nmembers <= 256;
     if (fused) {
         for (int m = 0; m < nmembers; ++m) compact[m] = -1;
         for (int q = 0; q < npairs && fused; ++q)

@@ -16,6 +16,7 @@ VARIANTS = {
     "tpw8": ["-DEDT_SLERP_STATS_TPW=8"],
     "nont": ["-DEDT_NT_SLERP=0"],
     "blendold": ["-DEDT_SLERP_BLEND_TILE=0"],
+    "popcoloc": ["-DEDT_SLERP_POP_FUSED=0"],
 }
 
 

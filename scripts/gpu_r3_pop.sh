@@ -5,7 +5,8 @@ set -u
 cd "$(dirname "$0")/.."
 R=$(pwd); OUT=$R/gpurun_out/${TAG:-r3p}
 mkdir -p $OUT
-timeout -k 10 400 python -u scripts/pop_slerp_probe.py --rounds 3 > $OUT/pop_probe.log 2>&1 || { tail -20 $OUT/pop_probe.log; exit 3; }
+V=""; [ -d variants_slerp ] && V="--variants variants_slerp"
+timeout -k 10 600 python -u scripts/pop_slerp_probe.py --rounds 3 $V > $OUT/pop_probe.log 2>&1 || { tail -20 $OUT/pop_probe.log; exit 3; }
 tail -1 $OUT/pop_probe.log
 (cd /tmp && export TMPDIR=/tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv \
     -d $OUT/pkt -o pop -- python3 $R/scripts/pop_slerp_probe.py --rounds 1 > $OUT/pkt.log 2>&1) || exit 4

@@ -32,7 +32,9 @@ def fill(dst, gen, scale, base=None, rel=0.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--variants", default="", help="also run every lib*.so in DIR (build_slerp_variants.py)")
     a = ap.parse_args()
+    from evolutionarydistributedtraining_amd import _lib as L
     from evolutionarydistributedtraining_amd import ops
     from evolutionarydistributedtraining_amd.layouts import qwen2p5_7b_body
     dev = torch.device("cuda:0")
@@ -70,12 +72,23 @@ def main():
     for m in members:
         fill(m, gen, 0.02, base=base, rel=0.005)       # one lineage: every segment in the lerp branch
     del base
-    run("lineage_speculative", True)
-    run("lineage_gram_two_pass", False)
+    import glob
+    libs = [("", L.load_library())] + [("/" + os.path.basename(f)[3:-3], L.load_library(f))
+                                       for f in sorted(glob.glob(os.path.join(a.variants, "lib*.so")))] \
+        if a.variants else [("", L.load_library())]
+    intree = L._lib
+
+    def forms(tag):
+        for sfx, lb in libs:
+            L._lib = lb                                # ops.* call through L.lib(): this build
+            run(f"{tag}_speculative{sfx}", True)
+            run(f"{tag}_gram_two_pass{sfx}", False)
+        L._lib = intree
+
+    forms("lineage")
     for m in members:
         fill(m, gen, 0.02)                             # independent members: the SLERP branch
-    run("independent_speculative_redo", True)
-    run("independent_gram_two_pass", False)
+    forms("independent")
     print(json.dumps({"probe": "pop_slerp", "elements_per_member": P, "results": res}))
 
 
