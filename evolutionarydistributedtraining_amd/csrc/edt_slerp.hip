@@ -828,11 +828,11 @@ struct BlendChildren {
 
 template <int IDT, int ODT>
 __global__ __launch_bounds__(kBlock) void slerp_blend_population_kernel(BlendChildren B, const uint64_t* chunks,
-                                                                        int64_t nchunks) {
+                                                                        int64_t nchunks, uint64_t c0) {
     const uint64_t per_group = 8ull * (uint64_t)B.nchildren;
     const uint64_t r = blockIdx.x % per_group;
     const int child = (int)(r / 8);
-    const int64_t c = (int64_t)((blockIdx.x / per_group) * 8 + (r % 8));
+    const int64_t c = (int64_t)(c0 + (blockIdx.x / per_group) * 8 + (r % 8));
     if (c >= nchunks) return;
     const uint64_t start = chunks[3 * c], len = chunks[3 * c + 1], seg = chunks[3 * c + 2];
     if (B.redo[child] && !B.redo[child][seg]) return;      // speculative lerp output stands
@@ -856,6 +856,20 @@ __global__ __launch_bounds__(kBlock) void slerp_blend_population_kernel(BlendChi
     }
 }
 
+// Co-located launches (block -> (unit, child), all children of 8 consecutive units on the XCDs of
+// those units): `units` split into launches of whole groups of 8 units under the dispatch cap.
+template <typename F>
+inline int colocated_launches(uint64_t units, int nchildren, F&& launch) {
+    const uint64_t per_launch = kGridBlockCap / (8ull * (uint64_t)nchildren) * 8ull;   // units, a multiple of 8
+    for (uint64_t u0 = 0; u0 < units; u0 += per_launch) {
+        const uint64_t n = units - u0 < per_launch ? units - u0 : per_launch;
+        launch(u0, (unsigned)((n + 7) / 8 * 8ull * (uint64_t)nchildren));
+        int rc = check_launch("co-located population kernel");
+        if (rc) return rc;
+    }
+    return EDT_OK;
+}
+
 // Speculative population pass for more than 8 distinct parents: block (unit, child) with the
 // co-located placement above, a unit being 4 tiles of a chunk (one per wave): the blocks of every
 // child for one unit carry the same blockIdx % 8 (one XCD, one L2). Each forms its child's tile
@@ -863,12 +877,12 @@ __global__ __launch_bounds__(kBlock) void slerp_blend_population_kernel(BlendChi
 // lerp-branch output in the same pass. Shared parents cross HBM once for all children.
 template <int IDT, int ODT>
 __global__ __launch_bounds__(kBlock) void slerp_pop_stats_lerp_kernel(BlendChildren B, const uint64_t* chunks,
-                                                                      int64_t nchunks, const double* tvals) {
+                                                                      int64_t nchunks, const double* tvals, uint64_t u0) {
     constexpr int upc = kTileSlots / 4;
     const uint64_t per_group = 8ull * (uint64_t)B.nchildren;
     const uint64_t r = blockIdx.x % per_group;
     const int child = (int)(r / 8);
-    const uint64_t u = (blockIdx.x / per_group) * 8 + (r % 8);
+    const uint64_t u = u0 + (blockIdx.x / per_group) * 8 + (r % 8);
     const uint64_t units = (uint64_t)nchunks * upc;
     if (u >= units) return;
     const uint64_t c = u / upc;
@@ -1525,18 +1539,16 @@ int edt_slerp_population(const void* const* members, int nmembers, int in_dt, co
             B.out[k] = outs[q];
             B.coef[k] = coef + 2 * (size_t)nseg * q;
         }
-        const uint64_t blocks = ((uint64_t)nchunks + 7) / 8 * 8ull * (uint64_t)B.nchildren;
-        if (blocks > kGridBlockCap) return fail(EDT_ERR_ARG, "too many chunks for one launch");
-        const unsigned gb = (unsigned)blocks;
-        if (in_dt == EDT_F32 && out_dt == EDT_F32)
-            slerp_blend_population_kernel<EDT_F32, EDT_F32><<<gb, kBlock, 0, s>>>(B, chunk_desc, nchunks);
-        else if (in_dt == EDT_F32)
-            slerp_blend_population_kernel<EDT_F32, EDT_BF16><<<gb, kBlock, 0, s>>>(B, chunk_desc, nchunks);
-        else if (out_dt == EDT_F32)
-            slerp_blend_population_kernel<EDT_BF16, EDT_F32><<<gb, kBlock, 0, s>>>(B, chunk_desc, nchunks);
-        else
-            slerp_blend_population_kernel<EDT_BF16, EDT_BF16><<<gb, kBlock, 0, s>>>(B, chunk_desc, nchunks);
-        rc = check_launch("slerp_blend_population_kernel");
+        rc = colocated_launches((uint64_t)nchunks, B.nchildren, [&](uint64_t c0, unsigned gb) {
+            if (in_dt == EDT_F32 && out_dt == EDT_F32)
+                slerp_blend_population_kernel<EDT_F32, EDT_F32><<<gb, kBlock, 0, s>>>(B, chunk_desc, nchunks, c0);
+            else if (in_dt == EDT_F32)
+                slerp_blend_population_kernel<EDT_F32, EDT_BF16><<<gb, kBlock, 0, s>>>(B, chunk_desc, nchunks, c0);
+            else if (out_dt == EDT_F32)
+                slerp_blend_population_kernel<EDT_BF16, EDT_F32><<<gb, kBlock, 0, s>>>(B, chunk_desc, nchunks, c0);
+            else
+                slerp_blend_population_kernel<EDT_BF16, EDT_BF16><<<gb, kBlock, 0, s>>>(B, chunk_desc, nchunks, c0);
+        });
         if (rc) return rc;
     }
     return EDT_OK;
@@ -1762,11 +1774,8 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
                 B.redo[k] = redo + (size_t)nseg * q;
                 B.slots[k] = partial + 3 * (size_t)nchunks * npairs + 3 * (size_t)kPairRows * nchunks * q;
             }
-            // pass 0: one block per (unit = chunk x slot group, child); pass 1: per (chunk, child)
+            // pass 0: one block per (unit = 4 tiles of a chunk, child); pass 1: per (chunk, child)
             const uint64_t units = pass == 0 ? (uint64_t)nchunks * (kTileSlots / 4) : (uint64_t)nchunks;
-            const uint64_t blocks = (units + 7) / 8 * 8ull * (uint64_t)B.nchildren;
-            if (blocks > kGridBlockCap) return fail(EDT_ERR_ARG, "too many chunks for one launch");
-            const unsigned gb = (unsigned)blocks;
 #define EDT_SPEC_POP(KERNEL, ...)                                                                   \
     do {                                                                                            \
         if (in_dt == EDT_F32 && out_dt == EDT_F32) KERNEL<EDT_F32, EDT_F32><<<gb, kBlock, 0, s>>>(__VA_ARGS__);   \
@@ -1774,10 +1783,11 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
         else if (out_dt == EDT_F32) KERNEL<EDT_BF16, EDT_F32><<<gb, kBlock, 0, s>>>(__VA_ARGS__);                 \
         else KERNEL<EDT_BF16, EDT_BF16><<<gb, kBlock, 0, s>>>(__VA_ARGS__);                                       \
     } while (0)
-            if (pass == 0) EDT_SPEC_POP(slerp_pop_stats_lerp_kernel, B, chunk_desc, nchunks, t);
-            else EDT_SPEC_POP(slerp_blend_population_kernel, B, chunk_desc, nchunks);
+            int rc = colocated_launches(units, B.nchildren, [&](uint64_t u0, unsigned gb) {
+                if (pass == 0) EDT_SPEC_POP(slerp_pop_stats_lerp_kernel, B, chunk_desc, nchunks, t, u0);
+                else EDT_SPEC_POP(slerp_blend_population_kernel, B, chunk_desc, nchunks, u0);
+            });
 #undef EDT_SPEC_POP
-            int rc = check_launch(pass == 0 ? "slerp_pop_stats_lerp_kernel" : "slerp_blend_population_kernel");
             if (rc) return rc;
         }
         if (pass == 0) {
