@@ -828,11 +828,11 @@ struct BlendChildren {
 
 template <int IDT, int ODT>
 __global__ __launch_bounds__(kBlock) void slerp_blend_population_kernel(BlendChildren B, const uint64_t* chunks,
-                                                                        int64_t nchunks, uint64_t c0) {
+                                                                        int64_t nchunks, uint64_t cbase) {
     const uint64_t per_group = 8ull * (uint64_t)B.nchildren;
     const uint64_t r = blockIdx.x % per_group;
     const int child = (int)(r / 8);
-    const int64_t c = (int64_t)(c0 + (blockIdx.x / per_group) * 8 + (r % 8));
+    const int64_t c = (int64_t)(cbase + (blockIdx.x / per_group) * 8 + (r % 8));
     if (c >= nchunks) return;
     const uint64_t start = chunks[3 * c], len = chunks[3 * c + 1], seg = chunks[3 * c + 2];
     if (B.redo[child] && !B.redo[child][seg]) return;      // speculative lerp output stands
