@@ -82,8 +82,16 @@ using edt::g_err;
 #ifndef EDT_SLERP_STATS_TPW
 #define EDT_SLERP_STATS_TPW 16
 #endif
-#ifndef EDT_SLERP_POP_FUSED     // speculative population pass: 1 = member-major Gram pass when the distinct
-#define EDT_SLERP_POP_FUSED 1   // parents fit one tile (<= 8); 0 = always the co-located per-child pass
+// Speculative population pass: 1 = the member-major Gram pass when the distinct parents fit one
+// tile (<= 8: each parent's registers feed every child, picked by a runtime index — a private array
+// in scratch); 0 = always the co-located per-child pass (block -> (unit, child), children of a unit
+// on one XCD, shared parents from L2). 8 x 7B bf16, lineage (profiles/r03_pop_probe*.json):
+// 42.4 ms co-located against 67.2 ms member-major (floor at 6 TB/s: 37.7 ms).
+#ifndef EDT_SLERP_POP_FUSED
+#define EDT_SLERP_POP_FUSED 0
+#endif
+#ifndef EDT_SLERP_GRAM_PIPE     // Gram stats pass: 1 = the next tile's loads issued before this tile's math
+#define EDT_SLERP_GRAM_PIPE 1
 #endif
 #ifndef EDT_SLERP_COEF_BLOCK    // 1: one workgroup per segment for the chunk-sum reduction (else one wave)
 #define EDT_SLERP_COEF_BLOCK 1

@@ -17,6 +17,8 @@ VARIANTS = {
     "nont": ["-DEDT_NT_SLERP=0"],
     "blendold": ["-DEDT_SLERP_BLEND_TILE=0"],
     "popcoloc": ["-DEDT_SLERP_POP_FUSED=0"],
+    "popfused": ["-DEDT_SLERP_POP_FUSED=1"],
+    "gramnopipe": ["-DEDT_SLERP_GRAM_PIPE=0"],
 }
 
 
