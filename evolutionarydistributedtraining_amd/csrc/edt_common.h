@@ -90,9 +90,6 @@ using edt::g_err;
 #ifndef EDT_SLERP_POP_FUSED
 #define EDT_SLERP_POP_FUSED 0
 #endif
-#ifndef EDT_SLERP_GRAM_PIPE     // Gram stats pass: 1 = the next tile's loads issued before this tile's math
-#define EDT_SLERP_GRAM_PIPE 1
-#endif
 #ifndef EDT_SLERP_COEF_BLOCK    // 1: one workgroup per segment for the chunk-sum reduction (else one wave)
 #define EDT_SLERP_COEF_BLOCK 1
 #endif

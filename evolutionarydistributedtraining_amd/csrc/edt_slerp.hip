@@ -739,41 +739,6 @@ __global__ __launch_bounds__(kBlock) void slerp_gram_kernel(Members mem, PopLerp
             l0 = (float)(1.0 - tvals[seg]);
             l1 = (float)tvals[seg];
         }
-        if constexpr (!EMIT && EDT_SLERP_GRAM_PIPE) {
-            // the next tile's M vectors are loaded before this tile's FMAs and butterflies, so a
-            // wave always has loads in flight (two register sets, the loop unrolled)
-            const uint64_t a = (start + kVec - 1) / kVec * kVec, b = (start + len) / kVec * kVec;
-            const int j0 = 16 * g + 4 * wave;
-            auto at = [&](int j) { return a + (uint64_t)j * kTileElems + (uint64_t)lane * kVec; };
-            auto valid = [&](int j) { return a < b && at(j) < b; };
-            Raw8<IDT> x[2][M];
-            if (valid(j0)) {
-#pragma unroll
-                for (int m = 0; m < M; ++m) x[0][m] = ld_raw<IDT, false>(mem.p[m], at(j0));
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int j = j0 + k;
-                if (k < 3 && valid(j + 1)) {
-#pragma unroll
-                    for (int m = 0; m < M; ++m) x[(k + 1) & 1][m] = ld_raw<IDT, false>(mem.p[m], at(j + 1));
-                }
-                double gs[NT];
-#pragma unroll
-                for (int q = 0; q < NT; ++q) gs[q] = 0.0;
-                if (valid(j)) gram_fma<M, kVec>(x[k & 1], gs);
-                if (j == 0)
-                    tile0_edge(start, len, [&](uint64_t i) {
-                        Raw1 e[M];
-#pragma unroll
-                        for (int m = 0; m < M; ++m) ld<IDT, 1>(mem.p[m], i, e[m].v);
-                        gram_fma<M, 1>(e, gs);
-                    });
-                double r[Red<NT>::N2];
-                tile_reduce<NT>(gs, r);
-                red_store<NT>(r, [&](int q, double v) { ts[4 * wave + k][q] = v; });
-            }
-        } else
 #pragma unroll(M <= 2 ? 4 : 1)
         for (int k = 0; k < 4; ++k) {
             const int j = 16 * g + 4 * wave + k;

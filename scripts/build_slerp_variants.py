@@ -18,7 +18,6 @@ VARIANTS = {
     "blendold": ["-DEDT_SLERP_BLEND_TILE=0"],
     "popcoloc": ["-DEDT_SLERP_POP_FUSED=0"],
     "popfused": ["-DEDT_SLERP_POP_FUSED=1"],
-    "gramnopipe": ["-DEDT_SLERP_GRAM_PIPE=0"],
 }
 
 

@@ -41,7 +41,7 @@ def main():
         out["pair_merge/gpt_1p3b/bf16"] = pm
     spec = traffic("pair_sums_kernel<1, true")
     stats = traffic("pair_sums_kernel<1, false")
-    blend = traffic("slerp_blend_kernel<1, 1, true, true>")
+    blend = traffic("slerp_blend_tile_kernel<1, 1, true>")
     if spec:
         out["slerp_7b/lineage"] = {"passes": [spec], "hbm_bytes_per_launch": spec["hbm_bytes_per_launch"],
                                    "algorithmic_bytes": 6 * P7,

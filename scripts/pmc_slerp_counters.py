@@ -1,6 +1,7 @@
 """Summarise scripts/pmc_slerp_counters.sh: per kernel (lerp, speculative pass, two-pass stats and
 blend) the median of every counter over its launches, plus the ratios the verdict asked for —
-waves per CU and occupancy (SQ_WAVE_CYCLES counts quad-cycles: x4 / GRBM_GUI_ACTIVE / 256 CUs),
+waves per CU and occupancy (SQ_WAVE_CYCLES counts quad-cycles, summed over the chip: x4; GRBM_GUI_ACTIVE
+is summed over the 8 XCDs: / 8 is the kernel's cycles — lerp's 1.17e8 over its 7.0 ms = 8 x 2.1 GHz),
 the share of wave time parked (SQ_WAIT_ANY) vs issuing, and write combining (64-B write requests
 of all write requests at the memory side).
 
@@ -14,9 +15,10 @@ import statistics
 import sys
 
 KERNELS = {"lerp": "lerp_kernel<1, 1, 1, 8>", "speculative": "pair_sums_kernel<1, true, 1>",
-           "stats": "pair_sums_kernel<1, false", "blend": "slerp_blend_kernel<1, 1, true, true>",
+           "stats": "pair_sums_kernel<1, false", "blend": "slerp_blend_tile_kernel<1, 1, true>",
            "tree_reduce": "tree_reduce_kernel"}
 CUS = 256
+XCDS = 8
 
 
 def main():
@@ -35,8 +37,9 @@ def main():
         rec = {"launches": max((len(v) for v in cs.values()), default=0), "counters": med}
         g = med.get("GRBM_GUI_ACTIVE")
         if g and "SQ_WAVE_CYCLES" in med:
-            rec["mean_waves_per_cu"] = round(4 * med["SQ_WAVE_CYCLES"] / g / CUS, 2)
-            rec["occupancy_of_32_waves_per_cu"] = round(4 * med["SQ_WAVE_CYCLES"] / g / CUS / 32, 3)
+            cyc = g / XCDS
+            rec["mean_waves_per_cu"] = round(4 * med["SQ_WAVE_CYCLES"] / cyc / CUS, 2)
+            rec["occupancy_of_32_waves_per_cu"] = round(4 * med["SQ_WAVE_CYCLES"] / cyc / CUS / 32, 3)
         if "SQ_WAVE_CYCLES" in med and "SQ_WAIT_ANY" in med:
             rec["wave_time_parked"] = round(med["SQ_WAIT_ANY"] / med["SQ_WAVE_CYCLES"], 3)
             rec["wave_time_issuing"] = round(med.get("SQ_ACTIVE_INST_ANY", 0) / med["SQ_WAVE_CYCLES"], 3)
