@@ -122,18 +122,19 @@ __device__ __forceinline__ void red_store(const double (&r)[Red<N>::N2], Store&&
 // body [a, b): tile j holds, on lane l, the 8 elements at a + 512 j + 8 l (when below b); tile 0's
 // lanes also take the < 16 head / tail elements (lane l the l-th of them) after their vector. Per
 // lane the products are accumulated in element order by fp64 FMAs; the wave's xor butterfly
-// (wave_sum) gives the TILE SUM; the chunk's sum is the perfect binary tree over its 128 tile sums
+// (wave_sum's order, formed on the VALU by tile_reduce) gives the TILE SUM; the chunk's sum is the perfect binary tree over its 128 tile sums
 // in order, adjacent pairs first ((t0 + t1) + (t2 + t3)) + ..., empty tiles 0.0. Every kernel forms
-// complete subtrees — one tile per wave (a level-0 row), four tiles per wave combined in registers
-// (level 2), sixteen per workgroup combined in LDS (level 4) — and writes them as rows;
+// complete subtrees — one tile per wave (a level-0 row), kStatsTPW tiles per wave combined in
+// registers (the read-only stats pass), sixteen per workgroup combined in LDS (level 4) — and
+// writes them as rows;
 // tree_reduce_kernel finishes each chunk's tree from its rows. So every form's per-chunk sums are
 // bit-identical whatever the work split, with no workgroup barrier in the pair passes.
 //
-// Why this shape (profiles/r03_spec_probe*.json, scripts/spec_probe.hip on the 7B body): the
+// Why this shape (profiles/r03_spec_probe_{a,b,c}.json, scripts/spec_probe.hip on the 7B body): the
 // speculative pass is lerp's stream (2 reads + 1 write per element) plus the sums; one tile per wave
-// in address order — lerp's own grid — costs nothing measurable for the fp64 math and butterflies
-// (6.94 ms vs lerp 6.92 with the row store removed); what does cost is the rows' second write
-// stream: 24-B rows scattered over the table +11 %, whole lines +1-3 %, and rows placed XCD-major
+// in address order — lerp's own grid — costs little for the fp64 math and butterflies (6.91-7.02 ms
+// vs lerp 6.80-6.92 with the row store removed); what does cost is the rows' second write stream:
+// 24-B rows scattered over the table +11 %, rows padded to whole lines +3-7 %, rows placed XCD-major
 // (each XCD's workgroups write one contiguous stretch, so its L2 writes back whole lines) +1.3 %.
 // The previous form (one workgroup per 64 Ki chunk, grid-stride, an LDS block reduction per chunk)
 // ran 7.1-8.3 ms depending on the allocation.
