@@ -4,7 +4,7 @@
 # library's sha256), and the SLERP counter passes (spec pass vs lerp).
 set -u
 cd "$(dirname "$0")/.."
-R=$(pwd); OUT=$R/gpurun_out/${TAG:-r3f}
+R=$(pwd); OUT=$R/gpurun_out/${TAG:-r3final}
 mkdir -p $OUT
 timeout -k 10 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 3; }
 tail -c 600 $OUT/bench.json; echo
