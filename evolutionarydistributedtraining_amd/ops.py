@@ -308,15 +308,46 @@ def _refdot_pass(plan: SlerpPlan, v0: torch.Tensor, v1: torch.Tensor, t: torch.T
             "edt_slerp_refdot_coef")
 
 
-def _speculation_pays(plan: SlerpPlan, in_bytes: int, out_bytes: int) -> bool:
+def _record_dots(plan: SlerpPlan, dots: torch.Tensor, attr: str) -> None:
+    """After a merge: the dots go to pinned host memory by an async copy on the merge's stream, with
+    an event, so the next call can judge its form without synchronising the device."""
+    host = getattr(plan, attr + "_host", None)
+    if host is None or host.shape != dots.shape:
+        host = torch.empty(dots.shape, dtype=dots.dtype, pin_memory=True)
+        setattr(plan, attr + "_host", host)
+    host.copy_(dots, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(dots.device))
+    setattr(plan, attr + "_event", ev)
+
+
+def _host_dots(plan: SlerpPlan, attr: str, wait: bool):
+    """The previous merge's dots on the host (numpy), or None while its copy is still in flight
+    (wait=False: never blocks; wait=True: waits for that copy only)."""
+    ev = getattr(plan, attr + "_event", None)
+    if ev is None:
+        return None
+    if wait:
+        ev.synchronize()
+    elif not ev.query():
+        return None
+    return getattr(plan, attr + "_host").numpy()
+
+
+def _speculation_pays(plan: SlerpPlan, in_bytes: int, out_bytes: int, wait: bool = True) -> bool:
     """Whether the speculative form is cheaper for the next merge on this plan, judged from the
     dots the previous merge on it produced (both forms write them): with a fraction f of the
     elements in SLERP-branch segments it moves (1 + f)(2 b_in + b_out) bytes per element against
-    4 b_in + b_out. No previous merge: speculate (EDT parents share a lineage)."""
+    4 b_in + b_out. No previous merge: speculate (EDT parents share a lineage). wait=False (what
+    slerp_arena uses): when the previous merge's dots have not reached the host yet — calls issued
+    back to back — the previous decision stands, so deciding never synchronises the device."""
     if getattr(plan, "_last_thr", None) is None:
         return True
     import numpy as np
-    dots = plan.dots[:plan.nseg].cpu().numpy()
+    dots = _host_dots(plan, "_dots", wait)
+    if dots is None:
+        return getattr(plan, "_last_speculate", True)
+    dots = dots[:plan.nseg]
     sizes = np.diff(np.asarray(plan.seg_offsets, dtype=np.int64))
     total = max(1, int(sizes.sum()))
     f = float(sizes[np.abs(dots) <= plan._last_thr].sum()) / total
@@ -358,9 +389,11 @@ def slerp_arena(plan: SlerpPlan, v0: torch.Tensor, v1: torch.Tensor, out: torch.
         L.check(lib.edt_slerp_blend(L.ptr(v0), L.ptr(v1), L.dtype_code(v0), L.ptr(out), L.dtype_code(out),
                                     L.ptr(plan.chunks), plan.nchunks, L.ptr(plan.coef), st), "edt_slerp_blend")
         plan._last_thr = float(dot_threshold)
+        _record_dots(plan, plan.dots[:max(1, plan.nseg)], "_dots")
         return
     if speculate is None:
-        speculate = _speculation_pays(plan, v0.element_size(), out.element_size())
+        speculate = _speculation_pays(plan, v0.element_size(), out.element_size(), wait=False)
+        plan._last_speculate = speculate
     if speculate and (_overlap(out, v0) or _overlap(out, v1)):
         speculate = False
     if speculate:
@@ -378,6 +411,7 @@ def slerp_arena(plan: SlerpPlan, v0: torch.Tensor, v1: torch.Tensor, out: torch.
                                     float(dot_threshold), float(eps), L.ptr(plan.partial), L.ptr(plan.coef),
                                     L.ptr(plan.dots), L.stream_ptr(v0.device)), "edt_slerp_merge")
     plan._last_thr = float(dot_threshold)
+    _record_dots(plan, plan.dots[:max(1, plan.nseg)], "_dots")
 
 
 def slerp_list(plan: SlerpPlan, v0s: list[torch.Tensor], v1s: list[torch.Tensor], outs: list[torch.Tensor],
@@ -437,12 +471,13 @@ def slerp_population(plan: SlerpPlan, members: list[torch.Tensor], pairs, outs: 
     if t.dtype != torch.float64 or t.numel() < plan.nseg:
         raise L.EdtError("t must be a float64 device tensor with one value per segment")
     if speculate is None:
-        prev = getattr(plan, "_pop_dots", None)
-        if prev is None or getattr(plan, "_last_thr", None) is None:
+        d = _host_dots(plan, "_pop_dots", wait=False) if getattr(plan, "_last_thr", None) is not None else None
+        if getattr(plan, "_pop_dots", None) is None or getattr(plan, "_last_thr", None) is None:
             speculate = True
+        elif d is None or d.shape[0] == 0:        # previous dots still in flight: keep its decision
+            speculate = getattr(plan, "_last_pop_speculate", True)
         else:
             import numpy as np
-            d = prev.cpu().numpy()
             sizes = np.diff(np.asarray(plan.seg_offsets, dtype=np.int64))
             f = float((sizes[None, :] * (np.abs(d) <= plan._last_thr)).sum()) / max(1, int(sizes.sum()) * d.shape[0])
             # member-major passes over D distinct parents: speculating costs (1 + f)(D b_in + Q b_out)
@@ -450,6 +485,7 @@ def slerp_population(plan: SlerpPlan, members: list[torch.Tensor], pairs, outs: 
             D = len({int(x) for p in pairs for x in p})
             bi, bo = members[0].element_size(), (outs[0].element_size() if outs else members[0].element_size())
             speculate = f < D * bi / max(1, D * bi + Q * bo)
+        plan._last_pop_speculate = speculate
     if any(_overlap(o, m) for o in outs for m in members):
         speculate = False
     if not speculate and not 1 <= M <= 8:
@@ -479,6 +515,7 @@ def slerp_population(plan: SlerpPlan, members: list[torch.Tensor], pairs, outs: 
                 "edt_slerp_population")
     plan._pop_dots = dots[:Q, :plan.nseg]
     plan._last_thr = float(dot_threshold)
+    _record_dots(plan, plan._pop_dots, "_pop_dots")
     return plan._pop_dots
 
 
