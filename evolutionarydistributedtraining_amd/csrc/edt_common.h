@@ -90,6 +90,9 @@ using edt::g_err;
 #ifndef EDT_SLERP_POP_FUSED
 #define EDT_SLERP_POP_FUSED 0
 #endif
+#ifndef EDT_SLERP_SPEC_WG_ROWS  // speculative pair pass: 0 = a level-0 row per wave (no barrier); 1 = the four
+#define EDT_SLERP_SPEC_WG_ROWS 0 // waves' tile sums combined through LDS into one level-2 row per workgroup
+#endif
 #ifndef EDT_SLERP_COEF_BLOCK    // 1: one workgroup per segment for the chunk-sum reduction (else one wave)
 #define EDT_SLERP_COEF_BLOCK 1
 #endif

@@ -147,6 +147,7 @@ constexpr int kWavesPerBlock = kBlock / 64;
 constexpr int kPairRows = kTileSlots;                         // rows per chunk, level 0
 constexpr int kGramRows = kTileSlots / 16;                    // rows per chunk, level 4
 constexpr int kStatsTPW = EDT_SLERP_STATS_TPW;                // tiles per wave of the read-only pass
+constexpr bool kSpecWgRows = EDT_SLERP_SPEC_WG_ROWS != 0;     // speculative pass: one row per workgroup
 
 // One-pass grids of `units` workgroups in address order (a unit = a fixed set of a chunk's tiles);
 // past the dispatch cap (a multiple of 8, so blockIdx % 8 stays the unit's XCD) they stride.
@@ -471,7 +472,18 @@ __global__ __launch_bounds__(kBlock) void pair_sums_kernel(const void* v0, const
             o = reinterpret_cast<void*>(seg_ptrs[3 * seg + 2]);
         }
         double* row = rows + (unit_slot(u, units) * kWavesPerBlock + wave) * 3;
-        if constexpr (EMIT) {
+        if constexpr (EMIT && kSpecWgRows) {
+            // one level-2 row per workgroup: the four waves' tile sums through LDS, combined as
+            // the tree does ((t0 + t1) + (t2 + t3)) — a quarter of the row bytes, one barrier
+            __shared__ double part[kWavesPerBlock][3];
+            pair_tile<IDT, NT, true, ODT>(a, b, o, chunks[3 * c], chunks[3 * c + 1], 4 * g + wave,
+                                          (float)(1.0 - tvals[seg]), (float)tvals[seg], &part[wave][0]);
+            __syncthreads();
+            if (threadIdx.x < 3) {
+                const int q = threadIdx.x;
+                rows[unit_slot(u, units) * 3 + q] = (part[0][q] + part[1][q]) + (part[2][q] + part[3][q]);
+            }
+        } else if constexpr (EMIT) {
             pair_tile<IDT, NT, true, ODT>(a, b, o, chunks[3 * c], chunks[3 * c + 1], 4 * g + wave,
                                           (float)(1.0 - tvals[seg]), (float)tvals[seg], row);
         } else {
@@ -501,7 +513,8 @@ int pair_sums(const void* v0, const void* v1, int in_dt, void* out, int out_dt, 
         int rc = check_launch(emit ? "pair_sums_kernel (speculative)" : "pair_sums_kernel");
         if (rc) return rc;
     }
-    // rows per chunk: 128 (level 0, one per unit's wave) or 128 / kStatsTPW
+    // rows per chunk: 128 (level 0, one per unit's wave), 32 (level 2, one per unit) or 128 / kStatsTPW
+    if (emit && kSpecWgRows) return launch_tree_reduce(rows, 3, upc, upc, 1, nchunks, partial, s);
     return launch_tree_reduce(rows, 3, upc * kWavesPerBlock, upc, kWavesPerBlock, nchunks, partial, s);
 }
 
@@ -829,7 +842,9 @@ struct BlendChildren {
 
 template <int IDT, int ODT>
 __global__ __launch_bounds__(kBlock) void slerp_blend_population_kernel(BlendChildren B, const uint64_t* chunks,
-                                                                        int64_t nchunks, uint64_t cbase) {
+                                                                        int64_t nchunks, uint64_t cbase,
+                                                                        const int32_t* any_redo = nullptr) {
+    if (any_redo && *any_redo == 0) return;       // no child needs a segment blended again
     const uint64_t per_group = 8ull * (uint64_t)B.nchildren;
     const uint64_t r = blockIdx.x % per_group;
     const int child = (int)(r / 8);
@@ -878,7 +893,9 @@ inline int colocated_launches(uint64_t units, int nchildren, F&& launch) {
 // lerp-branch output in the same pass. Shared parents cross HBM once for all children.
 template <int IDT, int ODT>
 __global__ __launch_bounds__(kBlock) void slerp_pop_stats_lerp_kernel(BlendChildren B, const uint64_t* chunks,
-                                                                      int64_t nchunks, const double* tvals, uint64_t u0) {
+                                                                      int64_t nchunks, const double* tvals, uint64_t u0,
+                                                                      int32_t* zero_word) {
+    if (zero_word && u0 == 0 && blockIdx.x == 0 && threadIdx.x == 0) *zero_word = 0;   // the any-redo flag
     constexpr int upc = kTileSlots / 4;
     const uint64_t per_group = 8ull * (uint64_t)B.nchildren;
     const uint64_t r = blockIdx.x % per_group;
@@ -1455,7 +1472,7 @@ uint64_t edt_slerp_population_speculative_doubles(int npairs, int64_t nchunks) {
     // co-located per-child form: each child's chunk rows + level-0 rows; member-major: <= 36 Gram sums
     const uint64_t pair = 3ull * (uint64_t)npairs * (1ull + kPairRows);
     const uint64_t gram = 36ull * (1ull + kGramRows);                    // 36: 8 x 9 / 2
-    return (uint64_t)nchunks * (pair > gram ? pair : gram);
+    return (uint64_t)nchunks * (pair > gram ? pair : gram) + 1;           // + the any-redo word
 }
 
 uint64_t edt_slerp_population_gram_doubles(int nmembers, int64_t nchunks) {
@@ -1761,6 +1778,9 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
         }
         return launch_blend_mm(mem, D, pb, in_dt, out_dt, chunk_desc, nchunks, s);
     }
+    // the any-redo word (the workspace's last double): zeroed by the first pass, set by any child's
+    // coefficient kernel that sends a segment to the SLERP branch; clear, the redo grid exits at once
+    int32_t* any = reinterpret_cast<int32_t*>(partial + edt_slerp_population_speculative_doubles(npairs, nchunks) - 1);
     for (int pass = 0; pass < 2; ++pass) {
         for (int q0 = 0; q0 < npairs; q0 += kBlendMaxChildren) {
             BlendChildren B;
@@ -1785,8 +1805,8 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
         else KERNEL<EDT_BF16, EDT_BF16><<<gb, kBlock, 0, s>>>(__VA_ARGS__);                                       \
     } while (0)
             int rc = colocated_launches(units, B.nchildren, [&](uint64_t u0, unsigned gb) {
-                if (pass == 0) EDT_SPEC_POP(slerp_pop_stats_lerp_kernel, B, chunk_desc, nchunks, t, u0);
-                else EDT_SPEC_POP(slerp_blend_population_kernel, B, chunk_desc, nchunks, u0);
+                if (pass == 0) EDT_SPEC_POP(slerp_pop_stats_lerp_kernel, B, chunk_desc, nchunks, t, u0, any);
+                else EDT_SPEC_POP(slerp_blend_population_kernel, B, chunk_desc, nchunks, u0, any);
             });
 #undef EDT_SPEC_POP
             if (rc) return rc;
@@ -1799,7 +1819,8 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
                 if (rc) return rc;
                 slerp_coef_kernel<<<coef_grid(nseg), kBlock, 0, s>>>(
                     partial + 3 * (size_t)nchunks * q, seg_first_chunk, nseg, t, (float)dot_threshold, (float)eps,
-                    coef + 2 * (size_t)nseg * q, dot_out ? dot_out + (size_t)nseg * q : nullptr, redo + (size_t)nseg * q);
+                    coef + 2 * (size_t)nseg * q, dot_out ? dot_out + (size_t)nseg * q : nullptr, redo + (size_t)nseg * q,
+                    any);
                 rc = check_launch("slerp_coef_kernel");
                 if (rc) return rc;
             }

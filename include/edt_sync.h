@@ -259,9 +259,11 @@ int edt_slerp_population(const void* const* members, int nmembers, int in_dt, co
 /* edt_slerp_population with edt_slerp_merge_speculative's first pass: one co-located launch
  * (every child of a chunk on one XCD, shared parents read once) forms each child's chunk sums and
  * writes its lerp-branch output; per child the coefficients flag (redo: [npairs][nseg] int32) the
- * SLERP-branch segments, which one co-located launch blends again. When the children's distinct
- * parents number <= 8 (and npairs <= 16) the first pass is member-major instead: one launch loads
- * each distinct parent's tile once, forms their Gram sums and writes every child's lerp output.
+ * SLERP-branch segments, which one co-located launch blends again (it exits at once when no child
+ * needs any). A build with EDT_SLERP_POP_FUSED=1 makes the first pass member-major instead when the
+ * children's distinct parents number <= 8 (and npairs <= 16): one launch loads each distinct
+ * parent's tile once, forms their Gram sums and writes every child's lerp output (slower with the
+ * canonical sum order: DESIGN §6.9).
  * partial: edt_slerp_population_speculative_doubles(npairs, nchunks) doubles of workspace.
  * Outputs must not overlap any member (n elements each). Bit-identical to edt_slerp_merge per
  * child either way. */
