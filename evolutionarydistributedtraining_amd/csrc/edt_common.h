@@ -90,8 +90,12 @@ using edt::g_err;
 #ifndef EDT_SLERP_POP_FUSED
 #define EDT_SLERP_POP_FUSED 0
 #endif
-#ifndef EDT_SLERP_SPEC_WG_ROWS  // speculative pair pass: 0 = a level-0 row per wave (no barrier); 1 = the four
-#define EDT_SLERP_SPEC_WG_ROWS 0 // waves' tile sums combined through LDS into one level-2 row per workgroup
+// Speculative passes (pair and co-located population): 1 = the four waves' tile sums combined
+// through LDS into one level-2 row per workgroup (a quarter of the row bytes, one barrier); 0 = a
+// level-0 row per wave, no barrier. 7B lineage merge, one box, interleaved (profiles/
+// r03_spec_wg_rows.jsonl): 7.01-7.03 ms against 7.14-7.17, lerp 6.96.
+#ifndef EDT_SLERP_SPEC_WG_ROWS
+#define EDT_SLERP_SPEC_WG_ROWS 1
 #endif
 #ifndef EDT_SLERP_COEF_BLOCK    // 1: one workgroup per segment for the chunk-sum reduction (else one wave)
 #define EDT_SLERP_COEF_BLOCK 1

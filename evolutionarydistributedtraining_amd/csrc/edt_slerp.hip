@@ -124,11 +124,13 @@ __device__ __forceinline__ void red_store(const double (&r)[Red<N>::N2], Store&&
 // lane the products are accumulated in element order by fp64 FMAs; the wave's xor butterfly
 // (wave_sum's order, formed on the VALU by tile_reduce) gives the TILE SUM; the chunk's sum is the perfect binary tree over its 128 tile sums
 // in order, adjacent pairs first ((t0 + t1) + (t2 + t3)) + ..., empty tiles 0.0. Every kernel forms
-// complete subtrees — one tile per wave (a level-0 row), kStatsTPW tiles per wave combined in
+// complete subtrees — one tile per wave (the speculative passes: the workgroup's four combined
+// through LDS into a level-2 row, kSpecWgRows; else a level-0 row), kStatsTPW tiles per wave combined in
 // registers (the read-only stats pass), sixteen per workgroup combined in LDS (level 4) — and
 // writes them as rows;
 // tree_reduce_kernel finishes each chunk's tree from its rows. So every form's per-chunk sums are
-// bit-identical whatever the work split, with no workgroup barrier in the pair passes.
+// bit-identical whatever the work split (the read-only pass needs no workgroup barrier; the
+// speculative passes take one: a quarter of the row bytes measured faster, EDT_SLERP_SPEC_WG_ROWS).
 //
 // Why this shape (profiles/r03_spec_probe_{a,b,c}.json, scripts/spec_probe.hip on the 7B body): the
 // speculative pass is lerp's stream (2 reads + 1 write per element) plus the sums; one tile per wave
@@ -441,7 +443,8 @@ __device__ __forceinline__ void for_range_elems(uint64_t start, uint64_t end, F&
 
 // The pair sums' rows, one workgroup per unit in address order (unit_slot: XCD-major rows).
 // EMIT (the speculative first pass, edt_slerp_merge_speculative): unit = 4 tiles, one per wave
-// (level-0 rows), lerp's own grid; the lerp-branch output (1-t) v0 + t v1 with the coefficients
+// (a level-2 row per workgroup, or level-0 rows per wave), lerp's own grid; the lerp-branch
+// output (1-t) v0 + t v1 with the coefficients
 // slerp_coefficients gives that branch is written in the same pass. Parents of one lineage
 // (fine-tunes of a common base) mostly have |dot| > 0.9995, where this output is final; the other
 // segments are blended again. Read-only (the two-pass stats): unit = 4 kStatsTPW tiles,
@@ -836,7 +839,7 @@ struct BlendChildren {
     void* out[kBlendMaxChildren];
     const float* coef[kBlendMaxChildren];     // [nseg][2] of the child
     const int32_t* redo[kBlendMaxChildren];   // [nseg] of the child, or null: blend every segment
-    double* slots[kBlendMaxChildren];         // the child's level-0 rows (speculative stats pass)
+    double* slots[kBlendMaxChildren];         // the child's row table (speculative stats pass)
     int nchildren;
 };
 
@@ -889,7 +892,7 @@ inline int colocated_launches(uint64_t units, int nchildren, F&& launch) {
 // Speculative population pass for more than 8 distinct parents: block (unit, child) with the
 // co-located placement above, a unit being 4 tiles of a chunk (one per wave): the blocks of every
 // child for one unit carry the same blockIdx % 8 (one XCD, one L2). Each forms its child's tile
-// sums exactly as pair_tile() does (level-0 rows, the child's own row table) and writes the
+// sums exactly as pair_sums_kernel does (the child's own row table) and writes the
 // lerp-branch output in the same pass. Shared parents cross HBM once for all children.
 template <int IDT, int ODT>
 __global__ __launch_bounds__(kBlock) void slerp_pop_stats_lerp_kernel(BlendChildren B, const uint64_t* chunks,
@@ -907,9 +910,22 @@ __global__ __launch_bounds__(kBlock) void slerp_pop_stats_lerp_kernel(BlendChild
     const int wave = (int)(threadIdx.x >> 6);
     const uint64_t seg = chunks[3 * c + 2];
     // default-policy loads: a parent's chunk is re-read by its other children from L2
-    pair_tile<IDT, false, true, ODT>(B.v0[child], B.v1[child], B.out[child], chunks[3 * c], chunks[3 * c + 1],
-                                     (int)(u % upc) * kWavesPerBlock + wave, (float)(1.0 - tvals[seg]),
-                                     (float)tvals[seg], B.slots[child] + (unit_slot(u, units) * kWavesPerBlock + wave) * 3);
+    if constexpr (kSpecWgRows) {                      // one level-2 row per block, as pair_sums_kernel
+        __shared__ double part[kWavesPerBlock][3];
+        pair_tile<IDT, false, true, ODT>(B.v0[child], B.v1[child], B.out[child], chunks[3 * c], chunks[3 * c + 1],
+                                         (int)(u % upc) * kWavesPerBlock + wave, (float)(1.0 - tvals[seg]),
+                                         (float)tvals[seg], &part[wave][0]);
+        __syncthreads();
+        if (threadIdx.x < 3) {
+            const int q = threadIdx.x;
+            B.slots[child][unit_slot(u, units) * 3 + q] = (part[0][q] + part[1][q]) + (part[2][q] + part[3][q]);
+        }
+    } else {
+        pair_tile<IDT, false, true, ODT>(B.v0[child], B.v1[child], B.out[child], chunks[3 * c], chunks[3 * c + 1],
+                                         (int)(u % upc) * kWavesPerBlock + wave, (float)(1.0 - tvals[seg]),
+                                         (float)tvals[seg],
+                                         B.slots[child] + (unit_slot(u, units) * kWavesPerBlock + wave) * 3);
+    }
 }
 
 // Per segment for the pair (i, j): slerp_coef_kernel's reduction over the chunks, reading the
@@ -1814,7 +1830,8 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
         if (pass == 0) {
             for (int q = 0; q < npairs; ++q) {
                 int rc = launch_tree_reduce(partial + 3 * (size_t)nchunks * npairs + 3 * (size_t)kPairRows * nchunks * q, 3,
-                                            kPairRows, kTileSlots / 4, kWavesPerBlock, nchunks,
+                                            kSpecWgRows ? kTileSlots / 4 : kPairRows, kTileSlots / 4,
+                                            kSpecWgRows ? 1 : kWavesPerBlock, nchunks,
                                             partial + 3 * (size_t)nchunks * q, s);
                 if (rc) return rc;
                 slerp_coef_kernel<<<coef_grid(nseg), kBlock, 0, s>>>(

@@ -180,7 +180,7 @@ int64_t edt_slerp_make_chunks(const uint64_t* seg_offsets_host, int nseg, uint32
 
 /* Chunk-sum tables. Every chunk's fp64 sums are formed in one canonical order (edt_slerp.hip:
  * per-lane FMA chains over 512-element tiles, the wave butterfly, a perfect binary tree over the
- * tiles), written as partial-tree rows with no workgroup barrier: a table of W sums per chunk
+ * tiles), written as partial-tree rows: a table of W sums per chunk
  * therefore needs edt_slerp_sums_doubles(W, nchunks) doubles — the chunk rows [nchunks][W] first
  * (what the coefficient passes read and what a caller may copy or all-gather), then the row
  * scratch the sum pass fills and folds into the rows (W = 3: and one flag word at the end). Every

@@ -18,7 +18,7 @@ VARIANTS = {
     "blendold": ["-DEDT_SLERP_BLEND_TILE=0"],
     "popcoloc": ["-DEDT_SLERP_POP_FUSED=0"],
     "popfused": ["-DEDT_SLERP_POP_FUSED=1"],
-    "wgrows": ["-DEDT_SLERP_SPEC_WG_ROWS=1"],
+    "waverows": ["-DEDT_SLERP_SPEC_WG_ROWS=0"],
 }
 
 
