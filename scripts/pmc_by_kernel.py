@@ -17,7 +17,8 @@ def per_kernel(root, counter):
         with open(path) as f:
             for row in csv.DictReader(f):
                 if row.get("Counter_Name") == counter:
-                    name = row["Kernel_Name"].split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")
+                    name = row["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "")
+                    name = name.split("(")[0]
                     vals.setdefault(name[:90], []).append(float(row["Counter_Value"]))
     return vals
 
