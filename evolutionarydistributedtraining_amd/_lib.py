@@ -53,6 +53,8 @@ SIGNATURES = [
     ("edt_slerp_coef", _I, [_P, _P, _I, _P, _D, _D, _P, _P, _P]),
     ("edt_slerp_blend", _I, [_P, _P, _I, _P, _I, _P, ctypes.c_int64, _P, _P]),
     ("edt_slerp_merge", _I, [_P, _P, _I, _P, _I, _P, ctypes.c_int64, _P, _I, _P, _D, _D, _P, _P, _P, _P]),
+    ("edt_slerp_merge_hold", _I, [_P, _P, _I, _P, _I, _P, ctypes.c_int64, _P, _I, _P, _D, _D, _P, _P, _P, _P]),
+    ("edt_slerp_hold_status", _I, [_P, ctypes.c_int64, _P]),
     ("edt_slerp_merge_speculative", _I, [_P, _P, _I, _P, _I, _P, ctypes.c_int64, _P, _I, _P, _D, _D, _P, _P, _P,
                                          _P, _U64, _P]),
     ("edt_slerp_merge_list", _I, [ctypes.POINTER(_P), ctypes.POINTER(_P), _I, ctypes.POINTER(_P), _I, _P,

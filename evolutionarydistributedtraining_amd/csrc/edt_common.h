@@ -97,6 +97,15 @@ using edt::g_err;
 #ifndef EDT_SLERP_SPEC_WG_ROWS
 #define EDT_SLERP_SPEC_WG_ROWS 1
 #endif
+// Far-parent SLERP with the parents held on chip (edt_slerp_merge_hold): level-4 groups (8 Ki
+// elements, 128 VGPRs of bf16 pairs) a wave keeps in registers across its phase's coefficient
+// wait, and the phase size (whole segments, closed at >= this many chunks of the plan).
+#ifndef EDT_SLERP_HOLD_SLOTS
+#define EDT_SLERP_HOLD_SLOTS 2
+#endif
+#ifndef EDT_SLERP_HOLD_PHASE
+#define EDT_SLERP_HOLD_PHASE 256
+#endif
 #ifndef EDT_SLERP_COEF_BLOCK    // 1: one workgroup per segment for the chunk-sum reduction (else one wave)
 #define EDT_SLERP_COEF_BLOCK 1
 #endif

@@ -325,22 +325,35 @@ __device__ __forceinline__ void pair_tile(const void* v0, const void* v1, void* 
 // transposed together: row r of the wave ends with tiles K r .. K r + K - 1, K = T / 4), then the
 // tree over the T tile sums in registers — within a row, then rows 0 + 1 and 2 + 3 by the level-16
 // swap, then the two halves by the level-32 swap — stored as one row of level log2 T.
-template <int IDT, bool NT, int T>
-__device__ __forceinline__ void pair_tiles(const void* v0, const void* v1, uint64_t start, uint64_t len, int m,
-                                           double* row) {
-    static_assert(T == 4 || T == 8 || T == 16, "tiles per wave");
-    constexpr int K = T / 4;
+// The lane's vectors of tiles T m .. T m + T - 1 (ZERO: out-of-range tiles set to 0, so a caller
+// holding them across phases owns defined registers).
+template <int IDT, bool NT, int T, bool ZERO = false>
+__device__ __forceinline__ void tiles_load(const void* v0, const void* v1, uint64_t start, uint64_t len, int m,
+                                           Raw8<IDT> (&x)[T], Raw8<IDT> (&y)[T]) {
     const uint64_t a = (start + kVec - 1) / kVec * kVec, b = (start + len) / kVec * kVec;
     const uint64_t i0 = a + (uint64_t)(T * m) * kTileElems + (uint64_t)(threadIdx.x & 63) * kVec;
-    Raw8<IDT> x[T], y[T];
 #pragma unroll
     for (int k = 0; k < T; ++k) {
         const uint64_t i = i0 + (uint64_t)k * kTileElems;
         if (a < b && i < b) {
             x[k] = ld_raw<IDT, NT>(v0, i);
             y[k] = ld_raw<IDT, NT>(v1, i);
+        } else if constexpr (ZERO) {
+            x[k] = Raw8<IDT>{};
+            y[k] = Raw8<IDT>{};
         }
     }
+}
+
+// The row of level log2 T from the loaded vectors (pair_tiles' arithmetic): store(q, value) is
+// called by lanes 0 .. 2 for the sums {v0.v0, v1.v1, v0.v1}.
+template <int IDT, int T, typename Store>
+__device__ __forceinline__ void tiles_sums(const void* v0, const void* v1, uint64_t start, uint64_t len, int m,
+                                           const Raw8<IDT> (&x)[T], const Raw8<IDT> (&y)[T], Store&& store) {
+    static_assert(T == 4 || T == 8 || T == 16, "tiles per wave");
+    constexpr int K = T / 4;
+    const uint64_t a = (start + kVec - 1) / kVec * kVec, b = (start + len) / kVec * kVec;
+    const uint64_t i0 = a + (uint64_t)(T * m) * kTileElems + (uint64_t)(threadIdx.x & 63) * kVec;
     double t[3 * T];                                 // tile-major: t[3 k + q]
 #pragma unroll
     for (int k = 0; k < T; ++k) {
@@ -371,7 +384,15 @@ __device__ __forceinline__ void pair_tiles(const void* v0, const void* v1, uint6
     const double s0 = total(0), s1 = total(1), s2 = total(2);
     const int lane = threadIdx.x & 63;
     const double x0 = lane == 0 ? s0 : lane == 1 ? s1 : s2;
-    if (lane < 3) row[lane] = x0;
+    if (lane < 3) store(lane, x0);
+}
+
+template <int IDT, bool NT, int T>
+__device__ __forceinline__ void pair_tiles(const void* v0, const void* v1, uint64_t start, uint64_t len, int m,
+                                           double* row) {
+    Raw8<IDT> x[T], y[T];
+    tiles_load<IDT, NT, T>(v0, v1, start, len, m, x, y);
+    tiles_sums<IDT, T>(v0, v1, start, len, m, x, y, [&](int q, double v) { row[q] = v; });
 }
 
 // The reference's branch and coefficients (EDT_RL/crossover.py:31-45) for an fp32 dot, in fp32 as
@@ -527,14 +548,29 @@ int pair_sums(const void* v0, const void* v1, int in_dt, void* out, int out_dt, 
 // wave sums, then the waves in order). Every coefficient kernel uses this one order.
 constexpr int kCoefThreads = EDT_SLERP_COEF_BLOCK ? kBlock : 64;
 
+// Loads / stores that bypass the CU's L1 (global_load / global_store ... sc1): the in-launch hand-offs
+// between workgroups of slerp_hold_kernel (every byte handed over is stored and loaded this way).
+__device__ __forceinline__ double ld_agent(const double* p) {
+    return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_agent(const float* p) {
+    return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename V>
+__device__ __forceinline__ void st_agent(V* p, V v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <bool AGENT = false>
 __device__ __forceinline__ bool segment_sums(const double* tab, int stride, int q0, int q1, int q2, int c0,
                                              int c1, double (&out)[3]) {
     const int tid = EDT_SLERP_COEF_BLOCK ? (int)threadIdx.x : (int)(threadIdx.x & 63);
+    auto at = [&](uint64_t k) { return AGENT ? ld_agent(tab + k) : tab[k]; };
     double s0 = 0.0, s1 = 0.0, s2 = 0.0;
     for (int c = c0 + tid; c < c1; c += kCoefThreads) {
-        s0 += tab[(uint64_t)c * stride + q0];
-        s1 += tab[(uint64_t)c * stride + q1];
-        s2 += tab[(uint64_t)c * stride + q2];
+        s0 += at((uint64_t)c * stride + q0);
+        s1 += at((uint64_t)c * stride + q1);
+        s2 += at((uint64_t)c * stride + q2);
     }
     s0 = wave_sum(s0);
     s1 = wave_sum(s1);
@@ -1065,6 +1101,281 @@ int slerp_blend_impl(const void* v0, const void* v1, int in_dt, void* out, int o
     return check_launch("slerp_blend_kernel");
 }
 
+// ---------------------------------------------------------------------------------------
+// Far-parent SLERP with part of the parents held on chip (edt_slerp_merge_hold). The two-pass
+// form moves 10 B per bf16 element (stats read 4, blend read 4 + write 2): every parent byte
+// crosses HBM twice because a segment's coefficients need its whole dot before its first output.
+// Here one persistent launch (one workgroup per CU, all resident: cooperative launch) walks the
+// arena in PHASES — runs of whole segments of >= kHoldPhaseChunks chunks — and per phase:
+//   1. stats: each wave takes the phase's level-4 groups (16 tiles of a chunk, 8 Ki elements)
+//      g = w, w + W, ... (address order across the chip), forms each group's canonical level-4
+//      row (tiles_sums: bit-identical to the stats pass) and KEEPS its last kHoldSlots groups'
+//      vectors in registers;
+//   2. arrival: rows stored write-through (sc1), one agent-scope ticket per workgroup; the last
+//      arriver finishes the chunk trees and segment sums in the coefficient kernel's order
+//      (segment_sums) and publishes the coefficients and a ready word (write-through);
+//   3. the PREVIOUS phase's streamed groups are read again and blended (this hides step 2);
+//   4. wait for the ready word, blend the held groups from registers (no second read).
+// A group held moves 6 B per element instead of 10; with 2 slots a wave holds 16 Ki elements,
+// the chip 16.8 M. Every sum, coefficient and output is bit-identical to edt_slerp_merge. Every
+// wait is bounded (kHoldTimeout): on expiry the error word is set and every wave leaves.
+
+constexpr int kHoldSlots = EDT_SLERP_HOLD_SLOTS;        // level-4 groups a wave keeps in registers
+constexpr int kGroupsPerChunk = kTileSlots / 16;        // 8
+constexpr int kHoldPhaseChunks = EDT_SLERP_HOLD_PHASE;  // a phase closes at >= this many chunks
+constexpr uint64_t kHoldTimeout = 200000000ull;         // wall_clock64 ticks (100 MHz): 2 s per wait
+
+// control words (int32) after the level-4 rows: [0] phases, [1] error, [2, 4) pad, then
+// cnt[nseg + 1] tickets, ready[nseg + 1], phase first chunk [nseg + 1], phase first segment [nseg + 1]
+inline uint64_t hold_ctl_ints(int nseg) { return 4 + 4ull * (uint64_t)(nseg + 1); }
+
+__global__ __launch_bounds__(kBlock) void slerp_hold_prep_kernel(const int32_t* seg_first, int nseg, int32_t* ctl) {
+    int32_t* cnt = ctl + 4;
+    int32_t* pfc = cnt + 2 * (nseg + 1);
+    int32_t* pfs = pfc + (nseg + 1);
+    for (int i = threadIdx.x; i < 2 * (nseg + 1); i += blockDim.x) cnt[i] = 0;     // tickets, ready words
+    if (threadIdx.x == 0) {
+        ctl[1] = 0;
+        int np = 0, s = 0;
+        while (s < nseg) {
+            const int c0 = seg_first[s];
+            pfc[np] = c0;
+            pfs[np] = s;
+            do { ++s; } while (s < nseg && seg_first[s] - c0 < kHoldPhaseChunks);
+            ++np;
+        }
+        pfc[np] = nseg > 0 ? seg_first[nseg] : 0;
+        pfs[np] = nseg;
+        ctl[0] = np;
+    }
+}
+
+// A group is handled as two halves of 8 tiles (64 VGPRs of bf16 pairs each): half h of group m
+// is tiles_load's / tiles_sums' unit 2 m + h, and the level-4 row is the sum of the two level-3
+// rows — the perfect tree's next level, so the row equals the stats pass's bit for bit.
+using HalfG = Raw8<EDT_BF16>[8];
+
+// Blend half h of group m of chunk [start, start + len) from the vectors in x / y (tile 0's head /
+// tail elements are read again: < 16 per chunk).
+template <int ODT>
+__device__ __forceinline__ void hold_blend_half(const void* v0, const void* v1, void* out, uint64_t start,
+                                                uint64_t len, int mh, const HalfG& x, const HalfG& y, float c0,
+                                                float c1) {
+    const uint64_t a = (start + kVec - 1) / kVec * kVec, b = (start + len) / kVec * kVec;
+    const uint64_t i0 = a + (uint64_t)(8 * mh) * kTileElems + (uint64_t)(threadIdx.x & 63) * kVec;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint64_t i = i0 + (uint64_t)k * kTileElems;
+        if (a < b && i < b) {
+            float r[kVec];
+#pragma unroll
+            for (int e = 0; e < kVec; ++e) r[e] = c0 * x[k][e] + c1 * y[k][e];
+            st<ODT, kVec>(out, i, r);
+        }
+    }
+    if (mh == 0)
+        tile0_edge(start, len, [&](uint64_t e) { lerp_elems<EDT_BF16, ODT, EDT_F32, 1>(v0, v1, out, e, c0, c1); });
+}
+
+// The level-3 row of half mh (lanes 0 .. 2 keep sum q), then, for the second half, the level-4 row
+// stored write-through.
+__device__ __forceinline__ void hold_sums_half(const void* v0, const void* v1, uint64_t start, uint64_t len, int mh,
+                                               const HalfG& x, const HalfG& y, double& keep, double* row) {
+    tiles_sums<EDT_BF16, 8>(v0, v1, start, len, mh, x, y, [&](int q, double v) {
+        if (mh & 1) st_agent(row + q, keep + v);
+        else keep = v;
+    });
+}
+
+// The last arriver of a phase: chunk trees from the level-4 rows, then per segment the coefficient
+// kernel's reduction and coefficients; then the ready word. All loads / stores of handed-over bytes
+// are agent-scope (sc1).
+__device__ __forceinline__ void hold_reduce(int c0, int c1, int s0, int s1, const double* rows, double* partial,
+                                            const int32_t* seg_first, const double* tvals, float thr, float eps,
+                                            float* coef, float* dot_out, int32_t* ready_word) {
+    for (int c = c0 + (int)threadIdx.x; c < c1; c += kBlock) {
+        const double* r = rows + (uint64_t)c * (kGroupsPerChunk * 3);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            double v[kGroupsPerChunk];
+#pragma unroll
+            for (int k = 0; k < kGroupsPerChunk; ++k) v[k] = ld_agent(r + 3 * k + q);
+            st_agent(partial + 3 * (uint64_t)c + q, ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7])));
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int s = s0; s < s1; ++s) {
+        double sums[3];
+        if (segment_sums<true>(partial, 3, 0, 1, 2, seg_first[s], seg_first[s + 1], sums)) {
+            float cc0, cc1, dot;
+            slerp_coefficients(sums[0], sums[1], sums[2], tvals[s], thr, eps, cc0, cc1, dot);
+            st_agent(coef + 2 * s, cc0);
+            st_agent(coef + 2 * s + 1, cc1);
+            if (dot_out) dot_out[s] = dot;
+        }
+        __syncthreads();                              // segment_sums' LDS words serve the next segment
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) st_agent(ready_word, 1);
+}
+
+template <int ODT>
+__global__ __launch_bounds__(kBlock, 1) void slerp_hold_kernel(const void* v0, const void* v1, void* out,
+                                                               const uint64_t* __restrict__ chunks,
+                                                               const int32_t* __restrict__ seg_first, int nseg,
+                                                               const double* __restrict__ tvals, float thr, float eps,
+                                                               double* partial, double* rows, float* coef,
+                                                               float* dot_out, int32_t* ctl) {
+    constexpr bool NT = EDT_NT_SLERP != 0;
+    constexpr int H = kHoldSlots;
+    const int wave = threadIdx.x >> 6;
+    const int W = (int)gridDim.x * kWavesPerBlock;
+    const int w = (int)blockIdx.x * kWavesPerBlock + wave;
+    int32_t* cnt = ctl + 4;
+    int32_t* ready = cnt + (nseg + 1);
+    const int32_t* pfc = ready + (nseg + 1);
+    const int32_t* pfs = pfc + (nseg + 1);
+    const int nphase = ctl[0];
+    __shared__ int32_t s_word;
+    auto row_of = [&](int c, int m) { return rows + ((uint64_t)c * kGroupsPerChunk + (uint64_t)m) * 3; };
+    Raw8<EDT_BF16> hx[H][2][8], hy[H][2][8];
+    int pc0 = 0, pnw = 0;                             // the previous phase: first chunk, this wave's groups
+    for (int p = 0; p <= nphase; ++p) {
+        int c0 = 0, nw = 0;
+        if (p < nphase) {
+            c0 = pfc[p];
+            const int G = (pfc[p + 1] - c0) * kGroupsPerChunk;
+            nw = w < G ? (G - 1 - w) / W + 1 : 0;
+            for (int k = 0; k < nw - H; ++k) {        // streamed: sums now, read again in step 3
+                const int g = w + k * W, c = c0 + g / kGroupsPerChunk, m = g % kGroupsPerChunk;
+                const uint64_t st0 = chunks[3 * (uint64_t)c], ln = chunks[3 * (uint64_t)c + 1];
+                double keep = 0.0;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    Raw8<EDT_BF16> x[8], y[8];
+                    tiles_load<EDT_BF16, NT, 8>(v0, v1, st0, ln, 2 * m + h, x, y);
+                    hold_sums_half(v0, v1, st0, ln, 2 * m + h, x, y, keep, row_of(c, m));
+                }
+            }
+#pragma unroll
+            for (int s = 0; s < H; ++s) {             // held: loaded into the slots (empty slots: zeros)
+                const int k = nw - H + s;
+                uint64_t st0 = 0, ln = 0;
+                int m = 0;
+                if (k >= 0) {
+                    const int g = w + k * W, c = c0 + g / kGroupsPerChunk;
+                    m = g % kGroupsPerChunk;
+                    st0 = chunks[3 * (uint64_t)c];
+                    ln = chunks[3 * (uint64_t)c + 1];
+                }
+#pragma unroll
+                for (int h = 0; h < 2; ++h) tiles_load<EDT_BF16, NT, 8, true>(v0, v1, st0, ln, 2 * m + h, hx[s][h], hy[s][h]);
+            }
+#pragma unroll
+            for (int s = 0; s < H; ++s) {
+                const int k = nw - H + s;
+                if (k >= 0) {
+                    const int g = w + k * W, c = c0 + g / kGroupsPerChunk, m = g % kGroupsPerChunk;
+                    const uint64_t st0 = chunks[3 * (uint64_t)c], ln = chunks[3 * (uint64_t)c + 1];
+                    double keep = 0.0;
+#pragma unroll
+                    for (int h = 0; h < 2; ++h)
+                        hold_sums_half(v0, v1, st0, ln, 2 * m + h, hx[s][h], hy[s][h], keep, row_of(c, m));
+                }
+            }
+            // arrival: every wave's row stores drained, then one ticket per workgroup
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                const int t = __hip_atomic_fetch_add(cnt + p, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                s_word = t == (int)gridDim.x - 1;
+            }
+            __syncthreads();
+            const bool last = s_word != 0;
+            __syncthreads();
+            if (last)
+                hold_reduce(c0, pfc[p + 1], pfs[p], pfs[p + 1], rows, partial, seg_first, tvals, thr, eps, coef,
+                            dot_out, ready + p);
+        }
+        for (int k = 0; k < pnw - H; ++k) {           // the previous phase's streamed groups, blended
+            const int g = w + k * W, c = pc0 + g / kGroupsPerChunk, m = g % kGroupsPerChunk;
+            const uint64_t st0 = chunks[3 * (uint64_t)c], ln = chunks[3 * (uint64_t)c + 1];
+            const uint64_t seg = chunks[3 * (uint64_t)c + 2];
+            const float f0 = ld_agent(coef + 2 * seg), f1 = ld_agent(coef + 2 * seg + 1);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                Raw8<EDT_BF16> x[8], y[8];
+                tiles_load<EDT_BF16, NT, 8>(v0, v1, st0, ln, 2 * m + h, x, y);
+                hold_blend_half<ODT>(v0, v1, out, st0, ln, 2 * m + h, x, y, f0, f1);
+            }
+        }
+        if (p < nphase) {
+            if (threadIdx.x == 0) {                   // bounded wait for this phase's coefficients
+                const uint64_t t0 = wall_clock64();
+                int ok = 1;
+                while (__hip_atomic_load(ready + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+                    if (__hip_atomic_load(ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
+                        wall_clock64() - t0 > kHoldTimeout) {
+                        ok = 0;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(8);
+                }
+                if (!ok) st_agent(ctl + 1, 1);
+                s_word = ok;
+            }
+            __syncthreads();
+            if (!s_word) return;                      // the whole workgroup leaves together
+#pragma unroll
+            for (int s = 0; s < H; ++s) {
+                const int k = nw - H + s;
+                if (k >= 0) {
+                    const int g = w + k * W, c = c0 + g / kGroupsPerChunk, m = g % kGroupsPerChunk;
+                    const uint64_t st0 = chunks[3 * (uint64_t)c], ln = chunks[3 * (uint64_t)c + 1];
+                    const uint64_t seg = chunks[3 * (uint64_t)c + 2];
+                    const float f0 = ld_agent(coef + 2 * seg), f1 = ld_agent(coef + 2 * seg + 1);
+#pragma unroll
+                    for (int h = 0; h < 2; ++h)
+                        hold_blend_half<ODT>(v0, v1, out, st0, ln, 2 * m + h, hx[s][h], hy[s][h], f0, f1);
+                }
+            }
+        }
+        pc0 = c0;
+        pnw = nw;
+    }
+}
+
+// host: the launch (bf16 parents, flat arenas); the workspace is edt_slerp_merge's
+int slerp_hold_impl(const void* v0, const void* v1, void* out, int out_dt, const uint64_t* chunk_desc, int64_t nchunks,
+                    const int32_t* seg_first, int nseg, const double* t, double thr, double eps, double* partial,
+                    float* coef, float* dot_out, hipStream_t s) {
+    const uint64_t avail = (edt_slerp_sums_doubles(3, nchunks) - 27ull * (uint64_t)nchunks) * 2;   // ints
+    if (hold_ctl_ints(nseg) > avail) return fail(EDT_ERR_ARG, "hold form: too many segments for the workspace");
+    if (nchunks > (int64_t)INT32_MAX / (kGroupsPerChunk * 2)) return fail(EDT_ERR_ARG, "hold form: too many chunks");
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return fail(EDT_ERR_LAUNCH, "hold form: device query failed");
+    const void* kern = out_dt == EDT_F32 ? reinterpret_cast<const void*>(&slerp_hold_kernel<EDT_F32>)
+                                         : reinterpret_cast<const void*>(&slerp_hold_kernel<EDT_BF16>);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, kBlock, 0) != hipSuccess || per < 1)
+        return fail(EDT_ERR_LAUNCH, "hold form: occupancy query failed");
+    double* rows = partial + 3 * (uint64_t)nchunks;
+    int32_t* ctl = reinterpret_cast<int32_t*>(partial + 27 * (uint64_t)nchunks);
+    slerp_hold_prep_kernel<<<1, kBlock, 0, s>>>(seg_first, nseg, ctl);
+    int rc = check_launch("slerp_hold_prep_kernel");
+    if (rc) return rc;
+    float fthr = (float)thr, feps = (float)eps;
+    void* args[] = {(void*)&v0, (void*)&v1, (void*)&out, (void*)&chunk_desc, (void*)&seg_first, (void*)&nseg,
+                    (void*)&t, (void*)&fthr, (void*)&feps, (void*)&partial, (void*)&rows, (void*)&coef,
+                    (void*)&dot_out, (void*)&ctl};
+    const hipError_t e = hipLaunchCooperativeKernel(kern, dim3((unsigned)(cus * per)), dim3(kBlock), args, 0, s);
+    if (e != hipSuccess) return fail(EDT_ERR_LAUNCH, "slerp_hold_kernel: launch failed: %s", hipGetErrorString(e));
+    return EDT_OK;
+}
+
 
 // ---------------------------------------------------------------------------------------
 // Reference-dot mode (opt-in): the reference's own fp32 dot of EDT_RL/crossover.py:20-29 restated
@@ -1472,6 +1783,34 @@ int edt_slerp_merge(const void* v0, const void* v1, int in_dt, void* out, int ou
     rc = edt_slerp_coef(partial, seg_first_chunk, nseg, t, dot_threshold, eps, coef, dot_out, stream);
     if (rc) return rc;
     return edt_slerp_blend(v0, v1, in_dt, out, out_dt, chunk_desc, nchunks, coef, stream);
+}
+
+int edt_slerp_merge_hold(const void* v0, const void* v1, int in_dt, void* out, int out_dt,
+                         const uint64_t* chunk_desc, int64_t nchunks, const int32_t* seg_first_chunk, int nseg,
+                         const double* t, double dot_threshold, double eps, double* partial, float* coef,
+                         float* dot_out, void* stream) {
+    g_err[0] = 0;
+    if ((in_dt | out_dt) & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
+    if (in_dt != EDT_BF16) return fail(EDT_ERR_ARG, "hold form: bf16 parents only (edt_slerp_merge takes fp32)");
+    if (nchunks < 0 || nseg < 0) return fail(EDT_ERR_ARG, "negative count");
+    if (nseg == 0) return EDT_OK;
+    if (!seg_first_chunk || !t || !partial || !coef || (nchunks > 0 && (!v0 || !v1 || !out || !chunk_desc)))
+        return fail(EDT_ERR_ARG, "null buffer");
+    if (nchunks > 0 && (!aligned16(v0) || !aligned16(v1) || !aligned16(out)))
+        return fail(EDT_ERR_ARG, "slerp buffers must be 16-byte aligned");
+    return slerp_hold_impl(v0, v1, out, out_dt, chunk_desc, nchunks, seg_first_chunk, nseg, t, dot_threshold, eps,
+                           partial, coef, dot_out, (hipStream_t)stream);
+}
+
+int edt_slerp_hold_status(const double* partial, int64_t nchunks, void* stream) {
+    g_err[0] = 0;
+    if (!partial || nchunks < 0) return fail(EDT_ERR_ARG, "bad workspace");
+    int32_t err = 0;
+    const int32_t* w = reinterpret_cast<const int32_t*>(partial + 27 * (uint64_t)nchunks) + 1;
+    if (hipMemcpyAsync(&err, w, sizeof(err), hipMemcpyDeviceToHost, (hipStream_t)stream) != hipSuccess ||
+        hipStreamSynchronize((hipStream_t)stream) != hipSuccess)
+        return fail(EDT_ERR_LAUNCH, "edt_slerp_hold_status: copy failed");
+    return err ? 1 : 0;
 }
 
 uint64_t edt_slerp_sums_doubles(int width, int64_t nchunks) {

@@ -214,6 +214,26 @@ int edt_slerp_merge(const void* v0, const void* v1, int in_dt, void* out, int ou
                     const double* t, double dot_threshold, double eps, double* partial, float* coef,
                     float* dot_out, void* stream);
 
+/* edt_slerp_merge for bf16 parents (flat arenas) in ONE persistent launch that keeps part of the
+ * parents on chip: per phase (runs of whole segments) the chip forms the chunk sums, holds the
+ * last groups it read in registers, and blends them once the phase's coefficients are published
+ * in-launch; the rest of the phase is read again. Parents far apart (the SLERP branch) move
+ * fewer than edt_slerp_merge's 4 b_in + b_out bytes per element. Same workspace (`partial`,
+ * edt_slerp_sums_doubles(3, nchunks) doubles) and arguments as edt_slerp_merge; outputs, chunk
+ * sums (partial[0, 3 nchunks)), coefficients and dots are bit-identical to it. `out` may be
+ * one of the parents or disjoint from both. in_dt must be EDT_BF16. Needs every workgroup of its
+ * grid resident (cooperative launch); each in-launch wait is bounded: edt_slerp_hold_status
+ * reports whether one expired. */
+int edt_slerp_merge_hold(const void* v0, const void* v1, int in_dt, void* out, int out_dt,
+                         const uint64_t* chunk_desc, int64_t nchunks, const int32_t* seg_first_chunk, int nseg,
+                         const double* t, double dot_threshold, double eps, double* partial, float* coef,
+                         float* dot_out, void* stream);
+
+/* Synchronises `stream`, then returns 0 when the last edt_slerp_merge_hold on this workspace
+ * completed, 1 when one of its in-launch waits expired (the outputs are then undefined), < 0 on
+ * error. */
+int edt_slerp_hold_status(const double* partial, int64_t nchunks, void* stream);
+
 /* edt_slerp_merge with a speculative first pass: the chunk sums and, in the same pass, the
  * lerp-branch output (1-t) v0 + t v1 of every segment; the coefficients then flag (redo[s] = 1,
  * nseg int32 of device workspace) the segments whose |dot| <= dot_threshold, and only their

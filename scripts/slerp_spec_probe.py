@@ -1,8 +1,9 @@
 """The speculative SLERP pass against lerp's identical stream on the 7B body (bf16, lineage parents:
 every segment in the lerp branch, so the speculative merge is one pass of 2 reads + 1 write per
 element, exactly lerp's bytes). Times, in one process on the same arenas and interleaved:
-edt_lerp, edt_slerp_merge_speculative, the two-pass edt_slerp_merge (stats + blend) and the
-stats pass alone (edt_slerp_stats, 4 B read per element).
+edt_lerp, edt_slerp_merge_speculative, the two-pass edt_slerp_merge (stats + blend), the
+one-launch edt_slerp_merge_hold (checked bit for bit against the two-pass output) and the stats
+pass alone (edt_slerp_stats, 4 B read per element).
 HIP events on the launch stream, median over rounds. Run it under rocprofv3 (--kernel-trace
 --stats, or one --pmc pass) to get the per-kernel figures.
 
@@ -71,13 +72,22 @@ def main():
                 L.ptr(v0), L.ptr(v1), 1, L.ptr(out), 1, L.ptr(plan.chunks), plan.nchunks, L.ptr(plan.seg_first),
                 plan.nseg, L.ptr(t), 0.9995, 1e-8, L.ptr(part), L.ptr(plan.coef), L.ptr(plan.dots), st)
 
+        def hold(lb=lb, part=part):
+            return lb.edt_slerp_merge_hold(
+                L.ptr(v0), L.ptr(v1), 1, L.ptr(out), 1, L.ptr(plan.chunks), plan.nchunks, L.ptr(plan.seg_first),
+                plan.nseg, L.ptr(t), 0.9995, 1e-8, L.ptr(part), L.ptr(plan.coef), L.ptr(plan.dots), st)
+
         def stats(lb=lb, part=part):
             return lb.edt_slerp_stats(L.ptr(v0), L.ptr(v1), 1, L.ptr(plan.chunks), plan.nchunks, L.ptr(part), st)
 
         sfx = "" if name == "intree" else f"/{name}"
+        if name == "intree":
+            part_intree = part
         cases["speculative" + sfx] = spec
         cases["two_pass" + sfx] = two
         cases["stats" + sfx] = stats
+        if hasattr(lb, "edt_slerp_merge_hold"):
+            cases["hold" + sfx] = hold
     for f in cases.values():
         assert f() == 0, L.last_error() if hasattr(L, "last_error") else "launch failed"
     torch.cuda.synchronize()
@@ -92,11 +102,22 @@ def main():
             torch.cuda.synchronize()
             times[k].append(e0.elapsed_time(e1))
     redo_n = int(redo.sum().item())
+    hold_check = None
+    if "hold" in cases:                     # the hold form against the two-pass form, bit for bit
+        cases["two_pass"]()
+        ref = out.clone()
+        ref_dots = plan.dots.clone()
+        out.fill_(float("nan"))
+        cases["hold"]()
+        status = int(lib.edt_slerp_hold_status(L.ptr(part_intree), plan.nchunks, st))
+        hold_check = {"status": status, "out_equal": bool(torch.equal(out.view(torch.int16), ref.view(torch.int16))),
+                      "dots_equal": bool(torch.equal(plan.dots, ref_dots))}
+        del ref
     # bytes: 6 per element (2 bf16 reads + 1 write); the stats pass reads 4
     res = {k: {"median_ms": round(statistics.median(v), 4), "min_ms": round(min(v), 4),
                "TBps": round((4 if k.startswith("stats") else 6) * P / statistics.median(v) / 1e9, 3)}
            for k, v in times.items()}
-    print(json.dumps({"probe": "slerp_spec", "elements": P, "far": a.far, "redo_segments": redo_n,
+    print(json.dumps({"probe": "slerp_spec", "elements": P, "far": a.far, "redo_segments": redo_n, "hold_check": hold_check,
                       "results": res}))
 
 
