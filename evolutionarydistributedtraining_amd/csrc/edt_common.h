@@ -103,6 +103,12 @@ using edt::g_err;
 #ifndef EDT_SLERP_HOLD_SLOTS
 #define EDT_SLERP_HOLD_SLOTS 2
 #endif
+#ifndef EDT_SLERP_HOLD_BPC      // workgroups per CU the hold kernel is compiled for (waves per SIMD)
+#define EDT_SLERP_HOLD_BPC 1
+#endif
+#ifndef EDT_SLERP_HOLD_UNIT     // tiles per load unit of the hold kernel's pipelined loops (4 or 8)
+#define EDT_SLERP_HOLD_UNIT 4
+#endif
 #ifndef EDT_SLERP_HOLD_PHASE
 #define EDT_SLERP_HOLD_PHASE 256
 #endif

@@ -1119,6 +1119,13 @@ int slerp_blend_impl(const void* v0, const void* v1, int in_dt, void* out, int o
 // A group held moves 6 B per element instead of 10; with 2 slots a wave holds 16 Ki elements,
 // the chip 16.8 M. Every sum, coefficient and output is bit-identical to edt_slerp_merge. Every
 // wait is bounded (kHoldTimeout): on expiry the error word is set and every wave leaves.
+// Measured (profiles/r03_slerp_hold_probe.json, 7B body, far parents): 16.9 ms against the
+// two-pass form's 11.3 ms; with nothing held (EDT_SLERP_HOLD_SLOTS=0: the two-pass bytes in this
+// launch) 15.6 ms, at 2 waves per SIMD the same; phases of 64 / 1024 chunks 17.3 / 16.3 ms. A
+// persistent grid of 1-2 waves per SIMD keeps 64-128 KiB of loads in flight per CU against the
+// one-shot grids' several hundred, and the registers that would hold parents are the ones more
+// loads in flight need: the re-read the form saves costs less than the parallelism it gives up.
+// Kept opt-in for A/B; edt_slerp_merge stays the far-parent form.
 
 constexpr int kHoldSlots = EDT_SLERP_HOLD_SLOTS;        // level-4 groups a wave keeps in registers
 constexpr int kGroupsPerChunk = kTileSlots / 16;        // 8
@@ -1150,21 +1157,25 @@ __global__ __launch_bounds__(kBlock) void slerp_hold_prep_kernel(const int32_t* 
     }
 }
 
-// A group is handled as two halves of 8 tiles (64 VGPRs of bf16 pairs each): half h of group m
-// is tiles_load's / tiles_sums' unit 2 m + h, and the level-4 row is the sum of the two level-3
-// rows — the perfect tree's next level, so the row equals the stats pass's bit for bit.
-using HalfG = Raw8<EDT_BF16>[8];
+// A group is handled in units of kHoldUnit tiles (32 VGPRs of bf16 pairs per 4 tiles): unit u of
+// group m is tiles_load's / tiles_sums' index (16 / U) m + u, and the level-4 row is the perfect
+// tree over the units' rows — ((u0 + u1) + (u2 + u3)) for U = 4, u0 + u1 for U = 8 — so it equals
+// the stats pass's row bit for bit.
+constexpr int kHoldUnit = EDT_SLERP_HOLD_UNIT;
+constexpr int kUnitsPerGroup = 16 / kHoldUnit;
+static_assert(kHoldUnit == 4 || kHoldUnit == 8, "hold unit: 4 or 8 tiles");
+using HoldU = Raw8<EDT_BF16>[kHoldUnit];
 
-// Blend half h of group m of chunk [start, start + len) from the vectors in x / y (tile 0's head /
-// tail elements are read again: < 16 per chunk).
+// Blend unit mu of chunk [start, start + len) from the vectors in x / y (tile 0's head / tail
+// elements are read again: < 16 per chunk).
 template <int ODT>
-__device__ __forceinline__ void hold_blend_half(const void* v0, const void* v1, void* out, uint64_t start,
-                                                uint64_t len, int mh, const HalfG& x, const HalfG& y, float c0,
+__device__ __forceinline__ void hold_blend_unit(const void* v0, const void* v1, void* out, uint64_t start,
+                                                uint64_t len, int mu, const HoldU& x, const HoldU& y, float c0,
                                                 float c1) {
     const uint64_t a = (start + kVec - 1) / kVec * kVec, b = (start + len) / kVec * kVec;
-    const uint64_t i0 = a + (uint64_t)(8 * mh) * kTileElems + (uint64_t)(threadIdx.x & 63) * kVec;
+    const uint64_t i0 = a + (uint64_t)(kHoldUnit * mu) * kTileElems + (uint64_t)(threadIdx.x & 63) * kVec;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < kHoldUnit; ++k) {
         const uint64_t i = i0 + (uint64_t)k * kTileElems;
         if (a < b && i < b) {
             float r[kVec];
@@ -1173,17 +1184,25 @@ __device__ __forceinline__ void hold_blend_half(const void* v0, const void* v1, 
             st<ODT, kVec>(out, i, r);
         }
     }
-    if (mh == 0)
+    if (mu == 0)
         tile0_edge(start, len, [&](uint64_t e) { lerp_elems<EDT_BF16, ODT, EDT_F32, 1>(v0, v1, out, e, c0, c1); });
 }
 
-// The level-3 row of half mh (lanes 0 .. 2 keep sum q), then, for the second half, the level-4 row
-// stored write-through.
-__device__ __forceinline__ void hold_sums_half(const void* v0, const void* v1, uint64_t start, uint64_t len, int mh,
-                                               const HalfG& x, const HalfG& y, double& keep, double* row) {
-    tiles_sums<EDT_BF16, 8>(v0, v1, start, len, mh, x, y, [&](int q, double v) {
-        if (mh & 1) st_agent(row + q, keep + v);
-        else keep = v;
+// Unit mu's row (lanes 0 .. 2 keep sum q in acc), folded into the level-4 row; the group's last unit
+// stores it write-through.
+__device__ __forceinline__ void hold_sums_unit(const void* v0, const void* v1, uint64_t start, uint64_t len, int mu,
+                                               const HoldU& x, const HoldU& y, double (&acc)[2], double* row) {
+    tiles_sums<EDT_BF16, kHoldUnit>(v0, v1, start, len, mu, x, y, [&](int q, double v) {
+        const int r = mu % kUnitsPerGroup;
+        if constexpr (kUnitsPerGroup == 2) {
+            if (r == 0) acc[0] = v;
+            else st_agent(row + q, acc[0] + v);
+        } else {
+            if (r == 0) acc[0] = v;
+            else if (r == 1) acc[0] = acc[0] + v;
+            else if (r == 2) acc[1] = v;
+            else st_agent(row + q, acc[0] + (acc[1] + v));
+        }
     });
 }
 
@@ -1222,14 +1241,12 @@ __device__ __forceinline__ void hold_reduce(int c0, int c1, int s0, int s1, cons
 }
 
 template <int ODT>
-__global__ __launch_bounds__(kBlock, 1) void slerp_hold_kernel(const void* v0, const void* v1, void* out,
-                                                               const uint64_t* __restrict__ chunks,
-                                                               const int32_t* __restrict__ seg_first, int nseg,
-                                                               const double* __restrict__ tvals, float thr, float eps,
-                                                               double* partial, double* rows, float* coef,
-                                                               float* dot_out, int32_t* ctl) {
+__global__ __launch_bounds__(kBlock, EDT_SLERP_HOLD_BPC) void slerp_hold_kernel(
+    const void* v0, const void* v1, void* out, const uint64_t* __restrict__ chunks,
+    const int32_t* __restrict__ seg_first, int nseg, const double* __restrict__ tvals, float thr, float eps,
+    double* partial, double* rows, float* coef, float* dot_out, int32_t* ctl) {
     constexpr bool NT = EDT_NT_SLERP != 0;
-    constexpr int H = kHoldSlots;
+    constexpr int H = kHoldSlots, HA = H > 0 ? H : 1, UPG = kUnitsPerGroup;
     const int wave = threadIdx.x >> 6;
     const int W = (int)gridDim.x * kWavesPerBlock;
     const int w = (int)blockIdx.x * kWavesPerBlock + wave;
@@ -1239,8 +1256,31 @@ __global__ __launch_bounds__(kBlock, 1) void slerp_hold_kernel(const void* v0, c
     const int32_t* pfs = pfc + (nseg + 1);
     const int nphase = ctl[0];
     __shared__ int32_t s_word;
-    auto row_of = [&](int c, int m) { return rows + ((uint64_t)c * kGroupsPerChunk + (uint64_t)m) * 3; };
-    Raw8<EDT_BF16> hx[H][2][8], hy[H][2][8];
+    // unit j of this wave's sequence in the phase starting at chunk cb: group w + (j / UPG) W, unit j % UPG
+    auto unit_at = [&](int cb, int j, int& c, int& mu) {
+        const int g = w + (j / UPG) * W;
+        c = cb + g / kGroupsPerChunk;
+        mu = UPG * (g % kGroupsPerChunk) + j % UPG;
+    };
+    auto unit_load = [&](int cb, int j, HoldU& x, HoldU& y) {
+        int c, mu;
+        unit_at(cb, j, c, mu);
+        tiles_load<EDT_BF16, NT, kHoldUnit>(v0, v1, chunks[3 * (uint64_t)c], chunks[3 * (uint64_t)c + 1], mu, x, y);
+    };
+    auto unit_sums = [&](int cb, int j, const HoldU& x, const HoldU& y, double (&acc)[2]) {
+        int c, mu;
+        unit_at(cb, j, c, mu);
+        hold_sums_unit(v0, v1, chunks[3 * (uint64_t)c], chunks[3 * (uint64_t)c + 1], mu, x, y, acc,
+                       rows + ((uint64_t)c * kGroupsPerChunk + (uint64_t)(mu / UPG)) * 3);
+    };
+    auto unit_blend = [&](int cb, int j, const HoldU& x, const HoldU& y) {
+        int c, mu;
+        unit_at(cb, j, c, mu);
+        const uint64_t seg = chunks[3 * (uint64_t)c + 2];
+        hold_blend_unit<ODT>(v0, v1, out, chunks[3 * (uint64_t)c], chunks[3 * (uint64_t)c + 1], mu, x, y,
+                             ld_agent(coef + 2 * seg), ld_agent(coef + 2 * seg + 1));
+    };
+    Raw8<EDT_BF16> hx[HA][UPG][kHoldUnit], hy[HA][UPG][kHoldUnit];
     int pc0 = 0, pnw = 0;                             // the previous phase: first chunk, this wave's groups
     for (int p = 0; p <= nphase; ++p) {
         int c0 = 0, nw = 0;
@@ -1248,41 +1288,42 @@ __global__ __launch_bounds__(kBlock, 1) void slerp_hold_kernel(const void* v0, c
             c0 = pfc[p];
             const int G = (pfc[p + 1] - c0) * kGroupsPerChunk;
             nw = w < G ? (G - 1 - w) / W + 1 : 0;
-            for (int k = 0; k < nw - H; ++k) {        // streamed: sums now, read again in step 3
-                const int g = w + k * W, c = c0 + g / kGroupsPerChunk, m = g % kGroupsPerChunk;
-                const uint64_t st0 = chunks[3 * (uint64_t)c], ln = chunks[3 * (uint64_t)c + 1];
-                double keep = 0.0;
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    Raw8<EDT_BF16> x[8], y[8];
-                    tiles_load<EDT_BF16, NT, 8>(v0, v1, st0, ln, 2 * m + h, x, y);
-                    hold_sums_half(v0, v1, st0, ln, 2 * m + h, x, y, keep, row_of(c, m));
+            {   // streamed groups: sums now, read again in step 3; unit j + 1 loads while unit j is summed
+                const int nu = UPG * (nw - H);
+                HoldU xa, ya, xb, yb;
+                double acc[2] = {0.0, 0.0};
+                if (nu > 0) unit_load(c0, 0, xa, ya);
+                for (int j = 0; j < nu; j += 2) {
+                    unit_load(c0, j + 1, xb, yb);
+                    unit_sums(c0, j, xa, ya, acc);
+                    if (j + 2 < nu) unit_load(c0, j + 2, xa, ya);
+                    unit_sums(c0, j + 1, xb, yb, acc);
                 }
             }
+            if constexpr (H > 0) {
+                const int j0 = UPG * (nw - H);        // held groups: every slot loaded (empty: zeros)
 #pragma unroll
-            for (int s = 0; s < H; ++s) {             // held: loaded into the slots (empty slots: zeros)
-                const int k = nw - H + s;
-                uint64_t st0 = 0, ln = 0;
-                int m = 0;
-                if (k >= 0) {
-                    const int g = w + k * W, c = c0 + g / kGroupsPerChunk;
-                    m = g % kGroupsPerChunk;
-                    st0 = chunks[3 * (uint64_t)c];
-                    ln = chunks[3 * (uint64_t)c + 1];
+                for (int s = 0; s < H; ++s) {
+#pragma unroll
+                    for (int u = 0; u < UPG; ++u) {
+                        const int j = j0 + UPG * s + u;
+                        uint64_t st0 = 0, ln = 0;
+                        int mu = 0;
+                        if (j >= 0) {
+                            int c;
+                            unit_at(c0, j, c, mu);
+                            st0 = chunks[3 * (uint64_t)c];
+                            ln = chunks[3 * (uint64_t)c + 1];
+                        }
+                        tiles_load<EDT_BF16, NT, kHoldUnit, true>(v0, v1, st0, ln, mu, hx[s][u], hy[s][u]);
+                    }
                 }
 #pragma unroll
-                for (int h = 0; h < 2; ++h) tiles_load<EDT_BF16, NT, 8, true>(v0, v1, st0, ln, 2 * m + h, hx[s][h], hy[s][h]);
-            }
+                for (int s = 0; s < H; ++s) {
+                    double acc[2] = {0.0, 0.0};
 #pragma unroll
-            for (int s = 0; s < H; ++s) {
-                const int k = nw - H + s;
-                if (k >= 0) {
-                    const int g = w + k * W, c = c0 + g / kGroupsPerChunk, m = g % kGroupsPerChunk;
-                    const uint64_t st0 = chunks[3 * (uint64_t)c], ln = chunks[3 * (uint64_t)c + 1];
-                    double keep = 0.0;
-#pragma unroll
-                    for (int h = 0; h < 2; ++h)
-                        hold_sums_half(v0, v1, st0, ln, 2 * m + h, hx[s][h], hy[s][h], keep, row_of(c, m));
+                    for (int u = 0; u < UPG; ++u)
+                        if (j0 + UPG * s >= 0) unit_sums(c0, j0 + UPG * s + u, hx[s][u], hy[s][u], acc);
                 }
             }
             // arrival: every wave's row stores drained, then one ticket per workgroup
@@ -1299,16 +1340,15 @@ __global__ __launch_bounds__(kBlock, 1) void slerp_hold_kernel(const void* v0, c
                 hold_reduce(c0, pfc[p + 1], pfs[p], pfs[p + 1], rows, partial, seg_first, tvals, thr, eps, coef,
                             dot_out, ready + p);
         }
-        for (int k = 0; k < pnw - H; ++k) {           // the previous phase's streamed groups, blended
-            const int g = w + k * W, c = pc0 + g / kGroupsPerChunk, m = g % kGroupsPerChunk;
-            const uint64_t st0 = chunks[3 * (uint64_t)c], ln = chunks[3 * (uint64_t)c + 1];
-            const uint64_t seg = chunks[3 * (uint64_t)c + 2];
-            const float f0 = ld_agent(coef + 2 * seg), f1 = ld_agent(coef + 2 * seg + 1);
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                Raw8<EDT_BF16> x[8], y[8];
-                tiles_load<EDT_BF16, NT, 8>(v0, v1, st0, ln, 2 * m + h, x, y);
-                hold_blend_half<ODT>(v0, v1, out, st0, ln, 2 * m + h, x, y, f0, f1);
+        {   // the previous phase's streamed groups, read again and blended (pipelined as above)
+            const int nu = UPG * (pnw - H);
+            HoldU xa, ya, xb, yb;
+            if (nu > 0) unit_load(pc0, 0, xa, ya);
+            for (int j = 0; j < nu; j += 2) {
+                unit_load(pc0, j + 1, xb, yb);
+                unit_blend(pc0, j, xa, ya);
+                if (j + 2 < nu) unit_load(pc0, j + 2, xa, ya);
+                unit_blend(pc0, j + 1, xb, yb);
             }
         }
         if (p < nphase) {
@@ -1328,18 +1368,13 @@ __global__ __launch_bounds__(kBlock, 1) void slerp_hold_kernel(const void* v0, c
             }
             __syncthreads();
             if (!s_word) return;                      // the whole workgroup leaves together
+            if constexpr (H > 0) {
+                const int j0 = UPG * (nw - H);
 #pragma unroll
-            for (int s = 0; s < H; ++s) {
-                const int k = nw - H + s;
-                if (k >= 0) {
-                    const int g = w + k * W, c = c0 + g / kGroupsPerChunk, m = g % kGroupsPerChunk;
-                    const uint64_t st0 = chunks[3 * (uint64_t)c], ln = chunks[3 * (uint64_t)c + 1];
-                    const uint64_t seg = chunks[3 * (uint64_t)c + 2];
-                    const float f0 = ld_agent(coef + 2 * seg), f1 = ld_agent(coef + 2 * seg + 1);
+                for (int s = 0; s < H; ++s)
 #pragma unroll
-                    for (int h = 0; h < 2; ++h)
-                        hold_blend_half<ODT>(v0, v1, out, st0, ln, 2 * m + h, hx[s][h], hy[s][h], f0, f1);
-                }
+                    for (int u = 0; u < UPG; ++u)
+                        if (j0 + UPG * s >= 0) unit_blend(c0, j0 + UPG * s + u, hx[s][u], hy[s][u]);
             }
         }
         pc0 = c0;

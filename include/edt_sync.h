@@ -216,14 +216,15 @@ int edt_slerp_merge(const void* v0, const void* v1, int in_dt, void* out, int ou
 
 /* edt_slerp_merge for bf16 parents (flat arenas) in ONE persistent launch that keeps part of the
  * parents on chip: per phase (runs of whole segments) the chip forms the chunk sums, holds the
- * last groups it read in registers, and blends them once the phase's coefficients are published
- * in-launch; the rest of the phase is read again. Parents far apart (the SLERP branch) move
- * fewer than edt_slerp_merge's 4 b_in + b_out bytes per element. Same workspace (`partial`,
+ * last groups each wave read in registers, and blends them once the phase's coefficients are
+ * published in-launch; the rest of the phase is read again. Same workspace (`partial`,
  * edt_slerp_sums_doubles(3, nchunks) doubles) and arguments as edt_slerp_merge; outputs, chunk
- * sums (partial[0, 3 nchunks)), coefficients and dots are bit-identical to it. `out` may be
- * one of the parents or disjoint from both. in_dt must be EDT_BF16. Needs every workgroup of its
- * grid resident (cooperative launch); each in-launch wait is bounded: edt_slerp_hold_status
- * reports whether one expired. */
+ * sums (partial[0, 3 nchunks)), coefficients and dots are bit-identical to it. `out` may be one
+ * of the parents or disjoint from both. in_dt must be EDT_BF16. Needs every workgroup of its grid
+ * resident (cooperative launch); each in-launch wait is bounded: edt_slerp_hold_status reports
+ * whether one expired. MEASURED SLOWER than edt_slerp_merge on MI355X (7B body, far parents:
+ * 16.9 ms against 11.3 ms; the same launch holding nothing 15.6 ms): the registers
+ * that hold parents are the ones a streaming wave needs for loads in flight. Kept for A/B. */
 int edt_slerp_merge_hold(const void* v0, const void* v1, int in_dt, void* out, int out_dt,
                          const uint64_t* chunk_desc, int64_t nchunks, const int32_t* seg_first_chunk, int nseg,
                          const double* t, double dot_threshold, double eps, double* partial, float* coef,
