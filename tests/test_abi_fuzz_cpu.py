@@ -105,7 +105,7 @@ def test_sgd_apply_sum_rejects(lib, kind, nacc, n, bad, which):
 
 
 @FUZZ
-@given(kind=st.sampled_from(["in_dt", "out_dt", "negative", "null"]), entry=st.sampled_from(["stats", "blend", "merge"]),
+@given(kind=st.sampled_from(["in_dt", "out_dt", "negative", "null"]), entry=st.sampled_from(["stats", "blend", "merge", "hold"]),
        nchunks=st.integers(1, 1 << 30), neg=st.integers(-(1 << 40), -1), bad=bad_dtype)
 def test_slerp_passes_reject(lib, kind, entry, nchunks, neg, bad):
     in_dt, out_dt, v0 = BF16, BF16, fake(0)
@@ -125,10 +125,20 @@ def test_slerp_passes_reject(lib, kind, entry, nchunks, neg, bad):
         rc = lib.edt_slerp_stats(v0, fake(1), in_dt, fake(2), nchunks, fake(3), None)
     elif entry == "blend":
         rc = lib.edt_slerp_blend(v0, fake(1), in_dt, fake(2), out_dt, fake(3), nchunks, fake(4), None)
-    else:
+    elif entry == "merge":
         rc = lib.edt_slerp_merge(v0, fake(1), in_dt, fake(2), out_dt, fake(3), nchunks, fake(4), 1, fake(5),
                                  0.9995, 1e-8, fake(6), fake(7), None, None)
+    else:
+        rc = lib.edt_slerp_merge_hold(v0, fake(1), in_dt, fake(2), out_dt, fake(3), nchunks, fake(4), 1, fake(5),
+                                      0.9995, 1e-8, fake(6), fake(7), None, None)
     _expect(lib, rc, needle)
+
+
+def test_slerp_hold_takes_bf16_parents_only(lib):
+    """The on-chip-hold form rejects fp32 parents before any launch (edt_slerp_merge takes them)."""
+    rc = lib.edt_slerp_merge_hold(fake(0), fake(1), F32, fake(2), F32, fake(3), 4, fake(4), 1, fake(5),
+                                  0.9995, 1e-8, fake(6), fake(7), None, None)
+    _expect(lib, rc, "bf16 parents only")
 
 
 @FUZZ
