@@ -59,6 +59,8 @@ SIGNATURES = [
                                          _P, _U64, _P]),
     ("edt_slerp_merge_list", _I, [ctypes.POINTER(_P), ctypes.POINTER(_P), _I, ctypes.POINTER(_P), _I, _P,
                                   ctypes.c_int64, _P, _I, _P, _D, _D, _P, _P, _P, _P, _U64, _P]),
+    ("edt_slerp_merge_list_speculative", _I, [ctypes.POINTER(_P), ctypes.POINTER(_P), _I, ctypes.POINTER(_P), _I,
+                                              _P, ctypes.c_int64, _P, _I, _P, _D, _D, _P, _P, _P, _P, _P, _U64, _P]),
     ("edt_slerp_sums_doubles", _U64, [_I, ctypes.c_int64]),
     ("edt_slerp_refdot_workspace_bytes", _U64, [_I, ctypes.c_int64, ctypes.c_uint32, _I]),
     ("edt_slerp_refdot_flags", _I, [_P, _I, _D, _D, _P, _P]),

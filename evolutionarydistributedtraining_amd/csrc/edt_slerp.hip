@@ -2220,16 +2220,14 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
     return EDT_OK;
 }
 
-int edt_slerp_merge_list(const void* const* v0_t, const void* const* v1_t, int in_dt, void* const* out_t,
-                         int out_dt, const uint64_t* chunk_desc, int64_t nchunks, const int32_t* seg_first_chunk,
-                         int nseg, const double* t, double dot_threshold, double eps, double* partial, float* coef,
-                         float* dot_out, void* workspace, uint64_t workspace_bytes, void* stream) {
-    g_err[0] = 0;
-    if ((in_dt | out_dt) & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
-    if (nseg < 0 || nchunks < 0) return fail(EDT_ERR_ARG, "negative count (segments %d, chunks %lld)", nseg, (long long)nchunks);
-    if (nseg == 0 || nchunks == 0) return EDT_OK;
+}   // extern "C"
+
+namespace {
+// The tensor-list forms' pointer table: {v0, v1, out} per segment, uploaded into `workspace` by a
+// stream-ordered copy (pageable source: staged before hipMemcpyAsync returns).
+int upload_seg_table(const void* const* v0_t, const void* const* v1_t, void* const* out_t, int nseg, void* workspace,
+                     uint64_t workspace_bytes, bool outputs_apart, hipStream_t s) {
     if (!v0_t || !v1_t || !out_t) return fail(EDT_ERR_ARG, "null tensor table");
-    if (!chunk_desc || !seg_first_chunk || !t || !partial || !coef) return fail(EDT_ERR_ARG, "null buffer");
     const uint64_t need = 3ull * sizeof(uint64_t) * (uint64_t)nseg;
     if (!workspace || workspace_bytes < need)
         return fail(EDT_ERR_ARG, "workspace of %llu bytes needed", (unsigned long long)need);
@@ -2240,19 +2238,74 @@ int edt_slerp_merge_list(const void* const* v0_t, const void* const* v1_t, int i
         // a null pointer is only valid for an empty segment (it has no chunks, so it is never read)
         if (!aligned16(v0_t[i]) || !aligned16(v1_t[i]) || !aligned16(out_t[i]))
             return fail(EDT_ERR_ARG, "tensor %d is not 16-byte aligned", i);
+        if (outputs_apart && out_t[i] && (out_t[i] == v0_t[i] || out_t[i] == v1_t[i]))
+            return fail(EDT_ERR_ARG, "tensor %d: the speculative form needs an output apart from its parents", i);
         h[3 * i] = reinterpret_cast<uintptr_t>(v0_t[i]);
         h[3 * i + 1] = reinterpret_cast<uintptr_t>(v1_t[i]);
         h[3 * i + 2] = reinterpret_cast<uintptr_t>(out_t[i]);
     }
-    // pageable source: staged before hipMemcpyAsync returns, stream-ordered on the device
-    hipError_t e = hipMemcpyAsync(workspace, h.data(), need, hipMemcpyHostToDevice, (hipStream_t)stream);
+    hipError_t e = hipMemcpyAsync(workspace, h.data(), need, hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return fail(EDT_ERR_LAUNCH, "tensor table upload failed: %s", hipGetErrorString(e));
+    return EDT_OK;
+}
+}   // namespace
+
+extern "C" {
+
+int edt_slerp_merge_list(const void* const* v0_t, const void* const* v1_t, int in_dt, void* const* out_t,
+                         int out_dt, const uint64_t* chunk_desc, int64_t nchunks, const int32_t* seg_first_chunk,
+                         int nseg, const double* t, double dot_threshold, double eps, double* partial, float* coef,
+                         float* dot_out, void* workspace, uint64_t workspace_bytes, void* stream) {
+    g_err[0] = 0;
+    if ((in_dt | out_dt) & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
+    if (nseg < 0 || nchunks < 0) return fail(EDT_ERR_ARG, "negative count (segments %d, chunks %lld)", nseg, (long long)nchunks);
+    if (nseg == 0 || nchunks == 0) return EDT_OK;
+    if (!v0_t || !v1_t || !out_t) return fail(EDT_ERR_ARG, "null tensor table");
+    if (!chunk_desc || !seg_first_chunk || !t || !partial || !coef) return fail(EDT_ERR_ARG, "null buffer");
+    int rc = upload_seg_table(v0_t, v1_t, out_t, nseg, workspace, workspace_bytes, false, (hipStream_t)stream);
+    if (rc) return rc;
     const uint64_t* seg_ptrs = static_cast<const uint64_t*>(workspace);
-    int rc = slerp_stats_impl(nullptr, nullptr, in_dt, chunk_desc, nchunks, partial, seg_ptrs, stream);
+    rc = slerp_stats_impl(nullptr, nullptr, in_dt, chunk_desc, nchunks, partial, seg_ptrs, stream);
     if (rc) return rc;
     rc = edt_slerp_coef(partial, seg_first_chunk, nseg, t, dot_threshold, eps, coef, dot_out, stream);
     if (rc) return rc;
     return slerp_blend_impl(nullptr, nullptr, in_dt, nullptr, out_dt, chunk_desc, nchunks, coef, seg_ptrs, stream);
+}
+
+int edt_slerp_merge_list_speculative(const void* const* v0_t, const void* const* v1_t, int in_dt, void* const* out_t,
+                                     int out_dt, const uint64_t* chunk_desc, int64_t nchunks,
+                                     const int32_t* seg_first_chunk, int nseg, const double* t, double dot_threshold,
+                                     double eps, double* partial, float* coef, float* dot_out, int32_t* redo,
+                                     void* workspace, uint64_t workspace_bytes, void* stream) {
+    g_err[0] = 0;
+    if ((in_dt | out_dt) & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
+    if (nseg < 0 || nchunks < 0) return fail(EDT_ERR_ARG, "negative count (segments %d, chunks %lld)", nseg, (long long)nchunks);
+    if (nseg == 0 || nchunks == 0) return EDT_OK;
+    if (!v0_t || !v1_t || !out_t) return fail(EDT_ERR_ARG, "null tensor table");
+    if (!chunk_desc || !seg_first_chunk || !t || !partial || !coef || !redo) return fail(EDT_ERR_ARG, "null buffer");
+    hipStream_t s = (hipStream_t)stream;
+    int rc = upload_seg_table(v0_t, v1_t, out_t, nseg, workspace, workspace_bytes, true, s);
+    if (rc) return rc;
+    const uint64_t* seg_ptrs = static_cast<const uint64_t*>(workspace);
+    // the any-redo word: the last double of the workspace, as edt_slerp_merge_speculative's
+    int32_t* any = reinterpret_cast<int32_t*>(partial + edt_slerp_sums_doubles(3, nchunks) - 1);
+    rc = pair_sums(nullptr, nullptr, in_dt, nullptr, out_dt, true, chunk_desc, nchunks, partial, t, seg_ptrs, s, any);
+    if (rc) return rc;
+    slerp_coef_kernel<<<coef_grid(nseg), kBlock, 0, s>>>(partial, seg_first_chunk, nseg, t, (float)dot_threshold,
+                                                         (float)eps, coef, dot_out, redo, any);
+    rc = check_launch("slerp_coef_kernel");
+    if (rc) return rc;
+    const unsigned g = slerp_spec_grid(nchunks);
+    constexpr bool kNtB = EDT_NT_SLERP != 0;
+    if (in_dt == EDT_F32 && out_dt == EDT_F32)
+        slerp_blend_kernel<EDT_F32, EDT_F32, false, false><<<g, kBlock, 0, s>>>(nullptr, nullptr, nullptr, chunk_desc, nchunks, coef, seg_ptrs, redo, any);
+    else if (in_dt == EDT_F32)
+        slerp_blend_kernel<EDT_F32, EDT_BF16, false, false><<<g, kBlock, 0, s>>>(nullptr, nullptr, nullptr, chunk_desc, nchunks, coef, seg_ptrs, redo, any);
+    else if (out_dt == EDT_F32)
+        slerp_blend_kernel<EDT_BF16, EDT_F32, kNtB, false><<<g, kBlock, 0, s>>>(nullptr, nullptr, nullptr, chunk_desc, nchunks, coef, seg_ptrs, redo, any);
+    else
+        slerp_blend_kernel<EDT_BF16, EDT_BF16, kNtB, false><<<g, kBlock, 0, s>>>(nullptr, nullptr, nullptr, chunk_desc, nchunks, coef, seg_ptrs, redo, any);
+    return check_launch("slerp_blend_kernel");
 }
 
 

@@ -414,12 +414,29 @@ def slerp_arena(plan: SlerpPlan, v0: torch.Tensor, v1: torch.Tensor, out: torch.
     _record_dots(plan, plan.dots[:max(1, plan.nseg)], "_dots")
 
 
+def _spans_apart(outs: list[torch.Tensor], ins: list[torch.Tensor]) -> bool:
+    """No output tensor's bytes overlap any input tensor's (sorted sweep over the spans)."""
+    spans = sorted((t.data_ptr(), t.data_ptr() + t.numel() * t.element_size(), k)
+                   for k, ts in ((0, ins), (1, outs)) for t in ts if t.numel())
+    last_end = {0: -1, 1: -1}
+    for a, e, k in spans:
+        if a < last_end[1 - k]:
+            return False
+        last_end[k] = max(last_end[k], e)
+    return True
+
+
 def slerp_list(plan: SlerpPlan, v0s: list[torch.Tensor], v1s: list[torch.Tensor], outs: list[torch.Tensor],
-               t: torch.Tensor, dot_threshold: float = 0.9995, eps: float = 1e-8) -> None:
+               t: torch.Tensor, dot_threshold: float = 0.9995, eps: float = 1e-8,
+               speculate: bool | None = None) -> None:
     """`slerp_arena` over separate tensors (one segment each, e.g. two models' state-dict
     tensors), writing straight into `outs` (e.g. the target model's parameters): no packing.
     Every tensor must be contiguous and 16-byte aligned; plan = make_slerp_plan(...,
-    relative=True) over the tensors' sizes."""
+    relative=True) over the tensors' sizes. speculate as slerp_arena's: True =
+    edt_slerp_merge_list_speculative (lerp-branch outputs written in the sums pass, only
+    SLERP-branch tensors blended again), False = the two-pass edt_slerp_merge_list, None = the
+    cheaper by the previous merge's dots on this plan; outputs that overlap a parent (e.g. merged
+    into the first parent's own tensors) always take the two-pass form. Bit-identical either way."""
     lib = L.lib()
     T = len(v0s)
     if not plan.relative or T != plan.nseg or len(v1s) != T or len(outs) != T:
@@ -435,11 +452,29 @@ def slerp_list(plan: SlerpPlan, v0s: list[torch.Tensor], v1s: list[torch.Tensor]
     if t.dtype != torch.float64 or t.numel() < T:
         raise L.EdtError("t must be a float64 device tensor with one value per segment")
     ws = torch.empty(max(1, 3 * T), dtype=torch.int64, device=t.device)
-    L.check(lib.edt_slerp_merge_list(L.ptr_array(v0s), L.ptr_array(v1s), L.dtype_code(in_dt),
-                                     L.ptr_array(outs), L.dtype_code(out_dt), L.ptr(plan.chunks), plan.nchunks,
-                                     L.ptr(plan.seg_first), T, L.ptr(t), float(dot_threshold), float(eps),
-                                     L.ptr(plan.partial), L.ptr(plan.coef), L.ptr(plan.dots), L.ptr(ws),
-                                     ws.numel() * 8, L.stream_ptr(t.device)), "edt_slerp_merge_list")
+    if speculate is None:
+        speculate = _speculation_pays(plan, v0s[0].element_size(), outs[0].element_size(), wait=False)
+        plan._last_speculate = speculate
+    if speculate and not _spans_apart(outs, v0s + v1s):
+        speculate = False
+    st = L.stream_ptr(t.device)
+    if speculate:
+        redo = getattr(plan, "_redo", None)
+        if redo is None:
+            redo = plan._redo = torch.empty(max(1, plan.nseg), dtype=torch.int32, device=t.device)
+        L.check(lib.edt_slerp_merge_list_speculative(
+            L.ptr_array(v0s), L.ptr_array(v1s), L.dtype_code(in_dt), L.ptr_array(outs), L.dtype_code(out_dt),
+            L.ptr(plan.chunks), plan.nchunks, L.ptr(plan.seg_first), T, L.ptr(t), float(dot_threshold), float(eps),
+            L.ptr(plan.partial), L.ptr(plan.coef), L.ptr(plan.dots), L.ptr(redo), L.ptr(ws), ws.numel() * 8, st),
+            "edt_slerp_merge_list_speculative")
+    else:
+        L.check(lib.edt_slerp_merge_list(L.ptr_array(v0s), L.ptr_array(v1s), L.dtype_code(in_dt),
+                                         L.ptr_array(outs), L.dtype_code(out_dt), L.ptr(plan.chunks), plan.nchunks,
+                                         L.ptr(plan.seg_first), T, L.ptr(t), float(dot_threshold), float(eps),
+                                         L.ptr(plan.partial), L.ptr(plan.coef), L.ptr(plan.dots), L.ptr(ws),
+                                         ws.numel() * 8, st), "edt_slerp_merge_list")
+    plan._last_thr = float(dot_threshold)
+    _record_dots(plan, plan.dots[:max(1, plan.nseg)], "_dots")
 
 
 def slerp_population(plan: SlerpPlan, members: list[torch.Tensor], pairs, outs: list[torch.Tensor],

@@ -262,6 +262,20 @@ int edt_slerp_merge_list(const void* const* v0_t, const void* const* v1_t, int i
                          double dot_threshold, double eps, double* partial, float* coef,
                          float* dot_out, void* workspace, uint64_t workspace_bytes, void* stream);
 
+/* edt_slerp_merge_list with edt_slerp_merge_speculative's first pass: the chunk sums and the
+ * lerp-branch output of every tensor in one pass over the tensors where they lie; only tensors
+ * whose |dot| <= dot_threshold (redo[s] = 1, nseg int32 of device workspace) are blended again.
+ * Parents of one lineage cost one pass instead of two. Outputs, sums and dots are bit-identical
+ * to edt_slerp_merge_list. Every out_t[i] must be apart from every parent tensor (an output equal
+ * to its own parent is rejected; the two-pass list form takes that case); `partial` as
+ * edt_slerp_merge_speculative's (its last double holds the any-redo word). */
+int edt_slerp_merge_list_speculative(const void* const* v0_t, const void* const* v1_t, int in_dt,
+                                     void* const* out_t, int out_dt, const uint64_t* chunk_desc, int64_t nchunks,
+                                     const int32_t* seg_first_chunk, int nseg, const double* t,
+                                     double dot_threshold, double eps, double* partial, float* coef,
+                                     float* dot_out, int32_t* redo, void* workspace, uint64_t workspace_bytes,
+                                     void* stream);
+
 /* SLERP children of a resident population (EDT_RL/edt.py:286-299: every selected pair of one
  * generation, EDT_RL/crossover.py:84-135 per child) in 2 + 2*npairs launches: ONE pass over the
  * nmembers (<= 8) flat member arenas forms every member's squared norm and every pair's dot per

@@ -2,6 +2,7 @@
 every segment in the lerp branch, so the speculative merge is one pass of 2 reads + 1 write per
 element, exactly lerp's bytes). Times, in one process on the same arenas and interleaved:
 edt_lerp, edt_slerp_merge_speculative, the two-pass edt_slerp_merge (stats + blend), the
+tensor-list forms over views of the same arenas (ops.slerp_list: two-pass and speculative), the
 one-launch edt_slerp_merge_hold (checked bit for bit against the two-pass output) and the stats
 pass alone (edt_slerp_stats, 4 B read per element).
 HIP events on the launch stream, median over rounds. Run it under rocprofv3 (--kernel-trace
@@ -58,6 +59,12 @@ def main():
             libs[os.path.basename(f)[3:-3]] = L.load_library(f)
 
     cases = {"lerp": lambda: lib.edt_lerp(L.ptr(v0), L.ptr(v1), 1, L.ptr(out), 1, 1, P, 0.43, st)}
+    # the tensor-list forms (the drop-in path over state-dict tensors) on views of the same arenas
+    sizes = [b - a for a, b in zip(lay.offsets, lay.offsets[1:])]
+    l0, l1, lo = list(torch.split(v0, sizes)), list(torch.split(v1, sizes)), list(torch.split(out, sizes))
+    lplan = ops.make_slerp_plan(lay.offsets, dev, relative=True)
+    cases["list_two_pass"] = lambda: ops.slerp_list(lplan, l0, l1, lo, t, speculate=False)
+    cases["list_speculative"] = lambda: ops.slerp_list(lplan, l0, l1, lo, t, speculate=True)
     for name, lb in libs.items():
         part = torch.empty(int(lb.edt_slerp_sums_doubles(3, plan.nchunks)), dtype=torch.float64, device=dev)
 
@@ -88,8 +95,11 @@ def main():
         cases["stats" + sfx] = stats
         if hasattr(lb, "edt_slerp_merge_hold"):
             cases["hold" + sfx] = hold
-    for f in cases.values():
-        assert f() == 0, L.last_error() if hasattr(L, "last_error") else "launch failed"
+    for k, f in cases.items():
+        if not k.startswith("list_"):
+            assert f() == 0, L.last_error() if hasattr(L, "last_error") else "launch failed"
+        else:
+            f()
     torch.cuda.synchronize()
     times = {k: [] for k in cases}
     s = torch.cuda.current_stream(dev)

@@ -407,6 +407,56 @@ def test_slerp_list_matches_arena(dev, ops, in_dt, out_dt):
         assert torch.equal(bits(torch.cat([x.cpu() for x in a0])), bits(ref.cpu()))
 
 
+@pytest.mark.parametrize("in_dt,out_dt", [(torch.float32, torch.float32), (torch.bfloat16, torch.float32),
+                                          (torch.bfloat16, torch.bfloat16)])
+def test_slerp_list_speculative_matches_two_pass(dev, ops, in_dt, out_dt):
+    """edt_slerp_merge_list_speculative (lerp-branch outputs written in the sums pass over the
+    tensors where they lie, SLERP-branch tensors blended again) is bit-identical to the two-pass
+    list form and to the arena form: outputs and dots, tensors on both sides of the threshold,
+    ragged and empty tensors, a zero tensor; the adaptive choice follows the previous dots; an
+    output equal to its parent is refused by the entry and handled by the two-pass form."""
+    from evolutionarydistributedtraining_amd import _lib as L
+    g = torch.Generator().manual_seed(79)
+    sizes = [0, 1, 7, 33, 4096, 70_001, 0, 129, 200_003, 65_536, 131_073]
+    rel = [0.1, 0.001, 0.2, 0.001, 0.05, 0.005, 0.1, 0.3, 0.002, 0.02, 0.0005]
+    offs = [0]
+    for x in sizes:
+        offs.append(offs[-1] + x)
+    v0 = torch.randn(offs[-1], generator=g) * 0.02
+    v1 = v0.clone()
+    for s_, r in enumerate(rel):
+        a, b = offs[s_], offs[s_ + 1]
+        v1[a:b] += torch.randn(b - a, generator=g) * 0.02 * r
+    v0[offs[7]:offs[8]] = 0
+    ts = torch.tensor([0.5, 0.0, 1.0, 0.43, 0.5, 0.7, 0.5, 0.2, 0.9, 0.3, 0.6], dtype=torch.float64).to(dev)
+    plan = ops.make_slerp_plan(offs, dev)
+    ref = torch.empty(offs[-1], dtype=out_dt, device=dev)
+    ops.slerp_arena(plan, v0.to(in_dt).to(dev), v1.to(in_dt).to(dev), ref, ts, speculate=False)
+    ref_dots = plan.dots.cpu().clone()
+    d = ref_dots[:len(sizes)].abs()
+    assert (d > 0.9995).any() and (d <= 0.9995).any()
+    a0 = [v0[a:b].to(in_dt).to(dev).clone() for a, b in zip(offs, offs[1:])]
+    a1 = [v1[a:b].to(in_dt).to(dev).clone() for a, b in zip(offs, offs[1:])]
+    lplan = ops.make_slerp_plan(offs, dev, relative=True)
+    for speculate in (False, True, None):
+        outs = [torch.full((x,), float("nan"), dtype=out_dt, device=dev) for x in sizes]
+        lplan.dots.fill_(float("nan"))
+        ops.slerp_list(lplan, a0, a1, outs, ts, speculate=speculate)
+        assert torch.equal(bits(torch.cat([o.cpu() for o in outs])), bits(ref.cpu())), speculate
+        assert torch.equal(lplan.dots.cpu(), ref_dots), speculate
+    if in_dt == out_dt:                     # in place over parent 0: the two-pass list form
+        c0 = [x.clone() for x in a0]
+        ops.slerp_list(lplan, c0, a1, c0, ts, speculate=True)
+        assert torch.equal(bits(torch.cat([x.cpu() for x in c0])), bits(ref.cpu()))
+        ws = torch.empty(3 * len(sizes), dtype=torch.int64, device=dev)
+        rc = L.lib().edt_slerp_merge_list_speculative(
+            L.ptr_array(a0), L.ptr_array(a1), L.dtype_code(in_dt), L.ptr_array(a0), L.dtype_code(out_dt),
+            L.ptr(lplan.chunks), lplan.nchunks, L.ptr(lplan.seg_first), lplan.nseg, L.ptr(ts), 0.9995, 1e-8,
+            L.ptr(lplan.partial), L.ptr(lplan.coef), None, L.ptr(lplan._redo), L.ptr(ws), ws.numel() * 8,
+            L.stream_ptr(dev))
+        assert rc != 0 and b"apart" in L.lib().edt_last_error()
+
+
 @pytest.mark.parametrize("in_dt,out_dt", [(torch.float32, torch.float32), (torch.bfloat16, torch.bfloat16)])
 @pytest.mark.parametrize("nmem", [1, 2, 3, 5, 8, 11])    # 11: > 8 distinct parents (speculative only)
 def test_slerp_population_matches_per_child(dev, ops, in_dt, out_dt, nmem):
