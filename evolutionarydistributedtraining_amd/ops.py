@@ -414,16 +414,24 @@ def slerp_arena(plan: SlerpPlan, v0: torch.Tensor, v1: torch.Tensor, out: torch.
     _record_dots(plan, plan.dots[:max(1, plan.nseg)], "_dots")
 
 
-def _spans_apart(outs: list[torch.Tensor], ins: list[torch.Tensor]) -> bool:
-    """No output tensor's bytes overlap any input tensor's (sorted sweep over the spans)."""
-    spans = sorted((t.data_ptr(), t.data_ptr() + t.numel() * t.element_size(), k)
-                   for k, ts in ((0, ins), (1, outs)) for t in ts if t.numel())
-    last_end = {0: -1, 1: -1}
-    for a, e, k in spans:
-        if a < last_end[1 - k]:
-            return False
-        last_end[k] = max(last_end[k], e)
-    return True
+def _spans_apart(out_ptrs, out_bytes, in_ptrs, in_bytes) -> bool:
+    """No output span [ptr, ptr + bytes) overlaps an input span: spans sorted by start, each checked
+    against the furthest end of the other kind before it (numpy; empty spans ignored)."""
+    import numpy as np
+    a = np.concatenate((np.asarray(in_ptrs, dtype=np.int64), np.asarray(out_ptrs, dtype=np.int64)))
+    n = np.concatenate((np.asarray(in_bytes, dtype=np.int64), np.asarray(out_bytes, dtype=np.int64)))
+    k = np.concatenate((np.zeros(len(in_ptrs), dtype=bool), np.ones(len(out_ptrs), dtype=bool)))
+    keep = n > 0
+    a, n, k = a[keep], n[keep], k[keep]
+    if a.size == 0:
+        return True
+    o = np.argsort(a, kind="stable")
+    a, e, k = a[o], a[o] + n[o], k[o]
+    far_out = np.maximum.accumulate(np.where(k, e, -1))       # furthest end of an output so far
+    far_in = np.maximum.accumulate(np.where(k, -1, e))
+    prev_out = np.concatenate(([-1], far_out[:-1]))
+    prev_in = np.concatenate(([-1], far_in[:-1]))
+    return not bool(np.any(np.where(k, a < prev_in, a < prev_out)))
 
 
 def slerp_list(plan: SlerpPlan, v0s: list[torch.Tensor], v1s: list[torch.Tensor], outs: list[torch.Tensor],
@@ -452,24 +460,29 @@ def slerp_list(plan: SlerpPlan, v0s: list[torch.Tensor], v1s: list[torch.Tensor]
     if t.dtype != torch.float64 or t.numel() < T:
         raise L.EdtError("t must be a float64 device tensor with one value per segment")
     ws = torch.empty(max(1, 3 * T), dtype=torch.int64, device=t.device)
+    p0, p1, po = ([x.data_ptr() for x in ts] for ts in (v0s, v1s, outs))
     if speculate is None:
         speculate = _speculation_pays(plan, v0s[0].element_size(), outs[0].element_size(), wait=False)
         plan._last_speculate = speculate
-    if speculate and not _spans_apart(outs, v0s + v1s):
-        speculate = False
+    if speculate:
+        import numpy as np
+        n = np.diff(np.asarray(plan.seg_offsets, dtype=np.int64))
+        nin, nout = n * v0s[0].element_size(), n * outs[0].element_size()
+        speculate = _spans_apart(po, nout, p0 + p1, np.concatenate((nin, nin)))
+    tab = [(ctypes.c_void_p * max(1, T))(*p) for p in (p0, p1, po)]
     st = L.stream_ptr(t.device)
     if speculate:
         redo = getattr(plan, "_redo", None)
         if redo is None:
             redo = plan._redo = torch.empty(max(1, plan.nseg), dtype=torch.int32, device=t.device)
         L.check(lib.edt_slerp_merge_list_speculative(
-            L.ptr_array(v0s), L.ptr_array(v1s), L.dtype_code(in_dt), L.ptr_array(outs), L.dtype_code(out_dt),
+            tab[0], tab[1], L.dtype_code(in_dt), tab[2], L.dtype_code(out_dt),
             L.ptr(plan.chunks), plan.nchunks, L.ptr(plan.seg_first), T, L.ptr(t), float(dot_threshold), float(eps),
             L.ptr(plan.partial), L.ptr(plan.coef), L.ptr(plan.dots), L.ptr(redo), L.ptr(ws), ws.numel() * 8, st),
             "edt_slerp_merge_list_speculative")
     else:
-        L.check(lib.edt_slerp_merge_list(L.ptr_array(v0s), L.ptr_array(v1s), L.dtype_code(in_dt),
-                                         L.ptr_array(outs), L.dtype_code(out_dt), L.ptr(plan.chunks), plan.nchunks,
+        L.check(lib.edt_slerp_merge_list(tab[0], tab[1], L.dtype_code(in_dt),
+                                         tab[2], L.dtype_code(out_dt), L.ptr(plan.chunks), plan.nchunks,
                                          L.ptr(plan.seg_first), T, L.ptr(t), float(dot_threshold), float(eps),
                                          L.ptr(plan.partial), L.ptr(plan.coef), L.ptr(plan.dots), L.ptr(ws),
                                          ws.numel() * 8, st), "edt_slerp_merge_list")

@@ -358,3 +358,22 @@ def test_examples_import_and_model_runs_on_cpu():
     assert bool((x[:, 1:] == (3 * x[:, :-1] + 1) % diloco_sim.VOCAB).all())
     loss = diloco_sim.loss_of(m, x)
     assert loss.ndim == 0 and float(loss) > 0
+
+
+def test_spans_apart_matches_brute_force():
+    """ops._spans_apart (the speculative list form's overlap check, numpy sweep) against a
+    pairwise check on random spans, empty spans included."""
+    import random
+    from evolutionarydistributedtraining_amd import ops
+
+    def brute(op, ob, ip, ib):
+        return not any(n and m and a < c + m and c < a + n for a, n in zip(op, ob) for c, m in zip(ip, ib))
+
+    rnd = random.Random(5)
+    for _ in range(3000):
+        ni, no = rnd.randint(0, 6), rnd.randint(0, 6)
+        ip = [rnd.randint(0, 200) for _ in range(ni)]
+        ib = [rnd.choice([0, 1, 5, 20, 50]) for _ in range(ni)]
+        op = [rnd.randint(0, 200) for _ in range(no)]
+        ob = [rnd.choice([0, 1, 5, 20, 50]) for _ in range(no)]
+        assert ops._spans_apart(op, ob, ip, ib) == brute(op, ob, ip, ib)
