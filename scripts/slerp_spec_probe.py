@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--far", action="store_true", help="independent parents (the SLERP branch)")
     ap.add_argument("--variants", default="")
+    ap.add_argument("--no-hold", action="store_true", help="skip the hold form (cooperative launch)")
     a = ap.parse_args()
     from evolutionarydistributedtraining_amd import _lib as L
     from evolutionarydistributedtraining_amd import ops
@@ -93,7 +94,7 @@ def main():
         cases["speculative" + sfx] = spec
         cases["two_pass" + sfx] = two
         cases["stats" + sfx] = stats
-        if hasattr(lb, "edt_slerp_merge_hold"):
+        if hasattr(lb, "edt_slerp_merge_hold") and not a.no_hold:
             cases["hold" + sfx] = hold
     for k, f in cases.items():
         if not k.startswith("list_"):
