@@ -99,8 +99,9 @@ def parse(argv=None):
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     p.add_argument("--ops", default="configs1_125m,pair_merge,slerp_7b,population_7b",
                    help="the other hot-path measurements in the same line ('none': skip): N=1 configs1_125m "
-                        "(BASELINE configs[1]: 125M x 8 resident), pair_merge, slerp_7b; N>1 population_7b "
-                        "(BASELINE configs[4] across the N GPUs)")
+                        "(BASELINE configs[1]: 125M x 8 resident), pair_merge, slerp_7b, population_7b "
+                        "(configs[4]: at N = 1 all 8 members resident on the GPU; at N > 1 "
+                        "across the N GPUs)")
     p.add_argument("--ops-cpu-seconds", type=float, default=4.0, help="CPU baseline budget per extra op")
     p.add_argument("--compare-schedules", type=int, default=1,
                    help="N>1: after the value, also time the other sharded schedules (exact/workers, "
@@ -624,6 +625,57 @@ def bench_population(args, rt, comm, kernels=None, layout_name="qwen2p5_7b_body"
     return res
 
 
+def bench_population_resident(args, dev, layout_name="qwen2p5_7b_body", members_n=8):
+    """BASELINE configs[4] on ONE GPU: a population of 8 members (7.07B bf16 bodies) SLERP-crossed
+    into 8 children, every buffer resident in HBM (16 x 14.1 GB = 226 GB; EDT_RL/edt.py:286-299 ->
+    EDT_RL/crossover.py:84-135 per child), as ops.slerp_population runs it: `speculative` = the
+    co-located single pass (members of one lineage: every tensor in the lerp branch), `two_pass` =
+    the Gram stats pass + the member-major blend (the SLERP-branch form; its cost does not depend
+    on the branch), on the same members. Children (c, c + 1): 8 distinct parents, each feeding two
+    children. `floor_bytes`: the form's least HBM bytes (each distinct parent read once per pass,
+    each child written once); `algo_bytes`: the generation's (every member once, every child once).
+    Skipped with a reason when the HBM left after the other extras cannot hold it."""
+    from evolutionarydistributedtraining_amd import ops
+    from evolutionarydistributedtraining_amd.layouts import LAYOUTS
+    lay = LAYOUTS[layout_name]()
+    P, bf, M = lay.total, torch.bfloat16, members_n
+    need = 2 * M * P * 2
+    free, _ = torch.cuda.mem_get_info(dev)
+    res = {"workload": f"SLERP population of {M} x {layout_name} (P={P}, bf16), all resident on one GPU",
+           "kernel": "edt_slerp_population_speculative / edt_slerp_population"}
+    if free < need + (6 << 30):
+        res["skipped"] = f"needs {need / 1e9:.0f} GB of HBM, {free / 1e9:.0f} GB free"
+        return res
+    members = [torch.empty(P, dtype=bf, device=dev) for _ in range(M)]
+    outs = [torch.empty(P, dtype=bf, device=dev) for _ in range(M)]
+    g = torch.Generator(device=dev).manual_seed(12)
+    step = 1 << 27
+    for s0 in range(0, P, step):                  # one lineage: a base + 0.5 % per member
+        e = min(P, s0 + step)
+        x = torch.randn(e - s0, generator=g, device=dev) * 0.02
+        for m in members:
+            m[s0:e] = (x + torch.randn(e - s0, generator=g, device=dev) * (0.02 * 0.005)).to(bf)
+        del x
+    pairs = [(c, (c + 1) % M) for c in range(M)]
+    plan = ops.make_slerp_plan(lay.offsets, dev)
+    t = torch.full((len(lay),), 0.5, dtype=torch.float64, device=dev)
+    res["pairs"] = pairs
+    algo = 2 * M * P * 2
+    for form, spec, floor in (("speculative", True, 2 * M * P * 2), ("two_pass", False, 3 * M * P * 2)):
+        ms = _event_ms(lambda: ops.slerp_population(plan, members, pairs, outs, t, speculate=spec), 3, 1)
+        res[form] = {"ms": round(ms, 3), "floor_bytes": floor, "algo_bytes": algo,
+                     "roofline": {"bound": "hbm", "achieved": round(floor / (ms / 1e3) / 1e9, 1),
+                                  "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                                  "frac": round(floor / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+                                  "algo_frac": round(algo / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)}}
+    dots = plan._pop_dots.float().abs() if getattr(plan, "_pop_dots", None) is not None else None
+    if dots is not None:
+        res["lerp_branch_fraction"] = round(float((dots > 0.9995).float().mean()), 4)
+    del members, outs
+    torch.cuda.empty_cache()
+    return res
+
+
 def stream_ceiling_ms(theta, workers, momentum, iters=10):
     """Median HIP-event time of edt_probe_stream over the step's own operands (None if the
     step runs without momentum: the probe always reads and writes a momentum stream)."""
@@ -1010,6 +1062,12 @@ def main():
                 except Exception as e:          # an extra: report it, keep the line
                     out[name] = {"error": f"{type(e).__name__}: {str(e)[:300]}"}
                     torch.cuda.empty_cache()
+        if "population_7b" in args.ops:          # last: it needs 226 GB of the HBM
+            try:
+                out["population_slerp_7b"] = bench_population_resident(args, dev, args.population_layout)
+            except Exception as e:              # an extra: report it, keep the line
+                out["population_slerp_7b"] = {"error": f"{type(e).__name__}: {str(e)[:300]}"}
+                torch.cuda.empty_cache()
     if args.cpu_baseline_seconds > 0:
         # rank 0 after the GPU phase, on this host's cores: the whole population's step (the
         # reference's master runs all K workers' deltas on its CPU)
