@@ -67,3 +67,21 @@ def test_multi_gpu_path_line_at_world_1():
     x = d["roofline"]["xgmi"]
     assert x["bound"] == "xgmi" and "wire_bytes_per_rank" in x
     assert "weak_scaling" in d and "extras_deadline" not in d
+
+
+def test_single_gpu_line_population_extra():
+    """The N = 1 line's BASELINE configs[4] sub-object (population_slerp_7b: 8 members and 8
+    children resident, both SLERP forms), here on the 125M layout: fields, roofline arithmetic,
+    every lineage tensor in the lerp branch."""
+    d = _run("--place-candidates", "1", "--ops", "population_7b", "--population-layout", "gpt2_small",
+             "--bcast-compare", "0")
+    _check_common(d, 1)
+    p = d["population_slerp_7b"]
+    assert "error" not in p and "skipped" not in p, p
+    assert len(p["pairs"]) == 8 and p["lerp_branch_fraction"] == 1.0
+    for form in ("speculative", "two_pass"):
+        f = p[form]
+        assert f["ms"] > 0 and f["floor_bytes"] >= f["algo_bytes"] > 0
+        r = f["roofline"]
+        assert r["achieved"] == pytest.approx(f["floor_bytes"] / (f["ms"] / 1e3) / 1e9, rel=1e-2)
+        assert r["frac"] == pytest.approx(r["achieved"] / r["peak"], abs=1e-3)
