@@ -4,7 +4,12 @@
  * run on the null stream through edt_outer_step, and theta and the momentum are compared bit for
  * bit with the CPU oracle's restatement of EDT_LM/diloco.py:238-289 (oracle/_build/liboracle.so,
  * test infrastructure). Then the error convention: a bad dtype code returns a negative EDT_ERR_*
- * and edt_last_error() says why. Prints "abi consumer ok" and exits 0 on success. */
+ * and edt_last_error() says why. Then the SLERP crossover over separate tensors as a binding of
+ * EDT_RL/crossover.py:84-135 would drive it (edt_slerp_make_chunks -> relative chunk starts ->
+ * edt_slerp_merge_list, and the single-pass edt_slerp_merge_list_speculative): parents of one
+ * lineage, so every tensor takes the lerp branch, whose output is compared bit for bit with the
+ * oracle's lerp, and the two forms with each other (outputs and dots). Prints "abi consumer ok"
+ * and exits 0 on success. */
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -16,6 +21,7 @@
 /* oracle/edt_oracle.c */
 int oracle_outer_step(void* theta, int gdt, const void* const* workers, int wdt, int K, void* mom,
                       int has_buf, uint64_t n, double lr, double mu, int nesterov, const uint8_t* tail);
+int oracle_lerp(const void* v0, const void* v1, int in_dt, void* out, int out_dt, int cdt, uint64_t n, double t);
 
 #define K 3
 #define CK(x)                                                                  \
@@ -31,6 +37,104 @@ static uint64_t lcg = 0x9E3779B97F4A7C15ull;
 static float uniform(void) { /* in (-1, 1) */
     lcg = lcg * 6364136223846793005ull + 1442695040888963407ull;
     return (float)((int64_t)(lcg >> 11) - (1ll << 52)) / (float)(1ll << 52);
+}
+
+#define NSEG 4
+/* The tensor-list SLERP of three ragged tensors (+ an empty one) through the C ABI, both forms. */
+static int slerp_list_check(void) {
+    const uint64_t sizes[NSEG] = {70001, 0, 131073, 4099};
+    uint64_t offs[NSEG + 1] = {0};
+    for (int s = 0; s < NSEG; ++s) offs[s + 1] = offs[s] + sizes[s];
+    int32_t first[NSEG + 1];
+    const int64_t nchunks = edt_slerp_make_chunks(offs, NSEG, 1u << 16, NULL, 0, first);
+    if (nchunks <= 0) {
+        fprintf(stderr, "edt_slerp_make_chunks: %lld %s\n", (long long)nchunks, edt_last_error());
+        return 1;
+    }
+    uint64_t* desc = malloc(3 * nchunks * sizeof(uint64_t));
+    if (edt_slerp_make_chunks(offs, NSEG, 1u << 16, desc, nchunks, first) != nchunks) return 1;
+    for (int64_t c = 0; c < nchunks; ++c) desc[3 * c] -= offs[desc[3 * c + 2]];    /* relative starts */
+    const double tv[NSEG] = {0.5, 0.3, 0.43, 0.9};
+    void *d_v0[NSEG], *d_v1[NSEG], *d_a[NSEG], *d_b[NSEG];
+    float *h0[NSEG], *h1[NSEG], *want[NSEG], *got = malloc(sizes[2] * sizeof(float) + 16);
+    for (int s = 0; s < NSEG; ++s) {
+        const size_t nb = sizes[s] * sizeof(float);
+        h0[s] = malloc(nb + 16);
+        h1[s] = malloc(nb + 16);
+        want[s] = malloc(nb + 16);
+        for (uint64_t i = 0; i < sizes[s]; ++i) {
+            h0[s][i] = 0.02f * uniform();
+            h1[s][i] = h0[s][i] * (1.0f + 1e-3f * uniform());      /* one lineage: |dot| > 0.9995 */
+        }
+        oracle_lerp(h0[s], h1[s], EDT_F32, want[s], EDT_F32, EDT_F32, sizes[s], tv[s]);
+        d_v0[s] = d_v1[s] = d_a[s] = d_b[s] = NULL;
+        if (!nb) continue;
+        CK(hipMalloc(&d_v0[s], nb));
+        CK(hipMalloc(&d_v1[s], nb));
+        CK(hipMalloc(&d_a[s], nb));
+        CK(hipMalloc(&d_b[s], nb));
+        CK(hipMemcpy(d_v0[s], h0[s], nb, hipMemcpyHostToDevice));
+        CK(hipMemcpy(d_v1[s], h1[s], nb, hipMemcpyHostToDevice));
+    }
+    void *d_desc, *d_first, *d_t, *d_partial, *d_coef, *d_dots_a, *d_dots_b, *d_redo, *d_ws;
+    const uint64_t nd = edt_slerp_sums_doubles(3, nchunks);
+    CK(hipMalloc(&d_desc, 3 * nchunks * sizeof(uint64_t)));
+    CK(hipMalloc(&d_first, sizeof(first)));
+    CK(hipMalloc(&d_t, sizeof(tv)));
+    CK(hipMalloc(&d_partial, nd * sizeof(double)));
+    CK(hipMalloc(&d_coef, 2 * NSEG * sizeof(float)));
+    CK(hipMalloc(&d_dots_a, NSEG * sizeof(float)));
+    CK(hipMalloc(&d_dots_b, NSEG * sizeof(float)));
+    CK(hipMalloc(&d_redo, NSEG * sizeof(int32_t)));
+    CK(hipMalloc(&d_ws, 3 * NSEG * sizeof(uint64_t)));
+    CK(hipMemcpy(d_desc, desc, 3 * nchunks * sizeof(uint64_t), hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_first, first, sizeof(first), hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_t, tv, sizeof(tv), hipMemcpyHostToDevice));
+    int rc = edt_slerp_merge_list((const void* const*)d_v0, (const void* const*)d_v1, EDT_F32, d_a, EDT_F32, d_desc,
+                                  nchunks, d_first, NSEG, d_t, 0.9995, 1e-8, d_partial, d_coef, d_dots_a, d_ws,
+                                  3 * NSEG * sizeof(uint64_t), NULL);
+    if (rc == 0)
+        rc = edt_slerp_merge_list_speculative((const void* const*)d_v0, (const void* const*)d_v1, EDT_F32, d_b,
+                                              EDT_F32, d_desc, nchunks, d_first, NSEG, d_t, 0.9995, 1e-8, d_partial,
+                                              d_coef, d_dots_b, d_redo, d_ws, 3 * NSEG * sizeof(uint64_t), NULL);
+    if (rc != 0) {
+        fprintf(stderr, "slerp list: %d %s\n", rc, edt_last_error());
+        return 1;
+    }
+    /* an output that is its own parent: the speculative form refuses it, nothing launched */
+    rc = edt_slerp_merge_list_speculative((const void* const*)d_v0, (const void* const*)d_v1, EDT_F32, d_v0,
+                                          EDT_F32, d_desc, nchunks, d_first, NSEG, d_t, 0.9995, 1e-8, d_partial,
+                                          d_coef, d_dots_b, d_redo, d_ws, 3 * NSEG * sizeof(uint64_t), NULL);
+    if (rc >= 0) {
+        fprintf(stderr, "speculative list form accepted an output aliasing its parent\n");
+        return 1;
+    }
+    CK(hipDeviceSynchronize());
+    float da[NSEG], db[NSEG];
+    CK(hipMemcpy(da, d_dots_a, sizeof(da), hipMemcpyDeviceToHost));
+    CK(hipMemcpy(db, d_dots_b, sizeof(db), hipMemcpyDeviceToHost));
+    for (int s = 0; s < NSEG; ++s) {
+        if (!sizes[s]) continue;
+        if (memcmp(&da[s], &db[s], sizeof(float)) != 0 || !(da[s] > 0.9995f)) {
+            fprintf(stderr, "tensor %d: dots %.9g / %.9g\n", s, da[s], db[s]);
+            return 1;
+        }
+        for (int form = 0; form < 2; ++form) {
+            CK(hipMemcpy(got, form ? d_b[s] : d_a[s], sizes[s] * sizeof(float), hipMemcpyDeviceToHost));
+            if (memcmp(got, want[s], sizes[s] * sizeof(float)) != 0) {
+                fprintf(stderr, "tensor %d (%s form) differs from the oracle's lerp\n", s,
+                        form ? "speculative" : "two-pass");
+                return 1;
+            }
+        }
+        hipFree(d_v0[s]);
+        hipFree(d_v1[s]);
+        hipFree(d_a[s]);
+        hipFree(d_b[s]);
+    }
+    printf("slerp list (two-pass and speculative): %lld chunks, bit-exact with the oracle's lerp branch\n",
+           (long long)nchunks);
+    return 0;
 }
 
 int main(void) {
@@ -90,6 +194,5 @@ int main(void) {
     for (int k = 0; k < K; ++k) hipFree(d_w[k]);
     hipFree(d_theta);
     hipFree(d_mom);
-    printf("abi consumer ok\n");
-    return 0;
+    return slerp_list_check() ? 1 : (printf("abi consumer ok\n"), 0);
 }

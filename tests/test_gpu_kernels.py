@@ -700,14 +700,16 @@ def test_errors_are_raised(dev, ops):
 def test_c_consumer_runs():
     """The plain-C consumer of include/edt_sync.h (tests/c_abi/abi_consumer.c, built by build()):
     hipMalloc'd buffers, two edt_outer_step calls on the null stream, bit-exact against the C
-    oracle, and the negative-code + edt_last_error() convention for a bad argument."""
+    oracle, and the negative-code + edt_last_error() convention for a bad argument; then the
+    tensor-list SLERP (two-pass and speculative) over separate hipMalloc'd tensors, bit-exact with
+    the oracle's lerp branch and with each other."""
     import subprocess
     exe = os.path.join(ROOT, "tests", "c_abi", "_build", "abi_consumer")
     if not os.path.exists(exe):
         subprocess.run(["make", "-s", "-C", os.path.dirname(os.path.dirname(exe))], check=True)
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120, cwd="/")
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "abi consumer ok" in r.stdout
+    assert "abi consumer ok" in r.stdout and "slerp list" in r.stdout
 
 
 def test_c_comm_consumer_runs():
