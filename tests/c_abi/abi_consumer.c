@@ -46,7 +46,9 @@ static int slerp_list_check(void) {
     uint64_t offs[NSEG + 1] = {0};
     for (int s = 0; s < NSEG; ++s) offs[s + 1] = offs[s] + sizes[s];
     int32_t first[NSEG + 1];
-    const int64_t nchunks = edt_slerp_make_chunks(offs, NSEG, 1u << 16, NULL, 0, first);
+    /* sizing call: no table given, so the count comes back as -(count) - 1 */
+    const int64_t need = edt_slerp_make_chunks(offs, NSEG, 1u << 16, NULL, 0, first);
+    const int64_t nchunks = need < 0 ? -need - 1 : need;
     if (nchunks <= 0) {
         fprintf(stderr, "edt_slerp_make_chunks: %lld %s\n", (long long)nchunks, edt_last_error());
         return 1;
