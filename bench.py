@@ -640,6 +640,7 @@ def bench_population_resident(args, dev, layout_name="qwen2p5_7b_body", members_
     lay = LAYOUTS[layout_name]()
     P, bf, M = lay.total, torch.bfloat16, members_n
     need = 2 * M * P * 2
+    torch.cuda.empty_cache()                      # blocks the earlier extras left cached count as free
     free, _ = torch.cuda.mem_get_info(dev)
     res = {"workload": f"SLERP population of {M} x {layout_name} (P={P}, bf16), all resident on one GPU",
            "kernel": "edt_slerp_population_speculative / edt_slerp_population"}
