@@ -664,11 +664,14 @@ def bench_population_resident(args, dev, layout_name="qwen2p5_7b_body", members_
     algo = 2 * M * P * 2
     for form, spec, floor in (("speculative", True, 2 * M * P * 2), ("two_pass", False, 3 * M * P * 2)):
         ms = _event_ms(lambda: ops.slerp_population(plan, members, pairs, outs, t, speculate=spec), 3, 1)
+        traffic, note = (_pmc_traffic(args, f"population_7b/{form}", with_note=True)
+                         if layout_name == "qwen2p5_7b_body" else (None, "PMC entries are for the 7B body"))
         res[form] = {"ms": round(ms, 3), "floor_bytes": floor, "algo_bytes": algo,
                      "roofline": {"bound": "hbm", "achieved": round(floor / (ms / 1e3) / 1e9, 1),
                                   "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                                   "frac": round(floor / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
-                                  "algo_frac": round(algo / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)}}
+                                  "algo_frac": round(algo / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+                                  "traffic": traffic, "traffic_source": note}}
     dots = plan._pop_dots.float().abs() if getattr(plan, "_pop_dots", None) is not None else None
     if dots is not None:
         res["lerp_branch_fraction"] = round(float((dots > 0.9995).float().mean()), 4)
