@@ -92,12 +92,13 @@ def test_lerp_fuzz(oracle, dev, n, t, dt, seed):
 @given(sizes_=st.lists(st.integers(0, 3000), min_size=1, max_size=5),
        ts=st.lists(st.floats(0.0, 1.0), min_size=5, max_size=5),
        spread=st.sampled_from([1e-4, 0.01, 0.05, 0.5, 2.0]), seed=st.integers(0, 2**31 - 1),
-       speculate=st.booleans())
-def test_slerp_fuzz(oracle, dev, sizes_, ts, spread, seed, speculate):
+       speculate=st.booleans(), layout=st.sampled_from(["arena", "list"]))
+def test_slerp_fuzz(oracle, dev, sizes_, ts, spread, seed, speculate, layout):
     """Multi-tensor SLERP (EDT_RL/crossover.py:11-43) over random segment sizes (empty included),
     per-segment t and parent distances from lineage (lerp branch) to far (SLERP branch), both
-    kernel forms: per segment the branch agrees with the oracle's (fp32) dot away from the
-    threshold, the lerp branch is bit-exact, and the SLERP branch is within the golden bar."""
+    kernel forms, over flat arenas or separate tensors (the tensor-list path): per segment the
+    branch agrees with the oracle's (fp32) dot away from the threshold, the lerp branch is
+    bit-exact, and the SLERP branch is within the golden bar."""
     from evolutionarydistributedtraining_amd import ops
     g = torch.Generator().manual_seed(seed)
     offs = [0]
@@ -107,10 +108,18 @@ def test_slerp_fuzz(oracle, dev, sizes_, ts, spread, seed, speculate):
     v0 = torch.randn(n, generator=g) * 0.02
     v1 = v0 + torch.randn(n, generator=g) * 0.02 * spread
     t = torch.tensor(ts[:len(sizes_)], dtype=torch.float64)
-    plan = ops.make_slerp_plan(offs, dev, chunk_elems=1024)
-    out_d = torch.empty(max(n, 1), dtype=torch.float32, device=dev)[:n]
-    ops.slerp_arena(plan, v0.to(dev), v1.to(dev), out_d, t.to(dev), speculate=speculate)
-    got = out_d.cpu()
+    if layout == "arena":
+        plan = ops.make_slerp_plan(offs, dev, chunk_elems=1024)
+        out_d = torch.empty(max(n, 1), dtype=torch.float32, device=dev)[:n]
+        ops.slerp_arena(plan, v0.to(dev), v1.to(dev), out_d, t.to(dev), speculate=speculate)
+        got = out_d.cpu()
+    else:
+        plan = ops.make_slerp_plan(offs, dev, chunk_elems=1024, relative=True)
+        pieces = list(zip(offs, offs[1:]))
+        outs = [torch.empty(b - a, dtype=torch.float32, device=dev) for a, b in pieces]
+        ops.slerp_list(plan, [v0[a:b].to(dev) for a, b in pieces], [v1[a:b].to(dev) for a, b in pieces], outs,
+                       t.to(dev), speculate=speculate)
+        got = torch.cat([o.cpu() for o in outs])
     for s in range(len(sizes_)):
         a, b = offs[s], offs[s + 1]
         if b == a:
