@@ -261,6 +261,18 @@ def slerp_coefficients(t: float, v0, v1, dot_threshold: float = 0.9995, eps: flo
     return np.sin(th0 - th_t) / np.sin(th0), np.sin(th_t) / np.sin(th0), dot
 
 
+def slerp_coefficients_at_dot(t: float, dot, dot_threshold: float = 0.9995):
+    """The reference's branch and (c0, c1) (EDT_RL/crossover.py:31-43) for a GIVEN fp32 dot: the
+    same numpy float32 ops as slerp_coefficients after its dot. Used to measure the formula's own
+    conditioning (how far c moves for a dot a few ulps away)."""
+    dot = np.float32(dot)
+    if np.abs(dot) > dot_threshold:
+        return np.float32(1 - t), np.float32(t)
+    th0 = np.arccos(dot)
+    th_t = th0 * t
+    return np.sin(th0 - th_t) / np.sin(th0), np.sin(th_t) / np.sin(th0)
+
+
 # ---- the reference's CPU loop as it runs (timing baseline, not a checker) ---------------------
 
 def torch_loop_outer_step(base_params: list[torch.Tensor], worker_params: list[list[torch.Tensor]],
