@@ -174,3 +174,84 @@ def _coef_allowance(oracle, t, dot, ddot):
     noise0 = abs(float(r0)) * rnd / max(float(th0 - tht), 1e-30)
     noise1 = abs(float(r1)) * rnd / max(float(tht), 1e-30)
     return (out[0] + noise0 + 4 * float(np.spacing(f(abs(r0)))), out[1] + noise1 + 4 * float(np.spacing(f(abs(r1)))))
+
+
+@settings(max_examples=30, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.function_scoped_fixture, HealthCheck.too_slow])
+@given(world=st.integers(1, 8), k_local=st.integers(1, 3),
+       shapes=st.lists(st.one_of(st.tuples(st.integers(1, 5000)), st.tuples(st.integers(1, 70), st.integers(1, 70))),
+                       min_size=1, max_size=6),
+       units=st.integers(1, 9), mode=st.sampled_from(["exact", "reduce_ordered"]), workers_bcast=st.booleans(),
+       dts=st.sampled_from(REGIMES))
+def test_sharded_schedules_fuzz_on_virtual_ranks(dev, world, k_local, shapes, units, mode, workers_bcast, dts):
+    """The HIP kernels inside the sharded schedules on random virtual worlds, layouts and bucket
+    sizes: exact (either broadcast) bit-exact with the fused single-GPU step over the whole
+    population; reduce_ordered bit-exact with per-rank edt_delta_partial + edt_sgd_apply_sum."""
+    from evolutionarydistributedtraining_amd import ops
+    from tests.virtual_schedules import population, run_sharded
+    tdt, wdt = dts
+    broadcast = "workers" if workers_bcast and mode == "exact" else "theta"
+    k_total = k_local * world
+    layout, theta, gens = population(shapes, tdt, wdt, k_total, steps=2, seed=world * 7 + units, device=dev)
+    res = run_sharded(world, layout, tdt, wdt, theta, gens, dev, mode=mode, broadcast=broadcast,
+                      bucket_elems=units * world * 64)
+    n = layout.total
+    th, mom = theta.clone(), torch.zeros(n, dtype=tdt, device=dev)
+    for i, ws in enumerate(gens):
+        if mode == "exact":
+            ops.outer_step(th, ws, mom, i > 0, 0.7, 0.9, True)
+        else:
+            accs = []
+            for r in range(world):
+                acc = torch.empty(n, device=dev)
+                ops.delta_partial(th, ws[r * k_local:(r + 1) * k_local], k_total, acc, False)
+                accs.append(acc)
+            ops.sgd_apply_sum(th, accs, mom, i > 0, 0.7, 0.9, True)
+    torch.cuda.synchronize()
+    for r in res:
+        assert torch.equal(bits(r["theta"][:n].cpu()), bits(th.cpu())), r
+    assert torch.equal(bits(res[0]["mom"].cpu()), bits(mom.cpu()))
+    if broadcast == "workers":
+        for r in res:
+            for w in r["workers"]:
+                assert torch.equal(bits(w[:n].cpu()), bits(th.to(wdt).cpu()))
+
+
+@settings(max_examples=25, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.function_scoped_fixture, HealthCheck.too_slow])
+@given(world=st.integers(1, 8), groups=st.integers(1, 4),
+       shapes=st.lists(st.one_of(st.tuples(st.integers(1, 20000)), st.tuples(st.integers(1, 90), st.integers(1, 90))),
+                       min_size=1, max_size=7),
+       seed=st.integers(0, 2**31 - 1))
+def test_sharded_population_fuzz_on_virtual_ranks(dev, world, groups, shapes, seed):
+    """The link-balanced population crossover with the HIP Gram / coefficient / blend passes on
+    random layouts (1,024-element chunks: many chunks per rank, ranges starting off the vector
+    grid), worlds and pipeline groups: every child bit-identical to edt_slerp_merge on its two
+    parents with the same chunk table."""
+    from evolutionarydistributedtraining_amd import ops
+    from evolutionarydistributedtraining_amd.collectives import VirtualWorld
+    from evolutionarydistributedtraining_amd.distributed import ShardedPopulationCrossover
+    from evolutionarydistributedtraining_amd.params import ParamLayout
+    layout = ParamLayout(shapes)
+    n = layout.total
+    g = torch.Generator().manual_seed(seed)
+    base = torch.randn(n, generator=g) * 0.02
+    members = [(base + torch.randn(n, generator=g) * 0.02 * (0.005 if r % 2 else 0.1)).bfloat16().to(dev)
+               for r in range(world)]
+    pairs = [((3 * c + 1) % world, (5 * c + 2) % world) for c in range(world)]
+    t = torch.rand(len(shapes), generator=g, dtype=torch.float64).to(dev)
+
+    def body(comm):
+        sp = ShardedPopulationCrossover(layout, torch.bfloat16, dev, comm=comm, chunk_elems=1024, groups=groups)
+        out = torch.empty(n, dtype=torch.bfloat16, device=dev)
+        sp.slerp_step(members[comm.rank], pairs, t, out)
+        torch.cuda.synchronize()
+        return out
+
+    res = VirtualWorld(world).run(body)
+    plan = ops.make_slerp_plan(layout.offsets, dev, chunk_elems=1024)
+    want = torch.empty(n, dtype=torch.bfloat16, device=dev)
+    for c, (i, j) in enumerate(pairs):
+        ops.slerp_arena(plan, members[i], members[j], want, t, speculate=False)
+        torch.cuda.synchronize()
+        assert torch.equal(res[c].view(torch.int16), want.view(torch.int16)), c
