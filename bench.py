@@ -67,6 +67,13 @@ XGMI_LINK_GBPS = 153.6 / 2    # per xGMI link and direction (153.6 GB/s both way
 DT = {"f32": torch.float32, "bf16": torch.bfloat16}
 
 
+def _free_device() -> None:
+    """Release cached device blocks, including the SLERP passes' pooled workspace (ops._scratch)."""
+    if "evolutionarydistributedtraining_amd.ops" in sys.modules:
+        sys.modules["evolutionarydistributedtraining_amd.ops"].release_scratch()
+    torch.cuda.empty_cache()
+
+
 def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -157,7 +164,7 @@ class Runtime:
 
     def empty_cache(self):
         if self.gpu:
-            torch.cuda.empty_cache()
+            _free_device()
 
     def device_info(self) -> dict:
         if not self.gpu:
@@ -314,6 +321,7 @@ def cpu_baseline(args, theta_dtype, worker_dtype, k):
     host's cores: `value`. Beside it (`c_port`) the same op sequence as the OpenMP C oracle."""
     from oracle import oracle
     out = reference_loop_baseline(args, theta_dtype, worker_dtype, k)
+    oracle.set_threads(out["cores"])
     n = args.cpu_sample_elems
     g = torch.Generator().manual_seed(1)
     theta = (torch.randn(n, generator=g) * 0.02).to(theta_dtype)
@@ -354,9 +362,48 @@ def _block_sample(layout, budget):
     return [layout.shapes[i] for i in idx], [layout.names[i] if layout.names else str(i) for i in idx]
 
 
+def _cgroup_cpu_quota():
+    """CPUs the cgroup's cpu.max quota allows (cgroup v2; v1's cfs files), or None when unlimited."""
+    import math
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        return None if q == "max" else max(1, math.ceil(int(q) / int(p)))
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            p = int(f.read())
+        return None if q <= 0 else max(1, math.ceil(q / p))
+    except (OSError, ValueError):
+        return None
+
+
+def host_cpu_share() -> dict:
+    """The host threads the CPU baseline runs on (torch.set_num_threads over the
+    host's cores): the CPUs this process may run on (sched_getaffinity), capped by a cgroup CPU
+    quota when one is lower (more threads than the quota only time-slice). Reported with
+    os.cpu_count() and the reason whenever the count is below the visible CPUs."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = _cgroup_cpu_quota()
+    threads = min(aff, quota) if quota else aff
+    visible = os.cpu_count() or aff
+    if threads < visible:
+        reason = (f"cgroup cpu.max quota of {quota} CPUs" if quota and quota < aff
+                  else f"process affinity: {aff} of {visible} CPUs")
+    else:
+        reason = "every visible CPU"
+    return {"threads": threads, "affinity": aff, "cgroup_quota": quota, "host_cpus_visible": visible,
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"), "reason": reason}
+
+
 def reference_loop_baseline(args, theta_dtype, worker_dtype, k):
     from evolutionarydistributedtraining_amd.layouts import LAYOUTS
     from oracle import oracle
+    share = host_cpu_share()
+    torch.set_num_threads(share["threads"])
     lay = LAYOUTS[args.layout]()
     shapes, names = _block_sample(lay, 4 * args.cpu_sample_elems)
     total = sum(int(torch.Size(s).numel()) for s in shapes)
@@ -372,7 +419,8 @@ def reference_loop_baseline(args, theta_dtype, worker_dtype, k):
     t, reps = _median_time(rep, args.cpu_baseline_seconds / 2)
     return {"value": round(k * total * torch.finfo(worker_dtype).bits / 8 / t / 1e9, 3), "unit": "GB/s",
             "cores": torch.get_num_threads(), "kind": "port", "cpu_model": _cpu_model(),
-            "host_cpus_visible": os.cpu_count(),
+            "host_cpus_visible": share["host_cpus_visible"], "affinity": share["affinity"],
+            "cgroup_quota": share["cgroup_quota"], "cores_reason": share["reason"],
             "sample": f"{len(shapes)} tensors of {args.layout} ({names[0]} .. {names[-1]}, {total} elements) x {k} "
                       f"workers, EDT_LM/diloco.py:238-289's per-tensor torch loop + torch.optim.SGD "
                       f"(oracle.torch_loop_outer_step), median of {reps} reps"}
@@ -452,7 +500,7 @@ def bench_config1(args, dev):
     per_elem = K * 4 + 16
     gbs = per_elem * P / (ms / 1e3) / 1e9
     del sync, theta, workers
-    torch.cuda.empty_cache()
+    _free_device()
     return {"workload": f"DiLoCo outer step, gpt2_small P={P} T={len(lay)}, population {K} fp32 workers resident, "
                         f"fp32 theta+momentum, lr {args.lr} mu {args.momentum} nesterov {bool(args.nesterov)}",
             "ms_per_step": round(ms, 4), "value": round(K * P * 4 / (ms / 1e3) / 1e9, 2), "unit": "GB/s",
@@ -480,7 +528,7 @@ def bench_pair_merge(args, dev):
     out = torch.empty(P, dtype=bf, device=dev)
     ms = _event_ms(lambda: ops.pair_merge(b1, b2, m1, m2, out, mom, True, 0.7, 0.9, True), args.steps, args.warmup)
     del b1, b2, m1, m2, mom, out
-    torch.cuda.empty_cache()
+    _free_device()
     bpe = 14
     gbs = bpe * P / (ms / 1e3) / 1e9
     res = {"workload": f"EDT-LM pair merge, gpt_1p3b P={P}, bf16 parents/child/momentum, lr 0.7 mu 0.9 nesterov",
@@ -490,6 +538,8 @@ def bench_pair_merge(args, dev):
                         "traffic": _pmc_traffic(args, "pair_merge/gpt_1p3b/bf16"),
                         "traffic_source": _pmc_traffic(args, "pair_merge/gpt_1p3b/bf16", with_note=True)[1]}}
     if args.ops_cpu_seconds > 0:
+        torch.set_num_threads(host_cpu_share()["threads"])
+        oracle.set_threads(torch.get_num_threads())
         n = args.cpu_sample_elems
         gc = torch.Generator().manual_seed(3)
         xs = [(torch.randn(n, generator=gc) * 0.02).to(bf) for _ in range(4)]
@@ -549,8 +599,9 @@ def bench_slerp_7b(args, dev):
                                      "traffic": _pmc_traffic(args, f"slerp_7b/{parents}"),
                                      "traffic_source": _pmc_traffic(args, f"slerp_7b/{parents}", with_note=True)[1]}}
     del v0, v1, out, plan
-    torch.cuda.empty_cache()
+    _free_device()
     if args.ops_cpu_seconds > 0:
+        torch.set_num_threads(host_cpu_share()["threads"])
         # the reference's numpy SLERP (oracle.slerp restates it op for op) over one whole
         # transformer block of the layout (layer 0: the attention projections, the three 67.9M-
         # element MLP matrices, the norms and biases — every tensor shape of the merge, the large
@@ -640,7 +691,7 @@ def bench_population_resident(args, dev, layout_name="qwen2p5_7b_body", members_
     lay = LAYOUTS[layout_name]()
     P, bf, M = lay.total, torch.bfloat16, members_n
     need = 2 * M * P * 2
-    torch.cuda.empty_cache()                      # blocks the earlier extras left cached count as free
+    _free_device()                      # blocks the earlier extras left cached count as free
     free, _ = torch.cuda.mem_get_info(dev)
     res = {"workload": f"SLERP population of {M} x {layout_name} (P={P}, bf16), all resident on one GPU",
            "kernel": "edt_slerp_population_speculative / edt_slerp_population"}
@@ -676,7 +727,7 @@ def bench_population_resident(args, dev, layout_name="qwen2p5_7b_body", members_
     if dots is not None:
         res["lerp_branch_fraction"] = round(float((dots > 0.9995).float().mean()), 4)
     del members, outs
-    torch.cuda.empty_cache()
+    _free_device()
     return res
 
 
@@ -1057,7 +1108,7 @@ def main():
         # the other hot-path kernels, one GPU, after the outer step's arenas are freed
         sync.theta = sync.workers = sync.state = None
         theta = workers = sync = step = None
-        torch.cuda.empty_cache()
+        _free_device()
         for name, fn in (("configs1_125m", bench_config1), ("pair_merge", bench_pair_merge),
                          ("slerp_7b", bench_slerp_7b)):
             if name in args.ops:
@@ -1065,13 +1116,13 @@ def main():
                     out[name] = fn(args, dev)
                 except Exception as e:          # an extra: report it, keep the line
                     out[name] = {"error": f"{type(e).__name__}: {str(e)[:300]}"}
-                    torch.cuda.empty_cache()
+                    _free_device()
         if "population_7b" in args.ops:          # last: it needs 226 GB of the HBM
             try:
                 out["population_slerp_7b"] = bench_population_resident(args, dev, args.population_layout)
             except Exception as e:              # an extra: report it, keep the line
                 out["population_slerp_7b"] = {"error": f"{type(e).__name__}: {str(e)[:300]}"}
-                torch.cuda.empty_cache()
+                _free_device()
     if args.cpu_baseline_seconds > 0:
         # rank 0 after the GPU phase, on this host's cores: the whole population's step (the
         # reference's master runs all K workers' deltas on its CPU)

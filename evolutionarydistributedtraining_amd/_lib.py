@@ -18,6 +18,7 @@ LIB_PATH = os.path.join(PKG_DIR, "libedt_sync.so")
 EDT_F32 = 0
 EDT_BF16 = 1
 EDT_MAX_WORKERS = 64
+EDT_ABI_VERSION = 4         # include/edt_sync.h: the revision these signatures and workspace sizes follow
 
 _DT = {torch.float32: EDT_F32, torch.bfloat16: EDT_BF16}
 
@@ -53,14 +54,22 @@ SIGNATURES = [
     ("edt_slerp_coef", _I, [_P, _P, _I, _P, _D, _D, _P, _P, _P]),
     ("edt_slerp_blend", _I, [_P, _P, _I, _P, _I, _P, ctypes.c_int64, _P, _P]),
     ("edt_slerp_merge", _I, [_P, _P, _I, _P, _I, _P, ctypes.c_int64, _P, _I, _P, _D, _D, _P, _P, _P, _P]),
-    ("edt_slerp_merge_hold", _I, [_P, _P, _I, _P, _I, _P, ctypes.c_int64, _P, _I, _P, _D, _D, _P, _P, _P, _P]),
-    ("edt_slerp_hold_status", _I, [_P, ctypes.c_int64, _P]),
     ("edt_slerp_merge_speculative", _I, [_P, _P, _I, _P, _I, _P, ctypes.c_int64, _P, _I, _P, _D, _D, _P, _P, _P,
                                          _P, _U64, _P]),
     ("edt_slerp_merge_list", _I, [ctypes.POINTER(_P), ctypes.POINTER(_P), _I, ctypes.POINTER(_P), _I, _P,
                                   ctypes.c_int64, _P, _I, _P, _D, _D, _P, _P, _P, _P, _U64, _P]),
     ("edt_slerp_merge_list_speculative", _I, [ctypes.POINTER(_P), ctypes.POINTER(_P), _I, ctypes.POINTER(_P), _I,
-                                              _P, ctypes.c_int64, _P, _I, _P, _D, _D, _P, _P, _P, _P, _P, _U64, _P]),
+                                              _P, _P, ctypes.c_int64, _P, _I, _P, _D, _D, _P, _P, _P, _P, _P, _U64,
+                                              _P]),
+    ("edt_slerp_seg_table", _I, [ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_P), _I, _P, _I, _I, _I, _P]),
+    ("edt_slerp_stats_table", _I, [_P, _I, _P, ctypes.c_int64, _P, _P]),
+    ("edt_slerp_blend_table", _I, [_P, _I, _I, _P, ctypes.c_int64, _P, _P, _P]),
+    ("edt_slerp_merge_table", _I, [_P, _I, _I, _P, ctypes.c_int64, _P, _I, _P, _D, _D, _P, _P, _P, _P]),
+    ("edt_slerp_merge_table_speculative", _I, [_P, _I, _I, _P, ctypes.c_int64, _P, _I, _P, _D, _D, _P, _P, _P, _P,
+                                               _P]),
+    ("edt_slerp_blend_segments", _I, [_P, _P, _I, _P, _I, _P, ctypes.c_int64, _P, _P, _P]),
+    ("edt_slerp_refdot_table", _I, [_P, _I, _P, ctypes.c_int64, _P, _I, ctypes.c_uint32, _P, _I, _D, _P, _P, _U64,
+                                    _P]),
     ("edt_slerp_sums_doubles", _U64, [_I, ctypes.c_int64]),
     ("edt_slerp_refdot_workspace_bytes", _U64, [_I, ctypes.c_int64, ctypes.c_uint32, _I]),
     ("edt_slerp_refdot_flags", _I, [_P, _I, _D, _D, _P, _P]),
@@ -81,6 +90,7 @@ SIGNATURES = [
     ("edt_probe_stream", _I, [_P, _I, ctypes.POINTER(_P), _I, _I, _P, _U64, _P]),
     ("edt_last_error", ctypes.c_char_p, []),
     ("edt_version", ctypes.c_char_p, []),
+    ("edt_abi_version", _I, []),
     ("edt_outer_step_bytes_per_elem", _I, [_I, _I, _I, _I]),
 ]
 
@@ -117,6 +127,12 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
             f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
     lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    ver = getattr(lib, "edt_abi_version", None)
+    if ver is None:
+        raise EdtError(f"{path} predates the versioned ABI: rebuild it (this binding follows ABI {EDT_ABI_VERSION})")
+    ver.restype, ver.argtypes = _I, []
+    if ver() != EDT_ABI_VERSION:
+        raise EdtError(f"{path} implements ABI {ver()}, this binding follows ABI {EDT_ABI_VERSION}: rebuild it")
     for name, res, args in SIGNATURES:
         fn = getattr(lib, name)
         fn.restype = res

@@ -67,14 +67,6 @@ using edt::g_err;
 #ifndef EDT_NT_SLERP            // non-temporal loads of the SLERP parents (stats and blend passes)
 #define EDT_NT_SLERP 1
 #endif
-#ifndef EDT_SLERP_BPC           // workgroups per CU for the grid-stride SLERP passes (redo / member-major blends)
-#define EDT_SLERP_BPC 256
-#endif
-#ifndef EDT_SLERP_GRID          // 1: the SLERP blends run one 2,048-element tile per workgroup in address
-                                // order (32 workgroups per 64 Ki chunk); 0: grid-stride over chunks,
-                                // EDT_SLERP_BPC per CU
-#define EDT_SLERP_GRID 1
-#endif
 // 512-element tiles per wave in the read-only chunk-sum pass (4, 8 or 16; the sums' order is the
 // same for every value, edt_slerp.hip). 7B body, bf16, one box (profiles/r03_slerp_stats_tpw.jsonl):
 // 4.44 / 4.21 / 4.09 ms for 4 / 8 / 16 — a read-only stream wants many bytes in flight per wave
@@ -82,35 +74,12 @@ using edt::g_err;
 #ifndef EDT_SLERP_STATS_TPW
 #define EDT_SLERP_STATS_TPW 16
 #endif
-// Speculative population pass: 1 = the member-major Gram pass when the distinct parents fit one
-// tile (<= 8: each parent's registers feed every child, picked by a runtime index — a private array
-// in scratch); 0 = always the co-located per-child pass (block -> (unit, child), children of a unit
-// on one XCD, shared parents from L2). 8 x 7B bf16, lineage (profiles/r03_pop_probe*.json):
-// 42.4 ms co-located against 67.2 ms member-major (floor at 6 TB/s: 37.7 ms).
-#ifndef EDT_SLERP_POP_FUSED
-#define EDT_SLERP_POP_FUSED 0
-#endif
 // Speculative passes (pair and co-located population): 1 = the four waves' tile sums combined
 // through LDS into one level-2 row per workgroup (a quarter of the row bytes, one barrier); 0 = a
 // level-0 row per wave, no barrier. 7B lineage merge, one box, interleaved (profiles/
 // r03_spec_wg_rows.jsonl): 7.01-7.03 ms against 7.14-7.17, lerp 6.96.
 #ifndef EDT_SLERP_SPEC_WG_ROWS
 #define EDT_SLERP_SPEC_WG_ROWS 1
-#endif
-// Far-parent SLERP with the parents held on chip (edt_slerp_merge_hold): level-4 groups (8 Ki
-// elements, 128 VGPRs of bf16 pairs) a wave keeps in registers across its phase's coefficient
-// wait, and the phase size (whole segments, closed at >= this many chunks of the plan).
-#ifndef EDT_SLERP_HOLD_SLOTS
-#define EDT_SLERP_HOLD_SLOTS 2
-#endif
-#ifndef EDT_SLERP_HOLD_BPC      // workgroups per CU the hold kernel is compiled for (waves per SIMD)
-#define EDT_SLERP_HOLD_BPC 1
-#endif
-#ifndef EDT_SLERP_HOLD_UNIT     // tiles per load unit of the hold kernel's pipelined loops (4 or 8)
-#define EDT_SLERP_HOLD_UNIT 4
-#endif
-#ifndef EDT_SLERP_HOLD_PHASE
-#define EDT_SLERP_HOLD_PHASE 256
 #endif
 #ifndef EDT_SLERP_COEF_BLOCK    // 1: one workgroup per segment for the chunk-sum reduction (else one wave)
 #define EDT_SLERP_COEF_BLOCK 1
@@ -170,10 +139,6 @@ __device__ __forceinline__ uint64_t xcd_block(uint64_t b, uint64_t G) {
     }
 }
 
-constexpr uint64_t kSlerpMaxBlocks = EDT_SLERP_GRID ? kGridBlockCap : 256ull * EDT_SLERP_BPC;
-inline unsigned slerp_grid(int64_t nchunks) {
-    return (unsigned)((uint64_t)nchunks < kSlerpMaxBlocks ? (uint64_t)nchunks : kSlerpMaxBlocks);
-}
 // the passes that skip most chunks (the speculative redo blends) or hold several parents' tiles in
 // registers (the member-major blends) stay grid-stride over chunks, EDT_SLERP_SPEC_BPC per CU
 #ifndef EDT_SLERP_SPEC_BPC
@@ -183,25 +148,6 @@ inline unsigned slerp_spec_grid(int64_t nchunks) {
     const uint64_t cap = 256ull * EDT_SLERP_SPEC_BPC;
     return (unsigned)((uint64_t)nchunks < cap ? (uint64_t)nchunks : cap);
 }
-// blend passes: tile q of chunk c is workgroup c * kTilesPerChunk + q, so the grid walks the arena
-// in address order one kTile at a time (chunks longer than kTilesPerChunk tiles loop)
-constexpr int kTile = kBlock * kVec;                 // 2,048 elements
-#ifndef EDT_SLERP_TPC
-#define EDT_SLERP_TPC 32
-#endif
-constexpr int kTilesPerChunk = EDT_SLERP_TPC;        // the plans' default chunk: 64 Ki elements
-#ifndef EDT_SLERP_BLEND_TILE    // 1: the full SLERP blend on the speculative pass's one-shot unit grid
-#define EDT_SLERP_BLEND_TILE 1  // (slerp_blend_tile_kernel); 0: slerp_blend_kernel's tile grid
-#endif
-#ifndef EDT_SLERP_BLEND_REV     // 1: the tile grid walks the arena from its end (probe: does the blend
-#define EDT_SLERP_BLEND_REV 0   // re-read what the stats pass left in the Infinity Cache last?)
-#endif
-inline unsigned slerp_tile_grid(int64_t nchunks) {
-    if (!EDT_SLERP_GRID) return slerp_grid(nchunks);
-    const uint64_t g = (uint64_t)nchunks * kTilesPerChunk;    // past the cap, for_blend_ranges grid-strides
-    return (unsigned)(g < kGridBlockCap ? g : kGridBlockCap);
-}
-
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));

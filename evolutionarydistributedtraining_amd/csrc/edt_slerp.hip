@@ -3,6 +3,9 @@
 // and population forms, with their C ABI entries (include/edt_sync.h).
 #include "edt_common.h"
 
+#include <algorithm>
+#include <vector>
+
 namespace {
 
 // ---------------------------------------------------------------------------------------
@@ -420,29 +423,15 @@ __device__ __forceinline__ void slerp_coefficients(double s00, double s11, doubl
     coefficients_from_dot(dot, t, thr, c0, c1);
 }
 
-// The element ranges a blend workgroup owns, as body(start, end, segment). TILES: one kTile of its
-// chunk (tiles kTilesPerChunk apart for longer chunks; grid slerp_tile_grid) — the full blends.
-// Else whole chunks, grid-stride (grid slerp_spec_grid) — the speculative redo blends, where most
-// segments are skipped and a workgroup per tile would cost more to dispatch than it saves (7B
-// lineage merge: 3.45 M empty workgroups = +1.1 ms). Tiles assume the plans' 64 Ki chunks: shorter
-// chunks stay correct, with idle workgroups.
-template <bool TILES, typename F>
+// The element ranges a blend workgroup owns, as body(start, end, segment): whole chunks,
+// grid-stride (grid slerp_spec_grid) — the speculative redo blends and the member-major blends,
+// where most segments may be skipped and a workgroup per tile would cost more to dispatch than it
+// saves (7B lineage merge: 3.45 M empty workgroups = +1.1 ms). The full blends run on the unit
+// grid of slerp_blend_tile_kernel.
+template <typename F>
 __device__ __forceinline__ void for_blend_ranges(const uint64_t* chunks, int64_t nchunks, F&& body) {
-    if constexpr (TILES && EDT_SLERP_GRID) {
-        // one tile per workgroup; a grid capped at kGridBlockCap strides over the rest
-        const uint64_t total = (uint64_t)nchunks * kTilesPerChunk;
-        for (uint64_t b0 = blockIdx.x; b0 < total; b0 += gridDim.x) {
-            const uint64_t b = EDT_SLERP_BLEND_REV ? total - 1 - b0 : b0;
-            const int64_t c = (int64_t)(b / kTilesPerChunk);
-            const uint64_t start = chunks[3 * c], len = chunks[3 * c + 1], seg = chunks[3 * c + 2];
-            for (uint64_t off = (b % kTilesPerChunk) * kTile; off < len;
-                 off += (uint64_t)kTilesPerChunk * kTile)
-                body(start + off, start + (off + kTile < len ? off + kTile : len), seg);
-        }
-    } else {
-        for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x)
-            body(chunks[3 * c], chunks[3 * c] + chunks[3 * c + 1], chunks[3 * c + 2]);
-    }
+    for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x)
+        body(chunks[3 * c], chunks[3 * c] + chunks[3 * c + 1], chunks[3 * c + 2]);
 }
 
 // f(N, i) over [start, end): the 16-B-aligned body in 8-element vectors (workgroup-strided), then
@@ -548,24 +537,10 @@ int pair_sums(const void* v0, const void* v1, int in_dt, void* out, int out_dt, 
 // wave sums, then the waves in order). Every coefficient kernel uses this one order.
 constexpr int kCoefThreads = EDT_SLERP_COEF_BLOCK ? kBlock : 64;
 
-// Loads / stores that bypass the CU's L1 (global_load / global_store ... sc1): the in-launch hand-offs
-// between workgroups of slerp_hold_kernel (every byte handed over is stored and loaded this way).
-__device__ __forceinline__ double ld_agent(const double* p) {
-    return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_agent(const float* p) {
-    return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <typename V>
-__device__ __forceinline__ void st_agent(V* p, V v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <bool AGENT = false>
 __device__ __forceinline__ bool segment_sums(const double* tab, int stride, int q0, int q1, int q2, int c0,
                                              int c1, double (&out)[3]) {
     const int tid = EDT_SLERP_COEF_BLOCK ? (int)threadIdx.x : (int)(threadIdx.x & 63);
-    auto at = [&](uint64_t k) { return AGENT ? ld_agent(tab + k) : tab[k]; };
+    auto at = [&](uint64_t k) { return tab[k]; };
     double s0 = 0.0, s1 = 0.0, s2 = 0.0;
     for (int c = c0 + tid; c < c1; c += kCoefThreads) {
         s0 += at((uint64_t)c * stride + q0);
@@ -623,14 +598,14 @@ __global__ __launch_bounds__(kBlock) void slerp_coef_kernel(const double* partia
     }
 }
 
-template <int IDT, int ODT, bool NT = (EDT_NT_SLERP != 0 && IDT == EDT_BF16), bool TILES = true>
+template <int IDT, int ODT, bool NT = (EDT_NT_SLERP != 0 && IDT == EDT_BF16)>
 __global__ __launch_bounds__(kBlock) void slerp_blend_kernel(const void* v0, const void* v1, void* out,
                                                              const uint64_t* chunks, int64_t nchunks,
                                                              const float* coef, const uint64_t* seg_ptrs,
                                                              const int32_t* redo = nullptr,
                                                              const int32_t* any_redo = nullptr) {
     if (any_redo && *any_redo == 0) return;       // no segment to blend again: the whole grid exits
-    for_blend_ranges<TILES>(chunks, nchunks, [&](uint64_t start, uint64_t end, uint64_t seg) {
+    for_blend_ranges(chunks, nchunks, [&](uint64_t start, uint64_t end, uint64_t seg) {
         if (redo && !redo[seg]) return;           // speculative lerp output already final
         const void* a = v0;
         const void* b = v1;
@@ -726,13 +701,6 @@ __device__ __forceinline__ void gram_fma(const X (&x)[M], double (&g)[M * (M + 1
     }
 }
 
-// The lerp-branch outputs of the children from the parents' registers (PopLerp below).
-struct PopLerp {
-    void* out[16];
-    int32_t a[16], b[16];      // compact member indices of the parents
-    int n;
-};
-
 template <int M, int N>
 __device__ __forceinline__ void pick(const float (&x)[M][N], int idx, float (&y)[N]) {
 #pragma unroll
@@ -743,38 +711,13 @@ __device__ __forceinline__ void pick(const float (&x)[M][N], int idx, float (&y)
         }
 }
 
-template <int M, typename X>
-__device__ __forceinline__ X pick_one(const X (&x)[M], int idx) {
-    X y = x[0];
-#pragma unroll
-    for (int m = 1; m < M; ++m)
-        if (m == idx) y = x[m];          // idx is uniform across the workgroup: no divergence
-    return y;
-}
-
-template <int ODT, int M, int N, typename X>
-__device__ __forceinline__ void emit_children(const PopLerp& po, const X (&x)[M], uint64_t i, float l0, float l1) {
-    for (int q = 0; q < po.n; ++q) {
-        const X u = pick_one<M>(x, po.a[q]), v = pick_one<M>(x, po.b[q]);
-        float o[N];
-#pragma unroll
-        for (int j = 0; j < N; ++j) o[j] = l0 * u[j] + l1 * v[j];
-        st<ODT, N>(po.out[q], i, o);
-    }
-}
-
 // Gram rows (level 4), one workgroup per unit of 16 tiles in address order: wave w takes tiles
 // 16 g + 4 w .. + 3 one after the other (one vector per member per lane: M loads in flight), each
 // tile's sums butterflied as pair_tile's and parked in LDS; after the barrier wave 0's lanes
 // (one per sum) combine the 16 tile sums as the tree does and store the unit's row (unit_slot).
-// EMIT (the member-major speculative pass, edt_slerp_population_speculative): each distinct
-// parent's vector is loaded ONCE into registers, its Gram sums accumulated and every child's
-// lerp-branch output written from the same registers — a shared parent crosses HBM once for all
-// its children.
-template <int IDT, int M, bool EMIT, int ODT>
-__global__ __launch_bounds__(kBlock) void slerp_gram_kernel(Members mem, PopLerp po, const uint64_t* chunks,
-                                                            int64_t nchunks, const double* tvals, double* rows,
-                                                            uint64_t u0) {
+template <int IDT, int M>
+__global__ __launch_bounds__(kBlock) void slerp_gram_kernel(Members mem, const uint64_t* chunks, int64_t nchunks,
+                                                            double* rows, uint64_t u0) {
     constexpr int NT = M * (M + 1) / 2;
     constexpr int upc = kTileSlots / 16;
     __shared__ double ts[16][NT];
@@ -786,12 +729,6 @@ __global__ __launch_bounds__(kBlock) void slerp_gram_kernel(Members mem, PopLerp
         const uint64_t c = u / upc;
         const int g = (int)(u % upc);
         const uint64_t start = chunks[3 * c], len = chunks[3 * c + 1];
-        float l0 = 0.f, l1 = 0.f;
-        if constexpr (EMIT) {
-            const uint64_t seg = chunks[3 * c + 2];
-            l0 = (float)(1.0 - tvals[seg]);
-            l1 = (float)tvals[seg];
-        }
 #pragma unroll(M <= 2 ? 4 : 1)
         for (int k = 0; k < 4; ++k) {
             const int j = 16 * g + 4 * wave + k;
@@ -804,14 +741,12 @@ __global__ __launch_bounds__(kBlock) void slerp_gram_kernel(Members mem, PopLerp
 #pragma unroll
                     for (int m = 0; m < M; ++m) x[m] = ld_raw<IDT, false>(mem.p[m], i);   // default policy
                     gram_fma<M, kVec>(x, gs);
-                    if constexpr (EMIT) emit_children<ODT, M, kVec>(po, x, i, l0, l1);
                 },
                 [&](uint64_t i) {
                     Raw1 x[M];
 #pragma unroll
                     for (int m = 0; m < M; ++m) ld<IDT, 1>(mem.p[m], i, x[m].v);
                     gram_fma<M, 1>(x, gs);
-                    if constexpr (EMIT) emit_children<ODT, M, 1>(po, x, i, l0, l1);
                 });
             double r[Red<NT>::N2];
             tile_reduce<NT>(gs, r);
@@ -829,36 +764,26 @@ __global__ __launch_bounds__(kBlock) void slerp_gram_kernel(Members mem, PopLerp
 }
 
 // host: the Gram sums of D compact members into gram (chunk rows [nchunks][NT], then the row
-// scratch); po != null: the member-major speculative pass (children's lerp-branch outputs too)
-inline int gram_sums(const Members& mem, int D, const PopLerp* po, int in_dt, int out_dt, const uint64_t* chunk_desc,
-                     int64_t nchunks, const double* t, double* gram, hipStream_t s) {
+// scratch)
+inline int gram_sums(const Members& mem, int D, int in_dt, const uint64_t* chunk_desc, int64_t nchunks, double* gram,
+                     hipStream_t s) {
     const int NT = D * (D + 1) / 2;
     double* rows = gram + (uint64_t)nchunks * NT;
     constexpr int upc = kTileSlots / 16;
     const uint64_t units = (uint64_t)nchunks * upc;
-    PopLerp none;
-    memset(&none, 0, sizeof(none));
-    const PopLerp& P = po ? *po : none;
     for (uint64_t u0 = 0; u0 < units; u0 += kUnitGridCap) {
     const unsigned g = unit_grid(units - u0);
-#define EDT_GS(I, M, E, O) slerp_gram_kernel<I, M, E, O><<<g, kBlock, 0, s>>>(mem, P, chunk_desc, nchunks, t, rows, u0)
-#define EDT_GM(M)                                                                      \
-    case M:                                                                            \
-        if (!po) {                                                                     \
-            if (in_dt == EDT_F32) EDT_GS(EDT_F32, M, false, EDT_F32);                  \
-            else EDT_GS(EDT_BF16, M, false, EDT_F32);                                  \
-        } else if (in_dt == EDT_F32 && out_dt == EDT_F32) EDT_GS(EDT_F32, M, true, EDT_F32);   \
-        else if (in_dt == EDT_F32) EDT_GS(EDT_F32, M, true, EDT_BF16);                 \
-        else if (out_dt == EDT_F32) EDT_GS(EDT_BF16, M, true, EDT_F32);                \
-        else EDT_GS(EDT_BF16, M, true, EDT_BF16);                                      \
+#define EDT_GM(M)                                                                                                   \
+    case M:                                                                                                         \
+        if (in_dt == EDT_F32) slerp_gram_kernel<EDT_F32, M><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0); \
+        else slerp_gram_kernel<EDT_BF16, M><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0);              \
         break;
     switch (D) {
         EDT_GM(1) EDT_GM(2) EDT_GM(3) EDT_GM(4) EDT_GM(5) EDT_GM(6) EDT_GM(7) EDT_GM(8)
         default: return fail(EDT_ERR_ARG, "Gram pass over %d members", D);
     }
 #undef EDT_GM
-#undef EDT_GS
-    int rc = check_launch(po ? "slerp_gram_kernel (speculative)" : "slerp_gram_kernel");
+    int rc = check_launch("slerp_gram_kernel");
     if (rc) return rc;
     }
     return launch_tree_reduce(rows, NT, kGramRows, upc, 1, nchunks, gram, s);
@@ -1012,10 +937,10 @@ __device__ __forceinline__ void blend_mm_elems(const Members& mem, const PopBlen
     }
 }
 
-template <int IDT, int ODT, int M, bool TILES>
+template <int IDT, int ODT, int M>
 __global__ __launch_bounds__(kBlock) void slerp_blend_mm_kernel(Members mem, PopBlend pb, const uint64_t* chunks,
                                                                 int64_t nchunks) {
-    for_blend_ranges<TILES>(chunks, nchunks, [&](uint64_t start, uint64_t end, uint64_t seg) {
+    for_blend_ranges(chunks, nchunks, [&](uint64_t start, uint64_t end, uint64_t seg) {
         uint32_t need = 0;                   // children whose output this segment still needs
         for (int q = 0; q < pb.n; ++q)
             if (!pb.redo[q] || pb.redo[q][seg]) need |= 1u << q;
@@ -1036,13 +961,13 @@ inline int launch_blend_mm(const Members& mem, int D, const PopBlend& pb, int in
 #define EDT_BMM(M)                                                                                            \
     case M:                                                                                                   \
         if (in_dt == EDT_F32 && out_dt == EDT_F32)                                                            \
-            slerp_blend_mm_kernel<EDT_F32, EDT_F32, M, false><<<g, kBlock, 0, s>>>(mem, pb, chunk_desc, nchunks);   \
+            slerp_blend_mm_kernel<EDT_F32, EDT_F32, M><<<g, kBlock, 0, s>>>(mem, pb, chunk_desc, nchunks);   \
         else if (in_dt == EDT_F32)                                                                            \
-            slerp_blend_mm_kernel<EDT_F32, EDT_BF16, M, false><<<g, kBlock, 0, s>>>(mem, pb, chunk_desc, nchunks);  \
+            slerp_blend_mm_kernel<EDT_F32, EDT_BF16, M><<<g, kBlock, 0, s>>>(mem, pb, chunk_desc, nchunks);  \
         else if (out_dt == EDT_F32)                                                                           \
-            slerp_blend_mm_kernel<EDT_BF16, EDT_F32, M, false><<<g, kBlock, 0, s>>>(mem, pb, chunk_desc, nchunks);  \
+            slerp_blend_mm_kernel<EDT_BF16, EDT_F32, M><<<g, kBlock, 0, s>>>(mem, pb, chunk_desc, nchunks);  \
         else                                                                                                  \
-            slerp_blend_mm_kernel<EDT_BF16, EDT_BF16, M, false><<<g, kBlock, 0, s>>>(mem, pb, chunk_desc, nchunks); \
+            slerp_blend_mm_kernel<EDT_BF16, EDT_BF16, M><<<g, kBlock, 0, s>>>(mem, pb, chunk_desc, nchunks); \
         break;
     switch (D) {
         EDT_BMM(1) EDT_BMM(2) EDT_BMM(3) EDT_BMM(4) EDT_BMM(5) EDT_BMM(6) EDT_BMM(7) EDT_BMM(8)
@@ -1067,350 +992,23 @@ int slerp_blend_impl(const void* v0, const void* v1, int in_dt, void* out, int o
     if (nchunks == 0) return EDT_OK;
     if (!chunk_desc || !coef) return fail(EDT_ERR_ARG, "null buffer");
     hipStream_t s = (hipStream_t)stream;
-    if (EDT_SLERP_BLEND_TILE) {
-        constexpr bool kNt = EDT_NT_SLERP != 0;
-        const uint64_t units = (uint64_t)nchunks * (kTileSlots / kWavesPerBlock);
-        for (uint64_t u0 = 0; u0 < units; u0 += kUnitGridCap) {
-            const unsigned g = unit_grid(units - u0);
+    constexpr bool kNt = EDT_NT_SLERP != 0;
+    const uint64_t units = (uint64_t)nchunks * (kTileSlots / kWavesPerBlock);
+    for (uint64_t u0 = 0; u0 < units; u0 += kUnitGridCap) {
+        const unsigned g = unit_grid(units - u0);
 #define EDT_BT(I, O, N) slerp_blend_tile_kernel<I, O, N><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, seg_ptrs, u0)
-            if (in_dt == EDT_F32 && out_dt == EDT_F32) EDT_BT(EDT_F32, EDT_F32, false);
-            else if (in_dt == EDT_F32) EDT_BT(EDT_F32, EDT_BF16, false);
-            else if (out_dt == EDT_F32 && nt) EDT_BT(EDT_BF16, EDT_F32, kNt);
-            else if (out_dt == EDT_F32) EDT_BT(EDT_BF16, EDT_F32, false);
-            else if (nt) EDT_BT(EDT_BF16, EDT_BF16, kNt);
-            else EDT_BT(EDT_BF16, EDT_BF16, false);
+        if (in_dt == EDT_F32 && out_dt == EDT_F32) EDT_BT(EDT_F32, EDT_F32, false);
+        else if (in_dt == EDT_F32) EDT_BT(EDT_F32, EDT_BF16, false);
+        else if (out_dt == EDT_F32 && nt) EDT_BT(EDT_BF16, EDT_F32, kNt);
+        else if (out_dt == EDT_F32) EDT_BT(EDT_BF16, EDT_F32, false);
+        else if (nt) EDT_BT(EDT_BF16, EDT_BF16, kNt);
+        else EDT_BT(EDT_BF16, EDT_BF16, false);
 #undef EDT_BT
-            int rc = check_launch("slerp_blend_tile_kernel");
-            if (rc) return rc;
-        }
-        return EDT_OK;
+        int rc = check_launch("slerp_blend_tile_kernel");
+        if (rc) return rc;
     }
-    const unsigned g = slerp_tile_grid(nchunks);
-    if (in_dt == EDT_F32 && out_dt == EDT_F32)
-        slerp_blend_kernel<EDT_F32, EDT_F32><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, seg_ptrs);
-    else if (in_dt == EDT_F32)
-        slerp_blend_kernel<EDT_F32, EDT_BF16><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, seg_ptrs);
-    else if (out_dt == EDT_F32 && nt)
-        slerp_blend_kernel<EDT_BF16, EDT_F32><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, seg_ptrs);
-    else if (out_dt == EDT_F32)
-        slerp_blend_kernel<EDT_BF16, EDT_F32, false><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, seg_ptrs);
-    else if (nt)
-        slerp_blend_kernel<EDT_BF16, EDT_BF16><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, seg_ptrs);
-    else
-        slerp_blend_kernel<EDT_BF16, EDT_BF16, false><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, seg_ptrs);
-    return check_launch("slerp_blend_kernel");
-}
-
-// ---------------------------------------------------------------------------------------
-// Far-parent SLERP with part of the parents held on chip (edt_slerp_merge_hold). The two-pass
-// form moves 10 B per bf16 element (stats read 4, blend read 4 + write 2): every parent byte
-// crosses HBM twice because a segment's coefficients need its whole dot before its first output.
-// Here one persistent launch (one workgroup per CU, all resident: cooperative launch) walks the
-// arena in PHASES — runs of whole segments of >= kHoldPhaseChunks chunks — and per phase:
-//   1. stats: each wave takes the phase's level-4 groups (16 tiles of a chunk, 8 Ki elements)
-//      g = w, w + W, ... (address order across the chip), forms each group's canonical level-4
-//      row (tiles_sums: bit-identical to the stats pass) and KEEPS its last kHoldSlots groups'
-//      vectors in registers;
-//   2. arrival: rows stored write-through (sc1), one agent-scope ticket per workgroup; the last
-//      arriver finishes the chunk trees and segment sums in the coefficient kernel's order
-//      (segment_sums) and publishes the coefficients and a ready word (write-through);
-//   3. the PREVIOUS phase's streamed groups are read again and blended (this hides step 2);
-//   4. wait for the ready word, blend the held groups from registers (no second read).
-// A group held moves 6 B per element instead of 10; with 2 slots a wave holds 16 Ki elements,
-// the chip 16.8 M. Every sum, coefficient and output is bit-identical to edt_slerp_merge. Every
-// wait is bounded (kHoldTimeout): on expiry the error word is set and every wave leaves.
-// Measured (profiles/r03_slerp_hold_probe.json, 7B body, far parents): 16.9 ms against the
-// two-pass form's 11.3 ms; with nothing held (EDT_SLERP_HOLD_SLOTS=0: the two-pass bytes in this
-// launch) 15.6 ms, at 2 waves per SIMD the same; phases of 64 / 1024 chunks 17.3 / 16.3 ms. A
-// persistent grid of 1-2 waves per SIMD keeps 64-128 KiB of loads in flight per CU against the
-// one-shot grids' several hundred, and the registers that would hold parents are the ones more
-// loads in flight need: the re-read the form saves costs less than the parallelism it gives up.
-// Kept opt-in for A/B; edt_slerp_merge stays the far-parent form.
-
-constexpr int kHoldSlots = EDT_SLERP_HOLD_SLOTS;        // level-4 groups a wave keeps in registers
-constexpr int kGroupsPerChunk = kTileSlots / 16;        // 8
-constexpr int kHoldPhaseChunks = EDT_SLERP_HOLD_PHASE;  // a phase closes at >= this many chunks
-constexpr uint64_t kHoldTimeout = 200000000ull;         // wall_clock64 ticks (100 MHz): 2 s per wait
-
-// control words (int32) after the level-4 rows: [0] phases, [1] error, [2, 4) pad, then
-// cnt[nseg + 1] tickets, ready[nseg + 1], phase first chunk [nseg + 1], phase first segment [nseg + 1]
-inline uint64_t hold_ctl_ints(int nseg) { return 4 + 4ull * (uint64_t)(nseg + 1); }
-
-__global__ __launch_bounds__(kBlock) void slerp_hold_prep_kernel(const int32_t* seg_first, int nseg, int32_t* ctl) {
-    int32_t* cnt = ctl + 4;
-    int32_t* pfc = cnt + 2 * (nseg + 1);
-    int32_t* pfs = pfc + (nseg + 1);
-    for (int i = threadIdx.x; i < 2 * (nseg + 1); i += blockDim.x) cnt[i] = 0;     // tickets, ready words
-    if (threadIdx.x == 0) {
-        ctl[1] = 0;
-        int np = 0, s = 0;
-        while (s < nseg) {
-            const int c0 = seg_first[s];
-            pfc[np] = c0;
-            pfs[np] = s;
-            do { ++s; } while (s < nseg && seg_first[s] - c0 < kHoldPhaseChunks);
-            ++np;
-        }
-        pfc[np] = nseg > 0 ? seg_first[nseg] : 0;
-        pfs[np] = nseg;
-        ctl[0] = np;
-    }
-}
-
-// A group is handled in units of kHoldUnit tiles (32 VGPRs of bf16 pairs per 4 tiles): unit u of
-// group m is tiles_load's / tiles_sums' index (16 / U) m + u, and the level-4 row is the perfect
-// tree over the units' rows — ((u0 + u1) + (u2 + u3)) for U = 4, u0 + u1 for U = 8 — so it equals
-// the stats pass's row bit for bit.
-constexpr int kHoldUnit = EDT_SLERP_HOLD_UNIT;
-constexpr int kUnitsPerGroup = 16 / kHoldUnit;
-static_assert(kHoldUnit == 4 || kHoldUnit == 8, "hold unit: 4 or 8 tiles");
-using HoldU = Raw8<EDT_BF16>[kHoldUnit];
-
-// Blend unit mu of chunk [start, start + len) from the vectors in x / y (tile 0's head / tail
-// elements are read again: < 16 per chunk).
-template <int ODT>
-__device__ __forceinline__ void hold_blend_unit(const void* v0, const void* v1, void* out, uint64_t start,
-                                                uint64_t len, int mu, const HoldU& x, const HoldU& y, float c0,
-                                                float c1) {
-    const uint64_t a = (start + kVec - 1) / kVec * kVec, b = (start + len) / kVec * kVec;
-    const uint64_t i0 = a + (uint64_t)(kHoldUnit * mu) * kTileElems + (uint64_t)(threadIdx.x & 63) * kVec;
-#pragma unroll
-    for (int k = 0; k < kHoldUnit; ++k) {
-        const uint64_t i = i0 + (uint64_t)k * kTileElems;
-        if (a < b && i < b) {
-            float r[kVec];
-#pragma unroll
-            for (int e = 0; e < kVec; ++e) r[e] = c0 * x[k][e] + c1 * y[k][e];
-            st<ODT, kVec>(out, i, r);
-        }
-    }
-    if (mu == 0)
-        tile0_edge(start, len, [&](uint64_t e) { lerp_elems<EDT_BF16, ODT, EDT_F32, 1>(v0, v1, out, e, c0, c1); });
-}
-
-// Unit mu's row (lanes 0 .. 2 keep sum q in acc), folded into the level-4 row; the group's last unit
-// stores it write-through.
-__device__ __forceinline__ void hold_sums_unit(const void* v0, const void* v1, uint64_t start, uint64_t len, int mu,
-                                               const HoldU& x, const HoldU& y, double (&acc)[2], double* row) {
-    tiles_sums<EDT_BF16, kHoldUnit>(v0, v1, start, len, mu, x, y, [&](int q, double v) {
-        const int r = mu % kUnitsPerGroup;
-        if constexpr (kUnitsPerGroup == 2) {
-            if (r == 0) acc[0] = v;
-            else st_agent(row + q, acc[0] + v);
-        } else {
-            if (r == 0) acc[0] = v;
-            else if (r == 1) acc[0] = acc[0] + v;
-            else if (r == 2) acc[1] = v;
-            else st_agent(row + q, acc[0] + (acc[1] + v));
-        }
-    });
-}
-
-// The last arriver of a phase: chunk trees from the level-4 rows, then per segment the coefficient
-// kernel's reduction and coefficients; then the ready word. All loads / stores of handed-over bytes
-// are agent-scope (sc1).
-__device__ __forceinline__ void hold_reduce(int c0, int c1, int s0, int s1, const double* rows, double* partial,
-                                            const int32_t* seg_first, const double* tvals, float thr, float eps,
-                                            float* coef, float* dot_out, int32_t* ready_word) {
-    for (int c = c0 + (int)threadIdx.x; c < c1; c += kBlock) {
-        const double* r = rows + (uint64_t)c * (kGroupsPerChunk * 3);
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            double v[kGroupsPerChunk];
-#pragma unroll
-            for (int k = 0; k < kGroupsPerChunk; ++k) v[k] = ld_agent(r + 3 * k + q);
-            st_agent(partial + 3 * (uint64_t)c + q, ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7])));
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int s = s0; s < s1; ++s) {
-        double sums[3];
-        if (segment_sums<true>(partial, 3, 0, 1, 2, seg_first[s], seg_first[s + 1], sums)) {
-            float cc0, cc1, dot;
-            slerp_coefficients(sums[0], sums[1], sums[2], tvals[s], thr, eps, cc0, cc1, dot);
-            st_agent(coef + 2 * s, cc0);
-            st_agent(coef + 2 * s + 1, cc1);
-            if (dot_out) dot_out[s] = dot;
-        }
-        __syncthreads();                              // segment_sums' LDS words serve the next segment
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) st_agent(ready_word, 1);
-}
-
-template <int ODT>
-__global__ __launch_bounds__(kBlock, EDT_SLERP_HOLD_BPC) void slerp_hold_kernel(
-    const void* v0, const void* v1, void* out, const uint64_t* __restrict__ chunks,
-    const int32_t* __restrict__ seg_first, int nseg, const double* __restrict__ tvals, float thr, float eps,
-    double* partial, double* rows, float* coef, float* dot_out, int32_t* ctl) {
-    constexpr bool NT = EDT_NT_SLERP != 0;
-    constexpr int H = kHoldSlots, HA = H > 0 ? H : 1, UPG = kUnitsPerGroup;
-    const int wave = threadIdx.x >> 6;
-    const int W = (int)gridDim.x * kWavesPerBlock;
-    const int w = (int)blockIdx.x * kWavesPerBlock + wave;
-    int32_t* cnt = ctl + 4;
-    int32_t* ready = cnt + (nseg + 1);
-    const int32_t* pfc = ready + (nseg + 1);
-    const int32_t* pfs = pfc + (nseg + 1);
-    const int nphase = ctl[0];
-    __shared__ int32_t s_word;
-    // unit j of this wave's sequence in the phase starting at chunk cb: group w + (j / UPG) W, unit j % UPG
-    auto unit_at = [&](int cb, int j, int& c, int& mu) {
-        const int g = w + (j / UPG) * W;
-        c = cb + g / kGroupsPerChunk;
-        mu = UPG * (g % kGroupsPerChunk) + j % UPG;
-    };
-    auto unit_load = [&](int cb, int j, HoldU& x, HoldU& y) {
-        int c, mu;
-        unit_at(cb, j, c, mu);
-        tiles_load<EDT_BF16, NT, kHoldUnit>(v0, v1, chunks[3 * (uint64_t)c], chunks[3 * (uint64_t)c + 1], mu, x, y);
-    };
-    auto unit_sums = [&](int cb, int j, const HoldU& x, const HoldU& y, double (&acc)[2]) {
-        int c, mu;
-        unit_at(cb, j, c, mu);
-        hold_sums_unit(v0, v1, chunks[3 * (uint64_t)c], chunks[3 * (uint64_t)c + 1], mu, x, y, acc,
-                       rows + ((uint64_t)c * kGroupsPerChunk + (uint64_t)(mu / UPG)) * 3);
-    };
-    auto unit_blend = [&](int cb, int j, const HoldU& x, const HoldU& y) {
-        int c, mu;
-        unit_at(cb, j, c, mu);
-        const uint64_t seg = chunks[3 * (uint64_t)c + 2];
-        hold_blend_unit<ODT>(v0, v1, out, chunks[3 * (uint64_t)c], chunks[3 * (uint64_t)c + 1], mu, x, y,
-                             ld_agent(coef + 2 * seg), ld_agent(coef + 2 * seg + 1));
-    };
-    Raw8<EDT_BF16> hx[HA][UPG][kHoldUnit], hy[HA][UPG][kHoldUnit];
-    int pc0 = 0, pnw = 0;                             // the previous phase: first chunk, this wave's groups
-    for (int p = 0; p <= nphase; ++p) {
-        int c0 = 0, nw = 0;
-        if (p < nphase) {
-            c0 = pfc[p];
-            const int G = (pfc[p + 1] - c0) * kGroupsPerChunk;
-            nw = w < G ? (G - 1 - w) / W + 1 : 0;
-            {   // streamed groups: sums now, read again in step 3; unit j + 1 loads while unit j is summed
-                const int nu = UPG * (nw - H);
-                HoldU xa, ya, xb, yb;
-                double acc[2] = {0.0, 0.0};
-                if (nu > 0) unit_load(c0, 0, xa, ya);
-                for (int j = 0; j < nu; j += 2) {
-                    unit_load(c0, j + 1, xb, yb);
-                    unit_sums(c0, j, xa, ya, acc);
-                    if (j + 2 < nu) unit_load(c0, j + 2, xa, ya);
-                    unit_sums(c0, j + 1, xb, yb, acc);
-                }
-            }
-            if constexpr (H > 0) {
-                const int j0 = UPG * (nw - H);        // held groups: every slot loaded (empty: zeros)
-#pragma unroll
-                for (int s = 0; s < H; ++s) {
-#pragma unroll
-                    for (int u = 0; u < UPG; ++u) {
-                        const int j = j0 + UPG * s + u;
-                        uint64_t st0 = 0, ln = 0;
-                        int mu = 0;
-                        if (j >= 0) {
-                            int c;
-                            unit_at(c0, j, c, mu);
-                            st0 = chunks[3 * (uint64_t)c];
-                            ln = chunks[3 * (uint64_t)c + 1];
-                        }
-                        tiles_load<EDT_BF16, NT, kHoldUnit, true>(v0, v1, st0, ln, mu, hx[s][u], hy[s][u]);
-                    }
-                }
-#pragma unroll
-                for (int s = 0; s < H; ++s) {
-                    double acc[2] = {0.0, 0.0};
-#pragma unroll
-                    for (int u = 0; u < UPG; ++u)
-                        if (j0 + UPG * s >= 0) unit_sums(c0, j0 + UPG * s + u, hx[s][u], hy[s][u], acc);
-                }
-            }
-            // arrival: every wave's row stores drained, then one ticket per workgroup
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                const int t = __hip_atomic_fetch_add(cnt + p, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                s_word = t == (int)gridDim.x - 1;
-            }
-            __syncthreads();
-            const bool last = s_word != 0;
-            __syncthreads();
-            if (last)
-                hold_reduce(c0, pfc[p + 1], pfs[p], pfs[p + 1], rows, partial, seg_first, tvals, thr, eps, coef,
-                            dot_out, ready + p);
-        }
-        {   // the previous phase's streamed groups, read again and blended (pipelined as above)
-            const int nu = UPG * (pnw - H);
-            HoldU xa, ya, xb, yb;
-            if (nu > 0) unit_load(pc0, 0, xa, ya);
-            for (int j = 0; j < nu; j += 2) {
-                unit_load(pc0, j + 1, xb, yb);
-                unit_blend(pc0, j, xa, ya);
-                if (j + 2 < nu) unit_load(pc0, j + 2, xa, ya);
-                unit_blend(pc0, j + 1, xb, yb);
-            }
-        }
-        if (p < nphase) {
-            if (threadIdx.x == 0) {                   // bounded wait for this phase's coefficients
-                const uint64_t t0 = wall_clock64();
-                int ok = 1;
-                while (__hip_atomic_load(ready + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-                    if (__hip_atomic_load(ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
-                        wall_clock64() - t0 > kHoldTimeout) {
-                        ok = 0;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(8);
-                }
-                if (!ok) st_agent(ctl + 1, 1);
-                s_word = ok;
-            }
-            __syncthreads();
-            if (!s_word) return;                      // the whole workgroup leaves together
-            if constexpr (H > 0) {
-                const int j0 = UPG * (nw - H);
-#pragma unroll
-                for (int s = 0; s < H; ++s)
-#pragma unroll
-                    for (int u = 0; u < UPG; ++u)
-                        if (j0 + UPG * s >= 0) unit_blend(c0, j0 + UPG * s + u, hx[s][u], hy[s][u]);
-            }
-        }
-        pc0 = c0;
-        pnw = nw;
-    }
-}
-
-// host: the launch (bf16 parents, flat arenas); the workspace is edt_slerp_merge's
-int slerp_hold_impl(const void* v0, const void* v1, void* out, int out_dt, const uint64_t* chunk_desc, int64_t nchunks,
-                    const int32_t* seg_first, int nseg, const double* t, double thr, double eps, double* partial,
-                    float* coef, float* dot_out, hipStream_t s) {
-    const uint64_t avail = (edt_slerp_sums_doubles(3, nchunks) - 27ull * (uint64_t)nchunks) * 2;   // ints
-    if (hold_ctl_ints(nseg) > avail) return fail(EDT_ERR_ARG, "hold form: too many segments for the workspace");
-    if (nchunks > (int64_t)INT32_MAX / (kGroupsPerChunk * 2)) return fail(EDT_ERR_ARG, "hold form: too many chunks");
-    int dev = 0, cus = 0, per = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        return fail(EDT_ERR_LAUNCH, "hold form: device query failed");
-    const void* kern = out_dt == EDT_F32 ? reinterpret_cast<const void*>(&slerp_hold_kernel<EDT_F32>)
-                                         : reinterpret_cast<const void*>(&slerp_hold_kernel<EDT_BF16>);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, kBlock, 0) != hipSuccess || per < 1)
-        return fail(EDT_ERR_LAUNCH, "hold form: occupancy query failed");
-    double* rows = partial + 3 * (uint64_t)nchunks;
-    int32_t* ctl = reinterpret_cast<int32_t*>(partial + 27 * (uint64_t)nchunks);
-    slerp_hold_prep_kernel<<<1, kBlock, 0, s>>>(seg_first, nseg, ctl);
-    int rc = check_launch("slerp_hold_prep_kernel");
-    if (rc) return rc;
-    float fthr = (float)thr, feps = (float)eps;
-    void* args[] = {(void*)&v0, (void*)&v1, (void*)&out, (void*)&chunk_desc, (void*)&seg_first, (void*)&nseg,
-                    (void*)&t, (void*)&fthr, (void*)&feps, (void*)&partial, (void*)&rows, (void*)&coef,
-                    (void*)&dot_out, (void*)&ctl};
-    const hipError_t e = hipLaunchCooperativeKernel(kern, dim3((unsigned)(cus * per)), dim3(kBlock), args, 0, s);
-    if (e != hipSuccess) return fail(EDT_ERR_LAUNCH, "slerp_hold_kernel: launch failed: %s", hipGetErrorString(e));
     return EDT_OK;
 }
-
 
 // ---------------------------------------------------------------------------------------
 // Reference-dot mode (opt-in): the reference's own fp32 dot of EDT_RL/crossover.py:20-29 restated
@@ -1820,34 +1418,6 @@ int edt_slerp_merge(const void* v0, const void* v1, int in_dt, void* out, int ou
     return edt_slerp_blend(v0, v1, in_dt, out, out_dt, chunk_desc, nchunks, coef, stream);
 }
 
-int edt_slerp_merge_hold(const void* v0, const void* v1, int in_dt, void* out, int out_dt,
-                         const uint64_t* chunk_desc, int64_t nchunks, const int32_t* seg_first_chunk, int nseg,
-                         const double* t, double dot_threshold, double eps, double* partial, float* coef,
-                         float* dot_out, void* stream) {
-    g_err[0] = 0;
-    if ((in_dt | out_dt) & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
-    if (in_dt != EDT_BF16) return fail(EDT_ERR_ARG, "hold form: bf16 parents only (edt_slerp_merge takes fp32)");
-    if (nchunks < 0 || nseg < 0) return fail(EDT_ERR_ARG, "negative count");
-    if (nseg == 0) return EDT_OK;
-    if (!seg_first_chunk || !t || !partial || !coef || (nchunks > 0 && (!v0 || !v1 || !out || !chunk_desc)))
-        return fail(EDT_ERR_ARG, "null buffer");
-    if (nchunks > 0 && (!aligned16(v0) || !aligned16(v1) || !aligned16(out)))
-        return fail(EDT_ERR_ARG, "slerp buffers must be 16-byte aligned");
-    return slerp_hold_impl(v0, v1, out, out_dt, chunk_desc, nchunks, seg_first_chunk, nseg, t, dot_threshold, eps,
-                           partial, coef, dot_out, (hipStream_t)stream);
-}
-
-int edt_slerp_hold_status(const double* partial, int64_t nchunks, void* stream) {
-    g_err[0] = 0;
-    if (!partial || nchunks < 0) return fail(EDT_ERR_ARG, "bad workspace");
-    int32_t err = 0;
-    const int32_t* w = reinterpret_cast<const int32_t*>(partial + 27 * (uint64_t)nchunks) + 1;
-    if (hipMemcpyAsync(&err, w, sizeof(err), hipMemcpyDeviceToHost, (hipStream_t)stream) != hipSuccess ||
-        hipStreamSynchronize((hipStream_t)stream) != hipSuccess)
-        return fail(EDT_ERR_LAUNCH, "edt_slerp_hold_status: copy failed");
-    return err ? 1 : 0;
-}
-
 uint64_t edt_slerp_sums_doubles(int width, int64_t nchunks) {
     // the chunk rows + the largest row scratch a pass writes for this width: level-0 rows (one per
     // tile) for the pair passes (width 3), level-4 rows for the Gram passes
@@ -1859,10 +1429,8 @@ uint64_t edt_slerp_sums_doubles(int width, int64_t nchunks) {
 
 uint64_t edt_slerp_population_speculative_doubles(int npairs, int64_t nchunks) {
     if (npairs < 0 || nchunks < 0) return 0;
-    // co-located per-child form: each child's chunk rows + level-0 rows; member-major: <= 36 Gram sums
-    const uint64_t pair = 3ull * (uint64_t)npairs * (1ull + kPairRows);
-    const uint64_t gram = 36ull * (1ull + kGramRows);                    // 36: 8 x 9 / 2
-    return (uint64_t)nchunks * (pair > gram ? pair : gram) + 1;           // + the any-redo word
+    // each child's chunk rows + its row scratch (level-0 rows), + the any-redo word
+    return (uint64_t)nchunks * 3ull * (uint64_t)npairs * (1ull + kPairRows) + 1;
 }
 
 uint64_t edt_slerp_population_gram_doubles(int nmembers, int64_t nchunks) {
@@ -1909,7 +1477,7 @@ int edt_slerp_population(const void* const* members, int nmembers, int in_dt, co
                 mem.p[D++] = members[m];
             }
         }
-    int rc = gram_sums(mem, D, nullptr, in_dt, out_dt, chunk_desc, nchunks, nullptr, gram, s);
+    int rc = gram_sums(mem, D, in_dt, chunk_desc, nchunks, gram, s);
     if (rc) return rc;
     const int M = D, NT = M * (M + 1) / 2;
     const unsigned gc = coef_grid(nseg);
@@ -1981,7 +1549,7 @@ int edt_slerp_gram(const void* const* members, int nmembers, int in_dt, const ui
         if (!members[m] || !aligned16(members[m])) return fail(EDT_ERR_ARG, "member %d is null or not 16-byte aligned", m);
         mem.p[m] = members[m];
     }
-    return gram_sums(mem, nmembers, nullptr, in_dt, EDT_F32, chunk_desc, nchunks, nullptr, gram, (hipStream_t)stream);
+    return gram_sums(mem, nmembers, in_dt, chunk_desc, nchunks, gram, (hipStream_t)stream);
 }
 
 int edt_slerp_gram_coef(const double* gram, int nmembers, const int32_t* pairs, int npairs,
@@ -2078,13 +1646,13 @@ int edt_slerp_merge_speculative(const void* v0, const void* v1, int in_dt, void*
     const unsigned g = slerp_spec_grid(nchunks);
     constexpr bool kNtB = EDT_NT_SLERP != 0;
     if (in_dt == EDT_F32 && out_dt == EDT_F32)
-        slerp_blend_kernel<EDT_F32, EDT_F32, false, false><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, nullptr, redo, any);
+        slerp_blend_kernel<EDT_F32, EDT_F32, false><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, nullptr, redo, any);
     else if (in_dt == EDT_F32)
-        slerp_blend_kernel<EDT_F32, EDT_BF16, false, false><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, nullptr, redo, any);
+        slerp_blend_kernel<EDT_F32, EDT_BF16, false><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, nullptr, redo, any);
     else if (out_dt == EDT_F32)
-        slerp_blend_kernel<EDT_BF16, EDT_F32, kNtB, false><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, nullptr, redo, any);
+        slerp_blend_kernel<EDT_BF16, EDT_F32, kNtB><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, nullptr, redo, any);
     else
-        slerp_blend_kernel<EDT_BF16, EDT_BF16, kNtB, false><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, nullptr, redo, any);
+        slerp_blend_kernel<EDT_BF16, EDT_BF16, kNtB><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, nullptr, redo, any);
     return check_launch("slerp_blend_kernel");
 }
 
@@ -2113,61 +1681,6 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
         }
     }
     hipStream_t s = (hipStream_t)stream;
-    // member-major first pass when the distinct parents fit one Gram tile (<= 8) and the children
-    // one launch (<= 16): every distinct parent read once per chunk, whatever the caches do
-    int compact[256];
-    int D = 0;
-    Members mem;
-    memset(&mem, 0, sizeof(mem));
-    bool fused = EDT_SLERP_POP_FUSED && npairs <= kBlendMaxChildren && nmembers <= 256;
-    if (fused) {
-        for (int m = 0; m < nmembers; ++m) compact[m] = -1;
-        for (int q = 0; q < npairs && fused; ++q)
-            for (int e = 0; e < 2; ++e) {
-                const int m = pairs[2 * q + e];
-                if (compact[m] < 0) {
-                    if (D == kGramMaxMembers) { fused = false; break; }
-                    compact[m] = D;
-                    mem.p[D++] = members[m];
-                }
-            }
-    }
-    if (fused) {
-        PopLerp po;
-        memset(&po, 0, sizeof(po));
-        po.n = npairs;
-        for (int q = 0; q < npairs; ++q) {
-            po.out[q] = outs[q];
-            po.a[q] = compact[pairs[2 * q]];
-            po.b[q] = compact[pairs[2 * q + 1]];
-        }
-        int rc = gram_sums(mem, D, &po, in_dt, out_dt, chunk_desc, nchunks, t, partial, s);
-        if (rc) return rc;
-        const int NT = D * (D + 1) / 2;
-        for (int q = 0; q < npairs; ++q) {
-            const int i = compact[pairs[2 * q]], j = compact[pairs[2 * q + 1]];
-            const int lo = i < j ? i : j, hi = i < j ? j : i;
-            slerp_gram_coef_kernel<<<coef_grid(nseg), kBlock, 0, s>>>(
-                partial, NT, tri_index(i, i, D), tri_index(j, j, D), tri_index(lo, hi, D), seg_first_chunk, nseg, t,
-                (float)dot_threshold, (float)eps, coef + 2 * (size_t)nseg * q,
-                dot_out ? dot_out + (size_t)nseg * q : nullptr, redo + (size_t)nseg * q);
-            rc = check_launch("slerp_gram_coef_kernel");
-            if (rc) return rc;
-        }
-    }
-    if (fused) {                             // the redo blends, member-major over the same D parents
-        PopBlend pb;
-        memset(&pb, 0, sizeof(pb));
-        pb.n = npairs;
-        for (int q = 0; q < npairs; ++q) {
-            pb.out[q] = outs[q];
-            pb.coef[q] = coef + 2 * (size_t)nseg * q;
-            pb.redo[q] = redo + (size_t)nseg * q;
-            pb.a[q] = compact[pairs[2 * q]];
-            pb.b[q] = compact[pairs[2 * q + 1]];
-        }
-        return launch_blend_mm(mem, D, pb, in_dt, out_dt, chunk_desc, nchunks, s);
-    }
     // the any-redo word (the workspace's last double): zeroed by the first pass, set by any child's
     // coefficient kernel that sends a segment to the SLERP branch; clear, the redo grid exits at once
     int32_t* any = reinterpret_cast<int32_t*>(partial + edt_slerp_population_speculative_doubles(npairs, nchunks) - 1);
@@ -2223,27 +1736,66 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
 }   // extern "C"
 
 namespace {
-// The tensor-list forms' pointer table: {v0, v1, out} per segment, uploaded into `workspace` by a
-// stream-ordered copy (pageable source: staged before hipMemcpyAsync returns).
-int upload_seg_table(const void* const* v0_t, const void* const* v1_t, void* const* out_t, int nseg, void* workspace,
-                     uint64_t workspace_bytes, bool outputs_apart, hipStream_t s) {
-    if (!v0_t || !v1_t || !out_t) return fail(EDT_ERR_ARG, "null tensor table");
+// The tensor-list forms: segment s is its own tensor triple {v0, v1, out}, read through a DEVICE
+// table of 3 x nseg uint64 pointers (edt_slerp_seg_table validates and writes its host image; the
+// caller uploads it once and reuses it while the tensors stay where they are).
+
+struct Span {
+    uintptr_t a, e;
+    bool out;
+};
+
+// No output span overlaps a parent span: spans sorted by start, each checked against the
+// furthest end of the other kind before it (empty spans ignored).
+bool spans_apart(std::vector<Span>& sp) {
+    std::sort(sp.begin(), sp.end(), [](const Span& x, const Span& y) { return x.a < y.a; });
+    uintptr_t far_in = 0, far_out = 0;
+    for (const Span& x : sp) {
+        if (x.out ? x.a < far_in : x.a < far_out) return false;
+        uintptr_t& f = x.out ? far_out : far_in;
+        if (x.e > f) f = x.e;
+    }
+    return true;
+}
+
+// the redo blends / any table blend with a redo mask: grid-stride over chunks (most are skipped)
+int blend_redo(const void* v0, const void* v1, int in_dt, void* out, int out_dt, const uint64_t* chunk_desc,
+               int64_t nchunks, const float* coef, const uint64_t* seg_ptrs, const int32_t* redo,
+               const int32_t* any, hipStream_t s) {
+    const unsigned g = slerp_spec_grid(nchunks);
+    constexpr bool kNtB = EDT_NT_SLERP != 0;
+    if (in_dt == EDT_F32 && out_dt == EDT_F32)
+        slerp_blend_kernel<EDT_F32, EDT_F32, false><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, seg_ptrs, redo, any);
+    else if (in_dt == EDT_F32)
+        slerp_blend_kernel<EDT_F32, EDT_BF16, false><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, seg_ptrs, redo, any);
+    else if (out_dt == EDT_F32)
+        slerp_blend_kernel<EDT_BF16, EDT_F32, kNtB><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, seg_ptrs, redo, any);
+    else
+        slerp_blend_kernel<EDT_BF16, EDT_BF16, kNtB><<<g, kBlock, 0, s>>>(v0, v1, out, chunk_desc, nchunks, coef, seg_ptrs, redo, any);
+    return check_launch("slerp_blend_kernel");
+}
+
+int table_args(const uint64_t* table, int in_dt, int out_dt, int64_t nchunks, int nseg) {
+    if ((in_dt | out_dt) & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
+    if (nseg < 0 || nchunks < 0) return fail(EDT_ERR_ARG, "negative count (segments %d, chunks %lld)", nseg, (long long)nchunks);
+    if (nchunks > 0 && !table) return fail(EDT_ERR_ARG, "null tensor table");
+    if (reinterpret_cast<uintptr_t>(table) & 7u) return fail(EDT_ERR_ARG, "tensor table must be 8-byte aligned");
+    return EDT_OK;
+}
+
+// the pointer-array entries: validate, then upload the table into `workspace` by a stream-ordered
+// copy (pageable source: staged before hipMemcpyAsync returns)
+int upload_seg_table(const void* const* v0_t, const void* const* v1_t, void* const* out_t, int nseg,
+                     const uint64_t* seg_numel, int in_dt, int out_dt, int apart, void* workspace,
+                     uint64_t workspace_bytes, hipStream_t s) {
     const uint64_t need = 3ull * sizeof(uint64_t) * (uint64_t)nseg;
     if (!workspace || workspace_bytes < need)
         return fail(EDT_ERR_ARG, "workspace of %llu bytes needed", (unsigned long long)need);
     if (reinterpret_cast<uintptr_t>(workspace) & 7u) return fail(EDT_ERR_ARG, "workspace must be 8-byte aligned");
     thread_local std::vector<uint64_t> h;
     h.assign(3 * (size_t)nseg, 0);
-    for (int i = 0; i < nseg; ++i) {
-        // a null pointer is only valid for an empty segment (it has no chunks, so it is never read)
-        if (!aligned16(v0_t[i]) || !aligned16(v1_t[i]) || !aligned16(out_t[i]))
-            return fail(EDT_ERR_ARG, "tensor %d is not 16-byte aligned", i);
-        if (outputs_apart && out_t[i] && (out_t[i] == v0_t[i] || out_t[i] == v1_t[i]))
-            return fail(EDT_ERR_ARG, "tensor %d: the speculative form needs an output apart from its parents", i);
-        h[3 * i] = reinterpret_cast<uintptr_t>(v0_t[i]);
-        h[3 * i + 1] = reinterpret_cast<uintptr_t>(v1_t[i]);
-        h[3 * i + 2] = reinterpret_cast<uintptr_t>(out_t[i]);
-    }
+    int rc = edt_slerp_seg_table(v0_t, v1_t, out_t, nseg, seg_numel, in_dt, out_dt, apart, h.data());
+    if (rc) return rc;
     hipError_t e = hipMemcpyAsync(workspace, h.data(), need, hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return fail(EDT_ERR_LAUNCH, "tensor table upload failed: %s", hipGetErrorString(e));
     return EDT_OK;
@@ -2251,6 +1803,109 @@ int upload_seg_table(const void* const* v0_t, const void* const* v1_t, void* con
 }   // namespace
 
 extern "C" {
+
+int edt_slerp_seg_table(const void* const* v0_t, const void* const* v1_t, void* const* out_t, int nseg,
+                        const uint64_t* seg_numel, int in_dt, int out_dt, int apart, uint64_t* table_host) {
+    g_err[0] = 0;
+    if ((in_dt | out_dt) & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
+    if (nseg < 0) return fail(EDT_ERR_ARG, "negative segment count");
+    if (nseg == 0) return EDT_OK;
+    if (!v0_t || !v1_t || !out_t || !table_host) return fail(EDT_ERR_ARG, "null tensor table");
+    if (apart && !seg_numel) return fail(EDT_ERR_ARG, "the overlap check needs the segment sizes");
+    const uint64_t isz = in_dt == EDT_BF16 ? 2 : 4, osz = out_dt == EDT_BF16 ? 2 : 4;
+    std::vector<Span> sp;
+    if (apart) sp.reserve(3 * (size_t)nseg);
+    for (int i = 0; i < nseg; ++i) {
+        // a null pointer is only valid for an empty segment (it has no chunks, so it is never read)
+        if (!aligned16(v0_t[i]) || !aligned16(v1_t[i]) || !aligned16(out_t[i]))
+            return fail(EDT_ERR_ARG, "tensor %d is not 16-byte aligned", i);
+        if (seg_numel && seg_numel[i] > 0 && (!v0_t[i] || !v1_t[i] || !out_t[i]))
+            return fail(EDT_ERR_ARG, "tensor %d is null", i);
+        table_host[3 * (size_t)i] = reinterpret_cast<uintptr_t>(v0_t[i]);
+        table_host[3 * (size_t)i + 1] = reinterpret_cast<uintptr_t>(v1_t[i]);
+        table_host[3 * (size_t)i + 2] = reinterpret_cast<uintptr_t>(out_t[i]);
+        if (apart && seg_numel[i] > 0) {
+            const uintptr_t p0 = reinterpret_cast<uintptr_t>(v0_t[i]), p1 = reinterpret_cast<uintptr_t>(v1_t[i]);
+            const uintptr_t po = reinterpret_cast<uintptr_t>(out_t[i]);
+            sp.push_back({p0, p0 + seg_numel[i] * isz, false});
+            sp.push_back({p1, p1 + seg_numel[i] * isz, false});
+            sp.push_back({po, po + seg_numel[i] * osz, true});
+        }
+    }
+    if (apart && !spans_apart(sp))
+        return fail(EDT_ERR_ARG, "an output overlaps a parent tensor: the single-pass form needs outputs apart");
+    return EDT_OK;
+}
+
+int edt_slerp_stats_table(const uint64_t* seg_table, int in_dt, const uint64_t* chunk_desc, int64_t nchunks,
+                          double* partial, void* stream) {
+    g_err[0] = 0;
+    int rc = table_args(seg_table, in_dt, EDT_F32, nchunks, 0);
+    if (rc) return rc;
+    return slerp_stats_impl(nullptr, nullptr, in_dt, chunk_desc, nchunks, partial, seg_table, stream);
+}
+
+int edt_slerp_blend_table(const uint64_t* seg_table, int in_dt, int out_dt, const uint64_t* chunk_desc,
+                          int64_t nchunks, const float* coef, const int32_t* redo, void* stream) {
+    g_err[0] = 0;
+    int rc = table_args(seg_table, in_dt, out_dt, nchunks, 0);
+    if (rc) return rc;
+    if (nchunks == 0) return EDT_OK;
+    if (!chunk_desc || !coef) return fail(EDT_ERR_ARG, "null buffer");
+    if (!redo) return slerp_blend_impl(nullptr, nullptr, in_dt, nullptr, out_dt, chunk_desc, nchunks, coef, seg_table, stream);
+    return blend_redo(nullptr, nullptr, in_dt, nullptr, out_dt, chunk_desc, nchunks, coef, seg_table, redo, nullptr,
+                      (hipStream_t)stream);
+}
+
+int edt_slerp_blend_segments(const void* v0, const void* v1, int in_dt, void* out, int out_dt,
+                             const uint64_t* chunk_desc, int64_t nchunks, const float* coef, const int32_t* redo,
+                             void* stream) {
+    g_err[0] = 0;
+    if ((in_dt | out_dt) & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
+    if (nchunks < 0) return fail(EDT_ERR_ARG, "negative chunk count");
+    if (nchunks == 0) return EDT_OK;
+    if (!v0 || !v1 || !out || !chunk_desc || !coef || !redo) return fail(EDT_ERR_ARG, "null buffer");
+    if (!aligned16(v0) || !aligned16(v1) || !aligned16(out))
+        return fail(EDT_ERR_ARG, "slerp buffers must be 16-byte aligned");
+    return blend_redo(v0, v1, in_dt, out, out_dt, chunk_desc, nchunks, coef, nullptr, redo, nullptr, (hipStream_t)stream);
+}
+
+int edt_slerp_merge_table(const uint64_t* seg_table, int in_dt, int out_dt, const uint64_t* chunk_desc,
+                          int64_t nchunks, const int32_t* seg_first_chunk, int nseg, const double* t,
+                          double dot_threshold, double eps, double* partial, float* coef, float* dot_out,
+                          void* stream) {
+    g_err[0] = 0;
+    int rc = table_args(seg_table, in_dt, out_dt, nchunks, nseg);
+    if (rc) return rc;
+    if (nseg == 0 || nchunks == 0) return EDT_OK;
+    if (!chunk_desc || !seg_first_chunk || !t || !partial || !coef) return fail(EDT_ERR_ARG, "null buffer");
+    rc = slerp_stats_impl(nullptr, nullptr, in_dt, chunk_desc, nchunks, partial, seg_table, stream);
+    if (rc) return rc;
+    rc = edt_slerp_coef(partial, seg_first_chunk, nseg, t, dot_threshold, eps, coef, dot_out, stream);
+    if (rc) return rc;
+    return slerp_blend_impl(nullptr, nullptr, in_dt, nullptr, out_dt, chunk_desc, nchunks, coef, seg_table, stream);
+}
+
+int edt_slerp_merge_table_speculative(const uint64_t* seg_table, int in_dt, int out_dt, const uint64_t* chunk_desc,
+                                      int64_t nchunks, const int32_t* seg_first_chunk, int nseg, const double* t,
+                                      double dot_threshold, double eps, double* partial, float* coef,
+                                      float* dot_out, int32_t* redo, void* stream) {
+    g_err[0] = 0;
+    int rc = table_args(seg_table, in_dt, out_dt, nchunks, nseg);
+    if (rc) return rc;
+    if (nseg == 0 || nchunks == 0) return EDT_OK;
+    if (!chunk_desc || !seg_first_chunk || !t || !partial || !coef || !redo) return fail(EDT_ERR_ARG, "null buffer");
+    hipStream_t s = (hipStream_t)stream;
+    // the any-redo word: the last double of the workspace, as edt_slerp_merge_speculative's
+    int32_t* any = reinterpret_cast<int32_t*>(partial + edt_slerp_sums_doubles(3, nchunks) - 1);
+    rc = pair_sums(nullptr, nullptr, in_dt, nullptr, out_dt, true, chunk_desc, nchunks, partial, t, seg_table, s, any);
+    if (rc) return rc;
+    slerp_coef_kernel<<<coef_grid(nseg), kBlock, 0, s>>>(partial, seg_first_chunk, nseg, t, (float)dot_threshold,
+                                                         (float)eps, coef, dot_out, redo, any);
+    rc = check_launch("slerp_coef_kernel");
+    if (rc) return rc;
+    return blend_redo(nullptr, nullptr, in_dt, nullptr, out_dt, chunk_desc, nchunks, coef, seg_table, redo, any, s);
+}
 
 int edt_slerp_merge_list(const void* const* v0_t, const void* const* v1_t, int in_dt, void* const* out_t,
                          int out_dt, const uint64_t* chunk_desc, int64_t nchunks, const int32_t* seg_first_chunk,
@@ -2262,50 +1917,31 @@ int edt_slerp_merge_list(const void* const* v0_t, const void* const* v1_t, int i
     if (nseg == 0 || nchunks == 0) return EDT_OK;
     if (!v0_t || !v1_t || !out_t) return fail(EDT_ERR_ARG, "null tensor table");
     if (!chunk_desc || !seg_first_chunk || !t || !partial || !coef) return fail(EDT_ERR_ARG, "null buffer");
-    int rc = upload_seg_table(v0_t, v1_t, out_t, nseg, workspace, workspace_bytes, false, (hipStream_t)stream);
+    int rc = upload_seg_table(v0_t, v1_t, out_t, nseg, nullptr, in_dt, out_dt, 0, workspace, workspace_bytes,
+                              (hipStream_t)stream);
     if (rc) return rc;
-    const uint64_t* seg_ptrs = static_cast<const uint64_t*>(workspace);
-    rc = slerp_stats_impl(nullptr, nullptr, in_dt, chunk_desc, nchunks, partial, seg_ptrs, stream);
-    if (rc) return rc;
-    rc = edt_slerp_coef(partial, seg_first_chunk, nseg, t, dot_threshold, eps, coef, dot_out, stream);
-    if (rc) return rc;
-    return slerp_blend_impl(nullptr, nullptr, in_dt, nullptr, out_dt, chunk_desc, nchunks, coef, seg_ptrs, stream);
+    return edt_slerp_merge_table(static_cast<const uint64_t*>(workspace), in_dt, out_dt, chunk_desc, nchunks,
+                                 seg_first_chunk, nseg, t, dot_threshold, eps, partial, coef, dot_out, stream);
 }
 
 int edt_slerp_merge_list_speculative(const void* const* v0_t, const void* const* v1_t, int in_dt, void* const* out_t,
-                                     int out_dt, const uint64_t* chunk_desc, int64_t nchunks,
-                                     const int32_t* seg_first_chunk, int nseg, const double* t, double dot_threshold,
-                                     double eps, double* partial, float* coef, float* dot_out, int32_t* redo,
-                                     void* workspace, uint64_t workspace_bytes, void* stream) {
+                                     int out_dt, const uint64_t* seg_numel, const uint64_t* chunk_desc,
+                                     int64_t nchunks, const int32_t* seg_first_chunk, int nseg, const double* t,
+                                     double dot_threshold, double eps, double* partial, float* coef, float* dot_out,
+                                     int32_t* redo, void* workspace, uint64_t workspace_bytes, void* stream) {
     g_err[0] = 0;
     if ((in_dt | out_dt) & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
     if (nseg < 0 || nchunks < 0) return fail(EDT_ERR_ARG, "negative count (segments %d, chunks %lld)", nseg, (long long)nchunks);
     if (nseg == 0 || nchunks == 0) return EDT_OK;
     if (!v0_t || !v1_t || !out_t) return fail(EDT_ERR_ARG, "null tensor table");
+    if (!seg_numel) return fail(EDT_ERR_ARG, "null segment sizes");
     if (!chunk_desc || !seg_first_chunk || !t || !partial || !coef || !redo) return fail(EDT_ERR_ARG, "null buffer");
-    hipStream_t s = (hipStream_t)stream;
-    int rc = upload_seg_table(v0_t, v1_t, out_t, nseg, workspace, workspace_bytes, true, s);
+    int rc = upload_seg_table(v0_t, v1_t, out_t, nseg, seg_numel, in_dt, out_dt, 1, workspace, workspace_bytes,
+                              (hipStream_t)stream);
     if (rc) return rc;
-    const uint64_t* seg_ptrs = static_cast<const uint64_t*>(workspace);
-    // the any-redo word: the last double of the workspace, as edt_slerp_merge_speculative's
-    int32_t* any = reinterpret_cast<int32_t*>(partial + edt_slerp_sums_doubles(3, nchunks) - 1);
-    rc = pair_sums(nullptr, nullptr, in_dt, nullptr, out_dt, true, chunk_desc, nchunks, partial, t, seg_ptrs, s, any);
-    if (rc) return rc;
-    slerp_coef_kernel<<<coef_grid(nseg), kBlock, 0, s>>>(partial, seg_first_chunk, nseg, t, (float)dot_threshold,
-                                                         (float)eps, coef, dot_out, redo, any);
-    rc = check_launch("slerp_coef_kernel");
-    if (rc) return rc;
-    const unsigned g = slerp_spec_grid(nchunks);
-    constexpr bool kNtB = EDT_NT_SLERP != 0;
-    if (in_dt == EDT_F32 && out_dt == EDT_F32)
-        slerp_blend_kernel<EDT_F32, EDT_F32, false, false><<<g, kBlock, 0, s>>>(nullptr, nullptr, nullptr, chunk_desc, nchunks, coef, seg_ptrs, redo, any);
-    else if (in_dt == EDT_F32)
-        slerp_blend_kernel<EDT_F32, EDT_BF16, false, false><<<g, kBlock, 0, s>>>(nullptr, nullptr, nullptr, chunk_desc, nchunks, coef, seg_ptrs, redo, any);
-    else if (out_dt == EDT_F32)
-        slerp_blend_kernel<EDT_BF16, EDT_F32, kNtB, false><<<g, kBlock, 0, s>>>(nullptr, nullptr, nullptr, chunk_desc, nchunks, coef, seg_ptrs, redo, any);
-    else
-        slerp_blend_kernel<EDT_BF16, EDT_BF16, kNtB, false><<<g, kBlock, 0, s>>>(nullptr, nullptr, nullptr, chunk_desc, nchunks, coef, seg_ptrs, redo, any);
-    return check_launch("slerp_blend_kernel");
+    return edt_slerp_merge_table_speculative(static_cast<const uint64_t*>(workspace), in_dt, out_dt, chunk_desc,
+                                             nchunks, seg_first_chunk, nseg, t, dot_threshold, eps, partial, coef,
+                                             dot_out, redo, stream);
 }
 
 
@@ -2383,6 +2019,18 @@ int edt_slerp_refdot(const void* v0, const void* v1, int in_dt, const uint64_t* 
     g_err[0] = 0;
     return refdot_impl(v0, v1, in_dt, chunk_desc, nchunks, seg_first_chunk, nseg, chunk_elems, flag, threads, eps,
                        ref_dot, workspace, workspace_bytes, nullptr, stream);
+}
+
+int edt_slerp_refdot_table(const uint64_t* seg_table, int in_dt, const uint64_t* chunk_desc, int64_t nchunks,
+                           const int32_t* seg_first_chunk, int nseg, uint32_t chunk_elems, const int32_t* flag,
+                           int threads, double eps, float* ref_dot, void* workspace, uint64_t workspace_bytes,
+                           void* stream) {
+    g_err[0] = 0;
+    int rc = table_args(seg_table, in_dt, EDT_F32, nchunks, nseg);
+    if (rc) return rc;
+    if (nseg > 0 && !seg_table) return fail(EDT_ERR_ARG, "null tensor table");
+    return refdot_impl(nullptr, nullptr, in_dt, chunk_desc, nchunks, seg_first_chunk, nseg, chunk_elems, flag, threads,
+                       eps, ref_dot, workspace, workspace_bytes, seg_table, stream);
 }
 
 int edt_slerp_refdot_coef(const float* ref_dot, const int32_t* flag, int nseg, const double* t, double dot_threshold,

@@ -559,10 +559,102 @@ class ShardedPopulationCrossover:
                 ops_.append(("recv", out[lo:hi], j))
         return self.comm.p2p(ops_, async_op=True)
 
+    def _reference_dots(self, members, pairs, t, dots, dot_threshold, eps, ref):
+        """Reference-dot mode of the sharded generation (ops.RefDot): the reference's fp32 dot of
+        every flagged (child, segment) — the BLAS sdot chains and numpy's pairwise sum run over the
+        WHOLE segment in order, so each segment is computed by the rank that holds its first chunk:
+        from its own shards when the segment ends in its range, else after the later ranks send it
+        the rest of that segment of the parents it needs (only segments that straddle a range
+        boundary: at most N - 1). The values are all-gathered (host objects) and every rank forms
+        the reference's coefficients of every child from them (ops.reference_coefficients): the
+        children equal the reference's merges bit for bit with band < 0. Returns (coef [Q, nseg, 2],
+        dots [Q, nseg]) on the device."""
+        import numpy as np
+        k, N, Q = self.kernels, self.world, len(pairs)
+        plan, nseg = self.plan, self.plan.nseg
+        host = np.asarray(plan.chunks_host, dtype=np.int64).reshape(-1, 3)
+        first = np.searchsorted(host[:, 2], np.arange(nseg + 1), side="left") if len(host) \
+            else np.zeros(nseg + 1, dtype=np.int64)
+        d = dots[:Q, :nseg].detach().cpu().numpy().astype(np.float32)
+        if ref.band < 0:
+            flag = np.ones((Q, nseg), dtype=bool)
+        else:                               # refdot_flag_kernel's test, in fp32
+            flag = np.abs(np.abs(d) - np.float32(dot_threshold)) <= np.float32(ref.band)
+        flag &= (first[1:] > first[:-1])[None, :]          # segments with elements
+        owner = np.full(nseg, -1, dtype=np.int64)
+        for r in range(N):
+            a, b = self.ranges[r][:2]
+            owner[(first[:-1] >= a) & (first[:-1] < b)] = r
+        c0, c1 = self.ranges[self.rank][:2]
+        dt = members[0].dtype
+        # 1. the rest of each straddling flagged segment to its owner (same op order on every rank)
+        ops_, bufs = [], {}
+        for s in range(nseg):
+            r = int(owner[s])
+            if r < 0 or not flag[:, s].any() or first[s + 1] <= self.ranges[r][1]:
+                continue
+            need = sorted({int(x) for q in range(Q) if flag[q, s] for x in pairs[q]})
+            seg_lo = int(host[first[s], 0])
+            seg_hi = int(host[first[s + 1] - 1, 0] + host[first[s + 1] - 1, 1])
+            if r == self.rank:
+                own_hi = int(host[c1 - 1, 0] + host[c1 - 1, 1])
+                for m in need:
+                    buf = bufs[(s, m)] = torch.empty(seg_hi - seg_lo, dtype=dt, device=self.device)
+                    buf[:own_hi - seg_lo].copy_(members[m][seg_lo - self.base:own_hi - self.base])
+            for j in range(N):
+                if j == r:
+                    continue
+                ja, jb, jbase = self.ranges[j][:3]
+                lo, hi = max(int(first[s]), ja), min(int(first[s + 1]), jb)
+                if hi <= lo:
+                    continue
+                elo, ehi = int(host[lo, 0]), int(host[hi - 1, 0] + host[hi - 1, 1])
+                for m in need:
+                    if j == self.rank:
+                        ops_.append(("send", members[m][elo - jbase:ehi - jbase], r))
+                    elif r == self.rank:
+                        ops_.append(("recv", bufs[(s, m)][elo - seg_lo:ehi - seg_lo], j))
+        if ops_:
+            self.comm.p2p(ops_)
+        # 2. this rank's segments: whole ones from its shards (one pass per child), straddling ones
+        #    from the assembled buffers
+        mine = owner == self.rank
+        whole = mine & (first[1:] <= c1)
+        sf = torch.from_numpy(np.clip(first - c0, 0, max(0, c1 - c0)).astype(np.int32)).to(self.device)
+        found = []
+        for q, (i, j) in enumerate(pairs):
+            fq = flag[q] & whole
+            if fq.any():
+                val = k.slerp_refdot(members[i], members[j], self.local_chunks, sf, nseg, plan.chunk_elems,
+                                     torch.from_numpy(fq.astype(np.int32)).to(self.device), ref, eps)
+                vh = val[:nseg].cpu().numpy()
+                found.extend((q, int(s), float(vh[s])) for s in np.nonzero(fq)[0])
+        for s in sorted({s for (s, _) in bufs}):
+            seg_len = int(host[first[s + 1] - 1, 0] + host[first[s + 1] - 1, 1] - host[first[s], 0])
+            ce = plan.chunk_elems
+            rows = np.asarray([(x, min(ce, seg_len - x), 0) for x in range(0, seg_len, ce)], dtype=np.int64)
+            ch = torch.from_numpy(rows).to(self.device)
+            sf1 = torch.tensor([0, len(rows)], dtype=torch.int32).to(self.device)
+            one = torch.ones(1, dtype=torch.int32).to(self.device)
+            for q, (i, j) in enumerate(pairs):
+                if flag[q, s]:
+                    val = k.slerp_refdot(bufs[(s, i)], bufs[(s, j)], ch, sf1, 1, ce, one, ref, eps)
+                    found.append((q, int(s), float(val[:1].cpu().numpy()[0])))
+        # 3. every rank: all values, then the reference's coefficients of every child
+        final = d.copy()
+        for part in self.comm.all_gather_object(found):
+            for q, s, v in part:
+                final[q, s] = np.float32(v)
+        from .ops import reference_coefficients
+        coef = reference_coefficients(final, t[:nseg].detach().cpu().numpy(), dot_threshold)
+        return torch.from_numpy(coef).to(self.device), torch.from_numpy(final).to(self.device)
+
     @traced("edt/ShardedPopulationCrossover.slerp_step")
     def slerp_step(self, member: torch.Tensor, pairs, t: torch.Tensor, out: torch.Tensor,
-                   dot_threshold: float = 0.9995, eps: float = 1e-8) -> torch.Tensor:
-        """Child pairs[rank] into `out`; returns the per-segment dots of every child [N, nseg]."""
+                   dot_threshold: float = 0.9995, eps: float = 1e-8, ref_dot=None) -> torch.Tensor:
+        """Child pairs[rank] into `out`; returns the per-segment dots of every child [N, nseg].
+        ref_dot (ops.RefDot): the reference-dot mode (_reference_dots; the groups > 1 pipeline is
+        not used in that mode: the coefficients need every rank's values first)."""
         if len(pairs) != self.world:
             raise ValueError(f"{len(pairs)} children for {self.world} ranks")
         k, N = self.kernels, self.world
@@ -573,7 +665,7 @@ class ShardedPopulationCrossover:
                                                     device=self.device)
         c0, c1 = self.ranges[self.rank][:2]
         mine = self.granges[self.rank]
-        if self.groups > 1:
+        if self.groups > 1 and ref_dot is None:
             sh, handles = self._scatter_groups(member, "m")
             members = [sh[j] for j in range(N)]
             for g, h in enumerate(handles):
@@ -596,8 +688,10 @@ class ShardedPopulationCrossover:
                 ops_.append(("recv", gram[a:b], j))
         self.comm.p2p(ops_)
         coef, dots = k.slerp_gram_coef(self.plan, gram, N, pairs, t, dot_threshold, eps)
+        if ref_dot is not None:
+            coef, dots = self._reference_dots(members, pairs, t, dots, dot_threshold, eps, ref_dot)
         outs = [self._buf(("c", q), self.out_dtype)[:self.end - self.base] for q in range(N)]
-        if self.groups > 1:
+        if self.groups > 1 and ref_dot is None:
             handles = []
             for g in range(self.groups):
                 if g < len(mine):

@@ -5,8 +5,10 @@ on a worker, driven by EDT_EVOMERGE/edt.py:262-280 through the CLI
 
 The reference moves each tensor to the GPU and back and SLERPs it in numpy (its LazyTensorLoader,
 EDT_EVOMERGE/train/crossover.py:86-146); here both bodies are merged in HBM in one multi-tensor
-pass and the bf16 result is written straight into model_1's body (the reference's
-`model_merged.model.load_state_dict`, :142, rounds the fp32 SLERP to bf16 the same way).
+pass and the bf16 result becomes model_1's body (the reference's `model_merged.model.load_state_dict`,
+:142, rounds the fp32 SLERP to bf16 the same way): written to a fresh buffer in the single-pass form
+and model_1's parameters re-pointed at it (merge.slerp_into_module_), since writing into model_1's
+own tensors — the parent being read — would force the two-pass form.
 """
 from __future__ import annotations
 
@@ -16,7 +18,7 @@ import os
 import torch
 
 from .merge import (LazyTensorLoader, interpolate_t, lerp, maybe_torch, merge_plan, normalize, slerp,  # noqa: F401
-                    slerp_state_dicts, uniform_dna_crossover)
+                    slerp_into_module_, slerp_state_dicts, uniform_dna_crossover)
 
 __all__ = ["slerp", "lerp", "interpolate_t", "load_model_from_path", "run_slerp_merge_from_config",
            "run_linear_merge_5050", "crossover_main", "uniform_dna_crossover", "SELF_ATTN_T_CURVE",
@@ -51,9 +53,10 @@ def run_slerp_merge_from_config(merge_config_dict: dict, model_1, model_2, confi
     dev = torch.device(device) if device not in (None, "cpu") else None
     tsd = target.state_dict()
     if set(tsd) == {k for k, _ in plan}:
-        # the merge lands in the target's own tensors (== load_state_dict of the merged dict);
-        # the target may be model_1 itself (the reference passes base_model=model_1)
-        slerp_state_dicts(sd1, sd2, plan, out_dtype=out_dtype, device=dev, out=tsd)
+        # the merge lands in the target's parameters (== load_state_dict of the merged dict). The
+        # target may be model_1 itself (the reference passes base_model=model_1): then the children
+        # go to a fresh buffer in one pass and the parameters are re-pointed at it
+        slerp_into_module_(target, sd1, sd2, plan, out_dtype, device=dev)
     else:                                   # load_state_dict reports the key mismatch
         target.load_state_dict(slerp_state_dicts(sd1, sd2, plan, out_dtype=out_dtype, device=dev))
     base_model.save_pretrained(merge_output_path)

@@ -224,13 +224,38 @@ def lerp(t: float, v0: torch.Tensor, v1: torch.Tensor, out: torch.Tensor | None 
 # ------------------------------------------------------------------------------------------
 # SLERP over a multi-tensor arena
 
+_POOLS: dict = {}
+
+
+def _scratch(device: torch.device, ndoubles: int) -> torch.Tensor:
+    """float64 device workspace of `ndoubles` (a view) from one growing buffer per (device, stream).
+    The chunk-sum passes' rows and row scratch are only live inside one call, so every plan on a
+    stream shares one buffer instead of each cached plan holding its own (7B body: 107,893 chunks
+    x 387 doubles = 334 MB for a pair merge; the population speculative form 3,096 doubles per
+    chunk at 8 children = 2.7 GB). Calls on one stream run in order, so a later call
+    overwrites the rows only after the earlier call's kernels are done."""
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    key = (idx, torch.cuda.current_stream(dev).cuda_stream)
+    buf = _POOLS.get(key)
+    n = max(1, int(ndoubles))
+    if buf is None or buf.numel() < n:
+        _POOLS.pop(key, None)
+        buf = _POOLS[key] = torch.empty(n, dtype=torch.float64, device=dev)
+    return buf[:n]
+
+
+def release_scratch() -> None:
+    """Drop the pooled SLERP workspaces (bench.py frees them between workloads)."""
+    _POOLS.clear()
+
+
 @dataclass
 class SlerpPlan:
     """Chunk table for a segment layout, resident on the device (built once per layout)."""
     seg_offsets: list[int]
     chunks: torch.Tensor          # int64 [nchunks, 3] = start, length, segment
     seg_first: torch.Tensor       # int32 [nseg + 1]
-    partial: torch.Tensor         # float64 workspace: chunk rows [nchunks, 3], then the slot scratch
     coef: torch.Tensor            # float32 [nseg, 2]
     dots: torch.Tensor            # float32 [nseg]
     nchunks: int
@@ -241,6 +266,17 @@ class SlerpPlan:
     @property
     def nseg(self) -> int:
         return len(self.seg_offsets) - 1
+
+    @property
+    def partial(self) -> torch.Tensor:
+        """The pair passes' workspace: chunk rows [nchunks, 3] first, then the row scratch and the
+        any-redo word (edt_slerp_sums_doubles(3, nchunks) doubles, pooled per stream)."""
+        return _scratch(self.chunks.device, L.load_library().edt_slerp_sums_doubles(3, self.nchunks))
+
+    @property
+    def seg_numel(self):
+        import numpy as np
+        return np.diff(np.asarray(self.seg_offsets, dtype=np.int64))
 
 
 def make_slerp_plan(seg_offsets: list[int], device: torch.device,
@@ -264,8 +300,6 @@ def make_slerp_plan(seg_offsets: list[int], device: torch.device,
     chunks = torch.from_numpy(host).to(device)
     seg_first = torch.tensor(list(first), dtype=torch.int32).to(device)
     return SlerpPlan(list(seg_offsets), chunks, seg_first,
-                     torch.empty(max(1, int(lib.edt_slerp_sums_doubles(3, nchunks))), dtype=torch.float64,
-                                 device=device),
                      torch.empty((max(1, nseg), 2), dtype=torch.float32, device=device),
                      torch.empty(max(1, nseg), dtype=torch.float32, device=device), nchunks, relative, host,
                      int(chunk_elems))
@@ -273,39 +307,104 @@ def make_slerp_plan(seg_offsets: list[int], device: torch.device,
 
 @dataclass(frozen=True)
 class RefDot:
-    """Reference-dot mode for the SLERP branch decision (include/edt_sync.h, edt_slerp_refdot):
-    segments whose fp64 dot lies within `band` of DOT_THRESHOLD (band < 0: every segment) take the
-    reference's own fp32 dot — BLAS sdot norms + numpy's pairwise sum, restated bit for bit for
-    the reference host's numpy / OpenBLAS (`threads` = OpenBLAS's thread count for sdot there; 1 on
-    the pinned host) — and the branch and coefficients that follow from it. Without it (the
-    default) the kernels decide from their fp64 dot, the accurate one."""
+    """Reference-dot mode (include/edt_sync.h, edt_slerp_refdot): segments whose fp64 dot lies
+    within `band` of DOT_THRESHOLD (band < 0: every segment) take the reference's own fp32 dot —
+    BLAS sdot norms + numpy's pairwise sum, restated bit for bit for the reference host's numpy /
+    OpenBLAS (`threads` = OpenBLAS's thread count for sdot there; 1 on the pinned host) — and then
+    EVERY segment's branch and coefficients are formed from its dot exactly as
+    EDT_RL/crossover.py:31-43 forms them: numpy float32 arccos / sin / divisions on the host
+    (reference_coefficients). With band < 0 the merge is the reference's, bit for bit. Without it
+    (the default) the kernels decide from their fp64 dot, the accurate one, and form the
+    coefficients on the device. Every SLERP form takes it (arena, tensor list,
+    population, sharded population); it synchronises the host once per merge."""
     threads: int = 1
     band: float = -1.0
 
 
-def _refdot_pass(plan: SlerpPlan, v0: torch.Tensor, v1: torch.Tensor, t: torch.Tensor, dot_threshold: float,
-                 eps: float, ref: RefDot) -> None:
-    """After edt_slerp_coef: flag segments, recompute their dot the reference's way, overwrite
-    their coefficients and dots (plan.coef / plan.dots)."""
+def reference_coefficients(dots, t, dot_threshold: float = 0.9995):
+    """The reference's branch and (c0, c1) per segment (EDT_RL/crossover.py:31-43,
+    EDT_EVOMERGE/train/crossover.py:34-46) from fp32 dots, evaluated the way the reference does:
+    numpy float32 scalars (NEP 50: the python-float t and 1 - t enter as float32) — arccos, the
+    product th0 * t, sin, two divisions — or, where |dot| > DOT_THRESHOLD, the lerp weights
+    (1 - t, t). numpy's float32 arccos / sin are the reference's own dependency (SVML / numpy's SIMD
+    loops on an AVX-512 host): no device restatement of them is bit-exact. dots: float32 [..., nseg];
+    t: float64 [nseg]. Returns float32 [..., nseg, 2]."""
+    import numpy as np
+    d = np.asarray(dots, dtype=np.float32)
+    tt = np.broadcast_to(np.asarray(t, dtype=np.float64), d.shape)
+    tf = tt.astype(np.float32)
+    with np.errstate(invalid="ignore", divide="ignore", over="ignore"):
+        th0 = np.arccos(d)
+        th_t = th0 * tf
+        s0 = np.sin(th0 - th_t) / np.sin(th0)
+        s1 = np.sin(th_t) / np.sin(th0)
+    lerp = np.abs(d) > np.float32(dot_threshold)
+    out = np.empty(d.shape + (2,), dtype=np.float32)
+    out[..., 0] = np.where(lerp, (1.0 - tt).astype(np.float32), s0)
+    out[..., 1] = np.where(lerp, tf, s1)
+    return out
+
+
+def _refdot_ws(plan: SlerpPlan, ref: RefDot, dev) -> torch.Tensor:
     lib = L.lib()
-    dev, st = v0.device, L.stream_ptr(v0.device)
     need = int(lib.edt_slerp_refdot_workspace_bytes(plan.nseg, plan.nchunks, plan.chunk_elems, int(ref.threads)))
     if need == 0:
         raise L.EdtError(f"reference-dot mode needs chunks of a multiple of 8192 elements (plan: {plan.chunk_elems})")
     ws = getattr(plan, "_refdot_ws", None)
     if ws is None or ws.numel() * 8 < need:
         ws = plan._refdot_ws = torch.empty((need + 7) // 8, dtype=torch.float64, device=dev)
-        plan._refdot_flag = torch.empty(max(1, plan.nseg), dtype=torch.int32, device=dev)
-        plan._refdot_val = torch.empty(max(1, plan.nseg), dtype=torch.float32, device=dev)
-    L.check(lib.edt_slerp_refdot_flags(L.ptr(plan.dots), plan.nseg, float(dot_threshold), float(ref.band),
-                                       L.ptr(plan._refdot_flag), st), "edt_slerp_refdot_flags")
-    L.check(lib.edt_slerp_refdot(L.ptr(v0), L.ptr(v1), L.dtype_code(v0), L.ptr(plan.chunks), plan.nchunks,
-                                 L.ptr(plan.seg_first), plan.nseg, plan.chunk_elems, L.ptr(plan._refdot_flag),
-                                 int(ref.threads), float(eps), L.ptr(plan._refdot_val), L.ptr(ws), ws.numel() * 8, st),
-            "edt_slerp_refdot")
-    L.check(lib.edt_slerp_refdot_coef(L.ptr(plan._refdot_val), L.ptr(plan._refdot_flag), plan.nseg, L.ptr(t),
-                                      float(dot_threshold), L.ptr(plan.coef), L.ptr(plan.dots), st),
-            "edt_slerp_refdot_coef")
+    return ws
+
+
+def _ref_dots(plan: SlerpPlan, dots: torch.Tensor, ref: RefDot, in_dt: int, dot_threshold: float, eps: float,
+              v0: torch.Tensor | None = None, v1: torch.Tensor | None = None, table: torch.Tensor | None = None):
+    """Flag the segments of `dots` (fp32 device [nseg]) within ref.band of the threshold and
+    recompute their dot the reference's way over (v0, v1) arenas or a tensor-list table. Returns the
+    (flag int32, value float32) device tensors; nothing is synchronised."""
+    lib = L.lib()
+    dev, st = dots.device, L.stream_ptr(dots.device)
+    ws = _refdot_ws(plan, ref, dev)
+    flag = torch.empty(max(1, plan.nseg), dtype=torch.int32, device=dev)
+    val = torch.empty(max(1, plan.nseg), dtype=torch.float32, device=dev)
+    L.check(lib.edt_slerp_refdot_flags(L.ptr(dots), plan.nseg, float(dot_threshold), float(ref.band), L.ptr(flag), st),
+            "edt_slerp_refdot_flags")
+    if table is None:
+        L.check(lib.edt_slerp_refdot(L.ptr(v0), L.ptr(v1), in_dt, L.ptr(plan.chunks), plan.nchunks,
+                                     L.ptr(plan.seg_first), plan.nseg, plan.chunk_elems, L.ptr(flag),
+                                     int(ref.threads), float(eps), L.ptr(val), L.ptr(ws), ws.numel() * 8, st),
+                "edt_slerp_refdot")
+    else:
+        L.check(lib.edt_slerp_refdot_table(L.ptr(table), in_dt, L.ptr(plan.chunks), plan.nchunks,
+                                           L.ptr(plan.seg_first), plan.nseg, plan.chunk_elems, L.ptr(flag),
+                                           int(ref.threads), float(eps), L.ptr(val), L.ptr(ws), ws.numel() * 8, st),
+                "edt_slerp_refdot_table")
+    return flag, val
+
+
+def _reference_finish(dots: torch.Tensor, flag: torch.Tensor, val: torch.Tensor, t: torch.Tensor, nseg: int,
+                      dot_threshold: float, coef_used: torch.Tensor | None = None):
+    """Host part of the reference-dot mode (one synchronisation): the final fp32 dots (the
+    reference's where flagged), the reference's coefficients from them, and — given the
+    coefficients a pass already blended with (`coef_used`, [.., nseg, 2]) — the segments whose
+    coefficients changed. dots / flag / val: [..., nseg] device tensors. Returns (dots, coef,
+    changed) as device tensors shaped like the inputs (changed: int32 or None)."""
+    import numpy as np
+    shp = dots.shape
+    d = dots.reshape(-1, dots.shape[-1])[:, :nseg].cpu().numpy()
+    f = flag.reshape(-1, flag.shape[-1])[:, :nseg].cpu().numpy()
+    v = val.reshape(-1, val.shape[-1])[:, :nseg].cpu().numpy()
+    th = t[:nseg].cpu().numpy()
+    final = np.where(f != 0, v, d).astype(np.float32)
+    coef = reference_coefficients(final, th, dot_threshold)
+    dev = dots.device
+    dots_out = torch.from_numpy(final).to(dev).reshape(shp[:-1] + (nseg,))
+    coef_out = torch.from_numpy(coef).to(dev).reshape(shp[:-1] + (nseg, 2))
+    changed = None
+    if coef_used is not None:
+        used = coef_used.reshape(-1, coef_used.shape[-2], 2)[:, :nseg].cpu().numpy()
+        diff = (used.view(np.int32) != coef.view(np.int32)).any(axis=-1).astype(np.int32)
+        changed = torch.from_numpy(diff).to(dev).reshape(shp[:-1] + (nseg,))
+    return dots_out, coef_out, changed
 
 
 def _record_dots(plan: SlerpPlan, dots: torch.Tensor, attr: str) -> None:
@@ -359,6 +458,65 @@ def _overlap(a: torch.Tensor, b: torch.Tensor) -> bool:
     return a0 < b0 + b.numel() * b.element_size() and b0 < a0 + a.numel() * a.element_size()
 
 
+def _pair_ref_merge(plan: SlerpPlan, in_dt: int, out_dt: int, t: torch.Tensor, dot_threshold: float, eps: float,
+                    ref: RefDot, speculate: bool, arena=None, table=None, n: int = 0) -> None:
+    """The reference-dot mode of one pair (flat arenas (v0, v1, out) or a tensor-list table):
+      speculate=True   the speculative merge as usual (every segment's output = the blend with the
+                       device's coefficients), then the reference's dots and coefficients, and a
+                       re-blend of exactly the segments whose coefficients changed;
+      speculate=False  stats -> device coefficients (their dots flag the band) -> the reference's
+                       dots and coefficients -> one blend (an output may alias a parent).
+    Either way every segment ends as the blend with the reference's coefficients: bit-identical
+    across forms and layouts."""
+    lib = L.lib()
+    dev = t.device
+    st = L.stream_ptr(dev)
+    part = plan.partial
+    if arena is not None:
+        v0, v1, out = arena
+    if speculate:
+        redo = torch.empty(max(1, plan.nseg), dtype=torch.int32, device=dev)
+        if arena is not None:
+            L.check(lib.edt_slerp_merge_speculative(
+                L.ptr(v0), L.ptr(v1), in_dt, L.ptr(out), out_dt, L.ptr(plan.chunks), plan.nchunks,
+                L.ptr(plan.seg_first), plan.nseg, L.ptr(t), float(dot_threshold), float(eps), L.ptr(part),
+                L.ptr(plan.coef), L.ptr(plan.dots), L.ptr(redo), n, st), "edt_slerp_merge_speculative")
+        else:
+            L.check(lib.edt_slerp_merge_table_speculative(
+                L.ptr(table), in_dt, out_dt, L.ptr(plan.chunks), plan.nchunks, L.ptr(plan.seg_first), plan.nseg,
+                L.ptr(t), float(dot_threshold), float(eps), L.ptr(part), L.ptr(plan.coef), L.ptr(plan.dots),
+                L.ptr(redo), st), "edt_slerp_merge_table_speculative")
+    else:
+        if arena is not None:
+            L.check(lib.edt_slerp_stats(L.ptr(v0), L.ptr(v1), in_dt, L.ptr(plan.chunks), plan.nchunks, L.ptr(part),
+                                        st), "edt_slerp_stats")
+        else:
+            L.check(lib.edt_slerp_stats_table(L.ptr(table), in_dt, L.ptr(plan.chunks), plan.nchunks, L.ptr(part), st),
+                    "edt_slerp_stats_table")
+        L.check(lib.edt_slerp_coef(L.ptr(part), L.ptr(plan.seg_first), plan.nseg, L.ptr(t), float(dot_threshold),
+                                   float(eps), L.ptr(plan.coef), L.ptr(plan.dots), st), "edt_slerp_coef")
+    if arena is not None:
+        flag, val = _ref_dots(plan, plan.dots, ref, in_dt, dot_threshold, eps, v0=v0, v1=v1)
+    else:
+        flag, val = _ref_dots(plan, plan.dots, ref, in_dt, dot_threshold, eps, table=table)
+    dots, coef, changed = _reference_finish(plan.dots, flag, val, t, plan.nseg, dot_threshold,
+                                            plan.coef if speculate else None)
+    plan.dots[:plan.nseg].copy_(dots)
+    plan.coef[:plan.nseg].copy_(coef)
+    if arena is not None:
+        if speculate:
+            L.check(lib.edt_slerp_blend_segments(L.ptr(v0), L.ptr(v1), in_dt, L.ptr(out), out_dt, L.ptr(plan.chunks),
+                                                 plan.nchunks, L.ptr(plan.coef), L.ptr(changed), st),
+                    "edt_slerp_blend_segments")
+        else:
+            L.check(lib.edt_slerp_blend(L.ptr(v0), L.ptr(v1), in_dt, L.ptr(out), out_dt, L.ptr(plan.chunks),
+                                        plan.nchunks, L.ptr(plan.coef), st), "edt_slerp_blend")
+    else:
+        L.check(lib.edt_slerp_blend_table(L.ptr(table), in_dt, out_dt, L.ptr(plan.chunks), plan.nchunks,
+                                          L.ptr(plan.coef), L.ptr(changed) if speculate else None, st),
+                "edt_slerp_blend_table")
+
+
 def slerp_arena(plan: SlerpPlan, v0: torch.Tensor, v1: torch.Tensor, out: torch.Tensor,
                 t: torch.Tensor, dot_threshold: float = 0.9995, eps: float = 1e-8,
                 speculate: bool | None = None, ref_dot: RefDot | None = None) -> None:
@@ -368,7 +526,7 @@ def slerp_arena(plan: SlerpPlan, v0: torch.Tensor, v1: torch.Tensor, out: torch.
     only SLERP-branch segments blended again); False = the two-pass form; None = whichever the
     previous merge on this plan says is cheaper. Bit-identical results either way; an output
     that overlaps a parent always takes the two-pass form. ref_dot (RefDot): the reference-dot
-    mode, always the split two-pass form: stats -> coef -> refdot -> blend."""
+    mode (the reference's dots and coefficients, bit for bit with band < 0), either form."""
     lib = L.lib()
     L.require_device(v0, v1, out, t)
     if v1.dtype != v0.dtype or v0.numel() != plan.seg_offsets[-1] or v1.numel() != v0.numel() \
@@ -378,25 +536,15 @@ def slerp_arena(plan: SlerpPlan, v0: torch.Tensor, v1: torch.Tensor, out: torch.
         raise L.EdtError("t must be a float64 device tensor with one value per segment")
     if plan.relative:
         raise L.EdtError("a relative (tensor-list) plan drives slerp_list, not slerp_arena")
-    if ref_dot is not None:
-        st = L.stream_ptr(v0.device)
-        L.check(lib.edt_slerp_stats(L.ptr(v0), L.ptr(v1), L.dtype_code(v0), L.ptr(plan.chunks), plan.nchunks,
-                                    L.ptr(plan.partial), st), "edt_slerp_stats")
-        L.check(lib.edt_slerp_coef(L.ptr(plan.partial), L.ptr(plan.seg_first), plan.nseg, L.ptr(t),
-                                   float(dot_threshold), float(eps), L.ptr(plan.coef), L.ptr(plan.dots), st),
-                "edt_slerp_coef")
-        _refdot_pass(plan, v0, v1, t, dot_threshold, eps, ref_dot)
-        L.check(lib.edt_slerp_blend(L.ptr(v0), L.ptr(v1), L.dtype_code(v0), L.ptr(out), L.dtype_code(out),
-                                    L.ptr(plan.chunks), plan.nchunks, L.ptr(plan.coef), st), "edt_slerp_blend")
-        plan._last_thr = float(dot_threshold)
-        _record_dots(plan, plan.dots[:max(1, plan.nseg)], "_dots")
-        return
     if speculate is None:
         speculate = _speculation_pays(plan, v0.element_size(), out.element_size(), wait=False)
         plan._last_speculate = speculate
     if speculate and (_overlap(out, v0) or _overlap(out, v1)):
         speculate = False
-    if speculate:
+    if ref_dot is not None:
+        _pair_ref_merge(plan, L.dtype_code(v0), L.dtype_code(out), t, dot_threshold, eps, ref_dot, speculate,
+                        arena=(v0, v1, out), n=v0.numel())
+    elif speculate:
         redo = getattr(plan, "_redo", None)
         if redo is None:
             redo = plan._redo = torch.empty(max(1, plan.nseg), dtype=torch.int32, device=v0.device)
@@ -414,85 +562,146 @@ def slerp_arena(plan: SlerpPlan, v0: torch.Tensor, v1: torch.Tensor, out: torch.
     _record_dots(plan, plan.dots[:max(1, plan.nseg)], "_dots")
 
 
-def _spans_apart(out_ptrs, out_bytes, in_ptrs, in_bytes) -> bool:
-    """No output span [ptr, ptr + bytes) overlaps an input span: spans sorted by start, each checked
-    against the furthest end of the other kind before it (numpy; empty spans ignored)."""
-    import numpy as np
-    a = np.concatenate((np.asarray(in_ptrs, dtype=np.int64), np.asarray(out_ptrs, dtype=np.int64)))
-    n = np.concatenate((np.asarray(in_bytes, dtype=np.int64), np.asarray(out_bytes, dtype=np.int64)))
-    k = np.concatenate((np.zeros(len(in_ptrs), dtype=bool), np.ones(len(out_ptrs), dtype=bool)))
-    keep = n > 0
-    a, n, k = a[keep], n[keep], k[keep]
-    if a.size == 0:
-        return True
-    o = np.argsort(a, kind="stable")
-    a, e, k = a[o], a[o] + n[o], k[o]
-    far_out = np.maximum.accumulate(np.where(k, e, -1))       # furthest end of an output so far
-    far_in = np.maximum.accumulate(np.where(k, -1, e))
-    prev_out = np.concatenate(([-1], far_out[:-1]))
-    prev_in = np.concatenate(([-1], far_in[:-1]))
-    return not bool(np.any(np.where(k, a < prev_in, a < prev_out)))
+class SlerpListBinding:
+    """A tensor-list SLERP bound to its tensors (EDT_EVOMERGE/train/crossover.py:104-146's state-dict
+    tensors, merged where they lie): the per-tensor checks run once here and the validated
+    {v0, v1, out} pointer table (edt_slerp_seg_table) is uploaded once, so `merge` costs no
+    per-tensor host work. The tensors must stay where they are while the binding is used (it keeps
+    references to them; rebinding a module's parameters elsewhere needs a new binding)."""
+
+    def __init__(self, plan: SlerpPlan, v0s, v1s, outs):
+        import numpy as np
+        lib = L.lib()
+        T = len(v0s)
+        if not plan.relative or T != plan.nseg or len(v1s) != T or len(outs) != T:
+            raise L.EdtError("slerp_list needs a relative plan with one segment per tensor")
+        self.device = L.require_device(*v0s, *v1s, *outs)
+        in_dt, out_dt = (v0s[0].dtype, outs[0].dtype) if T else (torch.float32, torch.float32)
+        sizes = plan.seg_numel
+        for i in range(T):
+            n = int(sizes[i])
+            if v0s[i].numel() != n or v1s[i].numel() != n or outs[i].numel() != n:
+                raise L.EdtError(f"tensor {i} does not match the plan's layout")
+            if v0s[i].dtype != in_dt or v1s[i].dtype != in_dt or outs[i].dtype != out_dt:
+                raise L.EdtError("slerp_list: one input dtype and one output dtype")
+        self.plan, self.in_dt, self.out_dt = plan, L.dtype_code(in_dt), L.dtype_code(out_dt)
+        self.in_size, self.out_size = torch.empty(0, dtype=in_dt).element_size(), torch.empty(0, dtype=out_dt).element_size()
+        self._keep = (list(v0s), list(v1s), list(outs))
+        arr = [(ctypes.c_void_p * max(1, T))(*[x.data_ptr() for x in ts]) for ts in self._keep]
+        numel = (ctypes.c_uint64 * max(1, T))(*[int(x) for x in sizes])
+        host = np.zeros(max(1, 3 * T), dtype=np.uint64)
+        hp = host.ctypes.data_as(ctypes.c_void_p)
+        L.check(lib.edt_slerp_seg_table(arr[0], arr[1], arr[2], T, numel, self.in_dt, self.out_dt, 0, hp),
+                "edt_slerp_seg_table")
+        # outputs apart from every parent (a sorted-span check in C): the single-pass form is allowed
+        self.apart = lib.edt_slerp_seg_table(arr[0], arr[1], arr[2], T, numel, self.in_dt, self.out_dt, 1, hp) == 0
+        self.table = torch.from_numpy(host.view(np.int64)).to(self.device)
+
+    def merge(self, t: torch.Tensor, dot_threshold: float = 0.9995, eps: float = 1e-8,
+              speculate: bool | None = None, ref_dot: RefDot | None = None) -> None:
+        """slerp_list's merge over the bound tensors (same forms, same results)."""
+        lib, plan = L.lib(), self.plan
+        if t.dtype != torch.float64 or t.numel() < plan.nseg or t.device != self.device:
+            raise L.EdtError("t must be a float64 tensor on the tensors' device with one value per segment")
+        if speculate is None:
+            speculate = _speculation_pays(plan, self.in_size, self.out_size, wait=False)
+            plan._last_speculate = speculate
+        speculate = bool(speculate and self.apart)
+        st = L.stream_ptr(self.device)
+        if ref_dot is not None:
+            _pair_ref_merge(plan, self.in_dt, self.out_dt, t, dot_threshold, eps, ref_dot, speculate, table=self.table)
+        elif speculate:
+            redo = getattr(plan, "_redo", None)
+            if redo is None:
+                redo = plan._redo = torch.empty(max(1, plan.nseg), dtype=torch.int32, device=self.device)
+            L.check(lib.edt_slerp_merge_table_speculative(
+                L.ptr(self.table), self.in_dt, self.out_dt, L.ptr(plan.chunks), plan.nchunks, L.ptr(plan.seg_first),
+                plan.nseg, L.ptr(t), float(dot_threshold), float(eps), L.ptr(plan.partial), L.ptr(plan.coef),
+                L.ptr(plan.dots), L.ptr(redo), st), "edt_slerp_merge_table_speculative")
+        else:
+            L.check(lib.edt_slerp_merge_table(
+                L.ptr(self.table), self.in_dt, self.out_dt, L.ptr(plan.chunks), plan.nchunks, L.ptr(plan.seg_first),
+                plan.nseg, L.ptr(t), float(dot_threshold), float(eps), L.ptr(plan.partial), L.ptr(plan.coef),
+                L.ptr(plan.dots), st), "edt_slerp_merge_table")
+        plan._last_thr = float(dot_threshold)
+        _record_dots(plan, plan.dots[:max(1, plan.nseg)], "_dots")
+
+
+def bind_slerp_list(plan: SlerpPlan, v0s, v1s, outs) -> SlerpListBinding:
+    """A SlerpListBinding: validate once, merge many times without per-tensor host work."""
+    return SlerpListBinding(plan, v0s, v1s, outs)
 
 
 def slerp_list(plan: SlerpPlan, v0s: list[torch.Tensor], v1s: list[torch.Tensor], outs: list[torch.Tensor],
                t: torch.Tensor, dot_threshold: float = 0.9995, eps: float = 1e-8,
-               speculate: bool | None = None) -> None:
+               speculate: bool | None = None, ref_dot: RefDot | None = None) -> None:
     """`slerp_arena` over separate tensors (one segment each, e.g. two models' state-dict
     tensors), writing straight into `outs` (e.g. the target model's parameters): no packing.
     Every tensor must be contiguous and 16-byte aligned; plan = make_slerp_plan(...,
-    relative=True) over the tensors' sizes. speculate as slerp_arena's: True =
-    edt_slerp_merge_list_speculative (lerp-branch outputs written in the sums pass, only
-    SLERP-branch tensors blended again), False = the two-pass edt_slerp_merge_list, None = the
-    cheaper by the previous merge's dots on this plan; outputs that overlap a parent (e.g. merged
-    into the first parent's own tensors) always take the two-pass form. Bit-identical either way."""
+    relative=True) over the tensors' sizes. speculate as slerp_arena's: True = the single-pass
+    form (lerp-branch outputs written in the sums pass, only SLERP-branch tensors blended again),
+    False = the two-pass form, None = the cheaper by the previous merge's dots on this plan;
+    outputs that overlap any parent (e.g. merged into the first parent's own tensors) always take
+    the two-pass form. Bit-identical either way. ref_dot: the reference-dot mode, as slerp_arena's.
+    Validates and uploads the tensors' pointer table on every call; a caller that merges the same
+    tensors again holds a `bind_slerp_list` binding instead."""
+    SlerpListBinding(plan, v0s, v1s, outs).merge(t, dot_threshold, eps, speculate, ref_dot)
+
+
+def _population_ref(plan: SlerpPlan, members, pairs, outs, t, dots, coef_used, in_dt, out_dt, dot_threshold, eps,
+                    ref: RefDot, blend_all: bool):
+    """Reference-dot mode for every child of a population: per child the reference's dots over its
+    two parents (flagged by that child's dots), the reference's coefficients, then either the
+    blend of every child (blend_all: no output written yet) or per child the re-blend of the
+    segments whose coefficients changed. Returns (dots, coef) [Q, nseg(, 2)]."""
     lib = L.lib()
-    T = len(v0s)
-    if not plan.relative or T != plan.nseg or len(v1s) != T or len(outs) != T:
-        raise L.EdtError("slerp_list needs a relative plan with one segment per tensor")
-    L.require_device(*v0s, *v1s, *outs, t)
-    in_dt, out_dt = v0s[0].dtype, outs[0].dtype
-    for i in range(T):
-        n = plan.seg_offsets[i + 1] - plan.seg_offsets[i]
-        if v0s[i].numel() != n or v1s[i].numel() != n or outs[i].numel() != n:
-            raise L.EdtError(f"tensor {i} does not match the plan's layout")
-        if v0s[i].dtype != in_dt or v1s[i].dtype != in_dt or outs[i].dtype != out_dt:
-            raise L.EdtError("slerp_list: one input dtype and one output dtype")
-    if t.dtype != torch.float64 or t.numel() < T:
-        raise L.EdtError("t must be a float64 device tensor with one value per segment")
-    ws = torch.empty(max(1, 3 * T), dtype=torch.int64, device=t.device)
-    p0, p1, po = ([x.data_ptr() for x in ts] for ts in (v0s, v1s, outs))
-    if speculate is None:
-        speculate = _speculation_pays(plan, v0s[0].element_size(), outs[0].element_size(), wait=False)
-        plan._last_speculate = speculate
-    if speculate:
-        import numpy as np
-        n = np.diff(np.asarray(plan.seg_offsets, dtype=np.int64))
-        nin, nout = n * v0s[0].element_size(), n * outs[0].element_size()
-        speculate = _spans_apart(po, nout, p0 + p1, np.concatenate((nin, nin)))
-    tab = [(ctypes.c_void_p * max(1, T))(*p) for p in (p0, p1, po)]
-    st = L.stream_ptr(t.device)
-    if speculate:
-        redo = getattr(plan, "_redo", None)
-        if redo is None:
-            redo = plan._redo = torch.empty(max(1, plan.nseg), dtype=torch.int32, device=t.device)
-        L.check(lib.edt_slerp_merge_list_speculative(
-            tab[0], tab[1], L.dtype_code(in_dt), tab[2], L.dtype_code(out_dt),
-            L.ptr(plan.chunks), plan.nchunks, L.ptr(plan.seg_first), T, L.ptr(t), float(dot_threshold), float(eps),
-            L.ptr(plan.partial), L.ptr(plan.coef), L.ptr(plan.dots), L.ptr(redo), L.ptr(ws), ws.numel() * 8, st),
-            "edt_slerp_merge_list_speculative")
+    Q, dev = len(pairs), t.device
+    st = L.stream_ptr(dev)
+    flags, vals = [], []
+    for q, (i, j) in enumerate(pairs):
+        f, v = _ref_dots(plan, dots[q], ref, in_dt, dot_threshold, eps, v0=members[i], v1=members[j])
+        flags.append(f)
+        vals.append(v)
+    fd, cd, changed = _reference_finish(dots[:Q], torch.stack(flags), torch.stack(vals), t, plan.nseg,
+                                        dot_threshold, None if blend_all else coef_used[:Q])
+    coef = torch.empty((max(1, Q), max(1, plan.nseg), 2), dtype=torch.float32, device=dev)
+    coef[:Q, :plan.nseg].copy_(cd)
+    if blend_all:
+        for q0 in range(0, Q, 16):
+            q1 = min(Q, q0 + 16)
+            slerp_blend_children(members, pairs[q0:q1], outs[q0:q1], plan.chunks, plan.nchunks,
+                                 coef[q0:q1].contiguous(), max(1, plan.nseg))
     else:
-        L.check(lib.edt_slerp_merge_list(tab[0], tab[1], L.dtype_code(in_dt),
-                                         tab[2], L.dtype_code(out_dt), L.ptr(plan.chunks), plan.nchunks,
-                                         L.ptr(plan.seg_first), T, L.ptr(t), float(dot_threshold), float(eps),
-                                         L.ptr(plan.partial), L.ptr(plan.coef), L.ptr(plan.dots), L.ptr(ws),
-                                         ws.numel() * 8, st), "edt_slerp_merge_list")
-    plan._last_thr = float(dot_threshold)
-    _record_dots(plan, plan.dots[:max(1, plan.nseg)], "_dots")
+        for q, (i, j) in enumerate(pairs):
+            L.check(lib.edt_slerp_blend_segments(L.ptr(members[i]), L.ptr(members[j]), in_dt, L.ptr(outs[q]), out_dt,
+                                                 L.ptr(plan.chunks), plan.nchunks, L.ptr(coef[q]), L.ptr(changed[q]),
+                                                 st), "edt_slerp_blend_segments")
+    return fd, coef
+
+
+def slerp_refdot(v0: torch.Tensor, v1: torch.Tensor, chunks: torch.Tensor, seg_first: torch.Tensor, nseg: int,
+                 chunk_elems: int, flag: torch.Tensor, ref: RefDot, eps: float = 1e-8) -> torch.Tensor:
+    """The reference's fp32 dot (edt_slerp_refdot) of the flagged segments (flag: int32 device
+    [nseg]) of a chunk table over two flat buffers (chunk starts relative to them; seg_first: int32
+    device [nseg + 1] indexing the table's rows). float32 [nseg] device; unflagged entries are
+    undefined. The sharded population's per-rank pass (distributed.ShardedPopulationCrossover)."""
+    lib = L.lib()
+    dev = L.require_device(v0, v1, chunks, seg_first, flag)
+    nchunks = int(chunks.shape[0]) if chunks.dim() == 2 else int(chunks.numel()) // 3
+    need = int(lib.edt_slerp_refdot_workspace_bytes(nseg, nchunks, int(chunk_elems), int(ref.threads)))
+    if need == 0:
+        raise L.EdtError(f"reference-dot mode needs chunks of a multiple of 8192 elements (got {chunk_elems})")
+    ws = torch.empty((need + 7) // 8, dtype=torch.float64, device=dev)
+    val = torch.empty(max(1, nseg), dtype=torch.float32, device=dev)
+    L.check(lib.edt_slerp_refdot(L.ptr(v0), L.ptr(v1), L.dtype_code(v0), L.ptr(chunks), nchunks, L.ptr(seg_first),
+                                 nseg, int(chunk_elems), L.ptr(flag), int(ref.threads), float(eps), L.ptr(val),
+                                 L.ptr(ws), ws.numel() * 8, L.stream_ptr(dev)), "edt_slerp_refdot")
+    return val
 
 
 def slerp_population(plan: SlerpPlan, members: list[torch.Tensor], pairs, outs: list[torch.Tensor],
                      t: torch.Tensor, dot_threshold: float = 0.9995, eps: float = 1e-8,
-                     speculate: bool | None = None) -> torch.Tensor:
+                     speculate: bool | None = None, ref_dot: RefDot | None = None) -> torch.Tensor:
     """SLERP child q of members[pairs[q][0]], members[pairs[q][1]] into outs[q], for every q
     (EDT_RL/edt.py:286-299 -> EDT_RL/crossover.py:84-135 per child). Two forms, bit-identical to
     slerp_arena per child:
@@ -504,6 +713,8 @@ def slerp_population(plan: SlerpPlan, members: list[torch.Tensor], pairs, outs: 
       None             speculate when the previous call on this plan had few enough child elements
                        in SLERP-branch segments for the single pass to move fewer bytes
                        (f < D b_in / (D b_in + Q b_out), D distinct parents, Q children).
+    ref_dot: the reference-dot mode per child (as slerp_arena's; the Gram form runs its passes
+    separately: Gram sums -> coefficients' dots -> the reference's dots and coefficients -> blends).
     Returns the per-child, per-segment fp32 dots ([npairs, nseg])."""
     lib = L.lib()
     M, Q = len(members), len(pairs)
@@ -542,22 +753,35 @@ def slerp_population(plan: SlerpPlan, members: list[torch.Tensor], pairs, outs: 
     coef = torch.empty((max(1, Q), max(1, plan.nseg), 2), dtype=torch.float32, device=dev)
     dots = torch.empty((max(1, Q), max(1, plan.nseg)), dtype=torch.float32, device=dev)
     flat_pairs = (ctypes.c_int32 * max(1, 2 * Q))(*[int(x) for p in pairs for x in p])
-    if speculate:
-        part = torch.empty(max(1, int(lib.edt_slerp_population_speculative_doubles(Q, plan.nchunks))),
-                           dtype=torch.float64, device=dev)
+    icode, ocode = L.dtype_code(in_dt), L.dtype_code(out_dt)
+    if ref_dot is not None and not speculate and Q:
+        # the Gram form's passes separately: sums -> dots -> the reference's coefficients -> blends
+        gram = getattr(plan, "_gram", None)
+        need = int(lib.edt_slerp_population_gram_doubles(M, plan.nchunks))
+        if gram is None or gram.numel() < max(1, need):
+            gram = plan._gram = torch.empty(max(1, need), dtype=torch.float64, device=dev)
+        slerp_gram(members, plan.chunks, plan.nchunks, work=gram)
+        _, dots = slerp_gram_coef(plan, gram, M, pairs, t, dot_threshold, eps)
+        dots, coef = _population_ref(plan, members, pairs, outs, t, dots, None, icode, ocode, dot_threshold, eps,
+                                     ref_dot, blend_all=True)
+    elif speculate:
+        part = _scratch(dev, int(lib.edt_slerp_population_speculative_doubles(Q, plan.nchunks)))
         redo = torch.empty(max(1, Q * plan.nseg), dtype=torch.int32, device=dev)
         L.check(lib.edt_slerp_population_speculative(
-            L.ptr_array(members), M, L.dtype_code(in_dt), flat_pairs, Q, L.ptr_array(outs), L.dtype_code(out_dt),
+            L.ptr_array(members), M, icode, flat_pairs, Q, L.ptr_array(outs), ocode,
             L.ptr(plan.chunks), plan.nchunks, L.ptr(plan.seg_first), plan.nseg, L.ptr(t), float(dot_threshold),
             float(eps), L.ptr(part), L.ptr(coef), L.ptr(dots), L.ptr(redo), n, L.stream_ptr(dev)),
             "edt_slerp_population_speculative")
+        if ref_dot is not None and Q:
+            dots, coef = _population_ref(plan, members, pairs, outs, t, dots, coef, icode, ocode, dot_threshold, eps,
+                                         ref_dot, blend_all=False)
     else:
         need = int(lib.edt_slerp_population_gram_doubles(M, plan.nchunks))
         gram = getattr(plan, "_gram", None)
         if gram is None or gram.numel() < max(1, need):
             gram = plan._gram = torch.empty(max(1, need), dtype=torch.float64, device=dev)
-        L.check(lib.edt_slerp_population(L.ptr_array(members), M, L.dtype_code(in_dt), flat_pairs, Q,
-                                         L.ptr_array(outs), L.dtype_code(out_dt), L.ptr(plan.chunks), plan.nchunks,
+        L.check(lib.edt_slerp_population(L.ptr_array(members), M, icode, flat_pairs, Q,
+                                         L.ptr_array(outs), ocode, L.ptr(plan.chunks), plan.nchunks,
                                          L.ptr(plan.seg_first), plan.nseg, L.ptr(t), float(dot_threshold), float(eps),
                                          L.ptr(gram), L.ptr(coef), L.ptr(dots), L.stream_ptr(dev)),
                 "edt_slerp_population")
@@ -605,10 +829,12 @@ def pair_merge_population(children, lr: float, momentum_coef: float, nesterov: b
 # the population SLERP's three passes, separately (distributed.ShardedSlerpPopulation)
 
 def slerp_gram(members: list[torch.Tensor], chunks: torch.Tensor, nchunks: int,
-               gram: torch.Tensor | None = None) -> torch.Tensor:
+               gram: torch.Tensor | None = None, work: torch.Tensor | None = None) -> torch.Tensor:
     """Per-chunk Gram sums of M <= 8 member buffers over a chunk table (int64 [nchunks, 3] on the
     device, starts relative to the buffers): float64 [nchunks, M(M+1)/2] (edt_slerp_gram). `gram`
-    (optional) receives the rows; its first nchunks x M(M+1)/2 elements are written."""
+    (optional) receives the rows; its first nchunks x M(M+1)/2 elements are written. `work`
+    (optional, float64, >= edt_slerp_population_gram_doubles(M, nchunks)): the pass's workspace
+    when `gram` cannot hold the row scratch too (default: the stream's pooled workspace)."""
     lib = L.lib()
     M = len(members)
     L.require_device(*members, chunks)
@@ -621,7 +847,10 @@ def slerp_gram(members: list[torch.Tensor], chunks: torch.Tensor, nchunks: int,
     # the kernel needs the rows plus its slot scratch behind them; a smaller (or non-contiguous)
     # `gram` — e.g. a rank's rows of the whole table — gets its rows copied from a full-size buffer
     direct = gram is not None and gram.is_contiguous() and gram.numel() >= need
-    work = gram if direct else torch.empty(need, dtype=torch.float64, device=members[0].device)
+    if direct:
+        work = gram
+    elif work is None or work.dtype != torch.float64 or not work.is_contiguous() or work.numel() < need:
+        work = _scratch(members[0].device, need)
     L.check(lib.edt_slerp_gram(L.ptr_array(members), M, L.dtype_code(members[0]), L.ptr(chunks), nchunks,
                                L.ptr(work), L.stream_ptr(members[0].device)), "edt_slerp_gram")
     rows = work.view(-1)[:nchunks * NT].view(nchunks, NT) if not direct else gram

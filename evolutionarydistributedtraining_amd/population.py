@@ -57,7 +57,7 @@ class ResidentPopulation:
                  lr: float = 0.7, momentum: float = 0.9, nesterov: bool = True,
                  dot_threshold: float = 0.9995, eps: float = 1e-8, elitism: int = 0,
                  group=None, kernels=None, keep_previous: bool = False, slerp_chunk: int | None = None,
-                 comm=None, exchange: str = "per_child", exchange_groups: int = 1):
+                 comm=None, exchange: str = "per_child", exchange_groups: int = 1, ref_dot=None):
         if kind not in ("sgd", "slerp"):
             raise ValueError(kind)
         if kind == "sgd":
@@ -93,6 +93,8 @@ class ResidentPopulation:
         self._sharded = None
         self.lr, self.momentum, self.nesterov = lr, momentum, nesterov
         self.dot_threshold, self.eps = dot_threshold, eps
+        # SLERP: ops.RefDot = the reference host's own dots and coefficients (bit for bit, band < 0)
+        self.ref_dot = ref_dot
         self.elitism = elitism
         self.generation = 0
         self.genomes = [dict(g) for g in genomes]
@@ -366,16 +368,17 @@ class ResidentPopulation:
         where = {m: q for q, m in enumerate(srcs)}
         args = (self._plan, [got[m][0] for m in srcs], [(where[pairs[c][0]], where[pairs[c][1]]) for c in local],
                 [self._child[self._local(c)] for c in local], self._t, self.dot_threshold, self.eps)
+        rd = {"ref_dot": self.ref_dot} if self.ref_dot is not None else {}
         if hasattr(k, "slerp_population") and len(srcs) <= 8:
-            k.slerp_population(*args)
+            k.slerp_population(*args, **rd)
             return
         if hasattr(k, "slerp_population") and len(local) <= 16:
-            k.slerp_population(*args, speculate=True)
+            k.slerp_population(*args, speculate=True, **rd)
             return
         for c in local:
             i, j = pairs[c]
             k.slerp_arena(self._plan, got[i][0], got[j][0], self._child[self._local(c)], self._t,
-                          self.dot_threshold, self.eps)
+                          self.dot_threshold, self.eps, **rd)
 
     def _sharded_children(self, pairs):
         """This rank's child through the link-balanced schedule (bit-identical to the per-child
@@ -388,7 +391,8 @@ class ResidentPopulation:
                                                        groups=self.exchange_groups)
         m = self.rank
         if self.kind == "slerp":
-            self._sharded.slerp_step(self._params[0], pairs, self._t, self._child[0], self.dot_threshold, self.eps)
+            self._sharded.slerp_step(self._params[0], pairs, self._t, self._child[0], self.dot_threshold, self.eps,
+                                     ref_dot=self.ref_dot)
             return
         has = self.has_momentum[m] and self.momentum != 0
         self._sharded.pair_merge_step(self._base[0], self._trained[0], self._mom[0] if has else None, pairs,

@@ -24,9 +24,20 @@
 
 #include <stdint.h>
 
+/* ABI revision. 4 (round 4): the tensor-list SLERP reads a device pointer table
+ * (edt_slerp_seg_table + the *_table entries), edt_slerp_merge_list_speculative takes the segment
+ * sizes (full byte-range overlap check), edt_slerp_blend_segments / _blend_table / _refdot_table
+ * added, the on-chip-hold form removed. Workspace sizes come from the *_doubles / *_bytes functions
+ * of THIS build: a consumer compiled against another revision must be rebuilt
+ * (edt_abi_version() != EDT_ABI_VERSION: refuse to run). */
+#define EDT_ABI_VERSION 4
+
 #ifdef __cplusplus
 extern "C" {
 #endif
+
+/* EDT_ABI_VERSION of the loaded library. */
+int edt_abi_version(void);
 
 typedef enum { EDT_F32 = 0, EDT_BF16 = 1 } edt_dtype_t;
 
@@ -214,27 +225,6 @@ int edt_slerp_merge(const void* v0, const void* v1, int in_dt, void* out, int ou
                     const double* t, double dot_threshold, double eps, double* partial, float* coef,
                     float* dot_out, void* stream);
 
-/* edt_slerp_merge for bf16 parents (flat arenas) in ONE persistent launch that keeps part of the
- * parents on chip: per phase (runs of whole segments) the chip forms the chunk sums, holds the
- * last groups each wave read in registers, and blends them once the phase's coefficients are
- * published in-launch; the rest of the phase is read again. Same workspace (`partial`,
- * edt_slerp_sums_doubles(3, nchunks) doubles) and arguments as edt_slerp_merge; outputs, chunk
- * sums (partial[0, 3 nchunks)), coefficients and dots are bit-identical to it. `out` may be one
- * of the parents or disjoint from both. in_dt must be EDT_BF16. Needs every workgroup of its grid
- * resident (cooperative launch); each in-launch wait is bounded: edt_slerp_hold_status reports
- * whether one expired. MEASURED SLOWER than edt_slerp_merge on MI355X (7B body, far parents:
- * 16.9 ms against 11.3 ms; the same launch holding nothing 15.6 ms): the registers
- * that hold parents are the ones a streaming wave needs for loads in flight. Kept for A/B. */
-int edt_slerp_merge_hold(const void* v0, const void* v1, int in_dt, void* out, int out_dt,
-                         const uint64_t* chunk_desc, int64_t nchunks, const int32_t* seg_first_chunk, int nseg,
-                         const double* t, double dot_threshold, double eps, double* partial, float* coef,
-                         float* dot_out, void* stream);
-
-/* Synchronises `stream`, then returns 0 when the last edt_slerp_merge_hold on this workspace
- * completed, 1 when one of its in-launch waits expired (the outputs are then undefined), < 0 on
- * error. */
-int edt_slerp_hold_status(const double* partial, int64_t nchunks, void* stream);
-
 /* edt_slerp_merge with a speculative first pass: the chunk sums and, in the same pass, the
  * lerp-branch output (1-t) v0 + t v1 of every segment; the coefficients then flag (redo[s] = 1,
  * nseg int32 of device workspace) the segments whose |dot| <= dot_threshold, and only their
@@ -250,12 +240,38 @@ int edt_slerp_merge_speculative(const void* v0, const void* v1, int in_dt, void*
 
 /* Tensor-list form of edt_slerp_merge: segment i is its own tensor pair v0_t[i], v1_t[i] and is
  * written to out_t[i] (host arrays of nseg device pointers, each 16-byte aligned; NULL only for
- * empty segments), e.g. two
- * models' state-dict tensors merged straight into a third model's parameters
- * (EDT_EVOMERGE/train/crossover.py:104-146 without the state-dict copies). chunk_desc holds
- * starts RELATIVE to their segment (edt_slerp_make_chunks output minus seg_offsets[segment]).
- * The pointer table (24 bytes per segment) is copied into `workspace` (device, 8-byte aligned)
- * by a stream-ordered copy. */
+ * empty segments), e.g. two models' state-dict tensors merged straight into a third model's
+ * parameters (EDT_EVOMERGE/train/crossover.py:104-146 without the state-dict copies). chunk_desc
+ * holds starts RELATIVE to their segment (edt_slerp_make_chunks output minus
+ * seg_offsets[segment]). The kernels read the tensors through a DEVICE table of 3 x nseg uint64
+ * {v0, v1, out} pointers:
+ *   edt_slerp_seg_table   (HOST) validates the arrays (alignment; with `apart`, no output byte
+ *                         range [out, out + n*osize) overlaps any parent range — a sorted-span
+ *                         check over every tensor, seg_numel = the nseg sizes) and writes the
+ *                         table's host image (3 x nseg uint64). The caller uploads it once and
+ *                         reuses it while the tensors stay where they are: the *_table entries
+ *                         below then cost no per-tensor host work per call.
+ *   edt_slerp_merge_table / _speculative   edt_slerp_merge / _speculative over the table (the
+ *                         speculative one needs a table validated with apart = 1)
+ *   edt_slerp_stats_table / edt_slerp_blend_table   the passes alone; blend: redo (nseg int32,
+ *                         nullable) restricts it to segments with redo[s] != 0
+ *   edt_slerp_merge_list / _list_speculative   the same from host pointer arrays: the table is
+ *                         validated and copied into `workspace` (24 bytes per segment, device,
+ *                         8-byte aligned) by a stream-ordered copy on every call. */
+int edt_slerp_seg_table(const void* const* v0_t, const void* const* v1_t, void* const* out_t, int nseg,
+                        const uint64_t* seg_numel, int in_dt, int out_dt, int apart, uint64_t* table_host);
+int edt_slerp_stats_table(const uint64_t* seg_table, int in_dt, const uint64_t* chunk_desc, int64_t nchunks,
+                          double* partial, void* stream);
+int edt_slerp_blend_table(const uint64_t* seg_table, int in_dt, int out_dt, const uint64_t* chunk_desc,
+                          int64_t nchunks, const float* coef, const int32_t* redo, void* stream);
+int edt_slerp_merge_table(const uint64_t* seg_table, int in_dt, int out_dt, const uint64_t* chunk_desc,
+                          int64_t nchunks, const int32_t* seg_first_chunk, int nseg, const double* t,
+                          double dot_threshold, double eps, double* partial, float* coef, float* dot_out,
+                          void* stream);
+int edt_slerp_merge_table_speculative(const uint64_t* seg_table, int in_dt, int out_dt, const uint64_t* chunk_desc,
+                                      int64_t nchunks, const int32_t* seg_first_chunk, int nseg, const double* t,
+                                      double dot_threshold, double eps, double* partial, float* coef,
+                                      float* dot_out, int32_t* redo, void* stream);
 int edt_slerp_merge_list(const void* const* v0_t, const void* const* v1_t, int in_dt,
                          void* const* out_t, int out_dt, const uint64_t* chunk_desc, int64_t nchunks,
                          const int32_t* seg_first_chunk, int nseg, const double* t,
@@ -266,15 +282,23 @@ int edt_slerp_merge_list(const void* const* v0_t, const void* const* v1_t, int i
  * lerp-branch output of every tensor in one pass over the tensors where they lie; only tensors
  * whose |dot| <= dot_threshold (redo[s] = 1, nseg int32 of device workspace) are blended again.
  * Parents of one lineage cost one pass instead of two. Outputs, sums and dots are bit-identical
- * to edt_slerp_merge_list. Every out_t[i] must be apart from every parent tensor (an output equal
- * to its own parent is rejected; the two-pass list form takes that case); `partial` as
- * edt_slerp_merge_speculative's (its last double holds the any-redo word). */
+ * to edt_slerp_merge_list. No output may overlap any parent tensor (checked over the byte ranges
+ * from seg_numel, the nseg sizes on the host: EDT_ERR_ARG, and the two-pass list form takes
+ * that case); `partial` as edt_slerp_merge_speculative's (its last double holds the any-redo
+ * word). */
 int edt_slerp_merge_list_speculative(const void* const* v0_t, const void* const* v1_t, int in_dt,
-                                     void* const* out_t, int out_dt, const uint64_t* chunk_desc, int64_t nchunks,
+                                     void* const* out_t, int out_dt, const uint64_t* seg_numel,
+                                     const uint64_t* chunk_desc, int64_t nchunks,
                                      const int32_t* seg_first_chunk, int nseg, const double* t,
                                      double dot_threshold, double eps, double* partial, float* coef,
                                      float* dot_out, int32_t* redo, void* workspace, uint64_t workspace_bytes,
                                      void* stream);
+
+/* out = coef0*v0 + coef1*v1 (edt_slerp_blend's math) over the chunks whose segment has
+ * redo[s] != 0 only (nseg int32, device): the flat-arena re-blend of selected segments. */
+int edt_slerp_blend_segments(const void* v0, const void* v1, int in_dt, void* out, int out_dt,
+                             const uint64_t* chunk_desc, int64_t nchunks, const float* coef, const int32_t* redo,
+                             void* stream);
 
 /* SLERP children of a resident population (EDT_RL/edt.py:286-299: every selected pair of one
  * generation, EDT_RL/crossover.py:84-135 per child) in 2 + 2*npairs launches: ONE pass over the
@@ -295,10 +319,8 @@ int edt_slerp_population(const void* const* members, int nmembers, int in_dt, co
  * (every child of a chunk on one XCD, shared parents read once) forms each child's chunk sums and
  * writes its lerp-branch output; per child the coefficients flag (redo: [npairs][nseg] int32) the
  * SLERP-branch segments, which one co-located launch blends again (it exits at once when no child
- * needs any). A build with EDT_SLERP_POP_FUSED=1 makes the first pass member-major instead when the
- * children's distinct parents number <= 8 (and npairs <= 16): one launch loads each distinct
- * parent's tile once, forms their Gram sums and writes every child's lerp output (slower with the
- * canonical sum order: DESIGN §6.9).
+ * needs any). (A member-major first pass measured slower with the canonical sum order and was
+ * removed: DESIGN §6.9.)
  * partial: edt_slerp_population_speculative_doubles(npairs, nchunks) doubles of workspace.
  * Outputs must not overlap any member (n elements each). Bit-identical to edt_slerp_merge per
  * child either way. */
@@ -332,6 +354,11 @@ int edt_slerp_refdot_flags(const float* dots, int nseg, double dot_threshold, do
 int edt_slerp_refdot(const void* v0, const void* v1, int in_dt, const uint64_t* chunk_desc, int64_t nchunks,
                      const int32_t* seg_first_chunk, int nseg, uint32_t chunk_elems, const int32_t* flag, int threads,
                      double eps, float* ref_dot, void* workspace, uint64_t workspace_bytes, void* stream);
+/* edt_slerp_refdot over a tensor-list device table (edt_slerp_seg_table; chunk starts relative). */
+int edt_slerp_refdot_table(const uint64_t* seg_table, int in_dt, const uint64_t* chunk_desc, int64_t nchunks,
+                           const int32_t* seg_first_chunk, int nseg, uint32_t chunk_elems, const int32_t* flag,
+                           int threads, double eps, float* ref_dot, void* workspace, uint64_t workspace_bytes,
+                           void* stream);
 int edt_slerp_refdot_coef(const float* ref_dot, const int32_t* flag, int nseg, const double* t, double dot_threshold,
                           float* coef, float* dot_out, void* stream);
 

@@ -232,6 +232,15 @@ int oracle_max_threads(void) {
 #endif
 }
 
+/* The OpenMP team size of the loops above (bench.py's cpu_baseline: the host's CPU share). */
+int oracle_set_threads(int n) {
+#ifdef _OPENMP
+    extern void omp_set_num_threads(int);
+    if (n > 0) omp_set_num_threads(n);
+#endif
+    return oracle_max_threads();
+}
+
 /* ---- the reference's SLERP dot (EDT_RL/crossover.py:20-29), restated bit for bit ------------
  * dot = np.sum(normalize(v0) * normalize(v1)) on float32 arrays, normalize(v) = v / ||v|| when
  * ||v|| > eps (:57-61), ||v|| = np.linalg.norm = sqrt(v.ravel().dot(v.ravel())):

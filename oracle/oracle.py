@@ -50,6 +50,7 @@ def lib() -> ctypes.CDLL:
         l.oracle_delta_partial.argtypes = [_P, _I, ctypes.POINTER(_P), _I, _I, _I, _U64, _P, _I]
         l.oracle_sgd_apply.argtypes = [_P, _I, _P, _P, _I, _U64, _D, _D, _I]
         l.oracle_max_threads.argtypes = []
+        l.oracle_set_threads.argtypes = [_I]
         l.oracle_ref_sdot.argtypes = [_P, _P, ctypes.c_int64, _I]
         l.oracle_ref_sdot.restype = ctypes.c_float
         l.oracle_np_sum_f32.argtypes = [_P, ctypes.c_int64]
@@ -57,7 +58,7 @@ def lib() -> ctypes.CDLL:
         l.oracle_ref_slerp_dot.argtypes = [_P, _P, _I, ctypes.c_int64, _I, ctypes.c_float,
                                            ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
                                            ctypes.POINTER(ctypes.c_float)]
-        for f in (l.oracle_outer_step, l.oracle_pair_merge, l.oracle_lerp, l.oracle_max_threads,
+        for f in (l.oracle_outer_step, l.oracle_pair_merge, l.oracle_lerp, l.oracle_max_threads, l.oracle_set_threads,
                   l.oracle_delta_partial, l.oracle_sgd_apply, l.oracle_ref_slerp_dot):
             f.restype = _I
         _lib = l
@@ -155,6 +156,11 @@ def max_threads() -> int:
     return lib().oracle_max_threads()
 
 
+def set_threads(n: int) -> int:
+    """OpenMP team size of the C restatement's loops; returns the size now in effect."""
+    return lib().oracle_set_threads(int(n))
+
+
 # ------------------------------------------------------------------------------------------
 # SLERP restated in numpy (EDT_RL/crossover.py:11-81). numpy >= 2 (NEP 50): python floats
 # combine with float32 arrays/scalars as float32.
@@ -200,6 +206,20 @@ def ref_slerp_dot(v0, v1, threads: int = 1, eps: float = 1e-8):
                                     ctypes.byref(d), ctypes.byref(n0), ctypes.byref(n1))
     assert rc == 0, rc
     return np.float32(d.value), np.float32(n0.value), np.float32(n1.value)
+
+
+def slerp_parts_refdot(t: float, v0, v1, threads: int = 1, dot_threshold: float = 0.9995, eps: float = 1e-8):
+    """EDT_RL/crossover.py:11-43 with the dot from the pinned BLAS / numpy restatement
+    (ref_slerp_dot) instead of this host's live BLAS — the reference as it runs on the pinned
+    reference host, whatever BLAS kernel this host's numpy dispatches to: the coefficients and the
+    blend are numpy's own float32 ops, as slerp_parts'. Returns (result float32 ndarray, dot,
+    used_lerp_branch). On the fixture host it equals slerp_parts bit for bit (tests/test_refdot_cpu.py)."""
+    a = v0.detach().cpu().float().numpy() if isinstance(v0, torch.Tensor) else np.asarray(v0, dtype=np.float32)
+    b = v1.detach().cpu().float().numpy() if isinstance(v1, torch.Tensor) else np.asarray(v1, dtype=np.float32)
+    dot, _, _ = ref_slerp_dot(torch.from_numpy(np.ascontiguousarray(a)), torch.from_numpy(np.ascontiguousarray(b)),
+                              threads, eps)
+    c0, c1 = slerp_coefficients_at_dot(t, dot, dot_threshold)
+    return c0 * a + c1 * b, dot, bool(np.abs(dot) > dot_threshold)
 
 
 def canonical_chunk_sums(v0, v1, chunks) -> np.ndarray:

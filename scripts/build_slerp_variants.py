@@ -15,9 +15,6 @@ VARIANTS = {
     "tpw4": ["-DEDT_SLERP_STATS_TPW=4"],
     "tpw8": ["-DEDT_SLERP_STATS_TPW=8"],
     "nont": ["-DEDT_NT_SLERP=0"],
-    "blendold": ["-DEDT_SLERP_BLEND_TILE=0"],
-    "popcoloc": ["-DEDT_SLERP_POP_FUSED=0"],
-    "popfused": ["-DEDT_SLERP_POP_FUSED=1"],
     "waverows": ["-DEDT_SLERP_SPEC_WG_ROWS=0"],
 }
 

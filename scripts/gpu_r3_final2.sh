@@ -20,7 +20,7 @@ tail -c 400 $OUT/bench.json; echo
 timeout -k 10 1000 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread \
     > $OUT/pytest_gpu.log 2>&1; s=$?
 tail -3 $OUT/pytest_gpu.log; [ $s -eq 0 ] || exit $s
-# the SLERP forms side by side on the 7B body (arena / tensor-list, speculative / two-pass / hold)
+# the SLERP forms side by side on the 7B body (arena / tensor-list, speculative / two-pass)
 timeout -k 10 300 python scripts/slerp_spec_probe.py --rounds 5 > $OUT/probe_lineage.json 2> $OUT/probe.err || exit 8
 timeout -k 10 300 python scripts/slerp_spec_probe.py --rounds 5 --far > $OUT/probe_far.json 2>> $OUT/probe.err || exit 8
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit 9

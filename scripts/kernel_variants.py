@@ -280,7 +280,9 @@ def run_slerp_pop(names, rounds, layout_name="gpt_1p3b", P_members=8):
     t = torch.full((len(lay),), 0.5, dtype=torch.float64, device=dev)
     stream = L.stream_ptr(dev)
     plans = {ce: ops.make_slerp_plan(lay.offsets, dev, chunk_elems=ce) for ce in (1 << 14, 1 << 16)}
-    grams = {ce: torch.empty(pl.nchunks * 36, dtype=torch.float64, device=dev) for ce, pl in plans.items()}
+    # the Gram rows AND the row scratch the pass folds into them (edt_slerp_population_gram_doubles)
+    grams = {ce: torch.empty(int(L.lib().edt_slerp_population_gram_doubles(P_members, pl.nchunks)), dtype=torch.float64,
+                             device=dev) for ce, pl in plans.items()}
     coef = torch.empty(P_members * len(lay) * 2, dtype=torch.float32, device=dev)
     flat = (ctypes.c_int32 * (2 * P_members))(*[x for p in pairs for x in p])
     am, ao = L.ptr_array(mem), L.ptr_array(outs)

@@ -2,9 +2,9 @@
 every segment in the lerp branch, so the speculative merge is one pass of 2 reads + 1 write per
 element, exactly lerp's bytes). Times, in one process on the same arenas and interleaved:
 edt_lerp, edt_slerp_merge_speculative, the two-pass edt_slerp_merge (stats + blend), the
-tensor-list forms over views of the same arenas (ops.slerp_list: two-pass and speculative), the
-one-launch edt_slerp_merge_hold (checked bit for bit against the two-pass output) and the stats
-pass alone (edt_slerp_stats, 4 B read per element).
+tensor-list forms over views of the same arenas (ops.slerp_list: two-pass and speculative) and the
+stats pass alone (edt_slerp_stats, 4 B read per element). (r3's one-launch hold form was removed in
+r4: measured slower)
 HIP events on the launch stream, median over rounds. Run it under rocprofv3 (--kernel-trace
 --stats, or one --pmc pass) to get the per-kernel figures.
 
@@ -29,7 +29,6 @@ def main():
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--far", action="store_true", help="independent parents (the SLERP branch)")
     ap.add_argument("--variants", default="")
-    ap.add_argument("--no-hold", action="store_true", help="skip the hold form (cooperative launch)")
     a = ap.parse_args()
     from evolutionarydistributedtraining_amd import _lib as L
     from evolutionarydistributedtraining_amd import ops
@@ -66,6 +65,10 @@ def main():
     lplan = ops.make_slerp_plan(lay.offsets, dev, relative=True)
     cases["list_two_pass"] = lambda: ops.slerp_list(lplan, l0, l1, lo, t, speculate=False)
     cases["list_speculative"] = lambda: ops.slerp_list(lplan, l0, l1, lo, t, speculate=True)
+    # the same tensors bound once (ops.bind_slerp_list): no per-tensor host work per merge
+    bnd = ops.bind_slerp_list(lplan, l0, l1, lo)
+    cases["list_bound_two_pass"] = lambda: bnd.merge(t, speculate=False)
+    cases["list_bound_speculative"] = lambda: bnd.merge(t, speculate=True)
     for name, lb in libs.items():
         part = torch.empty(int(lb.edt_slerp_sums_doubles(3, plan.nchunks)), dtype=torch.float64, device=dev)
 
@@ -80,22 +83,13 @@ def main():
                 L.ptr(v0), L.ptr(v1), 1, L.ptr(out), 1, L.ptr(plan.chunks), plan.nchunks, L.ptr(plan.seg_first),
                 plan.nseg, L.ptr(t), 0.9995, 1e-8, L.ptr(part), L.ptr(plan.coef), L.ptr(plan.dots), st)
 
-        def hold(lb=lb, part=part):
-            return lb.edt_slerp_merge_hold(
-                L.ptr(v0), L.ptr(v1), 1, L.ptr(out), 1, L.ptr(plan.chunks), plan.nchunks, L.ptr(plan.seg_first),
-                plan.nseg, L.ptr(t), 0.9995, 1e-8, L.ptr(part), L.ptr(plan.coef), L.ptr(plan.dots), st)
-
         def stats(lb=lb, part=part):
             return lb.edt_slerp_stats(L.ptr(v0), L.ptr(v1), 1, L.ptr(plan.chunks), plan.nchunks, L.ptr(part), st)
 
         sfx = "" if name == "intree" else f"/{name}"
-        if name == "intree":
-            part_intree = part
         cases["speculative" + sfx] = spec
         cases["two_pass" + sfx] = two
         cases["stats" + sfx] = stats
-        if hasattr(lb, "edt_slerp_merge_hold") and not a.no_hold:
-            cases["hold" + sfx] = hold
     for k, f in cases.items():
         if not k.startswith("list_"):
             assert f() == 0, L.last_error() if hasattr(L, "last_error") else "launch failed"
@@ -113,22 +107,11 @@ def main():
             torch.cuda.synchronize()
             times[k].append(e0.elapsed_time(e1))
     redo_n = int(redo.sum().item())
-    hold_check = None
-    if "hold" in cases:                     # the hold form against the two-pass form, bit for bit
-        cases["two_pass"]()
-        ref = out.clone()
-        ref_dots = plan.dots.clone()
-        out.fill_(float("nan"))
-        cases["hold"]()
-        status = int(lib.edt_slerp_hold_status(L.ptr(part_intree), plan.nchunks, st))
-        hold_check = {"status": status, "out_equal": bool(torch.equal(out.view(torch.int16), ref.view(torch.int16))),
-                      "dots_equal": bool(torch.equal(plan.dots, ref_dots))}
-        del ref
     # bytes: 6 per element (2 bf16 reads + 1 write); the stats pass reads 4
     res = {k: {"median_ms": round(statistics.median(v), 4), "min_ms": round(min(v), 4),
                "TBps": round((4 if k.startswith("stats") else 6) * P / statistics.median(v) / 1e9, 3)}
            for k, v in times.items()}
-    print(json.dumps({"probe": "slerp_spec", "elements": P, "far": a.far, "redo_segments": redo_n, "hold_check": hold_check,
+    print(json.dumps({"probe": "slerp_spec", "elements": P, "far": a.far, "redo_segments": redo_n,
                       "results": res}))
 
 

@@ -97,16 +97,18 @@ static int slerp_list_check(void) {
                                   3 * NSEG * sizeof(uint64_t), NULL);
     if (rc == 0)
         rc = edt_slerp_merge_list_speculative((const void* const*)d_v0, (const void* const*)d_v1, EDT_F32, d_b,
-                                              EDT_F32, d_desc, nchunks, d_first, NSEG, d_t, 0.9995, 1e-8, d_partial,
-                                              d_coef, d_dots_b, d_redo, d_ws, 3 * NSEG * sizeof(uint64_t), NULL);
+                                              EDT_F32, sizes, d_desc, nchunks, d_first, NSEG, d_t, 0.9995, 1e-8,
+                                              d_partial, d_coef, d_dots_b, d_redo, d_ws, 3 * NSEG * sizeof(uint64_t),
+                                              NULL);
     if (rc != 0) {
         fprintf(stderr, "slerp list: %d %s\n", rc, edt_last_error());
         return 1;
     }
     /* an output that is its own parent: the speculative form refuses it, nothing launched */
     rc = edt_slerp_merge_list_speculative((const void* const*)d_v0, (const void* const*)d_v1, EDT_F32, d_v0,
-                                          EDT_F32, d_desc, nchunks, d_first, NSEG, d_t, 0.9995, 1e-8, d_partial,
-                                          d_coef, d_dots_b, d_redo, d_ws, 3 * NSEG * sizeof(uint64_t), NULL);
+                                          EDT_F32, sizes, d_desc, nchunks, d_first, NSEG, d_t, 0.9995, 1e-8,
+                                          d_partial, d_coef, d_dots_b, d_redo, d_ws, 3 * NSEG * sizeof(uint64_t),
+                                          NULL);
     if (rc >= 0) {
         fprintf(stderr, "speculative list form accepted an output aliasing its parent\n");
         return 1;
@@ -140,6 +142,10 @@ static int slerp_list_check(void) {
 }
 
 int main(void) {
+    if (edt_abi_version() != EDT_ABI_VERSION) {     /* workspace sizes and signatures follow the header */
+        fprintf(stderr, "library ABI %d, header ABI %d: rebuild\n", edt_abi_version(), EDT_ABI_VERSION);
+        return 1;
+    }
     const uint64_t n = 1000003; /* odd: exercises the scalar tail */
     const size_t nb = n * sizeof(float);
     float *theta = malloc(nb), *mom = malloc(nb), *w[K];

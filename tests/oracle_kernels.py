@@ -59,7 +59,7 @@ class ChunkGramKernels(OracleKernels):
         first.append(len(rows))
         host = np.asarray(rows, dtype=np.int64).reshape(-1, 3)
         return types.SimpleNamespace(seg_offsets=list(offsets), chunks=torch.from_numpy(host), chunks_host=host,
-                                     seg_first=first, nseg=len(offsets) - 1, nchunks=len(rows))
+                                     seg_first=first, nseg=len(offsets) - 1, nchunks=len(rows), chunk_elems=chunk_elems)
 
     def slerp_gram(self, members, chunks, nchunks, gram=None):
         M = len(members)
@@ -109,3 +109,16 @@ class ChunkGramKernels(OracleKernels):
             for q, (i, j) in enumerate(pairs):
                 outs[q][a:a + n] = (coef[q, s, 0] * members[i][a:a + n].float()
                                     + coef[q, s, 1] * members[j][a:a + n].float()).to(outs[q].dtype)
+
+    def slerp_refdot(self, v0, v1, chunks, seg_first, nseg, chunk_elems, flag, ref, eps=1e-8):
+        """edt_slerp_refdot's contract: the reference's fp32 dot (oracle.ref_slerp_dot, the pinned
+        BLAS / numpy restatement) of each flagged segment, its elements gathered from the chunk rows."""
+        val = torch.zeros(max(1, nseg), dtype=torch.float32)
+        for s in range(nseg):
+            if not int(flag[s]):
+                continue
+            rows = chunks[int(seg_first[s]):int(seg_first[s + 1])]
+            a = torch.cat([v0[int(r[0]):int(r[0]) + int(r[1])] for r in rows]) if len(rows) else v0[:0]
+            b = torch.cat([v1[int(r[0]):int(r[0]) + int(r[1])] for r in rows]) if len(rows) else v1[:0]
+            val[s] = float(self.o.ref_slerp_dot(a.contiguous(), b.contiguous(), ref.threads, eps)[0])
+        return val

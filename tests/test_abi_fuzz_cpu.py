@@ -105,7 +105,7 @@ def test_sgd_apply_sum_rejects(lib, kind, nacc, n, bad, which):
 
 
 @FUZZ
-@given(kind=st.sampled_from(["in_dt", "out_dt", "negative", "null"]), entry=st.sampled_from(["stats", "blend", "merge", "hold"]),
+@given(kind=st.sampled_from(["in_dt", "out_dt", "negative", "null"]), entry=st.sampled_from(["stats", "blend", "merge"]),
        nchunks=st.integers(1, 1 << 30), neg=st.integers(-(1 << 40), -1), bad=bad_dtype)
 def test_slerp_passes_reject(lib, kind, entry, nchunks, neg, bad):
     in_dt, out_dt, v0 = BF16, BF16, fake(0)
@@ -125,20 +125,10 @@ def test_slerp_passes_reject(lib, kind, entry, nchunks, neg, bad):
         rc = lib.edt_slerp_stats(v0, fake(1), in_dt, fake(2), nchunks, fake(3), None)
     elif entry == "blend":
         rc = lib.edt_slerp_blend(v0, fake(1), in_dt, fake(2), out_dt, fake(3), nchunks, fake(4), None)
-    elif entry == "merge":
+    else:
         rc = lib.edt_slerp_merge(v0, fake(1), in_dt, fake(2), out_dt, fake(3), nchunks, fake(4), 1, fake(5),
                                  0.9995, 1e-8, fake(6), fake(7), None, None)
-    else:
-        rc = lib.edt_slerp_merge_hold(v0, fake(1), in_dt, fake(2), out_dt, fake(3), nchunks, fake(4), 1, fake(5),
-                                      0.9995, 1e-8, fake(6), fake(7), None, None)
     _expect(lib, rc, needle)
-
-
-def test_slerp_hold_takes_bf16_parents_only(lib):
-    """The on-chip-hold form rejects fp32 parents before any launch (edt_slerp_merge takes them)."""
-    rc = lib.edt_slerp_merge_hold(fake(0), fake(1), F32, fake(2), F32, fake(3), 4, fake(4), 1, fake(5),
-                                  0.9995, 1e-8, fake(6), fake(7), None, None)
-    _expect(lib, rc, "bf16 parents only")
 
 
 @FUZZ
@@ -169,3 +159,40 @@ def test_success_clears_the_message(lib):
     _expect(lib, lib.edt_outer_step(fake(0), 7, arr([fake(1)]), F32, 1, fake(2), 1, 8, 0.7, 0.9, 1, None), "dtype")
     assert lib.edt_outer_step(None, F32, arr([None]), F32, 1, None, 0, 0, 0.7, 0.0, 0, None) == 0
     assert lib.edt_last_error() == b""
+
+
+def _table(lib, ptrs0, ptrs1, ptrso, sizes, apart, in_dt=F32, out_dt=F32):
+    n = len(sizes)
+    arr = lambda xs: (ctypes.c_void_p * max(1, n))(*xs)
+    numel = (ctypes.c_uint64 * max(1, n))(*sizes)
+    host = (ctypes.c_uint64 * max(1, 3 * n))()
+    rc = lib.edt_slerp_seg_table(arr(ptrs0), arr(ptrs1), arr(ptrso), n, numel, in_dt, out_dt, apart,
+                                 ctypes.cast(host, ctypes.c_void_p))
+    return rc, list(host)
+
+
+def test_seg_table_host_checks(lib):
+    """edt_slerp_seg_table (a host function): the {v0, v1, out} image in order; a misaligned tensor
+    refused; with apart = 1 every output byte range checked against every parent's (sorted spans):
+    an output inside ANOTHER tensor's parent, a partial overlap or an output equal to its own parent
+    refused, disjoint outputs accepted, empty tensors ignored."""
+    base = 1 << 40
+    p0, p1, po = [base, base + 4096], [base + 8192, base + 12288], [base + 16384, base + 20480]
+    sizes = [1000, 1000]                                   # 4000 bytes each (fp32)
+    rc, host = _table(lib, p0, p1, po, sizes, 1)
+    assert rc == 0 and host == [p0[0], p1[0], po[0], p0[1], p1[1], po[1]]
+    assert _table(lib, [base + 4], p1[:1], po[:1], [10], 0)[0] < 0              # not 16-byte aligned
+    assert _table(lib, p0, p1, [p0[0], po[1]], sizes, 1)[0] < 0                   # out == own parent
+    assert _table(lib, p0, p1, [po[0], p1[0]], sizes, 1)[0] < 0                   # out = another's parent
+    assert _table(lib, p0, p1, [po[0], p1[1] + 2048], sizes, 1)[0] < 0             # partial overlap
+    assert b"overlaps a parent" in lib.edt_last_error()
+    assert _table(lib, p0, p1, [p0[0], po[1]], sizes, 0)[0] == 0                  # two-pass: allowed
+    assert _table(lib, p0, p1, [p1[0], po[1]], [0, 1000], 1)[0] == 0              # empty spans ignored
+    # bf16 outputs are half the bytes: one right after the last parent's end, the next right after it
+    assert _table(lib, p0, p1, [p1[1] + 4000, p1[1] + 6000], [1000, 1000], 1, F32, BF16)[0] == 0
+    assert _table(lib, p0, p1, [p1[1] + 3984, p1[1] + 6000], [1000, 1000], 1, F32, BF16)[0] < 0
+
+
+def test_abi_version_matches_the_binding(lib):
+    from evolutionarydistributedtraining_amd import _lib as L
+    assert lib.edt_abi_version() == L.EDT_ABI_VERSION == 4

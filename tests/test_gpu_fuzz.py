@@ -5,6 +5,7 @@ lerp weights. The scalars are where the reference's conversions bite: torch roun
 bf16 for bf16 tensors, `mul_(s)` keeps the fp32 scalar, `/ K` is a true division, so a
 kernel that folded or rounded a scalar differently would show up here on some draw. Every case is
 bit-exact. Reference: EDT_LM/diloco.py:238-289, EDT_LM/train/crossover.py:50-51,150-237."""
+import numpy as np
 import pytest
 import torch
 from hypothesis import HealthCheck, given, settings
@@ -92,13 +93,18 @@ def test_lerp_fuzz(oracle, dev, n, t, dt, seed):
 @given(sizes_=st.lists(st.integers(0, 3000), min_size=1, max_size=5),
        ts=st.lists(st.floats(0.0, 1.0), min_size=5, max_size=5),
        spread=st.sampled_from([1e-4, 0.01, 0.05, 0.5, 2.0]), seed=st.integers(0, 2**31 - 1),
-       speculate=st.booleans(), layout=st.sampled_from(["arena", "list"]))
-def test_slerp_fuzz(oracle, dev, sizes_, ts, spread, seed, speculate, layout):
+       speculate=st.booleans(), layout=st.sampled_from(["arena", "list"]), ref=st.booleans())
+def test_slerp_fuzz(oracle, dev, sizes_, ts, spread, seed, speculate, layout, ref):
     """Multi-tensor SLERP (EDT_RL/crossover.py:11-43) over random segment sizes (empty included),
     per-segment t and parent distances from lineage (lerp branch) to far (SLERP branch), both
-    kernel forms, over flat arenas or separate tensors (the tensor-list path): per segment the
-    branch agrees with the oracle's (fp32) dot away from the threshold, the lerp branch is
-    bit-exact, and the SLERP branch is within the golden bar."""
+    kernel forms, over flat arenas or separate tensors (the tensor-list path).
+    ref=True (reference-dot mode, ops.RefDot): every segment, both branches, BIT-EXACT with the
+    reference restated on the pinned host (oracle.slerp_parts_refdot: its BLAS / numpy dot, numpy's
+    float32 coefficients and blend).
+    ref=False (the fp64-dot default): per segment the branch agrees with the oracle's (fp32) dot
+    away from the threshold, the lerp branch is bit-exact, the SLERP branch is within the golden
+    bar; and the device's coefficients are the reference formula at the device's OWN dot within a
+    fixed multiple of the formula's conditioning (_coef_strict: no dot uncertainty in it)."""
     from evolutionarydistributedtraining_amd import ops
     g = torch.Generator().manual_seed(seed)
     offs = [0]
@@ -108,23 +114,31 @@ def test_slerp_fuzz(oracle, dev, sizes_, ts, spread, seed, speculate, layout):
     v0 = torch.randn(n, generator=g) * 0.02
     v1 = v0 + torch.randn(n, generator=g) * 0.02 * spread
     t = torch.tensor(ts[:len(sizes_)], dtype=torch.float64)
+    ce = 8192 if ref else 1024              # the reference-dot mode's chunks: whole numpy buffers
+    rd = ops.RefDot() if ref else None
     if layout == "arena":
-        plan = ops.make_slerp_plan(offs, dev, chunk_elems=1024)
+        plan = ops.make_slerp_plan(offs, dev, chunk_elems=ce)
         out_d = torch.empty(max(n, 1), dtype=torch.float32, device=dev)[:n]
-        ops.slerp_arena(plan, v0.to(dev), v1.to(dev), out_d, t.to(dev), speculate=speculate)
+        ops.slerp_arena(plan, v0.to(dev), v1.to(dev), out_d, t.to(dev), speculate=speculate, ref_dot=rd)
         got = out_d.cpu()
     else:
-        plan = ops.make_slerp_plan(offs, dev, chunk_elems=1024, relative=True)
+        plan = ops.make_slerp_plan(offs, dev, chunk_elems=ce, relative=True)
         pieces = list(zip(offs, offs[1:]))
         outs = [torch.empty(b - a, dtype=torch.float32, device=dev) for a, b in pieces]
         ops.slerp_list(plan, [v0[a:b].to(dev) for a, b in pieces], [v1[a:b].to(dev) for a, b in pieces], outs,
-                       t.to(dev), speculate=speculate)
+                       t.to(dev), speculate=speculate, ref_dot=rd)
         got = torch.cat([o.cpu() for o in outs])
     coef, dots = plan.coef.cpu(), plan.dots.cpu()
     for s in range(len(sizes_)):
         a, b = offs[s], offs[s + 1]
         if b == a:
             continue
+        if ref:
+            want, wdot, _ = oracle.slerp_parts_refdot(float(t[s]), v0[a:b], v1[a:b])
+            assert float(dots[s]) == float(wdot), s
+            assert torch.equal(bits(got[a:b]), bits(torch.from_numpy(np.ascontiguousarray(np.ravel(want))))), s
+            continue
+        _coef_strict(float(t[s]), float(dots[s]), float(coef[s, 0]), float(coef[s, 1]))
         want = oracle.slerp(float(t[s]), v0[a:b], v1[a:b]).float()
         c0, c1, dot = oracle.slerp_coefficients(float(t[s]), v0[a:b], v1[a:b])
         if abs(abs(float(dot)) - 0.9995) < 1e-5:
@@ -145,6 +159,35 @@ def test_slerp_fuzz(oracle, dev, sizes_, ts, spread, seed, speculate, layout):
         tol = _tol(c0, c1, v0[a:b], v1[a:b]) + 1.01 * (abs(g0 - float(c0)) * v0[a:b].abs()
                                                          + abs(g1 - float(c1)) * v1[a:b].abs())
         assert (err <= tol).all(), (s, err.max().item())
+
+
+def _coef_strict(t, dot, g0, g1):
+    """The device's (c0, c1) against the reference formula in numpy float32 at the device's own
+    dot: no dot uncertainty, only the two implementations' transcendental rounding, so
+    the bar is a fixed number of ulps scaled by the formula's conditioning A (a 1-ulp move of th0
+    moves the result by ~A ulps: th0 (|cot th0| + (1 - t)|cot(th0 - th_t)| + t |cot th_t|), and
+    t / (1 - t) from th0 - th_t's cancellation). Host model of correctly rounded fp32 transcendentals
+    against numpy's stays under 1.8 (1 + A) ulps over 600k draws; the bar is 6 (1 + A). t > 0.99
+    (cancellation beyond the model) and the lerp branch are skipped."""
+    import numpy as np
+    f = np.float32
+    if abs(dot) > 0.9995 or t > 0.99:
+        return
+    r0, r1 = (float(x) for x in np.asarray(_np_coef(t, dot), dtype=np.float32))
+    th0 = float(np.arccos(f(dot)))
+    tht = th0 * t
+    cot = lambda x: abs(np.cos(x) / np.sin(x)) if abs(np.sin(x)) > 1e-30 else 0.0
+    A = th0 * (cot(th0) + (1 - t) * cot(th0 - tht) + t * cot(tht)) + t / (1 - t)
+    bar = 6 * (1 + A)
+    for g, r in ((g0, r0), (g1, r1)):
+        ulp = float(np.spacing(f(abs(r)))) if r != 0 else float(np.spacing(f(0)))
+        assert abs(g - r) <= bar * ulp + 1e-38, (t, dot, g, r, abs(g - r) / ulp, bar)
+
+
+def _np_coef(t, dot):
+    from evolutionarydistributedtraining_amd.ops import reference_coefficients
+    import numpy as np
+    return reference_coefficients(np.float32([dot]), np.float64([t]))[0]
 
 
 def _tol(c0, c1, v0, v1):

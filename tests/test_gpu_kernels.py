@@ -449,12 +449,26 @@ def test_slerp_list_speculative_matches_two_pass(dev, ops, in_dt, out_dt):
         ops.slerp_list(lplan, c0, a1, c0, ts, speculate=True)
         assert torch.equal(bits(torch.cat([x.cpu() for x in c0])), bits(ref.cpu()))
         ws = torch.empty(3 * len(sizes), dtype=torch.int64, device=dev)
+        numel = (L.ctypes.c_uint64 * len(sizes))(*sizes)
+        redo = torch.empty(len(sizes), dtype=torch.int32, device=dev)
         rc = L.lib().edt_slerp_merge_list_speculative(
-            L.ptr_array(a0), L.ptr_array(a1), L.dtype_code(in_dt), L.ptr_array(a0), L.dtype_code(out_dt),
+            L.ptr_array(a0), L.ptr_array(a1), L.dtype_code(in_dt), L.ptr_array(a0), L.dtype_code(out_dt), numel,
             L.ptr(lplan.chunks), lplan.nchunks, L.ptr(lplan.seg_first), lplan.nseg, L.ptr(ts), 0.9995, 1e-8,
-            L.ptr(lplan.partial), L.ptr(lplan.coef), None, L.ptr(lplan._redo), L.ptr(ws), ws.numel() * 8,
+            L.ptr(lplan.partial), L.ptr(lplan.coef), None, L.ptr(redo), L.ptr(ws), ws.numel() * 8,
             L.stream_ptr(dev))
         assert rc != 0 and b"apart" in L.lib().edt_last_error()
+        # ... and so is an output that overlaps ANOTHER tensor's parent (tied storage,
+        # partial overlap): tensor 3's output inside tensor 4's parent
+        outs_x = [torch.empty(x, dtype=out_dt, device=dev) for x in sizes]
+        big = a1[4]
+        outs_x[3] = big[:sizes[3]] if sizes[3] <= sizes[4] else outs_x[3]
+        if sizes[3] <= sizes[4] and in_dt == out_dt:
+            rc = L.lib().edt_slerp_merge_list_speculative(
+                L.ptr_array(a0), L.ptr_array(a1), L.dtype_code(in_dt), L.ptr_array(outs_x), L.dtype_code(out_dt),
+                numel, L.ptr(lplan.chunks), lplan.nchunks, L.ptr(lplan.seg_first), lplan.nseg, L.ptr(ts), 0.9995,
+                1e-8, L.ptr(lplan.partial), L.ptr(lplan.coef), None, L.ptr(redo), L.ptr(ws), ws.numel() * 8,
+                L.stream_ptr(dev))
+            assert rc != 0 and b"overlaps a parent" in L.lib().edt_last_error()
 
 
 @pytest.mark.parametrize("in_dt,out_dt", [(torch.float32, torch.float32), (torch.bfloat16, torch.bfloat16)])
@@ -574,73 +588,6 @@ def test_slerp_speculative_matches_two_pass(dev, ops, in_dt, out_dt):
         assert rc != 0
         with pytest.raises(EdtError):
             L.check(rc, "edt_slerp_merge_speculative")
-
-
-def _hold_merge(plan, v0, v1, out, ts, dev):
-    from evolutionarydistributedtraining_amd import _lib as L
-    lib = L.lib()
-    L.check(lib.edt_slerp_merge_hold(L.ptr(v0), L.ptr(v1), L.dtype_code(v0), L.ptr(out), L.dtype_code(out),
-                                     L.ptr(plan.chunks), plan.nchunks, L.ptr(plan.seg_first), plan.nseg, L.ptr(ts),
-                                     0.9995, 1e-8, L.ptr(plan.partial), L.ptr(plan.coef), L.ptr(plan.dots),
-                                     L.stream_ptr(dev)), "edt_slerp_merge_hold")
-    assert lib.edt_slerp_hold_status(L.ptr(plan.partial), plan.nchunks, L.stream_ptr(dev)) == 0, "in-launch wait expired"
-
-
-@pytest.mark.parametrize("out_dt", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("chunk_elems", [4096, 1 << 16])
-def test_slerp_hold_matches_two_pass(dev, ops, out_dt, chunk_elems):
-    """edt_slerp_merge_hold (one persistent launch: chunk sums, in-launch coefficients, the last
-    groups each wave read blended from registers, the rest read again) is bit-identical to
-    edt_slerp_merge: outputs, chunk sums and dots, with segments on both sides of the threshold,
-    ragged and empty segments, a zero segment, phases whose waves hold and stream groups, and the
-    output in place over parent 0."""
-    g = torch.Generator().manual_seed(78)
-    sizes = [0, 1, 7, 33, 4096, 70_001, 0, 129, 200_003, 65_536, 131_073, 3_000_017, 25_165_829, 11, 9_999_999]
-    offs = [0]
-    for x in sizes:
-        offs.append(offs[-1] + x)
-    v0 = torch.randn(offs[-1], generator=g) * 0.02
-    v1 = v0.clone()
-    rel = [0.1, 0.001, 0.2, 0.001, 0.05, 0.005, 0.1, 0.3, 0.002, 0.02, 0.0005, 1.0, 0.5, 0.01, 2.0]
-    for s_, r in enumerate(rel):
-        a, b = offs[s_], offs[s_ + 1]
-        v1[a:b] += torch.randn(b - a, generator=g) * 0.02 * r
-    v0[offs[7]:offs[8]] = 0
-    v0, v1 = v0.bfloat16().to(dev), v1.bfloat16().to(dev)
-    ts = torch.tensor([0.5, 0.0, 1.0, 0.43, 0.5, 0.7, 0.5, 0.2, 0.9, 0.3, 0.6, 0.5, 0.37, 0.5, 0.81],
-                      dtype=torch.float64).to(dev)
-    plan = ops.make_slerp_plan(offs, dev, chunk_elems=chunk_elems)
-    ref = torch.empty(offs[-1], dtype=out_dt, device=dev)
-    ops.slerp_arena(plan, v0, v1, ref, ts, speculate=False)
-    ref_dots = plan.dots.cpu().clone()
-    ref_sums = plan.partial[:3 * plan.nchunks].cpu().clone()
-    d = ref_dots[:len(sizes)].abs()
-    assert (d > 0.9995).any() and (d <= 0.9995).any()
-    for rep in range(2):                                       # a second launch reuses the control words
-        got = torch.full_like(ref, float("nan"))
-        plan.partial.fill_(float("nan"))
-        plan.dots.fill_(float("nan"))
-        _hold_merge(plan, v0, v1, got, ts, dev)
-        assert torch.equal(bits(got.cpu()), bits(ref.cpu())), rep
-        assert torch.equal(plan.dots.cpu(), ref_dots)
-        assert torch.equal(bits(plan.partial[:3 * plan.nchunks].cpu()), bits(ref_sums))
-    if out_dt == torch.bfloat16:                               # in place over parent 0
-        v0c = v0.clone()
-        _hold_merge(plan, v0c, v1, v0c, ts, dev)
-        assert torch.equal(bits(v0c.cpu()), bits(ref.cpu()))
-
-
-def test_slerp_hold_rejects(dev, ops):
-    """The hold form takes bf16 parents only and checks its arguments before any launch."""
-    from evolutionarydistributedtraining_amd import _lib as L
-    lib = L.lib()
-    plan = ops.make_slerp_plan([0, 4096], dev)
-    v = torch.zeros(4096, device=dev)
-    ts = torch.tensor([0.5], dtype=torch.float64, device=dev)
-    rc = lib.edt_slerp_merge_hold(L.ptr(v), L.ptr(v), L.dtype_code(v), L.ptr(v), L.dtype_code(v), L.ptr(plan.chunks),
-                                  plan.nchunks, L.ptr(plan.seg_first), plan.nseg, L.ptr(ts), 0.9995, 1e-8,
-                                  L.ptr(plan.partial), L.ptr(plan.coef), None, L.stream_ptr(dev))
-    assert rc != 0 and b"bf16" in L.lib().edt_last_error()
 
 
 def test_population_kernels_edges(dev, ops):

@@ -1,14 +1,19 @@
-"""Reference-dot mode on the MI355X (ops.RefDot -> edt_slerp_refdot_flags / edt_slerp_refdot /
-edt_slerp_refdot_coef): the device recomputes the reference's own fp32 dot of EDT_RL/crossover.py:20-29
-(BLAS sdot norms + numpy's buffered pairwise sum of the normalised products) bit for bit.
+"""Reference-dot mode on the MI355X (ops.RefDot): the device recomputes the reference's own fp32
+dot of EDT_RL/crossover.py:20-29 (BLAS sdot norms + numpy's buffered pairwise sum of the
+normalised products, edt_slerp_refdot) bit for bit, and the coefficients are the reference's own
+numpy float32 evaluation of crossover.py:31-43 (ops.reference_coefficients), so the merge IS the
+reference's, bit for bit, in every SLERP form.
 
   * the dot of every golden SLERP case equals the reference's recorded dot, bit for bit, and the
     restatement's (oracle.ref_slerp_dot) — fp32 and bf16 inputs, one multi-segment launch;
   * random layouts whose sizes cross every block edge of both reductions, BLAS thread splits 1 / 3;
-  * the 24 DOT_THRESHOLD cases (tests/golden/slerp_threshold.json): in this mode the kernel takes
-    the reference's branch on every case, the four straddles included, and its output is within
-    the ordinary 2e-6 SLERP bar of the reference's (the lerp branch bit for bit) — the fp64 default
-    keeps its documented contract (tests/test_slerp_threshold.py);
+  * all 100 golden SLERP cases: the OUTPUT equals the reference's recorded output bit for bit,
+    both branches, two-pass and speculative, flat arenas and tensor lists;
+  * the 24 DOT_THRESHOLD cases (tests/golden/slerp_threshold.json): the reference's branch on every
+    case (the four straddles included) and the reference's output bit for bit — at the recorded
+    sample indices and, over the whole tensor, against the restatement oracle.slerp_parts_refdot;
+  * every form agrees bit for bit: arena / tensor list (bound table) / population (Gram and
+    speculative) / the sharded population on virtual ranks, fp32 and bf16 children;
   * band flags: only segments near the threshold are recomputed, the others keep the fp64 dot."""
 import json
 import os
@@ -91,9 +96,10 @@ def _threshold_fixture():
 THR_CASES, _ = _threshold_fixture()
 
 
+@pytest.mark.parametrize("speculate", [False, True])
 @pytest.mark.parametrize("band", [-1.0, 1e-4])
 @pytest.mark.parametrize("c", THR_CASES, ids=[c["name"] for c in THR_CASES])
-def test_refdot_mode_takes_the_reference_branch_at_threshold(dev, c, band):
+def test_refdot_mode_is_the_reference_at_threshold(oracle, dev, c, band, speculate):
     from evolutionarydistributedtraining_amd import ops
     _, tensors = _threshold_fixture()
     if f"{c['name']}/v0" in tensors:
@@ -107,19 +113,16 @@ def test_refdot_mode_takes_the_reference_branch_at_threshold(dev, c, band):
     for o in c["outputs"]:
         t = torch.tensor([o["t"]], dtype=torch.float64, device=dev)
         out = torch.empty(n, dtype=torch.float32, device=dev)
-        ops.slerp_arena(plan, a.to(dev), b.to(dev), out, t, ref_dot=ops.RefDot(band=band))
+        ops.slerp_arena(plan, a.to(dev), b.to(dev), out, t, speculate=speculate, ref_dot=ops.RefDot(band=band))
         dot = plan.dots[0].item()
         assert dot == c["ref_dot"], (c["name"], dot, c["ref_dot"])        # the reference's own dot
-        got, ref = out.cpu()[idx], tensors[f"{o['key']}/out"]
-        if c["ref_lerp_branch"]:
-            assert torch.equal(got.view(torch.int32), ref.view(torch.int32)), c["name"]
-        else:
-            v0, v1 = a.double()[idx], b.double()[idx]
-            th = np.arccos(np.float32(dot), dtype=np.float32)
-            c0 = float(np.sin(th - th * np.float32(o["t"])) / np.sin(th))
-            c1 = float(np.sin(th * np.float32(o["t"])) / np.sin(th))
-            bar = 2e-6 * (abs(c0) * v0.abs() + abs(c1) * v1.abs())
-            assert ((got.double() - ref.double()).abs() <= bar + 1e-30).all(), c["name"]
+        got = out.cpu()
+        ref = tensors[f"{o['key']}/out"]
+        assert torch.equal(got[idx].view(torch.int32), ref.view(torch.int32)), (c["name"], o["t"])
+        want, wdot, lerp = oracle.slerp_parts_refdot(o["t"], a, b)
+        assert float(wdot) == c["ref_dot"] and lerp == c["ref_lerp_branch"]
+        assert np.array_equal(got.numpy().view(np.int32), np.ravel(want).view(np.int32)), (c["name"], o["t"])
+        assert abs(float(got.double().sum()) - o["sum_f64"]) <= 1e-9 * max(1.0, abs(o["sum_f64"]))
 
 
 def test_refdot_band_flags_only_near_threshold(oracle, dev):
@@ -134,12 +137,18 @@ def test_refdot_band_flags_only_near_threshold(oracle, dev):
     far = (torch.randn(70001, generator=g).to(a.dtype), torch.randn(70001, generator=g).to(a.dtype))   # dot ~ 0
     parts = [far, (a, b)]
     dots_band, plan, _ = _ref_dots(dev, parts, band=1e-3)
-    assert plan._refdot_flag[:2].cpu().tolist() == [0, 1]
     assert dots_band[1].item() == c["ref_dot"]
     dots_all, _, _ = _ref_dots(dev, parts, band=-1.0)
     want_far, _, _ = oracle.ref_slerp_dot(*far)
     assert np.float32(dots_all[0].item()) == want_far
     assert abs(dots_band[0].item() - float(want_far)) < 1e-5                # the fp64 dot, the usual bar
+    # not recomputed: the far segment's dot is the fp64 one of the default mode, bit for bit
+    from evolutionarydistributedtraining_amd import ops
+    out = torch.empty(plan.seg_offsets[-1], dtype=torch.float32, device=dev)
+    v0 = torch.cat([a_.reshape(-1) for a_, _ in parts]).to(dev)
+    v1 = torch.cat([b_.reshape(-1) for _, b_ in parts]).to(dev)
+    ops.slerp_arena(plan, v0, v1, out, torch.full((2,), 0.5, dtype=torch.float64, device=dev), speculate=False)
+    assert plan.dots[0].item() == dots_band[0].item()
 
 
 def test_refdot_large_tensor(oracle, dev):
@@ -168,3 +177,148 @@ def test_refdot_large_tensor(oracle, dev):
         os.makedirs(d, exist_ok=True)
         with open(os.path.join(d, "refdot_large.json"), "w") as f:
             json.dump({"elements": n, "dtype": "bf16", "merge_with_refdot_ms": round(ms, 3)}, f)
+
+
+def _golden_arena(golden, in_dtype):
+    """Every golden SLERP case of one input dtype as a segment of one arena (inputs repeated per t)."""
+    tens = golden.tensors("slerp")
+    cases = [c for c in golden.slerp_cases() if c["in_dtype"] == in_dtype]
+    parts = [(tens[f"{c['inputs']}/v0"].reshape(-1), tens[f"{c['inputs']}/v1"].reshape(-1)) for c in cases]
+    wants = [tens[f"{c['name']}/out"].reshape(-1).float() for c in cases]
+    return cases, parts, wants
+
+
+@pytest.mark.parametrize("speculate", [False, True])
+@pytest.mark.parametrize("layout", ["arena", "list", "bound"])
+@pytest.mark.parametrize("in_dtype", ["f32", "bf16"])
+def test_refdot_mode_golden_outputs_bit_exact(golden, dev, in_dtype, layout, speculate):
+    """All 100 golden SLERP cases in one multi-segment merge per input dtype: the reference's
+    recorded output, bit for bit, on both branches (generic, far, parallel, anti-parallel, zero,
+    both-zero, one element, long, near the threshold; t in {0, .43, .5, .57, 1})."""
+    from evolutionarydistributedtraining_amd import ops
+    cases, parts, wants = _golden_arena(golden, in_dtype)
+    offs = [0]
+    for a, _ in parts:
+        offs.append(offs[-1] + a.numel())
+    t = torch.tensor([c["t"] for c in cases], dtype=torch.float64, device=dev)
+    ref = ops.RefDot()
+    if layout == "arena":
+        plan = ops.make_slerp_plan(offs, dev)
+        v0 = torch.cat([a for a, _ in parts]).to(dev)
+        v1 = torch.cat([b for _, b in parts]).to(dev)
+        out = torch.empty(offs[-1], dtype=torch.float32, device=dev)
+        ops.slerp_arena(plan, v0, v1, out, t, speculate=speculate, ref_dot=ref)
+        got = [out[offs[i]:offs[i + 1]].cpu() for i in range(len(cases))]
+    else:
+        plan = ops.make_slerp_plan(offs, dev, relative=True)
+        v0s, v1s = [a.to(dev) for a, _ in parts], [b.to(dev) for _, b in parts]
+        outs = [torch.empty(a.numel(), dtype=torch.float32, device=dev) for a, _ in parts]
+        if layout == "list":
+            ops.slerp_list(plan, v0s, v1s, outs, t, speculate=speculate, ref_dot=ref)
+        else:
+            bnd = ops.bind_slerp_list(plan, v0s, v1s, outs)
+            for _ in range(2):                 # a bound table merges again without re-validation
+                bnd.merge(t, speculate=speculate, ref_dot=ref)
+        got = [o.cpu() for o in outs]
+    dots = plan.dots[:len(cases)].cpu().tolist()
+    for c, g, w, d in zip(cases, got, wants, dots):
+        assert d == c["ref_dot"], c["name"]
+        assert torch.equal(g.view(torch.int32), w.view(torch.int32)), c["name"]
+
+
+def _mixed_population(dev, dt, n_members=6, seed=91):
+    """Members over a layout of 9 tensors: lineage members (the lerp branch on most tensors), far
+    ones (the SLERP branch), one tensor per member placed near the threshold."""
+    from evolutionarydistributedtraining_amd.params import ParamLayout
+    sizes = [70001, 33, 131072, 5, 8192 * 3 + 7, 1, 65536, 200003, 640]
+    layout = ParamLayout([(n,) for n in sizes])
+    g = torch.Generator().manual_seed(seed)
+    base = torch.randn(layout.total, generator=g) * 0.02
+    mem = []
+    for m in range(n_members):
+        spread = [0.005, 0.03, 1.0][m % 3]
+        mem.append((base + torch.randn(layout.total, generator=g) * 0.02 * spread).to(dt).to(dev))
+    return layout, mem
+
+
+@pytest.mark.parametrize("out_dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_refdot_mode_every_form_identical(oracle, dev, dt, out_dt):
+    """The same children through every form in reference-dot mode: flat arena (two-pass /
+    speculative), tensor list (two-pass / speculative / bound table), the resident population
+    (Gram / speculative form): bit-identical, and each child equals the reference restatement
+    (oracle.slerp_parts_refdot, rounded to the child's dtype) on every tensor."""
+    from evolutionarydistributedtraining_amd import ops
+    layout, mem = _mixed_population(dev, dt)
+    n, offs = layout.total, layout.offsets
+    pairs = [(0, 1), (1, 2), (2, 0), (3, 5), (4, 4), (5, 3)]
+    t = torch.tensor([0.3, 0.5, 0.9, 0.43333333333333335, 0.0, 1.0, 0.5, 0.7, 0.999], dtype=torch.float64, device=dev)
+    ref = ops.RefDot()
+    plan = ops.make_slerp_plan(offs, dev)
+    lplan = ops.make_slerp_plan(offs, dev, relative=True)
+    results = {}
+    for spec in (False, True):
+        arena = []
+        for i, j in pairs:
+            o = torch.empty(n, dtype=out_dt, device=dev)
+            ops.slerp_arena(plan, mem[i], mem[j], o, t, speculate=spec, ref_dot=ref)
+            arena.append(o)
+        results[("arena", spec)] = arena
+        lists = []
+        for i, j in pairs:
+            o = torch.empty(n, dtype=out_dt, device=dev)
+            sp = lambda x: list(torch.split(x, layout.numels))
+            ops.slerp_list(lplan, sp(mem[i]), sp(mem[j]), sp(o), t, speculate=spec, ref_dot=ref)
+            lists.append(o)
+        results[("list", spec)] = lists
+        outs = [torch.empty(n, dtype=out_dt, device=dev) for _ in pairs]
+        ops.slerp_population(plan, mem, pairs, outs, t, speculate=spec, ref_dot=ref)
+        results[("population", spec)] = outs
+    torch.cuda.synchronize()
+    first = results[("arena", False)]
+    vb = torch.int16 if out_dt == torch.bfloat16 else torch.int32
+    for key, outs in results.items():
+        for q, (o, w) in enumerate(zip(outs, first)):
+            assert torch.equal(o.view(vb), w.view(vb)), (key, q)
+    branches = set()
+    for q, (i, j) in enumerate(pairs):
+        got = first[q].cpu()
+        for s in range(len(layout)):
+            a, b = offs[s], offs[s + 1]
+            want, _, lerp = oracle.slerp_parts_refdot(float(t[s]), mem[i][a:b].cpu(), mem[j][a:b].cpu())
+            branches.add(lerp)
+            want = torch.from_numpy(np.ascontiguousarray(np.ravel(want))).to(out_dt)
+            assert torch.equal(got[a:b].view(vb), want.view(vb)), (q, s)
+    assert branches == {True, False}
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_refdot_mode_sharded_population_virtual_ranks(dev, world):
+    """The link-balanced sharded population in reference-dot mode with the HIP kernels on virtual
+    ranks (segments straddling rank ranges: their parents' pieces sent to the owning rank): every
+    child equals the single-GPU arena merge in that mode, bit for bit."""
+    from evolutionarydistributedtraining_amd import ops
+    from evolutionarydistributedtraining_amd.collectives import VirtualWorld
+    from evolutionarydistributedtraining_amd.distributed import ShardedPopulationCrossover
+    layout, mem = _mixed_population(dev, torch.bfloat16, n_members=world, seed=93)
+    n = layout.total
+    pairs = [((3 * c + 1) % world, (5 * c + 2) % world) for c in range(world)]
+    t = torch.tensor([0.3, 0.5, 0.9, 0.4, 0.2, 0.6, 0.5, 0.7, 0.1], dtype=torch.float64, device=dev)
+    ref = ops.RefDot()
+
+    def body(comm):
+        sp = ShardedPopulationCrossover(layout, torch.bfloat16, dev, comm=comm, chunk_elems=8192)
+        out = torch.empty(n, dtype=torch.bfloat16, device=dev)
+        sp.slerp_step(mem[comm.rank], pairs, t, out, ref_dot=ref)
+        torch.cuda.synchronize()
+        return out, sp.ranges
+
+    res = VirtualWorld(world).run(body)
+    ranges = res[0][1]
+    assert any(ranges[r][4] not in layout.offsets for r in range(world - 1))      # a straddle
+    plan = ops.make_slerp_plan(layout.offsets, dev, chunk_elems=8192)
+    for c, (i, j) in enumerate(pairs):
+        want = torch.empty(n, dtype=torch.bfloat16, device=dev)
+        ops.slerp_arena(plan, mem[i], mem[j], want, t, speculate=False, ref_dot=ref)
+        torch.cuda.synchronize()
+        assert torch.equal(res[c][0].view(torch.int16), want.view(torch.int16)), c

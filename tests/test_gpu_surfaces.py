@@ -225,10 +225,14 @@ def test_rl_crossover_surface(golden, dev, tmp_path):
             assert ((out[k] - want).abs() <= _slerp_tol(want, a, b)).all(), (part, k)
 
 
-def test_evomerge_surface(golden, dev, tmp_path):
-    """run_slerp_merge_from_config on bf16 Qwen2 bodies, result written into model_1 (bf16)."""
+@pytest.mark.parametrize("ref", [False, True])
+def test_evomerge_surface(golden, dev, tmp_path, ref):
+    """run_slerp_merge_from_config on bf16 Qwen2 bodies, result written into model_1 (bf16): the
+    single pass into a fresh buffer, model_1's parameters re-pointed at it (merge.slerp_into_module_).
+    ref=True (merge.set_reference_dot(RefDot())): the reference's saved output, bit for bit."""
     from transformers import Qwen2Config, Qwen2ForCausalLM
     from evolutionarydistributedtraining_amd import evomerge_crossover as ev
+    from evolutionarydistributedtraining_amd import merge, ops
     t = golden.tensors("merge_models")
     rec = [r for r in golden.manifest["merge_models"] if r["name"] == "evomerge"][0]
     cfg = Qwen2Config(vocab_size=24, hidden_size=8, intermediate_size=16, num_hidden_layers=5,
@@ -241,14 +245,23 @@ def test_evomerge_surface(golden, dev, tmp_path):
             m.lm_head.weight.copy_(t["merge_models/evomerge/out_lm_head"])
         models.append(m.to(dev))
     merge_cfg = ev.slerp_config("a", "b", 5)
-    ev.run_slerp_merge_from_config(merge_cfg, models[0].model, models[1].model, cfg, cfg, str(tmp_path / "o"),
-                                   base_model=models[0])
+    before = {k: p.data_ptr() for k, p in models[0].model.named_parameters()}
+    prev = merge.set_reference_dot(ops.RefDot() if ref else None)
+    try:
+        ev.run_slerp_merge_from_config(merge_cfg, models[0].model, models[1].model, cfg, cfg, str(tmp_path / "o"),
+                                       base_model=models[0])
+    finally:
+        merge.set_reference_dot(prev)
+    after = {k: p.data_ptr() for k, p in models[0].model.named_parameters()}
+    assert all(after[k] != before[k] for k in rec["keys"])          # re-pointed at the fresh buffer
     sd = models[0].model.state_dict()
     n_exact = n = 0
     for k in rec["keys"]:
         want = t[f"merge_models/evomerge/out/{k}"]
         got = sd[k].cpu()
         assert got.dtype == torch.bfloat16
+        if ref:
+            assert torch.equal(got.view(torch.int16), want.view(torch.int16)), k
         d = (got.float() - want.float()).abs()
         assert (d <= _ulp_bf16(want) * 1.0001).all(), k          # fp32 result within tol -> <= 1 bf16 ulp
         n_exact += int((d == 0).sum())

@@ -360,20 +360,30 @@ def test_examples_import_and_model_runs_on_cpu():
     assert loss.ndim == 0 and float(loss) > 0
 
 
-def test_spans_apart_matches_brute_force():
-    """ops._spans_apart (the speculative list form's overlap check, numpy sweep) against a
-    pairwise check on random spans, empty spans included."""
+def test_seg_table_overlap_check_matches_brute_force():
+    """edt_slerp_seg_table's apart check (the single-pass list form's: a sorted-span sweep in C)
+    against a pairwise check of every output byte range with every parent byte range, on random
+    16-byte-aligned tensors of fp32 parents and fp32 / bf16 outputs, empty tensors included."""
+    import ctypes
     import random
-    from evolutionarydistributedtraining_amd import ops
+    from evolutionarydistributedtraining_amd import _lib as L
+    lib = L.load_library()
 
-    def brute(op, ob, ip, ib):
-        return not any(n and m and a < c + m and c < a + n for a, n in zip(op, ob) for c, m in zip(ip, ib))
+    def brute(spans_in, spans_out):
+        return not any(n and m and a < c + m and c < a + n for a, n in spans_out for c, m in spans_in)
 
     rnd = random.Random(5)
+    base = 1 << 40
     for _ in range(3000):
-        ni, no = rnd.randint(0, 6), rnd.randint(0, 6)
-        ip = [rnd.randint(0, 200) for _ in range(ni)]
-        ib = [rnd.choice([0, 1, 5, 20, 50]) for _ in range(ni)]
-        op = [rnd.randint(0, 200) for _ in range(no)]
-        ob = [rnd.choice([0, 1, 5, 20, 50]) for _ in range(no)]
-        assert ops._spans_apart(op, ob, ip, ib) == brute(op, ob, ip, ib)
+        T = rnd.randint(1, 5)
+        osz = rnd.choice([4, 2])
+        sizes = [rnd.choice([0, 1, 4, 5, 20, 50]) for _ in range(T)]
+        ptr = lambda: base + 16 * rnd.randint(0, 40)
+        p0, p1, po = [ptr() for _ in range(T)], [ptr() for _ in range(T)], [ptr() for _ in range(T)]
+        arr = lambda xs: (ctypes.c_void_p * T)(*xs)
+        host = (ctypes.c_uint64 * (3 * T))()
+        rc = lib.edt_slerp_seg_table(arr(p0), arr(p1), arr(po), T, (ctypes.c_uint64 * T)(*sizes), L.EDT_F32,
+                                     L.EDT_F32 if osz == 4 else L.EDT_BF16, 1, ctypes.cast(host, ctypes.c_void_p))
+        ins = [(p, 4 * n) for p, n in zip(p0 + p1, sizes + sizes)]
+        outs = [(p, osz * n) for p, n in zip(po, sizes)]
+        assert (rc == 0) == brute(ins, outs), (sizes, p0, p1, po, osz)
