@@ -8,6 +8,7 @@ raises `EdtError`.
 from __future__ import annotations
 
 import ctypes
+import threading
 from dataclasses import dataclass
 
 import torch
@@ -224,30 +225,35 @@ def lerp(t: float, v0: torch.Tensor, v1: torch.Tensor, out: torch.Tensor | None 
 # ------------------------------------------------------------------------------------------
 # SLERP over a multi-tensor arena
 
-_POOLS: dict = {}
+_TLS = threading.local()             # per host thread: {(device, stream): float64 buffer}
 
 
 def _scratch(device: torch.device, ndoubles: int) -> torch.Tensor:
-    """float64 device workspace of `ndoubles` (a view) from one growing buffer per (device, stream).
-    The chunk-sum passes' rows and row scratch are only live inside one call, so every plan on a
-    stream shares one buffer instead of each cached plan holding its own (7B body: 107,893 chunks
-    x 387 doubles = 334 MB for a pair merge; the population speculative form 3,096 doubles per
-    chunk at 8 children = 2.7 GB). Calls on one stream run in order, so a later call
-    overwrites the rows only after the earlier call's kernels are done."""
+    """float64 device workspace of `ndoubles` (a view) from one growing buffer per (device, stream)
+    of the calling host thread. The chunk-sum passes' rows and row scratch are only live inside one
+    call, so every plan shares one buffer instead of each cached plan holding its own (7B body:
+    107,893 chunks x 387 doubles = 334 MB for a pair merge; the population speculative form 3,096
+    doubles per chunk at 8 children = 2.7 GB). Calls issued by one thread on one
+    stream run in order, so a later call overwrites the rows only after the earlier call's kernels
+    are done; threads issuing onto one stream (virtual ranks) interleave their launches, hence a
+    buffer per thread (released with the thread)."""
+    pools = getattr(_TLS, "pools", None)
+    if pools is None:
+        pools = _TLS.pools = {}
     dev = torch.device(device)
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     key = (idx, torch.cuda.current_stream(dev).cuda_stream)
-    buf = _POOLS.get(key)
+    buf = pools.get(key)
     n = max(1, int(ndoubles))
     if buf is None or buf.numel() < n:
-        _POOLS.pop(key, None)
-        buf = _POOLS[key] = torch.empty(n, dtype=torch.float64, device=dev)
+        pools.pop(key, None)
+        buf = pools[key] = torch.empty(n, dtype=torch.float64, device=dev)
     return buf[:n]
 
 
 def release_scratch() -> None:
-    """Drop the pooled SLERP workspaces (bench.py frees them between workloads)."""
-    _POOLS.clear()
+    """Drop this thread's pooled SLERP workspaces (bench.py frees them between workloads)."""
+    _TLS.pools = {}
 
 
 @dataclass
