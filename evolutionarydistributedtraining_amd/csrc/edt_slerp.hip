@@ -1975,8 +1975,9 @@ static int refdot_impl(const void* v0, const void* v1, int in_dt, const uint64_t
         return fail(EDT_ERR_ARG, "reference-dot mode needs chunks of a multiple of %d elements (got %u)", kRefBuf,
                     chunk_elems);
     if (nseg == 0) return EDT_OK;
-    if (!chunk_desc || !seg_first_chunk || !ref_dot || !workspace) return fail(EDT_ERR_ARG, "null buffer");
-    if (!seg_ptrs && (!v0 || !v1)) return fail(EDT_ERR_ARG, "null buffer");
+    if (!seg_first_chunk || !ref_dot || !workspace) return fail(EDT_ERR_ARG, "null buffer");
+    // no chunks: nothing is read (every flagged segment's dot is the empty sum, 0)
+    if (nchunks > 0 && (!chunk_desc || (!seg_ptrs && (!v0 || !v1)))) return fail(EDT_ERR_ARG, "null buffer");
     const uint64_t need = edt_slerp_refdot_workspace_bytes(nseg, nchunks, chunk_elems, threads);
     if (workspace_bytes < need) return fail(EDT_ERR_ARG, "workspace of %llu bytes needed", (unsigned long long)need);
     if (reinterpret_cast<uintptr_t>(workspace) & 7u) return fail(EDT_ERR_ARG, "workspace must be 8-byte aligned");
