@@ -5,7 +5,7 @@ set -u
 cd "$(dirname "$0")/.."
 R=$(pwd); OUT=$R/gpurun_out/${TAG:-r4check}
 mkdir -p $OUT
-timeout -k 10 900 python -u -m pytest tests -m gpu --maxfail=10 -q --timeout 300 --timeout-method thread -p no:cacheprovider \
+timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu --maxfail=10 -q --timeout 300 --timeout-method thread -p no:cacheprovider \
     > $OUT/pytest_gpu.log 2>&1; s=$?
 tail -5 $OUT/pytest_gpu.log; [ $s -eq 0 ] || exit $s
 if [ "${PROBE:-1}" = 1 ]; then

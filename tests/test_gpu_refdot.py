@@ -266,10 +266,10 @@ def test_refdot_mode_every_form_identical(oracle, dev, dt, out_dt):
         results[("arena", spec)] = arena
         lists = []
         for i, j in pairs:
-            o = torch.empty(n, dtype=out_dt, device=dev)
-            sp = lambda x: list(torch.split(x, layout.numels))
-            ops.slerp_list(lplan, sp(mem[i]), sp(mem[j]), sp(o), t, speculate=spec, ref_dot=ref)
-            lists.append(o)
+            sp = lambda x: [p.clone() for p in torch.split(x, layout.numels)]    # separate (aligned) tensors
+            outs = [torch.empty(m, dtype=out_dt, device=dev) for m in layout.numels]
+            ops.slerp_list(lplan, sp(mem[i]), sp(mem[j]), outs, t, speculate=spec, ref_dot=ref)
+            lists.append(torch.cat(outs))
         results[("list", spec)] = lists
         outs = [torch.empty(n, dtype=out_dt, device=dev) for _ in pairs]
         ops.slerp_population(plan, mem, pairs, outs, t, speculate=spec, ref_dot=ref)
