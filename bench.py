@@ -131,6 +131,11 @@ def parse(argv=None):
                         "it has and every rank exits (0: no deadline)")
     p.add_argument("--config-layouts", default="configs2_125m_fp32=gpt2_small:f32,configs3_1p3b_bf16=gpt_1p3b:bf16",
                    help="N>1 baseline_configs: key=layout:dtype,... (BASELINE configs[2] and [3])")
+    p.add_argument("--parity-layout", default="tiny_llama",
+                   help="N > 1: layout of the post-timing parity check of the sharded schedule (gathered "
+                        "to rank 0 and compared with the single-GPU kernels); '' = skip")
+    p.add_argument("--parity-bucket-elems", type=int, default=1 << 20,
+                   help="bucket size of the parity check (several buckets even on the small layout)")
     p.add_argument("--population-layout", default="qwen2p5_7b_body",
                    help="N>1 population_slerp_7b: the member layout (BASELINE configs[4]: the 7.07B body)")
     return p.parse_args(argv)
@@ -213,7 +218,7 @@ class ExtrasDeadline:
 
     def _fire(self):
         self.fired = True
-        pending = [k for k in ("weak_scaling", "other_schedules", "baseline_configs", "population_slerp_7b")
+        pending = [k for k in ("parity", "weak_scaling", "other_schedules", "baseline_configs", "population_slerp_7b")
                    if self.out is not None and k not in self.out]
         self.emit({"extras_deadline": {"seconds": self.seconds, "unfinished_or_skipped": pending,
                                        "note": "the extras after the value did not finish in time; the "
@@ -312,6 +317,138 @@ def synth_sharded(theta: torch.Tensor, workers: list[torch.Tensor], rank: int) -
         theta[a:b].copy_(t)
         for w in workers:
             w[a:b].copy_(t + torch.randn(b - a, generator=gw, device=dev) * 1e-3)
+
+
+def _ordered_bits(x: torch.Tensor) -> torch.Tensor:
+    """Floats as integers in value order (int64): |a - b| of two of them is their distance in ulps."""
+    if x.dtype == torch.bfloat16:
+        i = x.view(torch.int16).to(torch.int64)
+        return torch.where(i < 0, -(i & 0x7FFF), i)
+    i = x.float().view(torch.int32).to(torch.int64)
+    return torch.where(i < 0, -(i & 0x7FFFFFFF), i)
+
+
+def _max_ulp(a: torch.Tensor, b: torch.Tensor) -> int:
+    if a.numel() == 0:
+        return 0
+    return int((_ordered_bits(a) - _ordered_bits(b)).abs().max().item())
+
+
+def _digest(*tensors) -> str:
+    import hashlib
+    h = hashlib.sha256()
+    for t in tensors:
+        h.update(t.detach().contiguous().cpu().view(torch.uint8).numpy().tobytes())
+    return h.hexdigest()[:16]
+
+
+def sharded_parity(args, comm, rt, kernels, mode, broadcast, k_local, tdt, wdt, steps=2) -> dict | None:
+    """Correctness of the N > 1 line's exchange (EDT_LM/diloco.py:238-289 across ranks): the timed
+    schedule (same mode, broadcast and workers per GPU) runs `steps` outer steps over a small layout
+    (several buckets), every rank's theta replica (and, broadcast='workers', its worker arenas) is
+    digested, and rank 0 recomputes the whole population on its own GPU from the same seeds with the
+    single-GPU kernels: `exact` must equal the fused kernel over all K workers bit for bit,
+    `reduce_ordered` per-rank edt_delta_partial + edt_sgd_apply_sum in rank order, `reduce` (RCCL's
+    own summation order) is reported in ulps. A collective that moved wrong bytes shows up here.
+    Every rank takes part; rank 0 returns the record."""
+    from evolutionarydistributedtraining_amd import ops
+    from evolutionarydistributedtraining_amd.distributed import ShardedOuterSync
+    from evolutionarydistributedtraining_amd.layouts import LAYOUTS
+    k = kernels or ops
+    lay = LAYOUTS[args.parity_layout]()
+    n, world, rank = lay.total, comm.world, comm.rank
+    sync = ShardedOuterSync(lay, tdt, wdt, k_local, rt.dev, args.lr, args.momentum, bool(args.nesterov), mode=mode,
+                            bucket_elems=args.parity_bucket_elems, broadcast=broadcast, comm=comm, kernels=kernels)
+    synth_sharded(sync.theta.flat, [w.flat for w in sync.workers], rank)
+    for _ in range(steps):
+        sync.step()
+    rt.sync()
+    theta = sync.gather_theta()[:n].clone()
+    rt.sync()
+    mine = [theta] + ([sync.worker_bufs[0][:n]] if sync.broadcast == "workers" else [])
+    digests = comm.all_gather_object(_digest(*mine))
+    sched, nb = f"{sync.mode}/{sync.broadcast}", len(sync.buckets)
+    w0 = sync.worker_bufs[0][:n].clone() if sync.broadcast == "workers" else None
+    del sync
+    rt.empty_cache()
+    if rank != 0:
+        return None
+    dev, K = rt.dev, k_local * world
+    th = torch.empty(n, dtype=tdt, device=dev)
+    ws = [torch.empty(n, dtype=wdt, device=dev) for _ in range(K)]
+    for r in range(world):                       # the ranks' inputs, from their seeds
+        synth_sharded(th, ws[r * k_local:(r + 1) * k_local], r)
+    mom = torch.zeros(n, dtype=tdt, device=dev) if args.momentum else None
+    for i in range(steps):
+        has = i > 0 and mom is not None
+        if sched.startswith("exact"):
+            k.outer_step(th, ws, mom, has, args.lr, args.momentum, bool(args.nesterov))
+        else:
+            accs = []
+            for r in range(world):
+                acc = torch.empty(n, dtype=torch.float32, device=dev)
+                k.delta_partial(th, ws[r * k_local:(r + 1) * k_local], K, acc, False)
+                accs.append(acc)
+            if hasattr(k, "sgd_apply_sum"):
+                k.sgd_apply_sum(th, accs, mom, has, args.lr, args.momentum, bool(args.nesterov))
+            else:
+                total = accs[0].clone()
+                for a in accs[1:]:
+                    total.add_(a)
+                k.sgd_apply(th, total, mom, has, args.lr, args.momentum, bool(args.nesterov))
+        if sched.endswith("/workers"):
+            for w in ws:
+                w.copy_(th)
+    rt.sync()
+    max_ulp = _max_ulp(theta, th)
+    bit_exact = bool(torch.equal(_ordered_bits(theta), _ordered_bits(th)))
+    want = [th] + ([th.to(wdt)] if w0 is not None else [])
+    if w0 is not None:
+        bit_exact = bit_exact and bool(torch.equal(_ordered_bits(w0), _ordered_bits(want[1])))
+        max_ulp = max(max_ulp, _max_ulp(w0, want[1]))
+    ref_digest = _digest(*want)
+    rec = {"schedule": sched, "layout": args.parity_layout, "params": n, "buckets": nb, "steps": steps,
+           "workers": K, "bit_exact": bit_exact, "max_ulp": max_ulp,
+           "replicas_identical": len(set(digests)) == 1, "replicas_equal_reference": all(d == ref_digest for d in digests),
+           "reference": ("the fused single-GPU kernel over all K workers (edt_outer_step)" if sched.startswith("exact")
+                         else "per-rank edt_delta_partial + edt_sgd_apply_sum in rank order")}
+    if sched.startswith("reduce/"):
+        rec["note"] = "RCCL's reduce-scatter sums in its own order: ulps, not bits (DESIGN.md §3)"
+    del th, ws, mom
+    rt.empty_cache()
+    return rec
+
+
+def population_parity(lay, rt, comm, kernels, member_seed, pairs, t, child) -> dict | None:
+    """Child 0 of the sharded population (on rank 0 after the timed runs) against the whole-
+    population passes on rank 0 alone (Gram sums -> coefficients -> blend over its two parents,
+    regenerated from their seeds): bit-identical to edt_slerp_merge by construction,
+    so any byte an exchange moved wrong shows. Rank 0 only."""
+    if comm.rank != 0:
+        return None
+    from evolutionarydistributedtraining_amd import ops
+    k = kernels or ops
+    dev, bf = rt.dev, torch.bfloat16
+    P = lay.total
+    i, j = pairs[0]
+    mem = []
+    for m in sorted({i, j}):
+        x = torch.empty(P, dtype=bf, device=dev)
+        member_seed(x, m)
+        mem.append(x)
+    idx = {m: q for q, m in enumerate(sorted({i, j}))}
+    plan = k.make_slerp_plan(lay.offsets, dev)
+    gram = k.slerp_gram(mem, plan.chunks, plan.nchunks)
+    coef, _ = k.slerp_gram_coef(plan, gram, len(mem), [(idx[i], idx[j])], t)
+    want = torch.empty(P, dtype=bf, device=dev)
+    k.slerp_blend_children(mem, [(idx[i], idx[j])], [want], plan.chunks, plan.nchunks, coef, plan.nseg)
+    rt.sync()
+    rec = {"child": 0, "parents": [i, j], "bit_exact": bool(torch.equal(want.view(torch.int16), child.view(torch.int16))),
+           "max_ulp": _max_ulp(want, child),
+           "reference": "the whole-population Gram / coefficient / blend passes on rank 0 (== edt_slerp_merge)"}
+    del mem, want, gram
+    rt.empty_cache()
+    return rec
 
 
 def cpu_baseline(args, theta_dtype, worker_dtype, k):
@@ -635,11 +772,13 @@ def bench_population(args, rt, comm, kernels=None, layout_name="qwen2p5_7b_body"
     lay = LAYOUTS[layout_name]()
     rank, world, dev = comm.rank, comm.world, rt.dev
     P, bf = lay.total, torch.bfloat16
-    g = torch.Generator(device=dev).manual_seed(100 + rank)
+    def member_seed(x, m):                  # member m, from its own seed (any rank can rebuild it)
+        g = torch.Generator(device=dev).manual_seed(100 + m)
+        for s0 in range(0, P, 1 << 28):
+            e = min(P, s0 + (1 << 28))
+            x[s0:e] = (torch.randn(e - s0, generator=g, device=dev) * 0.02).to(bf)
     member = torch.empty(P, dtype=bf, device=dev)
-    for s0 in range(0, P, 1 << 28):
-        e = min(P, s0 + (1 << 28))
-        member[s0:e] = (torch.randn(e - s0, generator=g, device=dev) * 0.02).to(bf)
+    member_seed(member, rank)
     out = torch.empty(P, dtype=bf, device=dev)
     t = torch.full((len(lay),), 0.5, dtype=torch.float64, device=dev)
     pairs = [((3 * c + 1) % world, (5 * c + 2) % world) for c in range(world)]
@@ -669,6 +808,10 @@ def bench_population(args, rt, comm, kernels=None, layout_name="qwen2p5_7b_body"
                              "frac": round(wire / (ms / 1e3) / 1e9 / peak, 4) if peak else None}}
         del sp
         rt.empty_cache()
+        rec = population_parity(lay, rt, comm, kernels, member_seed, pairs, t, out)
+        if rec is not None:
+            res[key]["parity"] = rec
+        comm.barrier()
     pc = PopulationCrossover(lay, bf, dev, comm=comm, kernels=kernels)
     res["per_child"] = {"ms": round(timed(lambda: pc.slerp_step(member, pairs, t, out), 3), 3)}
     del pc, member, out
@@ -871,8 +1014,20 @@ def run_sharded(args, comm, rt, json_out, kernels=None, exit_fn=None) -> dict | 
                 out["cpu_baseline"] = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
     comm.barrier()
     deadline = ExtrasDeadline(args.extras_deadline, rank, out, json_out, exit_fn=exit_fn)
+    mode_used, bcast_used = sync.mode, sync.broadcast
     sync = None
     rt.empty_cache()
+    if args.parity_layout:
+        # the exchange's correctness, first of the extras: the timed schedule on a small layout,
+        # gathered and compared on rank 0 with the single-GPU kernels
+        try:
+            par = sharded_parity(args, comm, rt, kernels, mode_used, bcast_used, k_local, tdt, wdt)
+        except Exception as e:     # an extra after the value: report it, keep the line
+            par = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
+            rt.empty_cache()
+        if out is not None:
+            out["parity"] = par
+        comm.barrier()
     if scaling == "strong" and args.weak_companion:     # (world 1: --sharded rehearsal)
         # the same schedule with the N = 1 population on EVERY rank (population x N): per-GPU
         # work fixed, so value_N / (N value_1) isolates the cost of the xGMI exchange

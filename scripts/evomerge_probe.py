@@ -1,0 +1,88 @@
+"""The EVOMERGE drop-in's merge at full size (EDT_EVOMERGE/train/crossover.py:104-146, BASELINE
+configs[4]'s per-child merge): two Qwen2.5-7B-shaped causal LMs in bf16 on the GPU, model_1.model
+merged with model_2.model INTO model_1 (the reference's base_model = model_1), timed as the surface
+runs it — merge.slerp_into_module_ (the single pass into a fresh buffer + re-pointing model_1's
+parameters) against writing into model_1's own tensors (the two-pass in-place form r3 used) — with
+host work included (state_dict, the key plan, the checks, the pointer table), wall clock around a
+device synchronize. Both must give the same bits. Lineage parents (model_2 = model_1 + small
+noise: every tensor takes the lerp branch, as fine-tunes of one base do) or --far.
+
+    python scripts/evomerge_probe.py [--rounds 5] [--far] [--layers 28]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--far", action="store_true")
+    ap.add_argument("--layers", type=int, default=28)
+    a = ap.parse_args()
+    from transformers import Qwen2Config, Qwen2ForCausalLM
+
+    from evolutionarydistributedtraining_amd import evomerge_crossover as ev
+    from evolutionarydistributedtraining_amd import merge
+    dev = torch.device("cuda:0")
+    cfg = Qwen2Config(vocab_size=152064, hidden_size=3584, intermediate_size=18944, num_hidden_layers=a.layers,
+                      num_attention_heads=28, num_key_value_heads=4, tie_word_embeddings=False)
+    torch.set_default_dtype(torch.bfloat16)
+    with torch.device(dev):
+        m1 = Qwen2ForCausalLM(cfg)
+        m2 = Qwen2ForCausalLM(cfg)
+    torch.set_default_dtype(torch.float32)
+    g = torch.Generator(device=dev).manual_seed(3)
+    with torch.no_grad():
+        for p1, p2 in zip(m1.model.parameters(), m2.model.parameters()):
+            p1.copy_(torch.randn(p1.shape, generator=g, device=dev) * 0.02)
+            noise = torch.randn(p1.shape, generator=g, device=dev) * 0.02
+            p2.copy_(noise if a.far else p1.float() + noise * 0.005)
+    n = sum(p.numel() for p in m1.model.parameters())
+    mcfg = ev.slerp_config("a", "b", cfg.num_hidden_layers)
+    keys = list(m1.model.state_dict().keys())
+    plan = merge.merge_plan(keys, cfg.num_hidden_layers, mcfg)
+    start = {k: v.clone() for k, v in m1.model.state_dict().items()}
+
+    def reset():
+        with torch.no_grad():
+            for k, p in m1.model.named_parameters():
+                p.data = start[k].clone()
+        torch.cuda.synchronize()
+
+    def rebind_merge():
+        merge.slerp_into_module_(m1.model, m1.model.state_dict(), m2.model.state_dict(), plan, torch.bfloat16,
+                                 device=dev)
+
+    def in_place_merge():
+        tsd = m1.model.state_dict()
+        merge.slerp_state_dicts(m1.model.state_dict(), m2.model.state_dict(), plan, out_dtype=torch.bfloat16,
+                                device=dev, out=tsd)
+
+    outs, times = {}, {}
+    for name, f in (("single_pass_rebind", rebind_merge), ("two_pass_in_place", in_place_merge)):
+        ts = []
+        for r in range(a.rounds + 1):
+            reset()
+            t0 = time.perf_counter()
+            f()
+            torch.cuda.synchronize()
+            ts.append((time.perf_counter() - t0) * 1e3)
+        times[name] = ts[1:]                       # the first call builds the cached plan
+        outs[name] = torch.cat([p.detach().reshape(-1) for p in m1.model.parameters()]).view(torch.int16).clone()
+    same = bool(torch.equal(outs["single_pass_rebind"], outs["two_pass_in_place"]))
+    res = {k: {"median_ms": round(statistics.median(v), 3), "min_ms": round(min(v), 3),
+               "TBps_algorithmic": round(6 * n / (statistics.median(v) / 1e3) / 1e12, 3)} for k, v in times.items()}
+    print(json.dumps({"probe": "evomerge_surface", "params_body": n, "tensors": len(keys), "far": a.far,
+                      "outputs_bit_identical": same, "results": res}))
+
+
+if __name__ == "__main__":
+    main()

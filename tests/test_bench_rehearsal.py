@@ -19,13 +19,15 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 LAYOUTS = {"rehearsal_main": [(64, 33), (257,), (31, 17), (1000,)],
+           "rehearsal_parity": [(61, 37), (129,), (5,), (3000,)],
            "rehearsal_c2": [(40, 24), (24,), (333,)],
            "rehearsal_c3": [(128, 9), (77,)],
            "rehearsal_pop": [(300,), (17, 19), (1024,)]}
 ARGS = ["--layout", "rehearsal_main", "--population", "4", "--steps", "2", "--warmup", "1",
         "--cpu-baseline-seconds", "0.2", "--cpu-sample-elems", "4096", "--bucket-elems", "2048",
         "--config-layouts", "configs2_125m_fp32=rehearsal_c2:f32,configs3_1p3b_bf16=rehearsal_c3:bf16",
-        "--population-layout", "rehearsal_pop", "--population-groups", "2"]
+        "--population-layout", "rehearsal_pop", "--population-groups", "2",
+        "--parity-layout", "rehearsal_parity", "--parity-bucket-elems", "1024"]
 
 
 def _rank_main():
@@ -54,14 +56,42 @@ def _rank_main():
                 time.sleep(120)                  # a peer that never answers: the deadline must fire
             return super().slerp_gram(members, chunks, nchunks, gram)
 
+    class Corrupting(TorchCollectives):
+        """Every received buffer's first element nudged after the collective lands: what a
+        collective that moved wrong bytes looks like to the schedule (REHEARSAL_CORRUPT=1)."""
+
+        def _after(self, work, out, async_op):
+            def nudge():
+                if out.numel():
+                    out.view(-1)[0] += 1
+            if not async_op:
+                nudge()
+                return work
+
+            class W:
+                def wait(self_inner):
+                    work.wait()
+                    nudge()
+            return W()
+
+        def all_gather(self, out, inp, async_op=False):
+            return self._after(super().all_gather(out, inp, async_op), out, async_op)
+
+        def all_to_all(self, out, inp, async_op=False):
+            return self._after(super().all_to_all(out, inp, async_op), out, async_op)
+
+        def reduce_scatter(self, out, inp, async_op=False):
+            return self._after(super().reduce_scatter(out, inp, async_op), out, async_op)
+
     torch.set_num_threads(2)
     dist.init_process_group("gloo", rank=int(os.environ["RANK"]), world_size=int(os.environ["WORLD_SIZE"]))
     args = bench.parse(json.loads(os.environ["REHEARSAL_ARGS"]))
-    bench.run_sharded(args, TorchCollectives(), bench.Runtime("cpu"), sys.stdout, kernels=Kernels(oracle))
+    comm = Corrupting() if os.environ.get("REHEARSAL_CORRUPT") == "1" else TorchCollectives()
+    bench.run_sharded(args, comm, bench.Runtime("cpu"), sys.stdout, kernels=Kernels(oracle))
     dist.destroy_process_group()
 
 
-def _launch(world, extra=(), hang_rank=-1, timeout=240):
+def _launch(world, extra=(), hang_rank=-1, timeout=240, corrupt=False):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
@@ -69,7 +99,8 @@ def _launch(world, extra=(), hang_rank=-1, timeout=240):
     for r in range(world):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), REHEARSAL_ARGS=json.dumps(ARGS + ["--gpus", str(world)] + list(extra)),
-                   REHEARSAL_HANG_RANK=str(hang_rank), OMP_NUM_THREADS="2")
+                   REHEARSAL_HANG_RANK=str(hang_rank), OMP_NUM_THREADS="2",
+                   REHEARSAL_CORRUPT="1" if corrupt else "0")
         procs.append(subprocess.Popen([sys.executable, "-c", "from tests.test_bench_rehearsal import _rank_main; "
                                        "_rank_main()"], cwd=ROOT, env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.PIPE, text=True))
@@ -110,6 +141,33 @@ def test_bench_line_at_world(world):
     assert "error" not in pop and {"sharded", "sharded_pipelined", "per_child"} <= set(pop), pop
     assert pop["sharded"]["wire_bytes_per_rank"] > 0
     assert "extras_deadline" not in d
+    par = d["parity"]                          # the exchange moved the right bytes
+    assert "error" not in par, par
+    assert par["bit_exact"] and par["max_ulp"] == 0 and par["replicas_identical"], par
+    assert par["replicas_equal_reference"] and par["buckets"] > 1 and par["schedule"] == d["config"]["parallelism"].split()[1]
+    assert pop["sharded"]["parity"]["bit_exact"], pop["sharded"]
+    assert pop["sharded_pipelined"]["parity"]["bit_exact"], pop["sharded_pipelined"]
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("corrupt", [False, True])
+@pytest.mark.parametrize("mode,world", [("exact", 2), ("reduce_ordered", 2), ("reduce_ordered", 3)])
+def test_bench_parity_per_schedule(mode, world, corrupt):
+    """The parity record of each bit-exact schedule: clean collectives give the single-GPU kernels'
+    bits; a collective that delivers one wrong element per buffer leaves the value reported but
+    flips the record (so the driver's first 8-GPU line is evidence of correctness, not only of
+    speed)."""
+    outs, lines = _launch(world, extra=["--mode", mode, "--broadcast", "theta", "--compare-schedules", "0",
+                                        "--config-companions", "0", "--weak-companion", "0", "--ops", "",
+                                        "--population", "6"], corrupt=corrupt)
+    assert all(rc == 0 for rc, _, _ in outs), [(rc, e[-2000:]) for rc, _, e in outs]
+    d = json.loads(lines[0])
+    par = d["parity"]
+    assert par["schedule"] == f"{mode}/theta" and par["workers"] == 6, par
+    if corrupt:
+        assert not par["bit_exact"] and par["max_ulp"] > 0 and not par["replicas_equal_reference"], par
+    else:
+        assert par["bit_exact"] and par["max_ulp"] == 0 and par["replicas_equal_reference"], par
 
 
 @pytest.mark.slow
