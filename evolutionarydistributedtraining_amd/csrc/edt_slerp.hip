@@ -86,6 +86,33 @@ __device__ __forceinline__ void tile_reduce(const double (&v)[N], double (&r)[Re
     for (int s = 0; s < N2; ++s) r[s] = row_butterfly(r[s]);
 }
 
+// tile_reduce's swap levels (32 and 16) alone: r[s] on lane l = the level-16 partial of value
+// red_index<N>(s, l), i.e. of the 16-lane row l / 16, position l % 16 in it.
+template <int N>
+__device__ __forceinline__ void tile_swap_levels(const double (&v)[N], double (&r)[Red<N>::N2]) {
+    constexpr int H1 = Red<N>::H1, N1 = Red<N>::N1, H2 = Red<N>::H2;
+    double r1[N1];
+#pragma unroll
+    for (int k = 0; k < H1; ++k) r1[k] = swap_sum<32>(v[k], v[H1 + k]);
+    if constexpr (N & 1) r1[H1] = swap_sum<32>(v[N - 1], v[N - 1]);
+#pragma unroll
+    for (int k = 0; k < H2; ++k) r[k] = swap_sum<16>(r1[k], r1[H2 + k]);
+    if constexpr (N1 & 1) r[H2] = swap_sum<16>(r1[N1 - 1], r1[N1 - 1]);
+}
+
+// row_butterfly's total (levels 8, 4, 2, 1 of the xor butterfly) of one row's 16 level-16
+// partials p[i] (i = position in the row), formed serially by one lane in the butterfly's own
+// pairing — lane 0's sums: (p0 + p8), then + (p4 + p12), ... — so bit-identical to it (fp64
+// addition is commutative: a lane forming partner + self gets the same bits).
+__device__ __forceinline__ double row_tree16(const double (&p)[16]) {
+    double q8[8], q4[4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) q8[i] = p[i] + p[i + 8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q4[i] = q8[i] + q8[i + 4];
+    return (q4[0] + q4[2]) + (q4[1] + q4[3]);
+}
+
 // Which value slot s of lane `lane` holds after tile_reduce<N>, and whether this lane is the one
 // writer of it (a leftover value at an odd level is held by both halves).
 template <int N>
@@ -711,56 +738,140 @@ __device__ __forceinline__ void pick(const float (&x)[M][N], int idx, float (&y)
         }
 }
 
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t x) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(x >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+}
+
+// The first element's products start each lane's chains: fma(x, y, +0.0) (the canonical chain's
+// first step from 0.0, one VOP3 FMA with an inline zero instead of a zero move + accumulate).
+template <int M, int N, typename X>
+__device__ __forceinline__ void gram_fma_first(const X (&x)[M], double (&g)[M * (M + 1) / 2]) {
+#pragma unroll
+    for (int a = 0; a < M; ++a) {
+        const double da = x[a][0];
+#pragma unroll
+        for (int b = a; b < M; ++b) g[tri_index(a, b, M)] = __builtin_fma(da, (double)x[b][0], 0.0);
+    }
+#pragma unroll
+    for (int j = 1; j < N; ++j) {
+#pragma unroll
+        for (int a = 0; a < M; ++a) {
+            const double da = x[a][j];
+#pragma unroll
+            for (int b = a; b < M; ++b) {
+                const double db = x[b][j];
+                g[tri_index(a, b, M)] = __builtin_fma(da, db, g[tri_index(a, b, M)]);
+            }
+        }
+    }
+}
+
 // Gram rows (level 4), one workgroup per unit of 16 tiles in address order: wave w takes tiles
-// 16 g + 4 w .. + 3 one after the other (one vector per member per lane: M loads in flight), each
-// tile's sums butterflied as pair_tile's and parked in LDS; after the barrier wave 0's lanes
-// (one per sum) combine the 16 tile sums as the tree does and store the unit's row (unit_slot).
+// 16 g + 4 w .. + 3 one after the other (one vector per member per lane: M loads in flight). Each
+// tile's NT sums go through the xor butterfly in two parts: the swap levels (32, 16) on the VALU,
+// transposed (tile_swap_levels), then the row levels (8 .. 1) SERIALLY — every lane parks its
+// level-16 partials in LDS and lane q reads value q's 16 partials and adds them in the butterfly's
+// own pairing (row_tree16): NT serial 15-add trees on NT lanes at once instead of NT / 4 values x 4
+// DPP levels on all lanes plus the per-slot stores, with bit-identical sums (r4: the M = 8 pass was
+// VALU-bound at ~970 instructions per tile-wave). Lane q keeps its tile sums as the tree's level-2
+// node over the wave's 4 tiles; the 4 waves' nodes meet in LDS, wave 0 stores the unit's row
+// (unit_slot). Every sum is bit-identical to pair_slot() on (vi, vj): the same per-lane FMA
+// sequence in element order (an FMA's product is exact, so vi*vj == vj*vi), the same butterfly and
+// tree; the coefficients therefore equal edt_slerp_merge's.
 template <int IDT, int M>
 __global__ __launch_bounds__(kBlock) void slerp_gram_kernel(Members mem, const uint64_t* chunks, int64_t nchunks,
                                                             double* rows, uint64_t u0) {
-    constexpr int NT = M * (M + 1) / 2;
+    constexpr int NT = M * (M + 1) / 2, N2 = Red<NT>::N2;
     constexpr int upc = kTileSlots / 16;
-    __shared__ double ts[16][NT];
+    // [wave][row][slot][position in row], 17 doubles per (row, slot): lane q's 16 reads start
+    // 2 banks apart from lane q + 1's instead of all on one bank
+    constexpr int kPad = 17;
+    __shared__ double part[kWavesPerBlock][4 * N2 * kPad];
+    __shared__ double ts2[kWavesPerBlock][NT];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t units = (uint64_t)nchunks * upc;
-    {   // one unit per workgroup
-        const uint64_t u = u0 + blockIdx.x;
-        if (u >= units) return;
-        const uint64_t c = u / upc;
-        const int g = (int)(u % upc);
-        const uint64_t start = chunks[3 * c], len = chunks[3 * c + 1];
-#pragma unroll(M <= 2 ? 4 : 1)
-        for (int k = 0; k < 4; ++k) {
-            const int j = 16 * g + 4 * wave + k;
-            double gs[NT];
+    const uint64_t u = u0 + blockIdx.x;
+    if (u >= units) return;
+    const uint64_t c = u / upc;
+    const int g = (int)(u % upc);
+    // the chunk bounds are uniform: in scalar registers, so the full-tile test below is a scalar branch
+    const uint64_t start = uniform_u64(chunks[3 * c]), len = uniform_u64(chunks[3 * c + 1]);
+    // lane q (< NT) reads value q's partials: the row and slot that hold it after the swap levels
+    int pos = 0;
+#pragma unroll
+    for (int row = 0; row < 4; ++row)
+#pragma unroll
+        for (int sl = 0; sl < N2; ++sl) {
+            bool owner;
+            if (red_index<NT>(sl, row * 16, owner) == lane) pos = row * N2 + sl;
+        }
+    const double* mine = &part[wave][pos * kPad];
+    double* put = &part[wave][(lane >> 4) * N2 * kPad + (lane & 15)];
+    const uint64_t end = start + len;
+    const uint64_t a = (start + kVec - 1) / kVec * kVec, b = end / kVec * kVec;
+    double n01 = 0.0, n23 = 0.0;                       // lane q: the tree's nodes over tiles k = 0-1, 2-3
+    // one tile: its sums' lane chains (FULL: the whole tile inside the chunk's aligned body, so no
+    // lane test and no zero start), the swap levels, the LDS round trip, the row tree on lane q
+    auto tile = [&](int k, auto full) {
+        const int j = 16 * g + 4 * wave + k;
+        double gs[NT];
+        const uint64_t i = a + (uint64_t)j * kTileElems + (uint64_t)lane * kVec;
+        if constexpr (decltype(full)::value) {
+            Raw8<IDT> x[M];
+#pragma unroll
+            for (int m = 0; m < M; ++m) x[m] = ld_raw<IDT, false>(mem.p[m], i);   // default policy
+            gram_fma_first<M, kVec>(x, gs);
+        } else {
 #pragma unroll
             for (int q = 0; q < NT; ++q) gs[q] = 0.0;
-            for_tile(start, len, j,
-                [&](uint64_t i) {
-                    Raw8<IDT> x[M];
+            if (a < b && i < b) {
+                Raw8<IDT> x[M];
 #pragma unroll
-                    for (int m = 0; m < M; ++m) x[m] = ld_raw<IDT, false>(mem.p[m], i);   // default policy
-                    gram_fma<M, kVec>(x, gs);
-                },
-                [&](uint64_t i) {
-                    Raw1 x[M];
-#pragma unroll
-                    for (int m = 0; m < M; ++m) ld<IDT, 1>(mem.p[m], i, x[m].v);
-                    gram_fma<M, 1>(x, gs);
-                });
-            double r[Red<NT>::N2];
-            tile_reduce<NT>(gs, r);
-            red_store<NT>(r, [&](int q, double x) { ts[4 * wave + k][q] = x; });
+                for (int m = 0; m < M; ++m) x[m] = ld_raw<IDT, false>(mem.p[m], i);
+                gram_fma<M, kVec>(x, gs);
+            }
         }
-        __syncthreads();
-        if (wave == 0 && lane < NT) {
-            double t8[8];
+        if (j == 0)
+            tile0_edge(start, len, [&](uint64_t e) {
+                Raw1 x[M];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) t8[i] = ts[2 * i][lane] + ts[2 * i + 1][lane];
-            const double q0 = (t8[0] + t8[1]) + (t8[2] + t8[3]), q1 = (t8[4] + t8[5]) + (t8[6] + t8[7]);
-            rows[unit_slot(u, units) * NT + lane] = q0 + q1;
-        }
+                for (int m = 0; m < M; ++m) ld<IDT, 1>(mem.p[m], e, x[m].v);
+                gram_fma<M, 1>(x, gs);
+            });
+        double r[N2];
+        tile_swap_levels<NT>(gs, r);
+#pragma unroll
+        for (int sl = 0; sl < N2; ++sl) put[sl * kPad] = r[sl];
+        // the wave's own LDS round trip: its stores complete before its loads (in-order per wave);
+        // the fences keep the compiler from moving the loads above the stores
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double p[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) p[t] = mine[t];
+        const double tsum = row_tree16(p);
+        if (k == 0) n01 = tsum;
+        else if (k == 1) n01 = n01 + tsum;
+        else if (k == 2) n23 = tsum;
+        else n23 = n23 + tsum;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");    // this tile's reads before the next stores
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    // uniform: every tile of the unit inside the aligned body (all but a segment's last unit)
+    if (a + (uint64_t)(16 * g + 16) * kTileElems <= b) {
+#pragma unroll(M <= 2 ? 4 : 1)
+        for (int k = 0; k < 4; ++k) tile(k, std::true_type{});
+    } else {
+#pragma unroll(M <= 2 ? 4 : 1)
+        for (int k = 0; k < 4; ++k) tile(k, std::false_type{});
     }
+    if (lane < NT) ts2[wave][lane] = n01 + n23;        // level 2: the wave's 4 tiles
+    __syncthreads();
+    if (wave == 0 && lane < NT)
+        rows[unit_slot(u, units) * NT + lane] = (ts2[0][lane] + ts2[1][lane]) + (ts2[2][lane] + ts2[3][lane]);
 }
 
 // host: the Gram sums of D compact members into gram (chunk rows [nchunks][NT], then the row
