@@ -78,6 +78,10 @@ using edt::g_err;
 // through LDS into one level-2 row per workgroup (a quarter of the row bytes, one barrier); 0 = a
 // level-0 row per wave, no barrier. 7B lineage merge, one box, interleaved (profiles/
 // r03_spec_wg_rows.jsonl): 7.01-7.03 ms against 7.14-7.17, lerp 6.96.
+// Gram pass: 1 = the next tile's member loads issued before this tile's sums (two register sets)
+#ifndef EDT_GRAM_PREFETCH
+#define EDT_GRAM_PREFETCH 0
+#endif
 #ifndef EDT_SLERP_SPEC_WG_ROWS
 #define EDT_SLERP_SPEC_WG_ROWS 1
 #endif

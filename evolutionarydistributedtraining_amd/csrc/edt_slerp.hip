@@ -813,15 +813,23 @@ __global__ __launch_bounds__(kBlock) void slerp_gram_kernel(Members mem, const u
     double n01 = 0.0, n23 = 0.0;                       // lane q: the tree's nodes over tiles k = 0-1, 2-3
     // one tile: its sums' lane chains (FULL: the whole tile inside the chunk's aligned body, so no
     // lane test and no zero start), the swap levels, the LDS round trip, the row tree on lane q
-    auto tile = [&](int k, auto full) {
+    auto load_tile = [&](int k, Raw8<IDT> (&x)[M]) {
+        const uint64_t i = a + (uint64_t)(16 * g + 4 * wave + k) * kTileElems + (uint64_t)lane * kVec;
+#pragma unroll
+        for (int m = 0; m < M; ++m) x[m] = ld_raw<IDT, false>(mem.p[m], i);   // default policy
+    };
+    auto tile = [&](int k, auto full, const Raw8<IDT> (&xin)[M]) {
         const int j = 16 * g + 4 * wave + k;
         double gs[NT];
         const uint64_t i = a + (uint64_t)j * kTileElems + (uint64_t)lane * kVec;
         if constexpr (decltype(full)::value) {
-            Raw8<IDT> x[M];
-#pragma unroll
-            for (int m = 0; m < M; ++m) x[m] = ld_raw<IDT, false>(mem.p[m], i);   // default policy
-            gram_fma_first<M, kVec>(x, gs);
+            if constexpr (EDT_GRAM_PREFETCH) {
+                gram_fma_first<M, kVec>(xin, gs);      // loaded one tile ahead
+            } else {
+                Raw8<IDT> x[M];
+                load_tile(k, x);
+                gram_fma_first<M, kVec>(x, gs);
+            }
         } else {
 #pragma unroll
             for (int q = 0; q < NT; ++q) gs[q] = 0.0;
@@ -861,12 +869,30 @@ __global__ __launch_bounds__(kBlock) void slerp_gram_kernel(Members mem, const u
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
     // uniform: every tile of the unit inside the aligned body (all but a segment's last unit)
+    Raw8<IDT> x0[M];
     if (a + (uint64_t)(16 * g + 16) * kTileElems <= b) {
+        if constexpr (EDT_GRAM_PREFETCH) {             // two register sets: tile k + 1's loads in flight
+            Raw8<IDT> x1[M];                           // while tile k is summed (sched_barrier: the
+            load_tile(0, x0);                          // scheduler may not sink them to their use)
+            load_tile(1, x1);
+            __builtin_amdgcn_sched_barrier(0);
+            tile(0, std::true_type{}, x0);
+            __builtin_amdgcn_sched_barrier(0);
+            load_tile(2, x0);
+            __builtin_amdgcn_sched_barrier(0);
+            tile(1, std::true_type{}, x1);
+            __builtin_amdgcn_sched_barrier(0);
+            load_tile(3, x1);
+            __builtin_amdgcn_sched_barrier(0);
+            tile(2, std::true_type{}, x0);
+            tile(3, std::true_type{}, x1);
+        } else {
 #pragma unroll(M <= 2 ? 4 : 1)
-        for (int k = 0; k < 4; ++k) tile(k, std::true_type{});
+            for (int k = 0; k < 4; ++k) tile(k, std::true_type{}, x0);
+        }
     } else {
 #pragma unroll(M <= 2 ? 4 : 1)
-        for (int k = 0; k < 4; ++k) tile(k, std::false_type{});
+        for (int k = 0; k < 4; ++k) tile(k, std::false_type{}, x0);
     }
     if (lane < NT) ts2[wave][lane] = n01 + n23;        // level 2: the wave's 4 tiles
     __syncthreads();

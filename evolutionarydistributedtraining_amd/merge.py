@@ -115,7 +115,22 @@ def t_for_key(key: str, num_layers: int, param_t: dict, global_t):
     return global_t
 
 
+_plan_memo: dict = {}
+
+
 def merge_plan(keys, num_layers: int, merge_config_dict: dict):
+    """[(key, t)] for the keys the merge covers (cached per (keys, num_layers, config))."""
+    import json
+    memo = (tuple(keys), num_layers, json.dumps(merge_config_dict, sort_keys=True, default=str))
+    got = _plan_memo.get(memo)
+    if got is None:
+        if len(_plan_memo) > 16:
+            _plan_memo.clear()
+        got = _plan_memo[memo] = _merge_plan(keys, num_layers, merge_config_dict)
+    return list(got)
+
+
+def _merge_plan(keys, num_layers: int, merge_config_dict: dict):
     """[(key, t)] in state-dict order, skipped keys removed."""
     param_t, global_t = parse_t_parameters(merge_config_dict)
     out = []
@@ -172,30 +187,39 @@ def _listable(tensors, dev) -> bool:
 
 def _writes_are_safe(pairs, outs) -> bool:
     """out[i] may alias its own inputs exactly (the blend is element-wise, after every sum);
-    any other overlap of an output with an input or another output is unsafe in one pass."""
-    spans = []
-    for i, ((a, b), o) in enumerate(zip(pairs, outs)):
-        for tag, t in (("in", a), ("in", b), ("out", o)):
-            n = t.numel() * t.element_size()
-            if n:
-                spans.append((t.data_ptr(), t.data_ptr() + n, tag, i))
-    groups = {}
-    for a, e, tag, i in spans:
-        groups.setdefault((a, e), []).append((tag, i))
-    for members in groups.values():
-        out_idx = {i for tag, i in members if tag == "out"}
-        if len(out_idx) > 1 or (out_idx and any(i not in out_idx for _, i in members)):
-            return False
-    end, open_out = -1, False
-    for (a, e) in sorted(groups):
-        has_out = any(tag == "out" for tag, _ in groups[(a, e)])
-        if a < end and (has_out or open_out):
-            return False
-        if e > end:
-            end, open_out = e, has_out
-        else:
-            open_out = open_out or has_out
-    return True
+    any other overlap of an output with an input or another output is unsafe in one pass.
+    Vectorised over the byte spans (numpy): identical spans grouped; a group holding an output
+    may hold only spans of that output's own pair; distinct groups that overlap are unsafe when
+    either holds an output (a sorted sweep: running furthest end of every group / of output groups)."""
+    ts = [t for (a, b), o in zip(pairs, outs) for t in (a, b, o)]
+    st = np.fromiter((t.data_ptr() for t in ts), dtype=np.int64, count=len(ts))
+    nb = np.fromiter((t.numel() * t.element_size() for t in ts), dtype=np.int64, count=len(ts))
+    kind_out = np.tile(np.array([False, False, True]), len(outs))
+    owner = np.repeat(np.arange(len(outs), dtype=np.int64), 3)
+    keep = nb > 0
+    st, en, kind_out, owner = st[keep], st[keep] + nb[keep], kind_out[keep], owner[keep]
+    if st.size == 0:
+        return True
+    order = np.lexsort((en, st))
+    st, en, kind_out, owner = st[order], en[order], kind_out[order], owner[order]
+    new_group = np.ones(st.size, dtype=bool)
+    new_group[1:] = (st[1:] != st[:-1]) | (en[1:] != en[:-1])
+    gid = np.cumsum(new_group) - 1
+    ng = int(gid[-1]) + 1
+    outs_per = np.bincount(gid, weights=kind_out, minlength=ng)
+    if (outs_per > 1).any():
+        return False                                         # two outputs on one span
+    big = np.iinfo(np.int64).max
+    out_owner = np.full(ng, -1, dtype=np.int64)
+    out_owner[gid[kind_out]] = owner[kind_out]
+    has_out = out_owner >= 0
+    if (has_out[gid] & (owner != out_owner[gid])).any():
+        return False                                         # an output on another pair's span
+    gst, gen = st[new_group], en[new_group]
+    prev_end = np.concatenate(([-1], np.maximum.accumulate(gen)[:-1]))
+    prev_out_end = np.concatenate(([-1], np.maximum.accumulate(np.where(has_out, gen, -1))[:-1]))
+    del big
+    return not bool(np.any((has_out & (gst < prev_end)) | (gst < prev_out_end)))
 
 
 def slerp_tensors(pairs, ts, out_dtype=torch.float32, device=None, dot_threshold=0.9995,
@@ -235,8 +259,9 @@ def slerp_tensors(pairs, ts, out_dtype=torch.float32, device=None, dot_threshold
             outs = [torch.empty(a.shape, dtype=out_dtype, device=dev) for a, _ in pairs]
         if _listable(outs, dev) and all(o.dtype == out_dtype for o in outs) and _writes_are_safe(pairs, outs):
             plan = _plan_for(offsets, dev, relative=True)
-            ops.slerp_list(plan, [a.detach() for a, _ in pairs], [b.detach() for _, b in pairs],
-                           [o.detach() for o in outs], tt, dot_threshold, eps, ref_dot=_ref_dot)
+            # the tensors as they are (the C ABI reads data pointers: no autograd, no detach needed)
+            ops.slerp_list(plan, [a for a, _ in pairs], [b for _, b in pairs], outs, tt, dot_threshold, eps,
+                           ref_dot=_ref_dot)
             return outs
     total = offsets[-1]
     v0 = torch.empty(total, dtype=in_dt, device=dev)
@@ -288,26 +313,34 @@ def fresh_outputs(like, dtype, device) -> list[torch.Tensor]:
         offs.append(o)
         o += (t.numel() + 7) // 8 * 8
     buf = torch.empty(max(o, 8), dtype=dtype, device=device)
-    return [buf[a:a + t.numel()].view(t.shape) for a, t in zip(offs, like)]
+    return [buf.as_strided(t.shape, _contig_strides(t.shape), a) for a, t in zip(offs, like)]
+
+
+def _contig_strides(shape):
+    st, acc = [], 1
+    for d in reversed(shape):
+        st.append(acc)
+        acc *= d
+    return tuple(reversed(st))
+
+
+def _spans(ts):
+    st = np.fromiter((t.data_ptr() for t in ts), dtype=np.int64, count=len(ts))
+    nb = np.fromiter((t.numel() * t.element_size() for t in ts), dtype=np.int64, count=len(ts))
+    keep = nb > 0
+    return st[keep], st[keep] + nb[keep]
 
 
 def _overlaps_any(outs, ins) -> bool:
-    spans = [(t.data_ptr(), t.data_ptr() + t.numel() * t.element_size()) for t in ins if t.numel()]
-    spans.sort()
-    import bisect
-    starts = [a for a, _ in spans]
-    far, ends = 0, []
-    for _, e in spans:
-        far = max(far, e)
-        ends.append(far)
-    for t in outs:
-        if not t.numel():
-            continue
-        a, e = t.data_ptr(), t.data_ptr() + t.numel() * t.element_size()
-        i = bisect.bisect_left(starts, e)           # spans starting before e
-        if i and ends[i - 1] > a:
-            return True
-    return False
+    """Some output byte span overlaps some input byte span (numpy: inputs sorted, running end)."""
+    a_in, e_in = _spans(ins)
+    a_out, e_out = _spans(outs)
+    if a_in.size == 0 or a_out.size == 0:
+        return False
+    o = np.argsort(a_in, kind="stable")
+    a_in, far = a_in[o], np.maximum.accumulate(e_in[o])
+    i = np.searchsorted(a_in, e_out, side="left")               # input spans starting before e
+    return bool(np.any((i > 0) & (far[np.maximum(i - 1, 0)] > a_out)))
 
 
 def slerp_into_module_(module: torch.nn.Module, sd1: dict, sd2: dict, plan, out_dtype, device=None,
@@ -321,16 +354,19 @@ def slerp_into_module_(module: torch.nn.Module, sd1: dict, sd2: dict, plan, out_
     parents (7B lineage: ~7 ms against ~11 ms). The parent's old storage is released once nothing
     else refers to it. Otherwise the merge writes into the module's tensors in place."""
     keys = [k for k, _ in plan]
-    tsd = module.state_dict()
     params = dict(module.named_parameters(remove_duplicate=False))
-    outs = [tsd[k] for k in keys]
+    if all(k in params for k in keys):
+        tsd, outs = None, [params[k] for k in keys]          # no state_dict walk: the parameters
+    else:
+        tsd = module.state_dict()
+        outs = [tsd[k] for k in keys]
     dev = device or _compute_device(*[t for k in keys for t in (sd1[k], sd2[k])])
     ins = [t for k in keys for t in (sd1[k], sd2[k])]
     rebind = (all(k in params for k in keys) and dev.type == "cuda" and _listable(ins, dev)
               and all(o.device == dev for o in outs) and _overlaps_any(outs, ins))
     if not rebind:
         slerp_state_dicts(sd1, sd2, plan, out_dtype=out_dtype, device=device, dot_threshold=dot_threshold,
-                          eps=eps, out=tsd)
+                          eps=eps, out=tsd if tsd is not None else dict(zip(keys, outs)))
         return
     fresh = fresh_outputs(outs, out_dtype, dev)
     slerp_state_dicts(sd1, sd2, plan, out_dtype=out_dtype, device=device, dot_threshold=dot_threshold, eps=eps,

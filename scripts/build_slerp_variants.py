@@ -16,6 +16,7 @@ VARIANTS = {
     "tpw8": ["-DEDT_SLERP_STATS_TPW=8"],
     "nont": ["-DEDT_NT_SLERP=0"],
     "waverows": ["-DEDT_SLERP_SPEC_WG_ROWS=0"],
+    "gramprefetch": ["-DEDT_GRAM_PREFETCH=1"],
 }
 
 

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--far", action="store_true")
     ap.add_argument("--layers", type=int, default=28)
+    ap.add_argument("--profile", action="store_true", help="cProfile one merge (host time split) to stderr")
     a = ap.parse_args()
     from transformers import Qwen2Config, Qwen2ForCausalLM
 
@@ -78,6 +79,19 @@ def main():
         times[name] = ts[1:]                       # the first call builds the cached plan
         outs[name] = torch.cat([p.detach().reshape(-1) for p in m1.model.parameters()]).view(torch.int16).clone()
     same = bool(torch.equal(outs["single_pass_rebind"], outs["two_pass_in_place"]))
+    if a.profile:                                  # where the host time of one merge goes
+        import cProfile
+        import io
+        import pstats
+        reset()
+        pr = cProfile.Profile()
+        pr.enable()
+        rebind_merge()
+        torch.cuda.synchronize()
+        pr.disable()
+        buf = io.StringIO()
+        pstats.Stats(pr, stream=buf).sort_stats("tottime").print_stats(18)
+        print(buf.getvalue(), file=sys.stderr)
     res = {k: {"median_ms": round(statistics.median(v), 3), "min_ms": round(min(v), 3),
                "TBps_algorithmic": round(6 * n / (statistics.median(v) / 1e3) / 1e12, 3)} for k, v in times.items()}
     print(json.dumps({"probe": "evomerge_surface", "params_body": n, "tensors": len(keys), "far": a.far,

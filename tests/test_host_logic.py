@@ -387,3 +387,61 @@ def test_seg_table_overlap_check_matches_brute_force():
         ins = [(p, 4 * n) for p, n in zip(p0 + p1, sizes + sizes)]
         outs = [(p, osz * n) for p, n in zip(po, sizes)]
         assert (rc == 0) == brute(ins, outs), (sizes, p0, p1, po, osz)
+
+
+def test_writes_are_safe_matches_brute_force():
+    """merge._writes_are_safe (vectorised sweep) against the rule it states, checked pairwise: an
+    output may coincide exactly with its own pair's inputs; any other overlap of an output with an
+    input or another output is unsafe; inputs may overlap each other."""
+    import random
+    rnd = random.Random(7)
+    buf = torch.empty(400, dtype=torch.uint8)
+
+    def brute(pairs, outs):
+        spans = []
+        for i, ((a, b), o) in enumerate(zip(pairs, outs)):
+            for kind, t in (("in", a), ("in", b), ("out", o)):
+                if t.numel():
+                    spans.append((t.data_ptr(), t.data_ptr() + t.numel(), kind, i))
+        for x in range(len(spans)):
+            for y in range(len(spans)):
+                if x == y:
+                    continue
+                (a0, e0, k0, i0), (a1, e1, k1, i1) = spans[x], spans[y]
+                if k0 != "out" or not (a0 < e1 and a1 < e0):
+                    continue
+                if k1 == "in" and i1 == i0 and (a0, e0) == (a1, e1):
+                    continue
+                return False
+        return True
+
+    def view():
+        a = rnd.randint(0, 380)
+        return buf[a:a + rnd.choice([0, 1, 5, 20])]
+
+    n_safe = 0
+    for _ in range(4000):
+        P = rnd.randint(1, 4)
+        pairs = [(view(), view()) for _ in range(P)]
+        outs = [pairs[i][0] if rnd.random() < 0.3 else view() for i in range(P)]
+        want = brute(pairs, outs)
+        assert merge._writes_are_safe(pairs, outs) == want, (pairs, outs)
+        n_safe += want
+    assert 200 < n_safe < 3800
+
+
+def test_overlaps_any_matches_brute_force():
+    import random
+    rnd = random.Random(9)
+    buf = torch.empty(300, dtype=torch.uint8)
+    view = lambda: buf[(a := rnd.randint(0, 280)):a + rnd.choice([0, 1, 4, 16])]
+    for _ in range(3000):
+        outs = [view() for _ in range(rnd.randint(0, 4))]
+        ins = [view() for _ in range(rnd.randint(0, 5))]
+        want = any(o.numel() and i.numel() and o.data_ptr() < i.data_ptr() + i.numel()
+                   and i.data_ptr() < o.data_ptr() + o.numel() for o in outs for i in ins)
+        assert merge._overlaps_any(outs, ins) == bool(want)
+    shapes = [(3, 5), (7,), (2, 2, 3)]
+    outs = merge.fresh_outputs([torch.empty(s) for s in shapes], torch.bfloat16, "cpu")
+    assert [o.shape for o in outs] == [torch.Size(s) for s in shapes]
+    assert all(o.is_contiguous() and o.data_ptr() % 16 == 0 for o in outs)
