@@ -274,7 +274,8 @@ class DirOuterSync:
     carry_inner_state: EDT_LM/diloco.py:295-300 — before the new weights are written, each
     worker's previous-generation `optimizer.pt` / `scheduler.pt` (step(prev_dirs=...), GenN of
     every machine) is copied over the one its inner loop left in its GenN+1 dir, where it exists,
-    so the next inner loop resumes the inner optimiser as the reference's does.
+    so the next inner loop resumes the inner optimiser as the reference's does — into the dirs the
+    new weights go to (out_dirs; the reference writes them over worker_dirs, its default here).
     place_momentum: after the first step, choose the outer momentum's HBM placement by measurement
     once (OuterSync.place_momentum; 0 = keep the first allocation). The θ and worker arenas stay
     resident across generations here, so the choice holds for the rest of the run — the drop-in
@@ -344,7 +345,9 @@ class DirOuterSync:
                                                                  self.place_candidates)
         out_dirs = worker_dirs if out_dirs is None else out_dirs
         if self.carry_inner_state:          # diloco.py:295-300, before the model write as there
-            for source, target in zip(prev_dirs, worker_dirs):
+            # beside the weights the next inner loop loads: out_dirs (== worker_dirs in the reference)
+            for source, target in zip(prev_dirs, out_dirs):
+                os.makedirs(target, exist_ok=True)
                 for fname in self.INNER_STATE_FILES:
                     src = os.path.join(source, fname)
                     if os.path.exists(src):

@@ -123,3 +123,19 @@ def test_dir_outer_sync_two_generations_carry_momentum_and_state(tmp_path, monke
     for i in range(K):
         assert open(os.path.join(nxt[i], "optimizer.pt"), "rb").read() == open(os.path.join(prev[i], "optimizer.pt"), "rb").read()
     assert sync.state.has_momentum and sync.state.steps == 2
+
+
+def test_dir_outer_sync_carry_goes_beside_the_weights(tmp_path, monkeypatch, oracle):
+    """out_dirs apart from worker_dirs: the carried inner state lands where the new
+    weights are written, so the next inner loop finds both together; worker_dirs keep their own."""
+    diloco = _oracle_sync(monkeypatch, oracle)
+    base, prev, curr = _layout(str(tmp_path), 2, 0, 4, [True, True])
+    outs = [os.path.join(str(tmp_path), f"out{i}") for i in range(2)]
+    before = [open(os.path.join(c, "optimizer.pt"), "rb").read() for c in curr]
+    sync = diloco.DirOuterSync(device="cpu", names=list(SHAPES), carry_inner_state=True)
+    sync.step(prev[0], curr, out_dirs=outs, prev_dirs=prev)
+    for i in range(2):
+        assert os.path.exists(os.path.join(outs[i], "model.safetensors"))
+        for f in ("optimizer.pt", "scheduler.pt"):
+            assert open(os.path.join(outs[i], f), "rb").read() == open(os.path.join(prev[i], f), "rb").read()
+        assert open(os.path.join(curr[i], "optimizer.pt"), "rb").read() == before[i]
