@@ -82,6 +82,9 @@ using edt::g_err;
 #ifndef EDT_GRAM_PREFETCH
 #define EDT_GRAM_PREFETCH 0
 #endif
+#ifndef EDT_GRAM_NT             // Gram pass: non-temporal member loads (each member is read once)
+#define EDT_GRAM_NT 0
+#endif
 #ifndef EDT_SLERP_SPEC_WG_ROWS
 #define EDT_SLERP_SPEC_WG_ROWS 1
 #endif

@@ -816,7 +816,7 @@ __global__ __launch_bounds__(kBlock) void slerp_gram_kernel(Members mem, const u
     auto load_tile = [&](int k, Raw8<IDT> (&x)[M]) {
         const uint64_t i = a + (uint64_t)(16 * g + 4 * wave + k) * kTileElems + (uint64_t)lane * kVec;
 #pragma unroll
-        for (int m = 0; m < M; ++m) x[m] = ld_raw<IDT, false>(mem.p[m], i);   // default policy
+        for (int m = 0; m < M; ++m) x[m] = ld_raw<IDT, EDT_GRAM_NT != 0>(mem.p[m], i);
     };
     auto tile = [&](int k, auto full, const Raw8<IDT> (&xin)[M]) {
         const int j = 16 * g + 4 * wave + k;

@@ -17,8 +17,8 @@ import os
 
 import torch
 
-from .merge import (LazyTensorLoader, interpolate_t, lerp, maybe_torch, merge_plan, normalize, slerp,  # noqa: F401
-                    slerp_into_module_, slerp_state_dicts, uniform_dna_crossover)
+from .merge import (LazyTensorLoader, interpolate_t, lerp, maybe_torch, merge_models_into_, merge_plan,  # noqa: F401
+                    normalize, slerp, slerp_state_dicts, uniform_dna_crossover)
 
 __all__ = ["slerp", "lerp", "interpolate_t", "load_model_from_path", "run_slerp_merge_from_config",
            "run_linear_merge_5050", "crossover_main", "uniform_dna_crossover", "SELF_ATTN_T_CURVE",
@@ -46,19 +46,10 @@ def run_slerp_merge_from_config(merge_config_dict: dict, model_1, model_2, confi
     """SLERP model_1 / model_2 (bodies, `.model`) into base_model.model and save base_model
     (EDT_EVOMERGE/train/crossover.py:104-146). `device` picks the GPU (None: current)."""
     num_layers = min(config_1.num_hidden_layers, config_2.num_hidden_layers)
-    sd1, sd2 = model_1.state_dict(), model_2.state_dict()
-    plan = merge_plan(list(sd1.keys()), num_layers, merge_config_dict)
-    target = base_model.model
-    out_dtype = next(target.parameters()).dtype
-    dev = torch.device(device) if device not in (None, "cpu") else None
-    tsd = target.state_dict()
-    if set(tsd) == {k for k, _ in plan}:
-        # the merge lands in the target's parameters (== load_state_dict of the merged dict). The
-        # target may be model_1 itself (the reference passes base_model=model_1): then the children
-        # go to a fresh buffer in one pass and the parameters are re-pointed at it
-        slerp_into_module_(target, sd1, sd2, plan, out_dtype, device=dev)
-    else:                                   # load_state_dict reports the key mismatch
-        target.load_state_dict(slerp_state_dicts(sd1, sd2, plan, out_dtype=out_dtype, device=dev))
+    # the merge lands in the target's parameters (== load_state_dict of the merged dict). The target
+    # may be model_1 itself (the reference passes base_model=model_1): then the children go to a
+    # fresh buffer in one pass and the parameters are re-pointed at it (merge.slerp_into_module_)
+    merge_models_into_(base_model.model, model_1, model_2, merge_config_dict, num_layers, device=device)
     base_model.save_pretrained(merge_output_path)
     print("SLERP merging complete! Model saved at:", merge_output_path)
     return merge_output_path

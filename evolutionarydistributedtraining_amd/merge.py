@@ -343,8 +343,20 @@ def _overlaps_any(outs, ins) -> bool:
     return bool(np.any((i > 0) & (far[np.maximum(i - 1, 0)] > a_out)))
 
 
+def module_tensors(module: torch.nn.Module) -> dict:
+    """module.state_dict()'s {key: tensor} — for a module whose state is its parameters (no
+    persistent buffers, no state-dict hooks), read straight from named_parameters without
+    state_dict's per-module walk and per-tensor detach (the kernels take data pointers)."""
+    for m in module.modules():
+        if m._state_dict_hooks or getattr(m, "_state_dict_pre_hooks", None):
+            return module.state_dict()
+        if any(b is not None and n not in m._non_persistent_buffers_set for n, b in m._buffers.items()):
+            return module.state_dict()
+    return dict(module.named_parameters(remove_duplicate=False))
+
+
 def slerp_into_module_(module: torch.nn.Module, sd1: dict, sd2: dict, plan, out_dtype, device=None,
-                       dot_threshold=0.9995, eps=1e-8) -> None:
+                       dot_threshold=0.9995, eps=1e-8, params: dict | None = None) -> None:
     """== module.load_state_dict(SLERP of sd1 / sd2 per plan) (EDT_EVOMERGE/train/crossover.py:142),
     in the fewest passes over HBM. When the module's own tensors are a parent's (the reference
     merges into model_1 itself) and everything is device-resident, the children are written to a
@@ -354,7 +366,7 @@ def slerp_into_module_(module: torch.nn.Module, sd1: dict, sd2: dict, plan, out_
     parents (7B lineage: ~7 ms against ~11 ms). The parent's old storage is released once nothing
     else refers to it. Otherwise the merge writes into the module's tensors in place."""
     keys = [k for k, _ in plan]
-    params = dict(module.named_parameters(remove_duplicate=False))
+    params = params if params is not None else dict(module.named_parameters(remove_duplicate=False))
     if all(k in params for k in keys):
         tsd, outs = None, [params[k] for k in keys]          # no state_dict walk: the parameters
     else:
@@ -374,6 +386,27 @@ def slerp_into_module_(module: torch.nn.Module, sd1: dict, sd2: dict, plan, out_
     with torch.no_grad():
         for k, f in zip(keys, fresh):
             params[k].data = f
+
+
+def merge_models_into_(target: torch.nn.Module, model_1: torch.nn.Module, model_2: torch.nn.Module,
+                       merge_config_dict: dict, num_layers: int, device=None) -> None:
+    """EDT_EVOMERGE/train/crossover.py:114-142 without the save: the SLERP of model_1 / model_2's
+    state (the key plan of merge_config_dict over num_layers) loaded into `target` (which may be
+    model_1 itself, as the reference passes it): slerp_into_module_ when the keys match, else
+    load_state_dict of the merged dict (which reports the mismatch as the reference's does)."""
+    sd1 = module_tensors(model_1)
+    sd2 = sd1 if model_2 is model_1 else module_tensors(model_2)
+    plan = merge_plan(list(sd1.keys()), num_layers, merge_config_dict)
+    out_dtype = next(target.parameters()).dtype
+    dev = torch.device(device) if device not in (None, "cpu") else None
+    tparams = sd1 if target is model_1 and isinstance(sd1, dict) else None
+    tkeys = set(tparams) if tparams is not None else set(module_tensors(target))
+    if tkeys == {k for k, _ in plan}:
+        slerp_into_module_(target, sd1, sd2, plan, out_dtype, device=dev,
+                           params=tparams if tparams is not None and all(
+                               isinstance(v, torch.nn.Parameter) for v in tparams.values()) else None)
+    else:
+        target.load_state_dict(slerp_state_dicts(sd1, sd2, plan, out_dtype=out_dtype, device=dev))
 
 
 def uniform_dna_crossover(dna1, dna2):

@@ -17,6 +17,8 @@ VARIANTS = {
     "nont": ["-DEDT_NT_SLERP=0"],
     "waverows": ["-DEDT_SLERP_SPEC_WG_ROWS=0"],
     "gramprefetch": ["-DEDT_GRAM_PREFETCH=1"],
+    "gramnt": ["-DEDT_GRAM_NT=1"],
+    "gramntpf": ["-DEDT_GRAM_NT=1", "-DEDT_GRAM_PREFETCH=1"],
 }
 
 

@@ -58,9 +58,8 @@ def main():
                 p.data = start[k].clone()
         torch.cuda.synchronize()
 
-    def rebind_merge():
-        merge.slerp_into_module_(m1.model, m1.model.state_dict(), m2.model.state_dict(), plan, torch.bfloat16,
-                                 device=dev)
+    def rebind_merge():                            # the surface minus save_pretrained
+        merge.merge_models_into_(m1.model, m1.model, m2.model, mcfg, cfg.num_hidden_layers, device=dev)
 
     def in_place_merge():
         tsd = m1.model.state_dict()
