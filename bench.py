@@ -319,6 +319,23 @@ def synth_sharded(theta: torch.Tensor, workers: list[torch.Tensor], rank: int) -
             w[a:b].copy_(t + torch.randn(b - a, generator=gw, device=dev) * 1e-3)
 
 
+def native_library_record() -> dict:
+    """In-run evidence of the code the line measured: the HIP library this process mapped (from
+    /proc/self/maps), its sha256 (the stamp the PMC traffic entries carry) and ABI revision."""
+    from evolutionarydistributedtraining_amd import _lib as L
+    rec = {"library": os.path.relpath(L.LIB_PATH, ROOT), "sha256": (L.library_sha256() or "")[:16]}
+    try:
+        rec["abi"] = int(L.load_library().edt_abi_version())
+    except Exception as e:     # noqa: BLE001 - a record, not a check
+        rec["abi"] = f"{type(e).__name__}"
+    try:
+        with open("/proc/self/maps") as f:
+            rec["mapped"] = any(os.path.realpath(L.LIB_PATH) in line for line in f)
+    except OSError:
+        rec["mapped"] = None
+    return rec
+
+
 def _ordered_bits(x: torch.Tensor) -> torch.Tensor:
     """Floats as integers in value order (int64): |a - b| of two of them is their distance in ulps."""
     if x.dtype == torch.bfloat16:
@@ -1003,7 +1020,7 @@ def run_sharded(args, comm, rt, json_out, kernels=None, exit_fn=None) -> dict | 
                        "population": k_total, "worker_dtype": args.worker_dtype,
                        "theta_dtype": args.theta_dtype, "parallelism": f"dp{world} {sched} (RCCL)"},
             "roofline": roofline,
-            "device": rt.device_info(),
+            "device": rt.device_info(), "native": native_library_record(), "native": native_library_record(),
         }
         # rank 0 times the CPU baseline first (the other ranks wait at the barrier), then every
         # extra runs under the deadline, so neither can be lost to a hang in an extra
@@ -1211,7 +1228,7 @@ def main():
                    "population": k_total, "worker_dtype": args.worker_dtype,
                    "theta_dtype": args.theta_dtype, "parallelism": "single GPU"},
         "roofline": roofline,
-        "device": rt.device_info(),
+        "device": rt.device_info(), "native": native_library_record(),
     }
 
     # what a plain device-to-device copy reaches on this device, same process

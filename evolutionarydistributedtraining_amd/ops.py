@@ -281,8 +281,12 @@ class SlerpPlan:
 
     @property
     def seg_numel(self):
-        import numpy as np
-        return np.diff(np.asarray(self.seg_offsets, dtype=np.int64))
+        """numpy int64 [nseg]: the segments' sizes (cached)."""
+        got = self.__dict__.get("_seg_numel")
+        if got is None:
+            import numpy as np
+            got = self.__dict__["_seg_numel"] = np.diff(np.asarray(self.seg_offsets, dtype=np.int64))
+        return got
 
 
 def make_slerp_plan(seg_offsets: list[int], device: torch.device,
@@ -453,8 +457,8 @@ def _speculation_pays(plan: SlerpPlan, in_bytes: int, out_bytes: int, wait: bool
     if dots is None:
         return getattr(plan, "_last_speculate", True)
     dots = dots[:plan.nseg]
-    sizes = np.diff(np.asarray(plan.seg_offsets, dtype=np.int64))
-    total = max(1, int(sizes.sum()))
+    sizes = plan.seg_numel
+    total = max(1, int(plan.seg_offsets[-1]))
     f = float(sizes[np.abs(dots) <= plan._last_thr].sum()) / total
     return (1 + f) * (2 * in_bytes + out_bytes) < 4 * in_bytes + out_bytes
 

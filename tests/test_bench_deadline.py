@@ -29,7 +29,7 @@ def test_deadline_fires_once_with_the_value_and_finished_extras():
     assert codes == [3]
     line = _line(buf)
     assert line["value"] == 123.0 and line["weak_scaling"] == {"ms_per_step": 2.0}
-    assert line["extras_deadline"]["unfinished_or_skipped"] == ["other_schedules", "baseline_configs",
+    assert line["extras_deadline"]["unfinished_or_skipped"] == ["parity", "other_schedules", "baseline_configs",
                                                                 "population_slerp_7b"]
     assert d.emit() is False            # the main thread arriving later prints nothing more
     assert len(buf.getvalue().splitlines()) == 1
