@@ -780,8 +780,9 @@ __device__ __forceinline__ void gram_fma_first(const X (&x)[M], double (&g)[M * 
 // sequence in element order (an FMA's product is exact, so vi*vj == vj*vi), the same butterfly and
 // tree; the coefficients therefore equal edt_slerp_merge's.
 template <int IDT, int M>
-__global__ __launch_bounds__(kBlock) void slerp_gram_kernel(Members mem, const uint64_t* chunks, int64_t nchunks,
-                                                            double* rows, uint64_t u0) {
+__global__ __launch_bounds__(kBlock, EDT_GRAM_MIN_BLOCKS) void slerp_gram_kernel(Members mem, const uint64_t* chunks,
+                                                                                 int64_t nchunks, double* rows,
+                                                                                 uint64_t u0) {
     constexpr int NT = M * (M + 1) / 2, N2 = Red<NT>::N2;
     constexpr int upc = kTileSlots / 16;
     // [wave][row][slot][position in row], 17 doubles per (row, slot): lane q's 16 reads start
