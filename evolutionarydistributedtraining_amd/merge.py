@@ -209,7 +209,6 @@ def _writes_are_safe(pairs, outs) -> bool:
     outs_per = np.bincount(gid, weights=kind_out, minlength=ng)
     if (outs_per > 1).any():
         return False                                         # two outputs on one span
-    big = np.iinfo(np.int64).max
     out_owner = np.full(ng, -1, dtype=np.int64)
     out_owner[gid[kind_out]] = owner[kind_out]
     has_out = out_owner >= 0
@@ -218,19 +217,20 @@ def _writes_are_safe(pairs, outs) -> bool:
     gst, gen = st[new_group], en[new_group]
     prev_end = np.concatenate(([-1], np.maximum.accumulate(gen)[:-1]))
     prev_out_end = np.concatenate(([-1], np.maximum.accumulate(np.where(has_out, gen, -1))[:-1]))
-    del big
     return not bool(np.any((has_out & (gst < prev_end)) | (gst < prev_out_end)))
 
 
 def slerp_tensors(pairs, ts, out_dtype=torch.float32, device=None, dot_threshold=0.9995,
-                  eps=1e-8, out=None) -> list[torch.Tensor]:
+                  eps=1e-8, out=None, _outs_apart=False) -> list[torch.Tensor]:
     """SLERP of each (v0, v1) pair with its own t, all in ONE multi-tensor pass.
 
     Inputs are upcast to float32 exactly like the reference's `.float().numpy()` when the two
     parents' dtypes differ; results are float32 (the reference returns float32) or `out_dtype`
     (rounded to nearest even, as load_state_dict into a bf16 model does). `out`: optional list of
     destination tensors (e.g. the target model's parameters, which may be the first parent's
-    own tensors), written in place.
+    own tensors), written in place. `_outs_apart` (internal): `out` is known to be apart from every
+    parent and 16-byte aligned (merge.fresh_outputs) — the host-side overlap rule is skipped (the C
+    table check still runs).
 
     Parents already on the device are read where they lie (edt_slerp_merge_list); anything
     else is first packed into two flat arenas (edt_slerp_merge)."""
@@ -257,11 +257,13 @@ def slerp_tensors(pairs, ts, out_dtype=torch.float32, device=None, dot_threshold
         outs = out
         if outs is None:
             outs = [torch.empty(a.shape, dtype=out_dtype, device=dev) for a, _ in pairs]
-        if _listable(outs, dev) and all(o.dtype == out_dtype for o in outs) and _writes_are_safe(pairs, outs):
+        if _outs_apart or (_listable(outs, dev) and all(o.dtype == out_dtype for o in outs)
+                           and _writes_are_safe(pairs, outs)):
             plan = _plan_for(offsets, dev, relative=True)
-            # the tensors as they are (the C ABI reads data pointers: no autograd, no detach needed)
-            ops.slerp_list(plan, [a for a, _ in pairs], [b for _, b in pairs], outs, tt, dot_threshold, eps,
-                           ref_dot=_ref_dot)
+            # the tensors as they are (the C ABI reads data pointers: no autograd, no detach needed);
+            # sizes and dtypes were checked above, so the binding skips its own per-tensor pass
+            ops.SlerpListBinding(plan, [a for a, _ in pairs], [b for _, b in pairs], outs, checked=True).merge(
+                tt, dot_threshold, eps, ref_dot=_ref_dot)
             return outs
     total = offsets[-1]
     v0 = torch.empty(total, dtype=in_dt, device=dev)
@@ -295,12 +297,13 @@ def slerp(t, v0, v1, DOT_THRESHOLD=0.9995, eps=1e-8):
 
 
 def slerp_state_dicts(sd1: dict, sd2: dict, plan, out_dtype=torch.float32, device=None,
-                      dot_threshold=0.9995, eps=1e-8, out: dict | None = None) -> dict:
+                      dot_threshold=0.9995, eps=1e-8, out: dict | None = None, _outs_apart=False) -> dict:
     """Merged state dict {key: tensor} for plan = [(key, t)] (see merge_plan). `out`: a state
     dict to write the results into (e.g. the target model's, == load_state_dict of the merge)."""
     keys = [k for k, _ in plan]
     res = slerp_tensors([(sd1[k], sd2[k]) for k in keys], [t for _, t in plan], out_dtype, device,
-                        dot_threshold, eps, out=None if out is None else [out[k] for k in keys])
+                        dot_threshold, eps, out=None if out is None else [out[k] for k in keys],
+                        _outs_apart=_outs_apart)
     return dict(zip(keys, res))
 
 
@@ -382,7 +385,7 @@ def slerp_into_module_(module: torch.nn.Module, sd1: dict, sd2: dict, plan, out_
         return
     fresh = fresh_outputs(outs, out_dtype, dev)
     slerp_state_dicts(sd1, sd2, plan, out_dtype=out_dtype, device=device, dot_threshold=dot_threshold, eps=eps,
-                      out=dict(zip(keys, fresh)))
+                      out=dict(zip(keys, fresh)), _outs_apart=True)
     with torch.no_grad():
         for k, f in zip(keys, fresh):
             params[k].data = f

@@ -579,26 +579,33 @@ class SlerpListBinding:
     per-tensor host work. The tensors must stay where they are while the binding is used (it keeps
     references to them; rebinding a module's parameters elsewhere needs a new binding)."""
 
-    def __init__(self, plan: SlerpPlan, v0s, v1s, outs):
+    def __init__(self, plan: SlerpPlan, v0s, v1s, outs, checked: bool = False):
+        """checked=True (merge.slerp_tensors): the caller has verified devices, contiguity, sizes
+        against the plan and the two dtypes; the per-tensor Python pass is skipped (alignment and
+        the overlap rule are checked in C either way)."""
         import numpy as np
         lib = L.lib()
         T = len(v0s)
         if not plan.relative or T != plan.nseg or len(v1s) != T or len(outs) != T:
             raise L.EdtError("slerp_list needs a relative plan with one segment per tensor")
-        self.device = L.require_device(*v0s, *v1s, *outs)
         in_dt, out_dt = (v0s[0].dtype, outs[0].dtype) if T else (torch.float32, torch.float32)
         sizes = plan.seg_numel
-        for i in range(T):
-            n = int(sizes[i])
-            if v0s[i].numel() != n or v1s[i].numel() != n or outs[i].numel() != n:
-                raise L.EdtError(f"tensor {i} does not match the plan's layout")
-            if v0s[i].dtype != in_dt or v1s[i].dtype != in_dt or outs[i].dtype != out_dt:
-                raise L.EdtError("slerp_list: one input dtype and one output dtype")
+        if checked and T:
+            self.device = v0s[0].device
+        else:
+            self.device = L.require_device(*v0s, *v1s, *outs)
+            for i in range(T):
+                n = int(sizes[i])
+                if v0s[i].numel() != n or v1s[i].numel() != n or outs[i].numel() != n:
+                    raise L.EdtError(f"tensor {i} does not match the plan's layout")
+                if v0s[i].dtype != in_dt or v1s[i].dtype != in_dt or outs[i].dtype != out_dt:
+                    raise L.EdtError("slerp_list: one input dtype and one output dtype")
         self.plan, self.in_dt, self.out_dt = plan, L.dtype_code(in_dt), L.dtype_code(out_dt)
         self.in_size, self.out_size = torch.empty(0, dtype=in_dt).element_size(), torch.empty(0, dtype=out_dt).element_size()
         self._keep = (list(v0s), list(v1s), list(outs))
         arr = [(ctypes.c_void_p * max(1, T))(*[x.data_ptr() for x in ts]) for ts in self._keep]
-        numel = (ctypes.c_uint64 * max(1, T))(*[int(x) for x in sizes])
+        numel_arr = np.ascontiguousarray(sizes, dtype=np.uint64)      # alive across both calls below
+        numel = numel_arr.ctypes.data_as(ctypes.c_void_p) if T else None
         host = np.zeros(max(1, 3 * T), dtype=np.uint64)
         hp = host.ctypes.data_as(ctypes.c_void_p)
         L.check(lib.edt_slerp_seg_table(arr[0], arr[1], arr[2], T, numel, self.in_dt, self.out_dt, 0, hp),
