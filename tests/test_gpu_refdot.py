@@ -322,3 +322,40 @@ def test_refdot_mode_sharded_population_virtual_ranks(dev, world):
         ops.slerp_arena(plan, mem[i], mem[j], want, t, speculate=False, ref_dot=ref)
         torch.cuda.synchronize()
         assert torch.equal(res[c][0].view(torch.int16), want.view(torch.int16)), c
+
+
+@pytest.mark.parametrize("threads", [1, 3])
+def test_refdot_mode_resident_population_generations(oracle, dev, threads):
+    """ResidentPopulation(kind="slerp", ref_dot=RefDot(threads)) over three generations (lineage
+    members -> the speculative form; then independent members; then their children -> the Gram
+    form by the previous dots): every child equals the reference restatement with that BLAS thread
+    split (oracle.slerp_parts_refdot) on every tensor, bit for bit."""
+    from evolutionarydistributedtraining_amd import ops
+    from evolutionarydistributedtraining_amd.population import ResidentPopulation
+    layout, _ = _mixed_population(dev, torch.bfloat16, n_members=1)
+    N = 6
+    genomes = [{"env": {"env_name": "ivy", "reward_dna": [m % 3, 1, 0], "agents": []}} for m in range(N)]
+    t = [0.3, 0.5, 0.9, 0.43333333333333335, 0.0, 1.0, 0.5, 0.7, 0.999]
+    pop = ResidentPopulation(layout, torch.bfloat16, dev, genomes, kind="slerp", seg_t=t,
+                             ref_dot=ops.RefDot(threads=threads))
+    g = torch.Generator().manual_seed(95)
+    base = torch.randn(layout.total, generator=g) * 0.02
+    for m in range(N):
+        pop.params(m).copy_((base + torch.randn(layout.total, generator=g) * 0.02 * 0.005).bfloat16())
+    offs = layout.offsets
+    for gen, pairs in enumerate([[((c + 1) % N, (c + 2) % N) for c in range(N)],
+                                 [((2 * c) % N, (2 * c + 3) % N) for c in range(N)],
+                                 [((c + 4) % N, c) for c in range(N)]]):
+        if gen == 1:
+            for m in range(N):
+                pop.params(m).copy_((torch.randn(layout.total, generator=g) * 0.02).bfloat16())
+        parents = [pop.params(m).cpu().clone() for m in range(N)]
+        pop.crossover(pairs)
+        torch.cuda.synchronize()
+        for c, (i, j) in enumerate(pairs):
+            got = pop.params(c).cpu()
+            for s in range(len(layout)):
+                a, b = offs[s], offs[s + 1]
+                want, _, _ = oracle.slerp_parts_refdot(t[s], parents[i][a:b], parents[j][a:b], threads=threads)
+                want = torch.from_numpy(np.ascontiguousarray(np.ravel(want))).bfloat16()
+                assert torch.equal(got[a:b].view(torch.int16), want.view(torch.int16)), (gen, c, s)
