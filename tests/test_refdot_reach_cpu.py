@@ -81,11 +81,22 @@ def _run(comm, layout, members, pairs, t, oracle, ref):
 
 @pytest.mark.parametrize("world", [1, 2, 3, 5])
 def test_sharded_reference_mode_equals_numpy_slerp(oracle, world):
+    _sharded_vs_reference(oracle, world, threads=1)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_reference_mode_blas_threads(oracle, world):
+    """A reference host whose OpenBLAS splits sdot over 3 threads: the split is over the WHOLE
+    segment, which the owning rank holds (straddling segments assembled): equal to the restatement."""
+    _sharded_vs_reference(oracle, world, threads=3)
+
+
+def _sharded_vs_reference(oracle, world, threads):
     layout = ParamLayout(SHAPES)
     members = _members(max(world, 2), layout.total)[:world] if world > 1 else _members(2, layout.total)[:1]
     pairs = _pairs(world)
     t = torch.tensor([0.3, 0.5, 0.9, 0.5, 0.43333333333333335, 0.7, 0.5, 1.0], dtype=torch.float64)
-    res = VirtualWorld(world).run(lambda comm: _run(comm, layout, members, pairs, t, oracle, RefDot(1, -1.0)))
+    res = VirtualWorld(world).run(lambda comm: _run(comm, layout, members, pairs, t, oracle, RefDot(threads, -1.0)))
     ranges = res[0][2]
     straddle = any(ranges[r][4] not in layout.offsets for r in range(world - 1))
     assert world == 1 or straddle, "the layout should put a rank boundary inside a tensor"
@@ -93,7 +104,10 @@ def test_sharded_reference_mode_equals_numpy_slerp(oracle, world):
     for c, (i, j) in enumerate(pairs):
         for s in range(len(SHAPES)):
             a, b = offs[s], offs[s + 1]
-            want, dot, _ = oracle.slerp_parts(float(t[s]), members[i][a:b], members[j][a:b])
+            if threads == 1:                  # numpy itself on this host (its BLAS runs sdot on one thread)
+                want, dot, _ = oracle.slerp_parts(float(t[s]), members[i][a:b], members[j][a:b])
+            else:
+                want, dot, _ = oracle.slerp_parts_refdot(float(t[s]), members[i][a:b], members[j][a:b], threads)
             got = res[c][0][a:b].numpy()
             assert np.array_equal(got.view(np.int32), np.asarray(want, dtype=np.float32).view(np.int32)), (c, s)
             assert np.float32(res[c][1][c, s].item()) == dot, (c, s)
