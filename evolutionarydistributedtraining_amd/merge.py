@@ -221,16 +221,14 @@ def _writes_are_safe(pairs, outs) -> bool:
 
 
 def slerp_tensors(pairs, ts, out_dtype=torch.float32, device=None, dot_threshold=0.9995,
-                  eps=1e-8, out=None, _outs_apart=False) -> list[torch.Tensor]:
+                  eps=1e-8, out=None) -> list[torch.Tensor]:
     """SLERP of each (v0, v1) pair with its own t, all in ONE multi-tensor pass.
 
     Inputs are upcast to float32 exactly like the reference's `.float().numpy()` when the two
     parents' dtypes differ; results are float32 (the reference returns float32) or `out_dtype`
     (rounded to nearest even, as load_state_dict into a bf16 model does). `out`: optional list of
     destination tensors (e.g. the target model's parameters, which may be the first parent's
-    own tensors), written in place. `_outs_apart` (internal): `out` is known to be apart from every
-    parent and 16-byte aligned (merge.fresh_outputs) — the host-side overlap rule is skipped (the C
-    table check still runs).
+    own tensors), written in place.
 
     Parents already on the device are read where they lie (edt_slerp_merge_list); anything
     else is first packed into two flat arenas (edt_slerp_merge)."""
@@ -257,8 +255,7 @@ def slerp_tensors(pairs, ts, out_dtype=torch.float32, device=None, dot_threshold
         outs = out
         if outs is None:
             outs = [torch.empty(a.shape, dtype=out_dtype, device=dev) for a, _ in pairs]
-        if _outs_apart or (_listable(outs, dev) and all(o.dtype == out_dtype for o in outs)
-                           and _writes_are_safe(pairs, outs)):
+        if _listable(outs, dev) and all(o.dtype == out_dtype for o in outs) and _writes_are_safe(pairs, outs):
             plan = _plan_for(offsets, dev, relative=True)
             # the tensors as they are (the C ABI reads data pointers: no autograd, no detach needed);
             # sizes and dtypes were checked above, so the binding skips its own per-tensor pass
@@ -297,26 +294,33 @@ def slerp(t, v0, v1, DOT_THRESHOLD=0.9995, eps=1e-8):
 
 
 def slerp_state_dicts(sd1: dict, sd2: dict, plan, out_dtype=torch.float32, device=None,
-                      dot_threshold=0.9995, eps=1e-8, out: dict | None = None, _outs_apart=False) -> dict:
+                      dot_threshold=0.9995, eps=1e-8, out: dict | None = None) -> dict:
     """Merged state dict {key: tensor} for plan = [(key, t)] (see merge_plan). `out`: a state
     dict to write the results into (e.g. the target model's, == load_state_dict of the merge)."""
     keys = [k for k, _ in plan]
     res = slerp_tensors([(sd1[k], sd2[k]) for k in keys], [t for _, t in plan], out_dtype, device,
-                        dot_threshold, eps, out=None if out is None else [out[k] for k in keys],
-                        _outs_apart=_outs_apart)
+                        dot_threshold, eps, out=None if out is None else [out[k] for k in keys])
     return dict(zip(keys, res))
+
+
+def _padded_offsets(ns):
+    """Element offsets of tensors of sizes `ns` packed with every start on a 16-byte boundary
+    (a multiple of 8 elements: the tensor-list kernels' alignment), and the total size."""
+    ns = np.asarray(ns, dtype=np.int64)
+    padded = (ns + 7) // 8 * 8
+    offs = np.zeros(len(ns), dtype=np.int64)
+    if len(ns):
+        np.cumsum(padded[:-1], out=offs[1:])
+    return offs, max(int(padded.sum()), 8)
 
 
 def fresh_outputs(like, dtype, device) -> list[torch.Tensor]:
     """Tensors shaped like `like`, carved from ONE new buffer with every start on a 16-byte
-    boundary (the tensor-list kernels' alignment): a merge's output apart from both parents, so
-    it can take the single-pass form (ops.slerp_list) instead of the two-pass in-place one."""
-    offs, o = [], 0
-    for t in like:
-        offs.append(o)
-        o += (t.numel() + 7) // 8 * 8
-    buf = torch.empty(max(o, 8), dtype=dtype, device=device)
-    return [buf.as_strided(t.shape, _contig_strides(t.shape), a) for a, t in zip(offs, like)]
+    boundary: a merge's output apart from both parents, so it can take the single-pass form
+    (ops.slerp_list) instead of the two-pass in-place one (the layout _rebind_merge writes)."""
+    offs, total = _padded_offsets([t.numel() for t in like])
+    buf = torch.empty(total, dtype=dtype, device=device)
+    return [buf.as_strided(t.shape, _contig_strides(t.shape), a) for a, t in zip(offs.tolist(), like)]
 
 
 def _contig_strides(shape):
@@ -346,16 +350,99 @@ def _overlaps_any(outs, ins) -> bool:
     return bool(np.any((i > 0) & (far[np.maximum(i - 1, 0)] > a_out)))
 
 
+class _NeedsStateDict(Exception):
+    pass
+
+
 def module_tensors(module: torch.nn.Module) -> dict:
     """module.state_dict()'s {key: tensor} — for a module whose state is its parameters (no
-    persistent buffers, no state-dict hooks), read straight from named_parameters without
-    state_dict's per-module walk and per-tensor detach (the kernels take data pointers)."""
-    for m in module.modules():
-        if m._state_dict_hooks or getattr(m, "_state_dict_pre_hooks", None):
-            return module.state_dict()
-        if any(b is not None and n not in m._non_persistent_buffers_set for n, b in m._buffers.items()):
-            return module.state_dict()
-    return dict(module.named_parameters(remove_duplicate=False))
+    persistent buffers, no state-dict hooks, no extra state), read in one walk of the module tree
+    in state_dict's own key order (a module's parameters, then its children), without state_dict's
+    per-module generator chain and per-tensor detach (the kernels take data pointers)."""
+    out = {}
+    base_extra = torch.nn.Module.get_extra_state
+
+    def walk(m, pre):
+        if m._state_dict_hooks or m._state_dict_pre_hooks or type(m).get_extra_state is not base_extra:
+            raise _NeedsStateDict
+        if m._buffers:
+            for n, b in m._buffers.items():
+                if b is not None and n not in m._non_persistent_buffers_set:
+                    raise _NeedsStateDict
+        for n, p in m._parameters.items():
+            if p is not None:
+                out[pre + n] = p
+        for n, c in m._modules.items():
+            if c is not None:
+                walk(c, pre + n + ".")
+
+    try:
+        walk(module, "")
+    except _NeedsStateDict:
+        return module.state_dict()
+    return out
+
+
+def _pair_pointers(pairs, dev):
+    """One pass over device-resident parent pairs: (v0 addresses, v1 addresses, sizes, dtype) as
+    numpy arrays when the tensor-list kernels can address every tensor where it lies (one dtype,
+    fp32 / bf16, on `dev`, contiguous, 16-byte aligned); None otherwise. Unequal shapes raise as
+    slerp_tensors does."""
+    if not pairs:
+        return None
+    dt = pairs[0][0].dtype
+    if dt not in (torch.float32, torch.bfloat16):
+        return None
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    p0, p1, ns = [], [], []
+    for a, b in pairs:
+        if a.dtype != dt or b.dtype != dt or not (a.is_cuda and b.is_cuda):
+            return None
+        if a.shape != b.shape:
+            raise EdtError(f"parents disagree on a tensor shape: {tuple(a.shape)} vs {tuple(b.shape)}")
+        if a.get_device() != idx or b.get_device() != idx or not (a.is_contiguous() and b.is_contiguous()):
+            return None
+        p0.append(a.data_ptr())
+        p1.append(b.data_ptr())
+        ns.append(a.numel())
+    p0 = np.array(p0, dtype=np.uint64)
+    p1 = np.array(p1, dtype=np.uint64)
+    if np.any((p0 | p1) % np.uint64(16)):
+        return None
+    return p0, p1, np.array(ns, dtype=np.int64), dt
+
+
+def _rebind_merge(params, keys, outs, sd1, sd2, plan, out_dtype, dev, dot_threshold, eps) -> bool:
+    """slerp_into_module_'s single-pass form, when it applies: the children written to ONE fresh
+    buffer (16-byte aligned starts, addresses computed before any view of it exists), the merge
+    launched, and only then — while the device runs it — the views carved and the parameters
+    re-pointed at them. False (nothing done) when the form does not apply: a parent not addressable
+    in place, an output dtype other than the merge's (a mixed-dtype module keeps its tensors), or
+    outputs apart from both parents (written in place in one pass already)."""
+    if any(o.dtype != out_dtype for o in outs):
+        return False
+    pairs = [(sd1[k], sd2[k]) for k in keys]
+    meta = _pair_pointers(pairs, dev)
+    if meta is None:
+        return False
+    p0, p1, ns, in_dt = meta
+    if not all(o is a for o, (a, _) in zip(outs, pairs)):      # all: the reference's case, target == model_1
+        if not (all(o.device == dev for o in outs) and _overlaps_any(outs, [t for p in pairs for t in p])):
+            return False
+    offs, total = _padded_offsets(ns)
+    buf = torch.empty(total, dtype=out_dtype, device=dev)
+    esz = buf.element_size()
+    po = np.uint64(buf.data_ptr()) + offs.astype(np.uint64) * np.uint64(esz)
+    offsets = [0]
+    offsets.extend(np.cumsum(ns).tolist())
+    splan = _plan_for(offsets, dev, relative=True)
+    tt = torch.tensor([t for _, t in plan], dtype=torch.float64).to(dev)
+    ops.SlerpListBinding.from_pointers(splan, p0, p1, po, in_dt, out_dtype, dev, keep=(buf, pairs)).merge(
+        tt, dot_threshold, eps, ref_dot=_ref_dot)
+    with torch.no_grad():                                        # overlaps the kernels
+        for k, o, a in zip(keys, outs, offs.tolist()):
+            params[k].data = buf.as_strided(o.shape, _contig_strides(o.shape), a)
+    return True
 
 
 def slerp_into_module_(module: torch.nn.Module, sd1: dict, sd2: dict, plan, out_dtype, device=None,
@@ -364,10 +451,10 @@ def slerp_into_module_(module: torch.nn.Module, sd1: dict, sd2: dict, plan, out_
     in the fewest passes over HBM. When the module's own tensors are a parent's (the reference
     merges into model_1 itself) and everything is device-resident, the children are written to a
     FRESH buffer by the single-pass form and the module's parameters are then re-pointed at it
-    (param.data = view): the same values as writing into the parent's tensors — which would force
-    the two-pass form, whose blend re-reads both parents after every sum — in one pass over the
-    parents (7B lineage: ~7 ms against ~11 ms). The parent's old storage is released once nothing
-    else refers to it. Otherwise the merge writes into the module's tensors in place."""
+    (param.data = view, _rebind_merge): the same values as writing into the parent's tensors —
+    which would force the two-pass form, whose blend re-reads both parents after every sum — in one
+    pass over the parents (7B lineage: ~7 ms against ~11 ms). The parent's old storage is released
+    once nothing else refers to it. Otherwise the merge writes into the module's tensors in place."""
     keys = [k for k, _ in plan]
     params = params if params is not None else dict(module.named_parameters(remove_duplicate=False))
     if all(k in params for k in keys):
@@ -376,19 +463,11 @@ def slerp_into_module_(module: torch.nn.Module, sd1: dict, sd2: dict, plan, out_
         tsd = module.state_dict()
         outs = [tsd[k] for k in keys]
     dev = device or _compute_device(*[t for k in keys for t in (sd1[k], sd2[k])])
-    ins = [t for k in keys for t in (sd1[k], sd2[k])]
-    rebind = (all(k in params for k in keys) and dev.type == "cuda" and _listable(ins, dev)
-              and all(o.device == dev for o in outs) and _overlaps_any(outs, ins))
-    if not rebind:
-        slerp_state_dicts(sd1, sd2, plan, out_dtype=out_dtype, device=device, dot_threshold=dot_threshold,
-                          eps=eps, out=tsd if tsd is not None else dict(zip(keys, outs)))
+    if tsd is None and dev.type == "cuda" and keys and _rebind_merge(
+            params, keys, outs, sd1, sd2, plan, out_dtype, dev, dot_threshold, eps):
         return
-    fresh = fresh_outputs(outs, out_dtype, dev)
-    slerp_state_dicts(sd1, sd2, plan, out_dtype=out_dtype, device=device, dot_threshold=dot_threshold, eps=eps,
-                      out=dict(zip(keys, fresh)), _outs_apart=True)
-    with torch.no_grad():
-        for k, f in zip(keys, fresh):
-            params[k].data = f
+    slerp_state_dicts(sd1, sd2, plan, out_dtype=out_dtype, device=device, dot_threshold=dot_threshold,
+                      eps=eps, out=tsd if tsd is not None else dict(zip(keys, outs)))
 
 
 def merge_models_into_(target: torch.nn.Module, model_1: torch.nn.Module, model_2: torch.nn.Module,

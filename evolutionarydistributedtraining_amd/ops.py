@@ -572,6 +572,9 @@ def slerp_arena(plan: SlerpPlan, v0: torch.Tensor, v1: torch.Tensor, out: torch.
     _record_dots(plan, plan.dots[:max(1, plan.nseg)], "_dots")
 
 
+_ELEM_SIZE = {torch.float32: 4, torch.bfloat16: 2, torch.float16: 2, torch.float64: 8}
+
+
 class SlerpListBinding:
     """A tensor-list SLERP bound to its tensors (EDT_EVOMERGE/train/crossover.py:104-146's state-dict
     tensors, merged where they lie): the per-tensor checks run once here and the validated
@@ -600,18 +603,41 @@ class SlerpListBinding:
                     raise L.EdtError(f"tensor {i} does not match the plan's layout")
                 if v0s[i].dtype != in_dt or v1s[i].dtype != in_dt or outs[i].dtype != out_dt:
                     raise L.EdtError("slerp_list: one input dtype and one output dtype")
+        keep = (list(v0s), list(v1s), list(outs))
+        p0, p1, po = (np.fromiter((x.data_ptr() for x in ts), dtype=np.uint64, count=T) for ts in keep)
+        self._bind(plan, p0, p1, po, in_dt, out_dt, keep)
+
+    @classmethod
+    def from_pointers(cls, plan: SlerpPlan, p0, p1, pout, in_dtype: torch.dtype, out_dtype: torch.dtype,
+                      device: torch.device, keep) -> "SlerpListBinding":
+        """A binding over raw device addresses (numpy uint64 [nseg] each: v0, v1, out of every
+        segment, sizes = the plan's), for a caller that has checked devices, contiguity, dtypes and
+        sizes itself (merge.slerp_into_module_: the children's addresses in a fresh buffer are known
+        before any view of it exists). Alignment and the overlap rule are still checked in C.
+        `keep`: whatever owns the memory (held as long as the binding)."""
+        self = cls.__new__(cls)
+        if not plan.relative or not (len(p0) == len(p1) == len(pout) == plan.nseg):
+            raise L.EdtError("slerp_list needs a relative plan with one segment per tensor")
+        self.device = device
+        self._bind(plan, p0, p1, pout, in_dtype, out_dtype, keep)
+        return self
+
+    def _bind(self, plan, p0, p1, po, in_dt, out_dt, keep):
+        import numpy as np
+        lib, T = L.lib(), plan.nseg
         self.plan, self.in_dt, self.out_dt = plan, L.dtype_code(in_dt), L.dtype_code(out_dt)
-        self.in_size, self.out_size = torch.empty(0, dtype=in_dt).element_size(), torch.empty(0, dtype=out_dt).element_size()
-        self._keep = (list(v0s), list(v1s), list(outs))
-        arr = [(ctypes.c_void_p * max(1, T))(*[x.data_ptr() for x in ts]) for ts in self._keep]
-        numel_arr = np.ascontiguousarray(sizes, dtype=np.uint64)      # alive across both calls below
+        self.in_size, self.out_size = _ELEM_SIZE[in_dt], _ELEM_SIZE[out_dt]
+        self._keep = keep
+        arrs = [np.ascontiguousarray(a if T else np.zeros(1), dtype=np.uint64) for a in (p0, p1, po)]
+        vp = ctypes.POINTER(ctypes.c_void_p)
+        a0, a1, a2 = (a.ctypes.data_as(vp) for a in arrs)
+        numel_arr = np.ascontiguousarray(plan.seg_numel, dtype=np.uint64)   # alive across both calls below
         numel = numel_arr.ctypes.data_as(ctypes.c_void_p) if T else None
         host = np.zeros(max(1, 3 * T), dtype=np.uint64)
         hp = host.ctypes.data_as(ctypes.c_void_p)
-        L.check(lib.edt_slerp_seg_table(arr[0], arr[1], arr[2], T, numel, self.in_dt, self.out_dt, 0, hp),
-                "edt_slerp_seg_table")
+        L.check(lib.edt_slerp_seg_table(a0, a1, a2, T, numel, self.in_dt, self.out_dt, 0, hp), "edt_slerp_seg_table")
         # outputs apart from every parent (a sorted-span check in C): the single-pass form is allowed
-        self.apart = lib.edt_slerp_seg_table(arr[0], arr[1], arr[2], T, numel, self.in_dt, self.out_dt, 1, hp) == 0
+        self.apart = lib.edt_slerp_seg_table(a0, a1, a2, T, numel, self.in_dt, self.out_dt, 1, hp) == 0
         self.table = torch.from_numpy(host.view(np.int64)).to(self.device)
 
     def merge(self, t: torch.Tensor, dot_threshold: float = 0.9995, eps: float = 1e-8,

@@ -570,3 +570,65 @@ def test_outer_step_surface_cpu_tails_bit_exact_with_reference(golden, dev):
                            cpu_tails=(32, c["torch_num_threads"]))
         got = flat([t.cpu() for t in base])
         assert torch.equal(bits(got), bits(flat(golden.tlist("diloco", f"{pre}/s{step}/out_theta", T)))), step
+
+
+def _qwen_pair(dev, far, seed=0):
+    from transformers import Qwen2Config, Qwen2ForCausalLM
+    cfg = Qwen2Config(vocab_size=40, hidden_size=32, intermediate_size=72, num_hidden_layers=4,
+                      num_attention_heads=4, num_key_value_heads=2, tie_word_embeddings=False)
+    g = torch.Generator().manual_seed(seed)
+    ms = [Qwen2ForCausalLM(cfg).to(torch.bfloat16) for _ in range(2)]
+    with torch.no_grad():
+        for p1, p2 in zip(ms[0].parameters(), ms[1].parameters()):
+            p1.copy_(torch.randn(p1.shape, generator=g) * 0.02)
+            noise = torch.randn(p1.shape, generator=g) * 0.02
+            p2.copy_(noise if far else p1.float() + noise * 0.005)
+    return cfg, [m.to(dev) for m in ms]
+
+
+@pytest.mark.parametrize("far", [False, True])
+def test_evomerge_rebind_equals_in_place(dev, far):
+    """merge_models_into_(model_1, model_1, model_2) — the single pass into a fresh buffer, then
+    model_1's parameters re-pointed — gives the bits of the in-place two-pass merge into model_1's
+    own tensors, leaves model_2 alone, and a second generation on the re-pointed parameters too."""
+    from evolutionarydistributedtraining_amd import evomerge_crossover as ev
+    from evolutionarydistributedtraining_amd import merge
+    cfg, (m1, m2) = _qwen_pair(dev, far)
+    mcfg = ev.slerp_config("a", "b", cfg.num_hidden_layers)
+    start = {k: v.clone() for k, v in m1.model.state_dict().items()}
+    m2_bits = {k: v.clone() for k, v in m2.model.state_dict().items()}
+    plan = merge.merge_plan(list(start), cfg.num_hidden_layers, mcfg)
+    for gen in range(2):
+        want_sd = {k: v.clone() for k, v in m1.model.state_dict().items()}
+        merge.slerp_state_dicts(dict(want_sd), m2.model.state_dict(), plan, out_dtype=torch.bfloat16,
+                                device=dev, out=want_sd)                      # in place, two-pass
+        before = {k: p.data_ptr() for k, p in m1.model.named_parameters()}
+        merge.merge_models_into_(m1.model, m1.model, m2.model, mcfg, cfg.num_hidden_layers, device=dev)
+        got = m1.model.state_dict()
+        for k, _ in plan:
+            assert got[k].data_ptr() != before[k]
+            assert got[k].dtype == torch.bfloat16 and got[k].is_contiguous()
+            assert torch.equal(got[k].view(torch.int16), want_sd[k].view(torch.int16)), (gen, k)
+        assert all(torch.equal(v, m2_bits[k]) for k, v in m2.model.state_dict().items())
+
+
+def test_evomerge_mixed_dtype_target_keeps_its_tensors(dev):
+    """A bf16 model_1 with one fp32 parameter: not re-pointed (a fresh bf16 buffer would change that
+    parameter's dtype); the merge is written into model_1's tensors in their own dtypes, as
+    load_state_dict does, each tensor equal to its own single-tensor merge."""
+    from evolutionarydistributedtraining_amd import evomerge_crossover as ev
+    from evolutionarydistributedtraining_amd import merge
+    cfg, (m1, m2) = _qwen_pair(dev, far=True, seed=1)
+    with torch.no_grad():
+        m1.model.norm.weight.data = m1.model.norm.weight.data.float()
+    mcfg = ev.slerp_config("a", "b", cfg.num_hidden_layers)
+    sd1 = {k: v.clone() for k, v in m1.model.state_dict().items()}
+    sd2 = m2.model.state_dict()
+    plan = merge.merge_plan(list(sd1), cfg.num_hidden_layers, mcfg)
+    before = {k: (p.data_ptr(), p.dtype) for k, p in m1.model.named_parameters()}
+    merge.merge_models_into_(m1.model, m1.model, m2.model, mcfg, cfg.num_hidden_layers, device=dev)
+    got = m1.model.state_dict()
+    for k, t in plan:
+        assert (got[k].data_ptr(), got[k].dtype) == before[k], k
+        want = merge.slerp_tensors([(sd1[k], sd2[k])], [t], out_dtype=torch.float32, device=dev)[0]
+        assert torch.equal(got[k], want.to(got[k].dtype)), k

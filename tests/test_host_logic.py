@@ -445,3 +445,44 @@ def test_overlaps_any_matches_brute_force():
     outs = merge.fresh_outputs([torch.empty(s) for s in shapes], torch.bfloat16, "cpu")
     assert [o.shape for o in outs] == [torch.Size(s) for s in shapes]
     assert all(o.is_contiguous() and o.data_ptr() % 16 == 0 for o in outs)
+
+
+def test_module_tensors_is_state_dict():
+    """merge.module_tensors: state_dict's keys, order and tensors for a parameters-only module;
+    state_dict itself when a module has persistent buffers, extra state or a state-dict hook."""
+    from transformers import Qwen2Config, Qwen2ForCausalLM
+    cfg = Qwen2Config(vocab_size=24, hidden_size=8, intermediate_size=16, num_hidden_layers=3,
+                      num_attention_heads=2, num_key_value_heads=1, tie_word_embeddings=True)
+    m = Qwen2ForCausalLM(cfg)
+    for mod in (m, m.model):
+        got, want = merge.module_tensors(mod), mod.state_dict()
+        assert list(got) == list(want)
+        assert all(got[k].data_ptr() == want[k].data_ptr() for k in want)
+        assert all(isinstance(v, torch.nn.Parameter) for v in got.values())
+
+    class WithBuffer(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.lin = torch.nn.Linear(2, 2)
+            self.register_buffer("count", torch.zeros(1))
+
+    class WithExtra(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.lin = torch.nn.Linear(2, 2)
+
+        def get_extra_state(self):
+            return {"x": 1}
+
+    for mod in (WithBuffer(), torch.nn.Sequential(WithExtra())):
+        assert list(merge.module_tensors(mod)) == list(mod.state_dict())
+    hooked = torch.nn.Sequential(torch.nn.Linear(2, 2))
+    hooked[0]._register_state_dict_hook(lambda mod, sd, prefix, local: sd.pop(prefix + "bias"))
+    assert list(merge.module_tensors(hooked)) == list(hooked.state_dict()) == ["0.weight"]
+
+
+def test_padded_offsets():
+    offs, total = merge._padded_offsets([3, 8, 0, 9, 1])
+    assert offs.tolist() == [0, 8, 16, 16, 32] and total == 40
+    offs, total = merge._padded_offsets([])
+    assert offs.size == 0 and total == 8
