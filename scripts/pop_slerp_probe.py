@@ -47,7 +47,7 @@ def main():
     plan = ops.make_slerp_plan(lay.offsets, dev)
     pairs = [((3 * c + 1) % N, (5 * c + 2) % N) for c in range(N)]
     s = torch.cuda.current_stream(dev)
-    res = {}
+    res, sigs = {}, {}
 
     def run(name, speculate):
         ts = []
@@ -60,11 +60,23 @@ def main():
             if r:
                 ts.append(e0.elapsed_time(e1))
         slerp_share = float((dots.abs() <= 0.9995).float().mean())
+        # the dots (every Gram / pair sum feeds them) and a strided sample of every child, against
+        # the first build's same form on the same members: a variant must give the same bits
+        sig = torch.cat([dots.reshape(-1).view(torch.int64).double(),
+                         torch.stack([o[::7919].view(torch.int16).double().sum() for o in outs])])
+        key = name.split("/")[0]
+        same = None
+        if key in sigs:
+            same = bool(torch.equal(sigs[key], sig))
+        else:
+            sigs[key] = sig
         res[name] = {"median_ms": round(statistics.median(ts), 3), "min_ms": round(min(ts), 3),
                      "children": N, "distinct_parents": len({m for p in pairs for m in p}),
                      "slerp_branch_segment_share": round(slerp_share, 3),
                      "GBps_algorithmic": round(2 * P * (len({m for p in pairs for m in p}) + N)
                                                / statistics.median(ts) / 1e6, 1)}
+        if same is not None:
+            res[name]["bit_identical_to_first_build"] = same
         print(name, res[name], flush=True)
 
     base = torch.empty(P, dtype=BF, device=dev)
