@@ -87,9 +87,6 @@ using edt::g_err;
 #ifndef EDT_GRAM_NT             // Gram pass: non-temporal member loads (each member is read once)
 #define EDT_GRAM_NT 1
 #endif
-#ifndef EDT_GRAM_GLDS           // Gram pass, bf16: the next tile staged by LDS-DMA instead of a second register set
-#define EDT_GRAM_GLDS 0
-#endif
 #ifndef EDT_GRAM_MIN_BLOCKS     // Gram pass: __launch_bounds__ minimum workgroups per CU (waves per SIMD)
 #define EDT_GRAM_MIN_BLOCKS 1
 #endif

@@ -790,8 +790,6 @@ __global__ __launch_bounds__(kBlock, EDT_GRAM_MIN_BLOCKS) void slerp_gram_kernel
     constexpr int kPad = 17;
     __shared__ double part[kWavesPerBlock][4 * N2 * kPad];
     __shared__ double ts2[kWavesPerBlock][NT];
-    constexpr bool kGlds = EDT_GRAM_GLDS != 0 && IDT == EDT_BF16;
-    __shared__ u32x4 stage[kGlds ? kWavesPerBlock : 1][kGlds ? M : 1][64];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t units = (uint64_t)nchunks * upc;
     const uint64_t u = u0 + blockIdx.x;
@@ -826,7 +824,7 @@ __global__ __launch_bounds__(kBlock, EDT_GRAM_MIN_BLOCKS) void slerp_gram_kernel
         double gs[NT];
         const uint64_t i = a + (uint64_t)j * kTileElems + (uint64_t)lane * kVec;
         if constexpr (decltype(full)::value) {
-            if constexpr (EDT_GRAM_PREFETCH || kGlds) {
+            if constexpr (EDT_GRAM_PREFETCH) {
                 gram_fma_first<M, kVec>(xin, gs);      // loaded one tile ahead
             } else {
                 Raw8<IDT> x[M];
@@ -874,32 +872,7 @@ __global__ __launch_bounds__(kBlock, EDT_GRAM_MIN_BLOCKS) void slerp_gram_kernel
     // uniform: every tile of the unit inside the aligned body (all but a segment's last unit)
     Raw8<IDT> x0[M];
     if (a + (uint64_t)(16 * g + 16) * kTileElems <= b) {
-        if constexpr (kGlds) {                         // tile k + 1 lands in the wave's LDS stage while
-            const int ws = __builtin_amdgcn_readfirstlane(wave);   // tile k is summed from registers
-            auto issue = [&](int k) {
-                const uint64_t i = a + (uint64_t)(16 * g + 4 * wave + k) * kTileElems + (uint64_t)lane * kVec;
-#pragma unroll
-                for (int m = 0; m < M; ++m)
-                    __builtin_amdgcn_global_load_lds(
-                        (const __attribute__((address_space(1))) void*)(static_cast<const uint16_t*>(mem.p[m]) + i),
-                        (__attribute__((address_space(3))) void*)&stage[ws][m][0], 16, 0, EDT_GRAM_NT ? 2 : 0);
-            };
-            // the issuing wave's own vmcnt orders its DMA before its ds_reads; lgkmcnt(0) retires the
-            // reads before the stage is written again
-            auto fetch = [&](Raw8<IDT> (&x)[M]) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-                for (int m = 0; m < M; ++m) x[m].w = stage[ws][m][lane];
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            };
-            issue(0);
-#pragma unroll 1
-            for (int k = 0; k < 4; ++k) {
-                fetch(x0);
-                if (k < 3) issue(k + 1);
-                tile(k, std::true_type{}, x0);
-            }
-        } else if constexpr (EDT_GRAM_PREFETCH) {             // two register sets: tile k + 1's loads in flight
+        if constexpr (EDT_GRAM_PREFETCH) {             // two register sets: tile k + 1's loads in flight
             Raw8<IDT> x1[M];                           // while tile k is summed (sched_barrier: the
             load_tile(0, x0);                          // scheduler may not sink them to their use)
             load_tile(1, x1);

@@ -19,7 +19,6 @@ VARIANTS = {
     "gramprefetch": ["-DEDT_GRAM_PREFETCH=1"],
     "gramnt": ["-DEDT_GRAM_NT=1"],
     "gramntpf": ["-DEDT_GRAM_NT=1", "-DEDT_GRAM_PREFETCH=1"],
-    "gramglds": ["-DEDT_GRAM_GLDS=1", "-DEDT_GRAM_PREFETCH=0"],
     "gramregs3": ["-DEDT_GRAM_PREFETCH=0"],
 }
 
