@@ -592,19 +592,30 @@ class SlerpListBinding:
         if not plan.relative or T != plan.nseg or len(v1s) != T or len(outs) != T:
             raise L.EdtError("slerp_list needs a relative plan with one segment per tensor")
         in_dt, out_dt = (v0s[0].dtype, outs[0].dtype) if T else (torch.float32, torch.float32)
-        sizes = plan.seg_numel
+        keep = (list(v0s), list(v1s), list(outs))
         if checked and T:
             self.device = v0s[0].device
+            p0, p1, po = (np.fromiter((x.data_ptr() for x in ts), dtype=np.uint64, count=T) for ts in keep)
         else:
-            self.device = L.require_device(*v0s, *v1s, *outs)
-            for i in range(T):
-                n = int(sizes[i])
-                if v0s[i].numel() != n or v1s[i].numel() != n or outs[i].numel() != n:
+            # one pass over the triples (what L.require_device and the size / dtype checks test)
+            p0, p1, po, devs = [], [], [], set()
+            for i, (x, y, o, n) in enumerate(zip(*keep, plan.seg_numel.tolist())):
+                if not (x.is_cuda and y.is_cuda and o.is_cuda):
+                    raise L.EdtError("outer-loop sync operands must be device-resident (HBM) tensors")
+                if not (x.is_contiguous() and y.is_contiguous() and o.is_contiguous()):
+                    raise L.EdtError("outer-loop sync operands must be contiguous")
+                if x.numel() != n or y.numel() != n or o.numel() != n:
                     raise L.EdtError(f"tensor {i} does not match the plan's layout")
-                if v0s[i].dtype != in_dt or v1s[i].dtype != in_dt or outs[i].dtype != out_dt:
+                if x.dtype != in_dt or y.dtype != in_dt or o.dtype != out_dt:
                     raise L.EdtError("slerp_list: one input dtype and one output dtype")
-        keep = (list(v0s), list(v1s), list(outs))
-        p0, p1, po = (np.fromiter((x.data_ptr() for x in ts), dtype=np.uint64, count=T) for ts in keep)
+                devs.update((x.get_device(), y.get_device(), o.get_device()))
+                p0.append(x.data_ptr())
+                p1.append(y.data_ptr())
+                po.append(o.data_ptr())
+            if len(devs) > 1:
+                raise L.EdtError(f"operands on different devices: {sorted(devs)}")
+            self.device = v0s[0].device if T else None
+            p0, p1, po = (np.array(p, dtype=np.uint64) for p in (p0, p1, po))
         self._bind(plan, p0, p1, po, in_dt, out_dt, keep)
 
     @classmethod
