@@ -277,15 +277,17 @@ class DirOuterSync:
     so the next inner loop resumes the inner optimiser as the reference's does — into the dirs the
     new weights go to (out_dirs; the reference writes them over worker_dirs, its default here).
     place_momentum: after the first step, choose the outer momentum's HBM placement by measurement
-    once (OuterSync.place_momentum; 0 = keep the first allocation). The θ and worker arenas stay
-    resident across generations here, so the choice holds for the rest of the run — the drop-in
-    form of the resident flow's placement."""
+    once among this many candidates (OuterSync.place_momentum; 0 or 1 = keep the first allocation).
+    The θ and worker arenas stay resident across generations here, so the choice holds for the rest
+    of the run — the drop-in form of the resident flow's placement. On by default
+    (r4): the first allocation ran the step 8-11 % slower in about half of the bench runs
+    (`roofline.unplaced_ms`), and the search costs a few probe launches once per run."""
 
     INNER_STATE_FILES = ("optimizer.pt", "scheduler.pt")
 
     def __init__(self, device=None, theta_dtype=None, worker_dtype=None, names=None,
                  lr=0.7, momentum=0.9, nesterov=True, state: OuterState | None = None,
-                 state_path: str | None = None, carry_inner_state: bool = False, place_momentum: int = 0):
+                 state_path: str | None = None, carry_inner_state: bool = False, place_momentum: int = 8):
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.theta_dtype, self.worker_dtype, self.names = theta_dtype, worker_dtype, names
         self.lr, self.momentum, self.nesterov = lr, momentum, nesterov
