@@ -187,37 +187,11 @@ def _listable(tensors, dev) -> bool:
 
 def _writes_are_safe(pairs, outs) -> bool:
     """out[i] may alias its own inputs exactly (the blend is element-wise, after every sum);
-    any other overlap of an output with an input or another output is unsafe in one pass.
-    Vectorised over the byte spans (numpy): identical spans grouped; a group holding an output
-    may hold only spans of that output's own pair; distinct groups that overlap are unsafe when
-    either holds an output (a sorted sweep: running furthest end of every group / of output groups)."""
+    any other overlap of an output with an input or another output is unsafe (ops.writes_safe)."""
     ts = [t for (a, b), o in zip(pairs, outs) for t in (a, b, o)]
     st = np.fromiter((t.data_ptr() for t in ts), dtype=np.int64, count=len(ts))
     nb = np.fromiter((t.numel() * t.element_size() for t in ts), dtype=np.int64, count=len(ts))
-    kind_out = np.tile(np.array([False, False, True]), len(outs))
-    owner = np.repeat(np.arange(len(outs), dtype=np.int64), 3)
-    keep = nb > 0
-    st, en, kind_out, owner = st[keep], st[keep] + nb[keep], kind_out[keep], owner[keep]
-    if st.size == 0:
-        return True
-    order = np.lexsort((en, st))
-    st, en, kind_out, owner = st[order], en[order], kind_out[order], owner[order]
-    new_group = np.ones(st.size, dtype=bool)
-    new_group[1:] = (st[1:] != st[:-1]) | (en[1:] != en[:-1])
-    gid = np.cumsum(new_group) - 1
-    ng = int(gid[-1]) + 1
-    outs_per = np.bincount(gid, weights=kind_out, minlength=ng)
-    if (outs_per > 1).any():
-        return False                                         # two outputs on one span
-    out_owner = np.full(ng, -1, dtype=np.int64)
-    out_owner[gid[kind_out]] = owner[kind_out]
-    has_out = out_owner >= 0
-    if (has_out[gid] & (owner != out_owner[gid])).any():
-        return False                                         # an output on another pair's span
-    gst, gen = st[new_group], en[new_group]
-    prev_end = np.concatenate(([-1], np.maximum.accumulate(gen)[:-1]))
-    prev_out_end = np.concatenate(([-1], np.maximum.accumulate(np.where(has_out, gen, -1))[:-1]))
-    return not bool(np.any((has_out & (gst < prev_end)) | (gst < prev_out_end)))
+    return ops.writes_safe(st, nb)
 
 
 def slerp_tensors(pairs, ts, out_dtype=torch.float32, device=None, dot_threshold=0.9995,

@@ -572,6 +572,43 @@ def slerp_arena(plan: SlerpPlan, v0: torch.Tensor, v1: torch.Tensor, out: torch.
     _record_dots(plan, plan.dots[:max(1, plan.nseg)], "_dots")
 
 
+def writes_safe(starts, nbytes) -> bool:
+    """The tensor-list SLERP's write rule over byte spans laid out as (v0, v1, out) per segment
+    (numpy int64 [3 nseg] each): out[i] may alias its own inputs exactly (the blend is element-wise,
+    after every sum); any other overlap of an output with an input or another output is unsafe in
+    either form. Identical spans are grouped; a group holding an output may hold only spans of that
+    output's own segment; distinct groups that overlap are unsafe when either holds an output (a
+    sorted sweep: running furthest end of every group / of the groups holding an output)."""
+    import numpy as np
+    st = np.asarray(starts, dtype=np.int64)
+    nb = np.asarray(nbytes, dtype=np.int64)
+    nseg = st.size // 3
+    kind_out = np.tile(np.array([False, False, True]), nseg)
+    owner = np.repeat(np.arange(nseg, dtype=np.int64), 3)
+    keep = nb > 0
+    st, en, kind_out, owner = st[keep], st[keep] + nb[keep], kind_out[keep], owner[keep]
+    if st.size == 0:
+        return True
+    order = np.lexsort((en, st))
+    st, en, kind_out, owner = st[order], en[order], kind_out[order], owner[order]
+    new_group = np.ones(st.size, dtype=bool)
+    new_group[1:] = (st[1:] != st[:-1]) | (en[1:] != en[:-1])
+    gid = np.cumsum(new_group) - 1
+    ng = int(gid[-1]) + 1
+    outs_per = np.bincount(gid, weights=kind_out, minlength=ng)
+    if (outs_per > 1).any():
+        return False                                         # two outputs on one span
+    out_owner = np.full(ng, -1, dtype=np.int64)
+    out_owner[gid[kind_out]] = owner[kind_out]
+    has_out = out_owner >= 0
+    if (has_out[gid] & (owner != out_owner[gid])).any():
+        return False                                         # an output on another segment's span
+    gst, gen = st[new_group], en[new_group]
+    prev_end = np.concatenate(([-1], np.maximum.accumulate(gen)[:-1]))
+    prev_out_end = np.concatenate(([-1], np.maximum.accumulate(np.where(has_out, gen, -1))[:-1]))
+    return not bool(np.any((has_out & (gst < prev_end)) | (gst < prev_out_end)))
+
+
 _ELEM_SIZE = {torch.float32: 4, torch.bfloat16: 2, torch.float16: 2, torch.float64: 8}
 
 
@@ -635,7 +672,7 @@ class SlerpListBinding:
 
     def _bind(self, plan, p0, p1, po, in_dt, out_dt, keep):
         import numpy as np
-        lib, T = L.lib(), plan.nseg
+        lib, T = L.load_library(), plan.nseg       # host validation only; merge() insists on the device
         self.plan, self.in_dt, self.out_dt = plan, L.dtype_code(in_dt), L.dtype_code(out_dt)
         self.in_size, self.out_size = _ELEM_SIZE[in_dt], _ELEM_SIZE[out_dt]
         self._keep = keep
@@ -649,6 +686,14 @@ class SlerpListBinding:
         L.check(lib.edt_slerp_seg_table(a0, a1, a2, T, numel, self.in_dt, self.out_dt, 0, hp), "edt_slerp_seg_table")
         # outputs apart from every parent (a sorted-span check in C): the single-pass form is allowed
         self.apart = lib.edt_slerp_seg_table(a0, a1, a2, T, numel, self.in_dt, self.out_dt, 1, hp) == 0
+        if not self.apart:
+            # the two-pass form still needs every output apart from everything but its own parents
+            n = numel_arr.astype(np.int64)
+            sizes = np.stack([n * self.in_size, n * self.in_size, n * self.out_size], axis=1).reshape(-1)
+            starts = np.stack([arrs[0], arrs[1], arrs[2]], axis=1).reshape(-1).astype(np.int64)
+            if not writes_safe(starts, sizes):
+                raise L.EdtError("a SLERP output overlaps another tensor's parent or output: no form is safe "
+                                 "(an output may only be its own parent exactly)")
         self.table = torch.from_numpy(host.view(np.int64)).to(self.device)
 
     def merge(self, t: torch.Tensor, dot_threshold: float = 0.9995, eps: float = 1e-8,

@@ -486,3 +486,39 @@ def test_padded_offsets():
     assert offs.tolist() == [0, 8, 16, 16, 32] and total == 40
     offs, total = merge._padded_offsets([])
     assert offs.size == 0 and total == 8
+
+
+def test_binding_from_pointers_host_checks():
+    """SlerpListBinding.from_pointers (merge._rebind_merge's binding: addresses in a fresh buffer
+    computed before any view exists): the C table check still refuses misaligned addresses and
+    a length that disagrees with the plan, and sets `apart` only when no output overlaps a parent."""
+    import numpy as np
+    from evolutionarydistributedtraining_amd import ops
+    from evolutionarydistributedtraining_amd._lib import EdtError
+    sizes = [24, 8, 40]
+    plan = ops.make_slerp_plan([0, 24, 32, 72], torch.device("cpu"), relative=True)
+    base = 1 << 40
+    p0 = np.array([base, base + 1024, base + 2048], dtype=np.uint64)
+    p1 = p0 + np.uint64(1 << 20)
+    po = p0 + np.uint64(2 << 20)
+    b = ops.SlerpListBinding.from_pointers(plan, p0, p1, po, torch.bfloat16, torch.bfloat16, torch.device("cpu"),
+                                           keep=None)
+    assert b.apart and b.table.numel() == 9
+    assert b.table.view(-1, 3)[:, 2].tolist() == po.astype(np.int64).tolist()
+    b = ops.SlerpListBinding.from_pointers(plan, p0, p1, p0.copy(), torch.bfloat16, torch.bfloat16,
+                                           torch.device("cpu"), keep=None)     # out == own v0: two-pass only
+    assert not b.apart
+    po2 = po.copy()
+    po2[1] = p1[2] + np.uint64(16)                  # inside another pair's v1 (40 bf16 = 80 B)
+    with pytest.raises(EdtError):
+        ops.SlerpListBinding.from_pointers(plan, p0, p1, po2, torch.bfloat16, torch.bfloat16,
+                                           torch.device("cpu"), keep=None)
+    po3 = po.copy()
+    po3[2] += np.uint64(2)                          # off a 16-byte boundary
+    with pytest.raises(EdtError):
+        ops.SlerpListBinding.from_pointers(plan, p0, p1, po3, torch.bfloat16, torch.bfloat16,
+                                           torch.device("cpu"), keep=None)
+    with pytest.raises(EdtError):
+        ops.SlerpListBinding.from_pointers(plan, p0[:2], p1[:2], po[:2], torch.bfloat16, torch.bfloat16,
+                                           torch.device("cpu"), keep=None)
+    assert sizes == plan.seg_numel.tolist()
