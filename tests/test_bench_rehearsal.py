@@ -118,9 +118,10 @@ def _launch(world, extra=(), hang_rank=-1, timeout=240, corrupt=False):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_bench_line_at_world(world):
-    outs, lines = _launch(world)
+    """world 8: the driver's node (population 8, one worker per rank; `auto` takes exact there)."""
+    outs, lines = _launch(world, extra=["--population", "8"] if world == 8 else ())
     assert all(rc == 0 for rc, _, _ in outs), [(rc, e[-2000:]) for rc, _, e in outs]
     assert len(lines) == 1, outs[0][1][-2000:]
     for rc, o, _ in outs[1:]:
@@ -147,6 +148,8 @@ def test_bench_line_at_world(world):
     assert par["replicas_equal_reference"] and par["buckets"] > 1 and par["schedule"] == d["config"]["parallelism"].split()[1]
     assert pop["sharded"]["parity"]["bit_exact"], pop["sharded"]
     assert pop["sharded_pipelined"]["parity"]["bit_exact"], pop["sharded_pipelined"]
+    if world == 8:
+        assert d["config"]["parallelism"].startswith("dp8 exact/"), d["config"]
 
 
 @pytest.mark.slow
