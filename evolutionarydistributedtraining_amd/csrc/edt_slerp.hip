@@ -767,6 +767,32 @@ __device__ __forceinline__ void gram_fma_first(const X (&x)[M], double (&g)[M * 
     }
 }
 
+// The ring layout (r4): a population whose children's parent pairs form paths and cycles (every
+// parent in at most two distinct pairs: a ring of children, a matching) needs the M norms and at
+// most M dots (m, m + 1 mod M) once its members are listed along the ring — 2M sums per element
+// instead of M(M+1)/2 (16 against 36 at M = 8). Sums [0, M): |v_m|^2; [M, 2M): v_m . v_{m+1 mod M}.
+// Each sum is the same per-lane FMA chain, butterfly and tree as in the triangle layout (an FMA's
+// product is exact, so the operand order does not matter): bit-identical values.
+template <int M, bool RING>
+struct GramLayout {
+    static constexpr int NT = RING ? 2 * M : M * (M + 1) / 2;
+};
+
+template <int M, int N, typename X>
+__device__ __forceinline__ void ring_fma(const X (&x)[M], double (&g)[2 * M], bool from_zero) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        double d[M];
+#pragma unroll
+        for (int m = 0; m < M; ++m) d[m] = x[m][j];
+        const bool z = from_zero && j == 0;
+#pragma unroll
+        for (int m = 0; m < M; ++m) g[m] = __builtin_fma(d[m], d[m], z ? 0.0 : g[m]);
+#pragma unroll
+        for (int m = 0; m < M; ++m) g[M + m] = __builtin_fma(d[m], d[(m + 1) % M], z ? 0.0 : g[M + m]);
+    }
+}
+
 // Gram rows (level 4), one workgroup per unit of 16 tiles in address order: wave w takes tiles
 // 16 g + 4 w .. + 3 one after the other (one vector per member per lane: M loads in flight). Each
 // tile's NT sums go through the xor butterfly in two parts: the swap levels (32, 16) on the VALU,
@@ -779,11 +805,11 @@ __device__ __forceinline__ void gram_fma_first(const X (&x)[M], double (&g)[M * 
 // (unit_slot). Every sum is bit-identical to pair_slot() on (vi, vj): the same per-lane FMA
 // sequence in element order (an FMA's product is exact, so vi*vj == vj*vi), the same butterfly and
 // tree; the coefficients therefore equal edt_slerp_merge's.
-template <int IDT, int M>
+template <int IDT, int M, bool RING = false>
 __global__ __launch_bounds__(kBlock, EDT_GRAM_MIN_BLOCKS) void slerp_gram_kernel(Members mem, const uint64_t* chunks,
                                                                                  int64_t nchunks, double* rows,
                                                                                  uint64_t u0) {
-    constexpr int NT = M * (M + 1) / 2, N2 = Red<NT>::N2;
+    constexpr int NT = GramLayout<M, RING>::NT, N2 = Red<NT>::N2;
     constexpr int upc = kTileSlots / 16;
     // [wave][row][slot][position in row], 17 doubles per (row, slot): lane q's 16 reads start
     // 2 banks apart from lane q + 1's instead of all on one bank
@@ -825,11 +851,13 @@ __global__ __launch_bounds__(kBlock, EDT_GRAM_MIN_BLOCKS) void slerp_gram_kernel
         const uint64_t i = a + (uint64_t)j * kTileElems + (uint64_t)lane * kVec;
         if constexpr (decltype(full)::value) {
             if constexpr (EDT_GRAM_PREFETCH) {
-                gram_fma_first<M, kVec>(xin, gs);      // loaded one tile ahead
+                if constexpr (RING) ring_fma<M, kVec>(xin, gs, true);
+                else gram_fma_first<M, kVec>(xin, gs);      // loaded one tile ahead
             } else {
                 Raw8<IDT> x[M];
                 load_tile(k, x);
-                gram_fma_first<M, kVec>(x, gs);
+                if constexpr (RING) ring_fma<M, kVec>(x, gs, true);
+                else gram_fma_first<M, kVec>(x, gs);
             }
         } else {
 #pragma unroll
@@ -838,7 +866,8 @@ __global__ __launch_bounds__(kBlock, EDT_GRAM_MIN_BLOCKS) void slerp_gram_kernel
                 Raw8<IDT> x[M];
 #pragma unroll
                 for (int m = 0; m < M; ++m) x[m] = ld_raw<IDT, false>(mem.p[m], i);
-                gram_fma<M, kVec>(x, gs);
+                if constexpr (RING) ring_fma<M, kVec>(x, gs, false);
+                else gram_fma<M, kVec>(x, gs);
             }
         }
         if (j == 0)
@@ -846,7 +875,8 @@ __global__ __launch_bounds__(kBlock, EDT_GRAM_MIN_BLOCKS) void slerp_gram_kernel
                 Raw1 x[M];
 #pragma unroll
                 for (int m = 0; m < M; ++m) ld<IDT, 1>(mem.p[m], e, x[m].v);
-                gram_fma<M, 1>(x, gs);
+                if constexpr (RING) ring_fma<M, 1>(x, gs, false);
+                else gram_fma<M, 1>(x, gs);
             });
         double r[N2];
         tile_swap_levels<NT>(gs, r);
@@ -901,12 +931,13 @@ __global__ __launch_bounds__(kBlock, EDT_GRAM_MIN_BLOCKS) void slerp_gram_kernel
         rows[unit_slot(u, units) * NT + lane] = (ts2[0][lane] + ts2[1][lane]) + (ts2[2][lane] + ts2[3][lane]);
 }
 
-// host: the Gram sums of D compact members into gram (chunk rows [nchunks][NT], then the row
-// scratch)
+// host: the Gram sums of D compact members into gram (chunk rows [nchunks][NT]); `rows`: the
+// level-4 row scratch (default: right after the chunk rows). ring: the ring layout (D >= 3).
 inline int gram_sums(const Members& mem, int D, int in_dt, const uint64_t* chunk_desc, int64_t nchunks, double* gram,
-                     hipStream_t s) {
-    const int NT = D * (D + 1) / 2;
-    double* rows = gram + (uint64_t)nchunks * NT;
+                     hipStream_t s, bool ring = false, double* rows = nullptr) {
+    if (ring && D < 3) return fail(EDT_ERR_ARG, "ring Gram layout over %d members", D);
+    const int NT = ring ? 2 * D : D * (D + 1) / 2;
+    if (!rows) rows = gram + (uint64_t)nchunks * NT;
     constexpr int upc = kTileSlots / 16;
     const uint64_t units = (uint64_t)nchunks * upc;
     for (uint64_t u0 = 0; u0 < units; u0 += kUnitGridCap) {
@@ -916,15 +947,118 @@ inline int gram_sums(const Members& mem, int D, int in_dt, const uint64_t* chunk
         if (in_dt == EDT_F32) slerp_gram_kernel<EDT_F32, M><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0); \
         else slerp_gram_kernel<EDT_BF16, M><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0);              \
         break;
-    switch (D) {
-        EDT_GM(1) EDT_GM(2) EDT_GM(3) EDT_GM(4) EDT_GM(5) EDT_GM(6) EDT_GM(7) EDT_GM(8)
-        default: return fail(EDT_ERR_ARG, "Gram pass over %d members", D);
+#define EDT_GR(M)                                                                                             \
+    case M:                                                                                                   \
+        if (in_dt == EDT_F32)                                                                                 \
+            slerp_gram_kernel<EDT_F32, M, true><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0);     \
+        else                                                                                                  \
+            slerp_gram_kernel<EDT_BF16, M, true><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0);    \
+        break;
+    if (ring) {
+        switch (D) {
+            EDT_GR(3) EDT_GR(4) EDT_GR(5) EDT_GR(6) EDT_GR(7) EDT_GR(8)
+            default: return fail(EDT_ERR_ARG, "ring Gram pass over %d members", D);
+        }
+    } else {
+        switch (D) {
+            EDT_GM(1) EDT_GM(2) EDT_GM(3) EDT_GM(4) EDT_GM(5) EDT_GM(6) EDT_GM(7) EDT_GM(8)
+            default: return fail(EDT_ERR_ARG, "Gram pass over %d members", D);
+        }
     }
 #undef EDT_GM
+#undef EDT_GR
     int rc = check_launch("slerp_gram_kernel");
     if (rc) return rc;
     }
     return launch_tree_reduce(rows, NT, kGramRows, upc, 1, nchunks, gram, s);
+}
+
+// How edt_slerp_population lays out its Gram sums: the distinct parents split into the connected
+// components of the "needs a dot" graph (an edge per child with two different parents); a
+// component that is a path or a cycle of >= 3 members takes the ring layout with its members
+// listed along it, any other (1-2 members, or a member in >= 3 distinct pairs) the triangle.
+// Every member belongs to one component, so each parent is still read once in the whole pass.
+struct GramPlan {
+    int ncomp = 0;
+    int comp_of[kGramMaxMembers];          // compact member -> component
+    int pos[kGramMaxMembers];              // compact member -> position in its component's list
+    int size[kGramMaxMembers];
+    bool ring[kGramMaxMembers];
+    int list[kGramMaxMembers][kGramMaxMembers];   // component -> members (compact), in layout order
+    uint64_t off[kGramMaxMembers];         // component's chunk rows in gram (doubles)
+    int nt(int k) const { return ring[k] ? 2 * size[k] : size[k] * (size[k] + 1) / 2; }
+    int norm_index(int c) const {
+        const int k = comp_of[c], p = pos[c];
+        return ring[k] ? p : tri_index(p, p, size[k]);
+    }
+    int dot_index(int c1, int c2) const {            // same component
+        const int k = comp_of[c1], M = size[k];
+        int p1 = pos[c1], p2 = pos[c2];
+        if (c1 == c2) return norm_index(c1);
+        if (ring[k]) return M + ((p1 + 1) % M == p2 ? p1 : p2);
+        if (p1 > p2) { const int t = p1; p1 = p2; p2 = t; }
+        return tri_index(p1, p2, M);
+    }
+};
+
+inline void plan_gram(int D, const int* a, const int* b, int npairs, int64_t nchunks, GramPlan& G) {
+    bool adj[kGramMaxMembers][kGramMaxMembers] = {};
+    int deg[kGramMaxMembers] = {};
+    for (int q = 0; q < npairs; ++q)
+        if (a[q] != b[q] && !adj[a[q]][b[q]]) {
+            adj[a[q]][b[q]] = adj[b[q]][a[q]] = true;
+            ++deg[a[q]];
+            ++deg[b[q]];
+        }
+    for (int c = 0; c < D; ++c) G.comp_of[c] = -1;
+    uint64_t off = 0;
+    for (int c0 = 0; c0 < D; ++c0) {
+        if (G.comp_of[c0] >= 0) continue;
+        const int k = G.ncomp++;
+        int members[kGramMaxMembers], n = 0, stack[kGramMaxMembers], top = 0;
+        stack[top++] = c0;
+        G.comp_of[c0] = k;
+        int maxdeg = 0;
+        while (top) {                                 // the component, in compact order below
+            const int c = stack[--top];
+            members[n++] = c;
+            maxdeg = deg[c] > maxdeg ? deg[c] : maxdeg;
+            for (int o = 0; o < D; ++o)
+                if (adj[c][o] && G.comp_of[o] < 0) {
+                    G.comp_of[o] = k;
+                    stack[top++] = o;
+                }
+        }
+        for (int x = 1; x < n; ++x)                   // sort: the triangle keeps compact order
+            for (int y = x; y > 0 && members[y] < members[y - 1]; --y) {
+                const int t = members[y]; members[y] = members[y - 1]; members[y - 1] = t;
+            }
+        G.size[k] = n;
+        G.ring[k] = n >= 3 && maxdeg <= 2;
+        if (G.ring[k]) {                              // walk the path (from an end) or the cycle
+            int start = members[0];
+            for (int x = 0; x < n; ++x)
+                if (deg[members[x]] < 2) { start = members[x]; break; }
+            int prev = -1, cur = start;
+            for (int x = 0; x < n; ++x) {
+                G.list[k][x] = cur;
+                int next = -1;
+                for (int o = 0; o < D && next < 0; ++o)
+                    if (adj[cur][o] && o != prev && G.comp_of[o] == k) {
+                        bool seen = false;
+                        for (int y = 0; y <= x; ++y) seen = seen || G.list[k][y] == o;
+                        if (!seen) next = o;
+                    }
+                prev = cur;
+                cur = next;
+            }
+        } else {
+            for (int x = 0; x < n; ++x) G.list[k][x] = members[x];
+        }
+        for (int x = 0; x < n; ++x) G.pos[G.list[k][x]] = x;
+        G.off[k] = off;
+        off += (uint64_t)nchunks * G.nt(k);
+    }
 }
 
 // The blends of every child in one launch, with pair_population_kernel's placement: the
@@ -1615,15 +1749,31 @@ int edt_slerp_population(const void* const* members, int nmembers, int in_dt, co
                 mem.p[D++] = members[m];
             }
         }
-    int rc = gram_sums(mem, D, in_dt, chunk_desc, nchunks, gram, s);
-    if (rc) return rc;
-    const int M = D, NT = M * (M + 1) / 2;
+    // the Gram sums per component of the pair graph (GramPlan): ring layout where it applies;
+    // the chunk rows of every component first, one shared level-4 row scratch after them (each
+    // component's pass has finished with it before the next one starts: one stream)
+    GramPlan G;
+    int rc = EDT_OK;
+    {
+        std::vector<int> A(npairs), B(npairs);
+        for (int q = 0; q < npairs; ++q) { A[q] = compact[pairs[2 * q]]; B[q] = compact[pairs[2 * q + 1]]; }
+        plan_gram(D, A.data(), B.data(), npairs, nchunks, G);
+    }
+    uint64_t scratch = 0;
+    for (int k = 0; k < G.ncomp; ++k) scratch += (uint64_t)nchunks * G.nt(k);
+    for (int k = 0; k < G.ncomp; ++k) {
+        Members gm;
+        memset(&gm, 0, sizeof(gm));
+        for (int x = 0; x < G.size[k]; ++x) gm.p[x] = mem.p[G.list[k][x]];
+        rc = gram_sums(gm, G.size[k], in_dt, chunk_desc, nchunks, gram + G.off[k], s, G.ring[k], gram + scratch);
+        if (rc) return rc;
+    }
     const unsigned gc = coef_grid(nseg);
     for (int q = 0; q < npairs; ++q) {
         const int i = compact[pairs[2 * q]], j = compact[pairs[2 * q + 1]];
-        const int lo = i < j ? i : j, hi = i < j ? j : i;
-        slerp_gram_coef_kernel<<<gc, kBlock, 0, s>>>(gram, NT, tri_index(i, i, M), tri_index(j, j, M),
-                                                     tri_index(lo, hi, M), seg_first_chunk, nseg, t,
+        const int k = G.comp_of[i];                   // i and j share a component
+        slerp_gram_coef_kernel<<<gc, kBlock, 0, s>>>(gram + G.off[k], G.nt(k), G.norm_index(i), G.norm_index(j),
+                                                     G.dot_index(i, j), seg_first_chunk, nseg, t,
                                                      (float)dot_threshold, (float)eps, coef + 2 * (size_t)nseg * q,
                                                      dot_out ? dot_out + (size_t)nseg * q : nullptr);
         rc = check_launch("slerp_gram_coef_kernel");

@@ -301,14 +301,17 @@ int edt_slerp_blend_segments(const void* v0, const void* v1, int in_dt, void* ou
                              void* stream);
 
 /* SLERP children of a resident population (EDT_RL/edt.py:286-299: every selected pair of one
- * generation, EDT_RL/crossover.py:84-135 per child) in 2 + 2*npairs launches: ONE pass over the
- * nmembers (<= 8) flat member arenas forms every member's squared norm and every pair's dot per
- * chunk (the Gram upper triangle, `gram`: edt_slerp_population_gram_doubles(nmembers, nchunks)
- * doubles of device workspace), then per child the coefficients (from pairs[2q], pairs[2q+1] =
- * member indices, host array) and the blend into outs[q] (host array of device pointers; no
- * output may alias a member). Each child's sums, coefficients and output are bit-identical to
- * edt_slerp_merge on (members[i], members[j]); the stats pass reads each member once instead of
- * two parents per child. coef: [npairs][nseg][2] floats; dot_out (nullable): [npairs][nseg]. */
+ * generation, EDT_RL/crossover.py:84-135 per child): ONE stats pass over the nmembers (<= 8) flat
+ * member arenas forms every parent's squared norm and the dots the children need per chunk, then
+ * per child the coefficients (from pairs[2q], pairs[2q+1] = member indices, host array) and the
+ * blend into outs[q] (host array of device pointers; no output may alias a member). The stats pass
+ * runs per connected component of the children's pair graph: a path or cycle of >= 3 parents (a
+ * ring of children, a matching) forms its 2M norms and ring dots, any other component the Gram
+ * upper triangle (r4); each parent is read once either way. `gram`:
+ * edt_slerp_population_gram_doubles(nmembers, nchunks) doubles of device workspace (layout
+ * internal to this call; edt_slerp_gram below keeps the triangle layout). Each child's sums,
+ * coefficients and output are bit-identical to edt_slerp_merge on (members[i], members[j]).
+ * coef: [npairs][nseg][2] floats; dot_out (nullable): [npairs][nseg]. */
 uint64_t edt_slerp_population_gram_doubles(int nmembers, int64_t nchunks);
 int edt_slerp_population(const void* const* members, int nmembers, int in_dt, const int32_t* pairs, int npairs,
                          void* const* outs, int out_dt, const uint64_t* chunk_desc, int64_t nchunks,

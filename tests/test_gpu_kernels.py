@@ -507,6 +507,53 @@ def test_slerp_population_matches_per_child(dev, ops, in_dt, out_dt, nmem):
             assert torch.equal(dots[q].cpu(), plan.dots[:len(sizes)].cpu()), (spec, q, i, j)
 
 
+def _pair_graphs():
+    import random
+    rnd = random.Random(5)
+    cases = {
+        "ring8": [(c, (c + 1) % 8) for c in range(8)],                       # the bench's ring
+        "matching8": [((3 * c + 1) % 8, (5 * c + 2) % 8) for c in range(8)],  # the probe's pairs
+        "ring5_selfpair": [(c, (c + 1) % 5) for c in range(5)] + [(2, 2)],
+        "path6": [(0, 1), (1, 2), (2, 3), (3, 4), (4, 5), (5, 4)],
+        "two_cycles": [(0, 1), (1, 2), (2, 0), (3, 4), (4, 5), (5, 6), (6, 3)],
+        "star": [(0, 1), (0, 2), (0, 3), (3, 0), (4, 5)],
+        "cycle_plus_pair": [(0, 1), (1, 2), (2, 3), (3, 0), (4, 5), (5, 5), (6, 6)],
+        "triangle": [(0, 1), (1, 2), (2, 0)],
+        "members_unused": [(5, 2), (2, 7), (7, 5)],
+    }
+    for k in range(6):
+        n = rnd.randint(3, 8)
+        cases[f"random{k}"] = [(rnd.randrange(n), rnd.randrange(n)) for _ in range(rnd.randint(1, 10))]
+    return cases
+
+
+@pytest.mark.parametrize("graph", sorted(_pair_graphs()))
+def test_slerp_population_pair_graphs(dev, ops, graph):
+    """edt_slerp_population's stats pass per component of the children's pair graph (r4): paths and
+    cycles of >= 3 parents take the ring layout (norms + ring dots), other components the triangle;
+    every child's outputs and dots stay bit-identical to edt_slerp_merge — rings, matchings, paths,
+    several cycles, a star, self-pairs, repeated pairs, members no child uses, random graphs."""
+    pairs = _pair_graphs()[graph]
+    nmem = max(max(p) for p in pairs) + 1
+    g = torch.Generator().manual_seed(len(graph) * 7 + nmem)
+    sizes = [0, 1, 7, 33, 4096, 70_001, 0, 129, 200_003]
+    offs = [0]
+    for x in sizes:
+        offs.append(offs[-1] + x)
+    base = torch.randn(offs[-1], generator=g) * 0.02
+    mem = [(base + torch.randn(offs[-1], generator=g) * (1e-5 if m % 2 else 1e-3)).to(torch.bfloat16).to(dev)
+           for m in range(nmem)]
+    ts = torch.tensor([0.5, 0.0, 1.0, 0.43333333333333335, 0.5, 0.7, 0.5, 0.2, 0.9], dtype=torch.float64).to(dev)
+    plan = ops.make_slerp_plan(offs, dev, chunk_elems=4096)
+    outs = [torch.full((offs[-1],), float("nan"), dtype=torch.bfloat16, device=dev) for _ in pairs]
+    dots = ops.slerp_population(plan, mem, pairs, outs, ts, speculate=False).clone()
+    for q, (i, j) in enumerate(pairs):
+        want = torch.empty(offs[-1], dtype=torch.bfloat16, device=dev)
+        ops.slerp_arena(plan, mem[i], mem[j], want, ts, speculate=False)
+        assert torch.equal(bits(outs[q].cpu()), bits(want.cpu())), (graph, q, i, j)
+        assert torch.equal(dots[q].cpu(), plan.dots[:len(sizes)].cpu()), (graph, q, i, j)
+
+
 @pytest.mark.parametrize("gdt,wdt", REGIMES)
 @pytest.mark.parametrize("n", [1, 8191, 70_001, 1_000_003])
 def test_pair_merge_population_matches_per_child(dev, ops, gdt, wdt, n):
