@@ -793,6 +793,36 @@ __device__ __forceinline__ void ring_fma(const X (&x)[M], double (&g)[2 * M], bo
     }
 }
 
+// The speculative ring form (edt_slerp_population_speculative when the children are edges of one
+// ring of parents, at most one child per edge): the ring pass also writes child c's lerp-branch
+// output (1 - t) v0 + t v1 (pair_tile's math: two rounded fp32 products, one rounded sum) from the
+// members' registers — edge c joins ring members c and c + 1 mod M, `flip` bit c: v0 is member
+// c + 1. One read of every parent, one write of every child, 2M sums per element.
+struct RingEmit {
+    void* out[kGramMaxMembers];              // the child on edge c (use bit c set)
+    const double* t;                         // per segment
+    uint32_t use, flip;
+    int32_t* zero_word;                      // the any-redo word, zeroed by block 0 of the first launch
+};
+
+template <int ODT, int N, typename X>
+__device__ __forceinline__ void ring_emit_one(const X& v0, const X& v1, void* out, uint64_t i, float l0, float l1) {
+    float o[N];
+#pragma unroll
+    for (int e = 0; e < N; ++e) o[e] = l0 * v0[e] + l1 * v1[e];
+    st<ODT, N>(out, i, o);
+}
+
+template <int M, int ODT, int N, typename X>
+__device__ __forceinline__ void ring_emit(const X (&x)[M], const RingEmit& E, uint64_t i, float l0, float l1) {
+#pragma unroll
+    for (int c = 0; c < M; ++c) {
+        if (!((E.use >> c) & 1u)) continue;              // uniform: scalar branches
+        if ((E.flip >> c) & 1u) ring_emit_one<ODT, N>(x[(c + 1) % M], x[c], E.out[c], i, l0, l1);
+        else ring_emit_one<ODT, N>(x[c], x[(c + 1) % M], E.out[c], i, l0, l1);
+    }
+}
+
 // Gram rows (level 4), one workgroup per unit of 16 tiles in address order: wave w takes tiles
 // 16 g + 4 w .. + 3 one after the other (one vector per member per lane: M loads in flight). Each
 // tile's NT sums go through the xor butterfly in two parts: the swap levels (32, 16) on the VALU,
@@ -805,11 +835,14 @@ __device__ __forceinline__ void ring_fma(const X (&x)[M], double (&g)[2 * M], bo
 // (unit_slot). Every sum is bit-identical to pair_slot() on (vi, vj): the same per-lane FMA
 // sequence in element order (an FMA's product is exact, so vi*vj == vj*vi), the same butterfly and
 // tree; the coefficients therefore equal edt_slerp_merge's.
-template <int IDT, int M, bool RING = false>
+template <int IDT, int M, bool RING = false, bool EMIT = false, int ODT = EDT_BF16>
 __global__ __launch_bounds__(kBlock, EDT_GRAM_MIN_BLOCKS) void slerp_gram_kernel(Members mem, const uint64_t* chunks,
                                                                                  int64_t nchunks, double* rows,
-                                                                                 uint64_t u0) {
+                                                                                 uint64_t u0, RingEmit E) {
+    static_assert(!EMIT || RING, "the emitting form is the ring layout's");
     constexpr int NT = GramLayout<M, RING>::NT, N2 = Red<NT>::N2;
+    if constexpr (EMIT)
+        if (E.zero_word && u0 == 0 && blockIdx.x == 0 && threadIdx.x == 0) *E.zero_word = 0;
     constexpr int upc = kTileSlots / 16;
     // [wave][row][slot][position in row], 17 doubles per (row, slot): lane q's 16 reads start
     // 2 banks apart from lane q + 1's instead of all on one bank
@@ -824,6 +857,12 @@ __global__ __launch_bounds__(kBlock, EDT_GRAM_MIN_BLOCKS) void slerp_gram_kernel
     const int g = (int)(u % upc);
     // the chunk bounds are uniform: in scalar registers, so the full-tile test below is a scalar branch
     const uint64_t start = uniform_u64(chunks[3 * c]), len = uniform_u64(chunks[3 * c + 1]);
+    float l0 = 0.f, l1 = 0.f;                          // the lerp-branch weights of the unit's segment
+    if constexpr (EMIT) {
+        const double tv = E.t[chunks[3 * c + 2]];
+        l0 = (float)(1.0 - tv);
+        l1 = (float)tv;
+    }
     // lane q (< NT) reads value q's partials: the row and slot that hold it after the swap levels
     int pos = 0;
 #pragma unroll
@@ -853,11 +892,13 @@ __global__ __launch_bounds__(kBlock, EDT_GRAM_MIN_BLOCKS) void slerp_gram_kernel
             if constexpr (EDT_GRAM_PREFETCH) {
                 if constexpr (RING) ring_fma<M, kVec>(xin, gs, true);
                 else gram_fma_first<M, kVec>(xin, gs);      // loaded one tile ahead
+                if constexpr (EMIT) ring_emit<M, ODT, kVec>(xin, E, i, l0, l1);
             } else {
                 Raw8<IDT> x[M];
                 load_tile(k, x);
                 if constexpr (RING) ring_fma<M, kVec>(x, gs, true);
                 else gram_fma_first<M, kVec>(x, gs);
+                if constexpr (EMIT) ring_emit<M, ODT, kVec>(x, E, i, l0, l1);
             }
         } else {
 #pragma unroll
@@ -868,6 +909,7 @@ __global__ __launch_bounds__(kBlock, EDT_GRAM_MIN_BLOCKS) void slerp_gram_kernel
                 for (int m = 0; m < M; ++m) x[m] = ld_raw<IDT, false>(mem.p[m], i);
                 if constexpr (RING) ring_fma<M, kVec>(x, gs, false);
                 else gram_fma<M, kVec>(x, gs);
+                if constexpr (EMIT) ring_emit<M, ODT, kVec>(x, E, i, l0, l1);
             }
         }
         if (j == 0)
@@ -877,6 +919,7 @@ __global__ __launch_bounds__(kBlock, EDT_GRAM_MIN_BLOCKS) void slerp_gram_kernel
                 for (int m = 0; m < M; ++m) ld<IDT, 1>(mem.p[m], e, x[m].v);
                 if constexpr (RING) ring_fma<M, 1>(x, gs, false);
                 else gram_fma<M, 1>(x, gs);
+                if constexpr (EMIT) ring_emit<M, ODT, 1>(x, E, e, l0, l1);
             });
         double r[N2];
         tile_swap_levels<NT>(gs, r);
@@ -938,21 +981,23 @@ inline int gram_sums(const Members& mem, int D, int in_dt, const uint64_t* chunk
     if (ring && D < 3) return fail(EDT_ERR_ARG, "ring Gram layout over %d members", D);
     const int NT = ring ? 2 * D : D * (D + 1) / 2;
     if (!rows) rows = gram + (uint64_t)nchunks * NT;
+    RingEmit E0;
+    memset(&E0, 0, sizeof(E0));
     constexpr int upc = kTileSlots / 16;
     const uint64_t units = (uint64_t)nchunks * upc;
     for (uint64_t u0 = 0; u0 < units; u0 += kUnitGridCap) {
     const unsigned g = unit_grid(units - u0);
 #define EDT_GM(M)                                                                                                   \
     case M:                                                                                                         \
-        if (in_dt == EDT_F32) slerp_gram_kernel<EDT_F32, M><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0); \
-        else slerp_gram_kernel<EDT_BF16, M><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0);              \
+        if (in_dt == EDT_F32) slerp_gram_kernel<EDT_F32, M><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0, E0); \
+        else slerp_gram_kernel<EDT_BF16, M><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0, E0);              \
         break;
 #define EDT_GR(M)                                                                                             \
     case M:                                                                                                   \
         if (in_dt == EDT_F32)                                                                                 \
-            slerp_gram_kernel<EDT_F32, M, true><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0);     \
+            slerp_gram_kernel<EDT_F32, M, true><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0, E0); \
         else                                                                                                  \
-            slerp_gram_kernel<EDT_BF16, M, true><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0);    \
+            slerp_gram_kernel<EDT_BF16, M, true><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0, E0); \
         break;
     if (ring) {
         switch (D) {
@@ -971,6 +1016,38 @@ inline int gram_sums(const Members& mem, int D, int in_dt, const uint64_t* chunk
     if (rc) return rc;
     }
     return launch_tree_reduce(rows, NT, kGramRows, upc, 1, nchunks, gram, s);
+}
+
+// host: the speculative ring pass — ring sums of the D members (ring order) into sums
+// ([nchunks][2D], rows scratch after them) and every child's lerp-branch output (E).
+inline int ring_spec_sums(const Members& mem, int D, int in_dt, int out_dt, const RingEmit& E,
+                          const uint64_t* chunk_desc, int64_t nchunks, double* sums, hipStream_t s) {
+    const int NT = 2 * D;
+    double* rows = sums + (uint64_t)nchunks * NT;
+    constexpr int upc = kTileSlots / 16;
+    const uint64_t units = (uint64_t)nchunks * upc;
+    for (uint64_t u0 = 0; u0 < units; u0 += kUnitGridCap) {
+        const unsigned g = unit_grid(units - u0);
+#define EDT_GE(M)                                                                                                  \
+    case M:                                                                                                        \
+        if (in_dt == EDT_F32 && out_dt == EDT_F32)                                                                 \
+            slerp_gram_kernel<EDT_F32, M, true, true, EDT_F32><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0, E);   \
+        else if (in_dt == EDT_F32)                                                                                 \
+            slerp_gram_kernel<EDT_F32, M, true, true, EDT_BF16><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0, E);  \
+        else if (out_dt == EDT_F32)                                                                                \
+            slerp_gram_kernel<EDT_BF16, M, true, true, EDT_F32><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0, E);  \
+        else                                                                                                       \
+            slerp_gram_kernel<EDT_BF16, M, true, true, EDT_BF16><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0, E); \
+        break;
+        switch (D) {
+            EDT_GE(3) EDT_GE(4) EDT_GE(5) EDT_GE(6) EDT_GE(7) EDT_GE(8)
+            default: return fail(EDT_ERR_ARG, "speculative ring pass over %d members", D);
+        }
+#undef EDT_GE
+        int rc = check_launch("slerp_gram_kernel (speculative ring)");
+        if (rc) return rc;
+    }
+    return launch_tree_reduce(rows, NT, kGramRows, upc, 1, nchunks, sums, s);
 }
 
 // How edt_slerp_population lays out its Gram sums: the distinct parents split into the connected
@@ -1166,7 +1243,8 @@ __global__ __launch_bounds__(kBlock) void slerp_pop_stats_lerp_kernel(BlendChild
 __global__ __launch_bounds__(kBlock) void slerp_gram_coef_kernel(const double* gram, int NT, int qi, int qj, int qd,
                                                                  const int32_t* first, int nseg,
                                                                  const double* tvals, float thr, float eps,
-                                                                 float* coef, float* dot_out, int32_t* redo = nullptr) {
+                                                                 float* coef, float* dot_out, int32_t* redo = nullptr,
+                                                                 int32_t* any_redo = nullptr) {
     const int seg = coef_segment();
     if (seg >= nseg) return;
     double sums[3];
@@ -1176,7 +1254,11 @@ __global__ __launch_bounds__(kBlock) void slerp_gram_coef_kernel(const double* g
     coef[2 * seg] = c0;
     coef[2 * seg + 1] = c1;
     if (dot_out) dot_out[seg] = dot;
-    if (redo) redo[seg] = fabsf(dot) > thr ? 0 : 1;   // as slerp_coef_kernel
+    if (redo) {                                       // as slerp_coef_kernel
+        const int32_t r = fabsf(dot) > thr ? 0 : 1;
+        redo[seg] = r;
+        if (r && any_redo) *any_redo = 1;
+    }
 }
 
 // The blends of every child in member-major form (the two-pass Gram form's second pass and the
@@ -1189,6 +1271,7 @@ struct PopBlend {
     const int32_t* redo[kBlendMaxChildren];   // [nseg] of the child, or null: blend every segment
     int32_t a[kBlendMaxChildren], b[kBlendMaxChildren];
     int n;
+    const int32_t* any;                       // nullable: the any-redo word (clear: nothing to blend)
 };
 
 template <int IDT, int ODT, int M, int N>
@@ -1212,6 +1295,7 @@ __device__ __forceinline__ void blend_mm_elems(const Members& mem, const PopBlen
 template <int IDT, int ODT, int M>
 __global__ __launch_bounds__(kBlock) void slerp_blend_mm_kernel(Members mem, PopBlend pb, const uint64_t* chunks,
                                                                 int64_t nchunks) {
+    if (pb.any && *pb.any == 0) return;      // no child needs a SLERP-branch segment
     for_blend_ranges(chunks, nchunks, [&](uint64_t start, uint64_t end, uint64_t seg) {
         uint32_t need = 0;                   // children whose output this segment still needs
         for (int q = 0; q < pb.n; ++q)
@@ -1972,6 +2056,74 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
     // the any-redo word (the workspace's last double): zeroed by the first pass, set by any child's
     // coefficient kernel that sends a segment to the SLERP branch; clear, the redo grid exits at once
     int32_t* any = reinterpret_cast<int32_t*>(partial + edt_slerp_population_speculative_doubles(npairs, nchunks) - 1);
+    // member-major ring form (r4): the distinct parents form ONE path or cycle of >= 3 and every
+    // child is one of its edges (at most one child per edge) — a ring of children. One pass reads
+    // every parent once, forms the 2D ring sums and writes every child's lerp-branch output; then
+    // the children's coefficients from those sums and the member-major redo blend.
+    {
+        std::vector<int> compact(nmembers, -1), A(npairs), B(npairs);
+        const void* dm[kGramMaxMembers];
+        int D = 0;
+        bool fits = npairs <= kGramMaxMembers;          // at most one child per ring edge
+        for (int q = 0; q < npairs && fits; ++q)
+            for (int e = 0; e < 2 && fits; ++e) {
+                const int m = pairs[2 * q + e];
+                if (compact[m] < 0) {
+                    if (D == kGramMaxMembers) { fits = false; break; }
+                    compact[m] = D;
+                    dm[D++] = members[m];
+                }
+                (e ? B : A)[q] = compact[m];
+            }
+        GramPlan G;
+        if (fits && D >= 3) plan_gram(D, A.data(), B.data(), npairs, nchunks, G);
+        if (fits && D >= 3 && G.ncomp == 1 && G.ring[0]) {
+            RingEmit E;
+            memset(&E, 0, sizeof(E));
+            uint32_t used = 0;
+            bool ring = true;
+            for (int q = 0; q < npairs && ring; ++q) {
+                const int pi = G.pos[A[q]], pj = G.pos[B[q]];
+                int e = -1;
+                bool flip = false;
+                if ((pi + 1) % D == pj) e = pi;
+                else if ((pj + 1) % D == pi) { e = pj; flip = true; }
+                if (e < 0 || ((used >> e) & 1u)) { ring = false; break; }
+                used |= 1u << e;
+                E.out[e] = outs[q];
+                if (flip) E.flip |= 1u << e;
+            }
+            if (ring) {
+                Members gm;
+                memset(&gm, 0, sizeof(gm));
+                for (int x = 0; x < D; ++x) gm.p[x] = dm[G.list[0][x]];
+                E.t = t;
+                E.use = used;
+                E.zero_word = any;
+                int rc = ring_spec_sums(gm, D, in_dt, out_dt, E, chunk_desc, nchunks, partial, s);
+                if (rc) return rc;
+                PopBlend pb;
+                memset(&pb, 0, sizeof(pb));
+                pb.n = npairs;
+                pb.any = any;
+                for (int q = 0; q < npairs; ++q) {
+                    float* cq = coef + 2 * (size_t)nseg * q;
+                    slerp_gram_coef_kernel<<<coef_grid(nseg), kBlock, 0, s>>>(
+                        partial, 2 * D, G.norm_index(A[q]), G.norm_index(B[q]), G.dot_index(A[q], B[q]),
+                        seg_first_chunk, nseg, t, (float)dot_threshold, (float)eps, cq,
+                        dot_out ? dot_out + (size_t)nseg * q : nullptr, redo + (size_t)nseg * q, any);
+                    rc = check_launch("slerp_gram_coef_kernel");
+                    if (rc) return rc;
+                    pb.out[q] = outs[q];
+                    pb.coef[q] = cq;
+                    pb.redo[q] = redo + (size_t)nseg * q;
+                    pb.a[q] = G.pos[A[q]];
+                    pb.b[q] = G.pos[B[q]];
+                }
+                return launch_blend_mm(gm, D, pb, in_dt, out_dt, chunk_desc, nchunks, s);
+            }
+        }
+    }
     for (int pass = 0; pass < 2; ++pass) {
         for (int q0 = 0; q0 < npairs; q0 += kBlendMaxChildren) {
             BlendChildren B;

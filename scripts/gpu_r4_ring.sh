@@ -10,10 +10,15 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_c
 tail -3 $OUT/pytest_pop.log; [ $s -eq 0 ] || exit $s
 (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
     -d $OUT/pop -o pop -- python3 $R/scripts/pop_slerp_probe.py --rounds 3 > $OUT/pop_probe.log 2>&1) || { tail -5 $OUT/pop_probe.log; exit 9; }
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
+    -d $OUT/popring -o pop -- python3 $R/scripts/pop_slerp_probe.py --rounds 3 --pairs ring > $OUT/pop_probe_ring.log 2>&1) || { tail -5 $OUT/pop_probe_ring.log; exit 10; }
+grep -v "^[EW]20" $OUT/pop_probe_ring.log | grep -v amdgpu | head -4
 grep -v "^[EW]20" $OUT/pop_probe.log | grep -v amdgpu | head -4
-python3 - $OUT/pop/pop_kernel_stats.csv <<'PY'
+python3 - $OUT/pop/pop_kernel_stats.csv $OUT/popring/pop_kernel_stats.csv <<'PY'
 import csv, sys
-for r in csv.DictReader(open(sys.argv[1])):
-    if "slerp" in r["Name"]:
-        print(r["Name"][:70], r["Calls"], round(float(r["AverageNs"]) / 1e6, 3))
+for f in sys.argv[1:]:
+    print(f)
+    for r in csv.DictReader(open(f)):
+        if "slerp" in r["Name"]:
+            print(" ", r["Name"][:80], r["Calls"], round(float(r["AverageNs"]) / 1e6, 3))
 PY

@@ -33,6 +33,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--variants", default="", help="also run every lib*.so in DIR (build_slerp_variants.py)")
+    ap.add_argument("--pairs", default="probe", choices=("probe", "ring"),
+                    help="probe: ((3c+1) % 8, (5c+2) % 8), a matching with every pair twice; ring: (c, c+1 % 8), "
+                         "the bench's ring of children")
     a = ap.parse_args()
     from evolutionarydistributedtraining_amd import _lib as L
     from evolutionarydistributedtraining_amd import ops
@@ -45,7 +48,8 @@ def main():
     outs = [torch.empty(P, dtype=BF, device=dev) for _ in range(N)]
     t = torch.rand(len(lay), dtype=torch.float64, generator=torch.Generator().manual_seed(4)).to(dev)
     plan = ops.make_slerp_plan(lay.offsets, dev)
-    pairs = [((3 * c + 1) % N, (5 * c + 2) % N) for c in range(N)]
+    pairs = ([((3 * c + 1) % N, (5 * c + 2) % N) for c in range(N)] if a.pairs == "probe"
+             else [(c, (c + 1) % N) for c in range(N)])
     s = torch.cuda.current_stream(dev)
     res, sigs = {}, {}
 
@@ -101,7 +105,7 @@ def main():
     for m in members:
         fill(m, gen, 0.02)                             # independent members: the SLERP branch
     forms("independent")
-    print(json.dumps({"probe": "pop_slerp", "elements_per_member": P, "results": res}))
+    print(json.dumps({"probe": "pop_slerp", "pairs": a.pairs, "elements_per_member": P, "results": res}))
 
 
 if __name__ == "__main__":

@@ -519,6 +519,9 @@ def _pair_graphs():
         "star": [(0, 1), (0, 2), (0, 3), (3, 0), (4, 5)],
         "cycle_plus_pair": [(0, 1), (1, 2), (2, 3), (3, 0), (4, 5), (5, 5), (6, 6)],
         "triangle": [(0, 1), (1, 2), (2, 0)],
+        "ring8_flipped": [(1, 0), (1, 2), (3, 2), (3, 4), (4, 5), (6, 5), (6, 7), (0, 7)],
+        "path4": [(0, 1), (2, 1), (2, 3)],
+        "ring6_relabelled": [(4, 1), (1, 5), (5, 0), (0, 3), (3, 2), (2, 4)],
         "members_unused": [(5, 2), (2, 7), (7, 5)],
     }
     for k in range(6):
@@ -527,12 +530,16 @@ def _pair_graphs():
     return cases
 
 
+@pytest.mark.parametrize("speculate", [False, True])
 @pytest.mark.parametrize("graph", sorted(_pair_graphs()))
-def test_slerp_population_pair_graphs(dev, ops, graph):
+def test_slerp_population_pair_graphs(dev, ops, graph, speculate):
     """edt_slerp_population's stats pass per component of the children's pair graph (r4): paths and
     cycles of >= 3 parents take the ring layout (norms + ring dots), other components the triangle;
-    every child's outputs and dots stay bit-identical to edt_slerp_merge — rings, matchings, paths,
-    several cycles, a star, self-pairs, repeated pairs, members no child uses, random graphs."""
+    the speculative form takes the member-major ring pass when the children are the edges of one
+    path or cycle (either orientation, one child per edge), else the co-located pass; every child's
+    outputs and dots stay bit-identical to edt_slerp_merge — rings, matchings, paths, several
+    cycles, a star, self-pairs, repeated pairs, members no child uses, random graphs, segments on
+    both sides of the threshold (the redo blend)."""
     pairs = _pair_graphs()[graph]
     nmem = max(max(p) for p in pairs) + 1
     g = torch.Generator().manual_seed(len(graph) * 7 + nmem)
@@ -546,7 +553,7 @@ def test_slerp_population_pair_graphs(dev, ops, graph):
     ts = torch.tensor([0.5, 0.0, 1.0, 0.43333333333333335, 0.5, 0.7, 0.5, 0.2, 0.9], dtype=torch.float64).to(dev)
     plan = ops.make_slerp_plan(offs, dev, chunk_elems=4096)
     outs = [torch.full((offs[-1],), float("nan"), dtype=torch.bfloat16, device=dev) for _ in pairs]
-    dots = ops.slerp_population(plan, mem, pairs, outs, ts, speculate=False).clone()
+    dots = ops.slerp_population(plan, mem, pairs, outs, ts, speculate=speculate).clone()
     for q, (i, j) in enumerate(pairs):
         want = torch.empty(offs[-1], dtype=torch.bfloat16, device=dev)
         ops.slerp_arena(plan, mem[i], mem[j], want, ts, speculate=False)
