@@ -18,20 +18,42 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 CALLS = 4                                      # bench_population_resident: _event_ms(fn, 3, 1) per form
 FORMS = {   # the kernels each form launches (tree_reduce / coef: both forms, a few MB: left out)
-    "speculative": ("slerp_pop_stats_lerp_kernel", "slerp_blend_population_kernel"),
+    "speculative": ("slerp_pop_stats_lerp_kernel", "slerp_blend_population_kernel",
+                    "slerp_gram_kernel (emitting ring)", "slerp_blend_mm_kernel (redo)"),
     "two_pass": ("slerp_gram_kernel", "slerp_blend_mm_kernel"),
 }
 
 
+def _form_starter(name):
+    """The form a call starts with this kernel (dispatch order): the speculative forms begin with the
+    co-located pass or the emitting ring pass (r4: slerp_gram_kernel<IDT, M, true, true, ODT>), the
+    two-pass form with a non-emitting Gram / ring pass; every later launch (blends, coefficients)
+    belongs to the call its starter opened — slerp_blend_mm_kernel serves both forms."""
+    if name.startswith("slerp_pop_stats_lerp_kernel"):
+        return "speculative"
+    if name.startswith("slerp_gram_kernel<"):
+        args = [a.strip() for a in name[len("slerp_gram_kernel<"):].split(">")[0].split(",")]
+        return "speculative" if len(args) >= 4 and args[3] == "true" else "two_pass"
+    return None
+
+
 def totals(root, counter):
-    out = {}
+    """{form: summed counter} over the slerp kernels, attributed by dispatch order."""
+    rows = []
     for path in glob.glob(os.path.join(root, counter, "**", "*counter_collection.csv"), recursive=True):
         with open(path) as f:
             for row in csv.DictReader(f):
                 if row.get("Counter_Name") != counter:
                     continue
-                name = row["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("<")[0]
-                out[name] = out.get(name, 0.0) + float(row["Counter_Value"])
+                name = row["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "")
+                if "slerp" in name:
+                    rows.append((int(row.get("Dispatch_Id") or 0), name, float(row["Counter_Value"])))
+    out, form = {}, None
+    for _, name, v in sorted(rows):
+        form = _form_starter(name) or form
+        if form and (name.startswith("slerp_gram_kernel") or name.startswith("slerp_blend")
+                     or name.startswith("slerp_pop_stats_lerp_kernel")):
+            out[form] = out.get(form, 0.0) + v
     return out
 
 
@@ -41,8 +63,8 @@ def main():
     f, w = totals(root, "FETCH_SIZE"), totals(root, "WRITE_SIZE")
     res = {}
     for form, kernels in FORMS.items():
-        fetch = sum(2 * 1024 * f.get(k, 0.0) for k in kernels) / CALLS
-        write = sum(1024 * w.get(k, 0.0) for k in kernels) / CALLS
+        fetch = 2 * 1024 * f.get(form, 0.0) / CALLS
+        write = 1024 * w.get(form, 0.0) / CALLS
         res[f"population_7b/{form}"] = {
             "kernels": list(kernels), "calls": CALLS, "fetch_bytes_x2": fetch, "write_bytes": write,
             "hbm_bytes_per_launch": int(round(fetch + write)),
