@@ -1018,12 +1018,12 @@ inline int gram_sums(const Members& mem, int D, int in_dt, const uint64_t* chunk
     return launch_tree_reduce(rows, NT, kGramRows, upc, 1, nchunks, gram, s);
 }
 
-// host: the speculative ring pass — ring sums of the D members (ring order) into sums
-// ([nchunks][2D], rows scratch after them) and every child's lerp-branch output (E).
+// host: the speculative ring pass — ring sums of the D members (ring order; D = 1, 2: the self-pair
+// and the two orientations of one pair) into sums ([nchunks][2D]; `rows`: the level-4 row scratch)
+// and every child's lerp-branch output (E).
 inline int ring_spec_sums(const Members& mem, int D, int in_dt, int out_dt, const RingEmit& E,
-                          const uint64_t* chunk_desc, int64_t nchunks, double* sums, hipStream_t s) {
+                          const uint64_t* chunk_desc, int64_t nchunks, double* sums, double* rows, hipStream_t s) {
     const int NT = 2 * D;
-    double* rows = sums + (uint64_t)nchunks * NT;
     constexpr int upc = kTileSlots / 16;
     const uint64_t units = (uint64_t)nchunks * upc;
     for (uint64_t u0 = 0; u0 < units; u0 += kUnitGridCap) {
@@ -1040,7 +1040,7 @@ inline int ring_spec_sums(const Members& mem, int D, int in_dt, int out_dt, cons
             slerp_gram_kernel<EDT_BF16, M, true, true, EDT_BF16><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0, E); \
         break;
         switch (D) {
-            EDT_GE(3) EDT_GE(4) EDT_GE(5) EDT_GE(6) EDT_GE(7) EDT_GE(8)
+            EDT_GE(1) EDT_GE(2) EDT_GE(3) EDT_GE(4) EDT_GE(5) EDT_GE(6) EDT_GE(7) EDT_GE(8)
             default: return fail(EDT_ERR_ARG, "speculative ring pass over %d members", D);
         }
 #undef EDT_GE
@@ -2056,15 +2056,18 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
     // the any-redo word (the workspace's last double): zeroed by the first pass, set by any child's
     // coefficient kernel that sends a segment to the SLERP branch; clear, the redo grid exits at once
     int32_t* any = reinterpret_cast<int32_t*>(partial + edt_slerp_population_speculative_doubles(npairs, nchunks) - 1);
-    // member-major ring form (r4): the distinct parents form ONE path or cycle of >= 3 and every
-    // child is one of its edges (at most one child per edge) — a ring of children. One pass reads
-    // every parent once, forms the 2D ring sums and writes every child's lerp-branch output; then
-    // the children's coefficients from those sums and the member-major redo blend.
+    // member-major ring form (r4): every component of the children's pair graph is a path or a
+    // cycle (1-2 parents, or >= 3 listed along it) and every child is one of its ring edges, at
+    // most one child per edge (a ring of children; a matching: a 2-parent component's two edges
+    // are its two orientations; a self-pair: a 1-parent ring). Per component one pass reads each
+    // of its parents once, forms the 2M ring sums and writes every child's lerp-branch output;
+    // then the children's coefficients from those sums and the member-major redo blends (which
+    // exit at once when no segment of any child needs the SLERP branch).
     {
-        std::vector<int> compact(nmembers, -1), A(npairs), B(npairs);
+        std::vector<int> compact(nmembers, -1), A(npairs), B(npairs), edge(npairs);
         const void* dm[kGramMaxMembers];
         int D = 0;
-        bool fits = npairs <= kGramMaxMembers;          // at most one child per ring edge
+        bool fits = npairs <= kGramMaxMembers;          // <= one child per ring edge, <= 8 edges
         for (int q = 0; q < npairs && fits; ++q)
             for (int e = 0; e < 2 && fits; ++e) {
                 const int m = pairs[2 * q + e];
@@ -2076,52 +2079,68 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
                 (e ? B : A)[q] = compact[m];
             }
         GramPlan G;
-        if (fits && D >= 3) plan_gram(D, A.data(), B.data(), npairs, nchunks, G);
-        if (fits && D >= 3 && G.ncomp == 1 && G.ring[0]) {
-            RingEmit E;
-            memset(&E, 0, sizeof(E));
-            uint32_t used = 0;
-            bool ring = true;
-            for (int q = 0; q < npairs && ring; ++q) {
-                const int pi = G.pos[A[q]], pj = G.pos[B[q]];
+        if (fits) {
+            plan_gram(D, A.data(), B.data(), npairs, nchunks, G);
+            for (int k = 0; k < G.ncomp && fits; ++k) fits = G.size[k] <= 2 || G.ring[k];
+        }
+        RingEmit E[kGramMaxMembers];
+        if (fits) {
+            memset(E, 0, sizeof(E));
+            for (int q = 0; q < npairs && fits; ++q) {
+                const int k = G.comp_of[A[q]], n = G.size[k], pi = G.pos[A[q]], pj = G.pos[B[q]];
                 int e = -1;
                 bool flip = false;
-                if ((pi + 1) % D == pj) e = pi;
-                else if ((pj + 1) % D == pi) { e = pj; flip = true; }
-                if (e < 0 || ((used >> e) & 1u)) { ring = false; break; }
-                used |= 1u << e;
-                E.out[e] = outs[q];
-                if (flip) E.flip |= 1u << e;
+                if ((pi + 1) % n == pj) e = pi;
+                else if ((pj + 1) % n == pi) { e = pj; flip = true; }
+                if (e < 0 || ((E[k].use >> e) & 1u)) { fits = false; break; }
+                E[k].use |= 1u << e;
+                E[k].out[e] = outs[q];
+                if (flip) E[k].flip |= 1u << e;
+                edge[q] = e;
             }
-            if (ring) {
-                Members gm;
-                memset(&gm, 0, sizeof(gm));
-                for (int x = 0; x < D; ++x) gm.p[x] = dm[G.list[0][x]];
-                E.t = t;
-                E.use = used;
-                E.zero_word = any;
-                int rc = ring_spec_sums(gm, D, in_dt, out_dt, E, chunk_desc, nchunks, partial, s);
+        }
+        if (fits) {
+            uint64_t off[kGramMaxMembers], scratch = 0;
+            for (int k = 0; k < G.ncomp; ++k) {
+                off[k] = scratch;
+                scratch += (uint64_t)nchunks * 2 * G.size[k];
+            }
+            Members gm[kGramMaxMembers];
+            for (int k = 0; k < G.ncomp; ++k) {           // the passes first: only the first zeroes `any`
+                memset(&gm[k], 0, sizeof(Members));
+                for (int x = 0; x < G.size[k]; ++x) gm[k].p[x] = dm[G.list[k][x]];
+                E[k].t = t;
+                E[k].zero_word = k == 0 ? any : nullptr;
+                int rc = ring_spec_sums(gm[k], G.size[k], in_dt, out_dt, E[k], chunk_desc, nchunks, partial + off[k],
+                                        partial + scratch, s);
                 if (rc) return rc;
+            }
+            for (int q = 0; q < npairs; ++q) {
+                const int k = G.comp_of[A[q]], n = G.size[k];
+                slerp_gram_coef_kernel<<<coef_grid(nseg), kBlock, 0, s>>>(
+                    partial + off[k], 2 * n, G.pos[A[q]], G.pos[B[q]], n + edge[q], seg_first_chunk, nseg, t,
+                    (float)dot_threshold, (float)eps, coef + 2 * (size_t)nseg * q,
+                    dot_out ? dot_out + (size_t)nseg * q : nullptr, redo + (size_t)nseg * q, any);
+                int rc = check_launch("slerp_gram_coef_kernel");
+                if (rc) return rc;
+            }
+            for (int k = 0; k < G.ncomp; ++k) {
                 PopBlend pb;
                 memset(&pb, 0, sizeof(pb));
-                pb.n = npairs;
                 pb.any = any;
                 for (int q = 0; q < npairs; ++q) {
-                    float* cq = coef + 2 * (size_t)nseg * q;
-                    slerp_gram_coef_kernel<<<coef_grid(nseg), kBlock, 0, s>>>(
-                        partial, 2 * D, G.norm_index(A[q]), G.norm_index(B[q]), G.dot_index(A[q], B[q]),
-                        seg_first_chunk, nseg, t, (float)dot_threshold, (float)eps, cq,
-                        dot_out ? dot_out + (size_t)nseg * q : nullptr, redo + (size_t)nseg * q, any);
-                    rc = check_launch("slerp_gram_coef_kernel");
-                    if (rc) return rc;
-                    pb.out[q] = outs[q];
-                    pb.coef[q] = cq;
-                    pb.redo[q] = redo + (size_t)nseg * q;
-                    pb.a[q] = G.pos[A[q]];
-                    pb.b[q] = G.pos[B[q]];
+                    if (G.comp_of[A[q]] != k) continue;
+                    pb.out[pb.n] = outs[q];
+                    pb.coef[pb.n] = coef + 2 * (size_t)nseg * q;
+                    pb.redo[pb.n] = redo + (size_t)nseg * q;
+                    pb.a[pb.n] = G.pos[A[q]];
+                    pb.b[pb.n] = G.pos[B[q]];
+                    ++pb.n;
                 }
-                return launch_blend_mm(gm, D, pb, in_dt, out_dt, chunk_desc, nchunks, s);
+                int rc = launch_blend_mm(gm[k], G.size[k], pb, in_dt, out_dt, chunk_desc, nchunks, s);
+                if (rc) return rc;
             }
+            return EDT_OK;
         }
     }
     for (int pass = 0; pass < 2; ++pass) {

@@ -522,6 +522,9 @@ def _pair_graphs():
         "ring8_flipped": [(1, 0), (1, 2), (3, 2), (3, 4), (4, 5), (6, 5), (6, 7), (0, 7)],
         "path4": [(0, 1), (2, 1), (2, 3)],
         "ring6_relabelled": [(4, 1), (1, 5), (5, 0), (0, 3), (3, 2), (2, 4)],
+        "matching_selfpair": [(0, 1), (1, 0), (2, 3), (3, 2), (4, 4)],
+        "path_and_pair": [(0, 1), (1, 2), (3, 4), (4, 3)],
+        "single_pair": [(1, 0)],
         "members_unused": [(5, 2), (2, 7), (7, 5)],
     }
     for k in range(6):
