@@ -804,11 +804,15 @@ def slerp_population(plan: SlerpPlan, members: list[torch.Tensor], pairs, outs: 
     """SLERP child q of members[pairs[q][0]], members[pairs[q][1]] into outs[q], for every q
     (EDT_RL/edt.py:286-299 -> EDT_RL/crossover.py:84-135 per child). Two forms, bit-identical to
     slerp_arena per child:
-      speculate=False  edt_slerp_population: ONE Gram stats pass over the (<= 8) members, then
-                       one co-located blend launch for all children;
-      speculate=True   edt_slerp_population_speculative: one co-located pass forms every child's
-                       sums and writes its lerp-branch output, then only SLERP-branch segments
-                       are blended again (parents of one lineage: a single pass);
+      speculate=False  edt_slerp_population: one stats pass per component of the children's
+                       pair graph over the (<= 8) distinct parents (r4: paths and cycles in the
+                       ring layout — each parent's norm and the children's dots only — else the
+                       Gram triangle), then one member-major blend launch for all children;
+      speculate=True   edt_slerp_population_speculative: one pass forms every child's sums and
+                       writes its lerp-branch output (r4: a member-major ring pass per component
+                       when every child is one edge of a path / cycle of parents, e.g. a ring of
+                       children or a matching; else the co-located pass), then only SLERP-branch
+                       segments are blended again (parents of one lineage: a single pass);
       None             speculate when the previous call on this plan had few enough child elements
                        in SLERP-branch segments for the single pass to move fewer bytes
                        (f < D b_in / (D b_in + Q b_out), D distinct parents, Q children).
