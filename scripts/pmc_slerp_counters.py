@@ -5,7 +5,7 @@ is summed over the 8 XCDs: / 8 is the kernel's cycles — lerp's 1.17e8 over its
 the share of wave time parked (SQ_WAIT_ANY) vs issuing, and write combining (64-B write requests
 of all write requests at the memory side).
 
-    python scripts/pmc_slerp_counters.py gpurun_out/<tag>/counters
+    python scripts/pmc_slerp_counters.py gpurun_out/<tag>/counters [pair|pop]
 """
 import csv
 import glob
@@ -14,21 +14,30 @@ import os
 import statistics
 import sys
 
-KERNELS = {"lerp": "lerp_kernel<1, 1, 1, 8>", "speculative": "pair_sums_kernel<1, true, 1>",
-           "stats": "pair_sums_kernel<1, false", "blend": "slerp_blend_tile_kernel<1, 1, true>",
-           "tree_reduce": "tree_reduce_kernel"}
+KERNEL_SETS = {
+    "pair": {"lerp": "lerp_kernel<1, 1, 1, 8>", "speculative": "pair_sums_kernel<1, true, 1>",
+             "stats": "pair_sums_kernel<1, false", "blend": "slerp_blend_tile_kernel<1, 1, true>",
+             "tree_reduce": "tree_reduce_kernel"},
+    # r4: BASELINE configs[4]'s population passes (scripts/pmc_pop_counters.sh)
+    "pop": {"gram": "slerp_gram_kernel<1, 8>", "blend_mm": "slerp_blend_mm_kernel<1, 1, 8>",
+            "pop_speculative": "slerp_pop_stats_lerp_kernel<1, 1>",
+            "ring_stats": "slerp_gram_kernel<1, 8, true, false", "ring_emit": "slerp_gram_kernel<1, 8, true, true",
+            "ring_emit_m2": "slerp_gram_kernel<1, 2, true, true", "triangle_m2": "slerp_gram_kernel<1, 2, false"},
+}
+KERNELS = KERNEL_SETS["pair"]
 CUS = 256
 XCDS = 8
 
 
 def main():
     root = sys.argv[1]
-    vals = {k: {} for k in KERNELS}
+    kernels = KERNEL_SETS[sys.argv[2]] if len(sys.argv) > 2 else KERNELS
+    vals = {k: {} for k in kernels}
     for path in glob.glob(os.path.join(root, "*", "**", "*counter_collection.csv"), recursive=True):
         with open(path) as f:
             for row in csv.DictReader(f):
                 name = row.get("Kernel_Name", "")
-                for k, sub in KERNELS.items():
+                for k, sub in kernels.items():
                     if sub in name:
                         vals[k].setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
     out = {}
@@ -43,6 +52,8 @@ def main():
         if "SQ_WAVE_CYCLES" in med and "SQ_WAIT_ANY" in med:
             rec["wave_time_parked"] = round(med["SQ_WAIT_ANY"] / med["SQ_WAVE_CYCLES"], 3)
             rec["wave_time_issuing"] = round(med.get("SQ_ACTIVE_INST_ANY", 0) / med["SQ_WAVE_CYCLES"], 3)
+        if g and "SQ_ACTIVE_INST_VALU" in med:          # rocprof's VALUBusy: x4 / SIMDs / GUI cycles
+            rec["valu_busy"] = round(med["SQ_ACTIVE_INST_VALU"] * 4 / (CUS * 4) / (g / XCDS), 3)
         if med.get("TCC_EA0_WRREQ_sum"):
             rec["write_requests_64B_share"] = round(med.get("TCC_EA0_WRREQ_64B_sum", 0) / med["TCC_EA0_WRREQ_sum"], 3)
         out[k] = rec
