@@ -21,6 +21,7 @@ VARIANTS = {
     "gramntpf": ["-DEDT_GRAM_NT=1", "-DEDT_GRAM_PREFETCH=1"],
     "gramregs3": ["-DEDT_GRAM_PREFETCH=0"],
     "grampf3": ["-DEDT_GRAM_MIN_BLOCKS=3"],
+    "gramnont": ["-DEDT_GRAM_NT=0"],
 }
 
 
