@@ -564,6 +564,34 @@ def test_slerp_population_pair_graphs(dev, ops, graph, speculate):
         assert torch.equal(dots[q].cpu(), plan.dots[:len(sizes)].cpu()), (graph, q, i, j)
 
 
+@pytest.mark.parametrize("in_dt,out_dt", [(torch.float32, torch.float32), (torch.bfloat16, torch.float32),
+                                          (torch.float32, torch.bfloat16)])
+@pytest.mark.parametrize("graph", ["ring8_flipped", "matching_selfpair", "two_cycles"])
+def test_slerp_population_pair_graphs_dtypes(dev, ops, graph, in_dt, out_dt):
+    """The per-component ring passes (both forms) in the other dtype routes: fp32 members, fp32
+    children — every child bit-identical to edt_slerp_merge."""
+    pairs = _pair_graphs()[graph]
+    nmem = max(max(p) for p in pairs) + 1
+    g = torch.Generator().manual_seed(nmem * 11)
+    sizes = [1, 7, 33, 4096, 70_001, 129, 20_003]
+    offs = [0]
+    for x in sizes:
+        offs.append(offs[-1] + x)
+    base = torch.randn(offs[-1], generator=g) * 0.02
+    mem = [(base + torch.randn(offs[-1], generator=g) * (1e-5 if m % 2 else 1e-3)).to(in_dt).to(dev)
+           for m in range(nmem)]
+    ts = torch.tensor([0.0, 1.0, 0.43333333333333335, 0.5, 0.7, 0.2, 0.9], dtype=torch.float64).to(dev)
+    plan = ops.make_slerp_plan(offs, dev, chunk_elems=4096)
+    for speculate in (False, True):
+        outs = [torch.full((offs[-1],), float("nan"), dtype=out_dt, device=dev) for _ in pairs]
+        dots = ops.slerp_population(plan, mem, pairs, outs, ts, speculate=speculate).clone()
+        for q, (i, j) in enumerate(pairs):
+            want = torch.empty(offs[-1], dtype=out_dt, device=dev)
+            ops.slerp_arena(plan, mem[i], mem[j], want, ts, speculate=False)
+            assert torch.equal(bits(outs[q].cpu()), bits(want.cpu())), (graph, speculate, q)
+            assert torch.equal(dots[q].cpu(), plan.dots[:len(sizes)].cpu()), (graph, speculate, q)
+
+
 @pytest.mark.parametrize("gdt,wdt", REGIMES)
 @pytest.mark.parametrize("n", [1, 8191, 70_001, 1_000_003])
 def test_pair_merge_population_matches_per_child(dev, ops, gdt, wdt, n):
