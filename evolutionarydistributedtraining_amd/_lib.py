@@ -83,6 +83,7 @@ SIGNATURES = [
     ("edt_slerp_population_speculative", _I, [ctypes.POINTER(_P), _I, _I, ctypes.POINTER(ctypes.c_int32), _I,
                                               ctypes.POINTER(_P), _I, _P, ctypes.c_int64, _P, _I, _P, _D, _D, _P,
                                               _P, _P, _P, _U64, _P]),
+    ("edt_slerp_population_layout", _I, [ctypes.POINTER(ctypes.c_int32), _I, _I, _I, ctypes.c_char_p, _I]),
     ("edt_slerp_gram", _I, [ctypes.POINTER(_P), _I, _I, _P, ctypes.c_int64, _P, _P]),
     ("edt_slerp_gram_coef", _I, [_P, _I, ctypes.POINTER(ctypes.c_int32), _I, _P, _I, _P, _D, _D, _P, _P, _P]),
     ("edt_slerp_blend_children", _I, [ctypes.POINTER(_P), _I, _I, ctypes.POINTER(ctypes.c_int32), _I,

@@ -87,6 +87,15 @@ using edt::g_err;
 #ifndef EDT_GRAM_NT             // Gram pass: non-temporal member loads (each member is read once)
 #define EDT_GRAM_NT 1
 #endif
+// Needed-sums pass (r5, edt_slerp.hip): elements converted to fp64 per group before the dot
+// slots' switches (4: two groups per lane vector; 2: four), and the next tile's loads in flight
+// while this tile is summed (two register sets, bf16 members).
+#ifndef EDT_NEED_GROUP
+#define EDT_NEED_GROUP 4
+#endif
+#ifndef EDT_NEED_PREFETCH
+#define EDT_NEED_PREFETCH 0
+#endif
 #ifndef EDT_GRAM_MIN_BLOCKS     // Gram pass: __launch_bounds__ minimum workgroups per CU (waves per SIMD)
 #define EDT_GRAM_MIN_BLOCKS 1
 #endif

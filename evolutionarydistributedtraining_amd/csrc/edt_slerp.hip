@@ -4,6 +4,7 @@
 #include "edt_common.h"
 
 #include <algorithm>
+#include <string>
 #include <vector>
 
 namespace {
@@ -1050,30 +1051,337 @@ inline int ring_spec_sums(const Members& mem, int D, int in_dt, int out_dt, cons
     return launch_tree_reduce(rows, NT, kGramRows, upc, 1, nchunks, sums, s);
 }
 
-// How edt_slerp_population lays out its Gram sums: the distinct parents split into the connected
-// components of the "needs a dot" graph (an edge per child with two different parents); a
-// component that is a path or a cycle of >= 3 members takes the ring layout with its members
-// listed along it, any other (1-2 members, or a member in >= 3 distinct pairs) the triangle.
-// Every member belongs to one component, so each parent is still read once in the whole pass.
+// ---- the needed-sums layout (r5): any pair graph --------------------------------------------------
+// A generation needs each distinct parent's norm and each distinct dot its children use — at most
+// D + 8 sums for 8 children, against the triangle's D(D+1)/2 (36 at D = 8). EDT_RL's roulette
+// selection (EDT_RL/edt.py:231-240, 268-269: 8 pairs drawn with replacement) gives graphs with a
+// parent in >= 3 pairs in most generations, so neither the ring (paths / cycles only) nor a fixed
+// layout covers them. Layout of a component of D members (listed in the kernel's order): sums
+// [0, D) = |v_m|^2, [D, D + ne) = the dots in the host's order, dot e joining members
+// (code[e] / 8, code[e] % 8). The members' operands stay in registers indexed at compile time:
+// per half tile each member's 4 elements are converted to fp64 once, the norms' FMAs are
+// unrolled, and each dot slot runs a uniform switch over its (u, v) pair whose arms are the 4
+// FMAs on the members' registers — no runtime-indexed register (r3's member-major pass lost to
+// scratch that way), no extra VALU for the selection (the switch is scalar branches). Same
+// per-lane chains in element order, same butterfly and tree as every other form: each sum is
+// bit-identical to pair_slot() on its two members, so every child's coefficients are
+// edt_slerp_merge's.
+constexpr int kNeedDots = 8;                  // dot slots per component
+constexpr int kNeedMaxOut = 16;               // children per component (emitting form)
+
+template <int D>
+struct NeedLayout {
+    static constexpr int NE = D * (D - 1) / 2 < kNeedDots ? D * (D - 1) / 2 : kNeedDots;
+    static constexpr int NT = D + NE;
+};
+
+inline int need_nt(int D) { return D + (D * (D - 1) / 2 < kNeedDots ? D * (D - 1) / 2 : kNeedDots); }
+inline int need_ne(int D) { return need_nt(D) - D; }
+
+// What one needed-sums pass forms (and, EMIT, writes). Passed by value: every field is uniform.
+struct NeedSpec {
+    int32_t ne;                               // dots in use
+    int32_t code[kNeedDots];                  // dot e: members u * 8 + v (u < v)
+    int32_t nemit;                            // EMIT: distinct ordered parent pairs
+    int32_t ea[kNeedDots], eb[kNeedDots];     // pair e: v0 = member ea[e], v1 = member eb[e]
+    int32_t ofirst[kNeedDots + 1];            // pair e's children: out[ofirst[e] .. ofirst[e + 1])
+    void* out[kNeedMaxOut];
+    const double* t;                          // per segment
+    int32_t* zero_word;                       // the any-redo word, zeroed by block 0 of the first launch
+};
+
+// acc += the dot of members (code / 8, code % 8) over N elements: one switch arm per pair, the
+// operands registers named at compile time (pairs with a member >= D have no arm). Each arm ends
+// with an empty asm statement carrying its own immediate: LLVM cannot merge arms whose last
+// instructions differ in an inline-asm immediate, so it neither sinks the FMAs out of the arms
+// (PHIs of the operands = register copies per FMA) nor turns the switch into an indexed load.
+template <int D, int N>
+__device__ __forceinline__ void need_dot(const double (&d)[D][N], int code, double& acc) {
+#define EDT_ND(U, V)                                                                        \
+    case U * 8 + V:                                                                         \
+        if constexpr (V < D) {                                                              \
+            _Pragma("unroll") for (int j = 0; j < N; ++j) acc = __builtin_fma(d[U][j], d[V][j], acc); \
+            asm volatile("; need dot %1" : "+v"(acc) : "n"(U * 8 + V));                     \
+        }                                                                                   \
+        break;
+    switch (code) {
+        EDT_ND(0, 1) EDT_ND(0, 2) EDT_ND(0, 3) EDT_ND(0, 4) EDT_ND(0, 5) EDT_ND(0, 6) EDT_ND(0, 7)
+        EDT_ND(1, 2) EDT_ND(1, 3) EDT_ND(1, 4) EDT_ND(1, 5) EDT_ND(1, 6) EDT_ND(1, 7)
+        EDT_ND(2, 3) EDT_ND(2, 4) EDT_ND(2, 5) EDT_ND(2, 6) EDT_ND(2, 7)
+        EDT_ND(3, 4) EDT_ND(3, 5) EDT_ND(3, 6) EDT_ND(3, 7)
+        EDT_ND(4, 5) EDT_ND(4, 6) EDT_ND(4, 7)
+        EDT_ND(5, 6) EDT_ND(5, 7)
+        EDT_ND(6, 7)
+        default: break;
+    }
+#undef EDT_ND
+}
+
+// The sums of N elements of every member (the lane's vector: N = 8, in two halves of 4; its
+// head / tail element: N = 1), continuing each chain.
+template <int D, int NE, int N, typename X>
+__device__ __forceinline__ void need_fma(const X (&x)[D], const NeedSpec& S, double (&g)[D + NE]) {
+    constexpr int H = N < EDT_NEED_GROUP ? N : EDT_NEED_GROUP;
+#pragma unroll
+    for (int h = 0; h < N / H; ++h) {
+        double d[D][H];
+#pragma unroll
+        for (int m = 0; m < D; ++m)
+#pragma unroll
+            for (int j = 0; j < H; ++j) d[m][j] = x[m][H * h + j];
+#pragma unroll
+        for (int m = 0; m < D; ++m)
+#pragma unroll
+            for (int j = 0; j < H; ++j) g[m] = __builtin_fma(d[m][j], d[m][j], g[m]);
+#pragma unroll
+        for (int e = 0; e < NE; ++e)
+            if (e < S.ne) need_dot<D, H>(d, S.code[e], g[D + e]);
+    }
+}
+
+// member `idx` of x (uniform): a scalar switch, one copy of the member's registers per arm (the
+// arms' asm immediates keep LLVM from turning the switch into an indexed private array: scratch)
+template <int M>
+__device__ __forceinline__ void need_pin(Raw8<EDT_BF16>& r) { asm volatile("; pick %1" : "+v"(r.w) : "n"(M)); }
+template <int M>
+__device__ __forceinline__ void need_pin(Raw8<EDT_F32>& r) { asm volatile("; pick %2" : "+v"(r.lo), "+v"(r.hi) : "n"(M)); }
+template <int M>
+__device__ __forceinline__ void need_pin(Raw1& r) { asm volatile("; pick %1" : "+v"(r.v[0]) : "n"(M)); }
+
+template <int D, typename X>
+__device__ __forceinline__ X need_pick(const X (&x)[D], int idx) {
+    X r;
+    switch (idx) {
+#define EDT_NP(M) case M: if constexpr (M < D) { r = x[M]; need_pin<M>(r); } break;
+        EDT_NP(0) EDT_NP(1) EDT_NP(2) EDT_NP(3) EDT_NP(4) EDT_NP(5) EDT_NP(6) EDT_NP(7)
+#undef EDT_NP
+        default: r = x[0]; break;
+    }
+    return r;
+}
+
+// EMIT: each distinct ordered pair's lerp-branch output l0 v0 + l1 v1 (pair_tile's math: two
+// rounded fp32 products, one rounded sum), stored to every child of that pair
+template <int ODT, int D, int N, typename X>
+__device__ __forceinline__ void need_emit(const X (&x)[D], const NeedSpec& S, uint64_t i, float l0, float l1) {
+#pragma unroll
+    for (int e = 0; e < kNeedDots; ++e) {
+        if (e >= S.nemit) break;
+        const X a = need_pick<D>(x, S.ea[e]), b = need_pick<D>(x, S.eb[e]);
+        float o[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) o[j] = l0 * a[j] + l1 * b[j];
+        for (int k = S.ofirst[e]; k < S.ofirst[e + 1]; ++k) st<ODT, N>(S.out[k], i, o);
+    }
+}
+
+// The needed sums as rows of level 4, one workgroup per unit of 16 tiles in address order (the
+// Gram kernel's grid, reduction and row format; tiles past the chunk's aligned body load zeros,
+// which leave every chain's bits unchanged). bf16 members: the next tile's loads in flight while
+// this tile is summed (two register sets).
+template <int IDT, int D, bool EMIT = false, int ODT = EDT_BF16>
+__global__ __launch_bounds__(kBlock, EDT_GRAM_MIN_BLOCKS) void slerp_need_kernel(Members mem, NeedSpec S,
+                                                                                 const uint64_t* chunks,
+                                                                                 int64_t nchunks, double* rows,
+                                                                                 uint64_t u0) {
+    constexpr int NE = NeedLayout<D>::NE, NT = NeedLayout<D>::NT, N2 = Red<NT>::N2;
+    constexpr bool kPrefetch = EDT_NEED_PREFETCH != 0 && IDT == EDT_BF16;
+    if constexpr (EMIT)
+        if (S.zero_word && u0 == 0 && blockIdx.x == 0 && threadIdx.x == 0) *S.zero_word = 0;
+    constexpr int upc = kTileSlots / 16;
+    constexpr int kPad = 17;
+    __shared__ double part[kWavesPerBlock][4 * N2 * kPad];
+    __shared__ double ts2[kWavesPerBlock][NT];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint64_t units = (uint64_t)nchunks * upc;
+    const uint64_t u = u0 + blockIdx.x;
+    if (u >= units) return;
+    const uint64_t c = u / upc;
+    const int g = (int)(u % upc);
+    const uint64_t start = uniform_u64(chunks[3 * c]), len = uniform_u64(chunks[3 * c + 1]);
+    float l0 = 0.f, l1 = 0.f;
+    if constexpr (EMIT) {
+        const double tv = S.t[chunks[3 * c + 2]];
+        l0 = (float)(1.0 - tv);
+        l1 = (float)tv;
+    }
+    int pos = 0;
+#pragma unroll
+    for (int row = 0; row < 4; ++row)
+#pragma unroll
+        for (int sl = 0; sl < N2; ++sl) {
+            bool owner;
+            if (red_index<NT>(sl, row * 16, owner) == lane) pos = row * N2 + sl;
+        }
+    const double* mine = &part[wave][pos * kPad];
+    double* put = &part[wave][(lane >> 4) * N2 * kPad + (lane & 15)];
+    const uint64_t a = (start + kVec - 1) / kVec * kVec, b = (start + len) / kVec * kVec;
+    double n01 = 0.0, n23 = 0.0;
+    // a member's tile: a uniform base (scalar registers, readfirstlane so LLVM cannot fold the lane
+    // offset into a per-member 64-bit address held in vector registers) + the lane's byte offset
+    constexpr uint32_t esz = IDT == EDT_BF16 ? 2 : 4;
+    auto member_base = [&](int m, uint64_t e0) {
+        return reinterpret_cast<const char*>(uniform_u64(reinterpret_cast<uint64_t>(mem.p[m]) + e0 * esz));
+    };
+    auto load_tile = [&](int k, Raw8<IDT> (&x)[D]) {
+        const uint64_t t0 = a + (uint64_t)(16 * g + 4 * wave + k) * kTileElems;     // uniform
+        const uint32_t off = (uint32_t)lane * (kVec * esz);
+        if (t0 + kTileElems <= b) {                    // the whole tile inside the aligned body
+#pragma unroll
+            for (int m = 0; m < D; ++m) x[m] = ld_raw<IDT, EDT_GRAM_NT != 0>(member_base(m, t0) + off, 0);
+        } else {
+#pragma unroll
+            for (int m = 0; m < D; ++m) x[m] = Raw8<IDT>{};
+            if (a < b && t0 + (uint64_t)lane * kVec < b) {
+#pragma unroll
+                for (int m = 0; m < D; ++m) x[m] = ld_raw<IDT, EDT_GRAM_NT != 0>(member_base(m, t0) + off, 0);
+            }
+        }
+    };
+    auto tile = [&](int k, const Raw8<IDT> (&x)[D]) {
+        const int j = 16 * g + 4 * wave + k;
+        const uint64_t i = a + (uint64_t)j * kTileElems + (uint64_t)lane * kVec;
+        double gs[NT];
+#pragma unroll
+        for (int q = 0; q < NT; ++q) gs[q] = 0.0;
+        need_fma<D, NE, kVec>(x, S, gs);
+        if constexpr (EMIT)
+            if (a < b && i < b) need_emit<ODT, D, kVec>(x, S, i, l0, l1);
+        if (j == 0)
+            tile0_edge(start, len, [&](uint64_t e) {
+                Raw1 y[D];
+#pragma unroll
+                for (int m = 0; m < D; ++m) ld<IDT, 1>(member_base(m, start), e - start, y[m].v);
+                need_fma<D, NE, 1>(y, S, gs);
+                if constexpr (EMIT) need_emit<ODT, D, 1>(y, S, e, l0, l1);
+            });
+        double r[N2];
+        tile_swap_levels<NT>(gs, r);
+#pragma unroll
+        for (int sl = 0; sl < N2; ++sl) put[sl * kPad] = r[sl];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double p[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) p[t] = mine[t];
+        const double tsum = row_tree16(p);
+        if (k == 0) n01 = tsum;
+        else if (k == 1) n01 = n01 + tsum;
+        else if (k == 2) n23 = tsum;
+        else n23 = n23 + tsum;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    if constexpr (kPrefetch) {                         // two register sets, two tile bodies in the code
+        Raw8<IDT> x0[D], x1[D];
+        load_tile(0, x0);
+#pragma unroll 1
+        for (int k = 0; k < 4; k += 2) {
+            load_tile(k + 1, x1);
+            __builtin_amdgcn_sched_barrier(0);
+            tile(k, x0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (k + 2 < 4) load_tile(k + 2, x0);
+            __builtin_amdgcn_sched_barrier(0);
+            tile(k + 1, x1);
+        }
+    } else {
+#pragma unroll 1
+        for (int k = 0; k < 4; ++k) {
+            Raw8<IDT> x[D];
+            load_tile(k, x);
+            tile(k, x);
+        }
+    }
+    if (lane < NT) ts2[wave][lane] = n01 + n23;
+    __syncthreads();
+    if (wave == 0 && lane < NT)
+        rows[unit_slot(u, units) * NT + lane] = (ts2[0][lane] + ts2[1][lane]) + (ts2[2][lane] + ts2[3][lane]);
+}
+
+// host: one needed-sums pass over the D members of `mem` (their order is the layout's) into sums
+// ([nchunks][need_nt(D)]; `rows`: the level-4 row scratch, nchunks x 8 x need_nt(D) doubles);
+// emit: also every child's lerp-branch output (S.out, S.t, S.zero_word).
+inline int need_sums(const Members& mem, int D, const NeedSpec& S, int in_dt, int out_dt, bool emit,
+                     const uint64_t* chunk_desc, int64_t nchunks, double* sums, double* rows, hipStream_t s) {
+    if (D < 1 || D > kGramMaxMembers) return fail(EDT_ERR_ARG, "needed-sums pass over %d members", D);
+    if (S.ne < 0 || S.ne > need_ne(D)) return fail(EDT_ERR_ARG, "%d dots over %d members", S.ne, D);
+    constexpr int upc = kTileSlots / 16;
+    const uint64_t units = (uint64_t)nchunks * upc;
+    for (uint64_t u0 = 0; u0 < units; u0 += kUnitGridCap) {
+        const unsigned g = unit_grid(units - u0);
+#define EDT_NK(M)                                                                                          \
+    case M:                                                                                                \
+        if (!emit) {                                                                                       \
+            if (in_dt == EDT_F32) slerp_need_kernel<EDT_F32, M><<<g, kBlock, 0, s>>>(mem, S, chunk_desc, nchunks, rows, u0); \
+            else slerp_need_kernel<EDT_BF16, M><<<g, kBlock, 0, s>>>(mem, S, chunk_desc, nchunks, rows, u0);    \
+        } else if (in_dt == EDT_F32 && out_dt == EDT_F32) {                                                \
+            slerp_need_kernel<EDT_F32, M, true, EDT_F32><<<g, kBlock, 0, s>>>(mem, S, chunk_desc, nchunks, rows, u0); \
+        } else if (in_dt == EDT_F32) {                                                                     \
+            slerp_need_kernel<EDT_F32, M, true, EDT_BF16><<<g, kBlock, 0, s>>>(mem, S, chunk_desc, nchunks, rows, u0); \
+        } else if (out_dt == EDT_F32) {                                                                    \
+            slerp_need_kernel<EDT_BF16, M, true, EDT_F32><<<g, kBlock, 0, s>>>(mem, S, chunk_desc, nchunks, rows, u0); \
+        } else {                                                                                           \
+            slerp_need_kernel<EDT_BF16, M, true, EDT_BF16><<<g, kBlock, 0, s>>>(mem, S, chunk_desc, nchunks, rows, u0); \
+        }                                                                                                  \
+        break;
+        switch (D) {
+            EDT_NK(1) EDT_NK(2) EDT_NK(3) EDT_NK(4) EDT_NK(5) EDT_NK(6) EDT_NK(7) EDT_NK(8)
+            default: break;
+        }
+#undef EDT_NK
+        int rc = check_launch(emit ? "slerp_need_kernel (speculative)" : "slerp_need_kernel");
+        if (rc) return rc;
+    }
+    return launch_tree_reduce(rows, need_nt(D), kGramRows, upc, 1, nchunks, sums, s);
+}
+
+// How edt_slerp_population lays out its sums: the distinct parents split into the connected
+// components of the "needs a dot" graph (an edge per child with two different parents). r5: a
+// component whose distinct dots fit its slots (need_ne: every pair up to 4 members, 8 dots above)
+// takes the NEEDED layout (its norms + its dots in order of first use); any other the triangle
+// (every pair). Every member belongs to one component, so each parent is still read once in the
+// whole pass. (r4's ring layout — paths and cycles only — is the legacy choice kept behind
+// EDT_POP_LAYOUT=ring for the A/B probe.)
+enum { kTri = 0, kRing = 1, kNeed = 2 };
+
+inline int pop_layout_legacy() {
+    static const int v = [] {
+        const char* e = getenv("EDT_POP_LAYOUT");
+        return e && strcmp(e, "ring") == 0 ? 1 : 0;
+    }();
+    return v;
+}
+
 struct GramPlan {
     int ncomp = 0;
     int comp_of[kGramMaxMembers];          // compact member -> component
     int pos[kGramMaxMembers];              // compact member -> position in its component's list
     int size[kGramMaxMembers];
-    bool ring[kGramMaxMembers];
+    int kind[kGramMaxMembers];
     int list[kGramMaxMembers][kGramMaxMembers];   // component -> members (compact), in layout order
+    NeedSpec need[kGramMaxMembers];        // kNeed: the component's dots (ne, code)
     uint64_t off[kGramMaxMembers];         // component's chunk rows in gram (doubles)
-    int nt(int k) const { return ring[k] ? 2 * size[k] : size[k] * (size[k] + 1) / 2; }
+    int nt(int k) const {
+        return kind[k] == kNeed ? need_nt(size[k]) : kind[k] == kRing ? 2 * size[k] : size[k] * (size[k] + 1) / 2;
+    }
     int norm_index(int c) const {
         const int k = comp_of[c], p = pos[c];
-        return ring[k] ? p : tri_index(p, p, size[k]);
+        return kind[k] == kTri ? tri_index(p, p, size[k]) : p;
     }
     int dot_index(int c1, int c2) const {            // same component
         const int k = comp_of[c1], M = size[k];
         int p1 = pos[c1], p2 = pos[c2];
         if (c1 == c2) return norm_index(c1);
-        if (ring[k]) return M + ((p1 + 1) % M == p2 ? p1 : p2);
+        if (kind[k] == kRing) return M + ((p1 + 1) % M == p2 ? p1 : p2);
         if (p1 > p2) { const int t = p1; p1 = p2; p2 = t; }
+        if (kind[k] == kNeed) {
+            for (int e = 0; e < need[k].ne; ++e)
+                if (need[k].code[e] == p1 * 8 + p2) return M + e;
+            return -1;
+        }
         return tri_index(p1, p2, M);
     }
 };
@@ -1087,6 +1395,7 @@ inline void plan_gram(int D, const int* a, const int* b, int npairs, int64_t nch
             ++deg[a[q]];
             ++deg[b[q]];
         }
+    const bool legacy = pop_layout_legacy() != 0;
     for (int c = 0; c < D; ++c) G.comp_of[c] = -1;
     uint64_t off = 0;
     for (int c0 = 0; c0 < D; ++c0) {
@@ -1095,24 +1404,26 @@ inline void plan_gram(int D, const int* a, const int* b, int npairs, int64_t nch
         int members[kGramMaxMembers], n = 0, stack[kGramMaxMembers], top = 0;
         stack[top++] = c0;
         G.comp_of[c0] = k;
-        int maxdeg = 0;
+        int maxdeg = 0, nedge2 = 0;
         while (top) {                                 // the component, in compact order below
             const int c = stack[--top];
             members[n++] = c;
             maxdeg = deg[c] > maxdeg ? deg[c] : maxdeg;
+            nedge2 += deg[c];
             for (int o = 0; o < D; ++o)
                 if (adj[c][o] && G.comp_of[o] < 0) {
                     G.comp_of[o] = k;
                     stack[top++] = o;
                 }
         }
-        for (int x = 1; x < n; ++x)                   // sort: the triangle keeps compact order
+        for (int x = 1; x < n; ++x)                   // sort: compact order
             for (int y = x; y > 0 && members[y] < members[y - 1]; --y) {
                 const int t = members[y]; members[y] = members[y - 1]; members[y - 1] = t;
             }
         G.size[k] = n;
-        G.ring[k] = n >= 3 && maxdeg <= 2;
-        if (G.ring[k]) {                              // walk the path (from an end) or the cycle
+        if (legacy) G.kind[k] = n >= 3 && maxdeg <= 2 ? kRing : kTri;
+        else G.kind[k] = nedge2 / 2 <= need_ne(n) ? kNeed : kTri;
+        if (G.kind[k] == kRing) {                     // walk the path (from an end) or the cycle
             int start = members[0];
             for (int x = 0; x < n; ++x)
                 if (deg[members[x]] < 2) { start = members[x]; break; }
@@ -1136,6 +1447,43 @@ inline void plan_gram(int D, const int* a, const int* b, int npairs, int64_t nch
         G.off[k] = off;
         off += (uint64_t)nchunks * G.nt(k);
     }
+    // the needed components' dots, in the order the children first use them
+    for (int k = 0; k < G.ncomp; ++k) {
+        memset(&G.need[k], 0, sizeof(NeedSpec));
+    }
+    for (int q = 0; q < npairs; ++q) {
+        if (a[q] == b[q]) continue;
+        const int k = G.comp_of[a[q]];
+        if (G.kind[k] != kNeed) continue;
+        int p1 = G.pos[a[q]], p2 = G.pos[b[q]];
+        if (p1 > p2) { const int t = p1; p1 = p2; p2 = t; }
+        NeedSpec& S = G.need[k];
+        bool seen = false;
+        for (int e = 0; e < S.ne; ++e) seen = seen || S.code[e] == p1 * 8 + p2;
+        if (!seen) S.code[S.ne++] = p1 * 8 + p2;
+    }
+}
+
+// The row scratch a plan's passes need after its chunk rows (doubles): the largest component's
+// level-4 rows (one component's pass at a time on one stream).
+inline uint64_t plan_row_scratch(const GramPlan& G, int64_t nchunks) {
+    uint64_t m = 0;
+    for (int k = 0; k < G.ncomp; ++k) {
+        const uint64_t r = (uint64_t)nchunks * kGramRows * G.nt(k);
+        m = r > m ? r : m;
+    }
+    return m;
+}
+
+// One component's stats pass (no outputs), whichever layout it took.
+inline int plan_component_sums(const GramPlan& G, int k, const void* const* dm, int in_dt, const uint64_t* chunk_desc,
+                               int64_t nchunks, double* gram, double* rows, hipStream_t s) {
+    Members gm;
+    memset(&gm, 0, sizeof(gm));
+    for (int x = 0; x < G.size[k]; ++x) gm.p[x] = dm[G.list[k][x]];
+    if (G.kind[k] == kNeed)
+        return need_sums(gm, G.size[k], G.need[k], in_dt, EDT_F32, false, chunk_desc, nchunks, gram + G.off[k], rows, s);
+    return gram_sums(gm, G.size[k], in_dt, chunk_desc, nchunks, gram + G.off[k], s, G.kind[k] == kRing, rows);
 }
 
 // The blends of every child in one launch, with pair_population_kernel's placement: the
@@ -1833,9 +2181,9 @@ int edt_slerp_population(const void* const* members, int nmembers, int in_dt, co
                 mem.p[D++] = members[m];
             }
         }
-    // the Gram sums per component of the pair graph (GramPlan): ring layout where it applies;
-    // the chunk rows of every component first, one shared level-4 row scratch after them (each
-    // component's pass has finished with it before the next one starts: one stream)
+    // the sums per component of the pair graph (GramPlan): the needed layout where it applies
+    // (r5); the chunk rows of every component first, one shared level-4 row scratch after them
+    // (each component's pass has finished with it before the next one starts: one stream)
     GramPlan G;
     int rc = EDT_OK;
     {
@@ -1846,10 +2194,7 @@ int edt_slerp_population(const void* const* members, int nmembers, int in_dt, co
     uint64_t scratch = 0;
     for (int k = 0; k < G.ncomp; ++k) scratch += (uint64_t)nchunks * G.nt(k);
     for (int k = 0; k < G.ncomp; ++k) {
-        Members gm;
-        memset(&gm, 0, sizeof(gm));
-        for (int x = 0; x < G.size[k]; ++x) gm.p[x] = mem.p[G.list[k][x]];
-        rc = gram_sums(gm, G.size[k], in_dt, chunk_desc, nchunks, gram + G.off[k], s, G.ring[k], gram + scratch);
+        rc = plan_component_sums(G, k, mem.p, in_dt, chunk_desc, nchunks, gram, gram + scratch, s);
         if (rc) return rc;
     }
     const unsigned gc = coef_grid(nseg);
@@ -2056,18 +2401,20 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
     // the any-redo word (the workspace's last double): zeroed by the first pass, set by any child's
     // coefficient kernel that sends a segment to the SLERP branch; clear, the redo grid exits at once
     int32_t* any = reinterpret_cast<int32_t*>(partial + edt_slerp_population_speculative_doubles(npairs, nchunks) - 1);
-    // member-major ring form (r4): every component of the children's pair graph is a path or a
-    // cycle (1-2 parents, or >= 3 listed along it) and every child is one of its ring edges, at
-    // most one child per edge (a ring of children; a matching: a 2-parent component's two edges
-    // are its two orientations; a self-pair: a 1-parent ring). Per component one pass reads each
-    // of its parents once, forms the 2M ring sums and writes every child's lerp-branch output;
-    // then the children's coefficients from those sums and the member-major redo blends (which
-    // exit at once when no segment of any child needs the SLERP branch).
+    // member-major form (r5: the needed layout; r4: the ring, EDT_POP_LAYOUT=ring): per component of
+    // the children's pair graph one pass reads each of its parents once, forms the component's
+    // needed sums (its norms + the dots its children use) AND writes every child's lerp-branch
+    // output from the members' registers (each distinct ordered pair computed once, stored to
+    // every child of it); then the children's coefficients from those sums and one member-major
+    // redo blend per component (which exits at once when no segment of any child needs the SLERP
+    // branch). Any pair graph over <= 8 distinct parents whose components fit their dot slots
+    // (every graph of <= 8 children) takes it; others the co-located pass below.
     {
         std::vector<int> compact(nmembers, -1), A(npairs), B(npairs), edge(npairs);
         const void* dm[kGramMaxMembers];
         int D = 0;
-        bool fits = npairs <= kGramMaxMembers;          // <= one child per ring edge, <= 8 edges
+        const bool legacy = pop_layout_legacy() != 0;
+        bool fits = npairs <= kBlendMaxChildren && (!legacy || npairs <= kGramMaxMembers);
         for (int q = 0; q < npairs && fits; ++q)
             for (int e = 0; e < 2 && fits; ++e) {
                 const int m = pairs[2 * q + e];
@@ -2081,10 +2428,19 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
         GramPlan G;
         if (fits) {
             plan_gram(D, A.data(), B.data(), npairs, nchunks, G);
-            for (int k = 0; k < G.ncomp && fits; ++k) fits = G.size[k] <= 2 || G.ring[k];
+            for (int k = 0; k < G.ncomp && fits; ++k)
+                fits = legacy ? (G.size[k] <= 2 || G.kind[k] == kRing) : G.kind[k] == kNeed;
+            if (fits && legacy) {                       // r4: 1-2 parents are rings too (2 D sums)
+                uint64_t off = 0;
+                for (int k = 0; k < G.ncomp; ++k) {
+                    G.kind[k] = kRing;
+                    G.off[k] = off;
+                    off += (uint64_t)nchunks * G.nt(k);
+                }
+            }
         }
         RingEmit E[kGramMaxMembers];
-        if (fits) {
+        if (fits && legacy) {
             memset(E, 0, sizeof(E));
             for (int q = 0; q < npairs && fits; ++q) {
                 const int k = G.comp_of[A[q]], n = G.size[k], pi = G.pos[A[q]], pj = G.pos[B[q]];
@@ -2099,26 +2455,59 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
                 edge[q] = e;
             }
         }
-        if (fits) {
-            uint64_t off[kGramMaxMembers], scratch = 0;
-            for (int k = 0; k < G.ncomp; ++k) {
-                off[k] = scratch;
-                scratch += (uint64_t)nchunks * 2 * G.size[k];
+        if (fits && !legacy) {                          // each component's distinct ordered pairs
+            for (int k = 0; k < G.ncomp && fits; ++k) {
+                NeedSpec& S = G.need[k];
+                int slot_of[kBlendMaxChildren], cnt[kNeedDots] = {};
+                for (int q = 0; q < npairs && fits; ++q) {
+                    if (G.comp_of[A[q]] != k) { slot_of[q] = -1; continue; }
+                    const int pa = G.pos[A[q]], pb = G.pos[B[q]];
+                    int e = 0;
+                    while (e < S.nemit && !(S.ea[e] == pa && S.eb[e] == pb)) ++e;
+                    if (e == S.nemit) {
+                        if (e == kNeedDots) { fits = false; break; }
+                        S.ea[e] = pa;
+                        S.eb[e] = pb;
+                        ++S.nemit;
+                    }
+                    slot_of[q] = e;
+                    ++cnt[e];
+                }
+                if (!fits) break;
+                S.ofirst[0] = 0;
+                for (int e = 0; e < S.nemit; ++e) S.ofirst[e + 1] = S.ofirst[e] + cnt[e];
+                int fill[kNeedDots];
+                for (int e = 0; e < S.nemit; ++e) fill[e] = S.ofirst[e];
+                for (int q = 0; q < npairs; ++q)
+                    if (G.comp_of[A[q]] == k) S.out[fill[slot_of[q]]++] = outs[q];
+                S.t = t;
             }
+        }
+        if (fits) {
+            uint64_t scratch = 0;
+            for (int k = 0; k < G.ncomp; ++k) scratch += (uint64_t)nchunks * G.nt(k);
             Members gm[kGramMaxMembers];
             for (int k = 0; k < G.ncomp; ++k) {           // the passes first: only the first zeroes `any`
                 memset(&gm[k], 0, sizeof(Members));
                 for (int x = 0; x < G.size[k]; ++x) gm[k].p[x] = dm[G.list[k][x]];
-                E[k].t = t;
-                E[k].zero_word = k == 0 ? any : nullptr;
-                int rc = ring_spec_sums(gm[k], G.size[k], in_dt, out_dt, E[k], chunk_desc, nchunks, partial + off[k],
+                int rc;
+                if (legacy) {
+                    E[k].t = t;
+                    E[k].zero_word = k == 0 ? any : nullptr;
+                    rc = ring_spec_sums(gm[k], G.size[k], in_dt, out_dt, E[k], chunk_desc, nchunks, partial + G.off[k],
                                         partial + scratch, s);
+                } else {
+                    G.need[k].zero_word = k == 0 ? any : nullptr;
+                    rc = need_sums(gm[k], G.size[k], G.need[k], in_dt, out_dt, true, chunk_desc, nchunks,
+                                   partial + G.off[k], partial + scratch, s);
+                }
                 if (rc) return rc;
             }
             for (int q = 0; q < npairs; ++q) {
                 const int k = G.comp_of[A[q]], n = G.size[k];
+                const int qd = legacy ? (A[q] == B[q] ? G.pos[A[q]] : n + edge[q]) : G.dot_index(A[q], B[q]);
                 slerp_gram_coef_kernel<<<coef_grid(nseg), kBlock, 0, s>>>(
-                    partial + off[k], 2 * n, G.pos[A[q]], G.pos[B[q]], n + edge[q], seg_first_chunk, nseg, t,
+                    partial + G.off[k], G.nt(k), G.norm_index(A[q]), G.norm_index(B[q]), qd, seg_first_chunk, nseg, t,
                     (float)dot_threshold, (float)eps, coef + 2 * (size_t)nseg * q,
                     dot_out ? dot_out + (size_t)nseg * q : nullptr, redo + (size_t)nseg * q, any);
                 int rc = check_launch("slerp_gram_coef_kernel");
@@ -2189,6 +2578,68 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
             }
         }
     }
+    return EDT_OK;
+}
+
+int edt_slerp_population_layout(const int32_t* pairs, int npairs, int nmembers, int speculate, char* buf,
+                                int buflen) {
+    // the plan edt_slerp_population(_speculative) makes for these pairs, as JSON (host only)
+    g_err[0] = 0;
+    if (!buf || buflen < 2) return fail(EDT_ERR_ARG, "null or short buffer");
+    if (npairs < 0 || nmembers < 1) return fail(EDT_ERR_ARG, "bad count");
+    if (npairs > 0 && !pairs) return fail(EDT_ERR_ARG, "null pairs");
+    std::vector<int> compact(nmembers, -1), orig, A(npairs), B(npairs);
+    for (int q = 0; q < npairs; ++q)
+        for (int e = 0; e < 2; ++e) {
+            const int m = pairs[2 * q + e];
+            if (m < 0 || m >= nmembers) return fail(EDT_ERR_ARG, "pair %d: member out of range", q);
+            if (compact[m] < 0) {
+                compact[m] = (int)orig.size();
+                orig.push_back(m);
+            }
+            (e ? B : A)[q] = compact[m];
+        }
+    const int D = (int)orig.size();
+    std::string js = "{\"distinct_parents\": " + std::to_string(D) + ", \"children\": " + std::to_string(npairs);
+    if (D > kGramMaxMembers) {
+        js += std::string(", \"form\": \"") + (speculate ? "co-located" : "unsupported") + "\", \"components\": []}";
+    } else {
+        GramPlan G;
+        plan_gram(D, A.data(), B.data(), npairs, 1, G);
+        bool mm = npairs <= kBlendMaxChildren;
+        const bool legacy = pop_layout_legacy() != 0;
+        std::string comps;
+        for (int k = 0; k < G.ncomp; ++k) {
+            int nemit = 0, ea[64], eb[64];
+            for (int q = 0; q < npairs; ++q) {
+                if (G.comp_of[A[q]] != k) continue;
+                int e = 0;
+                while (e < nemit && !(ea[e] == A[q] && eb[e] == B[q])) ++e;
+                if (e == nemit && nemit < 64) { ea[nemit] = A[q]; eb[nemit] = B[q]; ++nemit; }
+            }
+            if (legacy) mm = mm && (G.size[k] <= 2 || G.kind[k] == kRing);
+            else mm = mm && G.kind[k] == kNeed && nemit <= kNeedDots;
+            int ndots = 0;
+            for (int q = 0; q < npairs; ++q) {     // distinct unordered dots of the component
+                if (G.comp_of[A[q]] != k || A[q] == B[q]) continue;
+                bool seen = false;
+                for (int r = 0; r < q; ++r)
+                    seen = seen || (G.comp_of[A[r]] == k && ((A[r] == A[q] && B[r] == B[q]) || (A[r] == B[q] && B[r] == A[q])));
+                ndots += !seen;
+            }
+            std::string mem;
+            for (int x = 0; x < G.size[k]; ++x) mem += (x ? ", " : "") + std::to_string(orig[G.list[k][x]]);
+            const char* kind = G.kind[k] == kNeed ? "needed" : G.kind[k] == kRing ? "ring" : "triangle";
+            comps += std::string(k ? ", " : "") + "{\"members\": [" + mem + "], \"dots\": " + std::to_string(ndots) +
+                     ", \"sums\": " + std::to_string(G.nt(k)) + ", \"stats_layout\": \"" + kind +
+                     "\", \"emit_pairs\": " + std::to_string(nemit) + "}";
+        }
+        const char* form = speculate ? (mm ? "member-major" : "co-located") : "two-pass";
+        js += std::string(", \"form\": \"") + form + "\", \"legacy_ring\": " + (legacy ? "true" : "false") +
+              ", \"components\": [" + comps + "]}";
+    }
+    if ((int)js.size() + 1 > buflen) return fail(EDT_ERR_ARG, "buffer of %d bytes too short (%d)", buflen, (int)js.size() + 1);
+    memcpy(buf, js.c_str(), js.size() + 1);
     return EDT_OK;
 }
 

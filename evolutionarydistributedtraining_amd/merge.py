@@ -471,3 +471,19 @@ def uniform_dna_crossover(dna1, dna2):
     assert len(dna1) == len(dna2), "DNA lengths must be the same for uniform crossover."
     from_first = [np.random.rand() > 0.5 for _ in dna1]     # one draw per gene, in gene order
     return [a if f else b for a, b, f in zip(dna1, dna2, from_first)]
+
+
+def rl_t_per_segment(keys, num_layers: int | None = None):
+    """The t of every key under run_slerp_merge's config (EDT_RL/crossover.py:146-164: the
+    self_attn / mlp layer curves, global 0.5) routed as EDT_RL/crossover.py:108-122 routes it
+    (t_for_key); num_layers defaults to 1 + the largest layer index among the keys. Skipped keys
+    (a layer beyond num_layers) get the global t."""
+    if num_layers is None:
+        idx = [int(k.split(".")[1]) for k in keys if "layer" in k]
+        num_layers = 1 + max(idx) if idx else 0
+    param_t = {"self_attn": [0, 0.5, 0.3, 0.7, 1], "mlp": [1, 0.5, 0.7, 0.3, 0]}
+    ts = []
+    for k in keys:
+        v = t_for_key(k, num_layers, param_t, 0.5)
+        ts.append(0.5 if v is None else float(v))
+    return ts

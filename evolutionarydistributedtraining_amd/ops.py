@@ -999,3 +999,18 @@ def slerp_blend_children(members: list[torch.Tensor], pairs, outs: list[torch.Te
                                          L.ptr_array(outs), L.dtype_code(outs[0]), L.ptr(chunks), nchunks,
                                          L.ptr(coef), nseg, L.stream_ptr(members[0].device)),
             "edt_slerp_blend_children")
+
+
+def population_layout(pairs, nmembers: int, speculate: bool = True) -> dict:
+    """How edt_slerp_population(_speculative) lays out a generation for these pairs — the
+    library's own planner (edt_slerp_population_layout, host only): the form ("member-major" /
+    "co-located" speculative, "two-pass"), and per component of the children's pair graph its
+    members, distinct dots, sums per element and stats layout ("needed" / "triangle")."""
+    import json as _json
+    lib = L.load_library()
+    Q = len(pairs)
+    fp = (ctypes.c_int32 * max(1, 2 * Q))(*[int(x) for p in pairs for x in p])
+    buf = ctypes.create_string_buffer(8192)
+    L.check(lib.edt_slerp_population_layout(fp, Q, int(nmembers), int(bool(speculate)), buf, len(buf)),
+            "edt_slerp_population_layout")
+    return _json.loads(buf.value.decode())

@@ -138,3 +138,28 @@ def link_bytes(plan, member_bytes):
         for m, dst in p["send"]:
             out[(src, dst)] = out.get((src, dst), 0) + member_bytes
     return out
+
+
+def roulette_generation_pairs(n_members: int, generations: int, seed: int = 0,
+                              scales=(0.1, 1.0, 2.5), num_pairs: int | None = None):
+    """Pair graphs as the RL master draws them, for benches and tests: per generation, random
+    fitness for `n_members` genomes, then EDT_RL/edt.py:268-269's roulette_wheel_selection of
+    n = len(all_genomes) pairs (distinct parents per pair, sampled with replacement across pairs) at
+    a scale from `scales` (roulette_scale spans 0.1 .. 2.5 over a run), as member indices. Returns
+    [{"source": "roulette", "scale", "seed", "pairs"}]. A private random.Random drives the same
+    draws the master's global `random` makes (the functions above call the module's `random`, so
+    its state is saved and restored around each draw)."""
+    out = []
+    rng = random.Random(seed)
+    k = num_pairs if num_pairs is not None else n_members
+    for g in range(generations):
+        scale = scales[g % len(scales)]
+        genomes = [{"fitness": rng.uniform(0.05, 1.0), "model_path": f"m{m}"} for m in range(n_members)]
+        state = random.getstate()
+        random.seed(rng.getrandbits(64))
+        try:
+            pairs = pair_indices(roulette_wheel_selection(genomes, k, scale), genomes)
+        finally:
+            random.setstate(state)
+        out.append({"source": "roulette", "scale": scale, "seed": seed, "generation": g, "pairs": pairs})
+    return out

@@ -334,6 +334,14 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
                                      double dot_threshold, double eps, double* partial, float* coef,
                                      float* dot_out, int32_t* redo, uint64_t n, void* stream);
 
+/* The plan the two population entries above make for a pair graph, as JSON text into buf (host
+ * only, no device work): distinct parents, the form (speculative: "member-major" or "co-located";
+ * "two-pass"), and per connected component of the children's pair graph its members, distinct
+ * dots, sums per element and stats layout ("needed": the members' norms + the dots the children
+ * use; "triangle": every pair). For benches and logs. */
+int edt_slerp_population_layout(const int32_t* pairs, int npairs, int nmembers, int speculate, char* buf,
+                                int buflen);
+
 /* ---- reference-dot mode (opt-in; EDT_RL/crossover.py:20-31 on the reference host) -------------
  * The default coefficients come from an fp64 dot of the chunk sums (within ~3e-7 of the true
  * cosine). The reference decides its branch from an fp32 dot whose error grows with the tensor

@@ -1,0 +1,63 @@
+"""The population planner (edt_slerp_population_layout, host only: no GPU needed) on the graphs
+EDT_RL's selection draws and on the fallbacks. r5: every component whose distinct dots fit its
+slots takes the needed layout (norms + the children's dots); the speculative form is member-major
+for every graph of <= 8 children over <= 8 distinct parents."""
+import random
+
+import pytest
+
+from evolutionarydistributedtraining_amd import ops
+from evolutionarydistributedtraining_amd.schedule import roulette_generation_pairs
+
+
+def test_roulette_generations_take_the_needed_layout():
+    for g in roulette_generation_pairs(8, 300, seed=17):
+        pairs = g["pairs"]
+        lay = ops.population_layout(pairs, 8, True)
+        assert lay["form"] == "member-major", (pairs, lay)
+        D = len({m for p in pairs for m in p})
+        assert lay["distinct_parents"] == D
+        assert sum(len(c["members"]) for c in lay["components"]) == D
+        dots = {tuple(sorted(p)) for p in pairs if p[0] != p[1]}
+        assert sum(c["dots"] for c in lay["components"]) == len(dots)
+        for c in lay["components"]:
+            assert c["stats_layout"] == "needed"
+            n = len(c["members"])
+            assert c["sums"] == n + min(8, n * (n - 1) // 2)
+        two = ops.population_layout(pairs, 8, False)
+        assert two["form"] == "two-pass" and all(c["stats_layout"] == "needed" for c in two["components"])
+
+
+def test_selection_statistics_that_motivate_it():
+    """DESIGN §9.2's correction: under roulette selection most generations have a parent in >= 3
+    distinct pairs (r4's ring layout covers none of them); all are member-major now."""
+    hub = 0
+    gens = roulette_generation_pairs(8, 2000, seed=3)
+    for g in gens:
+        deg = {}
+        for a, b in {tuple(sorted(p)) for p in g["pairs"]}:
+            deg[a] = deg.get(a, 0) + 1
+            deg[b] = deg.get(b, 0) + 1
+        hub += max(deg.values()) >= 3
+    assert hub / len(gens) > 0.5
+
+
+@pytest.mark.parametrize("pairs,form,layouts", [
+    ([(c, (c + 1) % 8) for c in range(8)], "member-major", ["needed"]),
+    ([(a, b) for a in range(5) for b in range(a + 1, 5)], "co-located", ["triangle"]),
+    ([(m, m + 1) for m in range(8)], "co-located", []),
+    ([(0, 1), (1, 0), (0, 2), (2, 0), (1, 2), (2, 1), (0, 3), (3, 0), (1, 3)], "co-located", ["needed"]),
+    ([(3, 6)] * 8, "member-major", ["needed"]),
+    ([(4, 4), (2, 2)], "member-major", ["needed", "needed"]),
+])
+def test_fallbacks(pairs, form, layouts):
+    n = max(max(p) for p in pairs) + 1
+    lay = ops.population_layout(pairs, n, True)
+    assert lay["form"] == form, lay
+    assert [c["stats_layout"] for c in lay["components"]] == layouts, lay
+
+
+def test_layout_rejects_bad_pairs():
+    from evolutionarydistributedtraining_amd._lib import EdtError
+    with pytest.raises(EdtError):
+        ops.population_layout([(0, 9)], 8)
