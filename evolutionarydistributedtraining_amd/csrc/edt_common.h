@@ -91,10 +91,16 @@ using edt::g_err;
 // slots' switches (4: two groups per lane vector; 2: four), and the next tile's loads in flight
 // while this tile is summed (two register sets, bf16 members).
 #ifndef EDT_NEED_GROUP
-#define EDT_NEED_GROUP 4
+#define EDT_NEED_GROUP 8
 #endif
 #ifndef EDT_NEED_PREFETCH
 #define EDT_NEED_PREFETCH 0
+#endif
+#ifndef EDT_NEED_MIN_WAVES      // needed-sums pass: __launch_bounds__ minimum waves per SIMD
+#define EDT_NEED_MIN_WAVES 1
+#endif
+#ifndef EDT_NEED_GLDS           // needed-sums pass: the next tile staged in LDS by DMA (bf16 members)
+#define EDT_NEED_GLDS 1
 #endif
 #ifndef EDT_GRAM_MIN_BLOCKS     // Gram pass: __launch_bounds__ minimum workgroups per CU (waves per SIMD)
 #define EDT_GRAM_MIN_BLOCKS 1

@@ -168,6 +168,8 @@ struct ListArgs {
     float kdiv;
     float kinv;
     SgdScalars sgd;
+    const uint8_t* tail;        // nullable: bf16 scalar-tail bits, tensor t's from byte tail_off[t]
+    const uint64_t* tail_off;   // T
 };
 
 template <int GDT, int WDT, int KC, int DIV>
@@ -195,6 +197,7 @@ __device__ __forceinline__ void outer_list_chunk(const ListArgs& L, const uint64
     a.acc_in = 0;
     a.acc_store = 0;
     a.sgd = L.sgd;
+    if (L.tail) a.sgd.tail = L.tail + L.tail_off[t];     // the tensor's own bits, indexed locally
     a.w = L.w;
     a.T = L.T;
     a.t = t;
@@ -568,13 +571,15 @@ int edt_outer_step_ws(void* theta_g, int gdt, const void* const* theta_k, int wd
 
 uint64_t edt_outer_list_workspace_bytes(int T, int K) {
     if (T < 0 || K < 1) return 0;
-    return (uint64_t)(4 * (uint64_t)T + 1 + (uint64_t)K * T) * sizeof(uint64_t);
+    return (uint64_t)(5 * (uint64_t)T + 1 + (uint64_t)K * T) * sizeof(uint64_t);
 }
 
-int edt_outer_step_list(void* const* theta_t, int gdt, const void* const* theta_k, int wdt, int K,
-                        void* const* momentum_t, int has_momentum, const uint64_t* numel, int T,
-                        double lr, double momentum_coef, int nesterov, void* workspace,
-                        uint64_t workspace_bytes, void* stream) {
+}   // extern "C"
+
+static int outer_step_list_impl(void* const* theta_t, int gdt, const void* const* theta_k, int wdt, int K,
+                                void* const* momentum_t, int has_momentum, const uint64_t* numel, int T,
+                                double lr, double momentum_coef, int nesterov, const uint8_t* tail,
+                                const uint64_t* tail_off, void* workspace, uint64_t workspace_bytes, void* stream) {
     g_err[0] = 0;
     if (!valid_pair(gdt, wdt)) return fail(EDT_ERR_ARG, "unsupported dtype pair (gdt/wdt)");
     if (K < 1 || K > EDT_MAX_WORKERS)
@@ -588,7 +593,8 @@ int edt_outer_step_list(void* const* theta_t, int gdt, const void* const* theta_
     if (!workspace || workspace_bytes < need)
         return fail(EDT_ERR_ARG, "workspace of %llu bytes needed", (unsigned long long)need);
     if (reinterpret_cast<uintptr_t>(workspace) & 7u) return fail(EDT_ERR_ARG, "workspace must be 8-byte aligned");
-    // table: prefix[T+1] | numel[T] | theta[T] | mom[T] | w[K*T]   (all 8-byte words)
+    if (tail && (gdt != EDT_BF16 || !tail_off)) return fail(EDT_ERR_ARG, "tail bits need a bf16 master and byte offsets");
+    // table: prefix[T+1] | numel[T] | theta[T] | mom[T] | w[K*T] | tail_off[T]   (all 8-byte words)
     thread_local std::vector<uint64_t> h;
     h.assign(need / sizeof(uint64_t), 0);
     uint64_t* prefix = h.data();
@@ -596,6 +602,9 @@ int edt_outer_step_list(void* const* theta_t, int gdt, const void* const* theta_
     uint64_t* pth = nflag + T;
     uint64_t* pmo = pth + T;
     uint64_t* pw = pmo + T;
+    uint64_t* ptail = pw + (uint64_t)K * T;
+    if (tail)
+        for (int t = 0; t < T; ++t) ptail[t] = tail_off[t];
     for (int t = 0; t < T; ++t) {
         const uint64_t n = numel[t];
         if (n >= kVecFlag) return fail(EDT_ERR_ARG, "tensor %d too large", t);
@@ -639,11 +648,33 @@ int edt_outer_step_list(void* const* theta_t, int gdt, const void* const* theta_
     L.kdiv = (float)K;
     L.kinv = 1.0f / (float)K;
     L.sgd = sg;
+    L.tail = tail;
+    L.tail_off = d + 4 * (uint64_t)T + 1 + (uint64_t)K * T;
     const int div_exact = is_pow2(K) ? 0 : 1;
     const unsigned grid = chunks > kMaxBlocks ? (unsigned)kMaxBlocks : (unsigned)chunks;   // grid-stride
     if (gdt == EDT_F32 && wdt == EDT_F32) return launch_list_k<EDT_F32, EDT_F32>(L, div_exact, grid, st);
     if (gdt == EDT_F32) return launch_list_k<EDT_F32, EDT_BF16>(L, div_exact, grid, st);
     return launch_list_k<EDT_BF16, EDT_BF16>(L, div_exact, grid, st);
+}
+
+extern "C" {
+
+int edt_outer_step_list(void* const* theta_t, int gdt, const void* const* theta_k, int wdt, int K,
+                        void* const* momentum_t, int has_momentum, const uint64_t* numel, int T,
+                        double lr, double momentum_coef, int nesterov, void* workspace,
+                        uint64_t workspace_bytes, void* stream) {
+    return outer_step_list_impl(theta_t, gdt, theta_k, wdt, K, momentum_t, has_momentum, numel, T, lr,
+                                momentum_coef, nesterov, nullptr, nullptr, workspace, workspace_bytes, stream);
+}
+
+int edt_outer_step_list_tail(void* const* theta_t, int gdt, const void* const* theta_k, int wdt, int K,
+                             void* const* momentum_t, int has_momentum, const uint64_t* numel, int T,
+                             double lr, double momentum_coef, int nesterov, const uint8_t* tail_bits,
+                             const uint64_t* tail_byte_offset, void* workspace, uint64_t workspace_bytes,
+                             void* stream) {
+    return outer_step_list_impl(theta_t, gdt, theta_k, wdt, K, momentum_t, has_momentum, numel, T, lr,
+                                momentum_coef, nesterov, tail_bits, tail_byte_offset, workspace, workspace_bytes,
+                                stream);
 }
 
 int edt_delta_partial(const void* theta_g, int gdt, const void* const* theta_k, int wdt, int K_local,

@@ -1055,37 +1055,46 @@ inline int ring_spec_sums(const Members& mem, int D, int in_dt, int out_dt, cons
 // A generation needs each distinct parent's norm and each distinct dot its children use — at most
 // D + 8 sums for 8 children, against the triangle's D(D+1)/2 (36 at D = 8). EDT_RL's roulette
 // selection (EDT_RL/edt.py:231-240, 268-269: 8 pairs drawn with replacement) gives graphs with a
-// parent in >= 3 pairs in most generations, so neither the ring (paths / cycles only) nor a fixed
-// layout covers them. Layout of a component of D members (listed in the kernel's order): sums
-// [0, D) = |v_m|^2, [D, D + ne) = the dots in the host's order, dot e joining members
-// (code[e] / 8, code[e] % 8). The members' operands stay in registers indexed at compile time:
-// per half tile each member's 4 elements are converted to fp64 once, the norms' FMAs are
-// unrolled, and each dot slot runs a uniform switch over its (u, v) pair whose arms are the 4
-// FMAs on the members' registers — no runtime-indexed register (r3's member-major pass lost to
-// scratch that way), no extra VALU for the selection (the switch is scalar branches). Same
-// per-lane chains in element order, same butterfly and tree as every other form: each sum is
-// bit-identical to pair_slot() on its two members, so every child's coefficients are
-// edt_slerp_merge's.
-constexpr int kNeedDots = 8;                  // dot slots per component
-constexpr int kNeedMaxOut = 16;               // children per component (emitting form)
+// parent in >= 3 pairs in most generations, so r4's ring (paths / cycles only) does not cover
+// them. The host lists a component's D members in the cyclic order that puts the most of its dots
+// on consecutive members (a search over the orders: at most 5,040 at D = 8); those dots are RING
+// dots (c, c + 1 mod D) whose operands are registers named at compile time (a uniform mask skips
+// the unused ones), the rest CHORDS (<= 4; in 3,000 roulette-drawn generations, 99.4 % need <= 3)
+// whose member pair is picked per slot by a uniform switch — its arms are the FMAs on the members'
+// registers, so no register is indexed at run time (r3's member-major pass lost to scratch that
+// way) and the selection costs scalar branches only. Layout of a component: sums [0, D) = |v_m|^2,
+// [D, D + NR) = ring dot c, [D + NR, NT) = chord e. Same per-lane chains in element order, same
+// butterfly and tree as every other form: each sum is bit-identical to pair_slot() on its two
+// members, so every child's coefficients are edt_slerp_merge's.
+constexpr int kNeedChords = 4;                // chord dot slots (D >= 5)
+constexpr int kNeedChordEmits = 8;            // children on chords (distinct ordered pairs)
+constexpr int kNeedMaxOut = 16;               // duplicate children per component
 
 template <int D>
 struct NeedLayout {
-    static constexpr int NE = D * (D - 1) / 2 < kNeedDots ? D * (D - 1) / 2 : kNeedDots;
-    static constexpr int NT = D + NE;
+    static constexpr int NR = D >= 3 ? D : D - 1;                           // ring dots
+    static constexpr int NC = D <= 3 ? 0 : D == 4 ? 2 : kNeedChords;        // chord slots
+    static constexpr int NT = D + NR + NC;
 };
-
-inline int need_nt(int D) { return D + (D * (D - 1) / 2 < kNeedDots ? D * (D - 1) / 2 : kNeedDots); }
-inline int need_ne(int D) { return need_nt(D) - D; }
+inline int need_nr(int D) { return D >= 3 ? D : D - 1; }
+inline int need_nc(int D) { return D <= 3 ? 0 : D == 4 ? 2 : kNeedChords; }
+inline int need_nt(int D) { return D + need_nr(D) + need_nc(D); }
 
 // What one needed-sums pass forms (and, EMIT, writes). Passed by value: every field is uniform.
 struct NeedSpec {
-    int32_t ne;                               // dots in use
-    int32_t code[kNeedDots];                  // dot e: members u * 8 + v (u < v)
-    int32_t nemit;                            // EMIT: distinct ordered parent pairs
-    int32_t ea[kNeedDots], eb[kNeedDots];     // pair e: v0 = member ea[e], v1 = member eb[e]
-    int32_t ofirst[kNeedDots + 1];            // pair e's children: out[ofirst[e] .. ofirst[e + 1])
-    void* out[kNeedMaxOut];
+    uint32_t ring;                            // ring dot c (members c, c + 1 mod D) in use: bit c
+    int32_t nchord;
+    int32_t code[kNeedChords];                // chord e: members u * 8 + v (u < v)
+    // EMIT: children on ring edge c: (c, c + 1) -> out_fwd[c] (bit c of fwd), (c + 1, c) -> out_rev[c]
+    uint32_t fwd, rev;
+    void* out_fwd[kGramMaxMembers];
+    void* out_rev[kGramMaxMembers];
+    int32_t nemit;                            // children off the ring (chords, self-pairs): distinct
+    int32_t ea[kNeedChordEmits], eb[kNeedChordEmits];   // ordered pairs v0 = ea[e], v1 = eb[e]
+    void* out[kNeedChordEmits];
+    int32_t nextra;                           // further children of an emitted pair: slot c (fwd),
+    int32_t xslot[kNeedMaxOut];               // 8 + c (rev), 16 + e (chord pair e)
+    void* xout[kNeedMaxOut];
     const double* t;                          // per segment
     int32_t* zero_word;                       // the any-redo word, zeroed by block 0 of the first launch
 };
@@ -1117,10 +1126,12 @@ __device__ __forceinline__ void need_dot(const double (&d)[D][N], int code, doub
 #undef EDT_ND
 }
 
-// The sums of N elements of every member (the lane's vector: N = 8, in two halves of 4; its
-// head / tail element: N = 1), continuing each chain.
-template <int D, int NE, int N, typename X>
-__device__ __forceinline__ void need_fma(const X (&x)[D], const NeedSpec& S, double (&g)[D + NE]) {
+// The sums of N elements of every member (the lane's vector: N = 8; its head / tail element:
+// N = 1), continuing each chain: the members' fp64 values per group of EDT_NEED_GROUP elements,
+// the norms, the ring dots in use, the chords.
+template <int D, int N, typename X>
+__device__ __forceinline__ void need_fma(const X (&x)[D], const NeedSpec& S, double (&g)[NeedLayout<D>::NT]) {
+    constexpr int NR = NeedLayout<D>::NR, NC = NeedLayout<D>::NC;
     constexpr int H = N < EDT_NEED_GROUP ? N : EDT_NEED_GROUP;
 #pragma unroll
     for (int h = 0; h < N / H; ++h) {
@@ -1134,8 +1145,14 @@ __device__ __forceinline__ void need_fma(const X (&x)[D], const NeedSpec& S, dou
 #pragma unroll
             for (int j = 0; j < H; ++j) g[m] = __builtin_fma(d[m][j], d[m][j], g[m]);
 #pragma unroll
-        for (int e = 0; e < NE; ++e)
-            if (e < S.ne) need_dot<D, H>(d, S.code[e], g[D + e]);
+        for (int c = 0; c < NR; ++c)
+            if ((S.ring >> c) & 1u) {
+#pragma unroll
+                for (int j = 0; j < H; ++j) g[D + c] = __builtin_fma(d[c][j], d[(c + 1) % D][j], g[D + c]);
+            }
+#pragma unroll
+        for (int e = 0; e < NC; ++e)
+            if (e < S.nchord) need_dot<D, H>(d, S.code[e], g[D + NR + e]);
     }
 }
 
@@ -1160,18 +1177,104 @@ __device__ __forceinline__ X need_pick(const X (&x)[D], int idx) {
     return r;
 }
 
-// EMIT: each distinct ordered pair's lerp-branch output l0 v0 + l1 v1 (pair_tile's math: two
-// rounded fp32 products, one rounded sum), stored to every child of that pair
-template <int ODT, int D, int N, typename X>
-__device__ __forceinline__ void need_emit(const X (&x)[D], const NeedSpec& S, uint64_t i, float l0, float l1) {
+// Global-memory access through a pointer built from a uniform integer: the address space is
+// stated (global_* instructions, not flat_*: a flat access also counts on lgkmcnt and retires out
+// of order, so every LDS wait would drain it), the base stays in scalar registers.
+typedef __attribute__((address_space(1))) const char gcchar;
+typedef __attribute__((address_space(1))) char gchar;
+
+__device__ __forceinline__ gcchar* global_ptr(const void* p, uint64_t byte_off) {
+    return reinterpret_cast<gcchar*>(uniform_u64(reinterpret_cast<uint64_t>(p) + byte_off));
+}
+
+template <int IDT, bool NT>
+__device__ __forceinline__ Raw8<IDT> ld_raw_g(gcchar* p) {
+    typedef __attribute__((address_space(1))) const u32x4 gu4;
+    typedef __attribute__((address_space(1))) const f32x4 gf4;
+    Raw8<IDT> r;
+    if constexpr (IDT == EDT_BF16) {
+        if constexpr (NT) r.w = __builtin_nontemporal_load(reinterpret_cast<gu4*>(p));
+        else r.w = *reinterpret_cast<gu4*>(p);
+    } else {
+        if constexpr (NT) {
+            r.lo = __builtin_nontemporal_load(reinterpret_cast<gf4*>(p));
+            r.hi = __builtin_nontemporal_load(reinterpret_cast<gf4*>(p + 16));
+        } else {
+            r.lo = *reinterpret_cast<gf4*>(p);
+            r.hi = *reinterpret_cast<gf4*>(p + 16);
+        }
+    }
+    return r;
+}
+
+template <int IDT>
+__device__ __forceinline__ float ld1_g(gcchar* p) {
+    if constexpr (IDT == EDT_BF16) return __uint_as_float((uint32_t)*reinterpret_cast<__attribute__((address_space(1))) const uint16_t*>(p) << 16);
+    else return *reinterpret_cast<__attribute__((address_space(1))) const float*>(p);
+}
+
+// st<ODT, N>'s rounding and packing, stored through a global pointer
+template <int ODT, int N>
+__device__ __forceinline__ void st_g(gchar* p, const float (&x)[N]) {
+    if constexpr (ODT == EDT_F32) {
+        typedef __attribute__((address_space(1))) f32x4 gf4;
+        if constexpr (N == 8) {
+            *reinterpret_cast<gf4*>(p) = (f32x4){x[0], x[1], x[2], x[3]};
+            *reinterpret_cast<gf4*>(p + 16) = (f32x4){x[4], x[5], x[6], x[7]};
+        } else {
 #pragma unroll
-    for (int e = 0; e < kNeedDots; ++e) {
-        if (e >= S.nemit) break;
-        const X a = need_pick<D>(x, S.ea[e]), b = need_pick<D>(x, S.eb[e]);
+            for (int j = 0; j < N; ++j) reinterpret_cast<__attribute__((address_space(1))) float*>(p)[j] = x[j];
+        }
+    } else {
+        if constexpr (N == 8) {
+            typedef __attribute__((address_space(1))) u32x4 gu4;
+            u32x4 w;
+            w.x = pack_bf(x[0], x[1]); w.y = pack_bf(x[2], x[3]);
+            w.z = pack_bf(x[4], x[5]); w.w = pack_bf(x[6], x[7]);
+            *reinterpret_cast<gu4*>(p) = w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < N; ++j)
+                reinterpret_cast<__attribute__((address_space(1))) uint16_t*>(p)[j] = uint16_t(pack_bf(x[j], 0.f) & 0xffffu);
+        }
+    }
+}
+
+// EMIT: every child's lerp-branch output l0 v0 + l1 v1 (pair_tile's math: two rounded fp32
+// products, one rounded sum) — ring-edge children from registers named at compile time, the others
+// through need_pick — each distinct ordered pair computed once and stored to every child of it. A
+// lane's vector (N = 8) is stored through a uniform base (the tile's start, scalar registers) + the
+// lane's byte offset; its head / tail element (N = 1) at element i0.
+template <int ODT, int D, int N, typename X>
+__device__ __forceinline__ void need_emit(const X (&x)[D], const NeedSpec& S, uint64_t i0, uint32_t lane,
+                                          float l0, float l1) {
+    constexpr uint64_t osz = ODT == EDT_BF16 ? 2 : 4;
+    constexpr int NR = NeedLayout<D>::NR;
+    auto store = [&](void* out, const float (&o)[N]) {
+        if constexpr (N == kVec) {                // uniform tile start + the lane's offset
+            gchar* base = const_cast<gchar*>(global_ptr(out, i0 * osz));
+            st_g<ODT, N>(base + lane * (kVec * osz), o);
+        } else {                                  // i0: this lane's own element
+            st_g<ODT, N>(reinterpret_cast<gchar*>(reinterpret_cast<uint64_t>(out)) + i0 * osz, o);
+        }
+    };
+    auto emit = [&](const X& a, const X& b, void* out, int slot) {
         float o[N];
 #pragma unroll
         for (int j = 0; j < N; ++j) o[j] = l0 * a[j] + l1 * b[j];
-        for (int k = S.ofirst[e]; k < S.ofirst[e + 1]; ++k) st<ODT, N>(S.out[k], i, o);
+        store(out, o);
+        for (int k = 0; k < S.nextra; ++k)
+            if (S.xslot[k] == slot) store(S.xout[k], o);
+    };
+#pragma unroll
+    for (int c = 0; c < NR; ++c) {
+        if ((S.fwd >> c) & 1u) emit(x[c], x[(c + 1) % D], S.out_fwd[c], c);
+        if ((S.rev >> c) & 1u) emit(x[(c + 1) % D], x[c], S.out_rev[c], 8 + c);
+    }
+#pragma unroll
+    for (int e = 0; e < kNeedChordEmits; ++e) {
+        if (e >= S.nemit) break;
+        emit(need_pick<D>(x, S.ea[e]), need_pick<D>(x, S.eb[e]), S.out[e], 16 + e);
     }
 }
 
@@ -1180,12 +1283,18 @@ __device__ __forceinline__ void need_emit(const X (&x)[D], const NeedSpec& S, ui
 // which leave every chain's bits unchanged). bf16 members: the next tile's loads in flight while
 // this tile is summed (two register sets).
 template <int IDT, int D, bool EMIT = false, int ODT = EDT_BF16>
-__global__ __launch_bounds__(kBlock, EDT_GRAM_MIN_BLOCKS) void slerp_need_kernel(Members mem, NeedSpec S,
+__global__ __launch_bounds__(kBlock, EDT_NEED_MIN_WAVES) void slerp_need_kernel(Members mem, NeedSpec S,
                                                                                  const uint64_t* chunks,
                                                                                  int64_t nchunks, double* rows,
                                                                                  uint64_t u0) {
-    constexpr int NE = NeedLayout<D>::NE, NT = NeedLayout<D>::NT, N2 = Red<NT>::N2;
+    constexpr int NT = NeedLayout<D>::NT, N2 = Red<NT>::N2;
     constexpr bool kPrefetch = EDT_NEED_PREFETCH != 0 && IDT == EDT_BF16;
+    constexpr bool kGlds = EDT_NEED_GLDS != 0 && IDT == EDT_BF16 && !kPrefetch;
+    // LDS-DMA stages per wave: two (two tiles in flight besides the one in registers) where the
+    // registers already limit the pass to 2 waves per SIMD (the emitting form, D = 8), else one
+    // (3 waves per SIMD fit the LDS with one stage, not with two)
+    constexpr int kStages = kGlds ? (EMIT || D == 8 ? 2 : 1) : 1;
+    __shared__ u32x4 stage[kStages][kGlds ? kWavesPerBlock : 1][kGlds ? D : 1][64];
     if constexpr (EMIT)
         if (S.zero_word && u0 == 0 && blockIdx.x == 0 && threadIdx.x == 0) *S.zero_word = 0;
     constexpr int upc = kTileSlots / 16;
@@ -1220,40 +1329,41 @@ __global__ __launch_bounds__(kBlock, EDT_GRAM_MIN_BLOCKS) void slerp_need_kernel
     // a member's tile: a uniform base (scalar registers, readfirstlane so LLVM cannot fold the lane
     // offset into a per-member 64-bit address held in vector registers) + the lane's byte offset
     constexpr uint32_t esz = IDT == EDT_BF16 ? 2 : 4;
-    auto member_base = [&](int m, uint64_t e0) {
-        return reinterpret_cast<const char*>(uniform_u64(reinterpret_cast<uint64_t>(mem.p[m]) + e0 * esz));
-    };
+    auto member_base = [&](int m, uint64_t e0) { return global_ptr(mem.p[m], e0 * esz); };
     auto load_tile = [&](int k, Raw8<IDT> (&x)[D]) {
         const uint64_t t0 = a + (uint64_t)(16 * g + 4 * wave + k) * kTileElems;     // uniform
         const uint32_t off = (uint32_t)lane * (kVec * esz);
         if (t0 + kTileElems <= b) {                    // the whole tile inside the aligned body
 #pragma unroll
-            for (int m = 0; m < D; ++m) x[m] = ld_raw<IDT, EDT_GRAM_NT != 0>(member_base(m, t0) + off, 0);
+            for (int m = 0; m < D; ++m) x[m] = ld_raw_g<IDT, EDT_GRAM_NT != 0>(member_base(m, t0) + off);
         } else {
 #pragma unroll
             for (int m = 0; m < D; ++m) x[m] = Raw8<IDT>{};
             if (a < b && t0 + (uint64_t)lane * kVec < b) {
 #pragma unroll
-                for (int m = 0; m < D; ++m) x[m] = ld_raw<IDT, EDT_GRAM_NT != 0>(member_base(m, t0) + off, 0);
+                for (int m = 0; m < D; ++m) x[m] = ld_raw_g<IDT, EDT_GRAM_NT != 0>(member_base(m, t0) + off);
             }
         }
     };
-    auto tile = [&](int k, const Raw8<IDT> (&x)[D]) {
+    // `mid()` runs right after the tile's lerp-branch stores (the staged loop issues the next DMA
+    // there, so a counted vmcnt can leave it in flight past those stores)
+    auto tile = [&](int k, const Raw8<IDT> (&x)[D], auto&& mid) {
         const int j = 16 * g + 4 * wave + k;
         const uint64_t i = a + (uint64_t)j * kTileElems + (uint64_t)lane * kVec;
         double gs[NT];
 #pragma unroll
         for (int q = 0; q < NT; ++q) gs[q] = 0.0;
-        need_fma<D, NE, kVec>(x, S, gs);
-        if constexpr (EMIT)
-            if (a < b && i < b) need_emit<ODT, D, kVec>(x, S, i, l0, l1);
+        if constexpr (EMIT)               // first: the members' registers are all it needs
+            if (a < b && i < b) need_emit<ODT, D, kVec>(x, S, a + (uint64_t)j * kTileElems, (uint32_t)lane, l0, l1);
+        mid();
+        need_fma<D, kVec>(x, S, gs);
         if (j == 0)
             tile0_edge(start, len, [&](uint64_t e) {
                 Raw1 y[D];
 #pragma unroll
-                for (int m = 0; m < D; ++m) ld<IDT, 1>(member_base(m, start), e - start, y[m].v);
-                need_fma<D, NE, 1>(y, S, gs);
-                if constexpr (EMIT) need_emit<ODT, D, 1>(y, S, e, l0, l1);
+                for (int m = 0; m < D; ++m) y[m].v[0] = ld1_g<IDT>(member_base(m, start) + (uint32_t)(e - start) * esz);
+                need_fma<D, 1>(y, S, gs);
+                if constexpr (EMIT) need_emit<ODT, D, 1>(y, S, e, 0, l0, l1);
             });
         double r[N2];
         tile_swap_levels<NT>(gs, r);
@@ -1274,25 +1384,68 @@ __global__ __launch_bounds__(kBlock, EDT_GRAM_MIN_BLOCKS) void slerp_need_kernel
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
-    if constexpr (kPrefetch) {                         // two register sets, two tile bodies in the code
+    bool staged = false;
+    if constexpr (kGlds) if (a + (uint64_t)(16 * g + 16) * kTileElems <= b) {
+        staged = true;
+        // the unit's tiles are whole: tile k + 1 lands in the wave's LDS stage by DMA
+        // (global_load_lds, no registers) while tile k is summed from registers — two tiles of
+        // loads in flight per wave at the registers of one. vmcnt(0) before reading the stage
+        // (the wave's own DMA; its stores count too on gfx9), lgkmcnt(0) before the next DMA.
+        // Vector-memory operations retire in issue order (loads, stores and LDS-DMA alike), so
+        // with two stages the wait for tile k's DMA is vmcnt(D): only tile k + 1's D DMA
+        // operations, issued after every older load and store, may stay in flight.
+        auto issue = [&](int k) {
+            const uint64_t t0 = a + (uint64_t)(16 * g + 4 * wave + k) * kTileElems;
+#pragma unroll
+            for (int m = 0; m < D; ++m)
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(member_base(m, t0) + lane * (kVec * esz)),
+                    (__attribute__((address_space(3))) void*)&stage[k % kStages][wave][m][0], 16, 0, EDT_GRAM_NT ? 2 : 0);
+        };
+        auto fetch = [&](int k, Raw8<IDT> (&x)[D]) {
+            if (kStages == 2 && k + 1 < 4) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(D) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // the stage read in asm: the compiler's own wait before an LDS read after an LDS-DMA
+            // is vmcnt(0), which would drain the next tile's DMA too
+            const uint32_t sa = (uint32_t)(uintptr_t)&stage[k % kStages][wave][0][lane];
+#pragma unroll
+            for (int m = 0; m < D; ++m)
+                asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(x[m].w) : "v"(sa), "n"(m * 1024) : "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        };
+        issue(0);
+        if constexpr (kStages == 2) issue(1);
+#pragma unroll 1
+        for (int k = 0; k < 4; ++k) {
+            Raw8<IDT> x[D];
+            fetch(k, x);
+            if constexpr (kStages == 2) tile(k, x, [&] { if (k + 2 < 4) issue(k + 2); });
+            else {
+                if (k < 3) issue(k + 1);
+                tile(k, x, [] {});
+            }
+        }
+    }
+    if (staged) {
+    } else if constexpr (kPrefetch) {                  // two register sets, two tile bodies in the code
         Raw8<IDT> x0[D], x1[D];
         load_tile(0, x0);
 #pragma unroll 1
         for (int k = 0; k < 4; k += 2) {
             load_tile(k + 1, x1);
             __builtin_amdgcn_sched_barrier(0);
-            tile(k, x0);
+            tile(k, x0, [] {});
             __builtin_amdgcn_sched_barrier(0);
             if (k + 2 < 4) load_tile(k + 2, x0);
             __builtin_amdgcn_sched_barrier(0);
-            tile(k + 1, x1);
+            tile(k + 1, x1, [] {});
         }
     } else {
 #pragma unroll 1
         for (int k = 0; k < 4; ++k) {
             Raw8<IDT> x[D];
             load_tile(k, x);
-            tile(k, x);
+            tile(k, x, [] {});
         }
     }
     if (lane < NT) ts2[wave][lane] = n01 + n23;
@@ -1307,7 +1460,9 @@ __global__ __launch_bounds__(kBlock, EDT_GRAM_MIN_BLOCKS) void slerp_need_kernel
 inline int need_sums(const Members& mem, int D, const NeedSpec& S, int in_dt, int out_dt, bool emit,
                      const uint64_t* chunk_desc, int64_t nchunks, double* sums, double* rows, hipStream_t s) {
     if (D < 1 || D > kGramMaxMembers) return fail(EDT_ERR_ARG, "needed-sums pass over %d members", D);
-    if (S.ne < 0 || S.ne > need_ne(D)) return fail(EDT_ERR_ARG, "%d dots over %d members", S.ne, D);
+    if (S.nchord < 0 || S.nchord > need_nc(D)) return fail(EDT_ERR_ARG, "%d chords over %d members", S.nchord, D);
+    if (S.nemit < 0 || S.nemit > kNeedChordEmits || S.nextra < 0 || S.nextra > kNeedMaxOut)
+        return fail(EDT_ERR_ARG, "bad emit table");
     constexpr int upc = kTileSlots / 16;
     const uint64_t units = (uint64_t)nchunks * upc;
     for (uint64_t u0 = 0; u0 < units; u0 += kUnitGridCap) {
@@ -1340,8 +1495,8 @@ inline int need_sums(const Members& mem, int D, const NeedSpec& S, int in_dt, in
 
 // How edt_slerp_population lays out its sums: the distinct parents split into the connected
 // components of the "needs a dot" graph (an edge per child with two different parents). r5: a
-// component whose distinct dots fit its slots (need_ne: every pair up to 4 members, 8 dots above)
-// takes the NEEDED layout (its norms + its dots in order of first use); any other the triangle
+// component takes the NEEDED layout (its norms + its dots: ring dots along the cyclic order that
+// covers the most of them, the rest chords) when its chords fit their slots, else the triangle
 // (every pair). Every member belongs to one component, so each parent is still read once in the
 // whole pass. (r4's ring layout — paths and cycles only — is the legacy choice kept behind
 // EDT_POP_LAYOUT=ring for the A/B probe.)
@@ -1362,7 +1517,7 @@ struct GramPlan {
     int size[kGramMaxMembers];
     int kind[kGramMaxMembers];
     int list[kGramMaxMembers][kGramMaxMembers];   // component -> members (compact), in layout order
-    NeedSpec need[kGramMaxMembers];        // kNeed: the component's dots (ne, code)
+    NeedSpec need[kGramMaxMembers];        // kNeed: the component's ring mask and chords
     uint64_t off[kGramMaxMembers];         // component's chunk rows in gram (doubles)
     int nt(int k) const {
         return kind[k] == kNeed ? need_nt(size[k]) : kind[k] == kRing ? 2 * size[k] : size[k] * (size[k] + 1) / 2;
@@ -1371,20 +1526,51 @@ struct GramPlan {
         const int k = comp_of[c], p = pos[c];
         return kind[k] == kTri ? tri_index(p, p, size[k]) : p;
     }
+    // ring edge of positions (p1, p2) in a component of M members, or -1
+    static int ring_edge(int p1, int p2, int M) {
+        if (M == 2) return p1 != p2 ? 0 : -1;
+        if (M < 3) return -1;
+        if ((p1 + 1) % M == p2) return p1;
+        if ((p2 + 1) % M == p1) return p2;
+        return -1;
+    }
     int dot_index(int c1, int c2) const {            // same component
         const int k = comp_of[c1], M = size[k];
         int p1 = pos[c1], p2 = pos[c2];
         if (c1 == c2) return norm_index(c1);
         if (kind[k] == kRing) return M + ((p1 + 1) % M == p2 ? p1 : p2);
-        if (p1 > p2) { const int t = p1; p1 = p2; p2 = t; }
         if (kind[k] == kNeed) {
-            for (int e = 0; e < need[k].ne; ++e)
-                if (need[k].code[e] == p1 * 8 + p2) return M + e;
+            const int e = ring_edge(p1, p2, M);
+            if (e >= 0) return M + e;
+            if (p1 > p2) { const int t = p1; p1 = p2; p2 = t; }
+            for (int c = 0; c < need[k].nchord; ++c)
+                if (need[k].code[c] == p1 * 8 + p2) return M + need_nr(M) + c;
             return -1;
         }
+        if (p1 > p2) { const int t = p1; p1 = p2; p2 = t; }
         return tri_index(p1, p2, M);
     }
 };
+
+// The cyclic order of a component's n members (compact ids, sorted) that puts the most of its
+// dots on consecutive members: members[0] first, every order of the rest (n <= 8: <= 5,040), the
+// first best in lexicographic order kept (deterministic); stops early when every dot is covered.
+inline void need_cyclic_order(const int* members, int n, const bool (&adj)[kGramMaxMembers][kGramMaxMembers],
+                              int nedges, int* order) {
+    for (int x = 0; x < n; ++x) order[x] = members[x];
+    if (n <= 3) return;                               // every dot is a ring dot
+    int perm[kGramMaxMembers], best = -1;
+    for (int x = 0; x < n; ++x) perm[x] = members[x];
+    do {
+        int cov = 0;
+        for (int c = 0; c < n; ++c) cov += adj[perm[c]][perm[(c + 1) % n]];
+        if (cov > best) {
+            best = cov;
+            for (int x = 0; x < n; ++x) order[x] = perm[x];
+            if (cov == nedges) return;
+        }
+    } while (std::next_permutation(perm + 1, perm + n));
+}
 
 inline void plan_gram(int D, const int* a, const int* b, int npairs, int64_t nchunks, GramPlan& G) {
     bool adj[kGramMaxMembers][kGramMaxMembers] = {};
@@ -1397,10 +1583,10 @@ inline void plan_gram(int D, const int* a, const int* b, int npairs, int64_t nch
         }
     const bool legacy = pop_layout_legacy() != 0;
     for (int c = 0; c < D; ++c) G.comp_of[c] = -1;
-    uint64_t off = 0;
     for (int c0 = 0; c0 < D; ++c0) {
         if (G.comp_of[c0] >= 0) continue;
         const int k = G.ncomp++;
+        memset(&G.need[k], 0, sizeof(NeedSpec));
         int members[kGramMaxMembers], n = 0, stack[kGramMaxMembers], top = 0;
         stack[top++] = c0;
         G.comp_of[c0] = k;
@@ -1421,46 +1607,65 @@ inline void plan_gram(int D, const int* a, const int* b, int npairs, int64_t nch
                 const int t = members[y]; members[y] = members[y - 1]; members[y - 1] = t;
             }
         G.size[k] = n;
-        if (legacy) G.kind[k] = n >= 3 && maxdeg <= 2 ? kRing : kTri;
-        else G.kind[k] = nedge2 / 2 <= need_ne(n) ? kNeed : kTri;
-        if (G.kind[k] == kRing) {                     // walk the path (from an end) or the cycle
-            int start = members[0];
-            for (int x = 0; x < n; ++x)
-                if (deg[members[x]] < 2) { start = members[x]; break; }
-            int prev = -1, cur = start;
-            for (int x = 0; x < n; ++x) {
-                G.list[k][x] = cur;
-                int next = -1;
-                for (int o = 0; o < D && next < 0; ++o)
-                    if (adj[cur][o] && o != prev && G.comp_of[o] == k) {
-                        bool seen = false;
-                        for (int y = 0; y <= x; ++y) seen = seen || G.list[k][y] == o;
-                        if (!seen) next = o;
-                    }
-                prev = cur;
-                cur = next;
+        if (legacy) {
+            G.kind[k] = n >= 3 && maxdeg <= 2 ? kRing : kTri;
+            if (G.kind[k] == kRing) {                 // walk the path (from an end) or the cycle
+                int start = members[0];
+                for (int x = 0; x < n; ++x)
+                    if (deg[members[x]] < 2) { start = members[x]; break; }
+                int prev = -1, cur = start;
+                for (int x = 0; x < n; ++x) {
+                    G.list[k][x] = cur;
+                    int next = -1;
+                    for (int o = 0; o < D && next < 0; ++o)
+                        if (adj[cur][o] && o != prev && G.comp_of[o] == k) {
+                            bool seen = false;
+                            for (int y = 0; y <= x; ++y) seen = seen || G.list[k][y] == o;
+                            if (!seen) next = o;
+                        }
+                    prev = cur;
+                    cur = next;
+                }
+            } else {
+                for (int x = 0; x < n; ++x) G.list[k][x] = members[x];
             }
         } else {
-            for (int x = 0; x < n; ++x) G.list[k][x] = members[x];
+            need_cyclic_order(members, n, adj, nedge2 / 2, G.list[k]);
+            G.kind[k] = kNeed;                        // checked against the chord slots below
         }
         for (int x = 0; x < n; ++x) G.pos[G.list[k][x]] = x;
-        G.off[k] = off;
-        off += (uint64_t)nchunks * G.nt(k);
     }
-    // the needed components' dots, in the order the children first use them
-    for (int k = 0; k < G.ncomp; ++k) {
-        memset(&G.need[k], 0, sizeof(NeedSpec));
-    }
+    // the needed components' ring masks and chords (chords in the order the children first use them)
     for (int q = 0; q < npairs; ++q) {
         if (a[q] == b[q]) continue;
         const int k = G.comp_of[a[q]];
         if (G.kind[k] != kNeed) continue;
-        int p1 = G.pos[a[q]], p2 = G.pos[b[q]];
-        if (p1 > p2) { const int t = p1; p1 = p2; p2 = t; }
         NeedSpec& S = G.need[k];
+        int p1 = G.pos[a[q]], p2 = G.pos[b[q]];
+        const int e = GramPlan::ring_edge(p1, p2, G.size[k]);
+        if (e >= 0) {
+            S.ring |= 1u << e;
+            continue;
+        }
+        if (p1 > p2) { const int t = p1; p1 = p2; p2 = t; }
         bool seen = false;
-        for (int e = 0; e < S.ne; ++e) seen = seen || S.code[e] == p1 * 8 + p2;
-        if (!seen) S.code[S.ne++] = p1 * 8 + p2;
+        for (int c = 0; c < S.nchord; ++c) seen = seen || S.code[c] == p1 * 8 + p2;
+        if (seen) continue;
+        if (S.nchord == need_nc(G.size[k])) {         // more chords than slots: the triangle
+            G.kind[k] = kTri;
+            for (int x = 1; x < G.size[k]; ++x) {      // compact order again
+                int* L = G.list[k];
+                for (int y = x; y > 0 && L[y] < L[y - 1]; --y) { const int t = L[y]; L[y] = L[y - 1]; L[y - 1] = t; }
+            }
+            for (int x = 0; x < G.size[k]; ++x) G.pos[G.list[k][x]] = x;
+            continue;
+        }
+        S.code[S.nchord++] = p1 * 8 + p2;
+    }
+    uint64_t off = 0;
+    for (int k = 0; k < G.ncomp; ++k) {
+        G.off[k] = off;
+        off += (uint64_t)nchunks * G.nt(k);
     }
 }
 
@@ -2455,33 +2660,48 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
                 edge[q] = e;
             }
         }
-        if (fits && !legacy) {                          // each component's distinct ordered pairs
-            for (int k = 0; k < G.ncomp && fits; ++k) {
+        if (fits && !legacy) {                          // each child onto its component's emit table
+            for (int q = 0; q < npairs && fits; ++q) {
+                const int k = G.comp_of[A[q]], n = G.size[k];
                 NeedSpec& S = G.need[k];
-                int slot_of[kBlendMaxChildren], cnt[kNeedDots] = {};
-                for (int q = 0; q < npairs && fits; ++q) {
-                    if (G.comp_of[A[q]] != k) { slot_of[q] = -1; continue; }
-                    const int pa = G.pos[A[q]], pb = G.pos[B[q]];
+                const int pa = G.pos[A[q]], pb = G.pos[B[q]];
+                int slot = -1;
+                void** first = nullptr;
+                uint32_t* bits = nullptr;
+                if (pa != pb && pb == (pa + 1) % n && (n >= 3 || pa == 0)) {
+                    slot = pa;
+                    bits = &S.fwd;
+                    first = &S.out_fwd[pa];
+                } else if (pa != pb && pa == (pb + 1) % n && (n >= 3 || pb == 0)) {
+                    slot = 8 + pb;
+                    bits = &S.rev;
+                    first = &S.out_rev[pb];
+                }
+                if (bits) {
+                    const uint32_t bit = 1u << (slot & 7);
+                    if (!(*bits & bit)) {
+                        *bits |= bit;
+                        *first = outs[q];
+                        continue;
+                    }
+                } else {                                // a chord or a self-pair: a picked pair
                     int e = 0;
                     while (e < S.nemit && !(S.ea[e] == pa && S.eb[e] == pb)) ++e;
                     if (e == S.nemit) {
-                        if (e == kNeedDots) { fits = false; break; }
+                        if (e == kNeedChordEmits) { fits = false; break; }
                         S.ea[e] = pa;
                         S.eb[e] = pb;
+                        S.out[e] = outs[q];
                         ++S.nemit;
+                        continue;
                     }
-                    slot_of[q] = e;
-                    ++cnt[e];
+                    slot = 16 + e;
                 }
-                if (!fits) break;
-                S.ofirst[0] = 0;
-                for (int e = 0; e < S.nemit; ++e) S.ofirst[e + 1] = S.ofirst[e] + cnt[e];
-                int fill[kNeedDots];
-                for (int e = 0; e < S.nemit; ++e) fill[e] = S.ofirst[e];
-                for (int q = 0; q < npairs; ++q)
-                    if (G.comp_of[A[q]] == k) S.out[fill[slot_of[q]]++] = outs[q];
-                S.t = t;
+                if (S.nextra == kNeedMaxOut) { fits = false; break; }   // a duplicate: same registers
+                S.xslot[S.nextra] = slot;
+                S.xout[S.nextra++] = outs[q];
             }
+            for (int k = 0; k < G.ncomp; ++k) G.need[k].t = t;
         }
         if (fits) {
             uint64_t scratch = 0;
@@ -2610,15 +2830,23 @@ int edt_slerp_population_layout(const int32_t* pairs, int npairs, int nmembers, 
         const bool legacy = pop_layout_legacy() != 0;
         std::string comps;
         for (int k = 0; k < G.ncomp; ++k) {
-            int nemit = 0, ea[64], eb[64];
-            for (int q = 0; q < npairs; ++q) {
+            const int n = G.size[k];
+            int nemit = 0, picked = 0, ea[64], eb[64];
+            for (int q = 0; q < npairs; ++q) {        // distinct ordered pairs; those off the ring
                 if (G.comp_of[A[q]] != k) continue;
                 int e = 0;
                 while (e < nemit && !(ea[e] == A[q] && eb[e] == B[q])) ++e;
-                if (e == nemit && nemit < 64) { ea[nemit] = A[q]; eb[nemit] = B[q]; ++nemit; }
+                if (e < nemit || nemit == 64) continue;
+                ea[nemit] = A[q];
+                eb[nemit++] = B[q];
+                const int pa = G.pos[A[q]], pb = G.pos[B[q]];
+                picked += !(G.kind[k] == kNeed && pa != pb && GramPlan::ring_edge(pa, pb, n) >= 0);
             }
+            int dupes = 0;
+            for (int q = 0; q < npairs; ++q) dupes += G.comp_of[A[q]] == k;
+            dupes -= nemit;
             if (legacy) mm = mm && (G.size[k] <= 2 || G.kind[k] == kRing);
-            else mm = mm && G.kind[k] == kNeed && nemit <= kNeedDots;
+            else mm = mm && G.kind[k] == kNeed && picked <= kNeedChordEmits && dupes <= kNeedMaxOut;
             int ndots = 0;
             for (int q = 0; q < npairs; ++q) {     // distinct unordered dots of the component
                 if (G.comp_of[A[q]] != k || A[q] == B[q]) continue;
@@ -2630,9 +2858,11 @@ int edt_slerp_population_layout(const int32_t* pairs, int npairs, int nmembers, 
             std::string mem;
             for (int x = 0; x < G.size[k]; ++x) mem += (x ? ", " : "") + std::to_string(orig[G.list[k][x]]);
             const char* kind = G.kind[k] == kNeed ? "needed" : G.kind[k] == kRing ? "ring" : "triangle";
+            const int chords = G.kind[k] == kNeed ? G.need[k].nchord : 0;
             comps += std::string(k ? ", " : "") + "{\"members\": [" + mem + "], \"dots\": " + std::to_string(ndots) +
-                     ", \"sums\": " + std::to_string(G.nt(k)) + ", \"stats_layout\": \"" + kind +
-                     "\", \"emit_pairs\": " + std::to_string(nemit) + "}";
+                     ", \"chords\": " + std::to_string(chords) + ", \"sums\": " + std::to_string(G.nt(k)) +
+                     ", \"stats_layout\": \"" + kind + "\", \"emit_pairs\": " + std::to_string(nemit) +
+                     ", \"picked_pairs\": " + std::to_string(picked) + "}";
         }
         const char* form = speculate ? (mm ? "member-major" : "co-located") : "two-pass";
         js += std::string(", \"form\": \"") + form + "\", \"legacy_ring\": " + (legacy ? "true" : "false") +

@@ -2,7 +2,7 @@
 # r5 step A: needed-sums population passes — GPU parity, then the roulette probe in the legacy
 # (r4 ring / triangle / co-located) and the new layout, same box.
 set -o pipefail
-O=gpurun_out/r5a
+O=gpurun_out/${R5_OUT:-r5a}
 mkdir -p $O
 timeout -k 10 600 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread \
     tests/test_gpu_population_needed.py "tests/test_gpu_kernels.py::test_slerp_population_pair_graphs" \
@@ -13,4 +13,4 @@ EDT_POP_LAYOUT=ring timeout -k 10 400 python3 -u scripts/pop_roulette_probe.py -
     --out $O/pop_roulette_legacy.json > $O/pop_roulette_legacy.log 2>&1 || { tail -20 $O/pop_roulette_legacy.log; exit 1; }
 timeout -k 10 400 python3 -u scripts/pop_roulette_probe.py --graphs 6 --rounds 3 --ring --independent \
     --out $O/pop_roulette_needed.json > $O/pop_roulette_needed.log 2>&1 || { tail -20 $O/pop_roulette_needed.log; exit 1; }
-tail -2 $O/pop_roulette_legacy.log $O/pop_roulette_needed.log
+tail -n 2 $O/pop_roulette_legacy.log; tail -n 2 $O/pop_roulette_needed.log

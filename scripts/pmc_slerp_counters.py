@@ -23,6 +23,10 @@ KERNEL_SETS = {
             "pop_speculative": "slerp_pop_stats_lerp_kernel<1, 1>",
             "ring_stats": "slerp_gram_kernel<1, 8, true, false", "ring_emit": "slerp_gram_kernel<1, 8, true, true",
             "ring_emit_m2": "slerp_gram_kernel<1, 2, true, true", "triangle_m2": "slerp_gram_kernel<1, 2, false"},
+    # r5: the needed-sums passes (scripts/pmc_need_counters.sh), per member count
+    "need": {**{f"need_stats_d{d}": f"slerp_need_kernel<1, {d}, false" for d in range(2, 9)},
+             **{f"need_emit_d{d}": f"slerp_need_kernel<1, {d}, true" for d in range(2, 9)},
+             "blend_mm": "slerp_blend_mm_kernel<1, 1, "},
 }
 KERNELS = KERNEL_SETS["pair"]
 CUS = 256

@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--ring", action="store_true")
     ap.add_argument("--independent", action="store_true", help="also independent members (SLERP branch)")
     ap.add_argument("--out", default="")
+    ap.add_argument("--only", type=int, default=-1, help="run only graph k of the drawn list (-1: all)")
+    ap.add_argument("--forms", default="speculative,two_pass")
     a = ap.parse_args()
     from evolutionarydistributedtraining_amd import ops
     from evolutionarydistributedtraining_amd.layouts import qwen2p5_7b_body
@@ -57,6 +59,8 @@ def main():
     graphs = roulette_generation_pairs(N, a.graphs, seed=a.seed)
     if a.ring:
         graphs.append({"source": "ring", "scale": None, "pairs": [(c, (c + 1) % N) for c in range(N)]})
+    if a.only >= 0:
+        graphs = [graphs[a.only]]
     s = torch.cuda.current_stream(dev)
     res = []
 
@@ -66,6 +70,8 @@ def main():
         rec = {"members": kind, "source": g["source"], "scale": g["scale"], "pairs": pairs, "distinct_parents": D,
                "layout": ops.population_layout(pairs, N)}
         for form, spec, floor in (("speculative", True, 2 * P * (D + N)), ("two_pass", False, 2 * P * (2 * D + N))):
+            if form not in a.forms.split(","):
+                continue
             ts = []
             for r in range(a.rounds + 1):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -97,8 +103,8 @@ def main():
     if a.out:
         with open(a.out, "w") as f:
             json.dump(out, f, indent=1)
-    print(json.dumps({"summary": [(r["members"], r["distinct_parents"], r["speculative"]["median_ms"],
-                                   r["two_pass"]["median_ms"]) for r in res]}))
+    print(json.dumps({"summary": [(r["members"], r["distinct_parents"], r.get("speculative", {}).get("median_ms"),
+                                   r.get("two_pass", {}).get("median_ms")) for r in res]}))
 
 
 if __name__ == "__main__":

@@ -44,7 +44,9 @@ EDGE_CASES = {
     "all_on_one_pair": [(3, 6)] * 8,
     "pair_and_reverse": [(1, 2), (2, 1), (1, 2), (2, 1), (5, 0), (0, 5), (7, 7), (4, 4)],
     "star16": [(0, m) for m in range(1, 8)] + [(m, 0) for m in range(1, 8)] + [(2, 3), (3, 2)],
-    "emit_overflow": [(0, 1), (1, 0), (0, 2), (2, 0), (1, 2), (2, 1), (0, 3), (3, 0), (1, 3)],  # 9 ordered pairs
+    "k4_both_ways": [(0, 1), (1, 0), (0, 2), (2, 0), (1, 2), (2, 1), (0, 3), (3, 0), (1, 3)],
+    "emit_overflow": [(0, 1), (1, 2), (2, 3), (3, 4), (4, 0), (0, 2), (2, 0), (1, 3), (3, 1), (2, 4), (4, 2),
+                      (3, 0), (0, 3), (1, 1)],                                    # 9 picked pairs > 8
     "nine_parents": [(m, m + 1) for m in range(8)],
 }
 

@@ -1,7 +1,7 @@
 """The population planner (edt_slerp_population_layout, host only: no GPU needed) on the graphs
 EDT_RL's selection draws and on the fallbacks. r5: every component whose distinct dots fit its
-slots takes the needed layout (norms + the children's dots); the speculative form is member-major
-for every graph of <= 8 children over <= 8 distinct parents."""
+slots takes the needed layout (norms + the children's dots: ring dots along the best cyclic order,
+the rest chords); the speculative form is member-major for the graphs EDT_RL's selection draws."""
 import random
 
 import pytest
@@ -23,7 +23,10 @@ def test_roulette_generations_take_the_needed_layout():
         for c in lay["components"]:
             assert c["stats_layout"] == "needed"
             n = len(c["members"])
-            assert c["sums"] == n + min(8, n * (n - 1) // 2)
+            ring = n if n >= 3 else n - 1                 # ring dots (c, c + 1 mod n)
+            chords = 0 if n <= 3 else 2 if n == 4 else 4  # chord slots
+            assert c["sums"] == n + ring + chords
+            assert c["chords"] <= chords and c["picked_pairs"] <= 8
         two = ops.population_layout(pairs, 8, False)
         assert two["form"] == "two-pass" and all(c["stats_layout"] == "needed" for c in two["components"])
 
@@ -46,7 +49,10 @@ def test_selection_statistics_that_motivate_it():
     ([(c, (c + 1) % 8) for c in range(8)], "member-major", ["needed"]),
     ([(a, b) for a in range(5) for b in range(a + 1, 5)], "co-located", ["triangle"]),
     ([(m, m + 1) for m in range(8)], "co-located", []),
-    ([(0, 1), (1, 0), (0, 2), (2, 0), (1, 2), (2, 1), (0, 3), (3, 0), (1, 3)], "co-located", ["needed"]),
+    ([(0, 1), (1, 0), (0, 2), (2, 0), (1, 2), (2, 1), (0, 3), (3, 0), (1, 3)], "member-major", ["needed"]),
+    # 5 members, 4 chords in both orientations + a self-pair: 9 picked pairs > 8 slots
+    ([(0, 1), (1, 2), (2, 3), (3, 4), (4, 0), (0, 2), (2, 0), (1, 3), (3, 1), (2, 4), (4, 2), (3, 0), (0, 3),
+      (1, 1)], "co-located", ["needed"]),
     ([(3, 6)] * 8, "member-major", ["needed"]),
     ([(4, 4), (2, 2)], "member-major", ["needed", "needed"]),
 ])
