@@ -104,8 +104,9 @@ def parse(argv=None):
                         "timing the step's access pattern on each, once before the timed steps (placement.py); "
                         "1 keeps the first allocation")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
-    p.add_argument("--ops", default="configs1_125m,pair_merge,slerp_7b,population_7b",
-                   help="the other hot-path measurements in the same line ('none': skip): N=1 configs1_125m "
+    p.add_argument("--ops", default="list_form,configs1_125m,pair_merge,slerp_7b,population_7b",
+                   help="the other hot-path measurements in the same line ('none': skip): N=1 list_form "
+                        "(the drop-in tensor-list DiLoCo surface at 1.3B, first allocation), configs1_125m "
                         "(BASELINE configs[1]: 125M x 8 resident), pair_merge, slerp_7b, population_7b "
                         "(configs[4]: at N = 1 all 8 members resident on the GPU; at N > 1 "
                         "across the N GPUs)")
@@ -136,6 +137,10 @@ def parse(argv=None):
                         "to rank 0 and compared with the single-GPU kernels); '' = skip")
     p.add_argument("--parity-bucket-elems", type=int, default=1 << 20,
                    help="bucket size of the parity check (several buckets even on the small layout)")
+    p.add_argument("--population-generations", type=int, default=3,
+                   help="N=1 population_7b: roulette-drawn generations timed (scales 0.1, 1.0, 2.5 in turn)")
+    p.add_argument("--population-seed", type=int, default=2025, help="seed of the drawn generations")
+    p.add_argument("--population-reps", type=int, default=10, help="timed calls per form and generation (>= 10)")
     p.add_argument("--population-layout", default="qwen2p5_7b_body",
                    help="N>1 population_slerp_7b: the member layout (BASELINE configs[4]: the 7.07B body)")
     return p.parse_args(argv)
@@ -663,6 +668,58 @@ def bench_config1(args, dev):
                          "algo_bytes_per_launch": per_elem * P}}
 
 
+def bench_list_form(args, dev):
+    """The drop-in DiLoCo surface as INTEGRATION.md §1's recipe runs it: diloco.outer_step over
+    `list(model.parameters())`-style tensors — the 1.3B layout's 292 tensors, each its own
+    allocation, for theta and for each of the 8 workers (the reference reloads its models every
+    generation, EDT_LM/diloco.py:231-235, so nothing is an arena) — with the outer momentum on its
+    FIRST allocation (OuterState, no placement search), one edt_outer_step_list launch per step
+    (EDT_LM/diloco.py:238-289). `f32`: everything fp32 (48 B/elem, the headline regime);
+    `bf16` / `bf16_cpu_tails`: all-bf16 (24 B/elem), the second with the reference host's scalar-
+    tail masks (cpu_tails=(32, 8), edt_outer_step_list_tail: +1/8 B/elem read). kernel_ms: HIP
+    events around back-to-back calls (the launch stream stays busy, so the events time the
+    kernel); wall_ms: per call on the host clock, host work included."""
+    from evolutionarydistributedtraining_amd import diloco
+    from evolutionarydistributedtraining_amd.layouts import gpt_1p3b
+    lay = gpt_1p3b()
+    P, K = lay.total, 8
+    res = {"workload": f"diloco.outer_step over tensor lists, gpt_1p3b P={P} T={len(lay)}, {K} workers, "
+                       f"lr {args.lr} mu {args.momentum} nesterov {bool(args.nesterov)}, momentum on its first allocation",
+           "kernel": "outer_list_kernel (edt_outer_step_list / _tail)"}
+    for key, dt, tails in (("f32", torch.float32, None), ("bf16", torch.bfloat16, None),
+                           ("bf16_cpu_tails", torch.bfloat16, (32, 8))):
+        _free_device()
+        g = torch.Generator(device=dev).manual_seed(99)
+        thetas = [(torch.randn(shp, generator=g, device=dev) * 0.02).to(dt) for shp in lay.shapes]
+        workers = [[(t.float() + torch.randn(t.shape, generator=g, device=dev) * 1e-3).to(dt) for t in thetas]
+                   for _ in range(K)]
+        state = diloco.OuterState()
+        step = lambda: diloco.outer_step(thetas, workers, state, args.lr, args.momentum, bool(args.nesterov),
+                                         cpu_tails=tails)
+        step()                                        # first generation: the momentum is created
+        torch.cuda.synchronize()
+        ms = _event_ms(step, max(args.steps, 10), 2)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(5):
+            step()
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t0) / 5 * 1e3
+        b = torch.finfo(dt).bits // 8
+        per_elem = K * b + 4 * b + (1 / 8 if tails else 0)
+        gbs = per_elem * P / (ms / 1e3) / 1e9
+        rec = {"kernel_ms": round(ms, 4), "wall_ms": round(wall, 4), "bytes_per_elem": per_elem,
+               "algo_bytes_per_launch": int(per_elem * P), "cpu_tails": list(tails) if tails else None,
+               "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                            "frac": round(gbs / HBM_PEAK_GBPS, 4)}}
+        pk = f"list_form/gpt_1p3b/K{K}/{key}"
+        rec["roofline"]["traffic"], rec["roofline"]["traffic_source"] = _pmc_traffic(args, pk, with_note=True)
+        res[key] = rec
+        del thetas, workers, state, step
+    _free_device()
+    return res
+
+
 def bench_pair_merge(args, dev):
     """EDT-LM child (EDT_LM/train/crossover.py:150-237: lerp(.5) of the bases, mean of the two
     pseudo-gradients, Nesterov SGD with the carried momentum) over the 1.3B layout, bf16 parents,
@@ -837,24 +894,34 @@ def bench_population(args, rt, comm, kernels=None, layout_name="qwen2p5_7b_body"
 
 
 def bench_population_resident(args, dev, layout_name="qwen2p5_7b_body", members_n=8):
-    """BASELINE configs[4] on ONE GPU: a population of 8 members (7.07B bf16 bodies) SLERP-crossed
-    into 8 children, every buffer resident in HBM (16 x 14.1 GB = 226 GB; EDT_RL/edt.py:286-299 ->
-    EDT_RL/crossover.py:84-135 per child), as ops.slerp_population runs it: `speculative` = the
-    co-located single pass (members of one lineage: every tensor in the lerp branch), `two_pass` =
-    the Gram stats pass + the member-major blend (the SLERP-branch form; its cost does not depend
-    on the branch), on the same members. Children (c, c + 1): 8 distinct parents, each feeding two
-    children. `floor_bytes`: the form's least HBM bytes (each distinct parent read once per pass,
-    each child written once); `algo_bytes`: the generation's (every member once, every child once).
-    Skipped with a reason when the HBM left after the other extras cannot hold it."""
+    """BASELINE configs[4] on ONE GPU: a population of 8 members (7.07B bf16 bodies, one lineage)
+    SLERP-crossed into 8 children per generation, every buffer resident in HBM (16 x 14.1 GB =
+    226 GB), the generation as the RL master runs it: the pairs drawn by EDT_RL/edt.py:231-240's
+    roulette_wheel_selection (schedule.roulette_generation_pairs: n = 8 pairs, random fitness, scale
+    0.1 / 1.0 / 2.5 across the drawn generations as roulette_scale spans a run) and t per key from
+    EDT_RL/crossover.py:146-147's layer curves routed as :108-122 routes them (merge.rl_t_per_segment,
+    28 layers) — EDT_RL/edt.py:286-299 -> EDT_RL/crossover.py:84-135 per child. Each drawn generation
+    runs ops.slerp_population in both forms, `--population-reps` (>= 10) timed calls each:
+    `speculative` (the needed-sums member-major pass that writes every child's lerp-branch output +
+    the redo blend; members of one lineage: every segment in the lerp branch) and `two_pass` (the
+    needed-sums stats pass + the member-major blend). `floor_bytes`: the form's least HBM bytes
+    (each distinct parent read once per pass, each child written once); `algo_bytes`: the
+    generation's (every member once, every child once). The headline `speculative` / `two_pass`
+    are the drawn generations together (sum of floor bytes over sum of times); `ring` is the ring
+    of children (c, c + 1 mod 8) of r4's bench, kept as a labelled second case. Skipped with a
+    reason when the HBM left after the other extras cannot hold it."""
     from evolutionarydistributedtraining_amd import ops
     from evolutionarydistributedtraining_amd.layouts import LAYOUTS
+    from evolutionarydistributedtraining_amd.merge import rl_t_per_segment
+    from evolutionarydistributedtraining_amd.schedule import roulette_generation_pairs
     lay = LAYOUTS[layout_name]()
     P, bf, M = lay.total, torch.bfloat16, members_n
     need = 2 * M * P * 2
     _free_device()                      # blocks the earlier extras left cached count as free
     free, _ = torch.cuda.mem_get_info(dev)
-    res = {"workload": f"SLERP population of {M} x {layout_name} (P={P}, bf16), all resident on one GPU",
-           "kernel": "edt_slerp_population_speculative / edt_slerp_population"}
+    res = {"workload": f"SLERP population of {M} x {layout_name} (P={P}, bf16), all resident on one GPU, "
+                       f"pairs by EDT_RL's roulette selection, t by its layer curves",
+           "kernel": "edt_slerp_population_speculative / edt_slerp_population (slerp_need_kernel)"}
     if free < need + (6 << 30):
         res["skipped"] = f"needs {need / 1e9:.0f} GB of HBM, {free / 1e9:.0f} GB free"
         return res
@@ -868,24 +935,53 @@ def bench_population_resident(args, dev, layout_name="qwen2p5_7b_body", members_
         for m in members:
             m[s0:e] = (x + torch.randn(e - s0, generator=g, device=dev) * (0.02 * 0.005)).to(bf)
         del x
-    pairs = [(c, (c + 1) % M) for c in range(M)]
     plan = ops.make_slerp_plan(lay.offsets, dev)
-    t = torch.full((len(lay),), 0.5, dtype=torch.float64, device=dev)
-    res["pairs"] = pairs
+    t = torch.tensor(rl_t_per_segment(lay.names), dtype=torch.float64, device=dev)
+    reps = max(10, args.population_reps)
     algo = 2 * M * P * 2
-    for form, spec, floor in (("speculative", True, 2 * M * P * 2), ("two_pass", False, 3 * M * P * 2)):
-        ms = _event_ms(lambda: ops.slerp_population(plan, members, pairs, outs, t, speculate=spec), 3, 1)
-        traffic, note = (_pmc_traffic(args, f"population_7b/{form}", with_note=True)
+
+    def generation(pairs):
+        D = len({x for p in pairs for x in p})
+        rec = {"pairs": [list(p) for p in pairs], "distinct_parents": D,
+               "layout": ops.population_layout(pairs, M, True)}
+        for form, spec, floor in (("speculative", True, 2 * P * (D + M)), ("two_pass", False, 2 * P * (2 * D + M))):
+            ms = _event_ms(lambda: ops.slerp_population(plan, members, pairs, outs, t, speculate=spec), reps, 1)
+            rec[form] = {"ms": round(ms, 3), "floor_bytes": floor, "algo_bytes": algo,
+                         "floor_GBps": round(floor / (ms / 1e3) / 1e9, 1)}
+        dots = getattr(plan, "_pop_dots", None)
+        if dots is not None:
+            rec["lerp_branch_fraction"] = round(float((dots.float().abs() > 0.9995).float().mean()), 4)
+        return rec
+
+    gens = roulette_generation_pairs(M, args.population_generations, seed=args.population_seed)
+    drawn = []
+    for gdef in gens:
+        rec = generation([tuple(p) for p in gdef["pairs"]])
+        rec["scale"] = gdef["scale"]
+        drawn.append(rec)
+    res["pairs_source"] = (f"schedule.roulette_generation_pairs(8, {args.population_generations}, "
+                           f"seed={args.population_seed}): EDT_RL/edt.py:231-240 roulette_wheel_selection, "
+                           f"n = 8 pairs, scales {sorted({r['scale'] for r in drawn})}")
+    res["t_source"] = "merge.rl_t_per_segment: EDT_RL/crossover.py:146-147 layer curves, global 0.5"
+    res["timed_reps"] = reps
+    res["generations"] = drawn
+    for form in ("speculative", "two_pass"):
+        fb = sum(r[form]["floor_bytes"] for r in drawn)
+        ms = sum(r[form]["ms"] for r in drawn)
+        ab = algo * len(drawn)
+        key = f"population_7b/roulette/{form}"
+        traffic, note = (_pmc_traffic(args, key, with_note=True)
                          if layout_name == "qwen2p5_7b_body" else (None, "PMC entries are for the 7B body"))
-        res[form] = {"ms": round(ms, 3), "floor_bytes": floor, "algo_bytes": algo,
-                     "roofline": {"bound": "hbm", "achieved": round(floor / (ms / 1e3) / 1e9, 1),
+        res[form] = {"ms_per_generation": round(ms / len(drawn), 3), "floor_bytes_per_generation": fb // len(drawn),
+                     "algo_bytes": algo,
+                     "roofline": {"bound": "hbm", "achieved": round(fb / (ms / 1e3) / 1e9, 1),
                                   "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                                  "frac": round(floor / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
-                                  "algo_frac": round(algo / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
-                                  "traffic": traffic, "traffic_source": note}}
-    dots = plan._pop_dots.float().abs() if getattr(plan, "_pop_dots", None) is not None else None
-    if dots is not None:
-        res["lerp_branch_fraction"] = round(float((dots > 0.9995).float().mean()), 4)
+                                  "frac": round(fb / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+                                  "algo_frac": round(ab / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+                                  "traffic_per_generation": traffic, "traffic_source": note}}
+    ring = generation([(c, (c + 1) % M) for c in range(M)])
+    ring["note"] = "the ring of children (c, c + 1 mod 8): r4's bench pairs, which roulette selection rarely draws"
+    res["ring"] = ring
     del members, outs
     _free_device()
     return res
@@ -1281,8 +1377,8 @@ def main():
         sync.theta = sync.workers = sync.state = None
         theta = workers = sync = step = None
         _free_device()
-        for name, fn in (("configs1_125m", bench_config1), ("pair_merge", bench_pair_merge),
-                         ("slerp_7b", bench_slerp_7b)):
+        for name, fn in (("list_form", bench_list_form), ("configs1_125m", bench_config1),
+                         ("pair_merge", bench_pair_merge), ("slerp_7b", bench_slerp_7b)):
             if name in args.ops:
                 try:
                     out[name] = fn(args, dev)

@@ -37,6 +37,8 @@ SIGNATURES = [
     ("edt_outer_list_workspace_bytes", _U64, [_I, _I]),
     ("edt_outer_step_list", _I, [ctypes.POINTER(_P), _I, ctypes.POINTER(_P), _I, _I, ctypes.POINTER(_P), _I,
                                  ctypes.POINTER(_U64), _I, _D, _D, _I, _P, _U64, _P]),
+    ("edt_outer_step_list_tail", _I, [ctypes.POINTER(_P), _I, ctypes.POINTER(_P), _I, _I, ctypes.POINTER(_P), _I,
+                                      ctypes.POINTER(_U64), _I, _D, _D, _I, _P, ctypes.POINTER(_U64), _P, _U64, _P]),
     ("edt_delta_partial", _I, [_P, _I, ctypes.POINTER(_P), _I, _I, _I, _U64, _P, _I, _P]),
     ("edt_sgd_apply", _I, [_P, _I, _P, _P, _I, _U64, _D, _D, _I, _P]),
     ("edt_sgd_apply_sum", _I, [_P, _I, ctypes.POINTER(_P), _I, _P, _I, _U64, _D, _D, _I, _P]),

@@ -768,62 +768,6 @@ __device__ __forceinline__ void gram_fma_first(const X (&x)[M], double (&g)[M * 
     }
 }
 
-// The ring layout (r4): a population whose children's parent pairs form paths and cycles (every
-// parent in at most two distinct pairs: a ring of children, a matching) needs the M norms and at
-// most M dots (m, m + 1 mod M) once its members are listed along the ring — 2M sums per element
-// instead of M(M+1)/2 (16 against 36 at M = 8). Sums [0, M): |v_m|^2; [M, 2M): v_m . v_{m+1 mod M}.
-// Each sum is the same per-lane FMA chain, butterfly and tree as in the triangle layout (an FMA's
-// product is exact, so the operand order does not matter): bit-identical values.
-template <int M, bool RING>
-struct GramLayout {
-    static constexpr int NT = RING ? 2 * M : M * (M + 1) / 2;
-};
-
-template <int M, int N, typename X>
-__device__ __forceinline__ void ring_fma(const X (&x)[M], double (&g)[2 * M], bool from_zero) {
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-        double d[M];
-#pragma unroll
-        for (int m = 0; m < M; ++m) d[m] = x[m][j];
-        const bool z = from_zero && j == 0;
-#pragma unroll
-        for (int m = 0; m < M; ++m) g[m] = __builtin_fma(d[m], d[m], z ? 0.0 : g[m]);
-#pragma unroll
-        for (int m = 0; m < M; ++m) g[M + m] = __builtin_fma(d[m], d[(m + 1) % M], z ? 0.0 : g[M + m]);
-    }
-}
-
-// The speculative ring form (edt_slerp_population_speculative when the children are edges of one
-// ring of parents, at most one child per edge): the ring pass also writes child c's lerp-branch
-// output (1 - t) v0 + t v1 (pair_tile's math: two rounded fp32 products, one rounded sum) from the
-// members' registers — edge c joins ring members c and c + 1 mod M, `flip` bit c: v0 is member
-// c + 1. One read of every parent, one write of every child, 2M sums per element.
-struct RingEmit {
-    void* out[kGramMaxMembers];              // the child on edge c (use bit c set)
-    const double* t;                         // per segment
-    uint32_t use, flip;
-    int32_t* zero_word;                      // the any-redo word, zeroed by block 0 of the first launch
-};
-
-template <int ODT, int N, typename X>
-__device__ __forceinline__ void ring_emit_one(const X& v0, const X& v1, void* out, uint64_t i, float l0, float l1) {
-    float o[N];
-#pragma unroll
-    for (int e = 0; e < N; ++e) o[e] = l0 * v0[e] + l1 * v1[e];
-    st<ODT, N>(out, i, o);
-}
-
-template <int M, int ODT, int N, typename X>
-__device__ __forceinline__ void ring_emit(const X (&x)[M], const RingEmit& E, uint64_t i, float l0, float l1) {
-#pragma unroll
-    for (int c = 0; c < M; ++c) {
-        if (!((E.use >> c) & 1u)) continue;              // uniform: scalar branches
-        if ((E.flip >> c) & 1u) ring_emit_one<ODT, N>(x[(c + 1) % M], x[c], E.out[c], i, l0, l1);
-        else ring_emit_one<ODT, N>(x[c], x[(c + 1) % M], E.out[c], i, l0, l1);
-    }
-}
-
 // Gram rows (level 4), one workgroup per unit of 16 tiles in address order: wave w takes tiles
 // 16 g + 4 w .. + 3 one after the other (one vector per member per lane: M loads in flight). Each
 // tile's NT sums go through the xor butterfly in two parts: the swap levels (32, 16) on the VALU,
@@ -836,14 +780,11 @@ __device__ __forceinline__ void ring_emit(const X (&x)[M], const RingEmit& E, ui
 // (unit_slot). Every sum is bit-identical to pair_slot() on (vi, vj): the same per-lane FMA
 // sequence in element order (an FMA's product is exact, so vi*vj == vj*vi), the same butterfly and
 // tree; the coefficients therefore equal edt_slerp_merge's.
-template <int IDT, int M, bool RING = false, bool EMIT = false, int ODT = EDT_BF16>
+template <int IDT, int M>
 __global__ __launch_bounds__(kBlock, EDT_GRAM_MIN_BLOCKS) void slerp_gram_kernel(Members mem, const uint64_t* chunks,
                                                                                  int64_t nchunks, double* rows,
-                                                                                 uint64_t u0, RingEmit E) {
-    static_assert(!EMIT || RING, "the emitting form is the ring layout's");
-    constexpr int NT = GramLayout<M, RING>::NT, N2 = Red<NT>::N2;
-    if constexpr (EMIT)
-        if (E.zero_word && u0 == 0 && blockIdx.x == 0 && threadIdx.x == 0) *E.zero_word = 0;
+                                                                                 uint64_t u0) {
+    constexpr int NT = M * (M + 1) / 2, N2 = Red<NT>::N2;
     constexpr int upc = kTileSlots / 16;
     // [wave][row][slot][position in row], 17 doubles per (row, slot): lane q's 16 reads start
     // 2 banks apart from lane q + 1's instead of all on one bank
@@ -858,12 +799,6 @@ __global__ __launch_bounds__(kBlock, EDT_GRAM_MIN_BLOCKS) void slerp_gram_kernel
     const int g = (int)(u % upc);
     // the chunk bounds are uniform: in scalar registers, so the full-tile test below is a scalar branch
     const uint64_t start = uniform_u64(chunks[3 * c]), len = uniform_u64(chunks[3 * c + 1]);
-    float l0 = 0.f, l1 = 0.f;                          // the lerp-branch weights of the unit's segment
-    if constexpr (EMIT) {
-        const double tv = E.t[chunks[3 * c + 2]];
-        l0 = (float)(1.0 - tv);
-        l1 = (float)tv;
-    }
     // lane q (< NT) reads value q's partials: the row and slot that hold it after the swap levels
     int pos = 0;
 #pragma unroll
@@ -891,15 +826,11 @@ __global__ __launch_bounds__(kBlock, EDT_GRAM_MIN_BLOCKS) void slerp_gram_kernel
         const uint64_t i = a + (uint64_t)j * kTileElems + (uint64_t)lane * kVec;
         if constexpr (decltype(full)::value) {
             if constexpr (EDT_GRAM_PREFETCH) {
-                if constexpr (RING) ring_fma<M, kVec>(xin, gs, true);
-                else gram_fma_first<M, kVec>(xin, gs);      // loaded one tile ahead
-                if constexpr (EMIT) ring_emit<M, ODT, kVec>(xin, E, i, l0, l1);
+                gram_fma_first<M, kVec>(xin, gs);      // loaded one tile ahead
             } else {
                 Raw8<IDT> x[M];
                 load_tile(k, x);
-                if constexpr (RING) ring_fma<M, kVec>(x, gs, true);
-                else gram_fma_first<M, kVec>(x, gs);
-                if constexpr (EMIT) ring_emit<M, ODT, kVec>(x, E, i, l0, l1);
+                gram_fma_first<M, kVec>(x, gs);
             }
         } else {
 #pragma unroll
@@ -908,9 +839,7 @@ __global__ __launch_bounds__(kBlock, EDT_GRAM_MIN_BLOCKS) void slerp_gram_kernel
                 Raw8<IDT> x[M];
 #pragma unroll
                 for (int m = 0; m < M; ++m) x[m] = ld_raw<IDT, false>(mem.p[m], i);
-                if constexpr (RING) ring_fma<M, kVec>(x, gs, false);
-                else gram_fma<M, kVec>(x, gs);
-                if constexpr (EMIT) ring_emit<M, ODT, kVec>(x, E, i, l0, l1);
+                gram_fma<M, kVec>(x, gs);
             }
         }
         if (j == 0)
@@ -918,9 +847,7 @@ __global__ __launch_bounds__(kBlock, EDT_GRAM_MIN_BLOCKS) void slerp_gram_kernel
                 Raw1 x[M];
 #pragma unroll
                 for (int m = 0; m < M; ++m) ld<IDT, 1>(mem.p[m], e, x[m].v);
-                if constexpr (RING) ring_fma<M, 1>(x, gs, false);
-                else gram_fma<M, 1>(x, gs);
-                if constexpr (EMIT) ring_emit<M, ODT, 1>(x, E, e, l0, l1);
+                gram_fma<M, 1>(x, gs);
             });
         double r[N2];
         tile_swap_levels<NT>(gs, r);
@@ -976,79 +903,29 @@ __global__ __launch_bounds__(kBlock, EDT_GRAM_MIN_BLOCKS) void slerp_gram_kernel
 }
 
 // host: the Gram sums of D compact members into gram (chunk rows [nchunks][NT]); `rows`: the
-// level-4 row scratch (default: right after the chunk rows). ring: the ring layout (D >= 3).
+// level-4 row scratch (default: right after the chunk rows).
 inline int gram_sums(const Members& mem, int D, int in_dt, const uint64_t* chunk_desc, int64_t nchunks, double* gram,
-                     hipStream_t s, bool ring = false, double* rows = nullptr) {
-    if (ring && D < 3) return fail(EDT_ERR_ARG, "ring Gram layout over %d members", D);
-    const int NT = ring ? 2 * D : D * (D + 1) / 2;
+                     hipStream_t s, double* rows = nullptr) {
+    const int NT = D * (D + 1) / 2;
     if (!rows) rows = gram + (uint64_t)nchunks * NT;
-    RingEmit E0;
-    memset(&E0, 0, sizeof(E0));
-    constexpr int upc = kTileSlots / 16;
-    const uint64_t units = (uint64_t)nchunks * upc;
-    for (uint64_t u0 = 0; u0 < units; u0 += kUnitGridCap) {
-    const unsigned g = unit_grid(units - u0);
-#define EDT_GM(M)                                                                                                   \
-    case M:                                                                                                         \
-        if (in_dt == EDT_F32) slerp_gram_kernel<EDT_F32, M><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0, E0); \
-        else slerp_gram_kernel<EDT_BF16, M><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0, E0);              \
-        break;
-#define EDT_GR(M)                                                                                             \
-    case M:                                                                                                   \
-        if (in_dt == EDT_F32)                                                                                 \
-            slerp_gram_kernel<EDT_F32, M, true><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0, E0); \
-        else                                                                                                  \
-            slerp_gram_kernel<EDT_BF16, M, true><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0, E0); \
-        break;
-    if (ring) {
-        switch (D) {
-            EDT_GR(3) EDT_GR(4) EDT_GR(5) EDT_GR(6) EDT_GR(7) EDT_GR(8)
-            default: return fail(EDT_ERR_ARG, "ring Gram pass over %d members", D);
-        }
-    } else {
-        switch (D) {
-            EDT_GM(1) EDT_GM(2) EDT_GM(3) EDT_GM(4) EDT_GM(5) EDT_GM(6) EDT_GM(7) EDT_GM(8)
-            default: return fail(EDT_ERR_ARG, "Gram pass over %d members", D);
-        }
-    }
-#undef EDT_GM
-#undef EDT_GR
-    int rc = check_launch("slerp_gram_kernel");
-    if (rc) return rc;
-    }
-    return launch_tree_reduce(rows, NT, kGramRows, upc, 1, nchunks, gram, s);
-}
-
-// host: the speculative ring pass — ring sums of the D members (ring order; D = 1, 2: the self-pair
-// and the two orientations of one pair) into sums ([nchunks][2D]; `rows`: the level-4 row scratch)
-// and every child's lerp-branch output (E).
-inline int ring_spec_sums(const Members& mem, int D, int in_dt, int out_dt, const RingEmit& E,
-                          const uint64_t* chunk_desc, int64_t nchunks, double* sums, double* rows, hipStream_t s) {
-    const int NT = 2 * D;
     constexpr int upc = kTileSlots / 16;
     const uint64_t units = (uint64_t)nchunks * upc;
     for (uint64_t u0 = 0; u0 < units; u0 += kUnitGridCap) {
         const unsigned g = unit_grid(units - u0);
-#define EDT_GE(M)                                                                                                  \
-    case M:                                                                                                        \
-        if (in_dt == EDT_F32 && out_dt == EDT_F32)                                                                 \
-            slerp_gram_kernel<EDT_F32, M, true, true, EDT_F32><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0, E);   \
-        else if (in_dt == EDT_F32)                                                                                 \
-            slerp_gram_kernel<EDT_F32, M, true, true, EDT_BF16><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0, E);  \
-        else if (out_dt == EDT_F32)                                                                                \
-            slerp_gram_kernel<EDT_BF16, M, true, true, EDT_F32><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0, E);  \
-        else                                                                                                       \
-            slerp_gram_kernel<EDT_BF16, M, true, true, EDT_BF16><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0, E); \
+#define EDT_GM(M)                                                                                      \
+    case M:                                                                                            \
+        if (in_dt == EDT_F32) slerp_gram_kernel<EDT_F32, M><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0); \
+        else slerp_gram_kernel<EDT_BF16, M><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0);              \
         break;
         switch (D) {
-            EDT_GE(1) EDT_GE(2) EDT_GE(3) EDT_GE(4) EDT_GE(5) EDT_GE(6) EDT_GE(7) EDT_GE(8)
-            default: return fail(EDT_ERR_ARG, "speculative ring pass over %d members", D);
+            EDT_GM(1) EDT_GM(2) EDT_GM(3) EDT_GM(4) EDT_GM(5) EDT_GM(6) EDT_GM(7) EDT_GM(8)
+            default: return fail(EDT_ERR_ARG, "Gram pass over %d members", D);
         }
-#undef EDT_GE
-        int rc = check_launch("slerp_gram_kernel (speculative ring)");
+#undef EDT_GM
+        int rc = check_launch("slerp_gram_kernel");
         if (rc) return rc;
     }
-    return launch_tree_reduce(rows, NT, kGramRows, upc, 1, nchunks, sums, s);
+    return launch_tree_reduce(rows, NT, kGramRows, upc, 1, nchunks, gram, s);
 }
 
 // ---- the needed-sums layout (r5): any pair graph --------------------------------------------------
@@ -1498,17 +1375,9 @@ inline int need_sums(const Members& mem, int D, const NeedSpec& S, int in_dt, in
 // component takes the NEEDED layout (its norms + its dots: ring dots along the cyclic order that
 // covers the most of them, the rest chords) when its chords fit their slots, else the triangle
 // (every pair). Every member belongs to one component, so each parent is still read once in the
-// whole pass. (r4's ring layout — paths and cycles only — is the legacy choice kept behind
-// EDT_POP_LAYOUT=ring for the A/B probe.)
-enum { kTri = 0, kRing = 1, kNeed = 2 };
-
-inline int pop_layout_legacy() {
-    static const int v = [] {
-        const char* e = getenv("EDT_POP_LAYOUT");
-        return e && strcmp(e, "ring") == 0 ? 1 : 0;
-    }();
-    return v;
-}
+// whole pass. (r4's ring layout — paths and cycles only, a compile-time ring kernel — was measured
+// against it on roulette-drawn generations and removed: profiles/r05_pop_roulette_*.json.)
+enum { kTri = 0, kNeed = 2 };
 
 struct GramPlan {
     int ncomp = 0;
@@ -1520,7 +1389,7 @@ struct GramPlan {
     NeedSpec need[kGramMaxMembers];        // kNeed: the component's ring mask and chords
     uint64_t off[kGramMaxMembers];         // component's chunk rows in gram (doubles)
     int nt(int k) const {
-        return kind[k] == kNeed ? need_nt(size[k]) : kind[k] == kRing ? 2 * size[k] : size[k] * (size[k] + 1) / 2;
+        return kind[k] == kNeed ? need_nt(size[k]) : size[k] * (size[k] + 1) / 2;
     }
     int norm_index(int c) const {
         const int k = comp_of[c], p = pos[c];
@@ -1538,7 +1407,6 @@ struct GramPlan {
         const int k = comp_of[c1], M = size[k];
         int p1 = pos[c1], p2 = pos[c2];
         if (c1 == c2) return norm_index(c1);
-        if (kind[k] == kRing) return M + ((p1 + 1) % M == p2 ? p1 : p2);
         if (kind[k] == kNeed) {
             const int e = ring_edge(p1, p2, M);
             if (e >= 0) return M + e;
@@ -1581,7 +1449,6 @@ inline void plan_gram(int D, const int* a, const int* b, int npairs, int64_t nch
             ++deg[a[q]];
             ++deg[b[q]];
         }
-    const bool legacy = pop_layout_legacy() != 0;
     for (int c = 0; c < D; ++c) G.comp_of[c] = -1;
     for (int c0 = 0; c0 < D; ++c0) {
         if (G.comp_of[c0] >= 0) continue;
@@ -1590,11 +1457,10 @@ inline void plan_gram(int D, const int* a, const int* b, int npairs, int64_t nch
         int members[kGramMaxMembers], n = 0, stack[kGramMaxMembers], top = 0;
         stack[top++] = c0;
         G.comp_of[c0] = k;
-        int maxdeg = 0, nedge2 = 0;
+        int nedge2 = 0;
         while (top) {                                 // the component, in compact order below
             const int c = stack[--top];
             members[n++] = c;
-            maxdeg = deg[c] > maxdeg ? deg[c] : maxdeg;
             nedge2 += deg[c];
             for (int o = 0; o < D; ++o)
                 if (adj[c][o] && G.comp_of[o] < 0) {
@@ -1607,32 +1473,8 @@ inline void plan_gram(int D, const int* a, const int* b, int npairs, int64_t nch
                 const int t = members[y]; members[y] = members[y - 1]; members[y - 1] = t;
             }
         G.size[k] = n;
-        if (legacy) {
-            G.kind[k] = n >= 3 && maxdeg <= 2 ? kRing : kTri;
-            if (G.kind[k] == kRing) {                 // walk the path (from an end) or the cycle
-                int start = members[0];
-                for (int x = 0; x < n; ++x)
-                    if (deg[members[x]] < 2) { start = members[x]; break; }
-                int prev = -1, cur = start;
-                for (int x = 0; x < n; ++x) {
-                    G.list[k][x] = cur;
-                    int next = -1;
-                    for (int o = 0; o < D && next < 0; ++o)
-                        if (adj[cur][o] && o != prev && G.comp_of[o] == k) {
-                            bool seen = false;
-                            for (int y = 0; y <= x; ++y) seen = seen || G.list[k][y] == o;
-                            if (!seen) next = o;
-                        }
-                    prev = cur;
-                    cur = next;
-                }
-            } else {
-                for (int x = 0; x < n; ++x) G.list[k][x] = members[x];
-            }
-        } else {
-            need_cyclic_order(members, n, adj, nedge2 / 2, G.list[k]);
-            G.kind[k] = kNeed;                        // checked against the chord slots below
-        }
+        need_cyclic_order(members, n, adj, nedge2 / 2, G.list[k]);
+        G.kind[k] = kNeed;                            // checked against the chord slots below
         for (int x = 0; x < n; ++x) G.pos[G.list[k][x]] = x;
     }
     // the needed components' ring masks and chords (chords in the order the children first use them)
@@ -1688,7 +1530,7 @@ inline int plan_component_sums(const GramPlan& G, int k, const void* const* dm, 
     for (int x = 0; x < G.size[k]; ++x) gm.p[x] = dm[G.list[k][x]];
     if (G.kind[k] == kNeed)
         return need_sums(gm, G.size[k], G.need[k], in_dt, EDT_F32, false, chunk_desc, nchunks, gram + G.off[k], rows, s);
-    return gram_sums(gm, G.size[k], in_dt, chunk_desc, nchunks, gram + G.off[k], s, G.kind[k] == kRing, rows);
+    return gram_sums(gm, G.size[k], in_dt, chunk_desc, nchunks, gram + G.off[k], s, rows);
 }
 
 // The blends of every child in one launch, with pair_population_kernel's placement: the
@@ -2615,11 +2457,10 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
     // branch). Any pair graph over <= 8 distinct parents whose components fit their dot slots
     // (every graph of <= 8 children) takes it; others the co-located pass below.
     {
-        std::vector<int> compact(nmembers, -1), A(npairs), B(npairs), edge(npairs);
+        std::vector<int> compact(nmembers, -1), A(npairs), B(npairs);
         const void* dm[kGramMaxMembers];
         int D = 0;
-        const bool legacy = pop_layout_legacy() != 0;
-        bool fits = npairs <= kBlendMaxChildren && (!legacy || npairs <= kGramMaxMembers);
+        bool fits = npairs <= kBlendMaxChildren;
         for (int q = 0; q < npairs && fits; ++q)
             for (int e = 0; e < 2 && fits; ++e) {
                 const int m = pairs[2 * q + e];
@@ -2633,34 +2474,9 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
         GramPlan G;
         if (fits) {
             plan_gram(D, A.data(), B.data(), npairs, nchunks, G);
-            for (int k = 0; k < G.ncomp && fits; ++k)
-                fits = legacy ? (G.size[k] <= 2 || G.kind[k] == kRing) : G.kind[k] == kNeed;
-            if (fits && legacy) {                       // r4: 1-2 parents are rings too (2 D sums)
-                uint64_t off = 0;
-                for (int k = 0; k < G.ncomp; ++k) {
-                    G.kind[k] = kRing;
-                    G.off[k] = off;
-                    off += (uint64_t)nchunks * G.nt(k);
-                }
-            }
+            for (int k = 0; k < G.ncomp && fits; ++k) fits = G.kind[k] == kNeed;
         }
-        RingEmit E[kGramMaxMembers];
-        if (fits && legacy) {
-            memset(E, 0, sizeof(E));
-            for (int q = 0; q < npairs && fits; ++q) {
-                const int k = G.comp_of[A[q]], n = G.size[k], pi = G.pos[A[q]], pj = G.pos[B[q]];
-                int e = -1;
-                bool flip = false;
-                if ((pi + 1) % n == pj) e = pi;
-                else if ((pj + 1) % n == pi) { e = pj; flip = true; }
-                if (e < 0 || ((E[k].use >> e) & 1u)) { fits = false; break; }
-                E[k].use |= 1u << e;
-                E[k].out[e] = outs[q];
-                if (flip) E[k].flip |= 1u << e;
-                edge[q] = e;
-            }
-        }
-        if (fits && !legacy) {                          // each child onto its component's emit table
+        if (fits) {                                     // each child onto its component's emit table
             for (int q = 0; q < npairs && fits; ++q) {
                 const int k = G.comp_of[A[q]], n = G.size[k];
                 NeedSpec& S = G.need[k];
@@ -2710,22 +2526,14 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
             for (int k = 0; k < G.ncomp; ++k) {           // the passes first: only the first zeroes `any`
                 memset(&gm[k], 0, sizeof(Members));
                 for (int x = 0; x < G.size[k]; ++x) gm[k].p[x] = dm[G.list[k][x]];
-                int rc;
-                if (legacy) {
-                    E[k].t = t;
-                    E[k].zero_word = k == 0 ? any : nullptr;
-                    rc = ring_spec_sums(gm[k], G.size[k], in_dt, out_dt, E[k], chunk_desc, nchunks, partial + G.off[k],
-                                        partial + scratch, s);
-                } else {
-                    G.need[k].zero_word = k == 0 ? any : nullptr;
-                    rc = need_sums(gm[k], G.size[k], G.need[k], in_dt, out_dt, true, chunk_desc, nchunks,
+                G.need[k].zero_word = k == 0 ? any : nullptr;
+                int rc = need_sums(gm[k], G.size[k], G.need[k], in_dt, out_dt, true, chunk_desc, nchunks,
                                    partial + G.off[k], partial + scratch, s);
-                }
                 if (rc) return rc;
             }
             for (int q = 0; q < npairs; ++q) {
-                const int k = G.comp_of[A[q]], n = G.size[k];
-                const int qd = legacy ? (A[q] == B[q] ? G.pos[A[q]] : n + edge[q]) : G.dot_index(A[q], B[q]);
+                const int k = G.comp_of[A[q]];
+                const int qd = G.dot_index(A[q], B[q]);
                 slerp_gram_coef_kernel<<<coef_grid(nseg), kBlock, 0, s>>>(
                     partial + G.off[k], G.nt(k), G.norm_index(A[q]), G.norm_index(B[q]), qd, seg_first_chunk, nseg, t,
                     (float)dot_threshold, (float)eps, coef + 2 * (size_t)nseg * q,
@@ -2827,7 +2635,6 @@ int edt_slerp_population_layout(const int32_t* pairs, int npairs, int nmembers, 
         GramPlan G;
         plan_gram(D, A.data(), B.data(), npairs, 1, G);
         bool mm = npairs <= kBlendMaxChildren;
-        const bool legacy = pop_layout_legacy() != 0;
         std::string comps;
         for (int k = 0; k < G.ncomp; ++k) {
             const int n = G.size[k];
@@ -2845,8 +2652,7 @@ int edt_slerp_population_layout(const int32_t* pairs, int npairs, int nmembers, 
             int dupes = 0;
             for (int q = 0; q < npairs; ++q) dupes += G.comp_of[A[q]] == k;
             dupes -= nemit;
-            if (legacy) mm = mm && (G.size[k] <= 2 || G.kind[k] == kRing);
-            else mm = mm && G.kind[k] == kNeed && picked <= kNeedChordEmits && dupes <= kNeedMaxOut;
+            mm = mm && G.kind[k] == kNeed && picked <= kNeedChordEmits && dupes <= kNeedMaxOut;
             int ndots = 0;
             for (int q = 0; q < npairs; ++q) {     // distinct unordered dots of the component
                 if (G.comp_of[A[q]] != k || A[q] == B[q]) continue;
@@ -2857,7 +2663,7 @@ int edt_slerp_population_layout(const int32_t* pairs, int npairs, int nmembers, 
             }
             std::string mem;
             for (int x = 0; x < G.size[k]; ++x) mem += (x ? ", " : "") + std::to_string(orig[G.list[k][x]]);
-            const char* kind = G.kind[k] == kNeed ? "needed" : G.kind[k] == kRing ? "ring" : "triangle";
+            const char* kind = G.kind[k] == kNeed ? "needed" : "triangle";
             const int chords = G.kind[k] == kNeed ? G.need[k].nchord : 0;
             comps += std::string(k ? ", " : "") + "{\"members\": [" + mem + "], \"dots\": " + std::to_string(ndots) +
                      ", \"chords\": " + std::to_string(chords) + ", \"sums\": " + std::to_string(G.nt(k)) +
@@ -2865,8 +2671,7 @@ int edt_slerp_population_layout(const int32_t* pairs, int npairs, int nmembers, 
                      ", \"picked_pairs\": " + std::to_string(picked) + "}";
         }
         const char* form = speculate ? (mm ? "member-major" : "co-located") : "two-pass";
-        js += std::string(", \"form\": \"") + form + "\", \"legacy_ring\": " + (legacy ? "true" : "false") +
-              ", \"components\": [" + comps + "]}";
+        js += std::string(", \"form\": \"") + form + "\", \"components\": [" + comps + "]}";
     }
     if ((int)js.size() + 1 > buflen) return fail(EDT_ERR_ARG, "buffer of %d bytes too short (%d)", buflen, (int)js.size() + 1);
     memcpy(buf, js.c_str(), js.size() + 1);

@@ -101,14 +101,27 @@ class OuterState:
         return st
 
 
-def _tail_bits(cpu_tails, numels, device):
+def _tail_bits(cpu_tails, numels, device, state=None, per_tensor=False):
     """cpu_tails = (vec_elems, num_threads) of the reference's host -> the device bitmask of its
-    torch scalar-tail elements (torchcompat), or None."""
+    torch scalar-tail elements (torchcompat), or None. per_tensor: the tensor-list form's masks
+    ((bits, byte offsets), each tensor's from a byte boundary). With `state` the mask is kept on it
+    for the next generation (it depends only on the sizes and the host model; building it walks
+    every element once on the CPU)."""
     if cpu_tails is None:
         return None
-    from .torchcompat import torch_cpu_tail_bits
+    key = (tuple(int(n) for n in numels), tuple(cpu_tails), str(device), per_tensor)
+    cached = getattr(state, "_tail_cache", None) if state is not None else None
+    if cached is not None and cached[0] == key:
+        return cached[1]
+    from .torchcompat import torch_cpu_tail_bits, torch_cpu_tail_bits_per_tensor
     vec, threads = cpu_tails
-    return torch_cpu_tail_bits(numels, vec_elems=vec, num_threads=threads, device=device)
+    if per_tensor:
+        got = torch_cpu_tail_bits_per_tensor(numels, vec_elems=vec, num_threads=threads, device=device)
+    else:
+        got = torch_cpu_tail_bits(numels, vec_elems=vec, num_threads=threads, device=device)
+    if state is not None:
+        state._tail_cache = (key, got)
+    return got
 
 
 def _step_flat(theta: torch.Tensor, workers: list[torch.Tensor], state: OuterState, lr: float,
@@ -130,7 +143,7 @@ def _step_flat(theta: torch.Tensor, workers: list[torch.Tensor], state: OuterSta
 
 
 def _step_list(thetas: list[torch.Tensor], workers: list[list[torch.Tensor]], state: OuterState,
-               lr: float, momentum: float, nesterov: bool) -> None:
+               lr: float, momentum: float, nesterov: bool, tails=None) -> None:
     check_sgd_hparams(lr, momentum, nesterov)
     state.hparams = dict(lr=lr, momentum=momentum, nesterov=nesterov)
     moms = None
@@ -144,7 +157,7 @@ def _step_list(thetas: list[torch.Tensor], workers: list[list[torch.Tensor]], st
             moms = ParamLayout.of(thetas).views(flat)
             state._list_views = (flat, shapes, moms)
     ops.outer_step_list(thetas, workers, moms, state.has_momentum if momentum != 0 else False,
-                        lr, momentum, nesterov)
+                        lr, momentum, nesterov, tails=tails)
     if momentum != 0:
         state.has_momentum = True
     state.steps += 1
@@ -162,8 +175,9 @@ def outer_step(base_params, worker_params, state: OuterState | None = None, lr: 
     (`params.arena_of_module`), else over the tensor lists themselves (`ops.outer_step_list`,
     no packing). Only populations above 64 workers with separate tensors are packed first.
     cpu_tails = (Vec::size(), torch threads) of the reference's master, e.g. (32, 8): bf16 results
-    bit-exact with the reference run there, torch's scalar tails included (torchcompat; flat form,
-    separate tensors are packed).
+    bit-exact with the reference run there, torch's scalar tails included (torchcompat; r5: the
+    tensor-list form reads per-tensor masks, edt_outer_step_list_tail, so nothing is packed; the
+    masks are kept on `state` across generations).
     """
     state = state or OuterState()
     base_params = list(base_params)
@@ -178,10 +192,14 @@ def outer_step(base_params, worker_params, state: OuterState | None = None, lr: 
         theta = flat_view(base_params)
         flats = [flat_view(w) for w in worker_params]
         if theta is None or any(f is None for f in flats):
-            if cpu_tails is None and len(worker_params) <= L_MAX and base_params and all(p.is_cuda for p in base_params):
+            bf16_master = base_params and base_params[0].dtype == torch.bfloat16
+            if (cpu_tails is None or bf16_master) and len(worker_params) <= L_MAX and base_params \
+                    and all(p.is_cuda for p in base_params):
                 if len({w[0].dtype for w in worker_params}) != 1:
                     raise EdtError("all trained models must share one dtype")
-                _step_list(base_params, worker_params, state, lr, momentum, nesterov)
+                tails = _tail_bits(cpu_tails, [p.numel() for p in base_params], base_params[0].device, state,
+                                   per_tensor=True)
+                _step_list(base_params, worker_params, state, lr, momentum, nesterov, tails=tails)
                 return state
         copied = theta is None
         if copied:
@@ -191,7 +209,7 @@ def outer_step(base_params, worker_params, state: OuterState | None = None, lr: 
         if len(wdt) != 1:
             raise EdtError("all trained models must share one dtype")
         _step_flat(theta, flats, state, lr, momentum, nesterov,
-                   tail_bits=_tail_bits(cpu_tails, [p.numel() for p in base_params], theta.device))
+                   tail_bits=_tail_bits(cpu_tails, [p.numel() for p in base_params], theta.device, state))
         if copied:
             unpack_(theta, base_params)
     return state

@@ -83,10 +83,12 @@ def outer_step(theta: torch.Tensor, workers: list[torch.Tensor], momentum: torch
 
 def outer_step_list(thetas: list[torch.Tensor], workers: list[list[torch.Tensor]],
                     momenta: list[torch.Tensor] | None, has_momentum: bool, lr: float,
-                    momentum_coef: float, nesterov: bool) -> None:
+                    momentum_coef: float, nesterov: bool, tails=None) -> None:
     """`outer_step` over T separate tensors per model (e.g. `list(model.parameters())` of
     models loaded on the GPU) in ONE launch, without packing: thetas[t], workers[k][t],
-    momenta[t] (theta's dtype, required when momentum_coef != 0), all updated in place."""
+    momenta[t] (theta's dtype, required when momentum_coef != 0), all updated in place.
+    tails: (bits, byte offsets) from torchcompat.torch_cpu_tail_bits_per_tensor — the reference
+    host's bf16 scalar tails per tensor (edt_outer_step_list_tail; bf16 master only)."""
     lib = L.lib()
     T, K = len(thetas), len(workers)
     if K == 0:
@@ -131,9 +133,23 @@ def outer_step_list(thetas: list[torch.Tensor], workers: list[list[torch.Tensor]
     th_arr = (P_ * T)(*[t.data_ptr() for t in thetas])
     w_arr = (P_ * len(flat_w))(*[t.data_ptr() for t in flat_w])
     m_arr = (P_ * T)(*[t.data_ptr() for t in momenta]) if momenta is not None else None
-    L.check(lib.edt_outer_step_list(th_arr, L.dtype_code(gdt), w_arr, L.dtype_code(wdt), K, m_arr,
-                                    int(has_momentum), numel, T, float(lr), float(momentum_coef), int(nesterov),
-                                    L.ptr(ws), nbytes, L.stream_ptr(thetas[0].device)), "edt_outer_step_list")
+    if tails is None:
+        L.check(lib.edt_outer_step_list(th_arr, L.dtype_code(gdt), w_arr, L.dtype_code(wdt), K, m_arr,
+                                        int(has_momentum), numel, T, float(lr), float(momentum_coef), int(nesterov),
+                                        L.ptr(ws), nbytes, L.stream_ptr(thetas[0].device)), "edt_outer_step_list")
+        return
+    bits, offs = tails
+    if gdt != torch.bfloat16:
+        raise L.EdtError("scalar-tail bits apply to a bf16 master only")
+    if len(offs) != T or not bits.is_cuda or bits.dtype != torch.uint8 or bits.device != thetas[0].device:
+        raise L.EdtError("tails: a uint8 device mask and one byte offset per tensor")
+    if any(o + (n + 7) // 8 > bits.numel() for o, n in zip(offs, numels)):
+        raise L.EdtError("tails: the mask does not cover every tensor")
+    toff = (ctypes.c_uint64 * T)(*[int(o) for o in offs])
+    L.check(lib.edt_outer_step_list_tail(th_arr, L.dtype_code(gdt), w_arr, L.dtype_code(wdt), K, m_arr,
+                                         int(has_momentum), numel, T, float(lr), float(momentum_coef), int(nesterov),
+                                         L.ptr(bits), toff, L.ptr(ws), nbytes, L.stream_ptr(thetas[0].device)),
+            "edt_outer_step_list_tail")
 
 
 def delta_partial(theta: torch.Tensor, workers: list[torch.Tensor], k_total: int,

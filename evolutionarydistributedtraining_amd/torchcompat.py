@@ -44,3 +44,23 @@ def torch_cpu_tail_bits(numels, vec_elems: int = 32, num_threads: int = 1, grain
         mask[a:b] = 1
     bits = torch.from_numpy(np.packbits(mask, bitorder="little"))
     return bits.to(device) if device is not None else bits
+
+
+def torch_cpu_tail_bits_per_tensor(numels, vec_elems: int = 32, num_threads: int = 1, grain: int = TORCH_GRAIN,
+                                   device=None):
+    """The same tail elements for T separate tensors (the tensor-list step, edt_outer_step_list_tail):
+    each tensor's bits start at a byte boundary, indexed by the element's index inside its tensor.
+    Returns (bits uint8 [sum ceil(n / 8)], byte offset of each tensor's bits)."""
+    parts, offs, off = [], [], 0
+    for n in numels:
+        n = int(n)
+        nb = -(-n // 8)
+        offs.append(off)
+        if nb:
+            mask = np.zeros(nb * 8, dtype=np.uint8)
+            for a, b in torch_cpu_tail_ranges([n], vec_elems, num_threads, grain):
+                mask[a:b] = 1
+            parts.append(np.packbits(mask, bitorder="little"))
+        off += nb
+    bits = torch.from_numpy(np.concatenate(parts) if parts else np.zeros(1, dtype=np.uint8))
+    return (bits.to(device) if device is not None else bits), offs

@@ -115,6 +115,15 @@ int edt_outer_step_list(void* const* theta_t, int gdt, const void* const* theta_
                         void* const* momentum_t, int has_momentum, const uint64_t* numel, int T,
                         double lr, double momentum, int nesterov, void* workspace,
                         uint64_t workspace_bytes, void* stream);
+/* edt_outer_step_list with the reference host's bf16 scalar tails (edt_outer_step_tail's rule, r5):
+ * tail_bits (device, nullable) holds each tensor's 1-bit-per-element mask from byte
+ * tail_byte_offset[t] (host array, T entries), indexed by the element's index inside its tensor.
+ * gdt must be EDT_BF16 when tail_bits is given. */
+int edt_outer_step_list_tail(void* const* theta_t, int gdt, const void* const* theta_k, int wdt, int K,
+                             void* const* momentum_t, int has_momentum, const uint64_t* numel, int T,
+                             double lr, double momentum, int nesterov, const uint8_t* tail_bits,
+                             const uint64_t* tail_byte_offset, void* workspace, uint64_t workspace_bytes,
+                             void* stream);
 
 /* Partial delta sum for the sharded multi-GPU step (EDT_LM/diloco.py:243-246 restricted to the
  * workers resident on this rank): acc_f32[i] (+)= sum_{k<K_local} round_g((theta_k - theta_g)/K_total).

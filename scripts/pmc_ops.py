@@ -51,6 +51,32 @@ def main():
                                "hbm_bytes_per_launch": stats["hbm_bytes_per_launch"] + blend["hbm_bytes_per_launch"],
                                "algorithmic_bytes": 6 * P7, "moved_bytes": 10 * P7,
                                "note": "two-pass: chunk sums (4 B/elem read) + blend (4 B read, 2 B written)"}
+    # r5: the drop-in tensor-list step (bench_list_form): fp32, then bf16 without and with the
+    # tail masks — one template for both bf16 runs, so its launches are split in dispatch order
+    import csv
+    import glob
+
+    def ordered(counter, sub):
+        rows = []
+        for path in glob.glob(os.path.join(root, counter, "**", "*counter_collection.csv"), recursive=True):
+            with open(path) as fh:
+                for row in csv.DictReader(fh):
+                    if sub in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                        rows.append((int(row.get("Dispatch_Id") or 0), float(row["Counter_Value"])))
+        return [v for _, v in sorted(rows)]
+
+    for key, sub, part, bpe in (("f32", "outer_list_kernel<0, 0, 8", None, 48), ("bf16", "outer_list_kernel<1, 1, 8", 0, 24),
+                                ("bf16_cpu_tails", "outer_list_kernel<1, 1, 8", 1, 24.125)):
+        fs, ws = ordered("FETCH_SIZE", sub), ordered("WRITE_SIZE", sub)
+        if part is not None:
+            fs, ws = fs[part * len(fs) // 2:(part + 1) * len(fs) // 2], ws[part * len(ws) // 2:(part + 1) * len(ws) // 2]
+        if not fs or not ws:
+            continue
+        f, w = statistics.median(fs), statistics.median(ws)
+        out[f"list_form/gpt_1p3b/K8/{key}"] = {
+            "kernel": sub, "launches": min(len(fs), len(ws)), "fetch_bytes_x2": 2 * f * 1024, "write_bytes": w * 1024,
+            "hbm_bytes_per_launch": int(2 * f * 1024 + w * 1024), "algorithmic_bytes": int(bpe * P1),
+            "correction": "FETCH_SIZE x2 (16 B/lane loads), WRITE_SIZE x1"}
     from evolutionarydistributedtraining_amd._lib import library_sha256
     for rec in out.values():
         rec["lib_sha256"] = library_sha256()      # the build these counters were measured on

@@ -2,9 +2,9 @@
 sub-object (8 x 7B members resident, 8 children), from a FETCH_SIZE and a WRITE_SIZE
 rocprofv3 --pmc pass over `bench.py --ops population_7b` (scripts/profile_pmc_pop.sh): every launch
 of each form's kernels summed (FETCH_SIZE x 2 and KiB -> bytes: the gfx950 corrections of
-MI355X_MICROARCH.md) and divided by the calls the sub-object makes (1 warm-up + 3 timed per form).
-Writes ROOT/pmc_pop_traffic.json with entries `population_7b/speculative` and
-`population_7b/two_pass`, stamped with the library's sha256 (merge with scripts/merge_pmc.py).
+MI355X_MICROARCH.md) and divided by the calls (dispatch order: a call opens at its first pass).
+Writes ROOT/pmc_pop_traffic.json with entries `population_7b/{roulette,ring}/{speculative,two_pass}`
+(per generation), stamped with the library's sha256 (merge with scripts/merge_pmc.py).
 
     python scripts/pmc_population.py gpurun_out/pmc_pop
 """
@@ -16,29 +16,30 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-CALLS = 4                                      # bench_population_resident: _event_ms(fn, 3, 1) per form
-FORMS = {   # the kernels each form launches (tree_reduce / coef: both forms, a few MB: left out)
-    "speculative": ("slerp_pop_stats_lerp_kernel", "slerp_blend_population_kernel",
-                    "slerp_gram_kernel (emitting ring)", "slerp_blend_mm_kernel (redo)"),
-    "two_pass": ("slerp_gram_kernel", "slerp_blend_mm_kernel"),
-}
+# r5: bench_population_resident times G roulette-drawn generations then the ring of children, each
+# form 1 warm-up + R timed calls (--population-generations / --population-reps; the defaults below
+# must match the command in profile_pmc_pop.sh)
+GENERATIONS = int(os.environ.get("POP_GENERATIONS", 3))
+REPS = int(os.environ.get("POP_REPS", 10))
+STARTERS = ("slerp_need_kernel", "slerp_gram_kernel", "slerp_pop_stats_lerp_kernel")
+COUNTED = STARTERS + ("slerp_blend_mm_kernel", "slerp_blend_population_kernel")
 
 
-def _form_starter(name):
-    """The form a call starts with this kernel (dispatch order): the speculative forms begin with the
-    co-located pass or the emitting ring pass (r4: slerp_gram_kernel<IDT, M, true, true, ODT>), the
-    two-pass form with a non-emitting Gram / ring pass; every later launch (blends, coefficients)
-    belongs to the call its starter opened — slerp_blend_mm_kernel serves both forms."""
+def _form_of(name):
+    """The form a starter kernel opens: the emitting needed-sums pass (slerp_need_kernel<IDT, D,
+    true, ODT>) and the co-located pass are the speculative form's; a non-emitting needed-sums or
+    triangle Gram pass the two-pass form's."""
     if name.startswith("slerp_pop_stats_lerp_kernel"):
         return "speculative"
-    if name.startswith("slerp_gram_kernel<"):
-        args = [a.strip() for a in name[len("slerp_gram_kernel<"):].split(">")[0].split(",")]
-        return "speculative" if len(args) >= 4 and args[3] == "true" else "two_pass"
-    return None
+    if name.startswith("slerp_need_kernel<"):
+        args = [x.strip() for x in name[len("slerp_need_kernel<"):].split(">")[0].split(",")]
+        return "speculative" if len(args) >= 3 and args[2] == "true" else "two_pass"
+    return "two_pass"
 
 
-def totals(root, counter):
-    """{form: summed counter} over the slerp kernels, attributed by dispatch order."""
+def calls(root, counter):
+    """[(form, summed counter)] per population call, in dispatch order: a call opens at the first
+    starter kernel after a blend (a component's passes of one call follow each other)."""
     rows = []
     for path in glob.glob(os.path.join(root, counter, "**", "*counter_collection.csv"), recursive=True):
         with open(path) as f:
@@ -46,33 +47,42 @@ def totals(root, counter):
                 if row.get("Counter_Name") != counter:
                     continue
                 name = row["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "")
-                if "slerp" in name:
+                if name.startswith(COUNTED):
                     rows.append((int(row.get("Dispatch_Id") or 0), name, float(row["Counter_Value"])))
-    out, form = {}, None
+    out, prev_blend = [], True
     for _, name, v in sorted(rows):
-        form = _form_starter(name) or form
-        if form and (name.startswith("slerp_gram_kernel") or name.startswith("slerp_blend")
-                     or name.startswith("slerp_pop_stats_lerp_kernel")):
-            out[form] = out.get(form, 0.0) + v
+        starter = name.startswith(STARTERS)
+        if starter and prev_blend:
+            out.append([_form_of(name), 0.0])
+        prev_blend = not starter
+        if out:
+            out[-1][1] += v
     return out
 
 
 def main():
     from evolutionarydistributedtraining_amd._lib import library_sha256
     root = sys.argv[1]
-    f, w = totals(root, "FETCH_SIZE"), totals(root, "WRITE_SIZE")
+    f, w = calls(root, "FETCH_SIZE"), calls(root, "WRITE_SIZE")
+    n_roulette = GENERATIONS * 2 * (1 + REPS)
     res = {}
-    for form, kernels in FORMS.items():
-        fetch = 2 * 1024 * f.get(form, 0.0) / CALLS
-        write = 1024 * w.get(form, 0.0) / CALLS
-        res[f"population_7b/{form}"] = {
-            "kernels": list(kernels), "calls": CALLS, "fetch_bytes_x2": fetch, "write_bytes": write,
-            "hbm_bytes_per_launch": int(round(fetch + write)),
-            "correction": "FETCH_SIZE x2, WRITE_SIZE x1, KiB -> bytes; per call = all launches / calls",
-            "lib_sha256": library_sha256()}
+    for tag, lo, hi in (("roulette", 0, n_roulette), ("ring", n_roulette, n_roulette + 2 * (1 + REPS))):
+        for form in ("speculative", "two_pass"):
+            fs = [v for fm, v in f[lo:hi] if fm == form]
+            ws = [v for fm, v in w[lo:hi] if fm == form]
+            if not fs or not ws:
+                continue
+            fetch = 2 * 1024 * sum(fs) / len(fs)
+            write = 1024 * sum(ws) / len(ws)
+            res[f"population_7b/{tag}/{form}"] = {
+                "calls": len(fs), "fetch_bytes_x2": fetch, "write_bytes": write,
+                "hbm_bytes_per_launch": int(round(fetch + write)),
+                "note": "per call (a generation); roulette: the mean over the drawn generations",
+                "correction": "FETCH_SIZE x2, WRITE_SIZE x1, KiB -> bytes",
+                "lib_sha256": library_sha256()}
     with open(os.path.join(root, "pmc_pop_traffic.json"), "w") as fo:
         json.dump(res, fo, indent=1)
-    print(json.dumps({k: [v["hbm_bytes_per_launch"], v["lib_sha256"][:12]] for k, v in res.items()}))
+    print(json.dumps({k: [v["hbm_bytes_per_launch"], v["calls"], v["lib_sha256"][:12]] for k, v in res.items()}))
 
 
 if __name__ == "__main__":

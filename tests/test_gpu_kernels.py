@@ -592,6 +592,35 @@ def test_slerp_population_pair_graphs_dtypes(dev, ops, graph, in_dt, out_dt):
             assert torch.equal(dots[q].cpu(), plan.dots[:len(sizes)].cpu()), (graph, speculate, q)
 
 
+@pytest.mark.parametrize("threads,vec", [(1, 32), (8, 32), (3, 16)])
+def test_list_step_with_tails_equals_flat_tail_step(dev, ops, threads, vec):
+    """edt_outer_step_list_tail (r5: the tensor-list step with per-tensor tail masks) equals
+    edt_outer_step_tail over the same values packed flat, bit for bit, two generations — tensors
+    of ragged sizes, one 4-byte-shifted (the scalar body), all-bf16 Nesterov."""
+    from evolutionarydistributedtraining_amd.torchcompat import torch_cpu_tail_bits, torch_cpu_tail_bits_per_tensor
+    g = torch.Generator().manual_seed(threads * 100 + vec)
+    numels = [70_001, 5, 31, 257 * 160, 33, 300_007, 1]
+    bf = torch.bfloat16
+    K = 3
+    thetas = [(torch.randn(n, generator=g) * 0.02).to(bf).to(dev) for n in numels]
+    buf = (torch.randn(numels[2] + 2, generator=g) * 0.02).to(bf).to(dev)
+    thetas[2] = buf[2:]                                     # off a 16-byte boundary: the scalar body
+    thetas[2].copy_((torch.randn(numels[2], generator=g) * 0.02).to(bf).to(dev))
+    workers = [[(t.float() + torch.randn(t.numel(), generator=g).to(dev) * 1e-3).to(bf) for t in thetas]
+               for _ in range(K)]
+    flat_theta = torch.cat([t.clone() for t in thetas])
+    flat_workers = [torch.cat(w) for w in workers]
+    moms = [torch.zeros(n, dtype=bf, device=dev) for n in numels]
+    flat_mom = torch.zeros(sum(numels), dtype=bf, device=dev)
+    tails = torch_cpu_tail_bits_per_tensor(numels, vec_elems=vec, num_threads=threads, device=dev)
+    flat_bits = torch_cpu_tail_bits(numels, vec_elems=vec, num_threads=threads, device=dev)
+    for gen in range(2):
+        ops.outer_step_list(thetas, workers, moms, gen > 0, 0.7, 0.9, True, tails=tails)
+        ops.outer_step(flat_theta, flat_workers, flat_mom, gen > 0, 0.7, 0.9, True, tail_bits=flat_bits)
+        assert torch.equal(bits(torch.cat(thetas).cpu()), bits(flat_theta.cpu())), gen
+        assert torch.equal(bits(torch.cat(moms).cpu()), bits(flat_mom.cpu())), gen
+
+
 @pytest.mark.parametrize("gdt,wdt", REGIMES)
 @pytest.mark.parametrize("n", [1, 8191, 70_001, 1_000_003])
 def test_pair_merge_population_matches_per_child(dev, ops, gdt, wdt, n):

@@ -345,6 +345,25 @@ def test_torch_tail_bits_match_the_oracle_mask(oracle, threads, vec):
     assert np.array_equal(got, mask) and not np.unpackbits(bits, bitorder="little")[mask.size:].any()
 
 
+@pytest.mark.parametrize("threads,vec", [(1, 32), (8, 32), (3, 16)])
+def test_torch_tail_bits_per_tensor_match_the_oracle_mask(oracle, threads, vec):
+    """torch_cpu_tail_bits_per_tensor (the tensor-list step's masks, r5): tensor t's bits start at
+    byte offs[t] and, indexed inside the tensor, are exactly the oracle's mask of that tensor."""
+    import numpy as np
+
+    from evolutionarydistributedtraining_amd.torchcompat import torch_cpu_tail_bits_per_tensor
+    numels = [70_001, 5, 0, 31, 257 * 160, 33, 1_000_003, 1]
+    mask = oracle.torch_cpu_tail_mask(numels, vec_elems=vec, num_threads=threads).numpy()
+    bits, offs = torch_cpu_tail_bits_per_tensor(numels, vec_elems=vec, num_threads=threads)
+    allbits = np.unpackbits(bits.numpy(), bitorder="little")
+    start = 0
+    for n, o in zip(numels, offs):
+        got = allbits[8 * o: 8 * o + n]
+        assert np.array_equal(got, mask[start:start + n])
+        start += n
+    assert offs == [sum(-(-m // 8) for m in numels[:t]) for t in range(len(numels))]
+
+
 def test_examples_import_and_model_runs_on_cpu():
     """examples/diloco_sim.py and examples/edt_sim.py import without a GPU; the tiny LM and its
     synthetic batches run on the CPU (the simulations themselves are GPU tests, test_gpu_sim.py)."""

@@ -71,22 +71,25 @@ def test_population_rejects_a_separate_momentum_dtype():
 
 
 def test_population_pmc_attribution_follows_dispatch_order(tmp_path):
-    """scripts/pmc_population.py: launches count toward the form whose call they belong to, by
-    dispatch order — the emitting ring pass (slerp_gram_kernel<.., true, true, ..>) or the co-located
-    pass opens a speculative call, a non-emitting Gram / ring pass a two-pass call; the member-major
-    blend (both forms) and everything after follow the call that opened it."""
+    """scripts/pmc_population.py: launches count toward the call they belong to, by dispatch order —
+    a call opens at the first pass after a blend (its components' passes follow each other); the
+    emitting needed-sums pass (slerp_need_kernel<.., true, ..>) or the co-located pass opens a
+    speculative call, a non-emitting needed-sums / triangle Gram pass a two-pass call; the
+    member-major blend (both forms) closes it. Other kernels are not counted."""
     import csv
     sys.path.insert(0, os.path.join(ROOT, "scripts"))
     import pmc_population as P
     launches = [  # (kernel, FETCH_SIZE)
-        ("void (anonymous namespace)::slerp_gram_kernel<1, 8, true, true, 1>(Members)", 100.0),
+        ("void (anonymous namespace)::slerp_need_kernel<1, 5, true, 1>(Members, NeedSpec)", 100.0),
+        ("void (anonymous namespace)::slerp_need_kernel<1, 2, true, 1>(Members, NeedSpec)", 20.0),
         ("(anonymous namespace)::slerp_gram_coef_kernel(double const*)", 1.0),
-        ("void (anonymous namespace)::slerp_blend_mm_kernel<1, 1, 8>(Members, PopBlend)", 0.5),
+        ("void (anonymous namespace)::slerp_blend_mm_kernel<1, 1, 5>(Members, PopBlend)", 0.5),
+        ("void (anonymous namespace)::slerp_blend_mm_kernel<1, 1, 2>(Members, PopBlend)", 0.25),
         ("void (anonymous namespace)::slerp_pop_stats_lerp_kernel<1, 1>(BlendChildren)", 10.0),
         ("void (anonymous namespace)::slerp_blend_population_kernel<1, 1>(BlendChildren)", 2.0),
-        ("void (anonymous namespace)::slerp_gram_kernel<1, 8, true, false, 1>(Members)", 50.0),
+        ("void (anonymous namespace)::slerp_need_kernel<1, 8, false, 1>(Members, NeedSpec)", 50.0),
         ("void (anonymous namespace)::slerp_blend_mm_kernel<1, 1, 8>(Members, PopBlend)", 70.0),
-        ("void (anonymous namespace)::slerp_gram_kernel<1, 8, false, false, 1>(Members)", 5.0),
+        ("void (anonymous namespace)::slerp_gram_kernel<1, 8>(Members)", 5.0),
         ("void at::native::copy_kernel(float)", 1000.0),
     ]
     d = tmp_path / "FETCH_SIZE" / "run"
@@ -96,5 +99,7 @@ def test_population_pmc_attribution_follows_dispatch_order(tmp_path):
         w.writeheader()
         for i, (name, v) in enumerate(launches):
             w.writerow({"Dispatch_Id": i + 1, "Kernel_Name": name, "Counter_Name": "FETCH_SIZE", "Counter_Value": v})
-    got = P.totals(str(tmp_path), "FETCH_SIZE")
-    assert got == {"speculative": 100.0 + 0.5 + 10.0 + 2.0, "two_pass": 50.0 + 70.0 + 5.0}
+    got = P.calls(str(tmp_path), "FETCH_SIZE")
+    assert got == [["speculative", 100.0 + 20.0 + 0.5 + 0.25], ["speculative", 10.0 + 2.0],
+                   ["two_pass", 50.0 + 70.0], ["two_pass", 5.0]]
+
