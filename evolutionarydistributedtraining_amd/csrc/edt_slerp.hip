@@ -2749,6 +2749,37 @@ int upload_seg_table(const void* const* v0_t, const void* const* v1_t, void* con
 
 extern "C" {
 
+// apart = 0 (the two-pass form): an output may be exactly one of its own parents (written in place
+// after the stats pass read it), never overlap another tensor's parent or output. Spans grouped by
+// identical byte range, then swept in address order: a group holding an output must belong to one
+// segment and overlap no other group; input-only groups may overlap each other.
+struct SegSpan {
+    uintptr_t a, e;
+    int seg;
+    bool out;
+};
+
+inline bool in_place_safe(std::vector<SegSpan>& sp) {
+    std::sort(sp.begin(), sp.end(), [](const SegSpan& x, const SegSpan& y) {
+        return x.a != y.a ? x.a < y.a : x.e < y.e;
+    });
+    uintptr_t far_any = 0, far_out = 0;
+    for (size_t i = 0; i < sp.size();) {
+        size_t j = i;
+        bool out = false, one_seg = true;
+        for (; j < sp.size() && sp[j].a == sp[i].a && sp[j].e == sp[i].e; ++j) {
+            out = out || sp[j].out;
+            one_seg = one_seg && sp[j].seg == sp[i].seg;
+        }
+        if (out && !one_seg) return false;                 // an output shared with another tensor's span
+        if (sp[i].a < far_out || (out && sp[i].a < far_any)) return false;   // a partial overlap with an output
+        far_any = sp[i].e > far_any ? sp[i].e : far_any;
+        if (out) far_out = sp[i].e > far_out ? sp[i].e : far_out;
+        i = j;
+    }
+    return true;
+}
+
 int edt_slerp_seg_table(const void* const* v0_t, const void* const* v1_t, void* const* out_t, int nseg,
                         const uint64_t* seg_numel, int in_dt, int out_dt, int apart, uint64_t* table_host) {
     g_err[0] = 0;
@@ -2779,6 +2810,21 @@ int edt_slerp_seg_table(const void* const* v0_t, const void* const* v1_t, void* 
     }
     if (apart && !spans_apart(sp))
         return fail(EDT_ERR_ARG, "an output overlaps a parent tensor: the single-pass form needs outputs apart");
+    if (!apart && seg_numel) {
+        std::vector<SegSpan> ss;
+        ss.reserve(3 * (size_t)nseg);
+        for (int i = 0; i < nseg; ++i) {
+            if (!seg_numel[i]) continue;
+            const uintptr_t p0 = reinterpret_cast<uintptr_t>(v0_t[i]), p1 = reinterpret_cast<uintptr_t>(v1_t[i]);
+            const uintptr_t po = reinterpret_cast<uintptr_t>(out_t[i]);
+            ss.push_back({p0, p0 + seg_numel[i] * isz, i, false});
+            ss.push_back({p1, p1 + seg_numel[i] * isz, i, false});
+            ss.push_back({po, po + seg_numel[i] * osz, i, true});
+        }
+        if (!in_place_safe(ss))
+            return fail(EDT_ERR_ARG, "an output overlaps another tensor's parent or output (only its own parent, "
+                                     "exactly, may be written in place)");
+    }
     return EDT_OK;
 }
 

@@ -413,8 +413,13 @@ def _rebind_merge(params, keys, outs, sd1, sd2, plan, out_dtype, dev, dot_thresh
     tt = torch.tensor([t for _, t in plan], dtype=torch.float64).to(dev)
     ops.SlerpListBinding.from_pointers(splan, p0, p1, po, in_dt, out_dtype, dev, keep=(buf, pairs)).merge(
         tt, dot_threshold, eps, ref_dot=_ref_dot)
+    cur = torch.cuda.current_stream(dev)
     with torch.no_grad():                                        # overlaps the kernels
         for k, o, a in zip(keys, outs, offs.tolist()):
+            # the parameter's old storage may be its last reference: the caching allocator must
+            # not hand the block out again before the merge queued on this stream has read it
+            # (it may have been allocated on another stream than the one the merge runs on)
+            params[k].data.record_stream(cur)
             params[k].data = buf.as_strided(o.shape, _contig_strides(o.shape), a)
     return True
 

@@ -699,17 +699,10 @@ class SlerpListBinding:
         numel = numel_arr.ctypes.data_as(ctypes.c_void_p) if T else None
         host = np.zeros(max(1, 3 * T), dtype=np.uint64)
         hp = host.ctypes.data_as(ctypes.c_void_p)
+        # every output apart from everything but its own parents (the two-pass form's rule, r5: in C)
         L.check(lib.edt_slerp_seg_table(a0, a1, a2, T, numel, self.in_dt, self.out_dt, 0, hp), "edt_slerp_seg_table")
         # outputs apart from every parent (a sorted-span check in C): the single-pass form is allowed
         self.apart = lib.edt_slerp_seg_table(a0, a1, a2, T, numel, self.in_dt, self.out_dt, 1, hp) == 0
-        if not self.apart:
-            # the two-pass form still needs every output apart from everything but its own parents
-            n = numel_arr.astype(np.int64)
-            sizes = np.stack([n * self.in_size, n * self.in_size, n * self.out_size], axis=1).reshape(-1)
-            starts = np.stack([arrs[0], arrs[1], arrs[2]], axis=1).reshape(-1).astype(np.int64)
-            if not writes_safe(starts, sizes):
-                raise L.EdtError("a SLERP output overlaps another tensor's parent or output: no form is safe "
-                                 "(an output may only be its own parent exactly)")
         self.table = torch.from_numpy(host.view(np.int64)).to(self.device)
 
     def merge(self, t: torch.Tensor, dot_threshold: float = 0.9995, eps: float = 1e-8,
@@ -953,7 +946,8 @@ def slerp_gram(members: list[torch.Tensor], chunks: torch.Tensor, nchunks: int,
     device, starts relative to the buffers): float64 [nchunks, M(M+1)/2] (edt_slerp_gram). `gram`
     (optional) receives the rows; its first nchunks x M(M+1)/2 elements are written. `work`
     (optional, float64, >= edt_slerp_population_gram_doubles(M, nchunks)): the pass's workspace
-    when `gram` cannot hold the row scratch too (default: the stream's pooled workspace)."""
+    when `gram` cannot hold the row scratch too (default: the stream's pooled workspace). Returns
+    `gram`, or without one a tensor the caller owns (a view of `work` when `work` was given)."""
     lib = L.lib()
     M = len(members)
     L.require_device(*members, chunks)
@@ -966,15 +960,19 @@ def slerp_gram(members: list[torch.Tensor], chunks: torch.Tensor, nchunks: int,
     # the kernel needs the rows plus its slot scratch behind them; a smaller (or non-contiguous)
     # `gram` — e.g. a rank's rows of the whole table — gets its rows copied from a full-size buffer
     direct = gram is not None and gram.is_contiguous() and gram.numel() >= need
+    pooled = False
     if direct:
         work = gram
     elif work is None or work.dtype != torch.float64 or not work.is_contiguous() or work.numel() < need:
         work = _scratch(members[0].device, need)
+        pooled = True
     L.check(lib.edt_slerp_gram(L.ptr_array(members), M, L.dtype_code(members[0]), L.ptr(chunks), nchunks,
                                L.ptr(work), L.stream_ptr(members[0].device)), "edt_slerp_gram")
     rows = work.view(-1)[:nchunks * NT].view(nchunks, NT) if not direct else gram
     if gram is None:
-        return rows
+        # rows in the stream's pooled workspace would be overwritten by the next SLERP call on this
+        # thread and stream: the caller gets its own copy (rows in a caller's `work` stay views)
+        return rows.clone() if pooled else rows
     if not direct:
         gram.view(-1)[:nchunks * NT].copy_(rows.view(-1))
     return gram

@@ -256,7 +256,11 @@ int edt_slerp_merge_speculative(const void* v0, const void* v1, int in_dt, void*
  * {v0, v1, out} pointers:
  *   edt_slerp_seg_table   (HOST) validates the arrays (alignment; with `apart`, no output byte
  *                         range [out, out + n*osize) overlaps any parent range — a sorted-span
- *                         check over every tensor, seg_numel = the nseg sizes) and writes the
+ *                         check over every tensor, seg_numel = the nseg sizes; r5: without
+ *                         `apart` but with seg_numel, an output may be exactly one of its OWN
+ *                         parents and must overlap no other tensor's parent or output — the
+ *                         two-pass blend would race; seg_numel NULL skips the check and the
+ *                         caller guarantees it) and writes the
  *                         table's host image (3 x nseg uint64). The caller uploads it once and
  *                         reuses it while the tensors stay where they are: the *_table entries
  *                         below then cost no per-tensor host work per call.

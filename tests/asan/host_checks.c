@@ -136,7 +136,7 @@ static void sync_host_paths(void) {
     EXPECT_FAIL(edt_outer_step_ws(d, 0, w65, 0, 65, d, 0, 100, 0.7, 0.9, 1, NULL, NULL));
     void* tt[2] = {d, d};
     const uint64_t numel[2] = {100, 0};
-    EXPECT(edt_outer_list_workspace_bytes(2, 3) == (4 * 2 + 1 + 3 * 2) * 8);
+    EXPECT(edt_outer_list_workspace_bytes(2, 3) == (5 * 2 + 1 + 3 * 2) * 8);   /* r5: + the tail offsets */
     EXPECT_FAIL(edt_outer_step_list(tt, 0, w65, 0, 3, tt, 1, numel, 2, 0.7, 0.9, 1, NULL, 0, NULL));
     EXPECT_FAIL(edt_outer_step_list(tt, 0, w65, 0, 3, tt, 1, numel, 2, 0.7, 0.9, 1, d, 8, NULL));
     const void* nullw[6] = {d, NULL, d, d, d, d};
@@ -168,6 +168,41 @@ static void sync_host_paths(void) {
     EXPECT_FAIL(edt_slerp_blend_children(mem2, 2, 1, pairs, 17, outs17, 1, (const uint64_t*)d, 1, coef, 1, NULL));
     EXPECT_FAIL(edt_slerp_merge_speculative(d, dummy + 8, 1, dummy + 4, 1, (const uint64_t*)d, 1, first, 1, tv,
                                             0.9995, 1e-8, (double*)d, coef, NULL, (int32_t*)d, 100, NULL));
+    /* r5: the list step's tail masks need a bf16 master and byte offsets */
+    const uint64_t toff[2] = {0, 13};
+    EXPECT_FAIL(edt_outer_step_list_tail(tt, 0, w65, 0, 3, tt, 1, numel, 2, 0.7, 0.9, 1, (const uint8_t*)d, toff,
+                                         d, 1024, NULL));
+    EXPECT_FAIL(edt_outer_step_list_tail(tt, 1, w65, 1, 3, tt, 1, numel, 2, 0.7, 0.9, 1, (const uint8_t*)d, NULL,
+                                         d, 1024, NULL));
+    /* r5: the population planner (host only) — roulette-like graphs, the fallbacks, bad input */
+    char buf[4096];
+    const int32_t rl[16] = {0, 5, 5, 2, 0, 1, 5, 2, 6, 3, 6, 7, 5, 3, 7, 2};
+    EXPECT(edt_slerp_population_layout(rl, 8, 8, 1, buf, (int)sizeof(buf)) == 0);
+    EXPECT(strstr(buf, "\"member-major\"") != NULL && strstr(buf, "\"needed\"") != NULL);
+    int32_t k5[20];
+    int nk = 0;
+    for (int a = 0; a < 5; ++a)
+        for (int b = a + 1; b < 5; ++b) { k5[2 * nk] = a; k5[2 * nk + 1] = b; ++nk; }
+    EXPECT(edt_slerp_population_layout(k5, nk, 5, 1, buf, (int)sizeof(buf)) == 0);
+    EXPECT(strstr(buf, "\"co-located\"") != NULL && strstr(buf, "\"triangle\"") != NULL);
+    EXPECT_FAIL(edt_slerp_population_layout(rl, 8, 4, 1, buf, (int)sizeof(buf)));   /* member 5 of 4 */
+    EXPECT_FAIL(edt_slerp_population_layout(rl, 8, 8, 1, buf, 16));                  /* short buffer */
+    EXPECT_FAIL(edt_slerp_population_layout(rl, 8, 8, 1, NULL, 16));
+    /* r5: edt_slerp_seg_table's in-place rule (apart = 0 with sizes): an output may be exactly its
+     * own parent, never overlap another tensor's parent or output */
+    uint64_t host[6];
+    const uint64_t n2[2] = {16, 16};
+    const void* v0s[2] = {dummy, dummy + 64};
+    const void* v1s[2] = {dummy + 128, dummy + 192};
+    void* own[2] = {dummy, dummy + 192};                      /* in place: tensor 0 into v0, 1 into v1 */
+    EXPECT(edt_slerp_seg_table(v0s, v1s, own, 2, n2, 0, 0, 0, host) == 0);
+    void* other[2] = {dummy + 64, dummy + 256};               /* tensor 0 written over tensor 1's parent */
+    EXPECT_FAIL(edt_slerp_seg_table(v0s, v1s, other, 2, n2, 0, 0, 0, host));
+    void* partial[2] = {dummy + 8, dummy + 256};              /* across its own parent, not exactly it */
+    EXPECT_FAIL(edt_slerp_seg_table(v0s, v1s, partial, 2, n2, 0, 0, 0, host));
+    void* same[2] = {dummy + 256, dummy + 256};               /* two outputs on one buffer */
+    EXPECT_FAIL(edt_slerp_seg_table(v0s, v1s, same, 2, n2, 0, 0, 0, host));
+    EXPECT(edt_slerp_seg_table(v0s, v1s, other, 2, NULL, 0, 0, 0, host) == 0);   /* no sizes: caller's duty */
 }
 
 static void comm_host_paths(void) {

@@ -469,8 +469,9 @@ def test_slerp_list_speculative_matches_two_pass(dev, ops, in_dt, out_dt):
                 1e-8, L.ptr(lplan.partial), L.ptr(lplan.coef), None, L.ptr(redo), L.ptr(ws), ws.numel() * 8,
                 L.stream_ptr(dev))
             assert rc != 0 and b"overlaps a parent" in L.lib().edt_last_error()
-            # the Python binding refuses it for the two-pass form as well (its blend would race)
-            with pytest.raises(L.EdtError, match="no form is safe"):
+            # refused for the two-pass form as well (its blend would race): edt_slerp_seg_table's
+            # in-place rule (r5, in C) — an output may only be exactly its own parent
+            with pytest.raises(L.EdtError, match="overlaps another tensor's parent or output"):
                 ops.slerp_list(lplan, a0, a1, outs_x, ts)
 
 

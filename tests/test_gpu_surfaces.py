@@ -288,9 +288,11 @@ def test_single_tensor_slerp_api(golden, dev):
 
 
 def test_dir_outer_sync_two_generations(oracle, dev, tmp_path):
-    """DirOuterSync: checkpoint dirs in, fused step, checkpoint dirs out (EDT_LM/diloco.py:224-308),
-    two generations with the momentum carried across a master restart (state_path), vs the
-    oracle; outputs load with HF."""
+    """DirOuterSync with its DEFAULT arguments (so the one-time momentum placement search of
+    place_momentum=8 runs after the first step): checkpoint dirs in, fused step, checkpoint dirs out
+    (EDT_LM/diloco.py:224-308), two generations with the momentum carried across a master restart
+    (state_path), bit-identical to the oracle — theta every generation, the momentum at the end;
+    outputs load with HF."""
     from transformers import LlamaForCausalLM
     from evolutionarydistributedtraining_amd.diloco import DirOuterSync
     from evolutionarydistributedtraining_amd.params import ParamLayout, pack
@@ -321,6 +323,7 @@ def test_dir_outer_sync_two_generations(oracle, dev, tmp_path):
             sync = DirOuterSync(device=dev, names=layout.names, lr=0.7, momentum=0.9, nesterov=True,
                                 state_path=state_path)
         sync.step(prev, dirs)
+        assert sync.placement is not None          # the default search ran (and moved nothing's values)
         oracle.outer_step(theta, workers, mom, gen > 0, 0.7, 0.9, True)
         for d in dirs:
             got = LlamaForCausalLM.from_pretrained(d, dtype=torch.bfloat16)
