@@ -717,7 +717,48 @@ def bench_list_form(args, dev):
         res[key] = rec
         del thetas, workers, state, step
     _free_device()
+    res["same_memory"] = _list_vs_arena_same_memory(args, dev, lay, K)
+    _free_device()
     return res
+
+
+def _list_vs_arena_same_memory(args, dev, lay, K, rounds=3):
+    """The list kernel against the arena kernel on the SAME bytes (scripts/list_vs_arena_probe.py):
+    one set of flat arenas (theta, K workers, momentum) timed as edt_outer_step over the arenas and
+    as edt_outer_step_list over per-tensor views of them, interleaved rounds, median of rounds —
+    what separates list_form's first-allocation frac from the arena's is then where the allocator
+    put the streams, not the list kernel (r5: equal within 0.5 %)."""
+    import statistics
+    from evolutionarydistributedtraining_amd import ops
+    from evolutionarydistributedtraining_amd.torchcompat import torch_cpu_tail_bits, torch_cpu_tail_bits_per_tensor
+    P, out = lay.total, {}
+    lr, mu, nest = args.lr, args.momentum, bool(args.nesterov)
+    for key, dt in (("f32", torch.float32), ("bf16", torch.bfloat16)):
+        _free_device()
+        g = torch.Generator(device=dev).manual_seed(5)
+        theta = (torch.randn(P, generator=g, device=dev) * 0.02).to(dt)
+        workers = [(theta.float() + torch.randn(P, generator=g, device=dev) * 1e-3).to(dt) for _ in range(K)]
+        mom = torch.zeros(P, dtype=dt, device=dev)
+        tv, wv, mv = lay.views(theta), [lay.views(w) for w in workers], lay.views(mom)
+        forms = {"arena_ms": lambda: ops.outer_step(theta, workers, mom, True, lr, mu, nest),
+                 "list_ms": lambda: ops.outer_step_list(tv, wv, mv, True, lr, mu, nest)}
+        if dt == torch.bfloat16:
+            flat_bits = torch_cpu_tail_bits(lay.numels, 32, 8, device=dev)
+            tails = torch_cpu_tail_bits_per_tensor(lay.numels, 32, 8, device=dev)
+            forms["arena_tails_ms"] = lambda: ops.outer_step(theta, workers, mom, True, lr, mu, nest, tail_bits=flat_bits)
+            forms["list_tails_ms"] = lambda: ops.outer_step_list(tv, wv, mv, True, lr, mu, nest, tails=tails)
+        ms = {k: [] for k in forms}
+        for _ in range(rounds):
+            for k, fn in forms.items():
+                ms[k].append(_event_ms(fn, 10, 1))
+        rec = {k: round(statistics.median(v), 4) for k, v in ms.items()}
+        rec["list_over_arena"] = round(rec["list_ms"] / rec["arena_ms"], 4)
+        if "list_tails_ms" in rec:
+            rec["list_tails_over_arena_tails"] = round(rec["list_tails_ms"] / rec["arena_tails_ms"], 4)
+        out[key] = rec
+        del theta, workers, mom, tv, wv, mv, forms
+    out["note"] = f"flat arenas + per-tensor views of them, {rounds} interleaved rounds x 10 event-timed calls, median"
+    return out
 
 
 def bench_pair_merge(args, dev):

@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(PKG_DIR, "libedt_sync.so")
 EDT_F32 = 0
 EDT_BF16 = 1
 EDT_MAX_WORKERS = 64
-EDT_ABI_VERSION = 4         # include/edt_sync.h: the revision these signatures and workspace sizes follow
+EDT_ABI_VERSION = 5         # include/edt_sync.h: the revision these signatures and workspace sizes follow
 
 _DT = {torch.float32: EDT_F32, torch.bfloat16: EDT_BF16}
 

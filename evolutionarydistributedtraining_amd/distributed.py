@@ -570,6 +570,7 @@ class ShardedPopulationCrossover:
         children equal the reference's merges bit for bit with band < 0. Returns (coef [Q, nseg, 2],
         dots [Q, nseg]) on the device."""
         import numpy as np
+        ref.check_host()
         k, N, Q = self.kernels, self.world, len(pairs)
         plan, nseg = self.plan, self.plan.nseg
         host = np.asarray(plan.chunks_host, dtype=np.int64).reshape(-1, 3)

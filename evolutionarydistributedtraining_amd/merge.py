@@ -386,13 +386,14 @@ def _pair_pointers(pairs, dev):
     return p0, p1, np.array(ns, dtype=np.int64), dt
 
 
-def _rebind_merge(params, keys, outs, sd1, sd2, plan, out_dtype, dev, dot_threshold, eps) -> bool:
+def _rebind_merge(params, keys, outs, sd1, sd2, plan, out_dtype, dev, dot_threshold, eps, bound=None) -> bool:
     """slerp_into_module_'s single-pass form, when it applies: the children written to ONE fresh
     buffer (16-byte aligned starts, addresses computed before any view of it exists), the merge
     launched, and only then — while the device runs it — the views carved and the parameters
     re-pointed at them. False (nothing done) when the form does not apply: a parent not addressable
     in place, an output dtype other than the merge's (a mixed-dtype module keeps its tensors), or
-    outputs apart from both parents (written in place in one pass already)."""
+    outputs apart from both parents (written in place in one pass already). `bound` (a dict, the
+    surface cache): receives what a repeat of this merge needs (_Bound)."""
     if any(o.dtype != out_dtype for o in outs):
         return False
     pairs = [(sd1[k], sd2[k]) for k in keys]
@@ -421,11 +422,15 @@ def _rebind_merge(params, keys, outs, sd1, sd2, plan, out_dtype, dev, dot_thresh
             # (it may have been allocated on another stream than the one the merge runs on)
             params[k].data.record_stream(cur)
             params[k].data = buf.as_strided(o.shape, _contig_strides(o.shape), a)
+    if bound is not None:
+        bound.update(keys=keys, ts=[t for _, t in plan], tt=tt, splan=splan, ns=ns, offs=offs, total=total,
+                     in_dt=in_dt, out_dt=out_dtype, p0=po, p1=p1, buf=buf, shapes=[o.shape for o in outs],
+                     hold2=[b.data for _, b in pairs])
     return True
 
 
 def slerp_into_module_(module: torch.nn.Module, sd1: dict, sd2: dict, plan, out_dtype, device=None,
-                       dot_threshold=0.9995, eps=1e-8, params: dict | None = None) -> None:
+                       dot_threshold=0.9995, eps=1e-8, params: dict | None = None, bound: dict | None = None) -> None:
     """== module.load_state_dict(SLERP of sd1 / sd2 per plan) (EDT_EVOMERGE/train/crossover.py:142),
     in the fewest passes over HBM. When the module's own tensors are a parent's (the reference
     merges into model_1 itself) and everything is device-resident, the children are written to a
@@ -443,10 +448,86 @@ def slerp_into_module_(module: torch.nn.Module, sd1: dict, sd2: dict, plan, out_
         outs = [tsd[k] for k in keys]
     dev = device or _compute_device(*[t for k in keys for t in (sd1[k], sd2[k])])
     if tsd is None and dev.type == "cuda" and keys and _rebind_merge(
-            params, keys, outs, sd1, sd2, plan, out_dtype, dev, dot_threshold, eps):
+            params, keys, outs, sd1, sd2, plan, out_dtype, dev, dot_threshold, eps, bound):
         return
     slerp_state_dicts(sd1, sd2, plan, out_dtype=out_dtype, device=device, dot_threshold=dot_threshold,
                       eps=eps, out=tsd if tsd is not None else dict(zip(keys, outs)))
+
+
+class _Bound:
+    """What merge_models_into_ needs to repeat a merge of model_2 into model_1 without host work
+    before the launch (VERDICT r4 Next 3): the key plan and its device t, the chunk plan, the
+    parents' addresses and sizes, the packing of the fresh output buffer — and strong references
+    to the memory those addresses point at (model_1's tensors are views of `buf`, the previous
+    merge's output; `hold2`: model_2's tensors), so a launch over the cached addresses only ever
+    reads live memory of the recorded sizes, whatever the modules did meanwhile. Whether the
+    modules still hold exactly these tensors is checked while the device runs the merge
+    (_bound_merge); the entry dies with either module (weak references)."""
+
+    def __init__(self, key, model_1, model_2, dev, rec):
+        import weakref
+        self.key, self.dev = key, dev
+        drop = lambda _r, key=key: _bound_cache.pop(key, None)
+        self.r1, self.r2 = weakref.ref(model_1, drop), weakref.ref(model_2, drop)
+        for k, v in rec.items():
+            setattr(self, k, v)
+        self.all_keys = list(rec["all_keys"])
+        self.offs_bytes = self.offs.astype(np.uint64) * np.uint64(torch.empty(0, dtype=self.out_dt).element_size())
+        self.offs_list = self.offs.tolist()
+        self.strides = [_contig_strides(s) for s in self.shapes]
+
+
+_bound_cache: dict = {}
+
+
+def clear_merge_cache() -> None:
+    """Drop merge_models_into_'s cached bindings (and the references they hold)."""
+    if _bound_cache and torch.cuda.is_available():
+        torch.cuda.synchronize()                 # merges in flight may still read the held memory
+    _bound_cache.clear()
+
+
+def _bound_key(target, model_1, model_2, merge_config_dict, num_layers, dev):
+    import json
+    return (id(target), id(model_1), id(model_2), num_layers, str(dev),
+            json.dumps(merge_config_dict, sort_keys=True, default=str))
+
+
+def _bound_merge(b: _Bound, model_1, model_2) -> bool:
+    """The cached merge: a fresh output buffer, the binding over the cached addresses, the launch —
+    then, while the device runs it, the check that the modules still hold exactly the bound
+    tensors (the walk, keys, Parameters, addresses, sizes, dtypes: what the uncached path reads
+    before its launch) and the re-pointing of model_1's parameters at the new buffer. False
+    (nothing re-pointed, the entry dropped, the output discarded) when anything changed: the
+    caller merges the uncached way."""
+    buf = torch.empty(b.total, dtype=b.out_dt, device=b.dev)
+    po = np.uint64(buf.data_ptr()) + b.offs_bytes
+    ops.SlerpListBinding.from_pointers(b.splan, b.p0, b.p1, po, b.in_dt, b.out_dt, b.dev,
+                                       keep=(buf, b.buf, b.hold2)).merge(b.tt, ref_dot=_ref_dot)
+    cur = torch.cuda.current_stream(b.dev)
+    sd1 = module_tensors(model_1)
+    sd2 = module_tensors(model_2)
+    ok = isinstance(sd1, dict) and list(sd1.keys()) == b.all_keys and all(
+        isinstance(sd1[k], torch.nn.Parameter) for k in b.keys)
+    if ok:
+        pairs = [(sd1[k], sd2.get(k)) for k in b.keys]
+        ok = all(y is not None for _, y in pairs)
+    if ok:
+        meta = _pair_pointers(pairs, b.dev)
+        ok = (meta is not None and meta[3] == b.in_dt and np.array_equal(meta[0], b.p0)
+              and np.array_equal(meta[1], b.p1) and np.array_equal(meta[2], b.ns)
+              and [a.shape for a, _ in pairs] == b.shapes and next(model_1.parameters()).dtype == b.out_dt)
+    if not ok:
+        cur.synchronize()                       # the launch read the held memory: let it finish
+        _bound_cache.pop(b.key, None)
+        return False
+    with torch.no_grad():                        # overlaps the kernels
+        for k, shp, st, off in zip(b.keys, b.shapes, b.strides, b.offs_list):
+            p = sd1[k]
+            p.data.record_stream(cur)
+            p.data = buf.as_strided(shp, st, off)
+    b.p0, b.buf = po, buf
+    return True
 
 
 def merge_models_into_(target: torch.nn.Module, model_1: torch.nn.Module, model_2: torch.nn.Module,
@@ -454,18 +535,35 @@ def merge_models_into_(target: torch.nn.Module, model_1: torch.nn.Module, model_
     """EDT_EVOMERGE/train/crossover.py:114-142 without the save: the SLERP of model_1 / model_2's
     state (the key plan of merge_config_dict over num_layers) loaded into `target` (which may be
     model_1 itself, as the reference passes it): slerp_into_module_ when the keys match, else
-    load_state_dict of the merged dict (which reports the mismatch as the reference's does)."""
+    load_state_dict of the merged dict (which reports the mismatch as the reference's does).
+
+    Merging into model_1 again with the same model_2 and config (a resident population's next
+    generation) repeats the previous call's binding (_Bound): no module walk, key plan, per-tensor
+    check, t upload or chunk-plan lookup before the launch — those checks run while the device
+    merges, and a module that changed in between falls back to the uncached merge."""
+    dev = torch.device(device) if device not in (None, "cpu") else None
+    key = None
+    if target is model_1 and model_2 is not model_1:
+        key = _bound_key(target, model_1, model_2, merge_config_dict, num_layers, dev)
+        b = _bound_cache.get(key)
+        if b is not None and b.r1() is model_1 and b.r2() is model_2 and _bound_merge(b, model_1, model_2):
+            return
     sd1 = module_tensors(model_1)
     sd2 = sd1 if model_2 is model_1 else module_tensors(model_2)
     plan = merge_plan(list(sd1.keys()), num_layers, merge_config_dict)
     out_dtype = next(target.parameters()).dtype
-    dev = torch.device(device) if device not in (None, "cpu") else None
     tparams = sd1 if target is model_1 and isinstance(sd1, dict) else None
     tkeys = set(tparams) if tparams is not None else set(module_tensors(target))
     if tkeys == {k for k, _ in plan}:
-        slerp_into_module_(target, sd1, sd2, plan, out_dtype, device=dev,
-                           params=tparams if tparams is not None and all(
-                               isinstance(v, torch.nn.Parameter) for v in tparams.values()) else None)
+        is_params = tparams is not None and all(isinstance(v, torch.nn.Parameter) for v in tparams.values())
+        rec = {} if key is not None and is_params else None
+        slerp_into_module_(target, sd1, sd2, plan, out_dtype, device=dev, params=tparams if is_params else None,
+                           bound=rec)
+        if rec:                                   # the single-pass rebind ran: remember it
+            rec["all_keys"] = list(sd1.keys())
+            if len(_bound_cache) >= 4:
+                _bound_cache.pop(next(iter(_bound_cache)))
+            _bound_cache[key] = _Bound(key, model_1, model_2, rec["tt"].device, rec)
     else:
         target.load_state_dict(slerp_state_dicts(sd1, sd2, plan, out_dtype=out_dtype, device=dev))
 

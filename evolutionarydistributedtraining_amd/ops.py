@@ -331,6 +331,47 @@ def make_slerp_plan(seg_offsets: list[int], device: torch.device,
                      int(chunk_elems))
 
 
+# The host the reference-dot mode reproduces: the one tests/golden/ was recorded on
+# (tests/golden/refdot_host.json, tests/golden/gen_refdot_host.py).
+REFDOT_DOT_KERNEL = "openblas 0.3.29 SkylakeX"
+REFDOT_COEF_DISPATCH = (("arccos", "AVX512_SKX"), ("sin", "AVX512_SKX"))
+_REFDOT_CHECKED: set = set()
+
+
+class RefDotHostWarning(UserWarning):
+    """The running host's numpy dispatch or BLAS core differs from the reference-dot mode's."""
+
+
+_HOST_DISPATCH = None
+
+
+def host_dispatch() -> dict:
+    """The running host's side of the reference-dot mode (cached): numpy's version, the SIMD target
+    its float32 arccos / sin loops dispatch to (numpy.lib.introspect.opt_func_info; the
+    NPY_DISABLE_CPU_FEATURES / CPU features of this process), and numpy's BLAS core as
+    "<internal api> <version> <architecture>" (threadpoolctl; None when not importable)."""
+    global _HOST_DISPATCH
+    if _HOST_DISPATCH is None:
+        import numpy as np
+        from numpy.lib import introspect
+        disp = {}
+        for f in ("arccos", "sin"):
+            info = introspect.opt_func_info(func_name=f"^{f}$", signature="float32").get(f, {})
+            disp[f] = next(iter(info.values()), {}).get("current")
+        blas, threads = None, None
+        try:
+            from threadpoolctl import threadpool_info
+            for lib in threadpool_info():
+                if lib.get("user_api") == "blas" and "numpy" in str(lib.get("filepath", "")):
+                    blas = f"{lib.get('internal_api')} {lib.get('version')} {lib.get('architecture')}"
+                    threads = lib.get("num_threads")
+                    break
+        except ImportError:
+            pass
+        _HOST_DISPATCH = {"numpy": np.__version__, "coef_dispatch": disp, "blas": blas, "blas_threads": threads}
+    return _HOST_DISPATCH
+
+
 @dataclass(frozen=True)
 class RefDot:
     """Reference-dot mode (include/edt_sync.h, edt_slerp_refdot): segments whose fp64 dot lies
@@ -342,9 +383,49 @@ class RefDot:
     (reference_coefficients). With band < 0 the merge is the reference's, bit for bit. Without it
     (the default) the kernels decide from their fp64 dot, the accurate one, and form the
     coefficients on the device. Every SLERP form takes it (arena, tensor list,
-    population, sharded population); it synchronises the host once per merge."""
+    population, sharded population); it synchronises the host once per merge.
+
+    The mode reproduces ONE host: `dot_kernel` is the BLAS dot restated on the device and
+    `coef_dispatch` the SIMD targets numpy's float32 arccos / sin loops dispatch to there (the
+    targets compute different bits: AVX512_SKX's SVML arccos and the baseline libm one differ on
+    ~70 % of dots). The defaults are the host tests/golden/ was recorded on
+    (tests/golden/refdot_host.json). At first use the running host (host_dispatch()) is compared
+    with them: a difference warns (RefDotHostWarning) — or raises with strict=True — since the
+    coefficients would then not be the reference's bits on this host."""
     threads: int = 1
     band: float = -1.0
+    dot_kernel: str = REFDOT_DOT_KERNEL
+    coef_dispatch: tuple = REFDOT_COEF_DISPATCH
+    strict: bool = False
+
+    def host_mismatch(self) -> list[str]:
+        """What differs between the running host and the host this mode reproduces ([] = none)."""
+        host = host_dispatch()
+        out = [f"numpy float32 {f} dispatches to {host['coef_dispatch'].get(f)}, the modelled host's to {want}"
+               for f, want in self.coef_dispatch if host["coef_dispatch"].get(f) != want]
+        blas = host.get("blas")
+        if blas is not None and blas != self.dot_kernel:
+            out.append(f"numpy's BLAS dot is {blas}, the mode restates {self.dot_kernel}")
+        return out
+
+    def describe(self) -> dict:
+        """The modelled host, the running one and whether they agree (for logs and bench lines)."""
+        return {"dot_kernel": self.dot_kernel, "threads": self.threads, "coef_dispatch": dict(self.coef_dispatch),
+                "host": host_dispatch(), "mismatch": self.host_mismatch()}
+
+    def check_host(self) -> None:
+        """Warn (strict: raise EdtError) once per setting when the running host differs."""
+        key = (self.dot_kernel, self.coef_dispatch, self.strict)
+        if key in _REFDOT_CHECKED:
+            return
+        bad = self.host_mismatch()
+        if bad and self.strict:
+            raise L.EdtError("reference-dot mode: this host is not the one it reproduces: " + "; ".join(bad))
+        _REFDOT_CHECKED.add(key)
+        if bad:
+            import warnings
+            warnings.warn("reference-dot mode: this host differs from the modelled one, the coefficients may not "
+                          "be the reference's bits here: " + "; ".join(bad), RefDotHostWarning, stacklevel=3)
 
 
 def reference_coefficients(dots, t, dot_threshold: float = 0.9995):
@@ -388,6 +469,7 @@ def _ref_dots(plan: SlerpPlan, dots: torch.Tensor, ref: RefDot, in_dt: int, dot_
     recompute their dot the reference's way over (v0, v1) arenas or a tensor-list table. Returns the
     (flag int32, value float32) device tensors; nothing is synchronised."""
     lib = L.lib()
+    ref.check_host()
     dev, st = dots.device, L.stream_ptr(dots.device)
     ws = _refdot_ws(plan, ref, dev)
     flag = torch.empty(max(1, plan.nseg), dtype=torch.int32, device=dev)

@@ -24,13 +24,16 @@
 
 #include <stdint.h>
 
-/* ABI revision. 4 (round 4): the tensor-list SLERP reads a device pointer table
+/* ABI revision. 5 (round 5): the tensor-list outer step's workspace grew (per-tensor tail-mask
+ * offsets; edt_outer_list_workspace_bytes), edt_outer_step_list_tail and
+ * edt_slerp_population_layout added, edt_slerp_seg_table refuses in-place outputs that overlap
+ * another tensor. 4 (round 4): the tensor-list SLERP reads a device pointer table
  * (edt_slerp_seg_table + the *_table entries), edt_slerp_merge_list_speculative takes the segment
  * sizes (full byte-range overlap check), edt_slerp_blend_segments / _blend_table / _refdot_table
  * added, the on-chip-hold form removed. Workspace sizes come from the *_doubles / *_bytes functions
  * of THIS build: a consumer compiled against another revision must be rebuilt
  * (edt_abi_version() != EDT_ABI_VERSION: refuse to run). */
-#define EDT_ABI_VERSION 4
+#define EDT_ABI_VERSION 5
 
 #ifdef __cplusplus
 extern "C" {
@@ -318,9 +321,11 @@ int edt_slerp_blend_segments(const void* v0, const void* v1, int in_dt, void* ou
  * member arenas forms every parent's squared norm and the dots the children need per chunk, then
  * per child the coefficients (from pairs[2q], pairs[2q+1] = member indices, host array) and the
  * blend into outs[q] (host array of device pointers; no output may alias a member). The stats pass
- * runs per connected component of the children's pair graph: a path or cycle of >= 3 parents (a
- * ring of children, a matching) forms its 2M norms and ring dots, any other component the Gram
- * upper triangle (r4); each parent is read once either way. `gram`:
+ * runs per connected component of the children's pair graph (r5, any graph the reference's
+ * roulette selection draws): a component of D <= 8 parents forms its D norms and only the dots its
+ * children use — the edges of the best cyclic order of the parents (the ring) plus up to 4 chord
+ * slots (2 at D = 4, none below) — and falls back to the full Gram upper triangle when the children
+ * need more dots than that; each parent is read once either way. `gram`:
  * edt_slerp_population_gram_doubles(nmembers, nchunks) doubles of device workspace (layout
  * internal to this call; edt_slerp_gram below keeps the triangle layout). Each child's sums,
  * coefficients and output are bit-identical to edt_slerp_merge on (members[i], members[j]).
@@ -331,12 +336,13 @@ int edt_slerp_population(const void* const* members, int nmembers, int in_dt, co
                          const int32_t* seg_first_chunk, int nseg, const double* t, double dot_threshold,
                          double eps, double* gram, float* coef, float* dot_out, void* stream);
 
-/* edt_slerp_population with edt_slerp_merge_speculative's first pass: one co-located launch
- * (every child of a chunk on one XCD, shared parents read once) forms each child's chunk sums and
- * writes its lerp-branch output; per child the coefficients flag (redo: [npairs][nseg] int32) the
- * SLERP-branch segments, which one co-located launch blends again (it exits at once when no child
- * needs any). (A member-major first pass measured slower with the canonical sum order and was
- * removed: DESIGN §6.9.)
+/* edt_slerp_population with edt_slerp_merge_speculative's first pass, which also writes every
+ * child's lerp-branch output: when every component takes the needed-sums layout and npairs <= 16,
+ * one member-major launch per component (each parent read once, every child emitted from the
+ * parents' registers: ring-edge children directly, the others from a chord slot or a copy);
+ * otherwise one co-located launch (every child of a chunk on one XCD, shared parents read once).
+ * Per child the coefficients flag (redo: [npairs][nseg] int32) the SLERP-branch segments, which
+ * one launch blends again (it exits at once when no child needs any).
  * partial: edt_slerp_population_speculative_doubles(npairs, nchunks) doubles of workspace.
  * Outputs must not overlap any member (n elements each). Bit-identical to edt_slerp_merge per
  * child either way. */

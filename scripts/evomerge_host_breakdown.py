@@ -84,7 +84,52 @@ def main():
         steps.setdefault("device (events)", []).append(e0.elapsed_time(e1))
     res = {k: round(statistics.median(v[1:]), 4) for k, v in steps.items()}
     pre = sum(v for k, v in res.items() if k not in ("wall", "device (events)", "views + re-pointing (after the launch)"))
-    print(json.dumps({"probe": "evomerge_host_breakdown", "median_ms": res, "host_before_launch_ms": round(pre, 4)}))
+
+    # the repeat of the merge through merge_models_into_'s cached binding (merge._Bound), its steps
+    # one by one as merge._bound_merge runs them
+    merge.clear_merge_cache()
+    merge.merge_models_into_(m1, m1, m2, mcfg, cfg.num_hidden_layers, device=dev)
+    torch.cuda.synchronize()
+    steps = {}
+    for r in range(a.rounds + 1):
+        torch.cuda.synchronize()
+        t0 = t_start = time.perf_counter()
+        key = merge._bound_key(m1, m1, m2, mcfg, cfg.num_hidden_layers, dev)
+        b = merge._bound_cache[key]
+        assert b.r1() is m1 and b.r2() is m2
+        t0 = t("cache key + lookup", t0)
+        buf = torch.empty(b.total, dtype=b.out_dt, device=b.dev)
+        po = np.uint64(buf.data_ptr()) + b.offs_bytes
+        t0 = t("fresh buffer", t0)
+        bd = ops.SlerpListBinding.from_pointers(b.splan, b.p0, b.p1, po, b.in_dt, b.out_dt, b.dev, keep=(buf, b.buf, b.hold2))
+        t0 = t("binding (C checks + table upload)", t0)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        bd.merge(b.tt)
+        e1.record()
+        t0 = t("merge launches", t0)
+        sd1, sd2 = merge.module_tensors(m1), merge.module_tensors(m2)
+        pairs = [(sd1[k], sd2[k]) for k in b.keys]
+        meta = merge._pair_pointers(pairs, b.dev)
+        ok = np.array_equal(meta[0], b.p0) and np.array_equal(meta[1], b.p1)
+        t0 = t("module check (after the launch)", t0)
+        cur = torch.cuda.current_stream(b.dev)
+        with torch.no_grad():
+            for k, shp, st, off in zip(b.keys, b.shapes, b.strides, b.offs_list):
+                p = sd1[k]
+                p.data.record_stream(cur)
+                p.data = buf.as_strided(shp, st, off)
+        b.p0, b.buf = po, buf
+        t0 = t("re-pointing (after the launch)", t0)
+        torch.cuda.synchronize()
+        t("wall", t_start)
+        steps.setdefault("device (events)", []).append(e0.elapsed_time(e1))
+        assert ok
+    bres = {k: round(statistics.median(v[1:]), 4) for k, v in steps.items()}
+    bpre = sum(v for k, v in bres.items() if k in ("cache key + lookup", "fresh buffer", "binding (C checks + table upload)",
+                                                   "merge launches"))
+    print(json.dumps({"probe": "evomerge_host_breakdown", "median_ms": res, "host_before_launch_ms": round(pre, 4),
+                      "repeat_binding": {"median_ms": bres, "host_before_launch_ms": round(bpre, 4)}}))
 
 
 if __name__ == "__main__":

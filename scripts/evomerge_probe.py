@@ -7,7 +7,7 @@ host work included (state_dict, the key plan, the checks, the pointer table), wa
 device synchronize. Both must give the same bits. Lineage parents (model_2 = model_1 + small
 noise: every tensor takes the lerp branch, as fine-tunes of one base do) or --far.
 
-    python scripts/evomerge_probe.py [--rounds 5] [--far] [--layers 28]
+    python scripts/evomerge_probe.py [--rounds 5] [--far] [--layers 28] [--repoint]
 """
 import argparse
 import json
@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--far", action="store_true")
     ap.add_argument("--layers", type=int, default=28)
     ap.add_argument("--profile", action="store_true", help="cProfile one merge (host time split) to stderr")
+    ap.add_argument("--repoint", action="store_true", help="reset model_1 to fresh tensors (no repeat binding)")
     a = ap.parse_args()
     from transformers import Qwen2Config, Qwen2ForCausalLM
 
@@ -53,9 +54,15 @@ def main():
     start = {k: v.clone() for k, v in m1.model.state_dict().items()}
 
     def reset():
+        # the start values copied into model_1's tensors where they lie (a resident population's
+        # next generation: the same modules, the previous child's memory), so the repeat binding
+        # of merge_models_into_ applies; --repoint: fresh tensors every round (the uncached path)
         with torch.no_grad():
             for k, p in m1.model.named_parameters():
-                p.data = start[k].clone()
+                if a.repoint:
+                    p.data = start[k].clone()
+                else:
+                    p.copy_(start[k])
         torch.cuda.synchronize()
 
     def rebind_merge():                            # the surface minus save_pretrained
@@ -91,9 +98,33 @@ def main():
         buf = io.StringIO()
         pstats.Stats(pr, stream=buf).sort_stats("tottime").print_stats(18)
         print(buf.getvalue(), file=sys.stderr)
+    # the same merge as one arena pass (the single-pass speculative kernel over two flat arenas of
+    # the same bodies, HIP events): the device floor the surface is measured against
+    from evolutionarydistributedtraining_amd import ops
+    sd1, sd2 = m1.model.state_dict(), m2.model.state_dict()
+    offs = [0]
+    for k, _ in plan:
+        offs.append(offs[-1] + sd1[k].numel())
+    v0 = torch.cat([sd1[k].reshape(-1) for k, _ in plan])
+    v1 = torch.cat([sd2[k].reshape(-1) for k, _ in plan])
+    out = torch.empty_like(v0)
+    aplan = ops.make_slerp_plan(offs, dev)
+    tt = torch.tensor([t for _, t in plan], dtype=torch.float64, device=dev)
+    ev = []
+    for r in range(a.rounds + 1):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        ops.slerp_arena(aplan, v0, v1, out, tt, speculate=True)
+        e1.record()
+        torch.cuda.synchronize()
+        ev.append(e0.elapsed_time(e1))
+    times["arena_speculative_events"] = ev[1:]
+    del v0, v1, out
     res = {k: {"median_ms": round(statistics.median(v), 3), "min_ms": round(min(v), 3),
                "TBps_algorithmic": round(6 * n / (statistics.median(v) / 1e3) / 1e12, 3)} for k, v in times.items()}
     print(json.dumps({"probe": "evomerge_surface", "params_body": n, "tensors": len(keys), "far": a.far,
+                      "reset": "fresh tensors" if a.repoint else "copied in place (repeat binding)",
+                      "bound_entries": len(merge._bound_cache),
                       "outputs_bit_identical": same, "results": res}))
 
 

@@ -78,10 +78,20 @@ def test_single_gpu_line_population_extra():
     _check_common(d, 1)
     p = d["population_slerp_7b"]
     assert "error" not in p and "skipped" not in p, p
-    assert len(p["pairs"]) == 8 and p["lerp_branch_fraction"] == 1.0
+    assert "roulette_wheel_selection" in p["pairs_source"] and p["timed_reps"] >= 10
+    gens = p["generations"] + [p["ring"]]
+    assert len(p["generations"]) >= 3
+    for g in gens:
+        assert len(g["pairs"]) == 8 and g["lerp_branch_fraction"] == 1.0
+        assert g["distinct_parents"] == len({x for q in g["pairs"] for x in q})
+        assert g["layout"]["children"] == 8
+        for form in ("speculative", "two_pass"):
+            assert g[form]["ms"] > 0 and g[form]["floor_bytes"] > 0
     for form in ("speculative", "two_pass"):
         f = p[form]
-        assert f["ms"] > 0 and f["floor_bytes"] >= f["algo_bytes"] > 0
+        fb = sum(g[form]["floor_bytes"] for g in p["generations"])
+        ms = sum(g[form]["ms"] for g in p["generations"])
+        assert f["ms_per_generation"] == pytest.approx(ms / len(p["generations"]), rel=1e-3)
         r = f["roofline"]
-        assert r["achieved"] == pytest.approx(f["floor_bytes"] / (f["ms"] / 1e3) / 1e9, rel=1e-2)
+        assert r["achieved"] == pytest.approx(fb / (ms / 1e3) / 1e9, rel=1e-2)
         assert r["frac"] == pytest.approx(r["achieved"] / r["peak"], abs=1e-3)

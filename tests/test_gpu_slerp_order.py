@@ -69,3 +69,22 @@ def test_gram_sums_in_canonical_order(oracle, dev, M, dt):
             want = oracle.canonical_chunk_sums(mem[i], mem[j], plan.chunks_host)[:, 2]
             assert np.array_equal(gram[:, col].view(np.int64), want.view(np.int64)), (i, j)
             col += 1
+
+
+def test_gram_rows_are_owned_by_the_caller(dev):
+    """without `gram`, slerp_gram's rows come back in a tensor the caller owns — the
+    stream's pooled scratch the pass ran in is reused by the next SLERP call, which must leave the
+    returned rows untouched."""
+    from evolutionarydistributedtraining_amd import ops
+    offs = _layout()
+    mem = [m.to(dev) for m in _members(torch.bfloat16, 4, offs[-1], seed=23)]
+    plan = ops.make_slerp_plan(offs, dev)
+    gram = ops.slerp_gram(mem, plan.chunks, plan.nchunks)
+    keep = gram.clone()
+    t = torch.full((plan.nseg,), 0.4, dtype=torch.float64, device=dev)
+    outs = [torch.empty_like(mem[0]) for _ in range(3)]
+    ops.slerp_population(plan, [m.flip(0).contiguous() for m in mem], [(0, 1), (1, 2), (3, 0)], outs, t,
+                         speculate=False)
+    ops.slerp_gram([m * 2 for m in mem], plan.chunks, plan.nchunks)
+    torch.cuda.synchronize()
+    assert torch.equal(gram.view(torch.int64), keep.view(torch.int64))

@@ -635,3 +635,51 @@ def test_evomerge_mixed_dtype_target_keeps_its_tensors(dev):
         assert (got[k].data_ptr(), got[k].dtype) == before[k], k
         want = merge.slerp_tensors([(sd1[k], sd2[k])], [t], out_dtype=torch.float32, device=dev)[0]
         assert torch.equal(got[k], want.to(got[k].dtype)), k
+
+
+def test_evomerge_repeat_binding_follows_module_changes(dev, monkeypatch):
+    """merge_models_into_'s cached binding (merge._Bound, VERDICT r4 Next 3): the repeat of a merge
+    into model_1 launches over the cached addresses and checks the modules while the device runs.
+    Every generation equals the in-place two-pass merge bit for bit, whatever changed in between:
+    nothing (the cached launch), model_1 written in place (same addresses: cached), a model_2
+    parameter re-pointed, a model_1 Parameter replaced by a new one (both: the check fails, the
+    uncached merge runs, the new binding is recorded); the entry dies with model_2."""
+    import gc
+
+    from evolutionarydistributedtraining_amd import evomerge_crossover as ev
+    from evolutionarydistributedtraining_amd import merge
+    merge.clear_merge_cache()
+    cfg, (m1, m2) = _qwen_pair(dev, far=False, seed=7)
+    mcfg = ev.slerp_config("a", "b", cfg.num_hidden_layers)
+    plan = merge.merge_plan(list(m1.model.state_dict()), cfg.num_hidden_layers, mcfg)
+    hits = []
+    real = merge._bound_merge
+    monkeypatch.setattr(merge, "_bound_merge", lambda b, x, y: hits.append(real(b, x, y)) or hits[-1])
+
+    def change(gen):
+        with torch.no_grad():
+            if gen == 2:
+                m1.model.layers[0].mlp.up_proj.weight.mul_(1.5)               # in place: same addresses
+            elif gen == 3:
+                w = m2.model.layers[1].self_attn.q_proj.weight
+                w.data = w.data.clone() * 0.5                                # model_2 re-pointed
+            elif gen == 4:
+                lin = m1.model.layers[2].self_attn.o_proj
+                lin.weight = torch.nn.Parameter(lin.weight.detach().clone())  # a new Parameter
+
+    expect = [None, True, True, False, False, True]
+    for gen in range(6):
+        change(gen)
+        want = {k: v.clone() for k, v in m1.model.state_dict().items()}
+        merge.slerp_state_dicts(dict(want), m2.model.state_dict(), plan, out_dtype=torch.bfloat16, device=dev,
+                                out=want)
+        n = len(hits)
+        merge.merge_models_into_(m1.model, m1.model, m2.model, mcfg, cfg.num_hidden_layers, device=dev)
+        assert (hits[n] if len(hits) > n else None) == expect[gen], (gen, hits)
+        got = m1.model.state_dict()
+        for k, _ in plan:
+            assert torch.equal(got[k].view(torch.int16), want[k].view(torch.int16)), (gen, k)
+    assert len(merge._bound_cache) == 1
+    del m2
+    gc.collect()
+    assert len(merge._bound_cache) == 0
