@@ -876,14 +876,19 @@ def bench_slerp_7b(args, dev):
 
 def bench_population(args, rt, comm, kernels=None, layout_name="qwen2p5_7b_body"):
     """BASELINE configs[4] at N > 1: a population of N members (one 7.07B bf16 body per GPU,
-    qwen2p5_7b_body) SLERP-crossed into N children (t = 0.5, far parents: the SLERP branch), timed
-    link-balanced (distributed.ShardedPopulationCrossover: chunk-range shards of every member,
-    Gram rows all-gathered, children gathered back), the same with its exchanges pipelined over
-    chunk groups (`sharded_pipelined`), and per child (PopulationCrossover: each child's two parents
-    shipped whole). Max over ranks; every rank of `comm` takes part. `kernels`: the product ops
-    (default) or a host stand-in (the CPU rehearsal)."""
+    qwen2p5_7b_body) SLERP-crossed into N children (far parents: the SLERP branch), the N pairs
+    drawn by EDT_RL/edt.py:231-240's roulette_wheel_selection (schedule.roulette_generation_pairs,
+    the same seeded draw on every rank) and t per key from EDT_RL/crossover.py:146-147's layer
+    curves (merge.rl_t_per_segment), timed link-balanced (distributed.ShardedPopulationCrossover:
+    chunk-range shards of every member, the needed sums' table rows all-gathered, children gathered
+    back), the same with its exchanges pipelined over chunk groups (`sharded_pipelined`), and per
+    child (PopulationCrossover: each child's two parents shipped whole). Max over ranks; every rank
+    of `comm` takes part. `kernels`: the product ops (default) or a host stand-in (the CPU
+    rehearsal)."""
     from evolutionarydistributedtraining_amd.distributed import PopulationCrossover, ShardedPopulationCrossover
     from evolutionarydistributedtraining_amd.layouts import LAYOUTS
+    from evolutionarydistributedtraining_amd.merge import rl_t_per_segment
+    from evolutionarydistributedtraining_amd.schedule import roulette_generation_pairs
     lay = LAYOUTS[layout_name]()
     rank, world, dev = comm.rank, comm.world, rt.dev
     P, bf = lay.total, torch.bfloat16
@@ -895,10 +900,15 @@ def bench_population(args, rt, comm, kernels=None, layout_name="qwen2p5_7b_body"
     member = torch.empty(P, dtype=bf, device=dev)
     member_seed(member, rank)
     out = torch.empty(P, dtype=bf, device=dev)
-    t = torch.full((len(lay),), 0.5, dtype=torch.float64, device=dev)
-    pairs = [((3 * c + 1) % world, (5 * c + 2) % world) for c in range(world)]
+    ts = rl_t_per_segment(lay.names) if len(lay.names) == len(lay) else [0.5] * len(lay)   # unnamed: the global t
+    t = torch.tensor(ts, dtype=torch.float64, device=dev)
+    seed = getattr(args, "population_seed", 2025)
+    pairs = [tuple(p) for p in roulette_generation_pairs(world, 1, seed=seed)[0]["pairs"]] if world > 1 else [(0, 0)]
     res = {"workload": f"SLERP population of {world} x {layout_name} (P={P}, bf16), one member per GPU",
-           "pairs": pairs}
+           "pairs": [list(p) for p in pairs],
+           "pairs_source": f"schedule.roulette_generation_pairs({world}, 1, seed={seed}): EDT_RL/edt.py:231-240 "
+                           f"roulette_wheel_selection, n = {world} pairs",
+           "t_source": "merge.rl_t_per_segment: EDT_RL/crossover.py:146-147 layer curves, global 0.5"}
 
     def timed(step, n):
         for _ in range(2):
@@ -918,6 +928,11 @@ def bench_population(args, rt, comm, kernels=None, layout_name="qwen2p5_7b_body"
             continue
         sp = ShardedPopulationCrossover(lay, bf, dev, kind="slerp", comm=comm, groups=groups, kernels=kernels)
         ms = timed(lambda: sp.slerp_step(member, pairs, t, out), max(3, args.steps // 4))
+        if "sums_table" not in res:
+            tab = (kernels or sp.kernels).needed_table(pairs, world, sp.plan.nchunks)
+            res["sums_table"] = {"sums_per_chunk": sum(nt for _, nt in tab.blocks), "blocks": len(tab.blocks),
+                                 "triangle_sums_per_chunk": world * (world + 1) // 2,
+                                 "gathered_bytes_per_rank": tab.doubles * 8 * (world - 1) // world}
         res[key] = {"ms": round(ms, 3), "groups": groups, "wire_bytes_per_rank": wire,
                     "xgmi": {"achieved": round(wire / (ms / 1e3) / 1e9, 1), "peak": peak, "unit": "GB/s",
                              "frac": round(wire / (ms / 1e3) / 1e9 / peak, 4) if peak else None}}

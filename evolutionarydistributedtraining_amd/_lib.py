@@ -86,6 +86,13 @@ SIGNATURES = [
                                               ctypes.POINTER(_P), _I, _P, ctypes.c_int64, _P, _I, _P, _D, _D, _P,
                                               _P, _P, _P, _U64, _P]),
     ("edt_slerp_population_layout", _I, [ctypes.POINTER(ctypes.c_int32), _I, _I, _I, ctypes.c_char_p, _I]),
+    ("edt_slerp_needed_table", _I, [ctypes.POINTER(ctypes.c_int32), _I, _I, ctypes.c_int64, ctypes.POINTER(_U64),
+                                    ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
+                                    ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(_U64), ctypes.POINTER(_U64)]),
+    ("edt_slerp_needed_sums", _I, [ctypes.POINTER(_P), _I, _I, ctypes.POINTER(ctypes.c_int32), _I, _P, ctypes.c_int64,
+                                   ctypes.c_int64, ctypes.c_int64, _P, _P, _U64, _P]),
+    ("edt_slerp_needed_coef", _I, [_P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int32), _I, _I, _P, _I, _P, _D, _D,
+                                   _P, _P, _P]),
     ("edt_slerp_gram", _I, [ctypes.POINTER(_P), _I, _I, _P, ctypes.c_int64, _P, _P]),
     ("edt_slerp_gram_coef", _I, [_P, _I, ctypes.POINTER(ctypes.c_int32), _I, _P, _I, _P, _D, _D, _P, _P, _P]),
     ("edt_slerp_blend_children", _I, [ctypes.POINTER(_P), _I, _I, ctypes.POINTER(ctypes.c_int32), _I,

@@ -2609,6 +2609,152 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
     return EDT_OK;
 }
 
+// ---- the needed-sums passes as separate entries (r5: the sharded population,
+// distributed.ShardedPopulationCrossover — each rank forms the needed sums of its chunk range,
+// the table's rows are all-gathered, every rank forms every child's coefficients) ----
+
+namespace {
+// The distinct parents of `pairs` in first-use order (compact ids) and the GramPlan of the pair
+// graph: the same planning as edt_slerp_population, so a table row equals that pass's sums.
+struct NeededPlan {
+    int D = 0;
+    int orig[kGramMaxMembers];                 // compact -> member index
+    std::vector<int> A, B;                     // children's compact parents
+    GramPlan G;
+};
+
+int needed_plan(const int32_t* pairs, int npairs, int nmembers, int64_t nchunks, NeededPlan& P) {
+    if (nmembers < 1 || nmembers > kGramMaxMembers)
+        return fail(EDT_ERR_ARG, "member count %d out of range [1, %d]", nmembers, kGramMaxMembers);
+    if (npairs < 1 || !pairs) return fail(EDT_ERR_ARG, "no pairs");
+    if (nchunks < 0) return fail(EDT_ERR_ARG, "negative chunk count");
+    int compact[kGramMaxMembers];
+    for (int m = 0; m < nmembers; ++m) compact[m] = -1;
+    P.A.assign(npairs, 0);
+    P.B.assign(npairs, 0);
+    for (int q = 0; q < npairs; ++q)
+        for (int e = 0; e < 2; ++e) {
+            const int m = pairs[2 * q + e];
+            if (m < 0 || m >= nmembers) return fail(EDT_ERR_ARG, "pair %d: member out of range", q);
+            if (compact[m] < 0) {
+                compact[m] = P.D;
+                P.orig[P.D++] = m;
+            }
+            (e ? P.B : P.A)[q] = compact[m];
+        }
+    plan_gram(P.D, P.A.data(), P.B.data(), npairs, nchunks, P.G);
+    return EDT_OK;
+}
+
+// the two members (member indices) each column of block k holds the sum of
+void needed_columns(const NeededPlan& P, int k, int32_t* cols) {
+    const GramPlan& G = P.G;
+    const int M = G.size[k];
+    const int* L = G.list[k];
+    if (G.kind[k] == kTri) {
+        for (int i = 0; i < M; ++i)
+            for (int j = i; j < M; ++j) {
+                const int c = tri_index(i, j, M);
+                cols[2 * c] = P.orig[L[i]];
+                cols[2 * c + 1] = P.orig[L[j]];
+            }
+        return;
+    }
+    int c = 0;
+    for (int x = 0; x < M; ++x, ++c) { cols[2 * c] = P.orig[L[x]]; cols[2 * c + 1] = P.orig[L[x]]; }
+    for (int e = 0; e < need_nr(M); ++e, ++c) { cols[2 * c] = P.orig[L[e]]; cols[2 * c + 1] = P.orig[L[(e + 1) % M]]; }
+    for (int e = 0; e < need_nc(M); ++e, ++c) {
+        if (e < G.need[k].nchord) {
+            const int code = G.need[k].code[e];
+            cols[2 * c] = P.orig[L[code / 8]];
+            cols[2 * c + 1] = P.orig[L[code % 8]];
+        } else {                                       // an unused chord slot (its sum is not formed)
+            cols[2 * c] = cols[2 * c + 1] = -1;
+        }
+    }
+}
+}   // namespace
+
+int edt_slerp_needed_table(const int32_t* pairs, int npairs, int nmembers, int64_t nchunks, uint64_t* block_off,
+                           int32_t* block_nt, int32_t* ncomp, int32_t* col_members, uint64_t* table_doubles,
+                           uint64_t* scratch_doubles) {
+    g_err[0] = 0;
+    if (!block_off || !block_nt || !ncomp || !table_doubles || !scratch_doubles) return fail(EDT_ERR_ARG, "null output");
+    NeededPlan P;
+    int rc = needed_plan(pairs, npairs, nmembers, nchunks, P);
+    if (rc) return rc;
+    *ncomp = P.G.ncomp;
+    uint64_t tot = 0;
+    int col = 0;
+    for (int k = 0; k < P.G.ncomp; ++k) {
+        block_off[k] = P.G.off[k];
+        block_nt[k] = P.G.nt(k);
+        tot += (uint64_t)nchunks * P.G.nt(k);
+        if (col_members) needed_columns(P, k, col_members + 2 * col);
+        col += P.G.nt(k);
+    }
+    *table_doubles = tot;
+    *scratch_doubles = plan_row_scratch(P.G, nchunks);
+    return EDT_OK;
+}
+
+int edt_slerp_needed_sums(const void* const* members, int nmembers, int in_dt, const int32_t* pairs, int npairs,
+                          const uint64_t* chunk_desc, int64_t nchunks, int64_t table_chunks, int64_t row0,
+                          double* table, double* scratch, uint64_t scratch_doubles, void* stream) {
+    g_err[0] = 0;
+    if (in_dt & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
+    NeededPlan P;
+    int rc = needed_plan(pairs, npairs, nmembers, table_chunks, P);
+    if (rc) return rc;
+    if (nchunks < 0 || row0 < 0 || row0 + nchunks > table_chunks)
+        return fail(EDT_ERR_ARG, "rows [%lld, %lld) outside the table's %lld chunks", (long long)row0,
+                    (long long)(row0 + nchunks), (long long)table_chunks);
+    if (nchunks == 0) return EDT_OK;
+    if (!members || !chunk_desc || !table || !scratch) return fail(EDT_ERR_ARG, "null buffer");
+    if (scratch_doubles < plan_row_scratch(P.G, nchunks))
+        return fail(EDT_ERR_ARG, "scratch of %llu doubles, the passes need %llu", (unsigned long long)scratch_doubles,
+                    (unsigned long long)plan_row_scratch(P.G, nchunks));
+    Members mem;
+    memset(&mem, 0, sizeof(mem));
+    for (int d = 0; d < P.D; ++d) {
+        const void* m = members[P.orig[d]];
+        if (!m || !aligned16(m)) return fail(EDT_ERR_ARG, "member %d is null or not 16-byte aligned", P.orig[d]);
+        mem.p[d] = m;
+    }
+    for (int k = 0; k < P.G.ncomp; ++k) {
+        // rows [row0, row0 + nchunks) of the component's block (plan_component_sums adds the
+        // block's offset)
+        rc = plan_component_sums(P.G, k, mem.p, in_dt, chunk_desc, nchunks, table + (uint64_t)row0 * P.G.nt(k),
+                                 scratch, (hipStream_t)stream);
+        if (rc) return rc;
+    }
+    return EDT_OK;
+}
+
+int edt_slerp_needed_coef(const double* table, int64_t table_chunks, const int32_t* pairs, int npairs, int nmembers,
+                          const int32_t* seg_first_chunk, int nseg, const double* t, double dot_threshold, double eps,
+                          float* coef, float* dot_out, void* stream) {
+    g_err[0] = 0;
+    NeededPlan P;
+    int rc = needed_plan(pairs, npairs, nmembers, table_chunks, P);
+    if (rc) return rc;
+    if (nseg < 0) return fail(EDT_ERR_ARG, "negative count");
+    if (nseg == 0) return EDT_OK;
+    if (!table || !seg_first_chunk || !t || !coef) return fail(EDT_ERR_ARG, "null buffer");
+    hipStream_t s = (hipStream_t)stream;
+    for (int q = 0; q < npairs; ++q) {
+        const int i = P.A[q], j = P.B[q];
+        const int k = P.G.comp_of[i];
+        slerp_gram_coef_kernel<<<coef_grid(nseg), kBlock, 0, s>>>(
+            table + P.G.off[k], P.G.nt(k), P.G.norm_index(i), P.G.norm_index(j), P.G.dot_index(i, j), seg_first_chunk,
+            nseg, t, (float)dot_threshold, (float)eps, coef + 2 * (size_t)nseg * q,
+            dot_out ? dot_out + (size_t)nseg * q : nullptr);
+        rc = check_launch("slerp_gram_coef_kernel");
+        if (rc) return rc;
+    }
+    return EDT_OK;
+}
+
 int edt_slerp_population_layout(const int32_t* pairs, int npairs, int nmembers, int speculate, char* buf,
                                 int buflen) {
     // the plan edt_slerp_population(_speculative) makes for these pairs, as JSON (host only)

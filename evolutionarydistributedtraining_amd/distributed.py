@@ -402,11 +402,15 @@ class ShardedPopulationCrossover:
 
       1. members -> shards: rank r sends rank s the slice of its member in s's range (grouped p2p,
          every link busy: (N-1)/N of a member out and in per rank);
-      2. SLERP: per-chunk Gram sums of all N members over the rank's chunks (edt_slerp_gram),
-         all-gathered (nchunks x N(N+1)/2 doubles: ~31 MB at 7B), then every child's coefficients
-         (edt_slerp_gram_coef) — each chunk's sums come from the same kernel in the same order
-         wherever the chunk lives, so every child is bit-identical to edt_slerp_merge on its two
-         parents; then the rank's range of every child (edt_slerp_blend_children).
+      2. SLERP: per chunk of the rank's range the sums the generation needs — each distinct
+         parent's norm and each distinct dot its children use, per connected component of the
+         pair graph (edt_slerp_needed_sums: edt_slerp_population's needed-sums pass, r5; at most
+         D + 8 sums for 8 children against the Gram triangle's 36) — the table rows all-gathered
+         (nchunks x those sums doubles: ~12 MB at 7B for a roulette-drawn generation, against ~31 MB
+         for the triangle), then every child's coefficients (edt_slerp_needed_coef) — each chunk's
+         sums come from the same kernel in the same order wherever the chunk lives, so every child
+         is bit-identical to edt_slerp_merge on its two parents; then the rank's range of every
+         child (edt_slerp_blend_children).
          EDT-LM: the rank's range of every child (edt_pair_merge_population), nothing to gather;
       3. child shards -> children: the range of child c goes to rank c.
 
@@ -659,11 +663,10 @@ class ShardedPopulationCrossover:
         if len(pairs) != self.world:
             raise ValueError(f"{len(pairs)} children for {self.world} ranks")
         k, N = self.kernels, self.world
-        NT = N * (N + 1) // 2
-        gram = self._bufs.get("gram")
-        if gram is None:
-            gram = self._bufs["gram"] = torch.empty((max(1, self.plan.nchunks), NT), dtype=torch.float64,
-                                                    device=self.device)
+        layout = k.needed_table(pairs, N, self.plan.nchunks)
+        table = self._bufs.get("needed")
+        if table is None or table.numel() < max(1, layout.doubles):
+            table = self._bufs["needed"] = torch.empty(max(1, layout.doubles), dtype=torch.float64, device=self.device)
         c0, c1 = self.ranges[self.rank][:2]
         mine = self.granges[self.rank]
         if self.groups > 1 and ref_dot is None:
@@ -673,22 +676,23 @@ class ShardedPopulationCrossover:
                 h.wait()
                 if g < len(mine):
                     g0, g1 = mine[g][0] - c0, mine[g][1] - c0
-                    k.slerp_gram(members, self.local_chunks[g0:g1], g1 - g0, gram[c0 + g0:c0 + g1])
+                    k.slerp_needed_sums(members, layout, self.local_chunks[g0:g1], g1 - g0, table, c0 + g0)
         else:
             sh = self._scatter([member], "m")
             members = [sh[j][0] for j in range(N)]
             if self.nloc:
-                k.slerp_gram(members, self.local_chunks, self.nloc, gram[c0:c1])
-        ops_ = []                       # all-gather of the Gram rows: every rank's chunk range
-        for s in range(N):
-            if s != self.rank and self.nloc:
-                ops_.append(("send", gram[c0:c1], s))
-        for j in range(N):
-            a, b = self.ranges[j][:2]
-            if j != self.rank and b > a:
-                ops_.append(("recv", gram[a:b], j))
+                k.slerp_needed_sums(members, layout, self.local_chunks, self.nloc, table, c0)
+        ops_ = []                       # all-gather of the table rows: every rank's chunk range, per block
+        for b in range(len(layout.blocks)):
+            for s in range(N):
+                if s != self.rank and self.nloc:
+                    ops_.append(("send", layout.rows(table, b, c0, c1), s))
+            for j in range(N):
+                ja, jb = self.ranges[j][:2]
+                if j != self.rank and jb > ja:
+                    ops_.append(("recv", layout.rows(table, b, ja, jb), j))
         self.comm.p2p(ops_)
-        coef, dots = k.slerp_gram_coef(self.plan, gram, N, pairs, t, dot_threshold, eps)
+        coef, dots = k.slerp_needed_coef(self.plan, table, layout, t, dot_threshold, eps)
         if ref_dot is not None:
             coef, dots = self._reference_dots(members, pairs, t, dots, dot_threshold, eps, ref_dot)
         outs = [self._buf(("c", q), self.out_dtype)[:self.end - self.base] for q in range(N)]

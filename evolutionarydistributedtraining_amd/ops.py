@@ -896,14 +896,15 @@ def slerp_population(plan: SlerpPlan, members: list[torch.Tensor], pairs, outs: 
     (EDT_RL/edt.py:286-299 -> EDT_RL/crossover.py:84-135 per child). Two forms, bit-identical to
     slerp_arena per child:
       speculate=False  edt_slerp_population: one stats pass per component of the children's
-                       pair graph over the (<= 8) distinct parents (r4: paths and cycles in the
-                       ring layout — each parent's norm and the children's dots only — else the
-                       Gram triangle), then one member-major blend launch for all children;
+                       pair graph over the (<= 8) distinct parents (r5: the needed sums — each
+                       parent's norm and only the dots its children use, for any graph the
+                       reference's selection draws; the Gram triangle when a component needs more
+                       dots than its slots), then one member-major blend launch for all children;
       speculate=True   edt_slerp_population_speculative: one pass forms every child's sums and
-                       writes its lerp-branch output (r4: a member-major ring pass per component
-                       when every child is one edge of a path / cycle of parents, e.g. a ring of
-                       children or a matching; else the co-located pass), then only SLERP-branch
-                       segments are blended again (parents of one lineage: a single pass);
+                       writes its lerp-branch output (r5: a member-major needed-sums pass per
+                       component when every component takes the needed layout and there are <= 16
+                       children; else the co-located pass), then only SLERP-branch segments are
+                       blended again (parents of one lineage: a single pass);
       None             speculate when the previous call on this plan had few enough child elements
                        in SLERP-branch segments for the single pass to move fewer bytes
                        (f < D b_in / (D b_in + Q b_out), D distinct parents, Q children).
@@ -1078,6 +1079,101 @@ def slerp_gram_coef(plan: SlerpPlan, gram: torch.Tensor, nmembers: int, pairs, t
     L.check(lib.edt_slerp_gram_coef(L.ptr(gram), nmembers, fp, Q, L.ptr(plan.seg_first), plan.nseg, L.ptr(t),
                                     float(dot_threshold), float(eps), L.ptr(coef), L.ptr(dots),
                                     L.stream_ptr(dev)), "edt_slerp_gram_coef")
+    return coef, dots
+
+
+@dataclass(frozen=True)
+class NeededTable:
+    """The needed-sums table of one generation (edt_slerp_needed_table, host only): the pair graph's
+    components as blocks of `nchunks` rows, block k at blocks[k][0] doubles with blocks[k][1] sums
+    per row; columns[k][c] = the two members column c of block k sums over ((-1, -1): unused)."""
+    pairs: tuple
+    nmembers: int
+    nchunks: int
+    blocks: tuple
+    columns: tuple
+    doubles: int
+    scratch_doubles: int
+
+    def rows(self, table: torch.Tensor, k: int, a: int, b: int) -> torch.Tensor:
+        """Rows [a, b) of block k (a contiguous view of the table)."""
+        off, nt = self.blocks[k]
+        return table[off + a * nt:off + b * nt]
+
+
+_needed_memo: dict = {}
+
+
+def needed_table(pairs, nmembers: int, nchunks: int) -> NeededTable:
+    """The table layout the needed-sums passes use for these pairs (cached)."""
+    key = (tuple((int(a), int(b)) for a, b in pairs), int(nmembers), int(nchunks))
+    got = _needed_memo.get(key)
+    if got is not None:
+        return got
+    lib = L.load_library()
+    Q = len(key[0])
+    fp = (ctypes.c_int32 * max(1, 2 * Q))(*[x for p in key[0] for x in p])
+    off = (ctypes.c_uint64 * 8)()
+    nt = (ctypes.c_int32 * 8)()
+    nc = ctypes.c_int32()
+    cols = (ctypes.c_int32 * (2 * 36 * 8))()
+    tot, scr = ctypes.c_uint64(), ctypes.c_uint64()
+    L.check(lib.edt_slerp_needed_table(fp, Q, key[1], key[2], off, nt, ctypes.byref(nc), cols, ctypes.byref(tot),
+                                       ctypes.byref(scr)), "edt_slerp_needed_table")
+    blocks, columns, c = [], [], 0
+    for k in range(nc.value):
+        blocks.append((int(off[k]), int(nt[k])))
+        columns.append(tuple((int(cols[2 * (c + x)]), int(cols[2 * (c + x) + 1])) for x in range(nt[k])))
+        c += nt[k]
+    got = NeededTable(key[0], key[1], key[2], tuple(blocks), tuple(columns), int(tot.value), int(scr.value))
+    if len(_needed_memo) > 64:
+        _needed_memo.clear()
+    _needed_memo[key] = got
+    return got
+
+
+def slerp_needed_sums(members: list[torch.Tensor], layout: NeededTable, chunks: torch.Tensor, nchunks: int,
+                      table: torch.Tensor, row0: int, scratch: torch.Tensor | None = None) -> torch.Tensor:
+    """Rows [row0, row0 + nchunks) of every block of `layout`'s table (float64, >= layout.doubles)
+    over a chunk table of those chunks (starts relative to the member buffers):
+    edt_slerp_needed_sums. `scratch`: >= layout.scratch_doubles float64 (default: the stream's
+    pooled workspace)."""
+    lib = L.lib()
+    M = len(members)
+    if M != layout.nmembers:
+        raise L.EdtError("slerp_needed_sums: one buffer per member of the layout")
+    L.require_device(*members, chunks, table)
+    if table.dtype != torch.float64 or table.numel() < layout.doubles or not table.is_contiguous():
+        raise L.EdtError("table: contiguous float64 with the layout's doubles")
+    need = max(1, layout.scratch_doubles)
+    if scratch is None or scratch.dtype != torch.float64 or scratch.numel() < need:
+        scratch = _scratch(members[0].device, need)
+    Q = len(layout.pairs)
+    fp = (ctypes.c_int32 * max(1, 2 * Q))(*[x for p in layout.pairs for x in p])
+    L.check(lib.edt_slerp_needed_sums(L.ptr_array(members), M, L.dtype_code(members[0]), fp, Q, L.ptr(chunks),
+                                      int(nchunks), layout.nchunks, int(row0), L.ptr(table), L.ptr(scratch),
+                                      scratch.numel(), L.stream_ptr(members[0].device)), "edt_slerp_needed_sums")
+    return table
+
+
+def slerp_needed_coef(plan: SlerpPlan, table: torch.Tensor, layout: NeededTable, t: torch.Tensor,
+                      dot_threshold: float = 0.9995, eps: float = 1e-8):
+    """Coefficients [Q, nseg, 2] and dots [Q, nseg] of every child of `layout` from its complete
+    table (rows = plan's chunks): edt_slerp_needed_coef."""
+    lib = L.lib()
+    Q = len(layout.pairs)
+    if layout.nchunks != plan.nchunks or table.numel() < layout.doubles:
+        raise L.EdtError("the table does not cover the plan's chunks")
+    L.require_device(table, t)
+    if t.dtype != torch.float64 or t.numel() < plan.nseg:
+        raise L.EdtError("t must be a float64 device tensor with one value per segment")
+    dev = table.device
+    coef = torch.empty((max(1, Q), max(1, plan.nseg), 2), dtype=torch.float32, device=dev)
+    dots = torch.empty((max(1, Q), max(1, plan.nseg)), dtype=torch.float32, device=dev)
+    fp = (ctypes.c_int32 * max(1, 2 * Q))(*[x for p in layout.pairs for x in p])
+    L.check(lib.edt_slerp_needed_coef(L.ptr(table), layout.nchunks, fp, Q, layout.nmembers, L.ptr(plan.seg_first),
+                                      plan.nseg, L.ptr(t), float(dot_threshold), float(eps), L.ptr(coef), L.ptr(dots),
+                                      L.stream_ptr(dev)), "edt_slerp_needed_coef")
     return coef, dots
 
 

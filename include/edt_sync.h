@@ -353,6 +353,31 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
                                      double dot_threshold, double eps, double* partial, float* coef,
                                      float* dot_out, int32_t* redo, uint64_t n, void* stream);
 
+/* The needed-sums passes of edt_slerp_population as separate entries (r5: the link-balanced sharded
+ * population — each rank forms the sums of its chunk range, the table rows are all-gathered, every
+ * rank forms every child's coefficients; distributed.ShardedPopulationCrossover). The table of a
+ * generation (pairs over nmembers <= 8 members, nchunks chunks) is ncomp blocks, one per connected
+ * component of the children's pair graph: block k at block_off[k] doubles, nchunks rows of
+ * block_nt[k] sums (the component's norms and the dots its children use, or its Gram triangle
+ * when they need more dots than the slots). col_members (nullable, 2 x sum(block_nt) int32): the
+ * two members of each column, block after block (-1, -1: an unused slot). scratch_doubles: the
+ * row scratch a pass over up to nchunks chunks needs.
+ *   edt_slerp_needed_sums  rows [row0, row0 + nchunks) of every block, over a chunk table of those
+ *                          nchunks chunks (starts relative to the member buffers), table_chunks =
+ *                          the table's row count; a row is bit-identical to edt_slerp_population's
+ *                          sums of that chunk, wherever the chunk's elements lie (16-byte aligned)
+ *   edt_slerp_needed_coef  every child's coefficients and dots from the complete table
+ *                          (edt_slerp_gram_coef's output layout) */
+int edt_slerp_needed_table(const int32_t* pairs, int npairs, int nmembers, int64_t nchunks, uint64_t* block_off,
+                           int32_t* block_nt, int32_t* ncomp, int32_t* col_members, uint64_t* table_doubles,
+                           uint64_t* scratch_doubles);
+int edt_slerp_needed_sums(const void* const* members, int nmembers, int in_dt, const int32_t* pairs, int npairs,
+                          const uint64_t* chunk_desc, int64_t nchunks, int64_t table_chunks, int64_t row0,
+                          double* table, double* scratch, uint64_t scratch_doubles, void* stream);
+int edt_slerp_needed_coef(const double* table, int64_t table_chunks, const int32_t* pairs, int npairs, int nmembers,
+                          const int32_t* seg_first_chunk, int nseg, const double* t, double dot_threshold, double eps,
+                          float* coef, float* dot_out, void* stream);
+
 /* The plan the two population entries above make for a pair graph, as JSON text into buf (host
  * only, no device work): distinct parents, the form (speculative: "member-major" or "co-located";
  * "two-pass"), and per connected component of the children's pair graph its members, distinct

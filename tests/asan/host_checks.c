@@ -188,6 +188,21 @@ static void sync_host_paths(void) {
     EXPECT_FAIL(edt_slerp_population_layout(rl, 8, 4, 1, buf, (int)sizeof(buf)));   /* member 5 of 4 */
     EXPECT_FAIL(edt_slerp_population_layout(rl, 8, 8, 1, buf, 16));                  /* short buffer */
     EXPECT_FAIL(edt_slerp_population_layout(rl, 8, 8, 1, NULL, 16));
+    /* r5: the needed-sums table of the sharded population (host only) */
+    uint64_t boff[8], tdoubles = 0, sdoubles = 0;
+    int32_t bnt[8], ncomp = 0, cols[2 * 36 * 8];
+    EXPECT(edt_slerp_needed_table(rl, 8, 8, 100, boff, bnt, &ncomp, cols, &tdoubles, &sdoubles) == 0);
+    EXPECT(ncomp >= 1 && boff[0] == 0 && tdoubles >= 100ull * (uint64_t)bnt[0] && sdoubles > 0);
+    EXPECT(cols[0] >= 0 && cols[0] == cols[1]);                          /* column 0: a norm */
+    EXPECT_FAIL(edt_slerp_needed_table(rl, 8, 4, 100, boff, bnt, &ncomp, cols, &tdoubles, &sdoubles));
+    EXPECT_FAIL(edt_slerp_needed_table(rl, 0, 8, 100, boff, bnt, &ncomp, cols, &tdoubles, &sdoubles));
+    EXPECT_FAIL(edt_slerp_needed_table(rl, 8, 8, 100, NULL, bnt, &ncomp, cols, &tdoubles, &sdoubles));
+    const void* mem8[8] = {d, d, d, d, d, d, d, d};
+    EXPECT_FAIL(edt_slerp_needed_sums(mem8, 8, 1, rl, 8, (const uint64_t*)d, 10, 100, 95, (double*)d, (double*)d,
+                                      sdoubles, NULL));                  /* rows past the table */
+    EXPECT_FAIL(edt_slerp_needed_sums(mem8, 8, 1, rl, 8, (const uint64_t*)d, 10, 100, 0, (double*)d, (double*)d,
+                                      0, NULL));                         /* scratch too small */
+    EXPECT_FAIL(edt_slerp_needed_coef((const double*)d, 100, rl, 8, 9, first, 1, tv, 0.9995, 1e-8, coef, NULL, NULL));
     /* r5: edt_slerp_seg_table's in-place rule (apart = 0 with sizes): an output may be exactly its
      * own parent, never overlap another tensor's parent or output */
     uint64_t host[6];

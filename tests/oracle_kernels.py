@@ -103,6 +103,47 @@ class ChunkGramKernels(OracleKernels):
                 coef[p, s, 0], coef[p, s, 1], dots[p, s] = c0, c1, d
         return coef, dots
 
+    def needed_table(self, pairs, nmembers, nchunks):
+        """The library's own layout (edt_slerp_needed_table is host only)."""
+        from evolutionarydistributedtraining_amd import ops
+        return ops.needed_table(pairs, nmembers, nchunks)
+
+    def slerp_needed_sums(self, members, layout, chunks, nchunks, table, row0, scratch=None):
+        """edt_slerp_needed_sums' contract: every used column of every block, rows [row0, row0 +
+        nchunks), the same per-chunk sums as slerp_gram."""
+        for b, (off, nt) in enumerate(layout.blocks):
+            for c in range(nchunks):
+                a, n = int(chunks[c, 0]), int(chunks[c, 1])
+                for x, (i, j) in enumerate(layout.columns[b]):
+                    if i >= 0:
+                        table[off + (row0 + c) * nt + x] = (members[i][a:a + n].double()
+                                                            * members[j][a:a + n].double()).sum()
+        return table
+
+    def slerp_needed_coef(self, plan, table, layout, t, thr=0.9995, eps=1e-8):
+        """slerp_gram_coef's arithmetic on the needed table: each child's two norms and dot found
+        by their members in the layout's columns."""
+        where = {}
+        for b, (off, nt) in enumerate(layout.blocks):
+            for x, (i, j) in enumerate(layout.columns[b]):
+                if i >= 0:
+                    where.setdefault((i, j), (off, nt, x))
+                    where.setdefault((j, i), (off, nt, x))
+        col = lambda i, j: table[where[(i, j)][0]:where[(i, j)][0] + layout.nchunks * where[(i, j)][1]].view(
+            layout.nchunks, where[(i, j)][1])[:, where[(i, j)][2]]
+        M = layout.nmembers
+        gram = torch.zeros((max(1, layout.nchunks), M * (M + 1) // 2), dtype=torch.float64)
+        tri = {}
+        q = 0
+        for i in range(M):
+            for j in range(i, M):
+                tri[(i, j)] = q
+                q += 1
+        for (i, j) in where:
+            if i <= j:
+                gram[:layout.nchunks, tri[(i, j)]] = col(i, j)
+        return self.slerp_gram_coef(plan, gram, M, list(layout.pairs), t, thr, eps)
+
     def slerp_blend_children(self, members, pairs, outs, chunks, nchunks, coef, nseg):
         for c in range(nchunks):
             a, n, s = (int(x) for x in chunks[c])

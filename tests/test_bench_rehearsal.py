@@ -51,10 +51,10 @@ def _rank_main():
         def slerp_arena(self, plan, v0, v1, out, t, thr=0.9995, eps=1e-8, **kw):
             OracleKernels.slerp_arena(self, getattr(plan, "seg_offsets", plan), v0, v1, out, t, thr, eps)
 
-        def slerp_gram(self, members, chunks, nchunks, gram=None):
+        def slerp_needed_sums(self, members, layout, chunks, nchunks, table, row0, scratch=None):
             if dist.get_rank() == hang_rank:
                 time.sleep(120)                  # a peer that never answers: the deadline must fire
-            return super().slerp_gram(members, chunks, nchunks, gram)
+            return super().slerp_needed_sums(members, layout, chunks, nchunks, table, row0, scratch)
 
     class Corrupting(TorchCollectives):
         """Every received buffer's first element nudged after the collective lands: what a
@@ -141,6 +141,9 @@ def test_bench_line_at_world(world):
     pop = d["population_slerp_7b"]
     assert "error" not in pop and {"sharded", "sharded_pipelined", "per_child"} <= set(pop), pop
     assert pop["sharded"]["wire_bytes_per_rank"] > 0
+    assert "roulette_wheel_selection" in pop["pairs_source"] and len(pop["pairs"]) == world
+    tab = pop["sums_table"]                    # r5: only the needed sums are formed and gathered
+    assert 0 < tab["sums_per_chunk"] <= tab["triangle_sums_per_chunk"], tab
     assert "extras_deadline" not in d
     par = d["parity"]                          # the exchange moved the right bytes
     assert "error" not in par, par

@@ -150,6 +150,80 @@ def test_sharded_population_slerp_on_virtual_ranks(world, out_dt, groups):
         assert torch.equal(res[0][1][c], plan.dots[:plan.nseg]), c
 
 
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("gen", range(4))
+def test_sharded_population_roulette_graphs_on_virtual_ranks(world, gen):
+    """r5: the sharded population forms only the needed sums (edt_slerp_needed_sums over each rank's
+    chunk range, those table rows all-gathered) on pair graphs drawn by EDT_RL's roulette selection
+    (schedule.roulette_generation_pairs: world pairs over world members, hubs and repeated pairs):
+    every child bit-identical to edt_slerp_merge on its two parents, dots too, with 1 and 3 groups."""
+    from evolutionarydistributedtraining_amd.distributed import ShardedPopulationCrossover
+    from evolutionarydistributedtraining_amd.params import ParamLayout
+    from evolutionarydistributedtraining_amd.schedule import roulette_generation_pairs
+    layout = ParamLayout([(257, 301), (7,), (1,), (65537,), (3, 1001), (5,), (200_003,)])
+    n = layout.total
+    pairs = [tuple(p) for p in roulette_generation_pairs(world, gen + 1, seed=77)[gen]["pairs"]]
+    g = torch.Generator().manual_seed(10 + gen)
+    base = torch.randn(n, generator=g) * 0.02
+    members = [(base + torch.randn(n, generator=g) * 0.02 * (0.005 if r % 3 else 0.1)).bfloat16().to(DEV)
+               for r in range(world)]
+    t = torch.tensor([0.3, 0.5, 0.9, 0.5, 0.43, 0.7, 0.6], dtype=torch.float64, device=DEV)
+    lay = ops.needed_table(pairs, world, ops.make_slerp_plan(layout.offsets, DEV).nchunks)
+    assert sum(nt for _, nt in lay.blocks) <= world * (world + 1) // 2
+    plan = ops.make_slerp_plan(layout.offsets, DEV)
+    for groups in (1, 3):
+        def body(comm):
+            sp = ShardedPopulationCrossover(layout, torch.bfloat16, DEV, kind="slerp", out_dtype=torch.bfloat16,
+                                            comm=comm, groups=groups)
+            out = torch.full((n,), float("nan"), dtype=torch.bfloat16, device=DEV)
+            dots = sp.slerp_step(members[comm.rank], pairs, t, out)
+            return out, dots.clone()
+
+        res = VirtualWorld(world).run(body)
+        torch.cuda.synchronize()
+        for c, (i, j) in enumerate(pairs):
+            want = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+            ops.slerp_arena(plan, members[i], members[j], want, t, speculate=False)
+            torch.cuda.synchronize()
+            assert torch.equal(bits(res[c][0]), bits(want)), (groups, c, pairs)
+            assert torch.equal(res[0][1][c], plan.dots[:plan.nseg]), (groups, c)
+
+
+def test_needed_sums_entries_match_the_population_pass():
+    """edt_slerp_needed_sums over a chunk range (row0 > 0, a chunk table relative to a shard) writes
+    the same rows as the whole-table call, and edt_slerp_needed_coef gives edt_slerp_population's
+    coefficients and dots."""
+    from evolutionarydistributedtraining_amd.schedule import roulette_generation_pairs
+    sizes = [70_001, 9, 131_072, 4099, 1]
+    offs = [0]
+    for x in sizes:
+        offs.append(offs[-1] + x)
+    g = torch.Generator().manual_seed(3)
+    base = torch.randn(offs[-1], generator=g) * 0.02
+    mem = [(base + torch.randn(offs[-1], generator=g) * 1e-3).bfloat16().to(DEV) for _ in range(8)]
+    pairs = [tuple(p) for p in roulette_generation_pairs(8, 1, seed=5)[0]["pairs"]]
+    plan = ops.make_slerp_plan(offs, DEV, chunk_elems=8192)
+    lay = ops.needed_table(pairs, 8, plan.nchunks)
+    whole = torch.full((lay.doubles,), float("nan"), dtype=torch.float64, device=DEV)
+    ops.slerp_needed_sums(mem, lay, plan.chunks, plan.nchunks, whole, 0)
+    part = torch.full_like(whole, float("nan"))
+    cut = plan.nchunks // 3
+    base_el = int(plan.chunks_host[cut, 0]) // 8 * 8
+    shard = [m[base_el:].contiguous() for m in mem]
+    loc = plan.chunks[cut:].clone()
+    loc[:, 0] -= base_el
+    ops.slerp_needed_sums(mem, lay, plan.chunks[:cut], cut, part, 0)
+    ops.slerp_needed_sums(shard, lay, loc, plan.nchunks - cut, part, cut)
+    torch.cuda.synchronize()
+    assert torch.equal(whole.view(torch.int64), part.view(torch.int64))
+    t = torch.full((plan.nseg,), 0.4, dtype=torch.float64, device=DEV)
+    coef, dots = ops.slerp_needed_coef(plan, whole, lay, t)
+    outs = [torch.empty(offs[-1], dtype=torch.bfloat16, device=DEV) for _ in pairs]
+    want_dots = ops.slerp_population(plan, mem, pairs, outs, t, speculate=False).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(dots[:len(pairs), :plan.nseg].cpu(), want_dots[:len(pairs), :plan.nseg].cpu())
+
+
 @pytest.mark.parametrize("world", [2, 8])
 def test_sharded_population_pair_merge_on_virtual_ranks(world):
     """EDT-LM children through the shards (edt_pair_merge_population on every rank's range) equal

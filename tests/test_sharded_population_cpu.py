@@ -1,5 +1,6 @@
 """The link-balanced population crossover (distributed.ShardedPopulationCrossover) on CPU: every
-rank owns a range of whole SLERP chunks of all members, the Gram rows are all-gathered, every
+rank owns a range of whole SLERP chunks of all members, the needed sums' table rows (r5; the Gram
+triangle's before) are all-gathered, every
 child's range is blended locally and sent to the child's rank. Virtual ranks (world 2..8) and a
 gloo world-3 run, with the CPU stand-in kernels (tests/oracle_kernels.ChunkGramKernels: same
 chunk semantics as the HIP passes): each child must equal the same arithmetic on the whole
@@ -74,6 +75,33 @@ def test_sharded_slerp_population_virtual(oracle, world, groups):
     for c in range(world):
         assert torch.equal(res[c][0].view(torch.int32), want[c].view(torch.int32)), c
         assert torch.equal(res[c][1], wdots)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("gen", range(3))
+def test_sharded_slerp_roulette_graphs_virtual(oracle, world, gen):
+    """r5: pair graphs drawn by EDT_RL's roulette selection (hubs, repeated and reversed pairs,
+    members no child uses): only the needed sums' table rows move, and every child equals the
+    whole-population triangle arithmetic bit for bit, with 1 and 3 groups."""
+    from evolutionarydistributedtraining_amd import ops
+    from evolutionarydistributedtraining_amd.schedule import roulette_generation_pairs
+    from tests.oracle_kernels import ChunkGramKernels
+    layout = ParamLayout(SHAPES)
+    members = _members(world, layout.total)
+    pairs = [tuple(p) for p in roulette_generation_pairs(world, gen + 1, seed=31)[gen]["pairs"]]
+    t = torch.tensor([0.3, 0.5, 0.9, 0.5, 0.43, 0.7, 0.5], dtype=torch.float64)
+    want, wdots = _whole(ChunkGramKernels(oracle), layout, members, pairs, t)
+    lay = ops.needed_table(pairs, world, ChunkGramKernels(oracle).make_slerp_plan(layout.offsets, "cpu",
+                                                                                 chunk_elems=CHUNK).nchunks)
+    assert sum(nt for _, nt in lay.blocks) <= world * (world + 1) // 2
+    used = {(min(a, b), max(a, b)) for a, b in pairs} | {(m, m) for p in pairs for m in p}
+    cols = {(min(a, b), max(a, b)) for blk in lay.columns for a, b in blk if a >= 0}
+    assert used <= cols                       # every sum a child reads is a column
+    for groups in (1, 3):
+        res = VirtualWorld(world).run(lambda comm: _run(comm, layout, members, pairs, t, oracle, "slerp", groups))
+        for c in range(world):
+            assert torch.equal(res[c][0].view(torch.int32), want[c].view(torch.int32)), (groups, c)
+            assert torch.equal(res[c][1], wdots)
 
 
 @pytest.mark.parametrize("world", [2, 4])
