@@ -141,6 +141,9 @@ def parse(argv=None):
                    help="N=1 population_7b: roulette-drawn generations timed (scales 0.1, 1.0, 2.5 in turn)")
     p.add_argument("--population-seed", type=int, default=2025, help="seed of the drawn generations")
     p.add_argument("--population-reps", type=int, default=10, help="timed calls per form and generation (>= 10)")
+    p.add_argument("--list-same-memory", type=int, default=1,
+                   help="list_form: also time the list kernel against the arena kernel on the same bytes (0: skip, "
+                        "as the PMC passes do: their launches are attributed in dispatch order)")
     p.add_argument("--population-layout", default="qwen2p5_7b_body",
                    help="N>1 population_slerp_7b: the member layout (BASELINE configs[4]: the 7.07B body)")
     return p.parse_args(argv)
@@ -717,7 +720,8 @@ def bench_list_form(args, dev):
         res[key] = rec
         del thetas, workers, state, step
     _free_device()
-    res["same_memory"] = _list_vs_arena_same_memory(args, dev, lay, K)
+    if getattr(args, "list_same_memory", 1):
+        res["same_memory"] = _list_vs_arena_same_memory(args, dev, lay, K)
     _free_device()
     return res
 
@@ -1037,6 +1041,10 @@ def bench_population_resident(args, dev, layout_name="qwen2p5_7b_body", members_
                                   "traffic_per_generation": traffic, "traffic_source": note}}
     ring = generation([(c, (c + 1) % M) for c in range(M)])
     ring["note"] = "the ring of children (c, c + 1 mod 8): r4's bench pairs, which roulette selection rarely draws"
+    if layout_name == "qwen2p5_7b_body":
+        for form in ("speculative", "two_pass"):
+            ring[form]["traffic"], ring[form]["traffic_source"] = _pmc_traffic(args, f"population_7b/ring/{form}",
+                                                                               with_note=True)
     res["ring"] = ring
     del members, outs
     _free_device()

@@ -7,8 +7,10 @@ cd "$(dirname "$0")/.."
 R=$(pwd); OUT=$R/gpurun_out/pmc_pop
 mkdir -p $OUT
 ARGS="--layout gpt2_small --steps 1 --warmup 0 --cpu-baseline-seconds 0 --bcast-compare 0 --place-candidates 1 --ops population_7b --population-generations 3 --population-reps 10"
+# counters on the population passes only (torch's fill launches are not profiled)
+KRE="slerp"
 for C in FETCH_SIZE WRITE_SIZE; do
-  (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --pmc $C --output-format csv \
+  (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --pmc $C --kernel-include-regex "$KRE" --output-format csv \
       -d $OUT/$C -o pmc -- python3 $R/bench.py $ARGS > $OUT/$C.log 2>&1); s=$?
   echo "$C pass: status $s"; tail -1 $OUT/$C.log | cut -c1-200
   [ $s -eq 0 ] || exit $s
