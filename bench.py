@@ -104,10 +104,11 @@ def parse(argv=None):
                         "timing the step's access pattern on each, once before the timed steps (placement.py); "
                         "1 keeps the first allocation")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
-    p.add_argument("--ops", default="list_form,configs1_125m,pair_merge,slerp_7b,population_7b",
+    p.add_argument("--ops", default="list_form,configs1_125m,pair_merge,slerp_7b,lm_population,population_7b",
                    help="the other hot-path measurements in the same line ('none': skip): N=1 list_form "
                         "(the drop-in tensor-list DiLoCo surface at 1.3B, first allocation), configs1_125m "
-                        "(BASELINE configs[1]: 125M x 8 resident), pair_merge, slerp_7b, population_7b "
+                        "(BASELINE configs[1]: 125M x 8 resident), pair_merge, slerp_7b, lm_population (the "
+                        "EDT-LM generation at 1.3B, rank-selected pairs), population_7b "
                         "(configs[4]: at N = 1 all 8 members resident on the GPU; at N > 1 "
                         "across the N GPUs)")
     p.add_argument("--ops-cpu-seconds", type=float, default=4.0, help="CPU baseline budget per extra op")
@@ -809,6 +810,68 @@ def bench_pair_merge(args, dev):
     return res
 
 
+def bench_lm_population(args, dev, layout_name="gpt_1p3b", members_n=8):
+    """The EDT-LM generation as its master draws it (EDT_LM/edt_sim.py:215-248, EDT_LM/edt.py:226-260:
+    rank_based_selection of P - ELITISM distinct pairs, ELITISM = 0 as EDT_LM/evolution.json sets
+    it; schedule.rank_generation_pairs with random fitness) on ONE GPU: 8 members of the 1.3B layout
+    resident (bf16 base, trained model and outer momentum each), every child's
+    EDT_LM/train/crossover.py:150-237 merge (lerp(.5) of the bases + the mean pseudo-gradient +
+    Nesterov SGD on parent 1's carried momentum) in one edt_pair_merge_population launch per
+    generation (all children of a chunk on one XCD, so a shared parent crosses HBM once and is
+    served from L2 to its other children), `--population-reps` timed calls per drawn generation. floor_bytes: each
+    distinct parent's base + trained read once, each distinct donor momentum once, each child's
+    output and momentum written once; algo_bytes: 14 B per element per child (pair_merge's)."""
+    from evolutionarydistributedtraining_amd import ops
+    from evolutionarydistributedtraining_amd.layouts import LAYOUTS
+    from evolutionarydistributedtraining_amd.schedule import rank_generation_pairs
+    lay = LAYOUTS[layout_name]()
+    P, bf, M = lay.total, torch.bfloat16, members_n
+    _free_device()
+    g = torch.Generator(device=dev).manual_seed(31)
+    base, trained, mom = [], [], []
+    x = torch.randn(P, generator=g, device=dev) * 0.02
+    for m in range(M):                  # one lineage: members 0.5 % apart, a short inner run each
+        b = (x + torch.randn(P, generator=g, device=dev) * 1e-4).to(bf)
+        base.append(b)
+        trained.append((b.float() + torch.randn(P, generator=g, device=dev) * 1e-3).to(bf))
+        mom.append((torch.randn(P, generator=g, device=dev) * 1e-3).to(bf))
+    del x
+    outs = [torch.empty(P, dtype=bf, device=dev) for _ in range(M)]
+    out_mom = [torch.empty(P, dtype=bf, device=dev) for _ in range(M)]
+    reps = max(10, args.population_reps)
+    gens = rank_generation_pairs(M, args.population_generations, seed=args.population_seed)
+    drawn = []
+    for gd in gens:
+        pairs = [tuple(p) for p in gd["pairs"]]
+        children = [{"b1": base[i], "b2": base[j], "m1": trained[i], "m2": trained[j], "out": outs[c],
+                     "momentum": out_mom[c], "momentum_in": mom[i], "has_momentum": True}
+                    for c, (i, j) in enumerate(pairs)]
+        ms = _event_ms(lambda: ops.pair_merge_population(children, args.lr, args.momentum, bool(args.nesterov)),
+                       reps, 1)
+        D = len({x for p in pairs for x in p})
+        donors = len({i for i, _ in pairs})
+        floor = P * (4 * D + 2 * donors + 4 * len(pairs))
+        drawn.append({"pairs": [list(p) for p in pairs], "distinct_parents": D, "donors": donors, "ms": round(ms, 3),
+                      "floor_bytes": floor, "floor_GBps": round(floor / (ms / 1e3) / 1e9, 1)})
+    fb = sum(r["floor_bytes"] for r in drawn)
+    ms = sum(r["ms"] for r in drawn)
+    algo = 14 * P * M * len(drawn)
+    res = {"workload": f"EDT-LM generation, {M} x {layout_name} (P={P}) bf16 base / trained / momentum resident, "
+                       f"pairs by EDT-LM's rank selection, lr {args.lr} mu {args.momentum} nesterov {bool(args.nesterov)}",
+           "kernel": "edt_pair_merge_population (pair_population_kernel: every child of a chunk on one XCD)",
+           "pairs_source": (f"schedule.rank_generation_pairs({M}, {args.population_generations}, "
+                            f"seed={args.population_seed}): EDT_LM/edt_sim.py:177-214 rank_based_selection, "
+                            f"ELITISM 0 (EDT_LM/evolution.json)"),
+           "timed_reps": reps, "generations": drawn, "ms_per_generation": round(ms / len(drawn), 3),
+           "roofline": {"bound": "hbm", "achieved": round(fb / (ms / 1e3) / 1e9, 1), "peak": HBM_PEAK_GBPS,
+                        "unit": "GB/s", "frac": round(fb / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+                        "bytes": "floor (each distinct parent / donor read once, each child written once)",
+                        "algo_GBps": round(algo / (ms / 1e3) / 1e9, 1)}}
+    del base, trained, mom, outs, out_mom
+    _free_device()
+    return res
+
+
 def bench_slerp_7b(args, dev):
     """SLERP crossover (EDT_RL/crossover.py:11-43 per state-dict key; EDT_EVOMERGE/train/
     crossover.py:104-146 over Qwen2.5-7B's `model.model`) of two 7.07B-parameter bodies, bf16 in
@@ -1442,7 +1505,8 @@ def main():
         theta = workers = sync = step = None
         _free_device()
         for name, fn in (("list_form", bench_list_form), ("configs1_125m", bench_config1),
-                         ("pair_merge", bench_pair_merge), ("slerp_7b", bench_slerp_7b)):
+                         ("pair_merge", bench_pair_merge), ("slerp_7b", bench_slerp_7b),
+                         ("lm_population", bench_lm_population)):
             if name in args.ops:
                 try:
                     out[name] = fn(args, dev)

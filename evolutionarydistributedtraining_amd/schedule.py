@@ -163,3 +163,25 @@ def roulette_generation_pairs(n_members: int, generations: int, seed: int = 0,
             random.setstate(state)
         out.append({"source": "roulette", "scale": scale, "seed": seed, "generation": g, "pairs": pairs})
     return out
+
+
+def rank_generation_pairs(n_members: int, generations: int, seed: int = 0, elitism: int = 0):
+    """Pair graphs as the EDT-LM master draws them (EDT_LM/edt_sim.py:215-243, EDT_LM/edt.py:226-260):
+    per generation, random fitness for `n_members` genomes, rank_based_selection of
+    n_members - elitism distinct pairs, then (elite, elite) for the top `elitism` genomes, as
+    member indices. Same private-RNG discipline as roulette_generation_pairs."""
+    out = []
+    rng = random.Random(seed)
+    for g in range(generations):
+        genomes = [{"fitness": rng.uniform(0.05, 1.0), "model_path": f"m{m}"} for m in range(n_members)]
+        state = random.getstate()
+        random.seed(rng.getrandbits(64))
+        try:
+            sel = rank_based_selection(genomes, n_members - elitism) if n_members > 1 else [(genomes[0], genomes[0])]
+        finally:
+            random.setstate(state)
+        ranked = sorted(genomes, key=lambda x: x["fitness"], reverse=True)
+        sel += [(e, e) for e in ranked[:elitism]] if n_members > 1 else []
+        out.append({"source": "rank", "elitism": elitism, "seed": seed, "generation": g,
+                    "pairs": pair_indices(sel, genomes)})
+    return out

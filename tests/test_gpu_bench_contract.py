@@ -95,3 +95,21 @@ def test_single_gpu_line_population_extra():
         r = f["roofline"]
         assert r["achieved"] == pytest.approx(fb / (ms / 1e3) / 1e9, rel=1e-2)
         assert r["frac"] == pytest.approx(r["achieved"] / r["peak"], abs=1e-3)
+
+
+def test_single_gpu_line_lm_population_extra():
+    """The N = 1 line's EDT-LM generation (lm_population: 8 members of the 1.3B layout resident,
+    rank-selected pairs, one edt_pair_merge_population launch per generation): fields and the
+    roofline arithmetic over the drawn generations' floor bytes."""
+    d = _run("--place-candidates", "1", "--ops", "lm_population", "--bcast-compare", "0",
+             "--population-generations", "2")
+    _check_common(d, 1)
+    p = d["lm_population"]
+    assert "error" not in p, p
+    assert "rank_based_selection" in p["pairs_source"] and len(p["generations"]) == 2 and p["timed_reps"] >= 10
+    fb = sum(g["floor_bytes"] for g in p["generations"])
+    ms = sum(g["ms"] for g in p["generations"])
+    for g in p["generations"]:
+        assert len(g["pairs"]) == 8 and all(a != b for a, b in g["pairs"])
+        assert g["distinct_parents"] == len({x for q in g["pairs"] for x in q})
+    assert p["roofline"]["achieved"] == pytest.approx(fb / (ms / 1e3) / 1e9, rel=1e-2)

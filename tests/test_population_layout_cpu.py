@@ -67,3 +67,24 @@ def test_layout_rejects_bad_pairs():
     from evolutionarydistributedtraining_amd._lib import EdtError
     with pytest.raises(EdtError):
         ops.population_layout([(0, 9)], 8)
+
+
+def test_rank_generation_pairs_follow_the_lm_master():
+    """schedule.rank_generation_pairs: EDT_LM's rank_based_selection of P - ELITISM distinct
+    unordered pairs (two different parents each) + (elite, elite) pairs, deterministic per seed,
+    leaving the global random state alone."""
+    import random
+
+    from evolutionarydistributedtraining_amd.schedule import rank_generation_pairs
+    random.seed(123)
+    before = random.getstate()
+    gens = rank_generation_pairs(8, 20, seed=9)
+    assert random.getstate() == before
+    assert gens == rank_generation_pairs(8, 20, seed=9)
+    for g in gens:
+        pairs = g["pairs"]
+        assert len(pairs) == 8 and all(a != b for a, b in pairs)
+        assert len({tuple(sorted(p)) for p in pairs}) == 8
+    el = rank_generation_pairs(8, 5, seed=9, elitism=2)
+    for g in el:
+        assert len(g["pairs"]) == 8 and g["pairs"][-1][0] == g["pairs"][-1][1] and g["pairs"][-2][0] == g["pairs"][-2][1]
