@@ -404,9 +404,10 @@ class ShardedPopulationCrossover:
          every link busy: (N-1)/N of a member out and in per rank);
       2. SLERP: per chunk of the rank's range the sums the generation needs — each distinct
          parent's norm and each distinct dot its children use, per connected component of the
-         pair graph (edt_slerp_needed_sums: edt_slerp_population's needed-sums pass, r5; at most
-         D + 8 sums for 8 children against the Gram triangle's 36) — the table rows all-gathered
-         (nchunks x those sums doubles: ~12 MB at 7B for a roulette-drawn generation, against ~31 MB
+         pair graph (edt_slerp_needed_sums: edt_slerp_population's needed-sums pass, r5; a
+         component's row is its D norms, D ring-dot and <= 4 chord slots, against the Gram
+         triangle's 36 at N = 8) — the table rows all-gathered
+         (nchunks x those sums doubles: 12-16 MB at 7B for a roulette-drawn generation, against ~31 MB
          for the triangle), then every child's coefficients (edt_slerp_needed_coef) — each chunk's
          sums come from the same kernel in the same order wherever the chunk lives, so every child
          is bit-identical to edt_slerp_merge on its two parents; then the rank's range of every
