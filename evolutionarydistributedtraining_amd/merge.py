@@ -467,7 +467,7 @@ class _Bound:
     def __init__(self, key, model_1, model_2, dev, rec):
         import weakref
         self.key, self.dev = key, dev
-        drop = lambda _r, key=key: _bound_cache.pop(key, None)
+        drop = lambda _r, key=key, cache=_bound_cache: cache.pop(key, None)   # safe at interpreter exit
         self.r1, self.r2 = weakref.ref(model_1, drop), weakref.ref(model_2, drop)
         for k, v in rec.items():
             setattr(self, k, v)

@@ -779,13 +779,27 @@ class SlerpListBinding:
         a0, a1, a2 = (a.ctypes.data_as(vp) for a in arrs)
         numel_arr = np.ascontiguousarray(plan.seg_numel, dtype=np.uint64)   # alive across both calls below
         numel = numel_arr.ctypes.data_as(ctypes.c_void_p) if T else None
-        host = np.zeros(max(1, 3 * T), dtype=np.uint64)
-        hp = host.ctypes.data_as(ctypes.c_void_p)
+        n3 = max(1, 3 * T)
+        # the table image goes straight into the plan's pinned staging buffer and up by an async copy
+        # (a pageable upload waits for its staging: the largest host cost of a repeated binding); the
+        # buffer is rewritten only after the previous upload from it has completed
+        stage, ev = getattr(plan, "_table_stage", None), getattr(plan, "_table_stage_ev", None)
+        if stage is None or stage.numel() < n3:
+            stage = plan._table_stage = torch.zeros(n3, dtype=torch.int64, pin_memory=torch.cuda.is_available())
+        elif ev is not None:
+            ev.synchronize()
+        hp = ctypes.c_void_p(stage.data_ptr())
         # every output apart from everything but its own parents (the two-pass form's rule, r5: in C)
         L.check(lib.edt_slerp_seg_table(a0, a1, a2, T, numel, self.in_dt, self.out_dt, 0, hp), "edt_slerp_seg_table")
         # outputs apart from every parent (a sorted-span check in C): the single-pass form is allowed
         self.apart = lib.edt_slerp_seg_table(a0, a1, a2, T, numel, self.in_dt, self.out_dt, 1, hp) == 0
-        self.table = torch.from_numpy(host.view(np.int64)).to(self.device)
+        if self.device is not None and self.device.type == "cuda":
+            self.table = torch.empty(n3, dtype=torch.int64, device=self.device)
+            self.table.copy_(stage[:n3], non_blocking=True)
+            ev = plan._table_stage_ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+        else:
+            self.table = stage[:n3].clone()
 
     def merge(self, t: torch.Tensor, dot_threshold: float = 0.9995, eps: float = 1e-8,
               speculate: bool | None = None, ref_dot: RefDot | None = None) -> None:
