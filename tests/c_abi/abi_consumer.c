@@ -8,8 +8,8 @@
  * EDT_RL/crossover.py:84-135 would drive it (edt_slerp_make_chunks -> relative chunk starts ->
  * edt_slerp_merge_list, and the single-pass edt_slerp_merge_list_speculative): parents of one
  * lineage, so every tensor takes the lerp branch, whose output is compared bit for bit with the
- * oracle's lerp, and the two forms with each other (outputs and dots). Prints "abi consumer ok"
- * and exits 0 on success. */
+ * oracle's lerp, and the two forms with each other (outputs and dots). Then a resident
+ * population (population_check). Prints "abi consumer ok" and exits 0 on success. */
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -141,6 +141,130 @@ static int slerp_list_check(void) {
     return 0;
 }
 
+/* A resident population through the C ABI (BASELINE configs[4], EDT_RL/edt.py:286-299): 6 members
+ * of 5 ragged tensors in flat arenas, 8 children on a roulette-like pair graph (a hub parent, a
+ * repeated pair, a reversed pair, a self-pair), lineage members so most tensors take the lerp
+ * branch and two far members the SLERP branch. Three routes, every child bit for bit:
+ *   edt_slerp_population_speculative (the one-pass form) against edt_slerp_merge per child;
+ *   the sharded stages at one rank — edt_slerp_needed_table, edt_slerp_needed_sums over two chunk
+ *   ranges (rows written where they belong), edt_slerp_needed_coef, edt_slerp_blend_children —
+ *   against the same. */
+#define PM 6
+#define PQ 8
+#define PSEG 5
+static int population_check(void) {
+    const uint64_t sizes[PSEG] = {70001, 9, 131072, 4099, 1};
+    uint64_t offs[PSEG + 1] = {0};
+    for (int s = 0; s < PSEG; ++s) offs[s + 1] = offs[s] + sizes[s];
+    const uint64_t n = offs[PSEG];
+    int32_t first[PSEG + 1];
+    const int64_t need = edt_slerp_make_chunks(offs, PSEG, 8192u, NULL, 0, first);
+    const int64_t nchunks = need < 0 ? -need - 1 : need;
+    uint64_t* desc = malloc(3 * nchunks * sizeof(uint64_t));
+    if (nchunks <= 0 || edt_slerp_make_chunks(offs, PSEG, 8192u, desc, nchunks, first) != nchunks) return 1;
+    const int32_t pairs[2 * PQ] = {0, 5, 5, 2, 0, 1, 5, 3, 2, 5, 4, 4, 1, 0, 5, 2};
+    const double tv[PSEG] = {0.5, 0.3, 0.43, 0.9, 0.5};
+    float* base = malloc(n * sizeof(float));
+    for (uint64_t i = 0; i < n; ++i) base[i] = 0.02f * uniform();
+    void *d_mem[PM], *d_out[PQ], *d_out2[PQ], *d_want;
+    float* h = malloc(n * sizeof(float));
+    for (int m = 0; m < PM; ++m) {
+        const float rel = (m == 3 || m == 4) ? 0.5f : 1e-3f;          /* members 3, 4 far from the lineage */
+        for (uint64_t i = 0; i < n; ++i) h[i] = base[i] + 0.02f * rel * uniform();
+        CK(hipMalloc(&d_mem[m], n * sizeof(float)));
+        CK(hipMemcpy(d_mem[m], h, n * sizeof(float), hipMemcpyHostToDevice));
+    }
+    for (int q = 0; q < PQ; ++q) {
+        CK(hipMalloc(&d_out[q], n * sizeof(float)));
+        CK(hipMalloc(&d_out2[q], n * sizeof(float)));
+    }
+    CK(hipMalloc(&d_want, n * sizeof(float)));
+    void *d_desc, *d_first, *d_t, *d_partial, *d_coef, *d_dots, *d_redo, *d_pcoef, *d_pdots;
+    const uint64_t spec = edt_slerp_population_speculative_doubles(PQ, nchunks);
+    const uint64_t pair_nd = edt_slerp_sums_doubles(3, nchunks);
+    CK(hipMalloc(&d_desc, 3 * nchunks * sizeof(uint64_t)));
+    CK(hipMalloc(&d_first, sizeof(first)));
+    CK(hipMalloc(&d_t, sizeof(tv)));
+    CK(hipMalloc(&d_partial, (spec > pair_nd ? spec : pair_nd) * sizeof(double)));
+    CK(hipMalloc(&d_coef, 2 * PQ * PSEG * sizeof(float)));
+    CK(hipMalloc(&d_dots, PQ * PSEG * sizeof(float)));
+    CK(hipMalloc(&d_redo, PQ * PSEG * sizeof(int32_t)));
+    CK(hipMalloc(&d_pcoef, 2 * PSEG * sizeof(float)));
+    CK(hipMalloc(&d_pdots, PSEG * sizeof(float)));
+    CK(hipMemcpy(d_desc, desc, 3 * nchunks * sizeof(uint64_t), hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_first, first, sizeof(first), hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_t, tv, sizeof(tv), hipMemcpyHostToDevice));
+    int rc = edt_slerp_population_speculative((const void* const*)d_mem, PM, EDT_F32, pairs, PQ, d_out, EDT_F32, d_desc,
+                                              nchunks, d_first, PSEG, d_t, 0.9995, 1e-8, d_partial, d_coef, d_dots,
+                                              d_redo, n, NULL);
+    if (rc != 0) {
+        fprintf(stderr, "edt_slerp_population_speculative: %d %s\n", rc, edt_last_error());
+        return 1;
+    }
+    /* the sharded stages at one rank: the needed table, its rows in two chunk ranges */
+    uint64_t boff[8], tdoubles = 0, sdoubles = 0;
+    int32_t bnt[8], ncomp = 0;
+    rc = edt_slerp_needed_table(pairs, PQ, PM, nchunks, boff, bnt, &ncomp, NULL, &tdoubles, &sdoubles);
+    void *d_table, *d_scratch, *d_desc2;
+    CK(hipMalloc(&d_table, tdoubles * sizeof(double)));
+    CK(hipMalloc(&d_scratch, sdoubles * sizeof(double)));
+    const int64_t cut = nchunks / 3;
+    CK(hipMalloc(&d_desc2, 3 * nchunks * sizeof(uint64_t)));
+    CK(hipMemcpy(d_desc2, desc, 3 * nchunks * sizeof(uint64_t), hipMemcpyHostToDevice));
+    if (rc == 0)
+        rc = edt_slerp_needed_sums((const void* const*)d_mem, PM, EDT_F32, pairs, PQ, d_desc2, cut, nchunks, 0,
+                                   d_table, d_scratch, sdoubles, NULL);
+    if (rc == 0)
+        rc = edt_slerp_needed_sums((const void* const*)d_mem, PM, EDT_F32, pairs, PQ,
+                                   (const uint64_t*)d_desc2 + 3 * cut, nchunks - cut, nchunks, cut, d_table,
+                                   d_scratch, sdoubles, NULL);
+    if (rc == 0)
+        rc = edt_slerp_needed_coef(d_table, nchunks, pairs, PQ, PM, d_first, PSEG, d_t, 0.9995, 1e-8, d_coef, NULL,
+                                   NULL);
+    if (rc == 0)
+        rc = edt_slerp_blend_children((const void* const*)d_mem, PM, EDT_F32, pairs, PQ, d_out2, EDT_F32, d_desc,
+                                      nchunks, d_coef, PSEG, NULL);
+    if (rc != 0) {
+        fprintf(stderr, "needed-sums stages: %d %s\n", rc, edt_last_error());
+        return 1;
+    }
+    float *a = malloc(n * sizeof(float)), *b = malloc(n * sizeof(float)), *w = malloc(n * sizeof(float));
+    int slerp_branch = 0;
+    for (int q = 0; q < PQ; ++q) {
+        rc = edt_slerp_merge(d_mem[pairs[2 * q]], d_mem[pairs[2 * q + 1]], EDT_F32, d_want, EDT_F32, d_desc, nchunks,
+                             d_first, PSEG, d_t, 0.9995, 1e-8, d_partial, d_pcoef, d_pdots, NULL);
+        if (rc != 0) {
+            fprintf(stderr, "edt_slerp_merge: %d %s\n", rc, edt_last_error());
+            return 1;
+        }
+        CK(hipDeviceSynchronize());
+        float pd[PSEG];
+        CK(hipMemcpy(pd, d_pdots, sizeof(pd), hipMemcpyDeviceToHost));
+        for (int s = 0; s < PSEG; ++s) slerp_branch += !(pd[s] > 0.9995f || pd[s] < -0.9995f);
+        CK(hipMemcpy(w, d_want, n * sizeof(float), hipMemcpyDeviceToHost));
+        CK(hipMemcpy(a, d_out[q], n * sizeof(float), hipMemcpyDeviceToHost));
+        CK(hipMemcpy(b, d_out2[q], n * sizeof(float), hipMemcpyDeviceToHost));
+        if (memcmp(a, w, n * sizeof(float)) != 0 || memcmp(b, w, n * sizeof(float)) != 0) {
+            fprintf(stderr, "child %d (%d, %d) differs from edt_slerp_merge (speculative %d, stages %d)\n", q,
+                    pairs[2 * q], pairs[2 * q + 1], memcmp(a, w, n * sizeof(float)) != 0,
+                    memcmp(b, w, n * sizeof(float)) != 0);
+            return 1;
+        }
+    }
+    if (slerp_branch == 0) {
+        fprintf(stderr, "no child segment took the SLERP branch\n");
+        return 1;
+    }
+    for (int m = 0; m < PM; ++m) hipFree(d_mem[m]);
+    for (int q = 0; q < PQ; ++q) {
+        hipFree(d_out[q]);
+        hipFree(d_out2[q]);
+    }
+    printf("population (%d children over %d members, %d components): one-pass form and needed-sums stages "
+           "bit-identical to edt_slerp_merge per child (%d SLERP-branch segments)\n", PQ, PM, ncomp, slerp_branch);
+    return 0;
+}
+
 int main(void) {
     if (edt_abi_version() != EDT_ABI_VERSION) {     /* workspace sizes and signatures follow the header */
         fprintf(stderr, "library ABI %d, header ABI %d: rebuild\n", edt_abi_version(), EDT_ABI_VERSION);
@@ -202,5 +326,7 @@ int main(void) {
     for (int k = 0; k < K; ++k) hipFree(d_w[k]);
     hipFree(d_theta);
     hipFree(d_mom);
-    return slerp_list_check() ? 1 : (printf("abi consumer ok\n"), 0);
+    if (slerp_list_check() || population_check()) return 1;
+    printf("abi consumer ok\n");
+    return 0;
 }

@@ -767,14 +767,16 @@ def test_c_consumer_runs():
     hipMalloc'd buffers, two edt_outer_step calls on the null stream, bit-exact against the C
     oracle, and the negative-code + edt_last_error() convention for a bad argument; then the
     tensor-list SLERP (two-pass and speculative) over separate hipMalloc'd tensors, bit-exact with
-    the oracle's lerp branch and with each other."""
+    the oracle's lerp branch and with each other; then a resident population of 8 children over 6
+    members (r5): the one-pass form and the sharded needed-sums stages (table, sums over two chunk
+    ranges, coefficients, blends), every child bit-identical to edt_slerp_merge."""
     import subprocess
     exe = os.path.join(ROOT, "tests", "c_abi", "_build", "abi_consumer")
     if not os.path.exists(exe):
         subprocess.run(["make", "-s", "-C", os.path.dirname(os.path.dirname(exe))], check=True)
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120, cwd="/")
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "abi consumer ok" in r.stdout and "slerp list" in r.stdout
+    assert "abi consumer ok" in r.stdout and "slerp list" in r.stdout and "population (8 children" in r.stdout
 
 
 def test_c_comm_consumer_runs():
