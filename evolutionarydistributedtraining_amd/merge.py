@@ -502,8 +502,8 @@ def _bound_merge(b: _Bound, model_1, model_2) -> bool:
     caller merges the uncached way."""
     buf = torch.empty(b.total, dtype=b.out_dt, device=b.dev)
     po = np.uint64(buf.data_ptr()) + b.offs_bytes
-    ops.SlerpListBinding.from_pointers(b.splan, b.p0, b.p1, po, b.in_dt, b.out_dt, b.dev,
-                                       keep=(buf, b.buf, b.hold2)).merge(b.tt, ref_dot=_ref_dot)
+    ops.SlerpListBinding.from_checked(b.splan, b.p0, b.p1, po, b.in_dt, b.out_dt, b.dev,
+                                      keep=(buf, b.buf, b.hold2)).merge(b.tt, ref_dot=_ref_dot)
     cur = torch.cuda.current_stream(b.dev)
     sd1 = module_tensors(model_1)
     sd2 = module_tensors(model_2)

@@ -710,6 +710,28 @@ def writes_safe(starts, nbytes) -> bool:
 _ELEM_SIZE = {torch.float32: 4, torch.bfloat16: 2, torch.float16: 2, torch.float64: 8}
 
 
+def _table_stage(plan, n3: int) -> torch.Tensor:
+    """The plan's pinned staging buffer for a pointer-table image (>= n3 int64), once the previous
+    upload from it has completed: the image is written there and goes up by an async copy (a
+    pageable upload waits for its own staging, the largest host cost of a repeated binding)."""
+    stage, ev = getattr(plan, "_table_stage", None), getattr(plan, "_table_stage_ev", None)
+    if stage is None or stage.numel() < n3:
+        stage = plan._table_stage = torch.zeros(n3, dtype=torch.int64, pin_memory=torch.cuda.is_available())
+    elif ev is not None:
+        ev.synchronize()
+    return stage
+
+
+def _table_upload(plan, stage: torch.Tensor, n3: int, device) -> torch.Tensor:
+    if device is not None and device.type == "cuda":
+        table = torch.empty(n3, dtype=torch.int64, device=device)
+        table.copy_(stage[:n3], non_blocking=True)
+        ev = plan._table_stage_ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(device))
+        return table
+    return stage[:n3].clone()
+
+
 class SlerpListBinding:
     """A tensor-list SLERP bound to its tensors (EDT_EVOMERGE/train/crossover.py:104-146's state-dict
     tensors, merged where they lie): the per-tensor checks run once here and the validated
@@ -780,26 +802,37 @@ class SlerpListBinding:
         numel_arr = np.ascontiguousarray(plan.seg_numel, dtype=np.uint64)   # alive across both calls below
         numel = numel_arr.ctypes.data_as(ctypes.c_void_p) if T else None
         n3 = max(1, 3 * T)
-        # the table image goes straight into the plan's pinned staging buffer and up by an async copy
-        # (a pageable upload waits for its staging: the largest host cost of a repeated binding); the
-        # buffer is rewritten only after the previous upload from it has completed
-        stage, ev = getattr(plan, "_table_stage", None), getattr(plan, "_table_stage_ev", None)
-        if stage is None or stage.numel() < n3:
-            stage = plan._table_stage = torch.zeros(n3, dtype=torch.int64, pin_memory=torch.cuda.is_available())
-        elif ev is not None:
-            ev.synchronize()
+        stage = _table_stage(plan, n3)
         hp = ctypes.c_void_p(stage.data_ptr())
         # every output apart from everything but its own parents (the two-pass form's rule, r5: in C)
         L.check(lib.edt_slerp_seg_table(a0, a1, a2, T, numel, self.in_dt, self.out_dt, 0, hp), "edt_slerp_seg_table")
         # outputs apart from every parent (a sorted-span check in C): the single-pass form is allowed
         self.apart = lib.edt_slerp_seg_table(a0, a1, a2, T, numel, self.in_dt, self.out_dt, 1, hp) == 0
-        if self.device is not None and self.device.type == "cuda":
-            self.table = torch.empty(n3, dtype=torch.int64, device=self.device)
-            self.table.copy_(stage[:n3], non_blocking=True)
-            ev = plan._table_stage_ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(self.device))
-        else:
-            self.table = stage[:n3].clone()
+        self.table = _table_upload(plan, stage, n3, self.device)
+
+    @classmethod
+    def from_checked(cls, plan: SlerpPlan, p0, p1, pout, in_dtype: torch.dtype, out_dtype: torch.dtype,
+                     device: torch.device, keep) -> "SlerpListBinding":
+        """from_pointers for addresses that were validated before and cannot have changed
+        (merge._Bound's repeat: the parents' addresses are exactly those an earlier binding checked,
+        with their memory held; the outputs are views of a fresh buffer at 16-byte aligned offsets,
+        apart from every parent by construction). The table image is written without the C checks
+        (every invariant they test holds by construction), into the plan's pinned staging buffer."""
+        import numpy as np
+        self = cls.__new__(cls)
+        T = plan.nseg
+        if not plan.relative or not (len(p0) == len(p1) == len(pout) == T):
+            raise L.EdtError("slerp_list needs a relative plan with one segment per tensor")
+        self.device, self.plan = device, plan
+        self.in_dt, self.out_dt = L.dtype_code(in_dtype), L.dtype_code(out_dtype)
+        self.in_size, self.out_size = _ELEM_SIZE[in_dtype], _ELEM_SIZE[out_dtype]
+        self._keep, self.apart = keep, True
+        n3 = max(1, 3 * T)
+        stage = _table_stage(plan, n3)
+        img = stage.numpy()[:3 * T].reshape(T, 3).view(np.uint64)
+        img[:, 0], img[:, 1], img[:, 2] = p0, p1, pout
+        self.table = _table_upload(plan, stage, n3, device)
+        return self
 
     def merge(self, t: torch.Tensor, dot_threshold: float = 0.9995, eps: float = 1e-8,
               speculate: bool | None = None, ref_dot: RefDot | None = None) -> None:

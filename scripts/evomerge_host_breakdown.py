@@ -101,7 +101,7 @@ def main():
         buf = torch.empty(b.total, dtype=b.out_dt, device=b.dev)
         po = np.uint64(buf.data_ptr()) + b.offs_bytes
         t0 = t("fresh buffer", t0)
-        bd = ops.SlerpListBinding.from_pointers(b.splan, b.p0, b.p1, po, b.in_dt, b.out_dt, b.dev, keep=(buf, b.buf, b.hold2))
+        bd = ops.SlerpListBinding.from_checked(b.splan, b.p0, b.p1, po, b.in_dt, b.out_dt, b.dev, keep=(buf, b.buf, b.hold2))
         t0 = t("binding (C checks + table upload)", t0)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()

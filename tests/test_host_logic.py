@@ -541,3 +541,28 @@ def test_binding_from_pointers_host_checks():
         ops.SlerpListBinding.from_pointers(plan, p0[:2], p1[:2], po[:2], torch.bfloat16, torch.bfloat16,
                                            torch.device("cpu"), keep=None)
     assert sizes == plan.seg_numel.tolist()
+
+
+def test_binding_from_checked_writes_the_checked_image():
+    """SlerpListBinding.from_checked (merge._Bound's repeat: addresses validated before, outputs a
+    fresh buffer) writes the same table image as the C-checked binding, with the single-pass form
+    allowed, and refuses a plan of another segment count."""
+    import numpy as np
+
+    from evolutionarydistributedtraining_amd import ops
+    ns = np.array([70001, 9, 131072, 4099, 1, 8], dtype=np.int64)
+    T = len(ns)
+    o = np.zeros(T, dtype=np.uint64)
+    o[1:] = np.cumsum((ns + 7) // 8 * 8)[:-1].astype(np.uint64)
+    p0, p1, po = [np.uint64(b << 40) + o * np.uint64(2) for b in (1, 2, 3)]
+
+    class Plan:
+        relative, nseg, seg_numel = True, T, ns
+    plan = Plan()
+    fast = ops.SlerpListBinding.from_checked(plan, p0, p1, po, torch.bfloat16, torch.bfloat16, None, None)
+    slow = ops.SlerpListBinding.__new__(ops.SlerpListBinding)
+    slow.device = None
+    slow._bind(plan, p0, p1, po, torch.bfloat16, torch.bfloat16, None)
+    assert slow.apart and fast.apart and torch.equal(fast.table, slow.table)
+    with pytest.raises(ops.L.EdtError):
+        ops.SlerpListBinding.from_checked(plan, p0[:-1], p1[:-1], po[:-1], torch.bfloat16, torch.bfloat16, None, None)
