@@ -866,7 +866,10 @@ def bench_lm_population(args, dev, layout_name="gpt_1p3b", members_n=8):
            "roofline": {"bound": "hbm", "achieved": round(fb / (ms / 1e3) / 1e9, 1), "peak": HBM_PEAK_GBPS,
                         "unit": "GB/s", "frac": round(fb / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
                         "bytes": "floor (each distinct parent / donor read once, each child written once)",
-                        "algo_GBps": round(algo / (ms / 1e3) / 1e9, 1)}}
+                        "algo_GBps": round(algo / (ms / 1e3) / 1e9, 1),
+                        "floor_bytes_per_generation": fb // len(drawn)}}
+    res["roofline"]["traffic_per_generation"], res["roofline"]["traffic_source"] = _pmc_traffic(
+        args, "lm_population/gpt_1p3b/rank", with_note=True)
     del base, trained, mom, outs, out_mom
     _free_device()
     return res

@@ -42,8 +42,10 @@ def needs_build(out: str = OUT) -> bool:
 TU_FLAGS = {"edt_slerp.hip": ["-mllvm", "-structurizecfg-skip-uniform-regions=true"]}
 
 
-def build_library(force: bool = False, extra_flags: list[str] | None = None, out: str = OUT) -> str:
-    """One object per translation unit, compiled in parallel (build/obj), then linked."""
+def build_library(force: bool = False, extra_flags: list[str] | None = None, out: str = OUT,
+                  tu_extra: dict | None = None) -> str:
+    """One object per translation unit, compiled in parallel (build/obj), then linked. extra_flags:
+    added to every unit (variant builds: -D tunables); tu_extra: {file name: flags} for one unit."""
     if force or needs_build(out):
         from concurrent.futures import ThreadPoolExecutor
         objdir = os.path.join(ROOT, "build", "obj", os.path.basename(out))
@@ -53,6 +55,7 @@ def build_library(force: bool = False, extra_flags: list[str] | None = None, out
         def compile_one(src):
             obj = os.path.join(objdir, os.path.basename(src) + ".o")
             cmd = [hipcc(), *flags, *TU_FLAGS.get(os.path.basename(src), []), *(extra_flags or []),
+                   *(tu_extra or {}).get(os.path.basename(src), []),
                    "-I", os.path.dirname(HEADER), "-I", CSRC, "-c", src, "-o", obj]
             subprocess.run(cmd, check=True)
             return obj

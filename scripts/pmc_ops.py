@@ -51,6 +51,13 @@ def main():
                                "hbm_bytes_per_launch": stats["hbm_bytes_per_launch"] + blend["hbm_bytes_per_launch"],
                                "algorithmic_bytes": 6 * P7, "moved_bytes": 10 * P7,
                                "note": "two-pass: chunk sums (4 B/elem read) + blend (4 B read, 2 B written)"}
+    # r5: the EDT-LM generation on rank-selected pairs (bench_lm_population): one launch per call,
+    # the drawn generations' calls together (their floors differ: the mean floor is in the line)
+    lm = traffic("pair_population_kernel")
+    if lm:
+        lm.update(correction="FETCH_SIZE x2 (16 B/lane bf16 loads), WRITE_SIZE x1",
+                  note="per generation, median over the drawn generations' calls")
+        out["lm_population/gpt_1p3b/rank"] = lm
     # r5: the drop-in tensor-list step (bench_list_form): fp32, then bf16 without and with the
     # tail masks — one template for both bf16 runs, so its launches are split in dispatch order
     import csv
