@@ -13,7 +13,7 @@ import csv
 import sys
 
 
-def summarise(path, subs=("outer_kernel", "outer_list_kernel", "pair_kernel", "slerp", "lerp_kernel", "sgd_apply")):
+def summarise(path, subs=("outer_kernel", "outer_list_kernel", "pair_kernel", "pair_population", "slerp", "lerp_kernel", "sgd_apply")):
     groups = collections.defaultdict(list)
     with open(path) as f:
         for r in csv.DictReader(f):
