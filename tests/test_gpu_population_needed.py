@@ -106,3 +106,32 @@ def test_needed_layout_edge_cases(dev, ops, case, speculate):
 def test_roulette_drawn_dtype_routes(dev, ops, k, in_dt, out_dt):
     for speculate in (False, True):
         _check(ops, dev, ROULETTE[k], speculate, in_dt=in_dt, out_dt=out_dt, seed=100 + k)
+
+
+def _random_graphs(n, seed=77):
+    import random
+    rng = random.Random(seed)
+    out = []
+    for _ in range(n):
+        M = rng.randint(1, 8)
+        Q = rng.randint(1, 24)
+        pairs = []
+        for _q in range(Q):
+            a = rng.randrange(M)
+            b = a if rng.random() < 0.1 else rng.randrange(M)        # self pairs, repeats, reversals
+            pairs.append((a, b))
+        out.append(pairs)
+    return out
+
+
+RANDOM_GRAPHS = _random_graphs(40)
+
+
+@pytest.mark.parametrize("k", range(len(RANDOM_GRAPHS)))
+def test_random_pair_graphs_both_forms(dev, ops, k):
+    """Seeded random pair graphs over 1..8 members with 1..24 children (self pairs, repeated and
+    reversed pairs, isolated members, components of every size; the planner picks needed / triangle
+    / member-major / co-located per case): both forms bit-identical to edt_slerp_merge per child."""
+    pairs = RANDOM_GRAPHS[k]
+    for speculate in (False, True):
+        _check(ops, dev, pairs, speculate, seed=300 + k)

@@ -150,7 +150,7 @@ def test_sharded_population_slerp_on_virtual_ranks(world, out_dt, groups):
         assert torch.equal(res[0][1][c], plan.dots[:plan.nseg]), c
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("world", [2, 3, 4, 5, 8])
 @pytest.mark.parametrize("gen", range(4))
 def test_sharded_population_roulette_graphs_on_virtual_ranks(world, gen):
     """r5: the sharded population forms only the needed sums (edt_slerp_needed_sums over each rank's
