@@ -711,12 +711,19 @@ _ELEM_SIZE = {torch.float32: 4, torch.bfloat16: 2, torch.float16: 2, torch.float
 
 
 def _table_stage(plan, n3: int) -> torch.Tensor:
-    """The plan's pinned staging buffer for a pointer-table image (>= n3 int64), once the previous
-    upload from it has completed: the image is written there and goes up by an async copy (a
-    pageable upload waits for its own staging, the largest host cost of a repeated binding)."""
-    stage, ev = getattr(plan, "_table_stage", None), getattr(plan, "_table_stage_ev", None)
+    """One of the plan's two pinned staging buffers for a pointer-table image (>= n3 int64), in
+    turn, once the upload from it two bindings ago has completed: the image is written there and
+    goes up by an async copy (a pageable upload waits for its own staging, the largest host cost of
+    a repeated binding); alternating buffers, a binding never waits for the previous one's copy,
+    which may sit behind other work on the stream."""
+    stages = plan.__dict__.setdefault("_table_stages", [None, None])
+    events = plan.__dict__.setdefault("_table_stage_evs", [None, None])
+    k = plan.__dict__["_table_stage_next"] = 1 - plan.__dict__.get("_table_stage_next", 1)
+    stage, ev = stages[k], events[k]
     if stage is None or stage.numel() < n3:
-        stage = plan._table_stage = torch.zeros(n3, dtype=torch.int64, pin_memory=torch.cuda.is_available())
+        if ev is not None:
+            ev.synchronize()                     # the old buffer may still be read by its copy
+        stage = stages[k] = torch.zeros(n3, dtype=torch.int64, pin_memory=torch.cuda.is_available())
     elif ev is not None:
         ev.synchronize()
     return stage
@@ -726,8 +733,9 @@ def _table_upload(plan, stage: torch.Tensor, n3: int, device) -> torch.Tensor:
     if device is not None and device.type == "cuda":
         table = torch.empty(n3, dtype=torch.int64, device=device)
         table.copy_(stage[:n3], non_blocking=True)
-        ev = plan._table_stage_ev = torch.cuda.Event()
+        ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(device))
+        plan.__dict__["_table_stage_evs"][plan.__dict__["_table_stage_next"]] = ev
         return table
     return stage[:n3].clone()
 
