@@ -88,13 +88,9 @@ using edt::g_err;
 #define EDT_GRAM_NT 1
 #endif
 // Needed-sums pass (r5, edt_slerp.hip): elements converted to fp64 per group before the dot
-// slots' switches (4: two groups per lane vector; 2: four), and the next tile's loads in flight
-// while this tile is summed (two register sets, bf16 members).
+// slots' switches (4: two groups per lane vector; 2: four).
 #ifndef EDT_NEED_GROUP
 #define EDT_NEED_GROUP 8
-#endif
-#ifndef EDT_NEED_PREFETCH
-#define EDT_NEED_PREFETCH 0
 #endif
 #ifndef EDT_NEED_MIN_WAVES      // needed-sums pass: __launch_bounds__ minimum waves per SIMD
 #define EDT_NEED_MIN_WAVES 1

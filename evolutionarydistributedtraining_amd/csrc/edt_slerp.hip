@@ -1157,16 +1157,16 @@ __device__ __forceinline__ void need_emit(const X (&x)[D], const NeedSpec& S, ui
 
 // The needed sums as rows of level 4, one workgroup per unit of 16 tiles in address order (the
 // Gram kernel's grid, reduction and row format; tiles past the chunk's aligned body load zeros,
-// which leave every chain's bits unchanged). bf16 members: the next tile's loads in flight while
-// this tile is summed (two register sets).
+// which leave every chain's bits unchanged). bf16 members: the next tiles land in LDS by DMA while
+// this tile is summed from registers (below; a two-register-set prefetch measured slower: its
+// VGPRs cost a wave per SIMD).
 template <int IDT, int D, bool EMIT = false, int ODT = EDT_BF16>
 __global__ __launch_bounds__(kBlock, EDT_NEED_MIN_WAVES) void slerp_need_kernel(Members mem, NeedSpec S,
                                                                                  const uint64_t* chunks,
                                                                                  int64_t nchunks, double* rows,
                                                                                  uint64_t u0) {
     constexpr int NT = NeedLayout<D>::NT, N2 = Red<NT>::N2;
-    constexpr bool kPrefetch = EDT_NEED_PREFETCH != 0 && IDT == EDT_BF16;
-    constexpr bool kGlds = EDT_NEED_GLDS != 0 && IDT == EDT_BF16 && !kPrefetch;
+    constexpr bool kGlds = EDT_NEED_GLDS != 0 && IDT == EDT_BF16;
     // LDS-DMA stages per wave: two (two tiles in flight besides the one in registers) where the
     // registers already limit the pass to 2 waves per SIMD (the emitting form, D = 8), else one
     // (3 waves per SIMD fit the LDS with one stage, not with two)
@@ -1303,21 +1303,7 @@ __global__ __launch_bounds__(kBlock, EDT_NEED_MIN_WAVES) void slerp_need_kernel(
             }
         }
     }
-    if (staged) {
-    } else if constexpr (kPrefetch) {                  // two register sets, two tile bodies in the code
-        Raw8<IDT> x0[D], x1[D];
-        load_tile(0, x0);
-#pragma unroll 1
-        for (int k = 0; k < 4; k += 2) {
-            load_tile(k + 1, x1);
-            __builtin_amdgcn_sched_barrier(0);
-            tile(k, x0, [] {});
-            __builtin_amdgcn_sched_barrier(0);
-            if (k + 2 < 4) load_tile(k + 2, x0);
-            __builtin_amdgcn_sched_barrier(0);
-            tile(k + 1, x1, [] {});
-        }
-    } else {
+    if (!staged) {
 #pragma unroll 1
         for (int k = 0; k < 4; ++k) {
             Raw8<IDT> x[D];
