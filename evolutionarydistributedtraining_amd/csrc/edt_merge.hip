@@ -20,8 +20,7 @@ struct PairArgs {
 };
 
 // The merge of one child from its already-loaded inputs (lerp base from x = b1, y = b2; trained
-// weights d1 = m1, d2 = m2; carried buffer b_in): shared by pair_elems and the member-major
-// population kernel, so both compute the same bits.
+// weights d1 = m1, d2 = m2; carried buffer b_in).
 template <int GDT, int WDT, int N>
 __device__ __forceinline__ void pair_core(const PairArgs& a, uint64_t i, float (&x)[N], float (&y)[N],
                                           float (&d1)[N], float (&d2)[N], const float (&b_in)[N]) {
@@ -142,108 +141,10 @@ __global__ __launch_bounds__(kBlock) void pair_population_kernel(PopPairArgs P) 
 }
 
 
-// Member-major form (bf16 members and momenta, <= 8 distinct parents): each thread loads every
-// distinct parent's base / trained tile and every distinct donor momentum tile of its 8-element
-// slice once (all loads in flight together), then runs pair_core for each child from those
-// registers. A shared parent crosses HBM once per slice by construction, and the children's
-// bits are pair_elems' (same pair_core).
-constexpr int kMMParents = 8;
-struct PopMM {
-    const void* b[kMMParents];
-    const void* m[kMMParents];
-    const void* mom[kMMParents];
-    int32_t ia[kPopMaxChildren], ib[kPopMaxChildren], im[kPopMaxChildren];   // im < 0: no carried buffer
-    int np, nmom;                                                             // parents, donor buffers
-};
-
-template <int D>
-__device__ __forceinline__ u32x4 pick_tile(const u32x4 (&t)[D], int idx) {
-    // a bitwise blend per slot (idx is uniform): keeps the tiles in registers, where a select
-    // chain would be folded back into a dynamically indexed array (scratch memory)
-    u32x4 r = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-        const uint32_t m = 0u - (uint32_t)(d == idx);
-        r.x |= t[d].x & m;
-        r.y |= t[d].y & m;
-        r.z |= t[d].z & m;
-        r.w |= t[d].w & m;
-    }
-    return r;
-}
-
-__device__ __forceinline__ void unpack8(u32x4 w, float (&x)[8]) {
-    x[0] = bf_lo(w.x); x[1] = bf_hi(w.x); x[2] = bf_lo(w.y); x[3] = bf_hi(w.y);
-    x[4] = bf_lo(w.z); x[5] = bf_hi(w.z); x[6] = bf_lo(w.w); x[7] = bf_hi(w.w);
-}
-
-template <int D>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4)))
-void pair_population_mm_kernel(PopPairArgs P, PopMM M) {
-    const uint64_t n = P.c[0].n, nv = n / kVec;
-    const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (tid < nv) {
-        const uint64_t i = tid * kVec;
-        // every slot defined: pick_tile ANDs all D slots, including those past np / nmom
-        u32x4 tb[D] = {}, tm[D] = {}, tmo[D] = {};
-#pragma unroll
-        for (int d = 0; d < D; ++d)
-            if (d < M.np) {
-                tb[d] = *reinterpret_cast<const u32x4*>(static_cast<const uint16_t*>(M.b[d]) + i);
-                tm[d] = *reinterpret_cast<const u32x4*>(static_cast<const uint16_t*>(M.m[d]) + i);
-            }
-#pragma unroll
-        for (int d = 0; d < D; ++d)
-            if (d < M.nmom) tmo[d] = *reinterpret_cast<const u32x4*>(static_cast<const uint16_t*>(M.mom[d]) + i);
-        for (int q = 0; q < P.nchildren; ++q) {       // runtime child count: not unrolled
-            float x[kVec], y[kVec], d1[kVec], d2[kVec], b_in[kVec];
-            unpack8(pick_tile<D>(tb, M.ia[q]), x);
-            unpack8(pick_tile<D>(tb, M.ib[q]), y);
-            unpack8(pick_tile<D>(tm, M.ia[q]), d1);
-            unpack8(pick_tile<D>(tm, M.ib[q]), d2);
-            if (M.im[q] >= 0) unpack8(pick_tile<D>(tmo, M.im[q]), b_in);
-            else {
-#pragma unroll
-                for (int j = 0; j < kVec; ++j) b_in[j] = 0.f;
-            }
-            pair_core<EDT_BF16, EDT_BF16, kVec>(P.c[q], i, x, y, d1, d2, b_in);
-        }
-    }
-    const uint64_t t = nv * kVec + tid;                  // scalar tail (< 8 elements)
-    if (t < n)
-        for (int q = 0; q < P.nchildren; ++q) pair_elems<EDT_BF16, EDT_BF16, 1, false>(P.c[q], t);
-}
-
-// The same generation with the child loop inside the thread: each thread owns an 8-element slice
-// of the arena (one-pass grid, address order) and runs pair_elems for every child on it, so a
-// parent slice shared by several children is re-read within a few instructions by the same
-// thread (an L1 hit), not by another workgroup that may run after it has left the L2.
-#ifndef EDT_POP_LOOP
-#define EDT_POP_LOOP 0
-#endif
-#ifndef EDT_POP_MM              // member-major population kernel (bf16, <= 8 distinct parents): measured
-                                // 17.2-17.7 ms vs 15.9-16.7 co-located at 1.3B x 8 (8 parents), so off
-#define EDT_POP_MM 0
-#endif
-template <int GDT, int WDT, bool VEC>
-__global__ __launch_bounds__(kBlock) void pair_population_loop_kernel(PopPairArgs P) {
-    const uint64_t n = P.c[0].n;
-    const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if constexpr (VEC) {
-        const uint64_t nv = n / kVec;
-        if (tid < nv) {
-            for (int q = 0; q < P.nchildren; ++q) pair_elems<GDT, WDT, kVec, false>(P.c[q], tid * kVec);
-        }
-        const uint64_t t = nv * kVec + tid;
-        if (t < n) {
-            for (int q = 0; q < P.nchildren; ++q) pair_elems<GDT, WDT, 1, false>(P.c[q], t);
-        }
-    } else {
-        if (tid < n) {
-            for (int q = 0; q < P.nchildren; ++q) pair_elems<GDT, WDT, 1, false>(P.c[q], tid);
-        }
-    }
-}
+// Closed by measurement: a member-major form (each thread loads every distinct
+// parent's tiles once and runs the children from its registers: 17.2-17.7 ms r4, 20.4 / 26.9 ms
+// r5 on rank-selected pairs, against 15.7-16.7 co-located) and a child loop inside the thread
+// (parents re-read from L1): both removed.
 
 // ---------------------------------------------------------------------------------------
 // lerp with a scalar t (lerp_elems in edt_common.h)
@@ -360,70 +261,14 @@ int edt_pair_merge_population(const void* const* b1, const void* const* b2, cons
         vec = vec && aligned16(a.b1) && aligned16(a.b2) && aligned16(a.m1) && aligned16(a.m2) && aligned16(a.out) &&
               (!a.sgd.use_momentum || (aligned16(a.mom) && (!has || aligned16(a.mom_in))));
     }
-    // member-major when every child merges two bf16 parents of <= 8 distinct (base, trained)
-    // pairs and the vector body applies (EDT_POP_MM, off by default: see its definition)
-    if (EDT_POP_MM && vec && gdt == EDT_BF16 && wdt == EDT_BF16) {
-        PopMM M;
-        memset(&M, 0, sizeof(M));
-        int D = 0;
-        bool ok = true;
-        auto parent = [&](const void* b, const void* m) -> int {
-            for (int d = 0; d < D; ++d)
-                if (M.b[d] == b && M.m[d] == m) return d;
-            if (D == kMMParents) return -1;
-            M.b[D] = b;
-            M.m[D] = m;
-            return D++;
-        };
-        for (int c = 0; c < nchildren && ok; ++c) {
-            const PairArgs& a = P.c[c];
-            if (!a.b2) { ok = false; break; }
-            M.ia[c] = parent(a.b1, a.m1);
-            M.ib[c] = parent(a.b2, a.m2);
-            if (M.ia[c] < 0 || M.ib[c] < 0) { ok = false; break; }
-            M.im[c] = -1;
-            if (a.sgd.use_momentum && a.sgd.has_buf) {
-                int k = 0;
-                while (k < M.nmom && M.mom[k] != a.mom_in) ++k;
-                if (k == M.nmom) {
-                    if (M.nmom == kMMParents) { ok = false; break; }
-                    M.mom[M.nmom++] = a.mom_in;
-                }
-                M.im[c] = k;
-            }
-        }
-        if (ok && D >= 1) {
-            M.np = D;
-            const uint64_t nv = n / kVec;
-            const uint64_t bl = (nv + kBlock - 1) / kBlock + 1;
-            if (bl > kGridBlockCap) return fail(EDT_ERR_ARG, "too many elements for one launch");
-            hipStream_t s = (hipStream_t)stream;
-            const unsigned gm = (unsigned)bl;
-            if (M.nmom > D) D = M.nmom;         // tile arrays sized for parents and donors alike
-            switch (D) {
-                case 1: pair_population_mm_kernel<1><<<gm, kBlock, 0, s>>>(P, M); break;
-                case 2: pair_population_mm_kernel<2><<<gm, kBlock, 0, s>>>(P, M); break;
-                case 3: pair_population_mm_kernel<3><<<gm, kBlock, 0, s>>>(P, M); break;
-                case 4: pair_population_mm_kernel<4><<<gm, kBlock, 0, s>>>(P, M); break;
-                case 5: pair_population_mm_kernel<5><<<gm, kBlock, 0, s>>>(P, M); break;
-                case 6: pair_population_mm_kernel<6><<<gm, kBlock, 0, s>>>(P, M); break;
-                case 7: pair_population_mm_kernel<7><<<gm, kBlock, 0, s>>>(P, M); break;
-                default: pair_population_mm_kernel<8><<<gm, kBlock, 0, s>>>(P, M); break;
-            }
-            return check_launch("pair_population_mm_kernel");
-        }
-    }
     const uint64_t groups = (P.nchunks + 7) / 8;
-    const uint64_t blocks = EDT_POP_LOOP ? (vec ? (n / kVec + kBlock - 1) / kBlock + 1 : (n + kBlock - 1) / kBlock)
-                                         : groups * 8ull * (uint64_t)nchildren;
+    const uint64_t blocks = groups * 8ull * (uint64_t)nchildren;
     if (blocks > kGridBlockCap) return fail(EDT_ERR_ARG, "too many elements for one launch");
     const unsigned g = (unsigned)blocks;
     hipStream_t s = (hipStream_t)stream;
 #define EDT_POP(G, W)                                                                   \
     do {                                                                                \
-        if (EDT_POP_LOOP && vec) pair_population_loop_kernel<G, W, true><<<g, kBlock, 0, s>>>(P);   \
-        else if (EDT_POP_LOOP) pair_population_loop_kernel<G, W, false><<<g, kBlock, 0, s>>>(P);   \
-        else if (vec) pair_population_kernel<G, W, true><<<g, kBlock, 0, s>>>(P);       \
+        if (vec) pair_population_kernel<G, W, true><<<g, kBlock, 0, s>>>(P);            \
         else pair_population_kernel<G, W, false><<<g, kBlock, 0, s>>>(P);              \
     } while (0)
     if (gdt == EDT_F32 && wdt == EDT_F32) EDT_POP(EDT_F32, EDT_F32);

@@ -1,6 +1,6 @@
 """The EDT-LM generation (edt_pair_merge_population) on rank-selected pair graphs at 1.3B, bf16:
 the in-tree build against variant libraries (`--variants DIR`: every lib*.so there, e.g. built with
--DEDT_POP_MM=1 / 2), interleaved rounds, HIP-event medians; every variant's children and momenta
+variant tunables; r5 compared the member-major forms since removed), interleaved rounds, HIP-event medians; every variant's children and momenta
 compared bit for bit with the in-tree build's.
 
     python scripts/lm_population_probe.py [--variants variants] [--generations 3] [--rounds 3]
