@@ -561,7 +561,8 @@ def merge_models_into_(target: torch.nn.Module, model_1: torch.nn.Module, model_
                            bound=rec)
         if rec:                                   # the single-pass rebind ran: remember it
             rec["all_keys"] = list(sd1.keys())
-            if len(_bound_cache) >= 4:
+            if len(_bound_cache) >= 4:               # the oldest binding goes; merges in flight may
+                torch.cuda.current_stream(rec["tt"].device).synchronize()   # still read what it holds
                 _bound_cache.pop(next(iter(_bound_cache)))
             _bound_cache[key] = _Bound(key, model_1, model_2, rec["tt"].device, rec)
     else:
