@@ -88,3 +88,47 @@ def test_rank_generation_pairs_follow_the_lm_master():
     el = rank_generation_pairs(8, 5, seed=9, elitism=2)
     for g in el:
         assert len(g["pairs"]) == 8 and g["pairs"][-1][0] == g["pairs"][-1][1] and g["pairs"][-2][0] == g["pairs"][-2][1]
+
+
+def test_needed_table_covers_every_child_on_random_graphs():
+    """edt_slerp_needed_table on 300 seeded random pair graphs (1..8 members, 1..24 children, self
+    pairs, repeats, reversals): every child's two norms and its dot are columns of one block;
+    blocks are laid out back to back; a block's columns are its members' norms first; a block on
+    the needed layout has D + ring + <= 4 chord slots (triangle otherwise); the table and scratch
+    sizes follow; the planner's JSON view agrees (components, sums per block)."""
+    import random
+
+    from evolutionarydistributedtraining_amd import ops
+    rng = random.Random(4242)
+    for _ in range(300):
+        M = rng.randint(1, 8)
+        pairs = []
+        for _q in range(rng.randint(1, 24)):
+            a = rng.randrange(M)
+            pairs.append((a, a if rng.random() < 0.1 else rng.randrange(M)))
+        nch = rng.randint(1, 500)
+        lay = ops.needed_table(pairs, 8, nch)
+        cols = {}
+        off = 0
+        for b, ((o, nt), c) in enumerate(zip(lay.blocks, lay.columns)):
+            assert o == off and len(c) == nt
+            off += nch * nt
+            for x, (i, j) in enumerate(c):
+                if i >= 0:
+                    cols.setdefault(frozenset((i, j)), set()).add(b)
+        assert lay.doubles == off
+        for i, j in pairs:
+            bi, bj, bd = cols[frozenset((i,))], cols[frozenset((j,))], cols[frozenset((i, j))]
+            assert bi & bj & bd, (pairs, i, j)
+        js = ops.population_layout(pairs, 8, False)
+        assert len(js["components"]) == len(lay.blocks)
+        assert [c["sums"] for c in js["components"]] == [nt for _, nt in lay.blocks]
+        for comp, c in zip(js["components"], lay.columns):
+            D = len(comp["members"])
+            if comp["stats_layout"] == "needed":
+                assert [set(x) for x in c[:D]] == [{m} for m in comp["members"]]   # norms first
+                assert len(c) == 2 * D + (4 if D >= 5 else 2 if D == 4 else 0) - (1 if D <= 2 else 0)
+            else:                                                                # every pair once
+                mem = comp["members"]
+                assert sorted(tuple(sorted(x)) for x in c) == sorted(
+                    (mem[p], mem[q]) if mem[p] <= mem[q] else (mem[q], mem[p]) for p in range(D) for q in range(p, D))
