@@ -118,7 +118,9 @@ int edt_outer_step_list(void* const* theta_t, int gdt, const void* const* theta_
                         void* const* momentum_t, int has_momentum, const uint64_t* numel, int T,
                         double lr, double momentum, int nesterov, void* workspace,
                         uint64_t workspace_bytes, void* stream);
-/* edt_outer_step_list with the reference host's bf16 scalar tails (edt_outer_step_tail's rule, r5):
+/* edt_outer_step_list with the reference host's bf16 scalar tails (edt_outer_step_tail's rule, r5;
+ * replaces EDT_LM/diloco.py:238-289 run on a master whose torch CPU kernels round bf16 tails
+ * separately, over `model.parameters()` lists):
  * tail_bits (device, nullable) holds each tensor's 1-bit-per-element mask from byte
  * tail_byte_offset[t] (host array, T entries), indexed by the element's index inside its tensor.
  * gdt must be EDT_BF16 when tail_bits is given. */
@@ -355,7 +357,9 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
 
 /* The needed-sums passes of edt_slerp_population as separate entries (r5: the link-balanced sharded
  * population — each rank forms the sums of its chunk range, the table rows are all-gathered, every
- * rank forms every child's coefficients; distributed.ShardedPopulationCrossover). The table of a
+ * rank forms every child's coefficients; distributed.ShardedPopulationCrossover). Replaces, across
+ * the node's GPUs, the RL master's generation EDT_RL/edt.py:286-299 -> EDT_RL/crossover.py:84-135
+ * per child (the dots of EDT_RL/crossover.py:20-29). The table of a
  * generation (pairs over nmembers <= 8 members, nchunks chunks) is ncomp blocks, one per connected
  * component of the children's pair graph: block k at block_off[k] doubles, nchunks rows of
  * block_nt[k] sums (the component's norms and the dots its children use, or its Gram triangle
@@ -378,8 +382,8 @@ int edt_slerp_needed_coef(const double* table, int64_t table_chunks, const int32
                           const int32_t* seg_first_chunk, int nseg, const double* t, double dot_threshold, double eps,
                           float* coef, float* dot_out, void* stream);
 
-/* The plan the two population entries above make for a pair graph, as JSON text into buf (host
- * only, no device work): distinct parents, the form (speculative: "member-major" or "co-located";
+/* The plan the two population entries above make for a pair graph (the pairs of
+ * EDT_RL/edt.py:268-269's selection), as JSON text into buf (host only, no device work): distinct parents, the form (speculative: "member-major" or "co-located";
  * "two-pass"), and per connected component of the children's pair graph its members, distinct
  * dots, sums per element and stats layout ("needed": the members' norms + the dots the children
  * use; "triangle": every pair). For benches and logs. */
