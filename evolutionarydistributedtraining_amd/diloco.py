@@ -44,11 +44,18 @@ class OuterState:
     (EDT_LM/diloco.py:100,258-289). Also serialises to the torch `SGD.state_dict()` format
     (`outer_optim.pt`, as EDT_LM/train/crossover.py:231-232 writes per individual)."""
 
-    def __init__(self):
+    def __init__(self, place_momentum: int = 0):
         self.momentum: torch.Tensor | None = None   # flat, dtype of theta_g
         self.has_momentum = False                   # False until the first momentum step
         self.hparams = dict(DILOCO_DEFAULTS)
         self.steps = 0
+        # > 1: when outer_step creates the buffer over flat arenas (parameters bound with
+        # params.arena_of_module, so they stay where they are across generations), choose its HBM
+        # placement among this many candidates by measurement first (placement.place_momentum,
+        # as OuterSync.place_momentum / DirOuterSync do). The tensor-list form skips it: reloaded
+        # parameter tensors move, so no placement can hold.
+        self.place_momentum = int(place_momentum)
+        self.placement: dict | None = None
 
     def buffer_for(self, theta: torch.Tensor, numel: int | None = None) -> torch.Tensor:
         """The flat momentum for parameters like `theta` (numel: total count when theta is
@@ -129,7 +136,15 @@ def _step_flat(theta: torch.Tensor, workers: list[torch.Tensor], state: OuterSta
                tail_bits: torch.Tensor | None = None) -> None:
     check_sgd_hparams(lr, momentum, nesterov)
     state.hparams = dict(lr=lr, momentum=momentum, nesterov=nesterov)
+    fresh = state.momentum is None
     mom = state.buffer_for(theta) if momentum != 0 else None
+    if mom is not None and fresh and getattr(state, "place_momentum", 0) > 1 and theta.is_cuda:
+        from .placement import place_momentum
+        try:
+            state.momentum, state.placement = place_momentum(theta, workers, mom, state.place_momentum)
+            mom = state.momentum
+        except EdtError as e:                   # e.g. operands the probe cannot stream (alignment)
+            state.placement = {"candidates": 1, "probe_ms": [], "chosen": 0, "skipped": str(e)}
     has = state.has_momentum if momentum != 0 else False
     if tail_bits is not None and broadcast:              # the tail form has no fused broadcast
         ops.outer_step(theta, workers, mom, has, lr, momentum, nesterov, tail_bits=tail_bits)

@@ -60,8 +60,10 @@ def test_diloco_outer_step_surface(golden, oracle, dev):
     c = [c for c in golden.diloco_cases() if c["K"] == 3 and c["global_dtype"] == "f32"
          and c["worker_dtype"] == "f32" and c["nesterov"] and c["momentum"] == 0.9][0]
     T = len(c["shapes"])
-    for zero_copy in (True, False):
-        state = None
+    for zero_copy, placed in ((True, False), (False, False), (True, True)):
+        # placed: OuterState(place_momentum=4) — the buffer's placement chosen by measurement when
+        # the arena path creates it; values unchanged
+        state = OuterState(place_momentum=4) if placed else None
         for step in c["steps"]:
             pre = step["prefix"]
             base = torch.nn.ParameterList([torch.nn.Parameter(t.clone()) for t in golden.tlist("diloco", f"{pre}/base", T)]).to(dev)
@@ -79,6 +81,8 @@ def test_diloco_outer_step_surface(golden, oracle, dev):
             assert torch.equal(bits(got), bits(want)), (pre, zero_copy)
             assert torch.equal(bits(state.momentum.cpu()), bits(flat(golden.tlist("diloco", f"{pre}/out_buf", T))))
         assert isinstance(state, OuterState) and state.steps == 2
+        if placed:
+            assert state.placement is not None and state.placement["candidates"] >= 1, state.placement
 
 
 def _pair_case(golden, name):
