@@ -388,8 +388,9 @@ class RefDot:
     The mode reproduces ONE host: `dot_kernel` is the BLAS dot restated on the device and
     `coef_dispatch` the SIMD targets numpy's float32 arccos / sin loops dispatch to there (the
     targets compute different bits: AVX512_SKX's SVML arccos and the baseline libm one differ on
-    ~36 % of 400k float32 dots, sin 30 %: scripts/numpy_dispatch_probe.py). The defaults are the host tests/golden/ was recorded on
-    (tests/golden/refdot_host.json). At first use the running host (host_dispatch()) is compared
+    ~36 % of 400k float32 dots, sin 30 %: scripts/numpy_dispatch_probe.py). The defaults are the
+    host tests/golden/ was recorded on (tests/golden/refdot_host.json). At first use the running
+    host (host_dispatch()) is compared
     with them: a difference warns (RefDotHostWarning) — or raises with strict=True — since the
     coefficients would then not be the reference's bits on this host."""
     threads: int = 1
