@@ -265,12 +265,13 @@ def test_sharded_schedules_fuzz_on_virtual_ranks(dev, world, k_local, shapes, un
 @given(world=st.integers(1, 8), groups=st.integers(1, 4),
        shapes=st.lists(st.one_of(st.tuples(st.integers(1, 20000)), st.tuples(st.integers(1, 90), st.integers(1, 90))),
                        min_size=1, max_size=7),
-       seed=st.integers(0, 2**31 - 1))
-def test_sharded_population_fuzz_on_virtual_ranks(dev, world, groups, shapes, seed):
-    """The link-balanced population crossover with the HIP Gram / coefficient / blend passes on
-    random layouts (1,024-element chunks: many chunks per rank, ranges starting off the vector
-    grid), worlds and pipeline groups: every child bit-identical to edt_slerp_merge on its two
-    parents with the same chunk table."""
+       seed=st.integers(0, 2**31 - 1), roulette=st.booleans())
+def test_sharded_population_fuzz_on_virtual_ranks(dev, world, groups, shapes, seed, roulette):
+    """The link-balanced population crossover with the HIP needed-sums / coefficient / blend passes
+    on random layouts (1,024-element chunks: many chunks per rank, ranges starting off the vector
+    grid), worlds, pipeline groups and pair graphs (a fixed permutation-like graph, or r5: drawn by
+    EDT_RL's roulette selection): every child bit-identical to edt_slerp_merge on its two parents
+    with the same chunk table."""
     from evolutionarydistributedtraining_amd import ops
     from evolutionarydistributedtraining_amd.collectives import VirtualWorld
     from evolutionarydistributedtraining_amd.distributed import ShardedPopulationCrossover
@@ -282,6 +283,9 @@ def test_sharded_population_fuzz_on_virtual_ranks(dev, world, groups, shapes, se
     members = [(base + torch.randn(n, generator=g) * 0.02 * (0.005 if r % 2 else 0.1)).bfloat16().to(dev)
                for r in range(world)]
     pairs = [((3 * c + 1) % world, (5 * c + 2) % world) for c in range(world)]
+    if roulette and world > 1:
+        from evolutionarydistributedtraining_amd.schedule import roulette_generation_pairs
+        pairs = [tuple(p) for p in roulette_generation_pairs(world, 1, seed=seed)[0]["pairs"]]
     t = torch.rand(len(shapes), generator=g, dtype=torch.float64).to(dev)
 
     def body(comm):
@@ -298,3 +302,38 @@ def test_sharded_population_fuzz_on_virtual_ranks(dev, world, groups, shapes, se
         ops.slerp_arena(plan, members[i], members[j], want, t, speculate=False)
         torch.cuda.synchronize()
         assert torch.equal(res[c].view(torch.int16), want.view(torch.int16)), c
+
+
+@settings(max_examples=200, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.function_scoped_fixture, HealthCheck.too_slow])
+@given(shapes=st.lists(st.one_of(st.tuples(st.integers(1, 20000)), st.tuples(st.integers(1, 90), st.integers(1, 90))),
+                       min_size=1, max_size=6),
+       pairs=st.lists(st.tuples(st.integers(0, 7), st.integers(0, 7)), min_size=1, max_size=20),
+       dts=st.sampled_from([(torch.bfloat16, torch.bfloat16), (torch.float32, torch.float32),
+                            (torch.bfloat16, torch.float32), (torch.float32, torch.bfloat16)]),
+       speculate=st.booleans(), lineage=st.booleans(), seed=st.integers(0, 2**31 - 1))
+def test_population_fuzz(dev, shapes, pairs, dts, speculate, lineage, seed):
+    """ops.slerp_population (r5: the needed-sums passes, member-major or co-located, the triangle
+    fallback) on random layouts with 1,024-element chunks, random pair graphs over up to 8 members
+    (self pairs, repeats, reversals, isolated members), every dtype route, lineage or mixed members
+    (both branches), both forms: every child and its dots bit-identical to edt_slerp_merge."""
+    from evolutionarydistributedtraining_amd import ops
+    from evolutionarydistributedtraining_amd.params import ParamLayout
+    in_dt, out_dt = dts
+    layout = ParamLayout(shapes)
+    n = layout.total
+    M = max(max(p) for p in pairs) + 1
+    g = torch.Generator().manual_seed(seed)
+    base = torch.randn(n, generator=g) * 0.02
+    members = [(base + torch.randn(n, generator=g) * 0.02 * (0.005 if lineage or m % 2 else 0.3)).to(in_dt).to(dev)
+               for m in range(M)]
+    t = torch.rand(len(shapes), generator=g, dtype=torch.float64).to(dev)
+    plan = ops.make_slerp_plan(layout.offsets, dev, chunk_elems=1024)
+    outs = [torch.full((n,), float("nan"), dtype=out_dt, device=dev) for _ in pairs]
+    dots = ops.slerp_population(plan, members, pairs, outs, t, speculate=speculate).clone()
+    want = torch.empty(n, dtype=out_dt, device=dev)
+    for q, (i, j) in enumerate(pairs):
+        ops.slerp_arena(plan, members[i], members[j], want, t, speculate=False)
+        torch.cuda.synchronize()
+        assert torch.equal(bits(outs[q]), bits(want)), (q, i, j, speculate)
+        assert torch.equal(dots[q][:plan.nseg].cpu(), plan.dots[:plan.nseg].cpu()), (q, i, j)
