@@ -123,6 +123,10 @@ def parse(argv=None):
                         "pipelined over this many chunk groups per rank (1: only the unpipelined form)")
     p.add_argument("--bcast-compare", type=int, default=1,
                    help="N=1: also time the step fused with the worker broadcast against step + K copies")
+    p.add_argument("--kernel-trace", type=int, default=2,
+                   help="after the timed steps: this many more steps under torch.profiler, whose device "
+                        "kernel names / launches / durations go into the line as 'kernel_trace' (0: off; "
+                        "skipped under rocprofv3)")
     p.add_argument("--dry-run-launch", action="store_true",
                    help="each rank prints its rank environment and exits before device init")
     p.add_argument("--dry-run-sleep", type=float, default=0.0,
@@ -343,6 +347,31 @@ def native_library_record() -> dict:
     except OSError:
         rec["mapped"] = None
     return rec
+
+
+def kernel_trace(fn, reps: int) -> dict:
+    """In-run evidence of what the timed step launches: `reps` more calls of it under torch.profiler
+    after the timed region (Kineto over the ROCm tracer, which records every HIP dispatch of the
+    process, the library's own included): each device kernel's name, launch count and mean device
+    time. Skipped under rocprofv3, which holds the process's tracer itself."""
+    if any(k.startswith("ROCPROF") for k in os.environ):
+        return {"skipped": "running under rocprofv3"}
+    from torch.profiler import ProfilerActivity, profile
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+    agg: dict[str, list] = {}
+    for e in prof.events():
+        if e.device_type == torch.autograd.DeviceType.CUDA:
+            a = agg.setdefault(e.name, [0, 0.0])
+            a[0] += 1
+            a[1] += e.device_time
+    return {"tool": "torch.profiler (Kineto / ROCm tracer) in this process, after the timed steps",
+            "steps": reps,
+            "kernels": [{"name": n[:200], "launches": c, "mean_ms": round(t / c / 1e3, 4)}
+                        for n, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])]}
 
 
 def _ordered_bits(x: torch.Tensor) -> torch.Tensor:
@@ -1213,6 +1242,13 @@ def run_sharded(args, comm, rt, json_out, kernels=None, exit_fn=None) -> dict | 
     value = bytes_reduced / (ms_per_step / 1e3) / 1e9
     sched = f"{sync.mode}/{sync.broadcast}"
     wire_main = sync.wire_bytes()
+    trace = None
+    if args.kernel_trace > 0 and kernels is None:
+        # every rank runs the traced steps (they hold the step's collectives); rank 0 reports
+        try:
+            trace = kernel_trace(sync.step, args.kernel_trace)
+        except Exception as e:          # evidence, not the measurement: report it, keep the line
+            trace = {"error": f"{type(e).__name__}: {str(e)[:300]}"}
 
     out = None
     if rank == 0:
@@ -1246,8 +1282,10 @@ def run_sharded(args, comm, rt, json_out, kernels=None, exit_fn=None) -> dict | 
                        "population": k_total, "worker_dtype": args.worker_dtype,
                        "theta_dtype": args.theta_dtype, "parallelism": f"dp{world} {sched} (RCCL)"},
             "roofline": roofline,
-            "device": rt.device_info(), "native": native_library_record(), "native": native_library_record(),
+            "device": rt.device_info(), "native": native_library_record(),
         }
+        if trace is not None:
+            out["kernel_trace"] = trace
         # rank 0 times the CPU baseline first (the other ranks wait at the barrier), then every
         # extra runs under the deadline, so neither can be lost to a hang in an extra
         if args.cpu_baseline_seconds > 0:
@@ -1486,6 +1524,11 @@ def main():
                                  "before the placement search; kernel_ms is after it")
     if placement:
         roofline["momentum_placement"] = placement
+    if args.kernel_trace > 0:
+        try:
+            out["kernel_trace"] = kernel_trace(step, args.kernel_trace)
+        except Exception as e:          # evidence, not the measurement: report it, keep the line
+            out["kernel_trace"] = {"error": f"{type(e).__name__}: {str(e)[:300]}"}
     if args.bcast_compare:
         # the step with the broadcast of diloco.py:302-308 (every worker restarts from theta):
         # fused into the kernel's pass vs the step + K device copies

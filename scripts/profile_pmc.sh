@@ -10,7 +10,7 @@ mkdir -p $OUT
 ARGS="--steps 3 --warmup 1 --cpu-baseline-seconds 0 --ops none --bcast-compare 0 ${BENCH_ARGS:-}"
 for C in FETCH_SIZE WRITE_SIZE; do
   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --pmc $C --output-format csv \
-      -d $OUT/$C -o pmc -- python3 $R/bench.py $ARGS > $OUT/$C.log 2>&1); s=$?
+      -d $OUT/$C -o pmc -- python3 $R/bench.py --kernel-trace 0 $ARGS > $OUT/$C.log 2>&1); s=$?
   echo "$C pass: status $s"; tail -2 $OUT/$C.log
   [ $s -eq 0 ] || exit $s
 done

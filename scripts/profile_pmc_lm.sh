@@ -9,7 +9,7 @@ ARGS="--layout gpt2_small --steps 1 --warmup 0 --cpu-baseline-seconds 0 --ops-cp
 KRE="pair_population"
 for C in FETCH_SIZE WRITE_SIZE; do
   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --pmc $C --kernel-include-regex "$KRE" --output-format csv \
-      -d $OUT/$C -o pmc -- python3 $R/bench.py $ARGS > $OUT/$C.log 2>&1); s=$?
+      -d $OUT/$C -o pmc -- python3 $R/bench.py --kernel-trace 0 $ARGS > $OUT/$C.log 2>&1); s=$?
   echo "$C pass: status $s"; tail -1 $OUT/$C.log | cut -c1-200
   [ $s -eq 0 ] || exit $s
 done

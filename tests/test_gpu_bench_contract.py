@@ -58,6 +58,12 @@ def test_single_gpu_line():
     _check_common(d, 1)
     assert d["config"]["parallelism"] == "single GPU"
     assert d["roofline"]["kernel_ms"] <= d["ms_per_step"] * 1.05
+    # in-run evidence: the process's own tracer saw the library's fused step kernel
+    kt = d["kernel_trace"]
+    assert kt["steps"] == 2, kt
+    top = kt["kernels"][0]
+    assert "outer_kernel<" in top["name"] and top["launches"] == 2, kt
+    assert top["mean_ms"] > 0
 
 
 def test_multi_gpu_path_line_at_world_1():
@@ -67,6 +73,8 @@ def test_multi_gpu_path_line_at_world_1():
     x = d["roofline"]["xgmi"]
     assert x["bound"] == "xgmi" and "wire_bytes_per_rank" in x
     assert "weak_scaling" in d and "extras_deadline" not in d
+    kt = d["kernel_trace"]
+    assert "error" not in kt and any("outer_kernel" in k["name"] for k in kt["kernels"]), kt
 
 
 def test_single_gpu_line_population_extra():
