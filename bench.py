@@ -1242,13 +1242,6 @@ def run_sharded(args, comm, rt, json_out, kernels=None, exit_fn=None) -> dict | 
     value = bytes_reduced / (ms_per_step / 1e3) / 1e9
     sched = f"{sync.mode}/{sync.broadcast}"
     wire_main = sync.wire_bytes()
-    trace = None
-    if args.kernel_trace > 0 and kernels is None:
-        # every rank runs the traced steps (they hold the step's collectives); rank 0 reports
-        try:
-            trace = kernel_trace(sync.step, args.kernel_trace)
-        except Exception as e:          # evidence, not the measurement: report it, keep the line
-            trace = {"error": f"{type(e).__name__}: {str(e)[:300]}"}
 
     out = None
     if rank == 0:
@@ -1284,8 +1277,6 @@ def run_sharded(args, comm, rt, json_out, kernels=None, exit_fn=None) -> dict | 
             "roofline": roofline,
             "device": rt.device_info(), "native": native_library_record(),
         }
-        if trace is not None:
-            out["kernel_trace"] = trace
         # rank 0 times the CPU baseline first (the other ranks wait at the barrier), then every
         # extra runs under the deadline, so neither can be lost to a hang in an extra
         if args.cpu_baseline_seconds > 0:
@@ -1295,6 +1286,15 @@ def run_sharded(args, comm, rt, json_out, kernels=None, exit_fn=None) -> dict | 
                 out["cpu_baseline"] = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
     comm.barrier()
     deadline = ExtrasDeadline(args.extras_deadline, rank, out, json_out, exit_fn=exit_fn)
+    if args.kernel_trace > 0 and kernels is None:
+        # first extra: every rank runs the traced steps (they hold the step's collectives)
+        try:
+            trace = kernel_trace(sync.step, args.kernel_trace)
+        except Exception as e:          # evidence, not the measurement: report it, keep the line
+            trace = {"error": f"{type(e).__name__}: {str(e)[:300]}"}
+        if out is not None:
+            out["kernel_trace"] = trace
+        comm.barrier()
     mode_used, bcast_used = sync.mode, sync.broadcast
     sync = None
     rt.empty_cache()
