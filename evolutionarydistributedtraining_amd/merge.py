@@ -425,7 +425,8 @@ def _rebind_merge(params, keys, outs, sd1, sd2, plan, out_dtype, dev, dot_thresh
     if bound is not None:
         bound.update(keys=keys, ts=[t for _, t in plan], tt=tt, splan=splan, ns=ns, offs=offs, total=total,
                      in_dt=in_dt, out_dt=out_dtype, p0=po, p1=p1, buf=buf, shapes=[o.shape for o in outs],
-                     hold2=[b.data for _, b in pairs])
+                     hold2=[b.data for _, b in pairs],
+                     ends=(params[keys[0]], params[keys[-1]], pairs[0][1], pairs[-1][1]))
     return True
 
 
@@ -499,7 +500,13 @@ def _bound_merge(b: _Bound, model_1, model_2) -> bool:
     tensors (the walk, keys, Parameters, addresses, sizes, dtypes: what the uncached path reads
     before its launch) and the re-pointing of model_1's parameters at the new buffer. False
     (nothing re-pointed, the entry dropped, the output discarded) when anything changed: the
-    caller merges the uncached way."""
+    caller merges the uncached way. A module whose first or last merged tensor moved (a reload, a
+    re-pointing) is caught before the launch, so that case costs no wasted merge."""
+    f1, l1, f2, l2 = b.ends
+    if (f1.data_ptr() != int(b.p0[0]) or l1.data_ptr() != int(b.p0[-1]) or f2.data_ptr() != int(b.p1[0])
+            or l2.data_ptr() != int(b.p1[-1])):
+        _bound_cache.pop(b.key, None)
+        return False
     buf = torch.empty(b.total, dtype=b.out_dt, device=b.dev)
     po = np.uint64(buf.data_ptr()) + b.offs_bytes
     ops.SlerpListBinding.from_checked(b.splan, b.p0, b.p1, po, b.in_dt, b.out_dt, b.dev,

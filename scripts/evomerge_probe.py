@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--layers", type=int, default=28)
     ap.add_argument("--profile", action="store_true", help="cProfile one merge (host time split) to stderr")
     ap.add_argument("--repoint", action="store_true", help="reset model_1 to fresh tensors (no repeat binding)")
+    ap.add_argument("--same-memory", type=int, default=1,
+                    help="also time the surface with both models' parameters re-pointed at views of the arena "
+                         "leg's two arenas (the same parent bytes at the same addresses)")
     a = ap.parse_args()
     from transformers import Qwen2Config, Qwen2ForCausalLM
 
@@ -105,11 +108,55 @@ def main():
     offs = [0]
     for k, _ in plan:
         offs.append(offs[-1] + sd1[k].numel())
-    v0 = torch.cat([sd1[k].reshape(-1) for k, _ in plan])
+    v0 = torch.cat([start[k].reshape(-1) for k, _ in plan])      # the surface's parents, as arenas
     v1 = torch.cat([sd2[k].reshape(-1) for k, _ in plan])
-    out = torch.empty_like(v0)
+    del sd1, sd2
     aplan = ops.make_slerp_plan(offs, dev)
     tt = torch.tensor([t for _, t in plan], dtype=torch.float64, device=dev)
+    extra = {}
+    if a.same_memory and not a.repoint:
+        # the surface and the arena pass over the same memory: model_2's parameters re-pointed once
+        # at views of the arena v1; model_1 starts as views of v0 and then lives where the merge
+        # writes it (two blocks in turn, reset in place between rounds as above); after the rounds
+        # the arena pass reads model_1's block and v1 and writes the other block — exactly what
+        # the surface's next round would touch
+        pm1, pm2 = dict(m1.model.named_parameters()), dict(m2.model.named_parameters())
+        with torch.no_grad():
+            for i, (k, _) in enumerate(plan):
+                if k in pm2:
+                    pm2[k].data = v1[offs[i]:offs[i + 1]].view(pm2[k].shape)
+                if k in pm1:
+                    pm1[k].data = v0[offs[i]:offs[i + 1]].view(pm1[k].shape)
+        ts, out_blocks = [], []
+        for r in range(a.rounds + 2):
+            reset()
+            t0 = time.perf_counter()
+            rebind_merge()
+            torch.cuda.synchronize()
+            ts.append((time.perf_counter() - t0) * 1e3)
+            out_blocks.append(min(p.data_ptr() for p in m1.model.parameters()))
+        times["same_memory_rebind"] = ts[2:]         # the first call binds, the second repeats it
+        got = torch.cat([p.detach().reshape(-1) for p in m1.model.parameters()]).view(torch.int16)
+        extra["same_memory_bit_identical"] = bool(torch.equal(got, outs["single_pass_rebind"]))
+        del got
+        bound = next(iter(merge._bound_cache.values()))
+        extra["same_memory_packed"] = int(bound.total) == n and bound.buf.data_ptr() == out_blocks[-1]
+        reset()                                      # model_1's block holds the start values again
+        sm_v0 = bound.buf
+        sm_out = torch.empty_like(v0)
+        extra["same_memory_out_block"] = sm_out.data_ptr() in out_blocks[-3:-1]
+        if extra["same_memory_packed"]:
+            ev2 = []
+            for r in range(a.rounds + 1):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                ops.slerp_arena(aplan, sm_v0, v1, sm_out, tt, speculate=True)
+                e1.record()
+                torch.cuda.synchronize()
+                ev2.append(e0.elapsed_time(e1))
+            times["same_memory_arena_events"] = ev2[1:]
+        del sm_v0, sm_out, bound
+    out = torch.empty_like(v0)
     ev = []
     for r in range(a.rounds + 1):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -125,7 +172,7 @@ def main():
     print(json.dumps({"probe": "evomerge_surface", "params_body": n, "tensors": len(keys), "far": a.far,
                       "reset": "fresh tensors" if a.repoint else "copied in place (repeat binding)",
                       "bound_entries": len(merge._bound_cache),
-                      "outputs_bit_identical": same, "results": res}))
+                      "outputs_bit_identical": same, **extra, "results": res}))
 
 
 if __name__ == "__main__":

@@ -647,7 +647,8 @@ def test_evomerge_repeat_binding_follows_module_changes(dev, monkeypatch):
     Every generation equals the in-place two-pass merge bit for bit, whatever changed in between:
     nothing (the cached launch), model_1 written in place (same addresses: cached), a model_2
     parameter re-pointed, a model_1 Parameter replaced by a new one (both: the check fails, the
-    uncached merge runs, the new binding is recorded); the entry dies with model_2."""
+    uncached merge runs, the new binding is recorded), every model_1 tensor re-pointed (caught before
+    the launch: no cached launch is spent); the entry dies with model_2."""
     import gc
 
     from evolutionarydistributedtraining_amd import evomerge_crossover as ev
@@ -659,6 +660,10 @@ def test_evomerge_repeat_binding_follows_module_changes(dev, monkeypatch):
     hits = []
     real = merge._bound_merge
     monkeypatch.setattr(merge, "_bound_merge", lambda b, x, y: hits.append(real(b, x, y)) or hits[-1])
+    cached_launches = []
+    real_checked = merge.ops.SlerpListBinding.from_checked
+    monkeypatch.setattr(merge.ops.SlerpListBinding, "from_checked",
+                        lambda *a, **k: cached_launches.append(1) or real_checked(*a, **k))
 
     def change(gen):
         with torch.no_grad():
@@ -670,16 +675,21 @@ def test_evomerge_repeat_binding_follows_module_changes(dev, monkeypatch):
             elif gen == 4:
                 lin = m1.model.layers[2].self_attn.o_proj
                 lin.weight = torch.nn.Parameter(lin.weight.detach().clone())  # a new Parameter
+            elif gen == 6:
+                for p in m1.model.parameters():                               # a reload: all moved
+                    p.data = p.data.clone()
 
-    expect = [None, True, True, False, False, True]
-    for gen in range(6):
+    expect = [None, True, True, False, False, True, False, True]
+    for gen in range(8):
         change(gen)
         want = {k: v.clone() for k, v in m1.model.state_dict().items()}
         merge.slerp_state_dicts(dict(want), m2.model.state_dict(), plan, out_dtype=torch.bfloat16, device=dev,
                                 out=want)
-        n = len(hits)
+        n, c = len(hits), len(cached_launches)
         merge.merge_models_into_(m1.model, m1.model, m2.model, mcfg, cfg.num_hidden_layers, device=dev)
         assert (hits[n] if len(hits) > n else None) == expect[gen], (gen, hits)
+        if gen == 6:
+            assert len(cached_launches) == c, "a moved model_1 must be caught before the cached launch"
         got = m1.model.state_dict()
         for k, _ in plan:
             assert torch.equal(got[k].view(torch.int16), want[k].view(torch.int16)), (gen, k)
