@@ -278,8 +278,6 @@ class SlerpPlan:
     seg_offsets: list[int]
     chunks: torch.Tensor          # int64 [nchunks, 3] = start, length, segment
     seg_first: torch.Tensor       # int32 [nseg + 1]
-    coef: torch.Tensor            # float32 [nseg, 2]
-    dots: torch.Tensor            # float32 [nseg]
     nchunks: int
     relative: bool = False        # chunk starts relative to their segment (tensor-list form)
     chunks_host: object = None    # numpy int64 [nchunks, 3]: the same table on the host
@@ -288,6 +286,28 @@ class SlerpPlan:
     @property
     def nseg(self) -> int:
         return len(self.seg_offsets) - 1
+
+    def ws(self, name: str, n: int, dtype: torch.dtype) -> torch.Tensor:
+        """The calling host thread's device workspace `name` on this plan (>= n elements, grown on
+        demand; a view of n): plans are shared (merge._plan_for, the population planners) and host
+        threads (virtual ranks) may merge over one plan at the same time, each reading back its own
+        coefficients and dots."""
+        per = self.__dict__.setdefault("_ws_by_thread", {}).setdefault(threading.get_ident(), {})
+        n = max(1, int(n))
+        buf = per.get(name)
+        if buf is None or buf.numel() < n or buf.dtype != dtype:
+            buf = per[name] = torch.empty(n, dtype=dtype, device=self.chunks.device)
+        return buf[:n]
+
+    @property
+    def coef(self) -> torch.Tensor:
+        """float32 [nseg, 2]: the last merge's per-segment coefficients (this host thread's)."""
+        return self.ws("coef", 2 * max(1, self.nseg), torch.float32).view(max(1, self.nseg), 2)
+
+    @property
+    def dots(self) -> torch.Tensor:
+        """float32 [nseg]: the last merge's per-segment dots (this host thread's)."""
+        return self.ws("dots", self.nseg, torch.float32)
 
     @property
     def partial(self) -> torch.Tensor:
@@ -325,10 +345,7 @@ def make_slerp_plan(seg_offsets: list[int], device: torch.device,
         host[:, 0] -= np.asarray(seg_offsets, dtype=np.int64)[host[:, 2]]
     chunks = torch.from_numpy(host).to(device)
     seg_first = torch.tensor(list(first), dtype=torch.int32).to(device)
-    return SlerpPlan(list(seg_offsets), chunks, seg_first,
-                     torch.empty((max(1, nseg), 2), dtype=torch.float32, device=device),
-                     torch.empty(max(1, nseg), dtype=torch.float32, device=device), nchunks, relative, host,
-                     int(chunk_elems))
+    return SlerpPlan(list(seg_offsets), chunks, seg_first, nchunks, relative, host, int(chunk_elems))
 
 
 # The host the reference-dot mode reproduces: the one tests/golden/ was recorded on
@@ -458,10 +475,7 @@ def _refdot_ws(plan: SlerpPlan, ref: RefDot, dev) -> torch.Tensor:
     need = int(lib.edt_slerp_refdot_workspace_bytes(plan.nseg, plan.nchunks, plan.chunk_elems, int(ref.threads)))
     if need == 0:
         raise L.EdtError(f"reference-dot mode needs chunks of a multiple of 8192 elements (plan: {plan.chunk_elems})")
-    ws = getattr(plan, "_refdot_ws", None)
-    if ws is None or ws.numel() * 8 < need:
-        ws = plan._refdot_ws = torch.empty((need + 7) // 8, dtype=torch.float64, device=dev)
-    return ws
+    return plan.ws("refdot", (need + 7) // 8, torch.float64)
 
 
 def _ref_dots(plan: SlerpPlan, dots: torch.Tensor, ref: RefDot, in_dt: int, dot_threshold: float, eps: float,
@@ -516,30 +530,38 @@ def _reference_finish(dots: torch.Tensor, flag: torch.Tensor, val: torch.Tensor,
     return dots_out, coef_out, changed
 
 
+def _dots_state(plan) -> dict:
+    """The calling host thread's record of its previous merges' dots on this plan."""
+    per = plan.__dict__.setdefault("_dots_by_thread", {})
+    return per.setdefault(threading.get_ident(), {})
+
+
 def _record_dots(plan: SlerpPlan, dots: torch.Tensor, attr: str) -> None:
     """After a merge: the dots go to pinned host memory by an async copy on the merge's stream, with
-    an event, so the next call can judge its form without synchronising the device."""
-    host = getattr(plan, attr + "_host", None)
+    an event, so the next call (on this host thread) can judge its form without synchronising the
+    device."""
+    st = _dots_state(plan)
+    host = st.get(attr + "_host")
     if host is None or host.shape != dots.shape:
-        host = torch.empty(dots.shape, dtype=dots.dtype, pin_memory=True)
-        setattr(plan, attr + "_host", host)
+        host = st[attr + "_host"] = torch.empty(dots.shape, dtype=dots.dtype, pin_memory=True)
     host.copy_(dots, non_blocking=True)
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream(dots.device))
-    setattr(plan, attr + "_event", ev)
+    st[attr + "_event"] = ev
 
 
 def _host_dots(plan: SlerpPlan, attr: str, wait: bool):
     """The previous merge's dots on the host (numpy), or None while its copy is still in flight
     (wait=False: never blocks; wait=True: waits for that copy only)."""
-    ev = getattr(plan, attr + "_event", None)
+    st = _dots_state(plan)
+    ev = st.get(attr + "_event")
     if ev is None:
         return None
     if wait:
         ev.synchronize()
     elif not ev.query():
         return None
-    return getattr(plan, attr + "_host").numpy()
+    return st[attr + "_host"].numpy()
 
 
 def _speculation_pays(plan: SlerpPlan, in_bytes: int, out_bytes: int, wait: bool = True) -> bool:
@@ -654,9 +676,7 @@ def slerp_arena(plan: SlerpPlan, v0: torch.Tensor, v1: torch.Tensor, out: torch.
         _pair_ref_merge(plan, L.dtype_code(v0), L.dtype_code(out), t, dot_threshold, eps, ref_dot, speculate,
                         arena=(v0, v1, out), n=v0.numel())
     elif speculate:
-        redo = getattr(plan, "_redo", None)
-        if redo is None:
-            redo = plan._redo = torch.empty(max(1, plan.nseg), dtype=torch.int32, device=v0.device)
+        redo = plan.ws("redo", plan.nseg, torch.int32)
         L.check(lib.edt_slerp_merge_speculative(
             L.ptr(v0), L.ptr(v1), L.dtype_code(v0), L.ptr(out), L.dtype_code(out), L.ptr(plan.chunks), plan.nchunks,
             L.ptr(plan.seg_first), plan.nseg, L.ptr(t), float(dot_threshold), float(eps), L.ptr(plan.partial),
@@ -711,22 +731,30 @@ def writes_safe(starts, nbytes) -> bool:
 _ELEM_SIZE = {torch.float32: 4, torch.bfloat16: 2, torch.float16: 2, torch.float64: 8}
 
 
+def _stage_state(plan) -> dict:
+    """The calling host thread's staging state on this plan: plans are shared (merge._plan_for),
+    and host threads (virtual ranks) may bind on one plan at the same time."""
+    per = plan.__dict__.setdefault("_table_stage_state", {})
+    tid = threading.get_ident()
+    st = per.get(tid)
+    if st is None:
+        st = per[tid] = {"stages": [None, None], "events": [None, None], "next": 1}
+    return st
+
+
 def _table_stage(plan, n3: int) -> torch.Tensor:
-    """One of the plan's two pinned staging buffers for a pointer-table image (>= n3 int64), in
-    turn, once the upload from it two bindings ago has completed: the image is written there and
-    goes up by an async copy (a pageable upload waits for its own staging, the largest host cost of
-    a repeated binding); alternating buffers, a binding never waits for the previous one's copy,
-    which may sit behind other work on the stream."""
-    stages = plan.__dict__.setdefault("_table_stages", [None, None])
-    events = plan.__dict__.setdefault("_table_stage_evs", [None, None])
-    k = plan.__dict__["_table_stage_next"] = 1 - plan.__dict__.get("_table_stage_next", 1)
-    stage, ev = stages[k], events[k]
+    """One of the calling thread's two pinned staging buffers on this plan for a pointer-table image
+    (>= n3 int64), in turn, once the upload from it two bindings ago has completed: the image is
+    written there and goes up by an async copy (a pageable upload waits for its own staging, the
+    largest host cost of a repeated binding); alternating buffers, a binding never waits for the
+    previous one's copy, which may sit behind other work on the stream."""
+    st = _stage_state(plan)
+    k = st["next"] = 1 - st["next"]
+    stage, ev = st["stages"][k], st["events"][k]
+    if ev is not None:
+        ev.synchronize()                         # the buffer may still be read by its copy
     if stage is None or stage.numel() < n3:
-        if ev is not None:
-            ev.synchronize()                     # the old buffer may still be read by its copy
-        stage = stages[k] = torch.zeros(n3, dtype=torch.int64, pin_memory=torch.cuda.is_available())
-    elif ev is not None:
-        ev.synchronize()
+        stage = st["stages"][k] = torch.zeros(n3, dtype=torch.int64, pin_memory=torch.cuda.is_available())
     return stage
 
 
@@ -736,7 +764,8 @@ def _table_upload(plan, stage: torch.Tensor, n3: int, device) -> torch.Tensor:
         table.copy_(stage[:n3], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(device))
-        plan.__dict__["_table_stage_evs"][plan.__dict__["_table_stage_next"]] = ev
+        st = _stage_state(plan)
+        st["events"][st["next"]] = ev
         return table
     return stage[:n3].clone()
 
@@ -857,9 +886,7 @@ class SlerpListBinding:
         if ref_dot is not None:
             _pair_ref_merge(plan, self.in_dt, self.out_dt, t, dot_threshold, eps, ref_dot, speculate, table=self.table)
         elif speculate:
-            redo = getattr(plan, "_redo", None)
-            if redo is None:
-                redo = plan._redo = torch.empty(max(1, plan.nseg), dtype=torch.int32, device=self.device)
+            redo = plan.ws("redo", plan.nseg, torch.int32)
             L.check(lib.edt_slerp_merge_table_speculative(
                 L.ptr(self.table), self.in_dt, self.out_dt, L.ptr(plan.chunks), plan.nchunks, L.ptr(plan.seg_first),
                 plan.nseg, L.ptr(t), float(dot_threshold), float(eps), L.ptr(plan.partial), L.ptr(plan.coef),
@@ -1007,10 +1034,7 @@ def slerp_population(plan: SlerpPlan, members: list[torch.Tensor], pairs, outs: 
     icode, ocode = L.dtype_code(in_dt), L.dtype_code(out_dt)
     if ref_dot is not None and not speculate and Q:
         # the Gram form's passes separately: sums -> dots -> the reference's coefficients -> blends
-        gram = getattr(plan, "_gram", None)
-        need = int(lib.edt_slerp_population_gram_doubles(M, plan.nchunks))
-        if gram is None or gram.numel() < max(1, need):
-            gram = plan._gram = torch.empty(max(1, need), dtype=torch.float64, device=dev)
+        gram = plan.ws("gram", int(lib.edt_slerp_population_gram_doubles(M, plan.nchunks)), torch.float64)
         slerp_gram(members, plan.chunks, plan.nchunks, work=gram)
         _, dots = slerp_gram_coef(plan, gram, M, pairs, t, dot_threshold, eps)
         dots, coef = _population_ref(plan, members, pairs, outs, t, dots, None, icode, ocode, dot_threshold, eps,
@@ -1027,19 +1051,17 @@ def slerp_population(plan: SlerpPlan, members: list[torch.Tensor], pairs, outs: 
             dots, coef = _population_ref(plan, members, pairs, outs, t, dots, coef, icode, ocode, dot_threshold, eps,
                                          ref_dot, blend_all=False)
     else:
-        need = int(lib.edt_slerp_population_gram_doubles(M, plan.nchunks))
-        gram = getattr(plan, "_gram", None)
-        if gram is None or gram.numel() < max(1, need):
-            gram = plan._gram = torch.empty(max(1, need), dtype=torch.float64, device=dev)
+        gram = plan.ws("gram", int(lib.edt_slerp_population_gram_doubles(M, plan.nchunks)), torch.float64)
         L.check(lib.edt_slerp_population(L.ptr_array(members), M, icode, flat_pairs, Q,
                                          L.ptr_array(outs), ocode, L.ptr(plan.chunks), plan.nchunks,
                                          L.ptr(plan.seg_first), plan.nseg, L.ptr(t), float(dot_threshold), float(eps),
                                          L.ptr(gram), L.ptr(coef), L.ptr(dots), L.stream_ptr(dev)),
                 "edt_slerp_population")
-    plan._pop_dots = dots[:Q, :plan.nseg]
+    dots = dots[:Q, :plan.nseg]
+    plan._pop_dots = dots                        # the latest generation's (bench.py reads it)
     plan._last_thr = float(dot_threshold)
-    _record_dots(plan, plan._pop_dots, "_pop_dots")
-    return plan._pop_dots
+    _record_dots(plan, dots, "_pop_dots")
+    return dots
 
 
 def pair_merge_population(children, lr: float, momentum_coef: float, nesterov: bool) -> None:

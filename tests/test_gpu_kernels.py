@@ -702,7 +702,8 @@ def test_slerp_speculative_matches_two_pass(dev, ops, in_dt, out_dt):
         rc = L.lib().edt_slerp_merge_speculative(L.ptr(v0), L.ptr(v1), L.dtype_code(v0), L.ptr(v0), L.dtype_code(v0),
                                                  L.ptr(plan.chunks), plan.nchunks, L.ptr(plan.seg_first), plan.nseg,
                                                  L.ptr(ts), 0.9995, 1e-8, L.ptr(plan.partial), L.ptr(plan.coef), None,
-                                                 L.ptr(plan._redo), v0.numel(), L.stream_ptr(dev))
+                                                 L.ptr(plan.ws("redo", plan.nseg, torch.int32)), v0.numel(),
+                                                 L.stream_ptr(dev))
         assert rc != 0
         with pytest.raises(EdtError):
             L.check(rc, "edt_slerp_merge_speculative")

@@ -1,0 +1,125 @@
+"""Host threads merging over ONE shared SlerpPlan at the same time, each on its own stream (what
+virtual ranks and a threaded master do: plans are cached per layout, merge._plan_for). Every device
+workspace a merge writes through the plan — coefficients, dots, the redo flags, the Gram rows, the
+reference-dot workspace, the pointer-table staging — is the calling thread's (SlerpPlan.ws,
+ops._stage_state), so every thread's outputs and dots equal the serial run's bit for bit."""
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+from evolutionarydistributedtraining_amd import ops
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+SIZES = [70001, 8, 131072, 4099, 1, 65536 * 3 + 5, 1024, 333]
+NTHREADS, REPS = 4, 5
+
+
+def _data(seed, far_every=2):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    v0 = [torch.randn(n, generator=g, device=DEV).bfloat16() for n in SIZES]
+    v1 = []
+    for i, (a, n) in enumerate(zip(v0, SIZES)):
+        if i % far_every == 0:                     # far: the SLERP branch
+            v1.append(torch.randn(n, generator=g, device=DEV).bfloat16())
+        else:                                      # lineage: the lerp branch
+            v1.append((a.float() + 0.01 * torch.randn(n, generator=g, device=DEV)).bfloat16())
+    return v0, v1
+
+
+def _t(r):
+    return torch.tensor([0.15 + 0.1 * r + 0.01 * s for s in range(len(SIZES))], dtype=torch.float64, device=DEV)
+
+
+def _bits(x):
+    return x.view(torch.int16) if x.dtype == torch.bfloat16 else x.view(torch.int32)
+
+
+def _run_threads(fn):
+    errs, barrier = [], threading.Barrier(NTHREADS)
+    got = [None] * NTHREADS
+
+    def body(r):
+        try:
+            s = torch.cuda.Stream(DEV)
+            with torch.cuda.stream(s):
+                barrier.wait()
+                got[r] = [fn(r) for _ in range(REPS)]
+            s.synchronize()
+        except Exception as e:                     # noqa: BLE001 - re-raised below
+            errs.append(e)
+            barrier.abort()
+
+    ths = [threading.Thread(target=body, args=(r,)) for r in range(NTHREADS)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    if errs:
+        raise errs[0]
+    return got
+
+
+@pytest.mark.parametrize("speculate", [False, True])
+def test_list_merges_from_threads_on_one_plan(speculate):
+    plan = ops.make_slerp_plan([0] + np.cumsum(SIZES).tolist(), DEV, relative=True)
+    data = [_data(100 + r) for r in range(NTHREADS)]
+
+    def merge(r):
+        v0, v1 = data[r]
+        outs = [torch.empty_like(a) for a in v0]
+        ops.slerp_list(plan, v0, v1, outs, _t(r), speculate=speculate)
+        return outs, plan.dots[:len(SIZES)].clone()
+
+    want = [merge(r) for r in range(NTHREADS)]
+    torch.cuda.synchronize()
+    got = _run_threads(merge)
+    for r in range(NTHREADS):
+        for outs, dots in got[r]:
+            assert torch.equal(dots, want[r][1]), r
+            for a, b in zip(outs, want[r][0]):
+                assert torch.equal(_bits(a), _bits(b)), r
+
+
+@pytest.mark.parametrize("speculate", [False, True])
+def test_arena_merges_from_threads_on_one_plan(speculate):
+    offs = [0] + np.cumsum(SIZES).tolist()
+    plan = ops.make_slerp_plan(offs, DEV)
+    data = [tuple(torch.cat(x) for x in _data(200 + r)) for r in range(NTHREADS)]
+
+    def merge(r):
+        v0, v1 = data[r]
+        out = torch.empty_like(v0)
+        ops.slerp_arena(plan, v0, v1, out, _t(r), speculate=speculate)
+        return out, plan.coef[:len(SIZES)].clone()
+
+    want = [merge(r) for r in range(NTHREADS)]
+    torch.cuda.synchronize()
+    got = _run_threads(merge)
+    for r in range(NTHREADS):
+        for out, coef in got[r]:
+            assert torch.equal(coef, want[r][1]) and torch.equal(_bits(out), _bits(want[r][0])), r
+
+
+@pytest.mark.parametrize("speculate", [False, True])
+def test_population_from_threads_on_one_plan(speculate):
+    offs = [0] + np.cumsum(SIZES).tolist()
+    plan = ops.make_slerp_plan(offs, DEV)
+    members = [[torch.cat(_data(300 + 10 * r + m, far_every=3)[m % 2]) for m in range(4)] for r in range(NTHREADS)]
+    pairs = [(0, 1), (1, 2), (2, 0), (3, 1), (0, 3)]
+
+    def merge(r):
+        outs = [torch.empty_like(members[r][0]) for _ in pairs]
+        dots = ops.slerp_population(plan, members[r], pairs, outs, _t(r), speculate=speculate)
+        return outs, dots.clone()
+
+    want = [merge(r) for r in range(NTHREADS)]
+    torch.cuda.synchronize()
+    got = _run_threads(merge)
+    for r in range(NTHREADS):
+        for outs, dots in got[r]:
+            assert torch.equal(dots, want[r][1]), r
+            for a, b in zip(outs, want[r][0]):
+                assert torch.equal(_bits(a), _bits(b)), r

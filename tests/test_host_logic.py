@@ -566,3 +566,40 @@ def test_binding_from_checked_writes_the_checked_image():
     assert slow.apart and fast.apart and torch.equal(fast.table, slow.table)
     with pytest.raises(ops.L.EdtError):
         ops.SlerpListBinding.from_checked(plan, p0[:-1], p1[:-1], po[:-1], torch.bfloat16, torch.bfloat16, None, None)
+
+
+def test_table_staging_is_per_host_thread():
+    """The pinned pointer-table staging of a plan (ops._table_stage) belongs to the calling host
+    thread: plans are shared (merge._plan_for) and virtual-rank threads bind on one plan at once, so
+    two threads never write the same staging buffer; each thread alternates its own two."""
+    import threading
+
+    from evolutionarydistributedtraining_amd import ops
+
+    class Plan:
+        pass
+    plan = Plan()
+    got = {}
+    alive = threading.Barrier(3)                  # all three alive at once (idents are not reused)
+
+    def run(name):
+        bufs = []
+        for i in range(4):
+            st = ops._table_stage(plan, 12)
+            bufs.append(st.data_ptr())
+            ops._table_upload(plan, st, 12, None)
+            if i == 1:
+                alive.wait()
+        got[name] = bufs
+        alive.wait()
+
+    ths = [threading.Thread(target=run, args=(i,)) for i in range(3)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    sets = [set(v) for v in got.values()]
+    assert all(len(s) == 2 for s in sets)                       # two buffers per thread, in turn
+    assert all(v[0] == v[2] and v[1] == v[3] and v[0] != v[1] for v in got.values())
+    assert not (sets[0] & sets[1] or sets[0] & sets[2] or sets[1] & sets[2])
+    assert len(plan.__dict__["_table_stage_state"]) == 3
