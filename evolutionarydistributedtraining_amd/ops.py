@@ -244,6 +244,20 @@ def lerp(t: float, v0: torch.Tensor, v1: torch.Tensor, out: torch.Tensor | None 
 _TLS = threading.local()             # per host thread: {(device, stream): float64 buffer}
 
 
+def _thread_slot(owner: dict, name: str) -> dict:
+    """owner[name]'s dict for the calling host thread (created empty), held weakly by the thread
+    object: a plan's per-thread workspaces are released with the thread that made them."""
+    import weakref
+    per = owner.get(name)
+    if per is None:
+        per = owner.setdefault(name, weakref.WeakKeyDictionary())
+    th = threading.current_thread()
+    slot = per.get(th)
+    if slot is None:
+        slot = per.setdefault(th, {})
+    return slot
+
+
 def _scratch(device: torch.device, ndoubles: int) -> torch.Tensor:
     """float64 device workspace of `ndoubles` (a view) from one growing buffer per (device, stream)
     of the calling host thread. The chunk-sum passes' rows and row scratch are only live inside one
@@ -292,7 +306,7 @@ class SlerpPlan:
         demand; a view of n): plans are shared (merge._plan_for, the population planners) and host
         threads (virtual ranks) may merge over one plan at the same time, each reading back its own
         coefficients and dots."""
-        per = self.__dict__.setdefault("_ws_by_thread", {}).setdefault(threading.get_ident(), {})
+        per = _thread_slot(self.__dict__, "_ws_by_thread")
         n = max(1, int(n))
         buf = per.get(name)
         if buf is None or buf.numel() < n or buf.dtype != dtype:
@@ -532,8 +546,7 @@ def _reference_finish(dots: torch.Tensor, flag: torch.Tensor, val: torch.Tensor,
 
 def _dots_state(plan) -> dict:
     """The calling host thread's record of its previous merges' dots on this plan."""
-    per = plan.__dict__.setdefault("_dots_by_thread", {})
-    return per.setdefault(threading.get_ident(), {})
+    return _thread_slot(plan.__dict__, "_dots_by_thread")
 
 
 def _record_dots(plan: SlerpPlan, dots: torch.Tensor, attr: str) -> None:
@@ -734,11 +747,9 @@ _ELEM_SIZE = {torch.float32: 4, torch.bfloat16: 2, torch.float16: 2, torch.float
 def _stage_state(plan) -> dict:
     """The calling host thread's staging state on this plan: plans are shared (merge._plan_for),
     and host threads (virtual ranks) may bind on one plan at the same time."""
-    per = plan.__dict__.setdefault("_table_stage_state", {})
-    tid = threading.get_ident()
-    st = per.get(tid)
-    if st is None:
-        st = per[tid] = {"stages": [None, None], "events": [None, None], "next": 1}
+    st = _thread_slot(plan.__dict__, "_table_stage_state")
+    if not st:
+        st.update(stages=[None, None], events=[None, None], next=1)
     return st
 
 

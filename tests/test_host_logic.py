@@ -603,3 +603,7 @@ def test_table_staging_is_per_host_thread():
     assert all(v[0] == v[2] and v[1] == v[3] and v[0] != v[1] for v in got.values())
     assert not (sets[0] & sets[1] or sets[0] & sets[2] or sets[1] & sets[2])
     assert len(plan.__dict__["_table_stage_state"]) == 3
+    import gc
+    del ths, t
+    gc.collect()
+    assert len(plan.__dict__["_table_stage_state"]) == 0      # released with the threads
