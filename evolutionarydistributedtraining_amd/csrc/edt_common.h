@@ -64,6 +64,9 @@ using edt::g_err;
 // parent loads + one workgroup per segment for the chunk-sum reduction + 64 Ki-element chunks
 // 11.23 / 11.41 ms, against 12.14 / 12.27 ms for default loads, one wave per segment and 16 Ki
 // chunks. The population form (edt_slerp_population) keeps default-policy loads (2 % faster).
+#ifndef EDT_NT_SLERP_STORES     // non-temporal stores of the pair SLERP's children (the speculative
+#define EDT_NT_SLERP_STORES 1   // pass's lerp outputs, the blends): r5, 7B lineage 6.63 vs 7.16 ms,
+#endif                          // blend 6.44 vs 6.84 (profiles/r05_nt_stores_variants.log)
 #ifndef EDT_NT_SLERP            // non-temporal loads of the SLERP parents (stats and blend passes)
 #define EDT_NT_SLERP 1
 #endif

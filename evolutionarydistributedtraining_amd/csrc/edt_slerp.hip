@@ -331,7 +331,7 @@ __device__ __forceinline__ void pair_tile(const void* v0, const void* v1, void* 
             float o[kVec];
 #pragma unroll
             for (int e = 0; e < kVec; ++e) o[e] = l0 * x[e] + l1 * y[e];
-            st<ODT, kVec>(out, i, o);
+            st<ODT, kVec, (EDT_NT_SLERP_STORES != 0)>(out, i, o);
         }
     }
     if (j == 0)
@@ -646,7 +646,7 @@ __global__ __launch_bounds__(kBlock) void slerp_blend_kernel(const void* v0, con
         const float c0 = coef[2 * seg], c1 = coef[2 * seg + 1];
         for_range_elems(start, end, [&](auto tagN, uint64_t i) {
             constexpr int N = decltype(tagN)::value;
-            lerp_elems<IDT, ODT, EDT_F32, N, NT && N == kVec>(a, b, o, i, c0, c1);
+            lerp_elems<IDT, ODT, EDT_F32, N, NT && N == kVec, (EDT_NT_SLERP_STORES != 0)>(a, b, o, i, c0, c1);
         });
     });
 }
@@ -687,7 +687,7 @@ __global__ __launch_bounds__(kBlock) void slerp_blend_tile_kernel(const void* __
         float r[kVec];
 #pragma unroll
         for (int e = 0; e < kVec; ++e) r[e] = c0 * x[e] + c1 * y[e];
-        st<ODT, kVec>(o, i, r);
+        st<ODT, kVec, (EDT_NT_SLERP_STORES != 0)>(o, i, r);
     }
     if (j == 0)
         tile0_edge(start, len, [&](uint64_t e) {

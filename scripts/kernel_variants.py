@@ -106,6 +106,7 @@ VARIANTS.update({"f32_nt": ["-DEDT_NT_F32=1"], "f32_bpc64": ["-DEDT_BLOCKS_PER_C
                  "f32_nt_ntst": ["-DEDT_NT_F32=1", "-DEDT_NT_STORES=1"],
                  "f32_nt_bpc128": ["-DEDT_NT_F32=1", "-DEDT_BLOCKS_PER_CU=128"]})
 VARIANTS.update({f"pop{i}": [f"-DEDT_POP_ITERS={i}"] for i in (1, 2, 8, 16)})
+VARIANTS["r5ntst"] = []            # r5: the in-tree build after EDT_NT_SLERP_STORES (copied, not rebuilt)
 VARIANTS.update({"default": [], "f32_ntst": ["-DEDT_NT_STORES=1"], "nt_rmw": ["-DEDT_NT_RMW=1"],
                  "nt_rmw_st": ["-DEDT_NT_RMW=1", "-DEDT_NT_STORES=1"],
                  "s_bpc1024": ["-DEDT_SLERP_BPC=1024"], "s_bpc4096": ["-DEDT_SLERP_BPC=4096"]})
