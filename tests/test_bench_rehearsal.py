@@ -92,6 +92,9 @@ def _rank_main():
 
 
 def _launch(world, extra=(), hang_rank=-1, timeout=240, corrupt=False):
+    import tempfile
+    detail = os.path.join(tempfile.mkdtemp(prefix="edt_rehearsal_"), "detail.json")
+    extra = ["--detail-out", detail] + list(extra)
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
@@ -114,7 +117,19 @@ def _launch(world, extra=(), hang_rank=-1, timeout=240, corrupt=False):
             if p.poll() is None:
                 p.kill()
     lines = [l for l in outs[0][1].splitlines() if l.startswith("{")]
+    for l in lines:                  # the whole line fits the driver's stdout tail
+        assert len(l) <= 8000, len(l)
+    if lines and os.path.exists(detail):     # the printed line is the compact projection:
+        with open(detail) as f:              # tests read the full record from the sidecar
+            full = json.load(f)
+        lines = [json.dumps(dict(full, line=json.loads(lines[0])))]
     return outs, lines
+
+
+def bench_link_gbps():
+    sys.path.insert(0, ROOT)
+    import bench
+    return bench.XGMI_LINK_GBPS
 
 
 @pytest.mark.slow
@@ -129,6 +144,14 @@ def test_bench_line_at_world(world):
     d = json.loads(lines[0])
     assert d["n_gpus"] == world and d["value"] >= 0 and d["ms_per_step"] > 0     # tiny layout: ~0 GB/s
     assert d["roofline"]["xgmi"]["wire_bytes_per_rank"] > 0
+    line = d["line"]
+    assert "dropped" not in line and line["detail"].endswith("detail.json")
+    # the first hardware line states its own exchange floor (wire bytes / (N-1) links)
+    x = line["roofline"]["xgmi"]
+    assert x["floor_ms"] == pytest.approx(x["wire_bytes_per_rank"] / (bench_link_gbps() * (world - 1) * 1e9) * 1e3,
+                                          abs=1e-4)
+    assert all("xgmi_floor_ms" in v for v in line["other_schedules"].values())
+    assert line["population_slerp_7b"]["sharded"]["parity_bit_exact"] is True
     assert d["roofline"]["kernel_ms"] > 0 and d["roofline"]["algo_bytes_per_launch"] > 0
     assert d["cpu_baseline"]["value"] > 0 and "c_port" in d["cpu_baseline"]
     for key in ("weak_scaling", "other_schedules", "baseline_configs", "population_slerp_7b"):

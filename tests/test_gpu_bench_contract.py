@@ -3,7 +3,9 @@ driver parses (metric / value / unit / n_gpus / steps / warmup / ms_per_step / h
 scaling / vs_baseline / dtype / data / config), plus the `roofline` object (bound, achieved, peak,
 unit, frac = achieved / peak, traffic) and the `cpu_baseline` object (value, unit, cores, kind,
 sample) — for the single-GPU line and for the multi-GPU code path at world 1 (`--sharded`, which
-adds roofline.xgmi). Small layout and short budgets: the contract, not the numbers."""
+adds roofline.xgmi). Small layout and short budgets: the contract, not the numbers. The printed
+line is capped at bench.LINE_CAP characters (the driver keeps only the tail of stdout); the full
+record is the sidecar the line names as `detail`, and the sub-object checks read it from there."""
 import json
 import os
 import subprocess
@@ -18,19 +20,29 @@ TOP = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "h
        "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"}
 
 
-def _run(*extra):
+def _run(*extra, full=False):
+    import tempfile
+
     import torch
     if not torch.cuda.is_available():
         pytest.skip("needs a HIP device")
+    detail = os.path.join(tempfile.mkdtemp(prefix="edt_bench_"), "detail.json")
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
                                                            "MASTER_PORT")}
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--layout", "gpt2_small", "--steps", "3", "--warmup", "1",
-           "--cpu-baseline-seconds", "0.4", "--cpu-sample-elems", str(1 << 18), "--ops-cpu-seconds", "0.2", *extra]
+           "--cpu-baseline-seconds", "0.4", "--cpu-sample-elems", str(1 << 18), "--ops-cpu-seconds", "0.2",
+           "--detail-out", detail, *extra]
     p = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=110)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [l for l in p.stdout.splitlines() if l.strip()]
     assert len(lines) == 1, p.stdout              # stdout carries exactly the one JSON line
-    return json.loads(lines[0])
+    assert len(lines[0]) <= 8000, len(lines[0])   # the whole line fits the driver's stdout tail
+    line = json.loads(lines[0])
+    assert "dropped" not in line, line["dropped"]
+    if not full:
+        return line
+    with open(detail) as f:
+        return line, json.load(f)
 
 
 def _check_common(d, n_gpus):
@@ -81,10 +93,14 @@ def test_single_gpu_line_population_extra():
     """The N = 1 line's BASELINE configs[4] sub-object (population_slerp_7b: 8 members and 8
     children resident, both SLERP forms), here on the 125M layout: fields, roofline arithmetic,
     every lineage tensor in the lerp branch."""
-    d = _run("--place-candidates", "1", "--ops", "population_7b", "--population-layout", "gpt2_small",
-             "--bcast-compare", "0")
+    line, d = _run("--place-candidates", "1", "--ops", "population_7b", "--population-layout", "gpt2_small",
+                   "--bcast-compare", "0", full=True)
     _check_common(d, 1)
+    _check_common(line, 1)
     p = d["population_slerp_7b"]
+    lp = line["population_slerp_7b"]
+    assert lp["speculative"]["ms_per_generation"] == p["speculative"]["ms_per_generation"]
+    assert lp["two_pass"]["gen_ms"] == [g["two_pass"]["ms"] for g in p["generations"]]
     assert "error" not in p and "skipped" not in p, p
     assert "roulette_wheel_selection" in p["pairs_source"] and p["timed_reps"] >= 10
     gens = p["generations"] + [p["ring"]]
@@ -109,10 +125,11 @@ def test_single_gpu_line_lm_population_extra():
     """The N = 1 line's EDT-LM generation (lm_population: 8 members of the 1.3B layout resident,
     rank-selected pairs, one edt_pair_merge_population launch per generation): fields and the
     roofline arithmetic over the drawn generations' floor bytes."""
-    d = _run("--place-candidates", "1", "--ops", "lm_population", "--bcast-compare", "0",
-             "--population-generations", "2")
+    line, d = _run("--place-candidates", "1", "--ops", "lm_population", "--bcast-compare", "0",
+                   "--population-generations", "2", full=True)
     _check_common(d, 1)
     p = d["lm_population"]
+    assert line["lm_population"]["gen_ms"] == [g["ms"] for g in p["generations"]]
     assert "error" not in p, p
     assert "rank_based_selection" in p["pairs_source"] and len(p["generations"]) == 2 and p["timed_reps"] >= 10
     fb = sum(g["floor_bytes"] for g in p["generations"])
