@@ -60,6 +60,11 @@ using edt::g_err;
 #ifndef EDT_NT_LERP             // non-temporal loads of lerp's two (read-once) inputs
 #define EDT_NT_LERP 0
 #endif
+#ifndef EDT_NT_LERP_STORES      // non-temporal stores of lerp's child (written once, never re-read by
+#define EDT_NT_LERP_STORES 1    // the merge): r6, interleaved on the same buffers, bits identical —
+#endif                          // 1.3B 1.323 vs 1.340 ms, 7B body 6.957 vs 7.053 ms; the pair merge
+                                // measured no gain (3.05 vs 3.00 ms at 1.3B, equal at 7B) and keeps
+                                // ordinary stores (profiles/r06_store_kind_probe.jsonl)
 // SLERP of two Qwen2.5-7B bodies (bf16, profiles/r01_slerp_variants.json, two boxes): non-temporal
 // parent loads + one workgroup per segment for the chunk-sum reduction + 64 Ki-element chunks
 // 11.23 / 11.41 ms, against 12.14 / 12.27 ms for default loads, one wave per segment and 16 Ki

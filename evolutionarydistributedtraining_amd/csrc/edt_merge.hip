@@ -157,7 +157,7 @@ __global__ __launch_bounds__(kBlock) void lerp_kernel(const void* v0, const void
     if constexpr (N == kVec) {
         const uint64_t nv = n / kVec;
         for (uint64_t v = tid; v < nv; v += stride)
-            lerp_elems<IDT, ODT, CDT, kVec, EDT_NT_LERP != 0>(v0, v1, out, v * kVec, c0, c1);
+            lerp_elems<IDT, ODT, CDT, kVec, EDT_NT_LERP != 0, EDT_NT_LERP_STORES != 0>(v0, v1, out, v * kVec, c0, c1);
         const uint64_t t = nv * kVec + tid;
         if (t < n) lerp_elems<IDT, ODT, CDT, 1>(v0, v1, out, t, c0, c1);
     } else {

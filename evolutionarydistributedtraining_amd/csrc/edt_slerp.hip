@@ -2812,6 +2812,9 @@ int edt_slerp_population_layout(const int32_t* pairs, int npairs, int nmembers, 
 
 }   // extern "C"
 
+static int seg_table_impl(const void* const* v0_t, const void* const* v1_t, void* const* out_t, int nseg,
+                          const uint64_t* seg_numel, int in_dt, int out_dt, int apart, uint64_t* table_host);
+
 namespace {
 // The tensor-list forms: segment s is its own tensor triple {v0, v1, out}, read through a DEVICE
 // table of 3 x nseg uint64 pointers (edt_slerp_seg_table validates and writes its host image; the
@@ -2871,15 +2874,13 @@ int upload_seg_table(const void* const* v0_t, const void* const* v1_t, void* con
     if (reinterpret_cast<uintptr_t>(workspace) & 7u) return fail(EDT_ERR_ARG, "workspace must be 8-byte aligned");
     thread_local std::vector<uint64_t> h;
     h.assign(3 * (size_t)nseg, 0);
-    int rc = edt_slerp_seg_table(v0_t, v1_t, out_t, nseg, seg_numel, in_dt, out_dt, apart, h.data());
+    int rc = seg_table_impl(v0_t, v1_t, out_t, nseg, seg_numel, in_dt, out_dt, apart, h.data());
     if (rc) return rc;
     hipError_t e = hipMemcpyAsync(workspace, h.data(), need, hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return fail(EDT_ERR_LAUNCH, "tensor table upload failed: %s", hipGetErrorString(e));
     return EDT_OK;
 }
 }   // namespace
-
-extern "C" {
 
 // apart = 0 (the two-pass form): an output may be exactly one of its own parents (written in place
 // after the stats pass read it), never overlap another tensor's parent or output. Spans grouped by
@@ -2912,8 +2913,10 @@ inline bool in_place_safe(std::vector<SegSpan>& sp) {
     return true;
 }
 
-int edt_slerp_seg_table(const void* const* v0_t, const void* const* v1_t, void* const* out_t, int nseg,
-                        const uint64_t* seg_numel, int in_dt, int out_dt, int apart, uint64_t* table_host) {
+// seg_numel may be NULL only here, for edt_slerp_merge_list (its ABI carries no sizes: the
+// in-place rule is its caller's, as the header says); the public entry requires the sizes.
+static int seg_table_impl(const void* const* v0_t, const void* const* v1_t, void* const* out_t, int nseg,
+                          const uint64_t* seg_numel, int in_dt, int out_dt, int apart, uint64_t* table_host) {
     g_err[0] = 0;
     if ((in_dt | out_dt) & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
     if (nseg < 0) return fail(EDT_ERR_ARG, "negative segment count");
@@ -2958,6 +2961,17 @@ int edt_slerp_seg_table(const void* const* v0_t, const void* const* v1_t, void* 
                                      "exactly, may be written in place)");
     }
     return EDT_OK;
+}
+
+extern "C" {
+
+int edt_slerp_seg_table(const void* const* v0_t, const void* const* v1_t, void* const* out_t, int nseg,
+                        const uint64_t* seg_numel, int in_dt, int out_dt, int apart, uint64_t* table_host) {
+    if (nseg > 0 && !seg_numel) {
+        g_err[0] = 0;
+        return fail(EDT_ERR_ARG, "the overlap checks need the segment sizes (seg_numel)");
+    }
+    return seg_table_impl(v0_t, v1_t, out_t, nseg, seg_numel, in_dt, out_dt, apart, table_host);
 }
 
 int edt_slerp_stats_table(const uint64_t* seg_table, int in_dt, const uint64_t* chunk_desc, int64_t nchunks,

@@ -423,6 +423,9 @@ def _rebind_merge(params, keys, outs, sd1, sd2, plan, out_dtype, dev, dot_thresh
             params[k].data.record_stream(cur)
             params[k].data = buf.as_strided(o.shape, _contig_strides(o.shape), a)
     if bound is not None:
+        done = torch.cuda.Event()
+        done.record(cur)                         # the launch that read the held memory
+        bound.update(done=done)
         bound.update(keys=keys, ts=[t for _, t in plan], tt=tt, splan=splan, ns=ns, offs=offs, total=total,
                      in_dt=in_dt, out_dt=out_dtype, p0=po, p1=p1, buf=buf, shapes=[o.shape for o in outs],
                      hold2=[b.data for _, b in pairs],
@@ -468,7 +471,7 @@ class _Bound:
     def __init__(self, key, model_1, model_2, dev, rec):
         import weakref
         self.key, self.dev = key, dev
-        drop = lambda _r, key=key, cache=_bound_cache: cache.pop(key, None)   # safe at interpreter exit
+        drop = lambda _r, key=key, cache=_bound_cache, evict=_evict: evict(cache, key)   # safe at exit
         self.r1, self.r2 = weakref.ref(model_1, drop), weakref.ref(model_2, drop)
         for k, v in rec.items():
             setattr(self, k, v)
@@ -479,6 +482,19 @@ class _Bound:
 
 
 _bound_cache: dict = {}
+
+
+def _evict(cache: dict, key) -> None:
+    """Drop a cached binding once the last launch that read its held memory (`done`, an event on
+    the stream that launch ran on, whatever the device) has finished: the held tensors may be the
+    last references to a parent's storage, which must not be reused while a merge reads it."""
+    b = cache.pop(key, None)
+    ev = getattr(b, "done", None)
+    if ev is not None:
+        try:
+            ev.synchronize()
+        except Exception:        # noqa: BLE001 - interpreter shutdown: the runtime may be gone
+            pass
 
 
 def clear_merge_cache() -> None:
@@ -505,7 +521,7 @@ def _bound_merge(b: _Bound, model_1, model_2) -> bool:
     f1, l1, f2, l2 = b.ends
     if (f1.data_ptr() != int(b.p0[0]) or l1.data_ptr() != int(b.p0[-1]) or f2.data_ptr() != int(b.p1[0])
             or l2.data_ptr() != int(b.p1[-1])):
-        _bound_cache.pop(b.key, None)
+        _evict(_bound_cache, b.key)
         return False
     buf = torch.empty(b.total, dtype=b.out_dt, device=b.dev)
     po = np.uint64(buf.data_ptr()) + b.offs_bytes
@@ -524,9 +540,10 @@ def _bound_merge(b: _Bound, model_1, model_2) -> bool:
         ok = (meta is not None and meta[3] == b.in_dt and np.array_equal(meta[0], b.p0)
               and np.array_equal(meta[1], b.p1) and np.array_equal(meta[2], b.ns)
               and [a.shape for a, _ in pairs] == b.shapes and next(model_1.parameters()).dtype == b.out_dt)
+    b.done = torch.cuda.Event()
+    b.done.record(cur)
     if not ok:
-        cur.synchronize()                       # the launch read the held memory: let it finish
-        _bound_cache.pop(b.key, None)
+        _evict(_bound_cache, b.key)              # the launch read the held memory: let it finish
         return False
     with torch.no_grad():                        # overlaps the kernels
         for k, shp, st, off in zip(b.keys, b.shapes, b.strides, b.offs_list):
@@ -568,9 +585,8 @@ def merge_models_into_(target: torch.nn.Module, model_1: torch.nn.Module, model_
                            bound=rec)
         if rec:                                   # the single-pass rebind ran: remember it
             rec["all_keys"] = list(sd1.keys())
-            if len(_bound_cache) >= 4:               # the oldest binding goes; merges in flight may
-                torch.cuda.current_stream(rec["tt"].device).synchronize()   # still read what it holds
-                _bound_cache.pop(next(iter(_bound_cache)))
+            if len(_bound_cache) >= 4:               # the oldest binding goes, once its last merge
+                _evict(_bound_cache, next(iter(_bound_cache)))      # (any stream, any device) is done
             _bound_cache[key] = _Bound(key, model_1, model_2, rec["tt"].device, rec)
     else:
         target.load_state_dict(slerp_state_dicts(sd1, sd2, plan, out_dtype=out_dtype, device=dev))

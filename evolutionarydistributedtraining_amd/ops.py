@@ -302,15 +302,18 @@ class SlerpPlan:
         return len(self.seg_offsets) - 1
 
     def ws(self, name: str, n: int, dtype: torch.dtype) -> torch.Tensor:
-        """The calling host thread's device workspace `name` on this plan (>= n elements, grown on
-        demand; a view of n): plans are shared (merge._plan_for, the population planners) and host
-        threads (virtual ranks) may merge over one plan at the same time, each reading back its own
-        coefficients and dots."""
+        """The device workspace `name` on this plan of the calling host thread and its current
+        stream (>= n elements, grown on demand; a view of n): plans are shared (merge._plan_for, the
+        population planners), host threads (virtual ranks) may merge over one plan at the same time,
+        and one thread may issue merges over one plan on two streams without syncing between them —
+        each (thread, stream) reads back its own coefficients and dots, as _scratch keys its rows."""
         per = _thread_slot(self.__dict__, "_ws_by_thread")
         n = max(1, int(n))
-        buf = per.get(name)
+        dev = self.chunks.device
+        key = (name, torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else 0)
+        buf = per.get(key)
         if buf is None or buf.numel() < n or buf.dtype != dtype:
-            buf = per[name] = torch.empty(n, dtype=dtype, device=self.chunks.device)
+            buf = per[key] = torch.empty(n, dtype=dtype, device=dev)
         return buf[:n]
 
     @property
@@ -384,11 +387,14 @@ def host_dispatch() -> dict:
     global _HOST_DISPATCH
     if _HOST_DISPATCH is None:
         import numpy as np
-        from numpy.lib import introspect
         disp = {}
-        for f in ("arccos", "sin"):
-            info = introspect.opt_func_info(func_name=f"^{f}$", signature="float32").get(f, {})
-            disp[f] = next(iter(info.values()), {}).get("current")
+        try:                                    # numpy >= 2.0 only
+            from numpy.lib import introspect
+            for f in ("arccos", "sin"):
+                info = introspect.opt_func_info(func_name=f"^{f}$", signature="float32").get(f, {})
+                disp[f] = next(iter(info.values()), {}).get("current")
+        except (ImportError, AttributeError):
+            disp = {"arccos": "unknown", "sin": "unknown"}      # host_mismatch reports it (strict: raises)
         blas, threads = None, None
         try:
             from threadpoolctl import threadpool_info
@@ -431,7 +437,11 @@ class RefDot:
     strict: bool = False
 
     def host_mismatch(self) -> list[str]:
-        """What differs between the running host and the host this mode reproduces ([] = none)."""
+        """What differs between the running host and the host this mode reproduces ([] = none).
+        A dispatch numpy cannot report (numpy < 2: no numpy.lib.introspect) counts as a difference.
+        numpy's BLAS pool size is not compared: OpenBLAS decides per call how many threads sdot
+        uses (the golden host reported 8 and its dots are reproduced with threads = 1), so the pool
+        does not say it; `threads` is the parameter that does."""
         host = host_dispatch()
         out = [f"numpy float32 {f} dispatches to {host['coef_dispatch'].get(f)}, the modelled host's to {want}"
                for f, want in self.coef_dispatch if host["coef_dispatch"].get(f) != want]

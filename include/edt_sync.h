@@ -264,8 +264,8 @@ int edt_slerp_merge_speculative(const void* v0, const void* v1, int in_dt, void*
  *                         check over every tensor, seg_numel = the nseg sizes; r5: without
  *                         `apart` but with seg_numel, an output may be exactly one of its OWN
  *                         parents and must overlap no other tensor's parent or output — the
- *                         two-pass blend would race; seg_numel NULL skips the check and the
- *                         caller guarantees it) and writes the
+ *                         two-pass blend would race; r6: seg_numel is required whenever
+ *                         nseg > 0 — the checks need the sizes) and writes the
  *                         table's host image (3 x nseg uint64). The caller uploads it once and
  *                         reuses it while the tensors stay where they are: the *_table entries
  *                         below then cost no per-tensor host work per call.
@@ -275,7 +275,10 @@ int edt_slerp_merge_speculative(const void* v0, const void* v1, int in_dt, void*
  *                         nullable) restricts it to segments with redo[s] != 0
  *   edt_slerp_merge_list / _list_speculative   the same from host pointer arrays: the table is
  *                         validated and copied into `workspace` (24 bytes per segment, device,
- *                         8-byte aligned) by a stream-ordered copy on every call. */
+ *                         8-byte aligned) by a stream-ordered copy on every call. edt_slerp_merge_list
+ *                         takes no sizes, so its in-place rule (an output exactly its own parent
+ *                         or apart from every other tensor) is the caller's to keep; the
+ *                         speculative form checks its rule over seg_numel. */
 int edt_slerp_seg_table(const void* const* v0_t, const void* const* v1_t, void* const* out_t, int nseg,
                         const uint64_t* seg_numel, int in_dt, int out_dt, int apart, uint64_t* table_host);
 int edt_slerp_stats_table(const uint64_t* seg_table, int in_dt, const uint64_t* chunk_desc, int64_t nchunks,

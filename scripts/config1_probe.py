@@ -80,9 +80,9 @@ def measure(tag, lib, P, dev, draws, spacer_bytes=3 << 30):
         mom2, rep = place_momentum(theta, workers, mom, 8)
         placed = event_ms(stepper(lib, theta, workers, mom2))
         algo = 48 * P
-        print(json.dumps({"case": tag, "draw": d, "P": P, "ms": round(ms, 4), "frac": round(algo / ms / 1e9 / 8000, 4),
+        print(json.dumps({"case": tag, "draw": d, "P": P, "ms": round(ms, 4), "frac": round(algo / ms / 1e6 / 8000, 4),
                           "stream_ceiling_ms": round(ceil, 4), "ms_over_ceiling": round(ms / ceil, 4),
-                          "placed_ms": round(placed, 4), "placed_frac": round(algo / placed / 1e9 / 8000, 4),
+                          "placed_ms": round(placed, 4), "placed_frac": round(algo / placed / 1e6 / 8000, 4),
                           "placement": rep, "theta_addr_gib": round(theta.data_ptr() / 2**30, 3),
                           "mom_addr_gib": round(mom.data_ptr() / 2**30, 3)}), flush=True)
         held.append((theta, workers, mom, mom2))
@@ -90,11 +90,43 @@ def measure(tag, lib, P, dev, draws, spacer_bytes=3 << 30):
     torch.cuda.empty_cache()
 
 
+def joint(P, dev, draws=3, nth=4, nmom=6, nwork=3, spacer_bytes=3 << 29):
+    """Which operand's placement sets the time: per draw, the stream-ceiling probe over a grid of
+    theta x momentum candidates, and the best pair again with re-drawn worker sets."""
+    for d in range(draws):
+        held = [torch.empty((d + 1) * (5 << 30), dtype=torch.uint8, device=dev)]
+        theta, workers, mom = make_set(P, dev, 300 + d)
+        ths, moms = [theta], [mom]
+        for c in range(1, nth):
+            held.append(torch.empty(c * spacer_bytes, dtype=torch.uint8, device=dev))
+            ths.append(theta.clone())
+        for c in range(1, nmom):
+            held.append(torch.empty(c * spacer_bytes, dtype=torch.uint8, device=dev))
+            moms.append(mom.clone())
+        grid = [[round(probe_ms(t, workers, m, iters=5), 4) for m in moms] for t in ths]
+        bi, bj = min(((i, j) for i in range(nth) for j in range(nmom)), key=lambda ij: grid[ij[0]][ij[1]])
+        wsets = [round(grid[bi][bj], 4)]
+        for c in range(1, nwork):
+            held.append(torch.empty(c * (spacer_bytes << 2), dtype=torch.uint8, device=dev))
+            w2 = [w.clone() for w in workers]
+            wsets.append(round(probe_ms(ths[bi], w2, moms[bj], iters=5), 4))
+            held.append(w2)
+        print(json.dumps({"case": "joint", "draw": d, "P": P, "theta_x_momentum_ms": grid,
+                          "first_ms": grid[0][0], "momentum_only_best_ms": min(grid[0]),
+                          "theta_only_best_ms": min(r[0] for r in grid), "joint_best_ms": grid[bi][bj],
+                          "best_pair_with_redrawn_workers_ms": wsets}), flush=True)
+        del held, theta, workers, mom, ths, moms
+        torch.cuda.empty_cache()
+
+
 def main():
     dev = torch.device("cuda:0")
     P = gpt2_small().total
     lib = L.lib()
     draws = int(os.environ.get("DRAWS", "5"))
+    if os.environ.get("JOINT_ONLY") == "1":
+        joint(P, dev)
+        return
     measure("fresh", lib, P, dev, draws)
     # the bench's history: the 1.3B population allocated, stepped and freed before the 125M set
     P13 = gpt_1p3b().total
@@ -115,7 +147,7 @@ def main():
             for n in names:
                 times[n].append(event_ms(stepper(libs[n], theta, workers, mom), 10, 1))
         print(json.dumps({"case": "grid", "P": P, "median_ms": {n: round(statistics.median(v), 4) for n, v in times.items()},
-                          "frac": {n: round(48 * P / statistics.median(v) / 1e9 / 8000, 4) for n, v in times.items()}}),
+                          "frac": {n: round(48 * P / statistics.median(v) / 1e6 / 8000, 4) for n, v in times.items()}}),
               flush=True)
 
 

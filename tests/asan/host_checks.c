@@ -217,7 +217,7 @@ static void sync_host_paths(void) {
     EXPECT_FAIL(edt_slerp_seg_table(v0s, v1s, partial, 2, n2, 0, 0, 0, host));
     void* same[2] = {dummy + 256, dummy + 256};               /* two outputs on one buffer */
     EXPECT_FAIL(edt_slerp_seg_table(v0s, v1s, same, 2, n2, 0, 0, 0, host));
-    EXPECT(edt_slerp_seg_table(v0s, v1s, other, 2, NULL, 0, 0, 0, host) == 0);   /* no sizes: caller's duty */
+    EXPECT_FAIL(edt_slerp_seg_table(v0s, v1s, other, 2, NULL, 0, 0, 0, host));   /* r6: sizes required */
 }
 
 static void comm_host_paths(void) {
