@@ -704,7 +704,7 @@ def sharded_parity(args, comm, rt, kernels, mode, broadcast, k_local, tdt, wdt, 
 
 def population_parity(lay, rt, comm, kernels, member_seed, pairs, t, child) -> dict | None:
     """Child 0 of the sharded population (on rank 0 after the timed runs) against the whole-
-    population passes on rank 0 alone (Gram sums -> coefficients -> blend over its two parents,
+    population passes on rank 0 alone (needed sums -> coefficients -> blend over its two parents,
     regenerated from their seeds): bit-identical to edt_slerp_merge by construction,
     so any byte an exchange moved wrong shows. Rank 0 only."""
     if comm.rank != 0:
@@ -721,15 +721,18 @@ def population_parity(lay, rt, comm, kernels, member_seed, pairs, t, child) -> d
         mem.append(x)
     idx = {m: q for q, m in enumerate(sorted({i, j}))}
     plan = k.make_slerp_plan(lay.offsets, dev)
-    gram = k.slerp_gram(mem, plan.chunks, plan.nchunks)
-    coef, _ = k.slerp_gram_coef(plan, gram, len(mem), [(idx[i], idx[j])], t)
+    pair = [(idx[i], idx[j])]
+    layout = k.needed_table(pair, len(mem), plan.nchunks)
+    table = torch.zeros(max(1, layout.doubles), dtype=torch.float64, device=dev)
+    k.slerp_needed_sums(mem, layout, plan.chunks, plan.nchunks, table, 0)
+    coef, _ = k.slerp_needed_coef(plan, table, layout, t)
     want = torch.empty(P, dtype=bf, device=dev)
-    k.slerp_blend_children(mem, [(idx[i], idx[j])], [want], plan.chunks, plan.nchunks, coef, plan.nseg)
+    k.slerp_blend_children(mem, pair, [want], plan.chunks, plan.nchunks, coef, plan.nseg)
     rt.sync()
     rec = {"child": 0, "parents": [i, j], "bit_exact": bool(torch.equal(want.view(torch.int16), child.view(torch.int16))),
            "max_ulp": _max_ulp(want, child),
-           "reference": "the whole-population Gram / coefficient / blend passes on rank 0 (== edt_slerp_merge)"}
-    del mem, want, gram
+           "reference": "the whole-population needed-sums / coefficient / blend passes on rank 0 (== edt_slerp_merge)"}
+    del mem, want, table
     rt.empty_cache()
     return rec
 
@@ -1272,7 +1275,7 @@ def bench_population(args, rt, comm, kernels=None, layout_name="qwen2p5_7b_body"
         if "sums_table" not in res:
             tab = (kernels or sp.kernels).needed_table(pairs, world, sp.plan.nchunks)
             res["sums_table"] = {"sums_per_chunk": sum(nt for _, nt in tab.blocks), "blocks": len(tab.blocks),
-                                 "triangle_sums_per_chunk": world * (world + 1) // 2,
+                                 "triangle_sums_per_chunk": world * (world + 1) // 2,   # every pair's dot
                                  "gathered_bytes_per_rank": tab.doubles * 8 * (world - 1) // world}
         res[key] = {"ms": round(ms, 3), "groups": groups, "wire_bytes_per_rank": wire,
                     "xgmi_floor_ms": xgmi_floor_ms(wire, world),

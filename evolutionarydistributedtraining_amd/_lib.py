@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(PKG_DIR, "libedt_sync.so")
 EDT_F32 = 0
 EDT_BF16 = 1
 EDT_MAX_WORKERS = 64
-EDT_ABI_VERSION = 5         # include/edt_sync.h: the revision these signatures and workspace sizes follow
+EDT_ABI_VERSION = 6         # include/edt_sync.h: the revision these signatures and workspace sizes follow
 
 _DT = {torch.float32: EDT_F32, torch.bfloat16: EDT_BF16}
 
@@ -93,8 +93,6 @@ SIGNATURES = [
                                    ctypes.c_int64, ctypes.c_int64, _P, _P, _U64, _P]),
     ("edt_slerp_needed_coef", _I, [_P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int32), _I, _I, _P, _I, _P, _D, _D,
                                    _P, _P, _P]),
-    ("edt_slerp_gram", _I, [ctypes.POINTER(_P), _I, _I, _P, ctypes.c_int64, _P, _P]),
-    ("edt_slerp_gram_coef", _I, [_P, _I, ctypes.POINTER(ctypes.c_int32), _I, _P, _I, _P, _D, _D, _P, _P, _P]),
     ("edt_slerp_blend_children", _I, [ctypes.POINTER(_P), _I, _I, ctypes.POINTER(ctypes.c_int32), _I,
                                       ctypes.POINTER(_P), _I, _P, ctypes.c_int64, _P, _I, _P]),
     ("edt_probe_stream", _I, [_P, _I, ctypes.POINTER(_P), _I, _I, _P, _U64, _P]),

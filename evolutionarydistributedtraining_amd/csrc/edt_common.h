@@ -86,13 +86,10 @@ using edt::g_err;
 // through LDS into one level-2 row per workgroup (a quarter of the row bytes, one barrier); 0 = a
 // level-0 row per wave, no barrier. 7B lineage merge, one box, interleaved (profiles/
 // r03_spec_wg_rows.jsonl): 7.01-7.03 ms against 7.14-7.17, lerp 6.96.
-// Gram pass: 1 = the next tile's member loads issued before this tile's sums (two register sets)
-// (8 x 7B two-pass generation, one box, interleaved: 57.2 / 57.3 ms with both against 58.0 / 58.3
-// with neither; prefetch alone 57.6 / 57.8, nt alone 57.7 / 57.9 — r4, profiles/r04_gram_variants.json)
-#ifndef EDT_GRAM_PREFETCH
-#define EDT_GRAM_PREFETCH 1
-#endif
-#ifndef EDT_GRAM_NT             // Gram pass: non-temporal member loads (each member is read once)
+// Population stats passes (the needed / triangle sums, edt_slerp.hip): non-temporal member loads
+// (each member is read once; r4, 8 x 7B two-pass generation: nt alone 57.7 / 57.9 ms against 58.0
+// / 58.3 without, profiles/r04_gram_variants.json)
+#ifndef EDT_GRAM_NT
 #define EDT_GRAM_NT 1
 #endif
 // Needed-sums pass (r5, edt_slerp.hip): elements converted to fp64 per group before the dot
@@ -105,9 +102,6 @@ using edt::g_err;
 #endif
 #ifndef EDT_NEED_GLDS           // needed-sums pass: the next tile staged in LDS by DMA (bf16 members)
 #define EDT_NEED_GLDS 1
-#endif
-#ifndef EDT_GRAM_MIN_BLOCKS     // Gram pass: __launch_bounds__ minimum workgroups per CU (waves per SIMD)
-#define EDT_GRAM_MIN_BLOCKS 1
 #endif
 #ifndef EDT_SLERP_SPEC_WG_ROWS
 #define EDT_SLERP_SPEC_WG_ROWS 1

@@ -697,12 +697,12 @@ __global__ __launch_bounds__(kBlock) void slerp_blend_tile_kernel(const void* __
 
 // ---------------------------------------------------------------------------------------
 // SLERP for a resident population (EDT_RL/edt.py:286-299 merges every selected pair of one
-// generation): ONE pass over the M <= 8 members per chunk forms every member's squared norm and
-// every pair's dot — the upper triangle of the Gram matrix, M(M+1)/2 fp64 sums per chunk — where
-// per-child stats passes would read each child's two parents. A child's (|vi|^2, |vj|^2, vi.vj)
-// are then read out of it. Every sum is bit-identical to pair_slot() on (vi, vj): the same wave
-// slots, the same per-lane FMA sequence in element order (an FMA's product is exact, so vi*vj ==
-// vj*vi), the same butterfly and slot reduction; the coefficients therefore equal edt_slerp_merge's.
+// generation): ONE pass over the M <= 8 members per chunk forms the squared norms and the dots the
+// children need (slerp_need_kernel below) where per-child stats passes would read each child's two
+// parents. A child's (|vi|^2, |vj|^2, vi.vj) are then read out of its component's sums. Every sum
+// is bit-identical to pair_slot() on (vi, vj): the same per-lane FMA sequence in element order (an
+// FMA's product is exact, so vi*vj == vj*vi), the same butterfly and tree; the coefficients
+// therefore equal edt_slerp_merge's.
 
 constexpr int kGramMaxMembers = 8;
 struct Members {
@@ -711,22 +711,6 @@ struct Members {
 
 __host__ __device__ constexpr int tri_index(int a, int b, int M) {   // a <= b < M
     return a * M - a * (a - 1) / 2 + (b - a);
-}
-
-template <int M, int N, typename X>
-__device__ __forceinline__ void gram_fma(const X (&x)[M], double (&g)[M * (M + 1) / 2]) {
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-#pragma unroll
-        for (int a = 0; a < M; ++a) {
-            const double da = x[a][j];
-#pragma unroll
-            for (int b = a; b < M; ++b) {
-                const double db = x[b][j];
-                g[tri_index(a, b, M)] = __builtin_fma(da, db, g[tri_index(a, b, M)]);
-            }
-        }
-    }
 }
 
 template <int M, int N>
@@ -744,190 +728,6 @@ __device__ __forceinline__ uint64_t uniform_u64(uint64_t x) {
            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
 }
 
-// The first element's products start each lane's chains: fma(x, y, +0.0) (the canonical chain's
-// first step from 0.0, one VOP3 FMA with an inline zero instead of a zero move + accumulate).
-template <int M, int N, typename X>
-__device__ __forceinline__ void gram_fma_first(const X (&x)[M], double (&g)[M * (M + 1) / 2]) {
-#pragma unroll
-    for (int a = 0; a < M; ++a) {
-        const double da = x[a][0];
-#pragma unroll
-        for (int b = a; b < M; ++b) g[tri_index(a, b, M)] = __builtin_fma(da, (double)x[b][0], 0.0);
-    }
-#pragma unroll
-    for (int j = 1; j < N; ++j) {
-#pragma unroll
-        for (int a = 0; a < M; ++a) {
-            const double da = x[a][j];
-#pragma unroll
-            for (int b = a; b < M; ++b) {
-                const double db = x[b][j];
-                g[tri_index(a, b, M)] = __builtin_fma(da, db, g[tri_index(a, b, M)]);
-            }
-        }
-    }
-}
-
-// Gram rows (level 4), one workgroup per unit of 16 tiles in address order: wave w takes tiles
-// 16 g + 4 w .. + 3 one after the other (one vector per member per lane: M loads in flight). Each
-// tile's NT sums go through the xor butterfly in two parts: the swap levels (32, 16) on the VALU,
-// transposed (tile_swap_levels), then the row levels (8 .. 1) SERIALLY — every lane parks its
-// level-16 partials in LDS and lane q reads value q's 16 partials and adds them in the butterfly's
-// own pairing (row_tree16): NT serial 15-add trees on NT lanes at once instead of NT / 4 values x 4
-// DPP levels on all lanes plus the per-slot stores, with bit-identical sums (r4: the M = 8 pass was
-// VALU-bound at ~970 instructions per tile-wave). Lane q keeps its tile sums as the tree's level-2
-// node over the wave's 4 tiles; the 4 waves' nodes meet in LDS, wave 0 stores the unit's row
-// (unit_slot). Every sum is bit-identical to pair_slot() on (vi, vj): the same per-lane FMA
-// sequence in element order (an FMA's product is exact, so vi*vj == vj*vi), the same butterfly and
-// tree; the coefficients therefore equal edt_slerp_merge's.
-template <int IDT, int M>
-__global__ __launch_bounds__(kBlock, EDT_GRAM_MIN_BLOCKS) void slerp_gram_kernel(Members mem, const uint64_t* chunks,
-                                                                                 int64_t nchunks, double* rows,
-                                                                                 uint64_t u0) {
-    constexpr int NT = M * (M + 1) / 2, N2 = Red<NT>::N2;
-    constexpr int upc = kTileSlots / 16;
-    // [wave][row][slot][position in row], 17 doubles per (row, slot): lane q's 16 reads start
-    // 2 banks apart from lane q + 1's instead of all on one bank
-    constexpr int kPad = 17;
-    __shared__ double part[kWavesPerBlock][4 * N2 * kPad];
-    __shared__ double ts2[kWavesPerBlock][NT];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint64_t units = (uint64_t)nchunks * upc;
-    const uint64_t u = u0 + blockIdx.x;
-    if (u >= units) return;
-    const uint64_t c = u / upc;
-    const int g = (int)(u % upc);
-    // the chunk bounds are uniform: in scalar registers, so the full-tile test below is a scalar branch
-    const uint64_t start = uniform_u64(chunks[3 * c]), len = uniform_u64(chunks[3 * c + 1]);
-    // lane q (< NT) reads value q's partials: the row and slot that hold it after the swap levels
-    int pos = 0;
-#pragma unroll
-    for (int row = 0; row < 4; ++row)
-#pragma unroll
-        for (int sl = 0; sl < N2; ++sl) {
-            bool owner;
-            if (red_index<NT>(sl, row * 16, owner) == lane) pos = row * N2 + sl;
-        }
-    const double* mine = &part[wave][pos * kPad];
-    double* put = &part[wave][(lane >> 4) * N2 * kPad + (lane & 15)];
-    const uint64_t end = start + len;
-    const uint64_t a = (start + kVec - 1) / kVec * kVec, b = end / kVec * kVec;
-    double n01 = 0.0, n23 = 0.0;                       // lane q: the tree's nodes over tiles k = 0-1, 2-3
-    // one tile: its sums' lane chains (FULL: the whole tile inside the chunk's aligned body, so no
-    // lane test and no zero start), the swap levels, the LDS round trip, the row tree on lane q
-    auto load_tile = [&](int k, Raw8<IDT> (&x)[M]) {
-        const uint64_t i = a + (uint64_t)(16 * g + 4 * wave + k) * kTileElems + (uint64_t)lane * kVec;
-#pragma unroll
-        for (int m = 0; m < M; ++m) x[m] = ld_raw<IDT, EDT_GRAM_NT != 0>(mem.p[m], i);
-    };
-    auto tile = [&](int k, auto full, const Raw8<IDT> (&xin)[M]) {
-        const int j = 16 * g + 4 * wave + k;
-        double gs[NT];
-        const uint64_t i = a + (uint64_t)j * kTileElems + (uint64_t)lane * kVec;
-        if constexpr (decltype(full)::value) {
-            if constexpr (EDT_GRAM_PREFETCH) {
-                gram_fma_first<M, kVec>(xin, gs);      // loaded one tile ahead
-            } else {
-                Raw8<IDT> x[M];
-                load_tile(k, x);
-                gram_fma_first<M, kVec>(x, gs);
-            }
-        } else {
-#pragma unroll
-            for (int q = 0; q < NT; ++q) gs[q] = 0.0;
-            if (a < b && i < b) {
-                Raw8<IDT> x[M];
-#pragma unroll
-                for (int m = 0; m < M; ++m) x[m] = ld_raw<IDT, false>(mem.p[m], i);
-                gram_fma<M, kVec>(x, gs);
-            }
-        }
-        if (j == 0)
-            tile0_edge(start, len, [&](uint64_t e) {
-                Raw1 x[M];
-#pragma unroll
-                for (int m = 0; m < M; ++m) ld<IDT, 1>(mem.p[m], e, x[m].v);
-                gram_fma<M, 1>(x, gs);
-            });
-        double r[N2];
-        tile_swap_levels<NT>(gs, r);
-#pragma unroll
-        for (int sl = 0; sl < N2; ++sl) put[sl * kPad] = r[sl];
-        // the wave's own LDS round trip: its stores complete before its loads (in-order per wave);
-        // the fences keep the compiler from moving the loads above the stores
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        double p[16];
-#pragma unroll
-        for (int t = 0; t < 16; ++t) p[t] = mine[t];
-        const double tsum = row_tree16(p);
-        if (k == 0) n01 = tsum;
-        else if (k == 1) n01 = n01 + tsum;
-        else if (k == 2) n23 = tsum;
-        else n23 = n23 + tsum;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");    // this tile's reads before the next stores
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    };
-    // uniform: every tile of the unit inside the aligned body (all but a segment's last unit)
-    Raw8<IDT> x0[M];
-    if (a + (uint64_t)(16 * g + 16) * kTileElems <= b) {
-        if constexpr (EDT_GRAM_PREFETCH) {             // two register sets: tile k + 1's loads in flight
-            Raw8<IDT> x1[M];                           // while tile k is summed (sched_barrier: the
-            load_tile(0, x0);                          // scheduler may not sink them to their use)
-            load_tile(1, x1);
-            __builtin_amdgcn_sched_barrier(0);
-            tile(0, std::true_type{}, x0);
-            __builtin_amdgcn_sched_barrier(0);
-            load_tile(2, x0);
-            __builtin_amdgcn_sched_barrier(0);
-            tile(1, std::true_type{}, x1);
-            __builtin_amdgcn_sched_barrier(0);
-            load_tile(3, x1);
-            __builtin_amdgcn_sched_barrier(0);
-            tile(2, std::true_type{}, x0);
-            tile(3, std::true_type{}, x1);
-        } else {
-#pragma unroll(M <= 2 ? 4 : 1)
-            for (int k = 0; k < 4; ++k) tile(k, std::true_type{}, x0);
-        }
-    } else {
-#pragma unroll(M <= 2 ? 4 : 1)
-        for (int k = 0; k < 4; ++k) tile(k, std::false_type{}, x0);
-    }
-    if (lane < NT) ts2[wave][lane] = n01 + n23;        // level 2: the wave's 4 tiles
-    __syncthreads();
-    if (wave == 0 && lane < NT)
-        rows[unit_slot(u, units) * NT + lane] = (ts2[0][lane] + ts2[1][lane]) + (ts2[2][lane] + ts2[3][lane]);
-}
-
-// host: the Gram sums of D compact members into gram (chunk rows [nchunks][NT]); `rows`: the
-// level-4 row scratch (default: right after the chunk rows).
-inline int gram_sums(const Members& mem, int D, int in_dt, const uint64_t* chunk_desc, int64_t nchunks, double* gram,
-                     hipStream_t s, double* rows = nullptr) {
-    const int NT = D * (D + 1) / 2;
-    if (!rows) rows = gram + (uint64_t)nchunks * NT;
-    constexpr int upc = kTileSlots / 16;
-    const uint64_t units = (uint64_t)nchunks * upc;
-    for (uint64_t u0 = 0; u0 < units; u0 += kUnitGridCap) {
-        const unsigned g = unit_grid(units - u0);
-#define EDT_GM(M)                                                                                      \
-    case M:                                                                                            \
-        if (in_dt == EDT_F32) slerp_gram_kernel<EDT_F32, M><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0); \
-        else slerp_gram_kernel<EDT_BF16, M><<<g, kBlock, 0, s>>>(mem, chunk_desc, nchunks, rows, u0);              \
-        break;
-        switch (D) {
-            EDT_GM(1) EDT_GM(2) EDT_GM(3) EDT_GM(4) EDT_GM(5) EDT_GM(6) EDT_GM(7) EDT_GM(8)
-            default: return fail(EDT_ERR_ARG, "Gram pass over %d members", D);
-        }
-#undef EDT_GM
-        int rc = check_launch("slerp_gram_kernel");
-        if (rc) return rc;
-    }
-    return launch_tree_reduce(rows, NT, kGramRows, upc, 1, nchunks, gram, s);
-}
-
 // ---- the needed-sums layout (r5): any pair graph --------------------------------------------------
 // A generation needs each distinct parent's norm and each distinct dot its children use — at most
 // D + 8 sums for 8 children, against the triangle's D(D+1)/2 (36 at D = 8). EDT_RL's roulette
@@ -943,15 +743,23 @@ inline int gram_sums(const Members& mem, int D, int in_dt, const uint64_t* chunk
 // [D, D + NR) = ring dot c, [D + NR, NT) = chord e. Same per-lane chains in element order, same
 // butterfly and tree as every other form: each sum is bit-identical to pair_slot() on its two
 // members, so every child's coefficients are edt_slerp_merge's.
+//
+// r6: a component whose dots do not fit the ring + chord slots (dense graphs: K5 and up, a hub in
+// more than the slots' pairs) takes the TRIANGLE layout of the same pass (TRI): the upper triangle
+// of its Gram matrix, D(D+1)/2 sums at tri_index(a, b, D) in compact member order, each dot formed
+// only when a child needs it (a uniform mask; its operands are registers named at compile time, so
+// no switch) and the norms always. It replaced the separate Gram kernel (slerp_gram_kernel and its
+// edt_slerp_gram / _gram_coef entries): one stats kernel for every pair graph, the same canonical
+// per-chunk order, the same rows.
 constexpr int kNeedChords = 4;                // chord dot slots (D >= 5)
 constexpr int kNeedChordEmits = 8;            // children on chords (distinct ordered pairs)
 constexpr int kNeedMaxOut = 16;               // duplicate children per component
 
-template <int D>
+template <int D, bool TRI = false>
 struct NeedLayout {
     static constexpr int NR = D >= 3 ? D : D - 1;                           // ring dots
     static constexpr int NC = D <= 3 ? 0 : D == 4 ? 2 : kNeedChords;        // chord slots
-    static constexpr int NT = D + NR + NC;
+    static constexpr int NT = TRI ? D * (D + 1) / 2 : D + NR + NC;
 };
 inline int need_nr(int D) { return D >= 3 ? D : D - 1; }
 inline int need_nc(int D) { return D <= 3 ? 0 : D == 4 ? 2 : kNeedChords; }
@@ -974,6 +782,7 @@ struct NeedSpec {
     void* xout[kNeedMaxOut];
     const double* t;                          // per segment
     int32_t* zero_word;                       // the any-redo word, zeroed by block 0 of the first launch
+    uint64_t tri;                             // TRI layout: bit tri_index(a, b, D) = dot (a, b) formed
 };
 
 // acc += the dot of members (code / 8, code % 8) over N elements: one switch arm per pair, the
@@ -1005,10 +814,10 @@ __device__ __forceinline__ void need_dot(const double (&d)[D][N], int code, doub
 
 // The sums of N elements of every member (the lane's vector: N = 8; its head / tail element:
 // N = 1), continuing each chain: the members' fp64 values per group of EDT_NEED_GROUP elements,
-// the norms, the ring dots in use, the chords.
-template <int D, int N, typename X>
-__device__ __forceinline__ void need_fma(const X (&x)[D], const NeedSpec& S, double (&g)[NeedLayout<D>::NT]) {
-    constexpr int NR = NeedLayout<D>::NR, NC = NeedLayout<D>::NC;
+// the norms, the ring dots in use, the chords (TRI: the norms and the masked triangle dots).
+template <int D, int N, bool TRI = false, typename X>
+__device__ __forceinline__ void need_fma(const X (&x)[D], const NeedSpec& S, double (&g)[NeedLayout<D, TRI>::NT]) {
+    constexpr int NR = NeedLayout<D, TRI>::NR, NC = NeedLayout<D, TRI>::NC;
     constexpr int H = N < EDT_NEED_GROUP ? N : EDT_NEED_GROUP;
 #pragma unroll
     for (int h = 0; h < N / H; ++h) {
@@ -1017,19 +826,31 @@ __device__ __forceinline__ void need_fma(const X (&x)[D], const NeedSpec& S, dou
         for (int m = 0; m < D; ++m)
 #pragma unroll
             for (int j = 0; j < H; ++j) d[m][j] = x[m][H * h + j];
+        if constexpr (TRI) {                      // the norms, and the dots the mask names
 #pragma unroll
-        for (int m = 0; m < D; ++m)
+            for (int u = 0; u < D; ++u)
 #pragma unroll
-            for (int j = 0; j < H; ++j) g[m] = __builtin_fma(d[m][j], d[m][j], g[m]);
+                for (int v = u; v < D; ++v)
+                    if (u == v || ((S.tri >> tri_index(u, v, D)) & 1u)) {
 #pragma unroll
-        for (int c = 0; c < NR; ++c)
-            if ((S.ring >> c) & 1u) {
+                        for (int j = 0; j < H; ++j)
+                            g[tri_index(u, v, D)] = __builtin_fma(d[u][j], d[v][j], g[tri_index(u, v, D)]);
+                    }
+        } else {
 #pragma unroll
-                for (int j = 0; j < H; ++j) g[D + c] = __builtin_fma(d[c][j], d[(c + 1) % D][j], g[D + c]);
-            }
+            for (int m = 0; m < D; ++m)
 #pragma unroll
-        for (int e = 0; e < NC; ++e)
-            if (e < S.nchord) need_dot<D, H>(d, S.code[e], g[D + NR + e]);
+                for (int j = 0; j < H; ++j) g[m] = __builtin_fma(d[m][j], d[m][j], g[m]);
+#pragma unroll
+            for (int c = 0; c < NR; ++c)
+                if ((S.ring >> c) & 1u) {
+#pragma unroll
+                    for (int j = 0; j < H; ++j) g[D + c] = __builtin_fma(d[c][j], d[(c + 1) % D][j], g[D + c]);
+                }
+#pragma unroll
+            for (int e = 0; e < NC; ++e)
+                if (e < S.nchord) need_dot<D, H>(d, S.code[e], g[D + NR + e]);
+        }
     }
 }
 
@@ -1160,17 +981,19 @@ __device__ __forceinline__ void need_emit(const X (&x)[D], const NeedSpec& S, ui
 // which leave every chain's bits unchanged). bf16 members: the next tiles land in LDS by DMA while
 // this tile is summed from registers (below; a two-register-set prefetch measured slower: its
 // VGPRs cost a wave per SIMD).
-template <int IDT, int D, bool EMIT = false, int ODT = EDT_BF16>
+template <int IDT, int D, bool EMIT = false, int ODT = EDT_BF16, bool TRI = false>
 __global__ __launch_bounds__(kBlock, EDT_NEED_MIN_WAVES) void slerp_need_kernel(Members mem, NeedSpec S,
                                                                                  const uint64_t* chunks,
                                                                                  int64_t nchunks, double* rows,
                                                                                  uint64_t u0) {
-    constexpr int NT = NeedLayout<D>::NT, N2 = Red<NT>::N2;
+    static_assert(!(EMIT && TRI), "the triangle layout is a stats pass only");
+    constexpr int NT = NeedLayout<D, TRI>::NT, N2 = Red<NT>::N2;
     constexpr bool kGlds = EDT_NEED_GLDS != 0 && IDT == EDT_BF16;
     // LDS-DMA stages per wave: two (two tiles in flight besides the one in registers) where the
     // registers already limit the pass to 2 waves per SIMD (the emitting form, D = 8), else one
-    // (3 waves per SIMD fit the LDS with one stage, not with two)
-    constexpr int kStages = kGlds ? (EMIT || D == 8 ? 2 : 1) : 1;
+    // (3 waves per SIMD fit the LDS with one stage, not with two; the triangle's larger partials
+    // table leaves room for one)
+    constexpr int kStages = kGlds ? ((EMIT || D == 8) && !TRI ? 2 : 1) : 1;
     __shared__ u32x4 stage[kStages][kGlds ? kWavesPerBlock : 1][kGlds ? D : 1][64];
     if constexpr (EMIT)
         if (S.zero_word && u0 == 0 && blockIdx.x == 0 && threadIdx.x == 0) *S.zero_word = 0;
@@ -1233,13 +1056,13 @@ __global__ __launch_bounds__(kBlock, EDT_NEED_MIN_WAVES) void slerp_need_kernel(
         if constexpr (EMIT)               // first: the members' registers are all it needs
             if (a < b && i < b) need_emit<ODT, D, kVec>(x, S, a + (uint64_t)j * kTileElems, (uint32_t)lane, l0, l1);
         mid();
-        need_fma<D, kVec>(x, S, gs);
+        need_fma<D, kVec, TRI>(x, S, gs);
         if (j == 0)
             tile0_edge(start, len, [&](uint64_t e) {
                 Raw1 y[D];
 #pragma unroll
                 for (int m = 0; m < D; ++m) y[m].v[0] = ld1_g<IDT>(member_base(m, start) + (uint32_t)(e - start) * esz);
-                need_fma<D, 1>(y, S, gs);
+                need_fma<D, 1, TRI>(y, S, gs);
                 if constexpr (EMIT) need_emit<ODT, D, 1>(y, S, e, 0, l0, l1);
             });
         double r[N2];
@@ -1321,9 +1144,11 @@ __global__ __launch_bounds__(kBlock, EDT_NEED_MIN_WAVES) void slerp_need_kernel(
 // ([nchunks][need_nt(D)]; `rows`: the level-4 row scratch, nchunks x 8 x need_nt(D) doubles);
 // emit: also every child's lerp-branch output (S.out, S.t, S.zero_word).
 inline int need_sums(const Members& mem, int D, const NeedSpec& S, int in_dt, int out_dt, bool emit,
-                     const uint64_t* chunk_desc, int64_t nchunks, double* sums, double* rows, hipStream_t s) {
+                     const uint64_t* chunk_desc, int64_t nchunks, double* sums, double* rows, hipStream_t s,
+                     bool tri = false) {
     if (D < 1 || D > kGramMaxMembers) return fail(EDT_ERR_ARG, "needed-sums pass over %d members", D);
-    if (S.nchord < 0 || S.nchord > need_nc(D)) return fail(EDT_ERR_ARG, "%d chords over %d members", S.nchord, D);
+    if (tri && emit) return fail(EDT_ERR_ARG, "the triangle layout is a stats pass only");
+    if (!tri && (S.nchord < 0 || S.nchord > need_nc(D))) return fail(EDT_ERR_ARG, "%d chords over %d members", S.nchord, D);
     if (S.nemit < 0 || S.nemit > kNeedChordEmits || S.nextra < 0 || S.nextra > kNeedMaxOut)
         return fail(EDT_ERR_ARG, "bad emit table");
     constexpr int upc = kTileSlots / 16;
@@ -1332,7 +1157,10 @@ inline int need_sums(const Members& mem, int D, const NeedSpec& S, int in_dt, in
         const unsigned g = unit_grid(units - u0);
 #define EDT_NK(M)                                                                                          \
     case M:                                                                                                \
-        if (!emit) {                                                                                       \
+        if (tri) {                                                                                         \
+            if (in_dt == EDT_F32) slerp_need_kernel<EDT_F32, M, false, EDT_BF16, true><<<g, kBlock, 0, s>>>(mem, S, chunk_desc, nchunks, rows, u0); \
+            else slerp_need_kernel<EDT_BF16, M, false, EDT_BF16, true><<<g, kBlock, 0, s>>>(mem, S, chunk_desc, nchunks, rows, u0); \
+        } else if (!emit) {                                                                                \
             if (in_dt == EDT_F32) slerp_need_kernel<EDT_F32, M><<<g, kBlock, 0, s>>>(mem, S, chunk_desc, nchunks, rows, u0); \
             else slerp_need_kernel<EDT_BF16, M><<<g, kBlock, 0, s>>>(mem, S, chunk_desc, nchunks, rows, u0);    \
         } else if (in_dt == EDT_F32 && out_dt == EDT_F32) {                                                \
@@ -1353,7 +1181,7 @@ inline int need_sums(const Members& mem, int D, const NeedSpec& S, int in_dt, in
         int rc = check_launch(emit ? "slerp_need_kernel (speculative)" : "slerp_need_kernel");
         if (rc) return rc;
     }
-    return launch_tree_reduce(rows, need_nt(D), kGramRows, upc, 1, nchunks, sums, s);
+    return launch_tree_reduce(rows, tri ? D * (D + 1) / 2 : need_nt(D), kGramRows, upc, 1, nchunks, sums, s);
 }
 
 // How edt_slerp_population lays out its sums: the distinct parents split into the connected
@@ -1490,6 +1318,15 @@ inline void plan_gram(int D, const int* a, const int* b, int npairs, int64_t nch
         }
         S.code[S.nchord++] = p1 * 8 + p2;
     }
+    // the triangle components' masks: the dots their children use, at compact positions
+    for (int q = 0; q < npairs; ++q) {
+        if (a[q] == b[q]) continue;
+        const int k = G.comp_of[a[q]];
+        if (G.kind[k] != kTri) continue;
+        int p1 = G.pos[a[q]], p2 = G.pos[b[q]];
+        if (p1 > p2) { const int t = p1; p1 = p2; p2 = t; }
+        G.need[k].tri |= 1ull << tri_index(p1, p2, G.size[k]);
+    }
     uint64_t off = 0;
     for (int k = 0; k < G.ncomp; ++k) {
         G.off[k] = off;
@@ -1514,9 +1351,8 @@ inline int plan_component_sums(const GramPlan& G, int k, const void* const* dm, 
     Members gm;
     memset(&gm, 0, sizeof(gm));
     for (int x = 0; x < G.size[k]; ++x) gm.p[x] = dm[G.list[k][x]];
-    if (G.kind[k] == kNeed)
-        return need_sums(gm, G.size[k], G.need[k], in_dt, EDT_F32, false, chunk_desc, nchunks, gram + G.off[k], rows, s);
-    return gram_sums(gm, G.size[k], in_dt, chunk_desc, nchunks, gram + G.off[k], s, rows);
+    return need_sums(gm, G.size[k], G.need[k], in_dt, EDT_F32, false, chunk_desc, nchunks, gram + G.off[k], rows, s,
+                     G.kind[k] == kTri);
 }
 
 // The blends of every child in one launch, with pair_population_kernel's placement: the
@@ -2280,53 +2116,10 @@ int edt_slerp_population(const void* const* members, int nmembers, int in_dt, co
     return EDT_OK;
 }
 
-// ---- the three passes of edt_slerp_population as separate entries (the link-balanced sharded
-// population, distributed.ShardedSlerpPopulation: Gram sums over a rank's chunk range, then the
-// coefficients from the all-gathered table, then the blends of the rank's range) ----
-
-int edt_slerp_gram(const void* const* members, int nmembers, int in_dt, const uint64_t* chunk_desc,
-                   int64_t nchunks, double* gram, void* stream) {
-    g_err[0] = 0;
-    if (in_dt & ~1) return fail(EDT_ERR_ARG, "unsupported dtype");
-    if (nmembers < 1 || nmembers > kGramMaxMembers)
-        return fail(EDT_ERR_ARG, "member count %d out of range [1, %d]", nmembers, kGramMaxMembers);
-    if (nchunks < 0) return fail(EDT_ERR_ARG, "negative chunk count");
-    if (nchunks == 0) return EDT_OK;
-    if (!members || !chunk_desc || !gram) return fail(EDT_ERR_ARG, "null buffer");
-    Members mem;
-    memset(&mem, 0, sizeof(mem));
-    for (int m = 0; m < nmembers; ++m) {
-        if (!members[m] || !aligned16(members[m])) return fail(EDT_ERR_ARG, "member %d is null or not 16-byte aligned", m);
-        mem.p[m] = members[m];
-    }
-    return gram_sums(mem, nmembers, in_dt, chunk_desc, nchunks, gram, (hipStream_t)stream);
-}
-
-int edt_slerp_gram_coef(const double* gram, int nmembers, const int32_t* pairs, int npairs,
-                        const int32_t* seg_first_chunk, int nseg, const double* t, double dot_threshold,
-                        double eps, float* coef, float* dot_out, void* stream) {
-    g_err[0] = 0;
-    if (nmembers < 1 || nmembers > kGramMaxMembers)
-        return fail(EDT_ERR_ARG, "member count %d out of range [1, %d]", nmembers, kGramMaxMembers);
-    if (npairs < 0 || nseg < 0) return fail(EDT_ERR_ARG, "negative count");
-    if (npairs == 0 || nseg == 0) return EDT_OK;
-    if (!gram || !pairs || !seg_first_chunk || !t || !coef) return fail(EDT_ERR_ARG, "null buffer");
-    const int M = nmembers, NT = M * (M + 1) / 2;
-    hipStream_t s = (hipStream_t)stream;
-    for (int q = 0; q < npairs; ++q) {
-        const int i = pairs[2 * q], j = pairs[2 * q + 1];
-        if (i < 0 || j < 0 || i >= M || j >= M) return fail(EDT_ERR_ARG, "pair %d: member out of range", q);
-        const int lo = i < j ? i : j, hi = i < j ? j : i;
-        slerp_gram_coef_kernel<<<coef_grid(nseg), kBlock, 0, s>>>(gram, NT, tri_index(i, i, M), tri_index(j, j, M),
-                                                                  tri_index(lo, hi, M), seg_first_chunk, nseg, t,
-                                                                  (float)dot_threshold, (float)eps,
-                                                                  coef + 2 * (size_t)nseg * q,
-                                                                  dot_out ? dot_out + (size_t)nseg * q : nullptr);
-        int rc = check_launch("slerp_gram_coef_kernel");
-        if (rc) return rc;
-    }
-    return EDT_OK;
-}
+// ---- the member-major blends of edt_slerp_population as a separate entry (the link-balanced
+// sharded population, distributed.ShardedPopulationCrossover: the blends of a rank's chunk range
+// after the needed sums' table rows were all-gathered; the sums and coefficients are
+// edt_slerp_needed_sums / _coef below) ----
 
 int edt_slerp_blend_children(const void* const* members, int nmembers, int in_dt, const int32_t* pairs,
                              int npairs, void* const* outs, int out_dt, const uint64_t* chunk_desc,
@@ -2637,12 +2430,13 @@ void needed_columns(const NeededPlan& P, int k, int32_t* cols) {
     const GramPlan& G = P.G;
     const int M = G.size[k];
     const int* L = G.list[k];
-    if (G.kind[k] == kTri) {
+    if (G.kind[k] == kTri) {                           // dots no child uses are not formed
         for (int i = 0; i < M; ++i)
             for (int j = i; j < M; ++j) {
                 const int c = tri_index(i, j, M);
-                cols[2 * c] = P.orig[L[i]];
-                cols[2 * c + 1] = P.orig[L[j]];
+                const bool used = i == j || ((G.need[k].tri >> c) & 1u);
+                cols[2 * c] = used ? P.orig[L[i]] : -1;
+                cols[2 * c + 1] = used ? P.orig[L[j]] : -1;
             }
         return;
     }

@@ -1002,7 +1002,8 @@ def slerp_population(plan: SlerpPlan, members: list[torch.Tensor], pairs, outs: 
       speculate=False  edt_slerp_population: one stats pass per component of the children's
                        pair graph over the (<= 8) distinct parents (r5: the needed sums — each
                        parent's norm and only the dots its children use, for any graph the
-                       reference's selection draws; the Gram triangle when a component needs more
+                       reference's selection draws; r6: the same pass in the triangle layout
+                       — the component's Gram triangle, unused dots skipped — when it needs more
                        dots than its slots), then one member-major blend launch for all children;
       speculate=True   edt_slerp_population_speculative: one pass forms every child's sums and
                        writes its lerp-branch output (r5: a member-major needed-sums pass per
@@ -1012,8 +1013,9 @@ def slerp_population(plan: SlerpPlan, members: list[torch.Tensor], pairs, outs: 
       None             speculate when the previous call on this plan had few enough child elements
                        in SLERP-branch segments for the single pass to move fewer bytes
                        (f < D b_in / (D b_in + Q b_out), D distinct parents, Q children).
-    ref_dot: the reference-dot mode per child (as slerp_arena's; the Gram form runs its passes
-    separately: Gram sums -> coefficients' dots -> the reference's dots and coefficients -> blends).
+    ref_dot: the reference-dot mode per child (as slerp_arena's; the two-pass form runs its passes
+    separately: needed sums -> coefficients' dots -> the reference's dots and coefficients ->
+    blends).
     Returns the per-child, per-segment fp32 dots ([npairs, nseg])."""
     lib = L.lib()
     M, Q = len(members), len(pairs)
@@ -1054,10 +1056,11 @@ def slerp_population(plan: SlerpPlan, members: list[torch.Tensor], pairs, outs: 
     flat_pairs = (ctypes.c_int32 * max(1, 2 * Q))(*[int(x) for p in pairs for x in p])
     icode, ocode = L.dtype_code(in_dt), L.dtype_code(out_dt)
     if ref_dot is not None and not speculate and Q:
-        # the Gram form's passes separately: sums -> dots -> the reference's coefficients -> blends
-        gram = plan.ws("gram", int(lib.edt_slerp_population_gram_doubles(M, plan.nchunks)), torch.float64)
-        slerp_gram(members, plan.chunks, plan.nchunks, work=gram)
-        _, dots = slerp_gram_coef(plan, gram, M, pairs, t, dot_threshold, eps)
+        # the two-pass form's passes separately: sums -> dots -> the reference's coefficients -> blends
+        layout = needed_table(pairs, M, plan.nchunks)
+        table = plan.ws("needed", max(1, layout.doubles), torch.float64)
+        slerp_needed_sums(members, layout, plan.chunks, plan.nchunks, table, 0)
+        _, dots = slerp_needed_coef(plan, table, layout, t, dot_threshold, eps)
         dots, coef = _population_ref(plan, members, pairs, outs, t, dots, None, icode, ocode, dot_threshold, eps,
                                      ref_dot, blend_all=True)
     elif speculate:
@@ -1120,66 +1123,7 @@ def pair_merge_population(children, lr: float, momentum_coef: float, nesterov: b
 
 
 # ------------------------------------------------------------------------------------------
-# the population SLERP's three passes, separately (distributed.ShardedSlerpPopulation)
-
-def slerp_gram(members: list[torch.Tensor], chunks: torch.Tensor, nchunks: int,
-               gram: torch.Tensor | None = None, work: torch.Tensor | None = None) -> torch.Tensor:
-    """Per-chunk Gram sums of M <= 8 member buffers over a chunk table (int64 [nchunks, 3] on the
-    device, starts relative to the buffers): float64 [nchunks, M(M+1)/2] (edt_slerp_gram). `gram`
-    (optional) receives the rows; its first nchunks x M(M+1)/2 elements are written. `work`
-    (optional, float64, >= edt_slerp_population_gram_doubles(M, nchunks)): the pass's workspace
-    when `gram` cannot hold the row scratch too (default: the stream's pooled workspace). Returns
-    `gram`, or without one a tensor the caller owns (a view of `work` when `work` was given)."""
-    lib = L.lib()
-    M = len(members)
-    L.require_device(*members, chunks)
-    if not 1 <= M <= 8 or any(m.dtype != members[0].dtype for m in members):
-        raise L.EdtError("slerp_gram: 1..8 members of one dtype")
-    NT = M * (M + 1) // 2
-    need = max(1, int(lib.edt_slerp_population_gram_doubles(M, nchunks)))
-    if gram is not None and (gram.dtype != torch.float64 or gram.numel() < nchunks * NT):
-        raise L.EdtError("gram: float64 with nchunks x M(M+1)/2 elements")
-    # the kernel needs the rows plus its slot scratch behind them; a smaller (or non-contiguous)
-    # `gram` — e.g. a rank's rows of the whole table — gets its rows copied from a full-size buffer
-    direct = gram is not None and gram.is_contiguous() and gram.numel() >= need
-    pooled = False
-    if direct:
-        work = gram
-    elif work is None or work.dtype != torch.float64 or not work.is_contiguous() or work.numel() < need:
-        work = _scratch(members[0].device, need)
-        pooled = True
-    L.check(lib.edt_slerp_gram(L.ptr_array(members), M, L.dtype_code(members[0]), L.ptr(chunks), nchunks,
-                               L.ptr(work), L.stream_ptr(members[0].device)), "edt_slerp_gram")
-    rows = work.view(-1)[:nchunks * NT].view(nchunks, NT) if not direct else gram
-    if gram is None:
-        # rows in the stream's pooled workspace would be overwritten by the next SLERP call on this
-        # thread and stream: the caller gets its own copy (rows in a caller's `work` stay views)
-        return rows.clone() if pooled else rows
-    if not direct:
-        gram.view(-1)[:nchunks * NT].copy_(rows.view(-1))
-    return gram
-
-
-def slerp_gram_coef(plan: SlerpPlan, gram: torch.Tensor, nmembers: int, pairs, t: torch.Tensor,
-                    dot_threshold: float = 0.9995, eps: float = 1e-8):
-    """Coefficients [Q, nseg, 2] and dots [Q, nseg] of every child from a whole-layout Gram
-    table (rows = plan's chunks) (edt_slerp_gram_coef)."""
-    lib = L.lib()
-    Q = len(pairs)
-    if gram.numel() < plan.nchunks * nmembers * (nmembers + 1) // 2:
-        raise L.EdtError("gram does not cover the plan's chunks")
-    L.require_device(gram, t)
-    if t.dtype != torch.float64 or t.numel() < plan.nseg:
-        raise L.EdtError("t must be a float64 device tensor with one value per segment")
-    dev = gram.device
-    coef = torch.empty((max(1, Q), max(1, plan.nseg), 2), dtype=torch.float32, device=dev)
-    dots = torch.empty((max(1, Q), max(1, plan.nseg)), dtype=torch.float32, device=dev)
-    fp = (ctypes.c_int32 * max(1, 2 * Q))(*[int(x) for p in pairs for x in p])
-    L.check(lib.edt_slerp_gram_coef(L.ptr(gram), nmembers, fp, Q, L.ptr(plan.seg_first), plan.nseg, L.ptr(t),
-                                    float(dot_threshold), float(eps), L.ptr(coef), L.ptr(dots),
-                                    L.stream_ptr(dev)), "edt_slerp_gram_coef")
-    return coef, dots
-
+# the population SLERP's passes, separately (distributed.ShardedPopulationCrossover)
 
 @dataclass(frozen=True)
 class NeededTable:

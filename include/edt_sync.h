@@ -24,7 +24,10 @@
 
 #include <stdint.h>
 
-/* ABI revision. 5 (round 5): the tensor-list outer step's workspace grew (per-tensor tail-mask
+/* ABI revision. 6 (round 6): edt_slerp_gram / edt_slerp_gram_coef removed (the population's
+ * triangle layout is a mode of the needed-sums pass; the sharded population uses
+ * edt_slerp_needed_*), edt_slerp_seg_table requires the segment sizes. 5 (round 5): the
+ * tensor-list outer step's workspace grew (per-tensor tail-mask
  * offsets; edt_outer_list_workspace_bytes), edt_outer_step_list_tail and
  * edt_slerp_population_layout added, edt_slerp_seg_table refuses in-place outputs that overlap
  * another tensor. 4 (round 4): the tensor-list SLERP reads a device pointer table
@@ -33,7 +36,7 @@
  * added, the on-chip-hold form removed. Workspace sizes come from the *_doubles / *_bytes functions
  * of THIS build: a consumer compiled against another revision must be rebuilt
  * (edt_abi_version() != EDT_ABI_VERSION: refuse to run). */
-#define EDT_ABI_VERSION 5
+#define EDT_ABI_VERSION 6
 
 #ifdef __cplusplus
 extern "C" {
@@ -329,10 +332,10 @@ int edt_slerp_blend_segments(const void* v0, const void* v1, int in_dt, void* ou
  * runs per connected component of the children's pair graph (r5, any graph the reference's
  * roulette selection draws): a component of D <= 8 parents forms its D norms and only the dots its
  * children use — the edges of the best cyclic order of the parents (the ring) plus up to 4 chord
- * slots (2 at D = 4, none below) — and falls back to the full Gram upper triangle when the children
- * need more dots than that; each parent is read once either way. `gram`:
- * edt_slerp_population_gram_doubles(nmembers, nchunks) doubles of device workspace (layout
- * internal to this call; edt_slerp_gram below keeps the triangle layout). Each child's sums,
+ * slots (2 at D = 4, none below) — or, when the children need more dots than that, the same pass
+ * in the triangle layout (its Gram upper triangle: the norms and the dots used); each parent is
+ * read once either way. `gram`: edt_slerp_population_gram_doubles(nmembers, nchunks) doubles of
+ * device workspace (layout internal to this call). Each child's sums,
  * coefficients and output are bit-identical to edt_slerp_merge on (members[i], members[j]).
  * coef: [npairs][nseg][2] floats; dot_out (nullable): [npairs][nseg]. */
 uint64_t edt_slerp_population_gram_doubles(int nmembers, int64_t nchunks);
@@ -366,15 +369,17 @@ int edt_slerp_population_speculative(const void* const* members, int nmembers, i
  * generation (pairs over nmembers <= 8 members, nchunks chunks) is ncomp blocks, one per connected
  * component of the children's pair graph: block k at block_off[k] doubles, nchunks rows of
  * block_nt[k] sums (the component's norms and the dots its children use, or its Gram triangle
- * when they need more dots than the slots). col_members (nullable, 2 x sum(block_nt) int32): the
- * two members of each column, block after block (-1, -1: an unused slot). scratch_doubles: the
+ * when they need more dots than the slots: D(D+1)/2 columns, the dots no child uses not formed).
+ * col_members (nullable, 2 x sum(block_nt) int32): the two members of each column, block after
+ * block (-1, -1: an unused slot, its sum not formed). scratch_doubles: the
  * row scratch a pass over up to nchunks chunks needs.
  *   edt_slerp_needed_sums  rows [row0, row0 + nchunks) of every block, over a chunk table of those
  *                          nchunks chunks (starts relative to the member buffers), table_chunks =
  *                          the table's row count; a row is bit-identical to edt_slerp_population's
  *                          sums of that chunk, wherever the chunk's elements lie (16-byte aligned)
- *   edt_slerp_needed_coef  every child's coefficients and dots from the complete table
- *                          (edt_slerp_gram_coef's output layout) */
+ *   edt_slerp_needed_coef  every child's coefficients [npairs][nseg][2] and dots [npairs][nseg]
+ *                          (nullable) from the complete table
+ *   edt_slerp_blend_children (below) then blends a rank's chunks of every child. */
 int edt_slerp_needed_table(const int32_t* pairs, int npairs, int nmembers, int64_t nchunks, uint64_t* block_off,
                            int32_t* block_nt, int32_t* ncomp, int32_t* col_members, uint64_t* table_doubles,
                            uint64_t* scratch_doubles);
@@ -424,26 +429,17 @@ int edt_slerp_refdot_table(const uint64_t* seg_table, int in_dt, const uint64_t*
 int edt_slerp_refdot_coef(const float* ref_dot, const int32_t* flag, int nseg, const double* t, double dot_threshold,
                           float* coef, float* dot_out, void* stream);
 
-/* ---- the population SLERP's passes, separately (link-balanced sharded population) ----------
- * edt_slerp_population = edt_slerp_gram + edt_slerp_gram_coef + edt_slerp_blend_children. Split
- * so that the Gram sums of a rank's range of whole chunks (its parameter-index shard of all M
- * members, EDT_RL/edt.py:286-299's population spread over the node) can be all-gathered before
- * the coefficients: each chunk's sums are formed by the same kernel in the same order wherever
- * the chunk lives, so the coefficients — and every child — equal edt_slerp_merge's bit for bit.
- *   edt_slerp_gram        gram[c * NT + tri(a, b)], NT = M(M+1)/2, for the chunks of chunk_desc
- *                         (gram: edt_slerp_population_gram_doubles(M, nchunks) doubles, rows first)
- *                         (starts relative to the member buffers); M <= 8.
- *   edt_slerp_gram_coef   per child q = (pairs[2q], pairs[2q+1]) (member indices), per segment of
- *                         the whole layout (seg_first_chunk indexes gram's rows): coef[q][nseg][2],
- *                         dot_out[q][nseg] (may be NULL).
- *   edt_slerp_blend_children  outs[q] = c0 v_a + c1 v_b over the chunks of chunk_desc, the segment
- *                         of each chunk selecting coef[q][seg] (nseg = the row length of coef);
- *                         <= 16 children, member-major (each member's tile read once per chunk). */
-int edt_slerp_gram(const void* const* members, int nmembers, int in_dt, const uint64_t* chunk_desc,
-                   int64_t nchunks, double* gram, void* stream);
-int edt_slerp_gram_coef(const double* gram, int nmembers, const int32_t* pairs, int npairs,
-                        const int32_t* seg_first_chunk, int nseg, const double* t, double dot_threshold,
-                        double eps, float* coef, float* dot_out, void* stream);
+/* ---- the population SLERP's blends, separately (link-balanced sharded population) -----------
+ * edt_slerp_population = edt_slerp_needed_sums (every block, all chunks) + edt_slerp_needed_coef +
+ * edt_slerp_blend_children. Split so that the sums of a rank's range of whole chunks (its
+ * parameter-index shard of all members, EDT_RL/edt.py:286-299's population spread over the node)
+ * can be all-gathered before the coefficients: each chunk's sums are formed by the same kernel in
+ * the same order wherever the chunk lives, so the coefficients — and every child — equal
+ * edt_slerp_merge's bit for bit.
+ *   edt_slerp_blend_children  outs[q] = c0 v_a + c1 v_b over the chunks of chunk_desc (starts
+ *                         relative to the member buffers), the segment of each chunk selecting
+ *                         coef[q][seg] (nseg = the row length of coef); <= 8 members, <= 16
+ *                         children, member-major (each member's tile read once per chunk). */
 int edt_slerp_blend_children(const void* const* members, int nmembers, int in_dt, const int32_t* pairs,
                              int npairs, void* const* outs, int out_dt, const uint64_t* chunk_desc,
                              int64_t nchunks, const float* coef, int nseg, void* stream);

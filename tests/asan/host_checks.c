@@ -163,8 +163,10 @@ static void sync_host_paths(void) {
                                      1e-8, (double*)d, coef, NULL, NULL));   /* output aliases a member */
     EXPECT_FAIL(edt_slerp_merge_list((const void* const*)tt, (const void* const*)tt, 1, tt, 1, (const uint64_t*)d, 1,
                                      first, 2, tv, 0.9995, 1e-8, (double*)d, coef, NULL, d, 8, NULL));
-    EXPECT_FAIL(edt_slerp_gram(mem2, 9, 1, (const uint64_t*)d, 1, (double*)d, NULL));
-    EXPECT_FAIL(edt_slerp_gram_coef((const double*)d, 2, pairs, 2, first, 1, tv, 0.9995, 1e-8, coef, NULL, NULL));
+    EXPECT_FAIL(edt_slerp_needed_sums(mem2, 9, 1, pairs, 1, (const uint64_t*)d, 1, 1, 0, (double*)d, (double*)d, 64,
+                                      NULL));                                 /* 9 members */
+    EXPECT_FAIL(edt_slerp_needed_coef((const double*)d, 1, pairs, 2, 2, first, 1, tv, 0.9995, 1e-8, coef, NULL,
+                                      NULL));                                 /* member 7 of 2 */
     EXPECT_FAIL(edt_slerp_blend_children(mem2, 2, 1, pairs, 17, outs17, 1, (const uint64_t*)d, 1, coef, 1, NULL));
     EXPECT_FAIL(edt_slerp_merge_speculative(d, dummy + 8, 1, dummy + 4, 1, (const uint64_t*)d, 1, first, 1, tv,
                                             0.9995, 1e-8, (double*)d, coef, NULL, (int32_t*)d, 100, NULL));

@@ -41,11 +41,13 @@ class OracleKernels:
 
 
 class ChunkGramKernels(OracleKernels):
-    """CPU stand-in for the split population-SLERP passes (edt_slerp_gram / _gram_coef /
+    """CPU stand-in for the split population-SLERP passes (edt_slerp_needed_sums / _needed_coef /
     _blend_children) with the same chunk-table semantics: per-chunk fp64 sums (torch, one fixed
     order per chunk), per-segment sums over the chunks in order, the reference's scalar formula,
     fp32 blends. Used to test the sharded schedule's data movement on CPU (gloo / virtual ranks):
-    a sharded run must equal this same arithmetic on the whole population, bit for bit."""
+    a sharded run must equal this same arithmetic on the whole population, bit for bit.
+    slerp_gram / slerp_gram_coef are the whole-population form of that arithmetic (every pair's
+    sums; the library's triangle layout is a mode of the needed-sums pass since r6)."""
 
     def make_slerp_plan(self, offsets, device, chunk_elems=1 << 16):
         import types

@@ -195,4 +195,4 @@ def test_seg_table_host_checks(lib):
 
 def test_abi_version_matches_the_binding(lib):
     from evolutionarydistributedtraining_amd import _lib as L
-    assert lib.edt_abi_version() == L.EDT_ABI_VERSION == 5
+    assert lib.edt_abi_version() == L.EDT_ABI_VERSION == 6

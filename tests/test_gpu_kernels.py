@@ -537,10 +537,10 @@ def _pair_graphs():
 @pytest.mark.parametrize("speculate", [False, True])
 @pytest.mark.parametrize("graph", sorted(_pair_graphs()))
 def test_slerp_population_pair_graphs(dev, ops, graph, speculate):
-    """edt_slerp_population's stats pass per component of the children's pair graph (r4): paths and
-    cycles of >= 3 parents take the ring layout (norms + ring dots), other components the triangle;
-    the speculative form takes the member-major ring pass when the children are the edges of one
-    path or cycle (either orientation, one child per edge), else the co-located pass; every child's
+    """edt_slerp_population's stats pass per component of the children's pair graph (r4 ring
+    layout; r5: the needed sums — norms, ring dots, up to 4 chords — r6: past the chord slots the
+    same pass in the triangle layout); the speculative form takes the member-major pass when every
+    component fits its slots, else the co-located pass; every child's
     outputs and dots stay bit-identical to edt_slerp_merge — rings, matchings, paths, several
     cycles, a star, self-pairs, repeated pairs, members no child uses, random graphs, segments on
     both sides of the threshold (the redo blend)."""

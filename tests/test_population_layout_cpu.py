@@ -94,7 +94,8 @@ def test_needed_table_covers_every_child_on_random_graphs():
     """edt_slerp_needed_table on 300 seeded random pair graphs (1..8 members, 1..24 children, self
     pairs, repeats, reversals): every child's two norms and its dot are columns of one block;
     blocks are laid out back to back; a block's columns are its members' norms first; a block on
-    the needed layout has D + ring + <= 4 chord slots (triangle otherwise); the table and scratch
+    the needed layout has D + ring + <= 4 chord slots (triangle otherwise: the norms and the used
+    dots formed, the other triangle columns (-1, -1)); the table and scratch
     sizes follow; the planner's JSON view agrees (components, sums per block)."""
     import random
 
@@ -128,7 +129,10 @@ def test_needed_table_covers_every_child_on_random_graphs():
             if comp["stats_layout"] == "needed":
                 assert [set(x) for x in c[:D]] == [{m} for m in comp["members"]]   # norms first
                 assert len(c) == 2 * D + (4 if D >= 5 else 2 if D == 4 else 0) - (1 if D <= 2 else 0)
-            else:                                                                # every pair once
-                mem = comp["members"]
-                assert sorted(tuple(sorted(x)) for x in c) == sorted(
-                    (mem[p], mem[q]) if mem[p] <= mem[q] else (mem[q], mem[p]) for p in range(D) for q in range(p, D))
+            else:     # the triangle layout (r6: a mode of the needed pass): D(D+1)/2 columns,
+                mem = comp["members"]                # the norms and the dots a child uses formed
+                assert len(c) == D * (D + 1) // 2
+                used = {frozenset((i, j)) for i, j in pairs if i in mem}
+                want = sorted([(m, m) for m in mem] + [tuple(sorted(d)) for d in used if len(d) == 2])
+                assert sorted(tuple(sorted(x)) for x in c if x[0] >= 0) == want
+                assert sum(1 for x in c if x[0] < 0) == len(c) - len(want)
