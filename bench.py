@@ -269,20 +269,18 @@ def _free_port() -> int:
 
 # ------------------------------------------------------------------------------------------
 # The line. The driver keeps the last ~8,400 characters of stdout, so the printed line is a
-# projection of the full record, capped at LINE_CAP characters: every measured number the
-# judge reads (value, rooflines, traffic, CPU baselines, per-generation ms), without the
-# per-generation pair lists, planner layouts and free-text notes. The full record goes to a
-# sidecar JSON file (`--detail-out`), named in the line as `detail`.
+# projection of the full record, capped at LINE_CAP characters: the same keys at the same paths
+# (line["list_form"]["f32"]["roofline"]["frac"] is the record's), keeping every measured number the
+# judge reads (value, rooflines, traffic and its stamp, CPU baselines, per-generation ms in
+# `gen_ms`), without the per-generation pair lists, planner layouts and free-text notes. The full
+# record goes to a sidecar JSON file (`--detail-out`), named in the line as `detail`.
 
 LINE_CAP = 8000
+KEEP = True                       # a projection leaf: keep the value as it is
 
 
 def _r(x, nd=4):
     return round(x, nd) if isinstance(x, float) else x
-
-
-def _keep(d, keys):
-    return {k: _r(d[k]) for k in keys if isinstance(d, dict) and k in d}
 
 
 def _failed(v):
@@ -292,162 +290,113 @@ def _failed(v):
     return None
 
 
-def _c_roof(r, keys=("frac", "achieved", "traffic")):
-    return _keep(r or {}, keys)
+def _project(obj, spec):
+    """obj restricted to spec: KEEP keeps the value, a dict keeps those keys (recursively), a
+    callable maps the value; keys absent from obj are skipped; error records pass through."""
+    if spec is KEEP:
+        return _r(obj)
+    if callable(spec):
+        return spec(obj)
+    if not isinstance(obj, dict):
+        return obj
+    if _failed(obj):
+        return _failed(obj)
+    return {k: _project(obj[k], sub) for k, sub in spec.items() if k in obj}
 
 
-def _c_main_roofline(r):
-    out = {k: v for k, v in r.items() if k not in ("unplaced_note", "momentum_placement", "xgmi")}
-    mp = r.get("momentum_placement")
-    if isinstance(mp, dict):
-        out["momentum_placement"] = _failed(mp) or _keep(mp, ("candidates", "chosen", "probe_ms"))
-    if "xgmi" in r:
-        out["xgmi"] = r["xgmi"]
-    return out
+def _short(n):
+    return lambda v: str(v)[:n]
 
 
-def _c_cpu(c):
-    if not isinstance(c, dict):
-        return c
-    out = _failed(c) or _keep(c, ("value", "unit", "cores", "kind", "cpu_model", "cores_reason"))
-    if "sample" in c:
-        out["sample"] = str(c["sample"])[:200]
-    if isinstance(c.get("c_port"), dict):
-        out["c_port"] = _keep(c["c_port"], ("value", "unit", "cores", "kind"))
-    return out
-
-
-def _c_kernel_trace(kt):
-    if _failed(kt) or "kernels" not in (kt or {}):
-        return kt
-    ks = []
-    for k in kt["kernels"][:3]:
+def _trace_kernels(ks):
+    out = []
+    for k in ks[:3]:
         name = k["name"].replace("void ", "").replace("(anonymous namespace)::", "")
-        ks.append({"name": name.split("(")[0][:90], "launches": k["launches"], "mean_ms": k["mean_ms"]})
-    return {"tool": "torch.profiler", "steps": kt.get("steps"), "kernels": ks}
-
-
-def _c_list_form(v):
-    out = {"kernel": "outer_list_kernel"}
-    for key in ("f32", "bf16", "bf16_cpu_tails"):
-        if isinstance(v.get(key), dict):
-            rec = v[key]
-            out[key] = {**_keep(rec, ("kernel_ms", "wall_ms")), **_c_roof(rec.get("roofline"), ("frac", "traffic"))}
-    sm = v.get("same_memory")
-    if isinstance(sm, dict):
-        out["same_memory_list_over_arena"] = {k: sm[k].get("list_over_arena") for k in ("f32", "bf16")
-                                              if isinstance(sm.get(k), dict)}
+        out.append({"name": name.split("(")[0][:90], "launches": k["launches"], "mean_ms": k["mean_ms"]})
     return out
 
 
-def _c_configs1(v):
-    return {**_keep(v, ("ms_per_step", "value", "unplaced_ms", "unplaced_frac", "placement")),
-            **_c_roof(v.get("roofline"), ("frac", "achieved", "traffic"))}
+_ROOF = {"frac": KEEP, "achieved": KEEP, "traffic": KEEP}
+_MAIN_ROOFLINE = {k: KEEP for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_source", "kernel",
+                                    "kernel_ms", "bytes_per_elem", "algo_bytes_per_launch", "device_copy_GBps",
+                                    "stream_ceiling_GBps", "frac_of_stream_ceiling", "unplaced_ms", "unplaced_frac",
+                                    "stream_ceiling_error", "traffic_note", "schedule", "note")}
+_MAIN_ROOFLINE["note"] = _short(120)
+_MAIN_ROOFLINE["momentum_placement"] = {"candidates": KEEP, "chosen": KEEP, "probe_ms": KEEP}
+_MAIN_ROOFLINE["xgmi"] = {k: KEEP for k in ("bound", "achieved", "peak", "unit", "frac", "wire_bytes_per_rank",
+                                            "floor_ms")}
+_CPU = {"value": KEEP, "unit": KEEP, "cores": KEEP, "kind": KEEP, "cpu_model": KEEP, "cores_reason": KEEP,
+        "sample": _short(200), "c_port": {"value": KEEP, "unit": KEEP, "cores": KEEP, "kind": KEEP}, "error": KEEP}
+_LIST_FORM_ONE = {"kernel_ms": KEEP, "wall_ms": KEEP, "roofline": {"frac": KEEP, "traffic": KEEP}}
+_POP_FORM = {"ms_per_generation": KEEP, "roofline": {"frac": KEEP, "algo_frac": KEEP, "traffic_per_generation": KEEP}}
+_SHARDED = {"ms": KEEP, "groups": KEEP, "wire_bytes_per_rank": KEEP, "xgmi_floor_ms": KEEP, "xgmi": {"frac": KEEP},
+            "parity": {"bit_exact": KEEP, "max_ulp": KEEP}}
 
-
-def _c_pair_merge(v):
-    out = {**_keep(v, ("ms",)), **_c_roof(v.get("roofline"), ("frac", "traffic"))}
-    if isinstance(v.get("cpu_baseline"), dict):
-        out["cpu_GBps"] = v["cpu_baseline"].get("value")
-    return out
-
-
-def _c_slerp_7b(v):
-    out = {}
-    for key in ("lineage", "far"):
-        if isinstance(v.get(key), dict):
-            rec = v[key]
-            out[key] = {**_keep(rec, ("ms", "form")),
-                        **_c_roof(rec.get("roofline"), ("frac", "moved_frac", "traffic"))}
-    if isinstance(v.get("cpu_baseline"), dict):
-        out["cpu_GBps"] = v["cpu_baseline"].get("value")
-    return out
-
-
-def _c_lm_population(v):
-    r = v.get("roofline") or {}
-    out = {**_keep(v, ("ms_per_generation", "unplaced_ms_per_generation", "placement")),
-           **_keep(r, ("frac", "algo_GBps", "traffic_per_generation"))}
-    out["gen_ms"] = [g.get("ms") for g in v.get("generations", [])]
-    return out
-
-
-def _c_population_1gpu(v):
-    out = {}
-    for form in ("speculative", "two_pass"):
-        if isinstance(v.get(form), dict):
-            rec = v[form]
-            out[form] = {**_keep(rec, ("ms_per_generation", "unplaced_ms_per_generation")),
-                         **_c_roof(rec.get("roofline"), ("frac", "algo_frac", "traffic_per_generation"))}
-            out[form]["gen_ms"] = [g[form]["ms"] for g in v.get("generations", []) if form in g]
-    if "placement" in v:
-        out["placement"] = v["placement"]
-    if isinstance(v.get("ring"), dict):
-        out["ring_ms"] = {f: v["ring"][f]["ms"] for f in ("speculative", "two_pass") if f in v["ring"]}
-    lb = [g.get("lerp_branch_fraction") for g in v.get("generations", []) if "lerp_branch_fraction" in g]
-    if lb:
-        out["lerp_branch_fraction_min"] = min(lb)
-    return out
-
-
-def _c_population_sharded(v):
-    out = {"pairs": v.get("pairs")}
-    for key in ("sharded", "sharded_pipelined"):
-        if isinstance(v.get(key), dict):
-            rec = v[key]
-            out[key] = {**_keep(rec, ("ms", "groups", "wire_bytes_per_rank")),
-                        "xgmi_frac": (rec.get("xgmi") or {}).get("frac"),
-                        "parity_bit_exact": (rec.get("parity") or {}).get("bit_exact")}
-            if "xgmi_floor_ms" in rec:
-                out[key]["xgmi_floor_ms"] = rec["xgmi_floor_ms"]
-    if isinstance(v.get("per_child"), dict):
-        out["per_child_ms"] = v["per_child"].get("ms")
-    if isinstance(v.get("sums_table"), dict):
-        out["sums_per_chunk"] = v["sums_table"].get("sums_per_chunk")
-    return out
-
-
-def _c_parity(v):
-    return _failed(v) or _keep(v, ("schedule", "buckets", "workers", "bit_exact", "max_ulp", "replicas_identical",
-                                   "replicas_equal_reference"))
-
-
-def _c_schedules(v):
-    return {k: (_failed(s) or _keep(s, ("ms_per_step", "value", "wire_bytes_per_rank", "xgmi_floor_ms")))
-            for k, s in v.items()}
-
-
-def _c_configs(v):
-    return {k: (_failed(s) or _keep(s, ("layout", "dtype", "schedule", "ms_per_step", "value", "xgmi_floor_ms")))
-            for k, s in v.items()}
-
-
-_COMPACT = {"roofline": _c_main_roofline, "cpu_baseline": _c_cpu, "kernel_trace": _c_kernel_trace,
-            "list_form": _c_list_form, "configs1_125m": _c_configs1, "pair_merge": _c_pair_merge,
-            "slerp_7b": _c_slerp_7b, "lm_population": _c_lm_population, "parity": _c_parity,
-            "other_schedules": _c_schedules, "baseline_configs": _c_configs,
-            "step_with_broadcast": lambda v: {**_keep(v, ("fused_ms", "step_plus_copies_ms")),
-                                              **_c_roof(v.get("fused_roofline"), ("frac",))},
-            "weak_scaling": lambda v: _keep(v, ("workers_per_gpu", "ms_per_step", "value", "schedule",
-                                                "wire_bytes_per_rank", "xgmi_floor_ms"))}
+SPEC = {
+    **{k: KEEP for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                         "scaling", "vs_baseline", "dtype", "data", "config", "device", "native", "extras_deadline")},
+    "roofline": _MAIN_ROOFLINE,
+    "cpu_baseline": _CPU,
+    "kernel_trace": {"tool": _short(16), "steps": KEEP, "kernels": _trace_kernels},
+    "step_with_broadcast": {"fused_ms": KEEP, "step_plus_copies_ms": KEEP, "fused_roofline": {"frac": KEEP}},
+    "list_form": {"kernel": _short(40), "f32": _LIST_FORM_ONE, "bf16": _LIST_FORM_ONE, "bf16_cpu_tails": _LIST_FORM_ONE,
+                  "same_memory": {"f32": {"list_over_arena": KEEP},
+                                  "bf16": {"list_over_arena": KEEP, "list_tails_over_arena_tails": KEEP}}},
+    "configs1_125m": {"ms_per_step": KEEP, "value": KEEP, "unplaced_ms": KEEP, "unplaced_frac": KEEP,
+                      "placement": KEEP, "roofline": _ROOF},
+    "pair_merge": {"ms": KEEP, "roofline": _ROOF, "cpu_baseline": {"value": KEEP, "cores": KEEP}},
+    "slerp_7b": {"lineage": {"ms": KEEP, "form": KEEP, "roofline": {"frac": KEEP, "moved_frac": KEEP, "traffic": KEEP}},
+                 "far": {"ms": KEEP, "form": KEEP, "roofline": {"frac": KEEP, "moved_frac": KEEP, "traffic": KEEP}},
+                 "cpu_baseline": {"value": KEEP, "cores": KEEP}},
+    "lm_population": {"ms_per_generation": KEEP, "gen_ms": KEEP,
+                      "roofline": {"frac": KEEP, "algo_GBps": KEEP, "traffic_per_generation": KEEP}},
+    "population_slerp_7b": {"speculative": _POP_FORM, "two_pass": _POP_FORM, "gen_ms": KEEP, "ring_ms": KEEP,
+                            "lerp_branch_fraction_min": KEEP,
+                            # N > 1: the sharded crossover
+                            "pairs": KEEP, "sharded": _SHARDED, "sharded_pipelined": _SHARDED,
+                            "per_child": {"ms": KEEP}, "sums_table": {"sums_per_chunk": KEEP}},
+    "parity": {k: KEEP for k in ("schedule", "buckets", "workers", "bit_exact", "max_ulp", "replicas_identical",
+                                 "replicas_equal_reference")},
+    "weak_scaling": {k: KEEP for k in ("workers_per_gpu", "ms_per_step", "value", "schedule", "wire_bytes_per_rank",
+                                       "xgmi_floor_ms")},
+    "other_schedules": lambda v: {k: _project(x, {"ms_per_step": KEEP, "value": KEEP, "wire_bytes_per_rank": KEEP,
+                                                  "xgmi_floor_ms": KEEP}) for k, x in v.items()},
+    "baseline_configs": lambda v: {k: _project(x, {"layout": KEEP, "dtype": KEEP, "schedule": KEEP, "ms_per_step": KEEP,
+                                                   "value": KEEP, "xgmi_floor_ms": KEEP}) for k, x in v.items()},
+}
 # dropped whole, in this order, only if a line is still over the cap (never the contract fields)
 _DROP_ORDER = ("kernel_trace", "step_with_broadcast", "device", "weak_scaling", "other_schedules", "lm_population",
                "baseline_configs", "slerp_7b", "pair_merge", "population_slerp_7b", "list_form", "configs1_125m")
 
 
+def _with_gen_ms(full: dict) -> dict:
+    """The per-generation times, lifted out of the generation records the line drops."""
+    full = dict(full)
+    lm = full.get("lm_population")
+    if isinstance(lm, dict) and isinstance(lm.get("generations"), list):
+        full["lm_population"] = dict(lm, gen_ms=[g.get("ms") for g in lm["generations"]])
+    pop = full.get("population_slerp_7b")
+    if isinstance(pop, dict) and isinstance(pop.get("generations"), list):
+        extra = {"gen_ms": {f: [g[f]["ms"] for g in pop["generations"] if f in g] for f in ("speculative", "two_pass")}}
+        if isinstance(pop.get("ring"), dict):
+            extra["ring_ms"] = {f: pop["ring"][f]["ms"] for f in ("speculative", "two_pass") if f in pop["ring"]}
+        lb = [g["lerp_branch_fraction"] for g in pop["generations"] if "lerp_branch_fraction" in g]
+        if lb:
+            extra["lerp_branch_fraction_min"] = min(lb)
+        full["population_slerp_7b"] = dict(pop, **extra)
+    return full
+
+
 def compact_line(full: dict, detail: str | None = None, cap: int = LINE_CAP) -> dict:
-    """The printed line: `full` projected key by key (_COMPACT), `detail` (the sidecar's path)
-    added, and — only if still longer than `cap` characters — whole extras dropped in _DROP_ORDER
-    and named under `dropped`."""
+    """The printed line: `full` projected onto SPEC (same keys, same paths), `detail` (the sidecar's
+    path) added, and — only if still longer than `cap` characters — whole extras dropped in
+    _DROP_ORDER and named under `dropped`. Keys SPEC does not name pass through when short."""
+    full = _with_gen_ms(full)
     line = {}
     for k, v in full.items():
-        if _failed(v):
-            line[k] = _failed(v)
-        elif k == "population_slerp_7b" and isinstance(v, dict):
-            line[k] = _c_population_sharded(v) if ("sharded" in v or "per_child" in v) else _c_population_1gpu(v)
-        elif k in _COMPACT and isinstance(v, dict):
-            line[k] = _COMPACT[k](v)
-        else:
+        if k in SPEC:
+            line[k] = _project(v, SPEC[k])
+        elif len(json.dumps(v, default=str)) <= 200:
             line[k] = v
     if detail:
         line["detail"] = detail

@@ -348,7 +348,10 @@ int edt_slerp_population(const void* const* members, int nmembers, int in_dt, co
  * child's lerp-branch output: when every component takes the needed-sums layout and npairs <= 16,
  * one member-major launch per component (each parent read once, every child emitted from the
  * parents' registers: ring-edge children directly, the others from a chord slot or a copy);
- * otherwise one co-located launch (every child of a chunk on one XCD, shared parents read once).
+ * otherwise — the fallback for graphs the reference's 8-pair selection does not draw: more than 16
+ * children, more than 8 distinct parents, a component on the triangle layout, or more distinct
+ * chord children than the emit slots — one co-located launch (every child of a chunk on one XCD,
+ * shared parents read once).
  * Per child the coefficients flag (redo: [npairs][nseg] int32) the SLERP-branch segments, which
  * one launch blends again (it exits at once when no child needs any).
  * partial: edt_slerp_population_speculative_doubles(npairs, nchunks) doubles of workspace.

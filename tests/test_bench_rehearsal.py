@@ -151,7 +151,7 @@ def test_bench_line_at_world(world):
     assert x["floor_ms"] == pytest.approx(x["wire_bytes_per_rank"] / (bench_link_gbps() * (world - 1) * 1e9) * 1e3,
                                           abs=1e-4)
     assert all("xgmi_floor_ms" in v for v in line["other_schedules"].values())
-    assert line["population_slerp_7b"]["sharded"]["parity_bit_exact"] is True
+    assert line["population_slerp_7b"]["sharded"]["parity"]["bit_exact"] is True
     assert d["roofline"]["kernel_ms"] > 0 and d["roofline"]["algo_bytes_per_launch"] > 0
     assert d["cpu_baseline"]["value"] > 0 and "c_port" in d["cpu_baseline"]
     for key in ("weak_scaling", "other_schedules", "baseline_configs", "population_slerp_7b"):

@@ -100,7 +100,7 @@ def test_single_gpu_line_population_extra():
     p = d["population_slerp_7b"]
     lp = line["population_slerp_7b"]
     assert lp["speculative"]["ms_per_generation"] == p["speculative"]["ms_per_generation"]
-    assert lp["two_pass"]["gen_ms"] == [g["two_pass"]["ms"] for g in p["generations"]]
+    assert lp["gen_ms"]["two_pass"] == [g["two_pass"]["ms"] for g in p["generations"]]
     assert "error" not in p and "skipped" not in p, p
     assert "roulette_wheel_selection" in p["pairs_source"] and p["timed_reps"] >= 10
     gens = p["generations"] + [p["ring"]]
