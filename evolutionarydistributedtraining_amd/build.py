@@ -53,10 +53,11 @@ def _file_sha(path: str) -> str:
 
 
 def _flags_key(out: str, extra_flags, tu_extra) -> str:
-    """What, besides the sources, decides the library's bytes: the compiler flags (common, per
-    unit, variant) and the output name. Stored beside the library; a change forces a rebuild."""
+    """What, besides the sources, decides the library's bytes — the compiler flags (common, per
+    unit, variant) — and the output path, so two builds never share an object directory. Stored
+    beside the library; a change forces a rebuild."""
     rec = {"hipcc": HIPCC_FLAGS, "tu": TU_FLAGS, "extra": list(extra_flags or []),
-           "tu_extra": {k: list(v) for k, v in sorted((tu_extra or {}).items())}, "out": os.path.basename(out)}
+           "tu_extra": {k: list(v) for k, v in sorted((tu_extra or {}).items())}, "out": os.path.abspath(out)}
     return hashlib.sha256(json.dumps(rec, sort_keys=True).encode()).hexdigest()[:16]
 
 
