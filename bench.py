@@ -654,7 +654,7 @@ def sharded_parity(args, comm, rt, kernels, mode, broadcast, k_local, tdt, wdt, 
 def population_parity(lay, rt, comm, kernels, member_seed, pairs, t, child) -> dict | None:
     """Child 0 of the sharded population (on rank 0 after the timed runs) against the whole-
     population passes on rank 0 alone (needed sums -> coefficients -> blend over its two parents,
-    regenerated from their seeds): bit-identical to edt_slerp_merge by construction (DESIGN §7.2),
+    regenerated from their seeds): bit-identical to edt_slerp_merge by construction (DESIGN §7),
     so any byte an exchange moved wrong shows. Rank 0 only."""
     if comm.rank != 0:
         return None
@@ -1636,7 +1636,7 @@ def main():
     torch.cuda.synchronize()
     placement = None
     # the fused step on the first allocation, before any placement search: what the drop-in list
-    # path and any first-allocation user get (DESIGN §6.4), reported beside the placed value
+    # path and any first-allocation user get (DESIGN §6.2), reported beside the placed value
     unplaced_ms = _event_ms(step, 5, 0)
     if args.place_candidates > 1:
         # once per run, outside the timed region: the momentum buffer goes wherever the step's

@@ -356,7 +356,7 @@ def write_from_arena(path: str, layout: ParamLayout, flat: torch.Tensor, names: 
     A device arena streams through a pooled pinned staging pair (`staging_bytes` each), its D2H
     overlapping the writes: no whole-arena pinned buffer (pinning 14 GB for a 7B child costs
     1.1-1.2 s per process), and from a clean page cache 1.34-1.39 s against 1.55-1.61 s for one
-    write of an already pinned copy (scripts/write_probe.py --ab). A host tensor
+    write of an already pinned copy (scripts/write_probe.py --ab, profiles/HISTORY.md §B 8). A host tensor
     is written directly (threads > 1: that many writers at their own offsets)."""
     header = _header_bytes(layout, names or layout.names, flat.dtype, metadata)
     if flat.device.type == "cuda":

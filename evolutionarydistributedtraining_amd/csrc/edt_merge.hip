@@ -141,7 +141,7 @@ __global__ __launch_bounds__(kBlock) void pair_population_kernel(PopPairArgs P) 
 }
 
 
-// Closed by measurement: a member-major form (each thread loads every distinct
+// Closed by measurement (profiles/HISTORY.md §C): a member-major form (each thread loads every distinct
 // parent's tiles once and runs the children from its registers: 17.2-17.7 ms r4, 20.4 / 26.9 ms
 // r5 on rank-selected pairs, against 15.7-16.7 co-located) and a child loop inside the thread
 // (parents re-read from L1): both removed.

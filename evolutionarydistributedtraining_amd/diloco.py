@@ -312,7 +312,7 @@ class DirOuterSync:
     place_momentum: after the first step, choose the outer momentum's HBM placement by measurement
     once among this many candidates (OuterSync.place_momentum; 0 or 1 = keep the first allocation).
     The θ and worker arenas stay resident across generations here, so the choice holds for the rest
-    of the run — the drop-in form of the resident flow's placement (DESIGN §6.4). On by default
+    of the run — the drop-in form of the resident flow's placement (DESIGN §6.2). On by default
     (r4): the first allocation ran the step 8-11 % slower in about half of the bench runs
     (`roofline.unplaced_ms`), and the search costs a few probe launches once per run."""
 

@@ -382,7 +382,7 @@ class ResidentPopulation:
 
     def _sharded_children(self, pairs):
         """This rank's child through the link-balanced schedule (bit-identical to the per-child
-        kernels; DESIGN §7.2)."""
+        kernels; DESIGN §7)."""
         from .distributed import ShardedPopulationCrossover
         if self._sharded is None:
             self._sharded = ShardedPopulationCrossover(self.layout, self.dtype, self.device, kind=self.kind,

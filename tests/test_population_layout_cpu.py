@@ -32,7 +32,7 @@ def test_roulette_generations_take_the_needed_layout():
 
 
 def test_selection_statistics_that_motivate_it():
-    """DESIGN §9.2's correction: under roulette selection most generations have a parent in >= 3
+    """The r5 correction: under roulette selection most generations have a parent in >= 3
     distinct pairs (r4's ring layout covers none of them); all are member-major now."""
     hub = 0
     gens = roulette_generation_pairs(8, 2000, seed=3)
