@@ -123,3 +123,36 @@ def test_population_from_threads_on_one_plan(speculate):
             assert torch.equal(dots, want[r][1]), r
             for a, b in zip(outs, want[r][0]):
                 assert torch.equal(_bits(a), _bits(b)), r
+
+
+@pytest.mark.parametrize("speculate", [False, True])
+def test_one_thread_two_streams_on_one_plan(speculate):
+    """one host thread issuing merges over one plan on two streams without syncing
+    between them. The plan's per-merge workspaces (coefficients, dots, redo flags) are keyed by
+    (thread, stream) as the pooled row scratch is, so the two streams' merges never write each
+    other's coefficients: every output and each stream's coefficients equal the serial run's."""
+    offs = [0] + np.cumsum(SIZES).tolist()
+    plan = ops.make_slerp_plan(offs, DEV)
+    data = [tuple(torch.cat(x) for x in _data(400 + r)) for r in range(2)]
+    want = []
+    for r in range(2):
+        out = torch.empty_like(data[r][0])
+        ops.slerp_arena(plan, data[r][0], data[r][1], out, _t(r), speculate=speculate)
+        want.append((out, plan.coef[:len(SIZES)].clone()))
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(DEV) for _ in range(2)]
+    outs = [torch.empty_like(data[r][0]) for r in range(2)]
+    for s in streams:
+        s.wait_stream(torch.cuda.current_stream(DEV))
+    for _ in range(REPS):
+        for r in range(2):
+            with torch.cuda.stream(streams[r]):
+                ops.slerp_arena(plan, data[r][0], data[r][1], outs[r], _t(r), speculate=speculate)
+    coefs = []
+    for r in range(2):
+        with torch.cuda.stream(streams[r]):
+            coefs.append(plan.coef[:len(SIZES)].clone())
+    torch.cuda.synchronize()
+    for r in range(2):
+        assert torch.equal(_bits(outs[r]), _bits(want[r][0])), r
+        assert torch.equal(coefs[r], want[r][1]), r

@@ -106,3 +106,27 @@ def test_another_dispatch_breaks_the_golden_bits_and_is_flagged():
     assert res["host"]["coef_dispatch"] != RECORD["coef_dispatch"], res
     assert res["golden_mismatch"] > 0, res          # the dispatch changes the reference's bits
     assert res["warned"] and res["raised"], res
+
+
+def test_host_dispatch_without_numpy_introspect(monkeypatch):
+    """numpy < 2 has no numpy.lib.introspect. The dispatch is then recorded as unknown
+    (no ImportError on every reference-dot merge), which host_mismatch reports — a warning, or
+    EdtError with strict=True."""
+    import sys
+
+    import numpy.lib
+    import pytest
+
+    from evolutionarydistributedtraining_amd import _lib as L
+    from evolutionarydistributedtraining_amd import ops
+    monkeypatch.setattr(ops, "_HOST_DISPATCH", None)
+    monkeypatch.delattr(numpy.lib, "introspect", raising=False)
+    monkeypatch.setitem(sys.modules, "numpy.lib.introspect", None)
+    host = ops.host_dispatch()
+    assert host["coef_dispatch"] == {"arccos": "unknown", "sin": "unknown"}
+    bad = ops.RefDot().host_mismatch()
+    assert any("unknown" in b for b in bad)
+    monkeypatch.setattr(ops, "_REFDOT_CHECKED", set())
+    with pytest.raises(L.EdtError):
+        ops.RefDot(strict=True).check_host()
+    monkeypatch.setattr(ops, "_HOST_DISPATCH", None)
