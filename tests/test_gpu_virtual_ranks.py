@@ -189,6 +189,42 @@ def test_sharded_population_roulette_graphs_on_virtual_ranks(world, gen):
             assert torch.equal(res[0][1][c], plan.dots[:plan.nseg]), (groups, c)
 
 
+def test_sharded_population_dense_graph_takes_the_triangle_layout():
+    """r6: a pair graph past the chord slots (a hub in 7 of the 8 pairs) puts its component on the
+    triangle layout of the needed-sums pass; through the shards (world 8, the table rows of every
+    rank's chunk range all-gathered, 1 and 3 groups) every child and its dots stay bit-identical to
+    edt_slerp_merge on its two parents."""
+    from evolutionarydistributedtraining_amd.distributed import ShardedPopulationCrossover
+    from evolutionarydistributedtraining_amd.params import ParamLayout
+    world = 8
+    layout = ParamLayout([(257, 301), (7,), (1,), (65537,), (3, 1001), (5,), (200_003,)])
+    n = layout.total
+    pairs = [(0, m) for m in range(1, 8)] + [(1, 2)]
+    assert [c["stats_layout"] for c in ops.population_layout(pairs, world, False)["components"]] == ["triangle"]
+    g = torch.Generator().manual_seed(21)
+    base = torch.randn(n, generator=g) * 0.02
+    members = [(base + torch.randn(n, generator=g) * 0.02 * (0.005 if r % 2 else 0.5)).bfloat16().to(DEV)
+               for r in range(world)]
+    t = torch.tensor([0.3, 0.5, 0.9, 0.5, 0.43, 0.7, 0.6], dtype=torch.float64, device=DEV)
+    plan = ops.make_slerp_plan(layout.offsets, DEV)
+    for groups in (1, 3):
+        def body(comm):
+            sp = ShardedPopulationCrossover(layout, torch.bfloat16, DEV, kind="slerp", out_dtype=torch.bfloat16,
+                                            comm=comm, groups=groups)
+            out = torch.full((n,), float("nan"), dtype=torch.bfloat16, device=DEV)
+            dots = sp.slerp_step(members[comm.rank], pairs, t, out)
+            return out, dots.clone()
+
+        res = VirtualWorld(world).run(body)
+        torch.cuda.synchronize()
+        for c, (i, j) in enumerate(pairs):
+            want = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+            ops.slerp_arena(plan, members[i], members[j], want, t, speculate=False)
+            torch.cuda.synchronize()
+            assert torch.equal(bits(res[c][0]), bits(want)), (groups, c)
+            assert torch.equal(res[0][1][c], plan.dots[:plan.nseg]), (groups, c)
+
+
 def test_needed_sums_entries_match_the_population_pass():
     """edt_slerp_needed_sums over a chunk range (row0 > 0, a chunk table relative to a shard) writes
     the same rows as the whole-table call, and edt_slerp_needed_coef gives edt_slerp_population's
