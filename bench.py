@@ -44,10 +44,12 @@ oracle CPU baseline on a sample (`--ops none` drops them).
 
 Prints ONE JSON line on rank 0. Also reports the fused kernel's own duration (HIP events on the
 stream it is launched on), the HBM roofline fraction, and the CPU oracle timed on this host.
-At N=1, after the warm-up steps and before the timed ones, the momentum buffer's HBM placement is
-chosen by measurement (OuterSync.place_momentum, placement.py: the step's two read-modify-write
-streams run up to 11 % faster or slower depending on their relative physical placement); the
-candidates' probe times are in roofline.momentum_placement, and --place-candidates 1 disables it.
+At N=1, after the warm-up steps and before the timed ones, the operand set's HBM placement is
+chosen by measurement (OuterSync.place_arenas, placement.place_set: the step runs up to ~11 % faster
+or slower depending on where its streams sit — the momentum relative to theta inside one region,
+and the region the whole set landed in); each draw's best probe time is in roofline.placement, the
+chosen draw's momentum candidates in roofline.momentum_placement; --place-candidates 1 disables it
+and --place-draws 1 keeps the search to the momentum.
 """
 from __future__ import annotations
 
@@ -103,6 +105,10 @@ def parse(argv=None):
                    help="N=1: choose the momentum buffer's HBM placement among this many allocations by "
                         "timing the step's access pattern on each, once before the timed steps (placement.py); "
                         "1 keeps the first allocation")
+    p.add_argument("--place-draws", type=int, default=3,
+                   help="N=1: regions of HBM the whole operand set (theta, workers, momentum) is drawn in "
+                        "by the placement search (placement.place_set; the momentum placed inside each); "
+                        "1: the momentum search only")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     p.add_argument("--ops", default="list_form,configs1_125m,pair_merge,slerp_7b,lm_population,population_7b",
                    help="the other hot-path measurements in the same line ('none': skip): N=1 list_form "
@@ -323,6 +329,7 @@ _MAIN_ROOFLINE = {k: KEEP for k in ("bound", "achieved", "peak", "unit", "frac",
                                     "stream_ceiling_error", "traffic_note", "schedule", "note")}
 _MAIN_ROOFLINE["note"] = _short(120)
 _MAIN_ROOFLINE["momentum_placement"] = {"candidates": KEEP, "chosen": KEEP, "probe_ms": KEEP}
+_MAIN_ROOFLINE["placement"] = KEEP
 _MAIN_ROOFLINE["xgmi"] = {k: KEEP for k in ("bound", "achieved", "peak", "unit", "frac", "wire_bytes_per_rank",
                                             "floor_ms")}
 _CPU = {"value": KEEP, "unit": KEEP, "cores": KEEP, "kind": KEEP, "cpu_model": KEEP, "cores_reason": KEEP,
@@ -872,7 +879,7 @@ def bench_config1(args, dev):
     unplaced = _event_ms(sync.step, nsteps, args.warmup)
     placement = None
     if args.place_candidates > 1:
-        placement = sync.place_momentum(args.place_candidates)
+        placement = sync.place_arenas(max(1, args.place_draws + 1), args.place_candidates)
         ms = _event_ms(sync.step, nsteps, args.warmup)
     else:
         ms = unplaced
@@ -890,9 +897,19 @@ def bench_config1(args, dev):
                         "frac": round(gbs / HBM_PEAK_GBPS, 4), "bytes_per_elem": per_elem,
                         "algo_bytes_per_launch": per_elem * P, "traffic": traffic, "traffic_source": note}}
     if placement:
-        res["placement"] = placement if "error" in placement else {"chosen": placement.get("chosen"),
-                                                                   "probe_ms": placement.get("probe_ms")}
+        res["placement"] = _placement_record(placement)
     return res
+
+
+def _placement_record(rep: dict) -> dict:
+    """The line's view of a place_set report: each draw's best probe time, the chosen draw and,
+    inside it, the momentum candidates' probe times."""
+    if "error" in rep:
+        return rep
+    out = {"draws_ms": [d["best_ms"] for d in rep.get("draws", [])], "chosen_draw": rep.get("chosen_draw")}
+    if "draws_limited_by_memory" in rep:
+        out["draws_limited_by_memory"] = rep["draws_limited_by_memory"]
+    return out
 
 
 def bench_list_form(args, dev):
@@ -1639,10 +1656,11 @@ def main():
     # path and any first-allocation user get, reported beside the placed value
     unplaced_ms = _event_ms(step, 5, 0)
     if args.place_candidates > 1:
-        # once per run, outside the timed region: the momentum buffer goes wherever the step's
-        # access pattern runs fastest (placement.py); every later step uses that placement
+        # once per run, outside the timed region: the operand set goes wherever the step's access
+        # pattern runs fastest — `--place-draws` regions of HBM for theta and the workers, the
+        # momentum placed inside each (placement.place_set); every later step uses that placement
         try:
-            placement = sync.place_momentum(args.place_candidates)
+            placement = sync.place_arenas(args.place_draws, args.place_candidates)
         except Exception as e:          # a measurement extra: report it, keep the first allocation
             placement = {"error": f"{type(e).__name__}: {e}"}
         step()
@@ -1720,10 +1738,12 @@ def main():
         roofline["frac_of_stream_ceiling"] = round(roofline["achieved"] / ceil, 4)
     roofline["unplaced_ms"] = round(unplaced_ms, 4)
     roofline["unplaced_frac"] = round(algo_bytes / (unplaced_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)
-    roofline["unplaced_note"] = ("the fused step (HIP events, 5 launches) on the momentum's first allocation, "
+    roofline["unplaced_note"] = ("the fused step (HIP events, 5 launches) on the operands' first allocation, "
                                  "before the placement search; kernel_ms is after it")
     if placement:
-        roofline["momentum_placement"] = placement
+        roofline["placement"] = _placement_record(placement)
+        if "momentum" in placement:
+            roofline["momentum_placement"] = placement["momentum"]
     if args.kernel_trace > 0:
         try:
             out["kernel_trace"] = kernel_trace(step, args.kernel_trace)

@@ -269,6 +269,23 @@ class OuterSync:
                                                   candidates)
         return rep
 
+    def place_arenas(self, draws: int = 3, candidates: int = 8) -> dict:
+        """Choose where the whole operand set lives — θ, the workers and the outer momentum — by
+        measurement, once, for the life of the run (placement.place_set: `draws` regions of HBM,
+        the momentum placed inside each). The arenas are re-pointed at the chosen buffers with
+        their contents unchanged; a module bound to an arena (params.bind_module_) must be bound
+        again afterwards. With draws = 1 this is place_momentum."""
+        if self.momentum == 0:
+            return {"draws": [], "chosen_draw": None}
+        from .placement import place_set
+        mom = self.state.buffer_for(self.theta.flat)
+        th, ws, m, rep = place_set(self.theta.flat, [w.flat for w in self.workers], mom, draws, candidates)
+        self.theta.flat = th
+        for w, f in zip(self.workers, ws):
+            w.flat = f
+        self.state.momentum = m
+        return rep
+
     def broadcast_(self) -> None:
         """Start every worker from the new global weights (what saving base_model to every
         worker dir does, EDT_LM/diloco.py:302-308) as K device copies; step(broadcast=True) does

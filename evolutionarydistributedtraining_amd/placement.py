@@ -80,3 +80,46 @@ def place_momentum(theta: torch.Tensor, workers: list[torch.Tensor], momentum: t
     theta.copy_(saved_theta)
     del saved, saved_theta, bufs, spacers
     return chosen, {"candidates": fit, "probe_ms": [round(t, 4) for t in times], "chosen": best}
+
+
+def place_set(theta: torch.Tensor, workers: list[torch.Tensor], momentum: torch.Tensor, draws: int = 3,
+              candidates: int = 8, iters: int = 3, spacer_bytes: int = 7 << 30):
+    """Return (theta, workers, momentum, report): the whole operand set of the step in whichever of
+    `draws` regions of HBM runs its access pattern fastest, the momentum placed inside each region
+    by place_momentum. What place_momentum cannot reach: how fast a placement can be depends on the
+    region the whole set landed in (r6, profiles/r06_set_placement_probe.jsonl: three draws of the
+    1.3B fp32 x 8 set placed at 10.63 / 10.32 / 10.98 ms; at 125M the same, r06_config1_joint.jsonl),
+    so draw d > 0 copies theta and the workers into fresh allocations behind a held spacer of
+    d * spacer_bytes and places a momentum there too; the fastest draw is kept and the others freed.
+    Contents are unchanged (copies), only addresses move — the caller re-points whatever held the old
+    buffers (OuterSync.place_arenas re-points its arenas; modules bound to the old arenas must be
+    bound again). Draws are limited to what fits in free device memory with the momentum search's
+    room to spare; with one draw this is place_momentum."""
+    set_bytes = theta.numel() * theta.element_size() + sum(w.numel() * w.element_size() for w in workers)
+    mom_bytes = momentum.numel() * momentum.element_size()
+    mom0, rep0 = place_momentum(theta, workers, momentum, candidates, iters)
+    first = min(rep0["probe_ms"]) if rep0["probe_ms"] else probe_ms(theta, workers, mom0, iters)
+    best = {"draw": 0, "ms": first, "set": (theta, workers, mom0), "momentum": rep0}
+    report = {"draws": [{"best_ms": round(first, 4), "momentum_candidates": rep0["candidates"]}], "chosen_draw": 0}
+    spacers = []
+    for d in range(1, max(1, draws)):
+        free, _ = torch.cuda.mem_get_info(theta.device)
+        # the new set + its spacer, with room for place_momentum's copies and candidates after it
+        if free * 0.75 < set_bytes + d * spacer_bytes + 6 * mom_bytes:
+            report["draws_limited_by_memory"] = d
+            break
+        spacers.append(torch.empty(d * spacer_bytes, dtype=torch.uint8, device=theta.device))
+        th = torch.empty_like(theta).copy_(theta)
+        ws = [torch.empty_like(w).copy_(w) for w in workers]
+        m = torch.empty_like(mom0).copy_(mom0)
+        m, rep = place_momentum(th, ws, m, candidates, iters)
+        ms = min(rep["probe_ms"]) if rep["probe_ms"] else probe_ms(th, ws, m, iters)
+        report["draws"].append({"best_ms": round(ms, 4), "momentum_candidates": rep["candidates"]})
+        if ms < best["ms"]:
+            best = {"draw": d, "ms": ms, "set": (th, ws, m), "momentum": rep}
+        del th, ws, m
+    del spacers
+    report["chosen_draw"] = best["draw"]
+    report["momentum"] = best["momentum"]
+    th, ws, m = best["set"]
+    return th, ws, m, report

@@ -452,6 +452,45 @@ def test_momentum_placement_keeps_the_step_bit_identical(dev, tdt):
     assert torch.equal(a.state.momentum, b.state.momentum)
 
 
+@pytest.mark.parametrize("tdt", [torch.float32, torch.bfloat16])
+def test_arena_placement_keeps_the_step_bit_identical(dev, tdt):
+    """OuterSync.place_arenas (r6) draws the whole operand set — theta, the workers, the momentum —
+    in several regions of HBM and keeps the fastest: the arenas are re-pointed with their contents
+    unchanged (exact zeros included), and every later step is bit-identical to the unplaced run."""
+    from evolutionarydistributedtraining_amd.diloco import OuterSync
+    from evolutionarydistributedtraining_amd.params import ParamArena, ParamLayout
+    layout = ParamLayout([torch.Size((1000, 1000)), torch.Size((4097,)), torch.Size((3,))], ["a", "b", "c"])
+    g = torch.Generator(device=dev).manual_seed(12)
+    theta0 = (torch.randn(layout.total, generator=g, device=dev) * 0.02).to(tdt)
+    theta0[:5000] = 0
+    ws0 = [(theta0.float() + torch.randn(layout.total, generator=g, device=dev) * 1e-3).to(tdt) for _ in range(3)]
+    syncs = []
+    for place in (False, True):
+        theta = ParamArena(layout, tdt, dev)
+        theta.flat.copy_(theta0)
+        workers = [ParamArena(layout, tdt, dev) for _ in ws0]
+        for w, w0 in zip(workers, ws0):
+            w.flat.copy_(w0)
+        s = OuterSync(theta, workers, 0.7, 0.9, True)
+        s.step()
+        if place:
+            before = [theta.flat.clone(), s.state.momentum.clone()] + [w.flat.clone() for w in workers]
+            rep = s.place_arenas(draws=3, candidates=3)
+            assert len(rep["draws"]) == 3 and 0 <= rep["chosen_draw"] < 3, rep
+            assert rep["momentum"]["candidates"] == 3
+            after = [theta.flat, s.state.momentum] + [w.flat for w in workers]
+            assert all(torch.equal(x, y) for x, y in zip(before, after))
+        s.step()
+        s.step()
+        syncs.append(s)
+    a, b = syncs
+    vb = torch.int16 if tdt == torch.bfloat16 else torch.int32
+    assert torch.equal(a.theta.flat.view(vb), b.theta.flat.view(vb))
+    assert torch.equal(a.state.momentum.view(vb), b.state.momentum.view(vb))
+    for wa, wb in zip(a.workers, b.workers):
+        assert torch.equal(wa.flat.view(vb), wb.flat.view(vb))
+
+
 # ------------------------------------------------------------------------------------------
 # libedt_comm.so (include/edt_comm.h) at world size 1 on the one-GPU box: the collectives are
 # identities, the sharded reduce schedule equals the single-GPU fused step bit for bit (fp32 master)
