@@ -103,6 +103,7 @@ def place_set(theta: torch.Tensor, workers: list[torch.Tensor], momentum: torch.
     report = {"draws": [{"best_ms": round(first, 4), "momentum_candidates": rep0["candidates"]}], "chosen_draw": 0}
     spacers = []
     for d in range(1, max(1, draws)):
+        torch.cuda.empty_cache()                  # the previous draw's freed buffers back to the device
         free, _ = torch.cuda.mem_get_info(theta.device)
         # the new set + its spacer, with room for place_momentum's copies and candidates after it
         if free * 0.75 < set_bytes + d * spacer_bytes + 6 * mom_bytes:
@@ -119,6 +120,7 @@ def place_set(theta: torch.Tensor, workers: list[torch.Tensor], momentum: torch.
             best = {"draw": d, "ms": ms, "set": (th, ws, m), "momentum": rep}
         del th, ws, m
     del spacers
+    torch.cuda.empty_cache()
     report["chosen_draw"] = best["draw"]
     report["momentum"] = best["momentum"]
     th, ws, m = best["set"]
