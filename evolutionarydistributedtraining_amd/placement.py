@@ -7,13 +7,16 @@ read-write traffic), which the allocator decides: on one MI355X, the same launch
 workers took 10.66-10.85 ms with the momentum in most separate allocations and 11.3-11.9 ms when
 it came right after theta's (scripts/alloc_draws.py, profiles/r01_alloc_draws.json), and each
 placement keeps its speed for the life of the allocation (3 interleaved rounds within 0.4 %).
-The workers' placement does not matter.
+Inside one region the workers' placement does not matter; r6 found that the region the whole
+operand set lands in does (profiles/r06_set_placement_probe.jsonl: three draws of the 1.3B set,
+each with its momentum placed, at 10.63 / 10.32 / 10.98 ms; at 125M likewise).
 
-A resident run keeps its arenas for every generation, so it pays to choose the momentum's
-placement once, by measurement, when the buffer is created: `place_momentum` allocates a few
-candidate buffers, times `edt_probe_stream` (the step's exact access pattern with a trivial body)
-on each, keeps the fastest (with the momentum's contents) and frees the rest. No element is
-computed differently; only the address changes.
+A resident run keeps its arenas for every generation, so it pays to choose the placement once, by
+measurement, when the buffers are created: `place_momentum` allocates a few candidate momentum
+buffers, times `edt_probe_stream` (the step's exact access pattern with a trivial body) on each,
+keeps the fastest (with the momentum's contents) and frees the rest; `place_set` does that in
+several regions of HBM for the whole set (theta and the workers copied there) and keeps the
+fastest region. No element is computed differently; only the addresses change.
 """
 from __future__ import annotations
 
