@@ -328,16 +328,20 @@ class DirOuterSync:
     new weights go to (out_dirs; the reference writes them over worker_dirs, its default here).
     place_momentum: after the first step, choose the outer momentum's HBM placement by measurement
     once among this many candidates (OuterSync.place_momentum; 0 or 1 = keep the first allocation).
-    The θ and worker arenas stay resident across generations here, so the choice holds for the rest
-    of the run — the drop-in form of the resident flow's placement. On by default
-    (r4): the first allocation ran the step 8-11 % slower in about half of the bench runs
-    (`roofline.unplaced_ms`), and the search costs a few probe launches once per run."""
+    place_draws (r6): and draw the whole resident set (θ, the worker arenas, the momentum) in this
+    many regions of HBM, the momentum placed inside each (placement.place_set; 1 = the momentum
+    search only). The θ and worker arenas stay resident across generations here (the checkpoints
+    are read into them), so the choice holds for the rest of the run — the drop-in form of the
+    resident flow's placement. On by default (r4): the first allocation ran the step
+    8-11 % slower in about half of the bench runs (`roofline.unplaced_ms`), and the search costs a
+    few probe launches and one copy of the set per draw, once per run."""
 
     INNER_STATE_FILES = ("optimizer.pt", "scheduler.pt")
 
     def __init__(self, device=None, theta_dtype=None, worker_dtype=None, names=None,
                  lr=0.7, momentum=0.9, nesterov=True, state: OuterState | None = None,
-                 state_path: str | None = None, carry_inner_state: bool = False, place_momentum: int = 8):
+                 state_path: str | None = None, carry_inner_state: bool = False, place_momentum: int = 8,
+                 place_draws: int = 3):
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.theta_dtype, self.worker_dtype, self.names = theta_dtype, worker_dtype, names
         self.lr, self.momentum, self.nesterov = lr, momentum, nesterov
@@ -349,6 +353,7 @@ class DirOuterSync:
         self.state_path = state_path
         self.carry_inner_state = carry_inner_state
         self.place_candidates = place_momentum
+        self.place_draws = place_draws
         self.placement = None             # the placement search's report, once it has run
 
     def _layout_from(self, model_dir):
@@ -392,9 +397,13 @@ class DirOuterSync:
         _step_flat(self.theta.flat, workers, self.state, self.lr, self.momentum, self.nesterov)
         if self.place_candidates > 1 and self.placement is None and self.momentum != 0 \
                 and self.theta.flat.device.type == "cuda":
-            from .placement import place_momentum
-            self.state.momentum, self.placement = place_momentum(self.theta.flat, workers, self.state.momentum,
-                                                                 self.place_candidates)
+            from .placement import place_set
+            th, ws, m, self.placement = place_set(self.theta.flat, workers, self.state.momentum,
+                                                  max(1, self.place_draws), self.place_candidates)
+            self.theta.flat, self.state.momentum = th, m
+            for arena, flat in zip(self.workers, ws):
+                arena.flat = flat
+            workers = ws
         out_dirs = worker_dirs if out_dirs is None else out_dirs
         if self.carry_inner_state:          # diloco.py:295-300, before the model write as there
             # beside the weights the next inner loop loads: out_dirs (== worker_dirs in the reference)

@@ -126,5 +126,6 @@ def place_set(theta: torch.Tensor, workers: list[torch.Tensor], momentum: torch.
     torch.cuda.empty_cache()
     report["chosen_draw"] = best["draw"]
     report["momentum"] = best["momentum"]
+    report.update({k: best["momentum"][k] for k in ("candidates", "probe_ms", "chosen")})   # place_momentum's keys
     th, ws, m = best["set"]
     return th, ws, m, report

@@ -337,8 +337,9 @@ def test_dir_outer_sync_two_generations(oracle, dev, tmp_path):
 
 
 def test_dir_outer_sync_placed_momentum_and_inner_state_carry(oracle, dev, tmp_path):
-    """DirOuterSync(place_momentum=8, carry_inner_state=True): the momentum moved once after the
-    first step (resident arenas, so the placement holds), every later generation bit-identical to
+    """DirOuterSync(place_momentum=8, carry_inner_state=True): the whole resident set (θ, worker
+    arenas, momentum) placed once after the first step (placement.place_set; resident arenas, so
+    the placement holds), every later generation bit-identical to
     the oracle; each GenN+1 dir ends with its machine's GenN optimizer.pt / scheduler.pt
     (EDT_LM/diloco.py:295-300)."""
     from transformers import LlamaForCausalLM
@@ -377,6 +378,7 @@ def test_dir_outer_sync_placed_momentum_and_inner_state_carry(oracle, dev, tmp_p
             assert torch.equal(bits(pack(list(got.parameters()))), bits(theta)), (gen, d)
             assert (tmp_path / f"w{k}" / f"Gen{gen + 1:04d}" / "optimizer.pt").read_bytes() == f"opt w{k} g0".encode()
         assert sync.placement is not None and sync.placement["candidates"] >= 1
+        assert len(sync.placement["draws"]) >= 1 and sync.placement["chosen_draw"] is not None
         prev = dirs
     assert torch.equal(bits(sync.state.momentum.cpu()), bits(mom))
 
