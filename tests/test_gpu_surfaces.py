@@ -493,6 +493,29 @@ def test_arena_placement_keeps_the_step_bit_identical(dev, tdt):
         assert torch.equal(wa.flat.view(vb), wb.flat.view(vb))
 
 
+def test_place_set_one_draw_and_the_memory_limit(dev):
+    """place_set with one draw is the momentum search on the set where it lies (theta and the
+    workers returned as they were); a draw that does not fit free memory is not taken — the report
+    names it (draws_limited_by_memory) and the first draw's set comes back."""
+    from evolutionarydistributedtraining_amd.placement import place_set
+    n = 1 << 20
+    g = torch.Generator(device=dev).manual_seed(3)
+    theta = torch.randn(n, generator=g, device=dev)
+    workers = [theta + torch.randn(n, generator=g, device=dev) * 1e-3 for _ in range(2)]
+    mom = torch.randn(n, generator=g, device=dev) * 1e-3
+    keep = [theta.clone(), mom.clone()] + [w.clone() for w in workers]
+    th, ws, m, rep = place_set(theta, workers, mom, draws=1, candidates=3)
+    assert th is theta and all(a is b for a, b in zip(ws, workers))
+    assert len(rep["draws"]) == 1 and rep["chosen_draw"] == 0 and rep["candidates"] == 3
+    assert "draws_limited_by_memory" not in rep
+    assert all(torch.equal(x, y) for x, y in zip(keep, [th, m] + ws))
+    free, _ = torch.cuda.mem_get_info(dev)
+    th, ws, m, rep = place_set(theta, workers, m, draws=3, candidates=2, spacer_bytes=free)
+    assert rep["draws_limited_by_memory"] == 1 and rep["chosen_draw"] == 0 and len(rep["draws"]) == 1
+    assert th is theta and all(a is b for a, b in zip(ws, workers))
+    assert all(torch.equal(x, y) for x, y in zip(keep, [th, m] + ws))
+
+
 # ------------------------------------------------------------------------------------------
 # libedt_comm.so (include/edt_comm.h) at world size 1 on the one-GPU box: the collectives are
 # identities, the sharded reduce schedule equals the single-GPU fused step bit for bit (fp32 master)
