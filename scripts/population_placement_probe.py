@@ -11,7 +11,9 @@ different physical ranges) and the generation is timed on each.
          two parents into the candidate (the child's own access pattern: its parents read, it
          written), the fastest kept; the generation is timed again on the chosen arenas.
 
-    python scripts/population_placement_probe.py [lm|slerp] > profiles/r06_population_placement.jsonl
+  lm_set the whole EDT-LM set (members and children) drawn in several regions (r6 follow-up)
+
+    python scripts/population_placement_probe.py [lm|lm_set|slerp] > profiles/r06_population_placement.jsonl
 """
 import json
 import os
@@ -120,7 +122,46 @@ def slerp(draws):
                       "per_child_search": search, "placed_ms": round(placed, 3)}), flush=True)
 
 
+def _lm_set(dev, P, M, bf):
+    g = torch.Generator(device=dev).manual_seed(31)
+    x = torch.randn(P, generator=g, device=dev) * 0.02
+    base, trained, mom = [], [], []
+    for _ in range(M):
+        b = (x + torch.randn(P, generator=g, device=dev) * 1e-4).to(bf)
+        base.append(b)
+        trained.append((b.float() + torch.randn(P, generator=g, device=dev) * 1e-3).to(bf))
+        mom.append((torch.randn(P, generator=g, device=dev) * 1e-3).to(bf))
+    del x
+    return base, trained, mom
+
+
+def lm_set(draws):
+    """r6 follow-up: the whole EDT-LM set (members' base / trained / momentum and the children's
+    arenas) drawn `draws` times, each behind a held spacer of d x 9 GiB with the previous draw
+    freed; the same seeded contents every draw (identical work), the generation timed on each."""
+    dev = torch.device("cuda:0")
+    P, bf, M = gpt_1p3b().total, torch.bfloat16, 8
+    pairs = [tuple(p) for p in rank_generation_pairs(M, 1, seed=2025)[0]["pairs"]]
+    times = []
+    for d in range(draws):
+        torch.cuda.empty_cache()
+        spacer = torch.empty(d * 9 * GIB, dtype=torch.uint8, device=dev) if d else None
+        base, trained, mom = _lm_set(dev, P, M, bf)
+        outs = [torch.empty(P, dtype=bf, device=dev) for _ in range(M)]
+        omom = [torch.empty(P, dtype=bf, device=dev) for _ in range(M)]
+        children = [{"b1": base[i], "b2": base[j], "m1": trained[i], "m2": trained[j], "out": outs[c],
+                     "momentum": omom[c], "momentum_in": mom[i], "has_momentum": True}
+                    for c, (i, j) in enumerate(pairs)]
+        ms = event_ms(lambda: ops.pair_merge_population(children, 0.7, 0.9, True))
+        times.append(round(ms, 3))
+        print(json.dumps({"case": "lm_set_draw", "draw": d, "ms": round(ms, 3)}), flush=True)
+        del children, base, trained, mom, outs, omom, spacer
+    print(json.dumps({"case": "lm_set", "P": P, "pairs": [list(p) for p in pairs], "draw_ms": times,
+                      "spread": round(max(times) / min(times) - 1, 4)}), flush=True)
+
+
 if __name__ == "__main__":
     which = sys.argv[1] if len(sys.argv) > 1 else "lm"
     {"lm": lambda: lm(int(os.environ.get("DRAWS", "4"))),
+     "lm_set": lambda: lm_set(int(os.environ.get("DRAWS", "4"))),
      "slerp": lambda: slerp(int(os.environ.get("DRAWS", "3")))}[which]()
