@@ -121,7 +121,8 @@ int main(int argc, char** argv) {
             const float med = t[k][2];
             std::printf(", \"%s_ms\": %.4f, \"%s_TBps\": %.3f", names[k], med, names[k], algo / (med * 1e-3) / 1e12);
         }
-        std::printf("}\n");
+        std::printf(", \"va\": {\"th\": \"%p\", \"m\": \"%p\", \"th2\": \"%p\", \"m2\": \"%p\", \"w0\": \"%p\", \"w7\": \"%p\"}}\n",
+                    (void*)th, (void*)m, (void*)th2, (void*)m2, (void*)w[0], (void*)w[7]);
         std::fflush(stdout);
         CHECK(hipFree(th));
         CHECK(hipFree(m));
