@@ -377,7 +377,7 @@ class DirOuterSync:
         GenN of every worker, whose inner optimiser / scheduler files are carried into
         worker_dirs when carry_inner_state is set (EDT_LM/diloco.py:295-300)."""
         import shutil
-        from .checkpoint import read_many, save_to_dirs
+        from .checkpoint import copy_file, read_many, save_to_dirs
         if self.carry_inner_state and (prev_dirs is None or len(prev_dirs) != len(worker_dirs)):
             raise ValueError("carry_inner_state needs prev_dirs: the previous generation dir of every worker")
         if self.layout is None:
@@ -412,7 +412,7 @@ class DirOuterSync:
                 for fname in self.INNER_STATE_FILES:
                     src = os.path.join(source, fname)
                     if os.path.exists(src):
-                        shutil.copy(src, os.path.join(target, fname))
+                        copy_file(src, os.path.join(target, fname))
         save_to_dirs(out_dirs, self.layout, self.theta.flat)
         if self.state_path:                  # durable carry: write-then-rename
             self.state.save(self.state_path + ".tmp", self.layout)

@@ -7,6 +7,12 @@ worker's dir): K files of identical bytes. How fast can K copies land on this fi
              files either way, the reference's semantics
   link       one file written, then K - 1 hard links (one inode: NOT the reference's semantics; for
              comparison only)
+  write_replace  as write, over K existing files written and flushed just before (the outer step
+             replaces the workers' trained checkpoints)
+  unlink_write  as write_replace, each existing file unlinked first (the rename then replaces
+             nothing)
+  publish    as write_replace, the new file complete before the old one is unlinked and the new
+             one renamed into place (checkpoint._publish, r6)
 
 Files of --mib MiB (default: the 1.3B bf16 model, 2,510 MiB) in --dir (default $TMPDIR), page cache
 warm (no fsync: the best case of a shared disk, as profiles/r06_e2e_checkpoint_edge.jsonl); each
@@ -78,9 +84,27 @@ def main():
                              list(ThreadPoolExecutor(a.k).map(lambda p: copy_one(paths[0], p), paths[1:]))),
             "link": lambda: (write_one(paths[0], data), [os.link(paths[0], p) for p in paths[1:]]),
         }
+        def prefill():                    # the workers' trained files already there, flushed
+            clean()
+            list(ThreadPoolExecutor(a.k).map(lambda p: write_one(p, data), paths))
+            os.sync()
+
+        forms["write_replace"] = lambda: list(ThreadPoolExecutor(a.k).map(lambda p: write_one(p, data), paths))
+
+        def unlink_then_write(p):
+            os.remove(p)
+            write_one(p, data)
+        forms["unlink_write"] = lambda: list(ThreadPoolExecutor(a.k).map(unlink_then_write, paths))
+
+        def publish(p):                   # checkpoint._publish's order: tmp complete, unlink, rename
+            with open(p + ".tmp", "wb") as f:
+                f.write(data)
+            os.remove(p)
+            os.rename(p + ".tmp", p)
+        forms["publish"] = lambda: list(ThreadPoolExecutor(a.k).map(publish, paths))
         for rep in range(2):
             for name, fn in forms.items():
-                clean()
+                prefill() if name in ("write_replace", "unlink_write", "publish") else clean()
                 t0 = time.perf_counter()
                 try:
                     fn()

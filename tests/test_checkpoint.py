@@ -106,6 +106,39 @@ def test_broadcast_copies_are_independent_files(tmp_path):
         assert torch.equal(sd[name], v)
 
 
+def test_broadcast_over_existing_files_unlinks_then_renames(tmp_path):
+    """The broadcast lands over the workers' trained checkpoints (the outer step's out_dirs are its
+    worker dirs): each old file is unlinked before the complete new one is renamed into place
+    (checkpoint._publish: a rename that replaces nothing, so ext4 does not flush the new file
+    synchronously). The path ends with the new bytes on a new inode; another name of the old file
+    keeps the old bytes; copy_file does the same for the carried inner-state files."""
+    m = _tiny(torch.float32)
+    layout = ParamLayout.of_module(m)
+    flat = pack(list(m.parameters()))
+    dirs = [str(tmp_path / f"w{k}") for k in range(3)]
+    for d in dirs:
+        os.makedirs(d)
+        with open(os.path.join(d, "model.safetensors"), "wb") as f:
+            f.write(b"trained replica")
+    keep = str(tmp_path / "old_link")
+    os.link(os.path.join(dirs[0], "model.safetensors"), keep)
+    old_ino = os.stat(keep).st_ino
+    checkpoint.save_to_dirs(dirs, layout, flat)
+    files = [os.path.join(d, "model.safetensors") for d in dirs]
+    ref = open(files[0], "rb").read()
+    assert ref != b"trained replica" and all(open(f, "rb").read() == ref for f in files)
+    assert os.stat(files[0]).st_ino != old_ino and open(keep, "rb").read() == b"trained replica"
+    assert not any(n.endswith(".tmp") for d in dirs for n in os.listdir(d))
+    src, dst = str(tmp_path / "opt_src.pt"), os.path.join(dirs[1], "optimizer.pt")
+    open(src, "wb").write(b"carried")
+    open(dst, "wb").write(b"trained")
+    os.link(dst, str(tmp_path / "opt_link"))
+    checkpoint.copy_file(src, dst)
+    assert open(dst, "rb").read() == b"carried" and open(str(tmp_path / "opt_link"), "rb").read() == b"trained"
+    checkpoint.copy_file(src, os.path.join(dirs[2], "optimizer.pt"))     # no file there yet
+    assert open(os.path.join(dirs[2], "optimizer.pt"), "rb").read() == b"carried"
+
+
 def test_broadcast_over_a_sharded_replica_reads_back_the_broadcast(tmp_path):
     """A worker dir holding its trained replica as index + shards (a model too big for one
     file) receives the new global model from save_to_dirs (EDT_LM/diloco.py:302-308): the stale
