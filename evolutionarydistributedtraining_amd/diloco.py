@@ -397,9 +397,13 @@ class DirOuterSync:
         _step_flat(self.theta.flat, workers, self.state, self.lr, self.momentum, self.nesterov)
         if self.place_candidates > 1 and self.placement is None and self.momentum != 0 \
                 and self.theta.flat.device.type == "cuda":
+            import time
             from .placement import place_set
+            t0 = time.perf_counter()
             th, ws, m, self.placement = place_set(self.theta.flat, workers, self.state.momentum,
                                                   max(1, self.place_draws), self.place_candidates)
+            torch.cuda.synchronize(th.device)
+            self.placement["seconds"] = round(time.perf_counter() - t0, 3)     # once per run
             self.theta.flat, self.state.momentum = th, m
             for arena, flat in zip(self.workers, ws):
                 arena.flat = flat

@@ -1,4 +1,4 @@
-"""The checkpoint edge at the north star's sizes (SURVEY.md §8(f)1, DESIGN.md §6.8): safetensors
+"""The checkpoint edge at the north star's sizes (SURVEY.md §8(f)1, DESIGN.md §6.7): safetensors
 files -> pinned host -> HBM -> kernel -> files, as the reference's master does it through its shared
 disk (EDT_LM/diloco.py:231-235 gather, :302-308 broadcast; EDT_EVOMERGE/train/crossover.py:86-146).
 
@@ -91,11 +91,16 @@ def diloco(a, dev, root):
     del workers, mom, theta
     torch.cuda.empty_cache()
     # DirOuterSync end to end (generation 1: base + workers read; generation 2: theta resident)
-    sync = DirOuterSync(device=dev, names=lay.names)
+    sync = DirOuterSync(device=dev, names=lay.names, place_draws=a.place_draws)
     t1, _ = _sync_time(lambda: sync.step(base_dir, wdirs))
     t2, _ = _sync_time(lambda: sync.step(wdirs[0], wdirs))
+    t3, _ = _sync_time(lambda: sync.step(wdirs[0], wdirs))
+    pl = sync.placement or {}
     res["dir_outer_sync"] = {"generation_ms": round(t1 * 1e3, 1), "resident_theta_generation_ms": round(t2 * 1e3, 1),
-                             "metric_GBps_e2e": round(a.k * P * 2 / t2 / 1e9, 2)}
+                             "third_generation_ms": round(t3 * 1e3, 1),
+                             "metric_GBps_e2e": round(a.k * P * 2 / t2 / 1e9, 2),
+                             "placement": {"seconds": pl.get("seconds"), "place_draws": a.place_draws,
+                                           "draws_ms": [d["best_ms"] for d in pl.get("draws", [])]}}
     del sync
     torch.cuda.empty_cache()
     for d in [base_dir] + wdirs:
@@ -140,6 +145,7 @@ def main():
     ap.add_argument("--what", default="diloco,slerp")
     ap.add_argument("--dir", default=os.path.join(os.getcwd(), "e2e_ckpt_tmp"))
     ap.add_argument("--k", type=int, default=8)
+    ap.add_argument("--place-draws", type=int, default=3, help="DirOuterSync(place_draws=...)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     os.makedirs(a.dir, exist_ok=True)
