@@ -328,20 +328,21 @@ class DirOuterSync:
     new weights go to (out_dirs; the reference writes them over worker_dirs, its default here).
     place_momentum: after the first step, choose the outer momentum's HBM placement by measurement
     once among this many candidates (OuterSync.place_momentum; 0 or 1 = keep the first allocation).
-    place_draws (r6): and draw the whole resident set (θ, the worker arenas, the momentum) in this
-    many regions of HBM, the momentum placed inside each (placement.place_set; 1 = the momentum
-    search only). The θ and worker arenas stay resident across generations here (the checkpoints
-    are read into them), so the choice holds for the rest of the run — the drop-in form of the
-    resident flow's placement. On by default (r4): the first allocation ran the step
-    8-11 % slower in about half of the bench runs (`roofline.unplaced_ms`), and the search costs a
-    few probe launches and one copy of the set per draw, once per run."""
+    The θ and worker arenas stay resident across generations here (the checkpoints are read into
+    them), so the choice holds for the rest of the run. On by default (r4): the first
+    allocation ran the step 8-11 % slower in about half of the bench runs, and the search costs
+    0.19 s once at 1.3B x 8 bf16. place_draws > 1 (r6): also draw the whole resident set (θ, the
+    worker arenas, the momentum) in that many regions of HBM (placement.place_set). Off by default
+    here: a generation through checkpoint files takes ~1 s, of which the step is 12 ms, and three
+    draws cost 1.79 s once (profiles/r06_e2e_checkpoint_publish.jsonl) — OuterSync.place_arenas is
+    the resident kernel loop's form."""
 
     INNER_STATE_FILES = ("optimizer.pt", "scheduler.pt")
 
     def __init__(self, device=None, theta_dtype=None, worker_dtype=None, names=None,
                  lr=0.7, momentum=0.9, nesterov=True, state: OuterState | None = None,
                  state_path: str | None = None, carry_inner_state: bool = False, place_momentum: int = 8,
-                 place_draws: int = 3):
+                 place_draws: int = 1):
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.theta_dtype, self.worker_dtype, self.names = theta_dtype, worker_dtype, names
         self.lr, self.momentum, self.nesterov = lr, momentum, nesterov

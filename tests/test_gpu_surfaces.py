@@ -357,7 +357,7 @@ def test_dir_outer_sync_placed_momentum_and_inner_state_carry(oracle, dev, tmp_p
         (tmp_path / f"w{k}" / "Gen0000" / "optimizer.pt").write_bytes(f"opt w{k} g0".encode())
         (tmp_path / f"w{k}" / "Gen0000" / "scheduler.pt").write_bytes(f"sch w{k} g0".encode())
     sync = DirOuterSync(device=dev, names=layout.names, lr=0.7, momentum=0.9, nesterov=True,
-                        carry_inner_state=True, place_momentum=8)
+                        carry_inner_state=True, place_momentum=8, place_draws=3)
     theta = pack(list(base.parameters()))
     mom = torch.zeros_like(theta)
     prev = [str(tmp_path / f"w{k}" / "Gen0000") for k in range(K)]
