@@ -145,7 +145,7 @@ def main():
     ap.add_argument("--what", default="diloco,slerp")
     ap.add_argument("--dir", default=os.path.join(os.getcwd(), "e2e_ckpt_tmp"))
     ap.add_argument("--k", type=int, default=8)
-    ap.add_argument("--place-draws", type=int, default=3, help="DirOuterSync(place_draws=...)")
+    ap.add_argument("--place-draws", type=int, default=1, help="DirOuterSync(place_draws=...)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     os.makedirs(a.dir, exist_ok=True)
