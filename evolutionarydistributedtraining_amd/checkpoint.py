@@ -374,6 +374,69 @@ def _stream_write(path: str, header: bytes, flat: torch.Tensor, staging_bytes: i
     _publish(tmp, path)
 
 
+def _shard_groups(layout: ParamLayout, es: int, shard_bytes: int) -> list[tuple[int, int]]:
+    """Runs of whole tensors of at most shard_bytes each (a tensor larger than that is a shard of
+    its own), as save_pretrained's max_shard_size cuts them."""
+    groups, t0, acc = [], 0, 0
+    for k, m in enumerate(layout.numels):
+        b = m * es
+        if k > t0 and acc + b > shard_bytes:
+            groups.append((t0, k))
+            t0, acc = k, 0
+        acc += b
+    groups.append((t0, len(layout)))
+    return groups
+
+
+def write_sharded_from_arena(model_dir: str, layout: ParamLayout, flat: torch.Tensor, shard_bytes: int,
+                             names: list[str] | None = None, metadata: dict | None = None,
+                             staging_bytes: int = 64 << 20) -> list[str]:
+    """`flat` as HF's sharded layout in model_dir: model-0000i-of-0000N.safetensors (runs of whole
+    tensors of <= shard_bytes, `_shard_groups`) + model.safetensors.index.json, the shards written
+    by one thread each. The page cache takes one file at ~11-12 GB/s whatever the writer count
+    (profiles/HISTORY.md §B 8) but several files at once far faster, so a 7B child lands ~3x
+    sooner as four shards (profiles/r06_e2e_sharded_write.jsonl). Any single-file
+    model.safetensors and stale shards of another count are removed; the index is published last,
+    so a reader sees either the old files or the complete new set."""
+    from concurrent.futures import ThreadPoolExecutor
+    names = names or layout.names
+    es = flat.element_size()
+    groups = _shard_groups(layout, es, shard_bytes)
+    n = len(groups)
+    files = [f"model-{i + 1:05d}-of-{n:05d}.safetensors" for i in range(n)]
+    os.makedirs(model_dir, exist_ok=True)
+    # the writer threads order their copies after the caller's current stream (not their own default)
+    caller = torch.cuda.current_stream(flat.device) if flat.device.type == "cuda" else None
+
+    def one(i):
+        t0, t1 = groups[i]
+        sub = ParamLayout(layout.shapes[t0:t1], names[t0:t1])
+        part = flat[layout.offsets[t0]:layout.offsets[t0] + sub.total]
+        header = _header_bytes(sub, sub.names, flat.dtype, metadata)
+        target = os.path.join(model_dir, files[i])
+        if caller is not None:
+            with torch.cuda.device(part.device), torch.cuda.stream(caller):
+                _stream_write(target, header, part, staging_bytes)
+        else:
+            _write_file(target, header, part.contiguous())
+    if n > 1:
+        with ThreadPoolExecutor(max_workers=n) as ex:
+            list(ex.map(one, range(n)))
+    else:
+        one(0)
+    keep = set(files)
+    for f in os.listdir(model_dir):
+        if f == "model.safetensors" or (_SHARD_RE.match(f) and f not in keep):
+            os.remove(os.path.join(model_dir, f))
+    index = {"metadata": {"total_size": layout.total * es},
+             "weight_map": {nm: files[i] for i, (t0, t1) in enumerate(groups) for nm in names[t0:t1]}}
+    idx = os.path.join(model_dir, "model.safetensors.index.json")
+    with open(idx + ".tmp", "w") as f:
+        json.dump(index, f, indent=2)
+    _publish(idx + ".tmp", idx)
+    return files
+
+
 def write_from_arena(path: str, layout: ParamLayout, flat: torch.Tensor, names: list[str] | None = None,
                      metadata: dict | None = None, threads: int = 1, staging_bytes: int = 64 << 20,
                      writers: int = 1) -> None:

@@ -473,13 +473,30 @@ class ResidentPopulation:
         numpy's global RNG), so a resumed run continues draw for draw. The reference keeps
         this state in RAM and on the shared disk between its scripts (genome.json per dir,
         outer_optim.pt per individual)."""
+        from concurrent.futures import ThreadPoolExecutor
         from .checkpoint import write_from_arena
         names = self._names()
+        tasks = []
         for m in self.local_members():
             for tag, t in self._member_tensors(m):
                 d = os.path.join(path, f"member{m}", tag)
                 os.makedirs(d, exist_ok=True)
-                write_from_arena(os.path.join(d, "model.safetensors"), self.layout, t, names)
+                tasks.append((os.path.join(d, "model.safetensors"), t))
+        # one writer thread per file (the page cache takes one file at ~11-12 GB/s, several at
+        # once far faster: profiles/r06_e2e_sharded_write.jsonl), each ordered after the caller's
+        # current stream, which produced the arenas
+        dev = tasks[0][1].device if tasks else None
+        caller = torch.cuda.current_stream(dev) if dev is not None and dev.type == "cuda" else None
+
+        def one(task):
+            target, t = task
+            if caller is not None:
+                with torch.cuda.device(t.device), torch.cuda.stream(caller):
+                    write_from_arena(target, self.layout, t, names)
+            else:
+                write_from_arena(target, self.layout, t, names)
+        with ThreadPoolExecutor(max_workers=max(1, min(8, len(tasks)))) as ex:
+            list(ex.map(one, tasks))
         if self.rank == 0:
             meta = {"kind": self.kind, "population": self.P, "generation": self.generation,
                     "genomes": self.genomes, "has_momentum": self.has_momentum,

@@ -130,12 +130,22 @@ def slerp(a, dev, root):
     t_read, _ = _sync_time(lambda: checkpoint.read_many(list(zip(dirs, (v0, v1))), lay))
     t_merge, _ = _sync_time(lambda: ops.slerp_arena(plan, v0, v1, out, t))
     t_write, _ = _sync_time(lambda: checkpoint.write_from_arena(os.path.join(child, "model.safetensors"), lay, out))
+    sharded = os.path.join(root, "child_sharded")
+    t_shard, files = _sync_time(lambda: checkpoint.write_sharded_from_arena(sharded, lay, out, a.shard_bytes))
     res = {"layout": "qwen2p5_7b_body", "P": P, "dtype": "bf16",
            "phases": {"read_ms": round(t_read * 1e3, 1), "read_GBps": round(4 * P / t_read / 1e9, 2),
                       "merge_ms": round(t_merge * 1e3, 2), "write_ms": round(t_write * 1e3, 1),
                       "write_GBps": round(2 * P / t_write / 1e9, 2),
-                      "total_ms": round((t_read + t_merge + t_write) * 1e3, 1)}}
-    for d in dirs + [child]:
+                      "total_ms": round((t_read + t_merge + t_write) * 1e3, 1)},
+           "sharded_write": {"shard_bytes": a.shard_bytes, "shards": len(files), "ms": round(t_shard * 1e3, 1),
+                             "GBps": round(2 * P / t_shard / 1e9, 2),
+                             "total_ms": round((t_read + t_merge + t_shard) * 1e3, 1)}}
+    back = torch.empty_like(out)                  # the shards read back equal the child
+    checkpoint.read_many([(sharded, back)], lay)
+    torch.cuda.synchronize()
+    res["sharded_write"]["reads_back_equal"] = bool(torch.equal(back, out))
+    del back
+    for d in dirs + [child, sharded]:
         shutil.rmtree(d, ignore_errors=True)
     return res
 
@@ -146,6 +156,7 @@ def main():
     ap.add_argument("--dir", default=os.path.join(os.getcwd(), "e2e_ckpt_tmp"))
     ap.add_argument("--k", type=int, default=8)
     ap.add_argument("--place-draws", type=int, default=1, help="DirOuterSync(place_draws=...)")
+    ap.add_argument("--shard-bytes", type=int, default=4 << 30, help="slerp: write_sharded_from_arena's shard size")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     os.makedirs(a.dir, exist_ok=True)

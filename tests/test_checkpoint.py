@@ -244,3 +244,30 @@ def test_reader_fuzz(tmp_path_factory, shapes, ckpt_dt, arena_dt, cuts, staging,
     checkpoint.read_many(items, layout, threads=threads, staging_bytes=staging)
     for (_, flat), w in zip(items, want):
         assert torch.equal(flat, w)
+
+
+def test_sharded_write_reads_back_and_loads_in_hf(tmp_path):
+    """write_sharded_from_arena: HF's sharded layout (shards of whole tensors <= shard_bytes +
+    index) that read_into_arena and from_pretrained both load; a single-file save there before is
+    removed, and rewriting with another shard count leaves no stale shard behind."""
+    from transformers import LlamaForCausalLM
+    m = _tiny(torch.bfloat16)
+    m.save_pretrained(tmp_path / "src")
+    layout = ParamLayout.of_module(m)
+    flat = pack(list(m.parameters())) * 3
+    d = tmp_path / "child"
+    checkpoint.save_to_dirs([str(d)], layout, flat * 0)             # a single-file save first
+    files = checkpoint.write_sharded_from_arena(str(d), layout, flat, shard_bytes=4096)
+    assert len(files) > 2 and not (d / "model.safetensors").exists()
+    assert sorted(os.listdir(d)) == sorted(files + ["model.safetensors.index.json"])
+    back = torch.empty_like(flat)
+    checkpoint.read_into_arena(str(d), layout, back)
+    assert torch.equal(back, flat)
+    shutil.copy(tmp_path / "src" / "config.json", d / "config.json")
+    m2 = LlamaForCausalLM.from_pretrained(d, dtype=torch.bfloat16)
+    for a, b in zip(m2.parameters(), layout.views(flat)):
+        assert torch.equal(a, b)
+    few = checkpoint.write_sharded_from_arena(str(d), layout, flat + 1, shard_bytes=1 << 20)
+    assert len(few) == 1 and sorted(f for f in os.listdir(d) if f.endswith(".safetensors")) == few
+    checkpoint.read_into_arena(str(d), layout, back)
+    assert torch.equal(back, flat + 1)

@@ -50,3 +50,26 @@ def test_write_from_device_arena_rejects_a_strided_view(tmp_path, dev):
     x = torch.zeros(16, device=dev)[::2]
     with pytest.raises(ValueError):
         checkpoint.write_from_arena(str(tmp_path / "m.safetensors"), layout, x)
+
+
+@pytest.mark.parametrize("shard_bytes", [1 << 10, 300_000, 1 << 30])
+def test_sharded_write_from_device_arena(tmp_path, dev, shard_bytes):
+    """write_sharded_from_arena from a device arena just produced on the current stream: every
+    shard streamed whole (one writer thread and staging pair per shard), the index names each
+    tensor's shard, and the directory reads back into an arena bit for bit."""
+    import json
+    from safetensors.torch import load_file
+    layout = ParamLayout(SHAPES, NAMES)
+    g = torch.Generator(device=dev).manual_seed(7)
+    flat = (torch.randn(layout.total, device=dev, generator=g) * 3).to(torch.bfloat16)
+    files = checkpoint.write_sharded_from_arena(str(tmp_path), layout, flat, shard_bytes, staging_bytes=1 << 16)
+    idx = json.load(open(tmp_path / "model.safetensors.index.json"))
+    assert sorted(set(idx["weight_map"].values())) == sorted(files) and sorted(idx["weight_map"]) == sorted(NAMES)
+    host = flat.cpu()
+    for name, v in zip(NAMES, layout.views(host)):
+        assert torch.equal(load_file(str(tmp_path / idx["weight_map"][name]))[name], v), name
+    back = torch.empty_like(flat)
+    checkpoint.read_into_arena(str(tmp_path), layout, back)
+    torch.cuda.synchronize()
+    assert torch.equal(back.cpu(), host)
+    assert not any(p.name.endswith(".tmp") for p in tmp_path.iterdir())
