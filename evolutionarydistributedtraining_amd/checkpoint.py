@@ -257,19 +257,76 @@ def _host_copy(flat: torch.Tensor) -> torch.Tensor:
     return host
 
 
-def _publish(tmp: str, path: str) -> None:
-    """The complete file tmp becomes path. An existing path is unlinked first, so the rename
-    replaces nothing: ext4 (and overlay file systems over it, as on the GPU boxes) flushes a file's
-    delayed allocation synchronously when a rename replaces an existing file (auto_da_alloc), which
-    made the broadcast over the workers' trained checkpoints disk-bound — 8 x 2.6 GB in 3.2-4.1 s
-    replacing, 0.53 s unlinked first (profiles/r06_broadcast_write_probe.jsonl). The old file stays
-    until the new one is complete; the name is absent only between the unlink and the rename (the
-    reference's in-place save truncates the file before writing it)."""
+_TRASH = ".edt-old-"                  # an old file renamed away by _publish, deleted in the background
+_trash_seq = iter(range(1 << 62))
+_deleter = None
+_deleter_lock = threading.Lock()
+_pending_deletes: list = []
+
+
+def _unlink_quiet(path: str) -> None:
     try:
         os.remove(path)
     except FileNotFoundError:
         pass
+
+
+def _defer_delete(path: str) -> None:
+    global _deleter
+    with _deleter_lock:
+        if _deleter is None:
+            import atexit
+            from concurrent.futures import ThreadPoolExecutor
+            _deleter = ThreadPoolExecutor(max_workers=4, thread_name_prefix="edt-unlink")
+            atexit.register(flush_deletions)
+        _pending_deletes[:] = [f for f in _pending_deletes if not f.done()]
+        _pending_deletes.append(_deleter.submit(_unlink_quiet, path))
+
+
+def flush_deletions() -> None:
+    """Wait until every old file _publish renamed away has been deleted (also run at exit)."""
+    with _deleter_lock:
+        futs = list(_pending_deletes)
+        _pending_deletes.clear()
+    for f in futs:
+        f.result()
+
+
+def _publish(tmp: str, path: str) -> None:
+    """The complete file tmp becomes path without a rename that replaces a file: ext4 (and overlay
+    file systems over it, as on the GPU boxes) flushes a file's delayed allocation synchronously
+    when a rename replaces an existing file (auto_da_alloc), which made the broadcast over the
+    workers' trained checkpoints disk-bound — 8 x 2.6 GB in 3.2-4.1 s replacing, 0.53-0.60 s
+    unlinking the old file first (profiles/r06_broadcast_write_probe.jsonl). An existing path is
+    renamed away (path + .edt-old-<pid>-<n>), tmp renamed into the free name, and the old file —
+    whose unlink frees gigabytes of cached pages — deleted by a background thread, off the
+    caller's path (flush_deletions waits for it; old names left by a process that died first are
+    deleted by the next publish into that directory). The old file stays until the new one is
+    complete; the name is absent only between the two renames (the reference's in-place save
+    truncates the file before writing it)."""
+    d, base = os.path.split(path)
+    trash = f"{path}{_TRASH}{os.getpid()}-{next(_trash_seq)}"
+    try:
+        os.rename(path, trash)
+    except FileNotFoundError:
+        trash = None
     os.rename(tmp, path)
+    if trash is not None:
+        _defer_delete(trash)
+        prefix = base + _TRASH
+        for f in os.listdir(d or "."):          # left by a process that died before deleting
+            if f.startswith(prefix) and not _pid_alive(f[len(prefix):].split("-")[0]):
+                _defer_delete(os.path.join(d, f))
+
+
+def _pid_alive(pid: str) -> bool:
+    try:
+        os.kill(int(pid), 0)
+    except (ValueError, ProcessLookupError):
+        return False
+    except PermissionError:
+        return True
+    return True
 
 
 def copy_file(src: str, dst: str) -> None:

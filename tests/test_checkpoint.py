@@ -108,10 +108,12 @@ def test_broadcast_copies_are_independent_files(tmp_path):
 
 def test_broadcast_over_existing_files_unlinks_then_renames(tmp_path):
     """The broadcast lands over the workers' trained checkpoints (the outer step's out_dirs are its
-    worker dirs): each old file is unlinked before the complete new one is renamed into place
-    (checkpoint._publish: a rename that replaces nothing, so ext4 does not flush the new file
-    synchronously). The path ends with the new bytes on a new inode; another name of the old file
-    keeps the old bytes; copy_file does the same for the carried inner-state files."""
+    worker dirs): each old file is renamed away before the complete new one is renamed into place
+    (checkpoint._publish: no rename replaces a file, so ext4 does not flush the new file
+    synchronously) and deleted in the background. The path ends with the new bytes on a new inode;
+    another name of the old file keeps the old bytes; once flush_deletions returns nothing but the
+    new files is left; an old name left by a dead process is deleted by the next publish there;
+    copy_file unlinks an existing target for the carried inner-state files."""
     m = _tiny(torch.float32)
     layout = ParamLayout.of_module(m)
     flat = pack(list(m.parameters()))
@@ -123,7 +125,11 @@ def test_broadcast_over_existing_files_unlinks_then_renames(tmp_path):
     keep = str(tmp_path / "old_link")
     os.link(os.path.join(dirs[0], "model.safetensors"), keep)
     old_ino = os.stat(keep).st_ino
+    dead = os.path.join(dirs[1], "model.safetensors" + checkpoint._TRASH + "999999999-0")
+    open(dead, "wb").write(b"left by a dead process")
     checkpoint.save_to_dirs(dirs, layout, flat)
+    checkpoint.flush_deletions()
+    assert sorted(os.listdir(dirs[1])) == ["model.safetensors"] and os.listdir(dirs[2]) == ["model.safetensors"]
     files = [os.path.join(d, "model.safetensors") for d in dirs]
     ref = open(files[0], "rb").read()
     assert ref != b"trained replica" and all(open(f, "rb").read() == ref for f in files)
