@@ -1,4 +1,4 @@
-"""Probe the checkpoint write edge of a 7.07B bf16 child (14.1 GB, DESIGN.md §6.8): where the
+"""Probe the checkpoint write edge of a 7.07B bf16 child (14.1 GB, DESIGN.md §6.7): where the
 time of `checkpoint.write_from_arena` goes in a one-shot process (the reference's crossover CLI
 writes one child per process, EDT_EVOMERGE/train/crossover.py:86-146), and which host-buffer form
 writes fastest.
